@@ -1,0 +1,170 @@
+/*
+ * neus2_hip.h — C-ABI drop-in boundary of the MI355X (gfx950) NeuS2 training hot path.
+ *
+ * Plain pointers and sizes only (no torch / STL types). Every entry point returns an int
+ * status (0 = ok, nonzero = error; neus_last_error() gives the message), mirroring the
+ * reference's C++ exceptions that pybind11 turns into Python RuntimeError.
+ *
+ * Each entry point replaces one interface of the reference (zbqq/neus2 @ /root/reference):
+ *
+ *   Testbed surface (include/neural-graphics-primitives/testbed.h:63-940, src/python_api.cu:216-600)
+ *     neus_testbed_create              Testbed::Testbed                       src/testbed.cu:2583-2632
+ *     neus_testbed_set_dataset         Testbed::load_training_data -> load_nerf src/testbed_nerf.cu:2964-3095
+ *                                      (images/cameras decoded by the host mirror, nerf_loader.cu:197-751)
+ *     neus_testbed_reload_network      Testbed::reload_network_from_json -> reset_network src/testbed.cu:2084-2349
+ *     neus_testbed_train               Testbed::train(batch) x n_steps        src/testbed.cu:2640-2736
+ *     neus_testbed_get_stats           Testbed::m_training_step / m_loss_scalar / counters (python_api.cu:447-449)
+ *     neus_testbed_{get,set}_params    Trainer params / serialize             trainer.h:72-109, 281-300
+ *     neus_testbed_{get,set}_density_grid  Nerf::density_grid(_bitfield)      testbed.h:688-694
+ *     neus_testbed_init_data_parallel  (new) RCCL data parallelism over ray batches
+ *
+ *   Operator surface (my_tcnn DifferentiableObject / cpp_api.h:66-106 for the NerfNetwork, plus
+ *   the NeuS step kernels of src/testbed_nerf.cu), on caller-owned device buffers:
+ *     neus_net_forward                 NerfNetwork::forward_impl               nerf_network.h:145-328
+ *     neus_net_backward                NerfNetwork::backward_impl (Overwrite)  nerf_network.h:330-654
+ *     neus_grid_encode                 GridEncoding forward (kernel_grid)      grid.h:174-369
+ *     neus_sample_rays                 generate_training_samples_nerf_with_global_movement  testbed_nerf.cu:1263-1456
+ *     neus_loss_compact                compute_loss_kernel_train_nerf_with_global_movement  testbed_nerf.cu:1475-1997
+ *     neus_optimizer_step              Trainer::optimizer_step (Ema/ExpDecay/Adam)          trainer.h:170-172
+ *     neus_occ_update                  Testbed::update_density_grid_nerf                    testbed_nerf.cu:3293-3397
+ *
+ * Layouts (DESIGN.md §Data layout): coords AoS 7 x f32 (pos[3], dt, dir[3]) per sample;
+ * network output / dL/doutput AoS 16 x fp16 per sample; params fp32 [P] in the reference's
+ * set_params order [density MLP | rgb MLP | grid | variance(4)].
+ */
+#ifndef NEUS2_HIP_H
+#define NEUS2_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct NeusTestbed NeusTestbed;
+
+/* configs/nerf/base.json surface, parsed by the host mirror (neus2_amd/pyngp.py). */
+typedef struct NeusNetworkConfig {
+	/* encoding (grid.h GridEncodingTemplated; testbed.cu:2151-2197) */
+	uint32_t n_levels;
+	uint32_t n_features_per_level;   /* must be 2 */
+	uint32_t log2_hashmap_size;
+	uint32_t base_resolution;
+	float per_level_scale;           /* derived as testbed.cu:2185 when <= 0 */
+	float top_resolution;
+	float valid_level_scale;         /* progressive levels, grid.h:2427-2440 */
+	float base_valid_level_scale;
+	uint32_t base_training_step;
+	/* networks (nerf_network.h:53-96): FullyFusedMLP, ReLU, no output activation */
+	uint32_t n_neurons;              /* 16, 32 or 64 */
+	uint32_t n_density_hidden;       /* must be 1 on the GPU path */
+	uint32_t n_rgb_hidden;           /* must be 2 on the GPU path */
+	/* optimizer: Ema(decay) -> ExponentialDecay -> Adam */
+	float learning_rate, beta1, beta2, epsilon, l2_reg;
+	float ema_decay;
+	uint32_t decay_start, decay_interval;
+	float decay_base;
+	/* hyperparams (testbed.cu:2115-2137) */
+	float ek_loss_weight, mask_loss_weight;
+	uint32_t anneal_end;
+	uint32_t batch_size;             /* target compacted samples per step (2^18) */
+	float sdf_bias;                  /* -0.1 (nerf_network.h:87) */
+	float density_grid_decay;        /* 0.95 (testbed.h:659) */
+	uint32_t seed;                   /* 1337 (testbed.h:524) */
+	uint32_t fixed_rays_per_batch;   /* 0 = adaptive R (reference); >0 freezes R (benchmarks) */
+} NeusNetworkConfig;
+
+typedef struct NeusImage {
+	int32_t width, height;
+	const uint32_t* rgba8;           /* host pointer, width*height packed RGBA8 (R in the low byte) */
+	float focal[2];                  /* pixels */
+	float principal[2];              /* normalized [0,1] */
+	float xform[12];                 /* camera-to-world 3x4 row-major, ngp convention (nerf_loader.h:112-134) */
+} NeusImage;
+
+typedef struct NeusTrainStats {
+	uint32_t training_step;
+	uint32_t rays_per_batch;
+	uint32_t measured_batch_size;            /* compacted samples of the last step (Nc, per rank) */
+	uint32_t measured_batch_size_before_compaction; /* Npre requested, per rank */
+	uint32_t n_rays_total;
+	uint32_t valid_level;
+	uint32_t zero_records;
+	float loss;                               /* m_loss_scalar (EMA as the reference) */
+	float ek_loss;
+	float mask_loss;
+	float last_loss;                          /* last raw loss scalar */
+	float density_grid_mean;
+} NeusTrainStats;
+
+typedef struct NeusNetLayout {
+	uint64_t n_params, n_density, n_rgb, grid_offset, n_grid_params, variance_offset, n_matrix;
+	uint32_t density_input_width, rgb_input_width;
+} NeusNetLayout;
+
+const char* neus_last_error(void);
+int neus_device_count(int* count);
+int neus_device_synchronize(void);
+
+/* ------------------------------------------------------------------ Testbed */
+int neus_testbed_create(int device, NeusTestbed** out);
+int neus_testbed_destroy(NeusTestbed* tb);
+int neus_testbed_set_dataset(NeusTestbed* tb, uint32_t n_images, const NeusImage* images, float aabb_scale);
+int neus_testbed_reload_network(NeusTestbed* tb, const NeusNetworkConfig* cfg, const float* geometric_init /* nullable: n_density floats */);
+int neus_testbed_layout(NeusTestbed* tb, NeusNetLayout* out);
+int neus_testbed_train(NeusTestbed* tb, uint32_t n_steps);
+int neus_testbed_get_stats(NeusTestbed* tb, NeusTrainStats* out);
+int neus_testbed_get_params(NeusTestbed* tb, float* host_out, uint64_t n);
+int neus_testbed_set_params(NeusTestbed* tb, const float* host_in, uint64_t n);
+int neus_testbed_get_gradients(NeusTestbed* tb, float* host_out, uint64_t n);
+int neus_testbed_get_ema_params(NeusTestbed* tb, float* host_out, uint64_t n);
+int neus_testbed_get_density_grid(NeusTestbed* tb, float* grid_out /*128^3*/, uint8_t* bitfield_out /*128^3/8*8*/);
+int neus_testbed_set_density_grid(NeusTestbed* tb, const float* grid /*nullable*/, const uint8_t* bitfield /*nullable*/);
+int neus_testbed_get_rng(NeusTestbed* tb, uint64_t* state_inc /*4: rng, density_grid_rng*/);
+int neus_testbed_stream(NeusTestbed* tb, void** hip_stream);
+int neus_testbed_synchronize(NeusTestbed* tb);
+/* Per-phase step timing with hipEvents on the testbed stream (profiling on): ms_out[0..6] =
+ * occupancy update, ray sampling, inference encode, inference MLP, loss+compaction, backward,
+ * all-reduce+optimizer (mean ms per step); ms_out[7] = number of profiled steps. */
+int neus_testbed_set_profiling(NeusTestbed* tb, int on);
+int neus_testbed_kernel_times(NeusTestbed* tb, float* ms_out /* 8 entries */);
+
+/* ------------------------------------------------------------------ data parallel (RCCL over xGMI) */
+int neus_nccl_unique_id(uint8_t* out /* 128 bytes */);
+int neus_testbed_init_data_parallel(NeusTestbed* tb, int rank, int world, const uint8_t* unique_id /* 128 bytes */);
+
+/* ------------------------------------------------------------------ operator surface (device buffers) */
+/* Hash-grid forward on n positions (AoS, `coord_stride` floats per sample, xyz first).
+ * enc: [2L][ld] fp16, dydx: [6L][ld] f32 (nullable). */
+int neus_grid_encode(NeusTestbed* tb, void* stream, uint32_t n, uint32_t ld, const float* coords, uint32_t coord_stride,
+                     uint32_t valid_level, uint16_t* enc, float* dydx);
+/* NerfNetwork forward: coords AoS7 f32 -> out AoS16 fp16 (training weights). */
+int neus_net_forward(NeusTestbed* tb, void* stream, uint32_t n, const float* coords, uint32_t valid_level, uint16_t* out);
+/* NerfNetwork forward+backward (first- and second-order), gradient Overwrite into grads_out
+ * (fp32 [P], device). n must be a multiple of 128. */
+int neus_net_backward(NeusTestbed* tb, void* stream, uint32_t n, const float* coords, uint32_t valid_level, const uint16_t* dL_dout,
+                      uint32_t indeed_batch_size, float* grads_out);
+/* Training-sample generation with the testbed's dataset on the given bitfield. Outputs are
+ * per ray slot (canonical ray order): rays 6 f32, numsteps 2 u32 (n, base), coords AoS7.
+ * counters_out (host, 3 u32): numsteps_counter, n_kept, n_rays_with_samples. */
+int neus_sample_rays(NeusTestbed* tb, void* stream, uint32_t n_rays, uint32_t rank, uint32_t world, uint32_t n_rays_total,
+                     uint64_t rng_state, uint64_t rng_inc, uint32_t max_samples, const uint8_t* bitfield,
+                     float* rays, uint32_t* numsteps, float* coords, uint32_t* counters_out);
+/* NeuS composite + loss + compaction given network outputs. numsteps is rewritten to
+ * (n_compacted, compacted_base). counters_out (host): compacted_counter. */
+int neus_loss_compact(NeusTestbed* tb, void* stream, uint32_t n_rays, uint32_t rank, uint32_t world, uint32_t n_rays_total,
+                      uint64_t rng_state, uint64_t rng_inc, uint32_t max_compacted, const float* rays, uint32_t* numsteps,
+                      const float* coords, const uint16_t* net_out, float* coords_out, uint16_t* dL_dout,
+                      float* loss, float* ek_loss, float* mask_loss, uint32_t* counters_out);
+/* One Ema(Adam) step on the testbed's parameters with the given fp32 gradients (device). */
+int neus_optimizer_step(NeusTestbed* tb, void* stream, const float* grads);
+/* One occupancy-grid update (density_grid + bitfield) of the testbed's state. */
+int neus_occ_update(NeusTestbed* tb, void* stream, uint32_t n_uniform, uint32_t n_nonuniform);
+/* MFMA fragment-layout probe: C[32x32] = A[32x16] * B[16x32], fp16 row-major in, f32 out. */
+int neus_mfma_probe(const uint16_t* A, const uint16_t* B, float* C);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NEUS2_HIP_H */

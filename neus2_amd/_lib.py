@@ -1,0 +1,93 @@
+"""ctypes binding of the C-ABI in include/neus2_hip.h (libneus2_hip.so, built in-tree).
+
+The product path runs only through this library: if it is missing the import fails loudly
+(there is no CPU fallback).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libneus2_hip.so")
+
+
+class NeusNetworkConfig(C.Structure):
+    _fields_ = [
+        ("n_levels", C.c_uint32), ("n_features_per_level", C.c_uint32), ("log2_hashmap_size", C.c_uint32),
+        ("base_resolution", C.c_uint32), ("per_level_scale", C.c_float), ("top_resolution", C.c_float),
+        ("valid_level_scale", C.c_float), ("base_valid_level_scale", C.c_float), ("base_training_step", C.c_uint32),
+        ("n_neurons", C.c_uint32), ("n_density_hidden", C.c_uint32), ("n_rgb_hidden", C.c_uint32),
+        ("learning_rate", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float), ("epsilon", C.c_float), ("l2_reg", C.c_float),
+        ("ema_decay", C.c_float), ("decay_start", C.c_uint32), ("decay_interval", C.c_uint32), ("decay_base", C.c_float),
+        ("ek_loss_weight", C.c_float), ("mask_loss_weight", C.c_float), ("anneal_end", C.c_uint32), ("batch_size", C.c_uint32),
+        ("sdf_bias", C.c_float), ("density_grid_decay", C.c_float), ("seed", C.c_uint32), ("fixed_rays_per_batch", C.c_uint32),
+    ]
+
+
+class NeusImage(C.Structure):
+    _fields_ = [
+        ("width", C.c_int32), ("height", C.c_int32), ("rgba8", C.c_void_p),
+        ("focal", C.c_float * 2), ("principal", C.c_float * 2), ("xform", C.c_float * 12),
+    ]
+
+
+class NeusTrainStats(C.Structure):
+    _fields_ = [
+        ("training_step", C.c_uint32), ("rays_per_batch", C.c_uint32), ("measured_batch_size", C.c_uint32),
+        ("measured_batch_size_before_compaction", C.c_uint32), ("n_rays_total", C.c_uint32), ("valid_level", C.c_uint32),
+        ("zero_records", C.c_uint32), ("loss", C.c_float), ("ek_loss", C.c_float), ("mask_loss", C.c_float),
+        ("last_loss", C.c_float), ("density_grid_mean", C.c_float),
+    ]
+
+
+class NeusNetLayout(C.Structure):
+    _fields_ = [
+        ("n_params", C.c_uint64), ("n_density", C.c_uint64), ("n_rgb", C.c_uint64), ("grid_offset", C.c_uint64),
+        ("n_grid_params", C.c_uint64), ("variance_offset", C.c_uint64), ("n_matrix", C.c_uint64),
+        ("density_input_width", C.c_uint32), ("rgb_input_width", C.c_uint32),
+    ]
+
+
+# Every symbol declared in include/neus2_hip.h (checked by tests/test_capi.py).
+EXPORTS = [
+    "neus_last_error", "neus_device_count", "neus_device_synchronize",
+    "neus_testbed_create", "neus_testbed_destroy", "neus_testbed_set_dataset", "neus_testbed_reload_network",
+    "neus_testbed_layout", "neus_testbed_train", "neus_testbed_get_stats", "neus_testbed_get_params",
+    "neus_testbed_set_params", "neus_testbed_get_gradients", "neus_testbed_get_ema_params",
+    "neus_testbed_get_density_grid", "neus_testbed_set_density_grid", "neus_testbed_get_rng", "neus_testbed_stream",
+    "neus_testbed_synchronize", "neus_testbed_set_profiling", "neus_testbed_kernel_times",
+    "neus_nccl_unique_id", "neus_testbed_init_data_parallel",
+    "neus_grid_encode", "neus_net_forward", "neus_net_backward", "neus_sample_rays", "neus_loss_compact",
+    "neus_optimizer_step", "neus_occ_update", "neus_mfma_probe",
+]
+
+_lib = None
+
+
+def lib():
+    """Loads libneus2_hip.so. Raises if it has not been built (no fallback path exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    l = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+    l.neus_last_error.restype = C.c_char_p
+    for name in EXPORTS:
+        f = getattr(l, name)
+        if name != "neus_last_error":
+            f.restype = C.c_int
+    _lib = l
+    return l
+
+
+class NeusError(RuntimeError):
+    pass
+
+
+def check(rc):
+    if rc != 0:
+        msg = lib().neus_last_error()
+        raise NeusError(msg.decode() if msg else "neus error")
+    return rc

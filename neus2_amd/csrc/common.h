@@ -1,0 +1,129 @@
+// Shared device/host helpers for the gfx950 NeuS2 hot path.
+// Reference semantics cited per function; layouts documented in DESIGN.md §Data layout.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+#define NEUS_HD __host__ __device__ __forceinline__
+
+typedef _Float16 half_t;
+typedef half_t h8 __attribute__((ext_vector_type(8)));
+typedef half_t h4 __attribute__((ext_vector_type(4)));
+typedef half_t h2 __attribute__((ext_vector_type(2)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+namespace neus {
+
+// ----------------------------------------------------------- constants (testbed_nerf.cu:57-81)
+constexpr uint32_t NERF_GRIDSIZE = 128;
+constexpr uint32_t NERF_STEPS = 1024;
+constexpr uint32_t NERF_CASCADES = 8;
+constexpr float SQRT3 = 1.73205080757f;
+constexpr float STEPSIZE = SQRT3 / NERF_STEPS;
+constexpr float MIN_CONE_STEPSIZE = STEPSIZE;
+constexpr float MAX_CONE_STEPSIZE = STEPSIZE * (1 << (NERF_CASCADES - 1)) * NERF_STEPS / NERF_GRIDSIZE;
+constexpr uint32_t N_MAX_RANDOM_SAMPLES_PER_RAY = 8;
+constexpr float NERF_MIN_OPTICAL_THICKNESS = 0.1f;
+constexpr uint32_t GRID3 = NERF_GRIDSIZE * NERF_GRIDSIZE * NERF_GRIDSIZE;
+constexpr uint32_t MAX_LEVELS = 16;
+constexpr uint32_t OUT_W = 16;      // padded network output width (nerf_network.h:935)
+constexpr uint32_t COORD_W = 7;     // NerfCoordinate floats (nerf.h:76-102)
+
+// ----------------------------------------------------------- pcg32 (my_tcnn pcg32.h:43-170)
+struct pcg32 {
+	uint64_t state, inc;
+	NEUS_HD pcg32() : state(0x853c49e6748fea9bULL), inc(0xda3e39cb94b95bdbULL) {}
+	NEUS_HD pcg32(uint64_t s, uint64_t i) : state(s), inc(i) {}
+	NEUS_HD uint32_t next_uint() {
+		uint64_t oldstate = state;
+		state = oldstate * 0x5851f42d4c957f2dULL + inc;
+		uint32_t xorshifted = (uint32_t)(((oldstate >> 18u) ^ oldstate) >> 27u);
+		uint32_t rot = (uint32_t)(oldstate >> 59u);
+		return (xorshifted >> rot) | (xorshifted << ((~rot + 1u) & 31));
+	}
+	NEUS_HD float next_float() {
+		union { uint32_t u; float f; } x;
+		x.u = (next_uint() >> 9) | 0x3f800000u;
+		return x.f - 1.0f;
+	}
+	NEUS_HD void advance(int64_t delta_ = (1ll << 32)) {
+		uint64_t cur_mult = 0x5851f42d4c957f2dULL, cur_plus = inc, acc_mult = 1u, acc_plus = 0u;
+		uint64_t delta = (uint64_t)delta_;
+		while (delta > 0) {
+			if (delta & 1) { acc_mult *= cur_mult; acc_plus = acc_plus * cur_mult + cur_plus; }
+			cur_plus = (cur_mult + 1) * cur_plus; cur_mult *= cur_mult; delta /= 2;
+		}
+		state = acc_mult * state + acc_plus;
+	}
+};
+inline pcg32 make_pcg32(uint64_t initstate, uint64_t initseq = 1u) {
+	pcg32 r; r.state = 0U; r.inc = (initseq << 1u) | 1u; r.next_uint(); r.state += initstate; r.next_uint(); return r;
+}
+
+// ----------------------------------------------------------- half helpers
+NEUS_HD float rh(float f) { return (float)(half_t)f; }
+
+// fixed-operation-order expf, identical on CPU oracle and GPU (no contraction in callers)
+NEUS_HD float det_expf(float x) {
+	if (!(x < 88.5f)) return x != x ? x : __builtin_huge_valf();
+	if (x < -103.0f) return 0.0f;
+	float kf = rintf(x * 1.44269504088896341f);
+	float r = x - kf * 0.693145751953125f;
+	r = r - kf * 1.42860676533018672e-06f;
+	float p = 1.3888889225e-3f;
+	p = p * r + 8.3333337680e-3f;
+	p = p * r + 4.1666667908e-2f;
+	p = p * r + 1.6666667163e-1f;
+	p = p * r + 0.5f;
+	p = p * r + 1.0f;
+	p = p * r + 1.0f;
+	return ldexpf(p, (int)kf);
+}
+NEUS_HD float det_logistic(float x) { return 1.0f / (1.0f + det_expf(-x)); }
+
+// ----------------------------------------------------------- morton (my_tcnn common_device.h:335-365)
+NEUS_HD uint32_t expand_bits(uint32_t v) {
+	v = (v * 0x00010001u) & 0xFF0000FFu; v = (v * 0x00000101u) & 0x0F00F00Fu;
+	v = (v * 0x00000011u) & 0xC30C30C3u; v = (v * 0x00000005u) & 0x49249249u; return v;
+}
+NEUS_HD uint32_t morton3D(uint32_t x, uint32_t y, uint32_t z) { return expand_bits(x) | (expand_bits(y) << 1) | (expand_bits(z) << 2); }
+NEUS_HD uint32_t morton3D_invert(uint32_t x) {
+	x = x & 0x49249249; x = (x | (x >> 2)) & 0xc30c30c3; x = (x | (x >> 4)) & 0x0f00f00f;
+	x = (x | (x >> 8)) & 0xff0000ff; x = (x | (x >> 16)) & 0x0000ffff; return x;
+}
+
+// ----------------------------------------------------------- hash grid addressing (grid.h:118-153)
+struct GridLevels {
+	uint32_t n_levels;
+	uint32_t offset[MAX_LEVELS + 1];   // in entries (x2 features)
+	uint32_t res[MAX_LEVELS];
+	float scale[MAX_LEVELS];
+};
+NEUS_HD uint32_t grid_index(uint32_t hashmap_size, uint32_t resolution, uint32_t x, uint32_t y, uint32_t z) {
+	uint32_t stride = 1, index = 0;
+	index += x * stride; stride *= resolution;
+	if (stride <= hashmap_size) { index += y * stride; stride *= resolution; }
+	if (stride <= hashmap_size) { index += z * stride; stride *= resolution; }
+	if (hashmap_size < stride) index = x ^ (y * 2654435761u) ^ (z * 805459861u);
+	return index % hashmap_size;
+}
+
+// Device-resident per-step counters: the host never syncs inside a training step.
+struct StepState {
+	uint32_t rays_per_batch;          // R (adapted on device, testbed_nerf.cu:3399-3438)
+	uint32_t max_inference;           // next_multiple(min(Npre_prev, max_samples), 128)
+	uint32_t measured_before;         // Npre requested counter of the last step (per rank)
+	uint32_t numsteps_counter;        // this step: requested samples (all rays)
+	uint32_t n_kept;                  // this step: samples actually written
+	uint32_t compacted_counter;       // this step: requested compacted samples
+	uint32_t measured_batch_size;     // compacted counter of the last step (per rank)
+	uint32_t n_rays_with_samples;
+	uint32_t zero_records;
+	uint32_t n_rays_total;            // rays drawn since training step 0 (all ranks)
+	uint32_t n_train;                 // compacted training batch (target) or 0 when no samples
+	uint32_t pad[5];
+};
+
+} // namespace neus

@@ -1,0 +1,108 @@
+// Host-callable launchers of the gfx950 kernels (defined in the .hip files) and the structs
+// shared between the host orchestration (testbed.cpp) and the kernels.
+#pragma once
+#include "common.h"
+
+namespace neus {
+
+struct MlpPtrs {
+	const half_t* d0;  const half_t* d1;                     // density W0 [W][DIN], W1 [16][W]
+	const half_t* r0;  const half_t* r1;  const half_t* r2;  // rgb W0 [W][48], W1 [W][W], W2 [16][W]
+	const half_t* d0T; const half_t* d1T;                    // transposed copies [DIN][W], [W][16]
+	const half_t* r0T; const half_t* r1T; const half_t* r2T; // [48][W], [W][W], [W][16]
+	const half_t* var;                                       // variance param (fp16)
+	float sdf_bias;                                          // -0.1
+};
+
+struct TrainBufs {
+	// weight-gradient operands, SoA [rows][cols] fp16; density layers have 2*ld columns
+	half_t* d0_delta; half_t* d0_x;   // [W][2ld], [DIN][2ld]
+	half_t* d1_delta; half_t* d1_x;   // [16][2ld], [W][2ld]
+	half_t* r0_delta; half_t* r0_x;   // [W][ld], [48][ld]
+	half_t* r1_delta; half_t* r1_x;   // [W][ld], [W][ld]
+	half_t* r2_delta; half_t* r2_x;   // [16][ld], [W][ld]
+	half_t* dLdenc; half_t* genc;     // [L][ld] half2 (features 2l, 2l+1)
+	float4* v;                        // [ld]
+	float* var_grad;                  // scalar accumulator
+	float indeed_batch;
+};
+
+struct WGradJob { const half_t* D; const half_t* X; float* dW; uint32_t M, K, ncols, ldc; uint32_t tiles_m, tiles_k; };
+struct WGradJobs { WGradJob j[5]; uint32_t n_jobs; uint32_t split; uint32_t block_start[6]; const uint32_t* n_valid; };
+
+struct DevDataset {
+	const uint32_t* pixels;
+	const uint64_t* pix_off;
+	const int32_t* res;       // 2 per image
+	const float* focal;       // 2 per image
+	const float* pp;          // 2 per image
+	const float* xform;       // 12 per image (row-major 3x4)
+	uint32_t n_images;
+	float aabb_min[3], aabb_max[3];
+	float cone_angle;
+};
+
+struct DPInfo { uint32_t rank, world; };
+
+struct LossParams {
+	float loss_scale;      // LOSS_SCALE = 128 (testbed.h:246)
+	float ek_w, mask_w, cos_anneal;
+	uint32_t max_compacted; // target batch size
+	uint64_t rng_state, rng_inc;
+};
+
+struct AdamParams {
+	uint32_t n, n_matrix;
+	float loss_scale, lr, beta1, beta2, eps, l2_reg;
+	float ema_decay, ema_debias_old, ema_debias_new;
+	uint32_t optimize_matrix, optimize_non_matrix;
+};
+
+struct TransposeJob { const half_t* src; half_t* dst; uint32_t rows, cols; };
+struct TransposeJobs { TransposeJob j[8]; uint32_t n; };
+
+// grid.hip
+void launch_grid_encode(hipStream_t s, const uint32_t* n_ptr, uint32_t n_fixed, uint32_t ld, const float* coords, uint32_t coord_stride,
+                        const GridLevels& gl, uint32_t valid_level, const half_t* grid, uint32_t* enc, float* dydx, uint32_t grid_x);
+void launch_grid_scatter(hipStream_t s, const uint32_t* n_ptr, uint32_t n_fixed, uint32_t ld, const float* coords, uint32_t coord_stride,
+                         const GridLevels& gl, uint32_t valid_level, const half_t* dLdenc, const half_t* g, const float4* v, float* grads, uint32_t grid_x);
+// mlp.hip
+bool mlp_supported(uint32_t n_levels, uint32_t width);
+void launch_mlp_forward(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_ptr, uint32_t n_fixed, uint32_t ld, const float* coords,
+                        const half_t* enc, const float* dydx, const MlpPtrs& w, half_t* out, uint32_t blocks);
+void launch_mlp_density(hipStream_t s, uint32_t L, uint32_t W, uint32_t n, uint32_t ld, const float* pos, const half_t* enc,
+                        const MlpPtrs& w, float* density);
+void launch_mlp_train(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_valid_ptr, uint32_t n, uint32_t ld, const float* coords,
+                      const half_t* enc, const float* dydx, const half_t* dL_dout, const MlpPtrs& w, const TrainBufs& tb);
+void launch_wgrad(hipStream_t s, const WGradJobs& jobs, uint32_t n_blocks);
+void launch_mfma_probe(hipStream_t s, const half_t* A, const half_t* B, float* C);
+// march.hip
+void launch_march_count(hipStream_t s, uint32_t cap, const StepState* st, DPInfo dp, const DevDataset& ds, const uint8_t* bitfield,
+                        uint64_t rng_state, uint64_t rng_inc, float* rays, float* startt, uint32_t* nreq);
+void launch_march_write(hipStream_t s, uint32_t cap, StepState* st, const DevDataset& ds, const uint8_t* bitfield, const float* rays,
+                        const float* startt, const uint32_t* nreq, const uint32_t* base, uint32_t* numsteps, float* coords);
+void launch_loss_count(hipStream_t s, uint32_t cap, const StepState* st, const DevDataset& ds, const float* rays, const uint32_t* numsteps,
+                       const float* coords, const half_t* net_out, float cos_anneal, uint32_t* ccount);
+void launch_loss_write(hipStream_t s, uint32_t cap, StepState* st, DPInfo dp, const DevDataset& ds, const LossParams& lp, const float* rays,
+                       uint32_t* numsteps, const float* coords, const half_t* net_out, const uint32_t* ccount, const uint32_t* cbase,
+                       float* coords_out, half_t* dL_dout, float* loss, float* ek, float* mask);
+void launch_rollover(hipStream_t s, uint32_t n_elements, const StepState* st, float* coords, half_t* dL_dout);
+void launch_step_counters(hipStream_t s, StepState* st, uint32_t target_batch, uint32_t max_samples, uint32_t world, uint32_t fixed_rays);
+// scan.hip
+size_t scan_temp_bytes(uint32_t n);
+void launch_exclusive_scan(hipStream_t s, void* temp, size_t temp_bytes, const uint32_t* in, uint32_t* out, uint32_t n);
+void launch_sum_f32(hipStream_t s, void* temp, size_t temp_bytes, const float* in, float* out, uint32_t n);
+// optim.hip
+void launch_adam_ema(hipStream_t s, const AdamParams& p, float* weights_fp, half_t* weights_h, const float* grads, float* m1, float* m2,
+                     uint32_t* steps, float* ema_tmp, half_t* ema_h);
+void launch_cast_half(hipStream_t s, uint32_t n, const float* in, half_t* out);
+void launch_transpose_w(hipStream_t s, const TransposeJobs& jobs);
+void launch_grid_samples(hipStream_t s, uint32_t n, uint32_t out_offset, uint64_t rng_state, uint64_t rng_inc, uint32_t step,
+                         const float* aabb_min, const float* aabb_max, const float* grid_in, float* pos, uint32_t* indices,
+                         uint32_t n_cascades, float thresh);
+void launch_splat_max(hipStream_t s, uint32_t n, const uint32_t* indices, const float* density, float* grid_tmp);
+void launch_ema_grid(hipStream_t s, uint32_t n, float decay, float* grid, const float* tmp);
+void launch_grid_mean(hipStream_t s, const float* grid, float* partial, float* mean);
+void launch_bitfield(hipStream_t s, const float* grid, uint8_t* bitfield, const float* mean, uint32_t n_cascades);
+
+} // namespace neus

@@ -1,0 +1,565 @@
+// NeuS2 SDF + colour MLPs on gfx950 MFMA (v_mfma_f32_32x32x16_f16, fp16 in / fp32 accumulate).
+//
+// Formulation: every layer is computed TRANSPOSED, Y[neuron][sample] = W[neuron][k] X[k][sample],
+// with 32 samples on the MFMA column (lane & 31) and the neurons in the accumulator registers.
+// A 32x32 accumulator tile is then directly the B operand of the next layer (the contraction
+// runs over its rows), so activations never leave registers between layers. The k order of a
+// fragment built from an accumulator is permuted:   element j of lane half h <-> row pi(j,h),
+//      pi(j,h) = 8*(j>>2) + 4*h + (j&3)      (16-row k-step)
+// and every A (weight) fragment is loaded with the same permutation (loadA), as is every B
+// fragment built from memory, so all products are consistent.
+//
+// Reference semantics (per sample):
+//   density MLP  fully_fused_mlp.cu:678-812 (1 hidden ReLU layer, linear 16-wide output)
+//   grad SDF     nerf_network.h:228-253 + kernel_grid_backward_input (grid.h:803-830)
+//   SH deg 4     spherical_harmonics.h:47-100
+//   rgb MLP      fully_fused_mlp.cu (2 hidden ReLU layers) ; output packing nerf_network.h:287-324
+//   backward     nerf_network.h:330-601, FullyFusedMLP::backward_backward_input (:1088-1198)
+// Storage rounding points (fp16) follow the reference: hidden activations, deltas, the
+// density output, dSDF/d(input), the network output and dL/doutput.
+#include "kernels.h"
+#include <algorithm>
+
+namespace neus {
+
+__device__ __forceinline__ f16v mfma(h8 a, h8 b, f16v c) { return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0); }
+__device__ __forceinline__ constexpr int pi_row(int j, int h) { return 8 * (j >> 2) + 4 * h + (j & 3); }
+// accumulator register i of lane half h holds row acc_row(i,h) of the 32-row tile
+__device__ __forceinline__ constexpr int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
+
+__device__ __forceinline__ h8 loadA(const half_t* __restrict__ W, uint32_t ld, uint32_t M, uint32_t row, uint32_t kbase, uint32_t h) {
+	h8 a;
+	if (row < M) {
+		const half_t* p = W + (size_t)row * ld + kbase + 4 * h;
+		const h4 lo = *(const h4*)p;
+		const h4 hi = *(const h4*)(p + 8);
+		a = (h8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+	} else {
+		a = (h8){0, 0, 0, 0, 0, 0, 0, 0};
+	}
+	return a;
+}
+// B fragment (k-step s of an accumulator tile), optional ReLU mask source
+__device__ __forceinline__ h8 accB(const f16v& acc, int s) {
+	h8 b;
+#pragma unroll
+	for (int j = 0; j < 8; ++j) b[j] = (half_t)acc[8 * s + j];
+	return b;
+}
+__device__ __forceinline__ h8 shfl_xor_h8(h8 v, int m) {
+	union { h8 h; int i[4]; } u;
+	u.h = v;
+#pragma unroll
+	for (int k = 0; k < 4; ++k) u.i[k] = __shfl_xor(u.i[k], m);
+	return u.h;
+}
+__device__ __forceinline__ f16v zero16() { f16v z; for (int i = 0; i < 16; ++i) z[i] = 0.f; return z; }
+__device__ __forceinline__ f16v relu16(f16v a) { for (int i = 0; i < 16; ++i) a[i] = a[i] > 0.f ? a[i] : 0.f; return a; }
+// round an accumulator tile to fp16 storage precision
+__device__ __forceinline__ f16v rh16(f16v a) { for (int i = 0; i < 16; ++i) a[i] = rh(a[i]); return a; }
+
+template <int L> struct Dims {
+	static constexpr int DIN = ((3 + 2 * L) + 15) / 16 * 16;
+	static constexpr int DKS = DIN / 16;           // density-input k-steps
+	static constexpr int DMT = (DIN + 31) / 32;    // M tiles of a DIN-row result
+	static constexpr int NF = 2 * L;               // encoding features
+};
+
+// Forward state kept in registers for one 32-sample chunk.
+template <int L, int W> struct Fwd {
+	static constexpr int MT = (W + 31) / 32;   // hidden tiles
+	static constexpr int HKS = W / 16;          // hidden k-steps
+	h8 dinB[Dims<L>::DKS];
+	f16v H0[MT];          // density hidden (post-ReLU, fp16-rounded)
+	f16v D1;              // density output (fp16-rounded), rows 0..15 in regs 0..7
+	h8 GhB[HKS];          // relu'(H0) . W1d[0]  (also b2 of the double backward)
+	f16v Gi[Dims<L>::DMT];// dSDF/d(density input) (fp16-rounded)
+	float grad[3];        // dSDF/dx
+	h8 rinB[3];           // rgb input fragments
+	f16v H1[MT], H2[MT];  // rgb hidden (post-ReLU, fp16)
+	f16v O;               // rgb output (fp16-rounded)
+};
+
+// Reads this lane's encoding features and builds the density-input B fragments.
+template <int L>
+__device__ __forceinline__ void build_din(h8* dinB, const float x[3], const half_t* __restrict__ enc_h /*[L][ld] half2*/, uint32_t ld, uint32_t i, int h) {
+	constexpr int DIN = Dims<L>::DIN;
+	float dv[DIN];
+#pragma unroll
+	for (int k = 0; k < DIN; ++k) {
+		if (k < 3) dv[k] = rh(rh(x[k]) - 0.5f);
+		else if (k < 3 + 2 * L) dv[k] = (float)enc_h[((size_t)((k - 3) >> 1) * ld + i) * 2 + ((k - 3) & 1)];  // [L][ld] half2
+		else dv[k] = 0.f;
+	}
+#pragma unroll
+	for (int ks = 0; ks < Dims<L>::DKS; ++ks)
+#pragma unroll
+		for (int j = 0; j < 8; ++j) dinB[ks][j] = (half_t)(h ? dv[16 * ks + pi_row(j, 1)] : dv[16 * ks + pi_row(j, 0)]);
+}
+
+__device__ __forceinline__ void sh16(const float wd[3], float out[16]) {
+	const float x = wd[0] * 2.f - 1.f, y = wd[1] * 2.f - 1.f, z = wd[2] * 2.f - 1.f;
+	const float xy = x * y, xz = x * z, yz = y * z, x2 = x * x, y2 = y * y, z2 = z * z;
+	out[0] = 0.28209479177387814f;
+	out[1] = -0.48860251190291987f * y;
+	out[2] = 0.48860251190291987f * z;
+	out[3] = -0.48860251190291987f * x;
+	out[4] = 1.0925484305920792f * xy;
+	out[5] = -1.0925484305920792f * yz;
+	out[6] = 0.94617469575755997f * z2 - 0.31539156525251999f;
+	out[7] = -1.0925484305920792f * xz;
+	out[8] = 0.54627421529603959f * x2 - 0.54627421529603959f * y2;
+	out[9] = 0.59004358992664352f * y * (-3.0f * x2 + y2);
+	out[10] = 2.8906114426405538f * xy * z;
+	out[11] = 0.45704579946446572f * y * (1.0f - 5.0f * z2);
+	out[12] = 0.3731763325901154f * z * (5.0f * z2 - 3.0f);
+	out[13] = 0.45704579946446572f * x * (1.0f - 5.0f * z2);
+	out[14] = 1.4453057213202769f * z * (x2 - y2);
+	out[15] = 0.59004358992664352f * x * (-x2 + 3.0f * y2);
+}
+
+// Full NerfNetwork forward for this lane's sample (r = lane & 31, h = lane >> 5).
+// Every lane of the wave must call this (MFMA), valid or not.
+template <int L, int W>
+__device__ __forceinline__ void forward_chunk(Fwd<L, W>& F, const MlpPtrs& w, const float x[3], const float wd[3],
+                                              const half_t* __restrict__ enc_h, const float* __restrict__ dydx, uint32_t ld,
+                                              uint32_t i, bool valid, int r, int h) {
+	constexpr int DIN = Dims<L>::DIN, DKS = Dims<L>::DKS, DMT = Dims<L>::DMT;
+	constexpr int MT = Fwd<L, W>::MT, HKS = Fwd<L, W>::HKS;
+	build_din<L>(F.dinB, x, enc_h, ld, valid ? i : 0, h);
+	// density layer 0 + ReLU
+#pragma unroll
+	for (int mt = 0; mt < MT; ++mt) {
+		f16v acc = zero16();
+#pragma unroll
+		for (int ks = 0; ks < DKS; ++ks) acc = mfma(loadA(w.d0, DIN, W, 32 * mt + r, 16 * ks, h), F.dinB[ks], acc);
+		F.H0[mt] = rh16(relu16(acc));
+	}
+	// density layer 1 (16 outputs)
+	{
+		f16v acc = zero16();
+#pragma unroll
+		for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.d1, W, 16, r, 16 * ks, h), accB(F.H0[ks >> 1], ks & 1), acc);
+		F.D1 = rh16(acc);
+	}
+	// G_h = relu'(H0) . W1d[0]: row 0 of W1d loaded in the same (pi) order as the H0 fragments
+#pragma unroll
+	for (int ks = 0; ks < HKS; ++ks) {
+		const h8 w1row = loadA(w.d1, W, 16, 0, 16 * ks, h);
+		const f16v& hh = F.H0[ks >> 1];
+		h8 g;
+#pragma unroll
+		for (int j = 0; j < 8; ++j) g[j] = hh[8 * (ks & 1) + j] > 0.f ? w1row[j] : (half_t)0.f;
+		F.GhB[ks] = g;
+	}
+	// G_in = W0d^T G_h  (DIN rows)
+#pragma unroll
+	for (int mt = 0; mt < DMT; ++mt) {
+		f16v acc = zero16();
+#pragma unroll
+		for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.d0T, W, DIN, 32 * mt + r, 16 * ks, h), F.GhB[ks], acc);
+		F.Gi[mt] = rh16(acc);
+	}
+	// dSDF/dx = sum_k G_in[k] dy/dx[k] (+ identity rows 0..2), split over the two lane halves
+	float part[3] = {0.f, 0.f, 0.f};
+	const uint32_t ii = valid ? i : 0;
+#pragma unroll
+	for (int mt = 0; mt < DMT; ++mt)
+#pragma unroll
+		for (int reg = 0; reg < 16; ++reg) {
+			const int k = 32 * mt + acc_row(reg, h);
+			const float gv = F.Gi[mt][reg];
+			if (k < 3) {
+				part[0] += (k == 0) ? gv : 0.f; part[1] += (k == 1) ? gv : 0.f; part[2] += (k == 2) ? gv : 0.f;
+			} else if (k < 3 + 2 * L) {
+				const float* dp = dydx + (size_t)(3 * (k - 3)) * ld + ii;
+				part[0] += gv * dp[0];
+				part[1] += gv * dp[ld];
+				part[2] += gv * dp[2 * (size_t)ld];
+			}
+		}
+#pragma unroll
+	for (int d = 0; d < 3; ++d) F.grad[d] = part[d] + __shfl_xor(part[d], 32);
+	// rgb input fragments: ks0 = density output, ks1 = SH, ks2 = [xyz, grad, 0...]
+	F.rinB[0] = accB(F.D1, 0);
+	{
+		float sh[16]; sh16(wd, sh);
+#pragma unroll
+		for (int j = 0; j < 8; ++j) F.rinB[1][j] = (half_t)(h ? sh[pi_row(j, 1)] : sh[pi_row(j, 0)]);
+		float r32[16];
+#pragma unroll
+		for (int k = 0; k < 16; ++k) r32[k] = 0.f;
+		r32[0] = x[0]; r32[1] = x[1]; r32[2] = x[2];
+		r32[3] = F.grad[0]; r32[4] = F.grad[1]; r32[5] = F.grad[2];
+#pragma unroll
+		for (int j = 0; j < 8; ++j) F.rinB[2][j] = (half_t)(h ? r32[pi_row(j, 1)] : r32[pi_row(j, 0)]);
+	}
+	// rgb layers
+#pragma unroll
+	for (int mt = 0; mt < MT; ++mt) {
+		f16v acc = zero16();
+#pragma unroll
+		for (int ks = 0; ks < 3; ++ks) acc = mfma(loadA(w.r0, 48, W, 32 * mt + r, 16 * ks, h), F.rinB[ks], acc);
+		F.H1[mt] = rh16(relu16(acc));
+	}
+#pragma unroll
+	for (int mt = 0; mt < MT; ++mt) {
+		f16v acc = zero16();
+#pragma unroll
+		for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.r1, W, W, 32 * mt + r, 16 * ks, h), accB(F.H1[ks >> 1], ks & 1), acc);
+		F.H2[mt] = rh16(relu16(acc));
+	}
+	{
+		f16v acc = zero16();
+#pragma unroll
+		for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.r2, W, 16, r, 16 * ks, h), accB(F.H2[ks >> 1], ks & 1), acc);
+		F.O = rh16(acc);
+	}
+}
+
+// ------------------------------------------------------------------------------------------
+// Inference / pre-compaction forward: coords AoS7 -> out AoS16 fp16 (nerf_network.h:145-328).
+// n from device memory; 32 samples per wave-iteration, grid-strided.
+// ------------------------------------------------------------------------------------------
+template <int L, int W>
+__global__ void __launch_bounds__(256) k_mlp_forward(const uint32_t* __restrict__ n_ptr, uint32_t n_fixed, uint32_t ld,
+                                                     const float* __restrict__ coords, const half_t* __restrict__ enc_h,
+                                                     const float* __restrict__ dydx, MlpPtrs w, half_t* __restrict__ out) {
+	const uint32_t n = n_ptr ? *n_ptr : n_fixed;
+	const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+	const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+	const uint32_t n_waves = (gridDim.x * blockDim.x) >> 6;
+	const float var = (float)w.var[0];
+	const half_t bias_h = (half_t)w.sdf_bias;
+	for (uint32_t base = wave * 32; base < n; base += n_waves * 32) {
+		const uint32_t i = base + r;
+		const bool valid = i < n;
+		const uint32_t ic = valid ? i : 0;
+		const float* c = coords + (size_t)ic * COORD_W;
+		const float x[3] = {c[0], c[1], c[2]}, wd[3] = {c[4], c[5], c[6]};
+		Fwd<L, W> F;
+		forward_chunk<L, W>(F, w, x, wd, enc_h, dydx, ld, ic, valid, r, h);
+		const float row11 = __shfl_xor(F.O[7], 32);  // lane h=0 holds row 11 in reg 7
+		if (valid) {
+			h8 o;
+			if (h == 0) {
+				o[0] = (half_t)F.O[0]; o[1] = (half_t)F.O[1]; o[2] = (half_t)F.O[2];
+				o[3] = (half_t)F.D1[0] + bias_h;                     // half add (common_operation.cuh:964)
+				o[4] = (half_t)F.grad[0]; o[5] = (half_t)F.grad[1]; o[6] = (half_t)F.grad[2];
+				o[7] = (half_t)var;
+			} else {
+				o[0] = (half_t)wd[0]; o[1] = (half_t)wd[1]; o[2] = (half_t)wd[2];
+				o[3] = (half_t)row11;
+				o[4] = (half_t)F.O[4]; o[5] = (half_t)F.O[5]; o[6] = (half_t)F.O[6]; o[7] = (half_t)F.O[7];
+			}
+			*(h8*)(out + (size_t)i * OUT_W + 8 * h) = o;
+		}
+	}
+}
+
+// Density-only inference for the occupancy grid (NerfNetwork::density, nerf_network.h:656-739;
+// sdf_to_density_variance_buffer, common_operation.cuh:306-324 in fp16 arithmetic).
+template <int L, int W>
+__global__ void __launch_bounds__(256) k_mlp_density(uint32_t n, uint32_t ld, const float* __restrict__ pos,
+                                                     const half_t* __restrict__ enc_h, MlpPtrs w, float* __restrict__ density) {
+	constexpr int DIN = Dims<L>::DIN, DKS = Dims<L>::DKS, MT = (W + 31) / 32, HKS = W / 16;
+	const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+	const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+	const uint32_t n_waves = (gridDim.x * blockDim.x) >> 6;
+	const half_t var_h = w.var[0];
+	const half_t bias_h = (half_t)w.sdf_bias;
+	for (uint32_t base = wave * 32; base < n; base += n_waves * 32) {
+		const uint32_t i = base + r;
+		const bool valid = i < n;
+		const uint32_t ic = valid ? i : 0;
+		const float x[3] = {pos[3 * (size_t)ic], pos[3 * (size_t)ic + 1], pos[3 * (size_t)ic + 2]};
+		h8 dinB[DKS];
+		build_din<L>(dinB, x, enc_h, ld, ic, h);
+		f16v H0[MT];
+#pragma unroll
+		for (int mt = 0; mt < MT; ++mt) {
+			f16v acc = zero16();
+#pragma unroll
+			for (int ks = 0; ks < DKS; ++ks) acc = mfma(loadA(w.d0, DIN, W, 32 * mt + r, 16 * ks, h), dinB[ks], acc);
+			H0[mt] = rh16(relu16(acc));
+		}
+		f16v acc = zero16();
+#pragma unroll
+		for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.d1, W, 16, r, 16 * ks, h), accB(H0[ks >> 1], ks & 1), acc);
+		if (valid && h == 0) {
+			const half_t sdf = (half_t)acc[0] + bias_h;
+			const half_t s = (half_t)__expf((float)(var_h * (half_t)10.0f));
+			const half_t sig = (half_t)(1.0f / (1.0f + __expf(-(float)(sdf * s))));
+			const half_t dens = (s * sig) * ((half_t)1.0f - sig);
+			density[i] = (float)dens;
+		}
+	}
+}
+
+// ------------------------------------------------------------------------------------------
+// Training forward-recompute + first- and second-order backward for 32 compacted samples per
+// wave. Writes the weight-gradient GEMM operands (SoA fp16), the grid-scatter operands
+// (dL/denc, dSDF/denc as [2L][ld] fp16, v as float4) and the variance-gradient partial sum.
+// ------------------------------------------------------------------------------------------
+// store an accumulator tile (rows 32*mt + acc_row) into SoA [rows][ldc] at column col, rows < R
+__device__ __forceinline__ void store_acc(half_t* buf, size_t ldc, uint32_t col, const f16v& a, int mt, int R, int h) {
+#pragma unroll
+	for (int reg = 0; reg < 16; ++reg) {
+		const int row = 32 * mt + acc_row(reg, h);
+		if (row < R) buf[(size_t)row * ldc + col] = (half_t)a[reg];
+	}
+}
+// store a B fragment (k-step ks, pi order) into SoA rows 16ks + pi
+__device__ __forceinline__ void store_frag(half_t* buf, size_t ldc, uint32_t col, const h8& b, int ks, int R, int h) {
+#pragma unroll
+	for (int j = 0; j < 8; ++j) {
+		const int row = 16 * ks + (h ? pi_row(j, 1) : pi_row(j, 0));
+		if (row < R) buf[(size_t)row * ldc + col] = b[j];
+	}
+}
+
+template <int L, int W>
+__global__ void __launch_bounds__(256) k_mlp_train(const uint32_t* __restrict__ n_valid_ptr, uint32_t n, uint32_t ld,
+                                                   const float* __restrict__ coords, const half_t* __restrict__ enc_h,
+                                                   const float* __restrict__ dydx, const half_t* __restrict__ dL_dout,
+                                                   MlpPtrs w, TrainBufs tb) {
+	constexpr int DIN = Dims<L>::DIN, DKS = Dims<L>::DKS, DMT = Dims<L>::DMT;
+	constexpr int MT = Fwd<L, W>::MT, HKS = Fwd<L, W>::HKS;
+	if (n_valid_ptr && *n_valid_ptr == 0) return;  // zero compacted samples: nothing to train on
+	const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+	const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+	const uint32_t n_waves = (gridDim.x * blockDim.x) >> 6;
+	const size_t ld2 = 2 * (size_t)ld;
+	float var_part = 0.f;
+	for (uint32_t base = wave * 32; base < n; base += n_waves * 32) {
+		const uint32_t i = base + r;
+		const bool valid = i < n;
+		const uint32_t ic = valid ? i : 0;
+		const float* c = coords + (size_t)ic * COORD_W;
+		const float x[3] = {c[0], c[1], c[2]}, wd[3] = {c[4], c[5], c[6]};
+		Fwd<L, W> F;
+		forward_chunk<L, W>(F, w, x, wd, enc_h, dydx, ld, ic, valid, r, h);
+		const h8 dlo = *(const h8*)(dL_dout + (size_t)ic * OUT_W + 8 * h);   // h=0: rows 0..7, h=1: rows 8..15
+		const h8 dlo_o = shfl_xor_h8(dlo, 32);
+		const h8 dlo_lo = h ? dlo_o : dlo;   // rows 0..7 on every lane
+		const h8 dlo_hi = h ? dlo : dlo_o;   // rows 8..15 on every lane
+		if (valid && h == 0) var_part += (float)dlo_lo[7];
+		// delta_o (rows 0..2 = dL/drgb): B fragment, pi order -> lane h=0 elements 0..2
+		h8 dOB = (h8){0, 0, 0, 0, 0, 0, 0, 0};
+		if (h == 0) { dOB[0] = dlo_lo[0]; dOB[1] = dlo_lo[1]; dOB[2] = dlo_lo[2]; }
+		// rgb backward
+		f16v dH2[MT], dH1[MT];
+#pragma unroll
+		for (int mt = 0; mt < MT; ++mt) {
+			f16v acc = mfma(loadA(w.r2T, 16, W, 32 * mt + r, 0, h), dOB, zero16());
+#pragma unroll
+			for (int q = 0; q < 16; ++q) acc[q] = F.H2[mt][q] > 0.f ? rh(acc[q]) : 0.f;
+			dH2[mt] = acc;
+		}
+#pragma unroll
+		for (int mt = 0; mt < MT; ++mt) {
+			f16v acc = zero16();
+#pragma unroll
+			for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.r1T, W, W, 32 * mt + r, 16 * ks, h), accB(dH2[ks >> 1], ks & 1), acc);
+#pragma unroll
+			for (int q = 0; q < 16; ++q) acc[q] = F.H1[mt][q] > 0.f ? rh(acc[q]) : 0.f;
+			dH1[mt] = acc;
+		}
+		f16v dRin[2];
+#pragma unroll
+		for (int mt = 0; mt < 2; ++mt) {
+			f16v acc = zero16();
+#pragma unroll
+			for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.r0T, W, 48, 32 * mt + r, 16 * ks, h), accB(dH1[ks >> 1], ks & 1), acc);
+			dRin[mt] = rh16(acc);
+		}
+		// density backward: delta_D1 = dL/drgb_in[0:16], row 0 += dL_dout[3] (half add)
+		f16v dD1 = dRin[0];
+		if (h == 0) dD1[0] = (float)((half_t)dD1[0] + dlo_lo[3]);
+		const h8 dD1B = accB(dD1, 0);
+		f16v dH0[MT];
+#pragma unroll
+		for (int mt = 0; mt < MT; ++mt) {
+			f16v acc = mfma(loadA(w.d1T, 16, W, 32 * mt + r, 0, h), dD1B, zero16());
+#pragma unroll
+			for (int q = 0; q < 16; ++q) acc[q] = F.H0[mt][q] > 0.f ? rh(acc[q]) : 0.f;
+			dH0[mt] = acc;
+		}
+		f16v dDin[DMT];
+#pragma unroll
+		for (int mt = 0; mt < DMT; ++mt) {
+			f16v acc = zero16();
+#pragma unroll
+			for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.d0T, W, DIN, 32 * mt + r, 16 * ks, h), accB(dH0[ks >> 1], ks & 1), acc);
+			dDin[mt] = rh16(acc);
+		}
+		// v = dL/d(grad sdf) (nerf_network.h:478-504): rows 35..37 of dL/drgb_in live at
+		// tile 1: row 3 on h=0 reg 3, rows 4,5 on h=1 regs 0,1
+		const float o3 = __shfl_xor(dRin[1][3], 32), o0 = __shfl_xor(dRin[1][0], 32), o1 = __shfl_xor(dRin[1][1], 32);
+		float v[3];
+		v[0] = h ? o3 : dRin[1][3];
+		v[1] = h ? dRin[1][0] : o0;
+		v[2] = h ? dRin[1][1] : o1;
+		v[0] += (float)dlo_lo[4] / tb.indeed_batch; v[1] += (float)dlo_lo[5] / tb.indeed_batch; v[2] += (float)dlo_lo[6] / tb.indeed_batch;
+		v[0] += (float)dlo_hi[0]; v[1] += (float)dlo_hi[1]; v[2] += (float)dlo_hi[2];
+		// u = [v, dy/dx . v, 0] (grid.h:1182-1207), B fragments in pi order
+		h8 uB[DKS];
+#pragma unroll
+		for (int ks = 0; ks < DKS; ++ks)
+#pragma unroll
+			for (int j = 0; j < 8; ++j) {
+				const int k = 16 * ks + (h ? pi_row(j, 1) : pi_row(j, 0));
+				float val = 0.f;
+				if (k < 3) val = v[k];
+				else if (k < 3 + 2 * L) {
+					const float* dp = dydx + (size_t)(3 * (k - 3)) * ld + ic;
+					val = dp[0] * v[0] + dp[ld] * v[1] + dp[2 * (size_t)ld] * v[2];
+				}
+				uB[ks][j] = (half_t)val;
+			}
+		// h1' = relu'(H0) . (W0d u)
+		f16v H1p[MT];
+#pragma unroll
+		for (int mt = 0; mt < MT; ++mt) {
+			f16v acc = zero16();
+#pragma unroll
+			for (int ks = 0; ks < DKS; ++ks) acc = mfma(loadA(w.d0, DIN, W, 32 * mt + r, 16 * ks, h), uB[ks], acc);
+#pragma unroll
+			for (int q = 0; q < 16; ++q) acc[q] = F.H0[mt][q] > 0.f ? rh(acc[q]) : 0.f;
+			H1p[mt] = acc;
+		}
+		if (valid) {
+			// ---- weight-gradient operands
+#pragma unroll
+			for (int mt = 0; mt < MT; ++mt) {
+				store_acc(tb.d0_delta, ld2, i, dH0[mt], mt, W, h);
+				store_acc(tb.d1_x, ld2, i, F.H0[mt], mt, W, h);
+				store_acc(tb.d1_x, ld2, ld + i, H1p[mt], mt, W, h);
+				store_acc(tb.r0_delta, ld, i, dH1[mt], mt, W, h);
+				store_acc(tb.r1_delta, ld, i, dH2[mt], mt, W, h);
+				store_acc(tb.r1_x, ld, i, F.H1[mt], mt, W, h);
+				store_acc(tb.r2_x, ld, i, F.H2[mt], mt, W, h);
+			}
+#pragma unroll
+			for (int ks = 0; ks < HKS; ++ks) store_frag(tb.d0_delta, ld2, ld + i, F.GhB[ks], ks, W, h);
+#pragma unroll
+			for (int ks = 0; ks < DKS; ++ks) {
+				store_frag(tb.d0_x, ld2, i, F.dinB[ks], ks, DIN, h);
+				store_frag(tb.d0_x, ld2, ld + i, uB[ks], ks, DIN, h);
+			}
+			store_acc(tb.d1_delta, ld2, i, dD1, 0, 16, h);
+			{
+				h8 e0 = (h8){0, 0, 0, 0, 0, 0, 0, 0};
+				if (h == 0) e0[0] = (half_t)1.0f;
+				store_frag(tb.d1_delta, ld2, ld + i, e0, 0, 16, h);
+			}
+#pragma unroll
+			for (int ks = 0; ks < 3; ++ks) store_frag(tb.r0_x, ld, i, F.rinB[ks], ks, 48, h);
+			store_frag(tb.r2_delta, ld, i, dOB, 0, 16, h);
+			// ---- grid-scatter operands: dL/denc = dDin rows 3.., g = G_in rows 3..
+#pragma unroll
+			for (int mt = 0; mt < DMT; ++mt)
+#pragma unroll
+				for (int reg = 0; reg < 16; ++reg) {
+					const int k = 32 * mt + acc_row(reg, h);
+					if (k >= 3 && k < 3 + 2 * L) {
+						const size_t e = ((size_t)((k - 3) >> 1) * ld + i) * 2 + ((k - 3) & 1);  // [L][ld] half2
+						tb.dLdenc[e] = (half_t)dDin[mt][reg];
+						tb.genc[e] = (half_t)F.Gi[mt][reg];
+					}
+				}
+			if (h == 0) tb.v[i] = make_float4(v[0], v[1], v[2], 0.f);
+		}
+	}
+	// variance gradient: batch sum of dL/dout[7] (nerf_network.h:461-474)
+#pragma unroll
+	for (int off = 32; off > 0; off >>= 1) var_part += __shfl_xor(var_part, off);
+	if (lane == 0 && var_part != 0.f) __hip_atomic_fetch_add(tb.var_grad, var_part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ------------------------------------------------------------------------------------------
+// Weight gradients: dW[M][K] += sum_n D[M][n] X[K][n] over the batch (split-K over samples),
+// MFMA with natural k order (k = sample), fp32 accumulation, one atomic flush per block.
+// ------------------------------------------------------------------------------------------
+
+__global__ void __launch_bounds__(256) k_wgrad(WGradJobs jobs) {
+	__shared__ float red[4][32 * 32];
+	if (jobs.n_valid && *jobs.n_valid == 0) return;
+	uint32_t b = blockIdx.x, ji = 0;
+	while (ji + 1 < jobs.n_jobs && b >= jobs.block_start[ji + 1]) ++ji;
+	const WGradJob J = jobs.j[ji];
+	b -= jobs.block_start[ji];
+	const uint32_t tiles = J.tiles_m * J.tiles_k;
+	const uint32_t tile = b % tiles, sp = b / tiles;
+	const uint32_t mt = tile / J.tiles_k, kt = tile % J.tiles_k;
+	const uint32_t n0 = sp * jobs.split, n1 = min(J.ncols, n0 + jobs.split);
+	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+	const uint32_t row_m = 32 * mt + r, row_k = 32 * kt + r;
+	const bool okm = row_m < J.M, okk = row_k < J.K;
+	f16v acc = zero16();
+	for (uint32_t nb = n0 + 16 * wv; nb < n1; nb += 64) {
+		h8 a = (h8){0, 0, 0, 0, 0, 0, 0, 0}, bb = a;
+		if (okm) a = *(const h8*)(J.D + (size_t)row_m * J.ldc + nb + 8 * h);
+		if (okk) bb = *(const h8*)(J.X + (size_t)row_k * J.ldc + nb + 8 * h);
+		acc = mfma(a, bb, acc);
+	}
+#pragma unroll
+	for (int reg = 0; reg < 16; ++reg) red[wv][acc_row(reg, h) * 32 + r] = acc[reg];
+	__syncthreads();
+	for (uint32_t e = threadIdx.x; e < 1024; e += 256) {
+		const float s = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
+		const uint32_t m = 32 * mt + e / 32, k = 32 * kt + e % 32;
+		if (m < J.M && k < J.K && s != 0.f) __hip_atomic_fetch_add(J.dW + (size_t)m * J.K + k, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	}
+}
+
+// MFMA fragment-layout probe (exact-integer check from tests): C = A(32x16) * B(16x32) with
+// A, B given row-major, loaded in NATURAL k order.
+__global__ void k_mfma_probe(const half_t* A, const half_t* B, float* C) {
+	const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+	h8 a, b;
+#pragma unroll
+	for (int j = 0; j < 8; ++j) { a[j] = A[r * 16 + 8 * h + j]; b[j] = B[(8 * h + j) * 32 + r]; }
+	f16v c = mfma(a, b, zero16());
+#pragma unroll
+	for (int reg = 0; reg < 16; ++reg) C[acc_row(reg, h) * 32 + r] = c[reg];
+}
+
+// Explicit instantiations used by the host (L levels, W hidden width).
+// ---------------------------------------------------------------- host launchers
+// Supported (levels, width) instantiations; the host checks mlp_supported() at reload time.
+#define NEUS_MLP_CONFIGS(X) X(1, 16) X(1, 64) X(2, 64) X(4, 64) X(8, 64) X(14, 64) X(16, 64)
+
+bool mlp_supported(uint32_t L, uint32_t W) {
+#define X(l, w) if (L == l && W == w) return true;
+	NEUS_MLP_CONFIGS(X)
+#undef X
+	return false;
+}
+
+void launch_mlp_forward(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_ptr, uint32_t n_fixed, uint32_t ld, const float* coords,
+                        const half_t* enc, const float* dydx, const MlpPtrs& w, half_t* out, uint32_t blocks) {
+#define X(l, w_) if (L == l && W == w_) { k_mlp_forward<l, w_><<<blocks, 256, 0, s>>>(n_ptr, n_fixed, ld, coords, enc, dydx, w, out); return; }
+	NEUS_MLP_CONFIGS(X)
+#undef X
+}
+void launch_mlp_density(hipStream_t s, uint32_t L, uint32_t W, uint32_t n, uint32_t ld, const float* pos, const half_t* enc,
+                        const MlpPtrs& w, float* density) {
+	const uint32_t blocks = std::min<uint32_t>((n + 127) / 128, 4096);
+	if (n == 0) return;
+#define X(l, w_) if (L == l && W == w_) { k_mlp_density<l, w_><<<blocks, 256, 0, s>>>(n, ld, pos, enc, w, density); return; }
+	NEUS_MLP_CONFIGS(X)
+#undef X
+}
+void launch_mlp_train(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_valid_ptr, uint32_t n, uint32_t ld, const float* coords,
+                      const half_t* enc, const float* dydx, const half_t* dL_dout, const MlpPtrs& w, const TrainBufs& tb) {
+	const uint32_t blocks = std::min<uint32_t>((n + 127) / 128, 2048);
+	if (n == 0) return;
+#define X(l, w_) if (L == l && W == w_) { k_mlp_train<l, w_><<<blocks, 256, 0, s>>>(n_valid_ptr, n, ld, coords, enc, dydx, dL_dout, w, tb); return; }
+	NEUS_MLP_CONFIGS(X)
+#undef X
+}
+void launch_wgrad(hipStream_t s, const WGradJobs& jobs, uint32_t n_blocks) { if (n_blocks) k_wgrad<<<n_blocks, 256, 0, s>>>(jobs); }
+void launch_mfma_probe(hipStream_t s, const half_t* A, const half_t* B, float* C) { k_mfma_probe<<<1, 64, 0, s>>>(A, B, C); }
+
+} // namespace neus

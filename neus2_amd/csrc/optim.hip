@@ -1,0 +1,177 @@
+// Optimizer and occupancy-grid kernels for gfx950.
+//
+//   k_adam_ema       : Ema(ExponentialDecay(Adam)) step (adam.h:51-160, ema.h:45-110,
+//                      exponential_decay.h:61-80) fused with the fp16 weight cast and the EMA
+//                      (inference-weight) update: one streaming pass over the P parameters.
+//   k_transpose_w    : fp16 transposed copies of the MLP matrices for the MFMA backward.
+//   k_grid_samples   : generate_grid_samples_nerf_nonuniform (testbed_nerf.cu:640-669)
+//   k_splat_max      : splat_grid_samples_nerf_max_nearest_neighbor (testbed_nerf.cu:671-690)
+//   k_ema_grid       : ema_grid_samples_nerf (testbed_nerf.cu:710-740)
+//   k_grid_mean_*    : deterministic two-stage mean (testbed_nerf.cu:3384-3389)
+//   k_bitfield       : grid_to_bitfield + bitfield_max_pool (testbed_nerf.cu:748-795)
+#include "kernels.h"
+#include <algorithm>
+
+namespace neus {
+
+// grads fp32 (the reference keeps fp16 gradients); weights_fp fp32 master; weights_h fp16 copy
+// used by every kernel; ema_tmp fp32 running EMA; ema_h fp16 inference weights.
+__global__ void __launch_bounds__(256) k_adam_ema(AdamParams p, float* __restrict__ weights_fp, half_t* __restrict__ weights_h,
+                                                  const float* __restrict__ grads, float* __restrict__ m1, float* __restrict__ m2,
+                                                  uint32_t* __restrict__ steps, float* __restrict__ ema_tmp, half_t* __restrict__ ema_h) {
+	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < p.n; i += gridDim.x * blockDim.x) {
+		float gradient = grads[i] / p.loss_scale;
+		const bool is_matrix = i < p.n_matrix;
+		bool skip = is_matrix ? !p.optimize_matrix : (!p.optimize_non_matrix || gradient == 0.f);
+		float w = weights_fp[i];
+		if (!skip) {
+			if (is_matrix) gradient += p.l2_reg * w;
+			const float g2 = gradient * gradient;
+			const float fm = p.beta1 * m1[i] + (1 - p.beta1) * gradient;
+			const float sm = p.beta2 * m2[i] + (1 - p.beta2) * g2;
+			m1[i] = fm; m2[i] = sm;
+			const uint32_t cs = steps[i] + 1;
+			steps[i] = cs;
+			const float lr = p.lr * sqrtf(1 - powf(p.beta2, (float)cs)) / (1 - powf(p.beta1, (float)cs));
+			const float elr = fminf(fmaxf(lr / (sqrtf(sm) + p.eps), 0.0f), 3.402823466e+38f);
+			w = w - elr * fm;
+			weights_fp[i] = w;
+			weights_h[i] = (half_t)w;
+		}
+		const float wh = (float)weights_h[i];
+		const float f = (ema_tmp[i] * p.ema_decay * p.ema_debias_old + wh * (1 - p.ema_decay)) * p.ema_debias_new;
+		ema_tmp[i] = f;
+		ema_h[i] = (half_t)f;
+	}
+}
+
+__global__ void k_cast_half(uint32_t n, const float* __restrict__ in, half_t* __restrict__ out) {
+	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) out[i] = (half_t)in[i];
+}
+
+// dst[c][r] = src[r][c]  (all matrices are <= 64x64)
+__global__ void k_transpose_w(TransposeJobs jobs) {
+	const TransposeJob J = jobs.j[blockIdx.x];
+	for (uint32_t e = threadIdx.x; e < J.rows * J.cols; e += blockDim.x) {
+		const uint32_t r = e / J.cols, c = e % J.cols;
+		J.dst[(size_t)c * J.rows + r] = J.src[e];
+	}
+}
+
+// positions: 3 floats (warped) per sample; indices: density grid cell.
+__global__ void k_grid_samples(uint32_t n_elements, uint32_t out_offset, uint64_t rng_state, uint64_t rng_inc, uint32_t step,
+                               float aabb_min_x, float aabb_min_y, float aabb_min_z, float diag_x, float diag_y, float diag_z,
+                               const float* __restrict__ grid_in, float* __restrict__ pos, uint32_t* __restrict__ indices,
+                               uint32_t n_cascades, float thresh) {
+	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_elements; i += gridDim.x * blockDim.x) {
+		pcg32 rng(rng_state, rng_inc);
+		rng.advance((int64_t)(uint32_t)(i * 4));
+		const uint32_t level = (uint32_t)(rng.next_float() * n_cascades) % n_cascades;
+		uint32_t idx = 0;
+		for (uint32_t j = 0; j < 10; ++j) {
+			idx = ((i + step * n_elements) * 56924617u + j * 19349663u + 96925573u) % GRID3;
+			idx += level * GRID3;
+			if (grid_in[idx] > thresh) break;
+		}
+		const uint32_t pi = idx % GRID3;
+		const uint32_t x = morton3D_invert(pi >> 0), y = morton3D_invert(pi >> 1), z = morton3D_invert(pi >> 2);
+		const float rx = rng.next_float(), ry = rng.next_float(), rz = rng.next_float();
+		const float sc = scalbnf(1.0f, (int)level);
+		const float px = (((float)x + rx) / NERF_GRIDSIZE - 0.5f) * sc + 0.5f;
+		const float py = (((float)y + ry) / NERF_GRIDSIZE - 0.5f) * sc + 0.5f;
+		const float pz = (((float)z + rz) / NERF_GRIDSIZE - 0.5f) * sc + 0.5f;
+		const uint32_t o = out_offset + i;
+		pos[3 * (size_t)o + 0] = (px - aabb_min_x) / diag_x;
+		pos[3 * (size_t)o + 1] = (py - aabb_min_y) / diag_y;
+		pos[3 * (size_t)o + 2] = (pz - aabb_min_z) / diag_z;
+		indices[o] = idx;
+	}
+}
+
+__global__ void k_splat_max(uint32_t n, const uint32_t* __restrict__ indices, const float* __restrict__ density, float* __restrict__ grid_tmp) {
+	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+		atomicMax((uint32_t*)&grid_tmp[indices[i]], __float_as_uint(density[i]));
+}
+
+__global__ void k_ema_grid(uint32_t n, float decay, float* __restrict__ grid, const float* __restrict__ tmp) {
+	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+		const float prev = grid[i];
+		grid[i] = (prev < 0.f) ? prev : fmaxf(prev * decay, tmp[i]);
+	}
+}
+
+// Deterministic mean of max(grid,0)/G3: fixed-shape two-stage tree (fp32 partials of 1024 each).
+__global__ void __launch_bounds__(256) k_grid_mean_partial(const float* __restrict__ grid, float* __restrict__ partial) {
+	__shared__ float s[256];
+	const uint32_t b = blockIdx.x;  // GRID3 / 1024 blocks
+	float acc = 0.f;
+	for (int k = 0; k < 4; ++k) acc += fmaxf(grid[b * 1024 + k * 256 + threadIdx.x], 0.f) / (float)GRID3;
+	s[threadIdx.x] = acc;
+	__syncthreads();
+	for (int off = 128; off > 0; off >>= 1) { if (threadIdx.x < off) s[threadIdx.x] += s[threadIdx.x + off]; __syncthreads(); }
+	if (threadIdx.x == 0) partial[b] = s[0];
+}
+__global__ void __launch_bounds__(256) k_grid_mean_final(const float* __restrict__ partial, uint32_t n_partial, float* __restrict__ mean) {
+	__shared__ float s[256];
+	float acc = 0.f;
+	for (uint32_t k = threadIdx.x; k < n_partial; k += 256) acc += partial[k];
+	s[threadIdx.x] = acc;
+	__syncthreads();
+	for (int off = 128; off > 0; off >>= 1) { if (threadIdx.x < off) s[threadIdx.x] += s[threadIdx.x + off]; __syncthreads(); }
+	if (threadIdx.x == 0) *mean = s[0];
+}
+
+__global__ void k_grid_to_bitfield(uint32_t n_bytes_total, uint32_t n_nonzero, const float* __restrict__ grid, uint8_t* __restrict__ bf,
+                                   const float* __restrict__ mean) {
+	const float thresh = fminf(NERF_MIN_OPTICAL_THICKNESS, *mean);
+	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_bytes_total; i += gridDim.x * blockDim.x) {
+		if (i >= n_nonzero) { bf[i] = 0; continue; }
+		uint8_t bits = 0;
+#pragma unroll
+		for (uint8_t j = 0; j < 8; ++j) bits |= grid[i * 8 + j] > thresh ? ((uint8_t)1 << j) : 0;
+		bf[i] = bits;
+	}
+}
+__global__ void k_bitfield_max_pool(uint32_t n, const uint8_t* __restrict__ prev, uint8_t* __restrict__ next) {
+	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+		uint8_t bits = 0;
+#pragma unroll
+		for (uint8_t j = 0; j < 8; ++j) bits |= prev[i * 8 + j] > 0 ? ((uint8_t)1 << j) : 0;
+		const uint32_t x = morton3D_invert(i >> 0) + NERF_GRIDSIZE / 8, y = morton3D_invert(i >> 1) + NERF_GRIDSIZE / 8, z = morton3D_invert(i >> 2) + NERF_GRIDSIZE / 8;
+		// each destination byte is written by exactly one source thread of this level
+		next[morton3D(x, y, z)] |= bits;
+	}
+}
+
+// ---------------------------------------------------------------- host launchers
+static inline uint32_t nblk(uint64_t n, uint32_t cap = 4096) { return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, cap)); }
+void launch_adam_ema(hipStream_t s, const AdamParams& p, float* weights_fp, half_t* weights_h, const float* grads, float* m1, float* m2,
+                     uint32_t* steps, float* ema_tmp, half_t* ema_h) {
+	k_adam_ema<<<nblk(p.n, 8192), 256, 0, s>>>(p, weights_fp, weights_h, grads, m1, m2, steps, ema_tmp, ema_h);
+}
+void launch_cast_half(hipStream_t s, uint32_t n, const float* in, half_t* out) { k_cast_half<<<nblk(n), 256, 0, s>>>(n, in, out); }
+void launch_transpose_w(hipStream_t s, const TransposeJobs& jobs) { if (jobs.n) k_transpose_w<<<jobs.n, 256, 0, s>>>(jobs); }
+void launch_grid_samples(hipStream_t s, uint32_t n, uint32_t out_offset, uint64_t rng_state, uint64_t rng_inc, uint32_t step,
+                         const float* aabb_min, const float* aabb_max, const float* grid_in, float* pos, uint32_t* indices,
+                         uint32_t n_cascades, float thresh) {
+	if (!n) return;
+	k_grid_samples<<<nblk(n), 256, 0, s>>>(n, out_offset, rng_state, rng_inc, step, aabb_min[0], aabb_min[1], aabb_min[2],
+	                                        aabb_max[0] - aabb_min[0], aabb_max[1] - aabb_min[1], aabb_max[2] - aabb_min[2],
+	                                        grid_in, pos, indices, n_cascades, thresh);
+}
+void launch_splat_max(hipStream_t s, uint32_t n, const uint32_t* indices, const float* density, float* grid_tmp) {
+	if (n) k_splat_max<<<nblk(n), 256, 0, s>>>(n, indices, density, grid_tmp);
+}
+void launch_ema_grid(hipStream_t s, uint32_t n, float decay, float* grid, const float* tmp) { k_ema_grid<<<nblk(n), 256, 0, s>>>(n, decay, grid, tmp); }
+void launch_grid_mean(hipStream_t s, const float* grid, float* partial, float* mean) {
+	k_grid_mean_partial<<<GRID3 / 1024, 256, 0, s>>>(grid, partial);
+	k_grid_mean_final<<<1, 256, 0, s>>>(partial, GRID3 / 1024, mean);
+}
+void launch_bitfield(hipStream_t s, const float* grid, uint8_t* bitfield, const float* mean, uint32_t n_cascades) {
+	const uint32_t nbytes = GRID3 / 8;
+	k_grid_to_bitfield<<<nblk(nbytes * NERF_CASCADES), 256, 0, s>>>(nbytes * NERF_CASCADES, nbytes * n_cascades, grid, bitfield, mean);
+	for (uint32_t level = 1; level < NERF_CASCADES; ++level)
+		k_bitfield_max_pool<<<nblk(GRID3 / 64), 256, 0, s>>>(GRID3 / 64, bitfield + nbytes * (level - 1), bitfield + nbytes * level);
+}
+
+} // namespace neus

@@ -1,0 +1,739 @@
+// Host orchestration of the NeuS2 training hot path on gfx950 and its C-ABI (include/neus2_hip.h).
+//
+// NeusTestbed restates the training-relevant part of the reference Testbed
+// (include/neural-graphics-primitives/testbed.h:63-940; src/testbed.cu:2084-2349, 2640-2736;
+// src/testbed_nerf.cu:3293-3548, 3723-4016) MI355X-first:
+//   * one HIP stream per testbed, every counter device-resident (no host sync inside a step);
+//   * deterministic count -> scan -> write compaction instead of atomic appends;
+//   * fp32 gradients and master weights, fp16 weights for the kernels (the reference keeps fp16
+//     gradients), RCCL all-reduce of the gradient buffer for data parallelism over ray batches.
+#include "kernels.h"
+#include "../../include/neus2_hip.h"
+
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <random>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+using namespace neus;
+
+namespace {
+
+thread_local std::string g_err;
+
+#define HIP_CHECK(x)                                                                                   \
+	do {                                                                                               \
+		hipError_t e_ = (x);                                                                           \
+		if (e_ != hipSuccess) throw std::runtime_error(std::string(#x) + " failed: " + hipGetErrorString(e_)); \
+	} while (0)
+#define NCCL_CHECK(x)                                                                                  \
+	do {                                                                                               \
+		ncclResult_t r_ = (x);                                                                         \
+		if (r_ != ncclSuccess) throw std::runtime_error(std::string(#x) + " failed: " + ncclGetErrorString(r_)); \
+	} while (0)
+
+template <class T> struct Dev {
+	T* p = nullptr;
+	size_t n = 0;
+	void alloc(size_t k) {
+		if (k <= n && p) return;
+		release();
+		if (k == 0) return;
+		HIP_CHECK(hipMalloc((void**)&p, k * sizeof(T)));
+		n = k;
+	}
+	void release() { if (p) (void)hipFree(p); p = nullptr; n = 0; }
+	~Dev() { release(); }
+};
+
+constexpr uint32_t MAX_RAYS = 1u << 18;  // testbed_nerf.cu:3435 cap on rays_per_batch
+constexpr float LOSS_SCALE = 128.f;      // testbed.h:246
+
+uint32_t next_multiple(uint32_t v, uint32_t m) { return (v + m - 1) / m * m; }
+
+struct Layout {
+	uint32_t din, W, L;
+	uint32_t off_d0, off_d1, off_r0, off_r1, off_r2, n_density, n_rgb, n_matrix, grid_off, n_grid, var_off, P;
+};
+
+} // namespace
+
+struct NeusTestbed {
+	int device = 0;
+	hipStream_t stream = nullptr;
+	NeusNetworkConfig cfg{};
+	bool have_net = false, have_data = false;
+	Layout lay{};
+	GridLevels gl{};
+	// dataset
+	Dev<uint32_t> pixels; Dev<uint64_t> pix_off; Dev<int32_t> res; Dev<float> focal, pp, xform;
+	DevDataset ds{};
+	uint32_t max_cascade = 0;
+	float aabb_scale = 1.f;
+	// parameters
+	Dev<float> params_fp, grads, m1, m2, ema_tmp;
+	Dev<uint32_t> adam_steps;
+	Dev<half_t> params_h, ema_h, wT;
+	MlpPtrs mlp{};
+	// occupancy grid
+	Dev<float> density_grid, density_tmp, grid_mean, grid_partial, occ_pos, occ_density;
+	Dev<uint32_t> occ_idx;
+	Dev<uint8_t> bitfield;
+	uint32_t density_grid_ema_step = 0;
+	// step workspace
+	uint32_t batch = 0, max_samples = 0;
+	Dev<float> rays, startt, coords, coords_c, loss, ek, mask, loss_sum;
+	Dev<uint32_t> nreq, base, numsteps, ccount, cbase, enc;
+	Dev<float> dydx;
+	Dev<half_t> net_out, dL_dout, trainbuf;
+	Dev<float4> vbuf;
+	Dev<uint8_t> scan_tmp;
+	size_t scan_tmp_bytes = 0;
+	Dev<StepState> st;
+	TrainBufs tbuf{};
+	// RNG + counters (testbed.cu:2087-2101)
+	pcg32 rng, density_grid_rng;
+	uint32_t training_step = 0;
+	uint32_t adam_step = 0;
+	float lr_factor = 1.f;
+	// stats
+	float loss_scalar_ema = 0.f, last_loss = 0.f, ek_loss = 0.f, mask_loss = 0.f;
+	bool loss_ema_init = false;
+	float* pinned = nullptr;  // [0..3]: loss sum, ek sum, mask sum, grid mean ; [4..]: StepState copy
+	bool loss_pending = false;
+	// data parallel
+	ncclComm_t comm = nullptr;
+	uint32_t rank = 0, world = 1;
+	// profiling
+	bool profiling = false;
+	static constexpr int N_PHASES = 8;
+	hipEvent_t ev[N_PHASES + 1] = {};
+	double phase_ms[N_PHASES] = {};
+	uint32_t phase_steps = 0;
+
+	NeusTestbed(int dev) : device(dev) {
+		HIP_CHECK(hipSetDevice(device));
+		HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+		HIP_CHECK(hipHostMalloc((void**)&pinned, 64 * sizeof(float)));
+		for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
+		st.alloc(1);
+		HIP_CHECK(hipMemset(st.p, 0, sizeof(StepState)));
+	}
+	~NeusTestbed() {
+		if (stream) (void)hipStreamSynchronize(stream);
+		if (comm) ncclCommDestroy(comm);
+		for (auto& e : ev) if (e) (void)hipEventDestroy(e);
+		if (pinned) (void)hipHostFree(pinned);
+		if (stream) (void)hipStreamDestroy(stream);
+	}
+
+	// ------------------------------------------------------------ dataset (load_nerf, testbed_nerf.cu:2964-3095)
+	void set_dataset(uint32_t n_images, const NeusImage* imgs, float aabb_scale_) {
+		if (n_images == 0) throw std::runtime_error("set_dataset: no images");
+		aabb_scale = aabb_scale_;
+		const int s = (int)aabb_scale;
+		if (s < 1 || (s & (s - 1)) != 0) throw std::runtime_error("NeRF dataset's `aabb_scale` must be a power of two");
+		if (s > (1 << (NERF_CASCADES - 1))) throw std::runtime_error("NeRF dataset must have aabb_scale <= 128");
+		std::vector<uint64_t> offs(n_images);
+		std::vector<int32_t> r(2 * n_images);
+		std::vector<float> f(2 * n_images), p(2 * n_images), x(12 * n_images);
+		uint64_t total = 0;
+		for (uint32_t i = 0; i < n_images; ++i) {
+			offs[i] = total;
+			total += (uint64_t)imgs[i].width * imgs[i].height;
+			r[2 * i] = imgs[i].width; r[2 * i + 1] = imgs[i].height;
+			f[2 * i] = imgs[i].focal[0]; f[2 * i + 1] = imgs[i].focal[1];
+			p[2 * i] = imgs[i].principal[0]; p[2 * i + 1] = imgs[i].principal[1];
+			std::memcpy(&x[12 * i], imgs[i].xform, 12 * sizeof(float));
+		}
+		pixels.alloc(total); pix_off.alloc(n_images); res.alloc(2 * n_images); focal.alloc(2 * n_images); pp.alloc(2 * n_images); xform.alloc(12 * n_images);
+		for (uint32_t i = 0; i < n_images; ++i)
+			HIP_CHECK(hipMemcpy(pixels.p + offs[i], imgs[i].rgba8, (size_t)imgs[i].width * imgs[i].height * 4, hipMemcpyHostToDevice));
+		HIP_CHECK(hipMemcpy(pix_off.p, offs.data(), n_images * 8, hipMemcpyHostToDevice));
+		HIP_CHECK(hipMemcpy(res.p, r.data(), r.size() * 4, hipMemcpyHostToDevice));
+		HIP_CHECK(hipMemcpy(focal.p, f.data(), f.size() * 4, hipMemcpyHostToDevice));
+		HIP_CHECK(hipMemcpy(pp.p, p.data(), p.size() * 4, hipMemcpyHostToDevice));
+		HIP_CHECK(hipMemcpy(xform.p, x.data(), x.size() * 4, hipMemcpyHostToDevice));
+		ds.pixels = pixels.p; ds.pix_off = pix_off.p; ds.res = res.p; ds.focal = focal.p; ds.pp = pp.p; ds.xform = xform.p;
+		ds.n_images = n_images;
+		const float infl = 0.5f * (float)std::min(1 << (NERF_CASCADES - 1), s);
+		for (int d = 0; d < 3; ++d) { ds.aabb_min[d] = 0.5f - infl; ds.aabb_max[d] = 0.5f + infl; }
+		max_cascade = 0;
+		while ((1 << max_cascade) < s) ++max_cascade;
+		ds.cone_angle = s <= 1 ? 0.0f : (1.0f / 256.0f);
+		have_data = true;
+		const uint32_t n_cells = GRID3 * (max_cascade + 1);
+		density_grid.alloc(n_cells); density_tmp.alloc(n_cells);
+		HIP_CHECK(hipMemset(density_grid.p, 0, n_cells * 4));
+		bitfield.alloc(GRID3 / 8 * NERF_CASCADES);
+		HIP_CHECK(hipMemset(bitfield.p, 0xff, GRID3 / 8 * NERF_CASCADES));
+		grid_mean.alloc(4); grid_partial.alloc(GRID3 / 1024);
+		HIP_CHECK(hipMemset(grid_mean.p, 0, 16));
+	}
+
+	// ------------------------------------------------------------ network (reset_network, testbed.cu:2084-2349)
+	void reset_network(const NeusNetworkConfig& c, const float* geo) {
+		if (!have_data) throw std::runtime_error("reload_network: load training data first");
+		if (c.n_features_per_level != 2) throw std::runtime_error("GridEncoding: only n_features_per_level = 2 is supported");
+		if (c.n_levels == 0 || c.n_levels > MAX_LEVELS) throw std::runtime_error("GridEncoding: 1..16 levels supported");
+		if (c.n_density_hidden != 1 || c.n_rgb_hidden != 2) throw std::runtime_error("NerfNetwork: density 1 hidden layer, rgb 2 hidden layers required on gfx950");
+		if (!mlp_supported(c.n_levels, c.n_neurons)) throw std::runtime_error("NerfNetwork: unsupported (n_levels, n_neurons) combination for the gfx950 MLP kernels");
+		if (c.batch_size == 0 || c.batch_size % 128 != 0) throw std::runtime_error("batch_size must be a positive multiple of 128");
+		cfg = c;
+		// per_level_scale (testbed.cu:2184-2187), grid tables (grid.h:1466-1501)
+		float pls = c.per_level_scale;
+		if (pls <= 0.f) pls = c.n_levels > 1 ? std::exp(std::log(c.top_resolution * aabb_scale / (float)c.base_resolution) / (c.n_levels - 1)) : 2.0f;
+		cfg.per_level_scale = pls;
+		gl = GridLevels{};
+		gl.n_levels = c.n_levels;
+		uint32_t offset = 0;
+		for (uint32_t i = 0; i < c.n_levels; ++i) {
+			const float scale = exp2f(i * std::log2(pls)) * c.base_resolution - 1.0f;
+			const uint32_t resolution = (uint32_t)(std::ceil(scale)) + 1;
+			const uint32_t max_params = 0xffffffffu / 2;
+			uint32_t pil = std::pow((float)resolution, 3) > (float)max_params ? max_params : resolution * resolution * resolution;
+			pil = next_multiple(pil, 8u);
+			pil = std::min(pil, 1u << c.log2_hashmap_size);
+			gl.offset[i] = offset; gl.res[i] = resolution; gl.scale[i] = (float)(resolution - 1);
+			offset += pil;
+		}
+		gl.offset[c.n_levels] = offset;
+		// parameter layout (nerf_network.h:741-785)
+		Layout& l = lay;
+		l.L = c.n_levels; l.W = c.n_neurons; l.din = next_multiple(3 + 2 * c.n_levels, 16);
+		l.off_d0 = 0; l.off_d1 = l.W * l.din; l.n_density = l.off_d1 + 16 * l.W;
+		l.off_r0 = l.n_density; l.off_r1 = l.off_r0 + l.W * 48; l.off_r2 = l.off_r1 + l.W * l.W;
+		l.n_rgb = l.off_r2 + 16 * l.W - l.n_density;
+		l.n_matrix = l.n_density + l.n_rgb;
+		l.grid_off = l.n_matrix; l.n_grid = offset * 2;
+		l.var_off = l.grid_off + l.n_grid; l.P = l.var_off + 4;
+		const uint32_t P = l.P;
+		params_fp.alloc(P); grads.alloc(P); m1.alloc(P); m2.alloc(P); ema_tmp.alloc(P); adam_steps.alloc(P);
+		params_h.alloc(P); ema_h.alloc(P);
+		wT.alloc(l.din * l.W + l.W * 16 + 48 * l.W + l.W * l.W + l.W * 16 + 64);
+		// initial parameters (trainer.h:54-109): seed_seq{seed} -> pcg32
+		std::vector<float> h(P, 0.f);
+		{
+			std::seed_seq seq{c.seed};
+			std::vector<uint32_t> seeds(2);
+			seq.generate(seeds.begin(), seeds.end());
+			pcg32 rnd = make_pcg32(seeds.front());
+			auto xavier = [&](uint32_t off, uint32_t out, uint32_t in) {
+				const float scale = std::sqrt(6.0f / (float)(in + out));
+				for (uint32_t i = 0; i < out * in; ++i) h[off + i] = rnd.next_float() * 2.0f * scale - scale;
+			};
+			xavier(l.off_d0, l.W, l.din); xavier(l.off_d1, 16, l.W);
+			if (geo) std::memcpy(h.data(), geo, sizeof(float) * l.n_density);
+			xavier(l.off_r0, l.W, 48); xavier(l.off_r1, l.W, l.W); xavier(l.off_r2, 16, l.W);
+			// grid: generate_random_uniform(rnd, n, -1e-4, 1e-4) (random.h:67-91; 128-thread blocks)
+			const size_t N = l.n_grid, per = 4, n_threads = (N + per - 1) / per, n_pad = (n_threads + 127) / 128 * 128;
+			for (size_t i = 0; i < n_pad; ++i) {
+				pcg32 r = rnd; r.advance((int64_t)(i * per));
+				for (size_t j = 0; j < per; ++j) {
+					const size_t idx = i + n_pad * j;
+					if (idx >= N) break;
+					h[l.grid_off + idx] = r.next_float() * (1e-4f - -1e-4f) + -1e-4f;
+				}
+			}
+			rnd.advance((int64_t)N);
+			for (int k = 0; k < 4; ++k) h[l.var_off + k] = 0.3f;  // nerf_network.h:881-882
+		}
+		HIP_CHECK(hipMemcpy(params_fp.p, h.data(), (size_t)P * 4, hipMemcpyHostToDevice));
+		HIP_CHECK(hipMemset(m1.p, 0, (size_t)P * 4)); HIP_CHECK(hipMemset(m2.p, 0, (size_t)P * 4));
+		HIP_CHECK(hipMemset(ema_tmp.p, 0, (size_t)P * 4)); HIP_CHECK(hipMemset(adam_steps.p, 0, (size_t)P * 4));
+		HIP_CHECK(hipMemset(ema_h.p, 0, (size_t)P * 2)); HIP_CHECK(hipMemset(grads.p, 0, (size_t)P * 4));
+		launch_cast_half(stream, P, params_fp.p, params_h.p);
+		setup_mlp_ptrs();
+		prepare_weights();
+		// RNG state (testbed.cu:2087-2101)
+		rng = make_pcg32(c.seed);
+		density_grid_rng = make_pcg32(rng.next_uint());
+		(void)rng.next_uint();  // tv_loss_rng
+		training_step = 0; adam_step = 0; lr_factor = 1.f; density_grid_ema_step = 0;
+		loss_ema_init = false; loss_scalar_ema = last_loss = ek_loss = mask_loss = 0.f; loss_pending = false;
+		// workspace
+		batch = c.batch_size;
+		max_samples = batch * 16;  // testbed_nerf.cu:3725
+		rays.alloc(6 * (size_t)MAX_RAYS); startt.alloc(MAX_RAYS); nreq.alloc(MAX_RAYS); base.alloc(MAX_RAYS);
+		numsteps.alloc(2 * (size_t)MAX_RAYS); ccount.alloc(MAX_RAYS); cbase.alloc(MAX_RAYS);
+		loss.alloc(MAX_RAYS); ek.alloc(MAX_RAYS); mask.alloc(MAX_RAYS); loss_sum.alloc(4);
+		coords.alloc((size_t)max_samples * COORD_W); net_out.alloc((size_t)max_samples * OUT_W);
+		enc.alloc((size_t)l.L * max_samples); dydx.alloc((size_t)6 * l.L * max_samples);
+		coords_c.alloc((size_t)batch * COORD_W); dL_dout.alloc((size_t)batch * OUT_W);
+		const size_t ld = batch, ld2 = 2 * ld;
+		const size_t tb_elems = (size_t)l.W * ld2 + (size_t)l.din * ld2 + 16 * ld2 + (size_t)l.W * ld2 + (size_t)l.W * ld + 48 * ld +
+		                        2 * (size_t)l.W * ld + 16 * ld + (size_t)l.W * ld + 2 * (size_t)l.L * ld * 2 + 64;
+		trainbuf.alloc(tb_elems);
+		vbuf.alloc(batch);
+		half_t* q = trainbuf.p;
+		auto take = [&](size_t k) { half_t* r = q; q += (k + 7) / 8 * 8; return r; };
+		tbuf.d0_delta = take((size_t)l.W * ld2); tbuf.d0_x = take((size_t)l.din * ld2);
+		tbuf.d1_delta = take(16 * ld2); tbuf.d1_x = take((size_t)l.W * ld2);
+		tbuf.r0_delta = take((size_t)l.W * ld); tbuf.r0_x = take(48 * ld);
+		tbuf.r1_delta = take((size_t)l.W * ld); tbuf.r1_x = take((size_t)l.W * ld);
+		tbuf.r2_delta = take(16 * ld); tbuf.r2_x = take((size_t)l.W * ld);
+		tbuf.dLdenc = take(2 * (size_t)l.L * ld); tbuf.genc = take(2 * (size_t)l.L * ld);
+		tbuf.v = vbuf.p;
+		tbuf.var_grad = grads.p + l.var_off;
+		tbuf.indeed_batch = (float)batch * (float)world;
+		scan_tmp_bytes = scan_temp_bytes(MAX_RAYS);
+		scan_tmp.alloc(scan_tmp_bytes + 256);
+		const uint32_t n_occ = GRID3 * (max_cascade + 1) * 2;
+		occ_pos.alloc(3 * (size_t)n_occ); occ_idx.alloc(n_occ); occ_density.alloc(n_occ);
+		// device step state (Counters, testbed.h:596-616)
+		StepState s{};
+		s.rays_per_batch = c.fixed_rays_per_batch ? c.fixed_rays_per_batch : (1u << 12);
+		s.max_inference = max_samples;
+		HIP_CHECK(hipMemcpy(st.p, &s, sizeof(s), hipMemcpyHostToDevice));
+		HIP_CHECK(hipMemset(density_grid.p, 0, density_grid.n * 4));
+		HIP_CHECK(hipStreamSynchronize(stream));
+		have_net = true;
+	}
+
+	void setup_mlp_ptrs() {
+		const Layout& l = lay;
+		half_t* t = wT.p;
+		mlp.d0 = params_h.p + l.off_d0; mlp.d1 = params_h.p + l.off_d1;
+		mlp.r0 = params_h.p + l.off_r0; mlp.r1 = params_h.p + l.off_r1; mlp.r2 = params_h.p + l.off_r2;
+		auto take = [&](size_t k) { half_t* r = t; t += (k + 7) / 8 * 8; return r; };
+		mlp.d0T = take(l.din * l.W); mlp.d1T = take(l.W * 16); mlp.r0T = take(48 * l.W); mlp.r1T = take(l.W * l.W); mlp.r2T = take(l.W * 16);
+		mlp.var = params_h.p + l.var_off;
+		mlp.sdf_bias = cfg.sdf_bias;
+	}
+	void prepare_weights() {
+		const Layout& l = lay;
+		TransposeJobs tj{};
+		tj.j[0] = {mlp.d0, (half_t*)mlp.d0T, l.W, l.din};
+		tj.j[1] = {mlp.d1, (half_t*)mlp.d1T, 16, l.W};
+		tj.j[2] = {mlp.r0, (half_t*)mlp.r0T, l.W, 48};
+		tj.j[3] = {mlp.r1, (half_t*)mlp.r1T, l.W, l.W};
+		tj.j[4] = {mlp.r2, (half_t*)mlp.r2T, 16, l.W};
+		tj.n = 5;
+		launch_transpose_w(stream, tj);
+	}
+
+	// progressive levels (grid.h:2427-2440)
+	uint32_t valid_level_at(int step) const {
+		if (step <= 0) return cfg.n_levels;
+		const float v = std::ceil(cfg.base_valid_level_scale * cfg.n_levels + cfg.valid_level_scale * std::max(0, (int)(step - (int)cfg.base_training_step)));
+		return std::min(cfg.n_levels, (uint32_t)v);
+	}
+	float cos_anneal() const { return cfg.anneal_end == 0 ? 1.0f : std::min(1.0f, (float)training_step / cfg.anneal_end); }
+
+	// ------------------------------------------------------------ network stages
+	void encode(const uint32_t* n_ptr, uint32_t n_fixed, uint32_t n_cap, uint32_t ld, const float* c, uint32_t stride, uint32_t valid, bool want_dydx, hipStream_t s) {
+		const uint32_t gx = std::max<uint32_t>(1, std::min<uint32_t>((n_cap + 255) / 256, 2048));
+		launch_grid_encode(s, n_ptr, n_fixed, ld, c, stride, gl, valid, params_h.p + lay.grid_off, enc.p, want_dydx ? dydx.p : nullptr, gx);
+	}
+	void net_forward(const uint32_t* n_ptr, uint32_t n_fixed, uint32_t n_cap, const float* c, uint32_t valid, half_t* out, hipStream_t s) {
+		const uint32_t ld = n_cap;
+		encode(n_ptr, n_fixed, n_cap, ld, c, COORD_W, valid, true, s);
+		const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((n_cap + 127) / 128, 8192));
+		launch_mlp_forward(s, lay.L, lay.W, n_ptr, n_fixed, ld, c, (const half_t*)enc.p, dydx.p, mlp, out, blocks);
+	}
+	WGradJobs wgrad_jobs(uint32_t n, uint32_t ld, float* g, const uint32_t* n_valid) {
+		const Layout& l = lay;
+		WGradJobs J{};
+		auto job = [&](int k, const half_t* D, const half_t* X, uint32_t off, uint32_t M, uint32_t K, uint32_t ncols, uint32_t ldc) {
+			J.j[k] = {D, X, g + off, M, K, ncols, ldc, (M + 31) / 32, (K + 31) / 32};
+		};
+		job(0, tbuf.d0_delta, tbuf.d0_x, l.off_d0, l.W, l.din, 2 * ld, 2 * ld);
+		job(1, tbuf.d1_delta, tbuf.d1_x, l.off_d1, 16, l.W, 2 * ld, 2 * ld);
+		job(2, tbuf.r0_delta, tbuf.r0_x, l.off_r0, l.W, 48, ld, ld);
+		job(3, tbuf.r1_delta, tbuf.r1_x, l.off_r1, l.W, l.W, ld, ld);
+		job(4, tbuf.r2_delta, tbuf.r2_x, l.off_r2, 16, l.W, ld, ld);
+		J.n_jobs = 5;
+		J.split = 4096;
+		uint32_t b = 0;
+		for (int k = 0; k < 5; ++k) {
+			J.block_start[k] = b;
+			b += J.j[k].tiles_m * J.j[k].tiles_k * ((J.j[k].ncols + J.split - 1) / J.split);
+		}
+		J.block_start[5] = b;
+		J.n_valid = n_valid;
+		(void)n;
+		return J;
+	}
+	// forward recompute + backward into g (fp32 [P], zeroed by the caller)
+	void net_backward(const uint32_t* n_valid_ptr, const uint32_t* n_train_ptr, uint32_t n, const float* c, uint32_t valid,
+	                  const half_t* dlo, float* g, hipStream_t s) {
+		const uint32_t ld = n;
+		encode(n_train_ptr, n, n, ld, c, COORD_W, valid, true, s);
+		TrainBufs t = tbuf;
+		t.var_grad = g + lay.var_off;
+		launch_mlp_train(s, lay.L, lay.W, n_valid_ptr, n, ld, c, (const half_t*)enc.p, dydx.p, dlo, mlp, t);
+		WGradJobs J = wgrad_jobs(n, ld, g, n_train_ptr);
+		launch_wgrad(s, J, J.block_start[5]);
+		const uint32_t gx = std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, 2048));
+		launch_grid_scatter(s, n_train_ptr, n, ld, c, COORD_W, gl, valid, tbuf.dLdenc, tbuf.genc, tbuf.v, g + lay.grid_off, gx);
+	}
+
+	// ------------------------------------------------------------ occupancy grid (testbed_nerf.cu:3293-3397, 4003-4016)
+	void occ_update(uint32_t n_uniform, uint32_t n_nonuniform, uint32_t valid) {
+		hipStream_t s = stream;
+		const uint32_t n_cells = GRID3 * (max_cascade + 1);
+		if (training_step == 0) { HIP_CHECK(hipMemsetAsync(density_grid.p, 0, n_cells * 4, s)); density_grid_ema_step = 0; }
+		HIP_CHECK(hipMemsetAsync(density_tmp.p, 0, n_cells * 4, s));
+		const uint32_t N = n_uniform + n_nonuniform;
+		launch_grid_samples(s, n_uniform, 0, density_grid_rng.state, density_grid_rng.inc, density_grid_ema_step, ds.aabb_min, ds.aabb_max,
+		                    density_grid.p, occ_pos.p, occ_idx.p, max_cascade + 1, -0.01f);
+		density_grid_rng.advance();
+		launch_grid_samples(s, n_nonuniform, n_uniform, density_grid_rng.state, density_grid_rng.inc, density_grid_ema_step, ds.aabb_min, ds.aabb_max,
+		                    density_grid.p, occ_pos.p, occ_idx.p, max_cascade + 1, NERF_MIN_OPTICAL_THICKNESS);
+		density_grid_rng.advance();
+		// NerfNetwork::density on the samples in chunks that fit the encoding workspace
+		const uint32_t chunk = std::min<uint32_t>(N, max_samples);
+		for (uint32_t o = 0; o < N; o += chunk) {
+			const uint32_t m = std::min(chunk, N - o);
+			const uint32_t gx = std::max<uint32_t>(1, std::min<uint32_t>((m + 255) / 256, 4096));
+			launch_grid_encode(s, nullptr, m, m, occ_pos.p + 3 * (size_t)o, 3, gl, valid, params_h.p + lay.grid_off, enc.p, nullptr, gx);
+			launch_mlp_density(s, lay.L, lay.W, m, m, occ_pos.p + 3 * (size_t)o, (const half_t*)enc.p, mlp, occ_density.p + o);
+		}
+		launch_splat_max(s, N, occ_idx.p, occ_density.p, density_tmp.p);
+		launch_ema_grid(s, n_cells, cfg.density_grid_decay, density_grid.p, density_tmp.p);
+		++density_grid_ema_step;
+		launch_grid_mean(s, density_grid.p, grid_partial.p, grid_mean.p);
+		launch_bitfield(s, density_grid.p, bitfield.p, grid_mean.p, max_cascade + 1);
+	}
+
+	// ------------------------------------------------------------ optimizer (trainer.h:170-172)
+	void optimizer_step(const float* g) {
+		// ExponentialDecay (exponential_decay.h:61-80): evaluated with the nested step count before the Adam step
+		const uint32_t sb = adam_step;
+		if (sb == 0) lr_factor = 1.0f;
+		if (sb >= cfg.decay_start && (sb - cfg.decay_start) % cfg.decay_interval == 0 && sb <= 10000000u) lr_factor *= cfg.decay_base;
+		++adam_step;
+		AdamParams p{};
+		p.n = lay.P; p.n_matrix = lay.n_matrix; p.loss_scale = LOSS_SCALE;
+		p.lr = cfg.learning_rate * lr_factor; p.beta1 = cfg.beta1; p.beta2 = cfg.beta2; p.eps = cfg.epsilon; p.l2_reg = cfg.l2_reg;
+		p.ema_decay = cfg.ema_decay;
+		p.ema_debias_old = 1 - (float)std::pow(cfg.ema_decay, adam_step - 1);
+		p.ema_debias_new = 1.0f / (1 - (float)std::pow(cfg.ema_decay, adam_step));
+		p.optimize_matrix = 1; p.optimize_non_matrix = 1;
+		launch_adam_ema(stream, p, params_fp.p, params_h.p, g, m1.p, m2.p, adam_steps.p, ema_tmp.p, ema_h.p);
+		prepare_weights();
+	}
+
+	void mark(int i) { if (profiling) HIP_CHECK(hipEventRecord(ev[i], stream)); }
+
+	// ------------------------------------------------------------ one Testbed::train step (testbed.cu:2640-2736)
+	void train_step() {
+		if (!have_net) throw std::runtime_error("train: no network (reload_network first)");
+		hipStream_t s = stream;
+		const uint32_t valid = valid_level_at((int)training_step);
+		const uint32_t n_prep = std::min(16u, std::max(1u, training_step / 16u));
+		mark(0);
+		if (training_step % n_prep == 0) {
+			const uint32_t nc = GRID3 * (max_cascade + 1);
+			if (training_step < 256) occ_update(nc, 0, valid);
+			else occ_update(nc / 4, nc / 4, valid);
+		}
+		const bool get_loss = training_step % 16 == 0;
+		// ---- train_nerf_step (testbed_nerf.cu:3723-4001)
+		if (training_step == 0) HIP_CHECK(hipMemsetAsync(&st.p->n_rays_total, 0, 4, s));
+		HIP_CHECK(hipMemsetAsync(&st.p->n_kept, 0, 4, s));
+		HIP_CHECK(hipMemsetAsync(&st.p->n_rays_with_samples, 0, 4, s));
+		const DPInfo dp{rank, world};
+		mark(1);
+		launch_march_count(s, MAX_RAYS, st.p, dp, ds, bitfield.p, rng.state, rng.inc, rays.p, startt.p, nreq.p);
+		launch_exclusive_scan(s, scan_tmp.p, scan_tmp_bytes, nreq.p, base.p, MAX_RAYS);
+		launch_march_write(s, MAX_RAYS, st.p, ds, bitfield.p, rays.p, startt.p, nreq.p, base.p, numsteps.p, coords.p);
+		mark(2);
+		encode(&st.p->n_kept, 0, max_samples, max_samples, coords.p, COORD_W, valid, true, s);
+		mark(3);
+		{
+			const uint32_t blocks = 8192;
+			launch_mlp_forward(s, lay.L, lay.W, &st.p->n_kept, 0, max_samples, coords.p, (const half_t*)enc.p, dydx.p, mlp, net_out.p, blocks);
+		}
+		mark(4);
+		LossParams lp{};
+		lp.loss_scale = LOSS_SCALE; lp.ek_w = cfg.ek_loss_weight; lp.mask_w = cfg.mask_loss_weight; lp.cos_anneal = cos_anneal();
+		lp.max_compacted = batch; lp.rng_state = rng.state; lp.rng_inc = rng.inc;
+		launch_loss_count(s, MAX_RAYS, st.p, ds, rays.p, numsteps.p, coords.p, net_out.p, lp.cos_anneal, ccount.p);
+		launch_exclusive_scan(s, scan_tmp.p, scan_tmp_bytes, ccount.p, cbase.p, MAX_RAYS);
+		launch_loss_write(s, MAX_RAYS, st.p, dp, ds, lp, rays.p, numsteps.p, coords.p, net_out.p, ccount.p, cbase.p, coords_c.p, dL_dout.p,
+		                  loss.p, ek.p, mask.p);
+		launch_rollover(s, batch, st.p, coords_c.p, dL_dout.p);
+		mark(5);
+		HIP_CHECK(hipMemsetAsync(grads.p, 0, (size_t)lay.P * 4, s));
+		net_backward(&st.p->compacted_counter, &st.p->n_train, batch, coords_c.p, valid, dL_dout.p, grads.p, s);
+		mark(6);
+		if (world > 1) {
+			NCCL_CHECK(ncclGroupStart());
+			NCCL_CHECK(ncclAllReduce(grads.p, grads.p, lay.P, ncclFloat32, ncclSum, comm, s));
+			NCCL_CHECK(ncclAllReduce(&st.p->numsteps_counter, &st.p->numsteps_counter, 1, ncclUint32, ncclSum, comm, s));
+			NCCL_CHECK(ncclAllReduce(&st.p->compacted_counter, &st.p->compacted_counter, 1, ncclUint32, ncclSum, comm, s));
+			NCCL_CHECK(ncclGroupEnd());
+		}
+		if (get_loss) {
+			launch_sum_f32(s, scan_tmp.p, scan_tmp_bytes, loss.p, loss_sum.p + 0, MAX_RAYS);
+			launch_sum_f32(s, scan_tmp.p, scan_tmp_bytes, ek.p, loss_sum.p + 1, MAX_RAYS);
+			launch_sum_f32(s, scan_tmp.p, scan_tmp_bytes, mask.p, loss_sum.p + 2, MAX_RAYS);
+			HIP_CHECK(hipMemcpyAsync(pinned, loss_sum.p, 3 * 4, hipMemcpyDeviceToHost, s));
+			HIP_CHECK(hipMemcpyAsync(pinned + 4, st.p, sizeof(StepState), hipMemcpyDeviceToHost, s));
+			loss_pending = true;
+		}
+		launch_step_counters(s, st.p, batch, max_samples, world, cfg.fixed_rays_per_batch);
+		rng.advance();
+		// ---- optimizer (testbed_nerf.cu:3503-3508)
+		optimizer_step(grads.p);
+		mark(7);
+		++training_step;
+		if (profiling) accumulate_phases();
+	}
+
+	void accumulate_phases() {
+		HIP_CHECK(hipEventSynchronize(ev[7]));
+		for (int i = 0; i < 7; ++i) {
+			float ms = 0.f;
+			HIP_CHECK(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
+			phase_ms[i] += ms;
+		}
+		++phase_steps;
+	}
+
+	void consume_loss() {
+		if (!loss_pending) return;
+		HIP_CHECK(hipStreamSynchronize(stream));
+		const StepState* sst = (const StepState*)(pinned + 4);
+		const float measured = (float)sst->compacted_counter / (float)world;
+		const float scale = measured / (float)batch;
+		last_loss = pinned[0] * scale;
+		ek_loss = pinned[1] * scale;
+		mask_loss = pinned[2] * scale;
+		if (!loss_ema_init) { loss_scalar_ema = last_loss; loss_ema_init = true; }
+		else loss_scalar_ema = 0.99f * loss_scalar_ema + 0.01f * last_loss;
+		loss_pending = false;
+	}
+};
+
+namespace {
+template <class F> int guard(F&& f) {
+	try { f(); return 0; }
+	catch (const std::exception& e) { g_err = e.what(); return 1; }
+	catch (...) { g_err = "unknown error"; return 1; }
+}
+hipStream_t as_stream(NeusTestbed* tb, void* s) { return s ? (hipStream_t)s : tb->stream; }
+}
+
+extern "C" {
+
+const char* neus_last_error(void) { return g_err.c_str(); }
+int neus_device_count(int* count) { return guard([&] { HIP_CHECK(hipGetDeviceCount(count)); }); }
+int neus_device_synchronize(void) { return guard([&] { HIP_CHECK(hipDeviceSynchronize()); }); }
+
+int neus_testbed_create(int device, NeusTestbed** out) { return guard([&] { *out = new NeusTestbed(device); }); }
+int neus_testbed_destroy(NeusTestbed* tb) { return guard([&] { delete tb; }); }
+int neus_testbed_set_dataset(NeusTestbed* tb, uint32_t n_images, const NeusImage* images, float aabb_scale) {
+	return guard([&] { tb->set_dataset(n_images, images, aabb_scale); });
+}
+int neus_testbed_reload_network(NeusTestbed* tb, const NeusNetworkConfig* cfg, const float* geo) {
+	return guard([&] { tb->reset_network(*cfg, geo); });
+}
+int neus_testbed_layout(NeusTestbed* tb, NeusNetLayout* o) {
+	return guard([&] {
+		if (!tb->have_net) throw std::runtime_error("no network");
+		const Layout& l = tb->lay;
+		o->n_params = l.P; o->n_density = l.n_density; o->n_rgb = l.n_rgb; o->grid_offset = l.grid_off; o->n_grid_params = l.n_grid;
+		o->variance_offset = l.var_off; o->n_matrix = l.n_matrix; o->density_input_width = l.din; o->rgb_input_width = 48;
+	});
+}
+int neus_testbed_train(NeusTestbed* tb, uint32_t n_steps) {
+	return guard([&] {
+		HIP_CHECK(hipSetDevice(tb->device));
+		for (uint32_t i = 0; i < n_steps; ++i) tb->train_step();
+	});
+}
+int neus_testbed_get_stats(NeusTestbed* tb, NeusTrainStats* o) {
+	return guard([&] {
+		tb->consume_loss();
+		HIP_CHECK(hipStreamSynchronize(tb->stream));
+		StepState s{};
+		HIP_CHECK(hipMemcpy(&s, tb->st.p, sizeof(s), hipMemcpyDeviceToHost));
+		float mean = 0.f;
+		if (tb->grid_mean.p) HIP_CHECK(hipMemcpy(&mean, tb->grid_mean.p, 4, hipMemcpyDeviceToHost));
+		o->training_step = tb->training_step; o->rays_per_batch = s.rays_per_batch; o->measured_batch_size = s.measured_batch_size;
+		o->measured_batch_size_before_compaction = s.measured_before; o->n_rays_total = s.n_rays_total;
+		o->valid_level = tb->valid_level_at((int)tb->training_step); o->zero_records = s.zero_records;
+		o->loss = tb->loss_scalar_ema; o->ek_loss = tb->ek_loss; o->mask_loss = tb->mask_loss; o->last_loss = tb->last_loss;
+		o->density_grid_mean = mean;
+	});
+}
+static int copy_param_vec(NeusTestbed* tb, const float* dev, float* host, uint64_t n) {
+	return guard([&] {
+		if (!tb->have_net || n != tb->lay.P) throw std::runtime_error("parameter count mismatch");
+		HIP_CHECK(hipStreamSynchronize(tb->stream));
+		HIP_CHECK(hipMemcpy(host, dev, n * 4, hipMemcpyDeviceToHost));
+	});
+}
+int neus_testbed_get_params(NeusTestbed* tb, float* o, uint64_t n) { return copy_param_vec(tb, tb->params_fp.p, o, n); }
+int neus_testbed_get_gradients(NeusTestbed* tb, float* o, uint64_t n) { return copy_param_vec(tb, tb->grads.p, o, n); }
+int neus_testbed_get_ema_params(NeusTestbed* tb, float* o, uint64_t n) { return copy_param_vec(tb, tb->ema_tmp.p, o, n); }
+int neus_testbed_set_params(NeusTestbed* tb, const float* in, uint64_t n) {
+	return guard([&] {
+		if (!tb->have_net || n != tb->lay.P) throw std::runtime_error("parameter count mismatch");
+		HIP_CHECK(hipStreamSynchronize(tb->stream));
+		HIP_CHECK(hipMemcpy(tb->params_fp.p, in, n * 4, hipMemcpyHostToDevice));
+		launch_cast_half(tb->stream, (uint32_t)n, tb->params_fp.p, tb->params_h.p);
+		tb->prepare_weights();
+		HIP_CHECK(hipStreamSynchronize(tb->stream));
+	});
+}
+int neus_testbed_get_density_grid(NeusTestbed* tb, float* g, uint8_t* bf) {
+	return guard([&] {
+		HIP_CHECK(hipStreamSynchronize(tb->stream));
+		if (g) HIP_CHECK(hipMemcpy(g, tb->density_grid.p, (size_t)GRID3 * 4, hipMemcpyDeviceToHost));
+		if (bf) HIP_CHECK(hipMemcpy(bf, tb->bitfield.p, GRID3 / 8 * NERF_CASCADES, hipMemcpyDeviceToHost));
+	});
+}
+int neus_testbed_set_density_grid(NeusTestbed* tb, const float* g, const uint8_t* bf) {
+	return guard([&] {
+		HIP_CHECK(hipStreamSynchronize(tb->stream));
+		if (g) HIP_CHECK(hipMemcpy(tb->density_grid.p, g, (size_t)GRID3 * 4, hipMemcpyHostToDevice));
+		if (bf) HIP_CHECK(hipMemcpy(tb->bitfield.p, bf, GRID3 / 8 * NERF_CASCADES, hipMemcpyHostToDevice));
+	});
+}
+int neus_testbed_get_rng(NeusTestbed* tb, uint64_t* o) {
+	return guard([&] { o[0] = tb->rng.state; o[1] = tb->rng.inc; o[2] = tb->density_grid_rng.state; o[3] = tb->density_grid_rng.inc; });
+}
+int neus_testbed_stream(NeusTestbed* tb, void** s) { return guard([&] { *s = (void*)tb->stream; }); }
+int neus_testbed_synchronize(NeusTestbed* tb) { return guard([&] { HIP_CHECK(hipStreamSynchronize(tb->stream)); }); }
+int neus_testbed_set_profiling(NeusTestbed* tb, int on) {
+	return guard([&] { tb->profiling = on != 0; for (auto& m : tb->phase_ms) m = 0; tb->phase_steps = 0; });
+}
+int neus_testbed_kernel_times(NeusTestbed* tb, float* ms) {
+	return guard([&] {
+		for (int i = 0; i < NeusTestbed::N_PHASES; ++i) ms[i] = tb->phase_steps ? (float)(tb->phase_ms[i] / tb->phase_steps) : 0.f;
+		ms[7] = (float)tb->phase_steps;
+	});
+}
+
+int neus_nccl_unique_id(uint8_t* out) {
+	return guard([&] {
+		ncclUniqueId id;
+		NCCL_CHECK(ncclGetUniqueId(&id));
+		static_assert(sizeof(id) == 128, "ncclUniqueId size");
+		std::memcpy(out, &id, 128);
+	});
+}
+int neus_testbed_init_data_parallel(NeusTestbed* tb, int rank, int world, const uint8_t* uid) {
+	return guard([&] {
+		if (world < 1 || rank < 0 || rank >= world) throw std::runtime_error("invalid rank/world");
+		HIP_CHECK(hipSetDevice(tb->device));
+		tb->rank = (uint32_t)rank; tb->world = (uint32_t)world;
+		tb->tbuf.indeed_batch = (float)tb->batch * (float)world;
+		if (world > 1) {
+			ncclUniqueId id;
+			std::memcpy(&id, uid, 128);
+			NCCL_CHECK(ncclCommInitRank(&tb->comm, world, id, rank));
+		}
+	});
+}
+
+// ------------------------------------------------------------ operator surface
+int neus_grid_encode(NeusTestbed* tb, void* stream, uint32_t n, uint32_t ld, const float* coords, uint32_t stride, uint32_t valid,
+                     uint16_t* enc, float* dydx) {
+	return guard([&] {
+		if (!tb->have_net) throw std::runtime_error("no network");
+		const uint32_t gx = std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, 4096));
+		launch_grid_encode(as_stream(tb, stream), nullptr, n, ld, coords, stride, tb->gl, valid, tb->params_h.p + tb->lay.grid_off,
+		                   (uint32_t*)enc, dydx, gx);
+		HIP_CHECK(hipGetLastError());
+	});
+}
+int neus_net_forward(NeusTestbed* tb, void* stream, uint32_t n, const float* coords, uint32_t valid, uint16_t* out) {
+	return guard([&] {
+		if (!tb->have_net) throw std::runtime_error("no network");
+		if (n > tb->max_samples) throw std::runtime_error("neus_net_forward: n exceeds the workspace (16 x batch_size)");
+		tb->net_forward(nullptr, n, n, coords, valid, (half_t*)out, as_stream(tb, stream));
+		HIP_CHECK(hipGetLastError());
+	});
+}
+int neus_net_backward(NeusTestbed* tb, void* stream, uint32_t n, const float* coords, uint32_t valid, const uint16_t* dlo,
+                      uint32_t indeed, float* grads_out) {
+	return guard([&] {
+		if (!tb->have_net) throw std::runtime_error("no network");
+		if (n == 0 || n % 128 != 0) throw std::runtime_error("neus_net_backward: batch must be a positive multiple of 128 (fully_fused_mlp.cu:779-781)");
+		if (n > tb->batch) throw std::runtime_error("neus_net_backward: n exceeds batch_size");
+		hipStream_t s = as_stream(tb, stream);
+		HIP_CHECK(hipMemsetAsync(grads_out, 0, (size_t)tb->lay.P * 4, s));
+		const float saved = tb->tbuf.indeed_batch;
+		tb->tbuf.indeed_batch = (float)indeed;
+		tb->net_backward(nullptr, nullptr, n, coords, valid, (const half_t*)dlo, grads_out, s);
+		tb->tbuf.indeed_batch = saved;
+		HIP_CHECK(hipGetLastError());
+	});
+}
+int neus_sample_rays(NeusTestbed* tb, void* stream, uint32_t n_rays, uint32_t rank, uint32_t world, uint32_t n_rays_total,
+                     uint64_t rng_state, uint64_t rng_inc, uint32_t max_samples, const uint8_t* bitfield, float* rays, uint32_t* numsteps,
+                     float* coords, uint32_t* counters_out) {
+	return guard([&] {
+		if (!tb->have_data || !tb->have_net) throw std::runtime_error("no dataset/network");
+		if (n_rays == 0 || n_rays > MAX_RAYS) throw std::runtime_error("n_rays out of range");
+		hipStream_t s = as_stream(tb, stream);
+		Dev<StepState> sst; sst.alloc(1);
+		StepState h{}; h.rays_per_batch = n_rays; h.max_inference = max_samples; h.n_rays_total = n_rays_total;
+		HIP_CHECK(hipMemcpyAsync(sst.p, &h, sizeof(h), hipMemcpyHostToDevice, s));
+		Dev<float> st_t; st_t.alloc(n_rays); Dev<uint32_t> nr, bs; nr.alloc(n_rays); bs.alloc(n_rays);
+		Dev<uint8_t> tmp; const size_t tb_ = scan_temp_bytes(n_rays); tmp.alloc(tb_ + 256);
+		launch_march_count(s, n_rays, sst.p, DPInfo{rank, world}, tb->ds, bitfield, rng_state, rng_inc, rays, st_t.p, nr.p);
+		launch_exclusive_scan(s, tmp.p, tb_, nr.p, bs.p, n_rays);
+		launch_march_write(s, n_rays, sst.p, tb->ds, bitfield, rays, st_t.p, nr.p, bs.p, numsteps, coords);
+		HIP_CHECK(hipMemcpyAsync(&h, sst.p, sizeof(h), hipMemcpyDeviceToHost, s));
+		HIP_CHECK(hipStreamSynchronize(s));
+		counters_out[0] = h.numsteps_counter; counters_out[1] = h.n_kept; counters_out[2] = h.n_rays_with_samples;
+	});
+}
+int neus_loss_compact(NeusTestbed* tb, void* stream, uint32_t n_rays, uint32_t rank, uint32_t world, uint32_t n_rays_total,
+                      uint64_t rng_state, uint64_t rng_inc, uint32_t max_compacted, const float* rays, uint32_t* numsteps,
+                      const float* coords, const uint16_t* net_out, float* coords_out, uint16_t* dlo, float* loss, float* ek,
+                      float* mask, uint32_t* counters_out) {
+	return guard([&] {
+		if (!tb->have_data || !tb->have_net) throw std::runtime_error("no dataset/network");
+		hipStream_t s = as_stream(tb, stream);
+		Dev<StepState> sst; sst.alloc(1);
+		StepState h{}; h.rays_per_batch = n_rays; h.n_rays_total = n_rays_total;
+		HIP_CHECK(hipMemcpyAsync(sst.p, &h, sizeof(h), hipMemcpyHostToDevice, s));
+		Dev<uint32_t> cc, cb; cc.alloc(n_rays); cb.alloc(n_rays);
+		Dev<uint8_t> tmp; const size_t tb_ = scan_temp_bytes(n_rays); tmp.alloc(tb_ + 256);
+		LossParams lp{};
+		lp.loss_scale = LOSS_SCALE; lp.ek_w = tb->cfg.ek_loss_weight; lp.mask_w = tb->cfg.mask_loss_weight; lp.cos_anneal = tb->cos_anneal();
+		lp.max_compacted = max_compacted; lp.rng_state = rng_state; lp.rng_inc = rng_inc;
+		launch_loss_count(s, n_rays, sst.p, tb->ds, rays, numsteps, coords, (const half_t*)net_out, lp.cos_anneal, cc.p);
+		launch_exclusive_scan(s, tmp.p, tb_, cc.p, cb.p, n_rays);
+		launch_loss_write(s, n_rays, sst.p, DPInfo{rank, world}, tb->ds, lp, rays, numsteps, coords, (const half_t*)net_out, cc.p, cb.p,
+		                  coords_out, (half_t*)dlo, loss, ek, mask);
+		HIP_CHECK(hipMemcpyAsync(&h, sst.p, sizeof(h), hipMemcpyDeviceToHost, s));
+		HIP_CHECK(hipStreamSynchronize(s));
+		counters_out[0] = h.compacted_counter;
+	});
+}
+int neus_optimizer_step(NeusTestbed* tb, void* stream, const float* grads) {
+	return guard([&] {
+		if (!tb->have_net) throw std::runtime_error("no network");
+		if (stream && (hipStream_t)stream != tb->stream) HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+		tb->optimizer_step(grads);
+		HIP_CHECK(hipStreamSynchronize(tb->stream));
+	});
+}
+int neus_occ_update(NeusTestbed* tb, void* stream, uint32_t n_uniform, uint32_t n_nonuniform) {
+	return guard([&] {
+		if (!tb->have_net) throw std::runtime_error("no network");
+		(void)stream;
+		tb->occ_update(n_uniform, n_nonuniform, tb->valid_level_at((int)tb->training_step));
+		HIP_CHECK(hipStreamSynchronize(tb->stream));
+	});
+}
+int neus_mfma_probe(const uint16_t* A, const uint16_t* B, float* C) {
+	return guard([&] {
+		launch_mfma_probe(nullptr, (const half_t*)A, (const half_t*)B, C);
+		HIP_CHECK(hipDeviceSynchronize());
+	});
+}
+
+} // extern "C"

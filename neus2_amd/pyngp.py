@@ -1,0 +1,325 @@
+"""Python mirror of the reference's pybind11 `pyngp` module (src/python_api.cu:216-600) for the
+NeuS2 training path, implemented over the C-ABI of libneus2_hip.so (include/neus2_hip.h).
+
+Drop-in surface used by the reference drivers (scripts/run.py):
+    testbed = pyngp.Testbed(pyngp.TestbedMode.Nerf)
+    testbed.load_training_data("transforms.json")
+    testbed.reload_network_from_file("configs/nerf/base.json")
+    while testbed.frame(): ...   # one Testbed::train step per frame while shall_train
+    testbed.training_step, testbed.loss, testbed.ek_loss, testbed.mask_loss
+
+The transforms.json parser restates ngp::load_nerf (src/nerf_loader.cu:197-751) for the
+fields the NeuS2 path uses; images are decoded with PIL into RGBA8.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import enum
+import glob
+import json
+import math
+import os
+
+import numpy as np
+
+from . import config as _config
+from ._lib import NeusError, NeusImage, NeusNetLayout, NeusTrainStats, check, lib
+
+
+class TestbedMode(enum.IntEnum):
+    Nerf = 0
+    Sdf = 1
+    Image = 2
+    Volume = 3
+
+
+NERF_SCALE = 0.33  # nerf_loader.h:31
+
+
+def fov_to_focal_length(resolution, degrees):
+    return 0.5 * resolution / math.tan(0.5 * degrees * math.pi / 180.0)
+
+
+def nerf_matrix_to_ngp(m, scale, offset, from_na):
+    """NerfDataset::nerf_matrix_to_ngp (nerf_loader.h:112-134)."""
+    r = np.array(m, np.float32)[:3, :4].copy()
+    r[:, 1] *= -1
+    r[:, 2] *= -1
+    r[:, 3] = r[:, 3] * np.float32(scale) + np.asarray(offset, np.float32)
+    if from_na:
+        r[:, 1] *= -1
+        r[:, 2] *= -1
+    else:
+        r = r[[1, 2, 0], :]
+    return r
+
+
+def load_transforms(path):
+    """ngp::load_nerf (nerf_loader.cu:197-751) subset: from_na/scale/offset/aabb_scale, per-frame
+    intrinsic_matrix or fl_x/fl_y/camera_angle_x, cx/cy; RGBA PNG images (alpha premultiplied on
+    the device by read_rgba)."""
+    from PIL import Image
+    with open(path) as f:
+        js = json.load(f)
+    base = os.path.dirname(path)
+    scale = float(js.get("scale", NERF_SCALE))
+    offset = js.get("offset", [0.5, 0.5, 0.5])
+    if not isinstance(offset, list):
+        offset = [offset] * 3
+    offset = np.array(offset, np.float32)
+    from_na = "from_na" in js
+    aabb_scale = int(js.get("aabb_scale", 1))
+    if "aabb" in js:
+        a = np.array(js["aabb"], np.float32)
+        length = max(1e-6, float(np.max(np.abs(a[1] - a[0]))))
+        scale = 1.0 / length
+        offset = (a[1] + a[0]) * 0.5 * -scale + 0.5
+    images, focal, principal, xforms = [], [], [], []
+    for fr in js["frames"]:
+        p = os.path.join(base, fr["file_path"])
+        if not os.path.splitext(p)[1]:
+            p = p + ".png"
+        img = np.asarray(Image.open(p).convert("RGBA"), np.uint8)
+        h, w = img.shape[:2]
+        pp = np.array([0.5, 0.5], np.float32)
+        if "cx" in js:
+            pp[0] = float(js["cx"]) / float(js["w"])
+        if "cy" in js:
+            pp[1] = float(js["cy"]) / float(js["h"])
+
+        def read_fl(res, axis):
+            if axis + "_fov" in fr:
+                return fov_to_focal_length(res, float(fr[axis + "_fov"]))
+            if "fl_" + axis in js:
+                return float(js["fl_" + axis])
+            if "camera_angle_" + axis in js:
+                return fov_to_focal_length(res, float(js["camera_angle_" + axis]) * 180 / math.pi)
+            return 0.0
+
+        fx, fy = read_fl(w, "x"), read_fl(h, "y")
+        if fx != 0:
+            fl = [fx, fy if fy != 0 else fx]
+        elif fy != 0:
+            fl = [fy, fy]
+        elif "intrinsic_matrix" in fr:
+            K = fr["intrinsic_matrix"]
+            fl = [float(K[0][0]), float(K[1][1])]
+            pp = np.array([float(K[0][2]) / float(js["w"]), float(K[1][2]) / float(js["h"])], np.float32)
+        else:
+            raise RuntimeError("Couldn't read fov.")
+        m = fr.get("transform_matrix_start", fr.get("transform_matrix"))
+        xforms.append(nerf_matrix_to_ngp(m, scale, offset, from_na))
+        images.append(img)
+        focal.append(fl)
+        principal.append(pp)
+    return dict(images=images, focal=np.array(focal, np.float32), principal=np.array(principal, np.float32),
+                xforms=np.stack(xforms).astype(np.float32), aabb_scale=aabb_scale)
+
+
+def geometric_init_weights(n_levels, width=64, seed=1337, path_hint=True):
+    """Density-MLP geometric initialisation (my_tcnn/scripts/geometry_init_save_weights.py:291-331).
+    The reference loads utils/mlp_weights*.txt (nerf_network.h:787-813); that file is used when present,
+    otherwise the same recipe is generated deterministically: W0[:, :3] ~ N(0, sqrt(2)/sqrt(W)),
+    W0[:, 3:] = 0, W1 ~ N(sqrt(pi)/sqrt(W), 1e-5)."""
+    din = _config.density_input_width(n_levels)
+    if path_hint:
+        fname = {32: "utils/mlp_weights_hidden_layer_num_1_hidden_size_32.txt", 48: "utils/mlp_weights.txt"}.get(din)
+        if fname and os.path.exists(fname):
+            return np.loadtxt(fname, dtype=np.float32)[: width * din + 16 * width]
+    rng = np.random.default_rng(seed)
+    w0 = np.zeros((width, din), np.float32)
+    w0[:, :3] = rng.normal(0.0, math.sqrt(2) / math.sqrt(width), size=(width, 3))
+    w1 = rng.normal(math.sqrt(math.pi) / math.sqrt(width), 1e-5, size=(16, width)).astype(np.float32)
+    return np.concatenate([w0.reshape(-1), w1.reshape(-1)]).astype(np.float32)
+
+
+class _Training:
+    def __init__(self, tb):
+        self._tb = tb
+
+    @property
+    def n_images_for_training(self):
+        return self._tb._n_images
+
+    @property
+    def counters_rgb(self):
+        return self._tb.stats()
+
+
+class _Nerf:
+    def __init__(self, tb):
+        self.training = _Training(tb)
+
+
+class Testbed:
+    """pyngp.Testbed (python_api.cu:216-600), NeuS2 training subset."""
+
+    def __init__(self, mode: TestbedMode = TestbedMode.Nerf, device: int = 0):
+        if mode != TestbedMode.Nerf:
+            raise NeusError("only TestbedMode.Nerf (NeuS2) is implemented on the gfx950 path")
+        h = C.c_void_p()
+        check(lib().neus_testbed_create(C.c_int(device), C.byref(h)))
+        self._h = h
+        self._n_images = 0
+        self._images = None
+        self._net_cfg = None
+        self._cfg_dict = None
+        self.shall_train = True
+        self.nerf = _Nerf(self)
+        self.max_training_steps = None
+
+    def __del__(self):
+        try:
+            if getattr(self, "_h", None):
+                lib().neus_testbed_destroy(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ data
+    def load_training_data(self, path: str):
+        """Testbed::load_training_data (testbed.cu:93) -> load_nerf (testbed_nerf.cu:2964):
+        a transforms.json file, or a directory whose sorted *.json files are frames (first used)."""
+        if os.path.isdir(path):
+            files = sorted(f for f in glob.glob(os.path.join(path, "*.json")) if "downsample" not in os.path.basename(f))
+            if not files:
+                raise NeusError(f"no json files in {path}")
+            path = files[0]
+        d = load_transforms(path)
+        self.set_dataset(d["images"], d["focal"], d["principal"], d["xforms"], d["aabb_scale"])
+
+    def set_dataset(self, images, focal, principal, xforms, aabb_scale=1):
+        imgs = [np.ascontiguousarray(im, np.uint8) for im in images]
+        arr = (NeusImage * len(imgs))()
+        for i, im in enumerate(imgs):
+            arr[i].width = im.shape[1]
+            arr[i].height = im.shape[0]
+            arr[i].rgba8 = im.ctypes.data
+            arr[i].focal[:] = [float(v) for v in np.asarray(focal[i]).reshape(2)]
+            arr[i].principal[:] = [float(v) for v in np.asarray(principal[i]).reshape(2)]
+            arr[i].xform[:] = [float(v) for v in np.asarray(xforms[i], np.float32).reshape(12)]
+        check(lib().neus_testbed_set_dataset(self._h, C.c_uint32(len(imgs)), arr, C.c_float(aabb_scale)))
+        self._images = imgs
+        self._n_images = len(imgs)
+
+    # ------------------------------------------------------------------ network
+    def reload_network_from_file(self, path: str = "", batch_size=None, fixed_rays_per_batch=0):
+        """Testbed::reload_network_from_file (testbed.cu:164) -> reset_network (testbed.cu:2084)."""
+        cfg = _config.load_json(path)
+        self.reload_network_from_json(cfg, batch_size=batch_size, fixed_rays_per_batch=fixed_rays_per_batch)
+
+    def reload_network_from_json(self, cfg, batch_size=None, fixed_rays_per_batch=0, geometric_init=None):
+        if isinstance(cfg, str):
+            cfg = _config.parse_json_text(cfg)
+        c = _config.network_config(cfg, batch_size=batch_size, fixed_rays_per_batch=fixed_rays_per_batch)
+        geo = geometric_init if geometric_init is not None else geometric_init_weights(c.n_levels, c.n_neurons)
+        geo = np.ascontiguousarray(geo, np.float32)
+        check(lib().neus_testbed_reload_network(self._h, C.byref(c), C.c_void_p(geo.ctypes.data)))
+        self._net_cfg = c
+        self._cfg_dict = cfg
+        self._geo = geo
+
+    def layout(self):
+        l = NeusNetLayout()
+        check(lib().neus_testbed_layout(self._h, C.byref(l)))
+        return {k: getattr(l, k) for k, _ in l._fields_}
+
+    # ------------------------------------------------------------------ training
+    def frame(self):
+        """Testbed::frame (testbed.cu:1722-1783) without GUI: one training step while shall_train."""
+        if self.shall_train:
+            if self.max_training_steps is not None and self.training_step >= self.max_training_steps:
+                self.shall_train = False
+                return False
+            self.train(1)
+        return True
+
+    def train(self, n_steps: int = 1):
+        check(lib().neus_testbed_train(self._h, C.c_uint32(n_steps)))
+
+    def stats(self):
+        s = NeusTrainStats()
+        check(lib().neus_testbed_get_stats(self._h, C.byref(s)))
+        return {k: getattr(s, k) for k, _ in s._fields_}
+
+    @property
+    def training_step(self):
+        return self.stats()["training_step"]
+
+    @property
+    def loss(self):
+        return self.stats()["loss"]
+
+    @property
+    def ek_loss(self):
+        return self.stats()["ek_loss"]
+
+    @property
+    def mask_loss(self):
+        return self.stats()["mask_loss"]
+
+    def set_profiling(self, on=True):
+        check(lib().neus_testbed_set_profiling(self._h, C.c_int(1 if on else 0)))
+
+    def phase_times(self):
+        a = (C.c_float * 8)()
+        check(lib().neus_testbed_kernel_times(self._h, a))
+        keys = ["occupancy", "sample", "inference_encode", "inference_mlp", "loss", "backward", "optimizer"]
+        return dict(zip(keys, list(a)[:7])), int(a[7])
+
+    # ------------------------------------------------------------------ state access
+    def get_params(self):
+        n = self.layout()["n_params"]
+        out = np.zeros(n, np.float32)
+        check(lib().neus_testbed_get_params(self._h, C.c_void_p(out.ctypes.data), C.c_uint64(n)))
+        return out
+
+    def set_params(self, p):
+        p = np.ascontiguousarray(p, np.float32)
+        check(lib().neus_testbed_set_params(self._h, C.c_void_p(p.ctypes.data), C.c_uint64(p.size)))
+
+    def get_gradients(self):
+        n = self.layout()["n_params"]
+        out = np.zeros(n, np.float32)
+        check(lib().neus_testbed_get_gradients(self._h, C.c_void_p(out.ctypes.data), C.c_uint64(n)))
+        return out
+
+    def get_ema_params(self):
+        n = self.layout()["n_params"]
+        out = np.zeros(n, np.float32)
+        check(lib().neus_testbed_get_ema_params(self._h, C.c_void_p(out.ctypes.data), C.c_uint64(n)))
+        return out
+
+    def get_density_grid(self):
+        g = np.zeros(128 ** 3, np.float32)
+        bf = np.zeros(128 ** 3 // 8 * 8, np.uint8)
+        check(lib().neus_testbed_get_density_grid(self._h, C.c_void_p(g.ctypes.data), C.c_void_p(bf.ctypes.data)))
+        return g, bf
+
+    def set_density_grid(self, grid=None, bitfield=None):
+        g = None if grid is None else np.ascontiguousarray(grid, np.float32)
+        b = None if bitfield is None else np.ascontiguousarray(bitfield, np.uint8)
+        check(lib().neus_testbed_set_density_grid(self._h, C.c_void_p(g.ctypes.data if g is not None else 0),
+                                                  C.c_void_p(b.ctypes.data if b is not None else 0)))
+
+    def get_rng(self):
+        o = (C.c_uint64 * 4)()
+        check(lib().neus_testbed_get_rng(self._h, o))
+        return list(o)
+
+    def synchronize(self):
+        check(lib().neus_testbed_synchronize(self._h))
+
+    def init_data_parallel(self, rank, world, unique_id: bytes):
+        buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
+        check(lib().neus_testbed_init_data_parallel(self._h, C.c_int(rank), C.c_int(world), buf))
+
+    @property
+    def handle(self):
+        return self._h
+
+
+def nccl_unique_id() -> bytes:
+    buf = (C.c_uint8 * 128)()
+    check(lib().neus_nccl_unique_id(buf))
+    return bytes(buf)

@@ -1,0 +1,232 @@
+"""GPU parity tests: the HIP path (through the C-ABI) against the CPU oracle on the same seeded
+inputs. Bit-exact for integer/index data (ray slots, numsteps, compaction, sample coordinates);
+fp16-scale tolerances (stated per test) for floating-point outputs and gradients."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+from gpu_util import dev, host, ptr
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BATCH = 4096
+
+
+@pytest.fixture(scope="module")
+def env(torch_cuda):
+    from neus2_amd import pyngp, scenes
+    import oracle as O
+    sc = scenes.small_scene(n_views=8, width=64, height=48)
+    tb = pyngp.Testbed(pyngp.TestbedMode.Nerf)
+    tb.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
+    tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=BATCH)
+    cfg = O.make_cfg(per_level_scale=tb._net_cfg.per_level_scale)
+    ds = O.Dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"])
+    return dict(tb=tb, O=O, cfg=cfg, ds=ds, sc=sc, t=torch_cuda, scenes=scenes)
+
+
+def L():
+    from neus2_amd._lib import check, lib
+    return lib(), check
+
+
+def test_mfma_f16_layout_exact(torch_cuda):
+    """v_mfma_f32_32x32x16_f16 lane maps (natural k order) with exact small-integer data, asymmetric B."""
+    t = torch_cuda
+    rng = np.random.default_rng(0)
+    A = rng.integers(-4, 5, size=(32, 16)).astype(np.float16)
+    B = rng.integers(-4, 5, size=(16, 32)).astype(np.float16)
+    B[0, 1] = 7  # asymmetric
+    Cd = t.zeros((32, 32), dtype=t.float32, device="cuda")
+    lib, check = L()
+    check(lib.neus_mfma_probe(ptr(dev(t, A)), ptr(dev(t, B)), ptr(Cd)))
+    np.testing.assert_array_equal(Cd.cpu().numpy(), A.astype(np.float32) @ B.astype(np.float32))
+
+
+def test_param_init_matches_oracle(env):
+    """Trainer init (seed_seq{1337} -> pcg32; xavier; grid U(+-1e-4); variance 0.3) bit-exact."""
+    O, tb = env["O"], env["tb"]
+    geo = tb._geo
+    ref = np.zeros(O.layout(env["cfg"])["n_params"], np.float32)
+    O.lib().or_init_params(C.byref(env["cfg"]), C.c_uint32(1337), O.P(geo), O.P(ref))
+    got = tb.get_params()
+    np.testing.assert_array_equal(got, ref)
+
+
+def _perturbed(env, seed=11):
+    """Parameters that exercise every path: nonzero encoding columns of W0 and O(0.1) grid values."""
+    tb = env["tb"]
+    lay = tb.layout()
+    rng = np.random.default_rng(seed)
+    p = tb.get_params().copy()
+    din = lay["density_input_width"]
+    w0 = p[: 64 * din].reshape(64, din)
+    w0[:, 3:31] = rng.normal(0, 0.3, (64, 28))
+    p[: 64 * din] = w0.reshape(-1)
+    g0, g1 = lay["grid_offset"], lay["variance_offset"]
+    p[g0:g1] = rng.uniform(-0.1, 0.1, g1 - g0).astype(np.float32)
+    tb.set_params(p)
+    return p
+
+
+def _coords(n, seed=0):
+    rng = np.random.default_rng(seed)
+    c = np.zeros((n, 7), np.float32)
+    c[:, :3] = rng.uniform(0.05, 0.95, (n, 3))
+    d = rng.normal(size=(n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    c[:, 4:] = (d + 1) * 0.5
+    return c
+
+
+def test_grid_encode_parity(env):
+    """Hash-grid forward: enc within 1 fp16 ulp, dy/dx rel 1e-4 (fp32 interpolation, FMA order)."""
+    t, O, tb = env["t"], env["O"], env["tb"]
+    lib, check = L()
+    n = 1024
+    c = _coords(n, 1)
+    Lv = env["cfg"].n_levels
+    params = _perturbed(env)
+    for valid in (Lv, 3):
+        enc = t.zeros((Lv, n, 2), dtype=t.int16, device="cuda")
+        dydx = t.zeros((6 * Lv, n), dtype=t.float32, device="cuda")
+        check(lib.neus_grid_encode(tb.handle, None, C.c_uint32(n), C.c_uint32(n), ptr(dev(t, c)), C.c_uint32(7), C.c_uint32(valid), ptr(enc), ptr(dydx)))
+        t.cuda.synchronize()
+        got = host(enc, np.float16).astype(np.float32).transpose(1, 0, 2).reshape(n, 2 * Lv)
+        gdy = host(dydx, np.float32).reshape(Lv, 2, 3, n).transpose(3, 0, 1, 2).reshape(n, 2 * Lv, 3)
+        ref, rdy = O.grid_forward(env["cfg"], params, c[:, :3], valid)
+        ulp = np.abs(ref) * 2 ** -10 + 6e-8
+        assert np.all(np.abs(got - ref) <= ulp + 1e-12), np.abs(got - ref).max()
+        np.testing.assert_allclose(gdy, rdy, rtol=1e-4, atol=1e-6)
+
+
+def test_network_forward_parity(env):
+    """NerfNetwork forward (AoS16 fp16 out): rows 0..10 within fp16-accumulation tolerance."""
+    t, O, tb = env["t"], env["O"], env["tb"]
+    lib, check = L()
+    n = 2048
+    c = _coords(n, 2)
+    params = _perturbed(env, 12)
+    out = t.zeros((n, 16), dtype=t.int16, device="cuda")
+    for valid in (14, 4):
+        check(lib.neus_net_forward(tb.handle, None, C.c_uint32(n), ptr(dev(t, c)), C.c_uint32(valid), ptr(out)))
+        t.cuda.synchronize()
+        got = host(out, np.float16).astype(np.float32)
+        ref = O.network_forward(env["cfg"], params, c, valid).view(np.float16).astype(np.float32)
+        err = np.abs(got[:, :11] - ref[:, :11])
+        tol = 2e-3 + 4e-3 * np.abs(ref[:, :11])
+        assert np.mean(err <= tol) > 0.999 and err.max() < 5e-2, (err.max(), np.argwhere(err > tol)[:5])
+
+
+def test_network_backward_parity(env):
+    """First + second order parameter gradients: cosine >= 0.999 per block, rel-L2 <= 2e-2."""
+    t, O, tb = env["t"], env["O"], env["tb"]
+    lib, check = L()
+    n = 1024
+    c = _coords(n, 3)
+    params = _perturbed(env, 13)
+    rng = np.random.default_rng(4)
+    dl = np.zeros((n, 16), np.float32)
+    dl[:, :4] = rng.normal(0, 1e-2, (n, 4))
+    dl[:, 4:7] = rng.normal(0, 1.0, (n, 3))
+    dl[:, 7] = rng.normal(0, 1e-2, n)
+    dl[:, 8:11] = rng.normal(0, 1e-2, (n, 3))
+    dl16 = dl.astype(np.float16)
+    lay = tb.layout()
+    g = t.zeros(lay["n_params"], dtype=t.float32, device="cuda")
+    check(lib.neus_net_backward(tb.handle, None, C.c_uint32(n), ptr(dev(t, c)), C.c_uint32(14), ptr(dev(t, dl16)), C.c_uint32(n), ptr(g)))
+    t.cuda.synchronize()
+    got = g.cpu().numpy()
+    ref = O.network_backward(env["cfg"], params, c, 14, dl16.view(np.uint16), n)
+    blocks = {"density": (0, lay["n_density"]), "rgb": (lay["n_density"], lay["n_matrix"]),
+              "grid": (lay["grid_offset"], lay["variance_offset"]), "variance": (lay["variance_offset"], lay["variance_offset"] + 1)}
+    for name, (a, b) in blocks.items():
+        x, y = got[a:b].astype(np.float64), ref[a:b].astype(np.float64)
+        rel = np.linalg.norm(x - y) / max(np.linalg.norm(y), 1e-30)
+        cos = x @ y / max(np.linalg.norm(x) * np.linalg.norm(y), 1e-30)
+        assert rel <= 2e-2 and cos >= 0.999, (name, rel, cos)
+
+
+def _bitfield(env):
+    return env["scenes"].shell_bitfield(thickness=6.0 / 128)
+
+
+def test_sample_rays_bit_exact(env):
+    """Ray sampling + occupancy march: rays, numsteps, coords bit-identical to the oracle."""
+    t, O, tb = env["t"], env["O"], env["tb"]
+    lib, check = L()
+    bf = _bitfield(env)
+    n_rays, max_samples = 4096, 4096 * 16
+    rng_state, rng_inc = 0x1234567890ABCDEF, 0xDA3E39CB94B95BDB | 1
+    for (max_s, world, rank, total) in [(max_samples, 1, 0, 0), (20000, 1, 0, 12345), (max_samples, 2, 1, 8192)]:
+        rays = t.zeros((n_rays, 6), dtype=t.float32, device="cuda")
+        ns = t.zeros((n_rays, 2), dtype=t.int32, device="cuda")
+        co = t.zeros((max_s, 7), dtype=t.float32, device="cuda")
+        cnt = (C.c_uint32 * 3)()
+        check(lib.neus_sample_rays(tb.handle, None, C.c_uint32(n_rays), C.c_uint32(rank), C.c_uint32(world), C.c_uint32(total),
+                                   C.c_uint64(rng_state), C.c_uint64(rng_inc), C.c_uint32(max_s), ptr(dev(t, bf)),
+                                   ptr(rays), ptr(ns), ptr(co), cnt))
+        r_rays, r_ns, r_co, r_cnt, r_nr = O.generate_samples(env["ds"], bf, n_rays, total, rng_state, rng_inc, max_s,
+                                                             ray_offset=rank * n_rays, n_rays_global=world * n_rays)
+        g_ns = host(ns, np.uint32)
+        np.testing.assert_array_equal(g_ns, r_ns)
+        assert cnt[0] == r_cnt and cnt[2] == r_nr
+        np.testing.assert_array_equal(host(rays, np.uint32), r_rays.view(np.uint32))
+        nk = int(cnt[1])
+        assert nk == int((r_ns[:, 0]).sum())
+        np.testing.assert_array_equal(host(co, np.uint32)[:nk], r_co.view(np.uint32)[:nk])
+        assert nk > 0
+
+
+def test_loss_compaction_parity(env):
+    """Composite/loss/compaction on fixed network outputs: compaction bit-exact, dL/dout fp16-close."""
+    t, O, tb = env["t"], env["O"], env["tb"]
+    lib, check = L()
+    bf = _bitfield(env)
+    n_rays, max_s = 4096, 4096 * 16
+    rs, ri = 0x0BADF00D12345678, 0xDA3E39CB94B95BDB | 1
+    r_rays, r_ns, r_co, r_cnt, _ = O.generate_samples(env["ds"], bf, n_rays, 0, rs, ri, max_s)
+    nk = int(r_ns[:, 0].sum())
+    net = O.network_forward(env["cfg"], tb.get_params(), r_co[:nk], 14)
+    rng = np.random.default_rng(7)
+    net = net.view(np.float16).copy()
+    net[:, 3] = rng.normal(0.0, 0.05, nk).astype(np.float16)  # sdf spread so alphas vary
+    net[:, 7] = np.float16(0.35)
+    net = net.view(np.uint16)
+    for max_c in (BATCH, 2000):
+        nsd = dev(t, r_ns)
+        co = t.zeros((max_c, 7), dtype=t.float32, device="cuda")
+        dlo = t.zeros((max_c, 16), dtype=t.int16, device="cuda")
+        loss = t.zeros(n_rays, dtype=t.float32, device="cuda"); ek = t.zeros_like(loss); mk = t.zeros_like(loss)
+        cnt = (C.c_uint32 * 1)()
+        check(lib.neus_loss_compact(tb.handle, None, C.c_uint32(n_rays), C.c_uint32(0), C.c_uint32(1), C.c_uint32(0),
+                                    C.c_uint64(rs), C.c_uint64(ri), C.c_uint32(max_c), ptr(dev(t, r_rays)), ptr(nsd),
+                                    ptr(dev(t, r_co)), ptr(dev(t, net)), ptr(co), ptr(dlo), ptr(loss), ptr(ek), ptr(mk), cnt))
+        ref = O.compute_loss(env["ds"], n_rays, 0, rs, ri, max_c, r_rays, r_ns, r_co, net)
+        assert cnt[0] == ref["counter"]
+        np.testing.assert_array_equal(host(nsd, np.uint32), ref["numsteps"])
+        nc = min(ref["counter"], max_c)
+        np.testing.assert_array_equal(host(co, np.uint32)[:nc], ref["coords"].view(np.uint32)[:nc])
+        g = host(dlo, np.float16).astype(np.float32)[:nc, :11]
+        r = ref["dL_dout"].view(np.float16).astype(np.float32)[:nc, :11]
+        np.testing.assert_allclose(g, r, rtol=2e-3, atol=1e-6)
+        np.testing.assert_allclose(loss.cpu().numpy(), ref["loss"], rtol=1e-4, atol=1e-9)
+
+
+def test_train_steps_reduce_loss(env):
+    """End-to-end Testbed::train on the small synthetic scene: loss decreases, state consistent."""
+    from neus2_amd import pyngp
+    sc = env["sc"]
+    tb = pyngp.Testbed(pyngp.TestbedMode.Nerf)
+    tb.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
+    tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=BATCH)
+    tb.train(1)
+    l0 = tb.stats()["last_loss"]
+    tb.train(200)
+    st = tb.stats()
+    assert st["training_step"] == 201
+    assert np.isfinite(st["last_loss"]) and st["last_loss"] < l0, (l0, st)
+    assert st["measured_batch_size"] > 0
