@@ -95,11 +95,15 @@ typedef struct NeusTrainStats {
 	float mask_loss;
 	float last_loss;                          /* last raw loss scalar */
 	float density_grid_mean;
+	float ray_loss;                           /* mean Huber loss over the rays that had samples (last logged step) */
+	uint32_t n_rays_with_samples;             /* rays kept by the sampler in the last logged step */
 } NeusTrainStats;
 
 typedef struct NeusNetLayout {
 	uint64_t n_params, n_density, n_rgb, grid_offset, n_grid_params, variance_offset, n_matrix;
 	uint32_t density_input_width, rgb_input_width;
+	float per_level_scale;           /* derived per_level_scale actually used (testbed.cu:2185) */
+	uint32_t n_levels;
 } NeusNetLayout;
 
 const char* neus_last_error(void);
@@ -123,11 +127,16 @@ int neus_testbed_set_density_grid(NeusTestbed* tb, const float* grid /*nullable*
 int neus_testbed_get_rng(NeusTestbed* tb, uint64_t* state_inc /*4: rng, density_grid_rng*/);
 int neus_testbed_stream(NeusTestbed* tb, void** hip_stream);
 int neus_testbed_synchronize(NeusTestbed* tb);
-/* Per-phase step timing with hipEvents on the testbed stream (profiling on): ms_out[0..6] =
- * occupancy update, ray sampling, inference encode, inference MLP, loss+compaction, backward,
- * all-reduce+optimizer (mean ms per step); ms_out[7] = number of profiled steps. */
+/* Per-phase step timing with hipEvents recorded on the testbed stream (profiling on), mean ms per step:
+ * ms_out[0] occupancy update, [1] ray sampling (march count/scan/write), [2] inference hash-grid encode,
+ * [3] inference MLP, [4] loss + compaction + rollover, [5] training hash-grid encode, [6] fused MLP
+ * fwd/bwd/2nd-order, [7] weight-gradient GEMMs, [8] hash-grid gradient scatter, [9] all-reduce + counters,
+ * [10] Ema(Adam); ms_out[NEUS_N_PHASES] = number of profiled steps, [+1] mean pre-compaction samples per
+ * step (the inference kernels' n), [+2] mean compacted training samples per step. Phases 2, 3, 5-8 are
+ * single kernels. */
+#define NEUS_N_PHASES 11
 int neus_testbed_set_profiling(NeusTestbed* tb, int on);
-int neus_testbed_kernel_times(NeusTestbed* tb, float* ms_out /* 8 entries */);
+int neus_testbed_kernel_times(NeusTestbed* tb, float* ms_out /* NEUS_N_PHASES + 3 entries */);
 
 /* ------------------------------------------------------------------ data parallel (RCCL over xGMI) */
 int neus_nccl_unique_id(uint8_t* out /* 128 bytes */);

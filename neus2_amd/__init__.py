@@ -3,14 +3,7 @@
 Product path: libneus2_hip.so (hand-written HIP kernels + C++ Testbed + C-ABI, include/neus2_hip.h),
 driven through the pyngp mirror in neus2_amd.pyngp. There is no CPU fallback.
 """
-from . import config, scenes  # noqa: F401
+from . import config, pyngp, scenes  # noqa: F401
 from ._lib import LIB_PATH, NeusError, lib  # noqa: F401
 
 __all__ = ["config", "scenes", "lib", "LIB_PATH", "NeusError", "pyngp"]
-
-
-def __getattr__(name):
-    if name == "pyngp":
-        from . import pyngp
-        return pyngp
-    raise AttributeError(name)

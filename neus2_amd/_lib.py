@@ -37,7 +37,8 @@ class NeusTrainStats(C.Structure):
         ("training_step", C.c_uint32), ("rays_per_batch", C.c_uint32), ("measured_batch_size", C.c_uint32),
         ("measured_batch_size_before_compaction", C.c_uint32), ("n_rays_total", C.c_uint32), ("valid_level", C.c_uint32),
         ("zero_records", C.c_uint32), ("loss", C.c_float), ("ek_loss", C.c_float), ("mask_loss", C.c_float),
-        ("last_loss", C.c_float), ("density_grid_mean", C.c_float),
+        ("last_loss", C.c_float), ("density_grid_mean", C.c_float), ("ray_loss", C.c_float),
+        ("n_rays_with_samples", C.c_uint32),
     ]
 
 
@@ -46,6 +47,7 @@ class NeusNetLayout(C.Structure):
         ("n_params", C.c_uint64), ("n_density", C.c_uint64), ("n_rgb", C.c_uint64), ("grid_offset", C.c_uint64),
         ("n_grid_params", C.c_uint64), ("variance_offset", C.c_uint64), ("n_matrix", C.c_uint64),
         ("density_input_width", C.c_uint32), ("rgb_input_width", C.c_uint32),
+        ("per_level_scale", C.c_float), ("n_levels", C.c_uint32),
     ]
 
 

@@ -102,7 +102,8 @@ struct NeusTestbed {
 	uint32_t adam_step = 0;
 	float lr_factor = 1.f;
 	// stats
-	float loss_scalar_ema = 0.f, last_loss = 0.f, ek_loss = 0.f, mask_loss = 0.f;
+	float loss_scalar_ema = 0.f, last_loss = 0.f, ek_loss = 0.f, mask_loss = 0.f, ray_loss = 0.f;
+	uint32_t last_rays_with_samples = 0;
 	bool loss_ema_init = false;
 	float* pinned = nullptr;  // [0..3]: loss sum, ek sum, mask sum, grid mean ; [4..]: StepState copy
 	bool loss_pending = false;
@@ -111,9 +112,10 @@ struct NeusTestbed {
 	uint32_t rank = 0, world = 1;
 	// profiling
 	bool profiling = false;
-	static constexpr int N_PHASES = 8;
+	static constexpr int N_PHASES = NEUS_N_PHASES;
 	hipEvent_t ev[N_PHASES + 1] = {};
 	double phase_ms[N_PHASES] = {};
+	double phase_npre = 0, phase_ntrain = 0;
 	uint32_t phase_steps = 0;
 
 	NeusTestbed(int dev) : device(dev) {
@@ -361,14 +363,17 @@ struct NeusTestbed {
 	}
 	// forward recompute + backward into g (fp32 [P], zeroed by the caller)
 	void net_backward(const uint32_t* n_valid_ptr, const uint32_t* n_train_ptr, uint32_t n, const float* c, uint32_t valid,
-	                  const half_t* dlo, float* g, hipStream_t s) {
+	                  const half_t* dlo, float* g, hipStream_t s, bool marks = false) {
 		const uint32_t ld = n;
 		encode(n_train_ptr, n, n, ld, c, COORD_W, valid, true, s);
+		if (marks) mark(6);
 		TrainBufs t = tbuf;
 		t.var_grad = g + lay.var_off;
 		launch_mlp_train(s, lay.L, lay.W, n_valid_ptr, n, ld, c, (const half_t*)enc.p, dydx.p, dlo, mlp, t);
+		if (marks) mark(7);
 		WGradJobs J = wgrad_jobs(n, ld, g, n_train_ptr);
 		launch_wgrad(s, J, J.block_start[5]);
+		if (marks) mark(8);
 		const uint32_t gx = std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, 2048));
 		launch_grid_scatter(s, n_train_ptr, n, ld, c, COORD_W, gl, valid, tbuf.dLdenc, tbuf.genc, tbuf.v, g + lay.grid_off, gx);
 	}
@@ -459,10 +464,10 @@ struct NeusTestbed {
 		launch_loss_write(s, MAX_RAYS, st.p, dp, ds, lp, rays.p, numsteps.p, coords.p, net_out.p, ccount.p, cbase.p, coords_c.p, dL_dout.p,
 		                  loss.p, ek.p, mask.p);
 		launch_rollover(s, batch, st.p, coords_c.p, dL_dout.p);
-		mark(5);
 		HIP_CHECK(hipMemsetAsync(grads.p, 0, (size_t)lay.P * 4, s));
-		net_backward(&st.p->compacted_counter, &st.p->n_train, batch, coords_c.p, valid, dL_dout.p, grads.p, s);
-		mark(6);
+		mark(5);
+		net_backward(&st.p->compacted_counter, &st.p->n_train, batch, coords_c.p, valid, dL_dout.p, grads.p, s, true);
+		mark(9);
 		if (world > 1) {
 			NCCL_CHECK(ncclGroupStart());
 			NCCL_CHECK(ncclAllReduce(grads.p, grads.p, lay.P, ncclFloat32, ncclSum, comm, s));
@@ -480,20 +485,25 @@ struct NeusTestbed {
 		}
 		launch_step_counters(s, st.p, batch, max_samples, world, cfg.fixed_rays_per_batch);
 		rng.advance();
+		mark(10);
 		// ---- optimizer (testbed_nerf.cu:3503-3508)
 		optimizer_step(grads.p);
-		mark(7);
+		mark(11);
 		++training_step;
 		if (profiling) accumulate_phases();
 	}
 
 	void accumulate_phases() {
-		HIP_CHECK(hipEventSynchronize(ev[7]));
-		for (int i = 0; i < 7; ++i) {
+		HIP_CHECK(hipEventSynchronize(ev[N_PHASES]));
+		for (int i = 0; i < N_PHASES; ++i) {
 			float ms = 0.f;
 			HIP_CHECK(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
 			phase_ms[i] += ms;
 		}
+		StepState h{};
+		HIP_CHECK(hipMemcpy(&h, st.p, sizeof(StepState), hipMemcpyDeviceToHost));
+		phase_npre += h.n_kept;
+		phase_ntrain += std::min(h.compacted_counter / std::max(1u, world), batch);
 		++phase_steps;
 	}
 
@@ -506,6 +516,8 @@ struct NeusTestbed {
 		last_loss = pinned[0] * scale;
 		ek_loss = pinned[1] * scale;
 		mask_loss = pinned[2] * scale;
+		last_rays_with_samples = sst->n_rays_with_samples;
+		ray_loss = sst->n_rays_with_samples ? pinned[0] * (float)(sst->rays_per_batch * world) / (float)sst->n_rays_with_samples : 0.f;
 		if (!loss_ema_init) { loss_scalar_ema = last_loss; loss_ema_init = true; }
 		else loss_scalar_ema = 0.99f * loss_scalar_ema + 0.01f * last_loss;
 		loss_pending = false;
@@ -541,6 +553,7 @@ int neus_testbed_layout(NeusTestbed* tb, NeusNetLayout* o) {
 		const Layout& l = tb->lay;
 		o->n_params = l.P; o->n_density = l.n_density; o->n_rgb = l.n_rgb; o->grid_offset = l.grid_off; o->n_grid_params = l.n_grid;
 		o->variance_offset = l.var_off; o->n_matrix = l.n_matrix; o->density_input_width = l.din; o->rgb_input_width = 48;
+		o->per_level_scale = tb->cfg.per_level_scale; o->n_levels = l.L;
 	});
 }
 int neus_testbed_train(NeusTestbed* tb, uint32_t n_steps) {
@@ -562,6 +575,7 @@ int neus_testbed_get_stats(NeusTestbed* tb, NeusTrainStats* o) {
 		o->valid_level = tb->valid_level_at((int)tb->training_step); o->zero_records = s.zero_records;
 		o->loss = tb->loss_scalar_ema; o->ek_loss = tb->ek_loss; o->mask_loss = tb->mask_loss; o->last_loss = tb->last_loss;
 		o->density_grid_mean = mean;
+		o->ray_loss = tb->ray_loss; o->n_rays_with_samples = tb->last_rays_with_samples;
 	});
 }
 static int copy_param_vec(NeusTestbed* tb, const float* dev, float* host, uint64_t n) {
@@ -604,12 +618,14 @@ int neus_testbed_get_rng(NeusTestbed* tb, uint64_t* o) {
 int neus_testbed_stream(NeusTestbed* tb, void** s) { return guard([&] { *s = (void*)tb->stream; }); }
 int neus_testbed_synchronize(NeusTestbed* tb) { return guard([&] { HIP_CHECK(hipStreamSynchronize(tb->stream)); }); }
 int neus_testbed_set_profiling(NeusTestbed* tb, int on) {
-	return guard([&] { tb->profiling = on != 0; for (auto& m : tb->phase_ms) m = 0; tb->phase_steps = 0; });
+	return guard([&] { tb->profiling = on != 0; for (auto& m : tb->phase_ms) m = 0; tb->phase_steps = 0; tb->phase_npre = tb->phase_ntrain = 0; });
 }
 int neus_testbed_kernel_times(NeusTestbed* tb, float* ms) {
 	return guard([&] {
 		for (int i = 0; i < NeusTestbed::N_PHASES; ++i) ms[i] = tb->phase_steps ? (float)(tb->phase_ms[i] / tb->phase_steps) : 0.f;
-		ms[7] = (float)tb->phase_steps;
+		ms[NeusTestbed::N_PHASES] = (float)tb->phase_steps;
+		ms[NeusTestbed::N_PHASES + 1] = tb->phase_steps ? (float)(tb->phase_npre / tb->phase_steps) : 0.f;
+		ms[NeusTestbed::N_PHASES + 2] = tb->phase_steps ? (float)(tb->phase_ntrain / tb->phase_steps) : 0.f;
 	});
 }
 

@@ -151,6 +151,11 @@ class _Nerf:
         self.training = _Training(tb)
 
 
+# neus_testbed_kernel_times order (include/neus2_hip.h NEUS_N_PHASES)
+PHASES = ["occupancy", "sample", "inference_encode", "inference_mlp", "loss", "train_encode", "mlp_train", "wgrad",
+          "grid_scatter", "allreduce", "optimizer"]
+
+
 class Testbed:
     """pyngp.Testbed (python_api.cu:216-600), NeuS2 training subset."""
 
@@ -215,6 +220,7 @@ class Testbed:
         geo = geometric_init if geometric_init is not None else geometric_init_weights(c.n_levels, c.n_neurons)
         geo = np.ascontiguousarray(geo, np.float32)
         check(lib().neus_testbed_reload_network(self._h, C.byref(c), C.c_void_p(geo.ctypes.data)))
+        c.per_level_scale = self.layout()["per_level_scale"]
         self._net_cfg = c
         self._cfg_dict = cfg
         self._geo = geo
@@ -262,10 +268,11 @@ class Testbed:
         check(lib().neus_testbed_set_profiling(self._h, C.c_int(1 if on else 0)))
 
     def phase_times(self):
-        a = (C.c_float * 8)()
+        """Mean ms per profiled step for each of PHASES, plus (n_steps, mean Npre, mean Ntrain)."""
+        n = len(PHASES)
+        a = (C.c_float * (n + 3))()
         check(lib().neus_testbed_kernel_times(self._h, a))
-        keys = ["occupancy", "sample", "inference_encode", "inference_mlp", "loss", "backward", "optimizer"]
-        return dict(zip(keys, list(a)[:7])), int(a[7])
+        return dict(zip(PHASES, list(a)[:n])), dict(steps=int(a[n]), npre=float(a[n + 1]), ntrain=float(a[n + 2]))
 
     # ------------------------------------------------------------------ state access
     def get_params(self):

@@ -784,7 +784,8 @@ static inline void random_image_pos(pcg32& rng, int rx, int ry, float& x, float&
 struct RayGen { uint32_t n; float o[3], du[3], dir[3], startt, cone; bool valid; };
 
 static RayGen gen_ray(const OrDataset* ds, const uint8_t* bitfield, uint32_t i, uint32_t n_rays_global, uint32_t n_rays_total, pcg32 rng) {
-	RayGen g; g.valid = false; g.n = 0;
+	RayGen g; g.valid = false; g.n = 0; g.startt = 0.f; g.cone = ds->cone_angle;
+	for (int k = 0; k < 3; ++k) { g.o[k] = 0.f; g.du[k] = 0.f; g.dir[k] = 0.f; }
 	uint32_t img = image_idx(i, n_rays_global, n_rays_total, ds->n_images);
 	const int rx = ds->resolution[2 * img], ry = ds->resolution[2 * img + 1];
 	rng.advance((int64_t)(uint32_t)(i * N_MAX_RANDOM_SAMPLES_PER_RAY));

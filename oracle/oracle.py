@@ -55,6 +55,7 @@ def lib():
 
 
 def P(a):
+    """Raw pointer to a numpy buffer. The caller must hold a reference to `a` for the duration of the call."""
     return C.c_void_p(a.ctypes.data) if a is not None else C.c_void_p(0)
 
 
@@ -120,7 +121,8 @@ def grid_forward(cfg, params, pos, valid_level, want_dydx=True):
     L = cfg.n_levels
     enc = np.zeros((n, 2 * L), np.float32)
     dydx = np.zeros((n, 2 * L, 3), np.float32) if want_dydx else None
-    lib().or_grid_forward(C.byref(cfg), P(f32(params)), C.c_uint32(n), P(pos), C.c_uint32(valid_level), P(enc), P(dydx))
+    params = f32(params)
+    lib().or_grid_forward(C.byref(cfg), P(params), C.c_uint32(n), P(pos), C.c_uint32(valid_level), P(enc), P(dydx))
     return enc, dydx
 
 
@@ -128,7 +130,8 @@ def network_forward(cfg, params, coords, valid_level):
     coords = f32(coords)
     n = coords.shape[0]
     out = np.zeros((n, 16), np.uint16)
-    lib().or_network_forward(C.byref(cfg), P(f32(params)), C.c_uint32(n), P(coords), C.c_uint32(valid_level), P(out))
+    params = f32(params)
+    lib().or_network_forward(C.byref(cfg), P(params), C.c_uint32(n), P(coords), C.c_uint32(valid_level), P(out))
     return out
 
 
@@ -137,7 +140,8 @@ def network_backward(cfg, params, coords, valid_level, dL_dout_u16, indeed_batch
     n = coords.shape[0]
     grads = np.zeros(layout(cfg)["n_params"], np.float32)
     d = np.ascontiguousarray(dL_dout_u16, np.uint16)
-    lib().or_network_backward(C.byref(cfg), P(f32(params)), C.c_uint32(n), P(coords), C.c_uint32(valid_level), P(d),
+    params = f32(params)
+    lib().or_network_backward(C.byref(cfg), P(params), C.c_uint32(n), P(coords), C.c_uint32(valid_level), P(d),
                               C.c_uint32(indeed_batch_size), P(grads))
     return grads
 
@@ -173,7 +177,8 @@ def generate_samples(ds, bitfield, n_rays, n_rays_total, rng_state, rng_inc, max
     numsteps = np.zeros((n_rays, 2), np.uint32)
     coords = np.zeros((max_samples, 7), np.float32)
     nr = C.c_uint32(0)
-    counter = lib().or_generate_samples(C.byref(ds.c), P(np.ascontiguousarray(bitfield, np.uint8)), C.c_uint32(n_rays),
+    bitfield = np.ascontiguousarray(bitfield, np.uint8)
+    counter = lib().or_generate_samples(C.byref(ds.c), P(bitfield), C.c_uint32(n_rays),
                                         C.c_uint32(ray_offset), C.c_uint32(n_rays_global), C.c_uint32(n_rays_total),
                                         C.c_uint64(rng_state), C.c_uint64(rng_inc), C.c_uint32(max_samples),
                                         P(rays), P(numsteps), P(coords), C.byref(nr))
@@ -189,9 +194,10 @@ def compute_loss(ds, n_rays, n_rays_total, rng_state, rng_inc, max_compacted, ra
     loss = np.zeros(n_rays, np.float32)
     ek = np.zeros(n_rays, np.float32)
     mask = np.zeros(n_rays, np.float32)
+    rays, coords, net_out = f32(rays), f32(coords), np.ascontiguousarray(net_out, np.uint16)
     counter = lib().or_compute_loss(C.byref(ds.c), C.c_uint32(n_rays), C.c_uint32(ray_offset), C.c_uint32(n_rays_global),
                                     C.c_uint32(n_rays_total), C.c_uint64(rng_state), C.c_uint64(rng_inc), C.c_uint32(max_compacted),
-                                    P(f32(rays)), P(numsteps), P(f32(coords)), P(np.ascontiguousarray(net_out, np.uint16)),
+                                    P(rays), P(numsteps), P(coords), P(net_out),
                                     C.c_float(loss_scale), C.c_float(mean_density), C.c_float(ek_w), C.c_float(mask_w),
                                     C.c_float(cos_anneal), P(coords_out), P(dout), P(loss), P(ek), P(mask))
     return dict(numsteps=numsteps, coords=coords_out, dL_dout=dout, loss=loss, ek=ek, mask=mask, counter=int(counter))
@@ -203,16 +209,18 @@ def fill_rollover(n_elements, n_in, coords, dout):
 
 def adam_ema_step(weights, grads, m1, m2, steps, ema_tmp, ema_out, n_matrix, optimizer_step, lr=1e-3, beta1=0.9,
                   beta2=0.99, eps=1e-15, l2=1e-6, loss_scale=128.0, ema_decay=0.95):
+    grads = f32(grads)
     lib().or_adam_ema_step(C.c_uint32(weights.size), C.c_uint32(n_matrix), C.c_float(loss_scale), C.c_float(lr),
                            C.c_float(beta1), C.c_float(beta2), C.c_float(eps), C.c_float(l2), C.c_uint32(optimizer_step),
-                           C.c_float(ema_decay), P(weights), P(f32(grads)), P(m1), P(m2), P(steps), P(ema_tmp), P(ema_out))
+                           C.c_float(ema_decay), P(weights), P(grads), P(m1), P(m2), P(steps), P(ema_tmp), P(ema_out))
 
 
 def density_grid_update(cfg, params, valid_level, n_uniform, n_nonuniform, ema_step, rng_state, rng_inc, density_grid,
                         bitfield, decay=0.95, aabb_min=(0, 0, 0), aabb_max=(1, 1, 1)):
     st = C.c_uint64(rng_state)
     mean = C.c_float(0)
-    lib().or_density_grid_update(C.byref(cfg), P(f32(params)), C.c_uint32(valid_level), P(f32(aabb_min)), P(f32(aabb_max)),
+    params, amin, amax = f32(params), f32(aabb_min), f32(aabb_max)  # keep the buffers alive across the call
+    lib().or_density_grid_update(C.byref(cfg), P(params), C.c_uint32(valid_level), P(amin), P(amax),
                                  C.c_uint32(n_uniform), C.c_uint32(n_nonuniform), C.c_uint32(ema_step), C.c_float(decay),
                                  C.byref(st), C.c_uint64(rng_inc), P(density_grid), P(bitfield), C.byref(mean))
     return int(st.value), float(mean.value)

@@ -26,3 +26,13 @@ def torch_cuda():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch
+
+
+@pytest.fixture(autouse=True)
+def _release_device_buffers():
+    yield
+    try:
+        import gpu_util
+        gpu_util.release()
+    except Exception:
+        pass

@@ -4,8 +4,22 @@ import ctypes as C
 import numpy as np
 
 
+_KEEP = []
+
+
 def dev(t, a):
-    """numpy -> torch cuda tensor with the same bytes."""
+    """numpy -> torch cuda tensor with the same bytes. The tensor is kept alive until release()
+    so that an inline `ptr(dev(...))` cannot hand a freed (and reused) block to a kernel."""
+    x = _dev(t, a)
+    _KEEP.append(x)
+    return x
+
+
+def release():
+    _KEEP.clear()
+
+
+def _dev(t, a):
     a = np.ascontiguousarray(a)
     if a.dtype == np.float16 or a.dtype == np.uint16:
         return t.from_numpy(a.view(np.int16).copy()).cuda()
