@@ -888,6 +888,19 @@ uint32_t or_generate_samples(const OrDataset* ds, const uint8_t* bitfield, uint3
 // -------------------------------------------------------------------------------------------
 struct LossRay { uint32_t ncomp; };
 
+// Target pixel (sRGB) over a random background and the background itself (testbed_nerf.cu:1632-1660).
+static void ray_target(const OrDataset* ds, uint32_t ray_idx_global, uint32_t n_rays_global, uint32_t n_rays_total, pcg32 rng,
+                       float target[3], float bg[3], float tex[4]) {
+	rng.advance((int64_t)(uint32_t)(ray_idx_global * N_MAX_RANDOM_SAMPLES_PER_RAY));
+	uint32_t img = image_idx(ray_idx_global, n_rays_global, n_rays_total, ds->n_images);
+	const int rx = ds->resolution[2 * img], ry = ds->resolution[2 * img + 1];
+	float xy_x, xy_y; random_image_pos(rng, rx, ry, xy_x, xy_y);
+	bg[0] = rng.next_float(); bg[1] = rng.next_float(); bg[2] = rng.next_float();
+	for (int k = 0; k < 3; ++k) bg[k] = srgb_to_linear(bg[k]);
+	read_rgba_x_alpha(ds, img, xy_x, xy_y, tex);
+	for (int k = 0; k < 3; ++k) { target[k] = 1.0f * tex[k] + (1.0f - tex[3]) * bg[k]; target[k] = linear_to_srgb(target[k]); bg[k] = linear_to_srgb(bg[k]); }
+}
+
 static void loss_ray(const OrDataset* ds, uint32_t i, uint32_t ray_idx_global, uint32_t n_rays_global, uint32_t n_rays_total, pcg32 rng,
                      const float* ray, const uint32_t numsteps, const float* coords_in, const uint16_t* net_out,
                      uint32_t compacted_base, uint32_t compacted_numsteps_cap, bool write, float loss_scale_orig,
@@ -938,15 +951,8 @@ static void loss_ray(const OrDataset* ds, uint32_t i, uint32_t ray_idx_global, u
 	*ncomp_out = cn;
 	if (!write) return;
 
-	rng.advance((int64_t)(uint32_t)(ray_idx_global * N_MAX_RANDOM_SAMPLES_PER_RAY));
-	uint32_t img = image_idx(ray_idx_global, n_rays_global, n_rays_total, ds->n_images);
-	const int rx = ds->resolution[2 * img], ry = ds->resolution[2 * img + 1];
-	float xy_x, xy_y; random_image_pos(rng, rx, ry, xy_x, xy_y);
-	float bg[3]; bg[0] = rng.next_float(); bg[1] = rng.next_float(); bg[2] = rng.next_float();
-	for (int k = 0; k < 3; ++k) bg[k] = srgb_to_linear(bg[k]);
-	float tex[4]; read_rgba_x_alpha(ds, img, xy_x, xy_y, tex);
-	float target[3];
-	for (int k = 0; k < 3; ++k) { target[k] = 1.0f * tex[k] + (1.0f - tex[3]) * bg[k]; target[k] = linear_to_srgb(target[k]); bg[k] = linear_to_srgb(bg[k]); }
+	float target[3], bg[3], tex[4];
+	ray_target(ds, ray_idx_global, n_rays_global, n_rays_total, rng, target, bg, tex);
 	if (cn == numsteps) for (int k = 0; k < 3; ++k) rgb_ray[k] += T * bg[k];
 
 	uint32_t comp = std::min(compacted_numsteps_cap - std::min(compacted_numsteps_cap, compacted_base), cn);
@@ -1043,6 +1049,13 @@ static void loss_ray(const OrDataset* ds, uint32_t i, uint32_t ray_idx_global, u
 		for (int k = 0; k < 16; ++k) dout[16 * (size_t)j + k] = f2h(dl[k]);
 	}
 	ek_out[0] /= (float)comp * (float)n_rays_global;
+}
+
+void or_ray_target(const OrDataset* ds, uint32_t ray_idx_global, uint32_t n_rays_global, uint32_t n_rays_total, uint64_t rng_state,
+                   uint64_t rng_inc, float* target_srgb, float* bg_srgb) {
+	pcg32 rng; rng.state = rng_state; rng.inc = rng_inc;
+	float tex[4];
+	ray_target(ds, ray_idx_global, n_rays_global, n_rays_total, rng, target_srgb, bg_srgb, tex);
 }
 
 uint32_t or_compute_loss(const OrDataset* ds, uint32_t n_rays, uint32_t ray_offset, uint32_t n_rays_global, uint32_t n_rays_total,

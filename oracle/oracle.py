@@ -203,6 +203,14 @@ def compute_loss(ds, n_rays, n_rays_total, rng_state, rng_inc, max_compacted, ra
     return dict(numsteps=numsteps, coords=coords_out, dL_dout=dout, loss=loss, ek=ek, mask=mask, counter=int(counter))
 
 
+def ray_target(ds, ray_idx_global, n_rays_global, n_rays_total, rng_state, rng_inc):
+    t = np.zeros(3, np.float32)
+    b = np.zeros(3, np.float32)
+    lib().or_ray_target(C.byref(ds.c), C.c_uint32(ray_idx_global), C.c_uint32(n_rays_global), C.c_uint32(n_rays_total),
+                        C.c_uint64(rng_state), C.c_uint64(rng_inc), P(t), P(b))
+    return t, b
+
+
 def fill_rollover(n_elements, n_in, coords, dout):
     lib().or_fill_rollover(C.c_uint32(n_elements), C.c_uint32(n_in), P(coords), P(dout))
 

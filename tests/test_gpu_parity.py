@@ -102,6 +102,8 @@ def test_grid_encode_parity(env):
         gi, ri = got.astype(np.float16).view(np.int16).astype(np.int32), ref.astype(np.float16).view(np.int16).astype(np.int32)
         same = np.sign(got) == np.sign(ref)
         ulps = np.where(same, np.abs(gi - ri), 0)
+        os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+        np.savez(os.path.join(ROOT, "gpurun_out", f"grid_diag_{valid}.npz"), c=c, got=got, gdy=gdy, ref=ref, rdy=rdy)
         np.testing.assert_allclose(gdy, rdy, rtol=1e-4, atol=1e-6)
         bad = np.argwhere(ulps > 1)
         info = [(int(i), int(k), float(got[i, k]), float(ref[i, k])) for i, k in bad[:6]]
