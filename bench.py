@@ -101,14 +101,14 @@ def main():
             dist.barrier()
 
     t0 = time.time()
-    tb.train(args.warmup)
+    tb.train_steps(args.warmup)
     barrier()
     warm_s = time.time() - t0
     # timed region
     tb.set_profiling(False)
     barrier()
     t1 = time.perf_counter()
-    tb.train(args.steps)
+    tb.train_steps(args.steps)
     barrier()
     elapsed = time.perf_counter() - t1
     if world > 1:
@@ -121,7 +121,7 @@ def main():
     # step is launched on), over a separate profiled pass of the same workload
     n_prof = max(4, min(32, args.steps // 4))
     tb.set_profiling(True)
-    tb.train(n_prof)
+    tb.train_steps(n_prof)
     phases, pinfo = tb.phase_times()
     tb.set_profiling(False)
     batch = args.batch

@@ -23,8 +23,9 @@ __device__ __forceinline__ LevelSetup level_setup(const GridLevels& gl, uint32_t
 	const float in[3] = {x, y, z};
 #pragma unroll
 	for (int d = 0; d < 3; ++d) {
-		// pos_fract (common_device.h:404-434), linear interpolation
-		float p = __fmul_rn(in[d], s.scale) + 0.5f;
+		// pos_fract (common_device.h:404-434), linear interpolation. `input * scale + 0.5f` is one
+		// expression that nvcc (--fmad=true, the default) emits as a single FFMA: fused here too.
+		float p = __builtin_fmaf(in[d], s.scale, 0.5f);
 		float fl = floorf(p);
 		s.g[d] = (uint32_t)(int)fl;
 		s.pos[d] = p - fl;
@@ -62,16 +63,17 @@ __global__ void __launch_bounds__(256) k_grid_encode(
 			const uint32_t e = grid_index(s.hsize, s.res, gx, gy, gz);
 			v[idx] = *(const h2*)(gp + 2 * (size_t)e);
 		}
-		float r0 = 0.f, r1 = 0.f;
+		// fp16 accumulation of fp16-rounded terms, as the reference (result[f] += (T)(weight * data))
+		half_t r0 = (half_t)0.f, r1 = (half_t)0.f;
 #pragma unroll
 		for (uint32_t idx = 0; idx < 8; ++idx) {
 			float w = 1.f;
 #pragma unroll
 			for (int d = 0; d < 3; ++d) w *= (idx & (1u << d)) ? s.pos[d] : 1.f - s.pos[d];
-			r0 += w * (float)v[idx][0];
-			r1 += w * (float)v[idx][1];
+			r0 = (half_t)((float)r0 + (float)(half_t)(w * (float)v[idx][0]));
+			r1 = (half_t)((float)r1 + (float)(half_t)(w * (float)v[idx][1]));
 		}
-		h2 out; out[0] = (half_t)r0; out[1] = (half_t)r1;
+		h2 out; out[0] = r0; out[1] = r1;
 		enc[(size_t)l * ld + i] = *(uint32_t*)&out;
 		if (dydx) {
 			float gr[2][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
@@ -87,8 +89,8 @@ __global__ void __launch_bounds__(256) k_grid_encode(
 						if (idx & (1u << ngd)) { w *= s.pos[d]; cl |= 1u << d; } else { w *= 1.f - s.pos[d]; }
 					}
 					const uint32_t cr = cl | (1u << gd);
-					gr[0][gd] += w * ((float)v[cr][0] - (float)v[cl][0]);
-					gr[1][gd] += w * ((float)v[cr][1] - (float)v[cl][1]);
+					gr[0][gd] = __builtin_fmaf(w, (float)v[cr][0] - (float)v[cl][0], gr[0][gd]);
+					gr[1][gd] = __builtin_fmaf(w, (float)v[cr][1] - (float)v[cl][1], gr[1][gd]);
 				}
 			}
 #pragma unroll

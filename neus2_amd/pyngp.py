@@ -232,15 +232,30 @@ class Testbed:
 
     # ------------------------------------------------------------------ training
     def frame(self):
-        """Testbed::frame (testbed.cu:1722-1783) without GUI: one training step while shall_train."""
-        if self.shall_train:
-            if self.max_training_steps is not None and self.training_step >= self.max_training_steps:
-                self.shall_train = False
-                return False
-            self.train(1)
+        """Testbed::frame (testbed.cu:1722-1783) without GUI or rendering: one training step
+        (train_and_render -> train(m_training_batch_size)) while shall_train; a static scene stops
+        at hyperparams.first_frame_max_training_step (testbed.cu:1752-1758). Returns False when done."""
+        if not self.shall_train:
+            return False
+        limit = self.max_training_steps
+        if limit is None and self._cfg_dict is not None:
+            limit = self._cfg_dict.get("hyperparams", {}).get("first_frame_max_training_step")
+        if limit is not None and self.training_step >= int(limit):
+            self.shall_train = False
+            return False
+        self.train_steps(1)
         return True
 
-    def train(self, n_steps: int = 1):
+    def train(self, batch_size: int | None = None):
+        """Testbed::train(batch_size) (testbed.cu:2640-2736): ONE training step targeting `batch_size`
+        compacted samples. The device workspace is sized at reload_network_* time for the configured
+        batch; a different batch_size raises (call reload_network_from_json with batch_size=...)."""
+        if batch_size is not None and self._net_cfg is not None and int(batch_size) != int(self._net_cfg.batch_size):
+            raise NeusError(f"train({batch_size}): the network was configured for batch_size={self._net_cfg.batch_size}")
+        self.train_steps(1)
+
+    def train_steps(self, n_steps: int = 1):
+        """n consecutive Testbed::train steps in one call (no host synchronisation in between)."""
         check(lib().neus_testbed_train(self._h, C.c_uint32(n_steps)))
 
     def stats(self):

@@ -324,7 +324,7 @@ static inline LevelPos level_pos(const Net& n, uint32_t l, const float x[3]) {
 	LevelPos lp;
 	lp.scale = n.scale[l]; lp.res = n.res[l]; lp.off = n.off[l]; lp.hsize = n.off[l + 1] - n.off[l];
 	for (int d = 0; d < 3; ++d) {
-		float p = x[d] * lp.scale + 0.5f;
+		float p = std::fmaf(x[d], lp.scale, 0.5f);  // nvcc contracts `input * scale + 0.5f` to one FFMA
 		int tmp = (int)std::floor(p);
 		lp.grid[d] = (uint32_t)tmp;
 		lp.pos[d] = p - (float)tmp;
@@ -351,9 +351,10 @@ static void grid_forward_one(const Net& n, const float* gparams, const float x[3
 				else { w *= lp.pos[d]; pl[d] = lp.grid[d] + 1; }
 			}
 			uint32_t i = grid_index(lp.hsize, lp.res, pl);
-			r0 += w * g[i]; r1 += w * g[i + 1];
+			// the reference accumulates in the grid's precision: result[f] += (T)(weight * data), T = __half
+			r0 = rh(r0 + rh(w * g[i])); r1 = rh(r1 + rh(w * g[i + 1]));
 		}
-		enc[2 * l] = rh(r0); enc[2 * l + 1] = rh(r1);
+		enc[2 * l] = r0; enc[2 * l + 1] = r1;
 		if (dydx) {
 			float gr[2][3] = {{0, 0, 0}, {0, 0, 0}};
 			for (int gd = 0; gd < 3; ++gd) {
@@ -366,8 +367,9 @@ static void grid_forward_one(const Net& n, const float* gparams, const float x[3
 					}
 					pl[gd] = lp.grid[gd]; uint32_t il = grid_index(lp.hsize, lp.res, pl);
 					pl[gd] = lp.grid[gd] + 1; uint32_t ir = grid_index(lp.hsize, lp.res, pl);
-					gr[0][gd] += w * (g[ir] - g[il]);
-					gr[1][gd] += w * (g[ir + 1] - g[il + 1]);
+					// grads += weight * (right - left) * pos_derivative(=1): one FFMA under nvcc --fmad=true
+					gr[0][gd] = std::fmaf(w, g[ir] - g[il], gr[0][gd]);
+					gr[1][gd] = std::fmaf(w, g[ir + 1] - g[il + 1], gr[1][gd]);
 				}
 			}
 			for (int f = 0; f < 2; ++f) for (int d = 0; d < 3; ++d) dydx[6 * l + 3 * f + d] = gr[f][d];

@@ -83,7 +83,8 @@ def _coords(n, seed=0):
 
 
 def test_grid_encode_parity(env):
-    """Hash-grid forward: enc within 1 fp16 ulp, dy/dx rel 1e-4 (fp32 interpolation, FMA order)."""
+    """Hash-grid forward: enc (fp16-accumulated like the reference) and dy/dx (FMA-accumulated f32)
+    bit-exact against the oracle."""
     t, O, tb = env["t"], env["O"], env["tb"]
     lib, check = L()
     n = 1024
@@ -98,16 +99,10 @@ def test_grid_encode_parity(env):
         got = host(enc, np.float16).astype(np.float32).transpose(1, 0, 2).reshape(n, 2 * Lv)
         gdy = host(dydx, np.float32).reshape(Lv, 2, 3, n).transpose(3, 0, 1, 2).reshape(n, 2 * Lv, 3)
         ref, rdy = O.grid_forward(env["cfg"], params, c[:, :3], valid)
-        # fp16 storage of an fp32 trilinear sum: at most 1 fp16 ulp apart (same sign => int16 distance)
-        gi, ri = got.astype(np.float16).view(np.int16).astype(np.int32), ref.astype(np.float16).view(np.int16).astype(np.int32)
-        same = np.sign(got) == np.sign(ref)
-        ulps = np.where(same, np.abs(gi - ri), 0)
         os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
         np.savez(os.path.join(ROOT, "gpurun_out", f"grid_diag_{valid}.npz"), c=c, got=got, gdy=gdy, ref=ref, rdy=rdy)
-        np.testing.assert_allclose(gdy, rdy, rtol=1e-4, atol=1e-6)
-        bad = np.argwhere(ulps > 1)
-        info = [(int(i), int(k), float(got[i, k]), float(ref[i, k])) for i, k in bad[:6]]
-        assert ulps.max() <= 1 and np.all(np.abs(got - ref)[~same] < 1e-7), (ulps.max(), len(bad), info)
+        np.testing.assert_array_equal(got.view(np.uint32), ref.astype(np.float32).view(np.uint32))
+        np.testing.assert_array_equal(gdy.view(np.uint32), rdy.view(np.uint32))
 
 
 def test_network_forward_parity(env):
@@ -234,9 +229,9 @@ def test_train_steps_reduce_loss(env):
     tb = pyngp.Testbed(pyngp.TestbedMode.Nerf)
     tb.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
     tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=BATCH)
-    tb.train(32)
+    tb.train_steps(32)
     l0 = tb.stats()["ray_loss"]
-    tb.train(288)
+    tb.train_steps(288)
     st = tb.stats()
     assert st["training_step"] == 320
     assert np.isfinite(st["ray_loss"]) and st["ray_loss"] < 0.7 * l0, (l0, st)
