@@ -41,12 +41,20 @@ def parse():
     return p.parse_args()
 
 
-# Algorithmic HBM bytes per sample for the single-kernel phases (DESIGN.md "Roofline"). Compulsory streams
-# only: the hash-grid table (28 MB fp16) and the fp32 gradient table (59 MB) are MALL-resident (256 MB
-# Infinity Cache), so the 8-corner gathers are not HBM traffic; the grid_scatter line adds one
-# read-modify-write pass over the fp32 grid gradient per launch.
+# Algorithmic work per unit for the single-kernel phases. HBM bytes count compulsory
+# streams only: the hash-grid table (21 MB fp16) and the fp32 grid gradient (42 MB) stay resident in the
+# 256 MB Infinity Cache, so 8-corner gathers and atomics are not HBM traffic; grid_scatter adds one
+# read-modify-write pass over the fp32 grid gradient per launch. The fused inference kernel moves only
+# 60 B/sample through HBM, so its bound is the MFMA work (dense fp16 flops of the six layers).
 COORD_B = 7 * 4          # NerfCoordinate AoS (pos, dt, dir)
-OUT_B = 16 * 2           # network output / dL_dout rows, fp16 x 16
+OUT_B = 16 * 2           # network output / dL/dout rows, fp16 x 16
+MFMA_PEAK_TFLOPS = 2500.0  # MI355X dense fp16 (MI355X_MICROARCH.md)
+
+
+def flops_per_sample(L=14, W=64):
+    din = ((3 + 2 * L) + 15) // 16 * 16
+    # density L0, L1, dSDF/d(din) through W1 row 0 and W0^T, rgb L0 (48 in), L1, L2
+    return 2 * (din * W + W * 16 + W + W * din + 48 * W + W * W + W * 16)
 
 
 def bytes_per_sample(L=14, W=64, din=32):
@@ -54,8 +62,7 @@ def bytes_per_sample(L=14, W=64, din=32):
     dydx = 6 * 4 * L                    # f32 d(feature)/d(xyz)
     soa = 2 * 2 * (W + din + 16 + W) + 2 * (W + 48 + W + W + 16 + W)   # weight-grad operands, fp16
     return {
-        "inference_encode": COORD_B + enc + dydx,
-        "inference_mlp": COORD_B + enc + dydx + OUT_B,
+        "inference": COORD_B + OUT_B,
         "train_encode": COORD_B + enc + dydx,
         "mlp_train": COORD_B + enc + dydx + OUT_B + soa + 2 * enc + 16,
         "wgrad": soa,
@@ -63,11 +70,13 @@ def bytes_per_sample(L=14, W=64, din=32):
     }
 
 
-def kernel_bytes(name, npre, ntrain, grid_params, L=14):
-    b = bytes_per_sample(L)[name]
-    n = npre if name.startswith("inference") else ntrain
-    extra = 8 * grid_params if name == "grid_scatter" else 0
-    return n * b + extra
+def roofline(name, ms, npre, ntrain, grid_params, L=14):
+    """(bound, achieved, peak, unit, work per launch) of one single-kernel phase."""
+    if name == "inference":
+        fl = flops_per_sample(L) * npre
+        return "mfma", fl / (ms * 1e-3) / 1e12, MFMA_PEAK_TFLOPS, "TFLOP/s", fl
+    b = bytes_per_sample(L)[name] * ntrain + (8 * grid_params if name == "grid_scatter" else 0)
+    return "hbm", b / (ms * 1e-3) / 1e9, HBM_PEAK_GBS, "GB/s", b
 
 
 def main():
@@ -128,10 +137,14 @@ def main():
     samples = batch * world * args.steps
     value = samples / elapsed
     lay = tb.layout()
-    single = ("inference_encode", "inference_mlp", "train_encode", "mlp_train", "wgrad", "grid_scatter")
+    single = ("inference", "train_encode", "mlp_train", "wgrad", "grid_scatter")
     dom = max(single, key=lambda k: phases[k])
-    alg = kernel_bytes(dom, pinfo["npre"], pinfo["ntrain"], lay["n_grid_params"])
-    achieved = alg / (phases[dom] * 1e-3) / 1e9 if phases[dom] > 0 else 0.0
+    bound, achieved, peak, unit, work = roofline(dom, phases[dom], pinfo["npre"], pinfo["ntrain"], lay["n_grid_params"])
+    rl_all = {}
+    for k in single:
+        if phases[k] > 0:
+            bd, ac, pk, un, _ = roofline(k, phases[k], pinfo["npre"], pinfo["ntrain"], lay["n_grid_params"])
+            rl_all[k] = {"ms": round(phases[k], 4), "bound": bd, "achieved": round(ac, 2), "unit": un, "frac": round(ac / pk, 4)}
     out = {
         "metric": "training samples/sec (compacted NeuS2 training samples, DTU-scan24-shaped synthetic, base.json)",
         "value": value,
@@ -147,9 +160,10 @@ def main():
         "data": "synthetic (analytic sphere, 49 x 1600x1200 RGBA8 views; DTU scan24 unavailable offline)",
         "config": {"workload": "NeuS2 train step, Config S, base.json L=14 T=2^19 W=64, Nc=2^18/GPU, R=2^18/GPU fixed",
                    "global_batch": batch * world, "rays_per_gpu": args.rays, "parallelism": f"dp{world}"},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": TRAFFIC.get(dom), "bytes_per_launch": alg,
+        "roofline": {"bound": bound, "kernel": dom, "achieved": achieved, "peak": peak, "unit": unit,
+                     "frac": achieved / peak, "traffic": TRAFFIC.get(dom), "work_per_launch": work,
                      "launch_ms": phases[dom]},
+        "kernels": rl_all,
         "phase_ms": {k: round(v, 4) for k, v in phases.items()},
         "npre_per_step": pinfo["npre"], "ntrain_per_step": pinfo["ntrain"],
         "loss": st["ray_loss"],

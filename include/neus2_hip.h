@@ -125,16 +125,23 @@ int neus_testbed_get_ema_params(NeusTestbed* tb, float* host_out, uint64_t n);
 int neus_testbed_get_density_grid(NeusTestbed* tb, float* grid_out /*128^3*/, uint8_t* bitfield_out /*128^3/8*8*/);
 int neus_testbed_set_density_grid(NeusTestbed* tb, const float* grid /*nullable*/, const uint8_t* bitfield /*nullable*/);
 int neus_testbed_get_rng(NeusTestbed* tb, uint64_t* state_inc /*4: rng, density_grid_rng*/);
+/* Per-ray counters of the last step (first n rays, host buffers, each nullable): samples requested by
+ * the march, samples composited before transmittance < 1e-4, and numsteps = (compacted count, base). */
+int neus_testbed_ray_counts(NeusTestbed* tb, uint32_t n, uint32_t* nreq, uint32_t* ccount, uint32_t* numsteps /* 2n */);
+/* Development timing hook: regenerates the last step's samples and times `iters` launches of one
+ * kernel (0 march count, 1 march write, 2 loss transmittance scan, 3 fused inference, 4 loss alpha)
+ * in implementation `variant` (0 = production); mean ms per launch. */
+int neus_debug_time_kernel(NeusTestbed* tb, int kernel, int variant, int iters, float* ms_out);
 int neus_testbed_stream(NeusTestbed* tb, void** hip_stream);
 int neus_testbed_synchronize(NeusTestbed* tb);
 /* Per-phase step timing with hipEvents recorded on the testbed stream (profiling on), mean ms per step:
- * ms_out[0] occupancy update, [1] ray sampling (march count/scan/write), [2] inference hash-grid encode,
- * [3] inference MLP, [4] loss + compaction + rollover, [5] training hash-grid encode, [6] fused MLP
- * fwd/bwd/2nd-order, [7] weight-gradient GEMMs, [8] hash-grid gradient scatter, [9] all-reduce + counters,
- * [10] Ema(Adam); ms_out[NEUS_N_PHASES] = number of profiled steps, [+1] mean pre-compaction samples per
- * step (the inference kernels' n), [+2] mean compacted training samples per step. Phases 2, 3, 5-8 are
- * single kernels. */
-#define NEUS_N_PHASES 11
+ * ms_out[0] occupancy update, [1] ray sampling (march count/scan/write), [2] fused hash-grid encode +
+ * network forward on the pre-compaction samples, [3] loss + compaction + rollover, [4] training
+ * hash-grid encode, [5] fused MLP fwd/bwd/2nd-order, [6] weight-gradient GEMMs, [7] hash-grid gradient
+ * scatter, [8] all-reduce + counters, [9] Ema(Adam); ms_out[NEUS_N_PHASES] = number of profiled steps,
+ * [+1] mean pre-compaction samples per step (the inference kernel's n), [+2] mean compacted training
+ * samples per step. Phases 2 and 4-7 are single kernels. */
+#define NEUS_N_PHASES 10
 int neus_testbed_set_profiling(NeusTestbed* tb, int on);
 int neus_testbed_kernel_times(NeusTestbed* tb, float* ms_out /* NEUS_N_PHASES + 3 entries */);
 

@@ -13,6 +13,9 @@ typedef half_t h4 __attribute__((ext_vector_type(4)));
 typedef half_t h2 __attribute__((ext_vector_type(2)));
 typedef float f16v __attribute__((ext_vector_type(16)));
 typedef float f4v __attribute__((ext_vector_type(4)));
+// 4 B-aligned float vectors for the 28 B NerfCoordinate records (the hardware runs unaligned mode)
+typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
 
 namespace neus {
 
@@ -30,6 +33,8 @@ constexpr uint32_t GRID3 = NERF_GRIDSIZE * NERF_GRIDSIZE * NERF_GRIDSIZE;
 constexpr uint32_t MAX_LEVELS = 16;
 constexpr uint32_t OUT_W = 16;      // padded network output width (nerf_network.h:935)
 constexpr uint32_t COORD_W = 7;     // NerfCoordinate floats (nerf.h:76-102)
+constexpr uint32_t MARCH_SEG = 32;  // samples per march-write segment (checkpointed by the count pass)
+constexpr uint32_t MARCH_SEGS = NERF_STEPS / MARCH_SEG;
 
 // ----------------------------------------------------------- pcg32 (my_tcnn pcg32.h:43-170)
 struct pcg32 {

@@ -11,27 +11,10 @@
 // 4 MiB L2 while the blocks of that level run. Samples are grid-strided and the active count is
 // read from device memory, so the host never syncs and the launch is graph-capturable.
 #include "kernels.h"
+#include "grid_common.h"
 #include <algorithm>
 
 namespace neus {
-
-struct LevelSetup { float pos[3]; uint32_t g[3]; float scale; uint32_t hsize, res; };
-
-__device__ __forceinline__ LevelSetup level_setup(const GridLevels& gl, uint32_t l, float x, float y, float z) {
-	LevelSetup s;
-	s.scale = gl.scale[l]; s.res = gl.res[l]; s.hsize = gl.offset[l + 1] - gl.offset[l];
-	const float in[3] = {x, y, z};
-#pragma unroll
-	for (int d = 0; d < 3; ++d) {
-		// pos_fract (common_device.h:404-434), linear interpolation. `input * scale + 0.5f` is one
-		// expression that nvcc (--fmad=true, the default) emits as a single FFMA: fused here too.
-		float p = __builtin_fmaf(in[d], s.scale, 0.5f);
-		float fl = floorf(p);
-		s.g[d] = (uint32_t)(int)fl;
-		s.pos[d] = p - fl;
-	}
-	return s;
-}
 
 __device__ __forceinline__ uint32_t load_n(const uint32_t* n_ptr, uint32_t n_fixed) { return n_ptr ? *n_ptr : n_fixed; }
 
@@ -55,44 +38,13 @@ __global__ void __launch_bounds__(256) k_grid_encode(
 		}
 		const float* c = coords + (size_t)i * coord_stride;
 		LevelSetup s = level_setup(gl, l, c[0], c[1], c[2]);
-		// 8 corner gathers (half2 each), issued together
 		h2 v[8];
-#pragma unroll
-		for (uint32_t idx = 0; idx < 8; ++idx) {
-			const uint32_t gx = s.g[0] + (idx & 1), gy = s.g[1] + ((idx >> 1) & 1), gz = s.g[2] + ((idx >> 2) & 1);
-			const uint32_t e = grid_index(s.hsize, s.res, gx, gy, gz);
-			v[idx] = *(const h2*)(gp + 2 * (size_t)e);
-		}
-		// fp16 accumulation of fp16-rounded terms, as the reference (result[f] += (T)(weight * data))
-		half_t r0 = (half_t)0.f, r1 = (half_t)0.f;
-#pragma unroll
-		for (uint32_t idx = 0; idx < 8; ++idx) {
-			float w = 1.f;
-#pragma unroll
-			for (int d = 0; d < 3; ++d) w *= (idx & (1u << d)) ? s.pos[d] : 1.f - s.pos[d];
-			r0 = (half_t)((float)r0 + (float)(half_t)(w * (float)v[idx][0]));
-			r1 = (half_t)((float)r1 + (float)(half_t)(w * (float)v[idx][1]));
-		}
-		h2 out; out[0] = r0; out[1] = r1;
-		enc[(size_t)l * ld + i] = *(uint32_t*)&out;
+		gather_corners(s, gp, v);
+		const h2 out = interp_features(s, v);
+		enc[(size_t)l * ld + i] = *(const uint32_t*)&out;
 		if (dydx) {
-			float gr[2][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
-#pragma unroll
-			for (int gd = 0; gd < 3; ++gd) {
-#pragma unroll
-				for (uint32_t idx = 0; idx < 4; ++idx) {
-					float w = s.scale;
-					uint32_t cl = 0;
-#pragma unroll
-					for (int ngd = 0; ngd < 2; ++ngd) {
-						const int d = ngd >= gd ? ngd + 1 : ngd;
-						if (idx & (1u << ngd)) { w *= s.pos[d]; cl |= 1u << d; } else { w *= 1.f - s.pos[d]; }
-					}
-					const uint32_t cr = cl | (1u << gd);
-					gr[0][gd] = __builtin_fmaf(w, (float)v[cr][0] - (float)v[cl][0], gr[0][gd]);
-					gr[1][gd] = __builtin_fmaf(w, (float)v[cr][1] - (float)v[cl][1], gr[1][gd]);
-				}
-			}
+			float gr[2][3];
+			interp_dydx(s, v, gr);
 #pragma unroll
 			for (int f = 0; f < 2; ++f)
 #pragma unroll
@@ -105,8 +57,36 @@ __device__ __forceinline__ void atomic_add_f32(float* p, float v) {
 	__hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Wave-aggregated atomic add of (a0, a1) to gg[2e], gg[2e+1]: consecutive lanes with the same entry
+// (consecutive samples of one ray share coarse-level cells) are first summed with a segmented
+// shuffle scan, and only the last lane of each run issues the two fp32 atomics. All 64 lanes must
+// call this; `ok` masks lanes without a sample.
+__device__ __forceinline__ void wave_aggregated_add(float* gg, uint32_t e, float a0, float a1, bool ok) {
+	const int lane = threadIdx.x & 63;
+	if (!ok) { e = 0xffffffffu; a0 = a1 = 0.f; }
+	const uint32_t e_prev = __shfl_up(e, 1);
+	const bool head = lane == 0 || e_prev != e;
+	if (__ballot(!head) != 0) {  // at least one run longer than one lane
+		int rs = head ? lane : 0;
+#pragma unroll
+		for (int off = 1; off < 64; off <<= 1) { const int t = __shfl_up(rs, off); if (lane >= off) rs = max(rs, t); }
+#pragma unroll
+		for (int off = 1; off < 64; off <<= 1) {
+			const float t0 = __shfl_up(a0, off), t1 = __shfl_up(a1, off);
+			if (lane - off >= rs) { a0 += t0; a1 += t1; }
+		}
+		const uint32_t e_next = __shfl_down(e, 1);
+		const bool tail = lane == 63 || e_next != e;
+		if (!tail) return;
+	}
+	if (!ok) return;
+	atomic_add_f32(gg + 2 * (size_t)e, a0);
+	atomic_add_f32(gg + 2 * (size_t)e + 1, a1);
+}
+
 // grads: fp32 grid gradient (grid part of the parameter gradient vector).
 // dLdenc, g: [L][ld] packed half2; v: [ld] float4 (dL/d grad_sdf, w unused).
+// Every lane of a wave stays in the loop (wave-wide shuffles), lanes past n are masked.
 __global__ void __launch_bounds__(256) k_grid_scatter(
 	const uint32_t* __restrict__ n_ptr, uint32_t n_fixed, uint32_t ld,
 	const float* __restrict__ coords, uint32_t coord_stride,
@@ -117,13 +97,16 @@ __global__ void __launch_bounds__(256) k_grid_scatter(
 	const uint32_t l = blockIdx.y;
 	if (l > valid_level) return;
 	float* gg = grads + (size_t)gl.offset[l] * 2;
-	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-		const float* c = coords + (size_t)i * coord_stride;
+	for (uint32_t b0 = blockIdx.x * blockDim.x; b0 < n; b0 += gridDim.x * blockDim.x) {
+		const uint32_t i = b0 + threadIdx.x;
+		const bool ok = i < n;
+		const uint32_t ic = ok ? i : 0;
+		const float* c = coords + (size_t)ic * coord_stride;
 		LevelSetup s = level_setup(gl, l, c[0], c[1], c[2]);
-		uint32_t a = dLdenc[(size_t)l * ld + i], b = g[(size_t)l * ld + i];
+		uint32_t a = dLdenc[(size_t)l * ld + ic], b = g[(size_t)l * ld + ic];
 		const h2 d1 = *(h2*)&a, g2 = *(h2*)&b;
 		const float dl0 = (float)d1[0], dl1 = (float)d1[1], g0 = (float)g2[0], g1 = (float)g2[1];
-		const float4 vv = v4[i];
+		const float4 vv = v4[ic];
 		const float vin[3] = {s.scale * vv.x, s.scale * vv.y, s.scale * vv.z};
 #pragma unroll
 		for (uint32_t idx = 0; idx < 8; ++idx) {
@@ -144,8 +127,7 @@ __global__ void __launch_bounds__(256) k_grid_scatter(
 			const float a1 = dl1 * w + g1 * w2;
 			const uint32_t gx = s.g[0] + (idx & 1), gy = s.g[1] + ((idx >> 1) & 1), gz = s.g[2] + ((idx >> 2) & 1);
 			const uint32_t e = grid_index(s.hsize, s.res, gx, gy, gz);
-			atomic_add_f32(gg + 2 * (size_t)e, a0);
-			atomic_add_f32(gg + 2 * (size_t)e + 1, a1);
+			wave_aggregated_add(gg, e, a0, a1, ok);
 		}
 	}
 }

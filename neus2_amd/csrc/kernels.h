@@ -10,6 +10,7 @@ struct MlpPtrs {
 	const half_t* r0;  const half_t* r1;  const half_t* r2;  // rgb W0 [W][48], W1 [W][W], W2 [16][W]
 	const half_t* d0T; const half_t* d1T;                    // transposed copies [DIN][W], [W][16]
 	const half_t* r0T; const half_t* r1T; const half_t* r2T; // [48][W], [W][W], [W][16]
+	const half_t* d0p; const half_t* d0Tp;                   // W0 with din-permuted columns / W0^T permuted rows (fused kernels)
 	const half_t* var;                                       // variance param (fp16)
 	float sdf_bias;                                          // -0.1
 };
@@ -51,6 +52,19 @@ struct LossParams {
 	uint64_t rng_state, rng_inc;
 };
 
+// per-sample / per-ray scratch of the restructured loss (march.hip)
+struct LossWork {
+	float4* sa;             // [samples] alpha, sigmoid(rgb)
+	float4* ck4;            // [samples / 8 + 1] state {T, rgb prefix} before each sample s with s % 8 == 0
+	float* cke;             // [samples / 8 + 1] eikonal-term prefix before the same samples
+	float* ekt;             // [samples] eikonal term
+	uint32_t* sample_ray;   // [samples] owning ray
+	const uint32_t* rbase;  // [rays] first sample of the ray (pre-compaction)
+	float4* racc;           // [rays] rgb_ray, weight_sum
+	float* rT;              // [rays] final transmittance
+	float4* rgr;            // [rays] dL/drgb_ray (Huber'), gws * (1 - weight_sum)
+};
+
 struct AdamParams {
 	uint32_t n, n_matrix;
 	float loss_scale, lr, beta1, beta2, eps, l2_reg;
@@ -68,24 +82,31 @@ void launch_grid_scatter(hipStream_t s, const uint32_t* n_ptr, uint32_t n_fixed,
                          const GridLevels& gl, uint32_t valid_level, const half_t* dLdenc, const half_t* g, const float4* v, float* grads, uint32_t grid_x);
 // mlp.hip
 bool mlp_supported(uint32_t n_levels, uint32_t width);
-void launch_mlp_forward(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_ptr, uint32_t n_fixed, uint32_t ld, const float* coords,
-                        const half_t* enc, const float* dydx, const MlpPtrs& w, half_t* out, uint32_t blocks);
-void launch_mlp_density(hipStream_t s, uint32_t L, uint32_t W, uint32_t n, uint32_t ld, const float* pos, const half_t* enc,
-                        const MlpPtrs& w, float* density);
+void mlp_din_permutation(uint32_t L, int32_t* perm /* DIN entries: physical row -> logical din index or -1 */);
+void launch_nerf_infer(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_ptr, uint32_t n_fixed, const float* coords, const GridLevels& gl,
+                       uint32_t valid_level, const half_t* grid, const MlpPtrs& w, half_t* out, uint32_t blocks);
+void launch_nerf_density(hipStream_t s, uint32_t L, uint32_t W, uint32_t n, const float* pos, const GridLevels& gl, uint32_t valid_level,
+                         const half_t* grid, const MlpPtrs& w, float* density);
 void launch_mlp_train(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_valid_ptr, uint32_t n, uint32_t ld, const float* coords,
                       const half_t* enc, const float* dydx, const half_t* dL_dout, const MlpPtrs& w, const TrainBufs& tb);
 void launch_wgrad(hipStream_t s, const WGradJobs& jobs, uint32_t n_blocks);
 void launch_mfma_probe(hipStream_t s, const half_t* A, const half_t* B, float* C);
 // march.hip
+void launch_bitfield_linear(hipStream_t s, const uint8_t* bitfield, uint32_t* lin /* GRID3 / 32 words */);
 void launch_march_count(hipStream_t s, uint32_t cap, const StepState* st, DPInfo dp, const DevDataset& ds, const uint8_t* bitfield,
-                        uint64_t rng_state, uint64_t rng_inc, float* rays, float* startt, uint32_t* nreq);
-void launch_march_write(hipStream_t s, uint32_t cap, StepState* st, const DevDataset& ds, const uint8_t* bitfield, const float* rays,
-                        const float* startt, const uint32_t* nreq, const uint32_t* base, uint32_t* numsteps, float* coords);
-void launch_loss_count(hipStream_t s, uint32_t cap, const StepState* st, const DevDataset& ds, const float* rays, const uint32_t* numsteps,
-                       const float* coords, const half_t* net_out, float cos_anneal, uint32_t* ccount);
-void launch_loss_write(hipStream_t s, uint32_t cap, StepState* st, DPInfo dp, const DevDataset& ds, const LossParams& lp, const float* rays,
-                       uint32_t* numsteps, const float* coords, const half_t* net_out, const uint32_t* ccount, const uint32_t* cbase,
-                       float* coords_out, half_t* dL_dout, float* loss, float* ek, float* mask);
+                        const uint32_t* lin, uint64_t rng_state, uint64_t rng_inc, float* rays, float* ckpt /* MARCH_SEGS per ray */, uint32_t* nreq);
+void launch_march_write(hipStream_t s, uint32_t cap, StepState* st, const DevDataset& ds, const uint8_t* bitfield, const uint32_t* lin,
+                        const float* rays, const float* ckpt, const uint32_t* nreq, const uint32_t* base, uint32_t* numsteps, float* coords,
+                        uint32_t* sample_ray);
+void launch_loss_alpha(hipStream_t s, uint32_t cap_samples, const StepState* st, const float* coords, const half_t* net_out, float cos_anneal,
+                       const LossWork& w);
+void launch_loss_scan_ray(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, const LossWork& w, uint32_t* ccount);
+void launch_loss_ray(hipStream_t s, uint32_t cap_rays, StepState* st, DPInfo dp, const DevDataset& ds, const LossParams& lp, uint32_t* numsteps,
+                     const uint32_t* ccount, const uint32_t* cbase, const LossWork& w, float* loss, float* ek, float* mask);
+void launch_loss_grad(hipStream_t s, uint32_t cap_samples, const StepState* st, DPInfo dp, const LossParams& lp, const float* coords,
+                      const half_t* net_out, const uint32_t* numsteps, const LossWork& w, float* coords_out, half_t* dL_dout);
+void debug_launch_loss_scan(hipStream_t s, int variant, uint32_t cap_rays, const uint32_t* numsteps, const LossWork& w, uint32_t* ccount);
+void launch_ray_index(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, StepState* st, uint32_t* sample_ray, uint32_t* rbase);
 void launch_rollover(hipStream_t s, uint32_t n_elements, const StepState* st, float* coords, half_t* dL_dout);
 void launch_step_counters(hipStream_t s, StepState* st, uint32_t target_batch, uint32_t max_samples, uint32_t world, uint32_t fixed_rays);
 // scan.hip
@@ -97,6 +118,8 @@ void launch_adam_ema(hipStream_t s, const AdamParams& p, float* weights_fp, half
                      uint32_t* steps, float* ema_tmp, half_t* ema_h);
 void launch_cast_half(hipStream_t s, uint32_t n, const float* in, half_t* out);
 void launch_transpose_w(hipStream_t s, const TransposeJobs& jobs);
+struct DinPerm { int32_t p[48]; uint32_t din, W; };
+void launch_permute_din(hipStream_t s, const half_t* d0, half_t* d0p, half_t* d0Tp, const DinPerm& perm);
 void launch_grid_samples(hipStream_t s, uint32_t n, uint32_t out_offset, uint64_t rng_state, uint64_t rng_inc, uint32_t step,
                          const float* aabb_min, const float* aabb_max, const float* grid_in, float* pos, uint32_t* indices,
                          uint32_t n_cascades, float thresh);

@@ -108,11 +108,96 @@ __device__ __forceinline__ void ray_intersect(const DevDataset& ds, const float 
 	tmin_o = tmin;
 }
 
+// ---------------------------------------------------------------- the occupancy march
+// Mip-0 occupancy as 32-bit words in (x, y, z/32) order: one address computation and one word load per
+// step instead of the Morton interleave of the reference's bitfield (built from it, same bits).
+__global__ void k_bitfield_linear(const uint8_t* __restrict__ bf, uint32_t* __restrict__ lin) {
+	const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+	if (w >= GRID3 / 32) return;
+	const uint32_t ix = w >> 9, iy = (w >> 2) & 127, iz0 = (w & 3) * 32;
+	uint32_t word = 0;
+	for (uint32_t b = 0; b < 32; ++b) {
+		const uint32_t idx = morton3D(ix, iy, iz0 + b);
+		word |= (uint32_t)((bf[idx / 8] >> (idx % 8)) & 1) << b;
+	}
+	lin[w] = word;
+}
+
+struct MarchRay { float o[3], dir[3], idir[3]; };
+
+// One iteration of the reference's march loop body (testbed_nerf.cu:1376-1405) with the same float
+// operation sequence: returns 0 once the ray has left the AABB, 1 at an occupied sample (pos and dt
+// set; the caller steps t += dt), 2 after skipping an empty voxel (t advanced). The loops around it
+// stay flat (one sample-or-skip per iteration) so lanes of a wave do not wait on each other's skips.
+// FAST: cone_angle == 0 (aabb_scale 1): constant dt, mip 0 answered from the linear bitfield, mip > 0
+// (only the exact box centre and faces) from the Morton one.
+template <bool FAST>
+__device__ __forceinline__ int march_step(const DevDataset& ds, const uint8_t* __restrict__ bf, const uint32_t* __restrict__ lin,
+                                          const MarchRay& r, float& t, float& dt, float pos[3]) {
+#pragma unroll
+	for (int d = 0; d < 3; ++d) pos[d] = r.o[d] + t * r.dir[d];
+	if (!aabb_contains(ds, pos)) return 0;
+	uint32_t mip;
+	bool occ;
+	if (FAST) {
+		dt = MIN_CONE_STEPSIZE;  // calc_dt(t, 0)
+		mip = (uint32_t)mip_from_pos(pos[0], pos[1], pos[2]);  // dt * 256 < 1
+		if (mip == 0) {
+			// cascaded_grid_idx_at with scale 1: ((p - 0.5) * 1) + 0.5
+			const int ix = clampi((int)(((pos[0] - 0.5f) + 0.5f) * NERF_GRIDSIZE), 0, NERF_GRIDSIZE - 1);
+			const int iy = clampi((int)(((pos[1] - 0.5f) + 0.5f) * NERF_GRIDSIZE), 0, NERF_GRIDSIZE - 1);
+			const int iz = clampi((int)(((pos[2] - 0.5f) + 0.5f) * NERF_GRIDSIZE), 0, NERF_GRIDSIZE - 1);
+			occ = (lin[((uint32_t)ix << 9) | ((uint32_t)iy << 2) | ((uint32_t)iz >> 5)] >> (iz & 31)) & 1;
+		} else {
+			occ = occupied(pos[0], pos[1], pos[2], bf, mip);
+		}
+	} else {
+		dt = calc_dt(t, ds.cone_angle);
+		mip = (uint32_t)mip_from_dt(dt, pos[0], pos[1], pos[2]);
+		occ = occupied(pos[0], pos[1], pos[2], bf, mip);
+	}
+	if (occ) return 1;
+	if (FAST) {
+		// advance_to_next_voxel with a constant step; t / res is an exact power-of-two scaling
+		const uint32_t res = NERF_GRIDSIZE >> mip;
+		float tn = 3.402823466e+38f;
+#pragma unroll
+		for (int d = 0; d < 3; ++d) {
+			const float p = res * pos[d];
+			tn = fminf(tn, (floorf(p + 0.5f + 0.5f * signf(r.dir[d])) - p) * r.idir[d]);
+		}
+		const float t_target = t + fmaxf(ldexpf(tn, -(int)(7 - mip)), 0.0f);
+		do { t += MIN_CONE_STEPSIZE; } while (t < t_target);
+	} else {
+		t = advance_to_next_voxel(t, ds.cone_angle, pos, r.dir, r.idir, NERF_GRIDSIZE >> mip);
+	}
+	return 2;
+}
+
+template <bool FAST>
+__device__ __forceinline__ uint32_t march_count_ray(const DevDataset& ds, const uint8_t* __restrict__ bf, const uint32_t* __restrict__ lin,
+                                                    const MarchRay& r, float t, float* __restrict__ ckpt_ray) {
+	uint32_t n = 0;
+	while (n < NERF_STEPS) {
+		float dt, pos[3];
+		const int k = march_step<FAST>(ds, bf, lin, r, t, dt, pos);
+		if (k == 0) break;
+		if (k == 1) {
+			++n; t += dt;
+			if ((n & (MARCH_SEG - 1)) == 0 && n < NERF_STEPS) ckpt_ray[n / MARCH_SEG] = t;
+		}
+	}
+	return n;
+}
+
 // ---------------------------------------------------------------- pass 1: per-ray count
-// rays: 6 floats/ray (o, unnormalized d); startt: 1 float/ray; nreq: requested steps (0 = none)
+// rays: 6 floats/ray (o, unnormalized d); ckpt: MARCH_SEGS floats/ray = the march parameter t at which
+// the search for sample 32*s starts (s = 0: the jittered start), so the write pass can re-march each
+// 32-sample segment independently and bit-identically; nreq: requested steps (0 = none)
 __global__ void __launch_bounds__(256) k_march_count(uint32_t cap_rays, const StepState* __restrict__ st, DPInfo dp, DevDataset ds,
-                                                     const uint8_t* __restrict__ bitfield, uint64_t rng_state, uint64_t rng_inc,
-                                                     float* __restrict__ rays, float* __restrict__ startt_out, uint32_t* __restrict__ nreq) {
+                                                     const uint8_t* __restrict__ bitfield, const uint32_t* __restrict__ lin,
+                                                     uint64_t rng_state, uint64_t rng_inc,
+                                                     float* __restrict__ rays, float* __restrict__ ckpt, uint32_t* __restrict__ nreq) {
 	const uint32_t R = st->rays_per_batch;
 	const uint32_t n_rays_global = R * dp.world, n_rays_total = st->n_rays_total;
 	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cap_rays; i += gridDim.x * blockDim.x) {
@@ -143,65 +228,79 @@ __global__ void __launch_bounds__(256) k_march_count(uint32_t cap_rays, const St
 				tmin = fmaxf(tmin, 0.0f);
 				startt = tmin;
 				startt += calc_dt(startt, ds.cone_angle) * rng.next_float();
-				const float idir[3] = {1.0f / dir[0], 1.0f / dir[1], 1.0f / dir[2]};
-				float t = startt;
-				while (true) {
-					const float pos[3] = {o[0] + t * dir[0], o[1] + t * dir[1], o[2] + t * dir[2]};
-					if (!(aabb_contains(ds, pos) && n < NERF_STEPS)) break;
-					const float dt = calc_dt(t, ds.cone_angle);
-					const uint32_t mip = (uint32_t)mip_from_dt(dt, pos[0], pos[1], pos[2]);
-					if (occupied(pos[0], pos[1], pos[2], bitfield, mip)) { ++n; t += dt; }
-					else t = advance_to_next_voxel(t, ds.cone_angle, pos, dir, idir, NERF_GRIDSIZE >> mip);
-				}
+				MarchRay mr;
+#pragma unroll
+				for (int d = 0; d < 3; ++d) { mr.o[d] = o[d]; mr.dir[d] = dir[d]; mr.idir[d] = 1.0f / dir[d]; }
+				float* ck = ckpt + (size_t)i * MARCH_SEGS;
+				n = lin ? march_count_ray<true>(ds, bitfield, lin, mr, startt, ck) : march_count_ray<false>(ds, bitfield, lin, mr, startt, ck);
 			}
 		}
 		float* rr = rays + 6 * (size_t)i;
 		rr[0] = o[0]; rr[1] = o[1]; rr[2] = o[2]; rr[3] = du[0]; rr[4] = du[1]; rr[5] = du[2];
-		startt_out[i] = startt;
+		ckpt[(size_t)i * MARCH_SEGS] = startt;
 		nreq[i] = n;
 	}
 }
 
 // ---------------------------------------------------------------- pass 2: write kept rays
+// One thread per (ray, 32-sample segment): each re-marches its segment from the count pass's
+// checkpoint, so a few long rays (early training: ~500 samples each) spread over many lanes.
 __global__ void __launch_bounds__(256) k_march_write(uint32_t cap_rays, StepState* __restrict__ st, DevDataset ds,
-                                                     const uint8_t* __restrict__ bitfield, const float* __restrict__ rays,
-                                                     const float* __restrict__ startt_in, const uint32_t* __restrict__ nreq,
+                                                     const uint8_t* __restrict__ bitfield, const uint32_t* __restrict__ lin,
+                                                     const float* __restrict__ rays,
+                                                     const float* __restrict__ ckpt, const uint32_t* __restrict__ nreq,
                                                      const uint32_t* __restrict__ base, uint32_t* __restrict__ numsteps,
-                                                     float* __restrict__ coords) {
+                                                     float* __restrict__ coords, uint32_t* __restrict__ sample_ray) {
 	const uint32_t max_samples = st->max_inference;
-	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cap_rays; i += gridDim.x * blockDim.x) {
-		const uint32_t n = nreq[i], b = base[i];
-		if (i == cap_rays - 1) st->numsteps_counter = b + n;
+	const uint32_t n_tasks = cap_rays * MARCH_SEGS;
+	const uint32_t lane = threadIdx.x & 63;
+	for (uint32_t t0 = blockIdx.x * blockDim.x; t0 < n_tasks; t0 += gridDim.x * blockDim.x) {
+		const uint32_t task = t0 + threadIdx.x;
+		const bool in_range = task < n_tasks;
+		const uint32_t i = in_range ? task / MARCH_SEGS : 0, seg = task % MARCH_SEGS;
+		const uint32_t n = in_range ? nreq[i] : 0, b = in_range ? base[i] : 0;
 		const bool keep = n > 0 && b + n <= max_samples;
-		numsteps[2 * i] = keep ? n : 0;
-		numsteps[2 * i + 1] = b;
-		if (!keep) continue;
-		atomicMax(&st->n_kept, b + n);
-		atomicAdd(&st->n_rays_with_samples, 1u);
+		const bool head = in_range && seg == 0;
+		if (head) {
+			if (i == cap_rays - 1) st->numsteps_counter = b + n;
+			numsteps[2 * i] = keep ? n : 0;
+			numsteps[2 * i + 1] = b;
+		}
+		// kept-sample extent and kept-ray count: one atomic per wave (same-address atomics from
+		// every kept ray serialise at the L2)
+		uint32_t kmax = head && keep ? b + n : 0u, kcnt = head && keep ? 1u : 0u;
+		if (__ballot(kcnt != 0)) {
+#pragma unroll
+			for (int off = 32; off > 0; off >>= 1) { kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, off)); kcnt += (uint32_t)__shfl_xor((int)kcnt, off); }
+			if (lane == 0) { atomicMax(&st->n_kept, kmax); atomicAdd(&st->n_rays_with_samples, kcnt); }
+		}
+		if (!in_range || !keep || seg * MARCH_SEG >= n) continue;
 		const float* rr = rays + 6 * (size_t)i;
 		const float o[3] = {rr[0], rr[1], rr[2]};
 		const float nrm = sqrtf((rr[3] * rr[3] + rr[4] * rr[4]) + rr[5] * rr[5]);
 		float dir[3];
 #pragma unroll
 		for (int r = 0; r < 3; ++r) dir[r] = nrm > 0.f ? rr[3 + r] / nrm : rr[3 + r];
-		const float idir[3] = {1.0f / dir[0], 1.0f / dir[1], 1.0f / dir[2]};
+		MarchRay mr;
+#pragma unroll
+		for (int d = 0; d < 3; ++d) { mr.o[d] = o[d]; mr.dir[d] = dir[d]; mr.idir[d] = 1.0f / dir[d]; }
 		const float wd[3] = {(dir[0] + 1.0f) * 0.5f, (dir[1] + 1.0f) * 0.5f, (dir[2] + 1.0f) * 0.5f};
 		const float diag[3] = {ds.aabb_max[0] - ds.aabb_min[0], ds.aabb_max[1] - ds.aabb_min[1], ds.aabb_max[2] - ds.aabb_min[2]};
-		float* out = coords + (size_t)b * COORD_W;
-		uint32_t j = 0;
-		float t = startt_in[i];
-		while (true) {
-			const float pos[3] = {o[0] + t * dir[0], o[1] + t * dir[1], o[2] + t * dir[2]};
-			if (!(aabb_contains(ds, pos) && j < n)) break;
-			const float dt = calc_dt(t, ds.cone_angle);
-			const uint32_t mip = (uint32_t)mip_from_dt(dt, pos[0], pos[1], pos[2]);
-			if (occupied(pos[0], pos[1], pos[2], bitfield, mip)) {
-				float* cc = out + (size_t)j * COORD_W;
-				cc[0] = (pos[0] - ds.aabb_min[0]) / diag[0]; cc[1] = (pos[1] - ds.aabb_min[1]) / diag[1]; cc[2] = (pos[2] - ds.aabb_min[2]) / diag[2];
-				cc[3] = warp_dt(dt);
-				cc[4] = wd[0]; cc[5] = wd[1]; cc[6] = wd[2];
-				++j; t += dt;
-			} else t = advance_to_next_voxel(t, ds.cone_angle, pos, dir, idir, NERF_GRIDSIZE >> mip);
+		uint32_t j = seg * MARCH_SEG;
+		const uint32_t jend = min(n, j + MARCH_SEG);
+		float t = ckpt[(size_t)i * MARCH_SEGS + seg];
+		while (j < jend) {
+			float dt, pos[3];
+			const int k = lin ? march_step<true>(ds, bitfield, lin, mr, t, dt, pos) : march_step<false>(ds, bitfield, lin, mr, t, dt, pos);
+			if (k == 0) break;
+			if (k == 2) continue;
+			// NerfCoordinate (28 B): one 16 B + one 12 B store (4 B-aligned vector stores)
+			float* cc = coords + (size_t)(b + j) * COORD_W;
+			const f4u p4 = {(pos[0] - ds.aabb_min[0]) / diag[0], (pos[1] - ds.aabb_min[1]) / diag[1], (pos[2] - ds.aabb_min[2]) / diag[2], warp_dt(dt)};
+			*(f4u*)cc = p4;
+			*(f3u*)(cc + 4) = (f3u){wd[0], wd[1], wd[2]};
+			sample_ray[b + j] = i;
+			++j; t += dt;
 		}
 	}
 }
@@ -228,44 +327,135 @@ __device__ __forceinline__ Alpha neus_alpha(const half_t* lo, const float dir[3]
 	return a;
 }
 
-// ---------------------------------------------------------------- loss pass 1: compacted count
-__global__ void __launch_bounds__(256) k_loss_count(uint32_t cap_rays, const StepState* __restrict__ st, DevDataset ds,
-                                                    const float* __restrict__ rays, const uint32_t* __restrict__ numsteps,
-                                                    const float* __restrict__ coords, const half_t* __restrict__ net_out,
-                                                    float cos_anneal, uint32_t* __restrict__ ccount) {
-	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cap_rays; i += gridDim.x * blockDim.x) {
-		const uint32_t ns = numsteps[2 * i], base = numsteps[2 * i + 1];
-		uint32_t cn = 0;
-		if (ns > 0) {
-			const float* rr = rays + 6 * (size_t)i;
-			const float nr = sqrtf((rr[3] * rr[3] + rr[4] * rr[4]) + rr[5] * rr[5]);
-			float dir[3] = {nr > 0 ? rr[3] / nr : rr[3], nr > 0 ? rr[4] / nr : rr[4], nr > 0 ? rr[5] / nr : rr[5]};
-			float T = 1.f;
-			for (; cn < ns; ++cn) {
-				if (T < 1e-4f) break;
-				const half_t* lo = net_out + (size_t)(base + cn) * OUT_W;
-				const float* ci = coords + (size_t)(base + cn) * COORD_W;
-				if (cn == 0) {
-					float u[3] = {(float)lo[8] * 2.0f - 1.0f, (float)lo[9] * 2.0f - 1.0f, (float)lo[10] * 2.0f - 1.0f};
-					const float n2 = sqrtf((u[0] * u[0] + u[1] * u[1]) + u[2] * u[2]);
+// ---------------------------------------------------------------- loss, restructured for gfx950
+// The reference walks each ray's samples serially in one thread, twice (composite, then gradient).
+// Here only the transmittance recurrence stays serial, over 20 B per sample; everything pointwise
+// runs one thread per sample with coalesced loads/stores:
+//   A  k_loss_alpha     (per pre-compaction sample): alpha, sigmoid(rgb), eikonal term
+//   B  k_loss_scan_ray  (per ray, serial): T, cn (T < 1e-4 cut), rgb_ray, weight_sum; per-sample
+//                       prefix {T_before, rgb prefix incl. the sample}, eikonal prefix
+//      exclusive scan of cn -> compacted base
+//   C  k_loss_ray       (per ray): target pixel + background (same pcg32 stream as the sampler),
+//                       Huber loss, mask term, comp = min(cap - base, cn), numsteps := (comp, base)
+//   D  k_loss_grad      (per pre-compaction sample): dL/doutput of the compacted samples
+// The float operation sequence of every quantity is the reference's (and the oracle's), so the
+// compaction and the gradients stay bit-identical to the serial formulation.
+
+// direction used by the NeuS cosine: the network's warped-dir output rows 8..10 (BENT_DIR,
+// testbed_nerf.cu:1583-1588). Static scenes write the same warped dir for every sample of a ray,
+// so each sample can read its own row.
+__device__ __forceinline__ void bent_dir(const half_t* lo, float dir[3]) {
+	float u[3] = {(float)lo[8] * 2.0f - 1.0f, (float)lo[9] * 2.0f - 1.0f, (float)lo[10] * 2.0f - 1.0f};
+	const float n2 = sqrtf((u[0] * u[0] + u[1] * u[1]) + u[2] * u[2]);
 #pragma unroll
-					for (int k = 0; k < 3; ++k) dir[k] = n2 > 0 ? u[k] / n2 : u[k];
-				}
-				const Alpha a = neus_alpha(lo, dir, unwarp_dt(ci[3]), cos_anneal);
-				T *= (1.f - a.alpha);
-			}
-		}
-		ccount[i] = cn;
+	for (int k = 0; k < 3; ++k) dir[k] = n2 > 0 ? u[k] / n2 : u[k];
+}
+__device__ __forceinline__ float grad_norm(const half_t* lo) {
+	const float pg[3] = {(float)lo[4], (float)lo[5], (float)lo[6]};
+	return sqrt((double)(pg[0] * pg[0] + pg[1] * pg[1] + pg[2] * pg[2]) + 1e-6);
+}
+__device__ __forceinline__ void load_out(const half_t* net_out, uint32_t s, half_t lo[16]) {
+	const h8* p = (const h8*)(net_out + (size_t)s * OUT_W);
+	const h8 a = p[0], b = p[1];
+#pragma unroll
+	for (int k = 0; k < 8; ++k) { lo[k] = a[k]; lo[8 + k] = b[k]; }
+}
+
+__global__ void __launch_bounds__(256) k_loss_alpha(uint32_t cap, const StepState* __restrict__ st, const float* __restrict__ coords,
+                                                    const half_t* __restrict__ net_out, float cos_anneal, float4* __restrict__ sa,
+                                                    float* __restrict__ ekt) {
+	const uint32_t n = min(st->n_kept, cap);
+	for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < n; s += gridDim.x * blockDim.x) {
+		half_t lo[16]; load_out(net_out, s, lo);
+		float dir[3]; bent_dir(lo, dir);
+		const Alpha a = neus_alpha(lo, dir, unwarp_dt(coords[(size_t)s * COORD_W + 3]), cos_anneal);
+		sa[s] = make_float4(a.alpha, det_logistic((float)lo[0]), det_logistic((float)lo[1]), det_logistic((float)lo[2]));
+		const float gn = grad_norm(lo);
+		ekt[s] = (gn - 1.0f) * (gn - 1.0f);
 	}
 }
 
-// ---------------------------------------------------------------- loss pass 2: composite, loss, dL/dout
-__global__ void __launch_bounds__(256) k_loss_write(uint32_t cap_rays, StepState* __restrict__ st, DPInfo dp, DevDataset ds, LossParams lp,
-                                                    const float* __restrict__ rays, uint32_t* __restrict__ numsteps,
-                                                    const float* __restrict__ coords, const half_t* __restrict__ net_out,
-                                                    const uint32_t* __restrict__ ccount, const uint32_t* __restrict__ cbase,
-                                                    float* __restrict__ coords_out, half_t* __restrict__ dL_dout,
-                                                    float* __restrict__ loss_out, float* __restrict__ ek_out, float* __restrict__ mask_out) {
+// Transmittance recurrence state of a ray (reference order: w = a T; rgb += w c; ws += w; ek += e; T *= 1 - a).
+struct ScanState { float T, r0, r1, r2, ek; };
+constexpr uint32_t SCAN_CK = 8;  // checkpoint stride of the stored scan state (in global sample index)
+
+// Replays the recurrence from the last stored checkpoint at or before sample s (or the ray start)
+// through sample s; returns T before s in T_before, and the state after s.
+__device__ __forceinline__ ScanState scan_replay(uint32_t base, uint32_t s, const float4* __restrict__ sa, const float* __restrict__ ekt,
+                                                 const float4* __restrict__ ck4, const float* __restrict__ cke, float& T_before) {
+	const uint32_t g = s & ~(SCAN_CK - 1);
+	ScanState st{1.f, 0.f, 0.f, 0.f, 0.f};
+	uint32_t k = base;
+	if (g > base) { const float4 c = ck4[g / SCAN_CK]; st = {c.x, c.y, c.z, c.w, cke[g / SCAN_CK]}; k = g; }
+	for (; k <= s; ++k) {
+		const float4 q = sa[k];
+		const float w = q.x * st.T;
+		st.r0 += w * q.y; st.r1 += w * q.z; st.r2 += w * q.w;
+		st.ek += ekt[k];
+		if (k == s) T_before = st.T;
+		st.T *= (1.f - q.x);
+	}
+	return st;
+}
+
+// One thread per ray, software-pipelined: the next U samples' {alpha, rgb} and eikonal terms are in
+// flight while the current U go through the serial recurrence. Loads use clamped indices so they
+// issue unconditionally, ahead of the data-dependent exit. Consecutive rays go to consecutive BLOCKS:
+// the rays that carry samples are a prefix of the ray range (few and long early in training), and
+// this spreads them over all CUs. The state is stored only every SCAN_CK samples (scan_replay
+// rebuilds the rest exactly), which keeps the scattered per-lane stores off the critical path.
+template <bool STORE = true>
+__global__ void __launch_bounds__(256) k_loss_scan_ray(uint32_t cap_rays, const uint32_t* __restrict__ numsteps, const float4* __restrict__ sa,
+                                                       const float* __restrict__ ekt, float4* __restrict__ ck4, float* __restrict__ cke,
+                                                       uint32_t* __restrict__ ccount, float4* __restrict__ racc, float* __restrict__ rT) {
+	constexpr uint32_t U = 8;
+	const uint32_t stride = gridDim.x * blockDim.x;
+	for (uint32_t k = threadIdx.x * gridDim.x + blockIdx.x; k < ((cap_rays + stride - 1) / stride) * stride; k += stride) {
+		const uint32_t i = k;
+		if (i >= cap_rays) continue;
+		const uint32_t ns = numsteps[2 * i], base = numsteps[2 * i + 1];
+		uint32_t cn = 0;
+		float T = 1.f, r0 = 0.f, r1 = 0.f, r2 = 0.f, ws = 0.f, ek = 0.f;
+		if (ns > 0) {
+			const uint32_t last = base + ns - 1;
+			float4 qn[U]; float en[U];
+#pragma unroll
+			for (uint32_t u = 0; u < U; ++u) { const uint32_t s = min(base + u, last); qn[u] = sa[s]; en[u] = ekt[s]; }
+			bool done = false;
+			for (uint32_t c = 0; c < ns && !done; c += U) {
+				float4 q[U]; float e[U];
+#pragma unroll
+				for (uint32_t u = 0; u < U; ++u) { q[u] = qn[u]; e[u] = en[u]; }
+				if (c + U < ns) {
+#pragma unroll
+					for (uint32_t u = 0; u < U; ++u) { const uint32_t s = min(base + c + U + u, last); qn[u] = sa[s]; en[u] = ekt[s]; }
+				}
+#pragma unroll
+				for (uint32_t u = 0; u < U; ++u) {
+					if (c + u >= ns || T < 1e-4f) { done = true; break; }
+					const uint32_t s = base + c + u;
+					if (STORE && (s & (SCAN_CK - 1)) == 0) { ck4[s / SCAN_CK] = make_float4(T, r0, r1, r2); cke[s / SCAN_CK] = ek; }
+					const float w = q[u].x * T;
+					r0 += w * q[u].y; r1 += w * q[u].z; r2 += w * q[u].w;
+					ws += w;
+					ek += e[u];
+					T *= (1.f - q[u].x);
+					++cn;
+				}
+			}
+		}
+		ccount[i] = cn;
+		racc[i] = make_float4(r0, r1, r2, ws);
+		rT[i] = T;
+	}
+}
+
+__global__ void __launch_bounds__(256) k_loss_ray(uint32_t cap_rays, StepState* __restrict__ st, DPInfo dp, DevDataset ds, LossParams lp,
+                                                  uint32_t* __restrict__ numsteps, const uint32_t* __restrict__ ccount,
+                                                  const uint32_t* __restrict__ cbase, const float4* __restrict__ sa, const float* __restrict__ ekt,
+                                                  const float4* __restrict__ ck4, const float* __restrict__ cke,
+                                                  float4* __restrict__ racc, const float* __restrict__ rT, float4* __restrict__ rgr,
+                                                  float* __restrict__ loss_out, float* __restrict__ ek_out, float* __restrict__ mask_out) {
 	const uint32_t R = st->rays_per_batch;
 	const uint32_t n_rays_global = R * dp.world, n_rays_total = st->n_rays_total;
 	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cap_rays; i += gridDim.x * blockDim.x) {
@@ -274,30 +464,10 @@ __global__ void __launch_bounds__(256) k_loss_write(uint32_t cap_rays, StepState
 		if (i == cap_rays - 1) st->compacted_counter = cb + cn;
 		loss_out[i] = 0.f; ek_out[i] = 0.f; mask_out[i] = 0.f;
 		if (ns == 0) { numsteps[2 * i] = 0; numsteps[2 * i + 1] = cb; continue; }
-		const float* rr = rays + 6 * (size_t)i;
-		const float ro[3] = {rr[0], rr[1], rr[2]};
-		const float nr = sqrtf((rr[3] * rr[3] + rr[4] * rr[4]) + rr[5] * rr[5]);
-		float dir[3] = {nr > 0 ? rr[3] / nr : rr[3], nr > 0 ? rr[4] / nr : rr[4], nr > 0 ? rr[5] / nr : rr[5]};
-		const float diag[3] = {ds.aabb_max[0] - ds.aabb_min[0], ds.aabb_max[1] - ds.aabb_min[1], ds.aabb_max[2] - ds.aabb_min[2]};
-		// first pass: composite (rgb_ray, weight_sum) over the cn used samples
-		float T = 1.f, rgb_ray[3] = {0, 0, 0}, weight_sum = 0.f;
-		for (uint32_t j = 0; j < cn; ++j) {
-			const half_t* lo = net_out + (size_t)(base + j) * OUT_W;
-			const float* ci = coords + (size_t)(base + j) * COORD_W;
-			if (j == 0) {
-				float u[3] = {(float)lo[8] * 2.0f - 1.0f, (float)lo[9] * 2.0f - 1.0f, (float)lo[10] * 2.0f - 1.0f};
-				const float n2 = sqrtf((u[0] * u[0] + u[1] * u[1]) + u[2] * u[2]);
-#pragma unroll
-				for (int k = 0; k < 3; ++k) dir[k] = n2 > 0 ? u[k] / n2 : u[k];
-			}
-			const Alpha a = neus_alpha(lo, dir, unwarp_dt(ci[3]), lp.cos_anneal);
-			const float weight = a.alpha * T;
-#pragma unroll
-			for (int k = 0; k < 3; ++k) rgb_ray[k] += weight * det_logistic((float)lo[k]);
-			weight_sum += weight;
-			T *= (1.f - a.alpha);
-		}
-		// target pixel and background (same RNG stream as the sampler)
+		const float4 acc = racc[i];
+		float rgb_ray[3] = {acc.x, acc.y, acc.z}, weight_sum = acc.w;
+		const float T = rT[i];
+		// target pixel and background (same RNG stream as the sampler; testbed_nerf.cu:1632-1660)
 		const uint32_t ig = dp.rank * R + i;
 		pcg32 rng(lp.rng_state, lp.rng_inc);
 		rng.advance((int64_t)(uint32_t)(ig * N_MAX_RANDOM_SAMPLES_PER_RAY));
@@ -338,77 +508,111 @@ __global__ void __launch_bounds__(256) k_loss_write(uint32_t cap_rays, StepState
 		const float mean_loss = ((lloss[0] + lloss[1]) + lloss[2]) / 3.0f;
 		loss_out[i] = mean_loss / (float)n_rays_global;
 		mask_out[i] = -(mask_gt * logf(weight_sum) + (1 - mask_gt) * logf(1 - weight_sum));
-		const float loss_scale = lp.loss_scale / n_rays_global;
-		// gradient pass (testbed_nerf.cu:1775-1959)
-		float rgb2[3] = {0, 0, 0};
-		float ek_acc = 0.f;
-		T = 1.f;
-		for (uint32_t j = 0; j < comp; ++j) {
-			const float* ci = coords + (size_t)(base + j) * COORD_W;
-			float* co = coords_out + (size_t)(cb + j) * COORD_W;
+		float Tb;
+		const ScanState sc = scan_replay(base, base + comp - 1, sa, ekt, ck4, cke, Tb);
+		ek_out[i] = sc.ek / ((float)comp * (float)n_rays_global);
+		rgr[i] = make_float4(lgrad[0], lgrad[1], lgrad[2], gws * (1 - weight_sum));
+		racc[i] = make_float4(rgb_ray[0], rgb_ray[1], rgb_ray[2], 0.f);
+	}
+}
+
+// gradient of one compacted sample (testbed_nerf.cu:1775-1959)
+__global__ void __launch_bounds__(256) k_loss_grad(uint32_t cap, const StepState* __restrict__ st, DPInfo dp, LossParams lp,
+                                                   const float* __restrict__ coords, const half_t* __restrict__ net_out,
+                                                   const uint32_t* __restrict__ numsteps, const uint32_t* __restrict__ sample_ray,
+                                                   const uint32_t* __restrict__ rbase, const float4* __restrict__ sa, const float* __restrict__ ekt,
+                                                   const float4* __restrict__ ck4, const float* __restrict__ cke, const float4* __restrict__ racc,
+                                                   const float4* __restrict__ rgr, float* __restrict__ coords_out, half_t* __restrict__ dL_dout) {
+	const uint32_t n = min(st->n_kept, cap);
+	const uint32_t n_rays_global = st->rays_per_batch * dp.world;
+	const float loss_scale = lp.loss_scale / n_rays_global;
+	for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < n; s += gridDim.x * blockDim.x) {
+		const uint32_t r = sample_ray[s];
+		const uint32_t rb = rbase[r];
+		const uint32_t j = s - rb;
+		const uint32_t comp = numsteps[2 * r];
+		if (j >= comp) continue;
+		const uint32_t cb = numsteps[2 * r + 1];
+		const float* ci = coords + (size_t)s * COORD_W;
+		float* co = coords_out + (size_t)(cb + j) * COORD_W;
 #pragma unroll
-			for (int k = 0; k < COORD_W; ++k) co[k] = ci[k];
-			const half_t* lo = net_out + (size_t)(base + j) * OUT_W;
-			const Alpha a = neus_alpha(lo, dir, unwarp_dt(ci[3]), lp.cos_anneal);
-			float raw[3], rgb[3];
+		for (int k = 0; k < COORD_W; ++k) co[k] = ci[k];
+		half_t lo[16]; load_out(net_out, s, lo);
+		float dir[3]; bent_dir(lo, dir);
+		const Alpha a = neus_alpha(lo, dir, unwarp_dt(ci[3]), lp.cos_anneal);
+		float Tb;
+		const ScanState P = scan_replay(rb, s, sa, ekt, ck4, cke, Tb);
+		const float4 G = rgr[r], A = racc[r];
+		const float lgrad[3] = {G.x, G.y, G.z}, rgb_ray[3] = {A.x, A.y, A.z}, rgb2[3] = {P.r0, P.r1, P.r2};
+		const float4 q = sa[s];
+		const float rgb[3] = {q.y, q.z, q.w};
+		float raw[3];
 #pragma unroll
-			for (int k = 0; k < 3; ++k) { raw[k] = (float)lo[k]; rgb[k] = det_logistic(raw[k]); }
-			const float weight = a.alpha * T;
+		for (int k = 0; k < 3; ++k) raw[k] = (float)lo[k];
+		const float weight = a.alpha * Tb;
+		const float T = Tb * (1.f - a.alpha);
+		float dl[16];
 #pragma unroll
-			for (int k = 0; k < 3; ++k) rgb2[k] += weight * rgb[k];
-			T *= (1.f - a.alpha);
-			float dl[16];
+		for (int k = 0; k < 16; ++k) dl[k] = 0.0f;
 #pragma unroll
-			for (int k = 0; k < 16; ++k) dl[k] = 0.0f;
-#pragma unroll
-			for (int k = 0; k < 3; ++k) {
-				const float sig = det_logistic(raw[k]);
-				dl[k] = loss_scale * ((weight * lgrad[k]) * (sig * (1 - sig)) + fmaxf(0.0f, 0.0f * raw[k]));
-			}
-			float tr[3];
-#pragma unroll
-			for (int k = 0; k < 3; ++k) tr[k] = T * rgb[k] - (rgb_ray[k] - rgb2[k]);
-			const float dot = (lgrad[0] * tr[0] + lgrad[1] * tr[1]) + lgrad[2] * tr[2];
-			const float dloss_dalpha = (dot + gws * (1 - weight_sum)) / (1.0f - a.alpha + 1e-5);
-			float dadem = 0, dem_dsdf = 0, dem_dinvs = 0, dadpe = 0, dpe_dinvs = 0, dpe_dic = 0, dem_dic = 0;
-			if (!(a.p_div_c <= 0.0f || a.p_div_c >= 1.0f)) {
-				const float plus_x = a.inv_s * a.iter_cos * a.dt;
-				const float plus_e = det_expf(plus_x);
-				const float e_minus = det_expf(-a.next_sdf * a.inv_s);
-				dem_dsdf = -a.inv_s * e_minus;
-				dem_dinvs = -a.next_sdf * e_minus;
-				const float aa = 1 + e_minus;
-				const float bb = 1 + plus_e * e_minus;
-				const float cc = 1e-5 + 1 / (1 + plus_e * e_minus);
-				const float delta = aa * (bb * bb) * (cc * cc);
-				dadem = -(plus_e / (delta) - 1 / (aa * aa * cc));
-				dadpe = -e_minus / (delta);
-				dpe_dinvs = plus_e * a.iter_cos * a.dt;
-				dpe_dic = plus_e * a.inv_s * a.dt;
-				dem_dic = -a.inv_s * e_minus * a.dt * 0.5;
-			}
-			const float dloss_dinvs = dloss_dalpha * (dadem * dem_dinvs + dadpe * dpe_dinvs);
-			const float dloss_dvar = dloss_dinvs * a.inv_s * 10;
-			const float d_ic_tc = a.true_cos >= 0 ? 0.0f : 1.0f;
-			const float pg[3] = {(float)lo[4], (float)lo[5], (float)lo[6]};
-			const float gn = sqrt((double)(pg[0] * pg[0] + pg[1] * pg[1] + pg[2] * pg[2]) + 1e-6);
-			const float gn_inv = 1 - 1 / gn;
-			const float dloss_dnn = dloss_dalpha * (dadem * dem_dic + dpe_dic * dadpe) * d_ic_tc;
-			const float dloss_dsdf = dloss_dalpha * dadem * dem_dsdf;
-			dl[3] = loss_scale * dloss_dsdf;
-			ek_acc += (gn - 1.0f) * (gn - 1.0f);
-#pragma unroll
-			for (int k = 0; k < 3; ++k) dl[4 + k] = rh(lp.ek_w * 2 * lp.loss_scale * gn_inv * pg[k]);
-			dl[7] = rh(loss_scale * dloss_dvar);
-#pragma unroll
-			for (int k = 0; k < 3; ++k) dl[8 + k] = rh(loss_scale * dloss_dnn * dir[k]);
-			h8 o0, o1;
-#pragma unroll
-			for (int k = 0; k < 8; ++k) { o0[k] = (half_t)dl[k]; o1[k] = (half_t)dl[8 + k]; }
-			half_t* dst = dL_dout + (size_t)(cb + j) * OUT_W;
-			*(h8*)dst = o0; *(h8*)(dst + 8) = o1;
+		for (int k = 0; k < 3; ++k) {
+			const float sig = rgb[k];
+			dl[k] = loss_scale * ((weight * lgrad[k]) * (sig * (1 - sig)) + fmaxf(0.0f, 0.0f * raw[k]));
 		}
-		ek_out[i] = ek_acc / ((float)comp * (float)n_rays_global);
+		float tr[3];
+#pragma unroll
+		for (int k = 0; k < 3; ++k) tr[k] = T * rgb[k] - (rgb_ray[k] - rgb2[k]);
+		const float dot = (lgrad[0] * tr[0] + lgrad[1] * tr[1]) + lgrad[2] * tr[2];
+		const float dloss_dalpha = (dot + G.w) / (1.0f - a.alpha + 1e-5);
+		float dadem = 0, dem_dsdf = 0, dem_dinvs = 0, dadpe = 0, dpe_dinvs = 0, dpe_dic = 0, dem_dic = 0;
+		if (!(a.p_div_c <= 0.0f || a.p_div_c >= 1.0f)) {
+			const float plus_x = a.inv_s * a.iter_cos * a.dt;
+			const float plus_e = det_expf(plus_x);
+			const float e_minus = det_expf(-a.next_sdf * a.inv_s);
+			dem_dsdf = -a.inv_s * e_minus;
+			dem_dinvs = -a.next_sdf * e_minus;
+			const float aa = 1 + e_minus;
+			const float bb = 1 + plus_e * e_minus;
+			const float cc = 1e-5 + 1 / (1 + plus_e * e_minus);
+			const float delta = aa * (bb * bb) * (cc * cc);
+			dadem = -(plus_e / (delta) - 1 / (aa * aa * cc));
+			dadpe = -e_minus / (delta);
+			dpe_dinvs = plus_e * a.iter_cos * a.dt;
+			dpe_dic = plus_e * a.inv_s * a.dt;
+			dem_dic = -a.inv_s * e_minus * a.dt * 0.5;
+		}
+		const float dloss_dinvs = dloss_dalpha * (dadem * dem_dinvs + dadpe * dpe_dinvs);
+		const float dloss_dvar = dloss_dinvs * a.inv_s * 10;
+		const float d_ic_tc = a.true_cos >= 0 ? 0.0f : 1.0f;
+		const float pg[3] = {(float)lo[4], (float)lo[5], (float)lo[6]};
+		const float gn = grad_norm(lo);
+		const float gn_inv = 1 - 1 / gn;
+		const float dloss_dnn = dloss_dalpha * (dadem * dem_dic + dpe_dic * dadpe) * d_ic_tc;
+		const float dloss_dsdf = dloss_dalpha * dadem * dem_dsdf;
+		dl[3] = loss_scale * dloss_dsdf;
+#pragma unroll
+		for (int k = 0; k < 3; ++k) dl[4 + k] = rh(lp.ek_w * 2 * lp.loss_scale * gn_inv * pg[k]);
+		dl[7] = rh(loss_scale * dloss_dvar);
+#pragma unroll
+		for (int k = 0; k < 3; ++k) dl[8 + k] = rh(loss_scale * dloss_dnn * dir[k]);
+		h8 o0, o1;
+#pragma unroll
+		for (int k = 0; k < 8; ++k) { o0[k] = (half_t)dl[k]; o1[k] = (half_t)dl[8 + k]; }
+		half_t* dst = dL_dout + (size_t)(cb + j) * OUT_W;
+		*(h8*)dst = o0; *(h8*)(dst + 8) = o1;
+	}
+}
+
+// sample -> ray map and per-ray base for callers that bring their own numsteps (operator path);
+// the training step gets both from k_march_write / the march scan.
+__global__ void __launch_bounds__(256) k_ray_index(uint32_t cap_rays, const uint32_t* __restrict__ numsteps, StepState* __restrict__ st,
+                                                   uint32_t* __restrict__ sample_ray, uint32_t* __restrict__ rbase) {
+	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cap_rays; i += gridDim.x * blockDim.x) {
+		const uint32_t ns = numsteps[2 * i], base = numsteps[2 * i + 1];
+		rbase[i] = base;
+		if (ns == 0) continue;
+		for (uint32_t j = 0; j < ns; ++j) sample_ray[base + j] = i;
+		atomicMax(&st->n_kept, base + ns);
 	}
 }
 
@@ -453,22 +657,45 @@ __global__ void k_step_counters(StepState* st, uint32_t target_batch, uint32_t m
 
 // ---------------------------------------------------------------- host launchers
 static inline uint32_t ray_blocks(uint32_t cap) { return std::max<uint32_t>(1, std::min<uint32_t>((cap + 255) / 256, 2048)); }
+void launch_bitfield_linear(hipStream_t s, const uint8_t* bitfield, uint32_t* lin) {
+	k_bitfield_linear<<<GRID3 / 32 / 256, 256, 0, s>>>(bitfield, lin);
+}
 void launch_march_count(hipStream_t s, uint32_t cap, const StepState* st, DPInfo dp, const DevDataset& ds, const uint8_t* bitfield,
-                        uint64_t rng_state, uint64_t rng_inc, float* rays, float* startt, uint32_t* nreq) {
-	k_march_count<<<ray_blocks(cap), 256, 0, s>>>(cap, st, dp, ds, bitfield, rng_state, rng_inc, rays, startt, nreq);
+                        const uint32_t* lin, uint64_t rng_state, uint64_t rng_inc, float* rays, float* ckpt, uint32_t* nreq) {
+	k_march_count<<<ray_blocks(cap), 256, 0, s>>>(cap, st, dp, ds, bitfield, ds.cone_angle == 0.0f ? lin : nullptr, rng_state, rng_inc, rays, ckpt, nreq);
 }
-void launch_march_write(hipStream_t s, uint32_t cap, StepState* st, const DevDataset& ds, const uint8_t* bitfield, const float* rays,
-                        const float* startt, const uint32_t* nreq, const uint32_t* base, uint32_t* numsteps, float* coords) {
-	k_march_write<<<ray_blocks(cap), 256, 0, s>>>(cap, st, ds, bitfield, rays, startt, nreq, base, numsteps, coords);
+void launch_march_write(hipStream_t s, uint32_t cap, StepState* st, const DevDataset& ds, const uint8_t* bitfield, const uint32_t* lin,
+                        const float* rays, const float* ckpt, const uint32_t* nreq, const uint32_t* base, uint32_t* numsteps, float* coords,
+                        uint32_t* sample_ray) {
+	const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((cap * MARCH_SEGS + 255) / 256, 16384));
+	k_march_write<<<blocks, 256, 0, s>>>(cap, st, ds, bitfield, ds.cone_angle == 0.0f ? lin : nullptr, rays, ckpt, nreq, base, numsteps, coords, sample_ray);
 }
-void launch_loss_count(hipStream_t s, uint32_t cap, const StepState* st, const DevDataset& ds, const float* rays, const uint32_t* numsteps,
-                       const float* coords, const half_t* net_out, float cos_anneal, uint32_t* ccount) {
-	k_loss_count<<<ray_blocks(cap), 256, 0, s>>>(cap, st, ds, rays, numsteps, coords, net_out, cos_anneal, ccount);
+static inline uint32_t sample_blocks(uint32_t cap) { return std::max<uint32_t>(1, std::min<uint32_t>((cap + 255) / 256, 16384)); }
+void launch_loss_alpha(hipStream_t s, uint32_t cap_samples, const StepState* st, const float* coords, const half_t* net_out, float cos_anneal,
+                       const LossWork& w) {
+	k_loss_alpha<<<sample_blocks(cap_samples), 256, 0, s>>>(cap_samples, st, coords, net_out, cos_anneal, w.sa, w.ekt);
 }
-void launch_loss_write(hipStream_t s, uint32_t cap, StepState* st, DPInfo dp, const DevDataset& ds, const LossParams& lp, const float* rays,
-                       uint32_t* numsteps, const float* coords, const half_t* net_out, const uint32_t* ccount, const uint32_t* cbase,
-                       float* coords_out, half_t* dL_dout, float* loss, float* ek, float* mask) {
-	k_loss_write<<<ray_blocks(cap), 256, 0, s>>>(cap, st, dp, ds, lp, rays, numsteps, coords, net_out, ccount, cbase, coords_out, dL_dout, loss, ek, mask);
+void launch_loss_scan_ray(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, const LossWork& w, uint32_t* ccount) {
+	const uint32_t blocks = ray_blocks(cap_rays);
+	k_loss_scan_ray<true><<<blocks, 256, 0, s>>>(cap_rays, numsteps, w.sa, w.ekt, w.ck4, w.cke, ccount, w.racc, w.rT);
+}
+// timing experiments (neus_debug_time_kernel): variant 1 = the recurrence without its per-sample stores
+void debug_launch_loss_scan(hipStream_t s, int variant, uint32_t cap_rays, const uint32_t* numsteps, const LossWork& w, uint32_t* ccount) {
+	if (variant == 1) k_loss_scan_ray<false><<<ray_blocks(cap_rays), 256, 0, s>>>(cap_rays, numsteps, w.sa, w.ekt, w.ck4, w.cke, ccount, w.racc, w.rT);
+	else launch_loss_scan_ray(s, cap_rays, numsteps, w, ccount);
+}
+void launch_loss_ray(hipStream_t s, uint32_t cap_rays, StepState* st, DPInfo dp, const DevDataset& ds, const LossParams& lp, uint32_t* numsteps,
+                     const uint32_t* ccount, const uint32_t* cbase, const LossWork& w, float* loss, float* ek, float* mask) {
+	k_loss_ray<<<ray_blocks(cap_rays), 256, 0, s>>>(cap_rays, st, dp, ds, lp, numsteps, ccount, cbase, w.sa, w.ekt, w.ck4, w.cke, w.racc, w.rT,
+	                                                  w.rgr, loss, ek, mask);
+}
+void launch_loss_grad(hipStream_t s, uint32_t cap_samples, const StepState* st, DPInfo dp, const LossParams& lp, const float* coords,
+                      const half_t* net_out, const uint32_t* numsteps, const LossWork& w, float* coords_out, half_t* dL_dout) {
+	k_loss_grad<<<sample_blocks(cap_samples), 256, 0, s>>>(cap_samples, st, dp, lp, coords, net_out, numsteps, w.sample_ray, w.rbase, w.sa,
+	                                                         w.ekt, w.ck4, w.cke, w.racc, w.rgr, coords_out, dL_dout);
+}
+void launch_ray_index(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, StepState* st, uint32_t* sample_ray, uint32_t* rbase) {
+	k_ray_index<<<ray_blocks(cap_rays), 256, 0, s>>>(cap_rays, numsteps, st, sample_ray, rbase);
 }
 void launch_rollover(hipStream_t s, uint32_t n_elements, const StepState* st, float* coords, half_t* dL_dout) {
 	k_rollover<<<std::max<uint32_t>(1, std::min<uint32_t>((n_elements + 255) / 256, 2048)), 256, 0, s>>>(n_elements, st, coords, dL_dout);

@@ -9,6 +9,10 @@
 // and every A (weight) fragment is loaded with the same permutation (loadA), as is every B
 // fragment built from memory, so all products are consistent.
 //
+// Weights are staged once per block into LDS (row stride padded by 8 halves against bank
+// conflicts) and every A fragment is read from there: the register file holds activations only,
+// which keeps several waves per SIMD resident to hide the gather / HBM latency.
+//
 // Reference semantics (per sample):
 //   density MLP  fully_fused_mlp.cu:678-812 (1 hidden ReLU layer, linear 16-wide output)
 //   grad SDF     nerf_network.h:228-253 + kernel_grid_backward_input (grid.h:803-830)
@@ -18,6 +22,7 @@
 // Storage rounding points (fp16) follow the reference: hidden activations, deltas, the
 // density output, dSDF/d(input), the network output and dL/doutput.
 #include "kernels.h"
+#include "grid_common.h"
 #include <algorithm>
 
 namespace neus {
@@ -27,10 +32,13 @@ __device__ __forceinline__ constexpr int pi_row(int j, int h) { return 8 * (j >>
 // accumulator register i of lane half h holds row acc_row(i,h) of the 32-row tile
 __device__ __forceinline__ constexpr int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
 
-__device__ __forceinline__ h8 loadA(const half_t* __restrict__ W, uint32_t ld, uint32_t M, uint32_t row, uint32_t kbase, uint32_t h) {
+// A weight matrix [rows][ld] (fp16, row-major) in LDS or global memory.
+struct MatRef { const half_t* p; uint32_t ld; };
+
+__device__ __forceinline__ h8 loadA(MatRef W, uint32_t M, uint32_t row, uint32_t kbase, uint32_t h) {
 	h8 a;
 	if (row < M) {
-		const half_t* p = W + (size_t)row * ld + kbase + 4 * h;
+		const half_t* p = W.p + (size_t)row * W.ld + kbase + 4 * h;
 		const h4 lo = *(const h4*)p;
 		const h4 hi = *(const h4*)(p + 8);
 		a = (h8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -39,7 +47,7 @@ __device__ __forceinline__ h8 loadA(const half_t* __restrict__ W, uint32_t ld, u
 	}
 	return a;
 }
-// B fragment (k-step s of an accumulator tile), optional ReLU mask source
+// B fragment (k-step s of an accumulator tile)
 __device__ __forceinline__ h8 accB(const f16v& acc, int s) {
 	h8 b;
 #pragma unroll
@@ -65,36 +73,133 @@ template <int L> struct Dims {
 	static constexpr int NF = 2 * L;               // encoding features
 };
 
-// Forward state kept in registers for one 32-sample chunk.
-template <int L, int W> struct Fwd {
-	static constexpr int MT = (W + 31) / 32;   // hidden tiles
-	static constexpr int HKS = W / 16;          // hidden k-steps
-	h8 dinB[Dims<L>::DKS];
-	f16v H0[MT];          // density hidden (post-ReLU, fp16-rounded)
-	f16v D1;              // density output (fp16-rounded), rows 0..15 in regs 0..7
-	h8 GhB[HKS];          // relu'(H0) . W1d[0]  (also b2 of the double backward)
-	f16v Gi[Dims<L>::DMT];// dSDF/d(density input) (fp16-rounded)
-	float grad[3];        // dSDF/dx
-	h8 rinB[3];           // rgb input fragments
-	f16v H1[MT], H2[MT];  // rgb hidden (post-ReLU, fp16)
-	f16v O;               // rgb output (fp16-rounded)
+// ---------------------------------------------------------------- LDS weight staging
+// copy a [rows][cols] fp16 matrix (cols % 8 == 0) into LDS with row stride cols + 8
+__device__ __forceinline__ void stage_mat(half_t* dst, const half_t* __restrict__ src, uint32_t rows, uint32_t cols) {
+	const uint32_t cv = cols / 8, n = rows * cv;
+	for (uint32_t e = threadIdx.x; e < n; e += blockDim.x) {
+		const uint32_t r = e / cv, c = (e % cv) * 8;
+		*(h8*)(dst + (size_t)r * (cols + 8) + c) = *(const h8*)(src + (size_t)r * cols + c);
+	}
+}
+
+// Re-derives a weight view from an offset the compiler cannot see through, once per loop
+// iteration: without it the LDS fragment loads are loop-invariant and get hoisted into (and
+// exhaust) the register file.
+__device__ __forceinline__ MatRef rebase(MatRef m, uint32_t z) { return {m.p + z, m.ld}; }
+__device__ __forceinline__ uint32_t opaque_zero() { uint32_t z = 0; asm volatile("" : "+v"(z)); return z; }
+
+// Weight set of the forward pass. For the fused kernels d0 / d0T are the din-PERMUTED copies
+// (MlpPtrs::d0p / d0Tp, see din_logical), for the training kernel the logical ones.
+struct FwdW {
+	MatRef d0, d1, d0T, r0, r1, r2;
+	__device__ __forceinline__ FwdW at(uint32_t z) const { return {rebase(d0, z), rebase(d1, z), rebase(d0T, z), rebase(r0, z), rebase(r1, z), rebase(r2, z)}; }
+};
+template <int L, int W> struct FwdSmem {
+	static constexpr int DIN = Dims<L>::DIN;
+	static constexpr int D0 = 0, D1 = D0 + W * (DIN + 8), D0T = D1 + 16 * (W + 8), R0 = D0T + DIN * (W + 8);
+	static constexpr int R1 = R0 + W * (48 + 8), R2 = R1 + W * (W + 8), END = R2 + 16 * (W + 8);
+};
+template <int L, int W>
+__device__ __forceinline__ FwdW stage_fwd(half_t* sm, const half_t* d0, const half_t* d0T, const MlpPtrs& w) {
+	using S = FwdSmem<L, W>;
+	constexpr int DIN = Dims<L>::DIN;
+	stage_mat(sm + S::D0, d0, W, DIN);
+	stage_mat(sm + S::D1, w.d1, 16, W);
+	stage_mat(sm + S::D0T, d0T, DIN, W);
+	stage_mat(sm + S::R0, w.r0, W, 48);
+	stage_mat(sm + S::R1, w.r1, W, W);
+	stage_mat(sm + S::R2, w.r2, 16, W);
+	FwdW f;
+	f.d0 = {sm + S::D0, DIN + 8}; f.d1 = {sm + S::D1, W + 8}; f.d0T = {sm + S::D0T, W + 8};
+	f.r0 = {sm + S::R0, 48 + 8}; f.r1 = {sm + S::R1, W + 8}; f.r2 = {sm + S::R2, W + 8};
+	return f;
+}
+
+// ---------------------------------------------------------------- fused encode: din slot layout
+// In the fused kernels each sample is held by two lanes (r, h = 0/1). Lane half h evaluates the
+// hash-grid levels l = 2m + h (m = 0..M0-1) so both halves run the same instruction stream, and
+// owns the density-input slots q = 0..DIN/2-1 of its fragments (physical row 16(q>>3)+pi(q&7,h)):
+//   h = 0 : q 0..2 = x - 0.5, then features of levels 0, 2, 4, ...
+//   h = 1 : features of levels 1, 3, 5, ...
+// If h = 0 has one feature too many (L = 14: 3 + 14 > 16), its last feature moves to h = 1's
+// next free slot through one cross-half shuffle. The first layer's weight columns (and W0^T's
+// rows) are permuted on the host to this physical order (din_logical), so the product is the
+// reference's W0 . din.
+NEUS_HD int din_logical(int L, int h, int q) {
+	const int DIN = ((3 + 2 * L) + 15) / 16 * 16, HALF = DIN / 2;
+	const int M0 = (L + 1) / 2, M1 = L / 2;
+	const int NT = (3 + 2 * M0 > HALF) ? 3 + 2 * M0 - HALF : 0;
+	if (q >= HALF) return -1;
+	if (h == 0) {
+		if (q < 3) return q;
+		const int k = q - 3;
+		if (k < 2 * M0 - NT) return 3 + 2 * (2 * (k / 2)) + (k % 2);
+		return -1;
+	}
+	if (q < 2 * M1) return 3 + 2 * (2 * (q / 2) + 1) + (q % 2);
+	if (NT == 1 && q == 2 * M1) return 3 + 2 * (2 * (M0 - 1)) + 1;
+	return -1;
+}
+NEUS_HD int din_physical_row(int h, int q) { return 16 * (q >> 3) + 8 * ((q & 7) >> 2) + 4 * h + (q & 3); }
+
+template <int L> struct Fused {
+	static constexpr int DIN = Dims<L>::DIN, HALF = DIN / 2;
+	static constexpr int M0 = (L + 1) / 2, M1 = L / 2;
+	static constexpr int NT = (3 + 2 * M0 > HALF) ? 3 + 2 * M0 - HALF : 0;
+	static_assert(NT <= 1 && 2 * M1 + NT <= HALF && 3 + 2 * M0 - NT <= HALF, "din slot layout");
 };
 
-// Reads this lane's encoding features and builds the density-input B fragments.
-template <int L>
-__device__ __forceinline__ void build_din(h8* dinB, const float x[3], const half_t* __restrict__ enc_h /*[L][ld] half2*/, uint32_t ld, uint32_t i, int h) {
-	constexpr int DIN = Dims<L>::DIN;
-	float dv[DIN];
+// Evaluates this lane's levels for position x: features ev[m] (level 2m+h) and, if DYDX, dy/dx.
+template <int L, bool DYDX>
+__device__ __forceinline__ void fused_levels(const GridLevels& gl, uint32_t valid_level, const half_t* __restrict__ grid,
+                                             const float x[3], int h, h2 ev[], float dy[][2][3]) {
+	constexpr int M0 = Fused<L>::M0;
 #pragma unroll
-	for (int k = 0; k < DIN; ++k) {
-		if (k < 3) dv[k] = rh(rh(x[k]) - 0.5f);
-		else if (k < 3 + 2 * L) dv[k] = (float)enc_h[((size_t)((k - 3) >> 1) * ld + i) * 2 + ((k - 3) & 1)];  // [L][ld] half2
-		else dv[k] = 0.f;
+	for (int m = 0; m < M0; ++m) {
+		const int l0 = 2 * m, l1 = 2 * m + 1 < L ? 2 * m + 1 : 2 * m;
+		const uint32_t l = h ? (uint32_t)l1 : (uint32_t)l0;
+		const bool act = (h ? (2 * m + 1 < L) : true) && l <= valid_level;
+		ev[m] = (h2){(half_t)0.f, (half_t)0.f};
+		if (DYDX) {
+#pragma unroll
+			for (int f = 0; f < 2; ++f)
+#pragma unroll
+				for (int d = 0; d < 3; ++d) dy[m][f][d] = 0.f;
+		}
+		if (act) {
+			const float sc = h ? gl.scale[l1] : gl.scale[l0];
+			const uint32_t res = h ? gl.res[l1] : gl.res[l0];
+			const uint32_t o0 = h ? gl.offset[l1] : gl.offset[l0], o1 = h ? gl.offset[l1 + 1] : gl.offset[l0 + 1];
+			const LevelSetup s = level_setup(sc, res, o1 - o0, x[0], x[1], x[2]);
+			h2 v[8];
+			gather_corners(s, grid + (size_t)o0 * 2, v);
+			ev[m] = interp_features(s, v);
+			if (DYDX) interp_dydx(s, v, dy[m]);
+		}
 	}
-#pragma unroll
-	for (int ks = 0; ks < Dims<L>::DKS; ++ks)
-#pragma unroll
-		for (int j = 0; j < 8; ++j) dinB[ks][j] = (half_t)(h ? dv[16 * ks + pi_row(j, 1)] : dv[16 * ks + pi_row(j, 0)]);
+}
+
+// Value of slot q on this lane: h ? (h=1 mapping) : (h=0 mapping), all indices compile-time.
+template <int L>
+__device__ __forceinline__ float slot_value(int q, int h, const float xm[3], const h2 ev[], float tv) {
+	constexpr int M0 = Fused<L>::M0, M1 = Fused<L>::M1, NT = Fused<L>::NT;
+	float v0 = 0.f, v1 = 0.f;
+	if (q < 3) v0 = xm[q];
+	else if (q - 3 < 2 * M0 - NT) v0 = (float)ev[(q - 3) / 2][(q - 3) % 2];
+	if (q < 2 * M1) v1 = (float)ev[q / 2][q % 2];
+	else if (NT == 1 && q == 2 * M1) v1 = tv;
+	return h ? v1 : v0;
+}
+// d(slot q)/dx_d on this lane (0 for pads; the xyz slots are the identity, handled by the caller)
+template <int L>
+__device__ __forceinline__ float slot_dydx(int q, int h, int d, const float dy[][2][3], const float tdy[3]) {
+	constexpr int M0 = Fused<L>::M0, M1 = Fused<L>::M1, NT = Fused<L>::NT;
+	float v0 = 0.f, v1 = 0.f;
+	if (q >= 3 && q - 3 < 2 * M0 - NT) v0 = dy[(q - 3) / 2][(q - 3) % 2][d];
+	if (q < 2 * M1) v1 = dy[q / 2][q % 2][d];
+	else if (NT == 1 && q == 2 * M1) v1 = tdy[d];
+	return h ? v1 : v0;
 }
 
 __device__ __forceinline__ void sh16(const float wd[3], float out[16]) {
@@ -118,48 +223,261 @@ __device__ __forceinline__ void sh16(const float wd[3], float out[16]) {
 	out[15] = 0.59004358992664352f * x * (-x2 + 3.0f * y2);
 }
 
-// Full NerfNetwork forward for this lane's sample (r = lane & 31, h = lane >> 5).
-// Every lane of the wave must call this (MFMA), valid or not.
-template <int L, int W>
-__device__ __forceinline__ void forward_chunk(Fwd<L, W>& F, const MlpPtrs& w, const float x[3], const float wd[3],
-                                              const half_t* __restrict__ enc_h, const float* __restrict__ dydx, uint32_t ld,
-                                              uint32_t i, bool valid, int r, int h) {
-	constexpr int DIN = Dims<L>::DIN, DKS = Dims<L>::DKS, DMT = Dims<L>::DMT;
-	constexpr int MT = Fwd<L, W>::MT, HKS = Fwd<L, W>::HKS;
-	build_din<L>(F.dinB, x, enc_h, ld, valid ? i : 0, h);
-	// density layer 0 + ReLU
+// rgb MLP input fragments (ks0 = density output, ks1 = SH, ks2 = [xyz, grad sdf, 0...]) and the
+// three rgb layers; returns the fp16-rounded output tile.
+template <int W>
+__device__ __forceinline__ f16v rgb_forward(const FwdW& w, const f16v& D1, const float x[3], const float wd[3], const float grad[3],
+                                            int r, int h, h8 rinB[3], f16v* H1, f16v* H2) {
+	constexpr int MT = (W + 31) / 32, HKS = W / 16;
+	rinB[0] = accB(D1, 0);
+	{
+		float sh[16]; sh16(wd, sh);
+#pragma unroll
+		for (int j = 0; j < 8; ++j) rinB[1][j] = (half_t)(h ? sh[pi_row(j, 1)] : sh[pi_row(j, 0)]);
+		float r32[16];
+#pragma unroll
+		for (int k = 0; k < 16; ++k) r32[k] = 0.f;
+		r32[0] = x[0]; r32[1] = x[1]; r32[2] = x[2];
+		r32[3] = grad[0]; r32[4] = grad[1]; r32[5] = grad[2];
+#pragma unroll
+		for (int j = 0; j < 8; ++j) rinB[2][j] = (half_t)(h ? r32[pi_row(j, 1)] : r32[pi_row(j, 0)]);
+	}
 #pragma unroll
 	for (int mt = 0; mt < MT; ++mt) {
 		f16v acc = zero16();
 #pragma unroll
-		for (int ks = 0; ks < DKS; ++ks) acc = mfma(loadA(w.d0, DIN, W, 32 * mt + r, 16 * ks, h), F.dinB[ks], acc);
-		F.H0[mt] = rh16(relu16(acc));
+		for (int ks = 0; ks < 3; ++ks) acc = mfma(loadA(w.r0, W, 32 * mt + r, 16 * ks, h), rinB[ks], acc);
+		H1[mt] = rh16(relu16(acc));
 	}
-	// density layer 1 (16 outputs)
+#pragma unroll
+	for (int mt = 0; mt < MT; ++mt) {
+		f16v acc = zero16();
+#pragma unroll
+		for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.r1, W, 32 * mt + r, 16 * ks, h), accB(H1[ks >> 1], ks & 1), acc);
+		H2[mt] = rh16(relu16(acc));
+	}
+	f16v acc = zero16();
+#pragma unroll
+	for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.r2, 16, r, 16 * ks, h), accB(H2[ks >> 1], ks & 1), acc);
+	return rh16(acc);
+}
+
+// density layer 0 (+ReLU), layer 1 (16 outputs), G_h = relu'(H0) . W1d[0], G_in = W0d^T G_h
+template <int L, int W>
+__device__ __forceinline__ void density_forward(const FwdW& w, const h8* dinB, int r, int h, f16v* H0, f16v& D1, h8* GhB, f16v* Gi) {
+	constexpr int DIN = Dims<L>::DIN, DKS = Dims<L>::DKS, DMT = Dims<L>::DMT, MT = (W + 31) / 32, HKS = W / 16;
+#pragma unroll
+	for (int mt = 0; mt < MT; ++mt) {
+		f16v acc = zero16();
+#pragma unroll
+		for (int ks = 0; ks < DKS; ++ks) acc = mfma(loadA(w.d0, W, 32 * mt + r, 16 * ks, h), dinB[ks], acc);
+		H0[mt] = rh16(relu16(acc));
+	}
 	{
 		f16v acc = zero16();
 #pragma unroll
-		for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.d1, W, 16, r, 16 * ks, h), accB(F.H0[ks >> 1], ks & 1), acc);
-		F.D1 = rh16(acc);
+		for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.d1, 16, r, 16 * ks, h), accB(H0[ks >> 1], ks & 1), acc);
+		D1 = rh16(acc);
 	}
-	// G_h = relu'(H0) . W1d[0]: row 0 of W1d loaded in the same (pi) order as the H0 fragments
+	// row 0 of W1d loaded in the same (pi) order as the H0 fragments
 #pragma unroll
 	for (int ks = 0; ks < HKS; ++ks) {
-		const h8 w1row = loadA(w.d1, W, 16, 0, 16 * ks, h);
-		const f16v& hh = F.H0[ks >> 1];
+		const h8 w1row = loadA(w.d1, 16, 0, 16 * ks, h);
+		const f16v& hh = H0[ks >> 1];
 		h8 g;
 #pragma unroll
 		for (int j = 0; j < 8; ++j) g[j] = hh[8 * (ks & 1) + j] > 0.f ? w1row[j] : (half_t)0.f;
-		F.GhB[ks] = g;
+		GhB[ks] = g;
 	}
-	// G_in = W0d^T G_h  (DIN rows)
 #pragma unroll
 	for (int mt = 0; mt < DMT; ++mt) {
 		f16v acc = zero16();
 #pragma unroll
-		for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.d0T, W, DIN, 32 * mt + r, 16 * ks, h), F.GhB[ks], acc);
-		F.Gi[mt] = rh16(acc);
+		for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.d0T, DIN, 32 * mt + r, 16 * ks, h), GhB[ks], acc);
+		Gi[mt] = rh16(acc);
 	}
+}
+
+// ------------------------------------------------------------------------------------------
+// Fused pre-compaction forward (hash-grid encode + NerfNetwork::forward, nerf_network.h:145-328):
+// coords AoS7 -> out AoS16 fp16. The encodings and dy/dx never leave the registers; only the 28 B
+// coordinate and the 32 B output per sample touch HBM. n from device memory; 32 samples per
+// wave-iteration, grid-strided.
+// ------------------------------------------------------------------------------------------
+template <int L, int W>
+__global__ void __launch_bounds__(256) k_nerf_infer(const uint32_t* __restrict__ n_ptr, uint32_t n_fixed, const float* __restrict__ coords,
+                                                    const GridLevels gl, uint32_t valid_level, const half_t* __restrict__ grid,
+                                                    MlpPtrs wp, half_t* __restrict__ out) {
+	constexpr int DKS = Dims<L>::DKS, DMT = Dims<L>::DMT, HALF = Fused<L>::HALF, M0 = Fused<L>::M0, NT = Fused<L>::NT;
+	constexpr int MT = (W + 31) / 32, HKS = W / 16;
+	__shared__ half_t sm[FwdSmem<L, W>::END];
+	const FwdW w0 = stage_fwd<L, W>(sm, wp.d0p, wp.d0Tp, wp);
+	__syncthreads();
+	const uint32_t n = n_ptr ? *n_ptr : n_fixed;
+	const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+	const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+	const uint32_t n_waves = (gridDim.x * blockDim.x) >> 6;
+	const float var = (float)wp.var[0];
+	const half_t bias_h = (half_t)wp.sdf_bias;
+	for (uint32_t base = wave * 32; base < n; base += n_waves * 32) {
+		const FwdW w = w0.at(opaque_zero());
+		const uint32_t i = base + r;
+		const bool valid = i < n;
+		const uint32_t ic = valid ? i : 0;
+		const float* c = coords + (size_t)ic * COORD_W;
+		const float x[3] = {c[0], c[1], c[2]}, wd[3] = {c[4], c[5], c[6]};
+		// ---- encode this lane's levels
+		h2 ev[M0];
+		float dy[M0][2][3];
+		fused_levels<L, true>(gl, valid_level, grid, x, h, ev, dy);
+		float tv = 0.f, tdy[3] = {0.f, 0.f, 0.f};
+		if (NT == 1) {
+			tv = __shfl_xor((float)ev[M0 - 1][1], 32);
+#pragma unroll
+			for (int d = 0; d < 3; ++d) tdy[d] = __shfl_xor(dy[M0 - 1][1][d], 32);
+		}
+		const float xm[3] = {rh(rh(x[0]) - 0.5f), rh(rh(x[1]) - 0.5f), rh(rh(x[2]) - 0.5f)};
+		h8 dinB[DKS];
+#pragma unroll
+		for (int ks = 0; ks < DKS; ++ks)
+#pragma unroll
+			for (int j = 0; j < 8; ++j) dinB[ks][j] = (half_t)slot_value<L>(8 * ks + j, h, xm, ev, tv);
+		// ---- density MLP + dSDF/d(din)
+		f16v H0[MT], D1, Gi[DMT];
+		h8 GhB[HKS];
+		density_forward<L, W>(w, dinB, r, h, H0, D1, GhB, Gi);
+		// dSDF/dx = sum_q G_in[q] dy/dx[q] (+ identity for the xyz slots of h = 0), halves summed
+		float part[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+		for (int q = 0; q < HALF; ++q) {
+			const float gv = Gi[q / 16][q % 16];
+#pragma unroll
+			for (int d = 0; d < 3; ++d) {
+				const float id = (q == d) ? (h ? 0.f : 1.f) : 0.f;
+				part[d] += gv * (slot_dydx<L>(q, h, d, dy, tdy) + id);
+			}
+		}
+		float grad[3];
+#pragma unroll
+		for (int d = 0; d < 3; ++d) grad[d] = part[d] + __shfl_xor(part[d], 32);
+		// ---- colour MLP
+		h8 rinB[3];
+		f16v H1[MT], H2[MT];
+		const f16v O = rgb_forward<W>(w, D1, x, wd, grad, r, h, rinB, H1, H2);
+		const float row11 = __shfl_xor(O[7], 32);  // lane h=0 holds row 11 in reg 7
+		if (valid) {
+			h8 o;
+			if (h == 0) {
+				o[0] = (half_t)O[0]; o[1] = (half_t)O[1]; o[2] = (half_t)O[2];
+				o[3] = (half_t)D1[0] + bias_h;                     // half add (common_operation.cuh:964)
+				o[4] = (half_t)grad[0]; o[5] = (half_t)grad[1]; o[6] = (half_t)grad[2];
+				o[7] = (half_t)var;
+			} else {
+				o[0] = (half_t)wd[0]; o[1] = (half_t)wd[1]; o[2] = (half_t)wd[2];
+				o[3] = (half_t)row11;
+				o[4] = (half_t)O[4]; o[5] = (half_t)O[5]; o[6] = (half_t)O[6]; o[7] = (half_t)O[7];
+			}
+			*(h8*)(out + (size_t)i * OUT_W + 8 * h) = o;
+		}
+	}
+}
+
+// Density-only inference for the occupancy grid (NerfNetwork::density, nerf_network.h:656-739;
+// sdf_to_density_variance_buffer, common_operation.cuh:306-324 in fp16 arithmetic), with the
+// hash-grid encode fused in (no dy/dx needed).
+template <int L, int W>
+__global__ void __launch_bounds__(256) k_nerf_density(uint32_t n, const float* __restrict__ pos, const GridLevels gl, uint32_t valid_level,
+                                                      const half_t* __restrict__ grid, MlpPtrs wp, float* __restrict__ density) {
+	constexpr int DKS = Dims<L>::DKS, M0 = Fused<L>::M0, NT = Fused<L>::NT, MT = (W + 31) / 32, HKS = W / 16;
+	__shared__ half_t sm[FwdSmem<L, W>::END];
+	const FwdW w0 = stage_fwd<L, W>(sm, wp.d0p, wp.d0Tp, wp);
+	__syncthreads();
+	const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+	const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+	const uint32_t n_waves = (gridDim.x * blockDim.x) >> 6;
+	const half_t var_h = wp.var[0];
+	const half_t bias_h = (half_t)wp.sdf_bias;
+	for (uint32_t base = wave * 32; base < n; base += n_waves * 32) {
+		const FwdW w = w0.at(opaque_zero());
+		const uint32_t i = base + r;
+		const bool valid = i < n;
+		const uint32_t ic = valid ? i : 0;
+		const float x[3] = {pos[3 * (size_t)ic], pos[3 * (size_t)ic + 1], pos[3 * (size_t)ic + 2]};
+		h2 ev[M0];
+		float dy[1][2][3];
+		fused_levels<L, false>(gl, valid_level, grid, x, h, ev, dy);
+		const float tv = NT == 1 ? __shfl_xor((float)ev[M0 - 1][1], 32) : 0.f;
+		const float xm[3] = {rh(rh(x[0]) - 0.5f), rh(rh(x[1]) - 0.5f), rh(rh(x[2]) - 0.5f)};
+		h8 dinB[DKS];
+#pragma unroll
+		for (int ks = 0; ks < DKS; ++ks)
+#pragma unroll
+			for (int j = 0; j < 8; ++j) dinB[ks][j] = (half_t)slot_value<L>(8 * ks + j, h, xm, ev, tv);
+		f16v H0[MT];
+#pragma unroll
+		for (int mt = 0; mt < MT; ++mt) {
+			f16v acc = zero16();
+#pragma unroll
+			for (int ks = 0; ks < DKS; ++ks) acc = mfma(loadA(w.d0, W, 32 * mt + r, 16 * ks, h), dinB[ks], acc);
+			H0[mt] = rh16(relu16(acc));
+		}
+		f16v acc = zero16();
+#pragma unroll
+		for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.d1, 16, r, 16 * ks, h), accB(H0[ks >> 1], ks & 1), acc);
+		if (valid && h == 0) {
+			const half_t sdf = (half_t)acc[0] + bias_h;
+			const half_t s = (half_t)__expf((float)(var_h * (half_t)10.0f));
+			const half_t sig = (half_t)(1.0f / (1.0f + __expf(-(float)(sdf * s))));
+			const half_t dens = (s * sig) * ((half_t)1.0f - sig);
+			density[i] = (float)dens;
+		}
+	}
+}
+
+// ------------------------------------------------------------------------------------------
+// Training path: encodings and dy/dx come from k_grid_encode (logical din order).
+// ------------------------------------------------------------------------------------------
+// Forward state kept in registers for one 32-sample chunk.
+template <int L, int W> struct Fwd {
+	static constexpr int MT = (W + 31) / 32;   // hidden tiles
+	static constexpr int HKS = W / 16;          // hidden k-steps
+	h8 dinB[Dims<L>::DKS];
+	f16v H0[MT];          // density hidden (post-ReLU, fp16-rounded)
+	f16v D1;              // density output (fp16-rounded), rows 0..15 in regs 0..7
+	h8 GhB[HKS];          // relu'(H0) . W1d[0]  (also b2 of the double backward)
+	f16v Gi[Dims<L>::DMT];// dSDF/d(density input) (fp16-rounded)
+	float grad[3];        // dSDF/dx
+	h8 rinB[3];           // rgb input fragments
+	f16v H1[MT], H2[MT];  // rgb hidden (post-ReLU, fp16)
+	f16v O;               // rgb output (fp16-rounded)
+};
+
+// Reads this lane's encoding features and builds the density-input B fragments (logical order).
+template <int L>
+__device__ __forceinline__ void build_din(h8* dinB, const float x[3], const half_t* __restrict__ enc_h /*[L][ld] half2*/, uint32_t ld, uint32_t i, int h) {
+	constexpr int DIN = Dims<L>::DIN;
+	float dv[DIN];
+#pragma unroll
+	for (int k = 0; k < DIN; ++k) {
+		if (k < 3) dv[k] = rh(rh(x[k]) - 0.5f);
+		else if (k < 3 + 2 * L) dv[k] = (float)enc_h[((size_t)((k - 3) >> 1) * ld + i) * 2 + ((k - 3) & 1)];  // [L][ld] half2
+		else dv[k] = 0.f;
+	}
+#pragma unroll
+	for (int ks = 0; ks < Dims<L>::DKS; ++ks)
+#pragma unroll
+		for (int j = 0; j < 8; ++j) dinB[ks][j] = (half_t)(h ? dv[16 * ks + pi_row(j, 1)] : dv[16 * ks + pi_row(j, 0)]);
+}
+
+// Full NerfNetwork forward for this lane's sample from stored encodings (r = lane & 31, h = lane >> 5).
+// Every lane of the wave must call this (MFMA), valid or not.
+template <int L, int W>
+__device__ __forceinline__ void forward_chunk(Fwd<L, W>& F, const FwdW& w, const float x[3], const float wd[3],
+                                              const half_t* __restrict__ enc_h, const float* __restrict__ dydx, uint32_t ld,
+                                              uint32_t i, bool valid, int r, int h) {
+	constexpr int DMT = Dims<L>::DMT;
+	build_din<L>(F.dinB, x, enc_h, ld, valid ? i : 0, h);
+	density_forward<L, W>(w, F.dinB, r, h, F.H0, F.D1, F.GhB, F.Gi);
 	// dSDF/dx = sum_k G_in[k] dy/dx[k] (+ identity rows 0..2), split over the two lane halves
 	float part[3] = {0.f, 0.f, 0.f};
 	const uint32_t ii = valid ? i : 0;
@@ -180,121 +498,15 @@ __device__ __forceinline__ void forward_chunk(Fwd<L, W>& F, const MlpPtrs& w, co
 		}
 #pragma unroll
 	for (int d = 0; d < 3; ++d) F.grad[d] = part[d] + __shfl_xor(part[d], 32);
-	// rgb input fragments: ks0 = density output, ks1 = SH, ks2 = [xyz, grad, 0...]
-	F.rinB[0] = accB(F.D1, 0);
-	{
-		float sh[16]; sh16(wd, sh);
-#pragma unroll
-		for (int j = 0; j < 8; ++j) F.rinB[1][j] = (half_t)(h ? sh[pi_row(j, 1)] : sh[pi_row(j, 0)]);
-		float r32[16];
-#pragma unroll
-		for (int k = 0; k < 16; ++k) r32[k] = 0.f;
-		r32[0] = x[0]; r32[1] = x[1]; r32[2] = x[2];
-		r32[3] = F.grad[0]; r32[4] = F.grad[1]; r32[5] = F.grad[2];
-#pragma unroll
-		for (int j = 0; j < 8; ++j) F.rinB[2][j] = (half_t)(h ? r32[pi_row(j, 1)] : r32[pi_row(j, 0)]);
-	}
-	// rgb layers
-#pragma unroll
-	for (int mt = 0; mt < MT; ++mt) {
-		f16v acc = zero16();
-#pragma unroll
-		for (int ks = 0; ks < 3; ++ks) acc = mfma(loadA(w.r0, 48, W, 32 * mt + r, 16 * ks, h), F.rinB[ks], acc);
-		F.H1[mt] = rh16(relu16(acc));
-	}
-#pragma unroll
-	for (int mt = 0; mt < MT; ++mt) {
-		f16v acc = zero16();
-#pragma unroll
-		for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.r1, W, W, 32 * mt + r, 16 * ks, h), accB(F.H1[ks >> 1], ks & 1), acc);
-		F.H2[mt] = rh16(relu16(acc));
-	}
-	{
-		f16v acc = zero16();
-#pragma unroll
-		for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.r2, W, 16, r, 16 * ks, h), accB(F.H2[ks >> 1], ks & 1), acc);
-		F.O = rh16(acc);
-	}
+	F.O = rgb_forward<W>(w, F.D1, x, wd, F.grad, r, h, F.rinB, F.H1, F.H2);
 }
 
-// ------------------------------------------------------------------------------------------
-// Inference / pre-compaction forward: coords AoS7 -> out AoS16 fp16 (nerf_network.h:145-328).
-// n from device memory; 32 samples per wave-iteration, grid-strided.
-// ------------------------------------------------------------------------------------------
-template <int L, int W>
-__global__ void __launch_bounds__(256) k_mlp_forward(const uint32_t* __restrict__ n_ptr, uint32_t n_fixed, uint32_t ld,
-                                                     const float* __restrict__ coords, const half_t* __restrict__ enc_h,
-                                                     const float* __restrict__ dydx, MlpPtrs w, half_t* __restrict__ out) {
-	const uint32_t n = n_ptr ? *n_ptr : n_fixed;
-	const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-	const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-	const uint32_t n_waves = (gridDim.x * blockDim.x) >> 6;
-	const float var = (float)w.var[0];
-	const half_t bias_h = (half_t)w.sdf_bias;
-	for (uint32_t base = wave * 32; base < n; base += n_waves * 32) {
-		const uint32_t i = base + r;
-		const bool valid = i < n;
-		const uint32_t ic = valid ? i : 0;
-		const float* c = coords + (size_t)ic * COORD_W;
-		const float x[3] = {c[0], c[1], c[2]}, wd[3] = {c[4], c[5], c[6]};
-		Fwd<L, W> F;
-		forward_chunk<L, W>(F, w, x, wd, enc_h, dydx, ld, ic, valid, r, h);
-		const float row11 = __shfl_xor(F.O[7], 32);  // lane h=0 holds row 11 in reg 7
-		if (valid) {
-			h8 o;
-			if (h == 0) {
-				o[0] = (half_t)F.O[0]; o[1] = (half_t)F.O[1]; o[2] = (half_t)F.O[2];
-				o[3] = (half_t)F.D1[0] + bias_h;                     // half add (common_operation.cuh:964)
-				o[4] = (half_t)F.grad[0]; o[5] = (half_t)F.grad[1]; o[6] = (half_t)F.grad[2];
-				o[7] = (half_t)var;
-			} else {
-				o[0] = (half_t)wd[0]; o[1] = (half_t)wd[1]; o[2] = (half_t)wd[2];
-				o[3] = (half_t)row11;
-				o[4] = (half_t)F.O[4]; o[5] = (half_t)F.O[5]; o[6] = (half_t)F.O[6]; o[7] = (half_t)F.O[7];
-			}
-			*(h8*)(out + (size_t)i * OUT_W + 8 * h) = o;
-		}
-	}
-}
-
-// Density-only inference for the occupancy grid (NerfNetwork::density, nerf_network.h:656-739;
-// sdf_to_density_variance_buffer, common_operation.cuh:306-324 in fp16 arithmetic).
-template <int L, int W>
-__global__ void __launch_bounds__(256) k_mlp_density(uint32_t n, uint32_t ld, const float* __restrict__ pos,
-                                                     const half_t* __restrict__ enc_h, MlpPtrs w, float* __restrict__ density) {
-	constexpr int DIN = Dims<L>::DIN, DKS = Dims<L>::DKS, MT = (W + 31) / 32, HKS = W / 16;
-	const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-	const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-	const uint32_t n_waves = (gridDim.x * blockDim.x) >> 6;
-	const half_t var_h = w.var[0];
-	const half_t bias_h = (half_t)w.sdf_bias;
-	for (uint32_t base = wave * 32; base < n; base += n_waves * 32) {
-		const uint32_t i = base + r;
-		const bool valid = i < n;
-		const uint32_t ic = valid ? i : 0;
-		const float x[3] = {pos[3 * (size_t)ic], pos[3 * (size_t)ic + 1], pos[3 * (size_t)ic + 2]};
-		h8 dinB[DKS];
-		build_din<L>(dinB, x, enc_h, ld, ic, h);
-		f16v H0[MT];
-#pragma unroll
-		for (int mt = 0; mt < MT; ++mt) {
-			f16v acc = zero16();
-#pragma unroll
-			for (int ks = 0; ks < DKS; ++ks) acc = mfma(loadA(w.d0, DIN, W, 32 * mt + r, 16 * ks, h), dinB[ks], acc);
-			H0[mt] = rh16(relu16(acc));
-		}
-		f16v acc = zero16();
-#pragma unroll
-		for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.d1, W, 16, r, 16 * ks, h), accB(H0[ks >> 1], ks & 1), acc);
-		if (valid && h == 0) {
-			const half_t sdf = (half_t)acc[0] + bias_h;
-			const half_t s = (half_t)__expf((float)(var_h * (half_t)10.0f));
-			const half_t sig = (half_t)(1.0f / (1.0f + __expf(-(float)(sdf * s))));
-			const half_t dens = (s * sig) * ((half_t)1.0f - sig);
-			density[i] = (float)dens;
-		}
-	}
-}
+// backward weight set: transposed copies, staged after the forward set
+struct BwdW { MatRef r2T, r1T, r0T, d1T; };
+template <int L, int W> struct TrainSmem {
+	static constexpr int R2T = FwdSmem<L, W>::END, R1T = R2T + W * (16 + 8), R0T = R1T + W * (W + 8), D1T = R0T + 48 * (W + 8);
+	static constexpr int END = D1T + W * (16 + 8);
+};
 
 // ------------------------------------------------------------------------------------------
 // Training forward-recompute + first- and second-order backward for 32 compacted samples per
@@ -326,19 +538,31 @@ __global__ void __launch_bounds__(256) k_mlp_train(const uint32_t* __restrict__ 
 	constexpr int DIN = Dims<L>::DIN, DKS = Dims<L>::DKS, DMT = Dims<L>::DMT;
 	constexpr int MT = Fwd<L, W>::MT, HKS = Fwd<L, W>::HKS;
 	if (n_valid_ptr && *n_valid_ptr == 0) return;  // zero compacted samples: nothing to train on
+	__shared__ half_t sm[TrainSmem<L, W>::END];
+	using TS = TrainSmem<L, W>;
+	const FwdW fw0 = stage_fwd<L, W>(sm, w.d0, w.d0T, w);
+	stage_mat(sm + TS::R2T, w.r2T, W, 16);
+	stage_mat(sm + TS::R1T, w.r1T, W, W);
+	stage_mat(sm + TS::R0T, w.r0T, 48, W);
+	stage_mat(sm + TS::D1T, w.d1T, W, 16);
+	const BwdW bw0{{sm + TS::R2T, 16 + 8}, {sm + TS::R1T, W + 8}, {sm + TS::R0T, W + 8}, {sm + TS::D1T, 16 + 8}};
+	__syncthreads();
 	const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
 	const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
 	const uint32_t n_waves = (gridDim.x * blockDim.x) >> 6;
 	const size_t ld2 = 2 * (size_t)ld;
 	float var_part = 0.f;
 	for (uint32_t base = wave * 32; base < n; base += n_waves * 32) {
+		const uint32_t z = opaque_zero();
+		const FwdW fw = fw0.at(z);
+		const BwdW bw{rebase(bw0.r2T, z), rebase(bw0.r1T, z), rebase(bw0.r0T, z), rebase(bw0.d1T, z)};
 		const uint32_t i = base + r;
 		const bool valid = i < n;
 		const uint32_t ic = valid ? i : 0;
 		const float* c = coords + (size_t)ic * COORD_W;
 		const float x[3] = {c[0], c[1], c[2]}, wd[3] = {c[4], c[5], c[6]};
 		Fwd<L, W> F;
-		forward_chunk<L, W>(F, w, x, wd, enc_h, dydx, ld, ic, valid, r, h);
+		forward_chunk<L, W>(F, fw, x, wd, enc_h, dydx, ld, ic, valid, r, h);
 		const h8 dlo = *(const h8*)(dL_dout + (size_t)ic * OUT_W + 8 * h);   // h=0: rows 0..7, h=1: rows 8..15
 		const h8 dlo_o = shfl_xor_h8(dlo, 32);
 		const h8 dlo_lo = h ? dlo_o : dlo;   // rows 0..7 on every lane
@@ -351,7 +575,7 @@ __global__ void __launch_bounds__(256) k_mlp_train(const uint32_t* __restrict__ 
 		f16v dH2[MT], dH1[MT];
 #pragma unroll
 		for (int mt = 0; mt < MT; ++mt) {
-			f16v acc = mfma(loadA(w.r2T, 16, W, 32 * mt + r, 0, h), dOB, zero16());
+			f16v acc = mfma(loadA(bw.r2T, W, 32 * mt + r, 0, h), dOB, zero16());
 #pragma unroll
 			for (int q = 0; q < 16; ++q) acc[q] = F.H2[mt][q] > 0.f ? rh(acc[q]) : 0.f;
 			dH2[mt] = acc;
@@ -360,7 +584,7 @@ __global__ void __launch_bounds__(256) k_mlp_train(const uint32_t* __restrict__ 
 		for (int mt = 0; mt < MT; ++mt) {
 			f16v acc = zero16();
 #pragma unroll
-			for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.r1T, W, W, 32 * mt + r, 16 * ks, h), accB(dH2[ks >> 1], ks & 1), acc);
+			for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(bw.r1T, W, 32 * mt + r, 16 * ks, h), accB(dH2[ks >> 1], ks & 1), acc);
 #pragma unroll
 			for (int q = 0; q < 16; ++q) acc[q] = F.H1[mt][q] > 0.f ? rh(acc[q]) : 0.f;
 			dH1[mt] = acc;
@@ -370,7 +594,7 @@ __global__ void __launch_bounds__(256) k_mlp_train(const uint32_t* __restrict__ 
 		for (int mt = 0; mt < 2; ++mt) {
 			f16v acc = zero16();
 #pragma unroll
-			for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.r0T, W, 48, 32 * mt + r, 16 * ks, h), accB(dH1[ks >> 1], ks & 1), acc);
+			for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(bw.r0T, 48, 32 * mt + r, 16 * ks, h), accB(dH1[ks >> 1], ks & 1), acc);
 			dRin[mt] = rh16(acc);
 		}
 		// density backward: delta_D1 = dL/drgb_in[0:16], row 0 += dL_dout[3] (half add)
@@ -380,7 +604,7 @@ __global__ void __launch_bounds__(256) k_mlp_train(const uint32_t* __restrict__ 
 		f16v dH0[MT];
 #pragma unroll
 		for (int mt = 0; mt < MT; ++mt) {
-			f16v acc = mfma(loadA(w.d1T, 16, W, 32 * mt + r, 0, h), dD1B, zero16());
+			f16v acc = mfma(loadA(bw.d1T, W, 32 * mt + r, 0, h), dD1B, zero16());
 #pragma unroll
 			for (int q = 0; q < 16; ++q) acc[q] = F.H0[mt][q] > 0.f ? rh(acc[q]) : 0.f;
 			dH0[mt] = acc;
@@ -390,7 +614,7 @@ __global__ void __launch_bounds__(256) k_mlp_train(const uint32_t* __restrict__ 
 		for (int mt = 0; mt < DMT; ++mt) {
 			f16v acc = zero16();
 #pragma unroll
-			for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.d0T, W, DIN, 32 * mt + r, 16 * ks, h), accB(dH0[ks >> 1], ks & 1), acc);
+			for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(fw.d0T, DIN, 32 * mt + r, 16 * ks, h), accB(dH0[ks >> 1], ks & 1), acc);
 			dDin[mt] = rh16(acc);
 		}
 		// v = dL/d(grad sdf) (nerf_network.h:478-504): rows 35..37 of dL/drgb_in live at
@@ -423,7 +647,7 @@ __global__ void __launch_bounds__(256) k_mlp_train(const uint32_t* __restrict__ 
 		for (int mt = 0; mt < MT; ++mt) {
 			f16v acc = zero16();
 #pragma unroll
-			for (int ks = 0; ks < DKS; ++ks) acc = mfma(loadA(w.d0, DIN, W, 32 * mt + r, 16 * ks, h), uB[ks], acc);
+			for (int ks = 0; ks < DKS; ++ks) acc = mfma(loadA(fw.d0, W, 32 * mt + r, 16 * ks, h), uB[ks], acc);
 #pragma unroll
 			for (int q = 0; q < 16; ++q) acc[q] = F.H0[mt][q] > 0.f ? rh(acc[q]) : 0.f;
 			H1p[mt] = acc;
@@ -530,6 +754,13 @@ __global__ void k_mfma_probe(const half_t* A, const half_t* B, float* C) {
 // Supported (levels, width) instantiations; the host checks mlp_supported() at reload time.
 #define NEUS_MLP_CONFIGS(X) X(1, 16) X(1, 64) X(2, 64) X(4, 64) X(8, 64) X(14, 64) X(16, 64)
 
+void mlp_din_permutation(uint32_t L, int32_t* perm) {
+	const int DIN = ((3 + 2 * (int)L) + 15) / 16 * 16;
+	for (int p = 0; p < DIN; ++p) perm[p] = -1;
+	for (int h = 0; h < 2; ++h)
+		for (int q = 0; q < DIN / 2; ++q) perm[din_physical_row(h, q)] = din_logical((int)L, h, q);
+}
+
 bool mlp_supported(uint32_t L, uint32_t W) {
 #define X(l, w) if (L == l && W == w) return true;
 	NEUS_MLP_CONFIGS(X)
@@ -537,17 +768,17 @@ bool mlp_supported(uint32_t L, uint32_t W) {
 	return false;
 }
 
-void launch_mlp_forward(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_ptr, uint32_t n_fixed, uint32_t ld, const float* coords,
-                        const half_t* enc, const float* dydx, const MlpPtrs& w, half_t* out, uint32_t blocks) {
-#define X(l, w_) if (L == l && W == w_) { k_mlp_forward<l, w_><<<blocks, 256, 0, s>>>(n_ptr, n_fixed, ld, coords, enc, dydx, w, out); return; }
+void launch_nerf_infer(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_ptr, uint32_t n_fixed, const float* coords, const GridLevels& gl,
+                       uint32_t valid_level, const half_t* grid, const MlpPtrs& w, half_t* out, uint32_t blocks) {
+#define X(l, w_) if (L == l && W == w_) { k_nerf_infer<l, w_><<<blocks, 256, 0, s>>>(n_ptr, n_fixed, coords, gl, valid_level, grid, w, out); return; }
 	NEUS_MLP_CONFIGS(X)
 #undef X
 }
-void launch_mlp_density(hipStream_t s, uint32_t L, uint32_t W, uint32_t n, uint32_t ld, const float* pos, const half_t* enc,
-                        const MlpPtrs& w, float* density) {
-	const uint32_t blocks = std::min<uint32_t>((n + 127) / 128, 4096);
+void launch_nerf_density(hipStream_t s, uint32_t L, uint32_t W, uint32_t n, const float* pos, const GridLevels& gl, uint32_t valid_level,
+                         const half_t* grid, const MlpPtrs& w, float* density) {
+	const uint32_t blocks = std::min<uint32_t>((n + 127) / 128, 8192);
 	if (n == 0) return;
-#define X(l, w_) if (L == l && W == w_) { k_mlp_density<l, w_><<<blocks, 256, 0, s>>>(n, ld, pos, enc, w, density); return; }
+#define X(l, w_) if (L == l && W == w_) { k_nerf_density<l, w_><<<blocks, 256, 0, s>>>(n, pos, gl, valid_level, grid, w, density); return; }
 	NEUS_MLP_CONFIGS(X)
 #undef X
 }

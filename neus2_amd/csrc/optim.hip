@@ -49,6 +49,19 @@ __global__ void k_cast_half(uint32_t n, const float* __restrict__ in, half_t* __
 	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) out[i] = (half_t)in[i];
 }
 
+// Fused-kernel copies of the first density layer: W0 columns / W0^T rows in the physical din order
+// of the fused encode (mlp.hip din_logical); -1 entries are zero pads.
+__global__ void k_permute_din(const half_t* __restrict__ d0, half_t* __restrict__ d0p, half_t* __restrict__ d0Tp, DinPerm perm) {
+	const uint32_t n = perm.W * perm.din;
+	for (uint32_t e = threadIdx.x; e < n; e += blockDim.x) {
+		const uint32_t row = e / perm.din, p = e % perm.din;
+		const int32_t k = perm.p[p];
+		const half_t v = k >= 0 ? d0[(size_t)row * perm.din + k] : (half_t)0.f;
+		d0p[(size_t)row * perm.din + p] = v;
+		d0Tp[(size_t)p * perm.W + row] = v;
+	}
+}
+
 // dst[c][r] = src[r][c]  (all matrices are <= 64x64)
 __global__ void k_transpose_w(TransposeJobs jobs) {
 	const TransposeJob J = jobs.j[blockIdx.x];
@@ -151,6 +164,9 @@ void launch_adam_ema(hipStream_t s, const AdamParams& p, float* weights_fp, half
 }
 void launch_cast_half(hipStream_t s, uint32_t n, const float* in, half_t* out) { k_cast_half<<<nblk(n), 256, 0, s>>>(n, in, out); }
 void launch_transpose_w(hipStream_t s, const TransposeJobs& jobs) { if (jobs.n) k_transpose_w<<<jobs.n, 256, 0, s>>>(jobs); }
+void launch_permute_din(hipStream_t s, const half_t* d0, half_t* d0p, half_t* d0Tp, const DinPerm& perm) {
+	k_permute_din<<<1, 256, 0, s>>>(d0, d0p, d0Tp, perm);
+}
 void launch_grid_samples(hipStream_t s, uint32_t n, uint32_t out_offset, uint64_t rng_state, uint64_t rng_inc, uint32_t step,
                          const float* aabb_min, const float* aabb_max, const float* grid_in, float* pos, uint32_t* indices,
                          uint32_t n_cascades, float thresh) {

@@ -80,10 +80,12 @@ struct NeusTestbed {
 	Dev<uint32_t> adam_steps;
 	Dev<half_t> params_h, ema_h, wT;
 	MlpPtrs mlp{};
+	DinPerm din_perm{};
 	// occupancy grid
 	Dev<float> density_grid, density_tmp, grid_mean, grid_partial, occ_pos, occ_density;
 	Dev<uint32_t> occ_idx;
 	Dev<uint8_t> bitfield;
+	Dev<uint32_t> bf_lin;   // mip-0 occupancy in (x, y, z/32) word order for the constant-step march
 	uint32_t density_grid_ema_step = 0;
 	// step workspace
 	uint32_t batch = 0, max_samples = 0;
@@ -95,6 +97,10 @@ struct NeusTestbed {
 	Dev<uint8_t> scan_tmp;
 	size_t scan_tmp_bytes = 0;
 	Dev<StepState> st;
+	// restructured loss scratch (kernels.h LossWork)
+	Dev<float4> l_sa, l_ck4, l_racc, l_rgr;
+	Dev<float> l_ekt, l_cke, l_rT;
+	Dev<uint32_t> sample_ray;
 	TrainBufs tbuf{};
 	// RNG + counters (testbed.cu:2087-2101)
 	pcg32 rng, density_grid_rng;
@@ -174,6 +180,8 @@ struct NeusTestbed {
 		HIP_CHECK(hipMemset(density_grid.p, 0, n_cells * 4));
 		bitfield.alloc(GRID3 / 8 * NERF_CASCADES);
 		HIP_CHECK(hipMemset(bitfield.p, 0xff, GRID3 / 8 * NERF_CASCADES));
+		bf_lin.alloc(GRID3 / 32);
+		launch_bitfield_linear(stream, bitfield.p, bf_lin.p);
 		grid_mean.alloc(4); grid_partial.alloc(GRID3 / 1024);
 		HIP_CHECK(hipMemset(grid_mean.p, 0, 16));
 	}
@@ -217,7 +225,7 @@ struct NeusTestbed {
 		const uint32_t P = l.P;
 		params_fp.alloc(P); grads.alloc(P); m1.alloc(P); m2.alloc(P); ema_tmp.alloc(P); adam_steps.alloc(P);
 		params_h.alloc(P); ema_h.alloc(P);
-		wT.alloc(l.din * l.W + l.W * 16 + 48 * l.W + l.W * l.W + l.W * 16 + 64);
+		wT.alloc(l.din * l.W + l.W * 16 + 48 * l.W + l.W * l.W + l.W * 16 + 2 * l.din * l.W + 64);
 		// initial parameters (trainer.h:54-109): seed_seq{seed} -> pcg32
 		std::vector<float> h(P, 0.f);
 		{
@@ -261,11 +269,14 @@ struct NeusTestbed {
 		// workspace
 		batch = c.batch_size;
 		max_samples = batch * 16;  // testbed_nerf.cu:3725
-		rays.alloc(6 * (size_t)MAX_RAYS); startt.alloc(MAX_RAYS); nreq.alloc(MAX_RAYS); base.alloc(MAX_RAYS);
+		rays.alloc(6 * (size_t)MAX_RAYS); startt.alloc((size_t)MAX_RAYS * MARCH_SEGS); nreq.alloc(MAX_RAYS); base.alloc(MAX_RAYS);
 		numsteps.alloc(2 * (size_t)MAX_RAYS); ccount.alloc(MAX_RAYS); cbase.alloc(MAX_RAYS);
+		l_sa.alloc(max_samples); l_ekt.alloc(max_samples); sample_ray.alloc(max_samples);
+		l_ck4.alloc(max_samples / 8 + 1); l_cke.alloc(max_samples / 8 + 1);
+		l_racc.alloc(MAX_RAYS); l_rgr.alloc(MAX_RAYS); l_rT.alloc(MAX_RAYS);
 		loss.alloc(MAX_RAYS); ek.alloc(MAX_RAYS); mask.alloc(MAX_RAYS); loss_sum.alloc(4);
 		coords.alloc((size_t)max_samples * COORD_W); net_out.alloc((size_t)max_samples * OUT_W);
-		enc.alloc((size_t)l.L * max_samples); dydx.alloc((size_t)6 * l.L * max_samples);
+		enc.alloc((size_t)l.L * batch); dydx.alloc((size_t)6 * l.L * batch);  // training batch only: inference fuses the encode
 		coords_c.alloc((size_t)batch * COORD_W); dL_dout.alloc((size_t)batch * OUT_W);
 		const size_t ld = batch, ld2 = 2 * ld;
 		const size_t tb_elems = (size_t)l.W * ld2 + (size_t)l.din * ld2 + 16 * ld2 + (size_t)l.W * ld2 + (size_t)l.W * ld + 48 * ld +
@@ -304,6 +315,10 @@ struct NeusTestbed {
 		mlp.r0 = params_h.p + l.off_r0; mlp.r1 = params_h.p + l.off_r1; mlp.r2 = params_h.p + l.off_r2;
 		auto take = [&](size_t k) { half_t* r = t; t += (k + 7) / 8 * 8; return r; };
 		mlp.d0T = take(l.din * l.W); mlp.d1T = take(l.W * 16); mlp.r0T = take(48 * l.W); mlp.r1T = take(l.W * l.W); mlp.r2T = take(l.W * 16);
+		mlp.d0p = take(l.din * l.W); mlp.d0Tp = take(l.din * l.W);
+		din_perm = DinPerm{};
+		mlp_din_permutation(l.L, din_perm.p);
+		din_perm.din = l.din; din_perm.W = l.W;
 		mlp.var = params_h.p + l.var_off;
 		mlp.sdf_bias = cfg.sdf_bias;
 	}
@@ -317,6 +332,7 @@ struct NeusTestbed {
 		tj.j[4] = {mlp.r2, (half_t*)mlp.r2T, 16, l.W};
 		tj.n = 5;
 		launch_transpose_w(stream, tj);
+		launch_permute_din(stream, mlp.d0, (half_t*)mlp.d0p, (half_t*)mlp.d0Tp, din_perm);
 	}
 
 	// progressive levels (grid.h:2427-2440)
@@ -333,10 +349,8 @@ struct NeusTestbed {
 		launch_grid_encode(s, n_ptr, n_fixed, ld, c, stride, gl, valid, params_h.p + lay.grid_off, enc.p, want_dydx ? dydx.p : nullptr, gx);
 	}
 	void net_forward(const uint32_t* n_ptr, uint32_t n_fixed, uint32_t n_cap, const float* c, uint32_t valid, half_t* out, hipStream_t s) {
-		const uint32_t ld = n_cap;
-		encode(n_ptr, n_fixed, n_cap, ld, c, COORD_W, valid, true, s);
 		const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((n_cap + 127) / 128, 8192));
-		launch_mlp_forward(s, lay.L, lay.W, n_ptr, n_fixed, ld, c, (const half_t*)enc.p, dydx.p, mlp, out, blocks);
+		launch_nerf_infer(s, lay.L, lay.W, n_ptr, n_fixed, c, gl, valid, params_h.p + lay.grid_off, mlp, out, blocks);
 	}
 	WGradJobs wgrad_jobs(uint32_t n, uint32_t ld, float* g, const uint32_t* n_valid) {
 		const Layout& l = lay;
@@ -366,14 +380,14 @@ struct NeusTestbed {
 	                  const half_t* dlo, float* g, hipStream_t s, bool marks = false) {
 		const uint32_t ld = n;
 		encode(n_train_ptr, n, n, ld, c, COORD_W, valid, true, s);
-		if (marks) mark(6);
+		if (marks) mark(5);
 		TrainBufs t = tbuf;
 		t.var_grad = g + lay.var_off;
 		launch_mlp_train(s, lay.L, lay.W, n_valid_ptr, n, ld, c, (const half_t*)enc.p, dydx.p, dlo, mlp, t);
-		if (marks) mark(7);
+		if (marks) mark(6);
 		WGradJobs J = wgrad_jobs(n, ld, g, n_train_ptr);
 		launch_wgrad(s, J, J.block_start[5]);
-		if (marks) mark(8);
+		if (marks) mark(7);
 		const uint32_t gx = std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, 2048));
 		launch_grid_scatter(s, n_train_ptr, n, ld, c, COORD_W, gl, valid, tbuf.dLdenc, tbuf.genc, tbuf.v, g + lay.grid_off, gx);
 	}
@@ -391,19 +405,14 @@ struct NeusTestbed {
 		launch_grid_samples(s, n_nonuniform, n_uniform, density_grid_rng.state, density_grid_rng.inc, density_grid_ema_step, ds.aabb_min, ds.aabb_max,
 		                    density_grid.p, occ_pos.p, occ_idx.p, max_cascade + 1, NERF_MIN_OPTICAL_THICKNESS);
 		density_grid_rng.advance();
-		// NerfNetwork::density on the samples in chunks that fit the encoding workspace
-		const uint32_t chunk = std::min<uint32_t>(N, max_samples);
-		for (uint32_t o = 0; o < N; o += chunk) {
-			const uint32_t m = std::min(chunk, N - o);
-			const uint32_t gx = std::max<uint32_t>(1, std::min<uint32_t>((m + 255) / 256, 4096));
-			launch_grid_encode(s, nullptr, m, m, occ_pos.p + 3 * (size_t)o, 3, gl, valid, params_h.p + lay.grid_off, enc.p, nullptr, gx);
-			launch_mlp_density(s, lay.L, lay.W, m, m, occ_pos.p + 3 * (size_t)o, (const half_t*)enc.p, mlp, occ_density.p + o);
-		}
+		// NerfNetwork::density on the samples, hash-grid encode fused in
+		launch_nerf_density(s, lay.L, lay.W, N, occ_pos.p, gl, valid, params_h.p + lay.grid_off, mlp, occ_density.p);
 		launch_splat_max(s, N, occ_idx.p, occ_density.p, density_tmp.p);
 		launch_ema_grid(s, n_cells, cfg.density_grid_decay, density_grid.p, density_tmp.p);
 		++density_grid_ema_step;
 		launch_grid_mean(s, density_grid.p, grid_partial.p, grid_mean.p);
 		launch_bitfield(s, density_grid.p, bitfield.p, grid_mean.p, max_cascade + 1);
+		launch_bitfield_linear(s, bitfield.p, bf_lin.p);
 	}
 
 	// ------------------------------------------------------------ optimizer (trainer.h:170-172)
@@ -445,29 +454,26 @@ struct NeusTestbed {
 		HIP_CHECK(hipMemsetAsync(&st.p->n_rays_with_samples, 0, 4, s));
 		const DPInfo dp{rank, world};
 		mark(1);
-		launch_march_count(s, MAX_RAYS, st.p, dp, ds, bitfield.p, rng.state, rng.inc, rays.p, startt.p, nreq.p);
+		launch_march_count(s, MAX_RAYS, st.p, dp, ds, bitfield.p, bf_lin.p, rng.state, rng.inc, rays.p, startt.p, nreq.p);
 		launch_exclusive_scan(s, scan_tmp.p, scan_tmp_bytes, nreq.p, base.p, MAX_RAYS);
-		launch_march_write(s, MAX_RAYS, st.p, ds, bitfield.p, rays.p, startt.p, nreq.p, base.p, numsteps.p, coords.p);
+		launch_march_write(s, MAX_RAYS, st.p, ds, bitfield.p, bf_lin.p, rays.p, startt.p, nreq.p, base.p, numsteps.p, coords.p, sample_ray.p);
 		mark(2);
-		encode(&st.p->n_kept, 0, max_samples, max_samples, coords.p, COORD_W, valid, true, s);
+		launch_nerf_infer(s, lay.L, lay.W, &st.p->n_kept, 0, coords.p, gl, valid, params_h.p + lay.grid_off, mlp, net_out.p, 8192);
 		mark(3);
-		{
-			const uint32_t blocks = 8192;
-			launch_mlp_forward(s, lay.L, lay.W, &st.p->n_kept, 0, max_samples, coords.p, (const half_t*)enc.p, dydx.p, mlp, net_out.p, blocks);
-		}
-		mark(4);
 		LossParams lp{};
 		lp.loss_scale = LOSS_SCALE; lp.ek_w = cfg.ek_loss_weight; lp.mask_w = cfg.mask_loss_weight; lp.cos_anneal = cos_anneal();
 		lp.max_compacted = batch; lp.rng_state = rng.state; lp.rng_inc = rng.inc;
-		launch_loss_count(s, MAX_RAYS, st.p, ds, rays.p, numsteps.p, coords.p, net_out.p, lp.cos_anneal, ccount.p);
+		const LossWork w = loss_work(base.p);
+		launch_loss_alpha(s, max_samples, st.p, coords.p, net_out.p, lp.cos_anneal, w);
+		launch_loss_scan_ray(s, MAX_RAYS, numsteps.p, w, ccount.p);
 		launch_exclusive_scan(s, scan_tmp.p, scan_tmp_bytes, ccount.p, cbase.p, MAX_RAYS);
-		launch_loss_write(s, MAX_RAYS, st.p, dp, ds, lp, rays.p, numsteps.p, coords.p, net_out.p, ccount.p, cbase.p, coords_c.p, dL_dout.p,
-		                  loss.p, ek.p, mask.p);
+		launch_loss_ray(s, MAX_RAYS, st.p, dp, ds, lp, numsteps.p, ccount.p, cbase.p, w, loss.p, ek.p, mask.p);
+		launch_loss_grad(s, max_samples, st.p, dp, lp, coords.p, net_out.p, numsteps.p, w, coords_c.p, dL_dout.p);
 		launch_rollover(s, batch, st.p, coords_c.p, dL_dout.p);
 		HIP_CHECK(hipMemsetAsync(grads.p, 0, (size_t)lay.P * 4, s));
-		mark(5);
+		mark(4);
 		net_backward(&st.p->compacted_counter, &st.p->n_train, batch, coords_c.p, valid, dL_dout.p, grads.p, s, true);
-		mark(9);
+		mark(8);
 		if (world > 1) {
 			NCCL_CHECK(ncclGroupStart());
 			NCCL_CHECK(ncclAllReduce(grads.p, grads.p, lay.P, ncclFloat32, ncclSum, comm, s));
@@ -485,12 +491,19 @@ struct NeusTestbed {
 		}
 		launch_step_counters(s, st.p, batch, max_samples, world, cfg.fixed_rays_per_batch);
 		rng.advance();
-		mark(10);
+		mark(9);
 		// ---- optimizer (testbed_nerf.cu:3503-3508)
 		optimizer_step(grads.p);
-		mark(11);
+		mark(10);
 		++training_step;
 		if (profiling) accumulate_phases();
+	}
+
+	LossWork loss_work(const uint32_t* rbase) {
+		LossWork w{};
+		w.sa = l_sa.p; w.ck4 = l_ck4.p; w.cke = l_cke.p; w.ekt = l_ekt.p; w.sample_ray = sample_ray.p; w.rbase = rbase;
+		w.racc = l_racc.p; w.rT = l_rT.p; w.rgr = l_rgr.p;
+		return w;
 	}
 
 	void accumulate_phases() {
@@ -609,11 +622,68 @@ int neus_testbed_set_density_grid(NeusTestbed* tb, const float* g, const uint8_t
 	return guard([&] {
 		HIP_CHECK(hipStreamSynchronize(tb->stream));
 		if (g) HIP_CHECK(hipMemcpy(tb->density_grid.p, g, (size_t)GRID3 * 4, hipMemcpyHostToDevice));
-		if (bf) HIP_CHECK(hipMemcpy(tb->bitfield.p, bf, GRID3 / 8 * NERF_CASCADES, hipMemcpyHostToDevice));
+		if (bf) {
+			HIP_CHECK(hipMemcpy(tb->bitfield.p, bf, GRID3 / 8 * NERF_CASCADES, hipMemcpyHostToDevice));
+			launch_bitfield_linear(tb->stream, tb->bitfield.p, tb->bf_lin.p);
+			HIP_CHECK(hipStreamSynchronize(tb->stream));
+		}
 	});
 }
 int neus_testbed_get_rng(NeusTestbed* tb, uint64_t* o) {
 	return guard([&] { o[0] = tb->rng.state; o[1] = tb->rng.inc; o[2] = tb->density_grid_rng.state; o[3] = tb->density_grid_rng.inc; });
+}
+int neus_testbed_ray_counts(NeusTestbed* tb, uint32_t n, uint32_t* nreq, uint32_t* ccount, uint32_t* numsteps) {
+	return guard([&] {
+		if (!tb->have_net) throw std::runtime_error("no network");
+		n = std::min(n, MAX_RAYS);
+		HIP_CHECK(hipStreamSynchronize(tb->stream));
+		if (nreq) HIP_CHECK(hipMemcpy(nreq, tb->nreq.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+		if (ccount) HIP_CHECK(hipMemcpy(ccount, tb->ccount.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+		if (numsteps) HIP_CHECK(hipMemcpy(numsteps, tb->numsteps.p, (size_t)n * 8, hipMemcpyDeviceToHost));
+	});
+}
+int neus_debug_time_kernel(NeusTestbed* tb, int kernel, int variant, int iters, float* ms_out) {
+	return guard([&] {
+		if (!tb->have_net) throw std::runtime_error("no network");
+		NeusTestbed& t = *tb;
+		hipStream_t s = t.stream;
+		const DPInfo dp{t.rank, t.world};
+		const uint32_t valid = t.valid_level_at((int)t.training_step);
+		const uint32_t* lin = variant == 1 ? nullptr : t.bf_lin.p;
+		auto march = [&]() {
+			HIP_CHECK(hipMemsetAsync(&t.st.p->n_kept, 0, 4, s));
+			HIP_CHECK(hipMemsetAsync(&t.st.p->n_rays_with_samples, 0, 4, s));
+			launch_march_count(s, MAX_RAYS, t.st.p, dp, t.ds, t.bitfield.p, lin, t.rng.state, t.rng.inc, t.rays.p, t.startt.p, t.nreq.p);
+			launch_exclusive_scan(s, t.scan_tmp.p, t.scan_tmp_bytes, t.nreq.p, t.base.p, MAX_RAYS);
+			launch_march_write(s, MAX_RAYS, t.st.p, t.ds, t.bitfield.p, lin, t.rays.p, t.startt.p, t.nreq.p, t.base.p, t.numsteps.p, t.coords.p,
+			                   t.sample_ray.p);
+		};
+		march();
+		launch_nerf_infer(s, t.lay.L, t.lay.W, &t.st.p->n_kept, 0, t.coords.p, t.gl, valid, t.params_h.p + t.lay.grid_off, t.mlp, t.net_out.p, 8192);
+		const LossWork w = t.loss_work(t.base.p);
+		launch_loss_alpha(s, t.max_samples, t.st.p, t.coords.p, t.net_out.p, t.cos_anneal(), w);
+		hipEvent_t a, b;
+		HIP_CHECK(hipEventCreate(&a)); HIP_CHECK(hipEventCreate(&b));
+		HIP_CHECK(hipEventRecord(a, s));
+		for (int k = 0; k < iters; ++k) {
+			switch (kernel) {
+			case 0: launch_march_count(s, MAX_RAYS, t.st.p, dp, t.ds, t.bitfield.p, lin, t.rng.state, t.rng.inc, t.rays.p, t.startt.p, t.nreq.p); break;
+			case 1: launch_march_write(s, MAX_RAYS, t.st.p, t.ds, t.bitfield.p, lin, t.rays.p, t.startt.p, t.nreq.p, t.base.p, t.numsteps.p,
+			                           t.coords.p, t.sample_ray.p); break;
+			case 2: debug_launch_loss_scan(s, variant, MAX_RAYS, t.numsteps.p, w, t.ccount.p); break;
+			case 3: launch_nerf_infer(s, t.lay.L, t.lay.W, &t.st.p->n_kept, 0, t.coords.p, t.gl, valid, t.params_h.p + t.lay.grid_off, t.mlp,
+			                          t.net_out.p, 8192); break;
+			case 4: launch_loss_alpha(s, t.max_samples, t.st.p, t.coords.p, t.net_out.p, t.cos_anneal(), w); break;
+			default: throw std::runtime_error("unknown kernel id");
+			}
+		}
+		HIP_CHECK(hipEventRecord(b, s));
+		HIP_CHECK(hipEventSynchronize(b));
+		float ms = 0.f;
+		HIP_CHECK(hipEventElapsedTime(&ms, a, b));
+		*ms_out = ms / std::max(1, iters);
+		HIP_CHECK(hipEventDestroy(a)); HIP_CHECK(hipEventDestroy(b));
+	});
 }
 int neus_testbed_stream(NeusTestbed* tb, void** s) { return guard([&] { *s = (void*)tb->stream; }); }
 int neus_testbed_synchronize(NeusTestbed* tb) { return guard([&] { HIP_CHECK(hipStreamSynchronize(tb->stream)); }); }
@@ -665,7 +735,6 @@ int neus_grid_encode(NeusTestbed* tb, void* stream, uint32_t n, uint32_t ld, con
 int neus_net_forward(NeusTestbed* tb, void* stream, uint32_t n, const float* coords, uint32_t valid, uint16_t* out) {
 	return guard([&] {
 		if (!tb->have_net) throw std::runtime_error("no network");
-		if (n > tb->max_samples) throw std::runtime_error("neus_net_forward: n exceeds the workspace (16 x batch_size)");
 		tb->net_forward(nullptr, n, n, coords, valid, (half_t*)out, as_stream(tb, stream));
 		HIP_CHECK(hipGetLastError());
 	});
@@ -695,11 +764,14 @@ int neus_sample_rays(NeusTestbed* tb, void* stream, uint32_t n_rays, uint32_t ra
 		Dev<StepState> sst; sst.alloc(1);
 		StepState h{}; h.rays_per_batch = n_rays; h.max_inference = max_samples; h.n_rays_total = n_rays_total;
 		HIP_CHECK(hipMemcpyAsync(sst.p, &h, sizeof(h), hipMemcpyHostToDevice, s));
-		Dev<float> st_t; st_t.alloc(n_rays); Dev<uint32_t> nr, bs; nr.alloc(n_rays); bs.alloc(n_rays);
+		Dev<float> st_t; st_t.alloc((size_t)n_rays * MARCH_SEGS); Dev<uint32_t> nr, bs; nr.alloc(n_rays); bs.alloc(n_rays);
 		Dev<uint8_t> tmp; const size_t tb_ = scan_temp_bytes(n_rays); tmp.alloc(tb_ + 256);
-		launch_march_count(s, n_rays, sst.p, DPInfo{rank, world}, tb->ds, bitfield, rng_state, rng_inc, rays, st_t.p, nr.p);
+		Dev<uint32_t> lin; lin.alloc(GRID3 / 32);
+		launch_bitfield_linear(s, bitfield, lin.p);
+		launch_march_count(s, n_rays, sst.p, DPInfo{rank, world}, tb->ds, bitfield, lin.p, rng_state, rng_inc, rays, st_t.p, nr.p);
 		launch_exclusive_scan(s, tmp.p, tb_, nr.p, bs.p, n_rays);
-		launch_march_write(s, n_rays, sst.p, tb->ds, bitfield, rays, st_t.p, nr.p, bs.p, numsteps, coords);
+		Dev<uint32_t> sr; sr.alloc(std::max<uint32_t>(1, max_samples));
+		launch_march_write(s, n_rays, sst.p, tb->ds, bitfield, lin.p, rays, st_t.p, nr.p, bs.p, numsteps, coords, sr.p);
 		HIP_CHECK(hipMemcpyAsync(&h, sst.p, sizeof(h), hipMemcpyDeviceToHost, s));
 		HIP_CHECK(hipStreamSynchronize(s));
 		counters_out[0] = h.numsteps_counter; counters_out[1] = h.n_kept; counters_out[2] = h.n_rays_with_samples;
@@ -711,19 +783,33 @@ int neus_loss_compact(NeusTestbed* tb, void* stream, uint32_t n_rays, uint32_t r
                       float* mask, uint32_t* counters_out) {
 	return guard([&] {
 		if (!tb->have_data || !tb->have_net) throw std::runtime_error("no dataset/network");
+		if (n_rays == 0 || n_rays > MAX_RAYS) throw std::runtime_error("n_rays out of range");
 		hipStream_t s = as_stream(tb, stream);
+		// sample count of the caller's layout (operator path only; the training step keeps it on the device)
+		std::vector<uint32_t> hn(2 * (size_t)n_rays);
+		HIP_CHECK(hipMemcpyAsync(hn.data(), numsteps, hn.size() * 4, hipMemcpyDeviceToHost, s));
+		HIP_CHECK(hipStreamSynchronize(s));
+		uint32_t n_samples = 1;
+		for (uint32_t i = 0; i < n_rays; ++i) if (hn[2 * i]) n_samples = std::max(n_samples, hn[2 * i] + hn[2 * i + 1]);
 		Dev<StepState> sst; sst.alloc(1);
 		StepState h{}; h.rays_per_batch = n_rays; h.n_rays_total = n_rays_total;
 		HIP_CHECK(hipMemcpyAsync(sst.p, &h, sizeof(h), hipMemcpyHostToDevice, s));
-		Dev<uint32_t> cc, cb; cc.alloc(n_rays); cb.alloc(n_rays);
+		Dev<uint32_t> cc, cb, rb, sr; cc.alloc(n_rays); cb.alloc(n_rays); rb.alloc(n_rays); sr.alloc(n_samples);
+		Dev<float4> sa, ck4, racc, rgr; sa.alloc(n_samples); ck4.alloc(n_samples / 8 + 1); racc.alloc(n_rays); rgr.alloc(n_rays);
+		Dev<float> ekt, cke, rT; ekt.alloc(n_samples); cke.alloc(n_samples / 8 + 1); rT.alloc(n_rays);
 		Dev<uint8_t> tmp; const size_t tb_ = scan_temp_bytes(n_rays); tmp.alloc(tb_ + 256);
 		LossParams lp{};
 		lp.loss_scale = LOSS_SCALE; lp.ek_w = tb->cfg.ek_loss_weight; lp.mask_w = tb->cfg.mask_loss_weight; lp.cos_anneal = tb->cos_anneal();
 		lp.max_compacted = max_compacted; lp.rng_state = rng_state; lp.rng_inc = rng_inc;
-		launch_loss_count(s, n_rays, sst.p, tb->ds, rays, numsteps, coords, (const half_t*)net_out, lp.cos_anneal, cc.p);
+		LossWork w{};
+		w.sa = sa.p; w.ck4 = ck4.p; w.cke = cke.p; w.ekt = ekt.p; w.sample_ray = sr.p; w.rbase = rb.p; w.racc = racc.p; w.rT = rT.p; w.rgr = rgr.p;
+		const DPInfo dp{rank, world};
+		launch_ray_index(s, n_rays, numsteps, sst.p, sr.p, rb.p);
+		launch_loss_alpha(s, n_samples, sst.p, coords, (const half_t*)net_out, lp.cos_anneal, w);
+		launch_loss_scan_ray(s, n_rays, numsteps, w, cc.p);
 		launch_exclusive_scan(s, tmp.p, tb_, cc.p, cb.p, n_rays);
-		launch_loss_write(s, n_rays, sst.p, DPInfo{rank, world}, tb->ds, lp, rays, numsteps, coords, (const half_t*)net_out, cc.p, cb.p,
-		                  coords_out, (half_t*)dlo, loss, ek, mask);
+		launch_loss_ray(s, n_rays, sst.p, dp, tb->ds, lp, numsteps, cc.p, cb.p, w, loss, ek, mask);
+		launch_loss_grad(s, n_samples, sst.p, dp, lp, coords, (const half_t*)net_out, numsteps, w, coords_out, (half_t*)dlo);
 		HIP_CHECK(hipMemcpyAsync(&h, sst.p, sizeof(h), hipMemcpyDeviceToHost, s));
 		HIP_CHECK(hipStreamSynchronize(s));
 		counters_out[0] = h.compacted_counter;

@@ -152,8 +152,8 @@ class _Nerf:
 
 
 # neus_testbed_kernel_times order (include/neus2_hip.h NEUS_N_PHASES)
-PHASES = ["occupancy", "sample", "inference_encode", "inference_mlp", "loss", "train_encode", "mlp_train", "wgrad",
-          "grid_scatter", "allreduce", "optimizer"]
+PHASES = ["occupancy", "sample", "inference", "loss", "train_encode", "mlp_train", "wgrad", "grid_scatter", "allreduce",
+          "optimizer"]
 
 
 class Testbed:
@@ -328,6 +328,14 @@ class Testbed:
         o = (C.c_uint64 * 4)()
         check(lib().neus_testbed_get_rng(self._h, o))
         return list(o)
+
+    def ray_counts(self, n=None):
+        """(requested samples, composited samples, compacted samples) per ray of the last step."""
+        n = int(self.stats()["rays_per_batch"] if n is None else n)
+        a, b, c = np.zeros(n, np.uint32), np.zeros(n, np.uint32), np.zeros(2 * n, np.uint32)
+        check(lib().neus_testbed_ray_counts(self._h, C.c_uint32(n), C.c_void_p(a.ctypes.data), C.c_void_p(b.ctypes.data),
+                                            C.c_void_p(c.ctypes.data)))
+        return a, b, c.reshape(n, 2)[:, 0].copy()
 
     def synchronize(self):
         check(lib().neus_testbed_synchronize(self._h))
