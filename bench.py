@@ -30,7 +30,7 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
-    p.add_argument("--warmup", type=int, default=300)
+    p.add_argument("--warmup", type=int, default=800)  # past step ~660 every hash-grid level is active (valid_level schedule)
     p.add_argument("--views", type=int, default=49)
     p.add_argument("--width", type=int, default=1600)
     p.add_argument("--height", type=int, default=1200)

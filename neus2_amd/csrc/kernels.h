@@ -52,6 +52,18 @@ struct LossParams {
 	uint64_t rng_state, rng_inc;
 };
 
+// binned hash-grid gradient scatter (grid.hip)
+constexpr uint32_t SB_SHIFT = 13, SB_SIZE = 1u << SB_SHIFT;   // bucket = 8192 grid entries (64 KB of fp32 pairs in LDS)
+constexpr uint32_t SB_MAX_BUCKETS = 1024;                      // 16 levels x 2^19 entries
+constexpr uint32_t SB_CHUNK = 1u << 16;                        // records per accumulating workgroup
+struct ScatterWork {
+	uint32_t* counts;   // [n_buckets * n_blocks + 1] contributions per (bucket, block), bucket-major
+	uint32_t* offs;     // exclusive scan of counts
+	float2* rec_g;      // [capacity] contribution (feature 0, feature 1)
+	uint16_t* rec_i;    // [capacity] entry within the bucket
+	uint32_t n_buckets, n_blocks;
+};
+
 // per-sample / per-ray scratch of the restructured loss (march.hip)
 struct LossWork {
 	float4* sa;             // [samples] alpha, sigmoid(rgb)
@@ -78,8 +90,11 @@ struct TransposeJobs { TransposeJob j[8]; uint32_t n; };
 // grid.hip
 void launch_grid_encode(hipStream_t s, const uint32_t* n_ptr, uint32_t n_fixed, uint32_t ld, const float* coords, uint32_t coord_stride,
                         const GridLevels& gl, uint32_t valid_level, const half_t* grid, uint32_t* enc, float* dydx, uint32_t grid_x);
-void launch_grid_scatter(hipStream_t s, const uint32_t* n_ptr, uint32_t n_fixed, uint32_t ld, const float* coords, uint32_t coord_stride,
-                         const GridLevels& gl, uint32_t valid_level, const half_t* dLdenc, const half_t* g, const float4* v, float* grads, uint32_t grid_x);
+size_t scatter_records_capacity(uint32_t n_cap, uint32_t n_levels);
+uint32_t scatter_n_buckets(const GridLevels& gl);
+void launch_grid_scatter(hipStream_t s, const uint32_t* n_ptr, uint32_t n_cap, uint32_t ld, const float* coords, uint32_t coord_stride,
+                         const GridLevels& gl, uint32_t valid_level, const half_t* dLdenc, const half_t* g, const float4* v, float* grads,
+                         const ScatterWork& w, void* scan_tmp, size_t scan_tmp_bytes);
 // mlp.hip
 bool mlp_supported(uint32_t n_levels, uint32_t width);
 void mlp_din_permutation(uint32_t L, int32_t* perm /* DIN entries: physical row -> logical din index or -1 */);

@@ -262,6 +262,40 @@ __device__ __forceinline__ f16v rgb_forward(const FwdW& w, const f16v& D1, const
 	return rh16(acc);
 }
 
+// rgb input fragments and the two hidden layers only (training: the output layer is not needed)
+template <int W>
+__device__ __forceinline__ void rgb_hidden(const FwdW& w, const f16v& D1, const float x[3], const float wd[3], const float grad[3],
+                                           int r, int h, h8 rinB[3], f16v* H1, f16v* H2) {
+	constexpr int MT = (W + 31) / 32, HKS = W / 16;
+	rinB[0] = accB(D1, 0);
+	{
+		float sh[16]; sh16(wd, sh);
+#pragma unroll
+		for (int j = 0; j < 8; ++j) rinB[1][j] = (half_t)(h ? sh[pi_row(j, 1)] : sh[pi_row(j, 0)]);
+		float r32[16];
+#pragma unroll
+		for (int k = 0; k < 16; ++k) r32[k] = 0.f;
+		r32[0] = x[0]; r32[1] = x[1]; r32[2] = x[2];
+		r32[3] = grad[0]; r32[4] = grad[1]; r32[5] = grad[2];
+#pragma unroll
+		for (int j = 0; j < 8; ++j) rinB[2][j] = (half_t)(h ? r32[pi_row(j, 1)] : r32[pi_row(j, 0)]);
+	}
+#pragma unroll
+	for (int mt = 0; mt < MT; ++mt) {
+		f16v acc = zero16();
+#pragma unroll
+		for (int ks = 0; ks < 3; ++ks) acc = mfma(loadA(w.r0, W, 32 * mt + r, 16 * ks, h), rinB[ks], acc);
+		H1[mt] = rh16(relu16(acc));
+	}
+#pragma unroll
+	for (int mt = 0; mt < MT; ++mt) {
+		f16v acc = zero16();
+#pragma unroll
+		for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.r1, W, 32 * mt + r, 16 * ks, h), accB(H1[ks >> 1], ks & 1), acc);
+		H2[mt] = rh16(relu16(acc));
+	}
+}
+
 // density layer 0 (+ReLU), layer 1 (16 outputs), G_h = relu'(H0) . W1d[0], G_in = W0d^T G_h
 template <int L, int W>
 __device__ __forceinline__ void density_forward(const FwdW& w, const h8* dinB, int r, int h, f16v* H0, f16v& D1, h8* GhB, f16v* Gi) {
@@ -530,13 +564,20 @@ __device__ __forceinline__ void store_frag(half_t* buf, size_t ldc, uint32_t col
 	}
 }
 
+// Training is split in two kernels so that neither holds the whole forward + backward state
+// (one fused kernel spilled ~1 KB per lane):
+//   k_mlp_train_rgb     : forward recompute (density + grad SDF + colour hidden layers), colour
+//                         backward, dL/d(density output) and v = dL/d(grad SDF)
+//   k_mlp_train_density : density forward recompute, density backward (first order) and the
+//                         second-order front pass h1' = relu'(H0) . (W0 u)
+// They communicate through the weight-gradient operand buffers they write anyway (d1_delta, v).
 template <int L, int W>
-__global__ void __launch_bounds__(256) k_mlp_train(const uint32_t* __restrict__ n_valid_ptr, uint32_t n, uint32_t ld,
-                                                   const float* __restrict__ coords, const half_t* __restrict__ enc_h,
-                                                   const float* __restrict__ dydx, const half_t* __restrict__ dL_dout,
-                                                   MlpPtrs w, TrainBufs tb) {
-	constexpr int DIN = Dims<L>::DIN, DKS = Dims<L>::DKS, DMT = Dims<L>::DMT;
-	constexpr int MT = Fwd<L, W>::MT, HKS = Fwd<L, W>::HKS;
+__global__ void __launch_bounds__(256) k_mlp_train_rgb(const uint32_t* __restrict__ n_valid_ptr, uint32_t n, uint32_t ld,
+                                                       const float* __restrict__ coords, const half_t* __restrict__ enc_h,
+                                                       const float* __restrict__ dydx, const half_t* __restrict__ dL_dout,
+                                                       MlpPtrs w, TrainBufs tb) {
+	constexpr int DKS = Dims<L>::DKS, DMT = Dims<L>::DMT;
+	constexpr int MT = (W + 31) / 32, HKS = W / 16;
 	if (n_valid_ptr && *n_valid_ptr == 0) return;  // zero compacted samples: nothing to train on
 	__shared__ half_t sm[TrainSmem<L, W>::END];
 	using TS = TrainSmem<L, W>;
@@ -544,7 +585,6 @@ __global__ void __launch_bounds__(256) k_mlp_train(const uint32_t* __restrict__ 
 	stage_mat(sm + TS::R2T, w.r2T, W, 16);
 	stage_mat(sm + TS::R1T, w.r1T, W, W);
 	stage_mat(sm + TS::R0T, w.r0T, 48, W);
-	stage_mat(sm + TS::D1T, w.d1T, W, 16);
 	const BwdW bw0{{sm + TS::R2T, 16 + 8}, {sm + TS::R1T, W + 8}, {sm + TS::R0T, W + 8}, {sm + TS::D1T, 16 + 8}};
 	__syncthreads();
 	const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
@@ -561,8 +601,35 @@ __global__ void __launch_bounds__(256) k_mlp_train(const uint32_t* __restrict__ 
 		const uint32_t ic = valid ? i : 0;
 		const float* c = coords + (size_t)ic * COORD_W;
 		const float x[3] = {c[0], c[1], c[2]}, wd[3] = {c[4], c[5], c[6]};
-		Fwd<L, W> F;
-		forward_chunk<L, W>(F, fw, x, wd, enc_h, dydx, ld, ic, valid, r, h);
+		// ---- forward recompute up to the colour hidden layers
+		h8 dinB[DKS];
+		build_din<L>(dinB, x, enc_h, ld, ic, h);
+		f16v H0[MT], D1, Gi[DMT];
+		h8 GhB[HKS];
+		density_forward<L, W>(fw, dinB, r, h, H0, D1, GhB, Gi);
+		float part[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+		for (int mt = 0; mt < DMT; ++mt)
+#pragma unroll
+			for (int reg = 0; reg < 16; ++reg) {
+				const int k = 32 * mt + acc_row(reg, h);
+				const float gv = Gi[mt][reg];
+				if (k < 3) {
+					part[0] += (k == 0) ? gv : 0.f; part[1] += (k == 1) ? gv : 0.f; part[2] += (k == 2) ? gv : 0.f;
+				} else if (k < 3 + 2 * L) {
+					const float* dp = dydx + (size_t)(3 * (k - 3)) * ld + ic;
+					part[0] += gv * dp[0];
+					part[1] += gv * dp[ld];
+					part[2] += gv * dp[2 * (size_t)ld];
+				}
+			}
+		float grad[3];
+#pragma unroll
+		for (int d = 0; d < 3; ++d) grad[d] = part[d] + __shfl_xor(part[d], 32);
+		h8 rinB[3];
+		f16v H1[MT], H2[MT];
+		rgb_hidden<W>(fw, D1, x, wd, grad, r, h, rinB, H1, H2);
+		// ---- colour backward
 		const h8 dlo = *(const h8*)(dL_dout + (size_t)ic * OUT_W + 8 * h);   // h=0: rows 0..7, h=1: rows 8..15
 		const h8 dlo_o = shfl_xor_h8(dlo, 32);
 		const h8 dlo_lo = h ? dlo_o : dlo;   // rows 0..7 on every lane
@@ -571,13 +638,12 @@ __global__ void __launch_bounds__(256) k_mlp_train(const uint32_t* __restrict__ 
 		// delta_o (rows 0..2 = dL/drgb): B fragment, pi order -> lane h=0 elements 0..2
 		h8 dOB = (h8){0, 0, 0, 0, 0, 0, 0, 0};
 		if (h == 0) { dOB[0] = dlo_lo[0]; dOB[1] = dlo_lo[1]; dOB[2] = dlo_lo[2]; }
-		// rgb backward
 		f16v dH2[MT], dH1[MT];
 #pragma unroll
 		for (int mt = 0; mt < MT; ++mt) {
 			f16v acc = mfma(loadA(bw.r2T, W, 32 * mt + r, 0, h), dOB, zero16());
 #pragma unroll
-			for (int q = 0; q < 16; ++q) acc[q] = F.H2[mt][q] > 0.f ? rh(acc[q]) : 0.f;
+			for (int q = 0; q < 16; ++q) acc[q] = H2[mt][q] > 0.f ? rh(acc[q]) : 0.f;
 			dH2[mt] = acc;
 		}
 #pragma unroll
@@ -586,7 +652,7 @@ __global__ void __launch_bounds__(256) k_mlp_train(const uint32_t* __restrict__ 
 #pragma unroll
 			for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(bw.r1T, W, 32 * mt + r, 16 * ks, h), accB(dH2[ks >> 1], ks & 1), acc);
 #pragma unroll
-			for (int q = 0; q < 16; ++q) acc[q] = F.H1[mt][q] > 0.f ? rh(acc[q]) : 0.f;
+			for (int q = 0; q < 16; ++q) acc[q] = H1[mt][q] > 0.f ? rh(acc[q]) : 0.f;
 			dH1[mt] = acc;
 		}
 		f16v dRin[2];
@@ -597,16 +663,80 @@ __global__ void __launch_bounds__(256) k_mlp_train(const uint32_t* __restrict__ 
 			for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(bw.r0T, 48, 32 * mt + r, 16 * ks, h), accB(dH1[ks >> 1], ks & 1), acc);
 			dRin[mt] = rh16(acc);
 		}
-		// density backward: delta_D1 = dL/drgb_in[0:16], row 0 += dL_dout[3] (half add)
+		// delta_D1 = dL/drgb_in[0:16], row 0 += dL_dout[3] (half add)
 		f16v dD1 = dRin[0];
 		if (h == 0) dD1[0] = (float)((half_t)dD1[0] + dlo_lo[3]);
-		const h8 dD1B = accB(dD1, 0);
+		// v = dL/d(grad sdf) (nerf_network.h:478-504): rows 35..37 of dL/drgb_in live at
+		// tile 1: row 3 on h=0 reg 3, rows 4,5 on h=1 regs 0,1
+		const float o3 = __shfl_xor(dRin[1][3], 32), o0 = __shfl_xor(dRin[1][0], 32), o1 = __shfl_xor(dRin[1][1], 32);
+		float v[3];
+		v[0] = h ? o3 : dRin[1][3];
+		v[1] = h ? dRin[1][0] : o0;
+		v[2] = h ? dRin[1][1] : o1;
+		v[0] += (float)dlo_lo[4] / tb.indeed_batch; v[1] += (float)dlo_lo[5] / tb.indeed_batch; v[2] += (float)dlo_lo[6] / tb.indeed_batch;
+		v[0] += (float)dlo_hi[0]; v[1] += (float)dlo_hi[1]; v[2] += (float)dlo_hi[2];
+		if (valid) {
+#pragma unroll
+			for (int mt = 0; mt < MT; ++mt) {
+				store_acc(tb.r0_delta, ld, i, dH1[mt], mt, W, h);
+				store_acc(tb.r1_delta, ld, i, dH2[mt], mt, W, h);
+				store_acc(tb.r1_x, ld, i, H1[mt], mt, W, h);
+				store_acc(tb.r2_x, ld, i, H2[mt], mt, W, h);
+			}
+#pragma unroll
+			for (int ks = 0; ks < 3; ++ks) store_frag(tb.r0_x, ld, i, rinB[ks], ks, 48, h);
+			store_frag(tb.r2_delta, ld, i, dOB, 0, 16, h);
+			store_acc(tb.d1_delta, ld2, i, dD1, 0, 16, h);
+			if (h == 0) tb.v[i] = make_float4(v[0], v[1], v[2], 0.f);
+		}
+	}
+	// variance gradient: batch sum of dL/dout[7] (nerf_network.h:461-474)
+#pragma unroll
+	for (int off = 32; off > 0; off >>= 1) var_part += __shfl_xor(var_part, off);
+	if (lane == 0 && var_part != 0.f) __hip_atomic_fetch_add(tb.var_grad, var_part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int L, int W>
+__global__ void __launch_bounds__(256) k_mlp_train_density(const uint32_t* __restrict__ n_valid_ptr, uint32_t n, uint32_t ld,
+                                                           const float* __restrict__ coords, const half_t* __restrict__ enc_h,
+                                                           const float* __restrict__ dydx, MlpPtrs w, TrainBufs tb) {
+	constexpr int DIN = Dims<L>::DIN, DKS = Dims<L>::DKS, DMT = Dims<L>::DMT;
+	constexpr int MT = (W + 31) / 32, HKS = W / 16;
+	if (n_valid_ptr && *n_valid_ptr == 0) return;
+	__shared__ half_t sm[TrainSmem<L, W>::END];
+	using TS = TrainSmem<L, W>;
+	const FwdW fw0 = stage_fwd<L, W>(sm, w.d0, w.d0T, w);
+	stage_mat(sm + TS::D1T, w.d1T, W, 16);
+	const MatRef d1T0{sm + TS::D1T, 16 + 8};
+	__syncthreads();
+	const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+	const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+	const uint32_t n_waves = (gridDim.x * blockDim.x) >> 6;
+	const size_t ld2 = 2 * (size_t)ld;
+	for (uint32_t base = wave * 32; base < n; base += n_waves * 32) {
+		const uint32_t z = opaque_zero();
+		const FwdW fw = fw0.at(z);
+		const MatRef d1T = rebase(d1T0, z);
+		const uint32_t i = base + r;
+		const bool valid = i < n;
+		const uint32_t ic = valid ? i : 0;
+		const float* c = coords + (size_t)ic * COORD_W;
+		const float x[3] = {c[0], c[1], c[2]};
+		h8 dinB[DKS];
+		build_din<L>(dinB, x, enc_h, ld, ic, h);
+		f16v H0[MT], D1, Gi[DMT];
+		h8 GhB[HKS];
+		density_forward<L, W>(fw, dinB, r, h, H0, D1, GhB, Gi);
+		// delta_D1 from the colour kernel (d1_delta column i), B fragment in pi order
+		h8 dD1B;
+#pragma unroll
+		for (int j = 0; j < 8; ++j) dD1B[j] = tb.d1_delta[(size_t)(h ? pi_row(j, 1) : pi_row(j, 0)) * ld2 + ic];
 		f16v dH0[MT];
 #pragma unroll
 		for (int mt = 0; mt < MT; ++mt) {
-			f16v acc = mfma(loadA(bw.d1T, W, 32 * mt + r, 0, h), dD1B, zero16());
+			f16v acc = mfma(loadA(d1T, W, 32 * mt + r, 0, h), dD1B, zero16());
 #pragma unroll
-			for (int q = 0; q < 16; ++q) acc[q] = F.H0[mt][q] > 0.f ? rh(acc[q]) : 0.f;
+			for (int q = 0; q < 16; ++q) acc[q] = H0[mt][q] > 0.f ? rh(acc[q]) : 0.f;
 			dH0[mt] = acc;
 		}
 		f16v dDin[DMT];
@@ -617,15 +747,8 @@ __global__ void __launch_bounds__(256) k_mlp_train(const uint32_t* __restrict__ 
 			for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(fw.d0T, DIN, 32 * mt + r, 16 * ks, h), accB(dH0[ks >> 1], ks & 1), acc);
 			dDin[mt] = rh16(acc);
 		}
-		// v = dL/d(grad sdf) (nerf_network.h:478-504): rows 35..37 of dL/drgb_in live at
-		// tile 1: row 3 on h=0 reg 3, rows 4,5 on h=1 regs 0,1
-		const float o3 = __shfl_xor(dRin[1][3], 32), o0 = __shfl_xor(dRin[1][0], 32), o1 = __shfl_xor(dRin[1][1], 32);
-		float v[3];
-		v[0] = h ? o3 : dRin[1][3];
-		v[1] = h ? dRin[1][0] : o0;
-		v[2] = h ? dRin[1][1] : o1;
-		v[0] += (float)dlo_lo[4] / tb.indeed_batch; v[1] += (float)dlo_lo[5] / tb.indeed_batch; v[2] += (float)dlo_lo[6] / tb.indeed_batch;
-		v[0] += (float)dlo_hi[0]; v[1] += (float)dlo_hi[1]; v[2] += (float)dlo_hi[2];
+		const float4 v4 = tb.v[ic];
+		const float v[3] = {v4.x, v4.y, v4.z};
 		// u = [v, dy/dx . v, 0] (grid.h:1182-1207), B fragments in pi order
 		h8 uB[DKS];
 #pragma unroll
@@ -649,37 +772,28 @@ __global__ void __launch_bounds__(256) k_mlp_train(const uint32_t* __restrict__ 
 #pragma unroll
 			for (int ks = 0; ks < DKS; ++ks) acc = mfma(loadA(fw.d0, W, 32 * mt + r, 16 * ks, h), uB[ks], acc);
 #pragma unroll
-			for (int q = 0; q < 16; ++q) acc[q] = F.H0[mt][q] > 0.f ? rh(acc[q]) : 0.f;
+			for (int q = 0; q < 16; ++q) acc[q] = H0[mt][q] > 0.f ? rh(acc[q]) : 0.f;
 			H1p[mt] = acc;
 		}
 		if (valid) {
-			// ---- weight-gradient operands
 #pragma unroll
 			for (int mt = 0; mt < MT; ++mt) {
 				store_acc(tb.d0_delta, ld2, i, dH0[mt], mt, W, h);
-				store_acc(tb.d1_x, ld2, i, F.H0[mt], mt, W, h);
+				store_acc(tb.d1_x, ld2, i, H0[mt], mt, W, h);
 				store_acc(tb.d1_x, ld2, ld + i, H1p[mt], mt, W, h);
-				store_acc(tb.r0_delta, ld, i, dH1[mt], mt, W, h);
-				store_acc(tb.r1_delta, ld, i, dH2[mt], mt, W, h);
-				store_acc(tb.r1_x, ld, i, F.H1[mt], mt, W, h);
-				store_acc(tb.r2_x, ld, i, F.H2[mt], mt, W, h);
 			}
 #pragma unroll
-			for (int ks = 0; ks < HKS; ++ks) store_frag(tb.d0_delta, ld2, ld + i, F.GhB[ks], ks, W, h);
+			for (int ks = 0; ks < HKS; ++ks) store_frag(tb.d0_delta, ld2, ld + i, GhB[ks], ks, W, h);
 #pragma unroll
 			for (int ks = 0; ks < DKS; ++ks) {
-				store_frag(tb.d0_x, ld2, i, F.dinB[ks], ks, DIN, h);
+				store_frag(tb.d0_x, ld2, i, dinB[ks], ks, DIN, h);
 				store_frag(tb.d0_x, ld2, ld + i, uB[ks], ks, DIN, h);
 			}
-			store_acc(tb.d1_delta, ld2, i, dD1, 0, 16, h);
 			{
 				h8 e0 = (h8){0, 0, 0, 0, 0, 0, 0, 0};
 				if (h == 0) e0[0] = (half_t)1.0f;
 				store_frag(tb.d1_delta, ld2, ld + i, e0, 0, 16, h);
 			}
-#pragma unroll
-			for (int ks = 0; ks < 3; ++ks) store_frag(tb.r0_x, ld, i, F.rinB[ks], ks, 48, h);
-			store_frag(tb.r2_delta, ld, i, dOB, 0, 16, h);
 			// ---- grid-scatter operands: dL/denc = dDin rows 3.., g = G_in rows 3..
 #pragma unroll
 			for (int mt = 0; mt < DMT; ++mt)
@@ -689,16 +803,11 @@ __global__ void __launch_bounds__(256) k_mlp_train(const uint32_t* __restrict__ 
 					if (k >= 3 && k < 3 + 2 * L) {
 						const size_t e = ((size_t)((k - 3) >> 1) * ld + i) * 2 + ((k - 3) & 1);  // [L][ld] half2
 						tb.dLdenc[e] = (half_t)dDin[mt][reg];
-						tb.genc[e] = (half_t)F.Gi[mt][reg];
+						tb.genc[e] = (half_t)Gi[mt][reg];
 					}
 				}
-			if (h == 0) tb.v[i] = make_float4(v[0], v[1], v[2], 0.f);
 		}
 	}
-	// variance gradient: batch sum of dL/dout[7] (nerf_network.h:461-474)
-#pragma unroll
-	for (int off = 32; off > 0; off >>= 1) var_part += __shfl_xor(var_part, off);
-	if (lane == 0 && var_part != 0.f) __hip_atomic_fetch_add(tb.var_grad, var_part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -786,7 +895,9 @@ void launch_mlp_train(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_v
                       const half_t* enc, const float* dydx, const half_t* dL_dout, const MlpPtrs& w, const TrainBufs& tb) {
 	const uint32_t blocks = std::min<uint32_t>((n + 127) / 128, 2048);
 	if (n == 0) return;
-#define X(l, w_) if (L == l && W == w_) { k_mlp_train<l, w_><<<blocks, 256, 0, s>>>(n_valid_ptr, n, ld, coords, enc, dydx, dL_dout, w, tb); return; }
+#define X(l, w_) if (L == l && W == w_) { \
+		k_mlp_train_rgb<l, w_><<<blocks, 256, 0, s>>>(n_valid_ptr, n, ld, coords, enc, dydx, dL_dout, w, tb); \
+		k_mlp_train_density<l, w_><<<blocks, 256, 0, s>>>(n_valid_ptr, n, ld, coords, enc, dydx, w, tb); return; }
 	NEUS_MLP_CONFIGS(X)
 #undef X
 }

@@ -97,6 +97,10 @@ struct NeusTestbed {
 	Dev<uint8_t> scan_tmp;
 	size_t scan_tmp_bytes = 0;
 	Dev<StepState> st;
+	ScatterWork swork{};
+	Dev<uint32_t> sc_counts, sc_offs;
+	Dev<float2> sc_rec_g;
+	Dev<uint16_t> sc_rec_i;
 	// restructured loss scratch (kernels.h LossWork)
 	Dev<float4> l_sa, l_ck4, l_racc, l_rgr;
 	Dev<float> l_ekt, l_cke, l_rT;
@@ -294,7 +298,17 @@ struct NeusTestbed {
 		tbuf.v = vbuf.p;
 		tbuf.var_grad = grads.p + l.var_off;
 		tbuf.indeed_batch = (float)batch * (float)world;
-		scan_tmp_bytes = scan_temp_bytes(MAX_RAYS);
+		// binned grid-gradient scatter workspace (grid.hip)
+		swork = ScatterWork{};
+		swork.n_blocks = (batch + 255) / 256;
+		swork.n_buckets = scatter_n_buckets(gl);
+		if (swork.n_buckets > SB_MAX_BUCKETS) throw std::runtime_error("hash grid too large for the scatter buckets");
+		const size_t n_bins = (size_t)swork.n_buckets * swork.n_blocks + 1;
+		sc_counts.alloc(n_bins); sc_offs.alloc(n_bins);
+		const size_t n_rec = scatter_records_capacity(swork.n_blocks * 256, l.L);
+		sc_rec_g.alloc(n_rec); sc_rec_i.alloc(n_rec);
+		swork.counts = sc_counts.p; swork.offs = sc_offs.p; swork.rec_g = sc_rec_g.p; swork.rec_i = sc_rec_i.p;
+		scan_tmp_bytes = std::max(scan_temp_bytes(MAX_RAYS), scan_temp_bytes((uint32_t)n_bins));
 		scan_tmp.alloc(scan_tmp_bytes + 256);
 		const uint32_t n_occ = GRID3 * (max_cascade + 1) * 2;
 		occ_pos.alloc(3 * (size_t)n_occ); occ_idx.alloc(n_occ); occ_density.alloc(n_occ);
@@ -388,8 +402,8 @@ struct NeusTestbed {
 		WGradJobs J = wgrad_jobs(n, ld, g, n_train_ptr);
 		launch_wgrad(s, J, J.block_start[5]);
 		if (marks) mark(7);
-		const uint32_t gx = std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, 2048));
-		launch_grid_scatter(s, n_train_ptr, n, ld, c, COORD_W, gl, valid, tbuf.dLdenc, tbuf.genc, tbuf.v, g + lay.grid_off, gx);
+		launch_grid_scatter(s, n_train_ptr, n, ld, c, COORD_W, gl, valid, tbuf.dLdenc, tbuf.genc, tbuf.v, g + lay.grid_off, swork, scan_tmp.p,
+		                    scan_tmp_bytes);
 	}
 
 	// ------------------------------------------------------------ occupancy grid (testbed_nerf.cu:3293-3397, 4003-4016)
@@ -674,6 +688,15 @@ int neus_debug_time_kernel(NeusTestbed* tb, int kernel, int variant, int iters, 
 			case 3: launch_nerf_infer(s, t.lay.L, t.lay.W, &t.st.p->n_kept, 0, t.coords.p, t.gl, valid, t.params_h.p + t.lay.grid_off, t.mlp,
 			                          t.net_out.p, 8192); break;
 			case 4: launch_loss_alpha(s, t.max_samples, t.st.p, t.coords.p, t.net_out.p, t.cos_anneal(), w); break;
+			case 5: {  // both training-MLP kernels on the last step's compacted batch
+				TrainBufs tbuf = t.tbuf;
+				tbuf.var_grad = t.grads.p + t.lay.var_off;
+				launch_mlp_train(s, t.lay.L, t.lay.W, nullptr, t.batch, t.batch, t.coords_c.p, (const half_t*)t.enc.p, t.dydx.p, t.dL_dout.p, t.mlp, tbuf);
+				break;
+			}
+			case 6: { WGradJobs J = t.wgrad_jobs(t.batch, t.batch, t.grads.p, nullptr); launch_wgrad(s, J, J.block_start[5]); break; }
+			case 7: launch_grid_scatter(s, nullptr, t.batch, t.batch, t.coords_c.p, COORD_W, t.gl, valid, t.tbuf.dLdenc, t.tbuf.genc, t.tbuf.v,
+			                            t.grads.p + t.lay.grid_off, t.swork, t.scan_tmp.p, t.scan_tmp_bytes); break;
 			default: throw std::runtime_error("unknown kernel id");
 			}
 		}

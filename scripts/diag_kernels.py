@@ -10,9 +10,9 @@ sc = scenes.sphere_scene(49, 1600, 1200, principal=(823.2 / 1600, 619.1 / 1200))
 tb = pyngp.Testbed(pyngp.TestbedMode.Nerf)
 tb.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
 tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=1 << 18, fixed_rays_per_batch=1 << 18)
-tb.train_steps(int(os.environ.get("WARM", "120")))
-names = {0: "march_count", 1: "march_write", 2: "loss_scan", 3: "nerf_infer", 4: "loss_alpha"}
-for kern, variants in [(0, (0, 1)), (1, (0, 1)), (2, (0, 1)), (3, (0,)), (4, (0,))]:
+tb.train_steps(int(os.environ.get("WARM", "800")))
+names = {0: "march_count", 1: "march_write", 2: "loss_scan", 3: "nerf_infer", 4: "loss_alpha", 5: "mlp_train", 6: "wgrad", 7: "grid_scatter"}
+for kern, variants in [(0, (0,)), (1, (0,)), (2, (0,)), (3, (0,)), (4, (0,)), (5, (0,)), (6, (0,)), (7, (0,))]:
     for v in variants:
         ms = C.c_float()
         check(lib().neus_debug_time_kernel(tb.handle, kern, v, 10, C.byref(ms)))

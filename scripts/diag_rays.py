@@ -11,7 +11,7 @@ tb = pyngp.Testbed(pyngp.TestbedMode.Nerf)
 tb.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
 tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=1 << 18, fixed_rays_per_batch=1 << 18)
 out = {}
-for steps in (1, 50, 150, 500):
+for steps in (300, 800, 2000):
     tb.train_steps(steps - tb.training_step)
     nreq, cn, comp = tb.ray_counts()
     q = lambda a: [int(np.percentile(a, p)) for p in (50, 90, 99, 99.9, 100)]

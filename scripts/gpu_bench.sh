@@ -7,5 +7,5 @@ timeout -k 10 600 python bench.py --steps $STEPS --warmup $WARM --cpu-steps 6 > 
 rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench_$TAG.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_$TAG" -o run -- python3 "$R/bench.py" --steps 20 --warmup 30 --cpu-baseline 0 > "$R/gpurun_out/prof_$TAG.log" 2>&1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_$TAG" -o run -- python3 "$R/bench.py" --steps 20 --warmup 800 --cpu-baseline 0 > "$R/gpurun_out/prof_$TAG.log" 2>&1
 rc=$?; echo "rocprof rc=$rc"; exit $rc

@@ -1,5 +1,8 @@
 """Summarise a rocprofv3 --kernel-trace --stats run (rocpd SQLite db or kernel_stats.csv) into a
-markdown table: kernel, calls, total ms, average us, share. Usage: prof_summary.py <db|csv> [out.md]"""
+markdown table: kernel, calls, total ms, average us, share.
+Usage: prof_summary.py <db|csv> [out.md] [--last-steps K]
+--last-steps K (db only): only dispatches from the K-th last k_march_count launch on, i.e. the final K
+training steps (the steady state after the bench warm-up), with the per-step time of each kernel."""
 import csv
 import re
 import sqlite3
@@ -34,17 +37,39 @@ def rows_from(path):
     return out
 
 
+def rows_last_steps(path, k):
+    con = sqlite3.connect(path)
+    starts = [r[0] for r in con.execute("select start from kernels where name like '%k_march_count%' order by start")]
+    t0 = starts[-k]
+    out = {}
+    for name, dur in con.execute("select name, duration from kernels where start >= ?", (t0,)):
+        c, t = out.get(name, (0, 0.0))
+        out[name] = (c + 1, t + float(dur))
+    return [(n, c, t, t / c) for n, (c, t) in out.items()]
+
+
 def main():
-    rows = rows_from(sys.argv[1])
+    args = [a for a in sys.argv[1:]]
+    last = None
+    if "--last-steps" in args:
+        i = args.index("--last-steps")
+        last = int(args[i + 1])
+        del args[i:i + 2]
+    sys.argv = [sys.argv[0]] + args
+    rows = rows_last_steps(sys.argv[1], last) if last else rows_from(sys.argv[1])
     agg = {}
     for name, calls, tot, _ in rows:
         k = short(name)
         c, t = agg.get(k, (0, 0.0))
         agg[k] = (c + calls, t + tot)
     total = sum(t for _, t in agg.values())
-    lines = ["| kernel | calls | total ms | avg us | share |", "|---|---:|---:|---:|---:|"]
+    hdr = "| kernel | calls | total ms | avg us | share |" + (" us/step |" if last else "")
+    lines = [hdr, "|---|---:|---:|---:|---:|" + ("---:|" if last else "")]
     for k, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
-        lines.append(f"| {k} | {c} | {t / 1e6:.3f} | {t / c / 1e3:.1f} | {100 * t / total:.1f}% |")
+        extra = f" {t / last / 1e3:.1f} |" if last else ""
+        lines.append(f"| {k} | {c} | {t / 1e6:.3f} | {t / c / 1e3:.1f} | {100 * t / total:.1f}% |" + extra)
+    if last:
+        lines.append(f"\nGPU kernel time per step over the last {last} steps: {total / last / 1e6:.3f} ms")
     text = "\n".join(lines) + "\n"
     if len(sys.argv) > 2:
         open(sys.argv[2], "w").write(text)
