@@ -105,6 +105,7 @@ struct GridLevels {
 	uint32_t offset[MAX_LEVELS + 1];   // in entries (x2 features)
 	uint32_t res[MAX_LEVELS];
 	float scale[MAX_LEVELS];
+	uint32_t dense_bits;               // bit l: level l is dense (res^3 <= entries), else hashed with 2^k entries
 };
 NEUS_HD uint32_t grid_index(uint32_t hashmap_size, uint32_t resolution, uint32_t x, uint32_t y, uint32_t z) {
 	uint32_t stride = 1, index = 0;

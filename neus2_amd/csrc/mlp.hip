@@ -151,6 +151,11 @@ template <int L> struct Fused {
 };
 
 // Evaluates this lane's levels for position x: features ev[m] (level 2m+h) and, if DYDX, dy/dx.
+// Same arithmetic as grid_common.h (bit-identical features / dy/dx), restructured for issue count:
+// level parameters are selected per lane half without branches, corner indices share their
+// per-axis terms (dense levels: x + y res + z res^2; hashed levels: the xor hash masked by the
+// power-of-two table size, which is the reference's `% hashmap_size` there), and the corner
+// weights reuse the axis products in the reference's multiplication order.
 template <int L, bool DYDX>
 __device__ __forceinline__ void fused_levels(const GridLevels& gl, uint32_t valid_level, const half_t* __restrict__ grid,
                                              const float x[3], int h, h2 ev[], float dy[][2][3]) {
@@ -167,15 +172,80 @@ __device__ __forceinline__ void fused_levels(const GridLevels& gl, uint32_t vali
 #pragma unroll
 				for (int d = 0; d < 3; ++d) dy[m][f][d] = 0.f;
 		}
-		if (act) {
-			const float sc = h ? gl.scale[l1] : gl.scale[l0];
-			const uint32_t res = h ? gl.res[l1] : gl.res[l0];
-			const uint32_t o0 = h ? gl.offset[l1] : gl.offset[l0], o1 = h ? gl.offset[l1 + 1] : gl.offset[l0 + 1];
-			const LevelSetup s = level_setup(sc, res, o1 - o0, x[0], x[1], x[2]);
-			h2 v[8];
-			gather_corners(s, grid + (size_t)o0 * 2, v);
-			ev[m] = interp_features(s, v);
-			if (DYDX) interp_dydx(s, v, dy[m]);
+		// per-level branch (uniform once every level is active): the block boundary also keeps one
+		// level's gathers in flight at a time, which bounds VGPR pressure
+		if (!act) continue;
+		const float sc = h ? gl.scale[l1] : gl.scale[l0];
+		const uint32_t res = h ? gl.res[l1] : gl.res[l0];
+		const uint32_t o0 = h ? gl.offset[l1] : gl.offset[l0], o1 = h ? gl.offset[l1 + 1] : gl.offset[l0 + 1];
+		const bool dense = (gl.dense_bits >> l) & 1u;
+		const uint32_t hmask = (o1 - o0) - 1u;
+		// pos_fract (common_device.h:404-434)
+		float f[3]; uint32_t gp[3];
+		const float xin[3] = {x[0], x[1], x[2]};
+#pragma unroll
+		for (int d = 0; d < 3; ++d) {
+			const float p = __builtin_fmaf(xin[d], sc, 0.5f);
+			const float fl = floorf(p);
+			gp[d] = (uint32_t)(int)fl;
+			f[d] = p - fl;
+		}
+		// corner indices (grid.h:118-153)
+		uint32_t yz[4];
+#pragma unroll
+		for (int k = 0; k < 4; ++k) {
+			const uint32_t yy = gp[1] + (k & 1), zz = gp[2] + (k >> 1);
+			const uint32_t dn = yy * res + zz * (res * res);
+			const uint32_t hs = (yy * 2654435761u) ^ (zz * 805459861u);
+			yz[k] = dense ? dn : hs;
+		}
+		const half_t* gbase = grid + (size_t)o0 * 2;
+		h2 v[8];
+#pragma unroll
+		for (int c = 0; c < 8; ++c) {
+			const uint32_t xx = gp[0] + (c & 1);
+			const uint32_t k = c >> 1;
+			// dense corners past the last cell wrap as the reference's `% hashmap_size` (index < 2 size)
+			const uint32_t ed = xx + yz[k], eh = (xx ^ yz[k]) & hmask;
+			const uint32_t e = dense ? (ed >= o1 - o0 ? ed - (o1 - o0) : ed) : eh;
+			v[c] = *(const h2*)(gbase + 2 * (size_t)e);
+		}
+		// weights: ((1 * wx) * wy) * wz, as the reference's loop
+		const float wx[2] = {1.f - f[0], f[0]}, wy[2] = {1.f - f[1], f[1]}, wz[2] = {1.f - f[2], f[2]};
+		half_t r0 = (half_t)0.f, r1 = (half_t)0.f;
+#pragma unroll
+		for (int c = 0; c < 8; ++c) {
+			const float w = (wx[c & 1] * wy[(c >> 1) & 1]) * wz[c >> 2];
+			r0 = (half_t)((float)r0 + (float)(half_t)(w * (float)v[c][0]));
+			r1 = (half_t)((float)r1 + (float)(half_t)(w * (float)v[c][1]));
+		}
+		ev[m] = (h2){r0, r1};
+		if (DYDX) {
+			// weight = ((scale * w_a) * w_b) over the two non-gradient dims in increasing order
+			const float sx[2] = {sc * wx[0], sc * wx[1]}, sy[2] = {sc * wy[0], sc * wy[1]};
+			float g[2][3];
+#pragma unroll
+			for (int q = 0; q < 2; ++q)
+#pragma unroll
+				for (int d = 0; d < 3; ++d) g[q][d] = 0.f;
+#pragma unroll
+			for (int gd = 0; gd < 3; ++gd)
+#pragma unroll
+				for (int idx = 0; idx < 4; ++idx) {
+					const int b0 = idx & 1, b1 = (idx >> 1) & 1;
+					float w;
+					uint32_t cl;
+					if (gd == 0) { w = sy[b0] * wz[b1]; cl = (b0 << 1) | (b1 << 2); }
+					else if (gd == 1) { w = sx[b0] * wz[b1]; cl = b0 | (b1 << 2); }
+					else { w = sx[b0] * wy[b1]; cl = b0 | (b1 << 1); }
+					const uint32_t cr = cl | (1u << gd);
+					g[0][gd] = __builtin_fmaf(w, (float)v[cr][0] - (float)v[cl][0], g[0][gd]);
+					g[1][gd] = __builtin_fmaf(w, (float)v[cr][1] - (float)v[cl][1], g[1][gd]);
+				}
+#pragma unroll
+			for (int q = 0; q < 2; ++q)
+#pragma unroll
+				for (int d = 0; d < 3; ++d) dy[m][q][d] = g[q][d];
 		}
 	}
 }
@@ -200,6 +270,16 @@ __device__ __forceinline__ float slot_dydx(int q, int h, int d, const float dy[]
 	if (q < 2 * M1) v1 = dy[q / 2][q % 2][d];
 	else if (NT == 1 && q == 2 * M1) v1 = tdy[d];
 	return h ? v1 : v0;
+}
+
+// fp16 B fragment (k-step s) of an accumulator tile, optionally through ReLU: (half)max(acc, 0) is the
+// reference's fp16 storage of the post-activation value
+template <bool RELU>
+__device__ __forceinline__ h8 frag(const f16v& acc, int s) {
+	h8 b;
+#pragma unroll
+	for (int j = 0; j < 8; ++j) b[j] = (half_t)(RELU ? fmaxf(acc[8 * s + j], 0.f) : acc[8 * s + j]);
+	return b;
 }
 
 __device__ __forceinline__ void sh16(const float wd[3], float out[16]) {
@@ -335,8 +415,9 @@ __device__ __forceinline__ void density_forward(const FwdW& w, const h8* dinB, i
 // ------------------------------------------------------------------------------------------
 // Fused pre-compaction forward (hash-grid encode + NerfNetwork::forward, nerf_network.h:145-328):
 // coords AoS7 -> out AoS16 fp16. The encodings and dy/dx never leave the registers; only the 28 B
-// coordinate and the 32 B output per sample touch HBM. n from device memory; 32 samples per
-// wave-iteration, grid-strided.
+// coordinate and the 32 B output per sample touch HBM. Activations are kept as fp16 B fragments
+// (their storage precision), not fp32 tiles. n from device memory; 32 samples per wave-iteration,
+// grid-strided.
 // ------------------------------------------------------------------------------------------
 template <int L, int W>
 __global__ void __launch_bounds__(256) k_nerf_infer(const uint32_t* __restrict__ n_ptr, uint32_t n_fixed, const float* __restrict__ coords,
@@ -351,7 +432,7 @@ __global__ void __launch_bounds__(256) k_nerf_infer(const uint32_t* __restrict__
 	const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
 	const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
 	const uint32_t n_waves = (gridDim.x * blockDim.x) >> 6;
-	const float var = (float)wp.var[0];
+	const half_t var_h = wp.var[0];
 	const half_t bias_h = (half_t)wp.sdf_bias;
 	for (uint32_t base = wave * 32; base < n; base += n_waves * 32) {
 		const FwdW w = w0.at(opaque_zero());
@@ -376,39 +457,96 @@ __global__ void __launch_bounds__(256) k_nerf_infer(const uint32_t* __restrict__
 		for (int ks = 0; ks < DKS; ++ks)
 #pragma unroll
 			for (int j = 0; j < 8; ++j) dinB[ks][j] = (half_t)slot_value<L>(8 * ks + j, h, xm, ev, tv);
-		// ---- density MLP + dSDF/d(din)
-		f16v H0[MT], D1, Gi[DMT];
+		// ---- density MLP (fragments of the fp16-stored activations)
+		h8 H0B[HKS];
+#pragma unroll
+		for (int mt = 0; mt < MT; ++mt) {
+			f16v acc = zero16();
+#pragma unroll
+			for (int ks = 0; ks < DKS; ++ks) acc = mfma(loadA(w.d0, W, 32 * mt + r, 16 * ks, h), dinB[ks], acc);
+			H0B[2 * mt] = frag<true>(acc, 0); H0B[2 * mt + 1] = frag<true>(acc, 1);
+		}
+		h8 D1B;
+		{
+			f16v acc = zero16();
+#pragma unroll
+			for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.d1, 16, r, 16 * ks, h), H0B[ks], acc);
+			D1B = frag<false>(acc, 0);
+		}
+		// G_h = relu'(H0) . W1d[0]; G_in = W0d^T G_h (fp16-stored)
 		h8 GhB[HKS];
-		density_forward<L, W>(w, dinB, r, h, H0, D1, GhB, Gi);
+#pragma unroll
+		for (int ks = 0; ks < HKS; ++ks) {
+			const h8 w1row = loadA(w.d1, 16, 0, 16 * ks, h);
+#pragma unroll
+			for (int j = 0; j < 8; ++j) GhB[ks][j] = H0B[ks][j] > (half_t)0.f ? w1row[j] : (half_t)0.f;
+		}
 		// dSDF/dx = sum_q G_in[q] dy/dx[q] (+ identity for the xyz slots of h = 0), halves summed
 		float part[3] = {0.f, 0.f, 0.f};
 #pragma unroll
-		for (int q = 0; q < HALF; ++q) {
-			const float gv = Gi[q / 16][q % 16];
+		for (int mt = 0; mt < DMT; ++mt) {
+			f16v acc = zero16();
 #pragma unroll
-			for (int d = 0; d < 3; ++d) {
-				const float id = (q == d) ? (h ? 0.f : 1.f) : 0.f;
-				part[d] += gv * (slot_dydx<L>(q, h, d, dy, tdy) + id);
+			for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.d0T, Dims<L>::DIN, 32 * mt + r, 16 * ks, h), GhB[ks], acc);
+#pragma unroll
+			for (int reg = 0; reg < 16; ++reg) {
+				const int q = 16 * mt + reg;
+				if (q >= HALF) continue;
+				const float gv = rh(acc[reg]);
+#pragma unroll
+				for (int d = 0; d < 3; ++d) {
+					const float id = (q == d) ? (h ? 0.f : 1.f) : 0.f;
+					part[d] += gv * (slot_dydx<L>(q, h, d, dy, tdy) + id);
+				}
 			}
 		}
 		float grad[3];
 #pragma unroll
 		for (int d = 0; d < 3; ++d) grad[d] = part[d] + __shfl_xor(part[d], 32);
-		// ---- colour MLP
+		// ---- colour MLP: input [density out (16), SH4 (16), xyz, grad sdf, 0...]
 		h8 rinB[3];
-		f16v H1[MT], H2[MT];
-		const f16v O = rgb_forward<W>(w, D1, x, wd, grad, r, h, rinB, H1, H2);
-		const float row11 = __shfl_xor(O[7], 32);  // lane h=0 holds row 11 in reg 7
+		rinB[0] = D1B;
+		{
+			float sh[16]; sh16(wd, sh);
+#pragma unroll
+			for (int j = 0; j < 8; ++j) rinB[1][j] = (half_t)(h ? sh[pi_row(j, 1)] : sh[pi_row(j, 0)]);
+			float r32[16];
+#pragma unroll
+			for (int k = 0; k < 16; ++k) r32[k] = 0.f;
+			r32[0] = x[0]; r32[1] = x[1]; r32[2] = x[2];
+			r32[3] = grad[0]; r32[4] = grad[1]; r32[5] = grad[2];
+#pragma unroll
+			for (int j = 0; j < 8; ++j) rinB[2][j] = (half_t)(h ? r32[pi_row(j, 1)] : r32[pi_row(j, 0)]);
+		}
+		h8 H1B[HKS], H2B[HKS];
+#pragma unroll
+		for (int mt = 0; mt < MT; ++mt) {
+			f16v acc = zero16();
+#pragma unroll
+			for (int ks = 0; ks < 3; ++ks) acc = mfma(loadA(w.r0, W, 32 * mt + r, 16 * ks, h), rinB[ks], acc);
+			H1B[2 * mt] = frag<true>(acc, 0); H1B[2 * mt + 1] = frag<true>(acc, 1);
+		}
+#pragma unroll
+		for (int mt = 0; mt < MT; ++mt) {
+			f16v acc = zero16();
+#pragma unroll
+			for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.r1, W, 32 * mt + r, 16 * ks, h), H1B[ks], acc);
+			H2B[2 * mt] = frag<true>(acc, 0); H2B[2 * mt + 1] = frag<true>(acc, 1);
+		}
+		f16v O = zero16();
+#pragma unroll
+		for (int ks = 0; ks < HKS; ++ks) O = mfma(loadA(w.r2, 16, r, 16 * ks, h), H2B[ks], O);
+		const half_t row11 = (half_t)__shfl_xor(O[7], 32);  // lane h=0 holds row 11 in reg 7
 		if (valid) {
 			h8 o;
 			if (h == 0) {
 				o[0] = (half_t)O[0]; o[1] = (half_t)O[1]; o[2] = (half_t)O[2];
-				o[3] = (half_t)D1[0] + bias_h;                     // half add (common_operation.cuh:964)
+				o[3] = D1B[0] + bias_h;                              // half add (common_operation.cuh:964)
 				o[4] = (half_t)grad[0]; o[5] = (half_t)grad[1]; o[6] = (half_t)grad[2];
-				o[7] = (half_t)var;
+				o[7] = var_h;
 			} else {
 				o[0] = (half_t)wd[0]; o[1] = (half_t)wd[1]; o[2] = (half_t)wd[2];
-				o[3] = (half_t)row11;
+				o[3] = row11;
 				o[4] = (half_t)O[4]; o[5] = (half_t)O[5]; o[6] = (half_t)O[6]; o[7] = (half_t)O[7];
 			}
 			*(h8*)(out + (size_t)i * OUT_W + 8 * h) = o;
@@ -447,17 +585,17 @@ __global__ void __launch_bounds__(256) k_nerf_density(uint32_t n, const float* _
 		for (int ks = 0; ks < DKS; ++ks)
 #pragma unroll
 			for (int j = 0; j < 8; ++j) dinB[ks][j] = (half_t)slot_value<L>(8 * ks + j, h, xm, ev, tv);
-		f16v H0[MT];
+		h8 H0B[HKS];
 #pragma unroll
 		for (int mt = 0; mt < MT; ++mt) {
 			f16v acc = zero16();
 #pragma unroll
 			for (int ks = 0; ks < DKS; ++ks) acc = mfma(loadA(w.d0, W, 32 * mt + r, 16 * ks, h), dinB[ks], acc);
-			H0[mt] = rh16(relu16(acc));
+			H0B[2 * mt] = frag<true>(acc, 0); H0B[2 * mt + 1] = frag<true>(acc, 1);
 		}
 		f16v acc = zero16();
 #pragma unroll
-		for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.d1, 16, r, 16 * ks, h), accB(H0[ks >> 1], ks & 1), acc);
+		for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.d1, 16, r, 16 * ks, h), H0B[ks], acc);
 		if (valid && h == 0) {
 			const half_t sdf = (half_t)acc[0] + bias_h;
 			const half_t s = (half_t)__expf((float)(var_h * (half_t)10.0f));

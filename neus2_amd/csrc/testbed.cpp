@@ -217,6 +217,12 @@ struct NeusTestbed {
 			offset += pil;
 		}
 		gl.offset[c.n_levels] = offset;
+		gl.dense_bits = 0;
+		for (uint32_t i = 0; i < c.n_levels; ++i) {
+			const uint64_t r = gl.res[i], hs = gl.offset[i + 1] - gl.offset[i];
+			if (r * r * r <= hs) gl.dense_bits |= 1u << i;
+			else if ((hs & (hs - 1)) != 0) throw std::runtime_error("hashed grid level with a non-power-of-two table");
+		}
 		// parameter layout (nerf_network.h:741-785)
 		Layout& l = lay;
 		l.L = c.n_levels; l.W = c.n_neurons; l.din = next_multiple(3 + 2 * c.n_levels, 16);
