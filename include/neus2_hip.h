@@ -132,6 +132,9 @@ int neus_testbed_ray_counts(NeusTestbed* tb, uint32_t n, uint32_t* nreq, uint32_
  * kernel (0 march count, 1 march write, 2 loss transmittance scan, 3 fused inference, 4 loss alpha)
  * in implementation `variant` (0 = production); mean ms per launch. */
 int neus_debug_time_kernel(NeusTestbed* tb, int kernel, int variant, int iters, float* ms_out);
+// Development statistic of the last step's march: per ray {march_step calls, skip-loop additions,
+// samples} (3 x u32 per ray, n rays; cone_angle 0 only).
+int neus_debug_march_stats(NeusTestbed* tb, uint32_t n, uint32_t* out);
 int neus_testbed_stream(NeusTestbed* tb, void** hip_stream);
 int neus_testbed_synchronize(NeusTestbed* tb);
 /* Per-phase step timing with hipEvents recorded on the testbed stream (profiling on), mean ms per step:

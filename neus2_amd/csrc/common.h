@@ -33,8 +33,6 @@ constexpr uint32_t GRID3 = NERF_GRIDSIZE * NERF_GRIDSIZE * NERF_GRIDSIZE;
 constexpr uint32_t MAX_LEVELS = 16;
 constexpr uint32_t OUT_W = 16;      // padded network output width (nerf_network.h:935)
 constexpr uint32_t COORD_W = 7;     // NerfCoordinate floats (nerf.h:76-102)
-constexpr uint32_t MARCH_SEG = 32;  // samples per march-write segment (checkpointed by the count pass)
-constexpr uint32_t MARCH_SEGS = NERF_STEPS / MARCH_SEG;
 
 // ----------------------------------------------------------- pcg32 (my_tcnn pcg32.h:43-170)
 struct pcg32 {

@@ -108,11 +108,14 @@ void launch_wgrad(hipStream_t s, const WGradJobs& jobs, uint32_t n_blocks);
 void launch_mfma_probe(hipStream_t s, const half_t* A, const half_t* B, float* C);
 // march.hip
 void launch_bitfield_linear(hipStream_t s, const uint8_t* bitfield, uint32_t* lin /* GRID3 / 32 words */);
+// Ray generation + the occupancy march: rays (6 f32 per slot), tstart (1 per slot), nreq (requested
+// samples per slot), tbuf (NERF_STEPS f32 per slot: the t of every requested sample).
 void launch_march_count(hipStream_t s, uint32_t cap, const StepState* st, DPInfo dp, const DevDataset& ds, const uint8_t* bitfield,
-                        const uint32_t* lin, uint64_t rng_state, uint64_t rng_inc, float* rays, float* ckpt /* MARCH_SEGS per ray */, uint32_t* nreq);
-void launch_march_write(hipStream_t s, uint32_t cap, StepState* st, const DevDataset& ds, const uint8_t* bitfield, const uint32_t* lin,
-                        const float* rays, const float* ckpt, const uint32_t* nreq, const uint32_t* base, uint32_t* numsteps, float* coords,
-                        uint32_t* sample_ray);
+                        const uint32_t* lin, uint64_t rng_state, uint64_t rng_inc, float* rays, float* tstart, uint32_t* nreq, float* tbuf);
+void launch_march_write(hipStream_t s, uint32_t cap, StepState* st, const DevDataset& ds, const float* rays, const float* tbuf, const uint32_t* nreq,
+                        const uint32_t* base, uint32_t* numsteps, float* coords, uint32_t* sample_ray, uint32_t sample_cap /* >= max_inference */);
+void debug_launch_march_stats(hipStream_t s, uint32_t n_rays, const float* rays, const float* tstart, const uint32_t* lin, const DevDataset& ds,
+                              const uint8_t* bf, uint32_t* out);
 void launch_loss_alpha(hipStream_t s, uint32_t cap_samples, const StepState* st, const float* coords, const half_t* net_out, float cos_anneal,
                        const LossWork& w);
 void launch_loss_scan_ray(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, const LossWork& w, uint32_t* ccount);

@@ -1,6 +1,6 @@
 // NeuS ray sampling, SDF-to-alpha compositing, loss and deterministic compaction on gfx950.
 //
-//   k_march_count / k_march_write : generate_training_samples_nerf_with_global_movement
+//   k_ray_gen / k_march / k_march_write : generate_training_samples_nerf_with_global_movement
 //                                   (testbed_nerf.cu:1263-1456), static path
 //   k_loss_count  / k_loss_write  : compute_loss_kernel_train_nerf_with_global_movement
 //                                   (testbed_nerf.cu:1475-1997), static path
@@ -89,8 +89,9 @@ __device__ __forceinline__ void read_rgba(const DevDataset& ds, uint32_t img, fl
 	o[3] = a;
 }
 __device__ __forceinline__ bool aabb_contains(const DevDataset& ds, const float p[3]) {
-	return p[0] >= ds.aabb_min[0] && p[0] <= ds.aabb_max[0] && p[1] >= ds.aabb_min[1] && p[1] <= ds.aabb_max[1] &&
-	       p[2] >= ds.aabb_min[2] && p[2] <= ds.aabb_max[2];
+	// bitwise: no short-circuit branches in the march loop (same predicate)
+	return (p[0] >= ds.aabb_min[0]) & (p[0] <= ds.aabb_max[0]) & (p[1] >= ds.aabb_min[1]) & (p[1] <= ds.aabb_max[1]) &
+	       (p[2] >= ds.aabb_min[2]) & (p[2] <= ds.aabb_max[2]);
 }
 __device__ __forceinline__ void ray_intersect(const DevDataset& ds, const float o[3], const float d[3], float& tmin_o) {
 	float tmin = (ds.aabb_min[0] - o[0]) / d[0], tmax = (ds.aabb_max[0] - o[0]) / d[0];
@@ -141,14 +142,17 @@ __device__ __forceinline__ int march_step(const DevDataset& ds, const uint8_t* _
 	bool occ;
 	if (FAST) {
 		dt = MIN_CONE_STEPSIZE;  // calc_dt(t, 0)
-		mip = (uint32_t)mip_from_pos(pos[0], pos[1], pos[2]);  // dt * 256 < 1
-		if (mip == 0) {
+		// mip_from_pos (dt * 256 < 1) is 0 iff 0 < max|p - 0.5| < 0.5 (frexpf(0) has exponent 0 -> mip 1)
+		const float m = fmaxf(fmaxf(fabsf(pos[0] - 0.5f), fabsf(pos[1] - 0.5f)), fabsf(pos[2] - 0.5f));
+		if ((m > 0.0f) & (m < 0.5f)) {
+			mip = 0;
 			// cascaded_grid_idx_at with scale 1: ((p - 0.5) * 1) + 0.5
 			const int ix = clampi((int)(((pos[0] - 0.5f) + 0.5f) * NERF_GRIDSIZE), 0, NERF_GRIDSIZE - 1);
 			const int iy = clampi((int)(((pos[1] - 0.5f) + 0.5f) * NERF_GRIDSIZE), 0, NERF_GRIDSIZE - 1);
 			const int iz = clampi((int)(((pos[2] - 0.5f) + 0.5f) * NERF_GRIDSIZE), 0, NERF_GRIDSIZE - 1);
 			occ = (lin[((uint32_t)ix << 9) | ((uint32_t)iy << 2) | ((uint32_t)iz >> 5)] >> (iz & 31)) & 1;
 		} else {
+			mip = (uint32_t)mip_from_pos(pos[0], pos[1], pos[2]);
 			occ = occupied(pos[0], pos[1], pos[2], bf, mip);
 		}
 	} else {
@@ -174,35 +178,16 @@ __device__ __forceinline__ int march_step(const DevDataset& ds, const uint8_t* _
 	return 2;
 }
 
-template <bool FAST>
-__device__ __forceinline__ uint32_t march_count_ray(const DevDataset& ds, const uint8_t* __restrict__ bf, const uint32_t* __restrict__ lin,
-                                                    const MarchRay& r, float t, float* __restrict__ ckpt_ray) {
-	uint32_t n = 0;
-	while (n < NERF_STEPS) {
-		float dt, pos[3];
-		const int k = march_step<FAST>(ds, bf, lin, r, t, dt, pos);
-		if (k == 0) break;
-		if (k == 1) {
-			++n; t += dt;
-			if ((n & (MARCH_SEG - 1)) == 0 && n < NERF_STEPS) ckpt_ray[n / MARCH_SEG] = t;
-		}
-	}
-	return n;
-}
-
-// ---------------------------------------------------------------- pass 1: per-ray count
-// rays: 6 floats/ray (o, unnormalized d); ckpt: MARCH_SEGS floats/ray = the march parameter t at which
-// the search for sample 32*s starts (s = 0: the jittered start), so the write pass can re-march each
-// 32-sample segment independently and bit-identically; nreq: requested steps (0 = none)
-__global__ void __launch_bounds__(256) k_march_count(uint32_t cap_rays, const StepState* __restrict__ st, DPInfo dp, DevDataset ds,
-                                                     const uint8_t* __restrict__ bitfield, const uint32_t* __restrict__ lin,
-                                                     uint64_t rng_state, uint64_t rng_inc,
-                                                     float* __restrict__ rays, float* __restrict__ ckpt, uint32_t* __restrict__ nreq) {
+// ---------------------------------------------------------------- pass 0: ray generation
+// Thread per ray slot: pixel/image pick from the ray's pcg32 stream, pinhole ray, AABB entry and
+// jittered start (testbed_nerf.cu:1263-1375). rays: 6 floats (o, unnormalised d); tstart: the jittered
+// start t, or -1 for a dropped ray and for slots >= R (nothing to march).
+__global__ void __launch_bounds__(256) k_ray_gen(uint32_t cap_rays, const StepState* __restrict__ st, DPInfo dp, DevDataset ds,
+                                                 uint64_t rng_state, uint64_t rng_inc, float* __restrict__ rays, float* __restrict__ tstart) {
 	const uint32_t R = st->rays_per_batch;
 	const uint32_t n_rays_global = R * dp.world, n_rays_total = st->n_rays_total;
 	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cap_rays; i += gridDim.x * blockDim.x) {
-		uint32_t n = 0;
-		float o[3] = {0, 0, 0}, du[3] = {0, 0, 0}, startt = 0.f;
+		float o[3] = {0, 0, 0}, du[3] = {0, 0, 0}, startt = -1.0f;
 		if (i < R) {
 			const uint32_t ig = dp.rank * R + i;
 			pcg32 rng(rng_state, rng_inc);
@@ -228,81 +213,166 @@ __global__ void __launch_bounds__(256) k_march_count(uint32_t cap_rays, const St
 				tmin = fmaxf(tmin, 0.0f);
 				startt = tmin;
 				startt += calc_dt(startt, ds.cone_angle) * rng.next_float();
-				MarchRay mr;
-#pragma unroll
-				for (int d = 0; d < 3; ++d) { mr.o[d] = o[d]; mr.dir[d] = dir[d]; mr.idir[d] = 1.0f / dir[d]; }
-				float* ck = ckpt + (size_t)i * MARCH_SEGS;
-				n = lin ? march_count_ray<true>(ds, bitfield, lin, mr, startt, ck) : march_count_ray<false>(ds, bitfield, lin, mr, startt, ck);
 			}
 		}
 		float* rr = rays + 6 * (size_t)i;
 		rr[0] = o[0]; rr[1] = o[1]; rr[2] = o[2]; rr[3] = du[0]; rr[4] = du[1]; rr[5] = du[2];
-		ckpt[(size_t)i * MARCH_SEGS] = startt;
-		nreq[i] = n;
+		tstart[i] = startt;
 	}
 }
 
-// ---------------------------------------------------------------- pass 2: write kept rays
-// One thread per (ray, 32-sample segment): each re-marches its segment from the count pass's
-// checkpoint, so a few long rays (early training: ~500 samples each) spread over many lanes.
-__global__ void __launch_bounds__(256) k_march_write(uint32_t cap_rays, StepState* __restrict__ st, DevDataset ds,
-                                                     const uint8_t* __restrict__ bitfield, const uint32_t* __restrict__ lin,
-                                                     const float* __restrict__ rays,
-                                                     const float* __restrict__ ckpt, const uint32_t* __restrict__ nreq,
-                                                     const uint32_t* __restrict__ base, uint32_t* __restrict__ numsteps,
-                                                     float* __restrict__ coords, uint32_t* __restrict__ sample_ray) {
-	const uint32_t max_samples = st->max_inference;
-	const uint32_t n_tasks = cap_rays * MARCH_SEGS;
-	const uint32_t lane = threadIdx.x & 63;
-	for (uint32_t t0 = blockIdx.x * blockDim.x; t0 < n_tasks; t0 += gridDim.x * blockDim.x) {
-		const uint32_t task = t0 + threadIdx.x;
-		const bool in_range = task < n_tasks;
-		const uint32_t i = in_range ? task / MARCH_SEGS : 0, seg = task % MARCH_SEGS;
-		const uint32_t n = in_range ? nreq[i] : 0, b = in_range ? base[i] : 0;
-		const bool keep = n > 0 && b + n <= max_samples;
-		const bool head = in_range && seg == 0;
-		if (head) {
-			if (i == cap_rays - 1) st->numsteps_counter = b + n;
-			numsteps[2 * i] = keep ? n : 0;
-			numsteps[2 * i + 1] = b;
-		}
-		// kept-sample extent and kept-ray count: one atomic per wave (same-address atomics from
-		// every kept ray serialise at the L2)
-		uint32_t kmax = head && keep ? b + n : 0u, kcnt = head && keep ? 1u : 0u;
-		if (__ballot(kcnt != 0)) {
+__device__ __forceinline__ void load_march_ray(const float* __restrict__ rays, uint32_t i, MarchRay& mr) {
+	const float* rr = rays + 6 * (size_t)i;
+	const float du[3] = {rr[3], rr[4], rr[5]};
+	const float nrm = sqrtf((du[0] * du[0] + du[1] * du[1]) + du[2] * du[2]);
 #pragma unroll
-			for (int off = 32; off > 0; off >>= 1) { kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, off)); kcnt += (uint32_t)__shfl_xor((int)kcnt, off); }
-			if (lane == 0) { atomicMax(&st->n_kept, kmax); atomicAdd(&st->n_rays_with_samples, kcnt); }
-		}
-		if (!in_range || !keep || seg * MARCH_SEG >= n) continue;
-		const float* rr = rays + 6 * (size_t)i;
-		const float o[3] = {rr[0], rr[1], rr[2]};
-		const float nrm = sqrtf((rr[3] * rr[3] + rr[4] * rr[4]) + rr[5] * rr[5]);
-		float dir[3];
-#pragma unroll
-		for (int r = 0; r < 3; ++r) dir[r] = nrm > 0.f ? rr[3 + r] / nrm : rr[3 + r];
+	for (int d = 0; d < 3; ++d) { mr.o[d] = rr[d]; mr.dir[d] = nrm > 0.f ? du[d] / nrm : du[d]; mr.idir[d] = 1.0f / mr.dir[d]; }
+}
+
+// ---------------------------------------------------------------- pass 1: the march (count + t record)
+// The reference marches every ray twice inside one thread (count, then write after an atomicAdd).
+// Here the march runs once: each occupied sample's t goes to tbuf[ray][n] (NERF_STEPS floats per ray
+// slot, 1 GB at R = 2^18 of the 288 GB), and the write pass turns kept rays' t into coordinates in
+// parallel. Thread per ray slot: at R = 2^18 every ray is in flight at once (4 waves per SIMD), and
+// the loop is VALU-bound, so its body is kept branch-light (march_step).
+template <bool FAST>
+__global__ void __launch_bounds__(256) k_march(uint32_t cap_rays, DevDataset ds, const uint8_t* __restrict__ bitfield,
+                                               const uint32_t* __restrict__ lin, const float* __restrict__ rays, const float* __restrict__ tstart,
+                                               uint32_t* __restrict__ nreq, float* __restrict__ tbuf) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= cap_rays) return;
+	float t = tstart[i];
+	uint32_t n = 0;
+	if (t >= 0.f) {
 		MarchRay mr;
-#pragma unroll
-		for (int d = 0; d < 3; ++d) { mr.o[d] = o[d]; mr.dir[d] = dir[d]; mr.idir[d] = 1.0f / dir[d]; }
-		const float wd[3] = {(dir[0] + 1.0f) * 0.5f, (dir[1] + 1.0f) * 0.5f, (dir[2] + 1.0f) * 0.5f};
-		const float diag[3] = {ds.aabb_max[0] - ds.aabb_min[0], ds.aabb_max[1] - ds.aabb_min[1], ds.aabb_max[2] - ds.aabb_min[2]};
-		uint32_t j = seg * MARCH_SEG;
-		const uint32_t jend = min(n, j + MARCH_SEG);
-		float t = ckpt[(size_t)i * MARCH_SEGS + seg];
-		while (j < jend) {
+		load_march_ray(rays, i, mr);
+		float* __restrict__ tr = tbuf + (size_t)i * NERF_STEPS;
+		while (n < NERF_STEPS) {
 			float dt, pos[3];
-			const int k = lin ? march_step<true>(ds, bitfield, lin, mr, t, dt, pos) : march_step<false>(ds, bitfield, lin, mr, t, dt, pos);
+			const int k = march_step<FAST>(ds, bitfield, lin, mr, t, dt, pos);
 			if (k == 0) break;
-			if (k == 2) continue;
-			// NerfCoordinate (28 B): one 16 B + one 12 B store (4 B-aligned vector stores)
-			float* cc = coords + (size_t)(b + j) * COORD_W;
-			const f4u p4 = {(pos[0] - ds.aabb_min[0]) / diag[0], (pos[1] - ds.aabb_min[1]) / diag[1], (pos[2] - ds.aabb_min[2]) / diag[2], warp_dt(dt)};
-			*(f4u*)cc = p4;
-			*(f3u*)(cc + 4) = (f3u){wd[0], wd[1], wd[2]};
-			sample_ray[b + j] = i;
-			++j; t += dt;
+			if (k == 1) { tr[n] = t; ++n; t += dt; }
 		}
 	}
+	nreq[i] = n;
+}
+
+// ---------------------------------------------------------------- pass 2: write kept rays
+// (a) per ray slot: numsteps (n or 0, base), the requested total and the kept-sample extent / kept-ray
+//     count (one atomic pair per wave).
+__global__ void __launch_bounds__(256) k_march_numsteps(uint32_t cap_rays, StepState* __restrict__ st, const uint32_t* __restrict__ nreq,
+                                                        const uint32_t* __restrict__ base, uint32_t* __restrict__ numsteps) {
+	const uint32_t max_samples = st->max_inference;
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	const bool in_range = i < cap_rays;
+	const uint32_t n = in_range ? nreq[i] : 0, b = in_range ? base[i] : 0;
+	const bool keep = n > 0 && b + n <= max_samples;
+	if (in_range) {
+		if (i == cap_rays - 1) st->numsteps_counter = b + n;
+		numsteps[2 * i] = keep ? n : 0;
+		numsteps[2 * i + 1] = b;
+	}
+	uint32_t kmax = keep ? b + n : 0u, kcnt = keep ? 1u : 0u;
+	if (__ballot(kcnt != 0)) {
+#pragma unroll
+		for (int off = 32; off > 0; off >>= 1) { kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, off)); kcnt += (uint32_t)__shfl_xor((int)kcnt, off); }
+		if ((threadIdx.x & 63) == 0) { atomicMax(&st->n_kept, kmax); atomicAdd(&st->n_rays_with_samples, kcnt); }
+	}
+}
+
+// (b) block per WRITE_CHUNK consecutive output samples (balanced whatever the spread of samples over
+//     rays; kept rays form a prefix of the slot order since base is monotone). The block finds the
+//     ray slots overlapping its chunk by binary search over base, stages up to 256 of them (base, n,
+//     o, d) in LDS, and walks the chunk with consecutive threads on consecutive samples: ray by binary
+//     search over the staged bases, the ray's recorded t (contiguous per ray), NerfCoordinate with
+//     pos = o + t d exactly as the march computed it, warped dt, warped dir.
+constexpr uint32_t WRITE_CHUNK = 4096;
+__device__ __forceinline__ uint32_t last_le(const uint32_t* __restrict__ a, uint32_t n, uint32_t q) {  // last k < n with a[k] <= q (a[0] <= q)
+	uint32_t lo = 0, hi = n;
+	while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (a[mid] <= q) lo = mid; else hi = mid; }
+	return lo;
+}
+__global__ void __launch_bounds__(256) k_march_write(uint32_t cap_rays, const StepState* __restrict__ st, DevDataset ds,
+                                                     const float* __restrict__ rays, const float* __restrict__ tbuf,
+                                                     const uint32_t* __restrict__ nreq, const uint32_t* __restrict__ base,
+                                                     float* __restrict__ coords, uint32_t* __restrict__ sample_ray) {
+	__shared__ float s_ray[6][256];
+	__shared__ uint32_t s_b[256], s_n[256];
+	__shared__ uint32_t s_range[2];
+	const uint32_t max_samples = st->max_inference;
+	const uint32_t tid = threadIdx.x;
+	const uint32_t q0 = blockIdx.x * WRITE_CHUNK;
+	if (q0 >= max_samples) return;
+	const uint32_t q1 = min(q0 + WRITE_CHUNK, max_samples);
+	if (tid == 0) {
+		s_range[0] = last_le(base, cap_rays, q0);
+		s_range[1] = last_le(base, cap_rays, q1 - 1);
+	}
+	__syncthreads();
+	const uint32_t r_lo = s_range[0], r_hi = s_range[1];
+	const float diag[3] = {ds.aabb_max[0] - ds.aabb_min[0], ds.aabb_max[1] - ds.aabb_min[1], ds.aabb_max[2] - ds.aabb_min[2]};
+	for (uint32_t rb = r_lo; rb <= r_hi; rb += 256) {
+		const uint32_t nr = min(256u, r_hi + 1 - rb);
+		if (tid < nr) {
+			const uint32_t i = rb + tid;
+			const uint32_t n = nreq[i], b = base[i];
+			const bool keep = n > 0 && b + n <= max_samples;
+			s_b[tid] = b; s_n[tid] = keep ? n : 0u;
+			if (keep) {
+				MarchRay mr;
+				load_march_ray(rays, i, mr);
+#pragma unroll
+				for (int d = 0; d < 3; ++d) { s_ray[d][tid] = mr.o[d]; s_ray[3 + d][tid] = mr.dir[d]; }
+			}
+		}
+		__syncthreads();
+		// this batch's samples: up to the next batch's first base (or the chunk end)
+		const uint32_t qa = max(q0, s_b[0]);
+		const uint32_t qb = rb + nr > r_hi ? q1 : min(q1, base[rb + nr]);
+		for (uint32_t q = qa + tid; q < qb; q += 256) {
+			const uint32_t r = last_le(s_b, nr, q);
+			const uint32_t j = q - s_b[r];
+			if (j >= s_n[r]) continue;  // not a kept sample
+			const uint32_t i = rb + r;
+			const float t = tbuf[(size_t)i * NERF_STEPS + j];
+			const float o[3] = {s_ray[0][r], s_ray[1][r], s_ray[2][r]}, dir[3] = {s_ray[3][r], s_ray[4][r], s_ray[5][r]};
+			float pos[3];
+#pragma unroll
+			for (int d = 0; d < 3; ++d) pos[d] = o[d] + t * dir[d];
+			const float dt = ds.cone_angle == 0.0f ? MIN_CONE_STEPSIZE : calc_dt(t, ds.cone_angle);
+			// NerfCoordinate (28 B): one 16 B + one 12 B store (4 B-aligned vector stores)
+			float* cc = coords + (size_t)q * COORD_W;
+			const f4u p4 = {(pos[0] - ds.aabb_min[0]) / diag[0], (pos[1] - ds.aabb_min[1]) / diag[1], (pos[2] - ds.aabb_min[2]) / diag[2], warp_dt(dt)};
+			*(f4u*)cc = p4;
+			*(f3u*)(cc + 4) = (f3u){(dir[0] + 1.0f) * 0.5f, (dir[1] + 1.0f) * 0.5f, (dir[2] + 1.0f) * 0.5f};
+			sample_ray[q] = i;
+		}
+		__syncthreads();
+	}
+}
+
+// Development statistic: per ray, march_step calls and skip-loop additions of the march
+// (SIMT-efficiency analysis; neus_debug_march_stats).
+__global__ void k_march_stats(uint32_t n_rays, const float* __restrict__ rays, const float* __restrict__ tstart, const uint32_t* __restrict__ lin,
+                              DevDataset ds, const uint8_t* __restrict__ bf, uint32_t* __restrict__ out) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n_rays) return;
+	uint32_t outer = 0, inner = 0, n = 0;
+	float t = tstart[i];
+	if (t >= 0.f) {
+		MarchRay mr;
+		load_march_ray(rays, i, mr);
+		while (n < NERF_STEPS) {
+			float dt, pos[3];
+			const float t0 = t;
+			const int k = march_step<true>(ds, bf, lin, mr, t, dt, pos);
+			++outer;
+			if (k == 0) break;
+			if (k == 1) { ++n; t += dt; }
+			else inner += (uint32_t)((t - t0) / MIN_CONE_STEPSIZE + 0.5f);
+		}
+	}
+	out[3 * i] = outer; out[3 * i + 1] = inner; out[3 * i + 2] = n;
 }
 
 // ---------------------------------------------------------------- NeuS alpha (shared)
@@ -661,14 +731,21 @@ void launch_bitfield_linear(hipStream_t s, const uint8_t* bitfield, uint32_t* li
 	k_bitfield_linear<<<GRID3 / 32 / 256, 256, 0, s>>>(bitfield, lin);
 }
 void launch_march_count(hipStream_t s, uint32_t cap, const StepState* st, DPInfo dp, const DevDataset& ds, const uint8_t* bitfield,
-                        const uint32_t* lin, uint64_t rng_state, uint64_t rng_inc, float* rays, float* ckpt, uint32_t* nreq) {
-	k_march_count<<<ray_blocks(cap), 256, 0, s>>>(cap, st, dp, ds, bitfield, ds.cone_angle == 0.0f ? lin : nullptr, rng_state, rng_inc, rays, ckpt, nreq);
+                        const uint32_t* lin, uint64_t rng_state, uint64_t rng_inc, float* rays, float* tstart, uint32_t* nreq, float* tbuf) {
+	k_ray_gen<<<ray_blocks(cap), 256, 0, s>>>(cap, st, dp, ds, rng_state, rng_inc, rays, tstart);
+	const uint32_t blocks = (cap + 255) / 256;
+	if (ds.cone_angle == 0.0f) k_march<true><<<blocks, 256, 0, s>>>(cap, ds, bitfield, lin, rays, tstart, nreq, tbuf);
+	else k_march<false><<<blocks, 256, 0, s>>>(cap, ds, bitfield, nullptr, rays, tstart, nreq, tbuf);
 }
-void launch_march_write(hipStream_t s, uint32_t cap, StepState* st, const DevDataset& ds, const uint8_t* bitfield, const uint32_t* lin,
-                        const float* rays, const float* ckpt, const uint32_t* nreq, const uint32_t* base, uint32_t* numsteps, float* coords,
-                        uint32_t* sample_ray) {
-	const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((cap * MARCH_SEGS + 255) / 256, 16384));
-	k_march_write<<<blocks, 256, 0, s>>>(cap, st, ds, bitfield, ds.cone_angle == 0.0f ? lin : nullptr, rays, ckpt, nreq, base, numsteps, coords, sample_ray);
+void launch_march_write(hipStream_t s, uint32_t cap, StepState* st, const DevDataset& ds, const float* rays, const float* tbuf, const uint32_t* nreq,
+                        const uint32_t* base, uint32_t* numsteps, float* coords, uint32_t* sample_ray, uint32_t sample_cap) {
+	k_march_numsteps<<<(cap + 255) / 256, 256, 0, s>>>(cap, st, nreq, base, numsteps);
+	// one block per WRITE_CHUNK samples of the largest possible kept extent (max_inference <= sample_cap)
+	k_march_write<<<std::max<uint32_t>(1, (sample_cap + WRITE_CHUNK - 1) / WRITE_CHUNK), 256, 0, s>>>(cap, st, ds, rays, tbuf, nreq, base, coords, sample_ray);
+}
+void debug_launch_march_stats(hipStream_t s, uint32_t n_rays, const float* rays, const float* tstart, const uint32_t* lin, const DevDataset& ds,
+                              const uint8_t* bf, uint32_t* out) {
+	k_march_stats<<<(n_rays + 255) / 256, 256, 0, s>>>(n_rays, rays, tstart, lin, ds, bf, out);
 }
 static inline uint32_t sample_blocks(uint32_t cap) { return std::max<uint32_t>(1, std::min<uint32_t>((cap + 255) / 256, 16384)); }
 void launch_loss_alpha(hipStream_t s, uint32_t cap_samples, const StepState* st, const float* coords, const half_t* net_out, float cos_anneal,

@@ -89,7 +89,7 @@ struct NeusTestbed {
 	uint32_t density_grid_ema_step = 0;
 	// step workspace
 	uint32_t batch = 0, max_samples = 0;
-	Dev<float> rays, startt, coords, coords_c, loss, ek, mask, loss_sum;
+	Dev<float> rays, startt, tbuf_t, coords, coords_c, loss, ek, mask, loss_sum;
 	Dev<uint32_t> nreq, base, numsteps, ccount, cbase, enc;
 	Dev<float> dydx;
 	Dev<half_t> net_out, dL_dout, trainbuf;
@@ -279,7 +279,7 @@ struct NeusTestbed {
 		// workspace
 		batch = c.batch_size;
 		max_samples = batch * 16;  // testbed_nerf.cu:3725
-		rays.alloc(6 * (size_t)MAX_RAYS); startt.alloc((size_t)MAX_RAYS * MARCH_SEGS); nreq.alloc(MAX_RAYS); base.alloc(MAX_RAYS);
+		rays.alloc(6 * (size_t)MAX_RAYS); startt.alloc((size_t)MAX_RAYS); tbuf_t.alloc((size_t)MAX_RAYS * NERF_STEPS); nreq.alloc(MAX_RAYS); base.alloc(MAX_RAYS);
 		numsteps.alloc(2 * (size_t)MAX_RAYS); ccount.alloc(MAX_RAYS); cbase.alloc(MAX_RAYS);
 		l_sa.alloc(max_samples); l_ekt.alloc(max_samples); sample_ray.alloc(max_samples);
 		l_ck4.alloc(max_samples / 8 + 1); l_cke.alloc(max_samples / 8 + 1);
@@ -474,9 +474,9 @@ struct NeusTestbed {
 		HIP_CHECK(hipMemsetAsync(&st.p->n_rays_with_samples, 0, 4, s));
 		const DPInfo dp{rank, world};
 		mark(1);
-		launch_march_count(s, MAX_RAYS, st.p, dp, ds, bitfield.p, bf_lin.p, rng.state, rng.inc, rays.p, startt.p, nreq.p);
+		launch_march_count(s, MAX_RAYS, st.p, dp, ds, bitfield.p, bf_lin.p, rng.state, rng.inc, rays.p, startt.p, nreq.p, tbuf_t.p);
 		launch_exclusive_scan(s, scan_tmp.p, scan_tmp_bytes, nreq.p, base.p, MAX_RAYS);
-		launch_march_write(s, MAX_RAYS, st.p, ds, bitfield.p, bf_lin.p, rays.p, startt.p, nreq.p, base.p, numsteps.p, coords.p, sample_ray.p);
+		launch_march_write(s, MAX_RAYS, st.p, ds, rays.p, tbuf_t.p, nreq.p, base.p, numsteps.p, coords.p, sample_ray.p, max_samples);
 		mark(2);
 		launch_nerf_infer(s, lay.L, lay.W, &st.p->n_kept, 0, coords.p, gl, valid, params_h.p + lay.grid_off, mlp, net_out.p, 8192);
 		mark(3);
@@ -669,14 +669,14 @@ int neus_debug_time_kernel(NeusTestbed* tb, int kernel, int variant, int iters, 
 		hipStream_t s = t.stream;
 		const DPInfo dp{t.rank, t.world};
 		const uint32_t valid = t.valid_level_at((int)t.training_step);
-		const uint32_t* lin = variant == 1 ? nullptr : t.bf_lin.p;
+		const uint32_t* lin = t.bf_lin.p;
 		auto march = [&]() {
 			HIP_CHECK(hipMemsetAsync(&t.st.p->n_kept, 0, 4, s));
 			HIP_CHECK(hipMemsetAsync(&t.st.p->n_rays_with_samples, 0, 4, s));
-			launch_march_count(s, MAX_RAYS, t.st.p, dp, t.ds, t.bitfield.p, lin, t.rng.state, t.rng.inc, t.rays.p, t.startt.p, t.nreq.p);
+			launch_march_count(s, MAX_RAYS, t.st.p, dp, t.ds, t.bitfield.p, lin, t.rng.state, t.rng.inc, t.rays.p, t.startt.p, t.nreq.p, t.tbuf_t.p);
 			launch_exclusive_scan(s, t.scan_tmp.p, t.scan_tmp_bytes, t.nreq.p, t.base.p, MAX_RAYS);
-			launch_march_write(s, MAX_RAYS, t.st.p, t.ds, t.bitfield.p, lin, t.rays.p, t.startt.p, t.nreq.p, t.base.p, t.numsteps.p, t.coords.p,
-			                   t.sample_ray.p);
+			launch_march_write(s, MAX_RAYS, t.st.p, t.ds, t.rays.p, t.tbuf_t.p, t.nreq.p, t.base.p, t.numsteps.p, t.coords.p,
+			                   t.sample_ray.p, t.max_samples);
 		};
 		march();
 		launch_nerf_infer(s, t.lay.L, t.lay.W, &t.st.p->n_kept, 0, t.coords.p, t.gl, valid, t.params_h.p + t.lay.grid_off, t.mlp, t.net_out.p, 8192);
@@ -687,9 +687,9 @@ int neus_debug_time_kernel(NeusTestbed* tb, int kernel, int variant, int iters, 
 		HIP_CHECK(hipEventRecord(a, s));
 		for (int k = 0; k < iters; ++k) {
 			switch (kernel) {
-			case 0: launch_march_count(s, MAX_RAYS, t.st.p, dp, t.ds, t.bitfield.p, lin, t.rng.state, t.rng.inc, t.rays.p, t.startt.p, t.nreq.p); break;
-			case 1: launch_march_write(s, MAX_RAYS, t.st.p, t.ds, t.bitfield.p, lin, t.rays.p, t.startt.p, t.nreq.p, t.base.p, t.numsteps.p,
-			                           t.coords.p, t.sample_ray.p); break;
+			case 0: launch_march_count(s, MAX_RAYS, t.st.p, dp, t.ds, t.bitfield.p, lin, t.rng.state, t.rng.inc, t.rays.p, t.startt.p, t.nreq.p, t.tbuf_t.p); break;
+			case 1: launch_march_write(s, MAX_RAYS, t.st.p, t.ds, t.rays.p, t.tbuf_t.p, t.nreq.p, t.base.p, t.numsteps.p,
+			                           t.coords.p, t.sample_ray.p, t.max_samples); break;
 			case 2: debug_launch_loss_scan(s, variant, MAX_RAYS, t.numsteps.p, w, t.ccount.p); break;
 			case 3: launch_nerf_infer(s, t.lay.L, t.lay.W, &t.st.p->n_kept, 0, t.coords.p, t.gl, valid, t.params_h.p + t.lay.grid_off, t.mlp,
 			                          t.net_out.p, 8192); break;
@@ -712,6 +712,17 @@ int neus_debug_time_kernel(NeusTestbed* tb, int kernel, int variant, int iters, 
 		HIP_CHECK(hipEventElapsedTime(&ms, a, b));
 		*ms_out = ms / std::max(1, iters);
 		HIP_CHECK(hipEventDestroy(a)); HIP_CHECK(hipEventDestroy(b));
+	});
+}
+int neus_debug_march_stats(NeusTestbed* tb, uint32_t n, uint32_t* out) {
+	return guard([&] {
+		if (!tb->have_net) throw std::runtime_error("no network");
+		if (tb->ds.cone_angle != 0.0f) throw std::runtime_error("march stats: cone_angle 0 only");
+		n = std::min(n, MAX_RAYS);
+		Dev<uint32_t> o; o.alloc(3 * (size_t)n);
+		debug_launch_march_stats(tb->stream, n, tb->rays.p, tb->startt.p, tb->bf_lin.p, tb->ds, tb->bitfield.p, o.p);
+		HIP_CHECK(hipStreamSynchronize(tb->stream));
+		HIP_CHECK(hipMemcpy(out, o.p, 12 * (size_t)n, hipMemcpyDeviceToHost));
 	});
 }
 int neus_testbed_stream(NeusTestbed* tb, void** s) { return guard([&] { *s = (void*)tb->stream; }); }
@@ -793,14 +804,14 @@ int neus_sample_rays(NeusTestbed* tb, void* stream, uint32_t n_rays, uint32_t ra
 		Dev<StepState> sst; sst.alloc(1);
 		StepState h{}; h.rays_per_batch = n_rays; h.max_inference = max_samples; h.n_rays_total = n_rays_total;
 		HIP_CHECK(hipMemcpyAsync(sst.p, &h, sizeof(h), hipMemcpyHostToDevice, s));
-		Dev<float> st_t; st_t.alloc((size_t)n_rays * MARCH_SEGS); Dev<uint32_t> nr, bs; nr.alloc(n_rays); bs.alloc(n_rays);
+		Dev<float> st_t, tb_t; st_t.alloc(n_rays); tb_t.alloc((size_t)n_rays * NERF_STEPS); Dev<uint32_t> nr, bs; nr.alloc(n_rays); bs.alloc(n_rays);
 		Dev<uint8_t> tmp; const size_t tb_ = scan_temp_bytes(n_rays); tmp.alloc(tb_ + 256);
 		Dev<uint32_t> lin; lin.alloc(GRID3 / 32);
 		launch_bitfield_linear(s, bitfield, lin.p);
-		launch_march_count(s, n_rays, sst.p, DPInfo{rank, world}, tb->ds, bitfield, lin.p, rng_state, rng_inc, rays, st_t.p, nr.p);
+		launch_march_count(s, n_rays, sst.p, DPInfo{rank, world}, tb->ds, bitfield, lin.p, rng_state, rng_inc, rays, st_t.p, nr.p, tb_t.p);
 		launch_exclusive_scan(s, tmp.p, tb_, nr.p, bs.p, n_rays);
 		Dev<uint32_t> sr; sr.alloc(std::max<uint32_t>(1, max_samples));
-		launch_march_write(s, n_rays, sst.p, tb->ds, bitfield, lin.p, rays, st_t.p, nr.p, bs.p, numsteps, coords, sr.p);
+		launch_march_write(s, n_rays, sst.p, tb->ds, rays, tb_t.p, nr.p, bs.p, numsteps, coords, sr.p, max_samples);
 		HIP_CHECK(hipMemcpyAsync(&h, sst.p, sizeof(h), hipMemcpyDeviceToHost, s));
 		HIP_CHECK(hipStreamSynchronize(s));
 		counters_out[0] = h.numsteps_counter; counters_out[1] = h.n_kept; counters_out[2] = h.n_rays_with_samples;
