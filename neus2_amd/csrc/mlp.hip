@@ -126,150 +126,224 @@ __device__ __forceinline__ FwdW stage_fwd(half_t* sm, const half_t* d0, const ha
 // next free slot through one cross-half shuffle. The first layer's weight columns (and W0^T's
 // rows) are permuted on the host to this physical order (din_logical), so the product is the
 // reference's W0 . din.
+// Per-half select of two register values. Written on the bits: `h ? a[i] : a[j]` over a register
+// array is otherwise turned into a dynamically indexed array (a 16-way compare/select chain).
+__device__ __forceinline__ float hsel(int h, float v1, float v0) {
+	const uint32_t m = 0u - (uint32_t)h;
+	return __uint_as_float((__float_as_uint(v1) & m) | (__float_as_uint(v0) & ~m));
+}
+
+// Symmetric slot layout: slots 3.. hold the lane's own level features in the same order on both
+// halves (feature k of the lane's level list: level 2(k/2)+h, feature k%2), so all but the first three
+// slots need no per-half select. Slots 0..2 are xyz on h = 0; on h = 1 they take the features that do
+// not fit (the lane's own first, then h = 0's, moved over by one cross-half shuffle), then zeros.
 NEUS_HD int din_logical(int L, int h, int q) {
-	const int DIN = ((3 + 2 * L) + 15) / 16 * 16, HALF = DIN / 2;
+	const int DIN = ((3 + 2 * L) + 15) / 16 * 16, HALF = DIN / 2, FS = HALF - 3;
 	const int M0 = (L + 1) / 2, M1 = L / 2;
-	const int NT = (3 + 2 * M0 > HALF) ? 3 + 2 * M0 - HALF : 0;
+	const int OV0 = 2 * M0 > FS ? 2 * M0 - FS : 0, OV1 = 2 * M1 > FS ? 2 * M1 - FS : 0;
 	if (q >= HALF) return -1;
-	if (h == 0) {
-		if (q < 3) return q;
-		const int k = q - 3;
-		if (k < 2 * M0 - NT) return 3 + 2 * (2 * (k / 2)) + (k % 2);
-		return -1;
+	if (q >= 3) {
+		const int k = q - 3, M = h ? M1 : M0;
+		if (k >= 2 * M || k >= FS) return -1;
+		return 3 + 2 * (2 * (k / 2) + h) + (k % 2);
 	}
-	if (q < 2 * M1) return 3 + 2 * (2 * (q / 2) + 1) + (q % 2);
-	if (NT == 1 && q == 2 * M1) return 3 + 2 * (2 * (M0 - 1)) + 1;
+	if (h == 0) return q;
+	if (q < OV1) { const int k = FS + q; return 3 + 2 * (2 * (k / 2) + 1) + (k % 2); }
+	if (q < OV1 + OV0) { const int k = FS + q - OV1; return 3 + 2 * (2 * (k / 2)) + (k % 2); }
 	return -1;
 }
 NEUS_HD int din_physical_row(int h, int q) { return 16 * (q >> 3) + 8 * ((q & 7) >> 2) + 4 * h + (q & 3); }
 
 template <int L> struct Fused {
-	static constexpr int DIN = Dims<L>::DIN, HALF = DIN / 2;
+	static constexpr int DIN = Dims<L>::DIN, HALF = DIN / 2, FS = HALF - 3;
 	static constexpr int M0 = (L + 1) / 2, M1 = L / 2;
-	static constexpr int NT = (3 + 2 * M0 > HALF) ? 3 + 2 * M0 - HALF : 0;
-	static_assert(NT <= 1 && 2 * M1 + NT <= HALF && 3 + 2 * M0 - NT <= HALF, "din slot layout");
+	static constexpr int OV0 = 2 * M0 > FS ? 2 * M0 - FS : 0, OV1 = 2 * M1 > FS ? 2 * M1 - FS : 0;
+	static_assert(OV0 + OV1 <= 3, "din slot layout");
 };
 
 // Evaluates this lane's levels for position x: features ev[m] (level 2m+h) and, if DYDX, dy/dx.
-// Same arithmetic as grid_common.h (bit-identical features / dy/dx), restructured for issue count:
-// level parameters are selected per lane half without branches, corner indices share their
-// per-axis terms (dense levels: x + y res + z res^2; hashed levels: the xor hash masked by the
-// power-of-two table size, which is the reference's `% hashmap_size` there), and the corner
-// weights reuse the axis products in the reference's multiplication order.
+// Same arithmetic as grid_common.h (bit-identical features / dy/dx), restructured for issue count and
+// latency:
+//  * level parameters are selected per lane half without branches; inactive levels (beyond
+//    valid_level, or the missing odd level) are computed on valid addresses and zeroed by select;
+//  * corner indices share their per-axis terms (dense: x + y res + z res^2, wrapped as the reference's
+//    `% hashmap_size`; hashed: the xor hash masked by the power-of-two table size) and are formed as
+//    32-bit entry offsets from the uniform table base (scalar-base loads, no 64-bit address math);
+//  * software-pipelined: level m+1's 8 gathers are in flight while level m is interpolated;
+//  * both features go through packed fp32 (v_pk_mul/v_pk_fma) and packed fp16 adds; the fp16 feature
+//    accumulation result[f] += (half)(w * v) and the fmaf dy/dx terms are unchanged.
+typedef float f2v __attribute__((ext_vector_type(2)));
+struct LevelAddr { uint32_t e[8]; float f[3]; float sc; bool act; };
+// Per-level constants {scale bits, res, table offset, table size}, staged in LDS once per block and
+// read per lane by level index (a per-lane select between two levels' kernel-argument values would
+// need every constant materialised in VGPRs for the whole kernel).
+struct LevelSmem { uint4 p[16]; };
+__device__ __forceinline__ void stage_levels(LevelSmem& sl, const GridLevels& gl, uint32_t L) {
+	for (uint32_t t = threadIdx.x; t < L; t += blockDim.x)
+		sl.p[t] = make_uint4(__float_as_uint(gl.scale[t]), gl.res[t], gl.offset[t], gl.offset[t + 1] - gl.offset[t]);
+}
+template <int L>
+__device__ __forceinline__ void level_addr(const LevelSmem& sl, uint32_t dense_bits, uint32_t valid_level, const float x[3], int h, int m, LevelAddr& A) {
+	const int l0 = 2 * m, l1 = 2 * m + 1 < L ? 2 * m + 1 : 2 * m;
+	// opaque lane half: keeps the level-constant reads inside the loop body
+	h = h | (int)opaque_zero();
+	const uint32_t l = h ? (uint32_t)l1 : (uint32_t)l0;
+	A.act = (h ? (2 * m + 1 < L) : true) && l <= valid_level;
+	const uint4 P = sl.p[l];
+	A.sc = __uint_as_float(P.x);
+	const uint32_t res = P.y, o0 = P.z, hs = P.w;
+	const bool dense = (dense_bits >> l) & 1u;
+	uint32_t gp[3];
+#pragma unroll
+	for (int d = 0; d < 3; ++d) {
+		// pos_fract (common_device.h:404-434): one FFMA as nvcc emits `input * scale + 0.5f`
+		const float p = __builtin_fmaf(x[d], A.sc, 0.5f);
+		const float fl = floorf(p);
+		gp[d] = (uint32_t)(int)fl;
+		A.f[d] = p - fl;
+	}
+	// both index forms computed, merged by mask (a select here is turned into divergent branches)
+	const uint32_t dm = 0u - (uint32_t)dense;
+	uint32_t yz[4];
+#pragma unroll
+	for (int k = 0; k < 4; ++k) {
+		const uint32_t yy = gp[1] + (k & 1), zz = gp[2] + (k >> 1);
+		yz[k] = ((yy * res + zz * (res * res)) & dm) | (((yy * 2654435761u) ^ (zz * 805459861u)) & ~dm);
+	}
+#pragma unroll
+	for (int c = 0; c < 8; ++c) {
+		const uint32_t xx = gp[0] + (c & 1), k = c >> 1;
+		const uint32_t ed = xx + yz[k];
+		const uint32_t ew = min(ed, ed - hs);  // ed < 2 hs: the reference's % hashmap_size
+		A.e[c] = o0 + ((ew & dm) | ((xx ^ yz[k]) & (hs - 1u) & ~dm));
+	}
+}
+__device__ __forceinline__ void level_gather(const half_t* __restrict__ grid, const LevelAddr& A, uint32_t v[8]) {
+	const char* base = (const char*)grid;
+#pragma unroll
+	for (int c = 0; c < 8; ++c) v[c] = *(const uint32_t*)(base + (A.e[c] << 2));
+}
+__device__ __forceinline__ f2v h2f(uint32_t u) {
+	h2 hv = __builtin_bit_cast(h2, u);
+	return (f2v){(float)hv[0], (float)hv[1]};
+}
+template <bool DYDX>
+__device__ __forceinline__ void level_interp(const LevelAddr& A, const uint32_t v[8], h2& ev, float dy[2][3]) {
+	const float wx[2] = {1.f - A.f[0], A.f[0]}, wy[2] = {1.f - A.f[1], A.f[1]}, wz[2] = {1.f - A.f[2], A.f[2]};
+	f2v vf[8];
+#pragma unroll
+	for (int c = 0; c < 8; ++c) vf[c] = h2f(v[c]);
+	// weights ((1 * wx) * wy) * wz, as the reference's loop
+	h2 r = (h2){(half_t)0.f, (half_t)0.f};
+#pragma unroll
+	for (int c = 0; c < 8; ++c) {
+		const float w = (wx[c & 1] * wy[(c >> 1) & 1]) * wz[c >> 2];
+		const f2v t = (f2v){w, w} * vf[c];
+		r = r + (h2){(half_t)t[0], (half_t)t[1]};
+	}
+	ev = A.act ? r : (h2){(half_t)0.f, (half_t)0.f};
+	if (DYDX) {
+		// weight = (scale * w_a) * w_b over the two non-gradient dims in increasing order
+		const float sx[2] = {A.sc * wx[0], A.sc * wx[1]}, sy[2] = {A.sc * wy[0], A.sc * wy[1]};
+		f2v g[3] = {(f2v){0.f, 0.f}, (f2v){0.f, 0.f}, (f2v){0.f, 0.f}};
+#pragma unroll
+		for (int gd = 0; gd < 3; ++gd)
+#pragma unroll
+			for (int idx = 0; idx < 4; ++idx) {
+				const int b0 = idx & 1, b1 = (idx >> 1) & 1;
+				float w;
+				uint32_t cl;
+				if (gd == 0) { w = sy[b0] * wz[b1]; cl = (b0 << 1) | (b1 << 2); }
+				else if (gd == 1) { w = sx[b0] * wz[b1]; cl = b0 | (b1 << 2); }
+				else { w = sx[b0] * wy[b1]; cl = b0 | (b1 << 1); }
+				const uint32_t cr = cl | (1u << gd);
+				g[gd] = __builtin_elementwise_fma((f2v){w, w}, vf[cr] - vf[cl], g[gd]);
+			}
+#pragma unroll
+		for (int q = 0; q < 2; ++q)
+#pragma unroll
+			for (int d = 0; d < 3; ++d) {
+				dy[q][d] = A.act ? g[d][q] : 0.f;
+				// materialise here: sunk to its use in the MLP, the dy/dx arithmetic would keep all
+				// levels' corner values live instead of 6 floats per level
+				asm volatile("" : "+v"(dy[q][d]));
+			}
+	}
+}
 template <int L, bool DYDX>
-__device__ __forceinline__ void fused_levels(const GridLevels& gl, uint32_t valid_level, const half_t* __restrict__ grid,
+__device__ __forceinline__ void fused_levels(const LevelSmem& sl, uint32_t dense_bits, uint32_t valid_level, const half_t* __restrict__ grid,
                                              const float x[3], int h, h2 ev[], float dy[][2][3]) {
 	constexpr int M0 = Fused<L>::M0;
+	LevelAddr A[2];
+	uint32_t v[2][8];
+	level_addr<L>(sl, dense_bits, valid_level, x, h, 0, A[0]);
+	level_gather(grid, A[0], v[0]);
 #pragma unroll
 	for (int m = 0; m < M0; ++m) {
-		const int l0 = 2 * m, l1 = 2 * m + 1 < L ? 2 * m + 1 : 2 * m;
-		const uint32_t l = h ? (uint32_t)l1 : (uint32_t)l0;
-		const bool act = (h ? (2 * m + 1 < L) : true) && l <= valid_level;
-		ev[m] = (h2){(half_t)0.f, (half_t)0.f};
-		if (DYDX) {
-#pragma unroll
-			for (int f = 0; f < 2; ++f)
-#pragma unroll
-				for (int d = 0; d < 3; ++d) dy[m][f][d] = 0.f;
+		const int cur = m & 1, nxt = cur ^ 1;
+		if (m + 1 < M0) {
+			level_addr<L>(sl, dense_bits, valid_level, x, h, m + 1, A[nxt]);
+			level_gather(grid, A[nxt], v[nxt]);
 		}
-		// per-level branch (uniform once every level is active): the block boundary also keeps one
-		// level's gathers in flight at a time, which bounds VGPR pressure
-		if (!act) continue;
-		const float sc = h ? gl.scale[l1] : gl.scale[l0];
-		const uint32_t res = h ? gl.res[l1] : gl.res[l0];
-		const uint32_t o0 = h ? gl.offset[l1] : gl.offset[l0], o1 = h ? gl.offset[l1 + 1] : gl.offset[l0 + 1];
-		const bool dense = (gl.dense_bits >> l) & 1u;
-		const uint32_t hmask = (o1 - o0) - 1u;
-		// pos_fract (common_device.h:404-434)
-		float f[3]; uint32_t gp[3];
-		const float xin[3] = {x[0], x[1], x[2]};
-#pragma unroll
-		for (int d = 0; d < 3; ++d) {
-			const float p = __builtin_fmaf(xin[d], sc, 0.5f);
-			const float fl = floorf(p);
-			gp[d] = (uint32_t)(int)fl;
-			f[d] = p - fl;
-		}
-		// corner indices (grid.h:118-153)
-		uint32_t yz[4];
-#pragma unroll
-		for (int k = 0; k < 4; ++k) {
-			const uint32_t yy = gp[1] + (k & 1), zz = gp[2] + (k >> 1);
-			const uint32_t dn = yy * res + zz * (res * res);
-			const uint32_t hs = (yy * 2654435761u) ^ (zz * 805459861u);
-			yz[k] = dense ? dn : hs;
-		}
-		const half_t* gbase = grid + (size_t)o0 * 2;
-		h2 v[8];
-#pragma unroll
-		for (int c = 0; c < 8; ++c) {
-			const uint32_t xx = gp[0] + (c & 1);
-			const uint32_t k = c >> 1;
-			// dense corners past the last cell wrap as the reference's `% hashmap_size` (index < 2 size)
-			const uint32_t ed = xx + yz[k], eh = (xx ^ yz[k]) & hmask;
-			const uint32_t e = dense ? (ed >= o1 - o0 ? ed - (o1 - o0) : ed) : eh;
-			v[c] = *(const h2*)(gbase + 2 * (size_t)e);
-		}
-		// weights: ((1 * wx) * wy) * wz, as the reference's loop
-		const float wx[2] = {1.f - f[0], f[0]}, wy[2] = {1.f - f[1], f[1]}, wz[2] = {1.f - f[2], f[2]};
-		half_t r0 = (half_t)0.f, r1 = (half_t)0.f;
-#pragma unroll
-		for (int c = 0; c < 8; ++c) {
-			const float w = (wx[c & 1] * wy[(c >> 1) & 1]) * wz[c >> 2];
-			r0 = (half_t)((float)r0 + (float)(half_t)(w * (float)v[c][0]));
-			r1 = (half_t)((float)r1 + (float)(half_t)(w * (float)v[c][1]));
-		}
-		ev[m] = (h2){r0, r1};
-		if (DYDX) {
-			// weight = ((scale * w_a) * w_b) over the two non-gradient dims in increasing order
-			const float sx[2] = {sc * wx[0], sc * wx[1]}, sy[2] = {sc * wy[0], sc * wy[1]};
-			float g[2][3];
-#pragma unroll
-			for (int q = 0; q < 2; ++q)
-#pragma unroll
-				for (int d = 0; d < 3; ++d) g[q][d] = 0.f;
-#pragma unroll
-			for (int gd = 0; gd < 3; ++gd)
-#pragma unroll
-				for (int idx = 0; idx < 4; ++idx) {
-					const int b0 = idx & 1, b1 = (idx >> 1) & 1;
-					float w;
-					uint32_t cl;
-					if (gd == 0) { w = sy[b0] * wz[b1]; cl = (b0 << 1) | (b1 << 2); }
-					else if (gd == 1) { w = sx[b0] * wz[b1]; cl = b0 | (b1 << 2); }
-					else { w = sx[b0] * wy[b1]; cl = b0 | (b1 << 1); }
-					const uint32_t cr = cl | (1u << gd);
-					g[0][gd] = __builtin_fmaf(w, (float)v[cr][0] - (float)v[cl][0], g[0][gd]);
-					g[1][gd] = __builtin_fmaf(w, (float)v[cr][1] - (float)v[cl][1], g[1][gd]);
-				}
-#pragma unroll
-			for (int q = 0; q < 2; ++q)
-#pragma unroll
-				for (int d = 0; d < 3; ++d) dy[m][q][d] = g[q][d];
-		}
+		float dtmp[2][3];
+		level_interp<DYDX>(A[cur], v[cur], ev[m], DYDX ? dy[m] : dtmp);
 	}
 }
 
-// Value of slot q on this lane: h ? (h=1 mapping) : (h=0 mapping), all indices compile-time.
+// Overflow features (see din_logical): ov[j] on h = 1 is slot j (< 3): its own features k >= FS
+// first, then those of h = 0 (received by a cross-half shuffle).
 template <int L>
-__device__ __forceinline__ float slot_value(int q, int h, const float xm[3], const h2 ev[], float tv) {
-	constexpr int M0 = Fused<L>::M0, M1 = Fused<L>::M1, NT = Fused<L>::NT;
-	float v0 = 0.f, v1 = 0.f;
-	if (q < 3) v0 = xm[q];
-	else if (q - 3 < 2 * M0 - NT) v0 = (float)ev[(q - 3) / 2][(q - 3) % 2];
-	if (q < 2 * M1) v1 = (float)ev[q / 2][q % 2];
-	else if (NT == 1 && q == 2 * M1) v1 = tv;
-	return h ? v1 : v0;
+__device__ __forceinline__ void overflow_values(int h, const h2 ev[], float ov[3]) {
+	using F = Fused<L>;
+#pragma unroll
+	for (int j = 0; j < 3; ++j) ov[j] = 0.f;
+#pragma unroll
+	for (int j = 0; j < F::OV1; ++j) { const int k = F::FS + j; ov[j] = (float)ev[k / 2][k % 2]; }
+#pragma unroll
+	for (int j = 0; j < F::OV0; ++j) {
+		const int k = F::FS + j;
+		ov[F::OV1 + j] = __shfl_xor((float)ev[k / 2][k % 2], 32);
+	}
+}
+template <int L>
+__device__ __forceinline__ void overflow_dydx(const float dy[][2][3], float ovd[3][3]) {
+	using F = Fused<L>;
+#pragma unroll
+	for (int j = 0; j < 3; ++j)
+#pragma unroll
+		for (int d = 0; d < 3; ++d) ovd[j][d] = 0.f;
+#pragma unroll
+	for (int j = 0; j < F::OV1; ++j) { const int k = F::FS + j;
+#pragma unroll
+		for (int d = 0; d < 3; ++d) ovd[j][d] = dy[k / 2][k % 2][d]; }
+#pragma unroll
+	for (int j = 0; j < F::OV0; ++j) { const int k = F::FS + j;
+#pragma unroll
+		for (int d = 0; d < 3; ++d) ovd[F::OV1 + j][d] = __shfl_xor(dy[k / 2][k % 2][d], 32); }
+}
+// Value of slot q on this lane (indices compile-time; a per-half select only where the halves differ)
+template <int L>
+__device__ __forceinline__ float slot_value(int q, int h, const float xm[3], const h2 ev[], const float ov[3]) {
+	using F = Fused<L>;
+	if (q < 3) return h ? ov[q] : xm[q];
+	const int k = q - 3;
+	if (k >= F::FS) return 0.f;
+	const bool in0 = k < 2 * F::M0, in1 = k < 2 * F::M1;
+	const float v = in0 ? (float)ev[k / 2][k % 2] : 0.f;
+	if (in0 == in1) return v;
+	return h ? 0.f : v;
 }
 // d(slot q)/dx_d on this lane (0 for pads; the xyz slots are the identity, handled by the caller)
 template <int L>
-__device__ __forceinline__ float slot_dydx(int q, int h, int d, const float dy[][2][3], const float tdy[3]) {
-	constexpr int M0 = Fused<L>::M0, M1 = Fused<L>::M1, NT = Fused<L>::NT;
-	float v0 = 0.f, v1 = 0.f;
-	if (q >= 3 && q - 3 < 2 * M0 - NT) v0 = dy[(q - 3) / 2][(q - 3) % 2][d];
-	if (q < 2 * M1) v1 = dy[q / 2][q % 2][d];
-	else if (NT == 1 && q == 2 * M1) v1 = tdy[d];
-	return h ? v1 : v0;
+__device__ __forceinline__ float slot_dydx(int q, int h, int d, const float dy[][2][3], const float ovd[3][3]) {
+	using F = Fused<L>;
+	if (q < 3) return h ? ovd[q][d] : 0.f;
+	const int k = q - 3;
+	if (k >= F::FS) return 0.f;
+	const bool in0 = k < 2 * F::M0, in1 = k < 2 * F::M1;
+	const float v = in0 ? dy[k / 2][k % 2][d] : 0.f;
+	if (in0 == in1) return v;
+	return h ? 0.f : v;
 }
 
 // fp16 B fragment (k-step s) of an accumulator tile, optionally through ReLU: (half)max(acc, 0) is the
@@ -313,14 +387,14 @@ __device__ __forceinline__ f16v rgb_forward(const FwdW& w, const f16v& D1, const
 	{
 		float sh[16]; sh16(wd, sh);
 #pragma unroll
-		for (int j = 0; j < 8; ++j) rinB[1][j] = (half_t)(h ? sh[pi_row(j, 1)] : sh[pi_row(j, 0)]);
+		for (int j = 0; j < 8; ++j) rinB[1][j] = (half_t)hsel(h, sh[pi_row(j, 1)], sh[pi_row(j, 0)]);
 		float r32[16];
 #pragma unroll
 		for (int k = 0; k < 16; ++k) r32[k] = 0.f;
 		r32[0] = x[0]; r32[1] = x[1]; r32[2] = x[2];
 		r32[3] = grad[0]; r32[4] = grad[1]; r32[5] = grad[2];
 #pragma unroll
-		for (int j = 0; j < 8; ++j) rinB[2][j] = (half_t)(h ? r32[pi_row(j, 1)] : r32[pi_row(j, 0)]);
+		for (int j = 0; j < 8; ++j) rinB[2][j] = (half_t)hsel(h, r32[pi_row(j, 1)], r32[pi_row(j, 0)]);
 	}
 #pragma unroll
 	for (int mt = 0; mt < MT; ++mt) {
@@ -351,14 +425,14 @@ __device__ __forceinline__ void rgb_hidden(const FwdW& w, const f16v& D1, const 
 	{
 		float sh[16]; sh16(wd, sh);
 #pragma unroll
-		for (int j = 0; j < 8; ++j) rinB[1][j] = (half_t)(h ? sh[pi_row(j, 1)] : sh[pi_row(j, 0)]);
+		for (int j = 0; j < 8; ++j) rinB[1][j] = (half_t)hsel(h, sh[pi_row(j, 1)], sh[pi_row(j, 0)]);
 		float r32[16];
 #pragma unroll
 		for (int k = 0; k < 16; ++k) r32[k] = 0.f;
 		r32[0] = x[0]; r32[1] = x[1]; r32[2] = x[2];
 		r32[3] = grad[0]; r32[4] = grad[1]; r32[5] = grad[2];
 #pragma unroll
-		for (int j = 0; j < 8; ++j) rinB[2][j] = (half_t)(h ? r32[pi_row(j, 1)] : r32[pi_row(j, 0)]);
+		for (int j = 0; j < 8; ++j) rinB[2][j] = (half_t)hsel(h, r32[pi_row(j, 1)], r32[pi_row(j, 0)]);
 	}
 #pragma unroll
 	for (int mt = 0; mt < MT; ++mt) {
@@ -420,13 +494,15 @@ __device__ __forceinline__ void density_forward(const FwdW& w, const h8* dinB, i
 // grid-strided.
 // ------------------------------------------------------------------------------------------
 template <int L, int W>
-__global__ void __launch_bounds__(256) k_nerf_infer(const uint32_t* __restrict__ n_ptr, uint32_t n_fixed, const float* __restrict__ coords,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) k_nerf_infer(const uint32_t* __restrict__ n_ptr, uint32_t n_fixed, const float* __restrict__ coords,
                                                     const GridLevels gl, uint32_t valid_level, const half_t* __restrict__ grid,
                                                     MlpPtrs wp, half_t* __restrict__ out) {
-	constexpr int DKS = Dims<L>::DKS, DMT = Dims<L>::DMT, HALF = Fused<L>::HALF, M0 = Fused<L>::M0, NT = Fused<L>::NT;
+	constexpr int DKS = Dims<L>::DKS, DMT = Dims<L>::DMT, HALF = Fused<L>::HALF, M0 = Fused<L>::M0;
 	constexpr int MT = (W + 31) / 32, HKS = W / 16;
 	__shared__ half_t sm[FwdSmem<L, W>::END];
+	__shared__ LevelSmem s_lvl;
 	const FwdW w0 = stage_fwd<L, W>(sm, wp.d0p, wp.d0Tp, wp);
+	stage_levels(s_lvl, gl, L);
 	__syncthreads();
 	const uint32_t n = n_ptr ? *n_ptr : n_fixed;
 	const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
@@ -444,19 +520,17 @@ __global__ void __launch_bounds__(256) k_nerf_infer(const uint32_t* __restrict__
 		// ---- encode this lane's levels
 		h2 ev[M0];
 		float dy[M0][2][3];
-		fused_levels<L, true>(gl, valid_level, grid, x, h, ev, dy);
-		float tv = 0.f, tdy[3] = {0.f, 0.f, 0.f};
-		if (NT == 1) {
-			tv = __shfl_xor((float)ev[M0 - 1][1], 32);
-#pragma unroll
-			for (int d = 0; d < 3; ++d) tdy[d] = __shfl_xor(dy[M0 - 1][1][d], 32);
-		}
+		fused_levels<L, true>(s_lvl, gl.dense_bits, valid_level, grid, x, h, ev, dy);
+		__builtin_amdgcn_sched_barrier(0);  // keep the MLP's LDS weight reads out of the encode region
+		float ov[3], ovd[3][3];
+		overflow_values<L>(h, ev, ov);
+		overflow_dydx<L>(dy, ovd);
 		const float xm[3] = {rh(rh(x[0]) - 0.5f), rh(rh(x[1]) - 0.5f), rh(rh(x[2]) - 0.5f)};
 		h8 dinB[DKS];
 #pragma unroll
 		for (int ks = 0; ks < DKS; ++ks)
 #pragma unroll
-			for (int j = 0; j < 8; ++j) dinB[ks][j] = (half_t)slot_value<L>(8 * ks + j, h, xm, ev, tv);
+			for (int j = 0; j < 8; ++j) dinB[ks][j] = (half_t)slot_value<L>(8 * ks + j, h, xm, ev, ov);
 		// ---- density MLP (fragments of the fp16-stored activations)
 		h8 H0B[HKS];
 #pragma unroll
@@ -496,7 +570,7 @@ __global__ void __launch_bounds__(256) k_nerf_infer(const uint32_t* __restrict__
 #pragma unroll
 				for (int d = 0; d < 3; ++d) {
 					const float id = (q == d) ? (h ? 0.f : 1.f) : 0.f;
-					part[d] += gv * (slot_dydx<L>(q, h, d, dy, tdy) + id);
+					part[d] += gv * (slot_dydx<L>(q, h, d, dy, ovd) + id);
 				}
 			}
 		}
@@ -509,14 +583,14 @@ __global__ void __launch_bounds__(256) k_nerf_infer(const uint32_t* __restrict__
 		{
 			float sh[16]; sh16(wd, sh);
 #pragma unroll
-			for (int j = 0; j < 8; ++j) rinB[1][j] = (half_t)(h ? sh[pi_row(j, 1)] : sh[pi_row(j, 0)]);
+			for (int j = 0; j < 8; ++j) rinB[1][j] = (half_t)hsel(h, sh[pi_row(j, 1)], sh[pi_row(j, 0)]);
 			float r32[16];
 #pragma unroll
 			for (int k = 0; k < 16; ++k) r32[k] = 0.f;
 			r32[0] = x[0]; r32[1] = x[1]; r32[2] = x[2];
 			r32[3] = grad[0]; r32[4] = grad[1]; r32[5] = grad[2];
 #pragma unroll
-			for (int j = 0; j < 8; ++j) rinB[2][j] = (half_t)(h ? r32[pi_row(j, 1)] : r32[pi_row(j, 0)]);
+			for (int j = 0; j < 8; ++j) rinB[2][j] = (half_t)hsel(h, r32[pi_row(j, 1)], r32[pi_row(j, 0)]);
 		}
 		h8 H1B[HKS], H2B[HKS];
 #pragma unroll
@@ -560,9 +634,11 @@ __global__ void __launch_bounds__(256) k_nerf_infer(const uint32_t* __restrict__
 template <int L, int W>
 __global__ void __launch_bounds__(256) k_nerf_density(uint32_t n, const float* __restrict__ pos, const GridLevels gl, uint32_t valid_level,
                                                       const half_t* __restrict__ grid, MlpPtrs wp, float* __restrict__ density) {
-	constexpr int DKS = Dims<L>::DKS, M0 = Fused<L>::M0, NT = Fused<L>::NT, MT = (W + 31) / 32, HKS = W / 16;
+	constexpr int DKS = Dims<L>::DKS, M0 = Fused<L>::M0, MT = (W + 31) / 32, HKS = W / 16;
 	__shared__ half_t sm[FwdSmem<L, W>::END];
+	__shared__ LevelSmem s_lvl;
 	const FwdW w0 = stage_fwd<L, W>(sm, wp.d0p, wp.d0Tp, wp);
+	stage_levels(s_lvl, gl, L);
 	__syncthreads();
 	const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
 	const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -577,14 +653,15 @@ __global__ void __launch_bounds__(256) k_nerf_density(uint32_t n, const float* _
 		const float x[3] = {pos[3 * (size_t)ic], pos[3 * (size_t)ic + 1], pos[3 * (size_t)ic + 2]};
 		h2 ev[M0];
 		float dy[1][2][3];
-		fused_levels<L, false>(gl, valid_level, grid, x, h, ev, dy);
-		const float tv = NT == 1 ? __shfl_xor((float)ev[M0 - 1][1], 32) : 0.f;
+		fused_levels<L, false>(s_lvl, gl.dense_bits, valid_level, grid, x, h, ev, dy);
+		float ov[3];
+		overflow_values<L>(h, ev, ov);
 		const float xm[3] = {rh(rh(x[0]) - 0.5f), rh(rh(x[1]) - 0.5f), rh(rh(x[2]) - 0.5f)};
 		h8 dinB[DKS];
 #pragma unroll
 		for (int ks = 0; ks < DKS; ++ks)
 #pragma unroll
-			for (int j = 0; j < 8; ++j) dinB[ks][j] = (half_t)slot_value<L>(8 * ks + j, h, xm, ev, tv);
+			for (int j = 0; j < 8; ++j) dinB[ks][j] = (half_t)slot_value<L>(8 * ks + j, h, xm, ev, ov);
 		h8 H0B[HKS];
 #pragma unroll
 		for (int mt = 0; mt < MT; ++mt) {
@@ -638,7 +715,7 @@ __device__ __forceinline__ void build_din(h8* dinB, const float x[3], const half
 #pragma unroll
 	for (int ks = 0; ks < Dims<L>::DKS; ++ks)
 #pragma unroll
-		for (int j = 0; j < 8; ++j) dinB[ks][j] = (half_t)(h ? dv[16 * ks + pi_row(j, 1)] : dv[16 * ks + pi_row(j, 0)]);
+		for (int j = 0; j < 8; ++j) dinB[ks][j] = (half_t)hsel(h, dv[16 * ks + pi_row(j, 1)], dv[16 * ks + pi_row(j, 0)]);
 }
 
 // Full NerfNetwork forward for this lane's sample from stored encodings (r = lane & 31, h = lane >> 5).
@@ -1008,6 +1085,14 @@ void mlp_din_permutation(uint32_t L, int32_t* perm) {
 		for (int q = 0; q < DIN / 2; ++q) perm[din_physical_row(h, q)] = din_logical((int)L, h, q);
 }
 
+// blocks of `threads` that fit on the device at once (occupancy x CUs)
+static uint32_t resident_blocks(const void* kernel, int threads) {
+	int dev = 0, cus = 0, per_cu = 0;
+	if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 1u << 30;
+	if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0) != hipSuccess || per_cu <= 0) return 1u << 30;
+	return (uint32_t)(per_cu * cus);
+}
+
 bool mlp_supported(uint32_t L, uint32_t W) {
 #define X(l, w) if (L == l && W == w) return true;
 	NEUS_MLP_CONFIGS(X)
@@ -1017,7 +1102,10 @@ bool mlp_supported(uint32_t L, uint32_t W) {
 
 void launch_nerf_infer(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_ptr, uint32_t n_fixed, const float* coords, const GridLevels& gl,
                        uint32_t valid_level, const half_t* grid, const MlpPtrs& w, half_t* out, uint32_t blocks) {
-#define X(l, w_) if (L == l && W == w_) { k_nerf_infer<l, w_><<<blocks, 256, 0, s>>>(n_ptr, n_fixed, coords, gl, valid_level, grid, w, out); return; }
+	// persistent grid: at most the resident capacity (weights are staged once per block)
+#define X(l, w_) if (L == l && W == w_) { \
+		static const uint32_t cap = resident_blocks((const void*)k_nerf_infer<l, w_>, 256); \
+		k_nerf_infer<l, w_><<<std::min(blocks, cap), 256, 0, s>>>(n_ptr, n_fixed, coords, gl, valid_level, grid, w, out); return; }
 	NEUS_MLP_CONFIGS(X)
 #undef X
 }

@@ -1,13 +1,22 @@
-"""Summarise rocprofv3 counter_collection.csv files: per kernel (and grid size), mean counter value per dispatch."""
-import csv, collections, glob, sys
-for path in sys.argv[1:]:
+"""Summarise rocprofv3 counter_collection.csv files: per kernel (and grid size), mean counter value per
+dispatch. --last N keeps only each kernel's last N dispatches (the diag_one.py launches after warm-up)."""
+import argparse, csv, collections, glob
+ap = argparse.ArgumentParser()
+ap.add_argument("paths", nargs="+")
+ap.add_argument("--last", type=int, default=0)
+a = ap.parse_args()
+for path in a.paths:
     for f in glob.glob(path + "/**/*counter_collection.csv", recursive=True):
-        agg = collections.defaultdict(lambda: collections.defaultdict(float)); disp = collections.defaultdict(set)
+        rows = collections.defaultdict(list)
         for r in csv.DictReader(open(f)):
-            k = (r["Kernel_Name"].split("(")[0][:60], r["Grid_Size"])
-            agg[k][r["Counter_Name"]] += float(r["Counter_Value"]); disp[k].add(r["Dispatch_Id"])
+            rows[r["Kernel_Name"].split("(")[0][:60]].append(r)
         print(f)
-        for k, v in agg.items():
-            n = len(disp[k])
-            print(f"  {k[0]} grid={k[1]} dispatches={n}")
-            for c, x in sorted(v.items()): print(f"      {c:28s} {x / n:16.4g}")
+        for k, rs in rows.items():
+            ids = sorted({int(r["Dispatch_Id"]) for r in rs})
+            if a.last: ids = ids[-a.last:]
+            keep = set(ids)
+            agg = collections.defaultdict(float)
+            for r in rs:
+                if int(r["Dispatch_Id"]) in keep: agg[r["Counter_Name"]] += float(r["Counter_Value"])
+            print(f"  {k} dispatches={len(ids)} grid={rs[-1]['Grid_Size']}")
+            for c, x in sorted(agg.items()): print(f"      {c:32s} {x / len(ids):16.4g}")
