@@ -41,42 +41,46 @@ def parse():
     return p.parse_args()
 
 
-# Algorithmic work per unit for the single-kernel phases. HBM bytes count compulsory
-# streams only: the hash-grid table (21 MB fp16) and the fp32 grid gradient (42 MB) stay resident in the
-# 256 MB Infinity Cache, so 8-corner gathers and atomics are not HBM traffic; grid_scatter adds one
-# read-modify-write pass over the fp32 grid gradient per launch. The fused inference kernel moves only
-# 60 B/sample through HBM, so its bound is the MFMA work (dense fp16 flops of the six layers).
-COORD_B = 7 * 4          # NerfCoordinate AoS (pos, dt, dir)
-OUT_B = 16 * 2           # network output / dL/dout rows, fp16 x 16
+# Algorithmic work per unit, split over this build's kernels. L = 14,
+# F = 2, fp16 grid: a hash-grid gather is 8 corners x L x 4 B = 448 B per sample, the fused first+second
+# order grid-gradient RMW 2 x 448 = 896 B per compacted sample.
+#   unit "ray"   : 40 B (ray record + indices + pixel)                       -> march (ray gen + march)
+#   unit "pre"   : 596 B = 28 coords write (coord write pass) + 28 coords read + 448 gather + 32 output
+#                  write (fused inference: 508 B) + 60 loss reads (loss kernels)
+#   unit "train" : 1496 B = 60 compacted coords + dL/dout write (loss) + 28 coords + 448 gather (training
+#                  encode: 476 B) + 32 output + 32 dL/dout (training MLP: 64 B) + 896 grid RMW (scatter)
+# The SURVEY's figures count the gathers as HBM bytes; the 21 MB table mostly hits L2 / Infinity Cache,
+# so `traffic` (PMC) is reported next to them. MFMA flops (SURVEY: 28,672 per pre-compaction sample,
+# 92,160 per compacted sample) are reported alongside for the MLP kernels.
+GATHER_B = 8 * 14 * 4
+KERNELS = {
+    # name: (kernel id of neus_testbed_time_kernel, algorithmic bytes per unit, flops per unit)
+    "march": (0, 40, 0),
+    "march_write": (1, 28, 0),
+    "inference": (3, 28 + GATHER_B + 32, 28672),
+    "loss_alpha": (4, 60, 0),
+    "train_encode": (8, 28 + GATHER_B, 0),
+    "mlp_train": (5, 64, 92160 - 28672),
+    "grid_scatter": (7, 2 * GATHER_B, 0),
+}
 MFMA_PEAK_TFLOPS = 2500.0  # MI355X dense fp16 (MI355X_MICROARCH.md)
 
 
-def flops_per_sample(L=14, W=64):
-    din = ((3 + 2 * L) + 15) // 16 * 16
-    # density L0, L1, dSDF/d(din) through W1 row 0 and W0^T, rgb L0 (48 in), L1, L2
-    return 2 * (din * W + W * 16 + W + W * din + 48 * W + W * W + W * 16)
-
-
-def bytes_per_sample(L=14, W=64, din=32):
-    enc = 2 * 2 * L                     # fp16 features, 2 per level
-    dydx = 6 * 4 * L                    # f32 d(feature)/d(xyz)
-    soa = 2 * 2 * (W + din + 16 + W) + 2 * (W + 48 + W + W + 16 + W)   # weight-grad operands, fp16
-    return {
-        "inference": COORD_B + OUT_B,
-        "train_encode": COORD_B + enc + dydx,
-        "mlp_train": COORD_B + enc + dydx + OUT_B + soa + 2 * enc + 16,
-        "wgrad": soa,
-        "grid_scatter": COORD_B + 2 * enc + 16,
-    }
-
-
-def roofline(name, ms, npre, ntrain, grid_params, L=14):
-    """(bound, achieved, peak, unit, work per launch) of one single-kernel phase."""
-    if name == "inference":
-        fl = flops_per_sample(L) * npre
-        return "mfma", fl / (ms * 1e-3) / 1e12, MFMA_PEAK_TFLOPS, "TFLOP/s", fl
-    b = bytes_per_sample(L)[name] * ntrain + (8 * grid_params if name == "grid_scatter" else 0)
-    return "hbm", b / (ms * 1e-3) / 1e9, HBM_PEAK_GBS, "GB/s", b
+def kernel_rooflines(tb, iters=5):
+    """Per-kernel mean launch duration (hipEvents on the testbed stream around `iters` back-to-back
+    launches replayed on the final training state, neus_testbed_time_kernel) and the algorithmic HBM
+    roofline of each launch."""
+    out = {}
+    for name, (kid, bpu, fpu) in KERNELS.items():
+        ms, units = tb.time_kernel(kid, iters)
+        b = bpu * units
+        r = {"ms": round(ms, 4), "units": units, "bytes": b, "achieved": round(b / (ms * 1e-3) / 1e9, 1), "unit": "GB/s",
+             "frac": round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+        if fpu:
+            r["tflops"] = round(fpu * units / (ms * 1e-3) / 1e12, 1)
+            r["mfma_frac"] = round(r["tflops"] / MFMA_PEAK_TFLOPS, 4)
+        out[name] = r
+    return out
 
 
 def main():
@@ -126,25 +130,13 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     st = tb.stats()
-    # per-kernel timing with hipEvents recorded on the testbed's own stream (the stream every kernel of the
-    # step is launched on), over a separate profiled pass of the same workload
-    n_prof = max(4, min(32, args.steps // 4))
-    tb.set_profiling(True)
-    tb.train_steps(n_prof)
-    phases, pinfo = tb.phase_times()
-    tb.set_profiling(False)
     batch = args.batch
     samples = batch * world * args.steps
     value = samples / elapsed
-    lay = tb.layout()
-    single = ("inference", "train_encode", "mlp_train", "wgrad", "grid_scatter")
-    dom = max(single, key=lambda k: phases[k])
-    bound, achieved, peak, unit, work = roofline(dom, phases[dom], pinfo["npre"], pinfo["ntrain"], lay["n_grid_params"])
-    rl_all = {}
-    for k in single:
-        if phases[k] > 0:
-            bd, ac, pk, un, _ = roofline(k, phases[k], pinfo["npre"], pinfo["ntrain"], lay["n_grid_params"])
-            rl_all[k] = {"ms": round(phases[k], 4), "bound": bd, "achieved": round(ac, 2), "unit": un, "frac": round(ac / pk, 4)}
+    # per-kernel timing after the timed region, on its final state (hipEvents on the testbed stream)
+    kern = kernel_rooflines(tb)
+    dom = max(kern, key=lambda k: kern[k]["ms"])
+    d = kern[dom]
     out = {
         "metric": "training samples/sec (compacted NeuS2 training samples, DTU-scan24-shaped synthetic, base.json)",
         "value": value,
@@ -160,12 +152,10 @@ def main():
         "data": "synthetic (analytic sphere, 49 x 1600x1200 RGBA8 views; DTU scan24 unavailable offline)",
         "config": {"workload": "NeuS2 train step, Config S, base.json L=14 T=2^19 W=64, Nc=2^18/GPU, R=2^18/GPU fixed",
                    "global_batch": batch * world, "rays_per_gpu": args.rays, "parallelism": f"dp{world}"},
-        "roofline": {"bound": bound, "kernel": dom, "achieved": achieved, "peak": peak, "unit": unit,
-                     "frac": achieved / peak, "traffic": TRAFFIC.get(dom), "work_per_launch": work,
-                     "launch_ms": phases[dom]},
-        "kernels": rl_all,
-        "phase_ms": {k: round(v, 4) for k, v in phases.items()},
-        "npre_per_step": pinfo["npre"], "ntrain_per_step": pinfo["ntrain"],
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": d["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": d["frac"], "traffic": TRAFFIC.get(dom), "bytes_per_launch": d["bytes"], "units_per_launch": d["units"],
+                     "launch_ms": d["ms"]},
+        "kernels": kern,
         "loss": st["ray_loss"],
         "warmup_s": warm_s,
     }

@@ -57,7 +57,7 @@ EXPORTS = [
     "neus_testbed_create", "neus_testbed_destroy", "neus_testbed_set_dataset", "neus_testbed_reload_network",
     "neus_testbed_layout", "neus_testbed_train", "neus_testbed_get_stats", "neus_testbed_get_params",
     "neus_testbed_set_params", "neus_testbed_get_gradients", "neus_testbed_get_ema_params",
-    "neus_testbed_get_density_grid", "neus_testbed_set_density_grid", "neus_testbed_get_rng", "neus_testbed_ray_counts", "neus_debug_time_kernel", "neus_debug_march_stats", "neus_testbed_stream",
+    "neus_testbed_get_density_grid", "neus_testbed_set_density_grid", "neus_testbed_get_rng", "neus_testbed_ray_counts", "neus_debug_time_kernel", "neus_debug_march_stats", "neus_testbed_time_kernel", "neus_testbed_stream",
     "neus_testbed_synchronize", "neus_testbed_set_profiling", "neus_testbed_kernel_times",
     "neus_nccl_unique_id", "neus_testbed_init_data_parallel",
     "neus_grid_encode", "neus_net_forward", "neus_net_backward", "neus_sample_rays", "neus_loss_compact",

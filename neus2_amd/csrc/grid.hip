@@ -82,23 +82,79 @@ __device__ __forceinline__ bool wave_run_sum(uint32_t e, float& a0, float& a1, b
 	return ok;
 }
 
+// Slot of this lane's record in its bucket's per-block counter, with one LDS atomic per distinct
+// bucket of the wave (lanes of one bucket get consecutive slots).
+__device__ __forceinline__ uint32_t wave_bucket_slot(uint32_t* hist, uint32_t bkt, bool active) {
+	const uint32_t lane = threadIdx.x & 63;
+	uint64_t todo = __ballot(active);
+	uint32_t res = 0;
+	while (todo) {
+		const int leader = __ffsll((unsigned long long)todo) - 1;
+		const uint32_t lb = (uint32_t)__shfl((int)bkt, leader);
+		const uint64_t m = __ballot(active && bkt == lb);
+		uint32_t base = 0;
+		if ((int)lane == leader) base = atomicAdd(&hist[lb], (uint32_t)__popcll(m));
+		base = (uint32_t)__shfl((int)base, leader);
+		if (active && bkt == lb) res = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+		todo &= ~m;
+	}
+	return res;
+}
+
 // ---------------------------------------------------------------- hash-grid gradient scatter
 // Fused first-order (kernel_grid_backward, grid.h:371-500) and second-order
 // (kernel_grid_backward_input_backward_grid, grid.h:880-1007) gradient of every corner of every level.
 // The reference adds each corner with an fp16x2 global atomic at a random address; on MI355X float
 // atomics run at the memory side and a wave-instruction whose 64 lanes hit 64 random addresses runs
-// ~17x below the atomic byte rate. Here the contributions are instead binned by destination:
-//   k_scatter_bin<0>  per-block histogram of contributions over 8192-entry buckets (LDS atomics)
+// ~17x below the atomic byte rate, and float LDS atomics run at ~1/3 lane per clock per CU (integer
+// LDS atomics ~13, scripts/micro/lds_atomics.hip). So the contributions are binned by destination and
+// summed in integer fixed point:
+//   k_scatter_hist    per-block histogram of contributions over 4096-entry buckets
 //   exclusive scan    bucket-major [bucket][block] -> each block's slot range in each bucket
-//   k_scatter_bin<1>  recompute the contributions and write them to their bucket's slots
-//   k_scatter_accum   one workgroup per 64K-record chunk: accumulate in LDS (fp32), then add the
-//                     touched part of the bucket to the fp32 gradient with contiguous atomics
+//   k_scatter_bin     recompute the contributions; per wave and level, stage them in LDS, reserve one
+//                     contiguous run per bucket and write the records into their runs
+//   k_scatter_accum   one workgroup per bucket: sum its records in LDS as int64 fixed point (2^-32,
+//                     order-independent, so the gradient is bitwise deterministic) and store the
+//                     bucket's fp32 gradient (plain stores: the workgroup owns its entries)
 // Both bin passes evaluate the identical contribution sequence, so the slot counts always match.
-template <int PASS>
-__global__ void __launch_bounds__(256) k_scatter_bin(const uint32_t* __restrict__ n_ptr, uint32_t n_fixed, uint32_t ld,
-                                                     const float* __restrict__ coords, uint32_t coord_stride, const GridLevels gl,
-                                                     uint32_t valid_level, const uint32_t* __restrict__ dLdenc, const uint32_t* __restrict__ g,
-                                                     const float4* __restrict__ v4, ScatterWork w) {
+constexpr float SB_FIX_SCALE = 4294967296.0f;  // 2^32
+
+// Contribution of corner idx of level l for one sample (first + second order, both features).
+struct ScatterLevel { LevelSetup s; float dl0, dl1, g0, g1, vin[3]; uint32_t off; };
+__device__ __forceinline__ void corner_contribution(const ScatterLevel& L, uint32_t idx, uint32_t& gidx, float& a0, float& a1) {
+	// first order: w_corner; second order: sum_d (+/-) scale v_d prod_{other} w_other
+	float wc = 1.f;
+#pragma unroll
+	for (int d = 0; d < 3; ++d) wc *= (idx & (1u << d)) ? L.s.pos[d] : 1.f - L.s.pos[d];
+	float w2 = 0.f;
+#pragma unroll
+	for (int gd = 0; gd < 3; ++gd) {
+		float t = L.vin[gd];
+#pragma unroll
+		for (int d = 0; d < 3; ++d) if (d != gd) t *= (idx & (1u << d)) ? L.s.pos[d] : 1.f - L.s.pos[d];
+		w2 += (idx & (1u << gd)) ? t : -t;
+	}
+	a0 = L.dl0 * wc + L.g0 * w2;
+	a1 = L.dl1 * wc + L.g1 * w2;
+	const uint32_t gx = L.s.g[0] + (idx & 1), gy = L.s.g[1] + ((idx >> 1) & 1), gz = L.s.g[2] + ((idx >> 2) & 1);
+	gidx = L.off + grid_index(L.s.hsize, L.s.res, gx, gy, gz);
+}
+__device__ __forceinline__ ScatterLevel scatter_level(const GridLevels& gl, uint32_t l, float x, float y, float z, uint32_t ic, uint32_t ld,
+                                                      const uint32_t* __restrict__ dLdenc, const uint32_t* __restrict__ g, const float4 vv) {
+	ScatterLevel L;
+	L.s = level_setup(gl, l, x, y, z);
+	const uint32_t a = dLdenc[(size_t)l * ld + ic], b2 = g[(size_t)l * ld + ic];
+	const h2 d1 = *(const h2*)&a, g2 = *(const h2*)&b2;
+	L.dl0 = (float)d1[0]; L.dl1 = (float)d1[1]; L.g0 = (float)g2[0]; L.g1 = (float)g2[1];
+	L.vin[0] = L.s.scale * vv.x; L.vin[1] = L.s.scale * vv.y; L.vin[2] = L.s.scale * vv.z;
+	L.off = gl.offset[l];
+	return L;
+}
+
+__global__ void __launch_bounds__(256) k_scatter_hist(const uint32_t* __restrict__ n_ptr, uint32_t n_fixed, uint32_t ld,
+                                                      const float* __restrict__ coords, uint32_t coord_stride, const GridLevels gl,
+                                                      uint32_t valid_level, const uint32_t* __restrict__ dLdenc, const uint32_t* __restrict__ g,
+                                                      const float4* __restrict__ v4, ScatterWork w) {
 	__shared__ uint32_t hist[SB_MAX_BUCKETS];
 	for (uint32_t b = threadIdx.x; b < w.n_buckets; b += blockDim.x) hist[b] = 0;
 	__syncthreads();
@@ -110,83 +166,121 @@ __global__ void __launch_bounds__(256) k_scatter_bin(const uint32_t* __restrict_
 	const float x = c[0], y = c[1], z = c[2];
 	const float4 vv = v4[ic];
 	for (uint32_t l = 0; l < gl.n_levels && l <= valid_level; ++l) {
-		const LevelSetup s = level_setup(gl, l, x, y, z);
-		const uint32_t a = dLdenc[(size_t)l * ld + ic], b2 = g[(size_t)l * ld + ic];
-		const h2 d1 = *(const h2*)&a, g2 = *(const h2*)&b2;
-		const float dl0 = (float)d1[0], dl1 = (float)d1[1], g0 = (float)g2[0], g1 = (float)g2[1];
-		const float vin[3] = {s.scale * vv.x, s.scale * vv.y, s.scale * vv.z};
-		const uint32_t off = gl.offset[l];
+		const ScatterLevel L = scatter_level(gl, l, x, y, z, ic, ld, dLdenc, g, vv);
 #pragma unroll
 		for (uint32_t idx = 0; idx < 8; ++idx) {
-			// first order: w_corner; second order: sum_d (+/-) scale v_d prod_{other} w_other
-			float wc = 1.f;
-#pragma unroll
-			for (int d = 0; d < 3; ++d) wc *= (idx & (1u << d)) ? s.pos[d] : 1.f - s.pos[d];
-			float w2 = 0.f;
-#pragma unroll
-			for (int gd = 0; gd < 3; ++gd) {
-				float t = vin[gd];
-#pragma unroll
-				for (int d = 0; d < 3; ++d) if (d != gd) t *= (idx & (1u << d)) ? s.pos[d] : 1.f - s.pos[d];
-				w2 += (idx & (1u << gd)) ? t : -t;
-			}
-			float a0 = dl0 * wc + g0 * w2;
-			float a1 = dl1 * wc + g1 * w2;
-			const uint32_t gx = s.g[0] + (idx & 1), gy = s.g[1] + ((idx >> 1) & 1), gz = s.g[2] + ((idx >> 2) & 1);
-			const uint32_t gidx = off + grid_index(s.hsize, s.res, gx, gy, gz);
-			if (wave_run_sum(gidx, a0, a1, ok)) {
-				const uint32_t bkt = gidx >> SB_SHIFT;
-				if (PASS == 0) {
-					atomicAdd(&hist[bkt], 1u);
-				} else {
-					const uint32_t pos = w.offs[(size_t)bkt * w.n_blocks + blk] + atomicAdd(&hist[bkt], 1u);
-					w.rec_i[pos] = (uint16_t)(gidx & (SB_SIZE - 1));
-					w.rec_g[pos] = make_float2(a0, a1);
-				}
-			}
+			uint32_t gidx; float a0, a1;
+			corner_contribution(L, idx, gidx, a0, a1);
+			const bool emit = wave_run_sum(gidx, a0, a1, ok);
+			const uint32_t bkt = gidx >> SB_SHIFT;
+			// levels spanning a few buckets: one LDS add per (wave, bucket) instead of up to 64 on one counter
+			if (L.s.hsize <= 4 * SB_SIZE) (void)wave_bucket_slot(hist, bkt, emit);
+			else if (emit) atomicAdd(&hist[bkt], 1u);
 		}
 	}
-	if (PASS == 0) {
-		__syncthreads();
-		for (uint32_t b = threadIdx.x; b < w.n_buckets; b += blockDim.x) w.counts[(size_t)b * w.n_blocks + blk] = hist[b];
+	__syncthreads();
+	for (uint32_t b = threadIdx.x; b < w.n_buckets; b += blockDim.x) w.counts[(size_t)b * w.n_blocks + blk] = hist[b];
+}
+
+// Per wave and level: the wave's records (64 lanes x 8 corners) are staged in LDS in emission order
+// while their buckets are counted (as k_scatter_hist); each non-empty bucket then reserves its run with
+// one LDS atomic on the block's cursor for that bucket, and the staged records are written to their
+// run at a slot from a second per-bucket counter (lanes of one bucket get consecutive slots). The
+// block's cursors cover only the current level's buckets (one barrier pair per level), which keeps the
+// LDS footprint small enough for five workgroups per CU.
+constexpr int SB_WSTAGE = 64 * 8;
+__global__ void __launch_bounds__(256) k_scatter_bin(const uint32_t* __restrict__ n_ptr, uint32_t n_fixed, uint32_t ld,
+                                                     const float* __restrict__ coords, uint32_t coord_stride, const GridLevels gl,
+                                                     uint32_t valid_level, const uint32_t* __restrict__ dLdenc, const uint32_t* __restrict__ g,
+                                                     const float4* __restrict__ v4, ScatterWork w) {
+	__shared__ uint32_t cursor[SB_LEVEL_BUCKETS];                // next global slot of this block in the level's buckets
+	__shared__ uint32_t carry_b, carry_v;                        // a bucket shared with the previous level
+	__shared__ uint32_t wcnt[4][SB_LEVEL_BUCKETS], wbase[4][SB_LEVEL_BUCKETS];
+	__shared__ float2 st_g[4][SB_WSTAGE];
+	__shared__ uint32_t st_e[4][SB_WSTAGE];                       // gidx of the record, or ~0u for none
+	const uint32_t blk = blockIdx.x, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+	const uint32_t n = load_n(n_ptr, n_fixed);
+	const uint32_t i = blk * blockDim.x + threadIdx.x;
+	const bool ok = i < n;
+	const uint32_t ic = ok ? i : 0;
+	const float* c = coords + (size_t)ic * coord_stride;
+	const float x = c[0], y = c[1], z = c[2];
+	const float4 vv = v4[ic];
+	uint32_t* cnt = wcnt[wv];
+	uint32_t* bas = wbase[wv];
+	float2* sg = st_g[wv];
+	uint32_t* se = st_e[wv];
+	if (threadIdx.x == 0) { carry_b = ~0u; carry_v = 0; }
+	for (uint32_t l = 0; l < gl.n_levels && l <= valid_level; ++l) {
+		const uint32_t b_first = gl.offset[l] >> SB_SHIFT, nlb = ((gl.offset[l + 1] - 1) >> SB_SHIFT) - b_first + 1;
+		__syncthreads();  // previous level's cursors are final (carry_b / carry_v written)
+		for (uint32_t k = threadIdx.x; k < nlb; k += blockDim.x) {
+			const uint32_t b = b_first + k;
+			cursor[k] = b == carry_b ? carry_v : w.offs[(size_t)b * w.n_blocks + blk];
+		}
+		for (uint32_t k = lane; k < nlb; k += 64) cnt[k] = 0;
+		const ScatterLevel L = scatter_level(gl, l, x, y, z, ic, ld, dLdenc, g, vv);
+#pragma unroll
+		for (uint32_t idx = 0; idx < 8; ++idx) {
+			uint32_t gidx; float a0, a1;
+			corner_contribution(L, idx, gidx, a0, a1);
+			const bool emit = wave_run_sum(gidx, a0, a1, ok);
+			if (emit) atomicAdd(&cnt[(gidx >> SB_SHIFT) - b_first], 1u);
+			sg[idx * 64 + lane] = make_float2(a0, a1);
+			se[idx * 64 + lane] = emit ? gidx : ~0u;
+		}
+		__syncthreads();  // cursors loaded
+		for (uint32_t k = lane; k < nlb; k += 64) {
+			const uint32_t v = cnt[k];
+			bas[k] = v ? atomicAdd(&cursor[k], v) : 0u;
+			cnt[k] = 0;
+		}
+		for (uint32_t kk = 0; kk < 8; ++kk) {
+			const uint32_t e = se[kk * 64 + lane];
+			if (e != ~0u) {
+				const uint32_t lb = (e >> SB_SHIFT) - b_first;
+				const uint32_t gp = bas[lb] + atomicAdd(&cnt[lb], 1u);
+				w.rec_i[gp] = (uint16_t)(e & (SB_SIZE - 1));
+				w.rec_g[gp] = sg[kk * 64 + lane];
+			}
+		}
+		__syncthreads();  // all reservations of this level done
+		if (threadIdx.x == 0) { carry_b = b_first + nlb - 1; carry_v = cursor[nlb - 1]; }
 	}
 }
 
 __global__ void __launch_bounds__(256) k_scatter_accum(ScatterWork w, float* __restrict__ grads, uint32_t n_entries) {
-	__shared__ float acc[2 * SB_SIZE];
-	const size_t nb = (size_t)w.n_buckets * w.n_blocks;
-	const uint32_t total = w.offs[nb];
-	uint32_t c0 = blockIdx.x * SB_CHUNK;
-	if (c0 >= total) return;
-	const uint32_t c1 = min(total, c0 + SB_CHUNK);
-	// bucket holding record c0: the last b with start(b) <= c0, start(b) = offs[b * n_blocks]
-	uint32_t lo = 0, hi = w.n_buckets - 1;
-	while (lo < hi) {
-		const uint32_t mid = (lo + hi + 1) / 2;
-		if (w.offs[(size_t)mid * w.n_blocks] <= c0) lo = mid; else hi = mid - 1;
+	__shared__ unsigned long long acc[2 * SB_SIZE];  // feature planes, int64 fixed point (2^-32)
+	const uint32_t b = blockIdx.x;
+	for (uint32_t k = threadIdx.x; k < 2 * SB_SIZE; k += blockDim.x) acc[k] = 0ull;
+	__syncthreads();
+	const uint32_t c0 = w.offs[(size_t)b * w.n_blocks], c1 = w.offs[(size_t)(b + 1) * w.n_blocks];
+	auto fix = [](float v) {  // |v| < 2^31 (clamped) -> int64 multiple of 2^-32
+		return (unsigned long long)__float2ll_rn(fminf(fmaxf(v, -2147483520.0f), 2147483520.0f) * SB_FIX_SCALE);
+	};
+	auto add = [&](uint32_t e, float v0, float v1) {
+		atomicAdd(&acc[e], fix(v0));
+		atomicAdd(&acc[SB_SIZE + e], fix(v1));
+	};
+	// unaligned head and tail one per thread, the 8-aligned middle as groups of 8 per thread
+	const uint32_t a0 = min(c1, (c0 + 7u) & ~7u), a1 = max(a0, c1 & ~7u);
+	for (uint32_t r = c0 + threadIdx.x; r < a0; r += blockDim.x) { const float2 gv = w.rec_g[r]; add(w.rec_i[r], gv.x, gv.y); }
+	for (uint32_t r = a1 + threadIdx.x; r < c1; r += blockDim.x) { const float2 gv = w.rec_g[r]; add(w.rec_i[r], gv.x, gv.y); }
+	for (uint32_t gq = a0 / 8 + threadIdx.x; gq < a1 / 8; gq += blockDim.x) {
+		const uint4 ei = *(const uint4*)(w.rec_i + 8 * (size_t)gq);
+		const float4* gp = (const float4*)(w.rec_g + 8 * (size_t)gq);
+		const float4 v0 = gp[0], v1 = gp[1], v2 = gp[2], v3 = gp[3];
+		const uint32_t ew[4] = {ei.x, ei.y, ei.z, ei.w};
+		const float vv[16] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, v2.z, v2.w, v3.x, v3.y, v3.z, v3.w};
+#pragma unroll
+		for (int k = 0; k < 8; ++k) add((ew[k >> 1] >> (16 * (k & 1))) & 0xffffu, vv[2 * k], vv[2 * k + 1]);
 	}
-	uint32_t b = lo;
-	while (c0 < c1) {
-		const uint32_t bend = b + 1 < w.n_buckets ? min(c1, w.offs[(size_t)(b + 1) * w.n_blocks]) : c1;
-		for (uint32_t k = threadIdx.x; k < 2 * SB_SIZE; k += blockDim.x) acc[k] = 0.f;
-		__syncthreads();
-		for (uint32_t r = c0 + threadIdx.x; r < bend; r += blockDim.x) {
-			const uint32_t e = w.rec_i[r];
-			const float2 gv = w.rec_g[r];
-			atomicAdd(&acc[2 * e], gv.x);
-			atomicAdd(&acc[2 * e + 1], gv.y);
-		}
-		__syncthreads();
-		const uint32_t e0 = b << SB_SHIFT;
-		const uint32_t ne = min(SB_SIZE, n_entries - e0);
-		for (uint32_t k = threadIdx.x; k < 2 * ne; k += blockDim.x) {
-			const float vsum = acc[k];
-			if (vsum != 0.f) atomic_add_f32(grads + 2 * (size_t)e0 + k, vsum);
-		}
-		__syncthreads();
-		c0 = bend;
-		++b;
-	}
+	__syncthreads();
+	// the workgroup owns entries [b * SB_SIZE, +SB_SIZE): plain stores of the interleaved fp32 pairs
+	const uint32_t e0 = b << SB_SHIFT;
+	const uint32_t ne = min(SB_SIZE, n_entries - e0);
+	for (uint32_t k = threadIdx.x; k < 2 * ne; k += blockDim.x)
+		grads[2 * (size_t)e0 + k] = (float)((double)(long long)acc[(k & 1) * SB_SIZE + (k >> 1)] * (1.0 / 4294967296.0));
 }
 
 // ---------------------------------------------------------------- host launchers
@@ -196,19 +290,24 @@ void launch_grid_encode(hipStream_t s, const uint32_t* n_ptr, uint32_t n_fixed, 
 	k_grid_encode<<<dim3(grid_x, gl.n_levels), 256, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, grid, enc, dydx);
 }
 size_t scatter_records_capacity(uint32_t n_cap, uint32_t n_levels) { return (size_t)n_cap * n_levels * 8; }
-uint32_t scatter_n_buckets(const GridLevels& gl) { return (gl.offset[gl.n_levels] + SB_SIZE - 1) >> SB_SHIFT; }
+uint32_t scatter_n_buckets(const GridLevels& gl) {
+	for (uint32_t l = 0; l < gl.n_levels; ++l)
+		if (((gl.offset[l + 1] - 1) >> SB_SHIFT) - (gl.offset[l] >> SB_SHIFT) + 1 > SB_LEVEL_BUCKETS)
+			throw std::runtime_error("hash-grid level table too large for the scatter's per-level buckets");
+	return (gl.offset[gl.n_levels] + SB_SIZE - 1) >> SB_SHIFT;
+}
 void launch_grid_scatter(hipStream_t s, const uint32_t* n_ptr, uint32_t n_fixed, uint32_t ld, const float* coords, uint32_t coord_stride,
                          const GridLevels& gl, uint32_t valid_level, const half_t* dLdenc, const half_t* g, const float4* v, float* grads,
                          const ScatterWork& w, void* scan_tmp, size_t scan_tmp_bytes) {
 	// the grid always spans the workspace's sample capacity (w.n_blocks x 256 >= n, checked by the host)
-	const uint32_t nblk = w.n_blocks, n_cap = nblk * 256;
+	const uint32_t nblk = w.n_blocks;
 	const size_t nb = (size_t)w.n_buckets * w.n_blocks;
-	k_scatter_bin<0><<<nblk, 256, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, (const uint32_t*)dLdenc, (const uint32_t*)g, v, w);
+	k_scatter_hist<<<nblk, 256, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, (const uint32_t*)dLdenc, (const uint32_t*)g, v, w);
 	(void)hipMemsetAsync(w.counts + nb, 0, 4, s);
 	launch_exclusive_scan(s, scan_tmp, scan_tmp_bytes, w.counts, w.offs, (uint32_t)nb + 1);
-	k_scatter_bin<1><<<nblk, 256, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, (const uint32_t*)dLdenc, (const uint32_t*)g, v, w);
-	const uint32_t n_chunks = (uint32_t)((scatter_records_capacity(n_cap, gl.n_levels) + SB_CHUNK - 1) / SB_CHUNK);
-	k_scatter_accum<<<n_chunks, 256, 0, s>>>(w, grads, gl.offset[gl.n_levels]);
+	k_scatter_bin<<<nblk, 256, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, (const uint32_t*)dLdenc, (const uint32_t*)g, v, w);
+	// every bucket (also one without records: its entries' gradient is zero) is written by its workgroup
+	k_scatter_accum<<<w.n_buckets, 256, 0, s>>>(w, grads, gl.offset[gl.n_levels]);
 }
 
 } // namespace neus

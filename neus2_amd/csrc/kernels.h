@@ -53,9 +53,9 @@ struct LossParams {
 };
 
 // binned hash-grid gradient scatter (grid.hip)
-constexpr uint32_t SB_SHIFT = 13, SB_SIZE = 1u << SB_SHIFT;   // bucket = 8192 grid entries (64 KB of fp32 pairs in LDS)
-constexpr uint32_t SB_MAX_BUCKETS = 1024;                      // 16 levels x 2^19 entries
-constexpr uint32_t SB_CHUNK = 1u << 16;                        // records per accumulating workgroup
+constexpr uint32_t SB_SHIFT = 12, SB_SIZE = 1u << SB_SHIFT;   // bucket = 4096 grid entries (64 KB of int64 pairs in LDS)
+constexpr uint32_t SB_MAX_BUCKETS = 4096;                      // 16 levels x 2^19 entries / 4096 + level boundaries
+constexpr uint32_t SB_LEVEL_BUCKETS = (1u << 19) / SB_SIZE + 2; // buckets one level can touch (2^19-entry tables)
 struct ScatterWork {
 	uint32_t* counts;   // [n_buckets * n_blocks + 1] contributions per (bucket, block), bucket-major
 	uint32_t* offs;     // exclusive scan of counts

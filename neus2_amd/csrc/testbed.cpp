@@ -123,7 +123,14 @@ struct NeusTestbed {
 	// profiling
 	bool profiling = false;
 	static constexpr int N_PHASES = NEUS_N_PHASES;
-	hipEvent_t ev[N_PHASES + 1] = {};
+	// Two sets of phase events (steps alternate), so reading one step's timings never idles the GPU:
+	// the step after it is already queued. The phase marks skip the system-scope release fence (it
+	// writes back and invalidates the caches, which would slow the kernel after every mark).
+	hipEvent_t ev[2][N_PHASES + 1] = {};
+	hipEvent_t ev_done[2] = {};
+	StepState* prof_st = nullptr;  // pinned, one StepState copy per event set
+	bool prof_pending[2] = {false, false};
+	int prof_par = 0;
 	double phase_ms[N_PHASES] = {};
 	double phase_npre = 0, phase_ntrain = 0;
 	uint32_t phase_steps = 0;
@@ -132,14 +139,20 @@ struct NeusTestbed {
 		HIP_CHECK(hipSetDevice(device));
 		HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
 		HIP_CHECK(hipHostMalloc((void**)&pinned, 64 * sizeof(float)));
-		for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
+		for (auto& set : ev)
+			for (auto& e : set) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+		for (auto& e : ev_done) HIP_CHECK(hipEventCreate(&e));
+		HIP_CHECK(hipHostMalloc((void**)&prof_st, 2 * sizeof(StepState)));
 		st.alloc(1);
 		HIP_CHECK(hipMemset(st.p, 0, sizeof(StepState)));
 	}
 	~NeusTestbed() {
 		if (stream) (void)hipStreamSynchronize(stream);
 		if (comm) ncclCommDestroy(comm);
-		for (auto& e : ev) if (e) (void)hipEventDestroy(e);
+		for (auto& set : ev)
+			for (auto& e : set) if (e) (void)hipEventDestroy(e);
+		for (auto& e : ev_done) if (e) (void)hipEventDestroy(e);
+		if (prof_st) (void)hipHostFree(prof_st);
 		if (pinned) (void)hipHostFree(pinned);
 		if (stream) (void)hipStreamDestroy(stream);
 	}
@@ -453,7 +466,7 @@ struct NeusTestbed {
 		prepare_weights();
 	}
 
-	void mark(int i) { if (profiling) HIP_CHECK(hipEventRecord(ev[i], stream)); }
+	void mark(int i) { if (profiling) HIP_CHECK(hipEventRecord(ev[prof_par][i], stream)); }
 
 	// ------------------------------------------------------------ one Testbed::train step (testbed.cu:2640-2736)
 	void train_step() {
@@ -516,7 +529,13 @@ struct NeusTestbed {
 		optimizer_step(grads.p);
 		mark(10);
 		++training_step;
-		if (profiling) accumulate_phases();
+		if (profiling) {
+			HIP_CHECK(hipMemcpyAsync(&prof_st[prof_par], st.p, sizeof(StepState), hipMemcpyDeviceToHost, stream));
+			HIP_CHECK(hipEventRecord(ev_done[prof_par], stream));
+			prof_pending[prof_par] = true;
+			prof_par ^= 1;
+			if (prof_pending[prof_par]) accumulate_phases(prof_par);  // the previous step
+		}
 	}
 
 	LossWork loss_work(const uint32_t* rbase) {
@@ -526,18 +545,23 @@ struct NeusTestbed {
 		return w;
 	}
 
-	void accumulate_phases() {
-		HIP_CHECK(hipEventSynchronize(ev[N_PHASES]));
+	void accumulate_phases(int par) {
+		HIP_CHECK(hipEventSynchronize(ev_done[par]));
 		for (int i = 0; i < N_PHASES; ++i) {
 			float ms = 0.f;
-			HIP_CHECK(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
+			HIP_CHECK(hipEventElapsedTime(&ms, ev[par][i], ev[par][i + 1]));
 			phase_ms[i] += ms;
 		}
-		StepState h{};
-		HIP_CHECK(hipMemcpy(&h, st.p, sizeof(StepState), hipMemcpyDeviceToHost));
+		const StepState& h = prof_st[par];
 		phase_npre += h.n_kept;
 		phase_ntrain += std::min(h.compacted_counter / std::max(1u, world), batch);
 		++phase_steps;
+		prof_pending[par] = false;
+	}
+	void flush_phases() {
+		// oldest first: the set about to be reused is the older one
+		if (prof_pending[prof_par]) accumulate_phases(prof_par);
+		if (prof_pending[prof_par ^ 1]) accumulate_phases(prof_par ^ 1);
 	}
 
 	void consume_loss() {
@@ -662,8 +686,22 @@ int neus_testbed_ray_counts(NeusTestbed* tb, uint32_t n, uint32_t* nreq, uint32_
 		if (numsteps) HIP_CHECK(hipMemcpy(numsteps, tb->numsteps.p, (size_t)n * 8, hipMemcpyDeviceToHost));
 	});
 }
+static void time_kernel_impl(NeusTestbed* tb, int kernel, int variant, int iters, float* ms_out);
 int neus_debug_time_kernel(NeusTestbed* tb, int kernel, int variant, int iters, float* ms_out) {
+	return guard([&] { time_kernel_impl(tb, kernel, variant, iters, ms_out); });
+}
+int neus_testbed_time_kernel(NeusTestbed* tb, int kernel, int iters, float* ms_out, uint32_t* units_out) {
 	return guard([&] {
+		time_kernel_impl(tb, kernel, 0, iters, ms_out);
+		StepState h{};
+		HIP_CHECK(hipMemcpy(&h, tb->st.p, sizeof(StepState), hipMemcpyDeviceToHost));
+		// work units of one launch: ray slots (march), pre-compaction samples (write, inference, loss),
+		// compacted training samples (encode, MLP, weight gradients, grid scatter)
+		*units_out = kernel == 0 ? MAX_RAYS : (kernel <= 4 ? h.n_kept : tb->batch);
+	});
+}
+static void time_kernel_impl(NeusTestbed* tb, int kernel, int variant, int iters, float* ms_out) {
+	{
 		if (!tb->have_net) throw std::runtime_error("no network");
 		NeusTestbed& t = *tb;
 		hipStream_t s = t.stream;
@@ -678,10 +716,12 @@ int neus_debug_time_kernel(NeusTestbed* tb, int kernel, int variant, int iters, 
 			launch_march_write(s, MAX_RAYS, t.st.p, t.ds, t.rays.p, t.tbuf_t.p, t.nreq.p, t.base.p, t.numsteps.p, t.coords.p,
 			                   t.sample_ray.p, t.max_samples);
 		};
-		march();
-		launch_nerf_infer(s, t.lay.L, t.lay.W, &t.st.p->n_kept, 0, t.coords.p, t.gl, valid, t.params_h.p + t.lay.grid_off, t.mlp, t.net_out.p, 8192);
 		const LossWork w = t.loss_work(t.base.p);
-		launch_loss_alpha(s, t.max_samples, t.st.p, t.coords.p, t.net_out.p, t.cos_anneal(), w);
+		if (variant != 99) {  // 99: no re-preparation (counter runs: only the timed kernel is launched)
+			march();
+			launch_nerf_infer(s, t.lay.L, t.lay.W, &t.st.p->n_kept, 0, t.coords.p, t.gl, valid, t.params_h.p + t.lay.grid_off, t.mlp, t.net_out.p, 8192);
+			launch_loss_alpha(s, t.max_samples, t.st.p, t.coords.p, t.net_out.p, t.cos_anneal(), w);
+		}
 		hipEvent_t a, b;
 		HIP_CHECK(hipEventCreate(&a)); HIP_CHECK(hipEventCreate(&b));
 		HIP_CHECK(hipEventRecord(a, s));
@@ -703,6 +743,7 @@ int neus_debug_time_kernel(NeusTestbed* tb, int kernel, int variant, int iters, 
 			case 6: { WGradJobs J = t.wgrad_jobs(t.batch, t.batch, t.grads.p, nullptr); launch_wgrad(s, J, J.block_start[5]); break; }
 			case 7: launch_grid_scatter(s, nullptr, t.batch, t.batch, t.coords_c.p, COORD_W, t.gl, valid, t.tbuf.dLdenc, t.tbuf.genc, t.tbuf.v,
 			                            t.grads.p + t.lay.grid_off, t.swork, t.scan_tmp.p, t.scan_tmp_bytes); break;
+			case 8: t.encode(nullptr, t.batch, t.batch, t.batch, t.coords_c.p, COORD_W, valid, true, s); break;
 			default: throw std::runtime_error("unknown kernel id");
 			}
 		}
@@ -712,7 +753,7 @@ int neus_debug_time_kernel(NeusTestbed* tb, int kernel, int variant, int iters, 
 		HIP_CHECK(hipEventElapsedTime(&ms, a, b));
 		*ms_out = ms / std::max(1, iters);
 		HIP_CHECK(hipEventDestroy(a)); HIP_CHECK(hipEventDestroy(b));
-	});
+	}
 }
 int neus_debug_march_stats(NeusTestbed* tb, uint32_t n, uint32_t* out) {
 	return guard([&] {
@@ -728,10 +769,16 @@ int neus_debug_march_stats(NeusTestbed* tb, uint32_t n, uint32_t* out) {
 int neus_testbed_stream(NeusTestbed* tb, void** s) { return guard([&] { *s = (void*)tb->stream; }); }
 int neus_testbed_synchronize(NeusTestbed* tb) { return guard([&] { HIP_CHECK(hipStreamSynchronize(tb->stream)); }); }
 int neus_testbed_set_profiling(NeusTestbed* tb, int on) {
-	return guard([&] { tb->profiling = on != 0; for (auto& m : tb->phase_ms) m = 0; tb->phase_steps = 0; tb->phase_npre = tb->phase_ntrain = 0; });
+	return guard([&] {
+		tb->flush_phases();
+		tb->profiling = on != 0;
+		for (auto& m : tb->phase_ms) m = 0;
+		tb->phase_steps = 0; tb->phase_npre = tb->phase_ntrain = 0;
+	});
 }
 int neus_testbed_kernel_times(NeusTestbed* tb, float* ms) {
 	return guard([&] {
+		tb->flush_phases();
 		for (int i = 0; i < NeusTestbed::N_PHASES; ++i) ms[i] = tb->phase_steps ? (float)(tb->phase_ms[i] / tb->phase_steps) : 0.f;
 		ms[NeusTestbed::N_PHASES] = (float)tb->phase_steps;
 		ms[NeusTestbed::N_PHASES + 1] = tb->phase_steps ? (float)(tb->phase_npre / tb->phase_steps) : 0.f;

@@ -282,6 +282,14 @@ class Testbed:
     def set_profiling(self, on=True):
         check(lib().neus_testbed_set_profiling(self._h, C.c_int(1 if on else 0)))
 
+    def time_kernel(self, kernel, iters=5):
+        """(mean ms per launch, work units per launch) of one hot-path kernel replayed on the current
+        training state (neus_testbed_time_kernel; ids in include/neus2_hip.h)."""
+        ms = C.c_float()
+        units = C.c_uint32()
+        check(lib().neus_testbed_time_kernel(self._h, C.c_int(kernel), C.c_int(iters), C.byref(ms), C.byref(units)))
+        return float(ms.value), int(units.value)
+
     def phase_times(self):
         """Mean ms per profiled step for each of PHASES, plus (n_steps, mean Npre, mean Ntrain)."""
         n = len(PHASES)

@@ -1,7 +1,7 @@
 """Summarise a rocprofv3 --kernel-trace --stats run (rocpd SQLite db or kernel_stats.csv) into a
 markdown table: kernel, calls, total ms, average us, share.
 Usage: prof_summary.py <db|csv> [out.md] [--last-steps K]
---last-steps K (db only): only dispatches from the K-th last k_march_count launch on, i.e. the final K
+--last-steps K (db only): only dispatches from the K-th last k_ray_gen launch on, i.e. the final K
 training steps (the steady state after the bench warm-up), with the per-step time of each kernel."""
 import csv
 import re
@@ -39,7 +39,8 @@ def rows_from(path):
 
 def rows_last_steps(path, k):
     con = sqlite3.connect(path)
-    starts = [r[0] for r in con.execute("select start from kernels where name like '%k_march_count%' order by start")]
+    # one k_ray_gen launch per training step (k_march_count in older profiles)
+    starts = [r[0] for r in con.execute("select start from kernels where name like '%k_ray_gen%' or name like '%k_march_count%' order by start")]
     t0 = starts[-k]
     out = {}
     for name, dur in con.execute("select name, duration from kernels where start >= ?", (t0,)):
@@ -56,6 +57,10 @@ def main():
         last = int(args[i + 1])
         del args[i:i + 2]
     sys.argv = [sys.argv[0]] + args
+    import glob, os
+    if os.path.isdir(sys.argv[1]):
+        sys.argv[1] = (glob.glob(os.path.join(sys.argv[1], "**", "*.db"), recursive=True) or
+                       glob.glob(os.path.join(sys.argv[1], "**", "*kernel_stats.csv"), recursive=True))[0]
     rows = rows_last_steps(sys.argv[1], last) if last else rows_from(sys.argv[1])
     agg = {}
     for name, calls, tot, _ in rows:
