@@ -113,6 +113,8 @@ __device__ __forceinline__ uint32_t wave_bucket_slot(uint32_t* hist, uint32_t bk
 //   exclusive scan    bucket-major [bucket][block] -> each block's slot range in each bucket
 //   k_scatter_bin     recompute the contributions; per wave and level, stage them in LDS, reserve one
 //                     contiguous run per bucket and write the records into their runs
+//   records           (entry, fp16x2 contribution): the reference adds each corner's contribution as an
+//                     fp16x2 atomic operand (grid.h:371-500), i.e. rounded to half; so is the record
 //   k_scatter_accum   one workgroup per bucket: sum its records in LDS as int64 fixed point (2^-32,
 //                     order-independent, so the gradient is bitwise deterministic) and store the
 //                     bucket's fp32 gradient (plain stores: the workgroup owns its entries)
@@ -241,7 +243,8 @@ __global__ void __launch_bounds__(256) k_scatter_bin(const uint32_t* __restrict_
 				const uint32_t lb = (e >> SB_SHIFT) - b_first;
 				const uint32_t gp = bas[lb] + atomicAdd(&cnt[lb], 1u);
 				w.rec_i[gp] = (uint16_t)(e & (SB_SIZE - 1));
-				w.rec_g[gp] = sg[kk * 64 + lane];
+				const float2 v = sg[kk * 64 + lane];
+				w.rec_g[gp] = (h2){(half_t)v.x, (half_t)v.y};
 			}
 		}
 		__syncthreads();  // all reservations of this level done
@@ -264,16 +267,19 @@ __global__ void __launch_bounds__(256) k_scatter_accum(ScatterWork w, float* __r
 	};
 	// unaligned head and tail one per thread, the 8-aligned middle as groups of 8 per thread
 	const uint32_t a0 = min(c1, (c0 + 7u) & ~7u), a1 = max(a0, c1 & ~7u);
-	for (uint32_t r = c0 + threadIdx.x; r < a0; r += blockDim.x) { const float2 gv = w.rec_g[r]; add(w.rec_i[r], gv.x, gv.y); }
-	for (uint32_t r = a1 + threadIdx.x; r < c1; r += blockDim.x) { const float2 gv = w.rec_g[r]; add(w.rec_i[r], gv.x, gv.y); }
+	auto one = [&](uint32_t r) { const h2 gv = w.rec_g[r]; add(w.rec_i[r], (float)gv[0], (float)gv[1]); };
+	for (uint32_t r = c0 + threadIdx.x; r < a0; r += blockDim.x) one(r);
+	for (uint32_t r = a1 + threadIdx.x; r < c1; r += blockDim.x) one(r);
 	for (uint32_t gq = a0 / 8 + threadIdx.x; gq < a1 / 8; gq += blockDim.x) {
 		const uint4 ei = *(const uint4*)(w.rec_i + 8 * (size_t)gq);
-		const float4* gp = (const float4*)(w.rec_g + 8 * (size_t)gq);
-		const float4 v0 = gp[0], v1 = gp[1], v2 = gp[2], v3 = gp[3];
-		const uint32_t ew[4] = {ei.x, ei.y, ei.z, ei.w};
-		const float vv[16] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, v2.z, v2.w, v3.x, v3.y, v3.z, v3.w};
+		const uint4* gp = (const uint4*)(w.rec_g + 8 * (size_t)gq);
+		const uint4 u0 = gp[0], u1 = gp[1];
+		const uint32_t ew[4] = {ei.x, ei.y, ei.z, ei.w}, gw[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
 #pragma unroll
-		for (int k = 0; k < 8; ++k) add((ew[k >> 1] >> (16 * (k & 1))) & 0xffffu, vv[2 * k], vv[2 * k + 1]);
+		for (int k = 0; k < 8; ++k) {
+			const h2 gv = __builtin_bit_cast(h2, gw[k]);
+			add((ew[k >> 1] >> (16 * (k & 1))) & 0xffffu, (float)gv[0], (float)gv[1]);
+		}
 	}
 	__syncthreads();
 	// the workgroup owns entries [b * SB_SIZE, +SB_SIZE): plain stores of the interleaved fp32 pairs

@@ -59,7 +59,7 @@ constexpr uint32_t SB_LEVEL_BUCKETS = (1u << 19) / SB_SIZE + 2; // buckets one l
 struct ScatterWork {
 	uint32_t* counts;   // [n_buckets * n_blocks + 1] contributions per (bucket, block), bucket-major
 	uint32_t* offs;     // exclusive scan of counts
-	float2* rec_g;      // [capacity] contribution (feature 0, feature 1)
+	h2* rec_g;          // [capacity] contribution (feature 0, feature 1), fp16 as the reference's per-corner half2 atomic operand
 	uint16_t* rec_i;    // [capacity] entry within the bucket
 	uint32_t n_buckets, n_blocks;
 };

@@ -99,7 +99,7 @@ struct NeusTestbed {
 	Dev<StepState> st;
 	ScatterWork swork{};
 	Dev<uint32_t> sc_counts, sc_offs;
-	Dev<float2> sc_rec_g;
+	Dev<h2> sc_rec_g;
 	Dev<uint16_t> sc_rec_i;
 	// restructured loss scratch (kernels.h LossWork)
 	Dev<float4> l_sa, l_ck4, l_racc, l_rgr;

@@ -33,6 +33,14 @@ def L():
     return lib(), check
 
 
+def record(test, **metrics):
+    """Append measured parity metrics to gpurun_out/parity_metrics.jsonl (evidence for DESIGN.md)."""
+    import json
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "parity_metrics.jsonl"), "a") as f:
+        f.write(json.dumps({"test": test, **{k: float(v) for k, v in metrics.items()}}) + "\n")
+
+
 def test_mfma_f16_layout_exact(torch_cuda):
     """v_mfma_f32_32x32x16_f16 lane maps (natural k order) with exact small-integer data, asymmetric B."""
     t = torch_cuda
@@ -123,6 +131,7 @@ def test_network_forward_parity(env):
         # fp16 storage noise can flip a ReLU mask of a near-zero hidden unit, which moves that sample's
         # dSDF/dx (and the rgb logits fed by it) discontinuously; the reference has the same behaviour.
         ok_samples = np.all(err <= tol, axis=1)
+        record(f"forward_valid{valid}", frac_within_tol=ok_samples.mean(), median_abs_err=np.median(err), max_abs_err=err.max())
         assert ok_samples.mean() >= 0.995, (ok_samples.mean(), np.argwhere(err > tol)[:5])
         assert np.median(err) < 1e-3
 
@@ -153,6 +162,7 @@ def test_network_backward_parity(env):
         x, y = got[a:b].astype(np.float64), ref[a:b].astype(np.float64)
         rel = np.linalg.norm(x - y) / max(np.linalg.norm(y), 1e-30)
         cos = x @ y / max(np.linalg.norm(x) * np.linalg.norm(y), 1e-30)
+        record(f"backward_{name}", rel=rel, cos=cos)
         assert rel <= 2e-2 and cos >= 0.999, (name, rel, cos)
 
 
