@@ -21,9 +21,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-# HBM bytes per launch from rocprofv3 PMC passes (FETCH_SIZE/WRITE_SIZE, gfx950-corrected; see
-# profiles/README.md). Filled from the committed profile of this round; None where not collected.
-TRAFFIC = {}
+# Memory-side bytes per launch of the dominant kernel from rocprofv3 PMC passes (scripts/gpu_traffic.sh,
+# profiles/r01_pmc_traffic.md): reads = 128 B x TCC_EA0_RDREQ_128B + 64 B x the other requests (all of
+# this kernel's are 128-B requests; FETCH_SIZE tallies them at 64 B, the gfx950 half-count), writes =
+# WRITE_SIZE. L2-to-fabric traffic: Infinity Cache hits are included, so this bounds HBM bytes from above.
+TRAFFIC = {"inference": 5856.0e6 + 134.2e6}
 
 
 def parse():
@@ -66,8 +68,8 @@ KERNELS = {
 MFMA_PEAK_TFLOPS = 2500.0  # MI355X dense fp16 (MI355X_MICROARCH.md)
 
 
-def kernel_rooflines(tb, iters=5):
-    """Per-kernel mean launch duration (hipEvents on the testbed stream around `iters` back-to-back
+def kernel_rooflines(tb, iters=9):
+    """Per-kernel median launch duration (hipEvents on the testbed stream between `iters` back-to-back
     launches replayed on the final training state, neus_testbed_time_kernel) and the algorithmic HBM
     roofline of each launch."""
     out = {}

@@ -132,7 +132,7 @@ int neus_testbed_ray_counts(NeusTestbed* tb, uint32_t n, uint32_t* nreq, uint32_
  * kernel (0 march count, 1 march write, 2 loss transmittance scan, 3 fused inference, 4 loss alpha)
  * in implementation `variant` (0 = production); mean ms per launch. */
 int neus_debug_time_kernel(NeusTestbed* tb, int kernel, int variant, int iters, float* ms_out);
-/* Mean duration (hipEvents on the testbed stream around `iters` back-to-back launches) of one hot-path
+/* Median launch duration (hipEvents on the testbed stream between `iters` back-to-back launches) of one hot-path
  * kernel replayed on the current training state, and the work units of one launch.
  * kernel: 0 ray generation + march (units: ray slots), 1 coordinate write, 2 loss transmittance scan,
  * 3 fused inference, 4 loss alpha (units: pre-compaction samples), 5 training MLP, 6 weight gradients,

@@ -722,10 +722,12 @@ static void time_kernel_impl(NeusTestbed* tb, int kernel, int variant, int iters
 			launch_nerf_infer(s, t.lay.L, t.lay.W, &t.st.p->n_kept, 0, t.coords.p, t.gl, valid, t.params_h.p + t.lay.grid_off, t.mlp, t.net_out.p, 8192);
 			launch_loss_alpha(s, t.max_samples, t.st.p, t.coords.p, t.net_out.p, t.cos_anneal(), w);
 		}
-		hipEvent_t a, b;
-		HIP_CHECK(hipEventCreate(&a)); HIP_CHECK(hipEventCreate(&b));
-		HIP_CHECK(hipEventRecord(a, s));
+		// one event between consecutive launches (fence-free: timing only); the median launch is reported
+		iters = std::max(1, iters);
+		std::vector<hipEvent_t> evs((size_t)iters + 1);
+		for (auto& e : evs) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
 		for (int k = 0; k < iters; ++k) {
+			HIP_CHECK(hipEventRecord(evs[k], s));
 			switch (kernel) {
 			case 0: launch_march_count(s, MAX_RAYS, t.st.p, dp, t.ds, t.bitfield.p, lin, t.rng.state, t.rng.inc, t.rays.p, t.startt.p, t.nreq.p, t.tbuf_t.p); break;
 			case 1: launch_march_write(s, MAX_RAYS, t.st.p, t.ds, t.rays.p, t.tbuf_t.p, t.nreq.p, t.base.p, t.numsteps.p,
@@ -747,12 +749,13 @@ static void time_kernel_impl(NeusTestbed* tb, int kernel, int variant, int iters
 			default: throw std::runtime_error("unknown kernel id");
 			}
 		}
-		HIP_CHECK(hipEventRecord(b, s));
-		HIP_CHECK(hipEventSynchronize(b));
-		float ms = 0.f;
-		HIP_CHECK(hipEventElapsedTime(&ms, a, b));
-		*ms_out = ms / std::max(1, iters);
-		HIP_CHECK(hipEventDestroy(a)); HIP_CHECK(hipEventDestroy(b));
+		HIP_CHECK(hipEventRecord(evs[iters], s));
+		HIP_CHECK(hipStreamSynchronize(s));
+		std::vector<float> d((size_t)iters);
+		for (int k = 0; k < iters; ++k) HIP_CHECK(hipEventElapsedTime(&d[k], evs[k], evs[k + 1]));
+		std::sort(d.begin(), d.end());
+		*ms_out = d[(size_t)iters / 2];
+		for (auto& e : evs) HIP_CHECK(hipEventDestroy(e));
 	}
 }
 int neus_debug_march_stats(NeusTestbed* tb, uint32_t n, uint32_t* out) {

@@ -1,7 +1,7 @@
 """Summarise a rocprofv3 --kernel-trace --stats run (rocpd SQLite db or kernel_stats.csv) into a
 markdown table: kernel, calls, total ms, average us, share.
 Usage: prof_summary.py <db|csv> [out.md] [--last-steps K]
---last-steps K (db only): only dispatches from the K-th last k_ray_gen launch on, i.e. the final K
+--last-steps K (db only): only the final K training steps (delimited by the optimizer launches), i.e. the final K
 training steps (the steady state after the bench warm-up), with the per-step time of each kernel."""
 import csv
 import re
@@ -38,14 +38,16 @@ def rows_from(path):
 
 
 def rows_last_steps(path, k):
+    """Kernels of the last k training steps: the launches after the (k+1)-th last k_adam_ema up to and
+    including the last one (one optimizer launch per step; bench.py's kernel replays have none)."""
     con = sqlite3.connect(path)
-    # one k_ray_gen launch per training step (k_march_count in older profiles)
-    starts = [r[0] for r in con.execute("select start from kernels where name like '%k_ray_gen%' or name like '%k_march_count%' order by start")]
-    t0 = starts[-k]
+    ks = list(con.execute("select name, start, end from kernels order by start"))
+    adam = [i for i, r in enumerate(ks) if "k_adam_ema" in r[0]]
+    begin, last = adam[-k - 1] + 1, adam[-1]
     out = {}
-    for name, dur in con.execute("select name, duration from kernels where start >= ?", (t0,)):
+    for name, st, en in ks[begin:last + 1]:
         c, t = out.get(name, (0, 0.0))
-        out[name] = (c + 1, t + float(dur))
+        out[name] = (c + 1, t + float(en - st))
     return [(n, c, t, t / c) for n, (c, t) in out.items()]
 
 
