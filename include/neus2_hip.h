@@ -16,6 +16,7 @@
  *     neus_testbed_get_stats           Testbed::m_training_step / m_loss_scalar / counters (python_api.cu:447-449)
  *     neus_testbed_{get,set}_params    Trainer params / serialize             trainer.h:72-109, 281-300
  *     neus_testbed_{get,set}_density_grid  Nerf::density_grid(_bitfield)      testbed.h:688-694
+ *     neus_testbed_render              Testbed::render_to_cpu -> render_nerf / NerfTracer::trace  python_api.cu:123-169, testbed_nerf.cu:2397-2760
  *     neus_testbed_init_data_parallel  (new) RCCL data parallelism over ray batches
  *
  *   Operator surface (my_tcnn DifferentiableObject / cpp_api.h:66-106 for the NerfNetwork, plus
@@ -99,6 +100,19 @@ typedef struct NeusTrainStats {
 	uint32_t n_rays_with_samples;             /* rays kept by the sampler in the last logged step */
 } NeusTrainStats;
 
+/* Testbed::render_to_cpu (python_api.cu:123-169) after set_camera_to_training_view (testbed.cu:264-270). */
+typedef struct NeusRenderRequest {
+	int32_t width, height;
+	uint32_t spp;                    /* samples per pixel, accumulated in linear colour (render_buffer.cu:217-260) */
+	int32_t training_view;           /* >= 0: the camera of this training image; < 0: xform/focal/screen_center below */
+	float xform[12];                 /* camera-to-world 3x4 row-major (ngp convention) */
+	float focal[2];                  /* pixels at width x height */
+	float screen_center[2];          /* normalized principal point */
+	int32_t snap_to_pixel_centers;   /* render_utils.py:272 sets it for evaluation */
+	float min_transmittance;         /* nerf.rendering_min_transmittance (render_utils.py:275: 1e-4) */
+	int32_t use_ema;                 /* 1: inference params = EMA weights (the reference); 0: training weights */
+} NeusRenderRequest;
+
 typedef struct NeusNetLayout {
 	uint64_t n_params, n_density, n_rgb, grid_offset, n_grid_params, variance_offset, n_matrix;
 	uint32_t density_input_width, rgb_input_width;
@@ -124,6 +138,9 @@ int neus_testbed_get_gradients(NeusTestbed* tb, float* host_out, uint64_t n);
 int neus_testbed_get_ema_params(NeusTestbed* tb, float* host_out, uint64_t n);
 int neus_testbed_get_density_grid(NeusTestbed* tb, float* grid_out /*128^3*/, uint8_t* bitfield_out /*128^3/8*8*/);
 int neus_testbed_set_density_grid(NeusTestbed* tb, const float* grid /*nullable*/, const uint8_t* bitfield /*nullable*/);
+/* rgba_out: height*width*4 floats, linear colour, premultiplied alpha (the reference's render(..., linear=True)).
+ * n_iterations (nullable): march/composite iterations of the last spp. */
+int neus_testbed_render(NeusTestbed* tb, const NeusRenderRequest* req, float* rgba_out, uint32_t* n_iterations);
 int neus_testbed_get_rng(NeusTestbed* tb, uint64_t* state_inc /*4: rng, density_grid_rng*/);
 /* Per-ray counters of the last step (first n rays, host buffers, each nullable): samples requested by
  * the march, samples composited before transmittance < 1e-4, and numsteps = (compacted count, base). */

@@ -51,13 +51,21 @@ class NeusNetLayout(C.Structure):
     ]
 
 
+class NeusRenderRequest(C.Structure):
+    _fields_ = [
+        ("width", C.c_int32), ("height", C.c_int32), ("spp", C.c_uint32), ("training_view", C.c_int32),
+        ("xform", C.c_float * 12), ("focal", C.c_float * 2), ("screen_center", C.c_float * 2),
+        ("snap_to_pixel_centers", C.c_int32), ("min_transmittance", C.c_float), ("use_ema", C.c_int32),
+    ]
+
+
 # Every symbol declared in include/neus2_hip.h (checked by tests/test_capi.py).
 EXPORTS = [
     "neus_last_error", "neus_device_count", "neus_device_synchronize",
     "neus_testbed_create", "neus_testbed_destroy", "neus_testbed_set_dataset", "neus_testbed_reload_network",
     "neus_testbed_layout", "neus_testbed_train", "neus_testbed_get_stats", "neus_testbed_get_params",
     "neus_testbed_set_params", "neus_testbed_get_gradients", "neus_testbed_get_ema_params",
-    "neus_testbed_get_density_grid", "neus_testbed_set_density_grid", "neus_testbed_get_rng", "neus_testbed_ray_counts", "neus_debug_time_kernel", "neus_debug_march_stats", "neus_testbed_time_kernel", "neus_testbed_stream",
+    "neus_testbed_get_density_grid", "neus_testbed_set_density_grid", "neus_testbed_get_rng", "neus_testbed_render", "neus_testbed_ray_counts", "neus_debug_time_kernel", "neus_debug_march_stats", "neus_testbed_time_kernel", "neus_testbed_stream",
     "neus_testbed_synchronize", "neus_testbed_set_profiling", "neus_testbed_kernel_times",
     "neus_nccl_unique_id", "neus_testbed_init_data_parallel",
     "neus_grid_encode", "neus_net_forward", "neus_net_backward", "neus_sample_rays", "neus_loss_compact",

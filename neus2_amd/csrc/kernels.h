@@ -45,6 +45,18 @@ struct DevDataset {
 
 struct DPInfo { uint32_t rank, world; };
 
+// Render camera (Testbed::set_camera_to_training_view, testbed.cu:264-270; render_nerf, testbed_nerf.cu:2670-2760):
+// camera-to-world 3x4 row-major, focal length in pixels, screen centre (= the view's principal point), and the
+// sub-pixel offset of pixel_to_ray (ld_random_pixel_offset, computed on the host).
+struct RenderCamera {
+	float xform[12];
+	float focal[2], screen_center[2], pixel_offset[2];
+	uint32_t width, height;
+};
+constexpr float NERF_RENDERING_NEAR_DISTANCE = 0.2f;  // testbed_nerf.cu:57
+constexpr uint32_t MARCH_ITER = 10000;                  // testbed_nerf.cu:78
+constexpr uint32_t MAX_STEPS_INBETWEEN_COMPACTION = 8;  // testbed_nerf.cu:81
+
 struct LossParams {
 	float loss_scale;      // LOSS_SCALE = 128 (testbed.h:246)
 	float ek_w, mask_w, cos_anneal;
@@ -127,6 +139,17 @@ void debug_launch_loss_scan(hipStream_t s, int variant, uint32_t cap_rays, const
 void launch_ray_index(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, StepState* st, uint32_t* sample_ray, uint32_t* rbase);
 void launch_rollover(hipStream_t s, uint32_t n_elements, const StepState* st, float* coords, half_t* dL_dout);
 void launch_step_counters(hipStream_t s, StepState* st, uint32_t target_batch, uint32_t max_samples, uint32_t world, uint32_t fixed_rays);
+// render.hip (rays: RenderRay records, render_ray_bytes() each)
+size_t render_ray_bytes();
+void launch_render_init(hipStream_t s, const RenderCamera& cam, uint32_t sample_index, const DevDataset& ds, const uint8_t* bf, const uint32_t* lin,
+                        void* rays, float4* frame);
+void launch_render_compact(hipStream_t s, uint32_t n, const void* src, uint32_t* flags, uint32_t* base, void* dst, uint32_t* n_alive,
+                           void* scan_tmp, size_t scan_tmp_bytes);
+void launch_render_gen(hipStream_t s, uint32_t n_alive, uint32_t n_steps, const DevDataset& ds, const uint8_t* bf, const uint32_t* lin, void* rays,
+                       float* coords);
+void launch_render_composite(hipStream_t s, uint32_t n_alive, uint32_t n_steps, const float* coords, const half_t* net_out, float cos_anneal,
+                             float min_transmittance, void* rays, float4* frame);
+void launch_render_accumulate(hipStream_t s, uint32_t n, uint32_t spp, const float4* frame, float4* accum);
 // scan.hip
 size_t scan_temp_bytes(uint32_t n);
 void launch_exclusive_scan(hipStream_t s, void* temp, size_t temp_bytes, const uint32_t* in, uint32_t* out, uint32_t n);

@@ -56,6 +56,40 @@ constexpr float LOSS_SCALE = 128.f;      // testbed.h:246
 
 uint32_t next_multiple(uint32_t v, uint32_t m) { return (v + m - 1) / m * m; }
 
+// ld_random_pixel_offset (random_val.cuh:254-288, 317-322): scrambled Sobol 2-D value of the spp index,
+// offset = fract(0.5 - v(0) + v(spp)). Sobol dimension 0 is the bit reversal; dimension 1 has direction
+// numbers d[0] = 2^31, d[b] = d[b-1] ^ (d[b-1] >> 1).
+uint32_t rev_bits(uint32_t x) {
+	x = ((x & 0xaaaaaaaau) >> 1) | ((x & 0x55555555u) << 1); x = ((x & 0xccccccccu) >> 2) | ((x & 0x33333333u) << 2);
+	x = ((x & 0xf0f0f0f0u) >> 4) | ((x & 0x0f0f0f0fu) << 4); x = ((x & 0xff00ff00u) >> 8) | ((x & 0x00ff00ffu) << 8);
+	return (x >> 16) | (x << 16);
+}
+uint32_t nus_scramble(uint32_t x, uint32_t seed) {
+	x = rev_bits(x);
+	x += seed; x ^= x * 0x6c50b47cu; x ^= x * 0xb82f1e52u; x ^= x * 0xc7afe638u; x ^= x * 0x8d22f6e6u;
+	return rev_bits(x);
+}
+uint32_t sobol_dim(uint32_t index, uint32_t dim) {
+	uint32_t X = 0, d = 0x80000000u;
+	for (uint32_t bit = 0; bit < 32; ++bit) {
+		const uint32_t dir = dim == 0 ? (0x80000000u >> bit) : d;
+		if ((index >> bit) & 1) X ^= dir;
+		d ^= d >> 1;
+	}
+	return X;
+}
+void ld_random_val_2d(uint32_t index, uint32_t seed, float out[2]) {
+	const float S = float(1.0 / 4294967296.0);
+	index = nus_scramble(index, seed);
+	for (uint32_t i = 0; i < 2; ++i) out[i] = (float)nus_scramble(sobol_dim(index, i), seed ^ (i + (seed << 6) + (seed >> 2))) * S;
+}
+void ld_pixel_offset(uint32_t spp, float out[2]) {
+	float a[2], b[2];
+	ld_random_val_2d(0, 0xdeadbeefu, a);
+	ld_random_val_2d(spp, 0xdeadbeefu, b);
+	for (int k = 0; k < 2; ++k) { const float v = (0.5f - a[k]) + b[k]; out[k] = v - std::floor(v); }
+}
+
 struct Layout {
 	uint32_t din, W, L;
 	uint32_t off_d0, off_d1, off_r0, off_r1, off_r2, n_density, n_rgb, n_matrix, grid_off, n_grid, var_off, P;
@@ -73,6 +107,8 @@ struct NeusTestbed {
 	// dataset
 	Dev<uint32_t> pixels; Dev<uint64_t> pix_off; Dev<int32_t> res; Dev<float> focal, pp, xform;
 	DevDataset ds{};
+	std::vector<float> host_focal, host_pp, host_xform;
+	std::vector<int32_t> host_res;
 	uint32_t max_cascade = 0;
 	float aabb_scale = 1.f;
 	// parameters
@@ -81,6 +117,16 @@ struct NeusTestbed {
 	Dev<half_t> params_h, ema_h, wT;
 	MlpPtrs mlp{};
 	DinPerm din_perm{};
+	// inference params (EMA weights, the reference's Ema::custom_weights) for rendering
+	Dev<half_t> wT_ema;
+	MlpPtrs mlp_ema{};
+	// renderer workspace (NerfTracer, testbed_nerf.cu:2397-2630)
+	Dev<uint8_t> r_rays[2], r_scan_tmp;
+	Dev<uint32_t> r_flags, r_base, r_alive;
+	Dev<float> r_coords;
+	Dev<half_t> r_out;
+	Dev<float4> r_frame, r_accum;
+	size_t r_scan_bytes = 0;
 	// occupancy grid
 	Dev<float> density_grid, density_tmp, grid_mean, grid_partial, occ_pos, occ_density;
 	Dev<uint32_t> occ_idx;
@@ -186,6 +232,7 @@ struct NeusTestbed {
 		HIP_CHECK(hipMemcpy(xform.p, x.data(), x.size() * 4, hipMemcpyHostToDevice));
 		ds.pixels = pixels.p; ds.pix_off = pix_off.p; ds.res = res.p; ds.focal = focal.p; ds.pp = pp.p; ds.xform = xform.p;
 		ds.n_images = n_images;
+		host_focal = f; host_pp = p; host_xform = x; host_res = r;
 		const float infl = 0.5f * (float)std::min(1 << (NERF_CASCADES - 1), s);
 		for (int d = 0; d < 3; ++d) { ds.aabb_min[d] = 0.5f - infl; ds.aabb_max[d] = 0.5f + infl; }
 		max_cascade = 0;
@@ -249,6 +296,7 @@ struct NeusTestbed {
 		params_fp.alloc(P); grads.alloc(P); m1.alloc(P); m2.alloc(P); ema_tmp.alloc(P); adam_steps.alloc(P);
 		params_h.alloc(P); ema_h.alloc(P);
 		wT.alloc(l.din * l.W + l.W * 16 + 48 * l.W + l.W * l.W + l.W * 16 + 2 * l.din * l.W + 64);
+		wT_ema.alloc(wT.n);
 		// initial parameters (trainer.h:54-109): seed_seq{seed} -> pcg32
 		std::vector<float> h(P, 0.f);
 		{
@@ -342,20 +390,24 @@ struct NeusTestbed {
 	}
 
 	void setup_mlp_ptrs() {
+		setup_mlp_ptrs_for(params_h.p, wT.p, mlp);
+		setup_mlp_ptrs_for(ema_h.p, wT_ema.p, mlp_ema);
+		din_perm = DinPerm{};
+		mlp_din_permutation(lay.L, din_perm.p);
+		din_perm.din = lay.din; din_perm.W = lay.W;
+	}
+	void setup_mlp_ptrs_for(const half_t* base, half_t* t, MlpPtrs& mlp) {
 		const Layout& l = lay;
-		half_t* t = wT.p;
-		mlp.d0 = params_h.p + l.off_d0; mlp.d1 = params_h.p + l.off_d1;
-		mlp.r0 = params_h.p + l.off_r0; mlp.r1 = params_h.p + l.off_r1; mlp.r2 = params_h.p + l.off_r2;
+		mlp.d0 = base + l.off_d0; mlp.d1 = base + l.off_d1;
+		mlp.r0 = base + l.off_r0; mlp.r1 = base + l.off_r1; mlp.r2 = base + l.off_r2;
 		auto take = [&](size_t k) { half_t* r = t; t += (k + 7) / 8 * 8; return r; };
 		mlp.d0T = take(l.din * l.W); mlp.d1T = take(l.W * 16); mlp.r0T = take(48 * l.W); mlp.r1T = take(l.W * l.W); mlp.r2T = take(l.W * 16);
 		mlp.d0p = take(l.din * l.W); mlp.d0Tp = take(l.din * l.W);
-		din_perm = DinPerm{};
-		mlp_din_permutation(l.L, din_perm.p);
-		din_perm.din = l.din; din_perm.W = l.W;
-		mlp.var = params_h.p + l.var_off;
+		mlp.var = base + l.var_off;
 		mlp.sdf_bias = cfg.sdf_bias;
 	}
-	void prepare_weights() {
+	void prepare_weights() { prepare_weights_for(mlp); }
+	void prepare_weights_for(const MlpPtrs& mlp) {
 		const Layout& l = lay;
 		TransposeJobs tj{};
 		tj.j[0] = {mlp.d0, (half_t*)mlp.d0T, l.W, l.din};
@@ -467,6 +519,75 @@ struct NeusTestbed {
 	}
 
 	void mark(int i) { if (profiling) HIP_CHECK(hipEventRecord(ev[prof_par][i], stream)); }
+
+	// ------------------------------------------------------------ rendering (render_to_cpu, python_api.cu:123-169)
+	// NerfTracer::init_rays_from_camera + trace (testbed_nerf.cu:2397-2600) once per spp, accumulated in linear
+	// colour. The alive count is read back every iteration (it sets the steps per iteration, as the reference).
+	uint32_t render(const NeusRenderRequest& rq, float* host_rgba) {
+		if (!have_net) throw std::runtime_error("render: no network (reload_network first)");
+		if (rq.width <= 0 || rq.height <= 0) throw std::runtime_error("render: empty resolution");
+		const uint64_t n64 = (uint64_t)rq.width * (uint64_t)rq.height;
+		if (n64 > (1ull << 26)) throw std::runtime_error("render: at most 2^26 pixels per call");
+		const uint32_t n = (uint32_t)n64;
+		RenderCamera cam{};
+		cam.width = (uint32_t)rq.width; cam.height = (uint32_t)rq.height;
+		if (rq.training_view >= 0) {
+			if ((uint32_t)rq.training_view >= ds.n_images) throw std::runtime_error("render: training_view out of range");
+			const uint32_t v = (uint32_t)rq.training_view;
+			std::memcpy(cam.xform, &host_xform[12 * v], 12 * sizeof(float));
+			// set_camera_to_training_view: relative focal length = focal / res[fov_axis = 1], rescaled to the render height
+			for (int k = 0; k < 2; ++k) {
+				cam.focal[k] = host_focal[2 * v + k] / (float)host_res[2 * v + 1] * (float)rq.height;
+				cam.screen_center[k] = host_pp[2 * v + k];
+			}
+		} else {
+			std::memcpy(cam.xform, rq.xform, sizeof(cam.xform));
+			cam.focal[0] = rq.focal[0]; cam.focal[1] = rq.focal[1];
+			cam.screen_center[0] = rq.screen_center[0]; cam.screen_center[1] = rq.screen_center[1];
+		}
+		hipStream_t s = stream;
+		const size_t rb = render_ray_bytes();
+		r_rays[0].alloc(n * rb); r_rays[1].alloc(n * rb);
+		r_flags.alloc(n); r_base.alloc(n); r_alive.alloc(1);
+		r_coords.alloc((size_t)n * MAX_STEPS_INBETWEEN_COMPACTION * COORD_W);
+		r_out.alloc((size_t)n * MAX_STEPS_INBETWEEN_COMPACTION * OUT_W);
+		r_frame.alloc(n); r_accum.alloc(n);
+		const size_t sb = scan_temp_bytes(n);
+		if (sb > r_scan_bytes || !r_scan_tmp.p) { r_scan_tmp.alloc(sb + 256); r_scan_bytes = sb; }
+		const MlpPtrs& w = rq.use_ema ? mlp_ema : mlp;
+		const half_t* grid = (rq.use_ema ? ema_h.p : params_h.p) + lay.grid_off;
+		if (rq.use_ema) prepare_weights_for(mlp_ema);
+		const uint32_t valid = valid_level_at((int)training_step);
+		const uint32_t spp = std::max(1u, rq.spp);
+		uint32_t iters = 0;
+		for (uint32_t sp = 0; sp < spp; ++sp) {
+			const uint32_t offs_index = rq.snap_to_pixel_centers ? 0 : sp;
+			ld_pixel_offset(offs_index, cam.pixel_offset);
+			launch_render_init(s, cam, sp, ds, bitfield.p, bf_lin.p, r_rays[0].p, r_frame.p);
+			uint32_t n_alive = n, cur = 0;
+			iters = 0;
+			for (uint32_t i = 1; i < MARCH_ITER;) {
+				launch_render_compact(s, n_alive, r_rays[cur].p, r_flags.p, r_base.p, r_rays[cur ^ 1].p, r_alive.p, r_scan_tmp.p, r_scan_bytes);
+				cur ^= 1;
+				HIP_CHECK(hipMemcpyAsync(pinned + 32, r_alive.p, 4, hipMemcpyDeviceToHost, s));
+				HIP_CHECK(hipStreamSynchronize(s));
+				std::memcpy(&n_alive, pinned + 32, 4);
+				if (n_alive == 0) break;
+				const uint32_t n_steps = std::min(MAX_STEPS_INBETWEEN_COMPACTION, std::max(1u, n / n_alive));
+				launch_render_gen(s, n_alive, n_steps, ds, bitfield.p, bf_lin.p, r_rays[cur].p, r_coords.p);
+				const uint32_t n_el = n_alive * n_steps;
+				launch_nerf_infer(s, lay.L, lay.W, nullptr, n_el, r_coords.p, gl, valid, grid, w, r_out.p,
+				                  std::max<uint32_t>(1, std::min<uint32_t>((n_el + 127) / 128, 8192)));
+				launch_render_composite(s, n_alive, n_steps, r_coords.p, r_out.p, cos_anneal(), rq.min_transmittance, r_rays[cur].p, r_frame.p);
+				i += n_steps;
+				++iters;
+			}
+			launch_render_accumulate(s, n, sp, r_frame.p, r_accum.p);
+		}
+		HIP_CHECK(hipMemcpyAsync(host_rgba, r_accum.p, (size_t)n * 16, hipMemcpyDeviceToHost, s));
+		HIP_CHECK(hipStreamSynchronize(s));
+		return iters;
+	}
 
 	// ------------------------------------------------------------ one Testbed::train step (testbed.cu:2640-2736)
 	void train_step() {
@@ -671,6 +792,14 @@ int neus_testbed_set_density_grid(NeusTestbed* tb, const float* g, const uint8_t
 			launch_bitfield_linear(tb->stream, tb->bitfield.p, tb->bf_lin.p);
 			HIP_CHECK(hipStreamSynchronize(tb->stream));
 		}
+	});
+}
+int neus_testbed_render(NeusTestbed* tb, const NeusRenderRequest* rq, float* rgba_out, uint32_t* n_iterations) {
+	return guard([&] {
+		if (!rq || !rgba_out) throw std::runtime_error("render: null argument");
+		HIP_CHECK(hipSetDevice(tb->device));
+		const uint32_t it = tb->render(*rq, rgba_out);
+		if (n_iterations) *n_iterations = it;
 	});
 }
 int neus_testbed_get_rng(NeusTestbed* tb, uint64_t* o) {

@@ -23,6 +23,7 @@ import os
 import numpy as np
 
 from . import config as _config
+from . import _lib
 from ._lib import NeusError, NeusImage, NeusNetLayout, NeusTrainStats, check, lib
 
 
@@ -34,6 +35,51 @@ class TestbedMode(enum.IntEnum):
 
 
 NERF_SCALE = 0.33  # nerf_loader.h:31
+
+
+def srgb_to_linear(img):
+    """scripts/common.py:136-138"""
+    limit = 0.04045
+    return np.where(img > limit, np.power((img + 0.055) / 1.055, 2.4), img / 12.92)
+
+
+def linear_to_srgb(img):
+    """scripts/common.py:140-142"""
+    limit = 0.0031308
+    return np.where(img > limit, 1.055 * (np.maximum(img, 0) ** (1.0 / 2.4)) - 0.055, 12.92 * img)
+
+
+def mse2psnr(x):
+    """scripts/common.py:46"""
+    return -10. * np.log(x) / np.log(10.)
+
+
+def reference_image_linear(rgba8):
+    """read_image (common.py:144-158) of an 8-bit RGBA image: sRGB -> linear, alpha premultiplied."""
+    img = np.asarray(rgba8, np.float32) / 255.0
+    if img.shape[-1] == 4:
+        img[..., :3] = srgb_to_linear(img[..., :3]) * img[..., 3:4]
+    else:
+        img = srgb_to_linear(img)
+    return img
+
+
+def eval_psnr(image, rgba8, background_color=(0.0, 0.0, 0.0, 0.0)):
+    """render_img_training_view's metric (render_utils.py:252-359): the reference image composited on
+    the background in sRGB space, then PSNR of clip(srgb(pred)) vs clip(srgb(gt)) over rgb."""
+    ref = reference_image_linear(rgba8)
+    bg = np.asarray(background_color, np.float32)
+    if ref.shape[2] == 4:
+        a = ref[..., 3:4]
+        ref[..., :3] = np.divide(ref[..., :3], a, out=np.zeros_like(ref[..., :3]), where=a != 0)
+        ref[..., :3] = linear_to_srgb(ref[..., :3])
+        ref[..., :3] *= a
+        ref += (1.0 - a) * bg
+        ref[..., :3] = srgb_to_linear(ref[..., :3])
+    A = np.clip(linear_to_srgb(image[..., :3]), 0.0, 1.0)
+    R = np.clip(linear_to_srgb(ref[..., :3]), 0.0, 1.0)
+    mse = float(np.mean((A - R) ** 2))
+    return mse2psnr(mse), mse
 
 
 def fov_to_focal_length(resolution, degrees):
@@ -149,6 +195,7 @@ class _Training:
 class _Nerf:
     def __init__(self, tb):
         self.training = _Training(tb)
+        self.rendering_min_transmittance = 0.01  # testbed.h: Nerf::rendering_min_transmittance
 
 
 # neus_testbed_kernel_times order (include/neus2_hip.h NEUS_N_PHASES)
@@ -171,6 +218,10 @@ class Testbed:
         self._cfg_dict = None
         self.shall_train = True
         self.nerf = _Nerf(self)
+        # render state (testbed.h: m_snap_to_pixel_centers, m_background_color, camera)
+        self.snap_to_pixel_centers = False
+        self.background_color = [0.0, 0.0, 0.0, 0.0]
+        self._render_view = None
         self.max_training_steps = None
 
     def __del__(self):
@@ -245,6 +296,44 @@ class Testbed:
             return False
         self.train_steps(1)
         return True
+
+    # ------------------------------------------------------------------ rendering
+    def set_camera_to_training_view(self, view: int):
+        """Testbed::set_camera_to_training_view (testbed.cu:264-270): camera, focal length and screen
+        centre of training image `view`."""
+        if not 0 <= int(view) < self._n_images:
+            raise NeusError(f"training view {view} out of range (0..{self._n_images - 1})")
+        self._render_view = int(view)
+
+    def reset_camera(self):
+        """Testbed::reset_camera (testbed.cu:272-285); only the training-view camera is supported for
+        rendering, so this clears it."""
+        self._render_view = None
+
+    def render(self, width: int = 1920, height: int = 1080, spp: int = 1, linear: bool = True, use_ema: bool = True):
+        """Testbed::render_to_cpu (python_api.cu:123-169) for the NeuS Shade mode: `spp` frames of
+        NerfTracer::trace accumulated in linear colour, returned as float32 [height, width, 4] with
+        premultiplied alpha. The background colour is composited as tonemap_kernel
+        (render_buffer.cu:474-500) does; linear=False returns sRGB."""
+        if self._render_view is None:
+            raise NeusError("render: call set_camera_to_training_view(view) first")
+        rq = _lib.NeusRenderRequest()
+        rq.width, rq.height, rq.spp = int(width), int(height), int(spp)
+        rq.training_view = self._render_view
+        rq.snap_to_pixel_centers = int(bool(self.snap_to_pixel_centers))
+        rq.min_transmittance = float(self.nerf.rendering_min_transmittance)
+        rq.use_ema = int(bool(use_ema))
+        out = np.empty((int(height), int(width), 4), np.float32)
+        it = C.c_uint32()
+        check(lib().neus_testbed_render(self._h, C.byref(rq), C.c_void_p(out.ctypes.data), C.byref(it)))
+        self.last_render_iterations = it.value
+        bg = np.asarray(self.background_color, np.float32)
+        if bg[3] != 0:
+            bgl = np.where(bg[:3] <= 0.04045, bg[:3] / 12.92, ((bg[:3] + 0.055) / 1.055) ** 2.4)
+            out[..., :3] += bgl * (1 - out[..., 3:4]) * bg[3]
+        if not linear:
+            out[..., :3] = linear_to_srgb(out[..., :3])
+        return out
 
     def train(self, batch_size: int | None = None):
         """Testbed::train(batch_size) (testbed.cu:2640-2736): ONE training step targeting `batch_size`

@@ -1242,4 +1242,184 @@ int or_num_threads() {
 #endif
 }
 
+
+// -------------------------------------------------------------------------------------------
+// Rendering of one camera (Testbed::render_to_cpu, python_api.cu:123-169, Shade mode): per spp
+// init_rays_with_payload_kernel_nerf + advance_pos_nerf (testbed_nerf.cu:2208-2330, 797-846), then
+// NerfTracer::trace (:2479-2600): compact alive rays, n_steps = clamp(n_init / n_alive, 1, 8),
+// generate_next_nerf_network_inputs (:877-934), network inference, composite_kernel_nerf (:936-1106),
+// shade_kernel_nerf (:2148-2181) for rays with alpha > 0.001; accumulate_kernel in linear colour
+// (render_buffer.cu:217-260). Pixel offsets: ld_random_pixel_offset (random_val.cuh:254-322).
+// -------------------------------------------------------------------------------------------
+static inline uint32_t or_rev(uint32_t x) {
+	x = ((x & 0xaaaaaaaau) >> 1) | ((x & 0x55555555u) << 1); x = ((x & 0xccccccccu) >> 2) | ((x & 0x33333333u) << 2);
+	x = ((x & 0xf0f0f0f0u) >> 4) | ((x & 0x0f0f0f0fu) << 4); x = ((x & 0xff00ff00u) >> 8) | ((x & 0x00ff00ffu) << 8);
+	return (x >> 16) | (x << 16);
+}
+static inline uint32_t or_lk(uint32_t x, uint32_t seed) {  // laine_karras_permutation (random_val.cuh:236-243)
+	x += seed; x ^= x * 0x6c50b47cu; x ^= x * 0xb82f1e52u; x ^= x * 0xc7afe638u; x ^= x * 0x8d22f6e6u; return x;
+}
+static inline uint32_t or_scr(uint32_t x, uint32_t seed) { return or_rev(or_lk(or_rev(x), seed)); }
+static inline uint32_t or_hc(uint32_t seed, uint32_t v) { return seed ^ (v + (seed << 6) + (seed >> 2)); }
+static uint32_t or_sobol(uint32_t index, uint32_t dim) {  // random_val.cuh:159-252, dimensions 0 and 1
+	static uint32_t D[2][32];
+	static bool init = false;
+	if (!init) {
+		uint32_t d = 0x80000000u;
+		for (int b = 0; b < 32; ++b) { D[0][b] = 0x80000000u >> b; D[1][b] = d; d ^= d >> 1; }
+		init = true;
+	}
+	uint32_t X = 0;
+	for (uint32_t bit = 0; bit < 32; ++bit) X ^= ((index >> bit) & 1) * D[dim][bit];
+	return X;
+}
+static float or_ld_random_val(uint32_t index, uint32_t seed) {
+	index = or_scr(index, seed);
+	return (float)or_scr(or_sobol(index, 0), or_hc(seed, 0)) * float(1.0 / 4294967296.0);
+}
+static void or_ld_random_val_2d(uint32_t index, uint32_t seed, float o[2]) {
+	index = or_scr(index, seed);
+	for (uint32_t i = 0; i < 2; ++i) o[i] = (float)or_scr(or_sobol(index, i), or_hc(seed, i)) * float(1.0 / 4294967296.0);
+}
+
+struct OrRenderCamera { float xform[12]; float focal[2], screen_center[2]; uint32_t width, height; };
+struct OrRay { V3 o, d; float t; bool alive; uint32_t idx, n_steps; float rgba[4]; };
+
+float or_ld_random_val_export(uint32_t index, uint32_t seed) { return or_ld_random_val(index, seed); }
+uint32_t or_sobol_export(uint32_t index, uint32_t dim) { return or_sobol(index, dim & 1); }
+void or_ld_random_val_2d_export(uint32_t index, uint32_t seed, float* o) { or_ld_random_val_2d(index, seed, o); }
+
+void or_render(const OrNetCfg* c, const float* params, uint32_t valid_level, const OrDataset* ds, const uint8_t* bitfield,
+               const OrRenderCamera* cam, uint32_t spp, int snap, float min_transmittance, float cos_anneal, float* rgba_out,
+               uint32_t* n_iterations) {
+	Net net(*c);
+	std::vector<float> P = half_params(net, params);
+	AABB bb{{ds->aabb_min[0], ds->aabb_min[1], ds->aabb_min[2]}, {ds->aabb_max[0], ds->aabb_max[1], ds->aabb_max[2]}};
+	const float diag[3] = {bb.mx.x - bb.mn.x, bb.mx.y - bb.mn.y, bb.mx.z - bb.mn.z};
+	const uint32_t W = cam->width, H = cam->height, N = W * H;
+	const float cone = ds->cone_angle;
+	std::vector<float> frame(4 * (size_t)N), accum(4 * (size_t)N, 0.f);
+	std::vector<OrRay> rays(N);
+	for (uint32_t sp = 0; sp < std::max(1u, spp); ++sp) {
+		float a0[2], a1[2], off[2];
+		or_ld_random_val_2d(0, 0xdeadbeefu, a0);
+		or_ld_random_val_2d(snap ? 0 : sp, 0xdeadbeefu, a1);
+		for (int k = 0; k < 2; ++k) { const float v = (0.5f - a0[k]) + a1[k]; off[k] = v - std::floor(v); }
+		std::fill(frame.begin(), frame.end(), 0.f);
+#pragma omp parallel for schedule(dynamic, 256)
+		for (int64_t ii = 0; ii < (int64_t)N; ++ii) {
+			const uint32_t idx = (uint32_t)ii, x = idx % W, y = idx / W;
+			OrRay& r = rays[idx];
+			r.idx = idx; r.n_steps = 0; r.rgba[0] = r.rgba[1] = r.rgba[2] = r.rgba[3] = 0.f;
+			const float u = ((float)x + off[0]) / (float)W, v = ((float)y + off[1]) / (float)H;
+			const float dc[3] = {(u - cam->screen_center[0]) * (float)W / cam->focal[0], (v - cam->screen_center[1]) * (float)H / cam->focal[1], 1.0f};
+			float du[3];
+			for (int k = 0; k < 3; ++k) du[k] = (cam->xform[4 * k] * dc[0] + cam->xform[4 * k + 1] * dc[1]) + cam->xform[4 * k + 2] * dc[2];
+			r.o = {cam->xform[3], cam->xform[7], cam->xform[11]};
+			const float nrm = std::sqrt((du[0] * du[0] + du[1] * du[1]) + du[2] * du[2]);
+			r.d = nrm > 0.f ? V3{du[0] / nrm, du[1] / nrm, du[2] / nrm} : V3{du[0], du[1], du[2]};
+			float tmin, tmax; ray_intersect(bb, r.o, r.d, tmin, tmax);
+			float t = std::fmax(tmin, 0.2f) + 1e-6f;  // NERF_RENDERING_NEAR_DISTANCE
+			r.alive = aabb_contains(bb, V3{r.o.x + t * r.d.x, r.o.y + t * r.d.y, r.o.z + t * r.d.z});
+			if (r.alive) {  // advance_pos_nerf
+				const V3 idir = {1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z};
+				t += or_ld_random_val(sp, idx * 786433u) * calc_dt(t, cone);
+				while (true) {
+					const V3 pos = {r.o.x + t * r.d.x, r.o.y + t * r.d.y, r.o.z + t * r.d.z};
+					if (!aabb_contains(bb, pos)) { r.alive = false; break; }
+					const float dt = calc_dt(t, cone);
+					const uint32_t mip = (uint32_t)mip_from_dt(dt, pos);
+					if (density_grid_occupied_at(pos, bitfield, mip)) break;
+					t = advance_to_next_voxel(t, cone, pos, r.d, idir, NERF_GRIDSIZE >> mip);
+				}
+			}
+			r.t = t;
+		}
+		std::vector<uint32_t> alive;
+		for (uint32_t i = 0; i < N; ++i) if (rays[i].alive) alive.push_back(i);
+		uint32_t iters = 0;
+		for (uint32_t it = 1; it < 10000;) {  // MARCH_ITER
+			std::vector<uint32_t> next;
+			for (uint32_t id : alive) if (rays[id].alive) next.push_back(id);
+			alive.swap(next);
+			const uint32_t n_alive = (uint32_t)alive.size();
+			if (n_alive == 0) break;
+			const uint32_t n_steps = std::min(8u, std::max(1u, N / n_alive));
+#pragma omp parallel for schedule(dynamic, 64)
+			for (int64_t q = 0; q < (int64_t)n_alive; ++q) {
+				OrRay& r = rays[alive[q]];
+				const V3 idir = {1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z};
+				const float wd[3] = {(r.d.x + 1.0f) * 0.5f, (r.d.y + 1.0f) * 0.5f, (r.d.z + 1.0f) * 0.5f};
+				// generate_next_nerf_network_inputs
+				float coords[8][7];
+				uint32_t j = 0;
+				float t = r.t;
+				bool exited = false;
+				for (; j < n_steps; ++j) {
+					V3 pos; float dt;
+					while (true) {
+						pos = {r.o.x + t * r.d.x, r.o.y + t * r.d.y, r.o.z + t * r.d.z};
+						if (!aabb_contains(bb, pos)) { exited = true; break; }
+						dt = calc_dt(t, cone);
+						const uint32_t mip = (uint32_t)mip_from_dt(dt, pos);
+						if (density_grid_occupied_at(pos, bitfield, mip)) break;
+						t = advance_to_next_voxel(t, cone, pos, r.d, idir, NERF_GRIDSIZE >> mip);
+					}
+					if (exited) break;
+					float* cc = coords[j];
+					cc[0] = (pos.x - bb.mn.x) / diag[0]; cc[1] = (pos.y - bb.mn.y) / diag[1]; cc[2] = (pos.z - bb.mn.z) / diag[2];
+					cc[3] = warp_dt(dt); cc[4] = wd[0]; cc[5] = wd[1]; cc[6] = wd[2];
+					t += dt;
+				}
+				r.n_steps = j;
+				if (!exited) r.t = t;
+				// inference + composite_kernel_nerf
+				uint32_t k = 0;
+				for (; k < r.n_steps; ++k) {
+					uint16_t lo[16]; Ctx cx;
+					net_forward_one(net, P.data(), coords[k], valid_level, cx, lo);
+					const float T = 1.f - r.rgba[3];
+					const float dt = unwarp_dt(coords[k][3]);
+					float u3[3]; for (int e = 0; e < 3; ++e) u3[e] = h2f(lo[8 + e]) * 2.0f - 1.0f;
+					const float nr = std::sqrt((u3[0] * u3[0] + u3[1] * u3[1]) + u3[2] * u3[2]);
+					float dir[3]; for (int e = 0; e < 3; ++e) dir[e] = nr > 0 ? u3[e] / nr : u3[e];
+					const float inv_s = det_expf(rh(10.0f * h2f(lo[7])));
+					const float sdf = h2f(lo[3]);
+					const float pg[3] = {h2f(lo[4]), h2f(lo[5]), h2f(lo[6])};
+					const float true_cos = dir[0] * pg[0] + dir[1] * pg[1] + dir[2] * pg[2];
+					float b1 = (float)(-true_cos * 0.5 + 0.5); b1 = b1 > 0.0f ? b1 : 0.0f;
+					float b2 = -true_cos; b2 = b2 > 0.0f ? b2 : 0.0f;
+					const float iter_cos = -(b1 * (1.0 - cos_anneal) + b2 * cos_anneal);
+					const float next_sdf = sdf + iter_cos * dt * 0.5;
+					const float prev_sdf = sdf - iter_cos * dt * 0.5;
+					const float next_cdf = det_logistic(next_sdf * inv_s), prev_cdf = det_logistic(prev_sdf * inv_s);
+					const float p = prev_cdf - next_cdf, cc = prev_cdf;
+					const float alpha = clampf((p + 1e-5f) / (cc + 1e-5f), 0.0f, 1.0f);
+					const float weight = alpha * T;
+					for (int e = 0; e < 3; ++e) r.rgba[e] += det_logistic(h2f(lo[e])) * weight;
+					r.rgba[3] += weight;
+					if (r.rgba[3] > (1.0f - min_transmittance)) {
+						const float w = r.rgba[3];
+						for (int e = 0; e < 4; ++e) r.rgba[e] /= w;
+						break;
+					}
+				}
+				if (k < n_steps) {
+					r.alive = false;
+					if (r.rgba[3] > 0.001f) {
+						float* f = &frame[4 * (size_t)r.idx];
+						for (int e = 0; e < 3; ++e) f[e] = srgb_to_linear(r.rgba[e]);
+						f[3] = r.rgba[3];
+					}
+				}
+			}
+			it += n_steps;
+			++iters;
+		}
+		if (n_iterations) *n_iterations = iters;
+		const float s = (float)sp;
+		for (size_t i = 0; i < 4 * (size_t)N; ++i) accum[i] = (accum[i] * s + frame[i]) / (s + 1);
+	}
+	std::memcpy(rgba_out, accum.data(), accum.size() * sizeof(float));
+}
 } // extern "C"

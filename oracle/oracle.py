@@ -240,3 +240,41 @@ def det_expf(x):
 
 def num_threads():
     return lib().or_num_threads()
+
+
+class OrRenderCamera(C.Structure):
+    _fields_ = [("xform", C.c_float * 12), ("focal", C.c_float * 2), ("screen_center", C.c_float * 2),
+                ("width", C.c_uint32), ("height", C.c_uint32)]
+
+
+def render(cfg, params, valid_level, ds, bitfield, xform, focal, screen_center, width, height, spp=1, snap=True,
+           min_transmittance=1e-4, cos_anneal=1.0):
+    """CPU restatement of Testbed::render_to_cpu (Shade mode): float32 [H, W, 4] linear premultiplied."""
+    cam = OrRenderCamera()
+    cam.xform[:] = [float(v) for v in np.asarray(xform, np.float32).reshape(12)]
+    cam.focal[:] = [float(v) for v in np.asarray(focal).reshape(2)]
+    cam.screen_center[:] = [float(v) for v in np.asarray(screen_center).reshape(2)]
+    cam.width, cam.height = int(width), int(height)
+    out = np.zeros((int(height), int(width), 4), np.float32)
+    it = C.c_uint32()
+    params = f32(params)
+    bitfield = np.ascontiguousarray(bitfield, np.uint8)
+    lib().or_render(C.byref(cfg), P(params), C.c_uint32(valid_level), C.byref(ds.c), P(bitfield), C.byref(cam),
+                    C.c_uint32(spp), C.c_int(int(bool(snap))), C.c_float(min_transmittance), C.c_float(cos_anneal), P(out), C.byref(it))
+    return out, int(it.value)
+
+
+def ld_random_val(index, seed):
+    lib().or_ld_random_val_export.restype = C.c_float
+    return float(lib().or_ld_random_val_export(C.c_uint32(index), C.c_uint32(seed)))
+
+
+def ld_random_val_2d(index, seed):
+    o = np.zeros(2, np.float32)
+    lib().or_ld_random_val_2d_export(C.c_uint32(index), C.c_uint32(seed), P(o))
+    return o
+
+
+def sobol(index, dim):
+    lib().or_sobol_export.restype = C.c_uint32
+    return int(lib().or_sobol_export(C.c_uint32(index), C.c_uint32(dim)))

@@ -114,3 +114,24 @@ def test_cpu_trainer_step_counters():
     r = int(np.float32(512) * np.float32(512) / np.float32(meas))
     assert tr.R == min((r + 127) // 128 * 128, 1 << 18)
     assert not np.array_equal(tr.params, p0)
+
+
+def test_eval_psnr_matches_render_utils_formula():
+    """pyngp.eval_psnr restates render_img_training_view's metric (render_utils.py:252-359): the 8-bit
+    reference (sRGB, alpha) premultiplied in linear space, re-composited on a black background in sRGB,
+    PSNR = mse2psnr(mean((clip(srgb(pred)) - clip(srgb(gt)))^2))."""
+    import numpy as np
+    from neus2_amd import pyngp
+    rng = np.random.default_rng(0)
+    rgba8 = rng.integers(0, 256, (6, 5, 4)).astype(np.uint8)
+    s = rgba8[..., :3] / 255.0
+    a = rgba8[..., 3:4] / 255.0
+    gt_srgb = s * a  # black background: sRGB colour times alpha
+    pred = pyngp.srgb_to_linear(np.clip(gt_srgb + 0.05, 0, 1)).astype(np.float32)
+    pred = np.concatenate([pred, a.astype(np.float32)], -1)
+    psnr, mse = pyngp.eval_psnr(pred, rgba8)
+    want = np.mean((np.clip(gt_srgb + 0.05, 0, 1) - gt_srgb) ** 2)
+    assert abs(mse - want) < 1e-6
+    assert abs(psnr - (-10 * np.log10(want))) < 1e-3
+    exact = np.concatenate([pyngp.srgb_to_linear(gt_srgb), a], -1).astype(np.float32)
+    assert pyngp.eval_psnr(exact, rgba8)[0] > 60

@@ -268,3 +268,47 @@ def test_neus_loss_gradient_vs_autograd():
         np.testing.assert_allclose(go[:, 4:7], ek, rtol=2e-3, atol=1e-3 * np.abs(ek).max())
         n_checked += 1
     assert n_checked >= 10, n_checked
+
+
+def test_sobol_direction_numbers_match_reference_table():
+    """random_val.cuh:160-200: dimension 0 is the bit reversal; the first 16 dimension-1 direction
+    numbers of the reference's table (sobol(2^b, 1) = directions[1][b])."""
+    dim1 = [0x80000000, 0xc0000000, 0xa0000000, 0xf0000000, 0x88000000, 0xcc000000, 0xaa000000, 0xff000000,
+            0x80800000, 0xc0c00000, 0xa0a00000, 0xf0f00000, 0x88880000, 0xcccc0000, 0xaaaa0000, 0xffff0000]
+    for b in range(32):
+        assert O.sobol(1 << b, 0) == 1 << (31 - b)
+    for b, want in enumerate(dim1):
+        assert O.sobol(1 << b, 1) == want
+    # XOR-linearity of a digital sequence
+    assert O.sobol(0b1011, 1) == dim1[0] ^ dim1[1] ^ dim1[3]
+
+
+def test_ld_random_val_properties():
+    """ld_random_val (random_val.cuh:284-288): values in [0,1), and the 2-D variant's dimension 0 equals
+    the 1-D value (both scramble index, then sobol dim 0 with hash_combine(seed, 0))."""
+    vals = [O.ld_random_val(i, 786433 * 7) for i in range(64)]
+    assert all(0.0 <= v < 1.0 for v in vals)
+    assert len(set(vals)) == 64
+    for i in range(8):
+        assert O.ld_random_val_2d(i, 0xdeadbeef)[0] == np.float32(O.ld_random_val(i, 0xdeadbeef))
+
+
+def test_oracle_render_small_scene():
+    """Oracle render (render_to_cpu restatement) of the small sphere scene with geometric-init weights:
+    finite, premultiplied colour <= alpha <= 1, more coverage at the image centre than in the corners
+    (the geometric init is a sphere SDF around the aabb centre), deterministic."""
+    from neus2_amd import scenes
+    sc = scenes.small_scene(n_views=2, width=32, height=24)
+    cfg = O.make_cfg(n_levels=4, per_level_scale=1.5)
+    params = O.init_params(cfg, 1337, geo=True)
+    ds = O.Dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"])
+    bf = np.full(128 ** 3 // 8 * 8, 0xff, np.uint8)
+    args = (cfg, params, 4, ds, bf, sc["xforms"][0], np.asarray(sc["focal"][0]) * 24 / 48, sc["principal"][0], 32, 24)
+    img, iters = O.render(*args, spp=1)
+    img2, _ = O.render(*args, spp=1)
+    assert iters > 0
+    assert np.isfinite(img).all()
+    np.testing.assert_array_equal(img, img2)
+    a = img[..., 3]
+    assert (a >= 0).all() and (a <= 1 + 1e-6).all()
+    assert a[8:16, 12:20].mean() > a[:4, :4].mean()
