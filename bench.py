@@ -40,6 +40,8 @@ def parse():
     p.add_argument("--rays", type=int, default=1 << 18)
     p.add_argument("--cpu-baseline", type=int, default=1)
     p.add_argument("--cpu-steps", type=int, default=8)
+    # quality half of the metric: PSNR after this many steps of the reference's (adaptive-R) training, N=1 only
+    p.add_argument("--psnr-steps", type=int, default=20000)
     return p.parse_args()
 
 
@@ -161,6 +163,9 @@ def main():
         "loss": st["ray_loss"],
         "warmup_s": warm_s,
     }
+    if world == 1 and args.psnr_steps > 0:
+        del tb
+        out["psnr"] = psnr_leg(sc, args.psnr_steps)
     if rank == 0 and args.cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(sc, args.cpu_steps)
     if rank == 0:
@@ -168,6 +173,36 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+
+
+def psnr_leg(sc, n_steps):
+    """PSNR@n_steps (BASELINE.json metric, second half) with the reference's training (adaptive rays per
+    batch, Nc = 2^18) and evaluation protocol (render_utils.py:252-359: view 0, spp 8, black background,
+    pixel centres, min transmittance 1e-4, EMA weights); scripts/psnr_run.py is the standalone version."""
+    from neus2_amd import pyngp
+    tb = pyngp.Testbed(pyngp.TestbedMode.Nerf)
+    tb.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
+    tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"))
+    t0 = time.perf_counter()
+    done = 0
+    while done < n_steps:
+        k = min(2000, n_steps - done)
+        tb.train_steps(k)
+        done += k
+        tb.synchronize()  # also a progress point for long runs
+    train_s = time.perf_counter() - t0
+    tb.background_color = [0.0, 0.0, 0.0, 0.0]
+    tb.snap_to_pixel_centers = True
+    tb.nerf.rendering_min_transmittance = 1e-4
+    tb.set_camera_to_training_view(0)
+    gt = sc["images"][0]
+    t1 = time.perf_counter()
+    img = tb.render(gt.shape[1], gt.shape[0], spp=8)
+    render_s = time.perf_counter() - t1
+    psnr, _ = pyngp.eval_psnr(img, gt)
+    return {"value": round(float(psnr), 3), "unit": "dB", "steps": n_steps, "train_wall_s": round(train_s, 2),
+            "render_s": round(render_s, 3), "protocol": "view 0, spp 8, black bg, snap_to_pixel_centers, min_T 1e-4, EMA weights",
+            "training": "reference schedule: adaptive rays/batch, Nc=2^18, base.json"}
 
 
 def cpu_baseline(sc, n_steps):

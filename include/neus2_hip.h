@@ -17,6 +17,9 @@
  *     neus_testbed_{get,set}_params    Trainer params / serialize             trainer.h:72-109, 281-300
  *     neus_testbed_{get,set}_density_grid  Nerf::density_grid(_bitfield)      testbed.h:688-694
  *     neus_testbed_render              Testbed::render_to_cpu -> render_nerf / NerfTracer::trace  python_api.cu:123-169, testbed_nerf.cu:2397-2760
+ *     neus_testbed_sdf_on_grid         Testbed::get_density_on_grid          testbed_nerf.cu:4096-4139
+ *     neus_testbed_marching_cubes      Testbed::marching_cubes / marching_cubes_gpu  testbed_nerf.cu:4175-4226, marching_cubes.cu:794-822
+ *     neus_testbed_get_mesh            Testbed::compute_marching_cubes_mesh (V, F)   python_api.cu:99-121
  *     neus_testbed_init_data_parallel  (new) RCCL data parallelism over ray batches
  *
  *   Operator surface (my_tcnn DifferentiableObject / cpp_api.h:66-106 for the NerfNetwork, plus
@@ -141,6 +144,20 @@ int neus_testbed_set_density_grid(NeusTestbed* tb, const float* grid /*nullable*
 /* rgba_out: height*width*4 floats, linear colour, premultiplied alpha (the reference's render(..., linear=True)).
  * n_iterations (nullable): march/composite iterations of the last spp. */
 int neus_testbed_render(NeusTestbed* tb, const NeusRenderRequest* req, float* rgba_out, uint32_t* n_iterations);
+/* get_density_on_grid (testbed_nerf.cu:4096-4139): raw SDF (inference/EMA weights) at the res[0]*res[1]*res[2]
+ * points x/res * (aabb_max - aabb_min) + aabb_min, x fastest; host_out gets the floats. */
+int neus_testbed_sdf_on_grid(NeusTestbed* tb, const int32_t res[3], const float aabb_min[3], const float aabb_max[3], float* host_out);
+/* Testbed::marching_cubes (testbed_nerf.cu:4175-4226): res rounded up to multiples of 16, SDF grid, mesh at
+ * `thresh` (0 for NeuS). With density_dev (device pointer, res^3 floats, x fastest) the grid is taken as
+ * given and res is used unrounded. Deterministic vertex / triangle order. */
+int neus_testbed_marching_cubes(NeusTestbed* tb, const int32_t res[3], const float aabb_min[3], const float aabb_max[3], float thresh,
+                                const float* density_dev, uint32_t* n_verts, uint32_t* n_tris);
+/* The last mesh: verts n_verts x 3 f32, tris n_tris x 3 u32 (host buffers, nullable). */
+int neus_testbed_get_mesh(NeusTestbed* tb, float* verts, uint32_t* tris);
+/* compute_mesh_vertex_colors (testbed_nerf.cu:4071-4094): n_verts x 3 f32 sRGB colours of the last mesh. */
+int neus_testbed_mesh_vertex_colors(NeusTestbed* tb, float* rgb);
+/* The marching-cubes case table the kernels use: 256 rows x 19 int8 (edge triples, -1 terminated). */
+int neus_mc_table(int8_t* out);
 int neus_testbed_get_rng(NeusTestbed* tb, uint64_t* state_inc /*4: rng, density_grid_rng*/);
 /* Per-ray counters of the last step (first n rays, host buffers, each nullable): samples requested by
  * the march, samples composited before transmittance < 1e-4, and numsteps = (compacted count, base). */

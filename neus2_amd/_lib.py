@@ -65,7 +65,8 @@ EXPORTS = [
     "neus_testbed_create", "neus_testbed_destroy", "neus_testbed_set_dataset", "neus_testbed_reload_network",
     "neus_testbed_layout", "neus_testbed_train", "neus_testbed_get_stats", "neus_testbed_get_params",
     "neus_testbed_set_params", "neus_testbed_get_gradients", "neus_testbed_get_ema_params",
-    "neus_testbed_get_density_grid", "neus_testbed_set_density_grid", "neus_testbed_get_rng", "neus_testbed_render", "neus_testbed_ray_counts", "neus_debug_time_kernel", "neus_debug_march_stats", "neus_testbed_time_kernel", "neus_testbed_stream",
+    "neus_testbed_get_density_grid", "neus_testbed_set_density_grid", "neus_testbed_get_rng", "neus_testbed_render", "neus_testbed_sdf_on_grid",
+    "neus_testbed_marching_cubes", "neus_testbed_get_mesh", "neus_testbed_mesh_vertex_colors", "neus_mc_table", "neus_testbed_ray_counts", "neus_debug_time_kernel", "neus_debug_march_stats", "neus_testbed_time_kernel", "neus_testbed_stream",
     "neus_testbed_synchronize", "neus_testbed_set_profiling", "neus_testbed_kernel_times",
     "neus_nccl_unique_id", "neus_testbed_init_data_parallel",
     "neus_grid_encode", "neus_net_forward", "neus_net_backward", "neus_sample_rays", "neus_loss_compact",
@@ -82,7 +83,7 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
-    l = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+    l = C.CDLL(LIB_PATH)
     l.neus_last_error.restype = C.c_char_p
     for name in EXPORTS:
         f = getattr(l, name)

@@ -114,6 +114,10 @@ void launch_nerf_infer(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_
                        uint32_t valid_level, const half_t* grid, const MlpPtrs& w, half_t* out, uint32_t blocks);
 void launch_nerf_density(hipStream_t s, uint32_t L, uint32_t W, uint32_t n, const float* pos, const GridLevels& gl, uint32_t valid_level,
                          const half_t* grid, const MlpPtrs& w, float* density);
+// raw SDF on a uniform grid (marching cubes input), grid points offset .. offset + n - 1 (x fastest)
+void launch_sdf_grid(hipStream_t s, uint32_t L, uint32_t W, const uint32_t res[3], const float render_min[3], const float render_max[3],
+                     const float train_min[3], const float train_max[3], uint64_t offset, uint32_t n, const GridLevels& gl, uint32_t valid_level,
+                     const half_t* grid, const MlpPtrs& w, float* sdf);
 void launch_mlp_train(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_valid_ptr, uint32_t n, uint32_t ld, const float* coords,
                       const half_t* enc, const float* dydx, const half_t* dL_dout, const MlpPtrs& w, const TrainBufs& tb);
 void launch_wgrad(hipStream_t s, const WGradJobs& jobs, uint32_t n_blocks);
@@ -150,6 +154,14 @@ void launch_render_gen(hipStream_t s, uint32_t n_alive, uint32_t n_steps, const 
 void launch_render_composite(hipStream_t s, uint32_t n_alive, uint32_t n_steps, const float* coords, const half_t* net_out, float cos_anneal,
                              float min_transmittance, void* rays, float4* frame);
 void launch_render_accumulate(hipStream_t s, uint32_t n, uint32_t spp, const float4* frame, float4* accum);
+// mc.hip (marching cubes over a density grid; chunked, deterministic)
+uint32_t mc_n_chunks(const uint32_t res[3]);
+void mc_table_host(int8_t* out /* 256 x 19 */);
+void launch_mc_count(hipStream_t s, const uint32_t res[3], const float amin[3], const float amax[3], float thresh, const float* density,
+                     uint32_t* cnt_v, uint32_t* cnt_t);
+void launch_mc_emit(hipStream_t s, const uint32_t res[3], const float amin[3], const float amax[3], float thresh, const float* density,
+                    const uint32_t* off_v, const uint32_t* off_t, float* verts, uint32_t* vidx, uint32_t* tris);
+void launch_mesh_coords(hipStream_t s, uint32_t n, const float* verts, const DevDataset& ds, float* coords);
 // scan.hip
 size_t scan_temp_bytes(uint32_t n);
 void launch_exclusive_scan(hipStream_t s, void* temp, size_t temp_bytes, const uint32_t* in, uint32_t* out, uint32_t n);

@@ -631,9 +631,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))
 // Density-only inference for the occupancy grid (NerfNetwork::density, nerf_network.h:656-739;
 // sdf_to_density_variance_buffer, common_operation.cuh:306-324 in fp16 arithmetic), with the
 // hash-grid encode fused in (no dy/dx needed).
-template <int L, int W>
-__global__ void __launch_bounds__(256) k_nerf_density(uint32_t n, const float* __restrict__ pos, const GridLevels gl, uint32_t valid_level,
-                                                      const half_t* __restrict__ grid, MlpPtrs wp, float* __restrict__ density) {
+// MODE 0: occupancy density of the positions in `pos` (AoS 3 f32).
+// MODE 1: raw SDF (NerfNetwork::sdf, nerf_network.h:656-722 -> grid_samples_half_to_float, testbed_nerf.cu:692-708)
+//         at the points of a uniform grid generated in-kernel (generate_grid_samples_nerf_uniform,
+//         testbed_nerf.cu:596-609: p = x * (1/res) * (aabb.max - aabb.min) + aabb.min, nvcc-contracted to an
+//         FMA, then warp_position into the training aabb); density[i] = float(sdf + bias) for grid point
+//         offset + i. No 12-B position buffer: 1024^3 points read nothing but the grid table.
+struct UniformGrid { uint32_t res[3]; float inv_res[3], rmin[3], rdiag[3], tmin[3], tdiag[3]; uint64_t offset; };
+
+template <int L, int W, int MODE>
+__global__ void __launch_bounds__(256) k_nerf_density(uint32_t n, const float* __restrict__ pos, const UniformGrid ug, const GridLevels gl,
+                                                      uint32_t valid_level, const half_t* __restrict__ grid, MlpPtrs wp, float* __restrict__ density) {
 	constexpr int DKS = Dims<L>::DKS, M0 = Fused<L>::M0, MT = (W + 31) / 32, HKS = W / 16;
 	__shared__ half_t sm[FwdSmem<L, W>::END];
 	__shared__ LevelSmem s_lvl;
@@ -650,7 +658,21 @@ __global__ void __launch_bounds__(256) k_nerf_density(uint32_t n, const float* _
 		const uint32_t i = base + r;
 		const bool valid = i < n;
 		const uint32_t ic = valid ? i : 0;
-		const float x[3] = {pos[3 * (size_t)ic], pos[3 * (size_t)ic + 1], pos[3 * (size_t)ic + 2]};
+		float x[3];
+		if (MODE == 0) {
+			x[0] = pos[3 * (size_t)ic]; x[1] = pos[3 * (size_t)ic + 1]; x[2] = pos[3 * (size_t)ic + 2];
+		} else {
+			const uint64_t g = ug.offset + ic;
+			const uint64_t rxy = (uint64_t)ug.res[0] * ug.res[1];
+			const uint32_t gz = (uint32_t)(g / rxy), gy = (uint32_t)((g - gz * rxy) / ug.res[0]);
+			const uint32_t gx = (uint32_t)(g - gz * rxy - (uint64_t)gy * ug.res[0]);
+			const uint32_t gi[3] = {gx, gy, gz};
+#pragma unroll
+			for (int k = 0; k < 3; ++k) {
+				const float pk = __builtin_fmaf(__fmul_rn((float)gi[k], ug.inv_res[k]), ug.rdiag[k], ug.rmin[k]);
+				x[k] = __fdiv_rn(__fsub_rn(pk, ug.tmin[k]), ug.tdiag[k]);
+			}
+		}
 		h2 ev[M0];
 		float dy[1][2][3];
 		fused_levels<L, false>(s_lvl, gl.dense_bits, valid_level, grid, x, h, ev, dy);
@@ -673,7 +695,9 @@ __global__ void __launch_bounds__(256) k_nerf_density(uint32_t n, const float* _
 		f16v acc = zero16();
 #pragma unroll
 		for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.d1, 16, r, 16 * ks, h), H0B[ks], acc);
-		if (valid && h == 0) {
+		if (MODE == 1) {
+			if (valid && h == 0) density[i] = (float)((half_t)acc[0] + bias_h);
+		} else if (valid && h == 0) {
 			const half_t sdf = (half_t)acc[0] + bias_h;
 			const half_t s = (half_t)__expf((float)(var_h * (half_t)10.0f));
 			const half_t sig = (half_t)(1.0f / (1.0f + __expf(-(float)(sdf * s))));
@@ -1113,7 +1137,23 @@ void launch_nerf_density(hipStream_t s, uint32_t L, uint32_t W, uint32_t n, cons
                          const half_t* grid, const MlpPtrs& w, float* density) {
 	const uint32_t blocks = std::min<uint32_t>((n + 127) / 128, 8192);
 	if (n == 0) return;
-#define X(l, w_) if (L == l && W == w_) { k_nerf_density<l, w_><<<blocks, 256, 0, s>>>(n, pos, gl, valid_level, grid, w, density); return; }
+#define X(l, w_) if (L == l && W == w_) { k_nerf_density<l, w_, 0><<<blocks, 256, 0, s>>>(n, pos, UniformGrid{}, gl, valid_level, grid, w, density); return; }
+	NEUS_MLP_CONFIGS(X)
+#undef X
+}
+void launch_sdf_grid(hipStream_t s, uint32_t L, uint32_t W, const uint32_t res[3], const float render_min[3], const float render_max[3],
+                     const float train_min[3], const float train_max[3], uint64_t offset, uint32_t n, const GridLevels& gl, uint32_t valid_level,
+                     const half_t* grid, const MlpPtrs& w, float* sdf) {
+	if (n == 0) return;
+	UniformGrid ug{};
+	for (int k = 0; k < 3; ++k) {
+		ug.res[k] = res[k]; ug.inv_res[k] = 1.f / (float)res[k];
+		ug.rmin[k] = render_min[k]; ug.rdiag[k] = render_max[k] - render_min[k];
+		ug.tmin[k] = train_min[k]; ug.tdiag[k] = train_max[k] - train_min[k];
+	}
+	ug.offset = offset;
+	const uint32_t blocks = std::min<uint32_t>((n + 127) / 128, 16384);
+#define X(l, w_) if (L == l && W == w_) { k_nerf_density<l, w_, 1><<<blocks, 256, 0, s>>>(n, nullptr, ug, gl, valid_level, grid, w, sdf); return; }
 	NEUS_MLP_CONFIGS(X)
 #undef X
 }

@@ -127,6 +127,12 @@ struct NeusTestbed {
 	Dev<half_t> r_out;
 	Dev<float4> r_frame, r_accum;
 	size_t r_scan_bytes = 0;
+	// marching cubes workspace and the last mesh (Testbed::m_mesh, testbed.h:596-610)
+	Dev<float> mc_density, mesh_v;
+	Dev<uint32_t> mc_vidx, mc_cnt, mesh_f;
+	Dev<uint8_t> mc_scan_tmp;
+	size_t mc_scan_bytes = 0;
+	uint32_t mesh_nv = 0, mesh_nt = 0;
 	// occupancy grid
 	Dev<float> density_grid, density_tmp, grid_mean, grid_partial, occ_pos, occ_density;
 	Dev<uint32_t> occ_idx;
@@ -589,6 +595,78 @@ struct NeusTestbed {
 		return iters;
 	}
 
+	// ------------------------------------------------------------ marching cubes (testbed_nerf.cu:4096-4226)
+	// get_density_on_grid: raw SDF of the inference (EMA) weights at every grid point, written to dst.
+	void sdf_on_grid(const uint32_t res[3], const float amin[3], const float amax[3], float* dst) {
+		if (!have_net) throw std::runtime_error("sdf_on_grid: no network");
+		prepare_weights_for(mlp_ema);
+		const uint64_t n = (uint64_t)res[0] * res[1] * res[2];
+		const uint32_t valid = valid_level_at((int)training_step);
+		for (uint64_t off = 0; off < n; off += (1ull << 30)) {
+			const uint32_t cnt = (uint32_t)std::min<uint64_t>(n - off, 1ull << 30);
+			launch_sdf_grid(stream, lay.L, lay.W, res, amin, amax, ds.aabb_min, ds.aabb_max, off, cnt, gl, valid, ema_h.p + lay.grid_off, mlp_ema,
+			                dst + off);
+		}
+	}
+	// Testbed::marching_cubes: SDF grid (unless a device density grid is given), then the deterministic
+	// count / scan / emit passes of mc.hip. The mesh stays on the device until get_mesh.
+	void marching_cubes(const int32_t res_in[3], const float amin[3], const float amax[3], float thresh, const float* density_dev) {
+		uint32_t res[3];
+		for (int k = 0; k < 3; ++k) {
+			if (res_in[k] < 2) throw std::runtime_error("marching_cubes: resolution must be >= 2");
+			res[k] = density_dev ? (uint32_t)res_in[k] : next_multiple((uint32_t)res_in[k], 16u);  // testbed_nerf.cu:4176-4178
+		}
+		const uint64_t n = (uint64_t)res[0] * res[1] * res[2];
+		if (n >= (1ull << 36)) throw std::runtime_error("marching_cubes: grid too large");
+		hipStream_t s = stream;
+		const float* d = density_dev;
+		if (!d) {
+			mc_density.alloc(n);
+			sdf_on_grid(res, amin, amax, mc_density.p);
+			d = mc_density.p;
+		}
+		const uint32_t nc = mc_n_chunks(res);
+		mc_cnt.alloc(4 * (size_t)nc + 4);
+		uint32_t *cv = mc_cnt.p, *ct = cv + nc, *ov = ct + nc, *ot = ov + nc;
+		launch_mc_count(s, res, amin, amax, thresh, d, cv, ct);
+		const size_t sb = scan_temp_bytes(nc);
+		if (sb > mc_scan_bytes || !mc_scan_tmp.p) { mc_scan_tmp.alloc(sb + 256); mc_scan_bytes = sb; }
+		launch_exclusive_scan(s, mc_scan_tmp.p, mc_scan_bytes, cv, ov, nc);
+		launch_exclusive_scan(s, mc_scan_tmp.p, mc_scan_bytes, ct, ot, nc);
+		uint32_t last[4];
+		HIP_CHECK(hipMemcpyAsync(pinned + 40, cv + nc - 1, 4, hipMemcpyDeviceToHost, s));
+		HIP_CHECK(hipMemcpyAsync(pinned + 41, ct + nc - 1, 4, hipMemcpyDeviceToHost, s));
+		HIP_CHECK(hipMemcpyAsync(pinned + 42, ov + nc - 1, 4, hipMemcpyDeviceToHost, s));
+		HIP_CHECK(hipMemcpyAsync(pinned + 43, ot + nc - 1, 4, hipMemcpyDeviceToHost, s));
+		HIP_CHECK(hipStreamSynchronize(s));
+		std::memcpy(last, pinned + 40, 16);
+		const uint64_t nv = (uint64_t)last[2] + last[0], nt = (uint64_t)last[3] + last[1];
+		if (nv >= (1ull << 32) || 3 * nt >= (1ull << 32)) throw std::runtime_error("marching_cubes: mesh exceeds 32-bit indices");
+		mesh_v.alloc(3 * std::max<uint64_t>(nv, 1));
+		mc_vidx.alloc(n);
+		mesh_f.alloc(3 * std::max<uint64_t>(nt, 1));
+		launch_mc_emit(s, res, amin, amax, thresh, d, ov, ot, mesh_v.p, mc_vidx.p, mesh_f.p);
+		HIP_CHECK(hipStreamSynchronize(s));
+		mesh_nv = (uint32_t)nv; mesh_nt = (uint32_t)nt;
+	}
+
+	// compute_mesh_vertex_colors (testbed_nerf.cu:4071-4094): network colour (inference weights) at each vertex,
+	// looking outward from the aabb centre; sRGB (the network is trained on sRGB targets).
+	void mesh_colors(float* host_rgb) {
+		if (!mesh_nv) return;
+		prepare_weights_for(mlp_ema);
+		Dev<float> c; Dev<half_t> o;
+		c.alloc((size_t)mesh_nv * COORD_W); o.alloc((size_t)mesh_nv * OUT_W);
+		launch_mesh_coords(stream, mesh_nv, mesh_v.p, ds, c.p);
+		launch_nerf_infer(stream, lay.L, lay.W, nullptr, mesh_nv, c.p, gl, valid_level_at((int)training_step), ema_h.p + lay.grid_off, mlp_ema, o.p,
+		                  std::max<uint32_t>(1, std::min<uint32_t>((mesh_nv + 127) / 128, 8192)));
+		std::vector<half_t> h((size_t)mesh_nv * OUT_W);
+		HIP_CHECK(hipMemcpyAsync(h.data(), o.p, h.size() * sizeof(half_t), hipMemcpyDeviceToHost, stream));
+		HIP_CHECK(hipStreamSynchronize(stream));
+		for (size_t i = 0; i < mesh_nv; ++i)
+			for (int k = 0; k < 3; ++k) host_rgb[3 * i + k] = 1.0f / (1.0f + std::exp(-(float)h[i * OUT_W + k]));
+	}
+
 	// ------------------------------------------------------------ one Testbed::train step (testbed.cu:2640-2736)
 	void train_step() {
 		if (!have_net) throw std::runtime_error("train: no network (reload_network first)");
@@ -802,6 +880,42 @@ int neus_testbed_render(NeusTestbed* tb, const NeusRenderRequest* rq, float* rgb
 		if (n_iterations) *n_iterations = it;
 	});
 }
+int neus_testbed_sdf_on_grid(NeusTestbed* tb, const int32_t res[3], const float aabb_min[3], const float aabb_max[3], float* host_out) {
+	return guard([&] {
+		HIP_CHECK(hipSetDevice(tb->device));
+		uint32_t r[3];
+		for (int k = 0; k < 3; ++k) { if (res[k] < 1) throw std::runtime_error("sdf_on_grid: empty resolution"); r[k] = (uint32_t)res[k]; }
+		const uint64_t n = (uint64_t)r[0] * r[1] * r[2];
+		tb->mc_density.alloc(n);
+		tb->sdf_on_grid(r, aabb_min, aabb_max, tb->mc_density.p);
+		HIP_CHECK(hipMemcpyAsync(host_out, tb->mc_density.p, n * 4, hipMemcpyDeviceToHost, tb->stream));
+		HIP_CHECK(hipStreamSynchronize(tb->stream));
+	});
+}
+int neus_testbed_marching_cubes(NeusTestbed* tb, const int32_t res[3], const float aabb_min[3], const float aabb_max[3], float thresh,
+                                const float* density_dev, uint32_t* n_verts, uint32_t* n_tris) {
+	return guard([&] {
+		HIP_CHECK(hipSetDevice(tb->device));
+		tb->marching_cubes(res, aabb_min, aabb_max, thresh, density_dev);
+		if (n_verts) *n_verts = tb->mesh_nv;
+		if (n_tris) *n_tris = tb->mesh_nt;
+	});
+}
+int neus_testbed_get_mesh(NeusTestbed* tb, float* verts, uint32_t* tris) {
+	return guard([&] {
+		HIP_CHECK(hipStreamSynchronize(tb->stream));
+		if (verts && tb->mesh_nv) HIP_CHECK(hipMemcpy(verts, tb->mesh_v.p, (size_t)tb->mesh_nv * 12, hipMemcpyDeviceToHost));
+		if (tris && tb->mesh_nt) HIP_CHECK(hipMemcpy(tris, tb->mesh_f.p, (size_t)tb->mesh_nt * 12, hipMemcpyDeviceToHost));
+	});
+}
+int neus_testbed_mesh_vertex_colors(NeusTestbed* tb, float* rgb) {
+	return guard([&] {
+		if (!rgb) throw std::runtime_error("mesh_vertex_colors: null output");
+		HIP_CHECK(hipSetDevice(tb->device));
+		tb->mesh_colors(rgb);
+	});
+}
+int neus_mc_table(int8_t* out) { return guard([&] { mc_table_host(out); }); }
 int neus_testbed_get_rng(NeusTestbed* tb, uint64_t* o) {
 	return guard([&] { o[0] = tb->rng.state; o[1] = tb->rng.inc; o[2] = tb->density_grid_rng.state; o[3] = tb->density_grid_rng.inc; });
 }

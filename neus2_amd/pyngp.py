@@ -37,6 +37,44 @@ class TestbedMode(enum.IntEnum):
 NERF_SCALE = 0.33  # nerf_loader.h:31
 
 
+def mesh_vertex_normals(V, F):
+    """compute_mesh_1ring (marching_cubes.cu:331-366, 699-705): per vertex, the sum of the (area-weighted)
+    normals of its faces, normalised as compute_marching_cubes_mesh does (python_api.cu:115-118)."""
+    N = np.zeros_like(V, dtype=np.float32)
+    if len(F):
+        P = V[F.astype(np.int64)]
+        n = np.cross(P[:, 1] - P[:, 0], P[:, 2] - P[:, 0]).astype(np.float32)
+        for k in range(3):
+            np.add.at(N, F[:, k].astype(np.int64), n)
+    ln = np.linalg.norm(N, axis=1, keepdims=True)
+    return np.divide(N, ln, out=np.zeros_like(N), where=ln > 0)
+
+
+def save_mesh(filename, V, N, Cc, F, scale=1.0, offset=(0.0, 0.0, 0.0)):
+    """save_mesh (marching_cubes.cu:826-960) for .ply / .obj without texture unwrapping."""
+    P = (np.asarray(V, np.float32) - np.asarray(offset, np.float32)) / np.float32(scale)
+    F = np.asarray(F, np.int64)
+    ext = os.path.splitext(filename)[1].lower()
+    with open(filename, "w") as f:
+        if ext == ".ply":
+            f.write("ply\nformat ascii 1.0\ncomment output from neus2_amd\nelement vertex %d\n"
+                    "property float x\nproperty float y\nproperty float z\nproperty float nx\nproperty float ny\nproperty float nz\n"
+                    "property uchar red\nproperty uchar green\nproperty uchar blue\nelement face %d\n"
+                    "property list uchar int vertex_index\nend_header\n" % (len(P), len(F)))
+            c8 = np.clip(np.asarray(Cc, np.float32) * 255.0, 0, 255).astype(np.uint8)
+            for p, n, c in zip(P, N, c8):
+                f.write("%0.5f %0.5f %0.5f %0.3f %0.3f %0.3f %d %d %d\n" % (p[0], p[1], p[2], n[0], n[1], n[2], c[0], c[1], c[2]))
+            for a, b, c in F:
+                f.write("3 %d %d %d\n" % (c, b, a))
+        else:
+            for p, c in zip(P, np.clip(Cc, 0, 1)):
+                f.write("v %0.5f %0.5f %0.5f %0.3f %0.3f %0.3f\n" % (p[0], p[1], p[2], c[0], c[1], c[2]))
+            for n in N:
+                f.write("vn %0.5f %0.5f %0.5f\n" % (n[0], n[1], n[2]))
+            for a, b, c in F:
+                f.write("f %d//%d %d//%d %d//%d\n" % (c + 1, c + 1, b + 1, b + 1, a + 1, a + 1))
+
+
 def srgb_to_linear(img):
     """scripts/common.py:136-138"""
     limit = 0.04045
@@ -159,7 +197,7 @@ def load_transforms(path):
         focal.append(fl)
         principal.append(pp)
     return dict(images=images, focal=np.array(focal, np.float32), principal=np.array(principal, np.float32),
-                xforms=np.stack(xforms).astype(np.float32), aabb_scale=aabb_scale)
+                xforms=np.stack(xforms).astype(np.float32), aabb_scale=aabb_scale, scale=scale, offset=offset)
 
 
 def geometric_init_weights(n_levels, width=64, seed=1337, path_hint=True):
@@ -243,6 +281,7 @@ class Testbed:
             path = files[0]
         d = load_transforms(path)
         self.set_dataset(d["images"], d["focal"], d["principal"], d["xforms"], d["aabb_scale"])
+        self._scale, self._offset = float(d["scale"]), np.asarray(d["offset"], np.float32)
 
     def set_dataset(self, images, focal, principal, xforms, aabb_scale=1):
         imgs = [np.ascontiguousarray(im, np.uint8) for im in images]
@@ -257,6 +296,10 @@ class Testbed:
         check(lib().neus_testbed_set_dataset(self._h, C.c_uint32(len(imgs)), arr, C.c_float(aabb_scale)))
         self._images = imgs
         self._n_images = len(imgs)
+        s = int(aabb_scale)
+        infl = 0.5 * min(1 << 7, s)
+        self._aabb = (np.full(3, 0.5 - infl, np.float32), np.full(3, 0.5 + infl, np.float32))
+        self._scale, self._offset = 1.0, np.zeros(3, np.float32)
 
     # ------------------------------------------------------------------ network
     def reload_network_from_file(self, path: str = "", batch_size=None, fixed_rays_per_batch=0):
@@ -334,6 +377,49 @@ class Testbed:
         if not linear:
             out[..., :3] = linear_to_srgb(out[..., :3])
         return out
+
+    # ------------------------------------------------------------------ meshes
+    def compute_marching_cubes_mesh(self, resolution=(256, 256, 256), aabb=None, thresh=None, density_grid=None):
+        """Testbed::compute_marching_cubes_mesh (python_api.cu:99-121): dict V (vertices), N (normalised
+        1-ring normals), C (vertex colours), F (faces). `aabb` = (min, max); None = the render aabb.
+        thresh None = m_mesh.thresh = 0 (the SDF level set). `density_grid` (torch cuda tensor of
+        res[2] x res[1] x res[0] floats) skips the network and meshes that grid as given."""
+        res = (C.c_int32 * 3)(*[int(r) for r in np.broadcast_to(np.asarray(resolution), 3)])
+        amin, amax = self._aabb if aabb is None else (np.asarray(aabb[0], np.float32), np.asarray(aabb[1], np.float32))
+        cmin, cmax = (C.c_float * 3)(*map(float, amin)), (C.c_float * 3)(*map(float, amax))
+        thresh = 0.0 if thresh is None else float(thresh)
+        nv, nt = C.c_uint32(), C.c_uint32()
+        dptr = C.c_void_p(density_grid.data_ptr()) if density_grid is not None else None
+        check(lib().neus_testbed_marching_cubes(self._h, res, cmin, cmax, C.c_float(thresh), dptr, C.byref(nv), C.byref(nt)))
+        V = np.zeros((nv.value, 3), np.float32)
+        F = np.zeros((nt.value, 3), np.uint32)
+        check(lib().neus_testbed_get_mesh(self._h, C.c_void_p(V.ctypes.data), C.c_void_p(F.ctypes.data)))
+        N = mesh_vertex_normals(V, F)
+        Cc = np.zeros_like(V)
+        if density_grid is None and nv.value:
+            check(lib().neus_testbed_mesh_vertex_colors(self._h, C.c_void_p(Cc.ctypes.data)))
+        return {"V": V, "N": N, "C": Cc, "F": F.astype(np.int32)}
+
+    def get_sdf_on_grid(self, resolution, aabb=None):
+        """Testbed::get_density_on_grid (testbed_nerf.cu:4096-4139) for NeuS: raw SDF of the inference (EMA)
+        weights at x / res * (aabb.max - aabb.min) + aabb.min; float32 [res_z, res_y, res_x]."""
+        r = [int(v) for v in np.broadcast_to(np.asarray(resolution), 3)]
+        res = (C.c_int32 * 3)(*r)
+        amin, amax = self._aabb if aabb is None else (np.asarray(aabb[0], np.float32), np.asarray(aabb[1], np.float32))
+        cmin, cmax = (C.c_float * 3)(*map(float, amin)), (C.c_float * 3)(*map(float, amax))
+        out = np.zeros((r[2], r[1], r[0]), np.float32)
+        check(lib().neus_testbed_sdf_on_grid(self._h, res, cmin, cmax, C.c_void_p(out.ctypes.data)))
+        return out
+
+    def compute_and_save_marching_cubes_mesh(self, filename, resolution=(256, 256, 256), aabb=None, thresh=None, unwrap_it=False):
+        """Testbed::compute_and_save_marching_cubes_mesh (testbed.cu:308-317) -> save_mesh
+        (marching_cubes.cu:826-960): .ply (ascii, with normals and 8-bit colours) or .obj, vertices mapped back
+        to the dataset's coordinates as (v - offset) / scale."""
+        if unwrap_it:
+            raise NeusError("unwrap_it (texture atlas export) is not supported")
+        m = self.compute_marching_cubes_mesh(resolution, aabb, thresh)
+        save_mesh(filename, m["V"], m["N"], m["C"], m["F"], self._scale, self._offset)
+        return m
 
     def train(self, batch_size: int | None = None):
         """Testbed::train(batch_size) (testbed.cu:2640-2736): ONE training step targeting `batch_size`

@@ -1422,4 +1422,69 @@ void or_render(const OrNetCfg* c, const float* params, uint32_t valid_level, con
 	}
 	std::memcpy(rgba_out, accum.data(), accum.size() * sizeof(float));
 }
+
+// -------------------------------------------------------------------------------------------
+// Marching cubes (marching_cubes.cu:276-420, gen_vertices / gen_faces) in the canonical deterministic
+// order: vertices by (grid point linear index, axis x < y < z), triangles by (cube linear index, table
+// row order). Vertex = fma(float(x) + dt, scale, aabb.min) per component (Eigen cwiseProduct + offset
+// under nvcc --fmad=true), dt = (thresh - f0) / (f1 - f0), scale = (max - min) / res. The case table is
+// passed in (oracle/mc_table.py builds it independently of the product). Call with null outputs to
+// count. Returns n_verts; *n_tris_out = triangles.
+// -------------------------------------------------------------------------------------------
+uint64_t or_marching_cubes(const float* d, uint32_t rx, uint32_t ry, uint32_t rz, float thresh, const float* amin, const float* amax,
+                           const int8_t* table /* 256 x 19 */, float* V, uint32_t* F, uint64_t* n_tris_out) {
+	const uint64_t r1 = rx, r2 = (uint64_t)rx * ry, n = r2 * rz;
+	float scale[3] = {(amax[0] - amin[0]) / (float)rx, (amax[1] - amin[1]) / (float)ry, (amax[2] - amin[2]) / (float)rz};
+	auto flags = [&](uint64_t p) {
+		const uint32_t z = (uint32_t)(p / r2), y = (uint32_t)((p % r2) / r1), x = (uint32_t)(p % r1);
+		const bool in0 = d[p] > thresh;
+		uint32_t f = 0;
+		if (x + 1 < rx && in0 != (d[p + 1] > thresh)) f |= 1;
+		if (y + 1 < ry && in0 != (d[p + r1] > thresh)) f |= 2;
+		if (z + 1 < rz && in0 != (d[p + r2] > thresh)) f |= 4;
+		return f;
+	};
+	std::vector<uint32_t> vbase(n);
+	uint64_t nv = 0;
+	for (uint64_t p = 0; p < n; ++p) {
+		vbase[p] = (uint32_t)nv;
+		const uint32_t f = flags(p);
+		if (!f) continue;
+		const uint32_t z = (uint32_t)(p / r2), y = (uint32_t)((p % r2) / r1), x = (uint32_t)(p % r1);
+		const uint64_t step[3] = {1, r1, r2};
+		for (int a = 0; a < 3; ++a) {
+			if (!((f >> a) & 1)) continue;
+			if (V) {
+				const float f0 = d[p], f1 = d[p + step[a]];
+				const float dt = (thresh - f0) / (f1 - f0);
+				float q[3] = {(float)x, (float)y, (float)z};
+				q[a] = q[a] + dt;
+				for (int k = 0; k < 3; ++k) V[3 * nv + k] = std::fma(q[k], scale[k], amin[k]);
+			}
+			++nv;
+		}
+	}
+	const uint64_t eoff[12] = {0, 1, r1, 0, r2, 1 + r2, r1 + r2, r2, 0, 1, 1 + r1, r1};
+	const int eax[12] = {0, 1, 0, 1, 0, 1, 0, 1, 2, 2, 2, 2};
+	uint64_t nt = 0;
+	for (uint64_t p = 0; p < n; ++p) {
+		const uint32_t z = (uint32_t)(p / r2), y = (uint32_t)((p % r2) / r1), x = (uint32_t)(p % r1);
+		if (x + 1 >= rx || y + 1 >= ry || z + 1 >= rz) continue;
+		uint32_t m = 0;
+		const uint64_t c[8] = {p, p + 1, p + 1 + r1, p + r1, p + r2, p + 1 + r2, p + 1 + r1 + r2, p + r1 + r2};
+		for (int k = 0; k < 8; ++k) m |= (uint32_t)(d[c[k]] > thresh) << k;
+		const int8_t* row = table + 19 * m;
+		for (int q = 0; q < 18 && row[q] >= 0; q += 3) {
+			if (F)
+				for (int j = 0; j < 3; ++j) {
+					const int e = row[q + j];
+					const uint64_t o = p + eoff[e];
+					F[3 * nt + j] = vbase[o] + (uint32_t)__builtin_popcount(flags(o) & ((1u << eax[e]) - 1));
+				}
+			++nt;
+		}
+	}
+	if (n_tris_out) *n_tris_out = nt;
+	return nv;
+}
 } // extern "C"

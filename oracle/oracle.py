@@ -278,3 +278,20 @@ def ld_random_val_2d(index, seed):
 def sobol(index, dim):
     lib().or_sobol_export.restype = C.c_uint32
     return int(lib().or_sobol_export(C.c_uint32(index), C.c_uint32(dim)))
+
+
+def marching_cubes(density, thresh, aabb_min=(0, 0, 0), aabb_max=(1, 1, 1), table=None):
+    """or_marching_cubes: density [rz][ry][rx] float32 -> V float32 [n, 3], F uint32 [m, 3]."""
+    import mc_table
+    d = np.ascontiguousarray(density, np.float32)
+    rz, ry, rx = d.shape
+    tab = np.ascontiguousarray(mc_table.build_table() if table is None else table, np.int8)
+    amin, amax = f32(aabb_min), f32(aabb_max)
+    f = lib().or_marching_cubes
+    f.restype = C.c_uint64
+    nt = C.c_uint64()
+    nv = f(P(d), C.c_uint32(rx), C.c_uint32(ry), C.c_uint32(rz), C.c_float(thresh), P(amin), P(amax), P(tab), None, None, C.byref(nt))
+    V = np.zeros((nv, 3), np.float32)
+    F = np.zeros((nt.value, 3), np.uint32)
+    f(P(d), C.c_uint32(rx), C.c_uint32(ry), C.c_uint32(rz), C.c_float(thresh), P(amin), P(amax), P(tab), P(V), P(F), C.byref(nt))
+    return V, F

@@ -77,3 +77,17 @@ def test_struct_layouts_match_header(tmp_path):
                 assert getattr(T, key.split(".")[1]).offset == int(v), key
     from neus2_amd.pyngp import PHASES
     assert len(PHASES) == int(vals["NEUS_N_PHASES"])
+
+
+def test_mc_table_matches_oracle_restatement():
+    """neus_mc_table (host-only entry point: the generated case table the kernels upload) equals the
+    oracle's independent restatement (oracle/mc_table.py)."""
+    import ctypes as C
+    import sys
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import mc_table
+    from neus2_amd._lib import check, lib
+    out = np.zeros((256, 19), np.int8)
+    check(lib().neus_mc_table(C.c_void_p(out.ctypes.data)))
+    np.testing.assert_array_equal(out, mc_table.build_table())

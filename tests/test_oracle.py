@@ -312,3 +312,52 @@ def test_oracle_render_small_scene():
     a = img[..., 3]
     assert (a >= 0).all() and (a <= 1 + 1e-6).all()
     assert a[8:16, 12:20].mean() > a[:4, :4].mean()
+
+
+def _sphere_sdf(res, r=0.3):
+    ax = (np.arange(res) / res).astype(np.float32)
+    z, y, x = np.meshgrid(ax, ax, ax, indexing="ij")
+    return (np.sqrt((x - .5) ** 2 + (y - .5) ** 2 + (z - .5) ** 2) - r).astype(np.float32)
+
+
+def test_mc_oracle_cpp_matches_python_restatement():
+    """or_marching_cubes (C++, fma vertices) and mc_table.marching_cubes (numpy) agree on a random field."""
+    import mc_table
+    d = np.random.default_rng(0).normal(size=(9, 10, 11)).astype(np.float32)
+    V, F = O.marching_cubes(d, 0.1)
+    V2, F2 = mc_table.marching_cubes(d, 0.1)
+    np.testing.assert_array_equal(F, F2)
+    np.testing.assert_allclose(V, V2, rtol=0, atol=1e-6)
+
+
+def test_mc_oracle_sphere_is_closed_and_accurate():
+    """The generated case table gives a closed, consistently oriented surface (every directed edge once,
+    its reverse once), outward normals, area and radius of the analytic sphere within grid error."""
+    import collections
+    d = _sphere_sdf(48)
+    V, F = O.marching_cubes(d, 0.0)
+    E = collections.Counter()
+    for a, b, c in F:
+        for u, v in ((a, b), (b, c), (c, a)):
+            E[(int(u), int(v))] += 1
+    assert max(E.values()) == 1
+    assert all((v, u) in E for (u, v) in E)
+    P = V[F.astype(np.int64)]
+    n = np.cross(P[:, 1] - P[:, 0], P[:, 2] - P[:, 0])
+    area = 0.5 * np.linalg.norm(n, axis=1)
+    out = ((n * (P.mean(1) - 0.5)).sum(1) > 0)
+    assert area[out].sum() / area.sum() > 0.999
+    assert abs(area.sum() - 4 * np.pi * 0.09) / (4 * np.pi * 0.09) < 0.01
+    assert np.abs(np.linalg.norm(V - 0.5, axis=1) - 0.3).max() < 2.0 / 48
+
+
+def test_mc_edge_cases():
+    """Empty / full grids give no mesh; a single set corner gives one triangle; res 2 is one cube."""
+    for v in (-1.0, 1.0):
+        V, F = O.marching_cubes(np.full((4, 5, 6), v, np.float32), 0.0)
+        assert len(V) == 0 and len(F) == 0
+    d = np.full((2, 2, 2), -1.0, np.float32)
+    d[0, 0, 0] = 1.0
+    V, F = O.marching_cubes(d, 0.0)
+    assert len(V) == 3 and len(F) == 1
+    np.testing.assert_allclose(sorted(map(tuple, V)), sorted([(0.25, 0, 0), (0, 0.25, 0), (0, 0, 0.25)]), atol=1e-7)
