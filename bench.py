@@ -42,6 +42,8 @@ def parse():
     p.add_argument("--cpu-steps", type=int, default=8)
     # quality half of the metric: PSNR after this many steps of the reference's (adaptive-R) training, N=1 only
     p.add_argument("--psnr-steps", type=int, default=20000)
+    # config 5: marching cubes at mc_res^3 over the PSNR leg's trained model (0 = skip)
+    p.add_argument("--mc-res", type=int, default=1024)
     return p.parse_args()
 
 
@@ -165,7 +167,10 @@ def main():
     }
     if world == 1 and args.psnr_steps > 0:
         del tb
-        out["psnr"] = psnr_leg(sc, args.psnr_steps)
+        out["psnr"], tb2 = psnr_leg(sc, args.psnr_steps)
+        if args.mc_res > 0:
+            out["marching_cubes"] = marching_cubes_leg(tb2, args.mc_res)
+        del tb2
     if rank == 0 and args.cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(sc, args.cpu_steps)
     if rank == 0:
@@ -200,9 +205,32 @@ def psnr_leg(sc, n_steps):
     img = tb.render(gt.shape[1], gt.shape[0], spp=8)
     render_s = time.perf_counter() - t1
     psnr, _ = pyngp.eval_psnr(img, gt)
-    return {"value": round(float(psnr), 3), "unit": "dB", "steps": n_steps, "train_wall_s": round(train_s, 2),
-            "render_s": round(render_s, 3), "protocol": "view 0, spp 8, black bg, snap_to_pixel_centers, min_T 1e-4, EMA weights",
-            "training": "reference schedule: adaptive rays/batch, Nc=2^18, base.json"}
+    out = {"value": round(float(psnr), 3), "unit": "dB", "steps": n_steps, "train_wall_s": round(train_s, 2),
+           "render_s": round(render_s, 3), "protocol": "view 0, spp 8, black bg, snap_to_pixel_centers, min_T 1e-4, EMA weights",
+           "training": "reference schedule: adaptive rays/batch, Nc=2^18, base.json"}
+    return out, tb
+
+
+def marching_cubes_leg(tb, res=1024, reps=3):
+    """BASELINE.json config 5: Testbed::marching_cubes at res^3 over the trained model (SDF of every grid point
+    through the fused encode + density MLP, then the count / scan / emit mesh kernels). Voxels/s of the whole
+    call (host sync at its end), best of `reps`; the mesh stays on the device."""
+    import ctypes as C
+    from neus2_amd._lib import check, lib
+    r = (C.c_int32 * 3)(res, res, res)
+    lo, hi = (C.c_float * 3)(0.0, 0.0, 0.0), (C.c_float * 3)(1.0, 1.0, 1.0)
+    nv, nt = C.c_uint32(), C.c_uint32()
+    best = None
+    for _ in range(reps):
+        tb.synchronize()
+        t0 = time.perf_counter()
+        check(lib().neus_testbed_marching_cubes(tb.handle, r, lo, hi, C.c_float(0.0), None, C.byref(nv), C.byref(nt)))
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    n = res ** 3
+    # algorithmic bytes per voxel (SURVEY.md §8(d) config 5): 448 B gather + 4 B density write + 2 x 16 B MC passes
+    return {"value": n / best, "unit": "voxels/s", "res": res, "ms": round(best * 1e3, 2), "n_verts": nv.value, "n_tris": nt.value,
+            "achieved_GBs": round(n * (448 + 4 + 32) / best / 1e9, 1)}
 
 
 def cpu_baseline(sc, n_steps):

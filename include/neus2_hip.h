@@ -76,6 +76,15 @@ typedef struct NeusNetworkConfig {
 	float density_grid_decay;        /* 0.95 (testbed.h:659) */
 	uint32_t seed;                   /* 1337 (testbed.h:524) */
 	uint32_t fixed_rays_per_batch;   /* 0 = adaptive R (reference); >0 freezes R (benchmarks) */
+	/* dynamic scenes (testbed.cu:2115-2133, base.json "hyperparams" / "globalmove") */
+	uint32_t predict_global_movement;          /* hyperparams.predict_global_movement */
+	uint32_t global_movement_steps;            /* predict_global_movement_training_step (50) */
+	uint32_t finetune_global_movement;         /* keep training the movement with the canonical network */
+	uint32_t reset_density_grid_after_global_movement;
+	float after_learning_rate;                 /* Adam learning rate for frames >= 1 */
+	float gm_learning_rate, gm_beta1, gm_beta2, gm_epsilon;   /* globalmove optimizer: ExponentialDecay(Adam) */
+	uint32_t gm_decay_start, gm_decay_interval;
+	float gm_decay_base;
 } NeusNetworkConfig;
 
 typedef struct NeusImage {
@@ -159,6 +168,18 @@ int neus_testbed_mesh_vertex_colors(NeusTestbed* tb, float* rgb);
 /* The marching-cubes case table the kernels use: 256 rows x 19 int8 (edge triples, -1 terminated). */
 int neus_mc_table(int8_t* out);
 int neus_testbed_get_rng(NeusTestbed* tb, uint64_t* state_inc /*4: rng, density_grid_rng*/);
+/* Dynamic scenes. Testbed::training_network_next_frame (testbed.cu:2001-2082) with load_nerf(frame)
+ * (testbed_nerf.cu:3096-3113): the next frame's images/cameras (same aabb), the frame's local movement folded
+ * into the accumulated ray transform (accumulate_global_movement, nerf_network.h:1163-1177), training
+ * weights := inference (EMA) weights (save/load_snapshot_incremental, testbed.cu:3180-3266), fresh optimizer and
+ * global-move trainer state, m_rng reset, training step 0, canonical training off for global_movement_steps. */
+int neus_testbed_next_frame(NeusTestbed* tb, uint32_t n_images, const NeusImage* images);
+/* Movement state. global12: accumulated rotation (3x3 row-major) + translation (testbed_nerf.cu:193-213);
+ * local12: DeltaNetwork params, transition[4] | rotation 6D[8] (transform_network.h:313-333). Each nullable. */
+int neus_testbed_get_movement(NeusTestbed* tb, float* global12, float* local12);
+int neus_testbed_set_movement(NeusTestbed* tb, const float* global12, const float* local12);
+/* frame_state (4 u32): current frame, canonical training step, train_canonical, train_delta. */
+int neus_testbed_frame_state(NeusTestbed* tb, uint32_t* out4);
 /* Per-ray counters of the last step (first n rays, host buffers, each nullable): samples requested by
  * the march, samples composited before transmittance < 1e-4, and numsteps = (compacted count, base). */
 int neus_testbed_ray_counts(NeusTestbed* tb, uint32_t n, uint32_t* nreq, uint32_t* ccount, uint32_t* numsteps /* 2n */);
@@ -203,6 +224,17 @@ int neus_net_forward(NeusTestbed* tb, void* stream, uint32_t n, const float* coo
  * (fp32 [P], device). n must be a multiple of 128. */
 int neus_net_backward(NeusTestbed* tb, void* stream, uint32_t n, const float* coords, uint32_t valid_level, const uint16_t* dL_dout,
                       uint32_t indeed_batch_size, float* grads_out);
+/* neus_net_backward plus dL/d(input position) per sample (dpos: [n][4] f32, device; the first-order gradient
+ * the global-movement backward consumes, nerf_network.h:602-631). */
+int neus_net_backward_pos(NeusTestbed* tb, void* stream, uint32_t n, const float* coords, uint32_t valid_level, const uint16_t* dL_dout,
+                          uint32_t indeed_batch_size, float* grads_out, float* dpos);
+/* DeltaNetwork forward with the testbed's local movement (add_global_movement_with_rotation_6d,
+ * common_operation.cuh:416-492): stride 7 (NerfCoordinate: position and direction) or 3 (position only). */
+int neus_delta_apply(NeusTestbed* tb, void* stream, uint32_t n, uint32_t stride, const float* in, float* out);
+/* DeltaNetwork backward (add_loss_to_rotation_6d_each + reduce_sum, common_operation.cuh:788-845,
+ * transform_network.h:206-245): coords = undeformed inputs, dpos = dL/d(deformed position) [n][4];
+ * grads12_host gets the fp16-valued, loss-scaled parameter gradients (no optimizer step). */
+int neus_delta_backward(NeusTestbed* tb, void* stream, uint32_t n, uint32_t stride, const float* coords, const float* dpos, float* grads12_host);
 /* Training-sample generation with the testbed's dataset on the given bitfield. Outputs are
  * per ray slot (canonical ray order): rays 6 f32, numsteps 2 u32 (n, base), coords AoS7.
  * counters_out (host, 3 u32): numsteps_counter, n_kept, n_rays_with_samples. */

@@ -22,6 +22,10 @@ class NeusNetworkConfig(C.Structure):
         ("ema_decay", C.c_float), ("decay_start", C.c_uint32), ("decay_interval", C.c_uint32), ("decay_base", C.c_float),
         ("ek_loss_weight", C.c_float), ("mask_loss_weight", C.c_float), ("anneal_end", C.c_uint32), ("batch_size", C.c_uint32),
         ("sdf_bias", C.c_float), ("density_grid_decay", C.c_float), ("seed", C.c_uint32), ("fixed_rays_per_batch", C.c_uint32),
+        ("predict_global_movement", C.c_uint32), ("global_movement_steps", C.c_uint32), ("finetune_global_movement", C.c_uint32),
+        ("reset_density_grid_after_global_movement", C.c_uint32), ("after_learning_rate", C.c_float),
+        ("gm_learning_rate", C.c_float), ("gm_beta1", C.c_float), ("gm_beta2", C.c_float), ("gm_epsilon", C.c_float),
+        ("gm_decay_start", C.c_uint32), ("gm_decay_interval", C.c_uint32), ("gm_decay_base", C.c_float),
     ]
 
 
@@ -71,6 +75,8 @@ EXPORTS = [
     "neus_nccl_unique_id", "neus_testbed_init_data_parallel",
     "neus_grid_encode", "neus_net_forward", "neus_net_backward", "neus_sample_rays", "neus_loss_compact",
     "neus_optimizer_step", "neus_occ_update", "neus_mfma_probe",
+    "neus_testbed_next_frame", "neus_testbed_get_movement", "neus_testbed_set_movement", "neus_testbed_frame_state",
+    "neus_net_backward_pos", "neus_delta_apply", "neus_delta_backward",
 ]
 
 _lib = None

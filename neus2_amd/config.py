@@ -119,6 +119,22 @@ def network_config(cfg: dict, batch_size: int | None = None, fixed_rays_per_batc
     c.density_grid_decay = 0.95
     c.seed = 1337
     c.fixed_rays_per_batch = int(fixed_rays_per_batch)
+    # dynamic scenes (testbed.cu:2115-2133, 2319-2329): hyperparams + the "globalmove" optimizer (defaults: the
+    # main optimizer config, as the reference falls back to it)
+    c.predict_global_movement = int(bool(hp.get("predict_global_movement", False)))
+    c.global_movement_steps = int(hp.get("predict_global_movement_training_step", 300))
+    c.finetune_global_movement = int(bool(hp.get("finetune_global_movement", True)))
+    c.reset_density_grid_after_global_movement = int(bool(hp.get("reset_density_grid_after_global_movement", True)))
+    c.after_learning_rate = float(adam.get("after_learning_rate", c.learning_rate))
+    gm_opt = cfg.get("globalmove", {}).get("optimizer", opt)
+    gm_adam, gm_decay = _leaf_optimizer(gm_opt), _find(gm_opt, "ExponentialDecay")
+    c.gm_learning_rate = float(gm_adam.get("learning_rate", 1e-3))
+    c.gm_beta1 = float(gm_adam.get("beta1", 0.9))
+    c.gm_beta2 = float(gm_adam.get("beta2", 0.999))
+    c.gm_epsilon = float(gm_adam.get("epsilon", 1e-8))
+    c.gm_decay_start = int(gm_decay.get("decay_start", 1 << 30)) if gm_decay else (1 << 30)
+    c.gm_decay_interval = int(gm_decay.get("decay_interval", 10000)) if gm_decay else 10000
+    c.gm_decay_base = float(gm_decay.get("decay_base", 0.33)) if gm_decay else 1.0
     if cfg.get("loss", {}).get("otype", "Huber") != "Huber":
         raise ValueError("only the Huber loss of configs/nerf/base.json is implemented on the gfx950 path")
     return c

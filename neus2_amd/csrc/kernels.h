@@ -26,7 +26,22 @@ struct TrainBufs {
 	float4* v;                        // [ld]
 	float* var_grad;                  // scalar accumulator
 	float indeed_batch;
+	float4* dpos;                     // [ld] dL/d(network input position), first order (null: not needed)
 };
+
+// Dynamic scenes. DeltaNetwork parameters in the reference's order: transition[4] |
+// rotation 6D[8] (transform_network.h:313-333); only slots 0..2 and 4..9 carry values.
+constexpr uint32_t DELTA_PARAMS = 12;
+struct DeltaState {
+	float p[DELTA_PARAMS];                      // fp32 master (the forward reads them fp16-rounded)
+	float m1[DELTA_PARAMS], m2[DELTA_PARAMS];   // Adam moments
+	uint32_t steps[DELTA_PARAMS];               // per-parameter Adam steps
+	float grad[DELTA_PARAMS];                   // last gradient (fp16 values, loss-scaled)
+	float R[9], Rinv[9], t[3];                  // k_delta_prepare: rotation (row-major), inverse, translation
+};
+struct DeltaAdam { float lr, beta1, beta2, eps, loss_scale; uint32_t optimize; };
+// Accumulated global movement applied to every ray (global_movement_with_rotation_6d, testbed_nerf.cu:193-213).
+struct RayMotion { float R[9]; float t[3]; uint32_t on; };
 
 struct WGradJob { const half_t* D; const half_t* X; float* dW; uint32_t M, K, ncols, ldc; uint32_t tiles_m, tiles_k; };
 struct WGradJobs { WGradJob j[5]; uint32_t n_jobs; uint32_t split; uint32_t block_start[6]; const uint32_t* n_valid; };
@@ -41,6 +56,7 @@ struct DevDataset {
 	uint32_t n_images;
 	float aabb_min[3], aabb_max[3];
 	float cone_angle;
+	RayMotion motion;         // frames >= 1 of a dynamic scene: o' = R o + t, d' = R d (normalized d)
 };
 
 struct DPInfo { uint32_t rank, world; };
@@ -162,6 +178,15 @@ void launch_mc_count(hipStream_t s, const uint32_t res[3], const float amin[3], 
 void launch_mc_emit(hipStream_t s, const uint32_t res[3], const float amin[3], const float amax[3], float thresh, const float* density,
                     const uint32_t* off_v, const uint32_t* off_t, float* verts, uint32_t* vidx, uint32_t* tris);
 void launch_mesh_coords(hipStream_t s, uint32_t n, const float* verts, const DevDataset& ds, float* coords);
+// transform_mesh_with_6d (testbed_nerf.cu:109-138): v' = R^-1 (v - t) with the accumulated movement
+void launch_mesh_unmove(hipStream_t s, uint32_t n, const RayMotion& m, float* verts);
+// motion.hip (dynamic scenes)
+void launch_delta_prepare(hipStream_t s, DeltaState* ds);
+void launch_delta_apply(hipStream_t s, const uint32_t* n_ptr, uint32_t n_cap, uint32_t stride, const float* in, float* out, const DeltaState* ds);
+void launch_delta_backward(hipStream_t s, const uint32_t* n_ptr, uint32_t n_cap, const float* coords, uint32_t stride, const float4* dpos,
+                           DeltaState* ds, float* partial, const DeltaAdam& a);
+size_t delta_partial_floats();
+void host_accumulate_movement(const float delta_p[DELTA_PARAMS], float accR[9], float acct[3]);
 // scan.hip
 size_t scan_temp_bytes(uint32_t n);
 void launch_exclusive_scan(hipStream_t s, void* temp, size_t temp_bytes, const uint32_t* in, uint32_t* out, uint32_t n);

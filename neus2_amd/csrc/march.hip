@@ -68,6 +68,19 @@ __global__ void __launch_bounds__(256) k_ray_gen(uint32_t cap_rays, const StepSt
 				float dir[3];
 #pragma unroll
 				for (int r = 0; r < 3; ++r) dir[r] = nrm > 0.f ? du[r] / nrm : du[r];
+				if (ds.motion.on) {
+					// global_movement_with_rotation_6d (testbed_nerf.cu:1380-1387): o' = R o + t, d' = R d; the
+					// record then holds the moved unit direction (load_march_ray does not renormalise it)
+					const float* M = ds.motion.R;
+					float mo[3], md[3];
+#pragma unroll
+					for (int r = 0; r < 3; ++r) {
+						mo[r] = ((M[3 * r] * o[0] + M[3 * r + 1] * o[1]) + M[3 * r + 2] * o[2]) + ds.motion.t[r];
+						md[r] = (M[3 * r] * dir[0] + M[3 * r + 1] * dir[1]) + M[3 * r + 2] * dir[2];
+					}
+#pragma unroll
+					for (int r = 0; r < 3; ++r) { o[r] = mo[r]; dir[r] = md[r]; du[r] = md[r]; }
+				}
 				float tmin; ray_intersect(ds, o, dir, tmin);
 				tmin = fmaxf(tmin, 0.0f);
 				startt = tmin;
@@ -80,12 +93,17 @@ __global__ void __launch_bounds__(256) k_ray_gen(uint32_t cap_rays, const StepSt
 	}
 }
 
-__device__ __forceinline__ void load_march_ray(const float* __restrict__ rays, uint32_t i, MarchRay& mr) {
+// unit: the record holds a unit direction already (moved rays of a dynamic scene)
+__device__ __forceinline__ void load_march_ray(const float* __restrict__ rays, uint32_t i, MarchRay& mr, bool unit) {
 	const float* rr = rays + 6 * (size_t)i;
 	const float du[3] = {rr[3], rr[4], rr[5]};
 	const float nrm = sqrtf((du[0] * du[0] + du[1] * du[1]) + du[2] * du[2]);
 #pragma unroll
-	for (int d = 0; d < 3; ++d) { mr.o[d] = rr[d]; mr.dir[d] = nrm > 0.f ? du[d] / nrm : du[d]; mr.idir[d] = 1.0f / mr.dir[d]; }
+	for (int d = 0; d < 3; ++d) {
+		mr.o[d] = rr[d];
+		mr.dir[d] = unit ? du[d] : (nrm > 0.f ? du[d] / nrm : du[d]);
+		mr.idir[d] = 1.0f / mr.dir[d];
+	}
 }
 
 // ---------------------------------------------------------------- pass 1: the march (count + t record)
@@ -104,7 +122,7 @@ __global__ void __launch_bounds__(256) k_march(uint32_t cap_rays, DevDataset ds,
 	uint32_t n = 0;
 	if (t >= 0.f) {
 		MarchRay mr;
-		load_march_ray(rays, i, mr);
+		load_march_ray(rays, i, mr, ds.motion.on != 0);
 		float* __restrict__ tr = tbuf + (size_t)i * NERF_STEPS;
 		while (n < NERF_STEPS) {
 			float dt, pos[3];
@@ -179,7 +197,7 @@ __global__ void __launch_bounds__(256) k_march_write(uint32_t cap_rays, const St
 			s_b[tid] = b; s_n[tid] = keep ? n : 0u;
 			if (keep) {
 				MarchRay mr;
-				load_march_ray(rays, i, mr);
+				load_march_ray(rays, i, mr, ds.motion.on != 0);
 #pragma unroll
 				for (int d = 0; d < 3; ++d) { s_ray[d][tid] = mr.o[d]; s_ray[3 + d][tid] = mr.dir[d]; }
 			}
@@ -220,7 +238,7 @@ __global__ void k_march_stats(uint32_t n_rays, const float* __restrict__ rays, c
 	float t = tstart[i];
 	if (t >= 0.f) {
 		MarchRay mr;
-		load_march_ray(rays, i, mr);
+		load_march_ray(rays, i, mr, ds.motion.on != 0);
 		while (n < NERF_STEPS) {
 			float dt, pos[3];
 			const float t0 = t;

@@ -296,6 +296,29 @@ void launch_mesh_coords(hipStream_t s, uint32_t n, const float* verts, const Dev
 	if (n) k_mesh_coords<<<(n + 255) / 256, 256, 0, s>>>(n, verts, ds, coords);
 }
 
+// transform_mesh_with_6d (testbed_nerf.cu:109-138): the mesh is extracted in the canonical frame; the
+// accumulated movement maps it back to the current frame, v' = R^-1 (v - t) (R^-1 passed in, host-inverted).
+__global__ void k_mesh_unmove(uint32_t n, RayMotion inv, float* __restrict__ verts) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	float* v = verts + 3 * (size_t)i;
+	const float p[3] = {v[0] - inv.t[0], v[1] - inv.t[1], v[2] - inv.t[2]};
+#pragma unroll
+	for (int k = 0; k < 3; ++k) v[k] = (inv.R[3 * k] * p[0] + inv.R[3 * k + 1] * p[1]) + inv.R[3 * k + 2] * p[2];
+}
+void launch_mesh_unmove(hipStream_t s, uint32_t n, const RayMotion& m, float* verts) {
+	if (!n || !m.on) return;
+	// Eigen Matrix3f::inverse by cofactors
+	const float* a = m.R;
+	const float c00 = a[4] * a[8] - a[5] * a[7], c01 = a[5] * a[6] - a[3] * a[8], c02 = a[3] * a[7] - a[4] * a[6];
+	const float id = 1.0f / ((a[0] * c00 + a[1] * c01) + a[2] * c02);
+	RayMotion inv = m;
+	inv.R[0] = c00 * id; inv.R[1] = (a[2] * a[7] - a[1] * a[8]) * id; inv.R[2] = (a[1] * a[5] - a[2] * a[4]) * id;
+	inv.R[3] = c01 * id; inv.R[4] = (a[0] * a[8] - a[2] * a[6]) * id; inv.R[5] = (a[2] * a[3] - a[0] * a[5]) * id;
+	inv.R[6] = c02 * id; inv.R[7] = (a[1] * a[6] - a[0] * a[7]) * id; inv.R[8] = (a[0] * a[4] - a[1] * a[3]) * id;
+	k_mesh_unmove<<<(n + 255) / 256, 256, 0, s>>>(n, inv, verts);
+}
+
 static McGrid mc_grid(const uint32_t res[3], const float amin[3], const float amax[3], float thresh) {
 	McGrid g{};
 	g.rx = res[0]; g.ry = res[1]; g.rz = res[2];

@@ -927,6 +927,8 @@ __global__ void __launch_bounds__(256) k_mlp_train_rgb(const uint32_t* __restric
 			store_frag(tb.r2_delta, ld, i, dOB, 0, 16, h);
 			store_acc(tb.d1_delta, ld2, i, dD1, 0, 16, h);
 			if (h == 0) tb.v[i] = make_float4(v[0], v[1], v[2], 0.f);
+			// dL/d(rgb input xyz rows 32..34) for the global-movement gradient (nerf_network.h:613-616)
+			if (tb.dpos && h == 0) tb.dpos[i] = make_float4(dRin[1][0], dRin[1][1], dRin[1][2], 0.f);
 		}
 	}
 	// variance gradient: batch sum of dL/dout[7] (nerf_network.h:461-474)
@@ -986,6 +988,29 @@ __global__ void __launch_bounds__(256) k_mlp_train_density(const uint32_t* __res
 			for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(fw.d0T, DIN, 32 * mt + r, 16 * ks, h), accB(dH0[ks >> 1], ks & 1), acc);
 			dDin[mt] = rh16(acc);
 		}
+		// dL/d(position) for the global-movement gradient (nerf_network.h:602-631): the grid's input gradient
+		// sum_k dL/denc_k dy_k/dx (kernel_grid_backward_input) plus the density input's xyz rows; the colour
+		// kernel stored the rgb input's xyz rows. Both lane halves hold parts of the k sum.
+		float pg[3] = {0.f, 0.f, 0.f}, pd[3] = {0.f, 0.f, 0.f};
+		if (tb.dpos) {
+#pragma unroll
+			for (int mt = 0; mt < DMT; ++mt)
+#pragma unroll
+				for (int reg = 0; reg < 16; ++reg) {
+					const int k = 32 * mt + acc_row(reg, h);
+					const float gv = dDin[mt][reg];
+					if (k < 3) {
+						pd[0] += (k == 0) ? gv : 0.f; pd[1] += (k == 1) ? gv : 0.f; pd[2] += (k == 2) ? gv : 0.f;
+					} else if (k < 3 + 2 * L) {
+						const float* dp = dydx + (size_t)(3 * (k - 3)) * ld + ic;
+						pg[0] += gv * dp[0];
+						pg[1] += gv * dp[ld];
+						pg[2] += gv * dp[2 * (size_t)ld];
+					}
+				}
+#pragma unroll
+			for (int d = 0; d < 3; ++d) { pg[d] += __shfl_xor(pg[d], 32); pd[d] += __shfl_xor(pd[d], 32); }
+		}
 		const float4 v4 = tb.v[ic];
 		const float v[3] = {v4.x, v4.y, v4.z};
 		// u = [v, dy/dx . v, 0] (grid.h:1182-1207), B fragments in pi order
@@ -1032,6 +1057,10 @@ __global__ void __launch_bounds__(256) k_mlp_train_density(const uint32_t* __res
 				h8 e0 = (h8){0, 0, 0, 0, 0, 0, 0, 0};
 				if (h == 0) e0[0] = (half_t)1.0f;
 				store_frag(tb.d1_delta, ld2, ld + i, e0, 0, 16, h);
+			}
+			if (tb.dpos && h == 0) {
+				const float4 rg = tb.dpos[i];
+				tb.dpos[i] = make_float4((pg[0] + rg.x) + pd[0], (pg[1] + rg.y) + pd[1], (pg[2] + rg.z) + pd[2], 0.f);
 			}
 			// ---- grid-scatter operands: dL/denc = dDin rows 3.., g = G_in rows 3..
 #pragma unroll

@@ -57,6 +57,17 @@ __global__ void __launch_bounds__(256) k_render_init(RenderCamera cam, uint32_t 
 	const float nrm = sqrtf((du[0] * du[0] + du[1] * du[1]) + du[2] * du[2]);
 #pragma unroll
 	for (int k = 0; k < 3; ++k) r.d[k] = nrm > 0.f ? du[k] / nrm : du[k];
+	if (ds.motion.on) {  // global_movement_with_rotation_6d on the camera ray (testbed_nerf.cu:2285-2294)
+		const float* M = ds.motion.R;
+		float mo[3], md[3];
+#pragma unroll
+		for (int k = 0; k < 3; ++k) {
+			mo[k] = ((M[3 * k] * r.o[0] + M[3 * k + 1] * r.o[1]) + M[3 * k + 2] * r.o[2]) + ds.motion.t[k];
+			md[k] = (M[3 * k] * r.d[0] + M[3 * k + 1] * r.d[1]) + M[3 * k + 2] * r.d[2];
+		}
+#pragma unroll
+		for (int k = 0; k < 3; ++k) { r.o[k] = mo[k]; r.d[k] = md[k]; }
+	}
 	float tmin; ray_intersect(ds, r.o, r.d, tmin);
 	float t = fmaxf(tmin, NERF_RENDERING_NEAR_DISTANCE) + 1e-6f;
 	float p[3];

@@ -133,6 +133,14 @@ struct NeusTestbed {
 	Dev<uint8_t> mc_scan_tmp;
 	size_t mc_scan_bytes = 0;
 	uint32_t mesh_nv = 0, mesh_nt = 0;
+	// dynamic scenes (testbed.h:455-477, 889-890): frame, phase flags, the DeltaNetwork state on the device,
+	// deformed copies of the sample coordinates, dL/d(position) of the training batch
+	uint32_t cur_frame = 0, canonical_step = 0, delta_step = 0;
+	bool train_canonical = true, train_delta = false;
+	float delta_lr_factor = 1.f;
+	Dev<DeltaState> delta;
+	Dev<float> delta_partial, coords_def, coords_cdef;
+	Dev<float4> dpos;
 	// occupancy grid
 	Dev<float> density_grid, density_tmp, grid_mean, grid_partial, occ_pos, occ_density;
 	Dev<uint32_t> occ_idx;
@@ -391,9 +399,70 @@ struct NeusTestbed {
 		s.max_inference = max_samples;
 		HIP_CHECK(hipMemcpy(st.p, &s, sizeof(s), hipMemcpyHostToDevice));
 		HIP_CHECK(hipMemset(density_grid.p, 0, density_grid.n * 4));
+		// dynamic scenes: identity accumulated movement, identity local movement (DeltaNetwork::initialize_params,
+		// transform_network.h:335-383; NerfNetwork::init_accumulation_movement, nerf_network.h:1042-1105)
+		coords_def.alloc((size_t)max_samples * COORD_W); coords_cdef.alloc((size_t)batch * COORD_W); dpos.alloc(batch);
+		delta.alloc(1); delta_partial.alloc(delta_partial_floats());
+		reset_delta();
+		ds.motion = RayMotion{};
+		ds.motion.R[0] = ds.motion.R[4] = ds.motion.R[8] = 1.f;
+		cur_frame = 0; canonical_step = 0; train_canonical = true; train_delta = false;
 		HIP_CHECK(hipStreamSynchronize(stream));
 		have_net = true;
 	}
+
+	// a fresh global-move trainer: identity local movement, zero Adam state (testbed.cu:2569-2578)
+	void reset_delta() {
+		DeltaState h{};
+		h.p[4] = 1.f; h.p[8] = 1.f;  // rotation 6D (1, 0, 0, 0, 1, 0)
+		HIP_CHECK(hipMemcpyAsync(delta.p, &h, sizeof(h), hipMemcpyHostToDevice, stream));
+		launch_delta_prepare(stream, delta.p);
+		delta_step = 0; delta_lr_factor = 1.f;
+	}
+
+	// ------------------------------------------------------------ dynamic scenes: next frame (testbed.cu:2001-2082)
+	void next_frame(uint32_t n_images, const NeusImage* imgs) {
+		if (!have_net) throw std::runtime_error("next_frame: no network");
+		HIP_CHECK(hipStreamSynchronize(stream));
+		consume_loss();
+		// accumulate_global_movement: fold this frame's local movement into the ray transform
+		DeltaState h{};
+		HIP_CHECK(hipMemcpy(&h, delta.p, sizeof(h), hipMemcpyDeviceToHost));
+		RayMotion m = ds.motion;
+		host_accumulate_movement(h.p, m.R, m.t);
+		m.on = 1;
+		// load_nerf(frame): the next frame's images and cameras (same aabb_scale)
+		set_dataset(n_images, imgs, aabb_scale);
+		ds.motion = m;
+		++cur_frame;
+		training_step = 0; canonical_step = 0;
+		// save/load_snapshot_incremental: the new trainer starts from the serialized inference (EMA) weights,
+		// fp16, with fresh optimizer state (Adam moments, per-parameter steps, EMA)
+		const uint32_t P = lay.P;
+		{
+			std::vector<half_t> eh(P);
+			HIP_CHECK(hipMemcpy(eh.data(), ema_h.p, (size_t)P * 2, hipMemcpyDeviceToHost));
+			std::vector<float> ef(P);
+			for (uint32_t i = 0; i < P; ++i) ef[i] = (float)eh[i];
+			HIP_CHECK(hipMemcpy(params_fp.p, ef.data(), (size_t)P * 4, hipMemcpyHostToDevice));
+			HIP_CHECK(hipMemcpy(params_h.p, eh.data(), (size_t)P * 2, hipMemcpyHostToDevice));
+		}
+		HIP_CHECK(hipMemset(m1.p, 0, (size_t)P * 4)); HIP_CHECK(hipMemset(m2.p, 0, (size_t)P * 4));
+		HIP_CHECK(hipMemset(adam_steps.p, 0, (size_t)P * 4)); HIP_CHECK(hipMemset(ema_tmp.p, 0, (size_t)P * 4));
+		adam_step = 0; lr_factor = 1.f;
+		prepare_weights();
+		// reset_network_incremental (testbed.cu:2351-2370): m_rng = seed, rays_per_batch = 4096, counters
+		rng = make_pcg32(cfg.seed);
+		StepState s{};
+		s.rays_per_batch = cfg.fixed_rays_per_batch ? cfg.fixed_rays_per_batch : (1u << 12);
+		s.max_inference = max_samples;
+		HIP_CHECK(hipMemcpy(st.p, &s, sizeof(s), hipMemcpyHostToDevice));
+		reset_delta();
+		train_canonical = false;
+		train_delta = cfg.predict_global_movement != 0;
+		HIP_CHECK(hipStreamSynchronize(stream));
+	}
+	uint32_t gm_steps() const { return cfg.predict_global_movement ? cfg.global_movement_steps : 0u; }
 
 	void setup_mlp_ptrs() {
 		setup_mlp_ptrs_for(params_h.p, wT.p, mlp);
@@ -468,7 +537,7 @@ struct NeusTestbed {
 	}
 	// forward recompute + backward into g (fp32 [P], zeroed by the caller)
 	void net_backward(const uint32_t* n_valid_ptr, const uint32_t* n_train_ptr, uint32_t n, const float* c, uint32_t valid,
-	                  const half_t* dlo, float* g, hipStream_t s, bool marks = false) {
+	                  const half_t* dlo, float* g, hipStream_t s, bool marks = false, bool canonical = true) {
 		const uint32_t ld = n;
 		encode(n_train_ptr, n, n, ld, c, COORD_W, valid, true, s);
 		if (marks) mark(5);
@@ -476,6 +545,7 @@ struct NeusTestbed {
 		t.var_grad = g + lay.var_off;
 		launch_mlp_train(s, lay.L, lay.W, n_valid_ptr, n, ld, c, (const half_t*)enc.p, dydx.p, dlo, mlp, t);
 		if (marks) mark(6);
+		if (!canonical) { if (marks) mark(7); return; }  // global-movement phase: canonical gradients unused
 		WGradJobs J = wgrad_jobs(n, ld, g, n_train_ptr);
 		launch_wgrad(s, J, J.block_start[5]);
 		if (marks) mark(7);
@@ -484,7 +554,7 @@ struct NeusTestbed {
 	}
 
 	// ------------------------------------------------------------ occupancy grid (testbed_nerf.cu:3293-3397, 4003-4016)
-	void occ_update(uint32_t n_uniform, uint32_t n_nonuniform, uint32_t valid) {
+	void occ_update(uint32_t n_uniform, uint32_t n_nonuniform, uint32_t valid, bool use_delta = false) {
 		hipStream_t s = stream;
 		const uint32_t n_cells = GRID3 * (max_cascade + 1);
 		if (training_step == 0) { HIP_CHECK(hipMemsetAsync(density_grid.p, 0, n_cells * 4, s)); density_grid_ema_step = 0; }
@@ -496,7 +566,9 @@ struct NeusTestbed {
 		launch_grid_samples(s, n_nonuniform, n_uniform, density_grid_rng.state, density_grid_rng.inc, density_grid_ema_step, ds.aabb_min, ds.aabb_max,
 		                    density_grid.p, occ_pos.p, occ_idx.p, max_cascade + 1, NERF_MIN_OPTICAL_THICKNESS);
 		density_grid_rng.advance();
-		// NerfNetwork::density on the samples, hash-grid encode fused in
+		// NerfNetwork::density on the samples, hash-grid encode fused in; with the DeltaNetwork active the
+		// positions are moved first (nerf_network.h:664-675)
+		if (use_delta) launch_delta_apply(s, nullptr, N, 3, occ_pos.p, occ_pos.p, delta.p);
 		launch_nerf_density(s, lay.L, lay.W, N, occ_pos.p, gl, valid, params_h.p + lay.grid_off, mlp, occ_density.p);
 		launch_splat_max(s, N, occ_idx.p, occ_density.p, density_tmp.p);
 		launch_ema_grid(s, n_cells, cfg.density_grid_decay, density_grid.p, density_tmp.p);
@@ -515,7 +587,7 @@ struct NeusTestbed {
 		++adam_step;
 		AdamParams p{};
 		p.n = lay.P; p.n_matrix = lay.n_matrix; p.loss_scale = LOSS_SCALE;
-		p.lr = cfg.learning_rate * lr_factor; p.beta1 = cfg.beta1; p.beta2 = cfg.beta2; p.eps = cfg.epsilon; p.l2_reg = cfg.l2_reg;
+		p.lr = (cur_frame ? cfg.after_learning_rate : cfg.learning_rate) * lr_factor;  // testbed.cu:2695-2702 p.beta1 = cfg.beta1; p.beta2 = cfg.beta2; p.eps = cfg.epsilon; p.l2_reg = cfg.l2_reg;
 		p.ema_decay = cfg.ema_decay;
 		p.ema_debias_old = 1 - (float)std::pow(cfg.ema_decay, adam_step - 1);
 		p.ema_debias_new = 1.0f / (1 - (float)std::pow(cfg.ema_decay, adam_step));
@@ -646,6 +718,7 @@ struct NeusTestbed {
 		mc_vidx.alloc(n);
 		mesh_f.alloc(3 * std::max<uint64_t>(nt, 1));
 		launch_mc_emit(s, res, amin, amax, thresh, d, ov, ot, mesh_v.p, mc_vidx.p, mesh_f.p);
+		if (!density_dev) launch_mesh_unmove(s, (uint32_t)nv, ds.motion, mesh_v.p);  // transform_mesh_with_6d
 		HIP_CHECK(hipStreamSynchronize(s));
 		mesh_nv = (uint32_t)nv; mesh_nt = (uint32_t)nt;
 	}
@@ -671,17 +744,30 @@ struct NeusTestbed {
 	void train_step() {
 		if (!have_net) throw std::runtime_error("train: no network (reload_network first)");
 		hipStream_t s = stream;
-		const uint32_t valid = valid_level_at((int)training_step);
-		const uint32_t n_prep = std::min(16u, std::max(1u, training_step / 16u));
+		// dynamic scenes (testbed.cu:2651-2712): progressive levels count from the end of the global-movement
+		// phase; at its end canonical training starts (and the movement keeps training when finetuned)
+		const bool dyn = cur_frame >= 1;
+		if (dyn && training_step == gm_steps()) {
+			train_canonical = true;
+			if (!cfg.finetune_global_movement) train_delta = false;
+			if (cfg.reset_density_grid_after_global_movement) {
+				HIP_CHECK(hipMemsetAsync(density_grid.p, 0, density_grid.n * 4, s));
+				density_grid_ema_step = 0;
+			}
+		}
+		const bool use_delta = dyn && train_delta;
+		const uint32_t valid = valid_level_at(dyn ? (int)training_step - (int)gm_steps() : (int)training_step);
+		if (use_delta) launch_delta_prepare(s, delta.p);
+		const uint32_t n_prep = std::min(16u, std::max(1u, canonical_step / 16u));
 		mark(0);
-		if (training_step % n_prep == 0) {
+		if (canonical_step % n_prep == 0) {
 			const uint32_t nc = GRID3 * (max_cascade + 1);
-			if (training_step < 256) occ_update(nc, 0, valid);
-			else occ_update(nc / 4, nc / 4, valid);
+			if (training_step < 256) occ_update(nc, 0, valid, use_delta);
+			else occ_update(nc / 4, nc / 4, valid, use_delta);
 		}
 		const bool get_loss = training_step % 16 == 0;
 		// ---- train_nerf_step (testbed_nerf.cu:3723-4001)
-		if (training_step == 0) HIP_CHECK(hipMemsetAsync(&st.p->n_rays_total, 0, 4, s));
+		if (training_step == 0 || canonical_step == 0) HIP_CHECK(hipMemsetAsync(&st.p->n_rays_total, 0, 4, s));
 		HIP_CHECK(hipMemsetAsync(&st.p->n_kept, 0, 4, s));
 		HIP_CHECK(hipMemsetAsync(&st.p->n_rays_with_samples, 0, 4, s));
 		const DPInfo dp{rank, world};
@@ -690,7 +776,10 @@ struct NeusTestbed {
 		launch_exclusive_scan(s, scan_tmp.p, scan_tmp_bytes, nreq.p, base.p, MAX_RAYS);
 		launch_march_write(s, MAX_RAYS, st.p, ds, rays.p, tbuf_t.p, nreq.p, base.p, numsteps.p, coords.p, sample_ray.p, max_samples);
 		mark(2);
-		launch_nerf_infer(s, lay.L, lay.W, &st.p->n_kept, 0, coords.p, gl, valid, params_h.p + lay.grid_off, mlp, net_out.p, 8192);
+		// DeltaNetwork forward on the samples (nerf_network.h:162-182); the loss keeps the undeformed records
+		const float* c_in = coords.p;
+		if (use_delta) { launch_delta_apply(s, &st.p->n_kept, max_samples, COORD_W, coords.p, coords_def.p, delta.p); c_in = coords_def.p; }
+		launch_nerf_infer(s, lay.L, lay.W, &st.p->n_kept, 0, c_in, gl, valid, params_h.p + lay.grid_off, mlp, net_out.p, 8192);
 		mark(3);
 		LossParams lp{};
 		lp.loss_scale = LOSS_SCALE; lp.ek_w = cfg.ek_loss_weight; lp.mask_w = cfg.mask_loss_weight; lp.cos_anneal = cos_anneal();
@@ -704,7 +793,15 @@ struct NeusTestbed {
 		launch_rollover(s, batch, st.p, coords_c.p, dL_dout.p);
 		HIP_CHECK(hipMemsetAsync(grads.p, 0, (size_t)lay.P * 4, s));
 		mark(4);
-		net_backward(&st.p->compacted_counter, &st.p->n_train, batch, coords_c.p, valid, dL_dout.p, grads.p, s, true);
+		if (use_delta) {
+			// the training forward runs on the deformed batch; dL/d(position) feeds the DeltaNetwork backward
+			launch_delta_apply(s, nullptr, batch, COORD_W, coords_c.p, coords_cdef.p, delta.p);
+			tbuf.dpos = dpos.p;
+			net_backward(&st.p->compacted_counter, &st.p->n_train, batch, coords_cdef.p, valid, dL_dout.p, grads.p, s, true, train_canonical);
+			tbuf.dpos = nullptr;
+		} else {
+			net_backward(&st.p->compacted_counter, &st.p->n_train, batch, coords_c.p, valid, dL_dout.p, grads.p, s, true, train_canonical);
+		}
 		mark(8);
 		if (world > 1) {
 			NCCL_CHECK(ncclGroupStart());
@@ -724,10 +821,22 @@ struct NeusTestbed {
 		launch_step_counters(s, st.p, batch, max_samples, world, cfg.fixed_rays_per_batch);
 		rng.advance();
 		mark(9);
-		// ---- optimizer (testbed_nerf.cu:3503-3508)
-		optimizer_step(grads.p);
+		// ---- optimizers (testbed_nerf.cu:3503-3508): the canonical trainer, the global-move trainer
+		if (!dyn || train_canonical) optimizer_step(grads.p);
+		if (use_delta) {
+			// ExponentialDecay of the globalmove optimizer (exponential_decay.h:61-80), its own step count
+			if (delta_step == 0) delta_lr_factor = 1.f;
+			if (delta_step >= cfg.gm_decay_start && (delta_step - cfg.gm_decay_start) % std::max(1u, cfg.gm_decay_interval) == 0)
+				delta_lr_factor *= cfg.gm_decay_base;
+			++delta_step;
+			DeltaAdam a{cfg.gm_learning_rate * delta_lr_factor, cfg.gm_beta1, cfg.gm_beta2, cfg.gm_epsilon, LOSS_SCALE, 1u};
+			launch_delta_backward(s, &st.p->n_train, batch, coords_c.p, COORD_W, dpos.p, delta.p, delta_partial.p, a);
+		}
 		mark(10);
 		++training_step;
+		// m_canonical_training_step (testbed_nerf.cu:3512-3527)
+		if (!cfg.predict_global_movement || cur_frame == 0) canonical_step = training_step;
+		else if (training_step >= gm_steps()) canonical_step = training_step - gm_steps();
 		if (profiling) {
 			HIP_CHECK(hipMemcpyAsync(&prof_st[prof_par], st.p, sizeof(StepState), hipMemcpyDeviceToHost, stream));
 			HIP_CHECK(hipEventRecord(ev_done[prof_par], stream));
@@ -916,6 +1025,48 @@ int neus_testbed_mesh_vertex_colors(NeusTestbed* tb, float* rgb) {
 	});
 }
 int neus_mc_table(int8_t* out) { return guard([&] { mc_table_host(out); }); }
+int neus_testbed_next_frame(NeusTestbed* tb, uint32_t n_images, const NeusImage* images) {
+	return guard([&] {
+		HIP_CHECK(hipSetDevice(tb->device));
+		tb->next_frame(n_images, images);
+	});
+}
+int neus_testbed_get_movement(NeusTestbed* tb, float* global12, float* local12) {
+	return guard([&] {
+		if (global12) { std::memcpy(global12, tb->ds.motion.R, 9 * 4); std::memcpy(global12 + 9, tb->ds.motion.t, 3 * 4); }
+		if (local12) {
+			if (!tb->have_net) throw std::runtime_error("get_movement: no network");
+			DeltaState h{};
+			HIP_CHECK(hipStreamSynchronize(tb->stream));
+			HIP_CHECK(hipMemcpy(&h, tb->delta.p, sizeof(h), hipMemcpyDeviceToHost));
+			std::memcpy(local12, h.p, DELTA_PARAMS * 4);
+		}
+	});
+}
+int neus_testbed_set_movement(NeusTestbed* tb, const float* global12, const float* local12) {
+	return guard([&] {
+		if (global12) {
+			std::memcpy(tb->ds.motion.R, global12, 9 * 4); std::memcpy(tb->ds.motion.t, global12 + 9, 3 * 4);
+			const float I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+			bool ident = global12[9] == 0.f && global12[10] == 0.f && global12[11] == 0.f;
+			for (int k = 0; k < 9; ++k) ident = ident && global12[k] == I[k];
+			tb->ds.motion.on = ident ? 0u : 1u;
+		}
+		if (local12) {
+			if (!tb->have_net) throw std::runtime_error("set_movement: no network");
+			DeltaState h{};
+			HIP_CHECK(hipStreamSynchronize(tb->stream));
+			HIP_CHECK(hipMemcpy(&h, tb->delta.p, sizeof(h), hipMemcpyDeviceToHost));
+			std::memcpy(h.p, local12, DELTA_PARAMS * 4);
+			HIP_CHECK(hipMemcpy(tb->delta.p, &h, sizeof(h), hipMemcpyHostToDevice));
+			launch_delta_prepare(tb->stream, tb->delta.p);
+			HIP_CHECK(hipStreamSynchronize(tb->stream));
+		}
+	});
+}
+int neus_testbed_frame_state(NeusTestbed* tb, uint32_t* o) {
+	return guard([&] { o[0] = tb->cur_frame; o[1] = tb->canonical_step; o[2] = tb->train_canonical; o[3] = tb->train_delta; });
+}
 int neus_testbed_get_rng(NeusTestbed* tb, uint64_t* o) {
 	return guard([&] { o[0] = tb->rng.state; o[1] = tb->rng.inc; o[2] = tb->density_grid_rng.state; o[3] = tb->density_grid_rng.inc; });
 }
@@ -1085,6 +1236,46 @@ int neus_net_backward(NeusTestbed* tb, void* stream, uint32_t n, const float* co
 		tb->net_backward(nullptr, nullptr, n, coords, valid, (const half_t*)dlo, grads_out, s);
 		tb->tbuf.indeed_batch = saved;
 		HIP_CHECK(hipGetLastError());
+	});
+}
+int neus_net_backward_pos(NeusTestbed* tb, void* stream, uint32_t n, const float* coords, uint32_t valid, const uint16_t* dlo,
+                          uint32_t indeed, float* grads_out, float* dpos) {
+	return guard([&] {
+		if (!tb->have_net) throw std::runtime_error("no network");
+		if (n == 0 || n % 128 != 0) throw std::runtime_error("neus_net_backward_pos: batch must be a positive multiple of 128");
+		if (n > tb->batch) throw std::runtime_error("neus_net_backward_pos: n exceeds batch_size");
+		hipStream_t s = as_stream(tb, stream);
+		HIP_CHECK(hipMemsetAsync(grads_out, 0, (size_t)tb->lay.P * 4, s));
+		const float saved = tb->tbuf.indeed_batch;
+		tb->tbuf.indeed_batch = (float)indeed;
+		tb->tbuf.dpos = (float4*)dpos;
+		tb->net_backward(nullptr, nullptr, n, coords, valid, (const half_t*)dlo, grads_out, s);
+		tb->tbuf.dpos = nullptr;
+		tb->tbuf.indeed_batch = saved;
+		HIP_CHECK(hipGetLastError());
+	});
+}
+int neus_delta_apply(NeusTestbed* tb, void* stream, uint32_t n, uint32_t stride, const float* in, float* out) {
+	return guard([&] {
+		if (!tb->have_net) throw std::runtime_error("no network");
+		if (stride != 3 && stride != COORD_W) throw std::runtime_error("neus_delta_apply: stride must be 3 or 7");
+		hipStream_t s = as_stream(tb, stream);
+		launch_delta_prepare(s, tb->delta.p);
+		launch_delta_apply(s, nullptr, n, stride, in, out, tb->delta.p);
+		HIP_CHECK(hipGetLastError());
+	});
+}
+int neus_delta_backward(NeusTestbed* tb, void* stream, uint32_t n, uint32_t stride, const float* coords, const float* dpos, float* grads12) {
+	return guard([&] {
+		if (!tb->have_net) throw std::runtime_error("no network");
+		hipStream_t s = as_stream(tb, stream);
+		launch_delta_prepare(s, tb->delta.p);
+		DeltaAdam a{0.f, 0.f, 0.f, 0.f, LOSS_SCALE, 0u};
+		launch_delta_backward(s, nullptr, n, coords, stride, (const float4*)dpos, tb->delta.p, tb->delta_partial.p, a);
+		DeltaState h{};
+		HIP_CHECK(hipMemcpyAsync(&h, tb->delta.p, sizeof(h), hipMemcpyDeviceToHost, s));
+		HIP_CHECK(hipStreamSynchronize(s));
+		std::memcpy(grads12, h.grad, DELTA_PARAMS * 4);
 	});
 }
 int neus_sample_rays(NeusTestbed* tb, void* stream, uint32_t n_rays, uint32_t rank, uint32_t world, uint32_t n_rays_total,
