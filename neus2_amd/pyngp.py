@@ -217,6 +217,19 @@ def geometric_init_weights(n_levels, width=64, seed=1337, path_hint=True):
     return np.concatenate([w0.reshape(-1), w1.reshape(-1)]).astype(np.float32)
 
 
+def _images_array(imgs, focal, principal, xforms):
+    """NeusImage records over host RGBA8 arrays (the arrays must outlive the C call)."""
+    arr = (NeusImage * len(imgs))()
+    for i, im in enumerate(imgs):
+        arr[i].width = im.shape[1]
+        arr[i].height = im.shape[0]
+        arr[i].rgba8 = im.ctypes.data
+        arr[i].focal[:] = [float(v) for v in np.asarray(focal[i]).reshape(2)]
+        arr[i].principal[:] = [float(v) for v in np.asarray(principal[i]).reshape(2)]
+        arr[i].xform[:] = [float(v) for v in np.asarray(xforms[i], np.float32).reshape(12)]
+    return arr
+
+
 class _Training:
     def __init__(self, tb):
         self._tb = tb
@@ -278,21 +291,79 @@ class Testbed:
             files = sorted(f for f in glob.glob(os.path.join(path, "*.json")) if "downsample" not in os.path.basename(f))
             if not files:
                 raise NeusError(f"no json files in {path}")
-            path = files[0]
-        d = load_transforms(path)
+        else:
+            files = [path]
+        d = load_transforms(files[0])
         self.set_dataset(d["images"], d["focal"], d["principal"], d["xforms"], d["aabb_scale"])
         self._scale, self._offset = float(d["scale"]), np.asarray(d["offset"], np.float32)
+        self._frames = files  # all_json_paths (testbed_nerf.cu:2967-2994): one transforms file per time frame
+
+    def set_dataset_frames(self, frames):
+        """A dynamic sequence given in memory: a list of dicts (images, focal, principal, xforms[, aabb_scale]),
+        one per time frame; frame 0 is loaded (the in-memory twin of a directory of per-frame json files)."""
+        f0 = frames[0]
+        self.set_dataset(f0["images"], f0["focal"], f0["principal"], f0["xforms"], f0.get("aabb_scale", 1))
+        self._frames = list(frames)
+
+    # ------------------------------------------------------------------ dynamic scenes
+    @property
+    def all_training_time_frame(self):
+        return len(getattr(self, "_frames", None) or [None])
+
+    @property
+    def current_training_time_frame(self):
+        return self.frame_state()["frame"]
+
+    def _hyper(self, key, default):
+        return (self._cfg_dict or {}).get("hyperparams", {}).get(key, default)
+
+    @property
+    def first_frame_max_training_step(self):
+        return int(self._hyper("first_frame_max_training_step", 2000))
+
+    @property
+    def next_frame_max_training_step(self):
+        return int(self._hyper("next_frame_max_training_step", 1000))
+
+    def frame_state(self):
+        o = (C.c_uint32 * 4)()
+        check(lib().neus_testbed_frame_state(self._h, o))
+        return {"frame": o[0], "canonical_step": o[1], "train_canonical": bool(o[2]), "train_delta": bool(o[3])}
+
+    def training_network_next_frame(self):
+        """Testbed::training_network_next_frame (testbed.cu:2001-2082): False on the last frame, else loads the next
+        frame (load_nerf(frame), testbed_nerf.cu:3096-3113) and restarts training on it with the global-movement
+        phase first."""
+        k = self.current_training_time_frame
+        if k >= self.all_training_time_frame - 1:
+            return False
+        nxt = self._frames[k + 1]
+        d = load_transforms(nxt) if isinstance(nxt, str) else nxt
+        imgs = [np.ascontiguousarray(im, np.uint8) for im in d["images"]]
+        arr = _images_array(imgs, d["focal"], d["principal"], d["xforms"])
+        check(lib().neus_testbed_next_frame(self._h, C.c_uint32(len(imgs)), arr))
+        self._images = imgs
+        self._n_images = len(imgs)
+        return True
+
+    def get_movement(self):
+        """(accumulated 3x4 [R | t] of the rays, DeltaNetwork params transition[4] | rotation 6D[8])."""
+        g, l = (C.c_float * 12)(), (C.c_float * 12)()
+        check(lib().neus_testbed_get_movement(self._h, g, l))
+        g = np.array(g, np.float32)
+        return np.concatenate([g[:9].reshape(3, 3), g[9:].reshape(3, 1)], 1), np.array(l, np.float32)
+
+    def set_movement(self, global_Rt=None, local=None):
+        g = None if global_Rt is None else np.concatenate([np.asarray(global_Rt, np.float32)[:, :3].reshape(-1),
+                                                          np.asarray(global_Rt, np.float32)[:, 3]]).astype(np.float32)
+        l = None if local is None else np.ascontiguousarray(local, np.float32)
+        check(lib().neus_testbed_set_movement(self._h, C.c_void_p(g.ctypes.data) if g is not None else None,
+                                              C.c_void_p(l.ctypes.data) if l is not None else None))
 
     def set_dataset(self, images, focal, principal, xforms, aabb_scale=1):
         imgs = [np.ascontiguousarray(im, np.uint8) for im in images]
-        arr = (NeusImage * len(imgs))()
-        for i, im in enumerate(imgs):
-            arr[i].width = im.shape[1]
-            arr[i].height = im.shape[0]
-            arr[i].rgba8 = im.ctypes.data
-            arr[i].focal[:] = [float(v) for v in np.asarray(focal[i]).reshape(2)]
-            arr[i].principal[:] = [float(v) for v in np.asarray(principal[i]).reshape(2)]
-            arr[i].xform[:] = [float(v) for v in np.asarray(xforms[i], np.float32).reshape(12)]
+        arr = _images_array(imgs, focal, principal, xforms)
+        self._frames = None
         check(lib().neus_testbed_set_dataset(self._h, C.c_uint32(len(imgs)), arr, C.c_float(aabb_scale)))
         self._images = imgs
         self._n_images = len(imgs)
@@ -331,12 +402,17 @@ class Testbed:
         at hyperparams.first_frame_max_training_step (testbed.cu:1752-1758). Returns False when done."""
         if not self.shall_train:
             return False
-        limit = self.max_training_steps
-        if limit is None and self._cfg_dict is not None:
-            limit = self._cfg_dict.get("hyperparams", {}).get("first_frame_max_training_step")
-        if limit is not None and self.training_step >= int(limit):
-            self.shall_train = False
-            return False
+        if self.max_training_steps is not None:
+            if self.training_step >= int(self.max_training_steps):
+                self.shall_train = False
+                return False
+        elif self._cfg_dict is not None:
+            # testbed.cu:1749-1756: a frame's step budget reached -> next frame (or stop after the last one)
+            k = self.current_training_time_frame
+            limit = self.first_frame_max_training_step if k == 0 else self.next_frame_max_training_step
+            if self.training_step >= limit and not self.training_network_next_frame():
+                self.shall_train = False
+                return False
         self.train_steps(1)
         return True
 

@@ -28,8 +28,9 @@ def look_at(pos, target):
     return M
 
 
-def render_sphere(M, width, height, focal, principal):
+def render_sphere(M, width, height, focal, principal, center=None):
     """Ray-sphere intersection per pixel centre; premultiplied RGBA8 (alpha = coverage)."""
+    CENTER = globals()["CENTER"] if center is None else np.asarray(center, np.float64)
     xs = (np.arange(width) + 0.5) / width
     ys = (np.arange(height) + 0.5) / height
     X, Y = np.meshgrid(xs, ys)
@@ -69,6 +70,25 @@ def sphere_scene(n_views=49, width=1600, height=1200, focal=(2892.0, 2892.0), pr
     n = len(images)
     return dict(images=images, xforms=np.stack(xforms), focal=np.tile(np.float32(focal), (n, 1)),
                 principal=np.tile(np.float32(principal), (n, 1)), aabb_scale=1)
+
+
+def dynamic_scene(n_frames=3, shift=(0.01, 0.0, 0.0), n_views=8, width=64, height=48, focal=60.0, distance=1.6):
+    """Config 4 (SURVEY.md §8(d) item 4): the sphere translated by `shift` per frame, fixed cameras on a ring;
+    one dataset dict per frame (set_dataset_frames)."""
+    frames = []
+    for f in range(n_frames):
+        c = CENTER + np.asarray(shift, np.float64) * f
+        images, xforms = [], []
+        for k in range(n_views):
+            th = 2 * np.pi * k / n_views
+            el = np.deg2rad(20.0 * np.sin(3 * th))
+            pos = CENTER + distance * np.array([np.sin(th) * np.cos(el), -np.sin(el), -np.cos(th) * np.cos(el)])
+            M = look_at(pos, CENTER)
+            xforms.append(M.astype(np.float32))
+            images.append(render_sphere(M, width, height, (focal, focal), (0.5, 0.5), center=c))
+        frames.append(dict(images=images, xforms=np.stack(xforms), focal=np.tile(np.float32([focal, focal]), (n_views, 1)),
+                           principal=np.tile(np.float32([0.5, 0.5]), (n_views, 1)), aabb_scale=1))
+    return frames
 
 
 def config1_scene():

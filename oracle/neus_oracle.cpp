@@ -258,7 +258,24 @@ struct OrDataset {
 	float aabb_min[3];
 	float aabb_max[3];
 	float cone_angle;           // 0 for aabb_scale 1 (testbed_nerf.cu:3091)
+	float motion_R[9];          // accumulated global movement, row-major (frames >= 1 of a dynamic scene)
+	float motion_t[3];
+	uint32_t motion_on;
 };
+
+namespace {
+// global_movement_with_rotation_6d (testbed_nerf.cu:193-213): o' = R o + t, d' = R d (d normalized)
+inline void move_ray(const OrDataset* ds, float o[3], float d[3]) {
+	if (!ds->motion_on) return;
+	const float* R = ds->motion_R;
+	float no[3], nd[3];
+	for (int k = 0; k < 3; ++k) {
+		no[k] = ((R[3 * k] * o[0] + R[3 * k + 1] * o[1]) + R[3 * k + 2] * o[2]) + ds->motion_t[k];
+		nd[k] = (R[3 * k] * d[0] + R[3 * k + 1] * d[1]) + R[3 * k + 2] * d[2];
+	}
+	for (int k = 0; k < 3; ++k) { o[k] = no[k]; d[k] = nd[k]; }
+}
+} // namespace
 
 // ---------------------------------------------------------------- grid tables
 // grid.h:1441-1501
@@ -534,7 +551,7 @@ static void net_forward_one(const Net& n, const float* P, const float* coord, ui
 // Weight-gradient accumulation target: double per param.
 // NerfNetwork::backward_impl (nerf_network.h:330-601) for one sample.
 static void net_backward_one(const Net& n, const float* P, const float* coord, uint32_t valid_level, const Ctx& cx,
-                             const uint16_t* dout16, float indeed_batch, double* G, double* var_grad_acc) {
+                             const uint16_t* dout16, float indeed_batch, double* G, double* var_grad_acc, float* dpos_out = nullptr) {
 	const OrNetCfg& c = n.c;
 	const uint32_t W = c.width, L = c.n_levels;
 	float dLo[16]; for (int k = 0; k < 16; ++k) dLo[k] = h2f(dout16[k]);
@@ -573,6 +590,14 @@ static void net_backward_one(const Net& n, const float* P, const float* coord, u
 	}
 	// variance gradient = batch sum of dL_dout[7] (nerf_network.h:461-474)
 	atomic_add_d(var_grad_acc, (double)dLo[7]);
+	// dL/d(position) for the DeltaNetwork (nerf_network.h:602-631): grid input gradient (kernel_grid_backward_input
+	// of dL/denc) + rgb input xyz rows + density input xyz rows
+	if (dpos_out)
+		for (int d = 0; d < 3; ++d) {
+			float s = 0;
+			for (uint32_t k = 0; k < 2 * L; ++k) s += dL_ddin[3 + k] * cx.dydx[3 * k + d];
+			dpos_out[d] = (s + dL_drin[32 + d]) + dL_ddin[d];
+		}
 	// v = dL/d(grad_sdf): rgb-input rows 35..37 + eikonal/indeed_batch + bent-dir rows 8..10 (nerf_network.h:478-504)
 	float v[3];
 	for (int d = 0; d < 3; ++d) {
@@ -752,6 +777,24 @@ void or_network_backward(const OrNetCfg* c, const float* params, uint32_t n_el, 
 	for (int k = 1; k < 4; ++k) grads[n.var_off + k] = 0.0f;
 }
 
+// or_network_backward plus dL/d(position) per sample (dpos: 4 floats per sample, the 4th 0).
+void or_network_backward_pos(const OrNetCfg* c, const float* params, uint32_t n_el, const float* coords, uint32_t valid_level,
+                             const uint16_t* dL_dout, uint32_t indeed_batch_size, float* grads, float* dpos) {
+	Net n(*c);
+	std::vector<float> P = half_params(n, params);
+	std::vector<double> G(n.n_params, 0.0);
+	double var_acc = 0.0;
+#pragma omp parallel for schedule(dynamic, 64)
+	for (int64_t i = 0; i < (int64_t)n_el; ++i) {
+		Ctx cx; net_forward_one(n, P.data(), coords + 7 * i, valid_level, cx, nullptr);
+		dpos[4 * i + 3] = 0.f;
+		net_backward_one(n, P.data(), coords + 7 * i, valid_level, cx, dL_dout + 16 * i, (float)indeed_batch_size, G.data(), &var_acc, dpos + 4 * i);
+	}
+	for (uint32_t i = 0; i < n.n_params; ++i) grads[i] = (float)G[i];
+	grads[n.var_off] = rh((float)var_acc);
+	for (int k = 1; k < 4; ++k) grads[n.var_off + k] = 0.0f;
+}
+
 // -------------------------------------------------------------------------------------------
 // generate_training_samples_nerf_with_global_movement (testbed_nerf.cu:1263-1456), static path
 // (identity global movement, zero distortion, no envmap, cone_angle from the dataset), with the
@@ -803,6 +846,10 @@ static RayGen gen_ray(const OrDataset* ds, const uint8_t* bitfield, uint32_t i, 
 	for (int r = 0; r < 3; ++r) g.o[r] = M[4 * r + 3];
 	float nrm = std::sqrt((g.du[0] * g.du[0] + g.du[1] * g.du[1]) + g.du[2] * g.du[2]);
 	if (nrm > 0) { for (int r = 0; r < 3; ++r) g.dir[r] = g.du[r] / nrm; } else { for (int r = 0; r < 3; ++r) g.dir[r] = g.du[r]; }
+	if (ds->motion_on) {  // moved ray; the record then holds the moved unit direction (testbed_nerf.cu:1380-1387)
+		move_ray(ds, g.o, g.dir);
+		for (int r = 0; r < 3; ++r) g.du[r] = g.dir[r];
+	}
 	AABB bb{{ds->aabb_min[0], ds->aabb_min[1], ds->aabb_min[2]}, {ds->aabb_max[0], ds->aabb_max[1], ds->aabb_max[2]}};
 	V3 o = {g.o[0], g.o[1], g.o[2]}, dir = {g.dir[0], g.dir[1], g.dir[2]};
 	float tmin, tmax; ray_intersect(bb, o, dir, tmin, tmax);
@@ -1318,6 +1365,11 @@ void or_render(const OrNetCfg* c, const float* params, uint32_t valid_level, con
 			r.o = {cam->xform[3], cam->xform[7], cam->xform[11]};
 			const float nrm = std::sqrt((du[0] * du[0] + du[1] * du[1]) + du[2] * du[2]);
 			r.d = nrm > 0.f ? V3{du[0] / nrm, du[1] / nrm, du[2] / nrm} : V3{du[0], du[1], du[2]};
+			if (ds->motion_on) {  // testbed_nerf.cu:2285-2294
+				float o3[3] = {r.o.x, r.o.y, r.o.z}, d3[3] = {r.d.x, r.d.y, r.d.z};
+				move_ray(ds, o3, d3);
+				r.o = {o3[0], o3[1], o3[2]}; r.d = {d3[0], d3[1], d3[2]};
+			}
 			float tmin, tmax; ray_intersect(bb, r.o, r.d, tmin, tmax);
 			float t = std::fmax(tmin, 0.2f) + 1e-6f;  // NERF_RENDERING_NEAR_DISTANCE
 			r.alive = aabb_contains(bb, V3{r.o.x + t * r.d.x, r.o.y + t * r.d.y, r.o.z + t * r.d.z});

@@ -30,6 +30,7 @@ class OrDataset(C.Structure):
         ("n_images", C.c_uint32), ("pixels", C.c_void_p), ("pixel_offsets", C.c_void_p),
         ("resolution", C.c_void_p), ("focal", C.c_void_p), ("principal", C.c_void_p), ("xform", C.c_void_p),
         ("aabb_min", C.c_float * 3), ("aabb_max", C.c_float * 3), ("cone_angle", C.c_float),
+        ("motion_R", C.c_float * 9), ("motion_t", C.c_float * 3), ("motion_on", C.c_uint32),
     ]
 
 
@@ -146,6 +147,19 @@ def network_backward(cfg, params, coords, valid_level, dL_dout_u16, indeed_batch
     return grads
 
 
+def network_backward_pos(cfg, params, coords, valid_level, dL_dout_u16, indeed_batch_size):
+    """network_backward plus dL/d(position) [n, 4] (the DeltaNetwork's input gradient)."""
+    coords = f32(coords)
+    n = coords.shape[0]
+    grads = np.zeros(layout(cfg)["n_params"], np.float32)
+    dpos = np.zeros((n, 4), np.float32)
+    d = np.ascontiguousarray(dL_dout_u16, np.uint16)
+    params = f32(params)
+    lib().or_network_backward_pos(C.byref(cfg), P(params), C.c_uint32(n), P(coords), C.c_uint32(valid_level), P(d),
+                                  C.c_uint32(indeed_batch_size), P(grads), P(dpos))
+    return grads, dpos
+
+
 class Dataset:
     """Host-side dataset view shared by oracle calls (RGBA8 images + ngp cameras)."""
 
@@ -169,6 +183,19 @@ class Dataset:
         self.c.aabb_min[:] = list(aabb_min)
         self.c.aabb_max[:] = list(aabb_max)
         self.c.cone_angle = cone_angle
+        self.set_motion(None)
+
+    def set_motion(self, Rt):
+        """Accumulated global movement of the rays (3x4 [R | t]); None = identity (static scene / frame 0)."""
+        if Rt is None:
+            self.c.motion_R[:] = [1, 0, 0, 0, 1, 0, 0, 0, 1]
+            self.c.motion_t[:] = [0, 0, 0]
+            self.c.motion_on = 0
+        else:
+            Rt = np.asarray(Rt, np.float32)
+            self.c.motion_R[:] = [float(v) for v in Rt[:, :3].reshape(-1)]
+            self.c.motion_t[:] = [float(v) for v in Rt[:, 3]]
+            self.c.motion_on = 1
 
 
 def generate_samples(ds, bitfield, n_rays, n_rays_total, rng_state, rng_inc, max_samples, ray_offset=0, n_rays_global=None):

@@ -285,6 +285,145 @@ def test_render_parity(torch_cuda):
     assert abs(psnr - psnr_ref) < 0.5
 
 
+def _moved_local():
+    p = np.zeros(12, np.float32)
+    p[:3] = [0.01, -0.02, 0.005]
+    p[4:10] = [0.99, 0.05, -0.02, -0.04, 1.01, 0.03]
+    return p
+
+
+def test_delta_network_parity(env):
+    """DeltaNetwork forward (add_global_movement_with_rotation_6d) bit-exact against oracle/motion.py on
+    NerfCoordinate and NerfPosition records; backward (add_loss_to_rotation_6d_each + reduce_sum) equal to the
+    restatement's fp16 gradients within one fp16 ulp (the device sums per-sample fp16 values in fp32)."""
+    import motion as M
+    t, tb = env["t"], env["tb"]
+    lib, check = L()
+    p = _moved_local()
+    tb.set_movement(local=p)
+    try:
+        rng = np.random.default_rng(21)
+        n = 3000
+        c7 = np.zeros((n, 7), np.float32)
+        c7[:, :3] = rng.uniform(0.05, 0.95, (n, 3))
+        d = rng.normal(size=(n, 3)); d /= np.linalg.norm(d, axis=1, keepdims=True)
+        c7[:, 4:] = (d + 1) * 0.5
+        c7[:, 3] = rng.uniform(0, 1, n)
+        for stride in (7, 3):
+            cin = np.ascontiguousarray(c7[:, :stride])
+            out = t.zeros((n, stride), dtype=t.float32, device="cuda")
+            check(lib.neus_delta_apply(tb.handle, None, C.c_uint32(n), C.c_uint32(stride), ptr(dev(t, cin)), ptr(out)))
+            t.cuda.synchronize()
+            np.testing.assert_array_equal(host(out, np.uint32), M.delta_apply(p, cin).view(np.uint32))
+        g = rng.normal(0, 1.0, (n, 4)).astype(np.float32)
+        g[:, 3] = 0
+        got = np.zeros(12, np.float32)
+        check(lib.neus_delta_backward(tb.handle, None, C.c_uint32(n), C.c_uint32(7), ptr(dev(t, c7)), ptr(dev(t, g)),
+                                      C.c_void_p(got.ctypes.data)))
+        ref = M.delta_grad(p, c7, g)
+        record("delta_backward", max_rel=float(np.max(np.abs(got - ref) / np.maximum(np.abs(ref), 1e-3))))
+        np.testing.assert_allclose(got, ref, rtol=2e-3, atol=1e-3)
+    finally:
+        ident = np.zeros(12, np.float32); ident[4] = 1; ident[8] = 1
+        tb.set_movement(local=ident)
+
+
+def test_net_backward_pos_parity(env):
+    """dL/d(position) of the training MLP kernels (grid input gradient + density/rgb input xyz rows, the
+    DeltaNetwork's upstream gradient) against the oracle: per-sample cosine and rel-L2 over the batch."""
+    t, O, tb = env["t"], env["O"], env["tb"]
+    lib, check = L()
+    n = 1024
+    c = _coords(n, 5)
+    params = _perturbed(env, 15)
+    rng = np.random.default_rng(6)
+    dl = np.zeros((n, 16), np.float32)
+    dl[:, :4] = rng.normal(0, 1e-2, (n, 4))
+    dl[:, 4:7] = rng.normal(0, 1.0, (n, 3))
+    dl16 = dl.astype(np.float16)
+    lay = tb.layout()
+    g = t.zeros(lay["n_params"], dtype=t.float32, device="cuda")
+    dp = t.zeros((n, 4), dtype=t.float32, device="cuda")
+    check(lib.neus_net_backward_pos(tb.handle, None, C.c_uint32(n), ptr(dev(t, c)), C.c_uint32(14), ptr(dev(t, dl16)), C.c_uint32(n),
+                                    ptr(g), ptr(dp)))
+    t.cuda.synchronize()
+    got = dp.cpu().numpy()[:, :3].astype(np.float64)
+    _, rdp = O.network_backward_pos(env["cfg"], params, c, 14, dl16.view(np.uint16), n)
+    ref = rdp[:, :3].astype(np.float64)
+    rel = np.linalg.norm(got - ref) / np.linalg.norm(ref)
+    cos = np.sum(got * ref) / (np.linalg.norm(got) * np.linalg.norm(ref))
+    record("net_backward_pos", rel=rel, cos=cos)
+    assert rel <= 2e-2 and cos >= 0.999, (rel, cos)
+
+
+def test_sample_rays_moved_bit_exact(env):
+    """Training rays under an accumulated global movement (frames >= 1): o' = R o + t, d' = R d before the
+    march (testbed_nerf.cu:1380-1387); rays, numsteps and sample coords bit-identical to the oracle."""
+    t, O, tb = env["t"], env["O"], env["tb"]
+    lib, check = L()
+    th = 0.05
+    Rt = np.zeros((3, 4), np.float32)
+    Rt[:, :3] = [[np.cos(th), -np.sin(th), 0], [np.sin(th), np.cos(th), 0], [0, 0, 1]]
+    Rt[:, 3] = [0.02, -0.01, 0.015]
+    Rt = np.float16(Rt).astype(np.float32)  # the accumulated buffers are fp16
+    tb.set_movement(global_Rt=Rt)
+    ds = O.Dataset(env["sc"]["images"], env["sc"]["focal"], env["sc"]["principal"], env["sc"]["xforms"])
+    ds.set_motion(Rt)
+    try:
+        bf = _bitfield(env)
+        n_rays, max_s = 4096, 4096 * 16
+        rs, ri = 0x7777AAAA12345678, 0xDA3E39CB94B95BDB | 1
+        rays = t.zeros((n_rays, 6), dtype=t.float32, device="cuda")
+        ns = t.zeros((n_rays, 2), dtype=t.int32, device="cuda")
+        co = t.zeros((max_s, 7), dtype=t.float32, device="cuda")
+        cnt = (C.c_uint32 * 3)()
+        check(lib.neus_sample_rays(tb.handle, None, C.c_uint32(n_rays), C.c_uint32(0), C.c_uint32(1), C.c_uint32(0),
+                                   C.c_uint64(rs), C.c_uint64(ri), C.c_uint32(max_s), ptr(dev(t, bf)), ptr(rays), ptr(ns), ptr(co), cnt))
+        r_rays, r_ns, r_co, r_cnt, r_nr = O.generate_samples(ds, bf, n_rays, 0, rs, ri, max_s)
+        np.testing.assert_array_equal(host(ns, np.uint32), r_ns)
+        assert cnt[0] == r_cnt and cnt[2] == r_nr and r_nr > 0
+        np.testing.assert_array_equal(host(rays, np.uint32), r_rays.view(np.uint32))
+        nk = int(cnt[1])
+        np.testing.assert_array_equal(host(co, np.uint32)[:nk], r_co.view(np.uint32)[:nk])
+    finally:
+        tb.set_movement(global_Rt=np.concatenate([np.eye(3, dtype=np.float32), np.zeros((3, 1), np.float32)], 1))
+
+
+def test_dynamic_sequence_training(torch_cuda):
+    """Config 4 (incremental training with predict_global_movement): frame 0 trains the canonical model; the
+    next frame (the sphere shifted by +0.02 in x) starts with the global-movement phase (canonical frozen, only
+    the DeltaNetwork trains), then canonical training with movement finetuning. The learned translation
+    points the right way (rays map the moved frame back to the canonical sphere: t_x < 0), the phases switch
+    at the configured step, and the next frame switch folds the movement into the ray transform."""
+    from neus2_amd import pyngp, scenes
+    frames = scenes.dynamic_scene(n_frames=3, shift=(0.02, 0.0, 0.0))
+    tb = pyngp.Testbed(pyngp.TestbedMode.Nerf)
+    tb.set_dataset_frames(frames)
+    tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=BATCH)
+    assert tb.all_training_time_frame == 3
+    tb.train_steps(300)
+    assert tb.training_network_next_frame()
+    fs = tb.frame_state()
+    assert fs["frame"] == 1 and not fs["train_canonical"] and fs["train_delta"] and tb.training_step == 0
+    tb.train_steps(50)
+    _, loc50 = tb.get_movement()
+    tb.train_steps(1)
+    fs = tb.frame_state()
+    assert fs["train_canonical"] and fs["train_delta"], fs
+    tb.train_steps(249)
+    _, loc = tb.get_movement()
+    st = tb.stats()
+    record("dynamic", t50_x=loc50[0], t_x=loc[0], t_y=loc[1], t_z=loc[2], loss=st["ray_loss"])
+    assert np.isfinite(loc).all() and np.isfinite(st["ray_loss"])
+    assert loc50[0] < 0 and loc[0] < loc50[0], (loc50, loc)
+    assert abs(loc[0]) > 2 * max(abs(loc[1]), abs(loc[2])), loc
+    assert tb.training_network_next_frame()
+    glob, loc2 = tb.get_movement()
+    assert glob[0, 3] < 0 and abs(glob[0, 3] - np.float16(loc[0])) < 2e-3, (glob, loc)
+    np.testing.assert_array_equal(loc2[:3], 0)
+    assert not tb.training_network_next_frame() or tb.current_training_time_frame == 2
+
+
 def _mc_testbed():
     from neus2_amd import pyngp, scenes
     sc = scenes.small_scene(n_views=8, width=64, height=48)

@@ -351,6 +351,52 @@ def test_mc_oracle_sphere_is_closed_and_accurate():
     assert np.abs(np.linalg.norm(V - 0.5, axis=1) - 0.3).max() < 2.0 / 48
 
 
+def _moved_params():
+    p = np.zeros(12, np.float32)
+    p[:3] = [0.01, -0.02, 0.005]
+    p[4:10] = [0.99, 0.05, -0.02, -0.04, 1.01, 0.03]
+    return p
+
+
+def test_motion_restatement_identity_and_gradient():
+    """oracle/motion.py (DeltaNetwork restatement): identity parameters move nothing (bit-exact), the rotation is
+    orthonormal, and the reference's closed-form gradient (add_loss_to_rotation_6d_each +
+    gradient_rotation_matrix_to_6d) agrees with central finite differences of the forward."""
+    import motion as M
+    rng = np.random.default_rng(0)
+    p = np.zeros(12, np.float32); p[4] = 1; p[8] = 1
+    c = rng.uniform(0, 1, (16, 7)).astype(np.float32)
+    moved = M.delta_apply(p, c)
+    np.testing.assert_array_equal(moved[:, :4], c[:, :4])  # positions and dt untouched
+    np.testing.assert_allclose(moved[:, 4:], c[:, 4:], atol=1.2e-7)  # dir: (2d - 1 + 1) / 2 rounds
+    p2 = _moved_params()
+    R = M.rot6d_to_matrix([M.rh(v) for v in p2[4:10]]).reshape(3, 3).astype(np.float64)
+    np.testing.assert_allclose(R @ R.T, np.eye(3), atol=1e-6)
+    g = rng.normal(size=(6, 4)).astype(np.float32)
+    x = rng.uniform(0, 1, (6, 3)).astype(np.float32)
+    an = M.delta_grad(p2, x, g)
+
+    def L(pp):
+        return float((M.delta_apply(pp, x).astype(np.float64) * g[:, :3]).sum())
+    for k in list(range(3)) + list(range(4, 10)):
+        e = np.zeros(12, np.float32); e[k] = 1e-2
+        num = (L(p2 + e) - L(p2 - e)) / 2e-2
+        assert abs(an[k] - num) <= 5e-3 + 5e-3 * abs(num), (k, an[k], num)
+    assert an[3] == 0 and an[10] == 0 and an[11] == 0
+
+
+def test_motion_accumulation():
+    """accumulate_global_movement: identity local movement keeps the accumulated transform; a pure translation t
+    adds R_local (t_acc + t) = t_acc + t."""
+    import motion as M
+    Rt = np.concatenate([np.eye(3, dtype=np.float32), np.float32([[0.1], [0.2], [0.3]])], 1)
+    p = np.zeros(12, np.float32); p[4] = 1; p[8] = 1
+    np.testing.assert_array_equal(M.accumulate_movement(p, Rt), np.float16(Rt).astype(np.float32))
+    p[:3] = [0.01, 0.02, -0.03]
+    out = M.accumulate_movement(p, Rt)
+    np.testing.assert_allclose(out[:, 3], [0.11, 0.22, 0.27], atol=2e-4)
+
+
 def test_mc_edge_cases():
     """Empty / full grids give no mesh; a single set corner gives one triangle; res 2 is one cube."""
     for v in (-1.0, 1.0):
