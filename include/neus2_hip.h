@@ -16,6 +16,7 @@
  *     neus_testbed_get_stats           Testbed::m_training_step / m_loss_scalar / counters (python_api.cu:447-449)
  *     neus_testbed_{get,set}_params    Trainer params / serialize             trainer.h:72-109, 281-300
  *     neus_testbed_{get,set}_density_grid  Nerf::density_grid(_bitfield)      testbed.h:688-694
+ *     neus_testbed_restore_state       Testbed::load_snapshot (counters, step, loss, grid bitfield)  testbed.cu:3197-3254
  *     neus_testbed_render              Testbed::render_to_cpu -> render_nerf / NerfTracer::trace  python_api.cu:123-169, testbed_nerf.cu:2397-2760
  *     neus_testbed_sdf_on_grid         Testbed::get_density_on_grid          testbed_nerf.cu:4096-4139
  *     neus_testbed_marching_cubes      Testbed::marching_cubes / marching_cubes_gpu  testbed_nerf.cu:4175-4226, marching_cubes.cu:794-822
@@ -150,6 +151,19 @@ int neus_testbed_get_gradients(NeusTestbed* tb, float* host_out, uint64_t n);
 int neus_testbed_get_ema_params(NeusTestbed* tb, float* host_out, uint64_t n);
 int neus_testbed_get_density_grid(NeusTestbed* tb, float* grid_out /*128^3*/, uint8_t* bitfield_out /*128^3/8*8*/);
 int neus_testbed_set_density_grid(NeusTestbed* tb, const float* grid /*nullable*/, const uint8_t* bitfield /*nullable*/);
+/* Testbed::load_snapshot's non-parameter state (testbed.cu:3210-3248), applied after reload_network + set_params +
+ * set_density_grid: training step, loss scalar, counters_rgb; the inference (EMA) weights := the loaded weights
+ * (Trainer::set_params, trainer.h:72-109); rebuild_bitfield != 0 recomputes the grid mean and occupancy bitfield
+ * from the density grid (update_density_grid_mean_and_bitfield). */
+typedef struct NeusRestoreState {
+	uint32_t training_step;
+	uint32_t rays_per_batch;                  /* multiple of 128, <= 2^18 */
+	uint32_t measured_batch_size;
+	uint32_t measured_batch_size_before_compaction;
+	float loss;
+	int32_t rebuild_bitfield;
+} NeusRestoreState;
+int neus_testbed_restore_state(NeusTestbed* tb, const NeusRestoreState* state);
 /* rgba_out: height*width*4 floats, linear colour, premultiplied alpha (the reference's render(..., linear=True)).
  * n_iterations (nullable): march/composite iterations of the last spp. */
 int neus_testbed_render(NeusTestbed* tb, const NeusRenderRequest* req, float* rgba_out, uint32_t* n_iterations);

@@ -46,6 +46,13 @@ class NeusTrainStats(C.Structure):
     ]
 
 
+class NeusRestoreState(C.Structure):
+    _fields_ = [
+        ("training_step", C.c_uint32), ("rays_per_batch", C.c_uint32), ("measured_batch_size", C.c_uint32),
+        ("measured_batch_size_before_compaction", C.c_uint32), ("loss", C.c_float), ("rebuild_bitfield", C.c_int32),
+    ]
+
+
 class NeusNetLayout(C.Structure):
     _fields_ = [
         ("n_params", C.c_uint64), ("n_density", C.c_uint64), ("n_rgb", C.c_uint64), ("grid_offset", C.c_uint64),
@@ -69,7 +76,7 @@ EXPORTS = [
     "neus_testbed_create", "neus_testbed_destroy", "neus_testbed_set_dataset", "neus_testbed_reload_network",
     "neus_testbed_layout", "neus_testbed_train", "neus_testbed_get_stats", "neus_testbed_get_params",
     "neus_testbed_set_params", "neus_testbed_get_gradients", "neus_testbed_get_ema_params",
-    "neus_testbed_get_density_grid", "neus_testbed_set_density_grid", "neus_testbed_get_rng", "neus_testbed_render", "neus_testbed_sdf_on_grid",
+    "neus_testbed_get_density_grid", "neus_testbed_set_density_grid", "neus_testbed_restore_state", "neus_testbed_get_rng", "neus_testbed_render", "neus_testbed_sdf_on_grid",
     "neus_testbed_marching_cubes", "neus_testbed_get_mesh", "neus_testbed_mesh_vertex_colors", "neus_mc_table", "neus_testbed_ray_counts", "neus_debug_time_kernel", "neus_debug_march_stats", "neus_testbed_time_kernel", "neus_testbed_stream",
     "neus_testbed_synchronize", "neus_testbed_set_profiling", "neus_testbed_kernel_times",
     "neus_nccl_unique_id", "neus_testbed_init_data_parallel",

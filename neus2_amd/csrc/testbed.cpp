@@ -981,6 +981,37 @@ int neus_testbed_set_density_grid(NeusTestbed* tb, const float* g, const uint8_t
 		}
 	});
 }
+// Testbed::load_snapshot after reset_network + Trainer::deserialize (testbed.cu:3197-3254, trainer.h:295-304):
+// training step, loss scalar, adaptive-batch counters; the inference (EMA) weights start as the loaded ones
+// (Trainer::set_params writes m_params_inference too); density grid mean + bitfield rebuilt
+// (update_density_grid_mean_and_bitfield, testbed.cu:3240).
+int neus_testbed_restore_state(NeusTestbed* tb, const NeusRestoreState* in) {
+	return guard([&] {
+		if (!in) throw std::runtime_error("restore_state: null argument");
+		if (!tb->have_net) throw std::runtime_error("restore_state: no network (reload_network first)");
+		if (in->rays_per_batch == 0 || in->rays_per_batch > MAX_RAYS || in->rays_per_batch % 128 != 0)
+			throw std::runtime_error("restore_state: rays_per_batch must be a positive multiple of 128 <= 2^18");
+		HIP_CHECK(hipSetDevice(tb->device));
+		HIP_CHECK(hipStreamSynchronize(tb->stream));
+		tb->consume_loss();
+		StepState s{};
+		HIP_CHECK(hipMemcpy(&s, tb->st.p, sizeof(s), hipMemcpyDeviceToHost));
+		s.rays_per_batch = in->rays_per_batch;
+		s.measured_batch_size = in->measured_batch_size;
+		s.measured_before = in->measured_batch_size_before_compaction;
+		HIP_CHECK(hipMemcpy(tb->st.p, &s, sizeof(s), hipMemcpyHostToDevice));
+		tb->training_step = in->training_step;
+		tb->loss_scalar_ema = tb->last_loss = in->loss;
+		tb->loss_ema_init = true;
+		HIP_CHECK(hipMemcpy(tb->ema_h.p, tb->params_h.p, (size_t)tb->lay.P * 2, hipMemcpyDeviceToDevice));
+		if (in->rebuild_bitfield) {
+			launch_grid_mean(tb->stream, tb->density_grid.p, tb->grid_partial.p, tb->grid_mean.p);
+			launch_bitfield(tb->stream, tb->density_grid.p, tb->bitfield.p, tb->grid_mean.p, tb->max_cascade + 1);
+			launch_bitfield_linear(tb->stream, tb->bitfield.p, tb->bf_lin.p);
+		}
+		HIP_CHECK(hipStreamSynchronize(tb->stream));
+	});
+}
 int neus_testbed_render(NeusTestbed* tb, const NeusRenderRequest* rq, float* rgba_out, uint32_t* n_iterations) {
 	return guard([&] {
 		if (!rq || !rgba_out) throw std::runtime_error("render: null argument");

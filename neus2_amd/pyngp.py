@@ -367,6 +367,8 @@ class Testbed:
         check(lib().neus_testbed_set_dataset(self._h, C.c_uint32(len(imgs)), arr, C.c_float(aabb_scale)))
         self._images = imgs
         self._n_images = len(imgs)
+        self._dataset_meta = {"xforms": list(xforms), "focal": list(focal), "principal": list(principal),
+                              "aabb_scale": float(aabb_scale)}
         s = int(aabb_scale)
         infl = 0.5 * min(1 << 7, s)
         self._aabb = (np.full(3, 0.5 - infl, np.float32), np.full(3, 0.5 + infl, np.float32))
@@ -389,6 +391,19 @@ class Testbed:
         self._net_cfg = c
         self._cfg_dict = cfg
         self._geo = geo
+
+    def save_snapshot(self, path: str, include_optimizer_state: bool = False):
+        """Testbed::save_snapshot (testbed.cu:3144-3178; python_api.cu:370): msgpack network config + snapshot."""
+        from . import snapshot
+        snapshot.save_snapshot(self, path, include_optimizer_state)
+
+    def load_snapshot(self, path: str):
+        """Testbed::load_snapshot (testbed.cu:3197-3254; python_api.cu:371). Needs a dataset loaded first
+        (the reference's snapshot-only render path, load_nerf from the stored metadata, is not built)."""
+        from . import snapshot
+        if not self._n_images:
+            raise NeusError("load_snapshot: load the training data first (set_dataset / load_training_data)")
+        snapshot.load_snapshot(self, path)
 
     def layout(self):
         l = NeusNetLayout()

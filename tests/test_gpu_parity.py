@@ -248,6 +248,46 @@ def test_train_steps_reduce_loss(env):
     assert st["measured_batch_size"] > 0 and st["zero_records"] == 0
 
 
+def test_snapshot_round_trip(env, tmp_path):
+    """save_snapshot -> load_snapshot into a fresh testbed (testbed.cu:3144-3254): params are the fp16 EMA
+    weights, grid fp16, counters / step / loss / movement restored, the occupancy bitfield rebuilt from the
+    grid is the saved one, the two testbeds render the same image bit-for-bit, and training resumes."""
+    from neus2_amd import pyngp
+    sc = env["sc"]
+    tb = pyngp.Testbed(pyngp.TestbedMode.Nerf)
+    tb.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
+    tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=BATCH)
+    tb.train_steps(48)
+    p = str(tmp_path / "s.msgpack")
+    tb.save_snapshot(p)
+    st0 = tb.stats()
+    tb2 = pyngp.Testbed(pyngp.TestbedMode.Nerf)
+    tb2.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
+    tb2.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=BATCH)
+    tb2.load_snapshot(p)
+    st1 = tb2.stats()
+    for k in ("training_step", "rays_per_batch", "measured_batch_size", "measured_batch_size_before_compaction"):
+        assert st1[k] == st0[k], k
+    assert st1["loss"] == pytest.approx(st0["loss"])
+    ema16 = tb.get_ema_params().astype(np.float16).astype(np.float32)
+    np.testing.assert_array_equal(tb2.get_params(), ema16)
+    g0, b0 = tb.get_density_grid()
+    g1, b1 = tb2.get_density_grid()
+    np.testing.assert_array_equal(g1, g0.astype(np.float16).astype(np.float32))
+    # the bitfield is rebuilt from the fp16 grid: equal to the saved one except where fp16 rounding crosses the
+    # occupancy threshold
+    assert (np.unpackbits(b0[: 128 ** 3 // 8]) != np.unpackbits(b1[: 128 ** 3 // 8])).mean() < 1e-3
+    tb2.set_density_grid(bitfield=b0)
+    for t in (tb, tb2):
+        t.snap_to_pixel_centers = True
+        t.set_camera_to_training_view(0)
+    # tb renders with its fp32-derived fp16 EMA weights; tb2 with fp16(fp32 EMA) - the same fp16 values
+    np.testing.assert_array_equal(tb.render(64, 48, spp=1), tb2.render(64, 48, spp=1))
+    tb2.train_steps(16)
+    st2 = tb2.stats()
+    assert st2["training_step"] == st0["training_step"] + 16 and np.isfinite(st2["ray_loss"])
+
+
 def test_render_parity(torch_cuda):
     """Testbed::render (NerfTracer: init/advance, compaction, generate_next, inference on the EMA weights,
     composite + shade, linear accumulation over spp) against the oracle's restatement after a short

@@ -1,0 +1,91 @@
+"""Snapshot format (Testbed::save_snapshot / load_snapshot, testbed.cu:3144-3254): the msgpack object the
+reference writes, built from a testbed's state and decoded back. CPU: the host encoder/decoder on a stand-in
+testbed (no device). GPU (test_gpu_parity.py::test_snapshot_round_trip): train, save, load into a fresh
+testbed, identical parameters / grid / counters and identical renders."""
+import os
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+class _FakeTestbed:
+    """The state accessors build_snapshot reads, with fixed values."""
+
+    def __init__(self, n_params=1000):
+        from neus2_amd import config
+        rng = np.random.default_rng(3)
+        self._cfg_dict = config.load_json(os.path.join(ROOT, "configs", "nerf", "base.json"))
+        self._params = rng.standard_normal(n_params).astype(np.float32)
+        self._grid = np.abs(rng.standard_normal(128 ** 3)).astype(np.float32)
+        self._images = [np.zeros((6, 8, 4), np.uint8)] * 3
+        self._dataset_meta = {"xforms": [np.eye(4)[:3]] * 3, "focal": [[10.0, 10.0]] * 3,
+                              "principal": [[0.5, 0.5]] * 3, "aabb_scale": 1.0}
+        self._scale, self._offset = 0.5, np.full(3, 0.5, np.float32)
+
+    def stats(self):
+        return {"training_step": 123, "rays_per_batch": 4096, "measured_batch_size": 5000,
+                "measured_batch_size_before_compaction": 9000, "loss": 0.25}
+
+    def get_ema_params(self):
+        return self._params
+
+    def get_params(self):
+        return self._params * 0
+
+    def get_density_grid(self):
+        return self._grid, None
+
+    def get_movement(self):
+        R = np.array([[0, -1, 0], [1, 0, 0], [0, 0, 1]], np.float32)
+        return np.concatenate([R, np.array([[0.1], [0.2], [0.3]], np.float32)], 1), np.arange(12, dtype=np.float32) / 16
+
+
+def test_snapshot_layout_and_round_trip(tmp_path):
+    from neus2_amd import snapshot
+    tb = _FakeTestbed()
+    cfg = snapshot.build_snapshot(tb)
+    p = tmp_path / "s.msgpack"
+    p.write_bytes(snapshot.pack(cfg))
+    back = snapshot.read_snapshot(str(p))
+    s = back["snapshot"]
+    # keys the reference writes (testbed.cu:3146-3172, trainer.h:284-286, nerf_network.h:1202-1245)
+    for k in ("n_params", "params_binary", "rotation", "transition", "local_rotation", "local_transition",
+              "density_grid_size", "density_grid_binary", "training_step", "loss"):
+        assert k in s, k
+    assert set(s["nerf"]["rgb"]) == {"rays_per_batch", "measured_batch_size", "measured_batch_size_before_compaction"}
+    assert isinstance(s["params_binary"], bytes) and len(s["params_binary"]) == 2 * tb._params.size
+    assert len(s["rotation"]) == 2 * 12 and len(s["transition"]) == 2 * 4
+    assert len(s["local_rotation"]) == 2 * 8 and len(s["local_transition"]) == 2 * 4
+    assert len(s["density_grid_binary"]) == 2 * 128 ** 3 and s["density_grid_size"] == 128
+    assert back["encoding"] == tb._cfg_dict["encoding"] and back["network"] == tb._cfg_dict["network"]
+    f = snapshot.restore_fields(back)
+    np.testing.assert_array_equal(f["params"], tb._params.astype(np.float16).astype(np.float32))
+    np.testing.assert_array_equal(f["grid"], tb._grid.astype(np.float16).astype(np.float32))
+    g, l = tb.get_movement()
+    np.testing.assert_array_equal(f["global_Rt"], g.astype(np.float16).astype(np.float32))
+    np.testing.assert_array_equal(f["local"], l.astype(np.float16).astype(np.float32))
+    assert (f["training_step"], f["rays_per_batch"], f["measured_batch_size"],
+            f["measured_batch_size_before_compaction"]) == (123, 4096, 5000, 9000)
+    assert f["loss"] == 0.25 and "snapshot" not in f["network"]
+
+
+def test_snapshot_errors(tmp_path):
+    from neus2_amd import snapshot
+    p = tmp_path / "n.msgpack"
+    p.write_bytes(snapshot.pack({"network": {}}))
+    with pytest.raises(RuntimeError, match="does not contain a snapshot"):
+        snapshot.read_snapshot(str(p))
+    cfg = snapshot.build_snapshot(_FakeTestbed())
+    cfg["snapshot"]["density_grid_size"] = 64
+    with pytest.raises(RuntimeError, match="Incompatible grid size"):
+        snapshot.restore_fields(cfg)
+    cfg["snapshot"]["density_grid_size"] = 128
+    cfg["snapshot"]["density_grid_binary"] = bytes(2 * 128 ** 3 * 2)
+    with pytest.raises(RuntimeError, match="cascades"):
+        snapshot.restore_fields(cfg)
+    cfg["snapshot"]["density_grid_binary"] = b""  # an untrained model's empty grid is valid
+    assert snapshot.restore_fields(cfg)["grid"].size == 0
+    with pytest.raises(NotImplementedError):
+        snapshot.build_snapshot(_FakeTestbed(), include_optimizer_state=True)
