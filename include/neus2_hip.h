@@ -263,6 +263,10 @@ int neus_loss_compact(NeusTestbed* tb, void* stream, uint32_t n_rays, uint32_t r
                       float* loss, float* ek_loss, float* mask_loss, uint32_t* counters_out);
 /* One Ema(Adam) step on the testbed's parameters with the given fp32 gradients (device). */
 int neus_optimizer_step(NeusTestbed* tb, void* stream, const float* grads);
+/* fill_rollover_and_rescale (my_tcnn common_device.h:515-535; testbed_nerf.cu:3922-3930): rows [n_in, n_elements)
+ * of coords (AoS7 f32) and dL_dout (AoS16 fp16) become copies of row i % n_in, dL_dout scaled by n_in / n_elements.
+ * n_in is clamped to n_elements; n_in = 0 leaves both untouched. Device buffers. */
+int neus_fill_rollover(NeusTestbed* tb, void* stream, uint32_t n_elements, uint32_t n_in, float* coords, uint16_t* dL_dout);
 /* One occupancy-grid update (density_grid + bitfield) of the testbed's state. */
 int neus_occ_update(NeusTestbed* tb, void* stream, uint32_t n_uniform, uint32_t n_nonuniform);
 /* MFMA fragment-layout probe: C[32x32] = A[32x16] * B[16x32], fp16 row-major in, f32 out. */

@@ -81,7 +81,7 @@ EXPORTS = [
     "neus_testbed_synchronize", "neus_testbed_set_profiling", "neus_testbed_kernel_times",
     "neus_nccl_unique_id", "neus_testbed_init_data_parallel",
     "neus_grid_encode", "neus_net_forward", "neus_net_backward", "neus_sample_rays", "neus_loss_compact",
-    "neus_optimizer_step", "neus_occ_update", "neus_mfma_probe",
+    "neus_optimizer_step", "neus_fill_rollover", "neus_occ_update", "neus_mfma_probe",
     "neus_testbed_next_frame", "neus_testbed_get_movement", "neus_testbed_set_movement", "neus_testbed_frame_state",
     "neus_net_backward_pos", "neus_delta_apply", "neus_delta_backward",
 ]

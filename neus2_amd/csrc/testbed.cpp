@@ -587,7 +587,8 @@ struct NeusTestbed {
 		++adam_step;
 		AdamParams p{};
 		p.n = lay.P; p.n_matrix = lay.n_matrix; p.loss_scale = LOSS_SCALE;
-		p.lr = (cur_frame ? cfg.after_learning_rate : cfg.learning_rate) * lr_factor;  // testbed.cu:2695-2702 p.beta1 = cfg.beta1; p.beta2 = cfg.beta2; p.eps = cfg.epsilon; p.l2_reg = cfg.l2_reg;
+		p.lr = (cur_frame ? cfg.after_learning_rate : cfg.learning_rate) * lr_factor;  // testbed.cu:2695-2702
+		p.beta1 = cfg.beta1; p.beta2 = cfg.beta2; p.eps = cfg.epsilon; p.l2_reg = cfg.l2_reg;
 		p.ema_decay = cfg.ema_decay;
 		p.ema_debias_old = 1 - (float)std::pow(cfg.ema_decay, adam_step - 1);
 		p.ema_debias_new = 1.0f / (1 - (float)std::pow(cfg.ema_decay, adam_step));
@@ -1376,6 +1377,17 @@ int neus_optimizer_step(NeusTestbed* tb, void* stream, const float* grads) {
 		if (stream && (hipStream_t)stream != tb->stream) HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
 		tb->optimizer_step(grads);
 		HIP_CHECK(hipStreamSynchronize(tb->stream));
+	});
+}
+int neus_fill_rollover(NeusTestbed* tb, void* stream, uint32_t n_elements, uint32_t n_in, float* coords, uint16_t* dL_dout) {
+	return guard([&] {
+		if (!tb) throw std::runtime_error("fill_rollover: null testbed");
+		hipStream_t s = as_stream(tb, stream);
+		Dev<StepState> sst; sst.alloc(1);
+		StepState h{}; h.compacted_counter = n_in;
+		HIP_CHECK(hipMemcpyAsync(sst.p, &h, sizeof(h), hipMemcpyHostToDevice, s));
+		launch_rollover(s, n_elements, sst.p, coords, (half_t*)dL_dout);
+		HIP_CHECK(hipStreamSynchronize(s));
 	});
 }
 int neus_occ_update(NeusTestbed* tb, void* stream, uint32_t n_uniform, uint32_t n_nonuniform) {
