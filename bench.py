@@ -21,11 +21,22 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-# Memory-side bytes per launch of the dominant kernel from rocprofv3 PMC passes (scripts/gpu_traffic.sh,
-# profiles/r01_pmc_traffic.md): reads = 128 B x TCC_EA0_RDREQ_128B + 64 B x the other requests (all of
-# this kernel's are 128-B requests; FETCH_SIZE tallies them at 64 B, the gfx950 half-count), writes =
-# WRITE_SIZE. L2-to-fabric traffic: Infinity Cache hits are included, so this bounds HBM bytes from above.
-TRAFFIC = {"inference": 5856.0e6 + 134.2e6}
+# Memory-side bytes per launch, measured by rocprofv3 PMC passes at HEAD (scripts/gpu_traffic.sh ->
+# profiles/traffic.json): reads = 128 B x TCC_EA0_RDREQ_128B + 64 B x the other read requests (FETCH_SIZE
+# tallies 128-B requests at 64 B, the gfx950 half-count), writes = WRITE_SIZE; L2-to-fabric traffic, so
+# Infinity Cache hits are included (an upper bound on DRAM bytes). Keyed by kernel and the number of
+# active hash-grid levels of the replayed state; `traffic` is null when no measurement of that state exists.
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
+
+
+def measured_traffic(kernel, levels):
+    try:
+        with open(TRAFFIC_FILE) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    e = t.get(f"{kernel}@L{levels}")
+    return None if e is None else e.get("bytes_per_launch")
 
 
 def parse():
@@ -47,9 +58,10 @@ def parse():
     return p.parse_args()
 
 
-# Algorithmic work per unit, split over this build's kernels. L = 14,
-# F = 2, fp16 grid: a hash-grid gather is 8 corners x L x 4 B = 448 B per sample, the fused first+second
-# order grid-gradient RMW 2 x 448 = 896 B per compacted sample.
+# Algorithmic work per unit, split over this build's kernels. F = 2, fp16
+# grid: a hash-grid gather is 8 corners x L_active x 4 B per sample (448 B with all 14 levels active), the
+# fused first+second order grid-gradient RMW 2 x that per compacted sample. L_active = valid_level + 1 of the
+# replayed state (progressive levels, grid.h:2427-2440): levels beyond it are neither read nor written.
 #   unit "ray"   : 40 B (ray record + indices + pixel)                       -> march (ray gen + march)
 #   unit "pre"   : 596 B = 28 coords write (coord write pass) + 28 coords read + 448 gather + 32 output
 #                  write (fused inference: 508 B) + 60 loss reads (loss kernels)
@@ -58,26 +70,27 @@ def parse():
 # The SURVEY's figures count the gathers as HBM bytes; the 21 MB table mostly hits L2 / Infinity Cache,
 # so `traffic` (PMC) is reported next to them. MFMA flops (SURVEY: 28,672 per pre-compaction sample,
 # 92,160 per compacted sample) are reported alongside for the MLP kernels.
-GATHER_B = 8 * 14 * 4
-KERNELS = {
-    # name: (kernel id of neus_testbed_time_kernel, algorithmic bytes per unit, flops per unit)
-    "march": (0, 40, 0),
-    "march_write": (1, 28, 0),
-    "inference": (3, 28 + GATHER_B + 32, 28672),
-    "loss_alpha": (4, 60, 0),
-    "train_encode": (8, 28 + GATHER_B, 0),
-    "mlp_train": (5, 64, 92160 - 28672),
-    "grid_scatter": (7, 2 * GATHER_B, 0),
-}
+def kernel_table(levels):
+    g = 8 * levels * 4
+    return {
+        # name: (kernel id of neus_testbed_time_kernel, algorithmic bytes per unit, flops per unit)
+        "march": (0, 40, 0),
+        "march_write": (1, 28, 0),
+        "inference": (3, 28 + g + 32, 28672),
+        "loss_alpha": (4, 60, 0),
+        "train_encode": (8, 28 + g, 0),
+        "mlp_train": (5, 64, 92160 - 28672),
+        "grid_scatter": (7, 2 * g, 0),
+    }
 MFMA_PEAK_TFLOPS = 2500.0  # MI355X dense fp16 (MI355X_MICROARCH.md)
 
 
-def kernel_rooflines(tb, iters=9):
+def kernel_rooflines(tb, levels, iters=9):
     """Per-kernel median launch duration (hipEvents on the testbed stream between `iters` back-to-back
     launches replayed on the final training state, neus_testbed_time_kernel) and the algorithmic HBM
-    roofline of each launch."""
+    roofline of each launch with `levels` active hash-grid levels."""
     out = {}
-    for name, (kid, bpu, fpu) in KERNELS.items():
+    for name, (kid, bpu, fpu) in kernel_table(levels).items():
         ms, units = tb.time_kernel(kid, iters)
         b = bpu * units
         r = {"ms": round(ms, 4), "units": units, "bytes": b, "achieved": round(b / (ms * 1e-3) / 1e9, 1), "unit": "GB/s",
@@ -126,6 +139,7 @@ def main():
     # timed region
     tb.set_profiling(False)
     barrier()
+    trained0 = tb.stats()["trained_samples_total"]
     t1 = time.perf_counter()
     tb.train_steps(args.steps)
     barrier()
@@ -137,10 +151,14 @@ def main():
         elapsed = float(tt.item())
     st = tb.stats()
     batch = args.batch
+    # every step trains on Nc = batch samples per GPU (the reference's m_training_batch_size; a short compaction
+    # is rollover-padded, fill_rollover_and_rescale); the non-rollover share is reported next to it
     samples = batch * world * args.steps
     value = samples / elapsed
+    real = (st["trained_samples_total"] - trained0) / max(1, batch * args.steps)
+    levels = min(st["valid_level"] + 1, tb.layout()["n_levels"])
     # per-kernel timing after the timed region, on its final state (hipEvents on the testbed stream)
-    kern = kernel_rooflines(tb)
+    kern = kernel_rooflines(tb, levels)
     dom = max(kern, key=lambda k: kern[k]["ms"])
     d = kern[dom]
     out = {
@@ -159,8 +177,9 @@ def main():
         "config": {"workload": "NeuS2 train step, Config S, base.json L=14 T=2^19 W=64, Nc=2^18/GPU, R=2^18/GPU fixed",
                    "global_batch": batch * world, "rays_per_gpu": args.rays, "parallelism": f"dp{world}"},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": d["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": d["frac"], "traffic": TRAFFIC.get(dom), "bytes_per_launch": d["bytes"], "units_per_launch": d["units"],
-                     "launch_ms": d["ms"]},
+                     "frac": d["frac"], "traffic": measured_traffic(dom, levels), "bytes_per_launch": d["bytes"],
+                     "units_per_launch": d["units"], "launch_ms": d["ms"], "levels_active": levels},
+        "non_rollover_fraction": round(real, 4),
         "kernels": kern,
         "loss": st["ray_loss"],
         "warmup_s": warm_s,

@@ -111,6 +111,7 @@ typedef struct NeusTrainStats {
 	float density_grid_mean;
 	float ray_loss;                           /* mean Huber loss over the rays that had samples (last logged step) */
 	uint32_t n_rays_with_samples;             /* rays kept by the sampler in the last logged step */
+	uint64_t trained_samples_total;           /* compacted (non-rollover) training samples since step 0, per rank */
 } NeusTrainStats;
 
 /* Testbed::render_to_cpu (python_api.cu:123-169) after set_camera_to_training_view (testbed.cu:264-270). */
@@ -149,6 +150,9 @@ int neus_testbed_get_params(NeusTestbed* tb, float* host_out, uint64_t n);
 int neus_testbed_set_params(NeusTestbed* tb, const float* host_in, uint64_t n);
 int neus_testbed_get_gradients(NeusTestbed* tb, float* host_out, uint64_t n);
 int neus_testbed_get_ema_params(NeusTestbed* tb, float* host_out, uint64_t n);
+/* The fp16 parameter copies the kernels read (network_precision_t params, trainer.h:72-109): which = 0 training
+ * weights, 1 inference (EMA) weights (Ema::custom_weights, ema.h:45-110). host_out: n fp16 bit patterns. */
+int neus_testbed_get_half_params(NeusTestbed* tb, int which, uint16_t* host_out, uint64_t n);
 int neus_testbed_get_density_grid(NeusTestbed* tb, float* grid_out /*128^3*/, uint8_t* bitfield_out /*128^3/8*8*/);
 int neus_testbed_set_density_grid(NeusTestbed* tb, const float* grid /*nullable*/, const uint8_t* bitfield /*nullable*/);
 /* Testbed::load_snapshot's non-parameter state (testbed.cu:3210-3248), applied after reload_network + set_params +

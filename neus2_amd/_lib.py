@@ -42,7 +42,7 @@ class NeusTrainStats(C.Structure):
         ("measured_batch_size_before_compaction", C.c_uint32), ("n_rays_total", C.c_uint32), ("valid_level", C.c_uint32),
         ("zero_records", C.c_uint32), ("loss", C.c_float), ("ek_loss", C.c_float), ("mask_loss", C.c_float),
         ("last_loss", C.c_float), ("density_grid_mean", C.c_float), ("ray_loss", C.c_float),
-        ("n_rays_with_samples", C.c_uint32),
+        ("n_rays_with_samples", C.c_uint32), ("trained_samples_total", C.c_uint64),
     ]
 
 
@@ -76,6 +76,7 @@ EXPORTS = [
     "neus_testbed_create", "neus_testbed_destroy", "neus_testbed_set_dataset", "neus_testbed_reload_network",
     "neus_testbed_layout", "neus_testbed_train", "neus_testbed_get_stats", "neus_testbed_get_params",
     "neus_testbed_set_params", "neus_testbed_get_gradients", "neus_testbed_get_ema_params",
+    "neus_testbed_get_half_params",
     "neus_testbed_get_density_grid", "neus_testbed_set_density_grid", "neus_testbed_restore_state", "neus_testbed_get_rng", "neus_testbed_render", "neus_testbed_sdf_on_grid",
     "neus_testbed_marching_cubes", "neus_testbed_get_mesh", "neus_testbed_mesh_vertex_colors", "neus_mc_table", "neus_testbed_ray_counts", "neus_debug_time_kernel", "neus_debug_march_stats", "neus_testbed_time_kernel", "neus_testbed_stream",
     "neus_testbed_synchronize", "neus_testbed_set_profiling", "neus_testbed_kernel_times",

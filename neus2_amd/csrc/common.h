@@ -127,7 +127,10 @@ struct StepState {
 	uint32_t zero_records;
 	uint32_t n_rays_total;            // rays drawn since training step 0 (all ranks)
 	uint32_t n_train;                 // compacted training batch (target) or 0 when no samples
-	uint32_t pad[5];
+	uint32_t pad0;
+	unsigned long long trained_total; // real (non-rollover) training samples since step 0, this rank: sum of min(Nc measured, batch)
+	uint32_t pad[2];
 };
+static_assert(sizeof(StepState) == 64, "StepState is one 64-B record");
 
 } // namespace neus

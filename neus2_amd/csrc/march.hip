@@ -552,6 +552,7 @@ __global__ void k_step_counters(StepState* st, uint32_t target_batch, uint32_t m
 	const uint32_t measured = st->compacted_counter / world;
 	st->measured_before = before;
 	st->measured_batch_size = measured;
+	st->trained_total += min(measured, target_batch);  // real training samples (the rest of the batch is rollover)
 	if (before == 0 || measured == 0) { st->zero_records = 1; return; }
 	st->zero_records = 0;
 	uint32_t mi = min(before, max_samples);

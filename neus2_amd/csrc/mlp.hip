@@ -276,14 +276,25 @@ __device__ __forceinline__ void fused_levels(const LevelSmem& sl, uint32_t dense
 	constexpr int M0 = Fused<L>::M0;
 	LevelAddr A[2];
 	uint32_t v[2][8];
+	// Level pair m (levels 2m, 2m+1) is skipped when both are beyond valid_level (kernel-uniform branch):
+	// the reference outputs zeros there without a lookup (grid.h:198-215), so no gather is issued.
 	level_addr<L>(sl, dense_bits, valid_level, x, h, 0, A[0]);
 	level_gather(grid, A[0], v[0]);
 #pragma unroll
 	for (int m = 0; m < M0; ++m) {
 		const int cur = m & 1, nxt = cur ^ 1;
-		if (m + 1 < M0) {
+		if (m + 1 < M0 && (uint32_t)(2 * (m + 1)) <= valid_level) {
 			level_addr<L>(sl, dense_bits, valid_level, x, h, m + 1, A[nxt]);
 			level_gather(grid, A[nxt], v[nxt]);
+		}
+		if (m > 0 && (uint32_t)(2 * m) > valid_level) {
+			ev[m] = (h2){(half_t)0.f, (half_t)0.f};
+			if (DYDX)
+#pragma unroll
+				for (int q = 0; q < 2; ++q)
+#pragma unroll
+					for (int d = 0; d < 3; ++d) dy[m][q][d] = 0.f;
+			continue;
 		}
 		float dtmp[2][3];
 		level_interp<DYDX>(A[cur], v[cur], ev[m], DYDX ? dy[m] : dtmp);

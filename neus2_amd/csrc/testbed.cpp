@@ -942,6 +942,7 @@ int neus_testbed_get_stats(NeusTestbed* tb, NeusTrainStats* o) {
 		o->loss = tb->loss_scalar_ema; o->ek_loss = tb->ek_loss; o->mask_loss = tb->mask_loss; o->last_loss = tb->last_loss;
 		o->density_grid_mean = mean;
 		o->ray_loss = tb->ray_loss; o->n_rays_with_samples = tb->last_rays_with_samples;
+		o->trained_samples_total = s.trained_total;
 	});
 }
 static int copy_param_vec(NeusTestbed* tb, const float* dev, float* host, uint64_t n) {
@@ -954,6 +955,14 @@ static int copy_param_vec(NeusTestbed* tb, const float* dev, float* host, uint64
 int neus_testbed_get_params(NeusTestbed* tb, float* o, uint64_t n) { return copy_param_vec(tb, tb->params_fp.p, o, n); }
 int neus_testbed_get_gradients(NeusTestbed* tb, float* o, uint64_t n) { return copy_param_vec(tb, tb->grads.p, o, n); }
 int neus_testbed_get_ema_params(NeusTestbed* tb, float* o, uint64_t n) { return copy_param_vec(tb, tb->ema_tmp.p, o, n); }
+int neus_testbed_get_half_params(NeusTestbed* tb, int which, uint16_t* o, uint64_t n) {
+	return guard([&] {
+		if (!tb->have_net || n != tb->lay.P) throw std::runtime_error("parameter count mismatch");
+		if (which != 0 && which != 1) throw std::runtime_error("get_half_params: which must be 0 (training) or 1 (inference)");
+		HIP_CHECK(hipStreamSynchronize(tb->stream));
+		HIP_CHECK(hipMemcpy(o, which ? tb->ema_h.p : tb->params_h.p, n * 2, hipMemcpyDeviceToHost));
+	});
+}
 int neus_testbed_set_params(NeusTestbed* tb, const float* in, uint64_t n) {
 	return guard([&] {
 		if (!tb->have_net || n != tb->lay.P) throw std::runtime_error("parameter count mismatch");

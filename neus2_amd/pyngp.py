@@ -586,6 +586,13 @@ class Testbed:
         check(lib().neus_testbed_get_ema_params(self._h, C.c_void_p(out.ctypes.data), C.c_uint64(n)))
         return out
 
+    def get_half_params(self, inference: bool = False):
+        """The fp16 parameter copy the kernels read: training weights, or the inference (EMA) weights."""
+        n = self.layout()["n_params"]
+        out = np.zeros(n, np.uint16)
+        check(lib().neus_testbed_get_half_params(self._h, C.c_int(1 if inference else 0), C.c_void_p(out.ctypes.data), C.c_uint64(n)))
+        return out.view(np.float16)
+
     def get_density_grid(self):
         g = np.zeros(128 ** 3, np.float32)
         bf = np.zeros(128 ** 3 // 8 * 8, np.uint8)

@@ -54,7 +54,7 @@ int main(void) {
   S(NeusNetworkConfig) S(NeusImage) S(NeusTrainStats) S(NeusNetLayout)
   O(NeusNetworkConfig, fixed_rays_per_batch) O(NeusNetworkConfig, seed) O(NeusNetworkConfig, batch_size)
   O(NeusImage, rgba8) O(NeusImage, xform)
-  O(NeusTrainStats, ray_loss) O(NeusTrainStats, n_rays_with_samples)
+  O(NeusTrainStats, ray_loss) O(NeusTrainStats, n_rays_with_samples) O(NeusTrainStats, trained_samples_total)
   O(NeusNetLayout, per_level_scale) O(NeusNetLayout, n_levels)
   printf("NEUS_N_PHASES %d\n", NEUS_N_PHASES);
   return 0;

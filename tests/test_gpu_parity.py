@@ -278,6 +278,10 @@ def test_snapshot_round_trip(env, tmp_path):
     # occupancy threshold
     assert (np.unpackbits(b0[: 128 ** 3 // 8]) != np.unpackbits(b1[: 128 ** 3 // 8])).mean() < 1e-3
     tb2.set_density_grid(bitfield=b0)
+    # the inference weights the renderer reads: fp16(fp32 EMA) on the device == the snapshot's fp16 params
+    h0, h1 = tb.get_half_params(inference=True), tb2.get_half_params(inference=True)
+    bad = np.flatnonzero(h0.view(np.uint16) != h1.view(np.uint16))
+    assert bad.size == 0, (bad[:8], h0[bad[:8]], h1[bad[:8]], ema16[bad[:8]])
     for t in (tb, tb2):
         t.snap_to_pixel_centers = True
         t.set_camera_to_training_view(0)

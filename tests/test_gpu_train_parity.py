@@ -43,8 +43,9 @@ def scene(torch_cuda):
 
 def test_optimizer_step_parity(scene, torch_cuda):
     """Trainer::optimizer_step = Ema(ExponentialDecay(Adam)) (adam.h:51-160, ema.h:45-110) for three steps
-    against or_adam_ema_step: fp32 master weights and the fp32 EMA within 2e-6 relative (device powf/sqrtf
-    vs libm: an ulp or two). Covers the zero-gradient skip of non-matrix (grid, variance) params, the L2 term
+    against or_adam_ema_step: fp32 master weights and the fp32 EMA within 2e-6 relative to max(|w|, lr) (device
+    powf/sqrtf vs libm: an ulp or two of the update; a weight that a step brings near zero keeps the absolute
+    error of the O(lr) terms it cancelled). Covers the zero-gradient skip of non-matrix (grid, variance) params, the L2 term
     and per-parameter step counts (a grid param first updated at step 2 gets step-1 bias correction)."""
     import oracle as O
     t = torch_cuda
@@ -69,7 +70,7 @@ def test_optimizer_step_parity(scene, torch_cuda):
         O.adam_ema_step(w, g, m1, m2, steps, ema_tmp, ema_out, n_matrix, k + 1, lr=1e-3, beta1=0.9, beta2=0.99, eps=1e-15, l2=1e-6)
         got = tb.get_params()
         got_ema = tb.get_ema_params()
-        dw = np.abs(got - w) / np.maximum(np.abs(w), 1e-4)
+        dw = np.abs(got - w) / np.maximum(np.abs(w), 1e-3)
         de = np.abs(got_ema - ema_tmp) / np.maximum(np.abs(ema_tmp), 1e-4)
         _record(f"adam_step{k + 1}", max_rel_w=dw.max(), max_rel_ema=de.max(), frac_ema_gt_2e6=(de > 2e-6).mean())
         assert dw.max() <= 2e-6, (k, dw.argmax(), got[dw.argmax()], w[dw.argmax()])
