@@ -30,6 +30,8 @@ constexpr float MAX_CONE_STEPSIZE = STEPSIZE * (1 << (NERF_CASCADES - 1)) * NERF
 constexpr uint32_t N_MAX_RANDOM_SAMPLES_PER_RAY = 8;
 constexpr float NERF_MIN_OPTICAL_THICKNESS = 0.1f;
 constexpr uint32_t GRID3 = NERF_GRIDSIZE * NERF_GRIDSIZE * NERF_GRIDSIZE;
+// Linear mip-0 occupancy for the constant-step march: GRID3 / 32 words in (x, y, z/32) order.
+constexpr uint32_t LIN_WORDS = GRID3 / 32;
 constexpr uint32_t MAX_LEVELS = 16;
 constexpr uint32_t OUT_W = 16;      // padded network output width (nerf_network.h:935)
 constexpr uint32_t COORD_W = 7;     // NerfCoordinate floats (nerf.h:76-102)

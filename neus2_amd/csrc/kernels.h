@@ -139,12 +139,17 @@ void launch_mlp_train(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_v
 void launch_wgrad(hipStream_t s, const WGradJobs& jobs, uint32_t n_blocks);
 void launch_mfma_probe(hipStream_t s, const half_t* A, const half_t* B, float* C);
 // march.hip
-void launch_bitfield_linear(hipStream_t s, const uint8_t* bitfield, uint32_t* lin /* GRID3 / 32 words */);
+void launch_bitfield_linear(hipStream_t s, const uint8_t* bitfield, uint32_t* lin /* LIN_WORDS */);
+// Sample runs of the march (march.hip): per ray slot up to NERF_STEPS records {t of the run's first sample,
+// (samples of the ray before the run) << 16 | run length}; a run's samples are t, t + dt(t), ... (the reference's
+// t += dt), at most MARCH_RUN_MAX of them. nrec: records per slot; counter: the persistent march's ray queue.
+constexpr uint32_t MARCH_RUN_MAX = 16;
+struct MarchWork { uint2* rec; uint32_t* nrec; uint32_t* counter; uint32_t waves; /* persistent march waves, 0 = one lane per ray */ };
 // Ray generation + the occupancy march: rays (6 f32 per slot), tstart (1 per slot), nreq (requested
-// samples per slot), tbuf (NERF_STEPS f32 per slot: the t of every requested sample).
+// samples per slot) and the sample runs (MarchWork).
 void launch_march_count(hipStream_t s, uint32_t cap, const StepState* st, DPInfo dp, const DevDataset& ds, const uint8_t* bitfield,
-                        const uint32_t* lin, uint64_t rng_state, uint64_t rng_inc, float* rays, float* tstart, uint32_t* nreq, float* tbuf);
-void launch_march_write(hipStream_t s, uint32_t cap, StepState* st, const DevDataset& ds, const float* rays, const float* tbuf, const uint32_t* nreq,
+                        const uint32_t* lin, uint64_t rng_state, uint64_t rng_inc, float* rays, float* tstart, uint32_t* nreq, const MarchWork& mw);
+void launch_march_write(hipStream_t s, uint32_t cap, StepState* st, const DevDataset& ds, const float* rays, const MarchWork& mw, const uint32_t* nreq,
                         const uint32_t* base, uint32_t* numsteps, float* coords, uint32_t* sample_ray, uint32_t sample_cap /* >= max_inference */);
 void debug_launch_march_stats(hipStream_t s, uint32_t n_rays, const float* rays, const float* tstart, const uint32_t* lin, const DevDataset& ds,
                               const uint8_t* bf, uint32_t* out);

@@ -35,14 +35,14 @@ __global__ void k_bitfield_linear(const uint8_t* __restrict__ bf, uint32_t* __re
 	}
 	lin[w] = word;
 }
-
-
 // ---------------------------------------------------------------- pass 0: ray generation
 // Thread per ray slot: pixel/image pick from the ray's pcg32 stream, pinhole ray, AABB entry and
 // jittered start (testbed_nerf.cu:1263-1375). rays: 6 floats (o, unnormalised d); tstart: the jittered
 // start t, or -1 for a dropped ray and for slots >= R (nothing to march).
 __global__ void __launch_bounds__(256) k_ray_gen(uint32_t cap_rays, const StepState* __restrict__ st, DPInfo dp, DevDataset ds,
-                                                 uint64_t rng_state, uint64_t rng_inc, float* __restrict__ rays, float* __restrict__ tstart) {
+                                                 uint64_t rng_state, uint64_t rng_inc, float* __restrict__ rays, float* __restrict__ tstart,
+                                                 uint32_t* __restrict__ march_queue) {
+	if (blockIdx.x == 0 && threadIdx.x == 0) *march_queue = 0;  // the march's ray queue (next kernel on the stream)
 	const uint32_t R = st->rays_per_batch;
 	const uint32_t n_rays_global = R * dp.world, n_rays_total = st->n_rays_total;
 	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cap_rays; i += gridDim.x * blockDim.x) {
@@ -106,32 +106,144 @@ __device__ __forceinline__ void load_march_ray(const float* __restrict__ rays, u
 	}
 }
 
-// ---------------------------------------------------------------- pass 1: the march (count + t record)
-// The reference marches every ray twice inside one thread (count, then write after an atomicAdd).
-// Here the march runs once: each occupied sample's t goes to tbuf[ray][n] (NERF_STEPS floats per ray
-// slot, 1 GB at R = 2^18 of the 288 GB), and the write pass turns kept rays' t into coordinates in
-// parallel. Thread per ray slot: at R = 2^18 every ray is in flight at once (4 waves per SIMD), and
-// the loop is VALU-bound, so its body is kept branch-light (march_step).
+// ---------------------------------------------------------------- pass 1: the march (count + sample runs)
+// The reference marches every ray twice inside one thread (count, then write after an atomicAdd). Here the march
+// runs once and records, per ray, runs of consecutive samples {t of the first sample, count} (MarchWork); the
+// write pass rebuilds each sample's t by replaying the run's t += dt, the same float additions.
+// Work distribution: persistent waves pull ray slots from a queue and refill idle lanes as their rays finish,
+// so a wave does not wait on its longest ray (path lengths through the occupancy grid vary ~10x).
+// FAST (cone_angle 0, constant dt): inside an occupied interior cell every further step is a sample for as long
+// as the cell index stays the same (same occupancy bit, inside the AABB, mip 0), so the run continues on the
+// position and cell index alone (no bitfield read, no store per sample). Cells with an index 0 / 127 (a position
+// on an AABB face takes mip 1) and the centre cell (max|p - 0.5| = 0 takes mip 1) go through march_step.
+struct RunAcc { float t0; uint32_t len, cum, nrec; };
+__device__ __forceinline__ void run_flush(uint2* __restrict__ rec, RunAcc& a) {
+	if (a.len) { rec[a.nrec++] = make_uint2(__float_as_uint(a.t0), (a.cum << 16) | a.len); a.cum += a.len; a.len = 0; }
+}
+// one sample at t, following the previous sample of the open run (if any)
+__device__ __forceinline__ void run_add(uint2* __restrict__ rec, RunAcc& a, float t) {
+	if (a.len == MARCH_RUN_MAX) run_flush(rec, a);
+	if (a.len == 0) a.t0 = t;
+	++a.len;
+}
+__device__ __forceinline__ void mip0_cell(const float pos[3], int c[3]) {  // cascaded_grid_idx_at, mip 0 (march_step)
+#pragma unroll
+	for (int d = 0; d < 3; ++d) c[d] = clampi((int)(((pos[d] - 0.5f) + 0.5f) * NERF_GRIDSIZE), 0, NERF_GRIDSIZE - 1);
+}
+
+// One march event of a lane's ray: a sample run within a cell (FAST) or one march_step. Returns false once the
+// ray is finished (left the AABB or NERF_STEPS samples).
+template <bool FAST>
+__device__ __forceinline__ bool march_event(const DevDataset& ds, const uint8_t* __restrict__ bf, const uint32_t* __restrict__ lin,
+                                            const MarchRay& mr, float& t, uint32_t& n, RunAcc& acc,
+                                            uint2* __restrict__ rec) {
+	if (FAST) {
+		float pos[3];
+#pragma unroll
+		for (int d = 0; d < 3; ++d) pos[d] = mr.o[d] + t * mr.dir[d];
+		if (!aabb_contains(ds, pos)) return false;
+		const float m = fmaxf(fmaxf(fabsf(pos[0] - 0.5f), fabsf(pos[1] - 0.5f)), fabsf(pos[2] - 0.5f));
+		int c[3] = {-1, -1, -1};
+		uint32_t mip = 0;
+		bool occ, interior = false;
+		if ((m > 0.0f) & (m < 0.5f)) {
+			mip0_cell(pos, c);
+			occ = (lin[((uint32_t)c[0] << 9) | ((uint32_t)c[1] << 2) | ((uint32_t)c[2] >> 5)] >> (c[2] & 31)) & 1;
+			interior = (c[0] >= 1) & (c[0] <= NERF_GRIDSIZE - 2) & (c[1] >= 1) & (c[1] <= NERF_GRIDSIZE - 2) & (c[2] >= 1) &
+			           (c[2] <= NERF_GRIDSIZE - 2) & !((c[0] == NERF_GRIDSIZE / 2) & (c[1] == NERF_GRIDSIZE / 2) & (c[2] == NERF_GRIDSIZE / 2));
+		} else {
+			mip = (uint32_t)mip_from_pos(pos[0], pos[1], pos[2]);
+			occ = occupied(pos[0], pos[1], pos[2], bf, mip);
+		}
+		if (occ) {
+			run_add(rec, acc, t); ++n; t += MIN_CONE_STEPSIZE;
+			if (interior) {
+				while (n < NERF_STEPS) {
+					float p2[3];
+#pragma unroll
+					for (int d = 0; d < 3; ++d) p2[d] = mr.o[d] + t * mr.dir[d];
+					int c2[3]; mip0_cell(p2, c2);
+					if ((c2[0] != c[0]) | (c2[1] != c[1]) | (c2[2] != c[2])) break;
+					run_add(rec, acc, t); ++n; t += MIN_CONE_STEPSIZE;
+				}
+			}
+			return n < NERF_STEPS;
+		}
+		run_flush(rec, acc);
+		// advance_to_next_voxel with a constant step (march_step)
+		const uint32_t res = NERF_GRIDSIZE >> mip;
+		float tn = 3.402823466e+38f;
+#pragma unroll
+		for (int d = 0; d < 3; ++d) {
+			const float p = res * pos[d];
+			tn = fminf(tn, (floorf(p + 0.5f + 0.5f * signf(mr.dir[d])) - p) * mr.idir[d]);
+		}
+		const float t_target = t + fmaxf(ldexpf(tn, -(int)(7 - mip)), 0.0f);
+		do { t += MIN_CONE_STEPSIZE; } while (t < t_target);
+		return true;
+	} else {
+		float dt, pos[3];
+		const int k = march_step<false>(ds, bf, lin, mr, t, dt, pos);
+		if (k == 0) return false;
+		if (k == 1) { run_add(rec, acc, t); ++n; t += dt; return n < NERF_STEPS; }
+		run_flush(rec, acc);
+		return true;
+	}
+}
+
 template <bool FAST>
 __global__ void __launch_bounds__(256) k_march(uint32_t cap_rays, DevDataset ds, const uint8_t* __restrict__ bitfield,
                                                const uint32_t* __restrict__ lin, const float* __restrict__ rays, const float* __restrict__ tstart,
-                                               uint32_t* __restrict__ nreq, float* __restrict__ tbuf) {
-	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-	if (i >= cap_rays) return;
-	float t = tstart[i];
+                                               uint32_t* __restrict__ nreq, MarchWork mw) {
+	const uint32_t lane = threadIdx.x & 63;
+	uint32_t i = 0;
+	bool alive = false, drained = false;
+	MarchRay mr;
+	float t = 0.f;
 	uint32_t n = 0;
-	if (t >= 0.f) {
-		MarchRay mr;
-		load_march_ray(rays, i, mr, ds.motion.on != 0);
-		float* __restrict__ tr = tbuf + (size_t)i * NERF_STEPS;
-		while (n < NERF_STEPS) {
-			float dt, pos[3];
-			const int k = march_step<FAST>(ds, bitfield, lin, mr, t, dt, pos);
-			if (k == 0) break;
-			if (k == 1) { tr[n] = t; ++n; t += dt; }
+	RunAcc acc{0.f, 0u, 0u, 0u};
+	uint2* rec = mw.rec;
+	while (true) {
+		// refill the idle lanes once a quarter of the wave is idle, or all of it (wave-uniform decision)
+		const uint64_t idle = __ballot(!alive && !drained);
+		const uint64_t live = __ballot(alive);
+		const uint32_t n_idle = (uint32_t)__popcll(idle);
+		if (n_idle >= 16 || (live == 0 && n_idle > 0)) {
+			uint32_t b = 0;
+			if (lane == 0) b = atomicAdd(mw.counter, n_idle);
+			b = (uint32_t)__shfl((int)b, 0);
+			if (!alive && !drained) {
+				i = b + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+				if (i >= cap_rays) {
+					drained = true;
+				} else {
+					t = tstart[i]; n = 0; acc = RunAcc{0.f, 0u, 0u, 0u};
+					rec = mw.rec + (size_t)i * NERF_STEPS;
+					if (t >= 0.f) { load_march_ray(rays, i, mr, ds.motion.on != 0); alive = true; }
+					else { nreq[i] = 0; mw.nrec[i] = 0; }  // dropped ray / slot beyond R: nothing to march
+				}
+			}
+			continue;
+		}
+		if (live == 0) break;  // every lane drained
+		if (alive && !march_event<FAST>(ds, bitfield, lin, mr, t, n, acc, rec)) {
+			run_flush(rec, acc);
+			nreq[i] = n; mw.nrec[i] = acc.nrec;
+			alive = false;
 		}
 	}
-	nreq[i] = n;
+}
+
+// t of local sample j of ray slot i from its runs: the run holding j, then the run's t += dt replayed
+template <bool FAST>
+__device__ __forceinline__ float run_sample_t(const MarchWork& mw, uint32_t i, uint32_t j, float cone) {
+	const uint2* __restrict__ rr = mw.rec + (size_t)i * NERF_STEPS;
+	uint32_t lo = 0, hi = mw.nrec[i];
+	while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if ((rr[mid].y >> 16) <= j) lo = mid; else hi = mid; }
+	const uint2 r = rr[lo];
+	float t = __uint_as_float(r.x);
+	for (uint32_t k = r.y >> 16; k < j; ++k) t += FAST ? MIN_CONE_STEPSIZE : calc_dt(t, cone);
+	return t;
 }
 
 // ---------------------------------------------------------------- pass 2: write kept rays
@@ -170,7 +282,7 @@ __device__ __forceinline__ uint32_t last_le(const uint32_t* __restrict__ a, uint
 	return lo;
 }
 __global__ void __launch_bounds__(256) k_march_write(uint32_t cap_rays, const StepState* __restrict__ st, DevDataset ds,
-                                                     const float* __restrict__ rays, const float* __restrict__ tbuf,
+                                                     const float* __restrict__ rays, const MarchWork mw,
                                                      const uint32_t* __restrict__ nreq, const uint32_t* __restrict__ base,
                                                      float* __restrict__ coords, uint32_t* __restrict__ sample_ray) {
 	__shared__ float s_ray[6][256];
@@ -211,7 +323,7 @@ __global__ void __launch_bounds__(256) k_march_write(uint32_t cap_rays, const St
 			const uint32_t j = q - s_b[r];
 			if (j >= s_n[r]) continue;  // not a kept sample
 			const uint32_t i = rb + r;
-			const float t = tbuf[(size_t)i * NERF_STEPS + j];
+			const float t = ds.cone_angle == 0.0f ? run_sample_t<true>(mw, i, j, 0.0f) : run_sample_t<false>(mw, i, j, ds.cone_angle);
 			const float o[3] = {s_ray[0][r], s_ray[1][r], s_ray[2][r]}, dir[3] = {s_ray[3][r], s_ray[4][r], s_ray[5][r]};
 			float pos[3];
 #pragma unroll
@@ -569,17 +681,18 @@ void launch_bitfield_linear(hipStream_t s, const uint8_t* bitfield, uint32_t* li
 	k_bitfield_linear<<<GRID3 / 32 / 256, 256, 0, s>>>(bitfield, lin);
 }
 void launch_march_count(hipStream_t s, uint32_t cap, const StepState* st, DPInfo dp, const DevDataset& ds, const uint8_t* bitfield,
-                        const uint32_t* lin, uint64_t rng_state, uint64_t rng_inc, float* rays, float* tstart, uint32_t* nreq, float* tbuf) {
-	k_ray_gen<<<ray_blocks(cap), 256, 0, s>>>(cap, st, dp, ds, rng_state, rng_inc, rays, tstart);
-	const uint32_t blocks = (cap + 255) / 256;
-	if (ds.cone_angle == 0.0f) k_march<true><<<blocks, 256, 0, s>>>(cap, ds, bitfield, lin, rays, tstart, nreq, tbuf);
-	else k_march<false><<<blocks, 256, 0, s>>>(cap, ds, bitfield, nullptr, rays, tstart, nreq, tbuf);
+                        const uint32_t* lin, uint64_t rng_state, uint64_t rng_inc, float* rays, float* tstart, uint32_t* nreq, const MarchWork& mw) {
+	k_ray_gen<<<ray_blocks(cap), 256, 0, s>>>(cap, st, dp, ds, rng_state, rng_inc, rays, tstart, mw.counter);
+	const uint32_t waves = mw.waves ? std::min(mw.waves, (cap + 63) / 64) : (cap + 63) / 64;
+	const uint32_t blocks = std::max<uint32_t>(1, (waves + 3) / 4);
+	if (ds.cone_angle == 0.0f) k_march<true><<<blocks, 256, 0, s>>>(cap, ds, bitfield, lin, rays, tstart, nreq, mw);
+	else k_march<false><<<blocks, 256, 0, s>>>(cap, ds, bitfield, nullptr, rays, tstart, nreq, mw);
 }
-void launch_march_write(hipStream_t s, uint32_t cap, StepState* st, const DevDataset& ds, const float* rays, const float* tbuf, const uint32_t* nreq,
+void launch_march_write(hipStream_t s, uint32_t cap, StepState* st, const DevDataset& ds, const float* rays, const MarchWork& mw, const uint32_t* nreq,
                         const uint32_t* base, uint32_t* numsteps, float* coords, uint32_t* sample_ray, uint32_t sample_cap) {
 	k_march_numsteps<<<(cap + 255) / 256, 256, 0, s>>>(cap, st, nreq, base, numsteps);
 	// one block per WRITE_CHUNK samples of the largest possible kept extent (max_inference <= sample_cap)
-	k_march_write<<<std::max<uint32_t>(1, (sample_cap + WRITE_CHUNK - 1) / WRITE_CHUNK), 256, 0, s>>>(cap, st, ds, rays, tbuf, nreq, base, coords, sample_ray);
+	k_march_write<<<std::max<uint32_t>(1, (sample_cap + WRITE_CHUNK - 1) / WRITE_CHUNK), 256, 0, s>>>(cap, st, ds, rays, mw, nreq, base, coords, sample_ray);
 }
 void debug_launch_march_stats(hipStream_t s, uint32_t n_rays, const float* rays, const float* tstart, const uint32_t* lin, const DevDataset& ds,
                               const uint8_t* bf, uint32_t* out) {

@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <random>
 #include <stdexcept>
@@ -149,8 +150,10 @@ struct NeusTestbed {
 	uint32_t density_grid_ema_step = 0;
 	// step workspace
 	uint32_t batch = 0, max_samples = 0;
-	Dev<float> rays, startt, tbuf_t, coords, coords_c, loss, ek, mask, loss_sum;
-	Dev<uint32_t> nreq, base, numsteps, ccount, cbase, enc;
+	Dev<float> rays, startt, coords, coords_c, loss, ek, mask, loss_sum;
+	Dev<uint32_t> nreq, base, numsteps, ccount, cbase, enc, march_nrec, march_queue;
+	Dev<uint2> march_rec;
+	MarchWork mwork{};
 	Dev<float> dydx;
 	Dev<half_t> net_out, dL_dout, trainbuf;
 	Dev<float4> vbuf;
@@ -258,7 +261,7 @@ struct NeusTestbed {
 		HIP_CHECK(hipMemset(density_grid.p, 0, n_cells * 4));
 		bitfield.alloc(GRID3 / 8 * NERF_CASCADES);
 		HIP_CHECK(hipMemset(bitfield.p, 0xff, GRID3 / 8 * NERF_CASCADES));
-		bf_lin.alloc(GRID3 / 32);
+		bf_lin.alloc(LIN_WORDS);
 		launch_bitfield_linear(stream, bitfield.p, bf_lin.p);
 		grid_mean.alloc(4); grid_partial.alloc(GRID3 / 1024);
 		HIP_CHECK(hipMemset(grid_mean.p, 0, 16));
@@ -354,7 +357,9 @@ struct NeusTestbed {
 		// workspace
 		batch = c.batch_size;
 		max_samples = batch * 16;  // testbed_nerf.cu:3725
-		rays.alloc(6 * (size_t)MAX_RAYS); startt.alloc((size_t)MAX_RAYS); tbuf_t.alloc((size_t)MAX_RAYS * NERF_STEPS); nreq.alloc(MAX_RAYS); base.alloc(MAX_RAYS);
+		rays.alloc(6 * (size_t)MAX_RAYS); startt.alloc((size_t)MAX_RAYS);
+		march_rec.alloc((size_t)MAX_RAYS * NERF_STEPS); march_nrec.alloc(MAX_RAYS); march_queue.alloc(1);
+		mwork = MarchWork{march_rec.p, march_nrec.p, march_queue.p, march_waves()}; nreq.alloc(MAX_RAYS); base.alloc(MAX_RAYS);
 		numsteps.alloc(2 * (size_t)MAX_RAYS); ccount.alloc(MAX_RAYS); cbase.alloc(MAX_RAYS);
 		l_sa.alloc(max_samples); l_ekt.alloc(max_samples); sample_ray.alloc(max_samples);
 		l_ck4.alloc(max_samples / 8 + 1); l_cke.alloc(max_samples / 8 + 1);
@@ -461,6 +466,13 @@ struct NeusTestbed {
 		train_canonical = false;
 		train_delta = cfg.predict_global_movement != 0;
 		HIP_CHECK(hipStreamSynchronize(stream));
+	}
+	// march waves launched (NEUS_MARCH_WAVES overrides). Default 0 = one lane per ray slot: the march is
+	// latency-bound (occupancy lookups), and measured on MI355X every wave fewer than the slots was slower
+	// (R = 2^18: 4096 waves 0.58 ms, 2048 0.75 ms, 1024 1.28 ms); the queue then only re-fills dropped slots.
+	uint32_t march_waves() const {
+		if (const char* e = std::getenv("NEUS_MARCH_WAVES")) return (uint32_t)std::strtoul(e, nullptr, 10);
+		return 0;
 	}
 	uint32_t gm_steps() const { return cfg.predict_global_movement ? cfg.global_movement_steps : 0u; }
 
@@ -773,9 +785,9 @@ struct NeusTestbed {
 		HIP_CHECK(hipMemsetAsync(&st.p->n_rays_with_samples, 0, 4, s));
 		const DPInfo dp{rank, world};
 		mark(1);
-		launch_march_count(s, MAX_RAYS, st.p, dp, ds, bitfield.p, bf_lin.p, rng.state, rng.inc, rays.p, startt.p, nreq.p, tbuf_t.p);
+		launch_march_count(s, MAX_RAYS, st.p, dp, ds, bitfield.p, bf_lin.p, rng.state, rng.inc, rays.p, startt.p, nreq.p, mwork);
 		launch_exclusive_scan(s, scan_tmp.p, scan_tmp_bytes, nreq.p, base.p, MAX_RAYS);
-		launch_march_write(s, MAX_RAYS, st.p, ds, rays.p, tbuf_t.p, nreq.p, base.p, numsteps.p, coords.p, sample_ray.p, max_samples);
+		launch_march_write(s, MAX_RAYS, st.p, ds, rays.p, mwork, nreq.p, base.p, numsteps.p, coords.p, sample_ray.p, max_samples);
 		mark(2);
 		// DeltaNetwork forward on the samples (nerf_network.h:162-182); the loss keeps the undeformed records
 		const float* c_in = coords.p;
@@ -1146,9 +1158,9 @@ static void time_kernel_impl(NeusTestbed* tb, int kernel, int variant, int iters
 		auto march = [&]() {
 			HIP_CHECK(hipMemsetAsync(&t.st.p->n_kept, 0, 4, s));
 			HIP_CHECK(hipMemsetAsync(&t.st.p->n_rays_with_samples, 0, 4, s));
-			launch_march_count(s, MAX_RAYS, t.st.p, dp, t.ds, t.bitfield.p, lin, t.rng.state, t.rng.inc, t.rays.p, t.startt.p, t.nreq.p, t.tbuf_t.p);
+			launch_march_count(s, MAX_RAYS, t.st.p, dp, t.ds, t.bitfield.p, lin, t.rng.state, t.rng.inc, t.rays.p, t.startt.p, t.nreq.p, t.mwork);
 			launch_exclusive_scan(s, t.scan_tmp.p, t.scan_tmp_bytes, t.nreq.p, t.base.p, MAX_RAYS);
-			launch_march_write(s, MAX_RAYS, t.st.p, t.ds, t.rays.p, t.tbuf_t.p, t.nreq.p, t.base.p, t.numsteps.p, t.coords.p,
+			launch_march_write(s, MAX_RAYS, t.st.p, t.ds, t.rays.p, t.mwork, t.nreq.p, t.base.p, t.numsteps.p, t.coords.p,
 			                   t.sample_ray.p, t.max_samples);
 		};
 		const LossWork w = t.loss_work(t.base.p);
@@ -1164,8 +1176,8 @@ static void time_kernel_impl(NeusTestbed* tb, int kernel, int variant, int iters
 		for (int k = 0; k < iters; ++k) {
 			HIP_CHECK(hipEventRecord(evs[k], s));
 			switch (kernel) {
-			case 0: launch_march_count(s, MAX_RAYS, t.st.p, dp, t.ds, t.bitfield.p, lin, t.rng.state, t.rng.inc, t.rays.p, t.startt.p, t.nreq.p, t.tbuf_t.p); break;
-			case 1: launch_march_write(s, MAX_RAYS, t.st.p, t.ds, t.rays.p, t.tbuf_t.p, t.nreq.p, t.base.p, t.numsteps.p,
+			case 0: launch_march_count(s, MAX_RAYS, t.st.p, dp, t.ds, t.bitfield.p, lin, t.rng.state, t.rng.inc, t.rays.p, t.startt.p, t.nreq.p, t.mwork); break;
+			case 1: launch_march_write(s, MAX_RAYS, t.st.p, t.ds, t.rays.p, t.mwork, t.nreq.p, t.base.p, t.numsteps.p,
 			                           t.coords.p, t.sample_ray.p, t.max_samples); break;
 			case 2: debug_launch_loss_scan(s, variant, MAX_RAYS, t.numsteps.p, w, t.ccount.p); break;
 			case 3: launch_nerf_infer(s, t.lay.L, t.lay.W, &t.st.p->n_kept, 0, t.coords.p, t.gl, valid, t.params_h.p + t.lay.grid_off, t.mlp,
@@ -1329,14 +1341,16 @@ int neus_sample_rays(NeusTestbed* tb, void* stream, uint32_t n_rays, uint32_t ra
 		Dev<StepState> sst; sst.alloc(1);
 		StepState h{}; h.rays_per_batch = n_rays; h.max_inference = max_samples; h.n_rays_total = n_rays_total;
 		HIP_CHECK(hipMemcpyAsync(sst.p, &h, sizeof(h), hipMemcpyHostToDevice, s));
-		Dev<float> st_t, tb_t; st_t.alloc(n_rays); tb_t.alloc((size_t)n_rays * NERF_STEPS); Dev<uint32_t> nr, bs; nr.alloc(n_rays); bs.alloc(n_rays);
+		Dev<float> st_t; st_t.alloc(n_rays); Dev<uint32_t> nr, bs, nrec, q; nr.alloc(n_rays); bs.alloc(n_rays); nrec.alloc(n_rays); q.alloc(1);
+		Dev<uint2> rec; rec.alloc((size_t)n_rays * NERF_STEPS);
+		const MarchWork mw{rec.p, nrec.p, q.p, tb->mwork.waves};
 		Dev<uint8_t> tmp; const size_t tb_ = scan_temp_bytes(n_rays); tmp.alloc(tb_ + 256);
-		Dev<uint32_t> lin; lin.alloc(GRID3 / 32);
+		Dev<uint32_t> lin; lin.alloc(LIN_WORDS);
 		launch_bitfield_linear(s, bitfield, lin.p);
-		launch_march_count(s, n_rays, sst.p, DPInfo{rank, world}, tb->ds, bitfield, lin.p, rng_state, rng_inc, rays, st_t.p, nr.p, tb_t.p);
+		launch_march_count(s, n_rays, sst.p, DPInfo{rank, world}, tb->ds, bitfield, lin.p, rng_state, rng_inc, rays, st_t.p, nr.p, mw);
 		launch_exclusive_scan(s, tmp.p, tb_, nr.p, bs.p, n_rays);
 		Dev<uint32_t> sr; sr.alloc(std::max<uint32_t>(1, max_samples));
-		launch_march_write(s, n_rays, sst.p, tb->ds, rays, tb_t.p, nr.p, bs.p, numsteps, coords, sr.p, max_samples);
+		launch_march_write(s, n_rays, sst.p, tb->ds, rays, mw, nr.p, bs.p, numsteps, coords, sr.p, max_samples);
 		HIP_CHECK(hipMemcpyAsync(&h, sst.p, sizeof(h), hipMemcpyDeviceToHost, s));
 		HIP_CHECK(hipStreamSynchronize(s));
 		counters_out[0] = h.numsteps_counter; counters_out[1] = h.n_kept; counters_out[2] = h.n_rays_with_samples;
