@@ -230,6 +230,14 @@ int neus_testbed_kernel_times(NeusTestbed* tb, float* ms_out /* NEUS_N_PHASES + 
 /* ------------------------------------------------------------------ data parallel (RCCL over xGMI) */
 int neus_nccl_unique_id(uint8_t* out /* 128 bytes */);
 int neus_testbed_init_data_parallel(NeusTestbed* tb, int rank, int world, const uint8_t* unique_id /* 128 bytes */);
+/* In-process ranks: `world` testbeds driven from `world` host threads exchange through host staging buffers
+ * (same step and collectives as the RCCL path: sharded occupancy update + max all-reduce, gradient / counter /
+ * loss / DeltaNetwork sum all-reduces). For several ranks on one device (tests); collectives block until every
+ * rank has arrived (120 s timeout -> error). The group must outlive its testbeds' training calls. */
+typedef struct NeusLocalGroup NeusLocalGroup;
+int neus_local_group_create(int world, NeusLocalGroup** out);
+int neus_local_group_destroy(NeusLocalGroup* group);
+int neus_testbed_init_local_group(NeusTestbed* tb, NeusLocalGroup* group, int rank);
 
 /* ------------------------------------------------------------------ operator surface (device buffers) */
 /* Hash-grid forward on n positions (AoS, `coord_stride` floats per sample, xyz first).

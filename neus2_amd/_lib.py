@@ -80,7 +80,8 @@ EXPORTS = [
     "neus_testbed_get_density_grid", "neus_testbed_set_density_grid", "neus_testbed_restore_state", "neus_testbed_get_rng", "neus_testbed_render", "neus_testbed_sdf_on_grid",
     "neus_testbed_marching_cubes", "neus_testbed_get_mesh", "neus_testbed_mesh_vertex_colors", "neus_mc_table", "neus_testbed_ray_counts", "neus_debug_time_kernel", "neus_debug_march_stats", "neus_testbed_time_kernel", "neus_testbed_stream",
     "neus_testbed_synchronize", "neus_testbed_set_profiling", "neus_testbed_kernel_times",
-    "neus_nccl_unique_id", "neus_testbed_init_data_parallel",
+    "neus_nccl_unique_id", "neus_testbed_init_data_parallel", "neus_local_group_create", "neus_local_group_destroy",
+    "neus_testbed_init_local_group",
     "neus_grid_encode", "neus_net_forward", "neus_net_backward", "neus_sample_rays", "neus_loss_compact",
     "neus_optimizer_step", "neus_fill_rollover", "neus_occ_update", "neus_mfma_probe",
     "neus_testbed_next_frame", "neus_testbed_get_movement", "neus_testbed_set_movement", "neus_testbed_frame_state",

@@ -190,6 +190,10 @@ void launch_delta_prepare(hipStream_t s, DeltaState* ds);
 void launch_delta_apply(hipStream_t s, const uint32_t* n_ptr, uint32_t n_cap, uint32_t stride, const float* in, float* out, const DeltaState* ds);
 void launch_delta_backward(hipStream_t s, const uint32_t* n_ptr, uint32_t n_cap, const float* coords, uint32_t stride, const float4* dpos,
                            DeltaState* ds, float* partial, const DeltaAdam& a);
+// the two halves of launch_delta_backward (a data-parallel step all-reduces the partial sums in between)
+void launch_delta_grad(hipStream_t s, const uint32_t* n_ptr, uint32_t n_cap, const float* coords, uint32_t stride, const float4* dpos,
+                       const DeltaState* ds, float* partial);
+void launch_delta_step(hipStream_t s, const float* partial, DeltaState* ds, const DeltaAdam& a);
 size_t delta_partial_floats();
 void host_accumulate_movement(const float delta_p[DELTA_PARAMS], float accR[9], float acct[3]);
 // scan.hip
@@ -203,8 +207,9 @@ void launch_cast_half(hipStream_t s, uint32_t n, const float* in, half_t* out);
 void launch_transpose_w(hipStream_t s, const TransposeJobs& jobs);
 struct DinPerm { int32_t p[48]; uint32_t din, W; };
 void launch_permute_din(hipStream_t s, const half_t* d0, half_t* d0p, half_t* d0Tp, const DinPerm& perm);
-void launch_grid_samples(hipStream_t s, uint32_t n, uint32_t out_offset, uint64_t rng_state, uint64_t rng_inc, uint32_t step,
-                         const float* aabb_min, const float* aabb_max, const float* grid_in, float* pos, uint32_t* indices,
+// samples [i_begin, i_end) of an n-sample generate_grid_samples_nerf_nonuniform call, written from out_base
+void launch_grid_samples(hipStream_t s, uint32_t n, uint32_t i_begin, uint32_t i_end, uint32_t out_base, uint64_t rng_state, uint64_t rng_inc,
+                         uint32_t step, const float* aabb_min, const float* aabb_max, const float* grid_in, float* pos, uint32_t* indices,
                          uint32_t n_cascades, float thresh);
 void launch_splat_max(hipStream_t s, uint32_t n, const uint32_t* indices, const float* density, float* grid_tmp);
 void launch_ema_grid(hipStream_t s, uint32_t n, float decay, float* grid, const float* tmp);

@@ -222,6 +222,13 @@ void launch_delta_backward(hipStream_t s, const uint32_t* n_ptr, uint32_t n_cap,
 	k_delta_grad<<<DELTA_BLOCKS, 256, 0, s>>>(n_ptr, n_cap, coords, stride, dpos, ds, partial);
 	k_delta_step<<<1, 64, 0, s>>>(partial, DELTA_BLOCKS, ds, a);
 }
+void launch_delta_grad(hipStream_t s, const uint32_t* n_ptr, uint32_t n_cap, const float* coords, uint32_t stride, const float4* dpos,
+                       const DeltaState* ds, float* partial) {
+	k_delta_grad<<<DELTA_BLOCKS, 256, 0, s>>>(n_ptr, n_cap, coords, stride, dpos, ds, partial);
+}
+void launch_delta_step(hipStream_t s, const float* partial, DeltaState* ds, const DeltaAdam& a) {
+	k_delta_step<<<1, 64, 0, s>>>(partial, DELTA_BLOCKS, ds, a);
+}
 size_t delta_partial_floats() { return (size_t)DELTA_BLOCKS * 9; }
 
 // accumulate_global_movement_rotation_6d_kernel (common_operation.cuh:551-585), run on the host at a frame

@@ -72,11 +72,13 @@ __global__ void k_transpose_w(TransposeJobs jobs) {
 }
 
 // positions: 3 floats (warped) per sample; indices: density grid cell.
-__global__ void k_grid_samples(uint32_t n_elements, uint32_t out_offset, uint64_t rng_state, uint64_t rng_inc, uint32_t step,
-                               float aabb_min_x, float aabb_min_y, float aabb_min_z, float diag_x, float diag_y, float diag_z,
+// Samples i_begin .. i_end - 1 of the n_elements of one generate call (a data-parallel rank evaluates its shard
+// of the global sample range), written from out_base on.
+__global__ void k_grid_samples(uint32_t n_elements, uint32_t i_begin, uint32_t i_end, uint32_t out_base, uint64_t rng_state, uint64_t rng_inc,
+                               uint32_t step, float aabb_min_x, float aabb_min_y, float aabb_min_z, float diag_x, float diag_y, float diag_z,
                                const float* __restrict__ grid_in, float* __restrict__ pos, uint32_t* __restrict__ indices,
                                uint32_t n_cascades, float thresh) {
-	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_elements; i += gridDim.x * blockDim.x) {
+	for (uint32_t i = i_begin + blockIdx.x * blockDim.x + threadIdx.x; i < i_end; i += gridDim.x * blockDim.x) {
 		pcg32 rng(rng_state, rng_inc);
 		rng.advance((int64_t)(uint32_t)(i * 4));
 		const uint32_t level = (uint32_t)(rng.next_float() * n_cascades) % n_cascades;
@@ -93,7 +95,7 @@ __global__ void k_grid_samples(uint32_t n_elements, uint32_t out_offset, uint64_
 		const float px = (((float)x + rx) / NERF_GRIDSIZE - 0.5f) * sc + 0.5f;
 		const float py = (((float)y + ry) / NERF_GRIDSIZE - 0.5f) * sc + 0.5f;
 		const float pz = (((float)z + rz) / NERF_GRIDSIZE - 0.5f) * sc + 0.5f;
-		const uint32_t o = out_offset + i;
+		const uint32_t o = out_base + (i - i_begin);
 		pos[3 * (size_t)o + 0] = (px - aabb_min_x) / diag_x;
 		pos[3 * (size_t)o + 1] = (py - aabb_min_y) / diag_y;
 		pos[3 * (size_t)o + 2] = (pz - aabb_min_z) / diag_z;
@@ -167,11 +169,11 @@ void launch_transpose_w(hipStream_t s, const TransposeJobs& jobs) { if (jobs.n) 
 void launch_permute_din(hipStream_t s, const half_t* d0, half_t* d0p, half_t* d0Tp, const DinPerm& perm) {
 	k_permute_din<<<1, 256, 0, s>>>(d0, d0p, d0Tp, perm);
 }
-void launch_grid_samples(hipStream_t s, uint32_t n, uint32_t out_offset, uint64_t rng_state, uint64_t rng_inc, uint32_t step,
-                         const float* aabb_min, const float* aabb_max, const float* grid_in, float* pos, uint32_t* indices,
+void launch_grid_samples(hipStream_t s, uint32_t n, uint32_t i_begin, uint32_t i_end, uint32_t out_base, uint64_t rng_state, uint64_t rng_inc,
+                         uint32_t step, const float* aabb_min, const float* aabb_max, const float* grid_in, float* pos, uint32_t* indices,
                          uint32_t n_cascades, float thresh) {
-	if (!n) return;
-	k_grid_samples<<<nblk(n), 256, 0, s>>>(n, out_offset, rng_state, rng_inc, step, aabb_min[0], aabb_min[1], aabb_min[2],
+	if (i_end <= i_begin) return;
+	k_grid_samples<<<nblk(i_end - i_begin), 256, 0, s>>>(n, i_begin, i_end, out_base, rng_state, rng_inc, step, aabb_min[0], aabb_min[1], aabb_min[2],
 	                                        aabb_max[0] - aabb_min[0], aabb_max[1] - aabb_min[1], aabb_max[2] - aabb_min[2],
 	                                        grid_in, pos, indices, n_cascades, thresh);
 }

@@ -13,7 +13,10 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <mutex>
 #include <cstdlib>
 #include <cstring>
 #include <random>
@@ -98,6 +101,43 @@ struct Layout {
 
 } // namespace
 
+// In-process data-parallel group: `world` testbeds driven from `world` host threads exchange through host staging
+// buffers (sum in rank order, max), with the same call sequence as the RCCL path. It lets the data-parallel step
+// (sharded occupancy update, gradient / counter / loss / DeltaNetwork all-reduces) run with several ranks on one
+// device, e.g. in tests; production ranks use RCCL (neus_testbed_init_data_parallel).
+struct NeusLocalGroup {
+	enum Op { SUM, MAX };
+	uint32_t world;
+	std::mutex mu;
+	std::condition_variable cv;
+	uint32_t arrived = 0, generation = 0;
+	std::vector<std::vector<uint8_t>> stage;
+	explicit NeusLocalGroup(uint32_t w) : world(w), stage(w) {}
+	void barrier() {
+		std::unique_lock<std::mutex> lk(mu);
+		const uint32_t gen = generation;
+		if (++arrived == world) { arrived = 0; ++generation; cv.notify_all(); return; }
+		if (!cv.wait_for(lk, std::chrono::seconds(120), [&] { return generation != gen; }))
+			throw std::runtime_error("local group: barrier timeout (a rank did not reach the collective)");
+	}
+	// in-place all-reduce of n elements of T on the device, on `s` (host-synchronous)
+	template <class T> void allreduce(uint32_t rank, T* dev, size_t n, Op op, hipStream_t s) {
+		std::vector<uint8_t>& mine = stage[rank];
+		mine.resize(n * sizeof(T));
+		HIP_CHECK(hipMemcpyAsync(mine.data(), dev, n * sizeof(T), hipMemcpyDeviceToHost, s));
+		HIP_CHECK(hipStreamSynchronize(s));
+		barrier();
+		std::vector<T> out(n);
+		for (uint32_t r = 0; r < world; ++r) {
+			const T* v = (const T*)stage[r].data();
+			for (size_t k = 0; k < n; ++k) out[k] = r == 0 ? v[k] : (op == SUM ? (T)(out[k] + v[k]) : std::max(out[k], v[k]));
+		}
+		barrier();  // every rank has read every stage before the next collective overwrites one
+		HIP_CHECK(hipMemcpyAsync(dev, out.data(), n * sizeof(T), hipMemcpyHostToDevice, s));
+		HIP_CHECK(hipStreamSynchronize(s));
+	}
+};
+
 struct NeusTestbed {
 	int device = 0;
 	hipStream_t stream = nullptr;
@@ -180,8 +220,9 @@ struct NeusTestbed {
 	bool loss_ema_init = false;
 	float* pinned = nullptr;  // [0..3]: loss sum, ek sum, mask sum, grid mean ; [4..]: StepState copy
 	bool loss_pending = false;
-	// data parallel
+	// data parallel: RCCL communicator (production) or an in-process group
 	ncclComm_t comm = nullptr;
+	NeusLocalGroup* group = nullptr;
 	uint32_t rank = 0, world = 1;
 	// profiling
 	bool profiling = false;
@@ -565,24 +606,46 @@ struct NeusTestbed {
 		                    scan_tmp_bytes);
 	}
 
+	// ------------------------------------------------------------ collectives
+	void coll_begin() { if (comm) NCCL_CHECK(ncclGroupStart()); }
+	void coll_end() { if (comm) NCCL_CHECK(ncclGroupEnd()); }
+	void allreduce_f32(float* p, size_t n, bool max_op = false) {
+		if (world == 1) return;
+		if (comm) NCCL_CHECK(ncclAllReduce(p, p, n, ncclFloat32, max_op ? ncclMax : ncclSum, comm, stream));
+		else if (group) group->allreduce<float>(rank, p, n, max_op ? NeusLocalGroup::MAX : NeusLocalGroup::SUM, stream);
+		else throw std::runtime_error("data parallel: no communicator");
+	}
+	void allreduce_u32(uint32_t* p, size_t n) {
+		if (world == 1) return;
+		if (comm) NCCL_CHECK(ncclAllReduce(p, p, n, ncclUint32, ncclSum, comm, stream));
+		else if (group) group->allreduce<uint32_t>(rank, p, n, NeusLocalGroup::SUM, stream);
+		else throw std::runtime_error("data parallel: no communicator");
+	}
+
 	// ------------------------------------------------------------ occupancy grid (testbed_nerf.cu:3293-3397, 4003-4016)
 	void occ_update(uint32_t n_uniform, uint32_t n_nonuniform, uint32_t valid, bool use_delta = false) {
 		hipStream_t s = stream;
 		const uint32_t n_cells = GRID3 * (max_cascade + 1);
 		if (training_step == 0) { HIP_CHECK(hipMemsetAsync(density_grid.p, 0, n_cells * 4, s)); density_grid_ema_step = 0; }
 		HIP_CHECK(hipMemsetAsync(density_tmp.p, 0, n_cells * 4, s));
-		const uint32_t N = n_uniform + n_nonuniform;
-		launch_grid_samples(s, n_uniform, 0, density_grid_rng.state, density_grid_rng.inc, density_grid_ema_step, ds.aabb_min, ds.aabb_max,
-		                    density_grid.p, occ_pos.p, occ_idx.p, max_cascade + 1, -0.01f);
+		// data parallel: rank r evaluates the global samples [lo, hi) (same density_grid_rng on every rank); the
+		// max-splatted grids are then max-all-reduced, which equals the single-GPU splat (max is exact)
+		const uint32_t NT = n_uniform + n_nonuniform;
+		const uint32_t lo = (uint32_t)((uint64_t)NT * rank / world), hi = (uint32_t)((uint64_t)NT * (rank + 1) / world);
+		const uint32_t N = hi - lo;
+		launch_grid_samples(s, n_uniform, std::min(lo, n_uniform), std::min(hi, n_uniform), 0, density_grid_rng.state, density_grid_rng.inc,
+		                    density_grid_ema_step, ds.aabb_min, ds.aabb_max, density_grid.p, occ_pos.p, occ_idx.p, max_cascade + 1, -0.01f);
 		density_grid_rng.advance();
-		launch_grid_samples(s, n_nonuniform, n_uniform, density_grid_rng.state, density_grid_rng.inc, density_grid_ema_step, ds.aabb_min, ds.aabb_max,
-		                    density_grid.p, occ_pos.p, occ_idx.p, max_cascade + 1, NERF_MIN_OPTICAL_THICKNESS);
+		launch_grid_samples(s, n_nonuniform, std::max(lo, n_uniform) - n_uniform, std::max(hi, n_uniform) - n_uniform,
+		                    std::max(lo, n_uniform) - lo, density_grid_rng.state, density_grid_rng.inc, density_grid_ema_step, ds.aabb_min,
+		                    ds.aabb_max, density_grid.p, occ_pos.p, occ_idx.p, max_cascade + 1, NERF_MIN_OPTICAL_THICKNESS);
 		density_grid_rng.advance();
 		// NerfNetwork::density on the samples, hash-grid encode fused in; with the DeltaNetwork active the
 		// positions are moved first (nerf_network.h:664-675)
 		if (use_delta) launch_delta_apply(s, nullptr, N, 3, occ_pos.p, occ_pos.p, delta.p);
 		launch_nerf_density(s, lay.L, lay.W, N, occ_pos.p, gl, valid, params_h.p + lay.grid_off, mlp, occ_density.p);
 		launch_splat_max(s, N, occ_idx.p, occ_density.p, density_tmp.p);
+		allreduce_f32(density_tmp.p, n_cells, true);
 		launch_ema_grid(s, n_cells, cfg.density_grid_decay, density_grid.p, density_tmp.p);
 		++density_grid_ema_step;
 		launch_grid_mean(s, density_grid.p, grid_partial.p, grid_mean.p);
@@ -815,18 +878,26 @@ struct NeusTestbed {
 		} else {
 			net_backward(&st.p->compacted_counter, &st.p->n_train, batch, coords_c.p, valid, dL_dout.p, grads.p, s, true, train_canonical);
 		}
+		// DeltaNetwork gradient partial sums (the first half of its backward; the Adam step follows the exchange)
+		if (use_delta) launch_delta_grad(s, &st.p->n_train, batch, coords_c.p, COORD_W, dpos.p, delta.p, delta_partial.p);
 		mark(8);
-		if (world > 1) {
-			NCCL_CHECK(ncclGroupStart());
-			NCCL_CHECK(ncclAllReduce(grads.p, grads.p, lay.P, ncclFloat32, ncclSum, comm, s));
-			NCCL_CHECK(ncclAllReduce(&st.p->numsteps_counter, &st.p->numsteps_counter, 1, ncclUint32, ncclSum, comm, s));
-			NCCL_CHECK(ncclAllReduce(&st.p->compacted_counter, &st.p->compacted_counter, 1, ncclUint32, ncclSum, comm, s));
-			NCCL_CHECK(ncclGroupEnd());
-		}
 		if (get_loss) {
 			launch_sum_f32(s, scan_tmp.p, scan_tmp_bytes, loss.p, loss_sum.p + 0, MAX_RAYS);
 			launch_sum_f32(s, scan_tmp.p, scan_tmp_bytes, ek.p, loss_sum.p + 1, MAX_RAYS);
 			launch_sum_f32(s, scan_tmp.p, scan_tmp_bytes, mask.p, loss_sum.p + 2, MAX_RAYS);
+		}
+		if (world > 1) {
+			// collective 1 (gradients; DeltaNetwork partials) and 3 (counters, loss scalars) of SURVEY §8(e), one group
+			coll_begin();
+			allreduce_f32(grads.p, lay.P);
+			allreduce_u32(&st.p->numsteps_counter, 1);
+			allreduce_u32(&st.p->compacted_counter, 1);
+			allreduce_u32(&st.p->n_rays_with_samples, 1);
+			if (use_delta) allreduce_f32(delta_partial.p, delta_partial_floats());
+			if (get_loss) allreduce_f32(loss_sum.p, 3);
+			coll_end();
+		}
+		if (get_loss) {
 			HIP_CHECK(hipMemcpyAsync(pinned, loss_sum.p, 3 * 4, hipMemcpyDeviceToHost, s));
 			HIP_CHECK(hipMemcpyAsync(pinned + 4, st.p, sizeof(StepState), hipMemcpyDeviceToHost, s));
 			loss_pending = true;
@@ -843,7 +914,7 @@ struct NeusTestbed {
 				delta_lr_factor *= cfg.gm_decay_base;
 			++delta_step;
 			DeltaAdam a{cfg.gm_learning_rate * delta_lr_factor, cfg.gm_beta1, cfg.gm_beta2, cfg.gm_epsilon, LOSS_SCALE, 1u};
-			launch_delta_backward(s, &st.p->n_train, batch, coords_c.p, COORD_W, dpos.p, delta.p, delta_partial.p, a);
+			launch_delta_step(s, delta_partial.p, delta.p, a);
 		}
 		mark(10);
 		++training_step;
@@ -1255,6 +1326,22 @@ int neus_testbed_init_data_parallel(NeusTestbed* tb, int rank, int world, const 
 			std::memcpy(&id, uid, 128);
 			NCCL_CHECK(ncclCommInitRank(&tb->comm, world, id, rank));
 		}
+	});
+}
+
+int neus_local_group_create(int world, NeusLocalGroup** out) {
+	return guard([&] {
+		if (world < 1 || world > 64) throw std::runtime_error("local group: world must be 1..64");
+		*out = new NeusLocalGroup((uint32_t)world);
+	});
+}
+int neus_local_group_destroy(NeusLocalGroup* g) { return guard([&] { delete g; }); }
+int neus_testbed_init_local_group(NeusTestbed* tb, NeusLocalGroup* g, int rank) {
+	return guard([&] {
+		if (!g || rank < 0 || (uint32_t)rank >= g->world) throw std::runtime_error("invalid local group / rank");
+		if (tb->comm) throw std::runtime_error("testbed already has an RCCL communicator");
+		tb->group = g; tb->rank = (uint32_t)rank; tb->world = g->world;
+		tb->tbuf.indeed_batch = (float)tb->batch * (float)tb->world;
 	});
 }
 

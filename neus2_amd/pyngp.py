@@ -630,6 +630,24 @@ class Testbed:
         return self._h
 
 
+class LocalGroup:
+    """In-process data-parallel group (neus_local_group_create): `world` testbeds, each trained from its own host
+    thread, exchange through host staging with the RCCL path's collectives (several ranks on one device)."""
+
+    def __init__(self, world: int):
+        self._h = C.c_void_p()
+        check(lib().neus_local_group_create(C.c_int(world), C.byref(self._h)))
+        self.world = world
+
+    def join(self, tb, rank: int):
+        check(lib().neus_testbed_init_local_group(tb.handle, self._h, C.c_int(rank)))
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().neus_local_group_destroy(self._h)
+            self._h = None
+
+
 def nccl_unique_id() -> bytes:
     buf = (C.c_uint8 * 128)()
     check(lib().neus_nccl_unique_id(buf))
