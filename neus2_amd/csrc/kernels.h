@@ -24,7 +24,8 @@ struct TrainBufs {
 	half_t* r2_delta; half_t* r2_x;   // [16][ld], [W][ld]
 	half_t* dLdenc; half_t* genc;     // [L][ld] half2 (features 2l, 2l+1)
 	float4* v;                        // [ld]
-	float* var_grad;                  // scalar accumulator
+	float* var_grad;                  // variance gradient (written by the weight-gradient reduction)
+	float* var_partial;               // [blocks of the colour kernel] per-block sums of dL/dout[7]
 	float indeed_batch;
 	float4* dpos;                     // [ld] dL/d(network input position), first order (null: not needed)
 };
@@ -44,7 +45,13 @@ struct DeltaAdam { float lr, beta1, beta2, eps, loss_scale; uint32_t optimize; }
 struct RayMotion { float R[9]; float t[3]; uint32_t on; };
 
 struct WGradJob { const half_t* D; const half_t* X; float* dW; uint32_t M, K, ncols, ldc; uint32_t tiles_m, tiles_k; };
-struct WGradJobs { WGradJob j[5]; uint32_t n_jobs; uint32_t split; uint32_t block_start[6]; const uint32_t* n_valid; };
+// Weight gradients without atomics: every (job, 32x32 tile, sample split) block writes its partial tile to
+// `partial` (block-major, 1024 floats each); k_wgrad_reduce sums the splits in a fixed order into dW, and the
+// colour kernel's per-block variance sums into var_grad (bitwise reproducible).
+struct WGradJobs {
+	WGradJob j[5]; uint32_t n_jobs; uint32_t split; uint32_t block_start[6]; const uint32_t* n_valid;
+	float* partial; const float* var_partial; uint32_t var_blocks; float* var_grad;
+};
 
 struct DevDataset {
 	const uint32_t* pixels;
@@ -130,6 +137,19 @@ void launch_nerf_infer(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_
                        uint32_t valid_level, const half_t* grid, const MlpPtrs& w, half_t* out, uint32_t blocks);
 void launch_nerf_density(hipStream_t s, uint32_t L, uint32_t W, uint32_t n, const float* pos, const GridLevels& gl, uint32_t valid_level,
                          const half_t* grid, const MlpPtrs& w, float* density);
+// Occupancy-grid update, fused (MODE 2 of k_nerf_density): density-grid samples [lo, lo + n) of the update's
+// uniform (n_u) + occupancy-biased (n_nu) samples generated in-kernel, density splatted (atomicMax) into grid_tmp.
+struct OccSampling {
+	uint32_t n_u, n_nu, lo;
+	uint64_t rng_u_state, rng_u_inc, rng_nu_state, rng_nu_inc;
+	uint32_t step, n_cascades;
+	float thresh_nu;
+	float amin[3], diag[3];
+	const float* grid_in;
+	float* grid_tmp;
+};
+void launch_occ_density(hipStream_t s, uint32_t L, uint32_t W, uint32_t n, const OccSampling& os, const GridLevels& gl, uint32_t valid_level,
+                        const half_t* grid, const MlpPtrs& w);
 // raw SDF on a uniform grid (marching cubes input), grid points offset .. offset + n - 1 (x fastest)
 void launch_sdf_grid(hipStream_t s, uint32_t L, uint32_t W, const uint32_t res[3], const float render_min[3], const float render_max[3],
                      const float train_min[3], const float train_max[3], uint64_t offset, uint32_t n, const GridLevels& gl, uint32_t valid_level,
@@ -137,6 +157,7 @@ void launch_sdf_grid(hipStream_t s, uint32_t L, uint32_t W, const uint32_t res[3
 void launch_mlp_train(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_valid_ptr, uint32_t n, uint32_t ld, const float* coords,
                       const half_t* enc, const float* dydx, const half_t* dL_dout, const MlpPtrs& w, const TrainBufs& tb);
 void launch_wgrad(hipStream_t s, const WGradJobs& jobs, uint32_t n_blocks);
+uint32_t mlp_train_blocks(uint32_t n);  // grid of the training MLP kernels (= the variance partial count)
 void launch_mfma_probe(hipStream_t s, const half_t* A, const half_t* B, float* C);
 // march.hip
 void launch_bitfield_linear(hipStream_t s, const uint8_t* bitfield, uint32_t* lin /* LIN_WORDS */);

@@ -23,6 +23,7 @@
 // density output, dSDF/d(input), the network output and dL/doutput.
 #include "kernels.h"
 #include "grid_common.h"
+#include "occ_common.h"
 #include <algorithm>
 
 namespace neus {
@@ -648,11 +649,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))
 //         testbed_nerf.cu:596-609: p = x * (1/res) * (aabb.max - aabb.min) + aabb.min, nvcc-contracted to an
 //         FMA, then warp_position into the training aabb); density[i] = float(sdf + bias) for grid point
 //         offset + i. No 12-B position buffer: 1024^3 points read nothing but the grid table.
+// MODE 2: the occupancy-grid update fused: sample g = os.lo + i of the update's global sample range is generated
+//         in-kernel (grid_sample: the uniform call for g < n_u, the occupancy-biased call after it), its density
+//         splatted into os.grid_tmp with the reference's atomicMax on the float bits (splat_grid_samples_nerf_max_
+//         nearest_neighbor) - no position, cell index or density buffer.
 struct UniformGrid { uint32_t res[3]; float inv_res[3], rmin[3], rdiag[3], tmin[3], tdiag[3]; uint64_t offset; };
 
 template <int L, int W, int MODE>
-__global__ void __launch_bounds__(256) k_nerf_density(uint32_t n, const float* __restrict__ pos, const UniformGrid ug, const GridLevels gl,
-                                                      uint32_t valid_level, const half_t* __restrict__ grid, MlpPtrs wp, float* __restrict__ density) {
+__global__ void __launch_bounds__(256) k_nerf_density(uint32_t n, const float* __restrict__ pos, const UniformGrid ug, const OccSampling os,
+                                                      const GridLevels gl, uint32_t valid_level, const half_t* __restrict__ grid, MlpPtrs wp,
+                                                      float* __restrict__ density) {
 	constexpr int DKS = Dims<L>::DKS, M0 = Fused<L>::M0, MT = (W + 31) / 32, HKS = W / 16;
 	__shared__ half_t sm[FwdSmem<L, W>::END];
 	__shared__ LevelSmem s_lvl;
@@ -670,8 +676,14 @@ __global__ void __launch_bounds__(256) k_nerf_density(uint32_t n, const float* _
 		const bool valid = i < n;
 		const uint32_t ic = valid ? i : 0;
 		float x[3];
+		uint32_t cell = 0;
 		if (MODE == 0) {
 			x[0] = pos[3 * (size_t)ic]; x[1] = pos[3 * (size_t)ic + 1]; x[2] = pos[3 * (size_t)ic + 2];
+		} else if (MODE == 2) {
+			const uint32_t g = os.lo + ic;
+			const bool uni = g < os.n_u;
+			grid_sample(uni ? os.n_u : os.n_nu, uni ? g : g - os.n_u, uni ? os.rng_u_state : os.rng_nu_state, uni ? os.rng_u_inc : os.rng_nu_inc,
+			            os.step, os.amin, os.diag, os.grid_in, os.n_cascades, uni ? -0.01f : os.thresh_nu, x, cell);
 		} else {
 			const uint64_t g = ug.offset + ic;
 			const uint64_t rxy = (uint64_t)ug.res[0] * ug.res[1];
@@ -713,7 +725,8 @@ __global__ void __launch_bounds__(256) k_nerf_density(uint32_t n, const float* _
 			const half_t s = (half_t)__expf((float)(var_h * (half_t)10.0f));
 			const half_t sig = (half_t)(1.0f / (1.0f + __expf(-(float)(sdf * s))));
 			const half_t dens = (s * sig) * ((half_t)1.0f - sig);
-			density[i] = (float)dens;
+			if (MODE == 2) atomicMax((uint32_t*)&os.grid_tmp[cell], __float_as_uint((float)dens));
+			else density[i] = (float)dens;
 		}
 	}
 }
@@ -942,10 +955,14 @@ __global__ void __launch_bounds__(256) k_mlp_train_rgb(const uint32_t* __restric
 			if (tb.dpos && h == 0) tb.dpos[i] = make_float4(dRin[1][0], dRin[1][1], dRin[1][2], 0.f);
 		}
 	}
-	// variance gradient: batch sum of dL/dout[7] (nerf_network.h:461-474)
+	// variance gradient: batch sum of dL/dout[7] (nerf_network.h:461-474); per block here, the blocks in a fixed
+	// order in k_wgrad_reduce
 #pragma unroll
 	for (int off = 32; off > 0; off >>= 1) var_part += __shfl_xor(var_part, off);
-	if (lane == 0 && var_part != 0.f) __hip_atomic_fetch_add(tb.var_grad, var_part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	__shared__ float s_var[4];
+	if (lane == 0) s_var[threadIdx.x >> 6] = var_part;
+	__syncthreads();
+	if (threadIdx.x == 0) tb.var_partial[blockIdx.x] = (s_var[0] + s_var[1]) + (s_var[2] + s_var[3]);
 }
 
 template <int L, int W>
@@ -1118,10 +1135,52 @@ __global__ void __launch_bounds__(256) k_wgrad(WGradJobs jobs) {
 #pragma unroll
 	for (int reg = 0; reg < 16; ++reg) red[wv][acc_row(reg, h) * 32 + r] = acc[reg];
 	__syncthreads();
-	for (uint32_t e = threadIdx.x; e < 1024; e += 256) {
-		const float s = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
+	float* out = jobs.partial + (size_t)blockIdx.x * 1024;
+	for (uint32_t e = threadIdx.x; e < 1024; e += 256) out[e] = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
+}
+
+// dW = each tile's split partials summed in a fixed order. Block = (job, tile, 64-element chunk of the tile);
+// its four waves sum the splits sp = g, g + 4, ... (g = wave) in order, then the four partial sums are added in
+// wave order. The block after the last tile sums the colour kernel's per-block variance partials in block order.
+constexpr uint32_t WR_CHUNKS = 1024 / 64;
+__global__ void __launch_bounds__(256) k_wgrad_reduce(WGradJobs jobs) {
+	if (jobs.n_valid && *jobs.n_valid == 0) return;
+	__shared__ float s_part[4][64];
+	uint32_t b = blockIdx.x / WR_CHUNKS, ji = 0, tile_base = 0;
+	const uint32_t chunk = blockIdx.x % WR_CHUNKS;
+	for (; ji < jobs.n_jobs; ++ji) {
+		const uint32_t t = jobs.j[ji].tiles_m * jobs.j[ji].tiles_k;
+		if (b < tile_base + t) break;
+		tile_base += t;
+	}
+	if (ji == jobs.n_jobs) {
+		if (chunk != 0) return;
+		// fixed-order tree: thread t sums the partials t, t + 256, ..., then a pairwise tree over the threads
+		__shared__ float s_v[256];
+		float v = 0.f;
+		for (uint32_t k = threadIdx.x; k < jobs.var_blocks; k += 256) v += jobs.var_partial[k];
+		s_v[threadIdx.x] = v;
+		__syncthreads();
+		for (uint32_t off = 128; off > 0; off >>= 1) {
+			if (threadIdx.x < off) s_v[threadIdx.x] += s_v[threadIdx.x + off];
+			__syncthreads();
+		}
+		if (threadIdx.x == 0) *jobs.var_grad = s_v[0];
+		return;
+	}
+	const WGradJob J = jobs.j[ji];
+	const uint32_t tiles = J.tiles_m * J.tiles_k, tile = b - tile_base;
+	const uint32_t mt = tile / J.tiles_k, kt = tile % J.tiles_k;
+	const uint32_t n_split = (J.ncols + jobs.split - 1) / jobs.split;
+	const uint32_t g = threadIdx.x >> 6, e = chunk * 64 + (threadIdx.x & 63);
+	float acc = 0.f;
+	for (uint32_t sp = g; sp < n_split; sp += 4) acc += jobs.partial[(size_t)(jobs.block_start[ji] + sp * tiles + tile) * 1024 + e];
+	s_part[g][threadIdx.x & 63] = acc;
+	__syncthreads();
+	if (g == 0) {
 		const uint32_t m = 32 * mt + e / 32, k = 32 * kt + e % 32;
-		if (m < J.M && k < J.K && s != 0.f) __hip_atomic_fetch_add(J.dW + (size_t)m * J.K + k, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+		const uint32_t l = threadIdx.x & 63;
+		if (m < J.M && k < J.K) J.dW[(size_t)m * J.K + k] = (s_part[0][l] + s_part[1][l]) + (s_part[2][l] + s_part[3][l]);
 	}
 }
 
@@ -1177,7 +1236,15 @@ void launch_nerf_density(hipStream_t s, uint32_t L, uint32_t W, uint32_t n, cons
                          const half_t* grid, const MlpPtrs& w, float* density) {
 	const uint32_t blocks = std::min<uint32_t>((n + 127) / 128, 8192);
 	if (n == 0) return;
-#define X(l, w_) if (L == l && W == w_) { k_nerf_density<l, w_, 0><<<blocks, 256, 0, s>>>(n, pos, UniformGrid{}, gl, valid_level, grid, w, density); return; }
+#define X(l, w_) if (L == l && W == w_) { k_nerf_density<l, w_, 0><<<blocks, 256, 0, s>>>(n, pos, UniformGrid{}, OccSampling{}, gl, valid_level, grid, w, density); return; }
+	NEUS_MLP_CONFIGS(X)
+#undef X
+}
+void launch_occ_density(hipStream_t s, uint32_t L, uint32_t W, uint32_t n, const OccSampling& os, const GridLevels& gl, uint32_t valid_level,
+                        const half_t* grid, const MlpPtrs& w) {
+	const uint32_t blocks = std::min<uint32_t>((n + 127) / 128, 8192);
+	if (n == 0) return;
+#define X(l, w_) if (L == l && W == w_) { k_nerf_density<l, w_, 2><<<blocks, 256, 0, s>>>(n, nullptr, UniformGrid{}, os, gl, valid_level, grid, w, nullptr); return; }
 	NEUS_MLP_CONFIGS(X)
 #undef X
 }
@@ -1193,13 +1260,13 @@ void launch_sdf_grid(hipStream_t s, uint32_t L, uint32_t W, const uint32_t res[3
 	}
 	ug.offset = offset;
 	const uint32_t blocks = std::min<uint32_t>((n + 127) / 128, 16384);
-#define X(l, w_) if (L == l && W == w_) { k_nerf_density<l, w_, 1><<<blocks, 256, 0, s>>>(n, nullptr, ug, gl, valid_level, grid, w, sdf); return; }
+#define X(l, w_) if (L == l && W == w_) { k_nerf_density<l, w_, 1><<<blocks, 256, 0, s>>>(n, nullptr, ug, OccSampling{}, gl, valid_level, grid, w, sdf); return; }
 	NEUS_MLP_CONFIGS(X)
 #undef X
 }
 void launch_mlp_train(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_valid_ptr, uint32_t n, uint32_t ld, const float* coords,
                       const half_t* enc, const float* dydx, const half_t* dL_dout, const MlpPtrs& w, const TrainBufs& tb) {
-	const uint32_t blocks = std::min<uint32_t>((n + 127) / 128, 2048);
+	const uint32_t blocks = mlp_train_blocks(n);
 	if (n == 0) return;
 #define X(l, w_) if (L == l && W == w_) { \
 		k_mlp_train_rgb<l, w_><<<blocks, 256, 0, s>>>(n_valid_ptr, n, ld, coords, enc, dydx, dL_dout, w, tb); \
@@ -1207,7 +1274,14 @@ void launch_mlp_train(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_v
 	NEUS_MLP_CONFIGS(X)
 #undef X
 }
-void launch_wgrad(hipStream_t s, const WGradJobs& jobs, uint32_t n_blocks) { if (n_blocks) k_wgrad<<<n_blocks, 256, 0, s>>>(jobs); }
+void launch_wgrad(hipStream_t s, const WGradJobs& jobs, uint32_t n_blocks) {
+	if (!n_blocks) return;
+	k_wgrad<<<n_blocks, 256, 0, s>>>(jobs);
+	uint32_t tiles = 0;
+	for (uint32_t k = 0; k < jobs.n_jobs; ++k) tiles += jobs.j[k].tiles_m * jobs.j[k].tiles_k;
+	k_wgrad_reduce<<<(tiles + 1) * WR_CHUNKS, 256, 0, s>>>(jobs);
+}
+uint32_t mlp_train_blocks(uint32_t n) { return std::min<uint32_t>((n + 127) / 128, 2048); }
 void launch_mfma_probe(hipStream_t s, const half_t* A, const half_t* B, float* C) { k_mfma_probe<<<1, 64, 0, s>>>(A, B, C); }
 
 } // namespace neus

@@ -1,0 +1,37 @@
+// One density-grid sample of generate_grid_samples_nerf_nonuniform (testbed_nerf.cu:640-669): a cascade level from
+// the sample's pcg32 stream (advanced by 4 per sample), a cell from the reference's hash of (i + step * n) that
+// retries up to 10 times for a cell above `thresh`, a jittered position in it warped into the aabb. Shared by the
+// separate sample pass (optim.hip) and the fused occupancy-density kernel (mlp.hip), so both give the same bits
+// (no FMA contraction inside, whatever the including file's flags).
+#pragma once
+#include "kernels.h"
+
+namespace neus {
+
+__device__ __forceinline__ void grid_sample(uint32_t n_elements, uint32_t i, uint64_t rng_state, uint64_t rng_inc, uint32_t step,
+                                            const float amin[3], const float diag[3], const float* __restrict__ grid_in, uint32_t n_cascades,
+                                            float thresh, float pos[3], uint32_t& idx_out) {
+#pragma clang fp contract(off)  // the same bits in every translation unit (and as the oracle's restatement)
+	pcg32 rng(rng_state, rng_inc);
+	rng.advance((int64_t)(uint32_t)(i * 4));
+	const uint32_t level = (uint32_t)(rng.next_float() * n_cascades) % n_cascades;
+	uint32_t idx = 0;
+	for (uint32_t j = 0; j < 10; ++j) {
+		idx = ((i + step * n_elements) * 56924617u + j * 19349663u + 96925573u) % GRID3;
+		idx += level * GRID3;
+		if (grid_in[idx] > thresh) break;
+	}
+	const uint32_t pi = idx % GRID3;
+	const uint32_t x = morton3D_invert(pi >> 0), y = morton3D_invert(pi >> 1), z = morton3D_invert(pi >> 2);
+	const float rx = rng.next_float(), ry = rng.next_float(), rz = rng.next_float();
+	const float sc = scalbnf(1.0f, (int)level);
+	const float px = (((float)x + rx) / NERF_GRIDSIZE - 0.5f) * sc + 0.5f;
+	const float py = (((float)y + ry) / NERF_GRIDSIZE - 0.5f) * sc + 0.5f;
+	const float pz = (((float)z + rz) / NERF_GRIDSIZE - 0.5f) * sc + 0.5f;
+	pos[0] = (px - amin[0]) / diag[0];
+	pos[1] = (py - amin[1]) / diag[1];
+	pos[2] = (pz - amin[2]) / diag[2];
+	idx_out = idx;
+}
+
+} // namespace neus

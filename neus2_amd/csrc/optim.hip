@@ -10,6 +10,7 @@
 //   k_grid_mean_*    : deterministic two-stage mean (testbed_nerf.cu:3384-3389)
 //   k_bitfield       : grid_to_bitfield + bitfield_max_pool (testbed_nerf.cu:748-795)
 #include "kernels.h"
+#include "occ_common.h"
 #include <algorithm>
 
 namespace neus {
@@ -78,27 +79,15 @@ __global__ void k_grid_samples(uint32_t n_elements, uint32_t i_begin, uint32_t i
                                uint32_t step, float aabb_min_x, float aabb_min_y, float aabb_min_z, float diag_x, float diag_y, float diag_z,
                                const float* __restrict__ grid_in, float* __restrict__ pos, uint32_t* __restrict__ indices,
                                uint32_t n_cascades, float thresh) {
+	const float amin[3] = {aabb_min_x, aabb_min_y, aabb_min_z}, diag[3] = {diag_x, diag_y, diag_z};
 	for (uint32_t i = i_begin + blockIdx.x * blockDim.x + threadIdx.x; i < i_end; i += gridDim.x * blockDim.x) {
-		pcg32 rng(rng_state, rng_inc);
-		rng.advance((int64_t)(uint32_t)(i * 4));
-		const uint32_t level = (uint32_t)(rng.next_float() * n_cascades) % n_cascades;
-		uint32_t idx = 0;
-		for (uint32_t j = 0; j < 10; ++j) {
-			idx = ((i + step * n_elements) * 56924617u + j * 19349663u + 96925573u) % GRID3;
-			idx += level * GRID3;
-			if (grid_in[idx] > thresh) break;
-		}
-		const uint32_t pi = idx % GRID3;
-		const uint32_t x = morton3D_invert(pi >> 0), y = morton3D_invert(pi >> 1), z = morton3D_invert(pi >> 2);
-		const float rx = rng.next_float(), ry = rng.next_float(), rz = rng.next_float();
-		const float sc = scalbnf(1.0f, (int)level);
-		const float px = (((float)x + rx) / NERF_GRIDSIZE - 0.5f) * sc + 0.5f;
-		const float py = (((float)y + ry) / NERF_GRIDSIZE - 0.5f) * sc + 0.5f;
-		const float pz = (((float)z + rz) / NERF_GRIDSIZE - 0.5f) * sc + 0.5f;
+		float p[3];
+		uint32_t idx;
+		grid_sample(n_elements, i, rng_state, rng_inc, step, amin, diag, grid_in, n_cascades, thresh, p, idx);
 		const uint32_t o = out_base + (i - i_begin);
-		pos[3 * (size_t)o + 0] = (px - aabb_min_x) / diag_x;
-		pos[3 * (size_t)o + 1] = (py - aabb_min_y) / diag_y;
-		pos[3 * (size_t)o + 2] = (pz - aabb_min_z) / diag_z;
+		pos[3 * (size_t)o + 0] = p[0];
+		pos[3 * (size_t)o + 1] = p[1];
+		pos[3 * (size_t)o + 2] = p[2];
 		indices[o] = idx;
 	}
 }

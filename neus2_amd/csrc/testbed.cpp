@@ -197,6 +197,7 @@ struct NeusTestbed {
 	Dev<float> dydx;
 	Dev<half_t> net_out, dL_dout, trainbuf;
 	Dev<float4> vbuf;
+	Dev<float> wgrad_partial, var_partial;  // weight-gradient split partials, per-block variance sums
 	Dev<uint8_t> scan_tmp;
 	size_t scan_tmp_bytes = 0;
 	Dev<StepState> st;
@@ -424,6 +425,9 @@ struct NeusTestbed {
 		tbuf.dLdenc = take(2 * (size_t)l.L * ld); tbuf.genc = take(2 * (size_t)l.L * ld);
 		tbuf.v = vbuf.p;
 		tbuf.var_grad = grads.p + l.var_off;
+		var_partial.alloc(mlp_train_blocks(batch));
+		tbuf.var_partial = var_partial.p;
+		wgrad_partial.alloc((size_t)wgrad_jobs(batch, batch, grads.p, nullptr).block_start[5] * 1024);
 		tbuf.indeed_batch = (float)batch * (float)world;
 		// binned grid-gradient scatter workspace (grid.hip)
 		swork = ScatterWork{};
@@ -585,7 +589,10 @@ struct NeusTestbed {
 		}
 		J.block_start[5] = b;
 		J.n_valid = n_valid;
-		(void)n;
+		J.partial = wgrad_partial.p;
+		J.var_partial = var_partial.p;
+		J.var_blocks = mlp_train_blocks(n);
+		J.var_grad = g + lay.var_off;
 		return J;
 	}
 	// forward recompute + backward into g (fp32 [P], zeroed by the caller)
@@ -633,18 +640,30 @@ struct NeusTestbed {
 		const uint32_t NT = n_uniform + n_nonuniform;
 		const uint32_t lo = (uint32_t)((uint64_t)NT * rank / world), hi = (uint32_t)((uint64_t)NT * (rank + 1) / world);
 		const uint32_t N = hi - lo;
-		launch_grid_samples(s, n_uniform, std::min(lo, n_uniform), std::min(hi, n_uniform), 0, density_grid_rng.state, density_grid_rng.inc,
-		                    density_grid_ema_step, ds.aabb_min, ds.aabb_max, density_grid.p, occ_pos.p, occ_idx.p, max_cascade + 1, -0.01f);
+		const pcg32 rng_u = density_grid_rng;
 		density_grid_rng.advance();
-		launch_grid_samples(s, n_nonuniform, std::max(lo, n_uniform) - n_uniform, std::max(hi, n_uniform) - n_uniform,
-		                    std::max(lo, n_uniform) - lo, density_grid_rng.state, density_grid_rng.inc, density_grid_ema_step, ds.aabb_min,
-		                    ds.aabb_max, density_grid.p, occ_pos.p, occ_idx.p, max_cascade + 1, NERF_MIN_OPTICAL_THICKNESS);
+		const pcg32 rng_nu = density_grid_rng;
 		density_grid_rng.advance();
-		// NerfNetwork::density on the samples, hash-grid encode fused in; with the DeltaNetwork active the
-		// positions are moved first (nerf_network.h:664-675)
-		if (use_delta) launch_delta_apply(s, nullptr, N, 3, occ_pos.p, occ_pos.p, delta.p);
-		launch_nerf_density(s, lay.L, lay.W, N, occ_pos.p, gl, valid, params_h.p + lay.grid_off, mlp, occ_density.p);
-		launch_splat_max(s, N, occ_idx.p, occ_density.p, density_tmp.p);
+		if (!use_delta) {
+			// sample generation + NerfNetwork::density + splat in one kernel
+			OccSampling os{};
+			os.n_u = n_uniform; os.n_nu = n_nonuniform; os.lo = lo;
+			os.rng_u_state = rng_u.state; os.rng_u_inc = rng_u.inc; os.rng_nu_state = rng_nu.state; os.rng_nu_inc = rng_nu.inc;
+			os.step = density_grid_ema_step; os.n_cascades = max_cascade + 1; os.thresh_nu = NERF_MIN_OPTICAL_THICKNESS;
+			for (int d = 0; d < 3; ++d) { os.amin[d] = ds.aabb_min[d]; os.diag[d] = ds.aabb_max[d] - ds.aabb_min[d]; }
+			os.grid_in = density_grid.p; os.grid_tmp = density_tmp.p;
+			launch_occ_density(s, lay.L, lay.W, N, os, gl, valid, params_h.p + lay.grid_off, mlp);
+		} else {
+			launch_grid_samples(s, n_uniform, std::min(lo, n_uniform), std::min(hi, n_uniform), 0, rng_u.state, rng_u.inc, density_grid_ema_step,
+			                    ds.aabb_min, ds.aabb_max, density_grid.p, occ_pos.p, occ_idx.p, max_cascade + 1, -0.01f);
+			launch_grid_samples(s, n_nonuniform, std::max(lo, n_uniform) - n_uniform, std::max(hi, n_uniform) - n_uniform,
+			                    std::max(lo, n_uniform) - lo, rng_nu.state, rng_nu.inc, density_grid_ema_step, ds.aabb_min, ds.aabb_max,
+			                    density_grid.p, occ_pos.p, occ_idx.p, max_cascade + 1, NERF_MIN_OPTICAL_THICKNESS);
+			// NerfNetwork::density on the moved positions (the DeltaNetwork is active, nerf_network.h:664-675)
+			launch_delta_apply(s, nullptr, N, 3, occ_pos.p, occ_pos.p, delta.p);
+			launch_nerf_density(s, lay.L, lay.W, N, occ_pos.p, gl, valid, params_h.p + lay.grid_off, mlp, occ_density.p);
+			launch_splat_max(s, N, occ_idx.p, occ_density.p, density_tmp.p);
+		}
 		allreduce_f32(density_tmp.p, n_cells, true);
 		launch_ema_grid(s, n_cells, cfg.density_grid_decay, density_grid.p, density_tmp.p);
 		++density_grid_ema_step;

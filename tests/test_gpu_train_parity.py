@@ -189,3 +189,19 @@ def test_train_trajectory_vs_oracle(scene, torch_cuda):
             assert np.sign(p_gpu[blocks[name][0]] - p0[blocks[name][0]]) == np.sign(p_cpu[blocks[name][0]] - p0[blocks[name][0]])
             continue
         assert cos >= 0.98 and rel <= 0.25, (name, cos, rel)
+
+
+def test_training_is_bitwise_reproducible(scene, torch_cuda):
+    """Two testbeds, same seed and data, 50 free-running steps each: parameters, EMA weights, occupancy grid and
+    losses are bitwise equal. Every reduction of the step is fixed-order (scan compaction, int64 fixed-point grid
+    scatter, split-ordered weight-gradient and variance sums, deterministic grid mean); the only atomics left are
+    the occupancy splat's atomicMax (order-independent)."""
+    tbs = [_testbed(scene) for _ in range(2)]
+    for tb in tbs:
+        tb.train_steps(50)
+    a, b = tbs
+    np.testing.assert_array_equal(a.get_params(), b.get_params())
+    np.testing.assert_array_equal(a.get_ema_params(), b.get_ema_params())
+    np.testing.assert_array_equal(a.get_density_grid()[0], b.get_density_grid()[0])
+    sa, sb = a.stats(), b.stats()
+    assert sa["loss"] == sb["loss"] and sa["rays_per_batch"] == sb["rays_per_batch"]
