@@ -112,6 +112,8 @@ typedef struct NeusTrainStats {
 	float ray_loss;                           /* mean Huber loss over the rays that had samples (last logged step) */
 	uint32_t n_rays_with_samples;             /* rays kept by the sampler in the last logged step */
 	uint64_t trained_samples_total;           /* compacted (non-rollover) training samples since step 0, per rank */
+	uint32_t march_first_pass_rays;           /* ray slots the next step's first march pass covers (0 = all) */
+	uint32_t kept_ray_extent;                 /* 1 + the last ray slot kept by the last step's sampler */
 } NeusTrainStats;
 
 /* Testbed::render_to_cpu (python_api.cu:123-169) after set_camera_to_training_view (testbed.cu:264-270). */
@@ -179,6 +181,9 @@ int neus_testbed_sdf_on_grid(NeusTestbed* tb, const int32_t res[3], const float 
  * given and res is used unrounded. Deterministic vertex / triangle order. */
 int neus_testbed_marching_cubes(NeusTestbed* tb, const int32_t res[3], const float aabb_min[3], const float aabb_max[3], float thresh,
                                 const float* density_dev, uint32_t* n_verts, uint32_t* n_tris);
+/* Grid points [offset, offset + count) (linear index, x fastest) of the SDF grid the last network marching_cubes
+ * computed (get_density_on_grid), to host floats: sub-block checks of large (1024^3) grids. */
+int neus_testbed_mc_density(NeusTestbed* tb, uint64_t offset, uint64_t count, float* host_out);
 /* The last mesh: verts n_verts x 3 f32, tris n_tris x 3 u32 (host buffers, nullable). */
 int neus_testbed_get_mesh(NeusTestbed* tb, float* verts, uint32_t* tris);
 /* compute_mesh_vertex_colors (testbed_nerf.cu:4071-4094): n_verts x 3 f32 sRGB colours of the last mesh. */

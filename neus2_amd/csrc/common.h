@@ -129,9 +129,10 @@ struct StepState {
 	uint32_t zero_records;
 	uint32_t n_rays_total;            // rays drawn since training step 0 (all ranks)
 	uint32_t n_train;                 // compacted training batch (target) or 0 when no samples
-	uint32_t pad0;
+	uint32_t march_est;               // ray slots the first march pass covers (0 = all); from the last step's kept extent
 	unsigned long long trained_total; // real (non-rollover) training samples since step 0, this rank: sum of min(Nc measured, batch)
-	uint32_t pad[2];
+	uint32_t march_total;             // samples requested by the first march pass's rays
+	uint32_t kept_extent;             // this step: 1 + the last kept ray slot (0 if none)
 };
 static_assert(sizeof(StepState) == 64, "StepState is one 64-B record");
 

@@ -165,10 +165,10 @@ void launch_bitfield_linear(hipStream_t s, const uint8_t* bitfield, uint32_t* li
 // (samples of the ray before the run) << 16 | run length}; a run's samples are t, t + dt(t), ... (the reference's
 // t += dt), at most MARCH_RUN_MAX of them. nrec: records per slot; counter: the persistent march's ray queue.
 constexpr uint32_t MARCH_RUN_MAX = 16;
-struct MarchWork { uint2* rec; uint32_t* nrec; uint32_t* counter; uint32_t waves; /* persistent march waves, 0 = one lane per ray */ };
+struct MarchWork { uint2* rec; uint32_t* nrec; uint32_t* counter /* 2: the two passes' ray queues */; uint32_t waves; /* 0 = one lane per ray */ };
 // Ray generation + the occupancy march: rays (6 f32 per slot), tstart (1 per slot), nreq (requested
 // samples per slot) and the sample runs (MarchWork).
-void launch_march_count(hipStream_t s, uint32_t cap, const StepState* st, DPInfo dp, const DevDataset& ds, const uint8_t* bitfield,
+void launch_march_count(hipStream_t s, uint32_t cap, uint32_t max_samples /* global cap: 16 x batch */, StepState* st, DPInfo dp, const DevDataset& ds, const uint8_t* bitfield,
                         const uint32_t* lin, uint64_t rng_state, uint64_t rng_inc, float* rays, float* tstart, uint32_t* nreq, const MarchWork& mw);
 void launch_march_write(hipStream_t s, uint32_t cap, StepState* st, const DevDataset& ds, const float* rays, const MarchWork& mw, const uint32_t* nreq,
                         const uint32_t* base, uint32_t* numsteps, float* coords, uint32_t* sample_ray, uint32_t sample_cap /* >= max_inference */);

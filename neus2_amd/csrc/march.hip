@@ -39,12 +39,15 @@ __global__ void k_bitfield_linear(const uint8_t* __restrict__ bf, uint32_t* __re
 // Thread per ray slot: pixel/image pick from the ray's pcg32 stream, pinhole ray, AABB entry and
 // jittered start (testbed_nerf.cu:1263-1375). rays: 6 floats (o, unnormalised d); tstart: the jittered
 // start t, or -1 for a dropped ray and for slots >= R (nothing to march).
-__global__ void __launch_bounds__(256) k_ray_gen(uint32_t cap_rays, const StepState* __restrict__ st, DPInfo dp, DevDataset ds,
+__global__ void __launch_bounds__(256) k_ray_gen(uint32_t cap_rays, const StepState* __restrict__ st_r, DPInfo dp, DevDataset ds,
                                                  uint64_t rng_state, uint64_t rng_inc, float* __restrict__ rays, float* __restrict__ tstart,
-                                                 uint32_t* __restrict__ march_queue) {
-	if (blockIdx.x == 0 && threadIdx.x == 0) *march_queue = 0;  // the march's ray queue (next kernel on the stream)
-	const uint32_t R = st->rays_per_batch;
-	const uint32_t n_rays_global = R * dp.world, n_rays_total = st->n_rays_total;
+                                                 uint32_t* __restrict__ march_queue, StepState* __restrict__ st_w) {
+	if (blockIdx.x == 0 && threadIdx.x == 0) {  // the march passes' ray queues and counters (next kernels on the stream)
+		march_queue[0] = 0; march_queue[1] = 0;
+		st_w->march_total = 0; st_w->kept_extent = 0;
+	}
+	const uint32_t R = st_r->rays_per_batch;
+	const uint32_t n_rays_global = R * dp.world, n_rays_total = st_r->n_rays_total;
 	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cap_rays; i += gridDim.x * blockDim.x) {
 		float o[3] = {0, 0, 0}, du[3] = {0, 0, 0}, startt = -1.0f;
 		if (i < R) {
@@ -191,12 +194,28 @@ __device__ __forceinline__ bool march_event(const DevDataset& ds, const uint8_t*
 	}
 }
 
+// Two passes over the ray slots. Only a prefix of the slots can be kept: slot i is kept iff n_i > 0 and
+// sum_{j<i} n_j + n_i <= max_inference (<= max_samples), so once the rays before slot `est` request max_samples
+// samples, every later ray is dropped whatever it would count. Pass 0 marches [0, est) (est from the previous
+// step's kept extent) and sums its counts; pass 1 marches [est, R) only when that sum is below max_samples, and
+// otherwise marks those slots dropped (nreq = 1: past the cap in the scan, nothing recorded). The kept rays, their
+// samples and every training result are those of marching all slots; the requested-sample counter then reads a
+// value at or above max_samples, which is all the reference ever uses of it (min(counter, max_samples),
+// testbed_nerf.cu:3036-3039; the rest is the GUI's text).
 template <bool FAST>
-__global__ void __launch_bounds__(256) k_march(uint32_t cap_rays, DevDataset ds, const uint8_t* __restrict__ bitfield,
-                                               const uint32_t* __restrict__ lin, const float* __restrict__ rays, const float* __restrict__ tstart,
-                                               uint32_t* __restrict__ nreq, MarchWork mw) {
+__global__ void __launch_bounds__(256) k_march(uint32_t cap_rays, uint32_t pass, uint32_t max_samples, StepState* __restrict__ st, DevDataset ds,
+                                               const uint8_t* __restrict__ bitfield, const uint32_t* __restrict__ lin, const float* __restrict__ rays,
+                                               const float* __restrict__ tstart, uint32_t* __restrict__ nreq, MarchWork mw) {
+	const uint32_t est = st->march_est ? min(st->march_est, cap_rays) : cap_rays;
+	const uint32_t lo = pass == 0 ? 0u : est, hi = pass == 0 ? est : cap_rays;
+	if (lo >= hi) return;
+	if (pass == 1 && st->march_total >= max_samples) {
+		for (uint32_t k = lo + blockIdx.x * blockDim.x + threadIdx.x; k < hi; k += gridDim.x * blockDim.x) { nreq[k] = 1; mw.nrec[k] = 0; }
+		return;
+	}
+	uint32_t* queue = mw.counter + pass;
 	const uint32_t lane = threadIdx.x & 63;
-	uint32_t i = 0;
+	uint32_t i = 0, total = 0;
 	bool alive = false, drained = false;
 	MarchRay mr;
 	float t = 0.f;
@@ -210,11 +229,11 @@ __global__ void __launch_bounds__(256) k_march(uint32_t cap_rays, DevDataset ds,
 		const uint32_t n_idle = (uint32_t)__popcll(idle);
 		if (n_idle >= 16 || (live == 0 && n_idle > 0)) {
 			uint32_t b = 0;
-			if (lane == 0) b = atomicAdd(mw.counter, n_idle);
+			if (lane == 0) b = atomicAdd(queue, n_idle);
 			b = (uint32_t)__shfl((int)b, 0);
 			if (!alive && !drained) {
-				i = b + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
-				if (i >= cap_rays) {
+				i = lo + b + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+				if (i >= hi) {
 					drained = true;
 				} else {
 					t = tstart[i]; n = 0; acc = RunAcc{0.f, 0u, 0u, 0u};
@@ -229,8 +248,14 @@ __global__ void __launch_bounds__(256) k_march(uint32_t cap_rays, DevDataset ds,
 		if (alive && !march_event<FAST>(ds, bitfield, lin, mr, t, n, acc, rec)) {
 			run_flush(rec, acc);
 			nreq[i] = n; mw.nrec[i] = acc.nrec;
+			total += n;
 			alive = false;
 		}
+	}
+	if (pass == 0) {  // the pass's requested samples (one atomic per wave)
+#pragma unroll
+		for (int off = 32; off > 0; off >>= 1) total += (uint32_t)__shfl_xor((int)total, off);
+		if (lane == 0 && total) atomicAdd(&st->march_total, total);
 	}
 }
 
@@ -261,11 +286,14 @@ __global__ void __launch_bounds__(256) k_march_numsteps(uint32_t cap_rays, StepS
 		numsteps[2 * i] = keep ? n : 0;
 		numsteps[2 * i + 1] = b;
 	}
-	uint32_t kmax = keep ? b + n : 0u, kcnt = keep ? 1u : 0u;
+	uint32_t kmax = keep ? b + n : 0u, kcnt = keep ? 1u : 0u, kext = keep ? i + 1 : 0u;
 	if (__ballot(kcnt != 0)) {
 #pragma unroll
-		for (int off = 32; off > 0; off >>= 1) { kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, off)); kcnt += (uint32_t)__shfl_xor((int)kcnt, off); }
-		if ((threadIdx.x & 63) == 0) { atomicMax(&st->n_kept, kmax); atomicAdd(&st->n_rays_with_samples, kcnt); }
+		for (int off = 32; off > 0; off >>= 1) {
+			kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, off)); kcnt += (uint32_t)__shfl_xor((int)kcnt, off);
+			kext = max(kext, (uint32_t)__shfl_xor((int)kext, off));
+		}
+		if ((threadIdx.x & 63) == 0) { atomicMax(&st->n_kept, kmax); atomicAdd(&st->n_rays_with_samples, kcnt); atomicMax(&st->kept_extent, kext); }
 	}
 }
 
@@ -660,7 +688,13 @@ __global__ void k_step_counters(StepState* st, uint32_t target_batch, uint32_t m
 	if (threadIdx.x != 0 || blockIdx.x != 0) return;
 	const uint32_t R = st->rays_per_batch;
 	st->n_rays_total += R * world;  // n_rays_total
-	const uint32_t before = st->numsteps_counter / world;
+	// next step's first march pass: the slots up to this step's kept extent plus a margin (all slots when every
+	// ray with samples fitted under this step's cap)
+	const bool fit = st->numsteps_counter <= st->max_inference;
+	const uint32_t ext = st->kept_extent + st->kept_extent / 4 + 1024;
+	st->march_est = fit ? 0u : (ext + 63u) / 64u * 64u;
+	// per rank: the cap on the next step's pre-compaction samples follows this rank's own request count
+	const uint32_t before = st->numsteps_counter;
 	const uint32_t measured = st->compacted_counter / world;
 	st->measured_before = before;
 	st->measured_batch_size = measured;
@@ -680,13 +714,15 @@ static inline uint32_t ray_blocks(uint32_t cap) { return std::max<uint32_t>(1, s
 void launch_bitfield_linear(hipStream_t s, const uint8_t* bitfield, uint32_t* lin) {
 	k_bitfield_linear<<<GRID3 / 32 / 256, 256, 0, s>>>(bitfield, lin);
 }
-void launch_march_count(hipStream_t s, uint32_t cap, const StepState* st, DPInfo dp, const DevDataset& ds, const uint8_t* bitfield,
+void launch_march_count(hipStream_t s, uint32_t cap, uint32_t max_samples, StepState* st, DPInfo dp, const DevDataset& ds, const uint8_t* bitfield,
                         const uint32_t* lin, uint64_t rng_state, uint64_t rng_inc, float* rays, float* tstart, uint32_t* nreq, const MarchWork& mw) {
-	k_ray_gen<<<ray_blocks(cap), 256, 0, s>>>(cap, st, dp, ds, rng_state, rng_inc, rays, tstart, mw.counter);
+	k_ray_gen<<<ray_blocks(cap), 256, 0, s>>>(cap, st, dp, ds, rng_state, rng_inc, rays, tstart, mw.counter, st);
 	const uint32_t waves = mw.waves ? std::min(mw.waves, (cap + 63) / 64) : (cap + 63) / 64;
 	const uint32_t blocks = std::max<uint32_t>(1, (waves + 3) / 4);
-	if (ds.cone_angle == 0.0f) k_march<true><<<blocks, 256, 0, s>>>(cap, ds, bitfield, lin, rays, tstart, nreq, mw);
-	else k_march<false><<<blocks, 256, 0, s>>>(cap, ds, bitfield, nullptr, rays, tstart, nreq, mw);
+	for (uint32_t pass = 0; pass < 2; ++pass) {
+		if (ds.cone_angle == 0.0f) k_march<true><<<blocks, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, lin, rays, tstart, nreq, mw);
+		else k_march<false><<<blocks, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, nullptr, rays, tstart, nreq, mw);
+	}
 }
 void launch_march_write(hipStream_t s, uint32_t cap, StepState* st, const DevDataset& ds, const float* rays, const MarchWork& mw, const uint32_t* nreq,
                         const uint32_t* base, uint32_t* numsteps, float* coords, uint32_t* sample_ray, uint32_t sample_cap) {

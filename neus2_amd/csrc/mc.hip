@@ -15,13 +15,12 @@
 // -ffp-contract=off they are bit-identical to the CPU oracle. Indices are 64-bit in the grid (1024^3
 // points and beyond) and 32-bit in the mesh.
 //
-// The triangle table is generated here (mc_build_table), not copied: per corner mask, crossing edges are
-// joined face by face into segments (a face with four crossings cuts off each set corner separately, a
-// symmetric rule, so neighbouring cubes agree and the mesh is watertight), segments are oriented with the
-// set corners on their left seen from outside the cube, chained into loops and fanned from the loop's
-// lowest edge id. oracle/mc_table.py restates the same construction for the parity tests.
+// The triangle table is the reference's constant table (mc_tables.h, marching_cubes.cu:401-658), so every case,
+// the ambiguous ones included, produces the reference's faces; only the vertex / triangle order differs
+// (deterministic here, atomic-append order there).
 #pragma clang fp contract(off)
 #include "kernels.h"
+#include "mc_tables.h"
 
 #include <cmath>
 #include <cstring>
@@ -35,76 +34,15 @@ constexpr int MC_ROW = 3 * MC_MAX_TRIS + 1;
 __constant__ int8_t c_mc_table[256][MC_ROW];
 __constant__ uint8_t c_mc_ntri[256];
 
-// corner k -> offset bits (x, y, z); edge e -> corners; edge e -> owning grid point offset and axis
-static const int CORNER[8][3] = {{0, 0, 0}, {1, 0, 0}, {1, 1, 0}, {0, 1, 0}, {0, 0, 1}, {1, 0, 1}, {1, 1, 1}, {0, 1, 1}};
-static const int EDGE[12][2] = {{0, 1}, {1, 2}, {3, 2}, {0, 3}, {4, 5}, {5, 6}, {7, 6}, {4, 7}, {0, 4}, {1, 5}, {2, 6}, {3, 7}};
-static const int FACE[6][4] = {{0, 3, 7, 4}, {1, 2, 6, 5}, {0, 1, 5, 4}, {3, 2, 6, 7}, {0, 1, 2, 3}, {4, 5, 6, 7}};
-static const int FACE_N[6][3] = {{-1, 0, 0}, {1, 0, 0}, {0, -1, 0}, {0, 1, 0}, {0, 0, -1}, {0, 0, 1}};
-
-static int edge_of(int a, int b) {
-	for (int e = 0; e < 12; ++e)
-		if ((EDGE[e][0] == a && EDGE[e][1] == b) || (EDGE[e][0] == b && EDGE[e][1] == a)) return e;
-	throw std::runtime_error("mc table: not an edge");
-}
-
-// Host: the case table (see the file comment); rows are edge triples terminated by -1.
+// The case table is the reference's (mc_tables.h, marching_cubes.cu:401-658), re-laid out as rows of up to
+// MC_MAX_TRIS edge triples, -1 terminated, plus the triangle count per case.
 static void mc_build_table(int8_t table[256][MC_ROW], uint8_t ntri[256]) {
 	for (int m = 0; m < 256; ++m) {
 		for (int k = 0; k < MC_ROW; ++k) table[m][k] = -1;
-		ntri[m] = 0;
-		if (m == 0 || m == 255) continue;
-		int nxt[12];
-		for (int e = 0; e < 12; ++e) nxt[e] = -1;
-		auto in = [&](int c) { return (m >> c) & 1; };
-		auto mid2 = [&](int e, int d) { return CORNER[EDGE[e][0]][d] + CORNER[EDGE[e][1]][d]; };  // 2 x midpoint
-		auto add_seg = [&](int f, int a, int b, int c) {
-			// cross(n, B - A) . (P - A) > 0 keeps the set corner P on the left (all in 2x units)
-			float A[3], B[3], P[3], n[3];
-			for (int d = 0; d < 3; ++d) { A[d] = (float)mid2(a, d); B[d] = (float)mid2(b, d); P[d] = 2.0f * CORNER[c][d]; n[d] = (float)FACE_N[f][d]; }
-			const float u[3] = {B[0] - A[0], B[1] - A[1], B[2] - A[2]};
-			const float cr[3] = {n[1] * u[2] - n[2] * u[1], n[2] * u[0] - n[0] * u[2], n[0] * u[1] - n[1] * u[0]};
-			const float s = cr[0] * (P[0] - A[0]) + cr[1] * (P[1] - A[1]) + cr[2] * (P[2] - A[2]);
-			if (s < 0) std::swap(a, b);
-			if (nxt[a] >= 0) throw std::runtime_error("mc table: edge with two successors");
-			nxt[a] = b;
-		};
-		for (int f = 0; f < 6; ++f) {
-			const int* cy = FACE[f];
-			int n_set = 0, set_c[4];
-			for (int i = 0; i < 4; ++i) if (in(cy[i])) set_c[n_set++] = cy[i];
-			if (n_set == 0 || n_set == 4) continue;
-			bool adjacent = false;
-			for (int i = 0; i < 4; ++i) adjacent |= in(cy[i]) && in(cy[(i + 1) % 4]);
-			if (n_set == 2 && !adjacent) {
-				for (int q = 0; q < 2; ++q) {
-					int i = 0;
-					while (cy[i] != set_c[q]) ++i;
-					add_seg(f, edge_of(set_c[q], cy[(i + 3) % 4]), edge_of(set_c[q], cy[(i + 1) % 4]), set_c[q]);
-				}
-			} else {
-				int xs[2], nx = 0;
-				for (int i = 0; i < 4; ++i) if (in(cy[i]) != in(cy[(i + 1) % 4])) xs[nx++] = edge_of(cy[i], cy[(i + 1) % 4]);
-				if (nx != 2) throw std::runtime_error("mc table: face with odd crossings");
-				add_seg(f, xs[0], xs[1], set_c[0]);
-			}
-		}
-		bool seen[12] = {};
-		int nt = 0;
-		for (int st = 0; st < 12; ++st) {
-			if (nxt[st] < 0 || seen[st]) continue;
-			int loop[12], len = 0, v = st;
-			do { loop[len++] = v; seen[v] = true; v = nxt[v]; } while (v != st);
-			int k = 0;
-			for (int i = 1; i < len; ++i) if (loop[i] < loop[k]) k = i;
-			int r[12];
-			for (int i = 0; i < len; ++i) r[i] = loop[(k + i) % len];
-			for (int i = 1; i + 1 < len; ++i) {
-				if (nt >= MC_MAX_TRIS) throw std::runtime_error("mc table: too many triangles");
-				table[m][3 * nt] = (int8_t)r[0]; table[m][3 * nt + 1] = (int8_t)r[i]; table[m][3 * nt + 2] = (int8_t)r[i + 1];
-				++nt;
-			}
-		}
-		ntri[m] = (uint8_t)nt;
+		int n = 0;
+		while (n < 15 && MC_TRIANGLE_TABLE[m][n] >= 0) { table[m][n] = MC_TRIANGLE_TABLE[m][n]; ++n; }
+		if (n % 3 != 0) throw std::runtime_error("mc table: row not made of triangles");
+		ntri[m] = (uint8_t)(n / 3);
 	}
 }
 

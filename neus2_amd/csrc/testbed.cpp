@@ -400,7 +400,7 @@ struct NeusTestbed {
 		batch = c.batch_size;
 		max_samples = batch * 16;  // testbed_nerf.cu:3725
 		rays.alloc(6 * (size_t)MAX_RAYS); startt.alloc((size_t)MAX_RAYS);
-		march_rec.alloc((size_t)MAX_RAYS * NERF_STEPS); march_nrec.alloc(MAX_RAYS); march_queue.alloc(1);
+		march_rec.alloc((size_t)MAX_RAYS * NERF_STEPS); march_nrec.alloc(MAX_RAYS); march_queue.alloc(2);
 		mwork = MarchWork{march_rec.p, march_nrec.p, march_queue.p, march_waves()}; nreq.alloc(MAX_RAYS); base.alloc(MAX_RAYS);
 		numsteps.alloc(2 * (size_t)MAX_RAYS); ccount.alloc(MAX_RAYS); cbase.alloc(MAX_RAYS);
 		l_sa.alloc(max_samples); l_ekt.alloc(max_samples); sample_ray.alloc(max_samples);
@@ -867,7 +867,7 @@ struct NeusTestbed {
 		HIP_CHECK(hipMemsetAsync(&st.p->n_rays_with_samples, 0, 4, s));
 		const DPInfo dp{rank, world};
 		mark(1);
-		launch_march_count(s, MAX_RAYS, st.p, dp, ds, bitfield.p, bf_lin.p, rng.state, rng.inc, rays.p, startt.p, nreq.p, mwork);
+		launch_march_count(s, MAX_RAYS, max_samples, st.p, dp, ds, bitfield.p, bf_lin.p, rng.state, rng.inc, rays.p, startt.p, nreq.p, mwork);
 		launch_exclusive_scan(s, scan_tmp.p, scan_tmp_bytes, nreq.p, base.p, MAX_RAYS);
 		launch_march_write(s, MAX_RAYS, st.p, ds, rays.p, mwork, nreq.p, base.p, numsteps.p, coords.p, sample_ray.p, max_samples);
 		mark(2);
@@ -909,7 +909,6 @@ struct NeusTestbed {
 			// collective 1 (gradients; DeltaNetwork partials) and 3 (counters, loss scalars) of SURVEY §8(e), one group
 			coll_begin();
 			allreduce_f32(grads.p, lay.P);
-			allreduce_u32(&st.p->numsteps_counter, 1);
 			allreduce_u32(&st.p->compacted_counter, 1);
 			allreduce_u32(&st.p->n_rays_with_samples, 1);
 			if (use_delta) allreduce_f32(delta_partial.p, delta_partial_floats());
@@ -1045,6 +1044,7 @@ int neus_testbed_get_stats(NeusTestbed* tb, NeusTrainStats* o) {
 		o->density_grid_mean = mean;
 		o->ray_loss = tb->ray_loss; o->n_rays_with_samples = tb->last_rays_with_samples;
 		o->trained_samples_total = s.trained_total;
+		o->march_first_pass_rays = s.march_est; o->kept_ray_extent = s.kept_extent;
 	});
 }
 static int copy_param_vec(NeusTestbed* tb, const float* dev, float* host, uint64_t n) {
@@ -1153,6 +1153,13 @@ int neus_testbed_marching_cubes(NeusTestbed* tb, const int32_t res[3], const flo
 		if (n_tris) *n_tris = tb->mesh_nt;
 	});
 }
+int neus_testbed_mc_density(NeusTestbed* tb, uint64_t offset, uint64_t count, float* host_out) {
+	return guard([&] {
+		if (!host_out || offset + count > tb->mc_density.n) throw std::runtime_error("mc_density: range outside the last SDF grid");
+		HIP_CHECK(hipStreamSynchronize(tb->stream));
+		HIP_CHECK(hipMemcpy(host_out, tb->mc_density.p + offset, count * 4, hipMemcpyDeviceToHost));
+	});
+}
 int neus_testbed_get_mesh(NeusTestbed* tb, float* verts, uint32_t* tris) {
 	return guard([&] {
 		HIP_CHECK(hipStreamSynchronize(tb->stream));
@@ -1248,7 +1255,7 @@ static void time_kernel_impl(NeusTestbed* tb, int kernel, int variant, int iters
 		auto march = [&]() {
 			HIP_CHECK(hipMemsetAsync(&t.st.p->n_kept, 0, 4, s));
 			HIP_CHECK(hipMemsetAsync(&t.st.p->n_rays_with_samples, 0, 4, s));
-			launch_march_count(s, MAX_RAYS, t.st.p, dp, t.ds, t.bitfield.p, lin, t.rng.state, t.rng.inc, t.rays.p, t.startt.p, t.nreq.p, t.mwork);
+			launch_march_count(s, MAX_RAYS, t.max_samples, t.st.p, dp, t.ds, t.bitfield.p, lin, t.rng.state, t.rng.inc, t.rays.p, t.startt.p, t.nreq.p, t.mwork);
 			launch_exclusive_scan(s, t.scan_tmp.p, t.scan_tmp_bytes, t.nreq.p, t.base.p, MAX_RAYS);
 			launch_march_write(s, MAX_RAYS, t.st.p, t.ds, t.rays.p, t.mwork, t.nreq.p, t.base.p, t.numsteps.p, t.coords.p,
 			                   t.sample_ray.p, t.max_samples);
@@ -1266,7 +1273,7 @@ static void time_kernel_impl(NeusTestbed* tb, int kernel, int variant, int iters
 		for (int k = 0; k < iters; ++k) {
 			HIP_CHECK(hipEventRecord(evs[k], s));
 			switch (kernel) {
-			case 0: launch_march_count(s, MAX_RAYS, t.st.p, dp, t.ds, t.bitfield.p, lin, t.rng.state, t.rng.inc, t.rays.p, t.startt.p, t.nreq.p, t.mwork); break;
+			case 0: launch_march_count(s, MAX_RAYS, t.max_samples, t.st.p, dp, t.ds, t.bitfield.p, lin, t.rng.state, t.rng.inc, t.rays.p, t.startt.p, t.nreq.p, t.mwork); break;
 			case 1: launch_march_write(s, MAX_RAYS, t.st.p, t.ds, t.rays.p, t.mwork, t.nreq.p, t.base.p, t.numsteps.p,
 			                           t.coords.p, t.sample_ray.p, t.max_samples); break;
 			case 2: debug_launch_loss_scan(s, variant, MAX_RAYS, t.numsteps.p, w, t.ccount.p); break;
@@ -1447,13 +1454,13 @@ int neus_sample_rays(NeusTestbed* tb, void* stream, uint32_t n_rays, uint32_t ra
 		Dev<StepState> sst; sst.alloc(1);
 		StepState h{}; h.rays_per_batch = n_rays; h.max_inference = max_samples; h.n_rays_total = n_rays_total;
 		HIP_CHECK(hipMemcpyAsync(sst.p, &h, sizeof(h), hipMemcpyHostToDevice, s));
-		Dev<float> st_t; st_t.alloc(n_rays); Dev<uint32_t> nr, bs, nrec, q; nr.alloc(n_rays); bs.alloc(n_rays); nrec.alloc(n_rays); q.alloc(1);
+		Dev<float> st_t; st_t.alloc(n_rays); Dev<uint32_t> nr, bs, nrec, q; nr.alloc(n_rays); bs.alloc(n_rays); nrec.alloc(n_rays); q.alloc(2);
 		Dev<uint2> rec; rec.alloc((size_t)n_rays * NERF_STEPS);
 		const MarchWork mw{rec.p, nrec.p, q.p, tb->mwork.waves};
 		Dev<uint8_t> tmp; const size_t tb_ = scan_temp_bytes(n_rays); tmp.alloc(tb_ + 256);
 		Dev<uint32_t> lin; lin.alloc(LIN_WORDS);
 		launch_bitfield_linear(s, bitfield, lin.p);
-		launch_march_count(s, n_rays, sst.p, DPInfo{rank, world}, tb->ds, bitfield, lin.p, rng_state, rng_inc, rays, st_t.p, nr.p, mw);
+		launch_march_count(s, n_rays, max_samples, sst.p, DPInfo{rank, world}, tb->ds, bitfield, lin.p, rng_state, rng_inc, rays, st_t.p, nr.p, mw);
 		launch_exclusive_scan(s, tmp.p, tb_, nr.p, bs.p, n_rays);
 		Dev<uint32_t> sr; sr.alloc(std::max<uint32_t>(1, max_samples));
 		launch_march_write(s, n_rays, sst.p, tb->ds, rays, mw, nr.p, bs.p, numsteps, coords, sr.p, max_samples);

@@ -91,9 +91,11 @@ class CpuTrainer:
     def finish(self, g, counters_sum=None):
         """Counters update (testbed_nerf.cu:3399-3438), RNG advance and the Ema(Adam) step."""
         W = self.world
-        numsteps_counter, compacted = counters_sum if counters_sum is not None else (self.last["numsteps_counter"], self.last["compacted"])
+        _, compacted = counters_sum if counters_sum is not None else (self.last["numsteps_counter"], self.last["compacted"])
         self.n_rays_total += self.R * W
-        before, measured = numsteps_counter // W, compacted // W
+        # the cap on the next step's pre-compaction samples follows this rank's own request count; the R
+        # adaptation follows the all-reduced compacted count (identical on every rank)
+        before, measured = self.last["numsteps_counter"], compacted // W
         if before > 0 and measured > 0:
             self.max_inference = (min(before, self.max_samples) + 127) // 128 * 128
             if not self.fixed_rays:

@@ -1,15 +1,13 @@
-"""TEST INFRASTRUCTURE ONLY: an independent restatement of the marching-cubes case table that the
-product (neus2_amd/csrc/mc.hip, `mc_build_table`) generates, used by the parity tests to check the GPU
-mesh face-for-face.
+"""TEST INFRASTRUCTURE ONLY: the marching-cubes case table for the parity tests and the numpy mesh restatement.
 
-Neither side copies a published triangle table. For each of the 256 corner masks the crossing edges are
-joined face by face into segments — on a face with four crossings, each set corner is cut off by its own
-segment (the rule is symmetric, so the two cubes sharing a face agree and the mesh is watertight) — the
-segments are oriented with the set corners on their left seen from outside the cube, chained into loops,
-and each loop is fanned into triangles from its lowest-numbered edge. Corner / edge numbering is the
-reference's (marching_cubes.cu:255-275, 377-420): corner bit k of the mask is set iff density > thresh.
+The table is the reference's constant `triangle_table` (src/marching_cubes.cu:401-658, the classic Lorensen /
+Bourke table via PyMCubes, BSD-3), stored as data in oracle/mc_triangle_table.npy (tools/extract_mc_table.py).
+Corner / edge numbering is the reference's (marching_cubes.cu:255-275, 377-420): corner bit k of the mask is set
+iff density > thresh.
 """
 from __future__ import annotations
+
+import os
 
 import numpy as np
 
@@ -21,70 +19,13 @@ EDGES = [(0, 1), (1, 2), (3, 2), (0, 3), (4, 5), (5, 6), (7, 6), (4, 7), (0, 4),
 EDGE_OWNER = [((0, 0, 0), 0), ((1, 0, 0), 1), ((0, 1, 0), 0), ((0, 0, 0), 1),
               ((0, 0, 1), 0), ((1, 0, 1), 1), ((0, 1, 1), 0), ((0, 0, 1), 1),
               ((0, 0, 0), 2), ((1, 0, 0), 2), ((1, 1, 0), 2), ((0, 1, 0), 2)]
-# faces: corners in cyclic order and outward normal
-FACES = [((0, 3, 7, 4), (-1, 0, 0)), ((1, 2, 6, 5), (1, 0, 0)), ((0, 1, 5, 4), (0, -1, 0)),
-         ((3, 2, 6, 7), (0, 1, 0)), ((0, 1, 2, 3), (0, 0, -1)), ((4, 5, 6, 7), (0, 0, 1))]
 MAX_TRIS = 6
-
-
-def _edge_of(a, b):
-    for e, (p, q) in enumerate(EDGES):
-        if {p, q} == {a, b}:
-            return e
-    raise KeyError((a, b))
-
-
-def _mid(e):
-    a, b = EDGES[e]
-    return (np.array(CORNERS[a], float) + np.array(CORNERS[b], float)) * 0.5
+_TABLE = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "mc_triangle_table.npy"))
 
 
 def case_triangles(mask):
-    if mask == 0 or mask == 255:
-        return []
-    inside = [(mask >> k) & 1 for k in range(8)]
-    nxt = {}
-    for corners, normal in FACES:
-        n = np.array(normal, float)
-        cyc = list(corners)
-        segs = []
-        set_corners = [c for c in cyc if inside[c]]
-        if len(set_corners) in (0, 4):
-            continue
-        if len(set_corners) == 2 and not any(inside[cyc[i]] and inside[cyc[(i + 1) % 4]] for i in range(4)):
-            # ambiguous face (diagonal set corners): cut off each set corner separately
-            for c in set_corners:
-                i = cyc.index(c)
-                segs.append((_edge_of(c, cyc[(i - 1) % 4]), _edge_of(c, cyc[(i + 1) % 4]), c))
-        else:
-            xs = [_edge_of(cyc[i], cyc[(i + 1) % 4]) for i in range(4) if inside[cyc[i]] != inside[cyc[(i + 1) % 4]]]
-            assert len(xs) == 2
-            segs.append((xs[0], xs[1], set_corners[0]))
-        for a, b, c in segs:
-            A, B, P = _mid(a), _mid(b), np.array(CORNERS[c], float)
-            # orient A->B with the set corner on the left seen from outside: cross(n, B - A) . (P - A) > 0
-            if np.dot(np.cross(n, B - A), P - A) < 0:
-                a, b = b, a
-            assert a not in nxt
-            nxt[a] = b
-    tris = []
-    seen = set()
-    for start in sorted(nxt):
-        if start in seen:
-            continue
-        loop = [start]
-        seen.add(start)
-        v = nxt[start]
-        while v != start:
-            loop.append(v)
-            seen.add(v)
-            v = nxt[v]
-        # fan from the smallest edge id of the loop
-        k = loop.index(min(loop))
-        loop = loop[k:] + loop[:k]
-        for i in range(1, len(loop) - 1):
-            tris.append((loop[0], loop[i], loop[i + 1]))
-    return tris
+    row = [int(v) for v in _TABLE[mask] if v >= 0]
+    return [tuple(row[i:i + 3]) for i in range(0, len(row), 3)]
 
 
 def build_table():

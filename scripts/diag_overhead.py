@@ -18,4 +18,6 @@ for w, n in ((5, 20), (200, 20), (800, 20)):
     done += n
     tb.set_profiling(True); tb.train_steps(n); tb.synchronize(); done += n
     ph = tb.phase_times(); tb.set_profiling(False)
+    st = tb.stats()
+    print(f"   march first pass {st['march_first_pass_rays']} kept extent {st['kept_ray_extent']} Npre {st['measured_batch_size_before_compaction']}", flush=True)
     print(f"after {w}: enqueue {1e3 * (t1 - t0) / n:.3f} ms/step, wall {1e3 * (t2 - t0) / n:.3f} ms/step, phases {ph}", flush=True)

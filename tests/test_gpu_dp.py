@@ -153,7 +153,7 @@ def test_dp_step_gradient_matches_oracle_and_ranks_stay_identical(scene):
     np.testing.assert_array_equal(a.get_params(), b.get_params())
     np.testing.assert_array_equal(a.get_ema_params(), b.get_ema_params())
     sa, sb = a.stats(), b.stats()
-    for k in ("training_step", "rays_per_batch", "measured_batch_size", "measured_batch_size_before_compaction", "n_rays_total", "loss"):
+    for k in ("training_step", "rays_per_batch", "measured_batch_size", "n_rays_total", "loss"):
         assert sa[k] == sb[k], k
     assert sa["n_rays_total"] == 12 * 2 * R
     np.testing.assert_array_equal(a.get_density_grid()[0], b.get_density_grid()[0])

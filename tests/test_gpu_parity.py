@@ -545,3 +545,88 @@ def test_sdf_on_grid_and_mesh(torch_cuda):
     paired = np.mean([(v, u) in E for (u, v) in E])
     record("mc_network", n_verts=len(V), n_tris=len(F), paired_edges=paired)
     assert max(E.values()) == 1 and paired > 0.98
+
+
+def test_marching_cubes_1024_network_subblocks(torch_cuda):
+    """Config 5 at full size: Testbed::marching_cubes at 1024^3 through the network. Rows of the 2^30-point SDF grid
+    (at the start, middle and end of the linear index range) against the oracle's forward at the same grid points
+    (the fp16 tolerance of test_sdf_on_grid_and_mesh), then the mesh: indices in range, vertices inside the aabb
+    and on a sign change of the SDF grid."""
+    import ctypes as C
+    import oracle as O
+    from neus2_amd._lib import check, lib
+    tb = _mc_testbed()
+    tb.train_steps(60)
+    st = tb.stats()
+    R = 1024
+    res = (C.c_int32 * 3)(R, R, R)
+    lo, hi = (C.c_float * 3)(0.0, 0.0, 0.0), (C.c_float * 3)(1.0, 1.0, 1.0)
+    nv, nt = C.c_uint32(), C.c_uint32()
+    check(lib().neus_testbed_marching_cubes(tb.handle, res, lo, hi, C.c_float(0.0), None, C.byref(nv), C.byref(nt)))
+    cfg = O.make_cfg(per_level_scale=tb._net_cfg.per_level_scale)
+    ema = tb.get_ema_params()
+    rows = [(0, 0), (511, 517), (1023, 1023)]  # (y, z) rows of 1024 x-consecutive points
+    for y, z in rows:
+        off = (z * R + y) * R
+        got = np.zeros(R, np.float32)
+        check(lib().neus_testbed_mc_density(tb.handle, C.c_uint64(off), C.c_uint64(R), C.c_void_p(got.ctypes.data)))
+        coords = np.zeros((R, 7), np.float32)
+        inv = np.float32(1.0 / R)
+        coords[:, 0] = (np.arange(R, dtype=np.float32) * inv).astype(np.float32)
+        coords[:, 1] = np.float32(y) * inv
+        coords[:, 2] = np.float32(z) * inv
+        coords[:, 4:] = 0.5
+        ref = O.network_forward(cfg, ema, coords, st["valid_level"]).view(np.float16)[:, 3].astype(np.float32) + np.float32(0.0)
+        err = np.abs(got - ref)
+        ok = err <= 2e-3 + 4e-3 * np.abs(ref)
+        record("mc1024_row", y=y, z=z, frac_within_tol=ok.mean(), max_abs_err=err.max())
+        assert ok.mean() >= 0.99, ((y, z), ok.mean(), err.max())
+    V = np.zeros((nv.value, 3), np.float32)
+    F = np.zeros((nt.value, 3), np.uint32)
+    check(lib().neus_testbed_get_mesh(tb.handle, C.c_void_p(V.ctypes.data), C.c_void_p(F.ctypes.data)))
+    record("mc1024_mesh", n_verts=nv.value, n_tris=nt.value)
+    assert nv.value > 10000 and nt.value > 10000
+    assert F.max() < nv.value
+    assert (V >= 0).all() and (V <= 1).all()
+    # every edge of a triangle joins two vertices at most one grid cell apart
+    e = np.linalg.norm(V[F[:, 0]] - V[F[:, 1]], axis=1)
+    assert e.max() <= np.sqrt(3) / R * 1.001
+
+
+def test_marching_cubes_64bit_grid_index(torch_cuda):
+    """A 1664^3 grid (4.6e9 points: point, vertex-slot and cube indices beyond 2^32, where the reference's uint32
+    index math wraps, marching_cubes.cu:285-287) of an analytic sphere's SDF, meshed from a device density grid:
+    every vertex lies on the sphere to within a grid spacing, including those whose grid points sit past linear
+    index 2^32, the vertex count matches the surface area, and faces reference existing vertices."""
+    import ctypes as C
+    from neus2_amd._lib import check, lib
+    t = torch_cuda
+    R = 1664
+    c, rad = 0.5, 0.45
+    d = t.empty((R, R, R), dtype=t.float32, device="cuda")
+    ax = (t.arange(R, device="cuda", dtype=t.float32) / R)
+    yy, xx = t.meshgrid(ax, ax, indexing="ij")
+    base = (xx - c) ** 2 + (yy - c) ** 2
+    for z in range(R):
+        d[z] = t.sqrt(base + (float(z) / R - c) ** 2) - rad
+    del yy, xx, base
+    tb = _mc_testbed()
+    res = (C.c_int32 * 3)(R, R, R)
+    lo, hi = (C.c_float * 3)(0.0, 0.0, 0.0), (C.c_float * 3)(1.0, 1.0, 1.0)
+    nv, nt = C.c_uint32(), C.c_uint32()
+    check(lib().neus_testbed_marching_cubes(tb.handle, res, lo, hi, C.c_float(0.0), C.c_void_p(d.data_ptr()), C.byref(nv), C.byref(nt)))
+    del d
+    t.cuda.empty_cache()
+    V = np.zeros((nv.value, 3), np.float32)
+    F = np.zeros((nt.value, 3), np.uint32)
+    check(lib().neus_testbed_get_mesh(tb.handle, C.c_void_p(V.ctypes.data), C.c_void_p(F.ctypes.data)))
+    r = np.linalg.norm(V.astype(np.float64) - c, axis=1)
+    h = 1.0 / R
+    beyond = V[:, 2] * R * R * R + V[:, 1] * R * R >= 2.0 ** 32  # vertices owned by grid points past 2^32
+    record("mc_64bit", n_verts=nv.value, n_tris=nt.value, n_beyond=beyond.sum(), max_dev=np.abs(r - rad).max() / h)
+    assert beyond.sum() > 1000
+    assert np.abs(r - rad).max() <= h
+    assert F.max() < nv.value
+    # one vertex per crossing edge: about 1.5 x area / h^2 for a sphere (x, y, z edge crossings ~ |n_x|+|n_y|+|n_z|)
+    expect = 4 * np.pi * rad * rad / (h * h) * 1.5
+    assert 0.9 * expect < nv.value < 1.1 * expect, (nv.value, expect)
