@@ -164,8 +164,14 @@ void launch_bitfield_linear(hipStream_t s, const uint8_t* bitfield, uint32_t* li
 // Sample runs of the march (march.hip): per ray slot up to NERF_STEPS records {t of the run's first sample,
 // (samples of the ray before the run) << 16 | run length}; a run's samples are t, t + dt(t), ... (the reference's
 // t += dt), at most MARCH_RUN_MAX of them. nrec: records per slot; counter: the persistent march's ray queue.
+// seg: per ray slot MARCH_SEG_RECS segment-local run records (the multi-lane march's scratch, split evenly over the
+// lanes of a ray; a segment never holds more runs than its ~NERF_STEPS / lanes steps).
 constexpr uint32_t MARCH_RUN_MAX = 16;
-struct MarchWork { uint2* rec; uint32_t* nrec; uint32_t* counter /* 2: the two passes' ray queues */; uint32_t waves; /* 0 = one lane per ray */ };
+constexpr uint32_t MARCH_SEG_RECS = NERF_STEPS + 64;
+struct MarchWork {
+	uint2* rec; uint32_t* nrec; uint32_t* counter /* 2: the two passes' ray queues */; uint32_t waves; /* 0 = one lane per ray */
+	uint2* seg; uint32_t lanes_per_ray;  /* 1 or 4 */
+};
 // Ray generation + the occupancy march: rays (6 f32 per slot), tstart (1 per slot), nreq (requested
 // samples per slot) and the sample runs (MarchWork).
 void launch_march_count(hipStream_t s, uint32_t cap, uint32_t max_samples /* global cap: 16 x batch */, StepState* st, DPInfo dp, const DevDataset& ds, const uint8_t* bitfield,

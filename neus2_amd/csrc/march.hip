@@ -119,27 +119,37 @@ __device__ __forceinline__ void load_march_ray(const float* __restrict__ rays, u
 // as the cell index stays the same (same occupancy bit, inside the AABB, mip 0), so the run continues on the
 // position and cell index alone (no bitfield read, no store per sample). Cells with an index 0 / 127 (a position
 // on an AABB face takes mip 1) and the centre cell (max|p - 0.5| = 0 takes mip 1) go through march_step.
-struct RunAcc { float t0; uint32_t len, cum, nrec; };
-__device__ __forceinline__ void run_flush(uint2* __restrict__ rec, RunAcc& a) {
-	if (a.len) { rec[a.nrec++] = make_uint2(__float_as_uint(a.t0), (a.cum << 16) | a.len); a.cum += a.len; a.len = 0; }
+// One march event of a lane's ray segment: a sample run within a cell (FAST) or one march_step. k is the index of
+// t in the ray's step sequence (t0 and its successive t += dt); the event stops at the segment end k_end (the first
+// step at or past it is the next segment's). Returns false once the ray is finished (left the AABB).
+// Sample runs go to `rec` as {t of the first sample, k_first << 8 | length} (segment-local records).
+struct SegAcc { float t0; uint32_t k0, len, nrec, n; };
+__device__ __forceinline__ void seg_flush(uint2* __restrict__ rec, SegAcc& a) {
+	if (a.len) { rec[a.nrec++] = make_uint2(__float_as_uint(a.t0), (a.k0 << 8) | a.len); a.len = 0; }
 }
-// one sample at t, following the previous sample of the open run (if any)
-__device__ __forceinline__ void run_add(uint2* __restrict__ rec, RunAcc& a, float t) {
-	if (a.len == MARCH_RUN_MAX) run_flush(rec, a);
-	if (a.len == 0) a.t0 = t;
-	++a.len;
+__device__ __forceinline__ void seg_add(uint2* __restrict__ rec, SegAcc& a, float t, uint32_t k) {
+	if (a.len == MARCH_RUN_MAX) seg_flush(rec, a);
+	if (a.len == 0) { a.t0 = t; a.k0 = k; }
+	++a.len; ++a.n;
 }
 __device__ __forceinline__ void mip0_cell(const float pos[3], int c[3]) {  // cascaded_grid_idx_at, mip 0 (march_step)
 #pragma unroll
 	for (int d = 0; d < 3; ++d) c[d] = clampi((int)(((pos[d] - 0.5f) + 0.5f) * NERF_GRIDSIZE), 0, NERF_GRIDSIZE - 1);
 }
+// the first VQ event intervals [k_first, k_after) of a segment (the visited steps where the true trajectory may join)
+constexpr int VQ = 4;
+struct Visits { uint32_t b[VQ], e[VQ]; uint32_t n; };
+__device__ __forceinline__ void visit(Visits& v, uint32_t kb, uint32_t ke) {
+#pragma unroll
+	for (int q = 0; q < VQ; ++q) if (v.n == (uint32_t)q) { v.b[q] = kb; v.e[q] = ke; }
+	++v.n;
+}
 
-// One march event of a lane's ray: a sample run within a cell (FAST) or one march_step. Returns false once the
-// ray is finished (left the AABB or NERF_STEPS samples).
 template <bool FAST>
 __device__ __forceinline__ bool march_event(const DevDataset& ds, const uint8_t* __restrict__ bf, const uint32_t* __restrict__ lin,
-                                            const MarchRay& mr, float& t, uint32_t& n, RunAcc& acc,
+                                            const MarchRay& mr, float& t, uint32_t& k, uint32_t k_end, SegAcc& acc, Visits& vis,
                                             uint2* __restrict__ rec) {
+	const uint32_t kb = k;
 	if (FAST) {
 		float pos[3];
 #pragma unroll
@@ -159,20 +169,22 @@ __device__ __forceinline__ bool march_event(const DevDataset& ds, const uint8_t*
 			occ = occupied(pos[0], pos[1], pos[2], bf, mip);
 		}
 		if (occ) {
-			run_add(rec, acc, t); ++n; t += MIN_CONE_STEPSIZE;
+			seg_add(rec, acc, t, k); t += MIN_CONE_STEPSIZE; ++k;
 			if (interior) {
-				while (n < NERF_STEPS) {
+				while (k < k_end) {
 					float p2[3];
 #pragma unroll
 					for (int d = 0; d < 3; ++d) p2[d] = mr.o[d] + t * mr.dir[d];
 					int c2[3]; mip0_cell(p2, c2);
 					if ((c2[0] != c[0]) | (c2[1] != c[1]) | (c2[2] != c[2])) break;
-					run_add(rec, acc, t); ++n; t += MIN_CONE_STEPSIZE;
+					seg_add(rec, acc, t, k); t += MIN_CONE_STEPSIZE; ++k;
 				}
 			}
-			return n < NERF_STEPS;
+			visit(vis, kb, k);
+			return true;
 		}
-		run_flush(rec, acc);
+		seg_flush(rec, acc);
+		visit(vis, kb, kb + 1);
 		// advance_to_next_voxel with a constant step (march_step)
 		const uint32_t res = NERF_GRIDSIZE >> mip;
 		float tn = 3.402823466e+38f;
@@ -182,16 +194,46 @@ __device__ __forceinline__ bool march_event(const DevDataset& ds, const uint8_t*
 			tn = fminf(tn, (floorf(p + 0.5f + 0.5f * signf(mr.dir[d])) - p) * mr.idir[d]);
 		}
 		const float t_target = t + fmaxf(ldexpf(tn, -(int)(7 - mip)), 0.0f);
-		do { t += MIN_CONE_STEPSIZE; } while (t < t_target);
+		do { t += MIN_CONE_STEPSIZE; ++k; } while (t < t_target);
 		return true;
 	} else {
 		float dt, pos[3];
-		const int k = march_step<false>(ds, bf, lin, mr, t, dt, pos);
-		if (k == 0) return false;
-		if (k == 1) { run_add(rec, acc, t); ++n; t += dt; return n < NERF_STEPS; }
-		run_flush(rec, acc);
+		// march_step without its skip loop (the steps of the skip are counted here)
+#pragma unroll
+		for (int d = 0; d < 3; ++d) pos[d] = mr.o[d] + t * mr.dir[d];
+		if (!aabb_contains(ds, pos)) return false;
+		dt = calc_dt(t, ds.cone_angle);
+		const uint32_t mip = (uint32_t)mip_from_dt(dt, pos[0], pos[1], pos[2]);
+		if (occupied(pos[0], pos[1], pos[2], bf, mip)) {
+			seg_add(rec, acc, t, k); t += dt; ++k;
+			visit(vis, kb, k);
+			return true;
+		}
+		seg_flush(rec, acc);
+		visit(vis, kb, kb + 1);
+		// advance_to_next_voxel (march_common.h) with the step count
+		const uint32_t res = NERF_GRIDSIZE >> mip;
+		float p[3], tt[3];
+#pragma unroll
+		for (int d = 0; d < 3; ++d) { p[d] = res * pos[d]; tt[d] = (floorf(p[d] + 0.5f + 0.5f * signf(mr.dir[d])) - p[d]) * mr.idir[d]; }
+		const float tn = fminf(fminf(tt[0], tt[1]), tt[2]);
+		const float t_target = t + fmaxf(tn / res, 0.0f);
+		do { t += calc_dt(t, ds.cone_angle); ++k; } while (t < t_target);
 		return true;
 	}
+}
+
+// Marches one segment [k, k_end) of a ray from the visited step (k, t); returns its exit: the first visited step at or
+// past k_end (k_end itself inside a sample run) as (k, t), or k = FINISHED when the ray left the AABB first.
+constexpr uint32_t FINISHED = 0xffffffffu;
+template <bool FAST>
+__device__ __forceinline__ void march_segment(const DevDataset& ds, const uint8_t* __restrict__ bf, const uint32_t* __restrict__ lin,
+                                              const MarchRay& mr, float& t, uint32_t& k, uint32_t k_end, SegAcc& acc, Visits& vis,
+                                              uint2* __restrict__ rec, uint32_t rec_cap) {
+	while (k < k_end) {
+		if (acc.nrec + 1 >= rec_cap || !march_event<FAST>(ds, bf, lin, mr, t, k, k_end, acc, vis, rec)) { k = FINISHED; break; }
+	}
+	seg_flush(rec, acc);
 }
 
 // Two passes over the ray slots. Only a prefix of the slots can be kept: slot i is kept iff n_i > 0 and
@@ -202,7 +244,16 @@ __device__ __forceinline__ bool march_event(const DevDataset& ds, const uint8_t*
 // samples and every training result are those of marching all slots; the requested-sample counter then reads a
 // value at or above max_samples, which is all the reference ever uses of it (min(counter, max_samples),
 // testbed_nerf.cu:3036-3039; the rest is the GUI's text).
-template <bool FAST>
+//
+// Each ray is marched by MG lanes at once. The march's t values are the sequence t0, t0 + dt, ... (every update of
+// the reference's loop is one t += dt, the skip included), so lane g starts at the first step k_g of the g-th slice
+// of [t0, t_exit) by stepping there, and marches its segment [k_g, k_{g+1}) as if k_g were visited. The true march
+// enters segment g at v_g, the exit of segment g - 1; the march is a deterministic function of its visited step, so
+// when lane g's trajectory visits v_g the two coincide from there and lane g keeps its samples at k >= v_g; when it
+// does not (a skip of the previous segment landed on a step lane g jumped over), lane g re-marches from v_g. The
+// checks run in segment order. Samples past NERF_STEPS are cut (the reference's loop stops there). The result is the
+// single-lane march's, sample for sample (tests/test_gpu_parity.py::test_sample_rays_bit_exact).
+template <bool FAST, int MG>
 __global__ void __launch_bounds__(256) k_march(uint32_t cap_rays, uint32_t pass, uint32_t max_samples, StepState* __restrict__ st, DevDataset ds,
                                                const uint8_t* __restrict__ bitfield, const uint32_t* __restrict__ lin, const float* __restrict__ rays,
                                                const float* __restrict__ tstart, uint32_t* __restrict__ nreq, MarchWork mw) {
@@ -213,43 +264,126 @@ __global__ void __launch_bounds__(256) k_march(uint32_t cap_rays, uint32_t pass,
 		for (uint32_t k = lo + blockIdx.x * blockDim.x + threadIdx.x; k < hi; k += gridDim.x * blockDim.x) { nreq[k] = 1; mw.nrec[k] = 0; }
 		return;
 	}
-	uint32_t* queue = mw.counter + pass;
-	const uint32_t lane = threadIdx.x & 63;
-	uint32_t i = 0, total = 0;
-	bool alive = false, drained = false;
-	MarchRay mr;
-	float t = 0.f;
-	uint32_t n = 0;
-	RunAcc acc{0.f, 0u, 0u, 0u};
-	uint2* rec = mw.rec;
-	while (true) {
-		// refill the idle lanes once a quarter of the wave is idle, or all of it (wave-uniform decision)
-		const uint64_t idle = __ballot(!alive && !drained);
-		const uint64_t live = __ballot(alive);
-		const uint32_t n_idle = (uint32_t)__popcll(idle);
-		if (n_idle >= 16 || (live == 0 && n_idle > 0)) {
-			uint32_t b = 0;
-			if (lane == 0) b = atomicAdd(queue, n_idle);
-			b = (uint32_t)__shfl((int)b, 0);
-			if (!alive && !drained) {
-				i = lo + b + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
-				if (i >= hi) {
-					drained = true;
+	constexpr uint32_t SEG_CAP = MARCH_SEG_RECS / MG;  // segment-local records per lane
+	const uint32_t lane = threadIdx.x & 63, g = lane % MG;
+	const uint32_t groups = (gridDim.x * blockDim.x) / MG;
+	uint32_t total = 0;
+	for (uint32_t i = lo + (blockIdx.x * blockDim.x + threadIdx.x) / MG; i - lo < ((hi - lo + groups - 1) / groups) * groups; i += groups) {
+		const bool have = i < hi;
+		const float t0 = have ? tstart[i] : -1.f;
+		MarchRay mr;
+		float t_exit = t0;
+		if (t0 >= 0.f) {
+			load_march_ray(rays, i, mr, ds.motion.on != 0);
+			float tx[3];
+#pragma unroll
+			for (int d = 0; d < 3; ++d) {
+				const float a = (ds.aabb_min[d] - mr.o[d]) * mr.idir[d], b = (ds.aabb_max[d] - mr.o[d]) * mr.idir[d];
+				tx[d] = fmaxf(a, b);
+			}
+			t_exit = fminf(fminf(tx[0], tx[1]), tx[2]);
+		}
+		const float span = t_exit - t0;
+		const bool split = t0 >= 0.f && span > 0.f && span < 1e4f;
+		// lane g's first step: step from t0 to the start of its slice (lane 0: t0 itself)
+		float t = t0;
+		uint32_t k = 0;
+		const bool active = t0 >= 0.f && (g == 0 || split);
+		if (active && g > 0) {
+			const float t_g = t0 + span * ((float)g / (float)MG);
+			while (t < t_g && k < 4 * NERF_STEPS) { t += FAST ? MIN_CONE_STEPSIZE : calc_dt(t, ds.cone_angle); ++k; }
+		}
+		uint32_t k_end = (uint32_t)__shfl((int)k, (int)((lane + 1) % 64));  // the next lane's start
+		if (g == MG - 1 || !split) k_end = FINISHED;
+		uint2* rec = mw.seg + ((size_t)i * MG + g) * SEG_CAP;
+		SegAcc acc{0.f, 0u, 0u, 0u, 0u};
+		Visits vis{};
+		vis.n = 0;
+		float et = t;
+		uint32_t ek = active ? k : FINISHED;
+		if (active) { march_segment<FAST>(ds, bitfield, lin, mr, et, ek, k_end, acc, vis, rec, SEG_CAP); }
+		// segment order: lane g joins the exit of lane g - 1
+		uint32_t vk = k;   // first valid step of this segment
+		for (int q = 1; q < MG; ++q) {
+			const uint32_t pk = (uint32_t)__shfl((int)ek, (int)(lane - 1) & 63);
+			const float pt = __shfl(et, (int)(lane - 1) & 63);
+			bool redo = false;
+			if (g == (uint32_t)q && active) {
+				if (pk == FINISHED || pk >= k_end) {  // the ray ended (or jumped past this segment) before it
+					acc.n = 0; acc.nrec = 0; vk = pk; ek = pk; et = pt;
 				} else {
-					t = tstart[i]; n = 0; acc = RunAcc{0.f, 0u, 0u, 0u};
-					rec = mw.rec + (size_t)i * NERF_STEPS;
-					if (t >= 0.f) { load_march_ray(rays, i, mr, ds.motion.on != 0); alive = true; }
-					else { nreq[i] = 0; mw.nrec[i] = 0; }  // dropped ray / slot beyond R: nothing to march
+					bool seen = false;
+#pragma unroll
+					for (int w = 0; w < VQ; ++w) seen |= (w < (int)vis.n) && pk >= vis.b[w] && pk < vis.e[w];
+					if (seen) vk = pk;
+					else redo = true;
 				}
 			}
-			continue;
+			if (__ballot(redo)) {
+				if (redo) {
+					acc = SegAcc{0.f, 0u, 0u, 0u, 0u}; vis.n = 0;
+					et = pt; ek = pk; vk = pk;
+					march_segment<FAST>(ds, bitfield, lin, mr, et, ek, k_end, acc, vis, rec, SEG_CAP);
+				}
+			}
 		}
-		if (live == 0) break;  // every lane drained
-		if (alive && !march_event<FAST>(ds, bitfield, lin, mr, t, n, acc, rec)) {
-			run_flush(rec, acc);
-			nreq[i] = n; mw.nrec[i] = acc.nrec;
-			total += n;
-			alive = false;
+		// samples of this segment at k >= vk (the first run may start before vk and is cut there)
+		uint32_t n_g = 0, r_first = 0;
+		float t_first = 0.f;
+		uint32_t cut = 0;  // samples dropped from the first kept run
+		if (active && vk != FINISHED) {
+			for (uint32_t r = 0; r < acc.nrec; ++r) {
+				const uint2 R = rec[r];
+				const uint32_t k0 = R.y >> 8, len = R.y & 0xff;
+				if (k0 + len <= vk) { r_first = r + 1; continue; }
+				if (r == r_first && k0 < vk) { cut = vk - k0; }
+				n_g += len - (r == r_first ? cut : 0u);
+			}
+		}
+		if (!active || vk == FINISHED) { n_g = 0; r_first = acc.nrec; }
+		// prefix over the ray's lanes (in segment order) of the samples, NERF_STEPS cap
+		uint32_t before = 0;
+		for (int q = 0; q < MG - 1; ++q) {
+			const uint32_t pn = (uint32_t)__shfl((int)n_g, (int)(lane - g + q));
+			if ((uint32_t)q < g) before += pn;
+		}
+		const uint32_t keep = before >= NERF_STEPS ? 0u : min(n_g, NERF_STEPS - before);
+		// records this lane emits for its `keep` samples, and their prefix over the lanes
+		uint32_t w_g = 0;
+		{
+			uint32_t got = 0;
+			for (uint32_t r = r_first; r < acc.nrec && got < keep; ++r) {
+				const uint32_t len = (rec[r].y & 0xff) - (r == r_first ? cut : 0u);
+				got += len; ++w_g;
+			}
+		}
+		uint32_t rbefore = 0, r_tot = 0;
+		for (int q = 0; q < MG; ++q) {
+			const uint32_t pw = (uint32_t)__shfl((int)w_g, (int)(lane - g + q));
+			if ((uint32_t)q < g) rbefore += pw;
+			r_tot += pw;
+		}
+		// final records: {t of the first sample, (samples of the ray before the run) << 16 | length}
+		uint2* out = mw.rec + (size_t)i * NERF_STEPS;
+		uint32_t written = 0, nr = rbefore;
+		for (uint32_t r = r_first; r < acc.nrec && written < keep; ++r) {
+			const uint2 R = rec[r];
+			uint32_t len = R.y & 0xff;
+			float tr = __uint_as_float(R.x);
+			if (r == r_first && cut) {
+				for (uint32_t c = 0; c < cut; ++c) tr += FAST ? MIN_CONE_STEPSIZE : calc_dt(tr, ds.cone_angle);
+				len -= cut;
+			}
+			len = min(len, keep - written);
+			out[nr++] = make_uint2(__float_as_uint(tr), ((before + written) << 16) | len);
+			written += len;
+		}
+		// the ray's sample total from its last lane
+		const uint32_t n_tot = (uint32_t)__shfl((int)(before + keep), (int)(lane - g + MG - 1));
+		if (have && g == 0) {
+			nreq[i] = t0 >= 0.f ? n_tot : 0u;
+			mw.nrec[i] = t0 >= 0.f ? r_tot : 0u;
+			total += t0 >= 0.f ? n_tot : 0u;
 		}
 	}
 	if (pass == 0) {  // the pass's requested samples (one atomic per wave)
@@ -720,8 +854,13 @@ void launch_march_count(hipStream_t s, uint32_t cap, uint32_t max_samples, StepS
 	const uint32_t waves = mw.waves ? std::min(mw.waves, (cap + 63) / 64) : (cap + 63) / 64;
 	const uint32_t blocks = std::max<uint32_t>(1, (waves + 3) / 4);
 	for (uint32_t pass = 0; pass < 2; ++pass) {
-		if (ds.cone_angle == 0.0f) k_march<true><<<blocks, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, lin, rays, tstart, nreq, mw);
-		else k_march<false><<<blocks, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, nullptr, rays, tstart, nreq, mw);
+		if (ds.cone_angle == 0.0f) {
+			if (mw.lanes_per_ray == 1) k_march<true, 1><<<blocks, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, lin, rays, tstart, nreq, mw);
+			else k_march<true, 4><<<blocks * 4, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, lin, rays, tstart, nreq, mw);
+		} else {
+			if (mw.lanes_per_ray == 1) k_march<false, 1><<<blocks, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, nullptr, rays, tstart, nreq, mw);
+			else k_march<false, 4><<<blocks * 4, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, nullptr, rays, tstart, nreq, mw);
+		}
 	}
 }
 void launch_march_write(hipStream_t s, uint32_t cap, StepState* st, const DevDataset& ds, const float* rays, const MarchWork& mw, const uint32_t* nreq,

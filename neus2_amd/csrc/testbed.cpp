@@ -192,7 +192,7 @@ struct NeusTestbed {
 	uint32_t batch = 0, max_samples = 0;
 	Dev<float> rays, startt, coords, coords_c, loss, ek, mask, loss_sum;
 	Dev<uint32_t> nreq, base, numsteps, ccount, cbase, enc, march_nrec, march_queue;
-	Dev<uint2> march_rec;
+	Dev<uint2> march_rec, march_seg;
 	MarchWork mwork{};
 	Dev<float> dydx;
 	Dev<half_t> net_out, dL_dout, trainbuf;
@@ -401,7 +401,8 @@ struct NeusTestbed {
 		max_samples = batch * 16;  // testbed_nerf.cu:3725
 		rays.alloc(6 * (size_t)MAX_RAYS); startt.alloc((size_t)MAX_RAYS);
 		march_rec.alloc((size_t)MAX_RAYS * NERF_STEPS); march_nrec.alloc(MAX_RAYS); march_queue.alloc(2);
-		mwork = MarchWork{march_rec.p, march_nrec.p, march_queue.p, march_waves()}; nreq.alloc(MAX_RAYS); base.alloc(MAX_RAYS);
+		march_seg.alloc((size_t)MAX_RAYS * MARCH_SEG_RECS);
+		mwork = MarchWork{march_rec.p, march_nrec.p, march_queue.p, march_waves(), march_seg.p, march_lanes()}; nreq.alloc(MAX_RAYS); base.alloc(MAX_RAYS);
 		numsteps.alloc(2 * (size_t)MAX_RAYS); ccount.alloc(MAX_RAYS); cbase.alloc(MAX_RAYS);
 		l_sa.alloc(max_samples); l_ekt.alloc(max_samples); sample_ray.alloc(max_samples);
 		l_ck4.alloc(max_samples / 8 + 1); l_cke.alloc(max_samples / 8 + 1);
@@ -518,6 +519,11 @@ struct NeusTestbed {
 	uint32_t march_waves() const {
 		if (const char* e = std::getenv("NEUS_MARCH_WAVES")) return (uint32_t)std::strtoul(e, nullptr, 10);
 		return 0;
+	}
+	// lanes marching one ray (segments of its step sequence, see march.hip); NEUS_MARCH_LANES=1 selects one lane per ray
+	uint32_t march_lanes() const {
+		if (const char* e = std::getenv("NEUS_MARCH_LANES")) return std::strtoul(e, nullptr, 10) == 1 ? 1u : 4u;
+		return 4;
 	}
 	uint32_t gm_steps() const { return cfg.predict_global_movement ? cfg.global_movement_steps : 0u; }
 
@@ -1456,7 +1462,8 @@ int neus_sample_rays(NeusTestbed* tb, void* stream, uint32_t n_rays, uint32_t ra
 		HIP_CHECK(hipMemcpyAsync(sst.p, &h, sizeof(h), hipMemcpyHostToDevice, s));
 		Dev<float> st_t; st_t.alloc(n_rays); Dev<uint32_t> nr, bs, nrec, q; nr.alloc(n_rays); bs.alloc(n_rays); nrec.alloc(n_rays); q.alloc(2);
 		Dev<uint2> rec; rec.alloc((size_t)n_rays * NERF_STEPS);
-		const MarchWork mw{rec.p, nrec.p, q.p, tb->mwork.waves};
+		Dev<uint2> seg; seg.alloc((size_t)n_rays * MARCH_SEG_RECS);
+		const MarchWork mw{rec.p, nrec.p, q.p, tb->mwork.waves, seg.p, tb->mwork.lanes_per_ray};
 		Dev<uint8_t> tmp; const size_t tb_ = scan_temp_bytes(n_rays); tmp.alloc(tb_ + 256);
 		Dev<uint32_t> lin; lin.alloc(LIN_WORDS);
 		launch_bitfield_linear(s, bitfield, lin.p);

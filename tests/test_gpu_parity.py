@@ -630,3 +630,47 @@ def test_marching_cubes_64bit_grid_index(torch_cuda):
     # one vertex per crossing edge: about 1.5 x area / h^2 for a sphere (x, y, z edge crossings ~ |n_x|+|n_y|+|n_z|)
     expect = 4 * np.pi * rad * rad / (h * h) * 1.5
     assert 0.9 * expect < nv.value < 1.1 * expect, (nv.value, expect)
+
+
+def test_multilane_march_equals_single_lane(env):
+    """The 4-lanes-per-ray segmented march (march.hip k_march<.., 4>: lanes start at slices of the ray's step
+    sequence, join the previous segment's exit, re-march when they missed it) against the one-lane march, bit for bit
+    (rays, numsteps, coordinates, counters), on random occupancy grids from sparse to full (many empty-cell skips
+    landing across segment starts, long sample runs, the NERF_STEPS cap on the full grid) and on the training bitfield."""
+    t = env["t"]
+    lib, check = L()
+    from neus2_amd import pyngp
+    sc = env["sc"]
+    tbs = {}
+    for lanes in ("1", "4"):
+        os.environ["NEUS_MARCH_LANES"] = lanes
+        tb = pyngp.Testbed(pyngp.TestbedMode.Nerf)
+        tb.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
+        tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=BATCH)
+        tbs[lanes] = tb
+    os.environ.pop("NEUS_MARCH_LANES", None)
+    rng = np.random.default_rng(17)
+    n_rays, max_s = 8192, 8192 * 64
+    bfs = [_bitfield(env)]
+    for p in (0.03, 0.3, 0.8, 1.0):
+        bf = np.zeros(128 ** 3 // 8 * 8, np.uint8)
+        bf[: 128 ** 3 // 8] = np.packbits(rng.random(128 ** 3) < p, bitorder="little")
+        bfs.append(bf)
+    for k, bf in enumerate(bfs):
+        out = {}
+        for lanes, tb in tbs.items():
+            rays = t.zeros((n_rays, 6), dtype=t.float32, device="cuda")
+            ns = t.zeros((n_rays, 2), dtype=t.int32, device="cuda")
+            co = t.zeros((max_s, 7), dtype=t.float32, device="cuda")
+            cnt = (C.c_uint32 * 3)()
+            check(lib.neus_sample_rays(tb.handle, None, C.c_uint32(n_rays), C.c_uint32(0), C.c_uint32(1), C.c_uint32(0),
+                                       C.c_uint64(0x243F6A8885A308D3 + k), C.c_uint64(0x13198A2E03707345 | 1), C.c_uint32(max_s), ptr(dev(t, bf)),
+                                       ptr(rays), ptr(ns), ptr(co), cnt))
+            out[lanes] = (host(rays, np.uint32).copy(), host(ns, np.uint32).copy(), host(co, np.uint32).copy(), tuple(cnt))
+        a, b = out["1"], out["4"]
+        assert a[3] == b[3], (k, a[3], b[3])
+        np.testing.assert_array_equal(a[0], b[0])
+        np.testing.assert_array_equal(a[1], b[1])
+        nk = int(a[3][1])
+        np.testing.assert_array_equal(a[2][:nk], b[2][:nk])
+        record("march_lanes", case=k, samples=nk, per_ray=nk / n_rays)
