@@ -170,7 +170,7 @@ constexpr uint32_t MARCH_RUN_MAX = 16;
 constexpr uint32_t MARCH_SEG_RECS = NERF_STEPS + 64;
 struct MarchWork {
 	uint2* rec; uint32_t* nrec; uint32_t* counter /* 2: the two passes' ray queues */; uint32_t waves; /* 0 = one lane per ray */
-	uint2* seg; uint32_t lanes_per_ray;  /* 1 or 4 */
+	uint2* seg; uint32_t lanes_per_ray;  /* 1, 4 or 8 */
 };
 // Ray generation + the occupancy march: rays (6 f32 per slot), tstart (1 per slot), nreq (requested
 // samples per slot) and the sample runs (MarchWork).

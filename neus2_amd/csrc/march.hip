@@ -245,7 +245,7 @@ __device__ __forceinline__ void march_segment(const DevDataset& ds, const uint8_
 // value at or above max_samples, which is all the reference ever uses of it (min(counter, max_samples),
 // testbed_nerf.cu:3036-3039; the rest is the GUI's text).
 //
-// Each ray is marched by MG lanes at once. The march's t values are the sequence t0, t0 + dt, ... (every update of
+// Each ray is marched by MG lanes at once (8 by default). The march's t values are the sequence t0, t0 + dt, ... (every update of
 // the reference's loop is one t += dt, the skip included), so lane g starts at the first step k_g of the g-th slice
 // of [t0, t_exit) by stepping there, and marches its segment [k_g, k_{g+1}) as if k_g were visited. The true march
 // enters segment g at v_g, the exit of segment g - 1; the march is a deterministic function of its visited step, so
@@ -856,9 +856,11 @@ void launch_march_count(hipStream_t s, uint32_t cap, uint32_t max_samples, StepS
 	for (uint32_t pass = 0; pass < 2; ++pass) {
 		if (ds.cone_angle == 0.0f) {
 			if (mw.lanes_per_ray == 1) k_march<true, 1><<<blocks, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, lin, rays, tstart, nreq, mw);
+			else if (mw.lanes_per_ray == 8) k_march<true, 8><<<blocks * 8, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, lin, rays, tstart, nreq, mw);
 			else k_march<true, 4><<<blocks * 4, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, lin, rays, tstart, nreq, mw);
 		} else {
 			if (mw.lanes_per_ray == 1) k_march<false, 1><<<blocks, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, nullptr, rays, tstart, nreq, mw);
+			else if (mw.lanes_per_ray == 8) k_march<false, 8><<<blocks * 8, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, nullptr, rays, tstart, nreq, mw);
 			else k_march<false, 4><<<blocks * 4, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, nullptr, rays, tstart, nreq, mw);
 		}
 	}

@@ -633,7 +633,7 @@ def test_marching_cubes_64bit_grid_index(torch_cuda):
 
 
 def test_multilane_march_equals_single_lane(env):
-    """The 4-lanes-per-ray segmented march (march.hip k_march<.., 4>: lanes start at slices of the ray's step
+    """The 4- and 8-lanes-per-ray segmented march (march.hip k_march<.., MG>: lanes start at slices of the ray's step
     sequence, join the previous segment's exit, re-march when they missed it) against the one-lane march, bit for bit
     (rays, numsteps, coordinates, counters), on random occupancy grids from sparse to full (many empty-cell skips
     landing across segment starts, long sample runs, the NERF_STEPS cap on the full grid) and on the training bitfield."""
@@ -642,7 +642,7 @@ def test_multilane_march_equals_single_lane(env):
     from neus2_amd import pyngp
     sc = env["sc"]
     tbs = {}
-    for lanes in ("1", "4"):
+    for lanes in ("1", "4", "8"):
         os.environ["NEUS_MARCH_LANES"] = lanes
         tb = pyngp.Testbed(pyngp.TestbedMode.Nerf)
         tb.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
@@ -667,10 +667,12 @@ def test_multilane_march_equals_single_lane(env):
                                        C.c_uint64(0x243F6A8885A308D3 + k), C.c_uint64(0x13198A2E03707345 | 1), C.c_uint32(max_s), ptr(dev(t, bf)),
                                        ptr(rays), ptr(ns), ptr(co), cnt))
             out[lanes] = (host(rays, np.uint32).copy(), host(ns, np.uint32).copy(), host(co, np.uint32).copy(), tuple(cnt))
-        a, b = out["1"], out["4"]
-        assert a[3] == b[3], (k, a[3], b[3])
-        np.testing.assert_array_equal(a[0], b[0])
-        np.testing.assert_array_equal(a[1], b[1])
+        a = out["1"]
         nk = int(a[3][1])
-        np.testing.assert_array_equal(a[2][:nk], b[2][:nk])
+        for lanes in ("4", "8"):
+            b = out[lanes]
+            assert a[3] == b[3], (k, lanes, a[3], b[3])
+            np.testing.assert_array_equal(a[0], b[0])
+            np.testing.assert_array_equal(a[1], b[1])
+            np.testing.assert_array_equal(a[2][:nk], b[2][:nk])
         record("march_lanes", case=k, samples=nk, per_ray=nk / n_rays)
