@@ -203,6 +203,36 @@ int neus_testbed_get_movement(NeusTestbed* tb, float* global12, float* local12);
 int neus_testbed_set_movement(NeusTestbed* tb, const float* global12, const float* local12);
 /* frame_state (4 u32): current frame, canonical training step, train_canonical, train_delta. */
 int neus_testbed_frame_state(NeusTestbed* tb, uint32_t* out4);
+/* Testbed::change_to_frame (testbed.cu:1939-1985; python_api.cu:437): frame index := frame, that frame's images and
+ * cameras (load_nerf(frame)), training step 0 and a fresh optimizer (Adam moments / steps / EMA state); the
+ * parameters, the accumulated movement and the phase flags stay (run_dynamic.py then calls load_snapshot). */
+int neus_testbed_change_frame(NeusTestbed* tb, uint32_t frame, uint32_t n_images, const NeusImage* images);
+/* Testbed::prepare_for_test (testbed.cu:1987-1999; python_api.cu:438): render, SDF grid and mesh colours go through
+ * the DeltaNetwork (m_use_delta) iff current frame != 0 and train_delta. Each training step sets the same flag
+ * (testbed.cu:2704-2710). out_use_delta (nullable) receives it. */
+int neus_testbed_prepare_for_test(NeusTestbed* tb, int* out_use_delta);
+/* Testbed::save_transform's values (testbed.cu:3118-3141, save_global_movement_rotation_6d_kernel,
+ * common_operation.cuh:588-623): the current frame's DeltaNetwork movement composed with the accumulated one,
+ * R = R_local R_acc (row-major 9) and t = R_local (t_acc + t_local) (3), rounded to fp16 (precision_t). */
+int neus_testbed_saved_transform(NeusTestbed* tb, float* out12);
+
+/* Loss-target and sampling options (testbed.h Nerf::Training; python_api.cu:530-560):
+ *   random_bg_color      nerf.training.random_bg_color (1, the default: a random background per ray)
+ *   background_color     testbed.background_color rgb (sRGB) - the fixed training background otherwise
+ *   color_space          testbed.color_space: 0 Linear (default), 1 SRGB (testbed_nerf.cu:1657-1671)
+ *   linear_colors        nerf.training.linear_colors: targets and rendering stay linear
+ *   cone_angle_constant  nerf.cone_angle_constant (load_nerf sets 0 for aabb_scale 1, else 1/256)
+ *   near_distance        nerf.training.near_distance (stored; the NeuS sampler does not read it) */
+typedef struct NeusTrainingOptions {
+	int32_t random_bg_color;
+	float background_color[3];
+	int32_t color_space;
+	int32_t linear_colors;
+	float cone_angle_constant;
+	float near_distance;
+} NeusTrainingOptions;
+int neus_testbed_get_training_options(NeusTestbed* tb, NeusTrainingOptions* out);
+int neus_testbed_set_training_options(NeusTestbed* tb, const NeusTrainingOptions* opts);
 /* Per-ray counters of the last step (first n rays, host buffers, each nullable): samples requested by
  * the march, samples composited before transmittance < 1e-4, and numsteps = (compacted count, base). */
 int neus_testbed_ray_counts(NeusTestbed* tb, uint32_t n, uint32_t* nreq, uint32_t* ccount, uint32_t* numsteps /* 2n */);

@@ -71,6 +71,13 @@ class NeusRenderRequest(C.Structure):
     ]
 
 
+class NeusTrainingOptions(C.Structure):
+    _fields_ = [
+        ("random_bg_color", C.c_int32), ("background_color", C.c_float * 3), ("color_space", C.c_int32),
+        ("linear_colors", C.c_int32), ("cone_angle_constant", C.c_float), ("near_distance", C.c_float),
+    ]
+
+
 # Every symbol declared in include/neus2_hip.h (checked by tests/test_capi.py).
 EXPORTS = [
     "neus_last_error", "neus_device_count", "neus_device_synchronize",
@@ -86,6 +93,8 @@ EXPORTS = [
     "neus_grid_encode", "neus_net_forward", "neus_net_backward", "neus_sample_rays", "neus_loss_compact",
     "neus_optimizer_step", "neus_fill_rollover", "neus_occ_update", "neus_mfma_probe",
     "neus_testbed_next_frame", "neus_testbed_get_movement", "neus_testbed_set_movement", "neus_testbed_frame_state",
+    "neus_testbed_change_frame", "neus_testbed_prepare_for_test", "neus_testbed_get_training_options",
+    "neus_testbed_set_training_options", "neus_testbed_saved_transform",
     "neus_net_backward_pos", "neus_delta_apply", "neus_delta_backward",
 ]
 

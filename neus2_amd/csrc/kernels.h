@@ -43,6 +43,9 @@ struct DeltaState {
 struct DeltaAdam { float lr, beta1, beta2, eps, loss_scale; uint32_t optimize; };
 // Accumulated global movement applied to every ray (global_movement_with_rotation_6d, testbed_nerf.cu:193-213).
 struct RayMotion { float R[9]; float t[3]; uint32_t on; };
+// Loss-target options; all-zero = the reference drivers' defaults (random background, colour space Linear,
+// linear_colors off: sRGB targets). mode: 0 Linear colour space, 1 SRGB colour space, 2 train in linear colours.
+struct TrainTarget { uint32_t fixed_bg; float bg[3]; uint32_t mode; };
 
 struct WGradJob { const half_t* D; const half_t* X; float* dW; uint32_t M, K, ncols, ldc; uint32_t tiles_m, tiles_k; };
 // Weight gradients without atomics: every (job, 32x32 tile, sample split) block writes its partial tile to
@@ -64,6 +67,7 @@ struct DevDataset {
 	float aabb_min[3], aabb_max[3];
 	float cone_angle;
 	RayMotion motion;         // frames >= 1 of a dynamic scene: o' = R o + t, d' = R d (normalized d)
+	TrainTarget target;       // background / colour space of the loss targets (testbed_nerf.cu:1642-1671)
 };
 
 struct DPInfo { uint32_t rank, world; };
@@ -153,7 +157,7 @@ void launch_occ_density(hipStream_t s, uint32_t L, uint32_t W, uint32_t n, const
 // raw SDF on a uniform grid (marching cubes input), grid points offset .. offset + n - 1 (x fastest)
 void launch_sdf_grid(hipStream_t s, uint32_t L, uint32_t W, const uint32_t res[3], const float render_min[3], const float render_max[3],
                      const float train_min[3], const float train_max[3], uint64_t offset, uint32_t n, const GridLevels& gl, uint32_t valid_level,
-                     const half_t* grid, const MlpPtrs& w, float* sdf);
+                     const half_t* grid, const MlpPtrs& w, float* sdf, const DeltaState* delta = nullptr);
 void launch_mlp_train(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_valid_ptr, uint32_t n, uint32_t ld, const float* coords,
                       const half_t* enc, const float* dydx, const half_t* dL_dout, const MlpPtrs& w, const TrainBufs& tb);
 void launch_wgrad(hipStream_t s, const WGradJobs& jobs, uint32_t n_blocks);
@@ -200,7 +204,7 @@ void launch_render_compact(hipStream_t s, uint32_t n, const void* src, uint32_t*
 void launch_render_gen(hipStream_t s, uint32_t n_alive, uint32_t n_steps, const DevDataset& ds, const uint8_t* bf, const uint32_t* lin, void* rays,
                        float* coords);
 void launch_render_composite(hipStream_t s, uint32_t n_alive, uint32_t n_steps, const float* coords, const half_t* net_out, float cos_anneal,
-                             float min_transmittance, void* rays, float4* frame);
+                             float min_transmittance, bool linear_colors, void* rays, float4* frame);
 void launch_render_accumulate(hipStream_t s, uint32_t n, uint32_t spp, const float4* frame, float4* accum);
 // mc.hip (marching cubes over a density grid; chunked, deterministic)
 uint32_t mc_n_chunks(const uint32_t res[3]);

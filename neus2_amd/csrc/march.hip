@@ -656,16 +656,22 @@ __global__ void __launch_bounds__(256) k_loss_ray(uint32_t cap_rays, StepState* 
 		const int rx = ds.res[2 * img], ry = ds.res[2 * img + 1];
 		float xx, yy; random_image_pos(rng, rx, ry, xx, yy);
 		float bg[3];
-		bg[0] = rng.next_float(); bg[1] = rng.next_float(); bg[2] = rng.next_float();
+		if (ds.target.fixed_bg) { bg[0] = ds.target.bg[0]; bg[1] = ds.target.bg[1]; bg[2] = ds.target.bg[2]; }
+		else { bg[0] = rng.next_float(); bg[1] = rng.next_float(); bg[2] = rng.next_float(); }
 #pragma unroll
 		for (int k = 0; k < 3; ++k) bg[k] = srgb_to_linear(bg[k]);
 		float tex[4]; read_rgba(ds, img, xx, yy, tex);
 		float target[3];
+		const uint32_t tmode = ds.target.mode;
 #pragma unroll
 		for (int k = 0; k < 3; ++k) {
-			target[k] = 1.0f * tex[k] + (1.0f - tex[3]) * bg[k];
-			target[k] = linear_to_srgb(target[k]);
-			bg[k] = linear_to_srgb(bg[k]);
+			if (tmode != 1) {  // Linear colour space (sRGB targets unless linear_colors) (:1658-1663)
+				target[k] = 1.0f * tex[k] + (1.0f - tex[3]) * bg[k];
+				if (tmode == 0) { target[k] = linear_to_srgb(target[k]); bg[k] = linear_to_srgb(bg[k]); }
+			} else {           // SRGB colour space (:1664-1670)
+				bg[k] = linear_to_srgb(bg[k]);
+				target[k] = tex[3] > 0.0f ? linear_to_srgb(1.0f * tex[k] / tex[3]) * tex[3] + (1.0f - tex[3]) * bg[k] : bg[k];
+			}
 		}
 		if (cn == ns) {
 #pragma unroll

@@ -653,7 +653,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))
 //         in-kernel (grid_sample: the uniform call for g < n_u, the occupancy-biased call after it), its density
 //         splatted into os.grid_tmp with the reference's atomicMax on the float bits (splat_grid_samples_nerf_max_
 //         nearest_neighbor) - no position, cell index or density buffer.
-struct UniformGrid { uint32_t res[3]; float inv_res[3], rmin[3], rdiag[3], tmin[3], tdiag[3]; uint64_t offset; };
+//         With ug.delta (m_use_delta after prepare_for_test, nerf_network.h:664-676) the point goes through the
+//         DeltaNetwork first: x' = R (x + t), as k_delta_apply.
+struct UniformGrid { uint32_t res[3]; float inv_res[3], rmin[3], rdiag[3], tmin[3], tdiag[3]; uint64_t offset; const DeltaState* delta; };
 
 template <int L, int W, int MODE>
 __global__ void __launch_bounds__(256) k_nerf_density(uint32_t n, const float* __restrict__ pos, const UniformGrid ug, const OccSampling os,
@@ -694,6 +696,13 @@ __global__ void __launch_bounds__(256) k_nerf_density(uint32_t n, const float* _
 			for (int k = 0; k < 3; ++k) {
 				const float pk = __builtin_fmaf(__fmul_rn((float)gi[k], ug.inv_res[k]), ug.rdiag[k], ug.rmin[k]);
 				x[k] = __fdiv_rn(__fsub_rn(pk, ug.tmin[k]), ug.tdiag[k]);
+			}
+			if (ug.delta) {
+				const float* R = ug.delta->R;
+				const float p[3] = {__fadd_rn(x[0], ug.delta->t[0]), __fadd_rn(x[1], ug.delta->t[1]), __fadd_rn(x[2], ug.delta->t[2])};
+#pragma unroll
+				for (int k = 0; k < 3; ++k)
+					x[k] = __fadd_rn(__fadd_rn(__fmul_rn(R[3 * k], p[0]), __fmul_rn(R[3 * k + 1], p[1])), __fmul_rn(R[3 * k + 2], p[2]));
 			}
 		}
 		h2 ev[M0];
@@ -1250,9 +1259,10 @@ void launch_occ_density(hipStream_t s, uint32_t L, uint32_t W, uint32_t n, const
 }
 void launch_sdf_grid(hipStream_t s, uint32_t L, uint32_t W, const uint32_t res[3], const float render_min[3], const float render_max[3],
                      const float train_min[3], const float train_max[3], uint64_t offset, uint32_t n, const GridLevels& gl, uint32_t valid_level,
-                     const half_t* grid, const MlpPtrs& w, float* sdf) {
+                     const half_t* grid, const MlpPtrs& w, float* sdf, const DeltaState* delta) {
 	if (n == 0) return;
 	UniformGrid ug{};
+	ug.delta = delta;
 	for (int k = 0; k < 3; ++k) {
 		ug.res[k] = res[k]; ug.inv_res[k] = 1.f / (float)res[k];
 		ug.rmin[k] = render_min[k]; ug.rdiag[k] = render_max[k] - render_min[k];

@@ -145,7 +145,7 @@ __global__ void __launch_bounds__(256) k_render_gen(uint32_t n_alive, uint32_t n
 // composite_kernel_nerf (Shade mode, no glow, show_accel < 0) + shade_kernel_nerf for rays that die here
 __global__ void __launch_bounds__(256) k_render_composite(uint32_t n_alive, uint32_t n_steps, const float* __restrict__ coords,
                                                           const half_t* __restrict__ net_out, float cos_anneal, float min_transmittance,
-                                                          RenderRay* __restrict__ rays, float4* __restrict__ frame) {
+                                                          uint32_t linear_colors, RenderRay* __restrict__ rays, float4* __restrict__ frame) {
 	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
 	if (i >= n_alive) return;
 	RenderRay& r = rays[i];
@@ -175,8 +175,10 @@ __global__ void __launch_bounds__(256) k_render_composite(uint32_t n_alive, uint
 	if (j < n_steps) {
 		r.alive = 0;
 		// compact_kernel_nerf keeps dead rays with alpha > 0.001 for shading; the frame starts cleared,
-		// so shade_kernel_nerf's `tmp + frame * (1 - tmp.w)` is tmp (sRGB network colour -> linear)
-		if (c.w > 0.001f) frame[r.idx] = make_float4(srgb_to_linear(c.x), srgb_to_linear(c.y), srgb_to_linear(c.z), c.w);
+		// so shade_kernel_nerf's `tmp + frame * (1 - tmp.w)` is tmp (sRGB network colour -> linear unless the
+		// network was trained in linear colours)
+		if (c.w > 0.001f)
+			frame[r.idx] = linear_colors ? c : make_float4(srgb_to_linear(c.x), srgb_to_linear(c.y), srgb_to_linear(c.z), c.w);
 	}
 }
 
@@ -211,8 +213,10 @@ void launch_render_gen(hipStream_t s, uint32_t n_alive, uint32_t n_steps, const 
 	if (n_alive) k_render_gen<<<nb(n_alive), 256, 0, s>>>(n_alive, n_steps, ds, bf, lin, (RenderRay*)rays, coords);
 }
 void launch_render_composite(hipStream_t s, uint32_t n_alive, uint32_t n_steps, const float* coords, const half_t* net_out, float cos_anneal,
-                             float min_transmittance, void* rays, float4* frame) {
-	if (n_alive) k_render_composite<<<nb(n_alive), 256, 0, s>>>(n_alive, n_steps, coords, net_out, cos_anneal, min_transmittance, (RenderRay*)rays, frame);
+                             float min_transmittance, bool linear_colors, void* rays, float4* frame) {
+	if (n_alive)
+		k_render_composite<<<nb(n_alive), 256, 0, s>>>(n_alive, n_steps, coords, net_out, cos_anneal, min_transmittance, linear_colors ? 1u : 0u,
+		                                                 (RenderRay*)rays, frame);
 }
 void launch_render_accumulate(hipStream_t s, uint32_t n, uint32_t spp, const float4* frame, float4* accum) {
 	if (n) k_render_accumulate<<<nb(n), 256, 0, s>>>(n, (float)spp, frame, accum);

@@ -164,7 +164,7 @@ struct NeusTestbed {
 	// renderer workspace (NerfTracer, testbed_nerf.cu:2397-2630)
 	Dev<uint8_t> r_rays[2], r_scan_tmp;
 	Dev<uint32_t> r_flags, r_base, r_alive;
-	Dev<float> r_coords;
+	Dev<float> r_coords, r_coords_def;
 	Dev<half_t> r_out;
 	Dev<float4> r_frame, r_accum;
 	size_t r_scan_bytes = 0;
@@ -178,6 +178,9 @@ struct NeusTestbed {
 	// deformed copies of the sample coordinates, dL/d(position) of the training batch
 	uint32_t cur_frame = 0, canonical_step = 0, delta_step = 0;
 	bool train_canonical = true, train_delta = false;
+	bool render_delta = false;     // prepare_for_test (testbed.cu:1987-1999): render / mesh through the DeltaNetwork
+	float near_distance = 0.f;     // nerf.training.near_distance: stored; the NeuS sampler does not read it (testbed_nerf.cu:1525)
+	int32_t color_space_when_linear = 0;  // color_space as set while linear_colors overrides it
 	float delta_lr_factor = 1.f;
 	Dev<DeltaState> delta;
 	Dev<float> delta_partial, coords_def, coords_cdef;
@@ -457,7 +460,9 @@ struct NeusTestbed {
 		reset_delta();
 		ds.motion = RayMotion{};
 		ds.motion.R[0] = ds.motion.R[4] = ds.motion.R[8] = 1.f;
-		cur_frame = 0; canonical_step = 0; train_canonical = true; train_delta = false;
+		// the frame index and the phase flags belong to the Testbed, not the network: reset_network keeps them
+		// (testbed.cu:2084-2349; load_snapshot on frame k of run_dynamic.py's test pass relies on it)
+		canonical_step = 0;
 		HIP_CHECK(hipStreamSynchronize(stream));
 		have_net = true;
 	}
@@ -511,6 +516,24 @@ struct NeusTestbed {
 		reset_delta();
 		train_canonical = false;
 		train_delta = cfg.predict_global_movement != 0;
+		HIP_CHECK(hipStreamSynchronize(stream));
+	}
+	// Testbed::change_to_frame (testbed.cu:1939-1985): load frame `k`'s images and restart the step count with a
+	// fresh optimizer (Adam moments, steps, EMA state); parameters, density grid state of the network, the ray
+	// movement and the training phase flags stay (run_dynamic.py follows it with load_snapshot).
+	void change_frame(uint32_t k, uint32_t n_images, const NeusImage* imgs) {
+		if (!have_net) throw std::runtime_error("change_to_frame: no network");
+		HIP_CHECK(hipStreamSynchronize(stream));
+		consume_loss();
+		const RayMotion m = ds.motion;
+		set_dataset(n_images, imgs, aabb_scale);
+		ds.motion = m;
+		cur_frame = k;
+		training_step = 0; canonical_step = 0;
+		const uint32_t P = lay.P;
+		HIP_CHECK(hipMemset(m1.p, 0, (size_t)P * 4)); HIP_CHECK(hipMemset(m2.p, 0, (size_t)P * 4));
+		HIP_CHECK(hipMemset(adam_steps.p, 0, (size_t)P * 4)); HIP_CHECK(hipMemset(ema_tmp.p, 0, (size_t)P * 4));
+		adam_step = 0; lr_factor = 1.f;
 		HIP_CHECK(hipStreamSynchronize(stream));
 	}
 	// march waves launched (NEUS_MARCH_WAVES overrides). Default 0 = one lane per ray slot: the march is
@@ -739,6 +762,9 @@ struct NeusTestbed {
 		if (rq.use_ema) prepare_weights_for(mlp_ema);
 		const uint32_t valid = valid_level_at((int)training_step);
 		const uint32_t spp = std::max(1u, rq.spp);
+		// m_use_delta (prepare_for_test): the network sees the sample positions through the DeltaNetwork
+		const bool use_delta = render_delta && cur_frame >= 1;
+		if (use_delta) { r_coords_def.alloc((size_t)n * MAX_STEPS_INBETWEEN_COMPACTION * COORD_W); launch_delta_prepare(s, delta.p); }
 		uint32_t iters = 0;
 		for (uint32_t sp = 0; sp < spp; ++sp) {
 			const uint32_t offs_index = rq.snap_to_pixel_centers ? 0 : sp;
@@ -756,9 +782,12 @@ struct NeusTestbed {
 				const uint32_t n_steps = std::min(MAX_STEPS_INBETWEEN_COMPACTION, std::max(1u, n / n_alive));
 				launch_render_gen(s, n_alive, n_steps, ds, bitfield.p, bf_lin.p, r_rays[cur].p, r_coords.p);
 				const uint32_t n_el = n_alive * n_steps;
-				launch_nerf_infer(s, lay.L, lay.W, nullptr, n_el, r_coords.p, gl, valid, grid, w, r_out.p,
+				const float* c_in = r_coords.p;
+				if (use_delta) { launch_delta_apply(s, nullptr, n_el, COORD_W, r_coords.p, r_coords_def.p, delta.p); c_in = r_coords_def.p; }
+				launch_nerf_infer(s, lay.L, lay.W, nullptr, n_el, c_in, gl, valid, grid, w, r_out.p,
 				                  std::max<uint32_t>(1, std::min<uint32_t>((n_el + 127) / 128, 8192)));
-				launch_render_composite(s, n_alive, n_steps, r_coords.p, r_out.p, cos_anneal(), rq.min_transmittance, r_rays[cur].p, r_frame.p);
+				launch_render_composite(s, n_alive, n_steps, r_coords.p, r_out.p, cos_anneal(), rq.min_transmittance, ds.target.mode == 2,
+				                        r_rays[cur].p, r_frame.p);
 				i += n_steps;
 				++iters;
 			}
@@ -776,10 +805,12 @@ struct NeusTestbed {
 		prepare_weights_for(mlp_ema);
 		const uint64_t n = (uint64_t)res[0] * res[1] * res[2];
 		const uint32_t valid = valid_level_at((int)training_step);
+		const bool use_delta = render_delta && cur_frame >= 1;
+		if (use_delta) launch_delta_prepare(stream, delta.p);
 		for (uint64_t off = 0; off < n; off += (1ull << 30)) {
 			const uint32_t cnt = (uint32_t)std::min<uint64_t>(n - off, 1ull << 30);
 			launch_sdf_grid(stream, lay.L, lay.W, res, amin, amax, ds.aabb_min, ds.aabb_max, off, cnt, gl, valid, ema_h.p + lay.grid_off, mlp_ema,
-			                dst + off);
+			                dst + off, use_delta ? delta.p : nullptr);
 		}
 	}
 	// Testbed::marching_cubes: SDF grid (unless a device density grid is given), then the deterministic
@@ -833,6 +864,10 @@ struct NeusTestbed {
 		Dev<float> c; Dev<half_t> o;
 		c.alloc((size_t)mesh_nv * COORD_W); o.alloc((size_t)mesh_nv * OUT_W);
 		launch_mesh_coords(stream, mesh_nv, mesh_v.p, ds, c.p);
+		if (render_delta && cur_frame >= 1) {  // m_use_delta: the vertices go through the DeltaNetwork too
+			launch_delta_prepare(stream, delta.p);
+			launch_delta_apply(stream, nullptr, mesh_nv, COORD_W, c.p, c.p, delta.p);
+		}
 		launch_nerf_infer(stream, lay.L, lay.W, nullptr, mesh_nv, c.p, gl, valid_level_at((int)training_step), ema_h.p + lay.grid_off, mlp_ema, o.p,
 		                  std::max<uint32_t>(1, std::min<uint32_t>((mesh_nv + 127) / 128, 8192)));
 		std::vector<half_t> h((size_t)mesh_nv * OUT_W);
@@ -858,6 +893,7 @@ struct NeusTestbed {
 			}
 		}
 		const bool use_delta = dyn && train_delta;
+		render_delta = use_delta;  // m_nerf_network->m_use_delta follows the training step (testbed.cu:2704-2710)
 		const uint32_t valid = valid_level_at(dyn ? (int)training_step - (int)gm_steps() : (int)training_step);
 		if (use_delta) launch_delta_prepare(s, delta.p);
 		const uint32_t n_prep = std::min(16u, std::max(1u, canonical_step / 16u));
@@ -1186,6 +1222,61 @@ int neus_testbed_next_frame(NeusTestbed* tb, uint32_t n_images, const NeusImage*
 	return guard([&] {
 		HIP_CHECK(hipSetDevice(tb->device));
 		tb->next_frame(n_images, images);
+	});
+}
+int neus_testbed_change_frame(NeusTestbed* tb, uint32_t frame, uint32_t n_images, const NeusImage* images) {
+	return guard([&] {
+		HIP_CHECK(hipSetDevice(tb->device));
+		tb->change_frame(frame, n_images, images);
+	});
+}
+int neus_testbed_prepare_for_test(NeusTestbed* tb, int* out_use_delta) {
+	return guard([&] {
+		tb->render_delta = tb->cur_frame != 0 && tb->train_delta;
+		if (out_use_delta) *out_use_delta = tb->render_delta ? 1 : 0;
+	});
+}
+int neus_testbed_saved_transform(NeusTestbed* tb, float* out12) {
+	return guard([&] {
+		if (!out12) throw std::runtime_error("saved_transform: null output");
+		if (!tb->have_net) throw std::runtime_error("save_transform: no network");
+		HIP_CHECK(hipStreamSynchronize(tb->stream));
+		DeltaState h{};
+		HIP_CHECK(hipMemcpy(&h, tb->delta.p, sizeof(h), hipMemcpyDeviceToHost));
+		float R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, t[3] = {0, 0, 0};
+		if (tb->ds.motion.on) { std::memcpy(R, tb->ds.motion.R, sizeof(R)); std::memcpy(t, tb->ds.motion.t, sizeof(t)); }
+		host_accumulate_movement(h.p, R, t);
+		std::memcpy(out12, R, sizeof(R)); std::memcpy(out12 + 9, t, sizeof(t));
+	});
+}
+int neus_testbed_get_training_options(NeusTestbed* tb, NeusTrainingOptions* o) {
+	return guard([&] {
+		if (!o) throw std::runtime_error("get_training_options: null output");
+		const TrainTarget& t = tb->ds.target;
+		o->random_bg_color = t.fixed_bg ? 0 : 1;
+		for (int k = 0; k < 3; ++k) o->background_color[k] = t.bg[k];
+		o->color_space = t.mode == 1 ? 1 : 0;
+		o->linear_colors = t.mode == 2 ? 1 : 0;
+		if (t.mode == 2) o->color_space = tb->color_space_when_linear;
+		o->cone_angle_constant = tb->ds.cone_angle;
+		o->near_distance = tb->near_distance;
+	});
+}
+int neus_testbed_set_training_options(NeusTestbed* tb, const NeusTrainingOptions* o) {
+	return guard([&] {
+		if (!o) throw std::runtime_error("set_training_options: null options");
+		if (o->color_space != 0 && o->color_space != 1) throw std::runtime_error("color_space must be 0 (Linear) or 1 (SRGB)");
+		if (!(o->cone_angle_constant >= 0.0f)) throw std::runtime_error("cone_angle_constant must be >= 0");
+		HIP_CHECK(hipStreamSynchronize(tb->stream));  // kernels in flight read ds by value; later steps see the new targets
+		TrainTarget t{};
+		t.fixed_bg = o->random_bg_color ? 0u : 1u;
+		for (int k = 0; k < 3; ++k) t.bg[k] = o->background_color[k];
+		// train_in_linear_colors wins over the colour space (testbed_nerf.cu:1658)
+		t.mode = o->linear_colors ? 2u : (o->color_space == 1 ? 1u : 0u);
+		tb->color_space_when_linear = o->color_space;
+		tb->ds.target = t;
+		tb->ds.cone_angle = o->cone_angle_constant;
+		tb->near_distance = o->near_distance;
 	});
 }
 int neus_testbed_get_movement(NeusTestbed* tb, float* global12, float* local12) {

@@ -34,6 +34,124 @@ class TestbedMode(enum.IntEnum):
     Volume = 3
 
 
+class ColorSpace(enum.IntEnum):
+    """EColorSpace (common.h; python_api.cu:278-281)."""
+    Linear = 0
+    SRGB = 1
+
+
+class TonemapCurve(enum.IntEnum):
+    """ETonemapCurve (common.h; python_api.cu:283-288)."""
+    Identity = 0
+    ACES = 1
+    Hable = 2
+    Reinhard = 3
+
+
+class BoundingBox:
+    """ngp::BoundingBox (bounding_box.cuh; python_api.cu:296-315): min / max corners; the default box is inside-out
+    (empty), which compute_*marching_cubes_mesh read as "use the render aabb"."""
+
+    def __init__(self, min=None, max=None):  # noqa: A002 - the reference's argument names
+        self.min = np.full(3, np.inf, np.float32) if min is None else np.asarray(min, np.float32).reshape(3).copy()
+        self.max = np.full(3, -np.inf, np.float32) if max is None else np.asarray(max, np.float32).reshape(3).copy()
+
+    def is_empty(self):
+        return bool(np.any(self.max < self.min))
+
+    def center(self):
+        return 0.5 * (self.max + self.min)
+
+    def diag(self):
+        return self.max - self.min
+
+    def contains(self, p):
+        p = np.asarray(p, np.float32)
+        return bool(np.all(p >= self.min) and np.all(p <= self.max))
+
+    def inflate(self, amount):
+        self.min -= np.float32(amount)
+        self.max += np.float32(amount)
+
+    def enlarge(self, other):
+        if isinstance(other, BoundingBox):
+            self.min = np.minimum(self.min, other.min)
+            self.max = np.maximum(self.max, other.max)
+        else:
+            p = np.asarray(other, np.float32)
+            self.min = np.minimum(self.min, p)
+            self.max = np.maximum(self.max, p)
+
+    def intersection(self, other):
+        return BoundingBox(np.maximum(self.min, other.min), np.minimum(self.max, other.max))
+
+    def intersects(self, other):
+        return not self.intersection(other).is_empty()
+
+    def get_vertices(self):
+        return np.array([[(self.max if i & 1 else self.min)[0], (self.max if i & 2 else self.min)[1],
+                          (self.max if i & 4 else self.min)[2]] for i in range(8)], np.float32)
+
+    def __repr__(self):
+        return f"BoundingBox(min={self.min.tolist()}, max={self.max.tolist()})"
+
+
+def _aabb_pair(aabb):
+    """None, an empty BoundingBox -> None (the render aabb); a BoundingBox or (min, max) -> float32 corners."""
+    if aabb is None:
+        return None
+    if isinstance(aabb, BoundingBox):
+        return None if aabb.is_empty() else (aabb.min.copy(), aabb.max.copy())
+    return np.asarray(aabb[0], np.float32), np.asarray(aabb[1], np.float32)
+
+
+def tonemap_curve(x, curve):
+    """tonemap(Array3f, ETonemapCurve) (render_buffer.cu:254-312), float32."""
+    x = np.asarray(x, np.float32)
+    curve = TonemapCurve(curve)
+    if curve == TonemapCurve.Identity:
+        return x
+    x = np.maximum(x, np.float32(0))
+    f = np.float32
+    if curve == TonemapCurve.ACES:
+        k0, k1, k2, k3, k4, k5 = f(0.6) * f(0.6) * f(2.51), f(0.6) * f(0.03), f(0), f(0.6) * f(0.6) * f(2.43), f(0.6) * f(0.59), f(0.14)
+    elif curve == TonemapCurve.Hable:
+        A, B, Cc, D, E, F = f(0.15), f(0.50), f(0.10), f(0.20), f(0.02), f(0.30)
+        k0, k1, k2, k3, k4, k5 = A * F - A * E, Cc * B * F - B * E, f(0), A * F, B * F, D * F * F
+        W = f(11.2)
+        white_scale = (k3 * (W * W) + k4 * W + k5) / (k0 * (W * W) + k1 * W + k2)
+        k0, k1, k2, k3, k4 = f(4) * k0 * white_scale, f(2) * k1 * white_scale, k2 * white_scale, f(4) * k3, f(2) * k4
+    else:  # Reinhard
+        Y = x[..., 0:1] * f(0.2126) + x[..., 1:2] * f(0.7152) + x[..., 2:3] * f(0.0722)
+        return (x * (f(1) / (Y + f(1)))).astype(np.float32)
+    sq = x * x
+    return ((sq * k0 + k1 * x + k2) / (k3 * sq + k4 * x + k5)).astype(np.float32)
+
+
+def tonemap_image(rgba, exposure=0.0, background_color=(0.0, 0.0, 0.0, 0.0), color_space=ColorSpace.Linear,
+                  curve=TonemapCurve.Identity, to_srgb=False):
+    """tonemap_kernel (render_buffer.cu:474-500) on the linear accumulation buffer (H x W x 4, float32): the sRGB
+    background composited behind it (converted to linear unless the colour space is SRGB; alpha += weight), then
+    tonemap(col, exposure, curve, color_space, output) (render_buffer.cu:314-334): SRGB colour space -> linear,
+    x 2^exposure, the curve, linear -> sRGB when to_srgb (render(linear=False)). No clamp (no DLSS)."""
+    out = np.array(rgba, np.float32, copy=True)
+    bg = np.asarray(background_color, np.float32).reshape(4).copy()
+    if ColorSpace(color_space) != ColorSpace.SRGB:
+        bg[:3] = srgb_to_linear(bg[:3]).astype(np.float32)
+    weight = (np.float32(1) - out[..., 3:4]) * bg[3]
+    out[..., :3] += bg[:3] * weight
+    out[..., 3:4] += weight
+    col = out[..., :3]
+    if ColorSpace(color_space) == ColorSpace.SRGB:
+        col = srgb_to_linear(col).astype(np.float32)
+    col = col * np.float32(2.0) ** np.float32(exposure)
+    col = tonemap_curve(col, curve)
+    if to_srgb:
+        col = linear_to_srgb(col).astype(np.float32)
+    out[..., :3] = col
+    return out
+
+
 NERF_SCALE = 0.33  # nerf_loader.h:31
 
 
@@ -138,6 +256,20 @@ def nerf_matrix_to_ngp(m, scale, offset, from_na):
     return r
 
 
+def ngp_matrix_to_nerf(m, scale, offset, from_na):
+    """NerfDataset::ngp_matrix_to_nerf (nerf_loader.h:135-155): the inverse of nerf_matrix_to_ngp."""
+    r = np.array(m, np.float32)[:3, :4].copy()
+    if from_na:
+        r[:, 1] *= -1
+        r[:, 2] *= -1
+    else:
+        r = r[[2, 0, 1], :]
+    r[:, 1] *= -1
+    r[:, 2] *= -1
+    r[:, 3] = (r[:, 3] - np.asarray(offset, np.float32)) / np.float32(scale)
+    return r
+
+
 def load_transforms(path):
     """ngp::load_nerf (nerf_loader.cu:197-751) subset: from_na/scale/offset/aabb_scale, per-frame
     intrinsic_matrix or fl_x/fl_y/camera_angle_x, cx/cy; RGBA PNG images (alpha premultiplied on
@@ -197,7 +329,7 @@ def load_transforms(path):
         focal.append(fl)
         principal.append(pp)
     return dict(images=images, focal=np.array(focal, np.float32), principal=np.array(principal, np.float32),
-                xforms=np.stack(xforms).astype(np.float32), aabb_scale=aabb_scale, scale=scale, offset=offset)
+                xforms=np.stack(xforms).astype(np.float32), aabb_scale=aabb_scale, scale=scale, offset=offset, from_na=from_na)
 
 
 def geometric_init_weights(n_levels, width=64, seed=1337, path_hint=True):
@@ -230,9 +362,65 @@ def _images_array(imgs, focal, principal, xforms):
     return arr
 
 
-class _Training:
+def _opt_property(field, conv=float):
+    """A Testbed::Nerf(::Training) member that lives in the device dataset (NeusTrainingOptions)."""
+
+    def get(self):
+        return conv(getattr(self._tb._get_options(), field))
+
+    def put(self, v):
+        o = self._tb._get_options()
+        setattr(o, field, conv(v))
+        self._tb._set_options(o)
+
+    return property(get, put)
+
+
+class _Dataset:
+    """Testbed::Nerf::Training::dataset (NerfDataset, python_api.cu:517-531), read-only view."""
+
     def __init__(self, tb):
         self._tb = tb
+
+    @property
+    def n_images(self):
+        return self._tb._n_images
+
+    @property
+    def scale(self):
+        return float(self._tb._scale)
+
+    @property
+    def offset(self):
+        return np.asarray(self._tb._offset, np.float32).copy()
+
+    @property
+    def aabb_scale(self):
+        return int((self._tb._dataset_meta or {}).get("aabb_scale", 1))
+
+    @property
+    def from_na(self):
+        return bool(self._tb._from_na)
+
+    @property
+    def render_aabb(self):
+        return BoundingBox(*self._tb._aabb)
+
+    @property
+    def transforms(self):
+        return [np.asarray(x, np.float32).reshape(3, 4).copy() for x in (self._tb._dataset_meta or {}).get("xforms", [])]
+
+
+class _Training:
+    """Testbed::Nerf::Training (python_api.cu:533-578), the members the NeuS2 path reads."""
+
+    random_bg_color = _opt_property("random_bg_color", bool)
+    linear_colors = _opt_property("linear_colors", bool)
+    near_distance = _opt_property("near_distance", float)
+
+    def __init__(self, tb):
+        self._tb = tb
+        self.dataset = _Dataset(tb)
 
     @property
     def n_images_for_training(self):
@@ -242,11 +430,33 @@ class _Training:
     def counters_rgb(self):
         return self._tb.stats()
 
+    @property
+    def transforms(self):
+        return self.dataset.transforms
+
+    @property
+    def snap_to_pixel_centers(self):
+        return False
+
+    @snap_to_pixel_centers.setter
+    def snap_to_pixel_centers(self, v):
+        if v:
+            raise NeusError("nerf.training.snap_to_pixel_centers: training rays use random sub-pixel positions on the gfx950 path")
+
 
 class _Nerf:
+    """Testbed::Nerf (python_api.cu:482-493)."""
+
+    cone_angle_constant = _opt_property("cone_angle_constant", float)
+
     def __init__(self, tb):
+        self._tb = tb
         self.training = _Training(tb)
         self.rendering_min_transmittance = 0.01  # testbed.h: Nerf::rendering_min_transmittance
+        # stored for script compatibility; the NeuS path has no camera distortion and no sharpening pass
+        self.sharpen = 0.0
+        self.render_with_camera_distortion = False
+        self.visualize_cameras = False
 
 
 # neus_testbed_kernel_times order (include/neus2_hip.h NEUS_N_PHASES)
@@ -268,12 +478,19 @@ class Testbed:
         self._net_cfg = None
         self._cfg_dict = None
         self.shall_train = True
+        self._dataset_meta = None
+        self._scale, self._offset, self._from_na = 1.0, np.zeros(3, np.float32), False
+        self._aabb = (np.zeros(3, np.float32), np.ones(3, np.float32))
         self.nerf = _Nerf(self)
-        # render state (testbed.h: m_snap_to_pixel_centers, m_background_color, camera)
+        # render state (testbed.h: m_snap_to_pixel_centers, m_background_color, m_exposure, m_color_space, camera)
         self.snap_to_pixel_centers = False
-        self.background_color = [0.0, 0.0, 0.0, 0.0]
-        self._render_view = None
+        self._background_color = np.zeros(4, np.float32)
+        self.exposure = 0.0
+        self._color_space = ColorSpace.Linear
+        self.tonemap_curve = TonemapCurve.Identity
+        self.render_mode = "Shade"
         self.max_training_steps = None
+        self.reset_camera()
 
     def __del__(self):
         try:
@@ -295,7 +512,7 @@ class Testbed:
             files = [path]
         d = load_transforms(files[0])
         self.set_dataset(d["images"], d["focal"], d["principal"], d["xforms"], d["aabb_scale"])
-        self._scale, self._offset = float(d["scale"]), np.asarray(d["offset"], np.float32)
+        self._scale, self._offset, self._from_na = float(d["scale"]), np.asarray(d["offset"], np.float32), bool(d["from_na"])
         self._frames = files  # all_json_paths (testbed_nerf.cu:2967-2994): one transforms file per time frame
 
     def set_dataset_frames(self, frames):
@@ -337,14 +554,54 @@ class Testbed:
         k = self.current_training_time_frame
         if k >= self.all_training_time_frame - 1:
             return False
-        nxt = self._frames[k + 1]
-        d = load_transforms(nxt) if isinstance(nxt, str) else nxt
-        imgs = [np.ascontiguousarray(im, np.uint8) for im in d["images"]]
+        d, imgs = self._frame_data(k + 1)
         arr = _images_array(imgs, d["focal"], d["principal"], d["xforms"])
         check(lib().neus_testbed_next_frame(self._h, C.c_uint32(len(imgs)), arr))
         self._images = imgs
         self._n_images = len(imgs)
+        self._dataset_meta = dict(self._dataset_meta or {}, xforms=list(d["xforms"]), focal=list(d["focal"]), principal=list(d["principal"]))
         return True
+
+    def _frame_data(self, k):
+        f = self._frames[k]
+        d = load_transforms(f) if isinstance(f, str) else f
+        imgs = [np.ascontiguousarray(im, np.uint8) for im in d["images"]]
+        return d, imgs
+
+    def change_to_frame(self, frame_idx: int):
+        """Testbed::change_to_frame (testbed.cu:1939-1985): frame `frame_idx`'s images, training step 0, a fresh
+        optimizer; the network, the movement and the phase flags stay (run_dynamic.py loads a snapshot next)."""
+        k = int(frame_idx)
+        if not 0 <= k < self.all_training_time_frame or not getattr(self, "_frames", None):
+            raise NeusError(f"change_to_frame({k}): the dataset has {self.all_training_time_frame} frame(s)")
+        d, imgs = self._frame_data(k)
+        arr = _images_array(imgs, d["focal"], d["principal"], d["xforms"])
+        check(lib().neus_testbed_change_frame(self._h, C.c_uint32(k), C.c_uint32(len(imgs)), arr))
+        self._images = imgs
+        self._n_images = len(imgs)
+        self._dataset_meta = dict(self._dataset_meta or {}, xforms=list(d["xforms"]), focal=list(d["focal"]), principal=list(d["principal"]))
+
+    def prepare_for_test(self):
+        """Testbed::prepare_for_test (testbed.cu:1987-1999): render / mesh through the DeltaNetwork iff the current
+        frame is not 0 and the movement is being trained. Returns the flag."""
+        u = C.c_int()
+        check(lib().neus_testbed_prepare_for_test(self._h, C.byref(u)))
+        return bool(u.value)
+
+    def saved_transform(self):
+        """(R 3x3, t 3) that save_transform writes: this frame's movement composed with the accumulated one."""
+        o = (C.c_float * 12)()
+        check(lib().neus_testbed_saved_transform(self._h, o))
+        a = np.array(o, np.float32)
+        return a[:9].reshape(3, 3), a[9:]
+
+    def save_transform(self, path: str):
+        """Testbed::save_transform (testbed.cu:3118-3141): three rows of the rotation and the translation, "%f"."""
+        R, t = self.saved_transform()
+        with open(path, "w") as f:
+            for r in R:
+                f.write("%f %f %f\n" % (r[0], r[1], r[2]))
+            f.write("%f %f %f\n\n" % (t[0], t[1], t[2]))
 
     def get_movement(self):
         """(accumulated 3x4 [R | t] of the rays, DeltaNetwork params transition[4] | rotation 6D[8])."""
@@ -372,7 +629,54 @@ class Testbed:
         s = int(aabb_scale)
         infl = 0.5 * min(1 << 7, s)
         self._aabb = (np.full(3, 0.5 - infl, np.float32), np.full(3, 0.5 + infl, np.float32))
-        self._scale, self._offset = 1.0, np.zeros(3, np.float32)
+        self._scale, self._offset, self._from_na = 1.0, np.zeros(3, np.float32), False
+
+    # ------------------------------------------------------------------ options (device dataset)
+    def _get_options(self):
+        o = _lib.NeusTrainingOptions()
+        check(lib().neus_testbed_get_training_options(self._h, C.byref(o)))
+        return o
+
+    def _set_options(self, o):
+        check(lib().neus_testbed_set_training_options(self._h, C.byref(o)))
+
+    @property
+    def background_color(self):
+        """m_background_color (sRGB rgba): composited by render() (tonemap_kernel) and, without
+        nerf.training.random_bg_color, the training background (testbed_nerf.cu:1642-1645)."""
+        return self._background_color.copy()
+
+    @background_color.setter
+    def background_color(self, v):
+        self._background_color = np.asarray(v, np.float32).reshape(4).copy()
+        o = self._get_options()
+        o.background_color[:] = [float(x) for x in self._background_color[:3]]
+        self._set_options(o)
+
+    @property
+    def color_space(self):
+        """m_color_space: the loss targets (testbed_nerf.cu:1657-1671) and render's tonemap input space."""
+        return self._color_space
+
+    @color_space.setter
+    def color_space(self, v):
+        self._color_space = ColorSpace(int(v))
+        o = self._get_options()
+        o.color_space = int(self._color_space)
+        self._set_options(o)
+
+    # ------------------------------------------------------------------ GUI (not part of the training path)
+    def want_repl(self):
+        return False
+
+    def init_window(self, width, height, hidden=False):
+        raise NeusError("init_window: the GLFW/ImGui viewer is not part of the gfx950 training path; use render()")
+
+    def destroy_window(self):
+        pass
+
+    def reset_accumulation(self):
+        pass
 
     # ------------------------------------------------------------------ network
     def reload_network_from_file(self, path: str = "", batch_size=None, fixed_rays_per_batch=0):
@@ -405,6 +709,14 @@ class Testbed:
             raise NeusError("load_snapshot: load the training data first (set_dataset / load_training_data)")
         snapshot.load_snapshot(self, path)
 
+    def n_params(self):
+        """Testbed::n_params: trainable parameters of the NeuS network (MLPs + hash grid + variance)."""
+        return int(self.layout()["n_params"])
+
+    def n_encoding_params(self):
+        """Testbed::n_encoding_params: hash-grid parameters."""
+        return int(self.layout()["n_grid_params"])
+
     def layout(self):
         l = NeusNetLayout()
         check(lib().neus_testbed_layout(self._h, C.byref(l)))
@@ -431,54 +743,134 @@ class Testbed:
         self.train_steps(1)
         return True
 
-    # ------------------------------------------------------------------ rendering
-    def set_camera_to_training_view(self, view: int):
-        """Testbed::set_camera_to_training_view (testbed.cu:264-270): camera, focal length and screen
-        centre of training image `view`."""
-        if not 0 <= int(view) < self._n_images:
-            raise NeusError(f"training view {view} out of range (0..{self._n_images - 1})")
-        self._render_view = int(view)
-
+    # ------------------------------------------------------------------ camera (testbed.cu:238-285, 1830-1844, 2738-2746)
     def reset_camera(self):
-        """Testbed::reset_camera (testbed.cu:272-285); only the training-view camera is supported for
-        rendering, so this clears it."""
+        """Testbed::reset_camera (testbed.cu:272-285): fov_axis 1, fov 50.625 deg, zoom 1, screen centre 0.5, the
+        default camera looking down -z from (0.5, 0.5, 2.0)."""
+        self.fov_axis = 1
+        self.fov = 50.625
+        self.zoom = 1.0
+        self._screen_center = np.array([0.5, 0.5], np.float32)
+        cam = np.array([[1, 0, 0, 0.5], [0, -1, 0, 0.5], [0, 0, -1, 0.5]], np.float32)
+        cam[:, 3] -= np.float32(1.5) * cam[:, 2]
+        self._camera = cam
         self._render_view = None
 
-    def render(self, width: int = 1920, height: int = 1080, spp: int = 1, linear: bool = True, use_ema: bool = True):
-        """Testbed::render_to_cpu (python_api.cu:123-169) for the NeuS Shade mode: `spp` frames of
-        NerfTracer::trace accumulated in linear colour, returned as float32 [height, width, 4] with
-        premultiplied alpha. The background colour is composited as tonemap_kernel
-        (render_buffer.cu:474-500) does; linear=False returns sRGB."""
-        if self._render_view is None:
-            raise NeusError("render: call set_camera_to_training_view(view) first")
+    @property
+    def fov(self):
+        """Testbed::fov: focal_length_to_fov(1, relative focal length[fov_axis]) in degrees."""
+        return float(2.0 * math.atan(0.5 / float(self._rel_focal[int(self.fov_axis)])) * 180.0 / math.pi)
+
+    @fov.setter
+    def fov(self, deg):
+        self._rel_focal = np.full(2, fov_to_focal_length(1, float(deg)), np.float32)
+        self._render_view = None
+
+    @property
+    def fov_xy(self):
+        return np.array([2.0 * math.atan(0.5 / float(f)) * 180.0 / math.pi for f in self._rel_focal], np.float32)
+
+    @fov_xy.setter
+    def fov_xy(self, v):
+        self._rel_focal = np.array([fov_to_focal_length(1, float(x)) for x in np.asarray(v).reshape(2)], np.float32)
+        self._render_view = None
+
+    @property
+    def screen_center(self):
+        return self._screen_center.copy()
+
+    @screen_center.setter
+    def screen_center(self, v):
+        self._screen_center = np.asarray(v, np.float32).reshape(2).copy()
+        self._render_view = None
+
+    @property
+    def camera_matrix(self):
+        """m_camera: camera-to-world 3x4 in the ngp convention."""
+        return self._camera.copy()
+
+    @camera_matrix.setter
+    def camera_matrix(self, m):
+        self._camera = np.asarray(m, np.float32).reshape(3, 4).copy()
+        self._render_view = None
+
+    def set_nerf_camera_matrix(self, cam):
+        """Testbed::set_nerf_camera_matrix (testbed.cu:238-240): m_camera = dataset.nerf_matrix_to_ngp(cam), a 3x4
+        (or 4x4) NeRF camera-to-world matrix in the dataset's original coordinates."""
+        self._camera = nerf_matrix_to_ngp(np.asarray(cam, np.float32)[:3, :4], self._scale, self._offset, self._from_na)
+        self._render_view = None
+
+    def set_camera_to_training_view(self, view: int):
+        """Testbed::set_camera_to_training_view (testbed.cu:264-270): the camera, relative focal length
+        (focal / resolution[fov_axis]) and screen centre (1 - principal point) of training image `view`."""
+        if not 0 <= int(view) < self._n_images:
+            raise NeusError(f"training view {view} out of range (0..{self._n_images - 1})")
+        v = int(view)
+        meta = self._dataset_meta
+        im = self._images[v]
+        res = np.array([im.shape[1], im.shape[0]], np.float32)
+        self._camera = np.asarray(meta["xforms"][v], np.float32).reshape(3, 4).copy()
+        self._rel_focal = (np.asarray(meta["focal"][v], np.float32).reshape(2) / res[int(self.fov_axis)]).astype(np.float32)
+        self._screen_center = (np.float32(1.0) - np.asarray(meta["principal"][v], np.float32).reshape(2)).astype(np.float32)
+        # the device computes this camera from its own copy of the view (bit-identical to the oracle's render)
+        self._render_view = v if int(self.fov_axis) == 1 else None
+
+    # ------------------------------------------------------------------ rendering
+    def _render_request(self, width, height, spp, use_ema):
         rq = _lib.NeusRenderRequest()
         rq.width, rq.height, rq.spp = int(width), int(height), int(spp)
-        rq.training_view = self._render_view
+        if self._render_view is not None and float(self.zoom) == 1.0:
+            rq.training_view = self._render_view
+        else:
+            # calc_focal_length = relative focal * resolution[fov_axis] * zoom; render_screen_center
+            rq.training_view = -1
+            rq.xform[:] = [float(x) for x in self._camera.reshape(12)]
+            z = np.float32(self.zoom)
+            fl = self._rel_focal * np.float32((int(width), int(height))[int(self.fov_axis)]) * z
+            rq.focal[:] = [float(x) for x in fl]
+            sc = (np.float32(0.5) - self._screen_center) * z + np.float32(0.5)
+            rq.screen_center[:] = [float(x) for x in sc]
         rq.snap_to_pixel_centers = int(bool(self.snap_to_pixel_centers))
         rq.min_transmittance = float(self.nerf.rendering_min_transmittance)
         rq.use_ema = int(bool(use_ema))
+        return rq
+
+    def render_accumulation(self, width: int = 1920, height: int = 1080, spp: int = 1, use_ema: bool = True):
+        """The linear accumulation buffer of `spp` NerfTracer::trace frames (render_buffer.cu:217-260): float32
+        [height, width, 4], premultiplied alpha, before tonemap_kernel."""
+        if not self._n_images:
+            raise NeusError("render: load the training data first")
+        rq = self._render_request(width, height, spp, use_ema)
         out = np.empty((int(height), int(width), 4), np.float32)
         it = C.c_uint32()
         check(lib().neus_testbed_render(self._h, C.byref(rq), C.c_void_p(out.ctypes.data), C.byref(it)))
         self.last_render_iterations = it.value
-        bg = np.asarray(self.background_color, np.float32)
-        if bg[3] != 0:
-            bgl = np.where(bg[:3] <= 0.04045, bg[:3] / 12.92, ((bg[:3] + 0.055) / 1.055) ** 2.4)
-            out[..., :3] += bgl * (1 - out[..., 3:4]) * bg[3]
-        if not linear:
-            out[..., :3] = linear_to_srgb(out[..., :3])
         return out
+
+    def render(self, width: int = 1920, height: int = 1080, spp: int = 1, linear: bool = True, start_t: float = -1.0,
+               end_t: float = -1.0, fps: float = 30.0, shutter_fraction: float = 1.0, use_ema: bool = True):
+        """Testbed::render_to_cpu (python_api.cu:123-169) for the NeuS Shade mode: `spp` frames accumulated in linear
+        colour from the current camera (set_camera_to_training_view / set_nerf_camera_matrix / camera_matrix with
+        fov, fov_axis, zoom, screen_center), then tonemap_kernel (render_buffer.cu:474-500): background_color
+        composited, exposure, tonemap_curve, sRGB output when linear=False. Camera paths (start_t >= 0) are not
+        supported."""
+        if start_t >= 0.0:
+            raise NeusError("render: camera paths (start_t/end_t) are not supported; set the camera per frame")
+        acc = self.render_accumulation(width, height, spp, use_ema)
+        return tonemap_image(acc, self.exposure, self._background_color, self._color_space, self.tonemap_curve, to_srgb=not linear)
 
     # ------------------------------------------------------------------ meshes
     def compute_marching_cubes_mesh(self, resolution=(256, 256, 256), aabb=None, thresh=None, density_grid=None):
         """Testbed::compute_marching_cubes_mesh (python_api.cu:99-121): dict V (vertices), N (normalised
-        1-ring normals), C (vertex colours), F (faces). `aabb` = (min, max); None = the render aabb.
+        1-ring normals), C (vertex colours), F (faces). `aabb`: a BoundingBox or (min, max); None or an empty
+        (inside-out) box = the render aabb.
         thresh None = m_mesh.thresh = 0 (the SDF level set). `density_grid` (torch cuda tensor of
         res[2] x res[1] x res[0] floats) skips the network and meshes that grid as given."""
         res = (C.c_int32 * 3)(*[int(r) for r in np.broadcast_to(np.asarray(resolution), 3)])
-        amin, amax = self._aabb if aabb is None else (np.asarray(aabb[0], np.float32), np.asarray(aabb[1], np.float32))
+        pair = _aabb_pair(aabb)
+        amin, amax = self._aabb if pair is None else pair
         cmin, cmax = (C.c_float * 3)(*map(float, amin)), (C.c_float * 3)(*map(float, amax))
-        thresh = 0.0 if thresh is None else float(thresh)
+        thresh = 0.0 if thresh is None or float(thresh) >= 3.0e38 else float(thresh)  # float max = m_mesh.thresh (0)
         nv, nt = C.c_uint32(), C.c_uint32()
         dptr = C.c_void_p(density_grid.data_ptr()) if density_grid is not None else None
         check(lib().neus_testbed_marching_cubes(self._h, res, cmin, cmax, C.c_float(thresh), dptr, C.byref(nv), C.byref(nt)))
@@ -496,7 +888,8 @@ class Testbed:
         weights at x / res * (aabb.max - aabb.min) + aabb.min; float32 [res_z, res_y, res_x]."""
         r = [int(v) for v in np.broadcast_to(np.asarray(resolution), 3)]
         res = (C.c_int32 * 3)(*r)
-        amin, amax = self._aabb if aabb is None else (np.asarray(aabb[0], np.float32), np.asarray(aabb[1], np.float32))
+        pair = _aabb_pair(aabb)
+        amin, amax = self._aabb if pair is None else pair
         cmin, cmax = (C.c_float * 3)(*map(float, amin)), (C.c_float * 3)(*map(float, amax))
         out = np.zeros((r[2], r[1], r[0]), np.float32)
         check(lib().neus_testbed_sdf_on_grid(self._h, res, cmin, cmax, C.c_void_p(out.ctypes.data)))

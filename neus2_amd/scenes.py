@@ -160,3 +160,33 @@ def _morton_invert(x):
     x = (x | (x >> 8)) & 0xff0000ff
     x = (x | (x >> 16)) & 0x0000ffff
     return x
+
+
+def write_transforms(scene, directory, scale=0.33, offset=(0.5, 0.5, 0.5), name="transforms.json"):
+    """Writes a scene (images, focal, principal, ngp xforms) as the reference's dataset format: RGBA PNGs plus a
+    transforms.json with fl_x / fl_y / cx / cy / w / h and NeRF camera-to-world matrices (ngp_matrix_to_nerf of the
+    ngp cameras, so load_transforms recovers them up to float rounding)."""
+    import json
+    import os
+    from PIL import Image
+    from .pyngp import ngp_matrix_to_nerf
+    os.makedirs(directory, exist_ok=True)
+    h, w = scene["images"][0].shape[:2]
+    frames = []
+    sub = "images" if name == "transforms.json" else os.path.splitext(name)[0]
+    for i, im in enumerate(scene["images"]):
+        fn = f"{sub}/{i:03d}.png"
+        os.makedirs(os.path.join(directory, sub), exist_ok=True)
+        Image.fromarray(np.asarray(im, np.uint8), "RGBA").save(os.path.join(directory, fn))
+        m = np.eye(4, dtype=np.float64)
+        m[:3, :4] = ngp_matrix_to_nerf(scene["xforms"][i], scale, offset, False)
+        frames.append({"file_path": fn, "transform_matrix": m.tolist()})
+    f0, p0 = np.asarray(scene["focal"][0], np.float64), np.asarray(scene["principal"][0], np.float64)
+    import math
+    js = {"w": w, "h": h, "fl_x": float(f0[0]), "fl_y": float(f0[1]), "cx": float(p0[0] * w), "cy": float(p0[1] * h),
+          "camera_angle_x": 2.0 * math.atan(0.5 * w / float(f0[0])),
+          "scale": float(scale), "offset": [float(v) for v in np.broadcast_to(offset, 3)], "aabb_scale": 1, "frames": frames}
+    path = os.path.join(directory, name)
+    with open(path, "w") as f:
+        json.dump(js, f, indent=1)
+    return path

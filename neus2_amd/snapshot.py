@@ -42,19 +42,45 @@ def _f16_array(b) -> np.ndarray:
     return np.frombuffer(bytes(b), np.float16).astype(np.float32)
 
 
+# NerfDataset::from_json (json_binding.h:161-201) reads these keys with .at(); the per-image ones live under
+# metadata[i] and xforms[i] (TrainingXForm start / end).
+DATASET_REQUIRED_KEYS = ("n_images", "xforms", "render_aabb", "up", "offset", "envmap_resolution", "scale", "aabb_scale",
+                         "from_mitsuba", "from_na")
+METADATA_REQUIRED_KEYS = ("resolution", "focal_length", "principal_point", "rolling_shutter", "camera_distortion")
+
+
 def dataset_json(tb) -> dict:
-    """NerfDataset to_json metadata (nerf_loader.h: to_json): cameras and scene transform, no pixels."""
+    """NerfDataset to_json (json_binding.h:131-159): per-image metadata (focal length in pixels, camera
+    distortion - none, so null -, normalised principal point, rolling shutter, resolution), per-image TrainingXForm
+    {start, end} 3x4 row lists, render_aabb {min, max}, up, offset, envmap_resolution, scale, aabb_scale and the
+    loader flags. No pixels (the reference does not serialise them either)."""
     imgs = tb._images or []
     meta = getattr(tb, "_dataset_meta", None) or {}
+    xforms = [np.asarray(x, np.float32).reshape(3, 4).tolist() for x in meta.get("xforms", [])]
+    focal = [[float(v) for v in np.broadcast_to(np.asarray(f, np.float32), (2,))] for f in meta.get("focal", [])]
+    principal = [[float(v) for v in np.asarray(p, np.float32).reshape(2)] for p in meta.get("principal", [])]
+    metadata = [{
+        "focal_length": focal[i],
+        "camera_distortion": None,
+        "principal_point": principal[i],
+        "rolling_shutter": [0.0, 0.0, 0.0, 0.0],
+        "resolution": [int(im.shape[1]), int(im.shape[0])],
+    } for i, im in enumerate(imgs)]
+    amin, amax = getattr(tb, "_aabb", (np.zeros(3), np.ones(3)))
     return {
         "n_images": len(imgs),
-        "image_resolution": [int(imgs[0].shape[1]), int(imgs[0].shape[0])] if imgs else [0, 0],
-        "aabb_scale": float(meta.get("aabb_scale", 1)),
-        "scale": float(getattr(tb, "_scale", 1.0)),
+        "metadata": metadata,
+        "xforms": [{"start": x, "end": x} for x in xforms],
+        "render_aabb": {"min": [float(v) for v in amin], "max": [float(v) for v in amax]},
+        "up": [0.0, 1.0, 0.0],
         "offset": [float(x) for x in np.asarray(getattr(tb, "_offset", np.zeros(3)), np.float32)],
-        "xforms": [np.asarray(x, np.float32).reshape(3, 4).tolist() for x in meta.get("xforms", [])],
-        "focal": [[float(v) for v in np.broadcast_to(np.asarray(f, np.float32), (2,))] for f in meta.get("focal", [])],
-        "principal": [[float(v) for v in np.asarray(p, np.float32).reshape(2)] for p in meta.get("principal", [])],
+        "envmap_resolution": [0, 0],
+        "scale": float(getattr(tb, "_scale", 1.0)),
+        "aabb_scale": int(meta.get("aabb_scale", 1)),
+        "from_mitsuba": False,
+        "from_na": bool(getattr(tb, "_from_na", False)),
+        "is_hdr": False,
+        "wants_importance_sampling": True,
     }
 
 

@@ -261,6 +261,9 @@ struct OrDataset {
 	float motion_R[9];          // accumulated global movement, row-major (frames >= 1 of a dynamic scene)
 	float motion_t[3];
 	uint32_t motion_on;
+	uint32_t fixed_bg;          // 0: random background per ray (nerf.training.random_bg_color, the default)
+	float bg_color[3];          // sRGB background when fixed_bg
+	uint32_t target_mode;       // 0 color_space Linear (sRGB targets), 1 color_space SRGB, 2 linear_colors
 };
 
 namespace {
@@ -944,10 +947,20 @@ static void ray_target(const OrDataset* ds, uint32_t ray_idx_global, uint32_t n_
 	uint32_t img = image_idx(ray_idx_global, n_rays_global, n_rays_total, ds->n_images);
 	const int rx = ds->resolution[2 * img], ry = ds->resolution[2 * img + 1];
 	float xy_x, xy_y; random_image_pos(rng, rx, ry, xy_x, xy_y);
-	bg[0] = rng.next_float(); bg[1] = rng.next_float(); bg[2] = rng.next_float();
+	// train_with_random_bg_color, else the testbed background colour (:1642-1645)
+	if (ds->fixed_bg) for (int k = 0; k < 3; ++k) bg[k] = ds->bg_color[k];
+	else { bg[0] = rng.next_float(); bg[1] = rng.next_float(); bg[2] = rng.next_float(); }
 	for (int k = 0; k < 3; ++k) bg[k] = srgb_to_linear(bg[k]);
 	read_rgba_x_alpha(ds, img, xy_x, xy_y, tex);
-	for (int k = 0; k < 3; ++k) { target[k] = 1.0f * tex[k] + (1.0f - tex[3]) * bg[k]; target[k] = linear_to_srgb(target[k]); bg[k] = linear_to_srgb(bg[k]); }
+	for (int k = 0; k < 3; ++k) {
+		if (ds->target_mode == 1) {  // color_space SRGB (:1664-1670)
+			bg[k] = linear_to_srgb(bg[k]);
+			target[k] = tex[3] > 0.0f ? linear_to_srgb(1.0f * tex[k] / tex[3]) * tex[3] + (1.0f - tex[3]) * bg[k] : bg[k];
+		} else {                     // color_space Linear; linear_colors (mode 2) keeps linear targets (:1658-1663)
+			target[k] = 1.0f * tex[k] + (1.0f - tex[3]) * bg[k];
+			if (ds->target_mode == 0) { target[k] = linear_to_srgb(target[k]); bg[k] = linear_to_srgb(bg[k]); }
+		}
+	}
 }
 
 static void loss_ray(const OrDataset* ds, uint32_t i, uint32_t ray_idx_global, uint32_t n_rays_global, uint32_t n_rays_total, pcg32 rng,

@@ -31,6 +31,7 @@ class OrDataset(C.Structure):
         ("resolution", C.c_void_p), ("focal", C.c_void_p), ("principal", C.c_void_p), ("xform", C.c_void_p),
         ("aabb_min", C.c_float * 3), ("aabb_max", C.c_float * 3), ("cone_angle", C.c_float),
         ("motion_R", C.c_float * 9), ("motion_t", C.c_float * 3), ("motion_on", C.c_uint32),
+        ("fixed_bg", C.c_uint32), ("bg_color", C.c_float * 3), ("target_mode", C.c_uint32),
     ]
 
 
@@ -196,6 +197,13 @@ class Dataset:
             self.c.motion_R[:] = [float(v) for v in Rt[:, :3].reshape(-1)]
             self.c.motion_t[:] = [float(v) for v in Rt[:, 3]]
             self.c.motion_on = 1
+
+    def set_target(self, background=None, mode=0):
+        """Loss targets (testbed_nerf.cu:1642-1671): background None = random per ray (random_bg_color), else a
+        fixed sRGB colour; mode 0 color_space Linear, 1 color_space SRGB, 2 linear_colors."""
+        self.c.fixed_bg = 0 if background is None else 1
+        self.c.bg_color[:] = [0.0, 0.0, 0.0] if background is None else [float(v) for v in list(background)[:3]]
+        self.c.target_mode = int(mode)
 
 
 def generate_samples(ds, bitfield, n_rays, n_rays_total, rng_state, rng_inc, max_samples, ray_offset=0, n_rays_global=None):

@@ -232,6 +232,60 @@ def test_loss_compaction_parity(env):
         np.testing.assert_allclose(loss.cpu().numpy(), ref["loss"], rtol=1e-4, atol=1e-9)
 
 
+def test_loss_target_options_parity(env):
+    """The loss targets under the reference's training options (testbed_nerf.cu:1642-1671): a fixed background
+    (random_bg_color False, background_color) and the SRGB colour space / linear_colors target modes, against the
+    oracle with the same options. Compaction bit-exact, dL/dout and loss fp16-close as above; each option must
+    change the loss (it is exercised)."""
+    t, O, tb = env["t"], env["O"], env["tb"]
+    from neus2_amd import pyngp
+    lib, check = L()
+    bf = _bitfield(env)
+    n_rays, max_s, max_c = 2048, 2048 * 16, BATCH
+    rs, ri = 0x0BADF00D12345678, 0xDA3E39CB94B95BDB | 1
+    ds = env["ds"]
+    r_rays, r_ns, r_co, _, _ = O.generate_samples(ds, bf, n_rays, 0, rs, ri, max_s)
+    nk = int(r_ns[:, 0].sum())
+    net = O.network_forward(env["cfg"], tb.get_params(), r_co[:nk], 14).view(np.float16).copy()
+    net[:, 3] = np.random.default_rng(8).normal(0.0, 0.05, nk).astype(np.float16)
+    net[:, 7] = np.float16(0.35)
+    net = net.view(np.uint16)
+    losses = []
+    cases = [(True, None, 0), (False, (1.0, 1.0, 1.0), 0), (False, (0.2, 0.5, 0.9), 1), (True, None, 1), (False, (1.0, 1.0, 1.0), 2)]
+    try:
+        for random_bg, bgc, mode in cases:
+            tb.nerf.training.random_bg_color = random_bg
+            if bgc is not None:
+                tb.background_color = [*bgc, 1.0]
+            tb.color_space = pyngp.ColorSpace.SRGB if mode == 1 else pyngp.ColorSpace.Linear
+            tb.nerf.training.linear_colors = mode == 2
+            ds.set_target(None if random_bg else tb.background_color[:3], mode)
+            nsd = dev(t, r_ns)
+            co = t.zeros((max_c, 7), dtype=t.float32, device="cuda")
+            dlo = t.zeros((max_c, 16), dtype=t.int16, device="cuda")
+            loss = t.zeros(n_rays, dtype=t.float32, device="cuda"); ek = t.zeros_like(loss); mk = t.zeros_like(loss)
+            cnt = (C.c_uint32 * 1)()
+            check(lib.neus_loss_compact(tb.handle, None, C.c_uint32(n_rays), C.c_uint32(0), C.c_uint32(1), C.c_uint32(0),
+                                        C.c_uint64(rs), C.c_uint64(ri), C.c_uint32(max_c), ptr(dev(t, r_rays)), ptr(nsd),
+                                        ptr(dev(t, r_co)), ptr(dev(t, net)), ptr(co), ptr(dlo), ptr(loss), ptr(ek), ptr(mk), cnt))
+            ref = O.compute_loss(ds, n_rays, 0, rs, ri, max_c, r_rays, r_ns, r_co, net)
+            assert cnt[0] == ref["counter"]
+            np.testing.assert_array_equal(host(nsd, np.uint32), ref["numsteps"])
+            nc = min(ref["counter"], max_c)
+            g = host(dlo, np.float16).astype(np.float32)[:nc, :11]
+            r = ref["dL_dout"].view(np.float16).astype(np.float32)[:nc, :11]
+            np.testing.assert_allclose(g, r, rtol=2e-3, atol=1e-6)
+            np.testing.assert_allclose(loss.cpu().numpy(), ref["loss"], rtol=1e-4, atol=1e-9)
+            losses.append(float(ref["loss"].sum()))
+    finally:
+        tb.nerf.training.random_bg_color = True
+        tb.nerf.training.linear_colors = False
+        tb.color_space = pyngp.ColorSpace.Linear
+        tb.background_color = [0.0, 0.0, 0.0, 1.0]
+        ds.set_target(None, 0)
+    assert len(set(np.round(losses, 6))) == len(losses), losses
+
+
 def test_train_steps_reduce_loss(env):
     """End-to-end Testbed::train on the small synthetic scene: loss decreases, state consistent."""
     from neus2_amd import pyngp
@@ -309,7 +363,11 @@ def test_render_parity(torch_cuda):
     tb.snap_to_pixel_centers = True
     tb.nerf.rendering_min_transmittance = 1e-4
     tb.set_camera_to_training_view(0)
-    img = tb.render(64, 48, spp=2)
+    img = tb.render_accumulation(64, 48, spp=2)
+    # render() = the accumulation through tonemap_kernel; a transparent black background and the Linear /
+    # Identity defaults leave it unchanged
+    tb.background_color = [0.0, 0.0, 0.0, 0.0]
+    np.testing.assert_array_equal(tb.render(64, 48, spp=2), img)
     cfg = O.make_cfg(per_level_scale=tb._net_cfg.per_level_scale)
     ds = O.Dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"])
     _, bf = tb.get_density_grid()
@@ -327,6 +385,85 @@ def test_render_parity(torch_cuda):
     psnr_ref, _ = pyngp.eval_psnr(ref, sc["images"][0])
     record("render_psnr", psnr=psnr, psnr_oracle=psnr_ref)
     assert abs(psnr - psnr_ref) < 0.5
+
+
+def test_free_camera_render_parity(torch_cuda):
+    """render() from a free camera (camera_matrix + fov / fov_axis, python_api.cu:425-430): focal length =
+    fov_to_focal_length(1, fov) * resolution[fov_axis] and screen centre 0.5 (calc_focal_length,
+    render_screen_center, testbed.cu:2738-2746), against the oracle's render of the same camera (tolerance as
+    test_render_parity). fov_axis 0 scales by the width."""
+    from neus2_amd import pyngp
+    import oracle as O
+    tb = _mc_testbed()
+    tb.train_steps(60)
+    st = tb.stats()
+    sc = tb._scene
+    tb.snap_to_pixel_centers = True
+    tb.nerf.rendering_min_transmittance = 1e-4
+    tb.background_color = [0.0, 0.0, 0.0, 0.0]
+    cfg = O.make_cfg(per_level_scale=tb._net_cfg.per_level_scale)
+    ds = O.Dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"])
+    _, bf = tb.get_density_grid()
+    for axis, fov in ((1, 40.0), (0, 55.0)):
+        tb.fov_axis = axis
+        tb.fov = fov
+        tb.camera_matrix = sc["xforms"][3]
+        img = tb.render(64, 48, spp=1)
+        fl = np.float32(pyngp.fov_to_focal_length(1, fov)) * np.float32((64, 48)[axis])
+        ref, _ = O.render(cfg, tb.get_ema_params(), st["valid_level"], ds, bf, sc["xforms"][3], np.float32([fl, fl]),
+                          np.float32([0.5, 0.5]), 64, 48, spp=1, snap=True, min_transmittance=1e-4, cos_anneal=1.0)
+        d = np.abs(img - ref)
+        record("render_free_camera", axis=axis, mean_abs=d.mean(), frac_gt_1e2=(d > 1e-2).mean(), alpha_mean=ref[..., 3].mean())
+        assert ref[..., 3].max() > 0.05
+        assert d.mean() <= 2e-3 and (d > 1e-2).mean() <= 0.01, (axis, d.mean(), (d > 1e-2).mean())
+
+
+def test_prepare_for_test_delta_sdf(torch_cuda):
+    """prepare_for_test on frame 1 with the movement training (m_use_delta, testbed.cu:1987-1999): the SDF grid
+    is the network at R (x + t) (NerfNetwork::sdf through the DeltaNetwork, nerf_network.h:664-676) - against the
+    oracle forward at oracle/motion.py's moved grid points; render and mesh colours go through it too (the image
+    changes). On frame 0 the flag is off."""
+    import motion as M
+    import oracle as O
+    from neus2_amd import pyngp, scenes
+    frames = scenes.dynamic_scene(n_frames=2, shift=(0.02, 0.0, 0.0))
+    tb = pyngp.Testbed(pyngp.TestbedMode.Nerf)
+    tb.set_dataset_frames(frames)
+    tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=BATCH)
+    tb.train_steps(60)
+    assert tb.prepare_for_test() is False
+    assert tb.training_network_next_frame()
+    tb.train_steps(4)  # global-movement phase: train_delta
+    assert tb.prepare_for_test() is True
+    p = _moved_local()
+    tb.set_movement(local=p)
+    st = tb.stats()
+    res = (12, 10, 9)
+    amin, amax = np.float32([0.2, 0.1, 0.15]), np.float32([0.8, 0.9, 0.85])
+    sdf = tb.get_sdf_on_grid(res, aabb=(amin, amax))
+    gz, gy, gx = np.meshgrid(*[np.arange(r, dtype=np.float32) for r in res[::-1]], indexing="ij")
+    pos = np.zeros((sdf.size, 3), np.float32)
+    for k, (g, r) in enumerate(zip((gx, gy, gz), res)):
+        a = (g.reshape(-1) * np.float32(1.0 / r)).astype(np.float32)
+        pos[:, k] = (a.astype(np.float64) * np.float64(amax[k] - amin[k]) + np.float64(amin[k])).astype(np.float32)
+    coords = np.zeros((sdf.size, 7), np.float32)
+    coords[:, :3] = M.delta_apply(p, pos)
+    coords[:, 4:] = 0.5
+    cfg = O.make_cfg(per_level_scale=tb._net_cfg.per_level_scale)
+    ref = O.network_forward(cfg, tb.get_ema_params(), coords, st["valid_level"]).view(np.float16)[:, 3].astype(np.float32)
+    err = np.abs(sdf.reshape(-1) - ref)
+    ok = err <= 2e-3 + 4e-3 * np.abs(ref)
+    record("delta_sdf_on_grid", frac_within_tol=ok.mean(), median_abs_err=np.median(err))
+    assert ok.mean() >= 0.995 and np.median(err) < 1e-3, (ok.mean(), err.max())
+    tb.set_camera_to_training_view(0)
+    a = tb.render_accumulation(32, 24)
+    ident = np.zeros(12, np.float32); ident[4] = 1; ident[8] = 1
+    tb.set_movement(local=ident)
+    b = tb.render_accumulation(32, 24)
+    assert np.isfinite(a).all() and np.abs(a - b).max() > 1e-4
+    R, t = tb.saved_transform()
+    g, _ = tb.get_movement()
+    np.testing.assert_allclose(R, g[:, :3], atol=1e-3)  # identity local movement: the accumulated one
 
 
 def _moved_local():
@@ -474,6 +611,7 @@ def _mc_testbed():
     tb = pyngp.Testbed(pyngp.TestbedMode.Nerf)
     tb.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
     tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=BATCH)
+    tb._scene = sc
     return tb
 
 

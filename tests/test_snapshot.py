@@ -89,3 +89,31 @@ def test_snapshot_errors(tmp_path):
     assert snapshot.restore_fields(cfg)["grid"].size == 0
     with pytest.raises(NotImplementedError):
         snapshot.build_snapshot(_FakeTestbed(), include_optimizer_state=True)
+
+
+def test_snapshot_dataset_schema():
+    """snapshot.nerf.dataset follows NerfDataset to_json (json_binding.h:131-159): every key from_json reads with
+    .at() (json_binding.h:161-201) is present, per image under metadata[i], and xforms[i] is a TrainingXForm
+    {start, end} of 3x4 rows."""
+    from neus2_amd import snapshot
+    tb = _FakeTestbed()
+    tb._aabb = (np.full(3, -0.5, np.float32), np.full(3, 1.5, np.float32))
+    tb._from_na = False
+    ds = snapshot.build_snapshot(tb)["snapshot"]["nerf"]["dataset"]
+    for k in snapshot.DATASET_REQUIRED_KEYS:
+        assert k in ds, k
+    assert ds["n_images"] == 3 and len(ds["metadata"]) == 3 and len(ds["xforms"]) == 3
+    for m in ds["metadata"]:
+        for k in snapshot.METADATA_REQUIRED_KEYS:
+            assert k in m, k
+        assert m["resolution"] == [8, 6] and m["focal_length"] == [10.0, 10.0] and m["principal_point"] == [0.5, 0.5]
+        assert m["rolling_shutter"] == [0.0, 0.0, 0.0, 0.0] and m["camera_distortion"] is None
+    for x in ds["xforms"]:
+        assert np.asarray(x["start"]).shape == (3, 4) and x["start"] == x["end"]
+    assert ds["render_aabb"] == {"min": [-0.5] * 3, "max": [1.5] * 3}
+    assert ds["up"] == [0.0, 1.0, 0.0] and ds["envmap_resolution"] == [0, 0]
+    assert ds["scale"] == 0.5 and ds["offset"] == [0.5] * 3 and ds["aabb_scale"] == 1
+    assert ds["from_mitsuba"] is False and ds["from_na"] is False
+    # msgpack round trip keeps the structure (null distortion, nested lists)
+    back = snapshot.unpack(snapshot.pack({"d": ds}))["d"]
+    assert back == ds
