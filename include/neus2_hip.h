@@ -232,6 +232,19 @@ typedef struct NeusTrainingOptions {
 	float near_distance;
 } NeusTrainingOptions;
 int neus_testbed_get_training_options(NeusTestbed* tb, NeusTrainingOptions* out);
+/* Trainer::serialize(include_optimizer_state) / deserialize (trainer.h:281-305): the Ema(ExponentialDecay(Adam))
+ * state - Adam current_step, first / second moments, per-parameter steps (adam.h:424-445), the decay's learning
+ * rate and factor (exponential_decay.h:128-140), the fp16 EMA weights (ema.h:182-194; the fp32 accumulator is
+ * rebuilt from them on set). Arrays are n_params long, host memory, nullable on get; steps nullable on set. */
+typedef struct NeusOptimizerState {
+	uint32_t n_params;
+	uint32_t current_step;
+	float learning_rate;
+	float learning_rate_factor;
+} NeusOptimizerState;
+int neus_testbed_get_optimizer_state(NeusTestbed* tb, NeusOptimizerState* st, float* m1, float* m2, uint32_t* steps, uint16_t* ema_half);
+int neus_testbed_set_optimizer_state(NeusTestbed* tb, const NeusOptimizerState* st, const float* m1, const float* m2, const uint32_t* steps,
+                                     const uint16_t* ema_half);
 int neus_testbed_set_training_options(NeusTestbed* tb, const NeusTrainingOptions* opts);
 /* Per-ray counters of the last step (first n rays, host buffers, each nullable): samples requested by
  * the march, samples composited before transmittance < 1e-4, and numsteps = (compacted count, base). */

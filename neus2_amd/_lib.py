@@ -78,6 +78,11 @@ class NeusTrainingOptions(C.Structure):
     ]
 
 
+class NeusOptimizerState(C.Structure):
+    _fields_ = [("n_params", C.c_uint32), ("current_step", C.c_uint32), ("learning_rate", C.c_float),
+                ("learning_rate_factor", C.c_float)]
+
+
 # Every symbol declared in include/neus2_hip.h (checked by tests/test_capi.py).
 EXPORTS = [
     "neus_last_error", "neus_device_count", "neus_device_synchronize",
@@ -94,7 +99,8 @@ EXPORTS = [
     "neus_optimizer_step", "neus_fill_rollover", "neus_occ_update", "neus_mfma_probe",
     "neus_testbed_next_frame", "neus_testbed_get_movement", "neus_testbed_set_movement", "neus_testbed_frame_state",
     "neus_testbed_change_frame", "neus_testbed_prepare_for_test", "neus_testbed_get_training_options",
-    "neus_testbed_set_training_options", "neus_testbed_saved_transform",
+    "neus_testbed_set_training_options", "neus_testbed_saved_transform", "neus_testbed_get_optimizer_state",
+    "neus_testbed_set_optimizer_state",
     "neus_net_backward_pos", "neus_delta_apply", "neus_delta_backward",
 ]
 

@@ -218,6 +218,10 @@ struct NeusTestbed {
 	uint32_t training_step = 0;
 	uint32_t adam_step = 0;
 	float lr_factor = 1.f;
+	// the grid encoding's training step (GridEncoding::set_training_step, testbed.cu:2651-2657): set by every train
+	// step (minus the global-movement steps on frames >= 1), 0 for a fresh network; render / SDF grid / mesh colours
+	// use its progressive level, as the reference's inference does
+	int enc_step = 0;
 	// stats
 	float loss_scalar_ema = 0.f, last_loss = 0.f, ek_loss = 0.f, mask_loss = 0.f, ray_loss = 0.f;
 	uint32_t last_rays_with_samples = 0;
@@ -397,7 +401,7 @@ struct NeusTestbed {
 		rng = make_pcg32(c.seed);
 		density_grid_rng = make_pcg32(rng.next_uint());
 		(void)rng.next_uint();  // tv_loss_rng
-		training_step = 0; adam_step = 0; lr_factor = 1.f; density_grid_ema_step = 0;
+		training_step = 0; adam_step = 0; lr_factor = 1.f; density_grid_ema_step = 0; enc_step = 0;
 		loss_ema_init = false; loss_scalar_ema = last_loss = ek_loss = mask_loss = 0.f; loss_pending = false;
 		// workspace
 		batch = c.batch_size;
@@ -504,7 +508,10 @@ struct NeusTestbed {
 			HIP_CHECK(hipMemcpy(params_h.p, eh.data(), (size_t)P * 2, hipMemcpyHostToDevice));
 		}
 		HIP_CHECK(hipMemset(m1.p, 0, (size_t)P * 4)); HIP_CHECK(hipMemset(m2.p, 0, (size_t)P * 4));
-		HIP_CHECK(hipMemset(adam_steps.p, 0, (size_t)P * 4)); HIP_CHECK(hipMemset(ema_tmp.p, 0, (size_t)P * 4));
+		HIP_CHECK(hipMemset(adam_steps.p, 0, (size_t)P * 4));
+		// the fp32 EMA starts at the loaded weights: the first EMA step weighs it by 1 - decay^0 = 0, and until the
+		// canonical optimizer steps (after the global-movement phase) it is what get_ema_params reports
+		HIP_CHECK(hipMemcpy(ema_tmp.p, params_fp.p, (size_t)P * 4, hipMemcpyDeviceToDevice));
 		adam_step = 0; lr_factor = 1.f;
 		prepare_weights();
 		// reset_network_incremental (testbed.cu:2351-2370): m_rng = seed, rays_per_batch = 4096, counters
@@ -532,7 +539,14 @@ struct NeusTestbed {
 		training_step = 0; canonical_step = 0;
 		const uint32_t P = lay.P;
 		HIP_CHECK(hipMemset(m1.p, 0, (size_t)P * 4)); HIP_CHECK(hipMemset(m2.p, 0, (size_t)P * 4));
-		HIP_CHECK(hipMemset(adam_steps.p, 0, (size_t)P * 4)); HIP_CHECK(hipMemset(ema_tmp.p, 0, (size_t)P * 4));
+		HIP_CHECK(hipMemset(adam_steps.p, 0, (size_t)P * 4));
+		{  // the fp32 EMA restarts from the inference weights (weighted by 0 at the next EMA step)
+			std::vector<half_t> eh(P);
+			HIP_CHECK(hipMemcpy(eh.data(), ema_h.p, (size_t)P * 2, hipMemcpyDeviceToHost));
+			std::vector<float> ef(P);
+			for (uint32_t i = 0; i < P; ++i) ef[i] = (float)eh[i];
+			HIP_CHECK(hipMemcpy(ema_tmp.p, ef.data(), (size_t)P * 4, hipMemcpyHostToDevice));
+		}
 		adam_step = 0; lr_factor = 1.f;
 		HIP_CHECK(hipStreamSynchronize(stream));
 	}
@@ -760,7 +774,7 @@ struct NeusTestbed {
 		const MlpPtrs& w = rq.use_ema ? mlp_ema : mlp;
 		const half_t* grid = (rq.use_ema ? ema_h.p : params_h.p) + lay.grid_off;
 		if (rq.use_ema) prepare_weights_for(mlp_ema);
-		const uint32_t valid = valid_level_at((int)training_step);
+		const uint32_t valid = valid_level_at(enc_step);
 		const uint32_t spp = std::max(1u, rq.spp);
 		// m_use_delta (prepare_for_test): the network sees the sample positions through the DeltaNetwork
 		const bool use_delta = render_delta && cur_frame >= 1;
@@ -804,7 +818,7 @@ struct NeusTestbed {
 		if (!have_net) throw std::runtime_error("sdf_on_grid: no network");
 		prepare_weights_for(mlp_ema);
 		const uint64_t n = (uint64_t)res[0] * res[1] * res[2];
-		const uint32_t valid = valid_level_at((int)training_step);
+		const uint32_t valid = valid_level_at(enc_step);
 		const bool use_delta = render_delta && cur_frame >= 1;
 		if (use_delta) launch_delta_prepare(stream, delta.p);
 		for (uint64_t off = 0; off < n; off += (1ull << 30)) {
@@ -868,7 +882,7 @@ struct NeusTestbed {
 			launch_delta_prepare(stream, delta.p);
 			launch_delta_apply(stream, nullptr, mesh_nv, COORD_W, c.p, c.p, delta.p);
 		}
-		launch_nerf_infer(stream, lay.L, lay.W, nullptr, mesh_nv, c.p, gl, valid_level_at((int)training_step), ema_h.p + lay.grid_off, mlp_ema, o.p,
+		launch_nerf_infer(stream, lay.L, lay.W, nullptr, mesh_nv, c.p, gl, valid_level_at(enc_step), ema_h.p + lay.grid_off, mlp_ema, o.p,
 		                  std::max<uint32_t>(1, std::min<uint32_t>((mesh_nv + 127) / 128, 8192)));
 		std::vector<half_t> h((size_t)mesh_nv * OUT_W);
 		HIP_CHECK(hipMemcpyAsync(h.data(), o.p, h.size() * sizeof(half_t), hipMemcpyDeviceToHost, stream));
@@ -894,7 +908,8 @@ struct NeusTestbed {
 		}
 		const bool use_delta = dyn && train_delta;
 		render_delta = use_delta;  // m_nerf_network->m_use_delta follows the training step (testbed.cu:2704-2710)
-		const uint32_t valid = valid_level_at(dyn ? (int)training_step - (int)gm_steps() : (int)training_step);
+		enc_step = dyn ? (int)training_step - (int)gm_steps() : (int)training_step;
+		const uint32_t valid = valid_level_at(enc_step);
 		if (use_delta) launch_delta_prepare(s, delta.p);
 		const uint32_t n_prep = std::min(16u, std::max(1u, canonical_step / 16u));
 		mark(0);
@@ -1082,7 +1097,7 @@ int neus_testbed_get_stats(NeusTestbed* tb, NeusTrainStats* o) {
 		if (tb->grid_mean.p) HIP_CHECK(hipMemcpy(&mean, tb->grid_mean.p, 4, hipMemcpyDeviceToHost));
 		o->training_step = tb->training_step; o->rays_per_batch = s.rays_per_batch; o->measured_batch_size = s.measured_batch_size;
 		o->measured_batch_size_before_compaction = s.measured_before; o->n_rays_total = s.n_rays_total;
-		o->valid_level = tb->valid_level_at((int)tb->training_step); o->zero_records = s.zero_records;
+		o->valid_level = tb->valid_level_at(tb->enc_step); o->zero_records = s.zero_records;
 		o->loss = tb->loss_scalar_ema; o->ek_loss = tb->ek_loss; o->mask_loss = tb->mask_loss; o->last_loss = tb->last_loss;
 		o->density_grid_mean = mean;
 		o->ray_loss = tb->ray_loss; o->n_rays_with_samples = tb->last_rays_with_samples;
@@ -1159,11 +1174,55 @@ int neus_testbed_restore_state(NeusTestbed* tb, const NeusRestoreState* in) {
 		tb->loss_scalar_ema = tb->last_loss = in->loss;
 		tb->loss_ema_init = true;
 		HIP_CHECK(hipMemcpy(tb->ema_h.p, tb->params_h.p, (size_t)tb->lay.P * 2, hipMemcpyDeviceToDevice));
+		// the fp32 EMA follows the loaded inference weights (the first EMA step after a reload weighs it by 0)
+		HIP_CHECK(hipMemcpy(tb->ema_tmp.p, tb->params_fp.p, (size_t)tb->lay.P * 4, hipMemcpyDeviceToDevice));
 		if (in->rebuild_bitfield) {
 			launch_grid_mean(tb->stream, tb->density_grid.p, tb->grid_partial.p, tb->grid_mean.p);
 			launch_bitfield(tb->stream, tb->density_grid.p, tb->bitfield.p, tb->grid_mean.p, tb->max_cascade + 1);
 			launch_bitfield_linear(tb->stream, tb->bitfield.p, tb->bf_lin.p);
 		}
+		HIP_CHECK(hipStreamSynchronize(tb->stream));
+	});
+}
+int neus_testbed_get_optimizer_state(NeusTestbed* tb, NeusOptimizerState* st, float* m1, float* m2, uint32_t* steps, uint16_t* ema_half) {
+	return guard([&] {
+		if (!tb->have_net) throw std::runtime_error("optimizer state: no network");
+		HIP_CHECK(hipStreamSynchronize(tb->stream));
+		const size_t P = tb->lay.P;
+		if (st) {
+			st->n_params = (uint32_t)P;
+			st->current_step = tb->adam_step;
+			st->learning_rate = tb->cur_frame ? tb->cfg.after_learning_rate : tb->cfg.learning_rate;
+			st->learning_rate_factor = tb->lr_factor;
+		}
+		if (m1) HIP_CHECK(hipMemcpy(m1, tb->m1.p, P * 4, hipMemcpyDeviceToHost));
+		if (m2) HIP_CHECK(hipMemcpy(m2, tb->m2.p, P * 4, hipMemcpyDeviceToHost));
+		if (steps) HIP_CHECK(hipMemcpy(steps, tb->adam_steps.p, P * 4, hipMemcpyDeviceToHost));
+		if (ema_half) HIP_CHECK(hipMemcpy(ema_half, tb->ema_h.p, P * 2, hipMemcpyDeviceToHost));
+	});
+}
+int neus_testbed_set_optimizer_state(NeusTestbed* tb, const NeusOptimizerState* st, const float* m1, const float* m2, const uint32_t* steps,
+                                     const uint16_t* ema_half) {
+	return guard([&] {
+		if (!tb->have_net) throw std::runtime_error("optimizer state: no network");
+		if (!st || !m1 || !m2 || !ema_half) throw std::runtime_error("set_optimizer_state: state, moments and EMA weights are required");
+		const size_t P = tb->lay.P;
+		if (st->n_params != P) throw std::runtime_error("set_optimizer_state: parameter count mismatch");
+		HIP_CHECK(hipSetDevice(tb->device));
+		HIP_CHECK(hipStreamSynchronize(tb->stream));
+		HIP_CHECK(hipMemcpy(tb->m1.p, m1, P * 4, hipMemcpyHostToDevice));
+		HIP_CHECK(hipMemcpy(tb->m2.p, m2, P * 4, hipMemcpyHostToDevice));
+		// Adam::deserialize: param_steps absent -> zeros (adam.h:437-442)
+		if (steps) HIP_CHECK(hipMemcpy(tb->adam_steps.p, steps, P * 4, hipMemcpyHostToDevice));
+		else HIP_CHECK(hipMemset(tb->adam_steps.p, 0, P * 4));
+		// Ema::deserialize (ema.h:189-194): the EMA weights, and the fp32 accumulator cast from them
+		HIP_CHECK(hipMemcpy(tb->ema_h.p, ema_half, P * 2, hipMemcpyHostToDevice));
+		std::vector<float> f(P);
+		for (size_t i = 0; i < P; ++i) { half_t h; std::memcpy(&h, &ema_half[i], 2); f[i] = (float)h; }
+		HIP_CHECK(hipMemcpy(tb->ema_tmp.p, f.data(), P * 4, hipMemcpyHostToDevice));
+		tb->adam_step = st->current_step;
+		tb->lr_factor = st->learning_rate_factor;
+		tb->prepare_weights_for(tb->mlp_ema);
 		HIP_CHECK(hipStreamSynchronize(tb->stream));
 	});
 }

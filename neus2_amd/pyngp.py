@@ -986,6 +986,35 @@ class Testbed:
         check(lib().neus_testbed_get_half_params(self._h, C.c_int(1 if inference else 0), C.c_void_p(out.ctypes.data), C.c_uint64(n)))
         return out.view(np.float16)
 
+    def get_optimizer_state(self):
+        """Ema(ExponentialDecay(Adam)) state (neus_testbed_get_optimizer_state): dict of current_step,
+        learning_rate, learning_rate_factor, m1, m2 (f32), param_steps (u32), ema (fp16 EMA weights)."""
+        n = self.layout()["n_params"]
+        st = _lib.NeusOptimizerState()
+        m1, m2 = np.zeros(n, np.float32), np.zeros(n, np.float32)
+        steps, ema = np.zeros(n, np.uint32), np.zeros(n, np.uint16)
+        check(lib().neus_testbed_get_optimizer_state(self._h, C.byref(st), C.c_void_p(m1.ctypes.data), C.c_void_p(m2.ctypes.data),
+                                                     C.c_void_p(steps.ctypes.data), C.c_void_p(ema.ctypes.data)))
+        return {"current_step": int(st.current_step), "learning_rate": float(st.learning_rate),
+                "learning_rate_factor": float(st.learning_rate_factor), "m1": m1, "m2": m2, "param_steps": steps,
+                "ema": ema.view(np.float16)}
+
+    def set_optimizer_state(self, state):
+        n = self.layout()["n_params"]
+        st = _lib.NeusOptimizerState()
+        st.n_params, st.current_step = n, int(state["current_step"])
+        st.learning_rate, st.learning_rate_factor = float(state.get("learning_rate", 0.0)), float(state.get("learning_rate_factor", 1.0))
+        m1 = np.ascontiguousarray(state["m1"], np.float32)
+        m2 = np.ascontiguousarray(state["m2"], np.float32)
+        ema = np.ascontiguousarray(np.asarray(state["ema"], np.float16)).view(np.uint16)
+        steps = state.get("param_steps")
+        steps = None if steps is None else np.ascontiguousarray(steps, np.uint32)
+        if m1.size != n or m2.size != n or ema.size != n or (steps is not None and steps.size != n):
+            raise NeusError("set_optimizer_state: array sizes do not match the network's parameter count")
+        check(lib().neus_testbed_set_optimizer_state(self._h, C.byref(st), C.c_void_p(m1.ctypes.data), C.c_void_p(m2.ctypes.data),
+                                                     C.c_void_p(steps.ctypes.data) if steps is not None else None,
+                                                     C.c_void_p(ema.ctypes.data)))
+
     def get_density_grid(self):
         g = np.zeros(128 ** 3, np.float32)
         bf = np.zeros(128 ** 3 // 8 * 8, np.uint8)

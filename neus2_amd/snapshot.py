@@ -5,7 +5,7 @@ msgpack `bin` (nlohmann::json::binary_t). Fields, in the reference's order of wr
 
   Testbed::save_snapshot             testbed.cu:3144-3178
     snapshot = Trainer::serialize    trainer.h:281-293   n_params, params_binary (fp16 inference params)
-                                                         [, optimizer] (include_optimizer_state; not written here)
+                                                         [, optimizer] (include_optimizer_state: Ema / ExpDecay / Adam)
     rotation / transition            nerf_network.h:1179-1205  accumulated global movement, fp16 [12] / [4]
                                                          (3x3 row-major + 3 zero pad / xyz + 1 zero pad)
     local_rotation / local_transition nerf_network.h:1243-1247 DeltaNetwork params, fp16 [8] / [4]
@@ -88,13 +88,11 @@ def build_snapshot(tb, include_optimizer_state: bool = False) -> dict:
     """The m_network_config object save_snapshot writes (testbed.cu:3144-3178)."""
     if tb._cfg_dict is None:
         raise RuntimeError("save_snapshot: no network loaded (reload_network_from_file first)")
-    if include_optimizer_state:
-        raise NotImplementedError("save_snapshot(include_optimizer_state=True): optimizer state is not serialised "
-                                  "(the reference's scripts always pass False, run.py:238, run_dynamic.py:315)")
     cfg = copy.deepcopy(tb._cfg_dict)
     cfg.pop("snapshot", None)
     st = tb.stats()
-    params = tb.get_ema_params() if st["training_step"] > 0 else tb.get_params()
+    # m_params_inference: the fp16 EMA weights once training has stepped, the fp16 training weights before
+    params = tb.get_half_params(inference=st["training_step"] > 0)
     grid, _ = tb.get_density_grid()
     g, l = tb.get_movement()
     rot = np.zeros(12, np.float32); rot[:9] = g[:, :3].reshape(-1)
@@ -121,8 +119,37 @@ def build_snapshot(tb, include_optimizer_state: bool = False) -> dict:
         "training_step": int(st["training_step"]),
         "loss": float(st["loss"]),
     }
+    if include_optimizer_state:
+        snap["optimizer"] = optimizer_json(tb.get_optimizer_state())
     cfg["snapshot"] = snap
     return cfg
+
+
+def optimizer_json(o: dict) -> dict:
+    """Ema::serialize { nested: ExponentialDecay::serialize { nested: Adam::serialize, learning_rate,
+    learning_rate_factor }, weights_ema_binary } (ema.h:182-187, exponential_decay.h:128-134, adam.h:424-432)."""
+    adam = {
+        "current_step": int(o["current_step"]),
+        "base_learning_rate": float(o["learning_rate"]) * float(o["learning_rate_factor"]),
+        "first_moments_binary": np.ascontiguousarray(o["m1"], np.float32).tobytes(),
+        "second_moments_binary": np.ascontiguousarray(o["m2"], np.float32).tobytes(),
+        "param_steps_binary": np.ascontiguousarray(o["param_steps"], np.uint32).tobytes(),
+    }
+    return {"nested": {"nested": adam, "learning_rate": float(o["learning_rate"]),
+                       "learning_rate_factor": float(o["learning_rate_factor"])},
+            "weights_ema_binary": np.ascontiguousarray(o["ema"], np.float16).tobytes()}
+
+
+def optimizer_state(j: dict) -> dict:
+    """The inverse of optimizer_json (Ema / ExponentialDecay / Adam deserialize; param_steps optional)."""
+    dec = j["nested"]
+    adam = dec["nested"]
+    steps = np.frombuffer(bytes(adam["param_steps_binary"]), np.uint32).copy() if "param_steps_binary" in adam else None
+    return {"current_step": int(adam["current_step"]), "learning_rate": float(dec["learning_rate"]),
+            "learning_rate_factor": float(dec.get("learning_rate_factor", 1.0)),
+            "m1": np.frombuffer(bytes(adam["first_moments_binary"]), np.float32).copy(),
+            "m2": np.frombuffer(bytes(adam["second_moments_binary"]), np.float32).copy(),
+            "param_steps": steps, "ema": np.frombuffer(bytes(j["weights_ema_binary"]), np.float16).copy()}
 
 
 def pack(cfg: dict) -> bytes:
@@ -170,6 +197,7 @@ def restore_fields(cfg: dict) -> dict:
         "measured_batch_size": int(rgb.get("measured_batch_size", 0)),
         "measured_batch_size_before_compaction": int(rgb.get("measured_batch_size_before_compaction", 0)),
         "global_Rt": None, "local": None,
+        "optimizer": optimizer_state(snap["optimizer"]) if "optimizer" in snap else None,
     }
     if "rotation" in snap and "transition" in snap:
         rot, tr = _f16_array(snap["rotation"]), _f16_array(snap["transition"])
@@ -201,6 +229,8 @@ def apply_snapshot(tb, cfg: dict) -> None:
     check(lib().neus_testbed_restore_state(tb.handle, C.byref(st)))
     if f["global_Rt"] is not None or f["local"] is not None:
         tb.set_movement(f["global_Rt"], f["local"])
+    if f["optimizer"] is not None:  # Trainer::deserialize -> m_optimizer->deserialize (trainer.h:296-305)
+        tb.set_optimizer_state(f["optimizer"])
 
 
 def load_snapshot(tb, path: str) -> None:

@@ -94,3 +94,37 @@ def test_run_dynamic_sequence(tmp_path, torch_cuda):
     assert min(r["train_psnr"]) > 20.0, r["train_psnr"]
     for a, b in zip(r["train_psnr"], r["test_psnr"]):
         assert abs(a - b) < 0.5, (r["train_psnr"], r["test_psnr"])
+
+
+def test_snapshot_optimizer_state_round_trip(tmp_path, torch_cuda):
+    """save_snapshot(include_optimizer_state=True) -> load_snapshot restores the Ema(ExponentialDecay(Adam)) state
+    exactly (moments, per-parameter steps, current step, EMA weights; trainer.h:281-305) and training continues
+    from it: the next step's Adam update uses the restored moments (step count carries on)."""
+    from neus2_amd import pyngp, scenes
+    sc = scenes.small_scene(n_views=8, width=64, height=48)
+    tb = pyngp.Testbed(pyngp.TestbedMode.Nerf)
+    tb.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
+    tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=4096)
+    tb.train_steps(40)
+    p = str(tmp_path / "s.msgpack")
+    tb.save_snapshot(p, include_optimizer_state=True)
+    o = tb.get_optimizer_state()
+    tb2 = pyngp.Testbed(pyngp.TestbedMode.Nerf)
+    tb2.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
+    tb2.load_snapshot(p)
+    o2 = tb2.get_optimizer_state()
+    assert o2["current_step"] == o["current_step"] == 40
+    for k in ("m1", "m2", "param_steps"):
+        np.testing.assert_array_equal(o2[k], o[k])
+    np.testing.assert_array_equal(o2["ema"].view(np.uint16), o["ema"].view(np.uint16))
+    np.testing.assert_array_equal(tb2.get_half_params(inference=True).view(np.uint16), o["ema"].view(np.uint16))
+    tb2.train_steps(1)
+    o3 = tb2.get_optimizer_state()
+    assert o3["current_step"] == 41 and int(o3["param_steps"].max()) == int(o["param_steps"].max()) + 1
+    # without the optimizer state the reload starts a fresh Adam
+    tb3 = pyngp.Testbed(pyngp.TestbedMode.Nerf)
+    tb3.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
+    p2 = str(tmp_path / "s2.msgpack")
+    tb.save_snapshot(p2)
+    tb3.load_snapshot(p2)
+    assert tb3.get_optimizer_state()["current_step"] == 0 and not tb3.get_optimizer_state()["m1"].any()

@@ -235,8 +235,8 @@ def test_loss_compaction_parity(env):
 def test_loss_target_options_parity(env):
     """The loss targets under the reference's training options (testbed_nerf.cu:1642-1671): a fixed background
     (random_bg_color False, background_color) and the SRGB colour space / linear_colors target modes, against the
-    oracle with the same options. Compaction bit-exact, dL/dout and loss fp16-close as above; each option must
-    change the loss (it is exercised)."""
+    oracle with the same options. Compaction bit-exact, dL/dout and loss fp16-close as above; the options must
+    change the loss (they are exercised)."""
     t, O, tb = env["t"], env["O"], env["tb"]
     from neus2_amd import pyngp
     lib, check = L()
@@ -283,7 +283,9 @@ def test_loss_target_options_parity(env):
         tb.color_space = pyngp.ColorSpace.Linear
         tb.background_color = [0.0, 0.0, 0.0, 1.0]
         ds.set_target(None, 0)
-    assert len(set(np.round(losses, 6))) == len(losses), losses
+    # the scene's alpha is 0 or 1, where the SRGB and Linear targets coincide (cases 0 and 3); the other options
+    # each change the loss
+    assert len(set(np.round(losses, 6))) == 4 and abs(losses[0] - losses[3]) < 1e-9, losses
 
 
 def test_train_steps_reduce_loss(env):
@@ -305,7 +307,8 @@ def test_train_steps_reduce_loss(env):
 def test_snapshot_round_trip(env, tmp_path):
     """save_snapshot -> load_snapshot into a fresh testbed (testbed.cu:3144-3254): params are the fp16 EMA
     weights, grid fp16, counters / step / loss / movement restored, the occupancy bitfield rebuilt from the
-    grid is the saved one, the two testbeds render the same image bit-for-bit, and training resumes."""
+    grid is the saved one, the two testbeds render the same image (up to the progressive-level state a load
+    resets), and training resumes."""
     from neus2_amd import pyngp
     sc = env["sc"]
     tb = pyngp.Testbed(pyngp.TestbedMode.Nerf)
@@ -339,8 +342,14 @@ def test_snapshot_round_trip(env, tmp_path):
     for t in (tb, tb2):
         t.snap_to_pixel_centers = True
         t.set_camera_to_training_view(0)
-    # tb renders with its fp32-derived fp16 EMA weights; tb2 with fp16(fp32 EMA) - the same fp16 values
-    np.testing.assert_array_equal(tb.render(64, 48, spp=1), tb2.render(64, 48, spp=1))
+    # tb renders with its fp32-derived fp16 EMA weights at the progressive level of its last step; tb2 with the same
+    # fp16 values but, like the reference after load_snapshot (a fresh GridEncoding, grid.h:1465, until the next
+    # train step sets its step), with every level. The levels above the trained ones hold init-scale features the
+    # density MLP's zero-initialised columns barely read, so the images agree closely, not bitwise.
+    assert st0["valid_level"] < tb.layout()["n_levels"] and st1["valid_level"] == tb.layout()["n_levels"]
+    a, b = tb.render(64, 48, spp=1), tb2.render(64, 48, spp=1)
+    record("snapshot_render", mean_abs=np.abs(a - b).mean(), max_abs=np.abs(a - b).max())
+    assert np.abs(a - b).mean() < 1e-3, np.abs(a - b).mean()
     tb2.train_steps(16)
     st2 = tb2.stats()
     assert st2["training_step"] == st0["training_step"] + 16 and np.isfinite(st2["ray_loss"])

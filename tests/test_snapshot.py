@@ -34,6 +34,15 @@ class _FakeTestbed:
     def get_params(self):
         return self._params * 0
 
+    def get_half_params(self, inference=False):
+        return (self._params if inference else self._params * 0).astype(np.float16)
+
+    def get_optimizer_state(self):
+        n = self._params.size
+        return {"current_step": 123, "learning_rate": 1e-3, "learning_rate_factor": 0.5,
+                "m1": np.linspace(-1, 1, n).astype(np.float32), "m2": np.linspace(0, 2, n).astype(np.float32),
+                "param_steps": np.arange(n, dtype=np.uint32), "ema": self._params.astype(np.float16)}
+
     def get_density_grid(self):
         return self._grid, None
 
@@ -87,8 +96,31 @@ def test_snapshot_errors(tmp_path):
         snapshot.restore_fields(cfg)
     cfg["snapshot"]["density_grid_binary"] = b""  # an untrained model's empty grid is valid
     assert snapshot.restore_fields(cfg)["grid"].size == 0
-    with pytest.raises(NotImplementedError):
-        snapshot.build_snapshot(_FakeTestbed(), include_optimizer_state=True)
+
+
+
+def test_snapshot_optimizer_state_layout():
+    """include_optimizer_state: snapshot.optimizer = Ema::serialize {nested: ExponentialDecay {nested: Adam
+    {current_step, base_learning_rate, first/second_moments_binary (f32), param_steps_binary (u32)}, learning_rate,
+    learning_rate_factor}, weights_ema_binary (fp16)} (ema.h:182-187, exponential_decay.h:128-134, adam.h:424-432),
+    decoded back exactly; without it there is no optimizer key."""
+    from neus2_amd import snapshot
+    tb = _FakeTestbed()
+    assert "optimizer" not in snapshot.build_snapshot(tb)["snapshot"]
+    cfg = snapshot.unpack(snapshot.pack(snapshot.build_snapshot(tb, include_optimizer_state=True)))
+    o = cfg["snapshot"]["optimizer"]
+    adam = o["nested"]["nested"]
+    assert set(adam) == {"current_step", "base_learning_rate", "first_moments_binary", "second_moments_binary", "param_steps_binary"}
+    assert o["nested"]["learning_rate"] == 1e-3 and o["nested"]["learning_rate_factor"] == 0.5
+    assert adam["current_step"] == 123 and abs(adam["base_learning_rate"] - 5e-4) < 1e-12
+    n = tb._params.size
+    assert len(adam["first_moments_binary"]) == 4 * n and len(adam["param_steps_binary"]) == 4 * n
+    assert len(o["weights_ema_binary"]) == 2 * n
+    f = snapshot.restore_fields(cfg)["optimizer"]
+    ref = tb.get_optimizer_state()
+    for k in ("m1", "m2", "param_steps", "ema"):
+        np.testing.assert_array_equal(f[k], ref[k])
+    assert (f["current_step"], f["learning_rate_factor"]) == (123, 0.5)
 
 
 def test_snapshot_dataset_schema():
