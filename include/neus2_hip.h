@@ -114,6 +114,8 @@ typedef struct NeusTrainStats {
 	uint64_t trained_samples_total;           /* compacted (non-rollover) training samples since step 0, per rank */
 	uint32_t march_first_pass_rays;           /* ray slots the next step's first march pass covers (0 = all) */
 	uint32_t kept_ray_extent;                 /* 1 + the last ray slot kept by the last step's sampler */
+	uint32_t nonfinite_loss;                  /* a logged loss sum was NaN / Inf (all-reduced, so every rank sees it) */
+	uint32_t training_aborted;                /* zero compacted samples (testbed_nerf.cu:3542-3548) or a non-finite loss */
 } NeusTrainStats;
 
 /* Testbed::render_to_cpu (python_api.cu:123-169) after set_camera_to_training_view (testbed.cu:264-270). */
@@ -286,6 +288,55 @@ typedef struct NeusLocalGroup NeusLocalGroup;
 int neus_local_group_create(int world, NeusLocalGroup** out);
 int neus_local_group_destroy(NeusLocalGroup* group);
 int neus_testbed_init_local_group(NeusTestbed* tb, NeusLocalGroup* group, int rank);
+
+/* ------------------------------------------------------------------ tcnn-shaped operator modules
+ * tcnn::cpp::Module (dependencies/my_tcnn/include/tiny-cuda-nn/cpp_api.h:66-110) over the gfx950 kernels, with
+ * explicit parameter pointers, a forward context and EGradientMode (object.h:90-94). Device buffers throughout;
+ * `stream` is the hipStream_t the call runs on (NULL: the null stream).
+ *   neus_module_create_network   the NeuS NerfNetwork (nerf_network.h; the full config object with "encoding",
+ *                                "network", "rgb_network"): input NerfCoordinate [n][7] f32 (pos, dt, dir), output
+ *                                [n][16] fp16; params [n_params] fp16 in the layout of neus_testbed_layout.
+ *   neus_module_create_encoding  the HashGrid encoding (create_encoding, grid.h): input [n][3] f32, output [L][n]
+ *                                half2 (features 2l, 2l+1 of level l adjacent; tcnn's SoA has them in separate rows),
+ *                                params [n_grid] fp16.
+ * Parameter gradients are fp32 (the reference's are param-precision fp16). Network backward needs n % 128 == 0;
+ * its dL_dinput ([n][7] f32) carries the position columns (dt / direction columns written 0). The network's
+ * eikonal second order is inside backward (as nerf_network.h:330-601); backward_backward_input is the encoding's
+ * (grid.h:1697-1800, without the dL_dinput term). Progressive levels follow set_training_step (grid.h:2427-2437;
+ * 0 = all levels). */
+typedef struct NeusModule NeusModule;
+typedef struct NeusContext NeusContext;
+enum { NEUS_GRADIENT_IGNORE = 0, NEUS_GRADIENT_OVERWRITE = 1, NEUS_GRADIENT_ACCUMULATE = 2 };
+enum { NEUS_PRECISION_FP32 = 0, NEUS_PRECISION_FP16 = 1 };
+typedef struct NeusModuleInfo {
+	uint64_t n_params;
+	uint32_t n_input_dims, n_output_dims;
+	int32_t param_precision, output_precision, gradient_precision;
+	uint32_t batch_capacity;
+	uint32_t n_levels;
+	uint64_t grid_offset;   /* first hash-grid parameter (network modules) */
+	float per_level_scale;
+} NeusModuleInfo;
+int neus_module_create_network(const char* config_json, uint32_t batch_capacity, NeusModule** out);
+int neus_module_create_encoding(uint32_t n_input_dims, const char* encoding_json, uint32_t batch_capacity, NeusModule** out);
+int neus_module_destroy(NeusModule* m);
+int neus_context_destroy(NeusContext* ctx);
+int neus_module_info(const NeusModule* m, NeusModuleInfo* out);
+/* Module::hyperparams as JSON text (len = its length; buf gets a NUL-terminated prefix of up to cap - 1 bytes). */
+int neus_module_hyperparams(const NeusModule* m, char* buf, uint64_t cap, uint64_t* len);
+int neus_module_set_training_step(NeusModule* m, int training_step);
+/* NeuS backward: the eikonal entries of dL_doutput are divided by this batch size (0 = each call's n). */
+int neus_module_set_indeed_batch_size(NeusModule* m, uint32_t indeed_batch_size);
+/* Module::initialize_params: fp32 initial parameters (trainer.h:54-109 seed_seq{seed} -> pcg32) into a device buffer. */
+int neus_module_initialize_params(NeusModule* m, uint64_t seed, float* params_full_precision);
+int neus_module_inference(NeusModule* m, void* stream, uint32_t n_elements, const float* input, void* output, const void* params);
+int neus_module_forward(NeusModule* m, void* stream, uint32_t n_elements, const float* input, void* output, const void* params,
+                        int prepare_input_gradients, NeusContext** ctx);
+int neus_module_backward(NeusModule* m, void* stream, const NeusContext* ctx, uint32_t n_elements, float* dL_dinput, const void* dL_doutput,
+                         void* dL_dparams, const float* input, const void* output, const void* params, int gradient_mode);
+int neus_module_backward_backward_input(NeusModule* m, void* stream, const NeusContext* ctx, uint32_t n_elements, const float* dL_ddLdinput,
+                                        const float* input, const void* dL_doutput, void* dL_dparams, void* dL_ddLdoutput,
+                                        float* dL_dinput, const void* params, int gradient_mode);
 
 /* ------------------------------------------------------------------ operator surface (device buffers) */
 /* Hash-grid forward on n positions (AoS, `coord_stride` floats per sample, xyz first).

@@ -43,7 +43,8 @@ class NeusTrainStats(C.Structure):
         ("zero_records", C.c_uint32), ("loss", C.c_float), ("ek_loss", C.c_float), ("mask_loss", C.c_float),
         ("last_loss", C.c_float), ("density_grid_mean", C.c_float), ("ray_loss", C.c_float),
         ("n_rays_with_samples", C.c_uint32), ("trained_samples_total", C.c_uint64),
-        ("march_first_pass_rays", C.c_uint32), ("kept_ray_extent", C.c_uint32),
+        ("march_first_pass_rays", C.c_uint32), ("kept_ray_extent", C.c_uint32), ("nonfinite_loss", C.c_uint32),
+        ("training_aborted", C.c_uint32),
     ]
 
 
@@ -83,6 +84,13 @@ class NeusOptimizerState(C.Structure):
                 ("learning_rate_factor", C.c_float)]
 
 
+class NeusModuleInfo(C.Structure):
+    _fields_ = [("n_params", C.c_uint64), ("n_input_dims", C.c_uint32), ("n_output_dims", C.c_uint32),
+                ("param_precision", C.c_int32), ("output_precision", C.c_int32), ("gradient_precision", C.c_int32),
+                ("batch_capacity", C.c_uint32), ("n_levels", C.c_uint32), ("grid_offset", C.c_uint64),
+                ("per_level_scale", C.c_float)]
+
+
 # Every symbol declared in include/neus2_hip.h (checked by tests/test_capi.py).
 EXPORTS = [
     "neus_last_error", "neus_device_count", "neus_device_synchronize",
@@ -101,6 +109,10 @@ EXPORTS = [
     "neus_testbed_change_frame", "neus_testbed_prepare_for_test", "neus_testbed_get_training_options",
     "neus_testbed_set_training_options", "neus_testbed_saved_transform", "neus_testbed_get_optimizer_state",
     "neus_testbed_set_optimizer_state",
+    "neus_module_create_network", "neus_module_create_encoding", "neus_module_destroy", "neus_context_destroy",
+    "neus_module_info", "neus_module_hyperparams", "neus_module_set_training_step", "neus_module_set_indeed_batch_size",
+    "neus_module_initialize_params", "neus_module_inference", "neus_module_forward", "neus_module_backward",
+    "neus_module_backward_backward_input",
     "neus_net_backward_pos", "neus_delta_apply", "neus_delta_backward",
 ]
 

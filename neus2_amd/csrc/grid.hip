@@ -289,7 +289,55 @@ __global__ void __launch_bounds__(256) k_scatter_accum(ScatterWork w, float* __r
 		grads[2 * (size_t)e0 + k] = (float)((double)(long long)acc[(k & 1) * SB_SIZE + (k >> 1)] * (1.0 / 4294967296.0));
 }
 
+// ---------------------------------------------------------------- operator-module helpers (neus_module_*)
+// dL/dx of the encoding (GridEncoding::backward's dL_dinput, kernel_grid_backward_input, grid.h:503-565):
+// dL_dx[i][d] = sum over levels / features of dL_dy[f][i] * dy_dx[f][d][i]; dL_dy is [L][ld] half2.
+__global__ void __launch_bounds__(256) k_enc_input_grad(uint32_t n, uint32_t ld, uint32_t L, const uint32_t* __restrict__ dLdy,
+                                                        const float* __restrict__ dydx, float* __restrict__ dLdx, uint32_t stride) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	float acc[3] = {0.f, 0.f, 0.f};
+	for (uint32_t l = 0; l < L; ++l) {
+		const uint32_t a = dLdy[(size_t)l * ld + i];
+		const h2 g = *(const h2*)&a;
+#pragma unroll
+		for (int f = 0; f < 2; ++f)
+#pragma unroll
+			for (int d = 0; d < 3; ++d) acc[d] += (float)g[f] * dydx[(size_t)(6 * l + 3 * f + d) * ld + i];
+	}
+#pragma unroll
+	for (int d = 0; d < 3; ++d) dLdx[(size_t)i * stride + d] = acc[d];
+}
+// dL/d(dL_dy) of backward_backward_input (kernel_grid_backward_input_backward_dLdoutput, grid.h:1092-1120):
+// out[f][i] = sum_d dL_ddLdx[i][d] * dy_dx[f][d][i], written as [L][ld] half2; and dL_ddLdx packed as float4
+// for the fused scatter's second-order term.
+__global__ void __launch_bounds__(256) k_enc_ddLdoutput(uint32_t n, uint32_t ld, uint32_t L, const float* __restrict__ ddx,
+                                                        const float* __restrict__ dydx, uint32_t* __restrict__ out, float4* __restrict__ v4) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	const float v[3] = {ddx[3 * (size_t)i], ddx[3 * (size_t)i + 1], ddx[3 * (size_t)i + 2]};
+	v4[i] = make_float4(v[0], v[1], v[2], 0.f);
+	if (!out) return;
+	for (uint32_t l = 0; l < L; ++l) {
+		h2 o;
+#pragma unroll
+		for (int f = 0; f < 2; ++f) {
+			float a = 0.f;
+#pragma unroll
+			for (int d = 0; d < 3; ++d) a += v[d] * dydx[(size_t)(6 * l + 3 * f + d) * ld + i];
+			o[f] = (half_t)a;
+		}
+		out[(size_t)l * ld + i] = *(const uint32_t*)&o;
+	}
+}
+
 // ---------------------------------------------------------------- host launchers
+void launch_enc_input_grad(hipStream_t s, uint32_t n, uint32_t ld, uint32_t L, const half_t* dLdy, const float* dydx, float* dLdx, uint32_t stride) {
+	if (n) k_enc_input_grad<<<(n + 255) / 256, 256, 0, s>>>(n, ld, L, (const uint32_t*)dLdy, dydx, dLdx, stride);
+}
+void launch_enc_ddLdoutput(hipStream_t s, uint32_t n, uint32_t ld, uint32_t L, const float* ddx, const float* dydx, half_t* out, float4* v4) {
+	if (n) k_enc_ddLdoutput<<<(n + 255) / 256, 256, 0, s>>>(n, ld, L, ddx, dydx, (uint32_t*)out, v4);
+}
 void launch_grid_encode(hipStream_t s, const uint32_t* n_ptr, uint32_t n_fixed, uint32_t ld, const float* coords, uint32_t coord_stride,
                         const GridLevels& gl, uint32_t valid_level, const half_t* grid, uint32_t* enc, float* dydx, uint32_t grid_x) {
 	if (!grid_x) return;

@@ -235,6 +235,10 @@ void launch_sum_f32(hipStream_t s, void* temp, size_t temp_bytes, const float* i
 void launch_adam_ema(hipStream_t s, const AdamParams& p, float* weights_fp, half_t* weights_h, const float* grads, float* m1, float* m2,
                      uint32_t* steps, float* ema_tmp, half_t* ema_h);
 void launch_cast_half(hipStream_t s, uint32_t n, const float* in, half_t* out);
+void launch_add_f32(hipStream_t s, uint32_t n, const float* src, float* dst);
+// operator-module encoding helpers (grid.hip)
+void launch_enc_input_grad(hipStream_t s, uint32_t n, uint32_t ld, uint32_t L, const half_t* dLdy, const float* dydx, float* dLdx, uint32_t stride);
+void launch_enc_ddLdoutput(hipStream_t s, uint32_t n, uint32_t ld, uint32_t L, const float* ddx, const float* dydx, half_t* out, float4* v4);
 void launch_transpose_w(hipStream_t s, const TransposeJobs& jobs);
 struct DinPerm { int32_t p[48]; uint32_t din, W; };
 void launch_permute_din(hipStream_t s, const half_t* d0, half_t* d0p, half_t* d0Tp, const DinPerm& perm);

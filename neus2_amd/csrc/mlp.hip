@@ -211,12 +211,22 @@ __device__ __forceinline__ void level_addr(const LevelSmem& sl, uint32_t dense_b
 		const uint32_t yy = gp[1] + (k & 1), zz = gp[2] + (k >> 1);
 		yz[k] = ((yy * res + zz * (res * res)) & dm) | (((yy * 2654435761u) ^ (zz * 805459861u)) & ~dm);
 	}
+	// A position inside the unit cube has every cell coordinate <= res - 1, so a dense corner index is below
+	// 2 hs and one conditional subtract is the reference's `% hashmap_size`. Positions outside it (a sample moved
+	// by the DeltaNetwork, a grid point beyond the aabb; negative cells wrap to huge unsigned values) take the
+	// true modulo, on the rare lanes that need it.
+	const bool outside = dense && (gp[0] >= res || gp[1] >= res || gp[2] >= res);
+	if (__builtin_expect(outside, 0)) {
 #pragma unroll
-	for (int c = 0; c < 8; ++c) {
-		const uint32_t xx = gp[0] + (c & 1), k = c >> 1;
-		const uint32_t ed = xx + yz[k];
-		const uint32_t ew = min(ed, ed - hs);  // ed < 2 hs: the reference's % hashmap_size
-		A.e[c] = o0 + ((ew & dm) | ((xx ^ yz[k]) & (hs - 1u) & ~dm));
+		for (int c = 0; c < 8; ++c) A.e[c] = o0 + (gp[0] + (c & 1) + yz[c >> 1]) % hs;
+	} else {
+#pragma unroll
+		for (int c = 0; c < 8; ++c) {
+			const uint32_t xx = gp[0] + (c & 1), k = c >> 1;
+			const uint32_t ed = xx + yz[k];
+			const uint32_t ew = min(ed, ed - hs);  // ed < 2 hs: the reference's % hashmap_size
+			A.e[c] = o0 + ((ew & dm) | ((xx ^ yz[k]) & (hs - 1u) & ~dm));
+		}
 	}
 }
 __device__ __forceinline__ void level_gather(const half_t* __restrict__ grid, const LevelAddr& A, uint32_t v[8]) {

@@ -46,6 +46,11 @@ __global__ void __launch_bounds__(256) k_adam_ema(AdamParams p, float* __restric
 	}
 }
 
+// EGradientMode::Accumulate of the operator modules: dst += src
+__global__ void k_add_f32(uint32_t n, const float* __restrict__ src, float* __restrict__ dst) {
+	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) dst[i] += src[i];
+}
+
 __global__ void k_cast_half(uint32_t n, const float* __restrict__ in, half_t* __restrict__ out) {
 	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) out[i] = (half_t)in[i];
 }
@@ -152,6 +157,9 @@ static inline uint32_t nblk(uint64_t n, uint32_t cap = 4096) { return (uint32_t)
 void launch_adam_ema(hipStream_t s, const AdamParams& p, float* weights_fp, half_t* weights_h, const float* grads, float* m1, float* m2,
                      uint32_t* steps, float* ema_tmp, half_t* ema_h) {
 	k_adam_ema<<<nblk(p.n, 8192), 256, 0, s>>>(p, weights_fp, weights_h, grads, m1, m2, steps, ema_tmp, ema_h);
+}
+void launch_add_f32(hipStream_t s, uint32_t n, const float* src, float* dst) {
+	if (n) k_add_f32<<<std::min<uint32_t>((n + 255) / 256, 8192), 256, 0, s>>>(n, src, dst);
 }
 void launch_cast_half(hipStream_t s, uint32_t n, const float* in, half_t* out) { k_cast_half<<<nblk(n), 256, 0, s>>>(n, in, out); }
 void launch_transpose_w(hipStream_t s, const TransposeJobs& jobs) { if (jobs.n) k_transpose_w<<<jobs.n, 256, 0, s>>>(jobs); }

@@ -8,6 +8,7 @@
 //   * fp32 gradients and master weights, fp16 weights for the kernels (the reference keeps fp16
 //     gradients), RCCL all-reduce of the gradient buffer for data parallelism over ray batches.
 #include "kernels.h"
+#include "json_lite.h"
 #include "../../include/neus2_hip.h"
 
 #include <rccl/rccl.h>
@@ -19,6 +20,7 @@
 #include <mutex>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <random>
 #include <stdexcept>
 #include <string>
@@ -178,6 +180,7 @@ struct NeusTestbed {
 	// deformed copies of the sample coordinates, dL/d(position) of the training batch
 	uint32_t cur_frame = 0, canonical_step = 0, delta_step = 0;
 	bool train_canonical = true, train_delta = false;
+	bool nonfinite = false, aborted = false;  // training health (consume_loss); cleared by reset_network
 	bool render_delta = false;     // prepare_for_test (testbed.cu:1987-1999): render / mesh through the DeltaNetwork
 	float near_distance = 0.f;     // nerf.training.near_distance: stored; the NeuS sampler does not read it (testbed_nerf.cu:1525)
 	int32_t color_space_when_linear = 0;  // color_space as set while linear_colors overrides it
@@ -319,10 +322,52 @@ struct NeusTestbed {
 	// ------------------------------------------------------------ network (reset_network, testbed.cu:2084-2349)
 	void reset_network(const NeusNetworkConfig& c, const float* geo) {
 		if (!have_data) throw std::runtime_error("reload_network: load training data first");
+		setup_network(c, geo);
+		alloc_step_workspace();
+	}
+
+	// initial parameters (trainer.h:54-109): seed_seq{seed} -> pcg32; xavier MLPs (the density MLP replaced by
+	// `geo` when given), hash grid U(-1e-4, 1e-4), variance 0.3
+	std::vector<float> initial_params(uint32_t seed, const float* geo) const {
+		const Layout& l = lay;
+		const uint32_t P = l.P;
+		std::vector<float> h(P, 0.f);
+		{
+			std::seed_seq seq{seed};
+			std::vector<uint32_t> seeds(2);
+			seq.generate(seeds.begin(), seeds.end());
+			pcg32 rnd = make_pcg32(seeds.front());
+			auto xavier = [&](uint32_t off, uint32_t out, uint32_t in) {
+				const float scale = std::sqrt(6.0f / (float)(in + out));
+				for (uint32_t i = 0; i < out * in; ++i) h[off + i] = rnd.next_float() * 2.0f * scale - scale;
+			};
+			xavier(l.off_d0, l.W, l.din); xavier(l.off_d1, 16, l.W);
+			if (geo) std::memcpy(h.data(), geo, sizeof(float) * l.n_density);
+			xavier(l.off_r0, l.W, 48); xavier(l.off_r1, l.W, l.W); xavier(l.off_r2, 16, l.W);
+			// grid: generate_random_uniform(rnd, n, -1e-4, 1e-4) (random.h:67-91; 128-thread blocks)
+			const size_t N = l.n_grid, per = 4, n_threads = (N + per - 1) / per, n_pad = (n_threads + 127) / 128 * 128;
+			for (size_t i = 0; i < n_pad; ++i) {
+				pcg32 r = rnd; r.advance((int64_t)(i * per));
+				for (size_t j = 0; j < per; ++j) {
+					const size_t idx = i + n_pad * j;
+					if (idx >= N) break;
+					h[l.grid_off + idx] = r.next_float() * (1e-4f - -1e-4f) + -1e-4f;
+				}
+			}
+			rnd.advance((int64_t)N);
+			for (int k = 0; k < 4; ++k) h[l.var_off + k] = 0.3f;  // nerf_network.h:881-882
+		}
+		return h;
+	}
+
+	// The network half of reset_network: config checks, grid tables, parameter layout and initial parameters, the
+	// fp16 / transposed weight copies and the workspace of one forward + backward over `batch` samples (encode,
+	// training MLP, weight gradients, grid scatter). The tcnn-shaped operator modules (neus_module_*) use only this.
+	void setup_network(const NeusNetworkConfig& c, const float* geo, bool with_mlp = true) {
 		if (c.n_features_per_level != 2) throw std::runtime_error("GridEncoding: only n_features_per_level = 2 is supported");
 		if (c.n_levels == 0 || c.n_levels > MAX_LEVELS) throw std::runtime_error("GridEncoding: 1..16 levels supported");
-		if (c.n_density_hidden != 1 || c.n_rgb_hidden != 2) throw std::runtime_error("NerfNetwork: density 1 hidden layer, rgb 2 hidden layers required on gfx950");
-		if (!mlp_supported(c.n_levels, c.n_neurons)) throw std::runtime_error("NerfNetwork: unsupported (n_levels, n_neurons) combination for the gfx950 MLP kernels");
+		if (with_mlp && (c.n_density_hidden != 1 || c.n_rgb_hidden != 2)) throw std::runtime_error("NerfNetwork: density 1 hidden layer, rgb 2 hidden layers required on gfx950");
+		if (with_mlp && !mlp_supported(c.n_levels, c.n_neurons)) throw std::runtime_error("NerfNetwork: unsupported (n_levels, n_neurons) combination for the gfx950 MLP kernels");
 		if (c.batch_size == 0 || c.batch_size % 128 != 0) throw std::runtime_error("batch_size must be a positive multiple of 128");
 		cfg = c;
 		// per_level_scale (testbed.cu:2184-2187), grid tables (grid.h:1466-1501)
@@ -363,33 +408,7 @@ struct NeusTestbed {
 		params_h.alloc(P); ema_h.alloc(P);
 		wT.alloc(l.din * l.W + l.W * 16 + 48 * l.W + l.W * l.W + l.W * 16 + 2 * l.din * l.W + 64);
 		wT_ema.alloc(wT.n);
-		// initial parameters (trainer.h:54-109): seed_seq{seed} -> pcg32
-		std::vector<float> h(P, 0.f);
-		{
-			std::seed_seq seq{c.seed};
-			std::vector<uint32_t> seeds(2);
-			seq.generate(seeds.begin(), seeds.end());
-			pcg32 rnd = make_pcg32(seeds.front());
-			auto xavier = [&](uint32_t off, uint32_t out, uint32_t in) {
-				const float scale = std::sqrt(6.0f / (float)(in + out));
-				for (uint32_t i = 0; i < out * in; ++i) h[off + i] = rnd.next_float() * 2.0f * scale - scale;
-			};
-			xavier(l.off_d0, l.W, l.din); xavier(l.off_d1, 16, l.W);
-			if (geo) std::memcpy(h.data(), geo, sizeof(float) * l.n_density);
-			xavier(l.off_r0, l.W, 48); xavier(l.off_r1, l.W, l.W); xavier(l.off_r2, 16, l.W);
-			// grid: generate_random_uniform(rnd, n, -1e-4, 1e-4) (random.h:67-91; 128-thread blocks)
-			const size_t N = l.n_grid, per = 4, n_threads = (N + per - 1) / per, n_pad = (n_threads + 127) / 128 * 128;
-			for (size_t i = 0; i < n_pad; ++i) {
-				pcg32 r = rnd; r.advance((int64_t)(i * per));
-				for (size_t j = 0; j < per; ++j) {
-					const size_t idx = i + n_pad * j;
-					if (idx >= N) break;
-					h[l.grid_off + idx] = r.next_float() * (1e-4f - -1e-4f) + -1e-4f;
-				}
-			}
-			rnd.advance((int64_t)N);
-			for (int k = 0; k < 4; ++k) h[l.var_off + k] = 0.3f;  // nerf_network.h:881-882
-		}
+		const std::vector<float> h = initial_params(c.seed, geo);
 		HIP_CHECK(hipMemcpy(params_fp.p, h.data(), (size_t)P * 4, hipMemcpyHostToDevice));
 		HIP_CHECK(hipMemset(m1.p, 0, (size_t)P * 4)); HIP_CHECK(hipMemset(m2.p, 0, (size_t)P * 4));
 		HIP_CHECK(hipMemset(ema_tmp.p, 0, (size_t)P * 4)); HIP_CHECK(hipMemset(adam_steps.p, 0, (size_t)P * 4));
@@ -403,21 +422,11 @@ struct NeusTestbed {
 		(void)rng.next_uint();  // tv_loss_rng
 		training_step = 0; adam_step = 0; lr_factor = 1.f; density_grid_ema_step = 0; enc_step = 0;
 		loss_ema_init = false; loss_scalar_ema = last_loss = ek_loss = mask_loss = 0.f; loss_pending = false;
-		// workspace
+		nonfinite = aborted = false;
+		// forward + backward workspace of one training batch
 		batch = c.batch_size;
 		max_samples = batch * 16;  // testbed_nerf.cu:3725
-		rays.alloc(6 * (size_t)MAX_RAYS); startt.alloc((size_t)MAX_RAYS);
-		march_rec.alloc((size_t)MAX_RAYS * NERF_STEPS); march_nrec.alloc(MAX_RAYS); march_queue.alloc(2);
-		march_seg.alloc((size_t)MAX_RAYS * MARCH_SEG_RECS);
-		mwork = MarchWork{march_rec.p, march_nrec.p, march_queue.p, march_waves(), march_seg.p, march_lanes()}; nreq.alloc(MAX_RAYS); base.alloc(MAX_RAYS);
-		numsteps.alloc(2 * (size_t)MAX_RAYS); ccount.alloc(MAX_RAYS); cbase.alloc(MAX_RAYS);
-		l_sa.alloc(max_samples); l_ekt.alloc(max_samples); sample_ray.alloc(max_samples);
-		l_ck4.alloc(max_samples / 8 + 1); l_cke.alloc(max_samples / 8 + 1);
-		l_racc.alloc(MAX_RAYS); l_rgr.alloc(MAX_RAYS); l_rT.alloc(MAX_RAYS);
-		loss.alloc(MAX_RAYS); ek.alloc(MAX_RAYS); mask.alloc(MAX_RAYS); loss_sum.alloc(4);
-		coords.alloc((size_t)max_samples * COORD_W); net_out.alloc((size_t)max_samples * OUT_W);
 		enc.alloc((size_t)l.L * batch); dydx.alloc((size_t)6 * l.L * batch);  // training batch only: inference fuses the encode
-		coords_c.alloc((size_t)batch * COORD_W); dL_dout.alloc((size_t)batch * OUT_W);
 		const size_t ld = batch, ld2 = 2 * ld;
 		const size_t tb_elems = (size_t)l.W * ld2 + (size_t)l.din * ld2 + 16 * ld2 + (size_t)l.W * ld2 + (size_t)l.W * ld + 48 * ld +
 		                        2 * (size_t)l.W * ld + 16 * ld + (size_t)l.W * ld + 2 * (size_t)l.L * ld * 2 + 64;
@@ -449,6 +458,24 @@ struct NeusTestbed {
 		swork.counts = sc_counts.p; swork.offs = sc_offs.p; swork.rec_g = sc_rec_g.p; swork.rec_i = sc_rec_i.p;
 		scan_tmp_bytes = std::max(scan_temp_bytes(MAX_RAYS), scan_temp_bytes((uint32_t)n_bins));
 		scan_tmp.alloc(scan_tmp_bytes + 256);
+		HIP_CHECK(hipStreamSynchronize(stream));
+	}
+
+	// The training-step half of reset_network: ray / march / loss / compaction buffers (per-step state sized for
+	// MAX_RAYS rays and 16 x batch samples), occupancy-update scratch, device counters, dynamic-scene state.
+	void alloc_step_workspace() {
+		rays.alloc(6 * (size_t)MAX_RAYS); startt.alloc((size_t)MAX_RAYS);
+		march_rec.alloc((size_t)MAX_RAYS * NERF_STEPS); march_nrec.alloc(MAX_RAYS); march_queue.alloc(2);
+		march_seg.alloc((size_t)MAX_RAYS * MARCH_SEG_RECS);
+		mwork = MarchWork{march_rec.p, march_nrec.p, march_queue.p, march_waves(), march_seg.p, march_lanes()}; nreq.alloc(MAX_RAYS); base.alloc(MAX_RAYS);
+		numsteps.alloc(2 * (size_t)MAX_RAYS); ccount.alloc(MAX_RAYS); cbase.alloc(MAX_RAYS);
+		l_sa.alloc(max_samples); l_ekt.alloc(max_samples); sample_ray.alloc(max_samples);
+		l_ck4.alloc(max_samples / 8 + 1); l_cke.alloc(max_samples / 8 + 1);
+		l_racc.alloc(MAX_RAYS); l_rgr.alloc(MAX_RAYS); l_rT.alloc(MAX_RAYS);
+		loss.alloc(MAX_RAYS); ek.alloc(MAX_RAYS); mask.alloc(MAX_RAYS); loss_sum.alloc(4);
+		coords.alloc((size_t)max_samples * COORD_W); net_out.alloc((size_t)max_samples * OUT_W);
+		coords_c.alloc((size_t)batch * COORD_W); dL_dout.alloc((size_t)batch * OUT_W);
+		const NeusNetworkConfig& c = cfg;
 		const uint32_t n_occ = GRID3 * (max_cascade + 1) * 2;
 		occ_pos.alloc(3 * (size_t)n_occ); occ_idx.alloc(n_occ); occ_density.alloc(n_occ);
 		// device step state (Counters, testbed.h:596-616)
@@ -1045,6 +1072,14 @@ struct NeusTestbed {
 		ray_loss = sst->n_rays_with_samples ? pinned[0] * (float)(sst->rays_per_batch * world) / (float)sst->n_rays_with_samples : 0.f;
 		if (!loss_ema_init) { loss_scalar_ema = last_loss; loss_ema_init = true; }
 		else loss_scalar_ema = 0.99f * loss_scalar_ema + 0.01f * last_loss;
+		// health: a non-finite loss sum (a NaN / Inf flag on the loss; the sums are all-reduced, so every
+		// rank raises it on the same step), and the zero-sample guard (testbed_nerf.cu:3542-3548: loss scalars 0,
+		// training stops - the Python frame() loop reads training_aborted)
+		if (!std::isfinite(pinned[0]) || !std::isfinite(pinned[1]) || !std::isfinite(pinned[2])) { nonfinite = true; aborted = true; }
+		if (sst->compacted_counter == 0) {
+			loss_scalar_ema = last_loss = ek_loss = mask_loss = 0.f;
+			aborted = true;
+		}
 		loss_pending = false;
 	}
 };
@@ -1103,6 +1138,8 @@ int neus_testbed_get_stats(NeusTestbed* tb, NeusTrainStats* o) {
 		o->ray_loss = tb->ray_loss; o->n_rays_with_samples = tb->last_rays_with_samples;
 		o->trained_samples_total = s.trained_total;
 		o->march_first_pass_rays = s.march_est; o->kept_ray_extent = s.kept_extent;
+		o->nonfinite_loss = tb->nonfinite ? 1u : 0u;
+		o->training_aborted = (tb->aborted || (tb->training_step > 0 && s.zero_records)) ? 1u : 0u;
 	});
 }
 static int copy_param_vec(NeusTestbed* tb, const float* dev, float* host, uint64_t n) {
@@ -1700,3 +1737,316 @@ int neus_mfma_probe(const uint16_t* A, const uint16_t* B, float* C) {
 }
 
 } // extern "C"
+
+// ============================================================ tcnn-shaped operator modules (cpp_api.h:66-110)
+// A module owns a private NeusTestbed core holding only the network half (setup_network): grid tables, parameter
+// layout, the fp16 / transposed weight copies the kernels read and one batch of forward / backward workspace. The
+// parameters come in through the explicit `params` pointer of every call (copied into the core's fp16 buffer and
+// re-prepared), as tcnn::cpp::Module does; gradients leave through dL_dparams with EGradientMode semantics
+// (object.h:90-94). Kinds: the NeuS NerfNetwork (nerf_network.h: encoding + density MLP + rgb MLP + variance,
+// input NerfCoordinate [n][7] f32, output [n][16] fp16) and the HashGrid encoding (grid.h, input [n][3] f32, output
+// [L][n] half2 = features 2l, 2l+1 of level l adjacent).
+namespace {
+
+NeusNetworkConfig module_config(const JsonValue& enc, const JsonValue& net, const JsonValue& rgb, uint32_t batch) {
+	NeusNetworkConfig c{};
+	const uint32_t nf = (uint32_t)enc.number("n_features_per_level", 2);
+	c.n_levels = enc.number("n_features", 0) > 0 ? (uint32_t)enc.number("n_features", 0) / nf : (uint32_t)enc.number("n_levels", 16);
+	c.n_features_per_level = nf;
+	c.log2_hashmap_size = (uint32_t)enc.number("log2_hashmap_size", 15);
+	c.base_resolution = (uint32_t)enc.number("base_resolution", 0);
+	if (!c.base_resolution) c.base_resolution = 1u << (c.log2_hashmap_size / 3);
+	c.per_level_scale = (float)enc.number("per_level_scale", 0.0);
+	c.top_resolution = (float)enc.number("top_resolution", 2048.0);
+	c.valid_level_scale = (float)enc.number("valid_level_scale", 0.02);
+	c.base_valid_level_scale = (float)enc.number("base_valid_level_scale", 0.2);
+	c.base_training_step = (uint32_t)enc.number("base_training_step", 100);
+	c.n_neurons = (uint32_t)net.number("n_neurons", 64);
+	if ((uint32_t)rgb.number("n_neurons", c.n_neurons) != c.n_neurons) throw std::runtime_error("density and rgb networks must share n_neurons");
+	c.n_density_hidden = (uint32_t)net.number("n_hidden_layers", 1);
+	c.n_rgb_hidden = (uint32_t)rgb.number("n_hidden_layers", 2);
+	c.batch_size = batch;
+	c.sdf_bias = -0.1f;
+	c.seed = 1337;
+	return c;
+}
+
+struct StreamSwap {  // run a call's launches on the caller's stream (NULL: the null stream, as tcnn's cudaStream_t 0)
+	NeusTestbed& t; hipStream_t saved;
+	StreamSwap(NeusTestbed& tb, void* s) : t(tb), saved(tb.stream) { t.stream = (hipStream_t)s; }
+	~StreamSwap() { t.stream = saved; }
+};
+
+}  // namespace
+
+struct NeusContext {
+	uint32_t n = 0;
+	Dev<float> dydx;  // encoding: dy/dx [6L][n] of the forward (prepare_input_gradients)
+};
+
+struct NeusModule {
+	enum Kind { Network = 0, Encoding = 1 } kind;
+	NeusTestbed core;
+	uint32_t capacity = 0, n_in = 0, n_out = 0;
+	int training_step = 0;              // GridEncoding::set_training_step (grid.h:2427-2437): 0 = every level
+	uint32_t indeed_batch = 0;          // NeuS backward normalisation of the eikonal entries; 0 = the call's n
+	std::string hyper;
+	Dev<float> gtmp;                    // gradients of an Accumulate call
+	Dev<float4> dpos, v4;
+	Dev<half_t> zero_h;
+	Dev<float4> zero_v;
+	explicit NeusModule(int device) : core(device) {}
+	uint64_t n_params() const { return kind == Network ? core.lay.P : core.lay.n_grid; }
+	uint32_t valid() const { return core.valid_level_at(training_step); }
+	void load_params(const void* params, hipStream_t s) {
+		if (!params) throw std::runtime_error("module: null params");
+		if (kind == Network) {
+			HIP_CHECK(hipMemcpyAsync(core.params_h.p, params, (size_t)core.lay.P * 2, hipMemcpyDeviceToDevice, s));
+			core.prepare_weights();
+		} else {
+			HIP_CHECK(hipMemcpyAsync(core.params_h.p + core.lay.grid_off, params, (size_t)core.lay.n_grid * 2, hipMemcpyDeviceToDevice, s));
+		}
+	}
+	void check_n(uint32_t n, bool backward) const {
+		if (n > capacity) throw std::runtime_error("module: n_elements exceeds the module's batch capacity");
+		if (backward && kind == Network && (n == 0 || n % 128 != 0))
+			throw std::runtime_error("module backward: n_elements must be a positive multiple of 128 (fully_fused_mlp.cu:779-781)");
+	}
+	// the destination of this call's parameter gradients (Overwrite: dL_dparams itself; Accumulate: a scratch buffer)
+	float* grad_target(void* dL_dparams, int mode) {
+		if (mode == NEUS_GRADIENT_IGNORE) return nullptr;
+		if (!dL_dparams) throw std::runtime_error("module: dL_dparams is null with a gradient mode other than Ignore");
+		if (mode == NEUS_GRADIENT_OVERWRITE) return (float*)dL_dparams;
+		if (mode != NEUS_GRADIENT_ACCUMULATE) throw std::runtime_error("module: unknown gradient mode");
+		return gtmp.p;
+	}
+	void finish_grad(void* dL_dparams, int mode, hipStream_t s) {
+		if (mode == NEUS_GRADIENT_ACCUMULATE) launch_add_f32(s, (uint32_t)n_params(), gtmp.p, (float*)dL_dparams);
+	}
+};
+
+static void module_common_init(NeusModule* m, uint32_t capacity) {
+	m->capacity = capacity;
+	const size_t P = m->n_params();
+	m->gtmp.alloc(P);
+	m->dpos.alloc(capacity); m->v4.alloc(capacity);
+	m->zero_h.alloc((size_t)2 * m->core.lay.L * capacity); m->zero_v.alloc(capacity);
+	HIP_CHECK(hipMemset(m->zero_h.p, 0, m->zero_h.n * sizeof(half_t)));
+	HIP_CHECK(hipMemset(m->zero_v.p, 0, m->zero_v.n * sizeof(float4)));
+	HIP_CHECK(hipStreamSynchronize(m->core.stream));
+}
+
+int neus_module_create_network(const char* config_json, uint32_t batch_capacity, NeusModule** out) {
+	return guard([&] {
+		if (!config_json || !out) throw std::runtime_error("neus_module_create_network: null argument");
+		if (batch_capacity == 0 || batch_capacity % 128 != 0 || batch_capacity > (1u << 24))
+			throw std::runtime_error("batch_capacity must be a positive multiple of 128 (<= 2^24)");
+		const JsonValue j = parse_json(config_json);
+		int dev = 0;
+		HIP_CHECK(hipGetDevice(&dev));
+		auto m = std::make_unique<NeusModule>(dev);
+		m->kind = NeusModule::Network;
+		m->core.setup_network(module_config(j.object("encoding"), j.object("network"), j.object("rgb_network"), batch_capacity), nullptr);
+		m->n_in = COORD_W; m->n_out = OUT_W;
+		const NeusNetworkConfig& c = m->core.cfg;
+		m->hyper = "{\"otype\": \"NerfNetwork\", \"n_levels\": " + std::to_string(c.n_levels) + ", \"n_neurons\": " + std::to_string(c.n_neurons) +
+		           ", \"log2_hashmap_size\": " + std::to_string(c.log2_hashmap_size) + ", \"per_level_scale\": " + std::to_string(c.per_level_scale) + "}";
+		module_common_init(m.get(), batch_capacity);
+		*out = m.release();
+	});
+}
+
+int neus_module_create_encoding(uint32_t n_input_dims, const char* encoding_json, uint32_t batch_capacity, NeusModule** out) {
+	return guard([&] {
+		if (!encoding_json || !out) throw std::runtime_error("neus_module_create_encoding: null argument");
+		if (n_input_dims != 3) throw std::runtime_error("HashGrid module: n_input_dims must be 3");
+		if (batch_capacity == 0 || batch_capacity % 128 != 0 || batch_capacity > (1u << 24))
+			throw std::runtime_error("batch_capacity must be a positive multiple of 128 (<= 2^24)");
+		const JsonValue j = parse_json(encoding_json);
+		const std::string ot = j.string("otype", "HashGrid");
+		if (ot != "HashGrid" && ot != "Grid") throw std::runtime_error("encoding module: only HashGrid is implemented on gfx950");
+		int dev = 0;
+		HIP_CHECK(hipGetDevice(&dev));
+		auto m = std::make_unique<NeusModule>(dev);
+		m->kind = NeusModule::Encoding;
+		JsonValue none; none.kind = JsonValue::Object;
+		m->core.setup_network(module_config(j, none, none, batch_capacity), nullptr, false);
+		m->n_in = 3; m->n_out = 2 * m->core.lay.L;
+		const NeusNetworkConfig& c = m->core.cfg;
+		m->hyper = "{\"otype\": \"HashGrid\", \"n_levels\": " + std::to_string(c.n_levels) + ", \"n_features_per_level\": 2, \"log2_hashmap_size\": " +
+		           std::to_string(c.log2_hashmap_size) + ", \"base_resolution\": " + std::to_string(c.base_resolution) + ", \"per_level_scale\": " +
+		           std::to_string(c.per_level_scale) + "}";
+		module_common_init(m.get(), batch_capacity);
+		*out = m.release();
+	});
+}
+
+int neus_module_destroy(NeusModule* m) { return guard([&] { delete m; }); }
+int neus_context_destroy(NeusContext* c) { return guard([&] { delete c; }); }
+
+int neus_module_info(const NeusModule* m, NeusModuleInfo* o) {
+	return guard([&] {
+		if (!m || !o) throw std::runtime_error("neus_module_info: null argument");
+		o->n_params = m->n_params();
+		o->n_input_dims = m->n_in;
+		o->n_output_dims = m->n_out;
+		o->param_precision = NEUS_PRECISION_FP16;
+		o->output_precision = NEUS_PRECISION_FP16;
+		o->gradient_precision = NEUS_PRECISION_FP32;
+		o->batch_capacity = m->capacity;
+		o->n_levels = m->core.lay.L;
+		o->grid_offset = m->kind == NeusModule::Network ? m->core.lay.grid_off : 0;
+		o->per_level_scale = m->core.cfg.per_level_scale;
+	});
+}
+
+int neus_module_hyperparams(const NeusModule* m, char* buf, uint64_t cap, uint64_t* len) {
+	return guard([&] {
+		if (!m) throw std::runtime_error("neus_module_hyperparams: null module");
+		if (len) *len = m->hyper.size();
+		if (buf && cap) { const size_t k = std::min<size_t>(cap - 1, m->hyper.size()); std::memcpy(buf, m->hyper.data(), k); buf[k] = 0; }
+	});
+}
+
+int neus_module_set_training_step(NeusModule* m, int training_step) { return guard([&] { m->training_step = training_step; }); }
+int neus_module_set_indeed_batch_size(NeusModule* m, uint32_t n) { return guard([&] { m->indeed_batch = n; }); }
+
+int neus_module_initialize_params(NeusModule* m, uint64_t seed, float* params_full_precision) {
+	return guard([&] {
+		if (!m || !params_full_precision) throw std::runtime_error("neus_module_initialize_params: null argument");
+		HIP_CHECK(hipSetDevice(m->core.device));
+		std::vector<float> h;
+		if (m->kind == NeusModule::Network) {
+			h = m->core.initial_params((uint32_t)seed, nullptr);
+		} else {  // a standalone GridEncoding draws from a fresh seed_seq{seed} generator (grid.h initialize_params)
+			h.assign(m->core.lay.n_grid, 0.f);
+			std::seed_seq seq{(uint32_t)seed};
+			std::vector<uint32_t> seeds(2);
+			seq.generate(seeds.begin(), seeds.end());
+			pcg32 rnd = make_pcg32(seeds.front());
+			const size_t N = h.size(), per = 4, n_threads = (N + per - 1) / per, n_pad = (n_threads + 127) / 128 * 128;
+			for (size_t i = 0; i < n_pad; ++i) {
+				pcg32 r = rnd; r.advance((int64_t)(i * per));
+				for (size_t k = 0; k < per; ++k) {
+					const size_t idx = i + n_pad * k;
+					if (idx >= N) break;
+					h[idx] = r.next_float() * (1e-4f - -1e-4f) + -1e-4f;
+				}
+			}
+		}
+		HIP_CHECK(hipMemcpy(params_full_precision, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+	});
+}
+
+static void module_forward(NeusModule* m, hipStream_t s, uint32_t n, const float* input, void* output, const void* params, NeusContext* ctx) {
+	if (!input || !output) throw std::runtime_error("module forward: null input / output");
+	m->check_n(n, false);
+	m->load_params(params, s);
+	NeusTestbed& t = m->core;
+	if (m->kind == NeusModule::Network) {
+		t.net_forward(nullptr, n, n, input, m->valid(), (half_t*)output, s);
+	} else {
+		float* dydx = nullptr;
+		if (ctx) { ctx->dydx.alloc((size_t)6 * t.lay.L * std::max(1u, n)); dydx = ctx->dydx.p; }
+		const uint32_t gx = std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, 4096));
+		launch_grid_encode(s, nullptr, n, n, input, 3, t.gl, m->valid(), t.params_h.p + t.lay.grid_off, (uint32_t*)output, dydx, gx);
+	}
+	HIP_CHECK(hipGetLastError());
+}
+
+int neus_module_inference(NeusModule* m, void* stream, uint32_t n, const float* input, void* output, const void* params) {
+	return guard([&] {
+		HIP_CHECK(hipSetDevice(m->core.device));
+		StreamSwap sw(m->core, stream);
+		module_forward(m, m->core.stream, n, input, output, params, nullptr);
+	});
+}
+
+int neus_module_forward(NeusModule* m, void* stream, uint32_t n, const float* input, void* output, const void* params,
+                        int prepare_input_gradients, NeusContext** ctx_out) {
+	return guard([&] {
+		if (!ctx_out) throw std::runtime_error("neus_module_forward: null context output");
+		HIP_CHECK(hipSetDevice(m->core.device));
+		StreamSwap sw(m->core, stream);
+		auto ctx = std::make_unique<NeusContext>();
+		ctx->n = n;
+		// the network's backward recomputes its forward; the encoding keeps dy/dx for dL_dinput and second order
+		(void)prepare_input_gradients;
+		module_forward(m, m->core.stream, n, input, output, params, m->kind == NeusModule::Encoding ? ctx.get() : nullptr);
+		*ctx_out = ctx.release();
+	});
+}
+
+int neus_module_backward(NeusModule* m, void* stream, const NeusContext* ctx, uint32_t n, float* dL_dinput, const void* dL_doutput,
+                         void* dL_dparams, const float* input, const void* output, const void* params, int gradient_mode) {
+	return guard([&] {
+		(void)output;
+		if (!ctx || ctx->n != n) throw std::runtime_error("module backward: the context is not from a forward over n_elements");
+		if (!input || !dL_doutput) throw std::runtime_error("module backward: null input / dL_doutput");
+		m->check_n(n, true);
+		HIP_CHECK(hipSetDevice(m->core.device));
+		StreamSwap sw(m->core, stream);
+		NeusTestbed& t = m->core;
+		hipStream_t s = t.stream;
+		float* g = m->grad_target(dL_dparams, gradient_mode);
+		if (!g && !dL_dinput) return;
+		m->load_params(params, s);
+		const uint32_t valid = m->valid();
+		if (m->kind == NeusModule::Network) {
+			// NerfNetwork::backward (nerf_network.h:330-601): first and second order in one pass; the Testbed's
+			// forward-recompute + backward writes every parameter gradient (Overwrite) into g
+			float* gg = g ? g : m->gtmp.p;
+			HIP_CHECK(hipMemsetAsync(gg, 0, (size_t)t.lay.P * 4, s));
+			const float saved = t.tbuf.indeed_batch;
+			t.tbuf.indeed_batch = (float)(m->indeed_batch ? m->indeed_batch : n);
+			t.tbuf.dpos = dL_dinput ? m->dpos.p : nullptr;
+			t.net_backward(nullptr, nullptr, n, input, valid, (const half_t*)dL_doutput, gg, s);
+			t.tbuf.dpos = nullptr;
+			t.tbuf.indeed_batch = saved;
+			if (dL_dinput) {  // position columns; dt and direction columns are 0 (the direction gradient is not propagated)
+				HIP_CHECK(hipMemset2DAsync(dL_dinput, COORD_W * 4, 0, COORD_W * 4, n, s));
+				HIP_CHECK(hipMemcpy2DAsync(dL_dinput, COORD_W * 4, m->dpos.p, 16, 12, n, hipMemcpyDeviceToDevice, s));
+			}
+		} else {
+			if (dL_dinput) {
+				if (!ctx->dydx.p) throw std::runtime_error("encoding backward: dL_dinput needs the forward's dy/dx");
+				launch_enc_input_grad(s, n, n, t.lay.L, (const half_t*)dL_doutput, ctx->dydx.p, dL_dinput, 3);
+			}
+			if (g)  // kernel_grid_backward (grid.h:371-500) through the fused binned scatter, second-order term zero
+				launch_grid_scatter(s, nullptr, n, n, input, 3, t.gl, valid, (const half_t*)dL_doutput, m->zero_h.p, m->zero_v.p, g, t.swork,
+				                    t.scan_tmp.p, t.scan_tmp_bytes);
+		}
+		if (g) m->finish_grad(dL_dparams, gradient_mode, s);
+		HIP_CHECK(hipGetLastError());
+	});
+}
+
+int neus_module_backward_backward_input(NeusModule* m, void* stream, const NeusContext* ctx, uint32_t n, const float* dL_ddLdinput,
+                                        const float* input, const void* dL_doutput, void* dL_dparams, void* dL_ddLdoutput, float* dL_dinput,
+                                        const void* params, int gradient_mode) {
+	return guard([&] {
+		if (m->kind == NeusModule::Network)
+			throw std::runtime_error("NerfNetwork: the eikonal second-order term is part of backward (nerf_network.h:330-601); "
+			                         "backward_backward_input is provided by the HashGrid encoding module");
+		if (dL_dinput) throw std::runtime_error("HashGrid backward_backward_input: dL_dinput (second derivative in x) is not provided");
+		if (!ctx || ctx->n != n || !ctx->dydx.p) throw std::runtime_error("backward_backward_input: needs the forward's context (dy/dx)");
+		if (!input || !dL_ddLdinput || !dL_doutput) throw std::runtime_error("backward_backward_input: null input");
+		m->check_n(n, true);
+		HIP_CHECK(hipSetDevice(m->core.device));
+		StreamSwap sw(m->core, stream);
+		NeusTestbed& t = m->core;
+		hipStream_t s = t.stream;
+		float* g = m->grad_target(dL_dparams, gradient_mode);
+		// dL_ddLdoutput (kernel_grid_backward_input_backward_dLdoutput) and dL_ddLdinput as float4 for the scatter
+		launch_enc_ddLdoutput(s, n, n, t.lay.L, dL_ddLdinput, ctx->dydx.p, (half_t*)dL_ddLdoutput, m->v4.p);
+		if (g) {
+			m->load_params(params, s);
+			// kernel_grid_backward_input_backward_grid (grid.h:880-1007): the fused scatter's second-order term with
+			// g = dL_doutput, v = dL_ddLdinput, first-order term zero
+			launch_grid_scatter(s, nullptr, n, n, input, 3, t.gl, m->valid(), m->zero_h.p, (const half_t*)dL_doutput, m->v4.p, g, t.swork,
+			                    t.scan_tmp.p, t.scan_tmp_bytes);
+			m->finish_grad(dL_dparams, gradient_mode, s);
+		}
+		HIP_CHECK(hipGetLastError());
+	});
+}

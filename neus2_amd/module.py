@@ -1,0 +1,149 @@
+"""tcnn-shaped operator modules over the gfx950 kernels (include/neus2_hip.h neus_module_*), mirroring
+tiny-cuda-nn's C++ API (dependencies/my_tcnn/include/tiny-cuda-nn/cpp_api.h:66-110) the reference's bindings wrap:
+create_network / create_encoding, n_params, initialize_params, inference, forward (-> Context), backward,
+backward_backward_input with explicit parameter pointers and EGradientMode (object.h:90-94).
+
+Arguments are torch CUDA tensors (device memory + the current stream); outputs are allocated here unless given.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import enum
+import json
+
+from ._lib import NeusError, NeusModuleInfo, check, lib
+
+
+class GradientMode(enum.IntEnum):
+    Ignore = 0
+    Overwrite = 1
+    Accumulate = 2
+
+
+def _p(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _stream():
+    import torch
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+class Context:
+    def __init__(self, h, n):
+        self._h, self.n = h, n
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().neus_context_destroy(self._h)
+            self._h = None
+
+
+class Module:
+    """tcnn::cpp::Module. kind 'network' = the NeuS NerfNetwork (input [n, 7] f32, output [n, 16] fp16),
+    'encoding' = the HashGrid encoding (input [n, 3] f32, output [L, n] half2 -> tensor [L, n, 2] fp16)."""
+
+    def __init__(self, handle, kind):
+        self._h, self.kind = handle, kind
+        info = NeusModuleInfo()
+        check(lib().neus_module_info(self._h, C.byref(info)))
+        self.info = {k: getattr(info, k) for k, _ in info._fields_}
+
+    @classmethod
+    def create_network(cls, config, batch_capacity=1 << 18):
+        """create_network_with_input_encoding for the NeuS network: `config` is the configs/nerf/*.json object
+        (or its text) with "encoding", "network" and "rgb_network"."""
+        text = config if isinstance(config, str) else json.dumps(config)
+        h = C.c_void_p()
+        check(lib().neus_module_create_network(text.encode(), C.c_uint32(batch_capacity), C.byref(h)))
+        return cls(h, "network")
+
+    @classmethod
+    def create_encoding(cls, encoding, batch_capacity=1 << 18, n_input_dims=3):
+        text = encoding if isinstance(encoding, str) else json.dumps(encoding)
+        h = C.c_void_p()
+        check(lib().neus_module_create_encoding(C.c_uint32(n_input_dims), text.encode(), C.c_uint32(batch_capacity), C.byref(h)))
+        return cls(h, "encoding")
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().neus_module_destroy(self._h)
+            self._h = None
+
+    @property
+    def n_params(self):
+        return int(self.info["n_params"])
+
+    @property
+    def n_input_dims(self):
+        return int(self.info["n_input_dims"])
+
+    @property
+    def n_output_dims(self):
+        return int(self.info["n_output_dims"])
+
+    def hyperparams(self):
+        n = C.c_uint64()
+        check(lib().neus_module_hyperparams(self._h, None, C.c_uint64(0), C.byref(n)))
+        buf = C.create_string_buffer(n.value + 1)
+        check(lib().neus_module_hyperparams(self._h, buf, C.c_uint64(n.value + 1), None))
+        return json.loads(buf.value.decode())
+
+    def name(self):
+        return self.hyperparams()["otype"]
+
+    def set_training_step(self, step: int):
+        check(lib().neus_module_set_training_step(self._h, C.c_int(int(step))))
+
+    def set_indeed_batch_size(self, n: int):
+        check(lib().neus_module_set_indeed_batch_size(self._h, C.c_uint32(int(n))))
+
+    def initialize_params(self, seed=1337):
+        import torch
+        out = torch.empty(self.n_params, dtype=torch.float32, device="cuda")
+        check(lib().neus_module_initialize_params(self._h, C.c_uint64(seed), _p(out)))
+        return out
+
+    def _out(self, n, output):
+        import torch
+        if output is not None:
+            return output
+        if self.kind == "network":
+            return torch.empty((n, 16), dtype=torch.float16, device="cuda")
+        return torch.empty((self.info["n_levels"], n, 2), dtype=torch.float16, device="cuda")
+
+    def inference(self, x, params, output=None):
+        n = x.shape[0]
+        out = self._out(n, output)
+        check(lib().neus_module_inference(self._h, _stream(), C.c_uint32(n), _p(x), _p(out), _p(params)))
+        return out
+
+    def forward(self, x, params, prepare_input_gradients=False, output=None):
+        n = x.shape[0]
+        out = self._out(n, output)
+        h = C.c_void_p()
+        check(lib().neus_module_forward(self._h, _stream(), C.c_uint32(n), _p(x), _p(out), _p(params),
+                                        C.c_int(int(bool(prepare_input_gradients))), C.byref(h)))
+        return Context(h, n), out
+
+    def backward(self, ctx, x, dL_doutput, params, dL_dparams=None, dL_dinput=None, mode=GradientMode.Overwrite, output=None):
+        check(lib().neus_module_backward(self._h, _stream(), ctx._h, C.c_uint32(ctx.n), _p(dL_dinput), _p(dL_doutput), _p(dL_dparams),
+                                         _p(x), _p(output), _p(params), C.c_int(int(mode))))
+        return dL_dparams, dL_dinput
+
+    def backward_backward_input(self, ctx, x, dL_ddLdinput, dL_doutput, params, dL_dparams=None, dL_ddLdoutput=None,
+                                mode=GradientMode.Overwrite):
+        if self.kind != "encoding":
+            raise NeusError("backward_backward_input: the NerfNetwork's second order is inside backward")
+        check(lib().neus_module_backward_backward_input(self._h, _stream(), ctx._h, C.c_uint32(ctx.n), _p(dL_ddLdinput), _p(x),
+                                                        _p(dL_doutput), _p(dL_dparams), _p(dL_ddLdoutput), None, _p(params),
+                                                        C.c_int(int(mode))))
+        return dL_dparams, dL_ddLdoutput
+
+
+def create_network(config, batch_capacity=1 << 18):
+    return Module.create_network(config, batch_capacity)
+
+
+def create_encoding(encoding, batch_capacity=1 << 18, n_input_dims=3):
+    return Module.create_encoding(encoding, batch_capacity, n_input_dims)

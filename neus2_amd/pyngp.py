@@ -741,6 +741,12 @@ class Testbed:
                 self.shall_train = False
                 return False
         self.train_steps(1)
+        st = self.stats()
+        if st["training_aborted"]:
+            # testbed_nerf.cu:3542-3548 (0 compacted samples: "Aborting training"), or a non-finite loss
+            import warnings
+            warnings.warn("NeuS training generated 0 samples or a non-finite loss; aborting training")
+            self.shall_train = False
         return True
 
     # ------------------------------------------------------------------ camera (testbed.cu:238-285, 1830-1844, 2738-2746)

@@ -128,3 +128,39 @@ def test_snapshot_optimizer_state_round_trip(tmp_path, torch_cuda):
     tb.save_snapshot(p2)
     tb3.load_snapshot(p2)
     assert tb3.get_optimizer_state()["current_step"] == 0 and not tb3.get_optimizer_state()["m1"].any()
+
+
+def test_zero_sample_and_nonfinite_guards(torch_cuda):
+    """The zero-sample guard (testbed_nerf.cu:3542-3548): cameras that look away from the aabb give no training
+    samples -> loss scalars 0, training_aborted, and frame() stops training. A NaN in the colour network -> the
+    logged loss sum is non-finite -> nonfinite_loss and training_aborted (SURVEY §5 health flag)."""
+    import warnings
+    from neus2_amd import pyngp, scenes
+    sc = scenes.small_scene(n_views=4, width=32, height=24)
+    away = []
+    for k in range(4):
+        m = np.zeros((3, 4), np.float32)
+        m[:, 0], m[:, 1], m[:, 2] = (1, 0, 0), (0, -1, 0), (0, 0, 1)  # looking along +z
+        m[:, 3] = (0.5 + 0.1 * k, 0.5, 3.0)                            # from beyond z = 1
+        away.append(m)
+    tb = pyngp.Testbed(pyngp.TestbedMode.Nerf)
+    tb.set_dataset(sc["images"], sc["focal"], sc["principal"], away, 1)
+    tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=4096)
+    with warnings.catch_warnings(record=True):
+        warnings.simplefilter("always")
+        assert tb.frame() is True
+    st = tb.stats()
+    assert st["measured_batch_size"] == 0 and st["training_aborted"] == 1 and st["loss"] == 0.0
+    assert tb.shall_train is False and tb.frame() is False
+    tb2 = pyngp.Testbed(pyngp.TestbedMode.Nerf)
+    tb2.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
+    tb2.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=4096)
+    tb2.train_steps(1)
+    assert tb2.stats()["training_aborted"] == 0 and tb2.stats()["nonfinite_loss"] == 0
+    p = tb2.get_params()
+    lay = tb2.layout()
+    p[lay["n_density"]:lay["n_matrix"]] = np.nan
+    tb2.set_params(p)
+    tb2.train_steps(16)  # the next logged step (every 16th)
+    st2 = tb2.stats()
+    assert st2["nonfinite_loss"] == 1 and st2["training_aborted"] == 1

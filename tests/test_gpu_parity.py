@@ -136,6 +136,31 @@ def test_network_forward_parity(env):
         assert np.median(err) < 1e-3
 
 
+def test_network_forward_outside_unit_cube(env):
+    """Positions outside [0,1]^3 (a DeltaNetwork-moved sample, a grid point past the aabb): the dense levels' corner
+    index wraps with the reference's `% hashmap_size` (grid.h:118-153), also for negative cells (huge unsigned
+    values) - the fused kernel's in-cube shortcut must not be taken there. Forward within the tolerance of
+    test_network_forward_parity against the oracle."""
+    t, O, tb = env["t"], env["O"], env["tb"]
+    lib, check = L()
+    n = 2048
+    c = _coords(n, 21)
+    rng = np.random.default_rng(22)
+    c[:, :3] = rng.uniform(-0.4, 1.4, (n, 3)).astype(np.float32)
+    c[:8, :3] = np.float32([[-1e-3, 0.5, 0.5], [1.0, 1.0, 1.0], [-2.5, 3.0, 0.2], [0.5, -0.75, 1.9],
+                            [1.0 - 1e-7, 0.0, 0.0], [0.0, 0.0, 0.0], [7.0, -7.0, 0.5], [0.25, 0.5, -1e-6]])
+    params = _perturbed(env, 23)
+    out = t.zeros((n, 16), dtype=t.int16, device="cuda")
+    check(lib.neus_net_forward(tb.handle, None, C.c_uint32(n), ptr(dev(t, c)), C.c_uint32(14), ptr(out)))
+    t.cuda.synchronize()
+    got = host(out, np.float16).astype(np.float32)
+    ref = O.network_forward(env["cfg"], params, c, 14).view(np.float16).astype(np.float32)
+    err = np.abs(got[:, :11] - ref[:, :11])
+    ok = np.all(err <= 2e-3 + 4e-3 * np.abs(ref[:, :11]), axis=1)
+    record("forward_outside_cube", frac_within_tol=ok.mean(), median_abs_err=np.median(err))
+    assert ok.mean() >= 0.995 and np.median(err) < 1e-3, ok.mean()
+
+
 def test_network_backward_parity(env):
     """First + second order parameter gradients: cosine >= 0.999 per block, rel-L2 <= 2e-2."""
     t, O, tb = env["t"], env["O"], env["tb"]
