@@ -55,6 +55,8 @@ def parse():
     p.add_argument("--psnr-steps", type=int, default=20000)
     # config 5: marching cubes at mc_res^3 over the PSNR leg's trained model (0 = skip)
     p.add_argument("--mc-res", type=int, default=1024)
+    # BASELINE.json words config 2 as a 16-level grid (the reference's base.json has 14): the same step at L=16
+    p.add_argument("--l16", type=int, default=1)
     return p.parse_args()
 
 
@@ -184,6 +186,8 @@ def main():
         "loss": st["ray_loss"],
         "warmup_s": warm_s,
     }
+    if world == 1 and args.l16:
+        out["levels16"] = l16_leg(sc, args)
     if world == 1 and args.psnr_steps > 0:
         del tb
         out["psnr"], tb2 = psnr_leg(sc, args.psnr_steps)
@@ -197,6 +201,32 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+
+
+def l16_leg(sc, args):
+    """The timed step of the main measurement with a 16-level hash grid (base.json otherwise): same data, batch,
+    rays and warmup / steps, wall clock between synchronised points."""
+    from neus2_amd import config, pyngp
+    cfg = config.load_json(os.path.join(ROOT, "configs", "nerf", "base.json"))
+    cfg["encoding"]["n_levels"] = 16
+    tb = pyngp.Testbed(pyngp.TestbedMode.Nerf)
+    tb.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
+    tb.reload_network_from_json(cfg, batch_size=args.batch, fixed_rays_per_batch=args.rays)
+    tb.train_steps(args.warmup)
+    tb.synchronize()
+    t = time.perf_counter()
+    tb.train_steps(args.steps)
+    tb.synchronize()
+    dt = time.perf_counter() - t
+    st = tb.stats()
+    levels = min(st["valid_level"] + 1, 16)
+    inf_ms, inf_units = tb.time_kernel(3, 9)
+    g = 8 * levels * 4
+    del tb
+    return {"value": args.batch * args.steps / dt, "unit": "samples/s", "ms_per_step": dt / args.steps * 1e3,
+            "levels_active": levels,
+            "inference": {"ms": round(inf_ms, 4), "units": inf_units,
+                          "achieved_GBs": round((28 + g + 32) * inf_units / (inf_ms * 1e-3) / 1e9, 1)}}
 
 
 def psnr_leg(sc, n_steps):

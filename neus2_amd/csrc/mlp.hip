@@ -560,7 +560,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))
 			f16v acc = zero16();
 #pragma unroll
 			for (int ks = 0; ks < DKS; ++ks) acc = mfma(loadA(w.d0, W, 32 * mt + r, 16 * ks, h), dinB[ks], acc);
-			H0B[2 * mt] = frag<true>(acc, 0); H0B[2 * mt + 1] = frag<true>(acc, 1);
+			H0B[2 * mt] = frag<true>(acc, 0);
+			if (2 * mt + 1 < HKS) H0B[2 * mt + 1] = frag<true>(acc, 1);  // W = 16: one 16-row half
 		}
 		h8 D1B;
 		{
@@ -620,14 +621,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))
 			f16v acc = zero16();
 #pragma unroll
 			for (int ks = 0; ks < 3; ++ks) acc = mfma(loadA(w.r0, W, 32 * mt + r, 16 * ks, h), rinB[ks], acc);
-			H1B[2 * mt] = frag<true>(acc, 0); H1B[2 * mt + 1] = frag<true>(acc, 1);
+			H1B[2 * mt] = frag<true>(acc, 0);
+			if (2 * mt + 1 < HKS) H1B[2 * mt + 1] = frag<true>(acc, 1);  // W = 16: one 16-row half
 		}
 #pragma unroll
 		for (int mt = 0; mt < MT; ++mt) {
 			f16v acc = zero16();
 #pragma unroll
 			for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.r1, W, 32 * mt + r, 16 * ks, h), H1B[ks], acc);
-			H2B[2 * mt] = frag<true>(acc, 0); H2B[2 * mt + 1] = frag<true>(acc, 1);
+			H2B[2 * mt] = frag<true>(acc, 0);
+			if (2 * mt + 1 < HKS) H2B[2 * mt + 1] = frag<true>(acc, 1);  // W = 16: one 16-row half
 		}
 		f16v O = zero16();
 #pragma unroll
@@ -732,7 +735,8 @@ __global__ void __launch_bounds__(256) k_nerf_density(uint32_t n, const float* _
 			f16v acc = zero16();
 #pragma unroll
 			for (int ks = 0; ks < DKS; ++ks) acc = mfma(loadA(w.d0, W, 32 * mt + r, 16 * ks, h), dinB[ks], acc);
-			H0B[2 * mt] = frag<true>(acc, 0); H0B[2 * mt + 1] = frag<true>(acc, 1);
+			H0B[2 * mt] = frag<true>(acc, 0);
+			if (2 * mt + 1 < HKS) H0B[2 * mt + 1] = frag<true>(acc, 1);  // W = 16: one 16-row half
 		}
 		f16v acc = zero16();
 #pragma unroll
