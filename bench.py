@@ -68,7 +68,7 @@ def parse():
 #   unit "pre"   : 596 B = 28 coords write (coord write pass) + 28 coords read + 448 gather + 32 output
 #                  write (fused inference: 508 B) + 60 loss reads (loss kernels)
 #   unit "train" : 1496 B = 60 compacted coords + dL/dout write (loss) + 28 coords + 448 gather (training
-#                  encode: 476 B) + 32 output + 32 dL/dout (training MLP: 64 B) + 896 grid RMW (scatter)
+#                  encode: 476 B) + 32 output + 32 dL/dout (training MLP kernels: 32 B each) + 896 grid RMW (scatter)
 # The SURVEY's figures count the gathers as HBM bytes; the 21 MB table mostly hits L2 / Infinity Cache,
 # so `traffic` (PMC) is reported next to them. MFMA flops (SURVEY: 28,672 per pre-compaction sample,
 # 92,160 per compacted sample) are reported alongside for the MLP kernels.
@@ -81,7 +81,10 @@ def kernel_table(levels):
         "inference": (3, 28 + g + 32, 28672),
         "loss_alpha": (4, 60, 0),
         "train_encode": (8, 28 + g, 0),
-        "mlp_train": (5, 64, 92160 - 28672),
+        # the two training-MLP kernels (fwd recompute + 1st / 2nd-order backward; SURVEY: 92,160 - 28,672 flops per
+        # compacted sample between them): dL/dout read by the colour kernel, the output-side operands by the density one
+        "mlp_train_rgb": (9, 32, 0),
+        "mlp_train_density": (10, 32, 0),
         "grid_scatter": (7, 2 * g, 0),
     }
 MFMA_PEAK_TFLOPS = 2500.0  # MI355X dense fp16 (MI355X_MICROARCH.md)

@@ -259,7 +259,8 @@ int neus_debug_time_kernel(NeusTestbed* tb, int kernel, int variant, int iters, 
  * kernel replayed on the current training state, and the work units of one launch.
  * kernel: 0 ray generation + march (units: ray slots), 1 coordinate write, 2 loss transmittance scan,
  * 3 fused inference, 4 loss alpha (units: pre-compaction samples), 5 training MLP, 6 weight gradients,
- * 7 grid-gradient scatter, 8 training-batch grid encode (units: compacted samples). */
+ * 7 grid-gradient scatter, 8 training-batch grid encode, 9 / 10 the colour / density training-MLP kernel alone
+ * (units: compacted samples). */
 int neus_testbed_time_kernel(NeusTestbed* tb, int kernel, int iters, float* ms_out, uint32_t* units_out);
 // Development statistic of the last step's march: per ray {march_step calls, skip-loop additions,
 // samples} (3 x u32 per ray, n rays; cone_angle 0 only).

@@ -63,6 +63,32 @@ struct pcg32 {
 		state = acc_mult * state + acc_plus;
 	}
 };
+// Jump-ahead table of one pcg32 stream (increment `inc`): t[j][k] = the affine map of advance(k << 12 j), j < 3,
+// k < 4096. advance(d) for d < 2^36 is then three table lookups and three 64-bit multiply-adds instead of
+// ~log2(d) squaring steps (the LCG's jumps compose exactly, so the state is bit-identical).
+struct PcgJump { unsigned long long mult, plus; };
+struct PcgJumpTable { const PcgJump* t; uint64_t inc; };  // t: 3 x 4096 entries
+constexpr uint32_t PCG_JUMP_BITS = 12, PCG_JUMP_N = 1u << PCG_JUMP_BITS, PCG_JUMP_LEVELS = 3;
+NEUS_HD PcgJump pcg_jump(uint64_t inc, uint64_t delta) {
+	uint64_t cur_mult = 0x5851f42d4c957f2dULL, cur_plus = inc, acc_mult = 1u, acc_plus = 0u;
+	while (delta > 0) {
+		if (delta & 1) { acc_mult *= cur_mult; acc_plus = acc_plus * cur_mult + cur_plus; }
+		cur_plus = (cur_mult + 1) * cur_plus; cur_mult *= cur_mult; delta /= 2;
+	}
+	return PcgJump{acc_mult, acc_plus};
+}
+NEUS_HD void pcg_advance(pcg32& r, uint64_t delta, const PcgJumpTable& jt) {
+	if (jt.t && r.inc == jt.inc && delta < (1ull << (PCG_JUMP_LEVELS * PCG_JUMP_BITS))) {
+#pragma unroll
+		for (uint32_t j = 0; j < PCG_JUMP_LEVELS; ++j) {
+			const PcgJump a = jt.t[j * PCG_JUMP_N + ((delta >> (j * PCG_JUMP_BITS)) & (PCG_JUMP_N - 1))];
+			r.state = a.mult * r.state + a.plus;
+		}
+	} else {
+		r.advance((int64_t)delta);
+	}
+}
+
 inline pcg32 make_pcg32(uint64_t initstate, uint64_t initseq = 1u) {
 	pcg32 r; r.state = 0U; r.inc = (initseq << 1u) | 1u; r.next_uint(); r.state += initstate; r.next_uint(); return r;
 }

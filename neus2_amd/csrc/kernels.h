@@ -89,6 +89,7 @@ struct LossParams {
 	float ek_w, mask_w, cos_anneal;
 	uint32_t max_compacted; // target batch size
 	uint64_t rng_state, rng_inc;
+	PcgJumpTable jt;
 };
 
 // binned hash-grid gradient scatter (grid.hip)
@@ -151,6 +152,8 @@ struct OccSampling {
 	float amin[3], diag[3];
 	const float* grid_in;
 	float* grid_tmp;
+	PcgJumpTable jt;
+	uint32_t exclusive;   // every cell receives exactly one sample (n_nu = 0, n_u = 128^3, one cascade): plain stores
 };
 void launch_occ_density(hipStream_t s, uint32_t L, uint32_t W, uint32_t n, const OccSampling& os, const GridLevels& gl, uint32_t valid_level,
                         const half_t* grid, const MlpPtrs& w);
@@ -159,7 +162,7 @@ void launch_sdf_grid(hipStream_t s, uint32_t L, uint32_t W, const uint32_t res[3
                      const float train_min[3], const float train_max[3], uint64_t offset, uint32_t n, const GridLevels& gl, uint32_t valid_level,
                      const half_t* grid, const MlpPtrs& w, float* sdf, const DeltaState* delta = nullptr);
 void launch_mlp_train(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_valid_ptr, uint32_t n, uint32_t ld, const float* coords,
-                      const half_t* enc, const float* dydx, const half_t* dL_dout, const MlpPtrs& w, const TrainBufs& tb);
+                      const half_t* enc, const float* dydx, const half_t* dL_dout, const MlpPtrs& w, const TrainBufs& tb, int part = 0 /* 0 both, 1 colour, 2 density */);
 void launch_wgrad(hipStream_t s, const WGradJobs& jobs, uint32_t n_blocks);
 uint32_t mlp_train_blocks(uint32_t n);  // grid of the training MLP kernels (= the variance partial count)
 void launch_mfma_probe(hipStream_t s, const half_t* A, const half_t* B, float* C);
@@ -175,6 +178,7 @@ constexpr uint32_t MARCH_SEG_RECS = NERF_STEPS + 64;
 struct MarchWork {
 	uint2* rec; uint32_t* nrec; uint32_t* counter /* 2: the two passes' ray queues */; uint32_t waves; /* 0 = one lane per ray */
 	uint2* seg; uint32_t lanes_per_ray;  /* 1, 4 or 8 */
+	PcgJumpTable jt;                      /* jump-ahead of the ray generator's per-ray rng offsets */
 };
 // Ray generation + the occupancy march: rays (6 f32 per slot), tstart (1 per slot), nreq (requested
 // samples per slot) and the sample runs (MarchWork).
@@ -245,7 +249,7 @@ void launch_permute_din(hipStream_t s, const half_t* d0, half_t* d0p, half_t* d0
 // samples [i_begin, i_end) of an n-sample generate_grid_samples_nerf_nonuniform call, written from out_base
 void launch_grid_samples(hipStream_t s, uint32_t n, uint32_t i_begin, uint32_t i_end, uint32_t out_base, uint64_t rng_state, uint64_t rng_inc,
                          uint32_t step, const float* aabb_min, const float* aabb_max, const float* grid_in, float* pos, uint32_t* indices,
-                         uint32_t n_cascades, float thresh);
+                         uint32_t n_cascades, float thresh, const PcgJumpTable& jt);
 void launch_splat_max(hipStream_t s, uint32_t n, const uint32_t* indices, const float* density, float* grid_tmp);
 void launch_ema_grid(hipStream_t s, uint32_t n, float decay, float* grid, const float* tmp);
 void launch_grid_mean(hipStream_t s, const float* grid, float* partial, float* mean);

@@ -41,7 +41,7 @@ __global__ void k_bitfield_linear(const uint8_t* __restrict__ bf, uint32_t* __re
 // start t, or -1 for a dropped ray and for slots >= R (nothing to march).
 __global__ void __launch_bounds__(256) k_ray_gen(uint32_t cap_rays, const StepState* __restrict__ st_r, DPInfo dp, DevDataset ds,
                                                  uint64_t rng_state, uint64_t rng_inc, float* __restrict__ rays, float* __restrict__ tstart,
-                                                 uint32_t* __restrict__ march_queue, StepState* __restrict__ st_w) {
+                                                 uint32_t* __restrict__ march_queue, StepState* __restrict__ st_w, PcgJumpTable jt) {
 	if (blockIdx.x == 0 && threadIdx.x == 0) {  // the march passes' ray queues and counters (next kernels on the stream)
 		march_queue[0] = 0; march_queue[1] = 0;
 		st_w->march_total = 0; st_w->kept_extent = 0;
@@ -55,7 +55,7 @@ __global__ void __launch_bounds__(256) k_ray_gen(uint32_t cap_rays, const StepSt
 			pcg32 rng(rng_state, rng_inc);
 			const uint32_t img = image_idx(ig, n_rays_global, n_rays_total, ds.n_images);
 			const int rx = ds.res[2 * img], ry = ds.res[2 * img + 1];
-			rng.advance((int64_t)(uint32_t)(ig * N_MAX_RANDOM_SAMPLES_PER_RAY));
+			pcg_advance(rng, (uint64_t)(uint32_t)(ig * N_MAX_RANDOM_SAMPLES_PER_RAY), jt);
 			float xx, yy; random_image_pos(rng, rx, ry, xx, yy);
 			float rgba[4]; read_rgba(ds, img, xx, yy, rgba);
 			bool drop = false;
@@ -589,7 +589,9 @@ template <bool STORE = true>
 __global__ void __launch_bounds__(256) k_loss_scan_ray(uint32_t cap_rays, const uint32_t* __restrict__ numsteps, const float4* __restrict__ sa,
                                                        const float* __restrict__ ekt, float4* __restrict__ ck4, float* __restrict__ cke,
                                                        uint32_t* __restrict__ ccount, float4* __restrict__ racc, float* __restrict__ rT) {
-	constexpr uint32_t U = 8;
+	// 16 samples per group, the next group's loads in flight: early in training a few hundred rays carry hundreds
+	// of samples each and the kernel time is their load-latency chain
+	constexpr uint32_t U = 16;
 	const uint32_t stride = gridDim.x * blockDim.x;
 	for (uint32_t k = threadIdx.x * gridDim.x + blockIdx.x; k < ((cap_rays + stride - 1) / stride) * stride; k += stride) {
 		const uint32_t i = k;
@@ -651,7 +653,7 @@ __global__ void __launch_bounds__(256) k_loss_ray(uint32_t cap_rays, StepState* 
 		// target pixel and background (same RNG stream as the sampler; testbed_nerf.cu:1632-1660)
 		const uint32_t ig = dp.rank * R + i;
 		pcg32 rng(lp.rng_state, lp.rng_inc);
-		rng.advance((int64_t)(uint32_t)(ig * N_MAX_RANDOM_SAMPLES_PER_RAY));
+		pcg_advance(rng, (uint64_t)(uint32_t)(ig * N_MAX_RANDOM_SAMPLES_PER_RAY), lp.jt);
 		const uint32_t img = image_idx(ig, n_rays_global, n_rays_total, ds.n_images);
 		const int rx = ds.res[2 * img], ry = ds.res[2 * img + 1];
 		float xx, yy; random_image_pos(rng, rx, ry, xx, yy);
@@ -856,7 +858,7 @@ void launch_bitfield_linear(hipStream_t s, const uint8_t* bitfield, uint32_t* li
 }
 void launch_march_count(hipStream_t s, uint32_t cap, uint32_t max_samples, StepState* st, DPInfo dp, const DevDataset& ds, const uint8_t* bitfield,
                         const uint32_t* lin, uint64_t rng_state, uint64_t rng_inc, float* rays, float* tstart, uint32_t* nreq, const MarchWork& mw) {
-	k_ray_gen<<<ray_blocks(cap), 256, 0, s>>>(cap, st, dp, ds, rng_state, rng_inc, rays, tstart, mw.counter, st);
+	k_ray_gen<<<ray_blocks(cap), 256, 0, s>>>(cap, st, dp, ds, rng_state, rng_inc, rays, tstart, mw.counter, st, mw.jt);
 	const uint32_t waves = mw.waves ? std::min(mw.waves, (cap + 63) / 64) : (cap + 63) / 64;
 	const uint32_t blocks = std::max<uint32_t>(1, (waves + 3) / 4);
 	for (uint32_t pass = 0; pass < 2; ++pass) {

@@ -698,7 +698,7 @@ __global__ void __launch_bounds__(256) k_nerf_density(uint32_t n, const float* _
 			const uint32_t g = os.lo + ic;
 			const bool uni = g < os.n_u;
 			grid_sample(uni ? os.n_u : os.n_nu, uni ? g : g - os.n_u, uni ? os.rng_u_state : os.rng_nu_state, uni ? os.rng_u_inc : os.rng_nu_inc,
-			            os.step, os.amin, os.diag, os.grid_in, os.n_cascades, uni ? -0.01f : os.thresh_nu, x, cell);
+			            os.step, os.amin, os.diag, os.grid_in, os.n_cascades, uni ? -0.01f : os.thresh_nu, x, cell, os.jt);
 		} else {
 			const uint64_t g = ug.offset + ic;
 			const uint64_t rxy = (uint64_t)ug.res[0] * ug.res[1];
@@ -748,7 +748,12 @@ __global__ void __launch_bounds__(256) k_nerf_density(uint32_t n, const float* _
 			const half_t s = (half_t)__expf((float)(var_h * (half_t)10.0f));
 			const half_t sig = (half_t)(1.0f / (1.0f + __expf(-(float)(sdf * s))));
 			const half_t dens = (s * sig) * ((half_t)1.0f - sig);
-			if (MODE == 2) atomicMax((uint32_t*)&os.grid_tmp[cell], __float_as_uint((float)dens));
+			if (MODE == 2) {
+				// an all-cells uniform pass over one cascade hits every cell exactly once (odd multiplier mod 2^21):
+				// the splat's max is then the sample itself - a plain store
+				if (os.exclusive) os.grid_tmp[cell] = (float)dens;
+				else atomicMax((uint32_t*)&os.grid_tmp[cell], __float_as_uint((float)dens));
+			}
 			else density[i] = (float)dens;
 		}
 	}
@@ -1149,11 +1154,33 @@ __global__ void __launch_bounds__(256) k_wgrad(WGradJobs jobs) {
 	const uint32_t row_m = 32 * mt + r, row_k = 32 * kt + r;
 	const bool okm = row_m < J.M, okk = row_k < J.K;
 	f16v acc = zero16();
-	for (uint32_t nb = n0 + 16 * wv; nb < n1; nb += 64) {
-		h8 a = (h8){0, 0, 0, 0, 0, 0, 0, 0}, bb = a;
-		if (okm) a = *(const h8*)(J.D + (size_t)row_m * J.ldc + nb + 8 * h);
-		if (okk) bb = *(const h8*)(J.X + (size_t)row_k * J.ldc + nb + 8 * h);
-		acc = mfma(a, bb, acc);
+	// Each wave takes 64-sample chunks (4 k-steps); lane half h owns the chunk's samples 32h .. 32h + 31, k-step u
+	// their 8u .. 8u + 7: a lane reads 64 contiguous bytes of its row per chunk, the two halves a whole 128-B line.
+	// Two chunks per trip: 16 loads in flight ahead of 8 MFMAs. The sample -> k assignment is the same for D and X,
+	// so the sum is the batch's; its order is fixed (deterministic).
+	const half_t* Dr = J.D + (size_t)row_m * J.ldc + 32 * h;
+	const half_t* Xr = J.X + (size_t)row_k * J.ldc + 32 * h;
+	const h8 z8 = (h8){0, 0, 0, 0, 0, 0, 0, 0};
+	uint32_t nb = n0 + 64 * wv;
+	for (; nb + 256 + 64 <= n1; nb += 512) {
+		h8 a[8], bb[8];
+#pragma unroll
+		for (int c = 0; c < 2; ++c)
+#pragma unroll
+			for (int u = 0; u < 4; ++u) {
+				a[4 * c + u] = okm ? *(const h8*)(Dr + nb + 256 * c + 8 * u) : z8;
+				bb[4 * c + u] = okk ? *(const h8*)(Xr + nb + 256 * c + 8 * u) : z8;
+			}
+#pragma unroll
+		for (int u = 0; u < 8; ++u) acc = mfma(a[u], bb[u], acc);
+	}
+	for (; nb + 64 <= n1; nb += 256) {
+#pragma unroll
+		for (int u = 0; u < 4; ++u) {
+			const h8 a = okm ? *(const h8*)(Dr + nb + 8 * u) : z8;
+			const h8 bb = okk ? *(const h8*)(Xr + nb + 8 * u) : z8;
+			acc = mfma(a, bb, acc);
+		}
 	}
 #pragma unroll
 	for (int reg = 0; reg < 16; ++reg) red[wv][acc_row(reg, h) * 32 + r] = acc[reg];
@@ -1289,12 +1316,12 @@ void launch_sdf_grid(hipStream_t s, uint32_t L, uint32_t W, const uint32_t res[3
 #undef X
 }
 void launch_mlp_train(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_valid_ptr, uint32_t n, uint32_t ld, const float* coords,
-                      const half_t* enc, const float* dydx, const half_t* dL_dout, const MlpPtrs& w, const TrainBufs& tb) {
+                      const half_t* enc, const float* dydx, const half_t* dL_dout, const MlpPtrs& w, const TrainBufs& tb, int part) {
 	const uint32_t blocks = mlp_train_blocks(n);
 	if (n == 0) return;
 #define X(l, w_) if (L == l && W == w_) { \
-		k_mlp_train_rgb<l, w_><<<blocks, 256, 0, s>>>(n_valid_ptr, n, ld, coords, enc, dydx, dL_dout, w, tb); \
-		k_mlp_train_density<l, w_><<<blocks, 256, 0, s>>>(n_valid_ptr, n, ld, coords, enc, dydx, w, tb); return; }
+		if (part != 2) k_mlp_train_rgb<l, w_><<<blocks, 256, 0, s>>>(n_valid_ptr, n, ld, coords, enc, dydx, dL_dout, w, tb); \
+		if (part != 1) k_mlp_train_density<l, w_><<<blocks, 256, 0, s>>>(n_valid_ptr, n, ld, coords, enc, dydx, w, tb); return; }
 	NEUS_MLP_CONFIGS(X)
 #undef X
 }

@@ -10,10 +10,10 @@ namespace neus {
 
 __device__ __forceinline__ void grid_sample(uint32_t n_elements, uint32_t i, uint64_t rng_state, uint64_t rng_inc, uint32_t step,
                                             const float amin[3], const float diag[3], const float* __restrict__ grid_in, uint32_t n_cascades,
-                                            float thresh, float pos[3], uint32_t& idx_out) {
+                                            float thresh, float pos[3], uint32_t& idx_out, const PcgJumpTable& jt) {
 #pragma clang fp contract(off)  // the same bits in every translation unit (and as the oracle's restatement)
 	pcg32 rng(rng_state, rng_inc);
-	rng.advance((int64_t)(uint32_t)(i * 4));
+	pcg_advance(rng, (uint64_t)(uint32_t)(i * 4), jt);
 	const uint32_t level = (uint32_t)(rng.next_float() * n_cascades) % n_cascades;
 	uint32_t idx = 0;
 	for (uint32_t j = 0; j < 10; ++j) {

@@ -83,12 +83,12 @@ __global__ void k_transpose_w(TransposeJobs jobs) {
 __global__ void k_grid_samples(uint32_t n_elements, uint32_t i_begin, uint32_t i_end, uint32_t out_base, uint64_t rng_state, uint64_t rng_inc,
                                uint32_t step, float aabb_min_x, float aabb_min_y, float aabb_min_z, float diag_x, float diag_y, float diag_z,
                                const float* __restrict__ grid_in, float* __restrict__ pos, uint32_t* __restrict__ indices,
-                               uint32_t n_cascades, float thresh) {
+                               uint32_t n_cascades, float thresh, PcgJumpTable jt) {
 	const float amin[3] = {aabb_min_x, aabb_min_y, aabb_min_z}, diag[3] = {diag_x, diag_y, diag_z};
 	for (uint32_t i = i_begin + blockIdx.x * blockDim.x + threadIdx.x; i < i_end; i += gridDim.x * blockDim.x) {
 		float p[3];
 		uint32_t idx;
-		grid_sample(n_elements, i, rng_state, rng_inc, step, amin, diag, grid_in, n_cascades, thresh, p, idx);
+		grid_sample(n_elements, i, rng_state, rng_inc, step, amin, diag, grid_in, n_cascades, thresh, p, idx, jt);
 		const uint32_t o = out_base + (i - i_begin);
 		pos[3 * (size_t)o + 0] = p[0];
 		pos[3 * (size_t)o + 1] = p[1];
@@ -168,11 +168,11 @@ void launch_permute_din(hipStream_t s, const half_t* d0, half_t* d0p, half_t* d0
 }
 void launch_grid_samples(hipStream_t s, uint32_t n, uint32_t i_begin, uint32_t i_end, uint32_t out_base, uint64_t rng_state, uint64_t rng_inc,
                          uint32_t step, const float* aabb_min, const float* aabb_max, const float* grid_in, float* pos, uint32_t* indices,
-                         uint32_t n_cascades, float thresh) {
+                         uint32_t n_cascades, float thresh, const PcgJumpTable& jt) {
 	if (i_end <= i_begin) return;
 	k_grid_samples<<<nblk(i_end - i_begin), 256, 0, s>>>(n, i_begin, i_end, out_base, rng_state, rng_inc, step, aabb_min[0], aabb_min[1], aabb_min[2],
 	                                        aabb_max[0] - aabb_min[0], aabb_max[1] - aabb_min[1], aabb_max[2] - aabb_min[2],
-	                                        grid_in, pos, indices, n_cascades, thresh);
+	                                        grid_in, pos, indices, n_cascades, thresh, jt);
 }
 void launch_splat_max(hipStream_t s, uint32_t n, const uint32_t* indices, const float* density, float* grid_tmp) {
 	if (n) k_splat_max<<<nblk(n), 256, 0, s>>>(n, indices, density, grid_tmp);

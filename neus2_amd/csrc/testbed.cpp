@@ -193,6 +193,7 @@ struct NeusTestbed {
 	Dev<uint32_t> occ_idx;
 	Dev<uint8_t> bitfield;
 	Dev<uint32_t> bf_lin;   // mip-0 occupancy in (x, y, z/32) word order for the constant-step march
+	Dev<PcgJump> pcg_tab;   // pcg32 jump-ahead table (common.h PcgJumpTable)
 	uint32_t density_grid_ema_step = 0;
 	// step workspace
 	uint32_t batch = 0, max_samples = 0;
@@ -260,7 +261,15 @@ struct NeusTestbed {
 		HIP_CHECK(hipHostMalloc((void**)&prof_st, 2 * sizeof(StepState)));
 		st.alloc(1);
 		HIP_CHECK(hipMemset(st.p, 0, sizeof(StepState)));
+		// pcg32 jump-ahead table of the streams this Testbed draws from (pcg32{seed} / pcg32{next_uint()}: increment 3)
+		std::vector<PcgJump> jt(PCG_JUMP_LEVELS * PCG_JUMP_N);
+		for (uint32_t j = 0; j < PCG_JUMP_LEVELS; ++j)
+			for (uint32_t k = 0; k < PCG_JUMP_N; ++k) jt[j * PCG_JUMP_N + k] = pcg_jump(PCG_INC, (uint64_t)k << (j * PCG_JUMP_BITS));
+		pcg_tab.alloc(jt.size());
+		HIP_CHECK(hipMemcpy(pcg_tab.p, jt.data(), jt.size() * sizeof(PcgJump), hipMemcpyHostToDevice));
 	}
+	static constexpr uint64_t PCG_INC = 3u;  // make_pcg32(s) = pcg32 stream 1: inc = (1 << 1) | 1
+	PcgJumpTable jump_table() const { return PcgJumpTable{pcg_tab.p, PCG_INC}; }
 	~NeusTestbed() {
 		if (stream) (void)hipStreamSynchronize(stream);
 		if (comm) ncclCommDestroy(comm);
@@ -467,7 +476,8 @@ struct NeusTestbed {
 		rays.alloc(6 * (size_t)MAX_RAYS); startt.alloc((size_t)MAX_RAYS);
 		march_rec.alloc((size_t)MAX_RAYS * NERF_STEPS); march_nrec.alloc(MAX_RAYS); march_queue.alloc(2);
 		march_seg.alloc((size_t)MAX_RAYS * MARCH_SEG_RECS);
-		mwork = MarchWork{march_rec.p, march_nrec.p, march_queue.p, march_waves(), march_seg.p, march_lanes()}; nreq.alloc(MAX_RAYS); base.alloc(MAX_RAYS);
+		mwork = MarchWork{march_rec.p, march_nrec.p, march_queue.p, march_waves(), march_seg.p, march_lanes(), jump_table()};
+		nreq.alloc(MAX_RAYS); base.alloc(MAX_RAYS);
 		numsteps.alloc(2 * (size_t)MAX_RAYS); ccount.alloc(MAX_RAYS); cbase.alloc(MAX_RAYS);
 		l_sa.alloc(max_samples); l_ekt.alloc(max_samples); sample_ray.alloc(max_samples);
 		l_ck4.alloc(max_samples / 8 + 1); l_cke.alloc(max_samples / 8 + 1);
@@ -705,7 +715,10 @@ struct NeusTestbed {
 		hipStream_t s = stream;
 		const uint32_t n_cells = GRID3 * (max_cascade + 1);
 		if (training_step == 0) { HIP_CHECK(hipMemsetAsync(density_grid.p, 0, n_cells * 4, s)); density_grid_ema_step = 0; }
-		HIP_CHECK(hipMemsetAsync(density_tmp.p, 0, n_cells * 4, s));
+		// the first 256 steps' all-cells uniform pass writes every cell exactly once (fused path, one cascade): on a
+		// single GPU no clearing is needed; with shards each rank writes only its cells, the rest must read 0
+		const bool exclusive = !use_delta && n_nonuniform == 0 && n_uniform == GRID3 && max_cascade == 0;
+		if (!exclusive || world > 1) HIP_CHECK(hipMemsetAsync(density_tmp.p, 0, n_cells * 4, s));
 		// data parallel: rank r evaluates the global samples [lo, hi) (same density_grid_rng on every rank); the
 		// max-splatted grids are then max-all-reduced, which equals the single-GPU splat (max is exact)
 		const uint32_t NT = n_uniform + n_nonuniform;
@@ -723,13 +736,15 @@ struct NeusTestbed {
 			os.step = density_grid_ema_step; os.n_cascades = max_cascade + 1; os.thresh_nu = NERF_MIN_OPTICAL_THICKNESS;
 			for (int d = 0; d < 3; ++d) { os.amin[d] = ds.aabb_min[d]; os.diag[d] = ds.aabb_max[d] - ds.aabb_min[d]; }
 			os.grid_in = density_grid.p; os.grid_tmp = density_tmp.p;
+			os.jt = jump_table();
+			os.exclusive = exclusive ? 1u : 0u;
 			launch_occ_density(s, lay.L, lay.W, N, os, gl, valid, params_h.p + lay.grid_off, mlp);
 		} else {
 			launch_grid_samples(s, n_uniform, std::min(lo, n_uniform), std::min(hi, n_uniform), 0, rng_u.state, rng_u.inc, density_grid_ema_step,
-			                    ds.aabb_min, ds.aabb_max, density_grid.p, occ_pos.p, occ_idx.p, max_cascade + 1, -0.01f);
+			                    ds.aabb_min, ds.aabb_max, density_grid.p, occ_pos.p, occ_idx.p, max_cascade + 1, -0.01f, jump_table());
 			launch_grid_samples(s, n_nonuniform, std::max(lo, n_uniform) - n_uniform, std::max(hi, n_uniform) - n_uniform,
 			                    std::max(lo, n_uniform) - lo, rng_nu.state, rng_nu.inc, density_grid_ema_step, ds.aabb_min, ds.aabb_max,
-			                    density_grid.p, occ_pos.p, occ_idx.p, max_cascade + 1, NERF_MIN_OPTICAL_THICKNESS);
+			                    density_grid.p, occ_pos.p, occ_idx.p, max_cascade + 1, NERF_MIN_OPTICAL_THICKNESS, jump_table());
 			// NerfNetwork::density on the moved positions (the DeltaNetwork is active, nerf_network.h:664-675)
 			launch_delta_apply(s, nullptr, N, 3, occ_pos.p, occ_pos.p, delta.p);
 			launch_nerf_density(s, lay.L, lay.W, N, occ_pos.p, gl, valid, params_h.p + lay.grid_off, mlp, occ_density.p);
@@ -963,7 +978,7 @@ struct NeusTestbed {
 		mark(3);
 		LossParams lp{};
 		lp.loss_scale = LOSS_SCALE; lp.ek_w = cfg.ek_loss_weight; lp.mask_w = cfg.mask_loss_weight; lp.cos_anneal = cos_anneal();
-		lp.max_compacted = batch; lp.rng_state = rng.state; lp.rng_inc = rng.inc;
+		lp.max_compacted = batch; lp.rng_state = rng.state; lp.rng_inc = rng.inc; lp.jt = jump_table();
 		const LossWork w = loss_work(base.p);
 		launch_loss_alpha(s, max_samples, st.p, coords.p, net_out.p, lp.cos_anneal, w);
 		launch_loss_scan_ray(s, MAX_RAYS, numsteps.p, w, ccount.p);
@@ -1474,10 +1489,11 @@ static void time_kernel_impl(NeusTestbed* tb, int kernel, int variant, int iters
 			case 3: launch_nerf_infer(s, t.lay.L, t.lay.W, &t.st.p->n_kept, 0, t.coords.p, t.gl, valid, t.params_h.p + t.lay.grid_off, t.mlp,
 			                          t.net_out.p, 8192); break;
 			case 4: launch_loss_alpha(s, t.max_samples, t.st.p, t.coords.p, t.net_out.p, t.cos_anneal(), w); break;
-			case 5: {  // both training-MLP kernels on the last step's compacted batch
+			case 5: case 9: case 10: {  // the training-MLP kernels (5 both, 9 colour, 10 density) on the last compacted batch
 				TrainBufs tbuf = t.tbuf;
 				tbuf.var_grad = t.grads.p + t.lay.var_off;
-				launch_mlp_train(s, t.lay.L, t.lay.W, nullptr, t.batch, t.batch, t.coords_c.p, (const half_t*)t.enc.p, t.dydx.p, t.dL_dout.p, t.mlp, tbuf);
+				launch_mlp_train(s, t.lay.L, t.lay.W, nullptr, t.batch, t.batch, t.coords_c.p, (const half_t*)t.enc.p, t.dydx.p, t.dL_dout.p, t.mlp, tbuf,
+				                 kernel == 5 ? 0 : kernel - 8);
 				break;
 			}
 			case 6: { WGradJobs J = t.wgrad_jobs(t.batch, t.batch, t.grads.p, nullptr); launch_wgrad(s, J, J.block_start[5]); break; }

@@ -202,15 +202,17 @@ def test_sample_rays_bit_exact(env):
     bf = _bitfield(env)
     n_rays, max_samples = 4096, 4096 * 16
     rng_state, rng_inc = 0x1234567890ABCDEF, 0xDA3E39CB94B95BDB | 1
-    for (max_s, world, rank, total) in [(max_samples, 1, 0, 0), (20000, 1, 0, 12345), (max_samples, 2, 1, 8192)]:
+    # the last case uses the Testbed's own stream increment (3): the device advances by its jump-ahead table
+    for (max_s, world, rank, total, inc) in [(max_samples, 1, 0, 0, rng_inc), (20000, 1, 0, 12345, rng_inc), (max_samples, 2, 1, 8192, rng_inc),
+                                             (max_samples, 1, 0, 777, 3)]:
         rays = t.zeros((n_rays, 6), dtype=t.float32, device="cuda")
         ns = t.zeros((n_rays, 2), dtype=t.int32, device="cuda")
         co = t.zeros((max_s, 7), dtype=t.float32, device="cuda")
         cnt = (C.c_uint32 * 3)()
         check(lib.neus_sample_rays(tb.handle, None, C.c_uint32(n_rays), C.c_uint32(rank), C.c_uint32(world), C.c_uint32(total),
-                                   C.c_uint64(rng_state), C.c_uint64(rng_inc), C.c_uint32(max_s), ptr(dev(t, bf)),
+                                   C.c_uint64(rng_state), C.c_uint64(inc), C.c_uint32(max_s), ptr(dev(t, bf)),
                                    ptr(rays), ptr(ns), ptr(co), cnt))
-        r_rays, r_ns, r_co, r_cnt, r_nr = O.generate_samples(env["ds"], bf, n_rays, total, rng_state, rng_inc, max_s,
+        r_rays, r_ns, r_co, r_cnt, r_nr = O.generate_samples(env["ds"], bf, n_rays, total, rng_state, inc, max_s,
                                                              ray_offset=rank * n_rays, n_rays_global=world * n_rays)
         g_ns = host(ns, np.uint32)
         np.testing.assert_array_equal(g_ns, r_ns)
