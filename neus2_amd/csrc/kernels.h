@@ -153,7 +153,7 @@ struct OccSampling {
 	const float* grid_in;
 	float* grid_tmp;
 	PcgJumpTable jt;
-	uint32_t exclusive;   // every cell receives exactly one sample (n_nu = 0, n_u = 128^3, one cascade): plain stores
+	uint32_t exclusive;   // the all-cells uniform pass over one cascade: index = cell (occ_common.h grid_sample_cell), plain stores
 };
 void launch_occ_density(hipStream_t s, uint32_t L, uint32_t W, uint32_t n, const OccSampling& os, const GridLevels& gl, uint32_t valid_level,
                         const half_t* grid, const MlpPtrs& w);

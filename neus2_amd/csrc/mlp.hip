@@ -694,6 +694,9 @@ __global__ void __launch_bounds__(256) k_nerf_density(uint32_t n, const float* _
 		uint32_t cell = 0;
 		if (MODE == 0) {
 			x[0] = pos[3 * (size_t)ic]; x[1] = pos[3 * (size_t)ic + 1]; x[2] = pos[3 * (size_t)ic + 2];
+		} else if (MODE == 2 && os.exclusive) {
+			cell = os.lo + ic;
+			grid_sample_cell(cell, os.rng_u_state, os.rng_u_inc, os.amin, os.diag, x, os.jt);
 		} else if (MODE == 2) {
 			const uint32_t g = os.lo + ic;
 			const bool uni = g < os.n_u;

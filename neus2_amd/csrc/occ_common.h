@@ -34,4 +34,28 @@ __device__ __forceinline__ void grid_sample(uint32_t n_elements, uint32_t i, uin
 	idx_out = idx;
 }
 
+// The same sample, addressed by its cell, for the all-cells uniform pass over one cascade (n = 128^3, thresh -0.01):
+// there the first hash try is always taken (densities are >= 0) and (i + step n) * 56924617 + 96925573 mod 2^21 is a
+// bijection (odd multiplier; n = 2^21 makes the step term vanish), so cell c holds exactly sample
+// i = (c - 96925573) * 56924617^-1 mod 2^21 (the inverse is 53369). Walking cells in order gives coalesced grid
+// reads / writes and spatially coherent hash-grid gathers; every sample's value is unchanged (a grid holding
+// NaN would make the reference retry another cell - training has diverged then, see the non-finite loss flag).
+__device__ __forceinline__ void grid_sample_cell(uint32_t c, uint64_t rng_state, uint64_t rng_inc, const float amin[3], const float diag[3],
+                                                 float pos[3], const PcgJumpTable& jt) {
+#pragma clang fp contract(off)
+	const uint32_t i = ((c - 96925573u) * 53369u) & (GRID3 - 1);
+	pcg32 rng(rng_state, rng_inc);
+	pcg_advance(rng, (uint64_t)(uint32_t)(i * 4), jt);
+	(void)rng.next_float();  // the cascade draw (one cascade: level 0)
+	const uint32_t x = morton3D_invert(c >> 0), y = morton3D_invert(c >> 1), z = morton3D_invert(c >> 2);
+	const float rx = rng.next_float(), ry = rng.next_float(), rz = rng.next_float();
+	const float sc = 1.0f;
+	const float px = (((float)x + rx) / NERF_GRIDSIZE - 0.5f) * sc + 0.5f;
+	const float py = (((float)y + ry) / NERF_GRIDSIZE - 0.5f) * sc + 0.5f;
+	const float pz = (((float)z + rz) / NERF_GRIDSIZE - 0.5f) * sc + 0.5f;
+	pos[0] = (px - amin[0]) / diag[0];
+	pos[1] = (py - amin[1]) / diag[1];
+	pos[2] = (pz - amin[2]) / diag[2];
+}
+
 } // namespace neus

@@ -719,8 +719,9 @@ struct NeusTestbed {
 		// single GPU no clearing is needed; with shards each rank writes only its cells, the rest must read 0
 		const bool exclusive = !use_delta && n_nonuniform == 0 && n_uniform == GRID3 && max_cascade == 0;
 		if (!exclusive || world > 1) HIP_CHECK(hipMemsetAsync(density_tmp.p, 0, n_cells * 4, s));
-		// data parallel: rank r evaluates the global samples [lo, hi) (same density_grid_rng on every rank); the
-		// max-splatted grids are then max-all-reduced, which equals the single-GPU splat (max is exact)
+		// data parallel: rank r evaluates the global samples [lo, hi) (same density_grid_rng on every rank; in the
+		// exclusive pass the cells [lo, hi), i.e. the samples that land there); the max-splatted grids are then
+		// max-all-reduced, which equals the single-GPU splat (max is exact)
 		const uint32_t NT = n_uniform + n_nonuniform;
 		const uint32_t lo = (uint32_t)((uint64_t)NT * rank / world), hi = (uint32_t)((uint64_t)NT * (rank + 1) / world);
 		const uint32_t N = hi - lo;
