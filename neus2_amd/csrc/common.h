@@ -98,6 +98,7 @@ NEUS_HD float rh(float f) { return (float)(half_t)f; }
 
 // fixed-operation-order expf, identical on CPU oracle and GPU (no contraction in callers)
 NEUS_HD float det_expf(float x) {
+#pragma clang fp contract(off)  // the same bits in every translation unit, whatever its contraction flags
 	if (!(x < 88.5f)) return x != x ? x : __builtin_huge_valf();
 	if (x < -103.0f) return 0.0f;
 	float kf = rintf(x * 1.44269504088896341f);
@@ -112,7 +113,10 @@ NEUS_HD float det_expf(float x) {
 	p = p * r + 1.0f;
 	return ldexpf(p, (int)kf);
 }
-NEUS_HD float det_logistic(float x) { return 1.0f / (1.0f + det_expf(-x)); }
+NEUS_HD float det_logistic(float x) {
+#pragma clang fp contract(off)
+	return 1.0f / (1.0f + det_expf(-x));
+}
 
 // ----------------------------------------------------------- morton (my_tcnn common_device.h:335-365)
 NEUS_HD uint32_t expand_bits(uint32_t v) {

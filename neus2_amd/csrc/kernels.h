@@ -114,6 +114,7 @@ struct LossWork {
 	const uint32_t* rbase;  // [rays] first sample of the ray (pre-compaction)
 	float4* racc;           // [rays] rgb_ray, weight_sum
 	float* rT;              // [rays] final transmittance
+	float* rek;             // [rays] eikonal-term sum (progressive inference: the state between rounds)
 	float4* rgr;            // [rays] dL/drgb_ray (Huber'), gws * (1 - weight_sum)
 };
 
@@ -139,7 +140,8 @@ void launch_grid_scatter(hipStream_t s, const uint32_t* n_ptr, uint32_t n_cap, u
 bool mlp_supported(uint32_t n_levels, uint32_t width);
 void mlp_din_permutation(uint32_t L, int32_t* perm /* DIN entries: physical row -> logical din index or -1 */);
 void launch_nerf_infer(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_ptr, uint32_t n_fixed, const float* coords, const GridLevels& gl,
-                       uint32_t valid_level, const half_t* grid, const MlpPtrs& w, half_t* out, uint32_t blocks);
+                       uint32_t valid_level, const half_t* grid, const MlpPtrs& w, half_t* out, uint32_t blocks,
+                       const uint32_t* idx = nullptr /* work item j -> sample idx[j] (progressive-inference rounds) */);
 void launch_nerf_density(hipStream_t s, uint32_t L, uint32_t W, uint32_t n, const float* pos, const GridLevels& gl, uint32_t valid_level,
                          const half_t* grid, const MlpPtrs& w, float* density);
 // Occupancy-grid update, fused (MODE 2 of k_nerf_density): density-grid samples [lo, lo + n) of the update's
@@ -191,6 +193,15 @@ void debug_launch_march_stats(hipStream_t s, uint32_t n_rays, const float* rays,
 void launch_loss_alpha(hipStream_t s, uint32_t cap_samples, const StepState* st, const float* coords, const half_t* net_out, float cos_anneal,
                        const LossWork& w);
 void launch_loss_scan_ray(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, const LossWork& w, uint32_t* ccount);
+// progressive (cut-off-aware) inference rounds (march.hip)
+void launch_loss_alpha_list(hipStream_t s, uint32_t cap_samples, const uint32_t* n_ptr, const uint32_t* idx, const float* coords,
+                            const half_t* net_out, float cos_anneal, const LossWork& w);
+void launch_chunk_count(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, uint32_t e1, uint32_t* m, uint32_t* counters /* zeroed */,
+                        uint32_t n_counters);
+void launch_chunk_write(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, const uint32_t* m, const uint32_t* pos /* exclusive scan of m */,
+                        uint32_t* list, uint32_t* counter);
+void launch_loss_scan_chunk(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, const LossWork& w, uint32_t* ccount, uint32_t e0,
+                            uint32_t e1, uint32_t e2, uint32_t* list /* nullptr in the last round */, uint32_t* next_counter);
 void launch_loss_ray(hipStream_t s, uint32_t cap_rays, StepState* st, DPInfo dp, const DevDataset& ds, const LossParams& lp, uint32_t* numsteps,
                      const uint32_t* ccount, const uint32_t* cbase, const LossWork& w, float* loss, float* ek, float* mask);
 void launch_loss_grad(hipStream_t s, uint32_t cap_samples, const StepState* st, DPInfo dp, const LossParams& lp, const float* coords,

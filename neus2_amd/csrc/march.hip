@@ -542,11 +542,13 @@ __global__ void k_march_stats(uint32_t n_rays, const float* __restrict__ rays, c
 // compaction and the gradients stay bit-identical to the serial formulation.
 
 
-__global__ void __launch_bounds__(256) k_loss_alpha(uint32_t cap, const StepState* __restrict__ st, const float* __restrict__ coords,
-                                                    const half_t* __restrict__ net_out, float cos_anneal, float4* __restrict__ sa,
-                                                    float* __restrict__ ekt) {
-	const uint32_t n = min(st->n_kept, cap);
-	for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < n; s += gridDim.x * blockDim.x) {
+// n = min(*n_ptr, cap) samples; with idx, work item j is sample idx[j] (a progressive-inference round)
+__global__ void __launch_bounds__(256) k_loss_alpha(uint32_t cap, const uint32_t* __restrict__ n_ptr, const uint32_t* __restrict__ idx,
+                                                    const float* __restrict__ coords, const half_t* __restrict__ net_out, float cos_anneal,
+                                                    float4* __restrict__ sa, float* __restrict__ ekt) {
+	const uint32_t n = min(*n_ptr, cap);
+	for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+		const uint32_t s = idx ? idx[j] : j;
 		half_t lo[16]; load_out(net_out, s, lo);
 		float dir[3]; bent_dir(lo, dir);
 		const Alpha a = neus_alpha(lo, dir, unwarp_dt(coords[(size_t)s * COORD_W + 3]), cos_anneal);
@@ -579,19 +581,20 @@ __device__ __forceinline__ ScanState scan_replay(uint32_t base, uint32_t s, cons
 	return st;
 }
 
-// One thread per ray, software-pipelined: the next U samples' {alpha, rgb} and eikonal terms are in
-// flight while the current U go through the serial recurrence. Loads use clamped indices so they
-// issue unconditionally, ahead of the data-dependent exit. Consecutive rays go to consecutive BLOCKS:
-// the rays that carry samples are a prefix of the ray range (few and long early in training), and
-// this spreads them over all CUs. The state is stored only every SCAN_CK samples (scan_replay
-// rebuilds the rest exactly), which keeps the scattered per-lane stores off the critical path.
+// The recurrence state a ray carries between progressive-inference rounds (cn = samples composited so far).
+struct RayScan { float T, r0, r1, r2, ws, ek; uint32_t cn; };
+
+// One thread per ray over all its samples, software-pipelined: the next U samples' {alpha, rgb} and eikonal terms
+// are in flight while the current U go through the serial recurrence. Loads use clamped indices so they issue
+// unconditionally, ahead of the data-dependent exit. Consecutive rays go to consecutive BLOCKS: the rays that carry
+// samples are a prefix of the ray range (few and long early in training), and this spreads them over all CUs. The
+// state is stored only every SCAN_CK samples (scan_replay rebuilds the rest exactly), which keeps the scattered
+// per-lane stores off the critical path. 16 samples per group: early in training a few hundred rays carry hundreds
+// of samples each and the kernel time is their load-latency chain.
 template <bool STORE = true>
 __global__ void __launch_bounds__(256) k_loss_scan_ray(uint32_t cap_rays, const uint32_t* __restrict__ numsteps, const float4* __restrict__ sa,
                                                        const float* __restrict__ ekt, float4* __restrict__ ck4, float* __restrict__ cke,
                                                        uint32_t* __restrict__ ccount, float4* __restrict__ racc, float* __restrict__ rT) {
-	// 16 samples per group, the next group's loads in flight: early in training a few hundred rays carry hundreds
-	// of samples each and the kernel time is their load-latency chain
-	constexpr uint32_t U = 16;
 	const uint32_t stride = gridDim.x * blockDim.x;
 	for (uint32_t k = threadIdx.x * gridDim.x + blockIdx.x; k < ((cap_rays + stride - 1) / stride) * stride; k += stride) {
 		const uint32_t i = k;
@@ -600,6 +603,7 @@ __global__ void __launch_bounds__(256) k_loss_scan_ray(uint32_t cap_rays, const 
 		uint32_t cn = 0;
 		float T = 1.f, r0 = 0.f, r1 = 0.f, r2 = 0.f, ws = 0.f, ek = 0.f;
 		if (ns > 0) {
+			constexpr uint32_t U = 16;
 			const uint32_t last = base + ns - 1;
 			float4 qn[U]; float en[U];
 #pragma unroll
@@ -630,6 +634,95 @@ __global__ void __launch_bounds__(256) k_loss_scan_ray(uint32_t cap_rays, const 
 		ccount[i] = cn;
 		racc[i] = make_float4(r0, r1, r2, ws);
 		rT[i] = T;
+	}
+}
+
+// ---------------------------------------------------------------- progressive (cut-off-aware) inference
+// Late in training most of a long ray's samples lie behind the surface, past the T < 1e-4 cut, and the loss never
+// reads their network outputs (23-45 % of the kept samples are composited at steps 800-2000). The
+// step then evaluates the network in rounds of per-ray sample chunks [e_k, e_k+1): round k infers only the chunk of
+// the rays whose recurrence is still open after round k-1. Every composited sample is evaluated exactly as in one
+// pass and the recurrence runs over the same samples in the same order, so the results are bit-identical; only
+// samples past the cut are never evaluated. The work lists hold sample indices; their order is immaterial (each
+// work item writes its own sample's slots).
+
+// Round 0's list: the first min(ns, e1) samples of every ray, at the exclusive scan of those counts
+// (k_chunk_count -> scan -> k_chunk_write; no atomics: one counter hit per wave serialises on a single address).
+__global__ void __launch_bounds__(256) k_chunk_count(uint32_t cap_rays, const uint32_t* __restrict__ numsteps, uint32_t e1,
+                                                     uint32_t* __restrict__ m, uint32_t* __restrict__ counters, uint32_t n_counters) {
+	if (blockIdx.x == 0 && threadIdx.x < n_counters) counters[threadIdx.x] = 0u;  // the rounds' list sizes
+	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cap_rays; i += gridDim.x * blockDim.x) m[i] = min(numsteps[2 * i], e1);
+}
+__global__ void __launch_bounds__(256) k_chunk_write(uint32_t cap_rays, const uint32_t* __restrict__ numsteps, const uint32_t* __restrict__ m,
+                                                     const uint32_t* __restrict__ pos, uint32_t* __restrict__ list, uint32_t* __restrict__ counter) {
+	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cap_rays; i += gridDim.x * blockDim.x) {
+		const uint32_t k = m[i], p = pos[i], base = numsteps[2 * i + 1];
+		for (uint32_t j = 0; j < k; ++j) list[p + j] = base + j;
+		if (i == cap_rays - 1) *counter = p + k;
+	}
+}
+
+// Round k's recurrence over [e0, e1) of each ray still open (all rays with samples when e0 == 0), continuing from
+// the stored state; rays that stay open append their next chunk [e1, min(ns, e2)) to the next round's list.
+__global__ void __launch_bounds__(256) k_loss_scan_chunk(uint32_t cap_rays, const uint32_t* __restrict__ numsteps, const float4* __restrict__ sa,
+                                                         const float* __restrict__ ekt, float4* __restrict__ ck4, float* __restrict__ cke,
+                                                         uint32_t* __restrict__ ccount, float4* __restrict__ racc, float* __restrict__ rT,
+                                                         float* __restrict__ rek, uint32_t e0, uint32_t e1, uint32_t e2,
+                                                         uint32_t* __restrict__ list, uint32_t* __restrict__ next_counter) {
+	const uint32_t stride = gridDim.x * blockDim.x;
+	for (uint32_t k = threadIdx.x * gridDim.x + blockIdx.x; k < ((cap_rays + stride - 1) / stride) * stride; k += stride) {
+		const uint32_t i = k;
+		if (i >= cap_rays) continue;
+		const uint32_t ns = numsteps[2 * i], base = numsteps[2 * i + 1];
+		RayScan S{1.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0u};
+		if (e0 > 0) {
+			S.cn = ccount[i];
+			if (S.cn != e0 || e0 >= ns) continue;  // closed in an earlier round (or no samples)
+			S.T = rT[i];
+			if (S.T < 1e-4f) continue;
+			const float4 a = racc[i];
+			S.r0 = a.x; S.r1 = a.y; S.r2 = a.z; S.ws = a.w; S.ek = rek[i];
+		}
+		const uint32_t to = min(ns, e1);
+		if (to > e0) {
+			// the same software-pipelined loop as k_loss_scan_ray, over [e0, to)
+			constexpr uint32_t U = 16;
+			const uint32_t last = base + to - 1;
+			float4 qn[U]; float en[U];
+#pragma unroll
+			for (uint32_t u = 0; u < U; ++u) { const uint32_t s = min(base + e0 + u, last); qn[u] = sa[s]; en[u] = ekt[s]; }
+			bool done = false;
+			for (uint32_t c = e0; c < to && !done; c += U) {
+				float4 q[U]; float e[U];
+#pragma unroll
+				for (uint32_t u = 0; u < U; ++u) { q[u] = qn[u]; e[u] = en[u]; }
+				if (c + U < to) {
+#pragma unroll
+					for (uint32_t u = 0; u < U; ++u) { const uint32_t s = min(base + c + U + u, last); qn[u] = sa[s]; en[u] = ekt[s]; }
+				}
+#pragma unroll
+				for (uint32_t u = 0; u < U; ++u) {
+					if (c + u >= to || S.T < 1e-4f) { done = true; break; }
+					const uint32_t s = base + c + u;
+					if ((s & (SCAN_CK - 1)) == 0) { ck4[s / SCAN_CK] = make_float4(S.T, S.r0, S.r1, S.r2); cke[s / SCAN_CK] = S.ek; }
+					const float w = q[u].x * S.T;
+					S.r0 += w * q[u].y; S.r1 += w * q[u].z; S.r2 += w * q[u].w;
+					S.ws += w;
+					S.ek += e[u];
+					S.T *= (1.f - q[u].x);
+					++S.cn;
+				}
+			}
+		}
+		ccount[i] = S.cn;
+		racc[i] = make_float4(S.r0, S.r1, S.r2, S.ws);
+		rT[i] = S.T;
+		rek[i] = S.ek;
+		if (list && S.cn == e1 && e1 < ns && S.T >= 1e-4f) {
+			const uint32_t m = min(ns, e2) - e1;
+			const uint32_t p = atomicAdd(next_counter, m);
+			for (uint32_t j = 0; j < m; ++j) list[p + j] = base + e1 + j;
+		}
 	}
 }
 
@@ -886,7 +979,24 @@ void debug_launch_march_stats(hipStream_t s, uint32_t n_rays, const float* rays,
 static inline uint32_t sample_blocks(uint32_t cap) { return std::max<uint32_t>(1, std::min<uint32_t>((cap + 255) / 256, 16384)); }
 void launch_loss_alpha(hipStream_t s, uint32_t cap_samples, const StepState* st, const float* coords, const half_t* net_out, float cos_anneal,
                        const LossWork& w) {
-	k_loss_alpha<<<sample_blocks(cap_samples), 256, 0, s>>>(cap_samples, st, coords, net_out, cos_anneal, w.sa, w.ekt);
+	k_loss_alpha<<<sample_blocks(cap_samples), 256, 0, s>>>(cap_samples, &st->n_kept, nullptr, coords, net_out, cos_anneal, w.sa, w.ekt);
+}
+void launch_loss_alpha_list(hipStream_t s, uint32_t cap_samples, const uint32_t* n_ptr, const uint32_t* idx, const float* coords,
+                            const half_t* net_out, float cos_anneal, const LossWork& w) {
+	k_loss_alpha<<<sample_blocks(cap_samples), 256, 0, s>>>(cap_samples, n_ptr, idx, coords, net_out, cos_anneal, w.sa, w.ekt);
+}
+void launch_chunk_count(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, uint32_t e1, uint32_t* m, uint32_t* counters,
+                        uint32_t n_counters) {
+	k_chunk_count<<<ray_blocks(cap_rays), 256, 0, s>>>(cap_rays, numsteps, e1, m, counters, n_counters);
+}
+void launch_chunk_write(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, const uint32_t* m, const uint32_t* pos, uint32_t* list,
+                        uint32_t* counter) {
+	k_chunk_write<<<ray_blocks(cap_rays), 256, 0, s>>>(cap_rays, numsteps, m, pos, list, counter);
+}
+void launch_loss_scan_chunk(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, const LossWork& w, uint32_t* ccount, uint32_t e0,
+                            uint32_t e1, uint32_t e2, uint32_t* list, uint32_t* next_counter) {
+	k_loss_scan_chunk<<<ray_blocks(cap_rays), 256, 0, s>>>(cap_rays, numsteps, w.sa, w.ekt, w.ck4, w.cke, ccount, w.racc, w.rT, w.rek, e0, e1, e2,
+	                                                       list, next_counter);
 }
 void launch_loss_scan_ray(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, const LossWork& w, uint32_t* ccount) {
 	const uint32_t blocks = ray_blocks(cap_rays);

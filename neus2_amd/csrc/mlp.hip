@@ -515,10 +515,10 @@ __device__ __forceinline__ void density_forward(const FwdW& w, const h8* dinB, i
 // (their storage precision), not fp32 tiles. n from device memory; 32 samples per wave-iteration,
 // grid-strided.
 // ------------------------------------------------------------------------------------------
-template <int L, int W>
+template <int L, int W, bool IDX>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) k_nerf_infer(const uint32_t* __restrict__ n_ptr, uint32_t n_fixed, const float* __restrict__ coords,
                                                     const GridLevels gl, uint32_t valid_level, const half_t* __restrict__ grid,
-                                                    MlpPtrs wp, half_t* __restrict__ out) {
+                                                    MlpPtrs wp, half_t* __restrict__ out, const uint32_t* __restrict__ idx) {
 	constexpr int DKS = Dims<L>::DKS, DMT = Dims<L>::DMT, HALF = Fused<L>::HALF, M0 = Fused<L>::M0;
 	constexpr int MT = (W + 31) / 32, HKS = W / 16;
 	__shared__ half_t sm[FwdSmem<L, W>::END];
@@ -534,10 +534,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))
 	const half_t bias_h = (half_t)wp.sdf_bias;
 	for (uint32_t base = wave * 32; base < n; base += n_waves * 32) {
 		const FwdW w = w0.at(opaque_zero());
-		const uint32_t i = base + r;
-		const bool valid = i < n;
-		const uint32_t ic = valid ? i : 0;
-		const float* c = coords + (size_t)ic * COORD_W;
+		const uint32_t j = base + r;
+		const bool valid = j < n;
+		const uint32_t i = valid ? (IDX ? idx[j] : j) : 0;
+		const float* c = coords + (size_t)i * COORD_W;
 		const float x[3] = {c[0], c[1], c[2]}, wd[3] = {c[4], c[5], c[6]};
 		// ---- encode this lane's levels
 		h2 ev[M0];
@@ -1277,11 +1277,14 @@ bool mlp_supported(uint32_t L, uint32_t W) {
 }
 
 void launch_nerf_infer(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_ptr, uint32_t n_fixed, const float* coords, const GridLevels& gl,
-                       uint32_t valid_level, const half_t* grid, const MlpPtrs& w, half_t* out, uint32_t blocks) {
-	// persistent grid: at most the resident capacity (weights are staged once per block)
+                       uint32_t valid_level, const half_t* grid, const MlpPtrs& w, half_t* out, uint32_t blocks, const uint32_t* idx) {
+	// persistent grid: at most the resident capacity (weights are staged once per block; both variants run at the
+	// same 3 waves per SIMD, amdgpu_waves_per_eu)
 #define X(l, w_) if (L == l && W == w_) { \
-		static const uint32_t cap = resident_blocks((const void*)k_nerf_infer<l, w_>, 256); \
-		k_nerf_infer<l, w_><<<std::min(blocks, cap), 256, 0, s>>>(n_ptr, n_fixed, coords, gl, valid_level, grid, w, out); return; }
+		static const uint32_t cap = resident_blocks((const void*)k_nerf_infer<l, w_, false>, 256); \
+		if (idx) k_nerf_infer<l, w_, true><<<std::min(blocks, cap), 256, 0, s>>>(n_ptr, n_fixed, coords, gl, valid_level, grid, w, out, idx); \
+		else k_nerf_infer<l, w_, false><<<std::min(blocks, cap), 256, 0, s>>>(n_ptr, n_fixed, coords, gl, valid_level, grid, w, out, nullptr); \
+		return; }
 	NEUS_MLP_CONFIGS(X)
 #undef X
 }

@@ -214,8 +214,15 @@ struct NeusTestbed {
 	Dev<uint16_t> sc_rec_i;
 	// restructured loss scratch (kernels.h LossWork)
 	Dev<float4> l_sa, l_ck4, l_racc, l_rgr;
-	Dev<float> l_ekt, l_cke, l_rT;
+	Dev<float> l_ekt, l_cke, l_rT, l_rek;
 	Dev<uint32_t> sample_ray;
+	// progressive (cut-off-aware) inference: 0 off, 1 auto (when under PROGRESSIVE_RATIO of the kept samples were
+	// composited at the last loss readback), 2 always; chunk ends of the rounds before the last (march.hip)
+	int progressive_mode = 1;
+	std::vector<uint32_t> chunk_ends{32, 80};
+	float last_keep_ratio = 1.f;
+	static constexpr float PROGRESSIVE_RATIO = 0.7f;
+	Dev<uint32_t> chunk_list, chunk_cnt;
 	TrainBufs tbuf{};
 	// RNG + counters (testbed.cu:2087-2101)
 	pcg32 rng, density_grid_rng;
@@ -481,7 +488,8 @@ struct NeusTestbed {
 		numsteps.alloc(2 * (size_t)MAX_RAYS); ccount.alloc(MAX_RAYS); cbase.alloc(MAX_RAYS);
 		l_sa.alloc(max_samples); l_ekt.alloc(max_samples); sample_ray.alloc(max_samples);
 		l_ck4.alloc(max_samples / 8 + 1); l_cke.alloc(max_samples / 8 + 1);
-		l_racc.alloc(MAX_RAYS); l_rgr.alloc(MAX_RAYS); l_rT.alloc(MAX_RAYS);
+		l_racc.alloc(MAX_RAYS); l_rgr.alloc(MAX_RAYS); l_rT.alloc(MAX_RAYS); l_rek.alloc(MAX_RAYS);
+		chunk_list.alloc(max_samples); chunk_cnt.alloc(16);
 		loss.alloc(MAX_RAYS); ek.alloc(MAX_RAYS); mask.alloc(MAX_RAYS); loss_sum.alloc(4);
 		coords.alloc((size_t)max_samples * COORD_W); net_out.alloc((size_t)max_samples * OUT_W);
 		coords_c.alloc((size_t)batch * COORD_W); dL_dout.alloc((size_t)batch * OUT_W);
@@ -975,14 +983,34 @@ struct NeusTestbed {
 		// DeltaNetwork forward on the samples (nerf_network.h:162-182); the loss keeps the undeformed records
 		const float* c_in = coords.p;
 		if (use_delta) { launch_delta_apply(s, &st.p->n_kept, max_samples, COORD_W, coords.p, coords_def.p, delta.p); c_in = coords_def.p; }
-		launch_nerf_infer(s, lay.L, lay.W, &st.p->n_kept, 0, c_in, gl, valid, params_h.p + lay.grid_off, mlp, net_out.p, 8192);
-		mark(3);
 		LossParams lp{};
 		lp.loss_scale = LOSS_SCALE; lp.ek_w = cfg.ek_loss_weight; lp.mask_w = cfg.mask_loss_weight; lp.cos_anneal = cos_anneal();
 		lp.max_compacted = batch; lp.rng_state = rng.state; lp.rng_inc = rng.inc; lp.jt = jump_table();
 		const LossWork w = loss_work(base.p);
-		launch_loss_alpha(s, max_samples, st.p, coords.p, net_out.p, lp.cos_anneal, w);
-		launch_loss_scan_ray(s, MAX_RAYS, numsteps.p, w, ccount.p);
+		if (progressive_mode == 2 || (progressive_mode == 1 && last_keep_ratio < PROGRESSIVE_RATIO)) {
+			// rounds of per-ray chunks, each: network on the round's samples, alpha, the recurrence continued (march.hip);
+			// the "infer" phase mark then covers the composite as well
+			const uint32_t nch = (uint32_t)chunk_ends.size() + 1;
+			// round 0's list through ccount / cbase (both rewritten before they are read: round 0 does not read ccount)
+			launch_chunk_count(s, MAX_RAYS, numsteps.p, chunk_ends[0], ccount.p, chunk_cnt.p, nch + 1);
+			launch_exclusive_scan(s, scan_tmp.p, scan_tmp_bytes, ccount.p, cbase.p, MAX_RAYS);
+			launch_chunk_write(s, MAX_RAYS, numsteps.p, ccount.p, cbase.p, chunk_list.p, chunk_cnt.p);
+			uint32_t e0 = 0;
+			for (uint32_t k = 0; k < nch; ++k) {
+				const uint32_t e1 = k + 1 < nch ? chunk_ends[k] : 0xffffffffu;
+				const uint32_t e2 = k + 2 < nch ? chunk_ends[k + 1] : 0xffffffffu;
+				launch_nerf_infer(s, lay.L, lay.W, chunk_cnt.p + k, 0, c_in, gl, valid, params_h.p + lay.grid_off, mlp, net_out.p, 8192, chunk_list.p);
+				launch_loss_alpha_list(s, max_samples, chunk_cnt.p + k, chunk_list.p, coords.p, net_out.p, lp.cos_anneal, w);
+				launch_loss_scan_chunk(s, MAX_RAYS, numsteps.p, w, ccount.p, e0, e1, e2, k + 1 < nch ? chunk_list.p : nullptr, chunk_cnt.p + k + 1);
+				e0 = e1;
+			}
+			mark(3);
+		} else {
+			launch_nerf_infer(s, lay.L, lay.W, &st.p->n_kept, 0, c_in, gl, valid, params_h.p + lay.grid_off, mlp, net_out.p, 8192);
+			mark(3);
+			launch_loss_alpha(s, max_samples, st.p, coords.p, net_out.p, lp.cos_anneal, w);
+			launch_loss_scan_ray(s, MAX_RAYS, numsteps.p, w, ccount.p);
+		}
 		launch_exclusive_scan(s, scan_tmp.p, scan_tmp_bytes, ccount.p, cbase.p, MAX_RAYS);
 		launch_loss_ray(s, MAX_RAYS, st.p, dp, ds, lp, numsteps.p, ccount.p, cbase.p, w, loss.p, ek.p, mask.p);
 		launch_loss_grad(s, max_samples, st.p, dp, lp, coords.p, net_out.p, numsteps.p, w, coords_c.p, dL_dout.p);
@@ -1052,7 +1080,7 @@ struct NeusTestbed {
 	LossWork loss_work(const uint32_t* rbase) {
 		LossWork w{};
 		w.sa = l_sa.p; w.ck4 = l_ck4.p; w.cke = l_cke.p; w.ekt = l_ekt.p; w.sample_ray = sample_ray.p; w.rbase = rbase;
-		w.racc = l_racc.p; w.rT = l_rT.p; w.rgr = l_rgr.p;
+		w.racc = l_racc.p; w.rT = l_rT.p; w.rgr = l_rgr.p; w.rek = l_rek.p;
 		return w;
 	}
 
@@ -1085,6 +1113,7 @@ struct NeusTestbed {
 		ek_loss = pinned[1] * scale;
 		mask_loss = pinned[2] * scale;
 		last_rays_with_samples = sst->n_rays_with_samples;
+		last_keep_ratio = sst->n_kept ? measured / (float)sst->n_kept : 1.f;  // composited / kept (progressive inference)
 		ray_loss = sst->n_rays_with_samples ? pinned[0] * (float)(sst->rays_per_batch * world) / (float)sst->n_rays_with_samples : 0.f;
 		if (!loss_ema_init) { loss_scalar_ema = last_loss; loss_ema_init = true; }
 		else loss_scalar_ema = 0.99f * loss_scalar_ema + 0.01f * last_loss;
@@ -1374,6 +1403,19 @@ int neus_testbed_get_training_options(NeusTestbed* tb, NeusTrainingOptions* o) {
 		o->near_distance = tb->near_distance;
 	});
 }
+int neus_testbed_set_progressive_inference(NeusTestbed* tb, int mode, const uint32_t* chunk_ends, uint32_t n_ends) {
+	return guard([&] {
+		if (mode < 0 || mode > 2) throw std::runtime_error("progressive inference mode must be 0 (off), 1 (auto) or 2 (always)");
+		if (chunk_ends && n_ends) {
+			if (n_ends > 14) throw std::runtime_error("at most 14 chunk ends");
+			for (uint32_t k = 0; k < n_ends; ++k)
+				if (chunk_ends[k] == 0 || (k && chunk_ends[k] <= chunk_ends[k - 1])) throw std::runtime_error("chunk ends must increase from >= 1");
+			tb->chunk_ends.assign(chunk_ends, chunk_ends + n_ends);
+		}
+		tb->progressive_mode = mode;
+	});
+}
+
 int neus_testbed_set_training_options(NeusTestbed* tb, const NeusTrainingOptions* o) {
 	return guard([&] {
 		if (!o) throw std::runtime_error("set_training_options: null options");

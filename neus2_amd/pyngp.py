@@ -631,6 +631,15 @@ class Testbed:
         self._aabb = (np.full(3, 0.5 - infl, np.float32), np.full(3, 0.5 + infl, np.float32))
         self._scale, self._offset, self._from_na = 1.0, np.zeros(3, np.float32), False
 
+    def set_progressive_inference(self, mode, chunk_ends=None):
+        """Training-step inference in rounds of per-ray sample chunks, skipping the samples past the T < 1e-4 cut
+        (bit-identical to one pass; an option of this implementation). mode: 0 off, 1 auto (default), 2 always;
+        chunk_ends: the increasing round boundaries (default 32, 80)."""
+        e = None if chunk_ends is None else np.ascontiguousarray(chunk_ends, np.uint32)
+        check(lib().neus_testbed_set_progressive_inference(self._h, C.c_int(int(mode)),
+                                                           None if e is None else C.c_void_p(e.ctypes.data),
+                                                           C.c_uint32(0 if e is None else len(e))))
+
     # ------------------------------------------------------------------ options (device dataset)
     def _get_options(self):
         o = _lib.NeusTrainingOptions()

@@ -27,3 +27,15 @@ for w in (5, 25, 200, 800, 2000):
     print(f"step {w}: Npre {st['measured_batch_size_before_compaction']} n_kept~{min(tot_req, 1 << 22)} sum nreq {tot_req} "
           f"sum ccount {tot_cc} ({tot_cc / max(1, tot_req):.3f}) rays with samples {int(has.sum())} "
           f"nreq p50/p90/p99/max {q} ccount/nreq mean {frac.mean():.3f} compacted {st['measured_batch_size']}", flush=True)
+    # samples a chunked (progressive) inference would evaluate: rounds of per-ray chunks [e_k, e_k+1) until the chunk
+    # that holds the ray's last composited sample; launches = rounds with any active ray
+    n, c = nreq[has].astype(np.int64), np.maximum(cc[has].astype(np.int64), 1)
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    np.savez_compressed(os.path.join(ROOT, "gpurun_out", f"cutoff_{w}.npz"), nreq=n.astype(np.uint16), cc=c.astype(np.uint16),
+                        ns=ns[has].astype(np.uint16))
+    for sched in ((16,), (32,), (8, 32), (16, 64), (16, 48, 112), (8, 16, 32, 64)):
+        ends = np.array(sched + (1 << 30,), np.int64)
+        k = np.searchsorted(ends, c)  # first chunk end >= c
+        inf = np.minimum(n, ends[k])
+        act = [int((k >= j).sum()) for j in range(len(ends))]
+        print(f"   chunks {sched}: inferred {int(inf.sum())} ({inf.sum() / max(1, tot_req):.3f}) active rays per round {act}", flush=True)

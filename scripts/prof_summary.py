@@ -77,6 +77,14 @@ def main():
         lines.append(f"| {k} | {c} | {t / 1e6:.3f} | {t / c / 1e3:.1f} | {100 * t / total:.1f}% |" + extra)
     if last:
         lines.append(f"\nGPU kernel time per step over the last {last} steps: {total / last / 1e6:.3f} ms")
+        # the launch sequence of the final step (start offset, duration), e.g. the progressive-inference rounds
+        con = sqlite3.connect(sys.argv[1])
+        ks = list(con.execute("select name, start, end from kernels order by start"))
+        adam = [i for i, r in enumerate(ks) if "k_adam_ema" in r[0]]
+        seq = ks[adam[-2] + 1:adam[-1] + 1]
+        t0 = seq[0][1]
+        lines.append("\nLaunch sequence of the final step (start us, duration us):\n")
+        lines += [f"    {(st - t0) / 1e3:9.1f} {(en - st) / 1e3:8.1f}  {short(n)}" for n, st, en in seq]
     text = "\n".join(lines) + "\n"
     if len(sys.argv) > 2:
         open(sys.argv[2], "w").write(text)
