@@ -166,7 +166,7 @@ void launch_sdf_grid(hipStream_t s, uint32_t L, uint32_t W, const uint32_t res[3
 void launch_mlp_train(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_valid_ptr, uint32_t n, uint32_t ld, const float* coords,
                       const half_t* enc, const float* dydx, const half_t* dL_dout, const MlpPtrs& w, const TrainBufs& tb, int part = 0 /* 0 both, 1 colour, 2 density */);
 void launch_wgrad(hipStream_t s, const WGradJobs& jobs, uint32_t n_blocks);
-uint32_t mlp_train_blocks(uint32_t n);  // grid of the training MLP kernels (= the variance partial count)
+uint32_t mlp_train_blocks(uint32_t L, uint32_t W, uint32_t n);  // grid of the training MLP kernels (= the variance partial count)
 void launch_mfma_probe(hipStream_t s, const half_t* A, const half_t* B, float* C);
 // march.hip
 void launch_bitfield_linear(hipStream_t s, const uint8_t* bitfield, uint32_t* lin /* LIN_WORDS */);

@@ -369,12 +369,22 @@ __device__ __forceinline__ float slot_dydx(int q, int h, int d, const float dy[]
 }
 
 // fp16 B fragment (k-step s) of an accumulator tile, optionally through ReLU: (half)max(acc, 0) is the
-// reference's fp16 storage of the post-activation value
+// reference's fp16 storage of the post-activation value. The ReLU runs on the rounded fp16 bits as a packed
+// int16 max with 0 (a set sign bit - negative values and -0 - gives +0): the same bits as rounding max(acc, 0)
+// for every non-NaN acc, in one packed op per 2 values instead of an fp32 max per value plus the IEEE-mode
+// quieting max the compiler puts before it (MFMA results are not known canonical). A NaN passes as NaN.
+typedef short s2v __attribute__((ext_vector_type(2)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef _Float16 hh2v __attribute__((ext_vector_type(2)));
 template <bool RELU>
 __device__ __forceinline__ h8 frag(const f16v& acc, int s) {
 	h8 b;
 #pragma unroll
-	for (int j = 0; j < 8; ++j) b[j] = (half_t)(RELU ? fmaxf(acc[8 * s + j], 0.f) : acc[8 * s + j]);
+	for (int j = 0; j < 8; j += 2) {
+		hh2v p = __builtin_convertvector((f2v){acc[8 * s + j], acc[8 * s + j + 1]}, hh2v);
+		if (RELU) p = __builtin_bit_cast(hh2v, __builtin_elementwise_max(__builtin_bit_cast(s2v, p), (s2v)0));
+		b[j] = p[0]; b[j + 1] = p[1];
+	}
 	return b;
 }
 
@@ -1323,7 +1333,7 @@ void launch_sdf_grid(hipStream_t s, uint32_t L, uint32_t W, const uint32_t res[3
 }
 void launch_mlp_train(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_valid_ptr, uint32_t n, uint32_t ld, const float* coords,
                       const half_t* enc, const float* dydx, const half_t* dL_dout, const MlpPtrs& w, const TrainBufs& tb, int part) {
-	const uint32_t blocks = mlp_train_blocks(n);
+	const uint32_t blocks = mlp_train_blocks(L, W, n);
 	if (n == 0) return;
 #define X(l, w_) if (L == l && W == w_) { \
 		if (part != 2) k_mlp_train_rgb<l, w_><<<blocks, 256, 0, s>>>(n_valid_ptr, n, ld, coords, enc, dydx, dL_dout, w, tb); \
@@ -1338,7 +1348,18 @@ void launch_wgrad(hipStream_t s, const WGradJobs& jobs, uint32_t n_blocks) {
 	for (uint32_t k = 0; k < jobs.n_jobs; ++k) tiles += jobs.j[k].tiles_m * jobs.j[k].tiles_k;
 	k_wgrad_reduce<<<(tiles + 1) * WR_CHUNKS, 256, 0, s>>>(jobs);
 }
-uint32_t mlp_train_blocks(uint32_t n) { return std::min<uint32_t>((n + 127) / 128, 2048); }
+// persistent grid: at most the resident capacity of the two training kernels, so the ~53 KB weight staging runs
+// once per block (one wave per SIMD: a grid of n / 128 blocks re-staged the weights for every 128 samples)
+uint32_t mlp_train_blocks(uint32_t L, uint32_t W, uint32_t n) {
+	uint32_t cap = 2048;
+#define X(l, w_) if (L == l && W == w_) { \
+		static const uint32_t c = std::min(resident_blocks((const void*)k_mlp_train_rgb<l, w_>, 256), \
+		                                   resident_blocks((const void*)k_mlp_train_density<l, w_>, 256)); \
+		cap = std::min(cap, c); }
+	NEUS_MLP_CONFIGS(X)
+#undef X
+	return std::max<uint32_t>(1, std::min<uint32_t>((n + 127) / 128, cap));
+}
 void launch_mfma_probe(hipStream_t s, const half_t* A, const half_t* B, float* C) { k_mfma_probe<<<1, 64, 0, s>>>(A, B, C); }
 
 } // namespace neus

@@ -458,7 +458,7 @@ struct NeusTestbed {
 		tbuf.dLdenc = take(2 * (size_t)l.L * ld); tbuf.genc = take(2 * (size_t)l.L * ld);
 		tbuf.v = vbuf.p;
 		tbuf.var_grad = grads.p + l.var_off;
-		var_partial.alloc(mlp_train_blocks(batch));
+		var_partial.alloc(mlp_train_blocks(l.L, l.W, batch));
 		tbuf.var_partial = var_partial.p;
 		wgrad_partial.alloc((size_t)wgrad_jobs(batch, batch, grads.p, nullptr).block_start[5] * 1024);
 		tbuf.indeed_batch = (float)batch * (float)world;
@@ -680,7 +680,7 @@ struct NeusTestbed {
 		J.n_valid = n_valid;
 		J.partial = wgrad_partial.p;
 		J.var_partial = var_partial.p;
-		J.var_blocks = mlp_train_blocks(n);
+		J.var_blocks = mlp_train_blocks(lay.L, lay.W, n);
 		J.var_grad = g + lay.var_off;
 		return J;
 	}
