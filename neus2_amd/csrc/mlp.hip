@@ -369,12 +369,10 @@ __device__ __forceinline__ float slot_dydx(int q, int h, int d, const float dy[]
 }
 
 // fp16 B fragment (k-step s) of an accumulator tile, optionally through ReLU: (half)max(acc, 0) is the
-// reference's fp16 storage of the post-activation value. The ReLU runs on the rounded fp16 bits as a packed
-// int16 max with 0 (a set sign bit - negative values and -0 - gives +0): the same bits as rounding max(acc, 0)
-// for every non-NaN acc, in one packed op per 2 values instead of an fp32 max per value plus the IEEE-mode
-// quieting max the compiler puts before it (MFMA results are not known canonical). A NaN passes as NaN.
-typedef short s2v __attribute__((ext_vector_type(2)));
-typedef float f2v __attribute__((ext_vector_type(2)));
+// reference's fp16 storage of the post-activation value. The ReLU runs after the packed conversion as a packed
+// fp16 max with 0 (rounding is monotone, so the values are those of rounding max(acc, 0); a NaN gives 0 as the
+// reference's `x > 0 ? x : 0`): one op per 2 values instead of an fp32 max per value plus the IEEE-mode
+// quieting max the compiler puts before it (MFMA results are not known canonical; conversion results are).
 typedef _Float16 hh2v __attribute__((ext_vector_type(2)));
 template <bool RELU>
 __device__ __forceinline__ h8 frag(const f16v& acc, int s) {
@@ -382,7 +380,7 @@ __device__ __forceinline__ h8 frag(const f16v& acc, int s) {
 #pragma unroll
 	for (int j = 0; j < 8; j += 2) {
 		hh2v p = __builtin_convertvector((f2v){acc[8 * s + j], acc[8 * s + j + 1]}, hh2v);
-		if (RELU) p = __builtin_bit_cast(hh2v, __builtin_elementwise_max(__builtin_bit_cast(s2v, p), (s2v)0));
+		if (RELU) p = __builtin_elementwise_max(p, (hh2v)0);
 		b[j] = p[0]; b[j + 1] = p[1];
 	}
 	return b;
@@ -516,6 +514,84 @@ __device__ __forceinline__ void density_forward(const FwdW& w, const h8* dinB, i
 		for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.d0T, DIN, 32 * mt + r, 16 * ks, h), GhB[ks], acc);
 		Gi[mt] = rh16(acc);
 	}
+}
+
+// The same two forwards with the fp16-stored activations held as B fragments (half the registers of fp32
+// tiles; the training kernels run at one wave per SIMD, so registers set their latency hiding). Fragment k of
+// tile mt holds the tile's registers 8k .. 8k+7, i.e. rows 16 (2 mt + k) + pi_row(j, h): exactly the k-step
+// 2 mt + k operand of the next layer and the rows store_frag writes. Values are bit-identical to rounding the
+// fp32 tiles (frag: (half)relu(acc) == (half)rh(relu(acc))).
+template <int L, int W>
+__device__ __forceinline__ void density_forward_frag(const FwdW& w, const h8* dinB, int r, int h, h8* H0B, h8& D1B, h8* GhB, f16v* Gi) {
+	constexpr int DIN = Dims<L>::DIN, DKS = Dims<L>::DKS, DMT = Dims<L>::DMT, MT = (W + 31) / 32, HKS = W / 16;
+#pragma unroll
+	for (int mt = 0; mt < MT; ++mt) {
+		f16v acc = zero16();
+#pragma unroll
+		for (int ks = 0; ks < DKS; ++ks) acc = mfma(loadA(w.d0, W, 32 * mt + r, 16 * ks, h), dinB[ks], acc);
+		H0B[2 * mt] = frag<true>(acc, 0);
+		if (2 * mt + 1 < HKS) H0B[2 * mt + 1] = frag<true>(acc, 1);  // W = 16: one 16-row half
+	}
+	{
+		f16v acc = zero16();
+#pragma unroll
+		for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.d1, 16, r, 16 * ks, h), H0B[ks], acc);
+		D1B = frag<false>(acc, 0);
+	}
+#pragma unroll
+	for (int ks = 0; ks < HKS; ++ks) {
+		const h8 w1row = loadA(w.d1, 16, 0, 16 * ks, h);
+#pragma unroll
+		for (int j = 0; j < 8; ++j) GhB[ks][j] = H0B[ks][j] > (half_t)0.f ? w1row[j] : (half_t)0.f;
+	}
+#pragma unroll
+	for (int mt = 0; mt < DMT; ++mt) {
+		f16v acc = zero16();
+#pragma unroll
+		for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.d0T, DIN, 32 * mt + r, 16 * ks, h), GhB[ks], acc);
+		Gi[mt] = rh16(acc);
+	}
+}
+template <int W>
+__device__ __forceinline__ void rgb_hidden_frag(const FwdW& w, const h8& D1B, const float x[3], const float wd[3], const float grad[3],
+                                                int r, int h, h8 rinB[3], h8* H1B, h8* H2B) {
+	constexpr int MT = (W + 31) / 32, HKS = W / 16;
+	rinB[0] = D1B;
+	{
+		float sh[16]; sh16(wd, sh);
+#pragma unroll
+		for (int j = 0; j < 8; ++j) rinB[1][j] = (half_t)hsel(h, sh[pi_row(j, 1)], sh[pi_row(j, 0)]);
+		float r32[16];
+#pragma unroll
+		for (int k = 0; k < 16; ++k) r32[k] = 0.f;
+		r32[0] = x[0]; r32[1] = x[1]; r32[2] = x[2];
+		r32[3] = grad[0]; r32[4] = grad[1]; r32[5] = grad[2];
+#pragma unroll
+		for (int j = 0; j < 8; ++j) rinB[2][j] = (half_t)hsel(h, r32[pi_row(j, 1)], r32[pi_row(j, 0)]);
+	}
+#pragma unroll
+	for (int mt = 0; mt < MT; ++mt) {
+		f16v acc = zero16();
+#pragma unroll
+		for (int ks = 0; ks < 3; ++ks) acc = mfma(loadA(w.r0, W, 32 * mt + r, 16 * ks, h), rinB[ks], acc);
+		H1B[2 * mt] = frag<true>(acc, 0);
+		if (2 * mt + 1 < HKS) H1B[2 * mt + 1] = frag<true>(acc, 1);
+	}
+#pragma unroll
+	for (int mt = 0; mt < MT; ++mt) {
+		f16v acc = zero16();
+#pragma unroll
+		for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w.r1, W, 32 * mt + r, 16 * ks, h), H1B[ks], acc);
+		H2B[2 * mt] = frag<true>(acc, 0);
+		if (2 * mt + 1 < HKS) H2B[2 * mt + 1] = frag<true>(acc, 1);
+	}
+}
+// relu'(Y) . acc as a fragment: (half)acc where the stored activation fragment m is > 0, else 0
+__device__ __forceinline__ h8 mask_frag(const f16v& acc, int k, const h8& m) {
+	h8 b;
+#pragma unroll
+	for (int j = 0; j < 8; ++j) b[j] = m[j] > (half_t)0.f ? (half_t)acc[8 * k + j] : (half_t)0.f;
+	return b;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -908,9 +984,9 @@ __global__ void __launch_bounds__(256) k_mlp_train_rgb(const uint32_t* __restric
 		// ---- forward recompute up to the colour hidden layers
 		h8 dinB[DKS];
 		build_din<L>(dinB, x, enc_h, ld, ic, h);
-		f16v H0[MT], D1, Gi[DMT];
-		h8 GhB[HKS];
-		density_forward<L, W>(fw, dinB, r, h, H0, D1, GhB, Gi);
+		h8 H0B[HKS], D1B, GhB[HKS];
+		f16v Gi[DMT];
+		density_forward_frag<L, W>(fw, dinB, r, h, H0B, D1B, GhB, Gi);
 		float part[3] = {0.f, 0.f, 0.f};
 #pragma unroll
 		for (int mt = 0; mt < DMT; ++mt)
@@ -931,8 +1007,8 @@ __global__ void __launch_bounds__(256) k_mlp_train_rgb(const uint32_t* __restric
 #pragma unroll
 		for (int d = 0; d < 3; ++d) grad[d] = part[d] + __shfl_xor(part[d], 32);
 		h8 rinB[3];
-		f16v H1[MT], H2[MT];
-		rgb_hidden<W>(fw, D1, x, wd, grad, r, h, rinB, H1, H2);
+		h8 H1B[HKS], H2B[HKS];
+		rgb_hidden_frag<W>(fw, D1B, x, wd, grad, r, h, rinB, H1B, H2B);
 		// ---- colour backward
 		const h8 dlo = *(const h8*)(dL_dout + (size_t)ic * OUT_W + 8 * h);   // h=0: rows 0..7, h=1: rows 8..15
 		const h8 dlo_o = shfl_xor_h8(dlo, 32);
@@ -942,29 +1018,27 @@ __global__ void __launch_bounds__(256) k_mlp_train_rgb(const uint32_t* __restric
 		// delta_o (rows 0..2 = dL/drgb): B fragment, pi order -> lane h=0 elements 0..2
 		h8 dOB = (h8){0, 0, 0, 0, 0, 0, 0, 0};
 		if (h == 0) { dOB[0] = dlo_lo[0]; dOB[1] = dlo_lo[1]; dOB[2] = dlo_lo[2]; }
-		f16v dH2[MT], dH1[MT];
+		h8 dH2B[HKS], dH1B[HKS];
 #pragma unroll
 		for (int mt = 0; mt < MT; ++mt) {
-			f16v acc = mfma(loadA(bw.r2T, W, 32 * mt + r, 0, h), dOB, zero16());
-#pragma unroll
-			for (int q = 0; q < 16; ++q) acc[q] = H2[mt][q] > 0.f ? rh(acc[q]) : 0.f;
-			dH2[mt] = acc;
+			const f16v acc = mfma(loadA(bw.r2T, W, 32 * mt + r, 0, h), dOB, zero16());
+			dH2B[2 * mt] = mask_frag(acc, 0, H2B[2 * mt]);
+			if (2 * mt + 1 < HKS) dH2B[2 * mt + 1] = mask_frag(acc, 1, H2B[2 * mt + 1]);
 		}
 #pragma unroll
 		for (int mt = 0; mt < MT; ++mt) {
 			f16v acc = zero16();
 #pragma unroll
-			for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(bw.r1T, W, 32 * mt + r, 16 * ks, h), accB(dH2[ks >> 1], ks & 1), acc);
-#pragma unroll
-			for (int q = 0; q < 16; ++q) acc[q] = H1[mt][q] > 0.f ? rh(acc[q]) : 0.f;
-			dH1[mt] = acc;
+			for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(bw.r1T, W, 32 * mt + r, 16 * ks, h), dH2B[ks], acc);
+			dH1B[2 * mt] = mask_frag(acc, 0, H1B[2 * mt]);
+			if (2 * mt + 1 < HKS) dH1B[2 * mt + 1] = mask_frag(acc, 1, H1B[2 * mt + 1]);
 		}
 		f16v dRin[2];
 #pragma unroll
 		for (int mt = 0; mt < 2; ++mt) {
 			f16v acc = zero16();
 #pragma unroll
-			for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(bw.r0T, 48, 32 * mt + r, 16 * ks, h), accB(dH1[ks >> 1], ks & 1), acc);
+			for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(bw.r0T, 48, 32 * mt + r, 16 * ks, h), dH1B[ks], acc);
 			dRin[mt] = rh16(acc);
 		}
 		// delta_D1 = dL/drgb_in[0:16], row 0 += dL_dout[3] (half add)
@@ -981,11 +1055,11 @@ __global__ void __launch_bounds__(256) k_mlp_train_rgb(const uint32_t* __restric
 		v[0] += (float)dlo_hi[0]; v[1] += (float)dlo_hi[1]; v[2] += (float)dlo_hi[2];
 		if (valid) {
 #pragma unroll
-			for (int mt = 0; mt < MT; ++mt) {
-				store_acc(tb.r0_delta, ld, i, dH1[mt], mt, W, h);
-				store_acc(tb.r1_delta, ld, i, dH2[mt], mt, W, h);
-				store_acc(tb.r1_x, ld, i, H1[mt], mt, W, h);
-				store_acc(tb.r2_x, ld, i, H2[mt], mt, W, h);
+			for (int ks = 0; ks < HKS; ++ks) {
+				store_frag(tb.r0_delta, ld, i, dH1B[ks], ks, W, h);
+				store_frag(tb.r1_delta, ld, i, dH2B[ks], ks, W, h);
+				store_frag(tb.r1_x, ld, i, H1B[ks], ks, W, h);
+				store_frag(tb.r2_x, ld, i, H2B[ks], ks, W, h);
 			}
 #pragma unroll
 			for (int ks = 0; ks < 3; ++ks) store_frag(tb.r0_x, ld, i, rinB[ks], ks, 48, h);
@@ -1034,27 +1108,26 @@ __global__ void __launch_bounds__(256) k_mlp_train_density(const uint32_t* __res
 		const float x[3] = {c[0], c[1], c[2]};
 		h8 dinB[DKS];
 		build_din<L>(dinB, x, enc_h, ld, ic, h);
-		f16v H0[MT], D1, Gi[DMT];
-		h8 GhB[HKS];
-		density_forward<L, W>(fw, dinB, r, h, H0, D1, GhB, Gi);
+		h8 H0B[HKS], D1B, GhB[HKS];
+		f16v Gi[DMT];
+		density_forward_frag<L, W>(fw, dinB, r, h, H0B, D1B, GhB, Gi);
 		// delta_D1 from the colour kernel (d1_delta column i), B fragment in pi order
 		h8 dD1B;
 #pragma unroll
 		for (int j = 0; j < 8; ++j) dD1B[j] = tb.d1_delta[(size_t)(h ? pi_row(j, 1) : pi_row(j, 0)) * ld2 + ic];
-		f16v dH0[MT];
+		h8 dH0B[HKS];
 #pragma unroll
 		for (int mt = 0; mt < MT; ++mt) {
-			f16v acc = mfma(loadA(d1T, W, 32 * mt + r, 0, h), dD1B, zero16());
-#pragma unroll
-			for (int q = 0; q < 16; ++q) acc[q] = H0[mt][q] > 0.f ? rh(acc[q]) : 0.f;
-			dH0[mt] = acc;
+			const f16v acc = mfma(loadA(d1T, W, 32 * mt + r, 0, h), dD1B, zero16());
+			dH0B[2 * mt] = mask_frag(acc, 0, H0B[2 * mt]);
+			if (2 * mt + 1 < HKS) dH0B[2 * mt + 1] = mask_frag(acc, 1, H0B[2 * mt + 1]);
 		}
 		f16v dDin[DMT];
 #pragma unroll
 		for (int mt = 0; mt < DMT; ++mt) {
 			f16v acc = zero16();
 #pragma unroll
-			for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(fw.d0T, DIN, 32 * mt + r, 16 * ks, h), accB(dH0[ks >> 1], ks & 1), acc);
+			for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(fw.d0T, DIN, 32 * mt + r, 16 * ks, h), dH0B[ks], acc);
 			dDin[mt] = rh16(acc);
 		}
 		// dL/d(position) for the global-movement gradient (nerf_network.h:602-631): the grid's input gradient
@@ -1098,22 +1171,21 @@ __global__ void __launch_bounds__(256) k_mlp_train_density(const uint32_t* __res
 				uB[ks][j] = (half_t)val;
 			}
 		// h1' = relu'(H0) . (W0d u)
-		f16v H1p[MT];
+		h8 H1pB[HKS];
 #pragma unroll
 		for (int mt = 0; mt < MT; ++mt) {
 			f16v acc = zero16();
 #pragma unroll
 			for (int ks = 0; ks < DKS; ++ks) acc = mfma(loadA(fw.d0, W, 32 * mt + r, 16 * ks, h), uB[ks], acc);
-#pragma unroll
-			for (int q = 0; q < 16; ++q) acc[q] = H0[mt][q] > 0.f ? rh(acc[q]) : 0.f;
-			H1p[mt] = acc;
+			H1pB[2 * mt] = mask_frag(acc, 0, H0B[2 * mt]);
+			if (2 * mt + 1 < HKS) H1pB[2 * mt + 1] = mask_frag(acc, 1, H0B[2 * mt + 1]);
 		}
 		if (valid) {
 #pragma unroll
-			for (int mt = 0; mt < MT; ++mt) {
-				store_acc(tb.d0_delta, ld2, i, dH0[mt], mt, W, h);
-				store_acc(tb.d1_x, ld2, i, H0[mt], mt, W, h);
-				store_acc(tb.d1_x, ld2, ld + i, H1p[mt], mt, W, h);
+			for (int ks = 0; ks < HKS; ++ks) {
+				store_frag(tb.d0_delta, ld2, i, dH0B[ks], ks, W, h);
+				store_frag(tb.d1_x, ld2, i, H0B[ks], ks, W, h);
+				store_frag(tb.d1_x, ld2, ld + i, H1pB[ks], ks, W, h);
 			}
 #pragma unroll
 			for (int ks = 0; ks < HKS; ++ks) store_frag(tb.d0_delta, ld2, ld + i, GhB[ks], ks, W, h);

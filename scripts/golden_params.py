@@ -21,14 +21,18 @@ for name, steps, extra in (("early", 12, None), ("late", 300, None)):
     res[name + "_grid"] = g
     res[name + "_counts"] = np.concatenate(tb.ray_counts(1 << 16)[:2])
     del tb
-np.savez(out, **res)
+import hashlib
+# digests of the full arrays + every 257th element (small enough to travel back from the GPU box)
+small = {k: v[::257].copy() for k, v in res.items()}
+small.update({k + "_sha": np.frombuffer(hashlib.sha256(v.tobytes()).digest(), np.uint8) for k, v in res.items()})
+np.savez(out, **small)
 if "--compare" in sys.argv:
     ref = np.load(sys.argv[sys.argv.index("--compare") + 1])
-    bad = [k for k in res if not np.array_equal(res[k].view(np.uint8), ref[k].view(np.uint8))]
+    bad = [k for k in res if not np.array_equal(small[k + "_sha"], ref[k + "_sha"])]
     for k in res:
         if k in bad:
-            a, b = res[k].astype(np.float64), ref[k].astype(np.float64)
-            print(f"{k}: DIFFERENT max|d| {np.abs(a - b).max():.3g} frac {np.mean(a != b):.3g}")
+            a, b = small[k].astype(np.float64), ref[k].astype(np.float64)
+            print(f"{k}: DIFFERENT (sampled) max|d| {np.abs(a - b).max():.3g} frac {np.mean(a != b):.3g}")
         else:
             print(f"{k}: identical")
     sys.exit(1 if bad else 0)
