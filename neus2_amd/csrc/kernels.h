@@ -115,6 +115,8 @@ struct LossWork {
 	float4* racc;           // [rays] rgb_ray, weight_sum
 	float* rT;              // [rays] final transmittance
 	float* rek;             // [rays] eikonal-term sum (progressive inference: the state between rounds)
+	uint32_t* long_rays;    // [rays] rays the transmittance scan runs one wave per ray (nullable: one thread per ray)
+	uint32_t* n_long;       // their count (zeroed by k_loss_alpha)
 	float4* rgr;            // [rays] dL/drgb_ray (Huber'), gws * (1 - weight_sum)
 };
 

@@ -545,7 +545,8 @@ __global__ void k_march_stats(uint32_t n_rays, const float* __restrict__ rays, c
 // n = min(*n_ptr, cap) samples; with idx, work item j is sample idx[j] (a progressive-inference round)
 __global__ void __launch_bounds__(256) k_loss_alpha(uint32_t cap, const uint32_t* __restrict__ n_ptr, const uint32_t* __restrict__ idx,
                                                     const float* __restrict__ coords, const half_t* __restrict__ net_out, float cos_anneal,
-                                                    float4* __restrict__ sa, float* __restrict__ ekt) {
+                                                    float4* __restrict__ sa, float* __restrict__ ekt, uint32_t* __restrict__ n_long) {
+	if (n_long && blockIdx.x == 0 && threadIdx.x == 0) *n_long = 0u;  // the transmittance scan's long-ray list (next kernel)
 	const uint32_t n = min(*n_ptr, cap);
 	for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
 		const uint32_t s = idx ? idx[j] : j;
@@ -561,6 +562,7 @@ __global__ void __launch_bounds__(256) k_loss_alpha(uint32_t cap, const uint32_t
 // Transmittance recurrence state of a ray (reference order: w = a T; rgb += w c; ws += w; ek += e; T *= 1 - a).
 struct ScanState { float T, r0, r1, r2, ek; };
 constexpr uint32_t SCAN_CK = 8;  // checkpoint stride of the stored scan state (in global sample index)
+constexpr uint32_t LONG_RAY = 32; // rays with more samples go to k_loss_scan_list
 
 // Replays the recurrence from the last stored checkpoint at or before sample s (or the ray start)
 // through sample s; returns T before s in T_before, and the state after s.
@@ -591,15 +593,18 @@ struct RayScan { float T, r0, r1, r2, ws, ek; uint32_t cn; };
 // state is stored only every SCAN_CK samples (scan_replay rebuilds the rest exactly), which keeps the scattered
 // per-lane stores off the critical path. 16 samples per group: early in training a few hundred rays carry hundreds
 // of samples each and the kernel time is their load-latency chain.
+// Rays with more than LONG_RAY samples are deferred to the long list (when given) for k_loss_scan_list.
 template <bool STORE = true>
 __global__ void __launch_bounds__(256) k_loss_scan_ray(uint32_t cap_rays, const uint32_t* __restrict__ numsteps, const float4* __restrict__ sa,
                                                        const float* __restrict__ ekt, float4* __restrict__ ck4, float* __restrict__ cke,
-                                                       uint32_t* __restrict__ ccount, float4* __restrict__ racc, float* __restrict__ rT) {
+                                                       uint32_t* __restrict__ ccount, float4* __restrict__ racc, float* __restrict__ rT,
+                                                       uint32_t* __restrict__ long_rays, uint32_t* __restrict__ n_long) {
 	const uint32_t stride = gridDim.x * blockDim.x;
 	for (uint32_t k = threadIdx.x * gridDim.x + blockIdx.x; k < ((cap_rays + stride - 1) / stride) * stride; k += stride) {
 		const uint32_t i = k;
 		if (i >= cap_rays) continue;
 		const uint32_t ns = numsteps[2 * i], base = numsteps[2 * i + 1];
+		if (long_rays && ns > LONG_RAY) { long_rays[atomicAdd(n_long, 1u)] = i; continue; }
 		uint32_t cn = 0;
 		float T = 1.f, r0 = 0.f, r1 = 0.f, r2 = 0.f, ws = 0.f, ek = 0.f;
 		if (ns > 0) {
@@ -634,6 +639,90 @@ __global__ void __launch_bounds__(256) k_loss_scan_ray(uint32_t cap_rays, const 
 		ccount[i] = cn;
 		racc[i] = make_float4(r0, r1, r2, ws);
 		rT[i] = T;
+	}
+}
+
+// The long rays (early in training a few thousand rays carry hundreds of samples each), 64 to a wave, one lane per
+// ray as k_loss_scan_ray but with the loads made coalesced: per 16-sample group, 16 lanes fetch one ray's 16
+// samples (256 B contiguous), 4 rays per load instruction, staged through LDS (row stride 17 float4: conflict-free
+// reads), the next groups' fetches in flight while the current one runs through the recurrence. One lane per ray
+// loading its own samples put 64 different lines behind every load instruction. Same float operation sequence, so
+// the results are k_loss_scan_ray's bits.
+__global__ void __launch_bounds__(64) k_loss_scan_list(const uint32_t* __restrict__ numsteps, const float4* __restrict__ sa,
+                                                       const float* __restrict__ ekt, float4* __restrict__ ck4, float* __restrict__ cke,
+                                                       uint32_t* __restrict__ ccount, float4* __restrict__ racc, float* __restrict__ rT,
+                                                       const uint32_t* __restrict__ long_rays, const uint32_t* __restrict__ n_long) {
+	constexpr uint32_t U = 16, PAD = U + 1;  // two groups in flight (slots A and B)
+	typedef float f4v __attribute__((ext_vector_type(4)));  // (HIP's float4 struct arrays are not kept in registers here)
+	__shared__ f4v s_q[64 * PAD];
+	__shared__ float s_e[64 * PAD];
+	const uint32_t lane = threadIdx.x, sub = lane >> 4, el = lane & 15;
+	const uint32_t nl = *n_long;
+	const char* sab = (const char*)sa;
+	const char* ekb = (const char*)ekt;
+	for (uint32_t w0 = blockIdx.x * 64; w0 < nl; w0 += gridDim.x * 64) {
+		const uint32_t k = w0 + lane;
+		const uint32_t i = k < nl ? long_rays[k] : 0u;
+		const uint32_t ns = k < nl ? numsteps[2 * i] : 0u, base = k < nl ? numsteps[2 * i + 1] : 0u;
+		// loader view: load instruction j fetches element el of ray 4 j + sub; past the ray's end it re-reads the ray's
+		// last sample (unconditional loads, 32-bit offsets from the uniform base; the values are never used)
+		uint32_t lb[U], ll[U];
+#pragma unroll
+		for (uint32_t j = 0; j < U; ++j) {
+			lb[j] = __shfl(base, 4 * j + sub);
+			const uint32_t n = __shfl(ns, 4 * j + sub);
+			ll[j] = lb[j] + (n ? n - 1u : 0u);
+		}
+		auto fetch = [&](f4v (&q)[U], float (&e)[U], uint32_t c) {
+#pragma unroll
+			for (uint32_t j = 0; j < U; ++j) {
+				const uint32_t g = min(lb[j] + c + el, ll[j]);
+				q[j] = *(const f4v*)(sab + (g << 4));
+				e[j] = *(const float*)(ekb + (g << 2));
+			}
+		};
+		uint32_t cn = 0;
+		float T = 1.f, r0 = 0.f, r1 = 0.f, r2 = 0.f, ws = 0.f, ek = 0.f;
+		bool live = ns > 0;  // the recurrence still runs (the reference's loop: j < numsteps and T >= 1e-4)
+		// one group: stage slot (q, e) = group c through LDS, refill the slot with group c + 2 U, run the recurrence
+		auto group = [&](f4v (&qs)[U], float (&es)[U], uint32_t c) {
+			__builtin_amdgcn_wave_barrier();
+#pragma unroll
+			for (uint32_t j = 0; j < U; ++j) { s_q[(4 * j + sub) * PAD + el] = qs[j]; s_e[(4 * j + sub) * PAD + el] = es[j]; }
+			__builtin_amdgcn_wave_barrier();
+			fetch(qs, es, c + 2 * U);
+			f4v q[U]; float e[U];
+#pragma unroll
+			for (uint32_t u = 0; u < U; ++u) { q[u] = s_q[lane * PAD + u]; e[u] = s_e[lane * PAD + u]; }
+			// branch-free: the state advances only while live (same operations, in the same order, on those samples)
+#pragma unroll
+			for (uint32_t u = 0; u < U; ++u) {
+				live = live && (c + u < ns) && !(T < 1e-4f);
+				const uint32_t s = base + c + u;
+				if (live && (s & (SCAN_CK - 1)) == 0) { ck4[s / SCAN_CK] = make_float4(T, r0, r1, r2); cke[s / SCAN_CK] = ek; }
+				const float w = q[u][0] * T;
+				const float n0 = r0 + w * q[u][1], n1 = r1 + w * q[u][2], n2 = r2 + w * q[u][3];
+				const float nws = ws + w, nek = ek + e[u], nT = T * (1.f - q[u][0]);
+				r0 = live ? n0 : r0; r1 = live ? n1 : r1; r2 = live ? n2 : r2;
+				ws = live ? nws : ws; ek = live ? nek : ek; T = live ? nT : T;
+				cn += live ? 1u : 0u;
+			}
+			__builtin_amdgcn_wave_barrier();
+		};
+		f4v qa[U], qb[U]; float ea[U], eb[U];
+		fetch(qa, ea, 0);
+		fetch(qb, eb, U);
+		for (uint32_t c = 0;; c += 2 * U) {
+			if (__ballot(live && c < ns) == 0) break;
+			group(qa, ea, c);
+			if (__ballot(live && c + U < ns) == 0) break;
+			group(qb, eb, c + U);
+		}
+		if (k < nl) {
+			ccount[i] = cn;
+			racc[i] = make_float4(r0, r1, r2, ws);
+			rT[i] = T;
+		}
 	}
 }
 
@@ -979,11 +1068,11 @@ void debug_launch_march_stats(hipStream_t s, uint32_t n_rays, const float* rays,
 static inline uint32_t sample_blocks(uint32_t cap) { return std::max<uint32_t>(1, std::min<uint32_t>((cap + 255) / 256, 16384)); }
 void launch_loss_alpha(hipStream_t s, uint32_t cap_samples, const StepState* st, const float* coords, const half_t* net_out, float cos_anneal,
                        const LossWork& w) {
-	k_loss_alpha<<<sample_blocks(cap_samples), 256, 0, s>>>(cap_samples, &st->n_kept, nullptr, coords, net_out, cos_anneal, w.sa, w.ekt);
+	k_loss_alpha<<<sample_blocks(cap_samples), 256, 0, s>>>(cap_samples, &st->n_kept, nullptr, coords, net_out, cos_anneal, w.sa, w.ekt, w.n_long);
 }
 void launch_loss_alpha_list(hipStream_t s, uint32_t cap_samples, const uint32_t* n_ptr, const uint32_t* idx, const float* coords,
                             const half_t* net_out, float cos_anneal, const LossWork& w) {
-	k_loss_alpha<<<sample_blocks(cap_samples), 256, 0, s>>>(cap_samples, n_ptr, idx, coords, net_out, cos_anneal, w.sa, w.ekt);
+	k_loss_alpha<<<sample_blocks(cap_samples), 256, 0, s>>>(cap_samples, n_ptr, idx, coords, net_out, cos_anneal, w.sa, w.ekt, nullptr);
 }
 void launch_chunk_count(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, uint32_t e1, uint32_t* m, uint32_t* counters,
                         uint32_t n_counters) {
@@ -998,14 +1087,23 @@ void launch_loss_scan_chunk(hipStream_t s, uint32_t cap_rays, const uint32_t* nu
 	k_loss_scan_chunk<<<ray_blocks(cap_rays), 256, 0, s>>>(cap_rays, numsteps, w.sa, w.ekt, w.ck4, w.cke, ccount, w.racc, w.rT, w.rek, e0, e1, e2,
 	                                                       list, next_counter);
 }
+// w.n_long is zeroed by the k_loss_alpha launch before it
 void launch_loss_scan_ray(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, const LossWork& w, uint32_t* ccount) {
 	const uint32_t blocks = ray_blocks(cap_rays);
-	k_loss_scan_ray<true><<<blocks, 256, 0, s>>>(cap_rays, numsteps, w.sa, w.ekt, w.ck4, w.cke, ccount, w.racc, w.rT);
+	k_loss_scan_ray<true><<<blocks, 256, 0, s>>>(cap_rays, numsteps, w.sa, w.ekt, w.ck4, w.cke, ccount, w.racc, w.rT, w.long_rays, w.n_long);
+	// the long rays, 64 to a one-wave block
+	if (w.long_rays) k_loss_scan_list<<<std::max<uint32_t>(1, std::min<uint32_t>((cap_rays + 63) / 64, 4096)), 64, 0, s>>>(
+		numsteps, w.sa, w.ekt, w.ck4, w.cke, ccount, w.racc, w.rT, w.long_rays, w.n_long);
 }
-// timing experiments (neus_debug_time_kernel): variant 1 = the recurrence without its per-sample stores
+// timing experiments (neus_debug_time_kernel): variant 1 = the recurrence without its per-sample stores, one
+// thread per ray for every ray
 void debug_launch_loss_scan(hipStream_t s, int variant, uint32_t cap_rays, const uint32_t* numsteps, const LossWork& w, uint32_t* ccount) {
-	if (variant == 1) k_loss_scan_ray<false><<<ray_blocks(cap_rays), 256, 0, s>>>(cap_rays, numsteps, w.sa, w.ekt, w.ck4, w.cke, ccount, w.racc, w.rT);
-	else launch_loss_scan_ray(s, cap_rays, numsteps, w, ccount);
+	if (variant == 1) k_loss_scan_ray<false><<<ray_blocks(cap_rays), 256, 0, s>>>(cap_rays, numsteps, w.sa, w.ekt, w.ck4, w.cke, ccount, w.racc, w.rT,
+	                                                                           nullptr, nullptr);
+	else {
+		if (w.n_long) (void)hipMemsetAsync(w.n_long, 0, 4, s);
+		launch_loss_scan_ray(s, cap_rays, numsteps, w, ccount);
+	}
 }
 void launch_loss_ray(hipStream_t s, uint32_t cap_rays, StepState* st, DPInfo dp, const DevDataset& ds, const LossParams& lp, uint32_t* numsteps,
                      const uint32_t* ccount, const uint32_t* cbase, const LossWork& w, float* loss, float* ek, float* mask) {

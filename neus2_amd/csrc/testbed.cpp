@@ -223,6 +223,7 @@ struct NeusTestbed {
 	float last_keep_ratio = 1.f;
 	static constexpr float PROGRESSIVE_RATIO = 0.7f;
 	Dev<uint32_t> chunk_list, chunk_cnt;
+	Dev<uint32_t> long_rays;  // the loss scan's wave-per-ray list (+ its counter in chunk_cnt[16])
 	TrainBufs tbuf{};
 	// RNG + counters (testbed.cu:2087-2101)
 	pcg32 rng, density_grid_rng;
@@ -489,7 +490,7 @@ struct NeusTestbed {
 		l_sa.alloc(max_samples); l_ekt.alloc(max_samples); sample_ray.alloc(max_samples);
 		l_ck4.alloc(max_samples / 8 + 1); l_cke.alloc(max_samples / 8 + 1);
 		l_racc.alloc(MAX_RAYS); l_rgr.alloc(MAX_RAYS); l_rT.alloc(MAX_RAYS); l_rek.alloc(MAX_RAYS);
-		chunk_list.alloc(max_samples); chunk_cnt.alloc(16);
+		chunk_list.alloc(max_samples); chunk_cnt.alloc(17); long_rays.alloc(MAX_RAYS);
 		loss.alloc(MAX_RAYS); ek.alloc(MAX_RAYS); mask.alloc(MAX_RAYS); loss_sum.alloc(4);
 		coords.alloc((size_t)max_samples * COORD_W); net_out.alloc((size_t)max_samples * OUT_W);
 		coords_c.alloc((size_t)batch * COORD_W); dL_dout.alloc((size_t)batch * OUT_W);
@@ -1081,6 +1082,7 @@ struct NeusTestbed {
 		LossWork w{};
 		w.sa = l_sa.p; w.ck4 = l_ck4.p; w.cke = l_cke.p; w.ekt = l_ekt.p; w.sample_ray = sample_ray.p; w.rbase = rbase;
 		w.racc = l_racc.p; w.rT = l_rT.p; w.rgr = l_rgr.p; w.rek = l_rek.p;
+		w.long_rays = long_rays.p; w.n_long = chunk_cnt.p + 16;
 		return w;
 	}
 
@@ -1749,6 +1751,8 @@ int neus_loss_compact(NeusTestbed* tb, void* stream, uint32_t n_rays, uint32_t r
 		lp.max_compacted = max_compacted; lp.rng_state = rng_state; lp.rng_inc = rng_inc;
 		LossWork w{};
 		w.sa = sa.p; w.ck4 = ck4.p; w.cke = cke.p; w.ekt = ekt.p; w.sample_ray = sr.p; w.rbase = rb.p; w.racc = racc.p; w.rT = rT.p; w.rgr = rgr.p;
+		Dev<uint32_t> lr, nl; lr.alloc(n_rays); nl.alloc(1);
+		w.long_rays = lr.p; w.n_long = nl.p;
 		const DPInfo dp{rank, world};
 		launch_ray_index(s, n_rays, numsteps, sst.p, sr.p, rb.p);
 		launch_loss_alpha(s, n_samples, sst.p, coords, (const half_t*)net_out, lp.cos_anneal, w);
