@@ -1224,8 +1224,15 @@ __global__ void __launch_bounds__(256) k_mlp_train_density(const uint32_t* __res
 // MFMA with natural k order (k = sample), fp32 accumulation, one atomic flush per block.
 // ------------------------------------------------------------------------------------------
 
+// A chunk (64 samples) of a wave's D and X rows is fetched cooperatively, row-contiguous (lane l: row l / 8 + 8 q,
+// 16 B segment l % 8: 8 lines per load instruction) and staged in LDS; the MFMA operands (lane (r, h): row r, the
+// chunk's samples 32 h + 8 u .. + 7) are read back from LDS. Fetching them straight from global memory put 64 lines
+// behind every load instruction and kept the texture-address unit ~75 % busy. The next chunk's fetch is in flight
+// while the current one runs; four accumulators (k-step u into acc[u]) keep independent MFMAs in flight.
 __global__ void __launch_bounds__(256) k_wgrad(WGradJobs jobs) {
-	__shared__ float red[4][32 * 32];
+	constexpr int LDR = 64 + 8;  // LDS row stride (halves)
+	__shared__ half_t s_op[4][2][32 * LDR];
+	float (*red)[32 * 32] = (float (*)[32 * 32])s_op;  // reused after the loop (4 x 4 KB <= 4 x 9 KB)
 	if (jobs.n_valid && *jobs.n_valid == 0) return;
 	uint32_t b = blockIdx.x, ji = 0;
 	while (ji + 1 < jobs.n_jobs && b >= jobs.block_start[ji + 1]) ++ji;
@@ -1236,39 +1243,52 @@ __global__ void __launch_bounds__(256) k_wgrad(WGradJobs jobs) {
 	const uint32_t mt = tile / J.tiles_k, kt = tile % J.tiles_k;
 	const uint32_t n0 = sp * jobs.split, n1 = min(J.ncols, n0 + jobs.split);
 	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
-	const uint32_t row_m = 32 * mt + r, row_k = 32 * kt + r;
-	const bool okm = row_m < J.M, okk = row_k < J.K;
-	f16v acc = zero16();
-	// Each wave takes 64-sample chunks (4 k-steps); lane half h owns the chunk's samples 32h .. 32h + 31, k-step u
-	// their 8u .. 8u + 7: a lane reads 64 contiguous bytes of its row per chunk, the two halves a whole 128-B line.
-	// Two chunks per trip: 16 loads in flight ahead of 8 MFMAs. The sample -> k assignment is the same for D and X,
-	// so the sum is the batch's; its order is fixed (deterministic).
-	const half_t* Dr = J.D + (size_t)row_m * J.ldc + 32 * h;
-	const half_t* Xr = J.X + (size_t)row_k * J.ldc + 32 * h;
-	const h8 z8 = (h8){0, 0, 0, 0, 0, 0, 0, 0};
-	uint32_t nb = n0 + 64 * wv;
-	for (; nb + 256 + 64 <= n1; nb += 512) {
-		h8 a[8], bb[8];
+	// loader view: rows lr + 8 q (q = 0..3), 16 B segment ls of the chunk's 128 B
+	const int lr = lane >> 3, ls = lane & 7;
+	const char* Db = (const char*)J.D;
+	const char* Xb = (const char*)J.X;
+	uint32_t offD[4], offX[4];
+	bool okD[4], okX[4];
 #pragma unroll
-		for (int c = 0; c < 2; ++c)
-#pragma unroll
-			for (int u = 0; u < 4; ++u) {
-				a[4 * c + u] = okm ? *(const h8*)(Dr + nb + 256 * c + 8 * u) : z8;
-				bb[4 * c + u] = okk ? *(const h8*)(Xr + nb + 256 * c + 8 * u) : z8;
-			}
-#pragma unroll
-		for (int u = 0; u < 8; ++u) acc = mfma(a[u], bb[u], acc);
+	for (int q = 0; q < 4; ++q) {
+		const uint32_t rm = 32 * mt + lr + 8 * q, rk = 32 * kt + lr + 8 * q;
+		okD[q] = rm < J.M; okX[q] = rk < J.K;
+		offD[q] = (rm * J.ldc + 8 * ls) * 2;  // byte offsets (operand buffers < 4 GB)
+		offX[q] = (rk * J.ldc + 8 * ls) * 2;
 	}
+	const h8 z8 = (h8){0, 0, 0, 0, 0, 0, 0, 0};
+	auto fetch = [&](uint32_t nb, h8 (&d)[4], h8 (&x)[4]) {
+#pragma unroll
+		for (int q = 0; q < 4; ++q) {
+			d[q] = okD[q] ? *(const h8*)(Db + offD[q] + 2 * nb) : z8;
+			x[q] = okX[q] ? *(const h8*)(Xb + offX[q] + 2 * nb) : z8;
+		}
+	};
+	half_t* sD = s_op[wv][0];
+	half_t* sX = s_op[wv][1];
+	f16v acc[4] = {zero16(), zero16(), zero16(), zero16()};
+	uint32_t nb = n0 + 64 * wv;
+	h8 d[4], x[4];
+	if (nb + 64 <= n1) fetch(nb, d, x);
 	for (; nb + 64 <= n1; nb += 256) {
+		__builtin_amdgcn_wave_barrier();
+#pragma unroll
+		for (int q = 0; q < 4; ++q) {
+			*(h8*)(sD + (lr + 8 * q) * LDR + 8 * ls) = d[q];
+			*(h8*)(sX + (lr + 8 * q) * LDR + 8 * ls) = x[q];
+		}
+		__builtin_amdgcn_wave_barrier();
+		if (nb + 256 + 64 <= n1) fetch(nb + 256, d, x);
 #pragma unroll
 		for (int u = 0; u < 4; ++u) {
-			const h8 a = okm ? *(const h8*)(Dr + nb + 8 * u) : z8;
-			const h8 bb = okk ? *(const h8*)(Xr + nb + 8 * u) : z8;
-			acc = mfma(a, bb, acc);
+			const h8 a = *(const h8*)(sD + r * LDR + 32 * h + 8 * u);
+			const h8 bb = *(const h8*)(sX + r * LDR + 32 * h + 8 * u);
+			acc[u] = mfma(a, bb, acc[u]);
 		}
 	}
+	__syncthreads();  // every wave is done with its staging rows before they hold the partials
 #pragma unroll
-	for (int reg = 0; reg < 16; ++reg) red[wv][acc_row(reg, h) * 32 + r] = acc[reg];
+	for (int reg = 0; reg < 16; ++reg) red[wv][acc_row(reg, h) * 32 + r] = (acc[0][reg] + acc[1][reg]) + (acc[2][reg] + acc[3][reg]);
 	__syncthreads();
 	float* out = jobs.partial + (size_t)blockIdx.x * 1024;
 	for (uint32_t e = threadIdx.x; e < 1024; e += 256) out[e] = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
