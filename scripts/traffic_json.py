@@ -17,7 +17,8 @@ def parse(path):
         m = re.match(r"\s+(\S.*?) dispatches=\d+ grid=\d+", line)
         if m:
             name = m.group(1)
-            cur = next((v for k, v in NAMES.items() if k in name and not (k == "k_march" and "write" in name)), None)
+            # k_march is the templated march itself ("k_march<"), not k_march_numsteps / k_march_write
+            cur = next((v for k, v in NAMES.items() if (k + "<" in name if k == "k_march" else k in name)), None)
             continue
         m = re.match(r"\s+(\w+)\s+([-+0-9.eE]+)$", line)
         if m and cur:
