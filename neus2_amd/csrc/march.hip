@@ -45,6 +45,7 @@ __global__ void __launch_bounds__(256) k_ray_gen(uint32_t cap_rays, const StepSt
 	if (blockIdx.x == 0 && threadIdx.x == 0) {  // the march passes' ray queues and counters (next kernels on the stream)
 		march_queue[0] = 0; march_queue[1] = 0;
 		st_w->march_total = 0; st_w->kept_extent = 0;
+		st_w->n_kept = 0; st_w->n_rays_with_samples = 0;  // this step's march maxima / counts (k_march, k_march_write)
 	}
 	const uint32_t R = st_r->rays_per_batch;
 	const uint32_t n_rays_global = R * dp.world, n_rays_total = st_r->n_rays_total;

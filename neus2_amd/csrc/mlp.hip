@@ -203,14 +203,29 @@ __device__ __forceinline__ void level_addr(const LevelSmem& sl, uint32_t dense_b
 		gp[d] = (uint32_t)(int)fl;
 		A.f[d] = p - fl;
 	}
-	// both index forms computed, merged by mask (a select here is turned into divergent branches)
-	const uint32_t dm = 0u - (uint32_t)dense;
+	// The pair's two levels are both dense or both hashed for most pairs (dense_bits is a prefix): a wave-uniform
+	// branch then computes only that index form; a mixed pair computes both, merged by mask (a per-lane select
+	// here is turned into divergent branches).
+	const uint32_t pair_dense = (dense_bits >> l0) & 1u, pair_dense1 = (dense_bits >> l1) & 1u;
 	uint32_t yz[4];
+	if (pair_dense & pair_dense1) {
 #pragma unroll
-	for (int k = 0; k < 4; ++k) {
-		const uint32_t yy = gp[1] + (k & 1), zz = gp[2] + (k >> 1);
-		yz[k] = ((yy * res + zz * (res * res)) & dm) | (((yy * 2654435761u) ^ (zz * 805459861u)) & ~dm);
+		for (int k = 0; k < 4; ++k) yz[k] = (gp[1] + (k & 1)) * res + (gp[2] + (k >> 1)) * (res * res);
+	} else if (!(pair_dense | pair_dense1)) {
+#pragma unroll
+		for (int k = 0; k < 4; ++k) yz[k] = ((gp[1] + (k & 1)) * 2654435761u) ^ ((gp[2] + (k >> 1)) * 805459861u);
+#pragma unroll
+		for (int c = 0; c < 8; ++c) A.e[c] = o0 + (((gp[0] + (c & 1)) ^ yz[c >> 1]) & (hs - 1u));
+		return;
+	} else {
+		const uint32_t dm = 0u - (uint32_t)dense;
+#pragma unroll
+		for (int k = 0; k < 4; ++k) {
+			const uint32_t yy = gp[1] + (k & 1), zz = gp[2] + (k >> 1);
+			yz[k] = ((yy * res + zz * (res * res)) & dm) | (((yy * 2654435761u) ^ (zz * 805459861u)) & ~dm);
+		}
 	}
+	const uint32_t dm = 0u - (uint32_t)dense;
 	// A position inside the unit cube has every cell coordinate <= res - 1, so a dense corner index is below
 	// 2 hs and one conditional subtract is the reference's `% hashmap_size`. Positions outside it (a sample moved
 	// by the DeltaNetwork, a grid point beyond the aabb; negative cells wrap to huge unsigned values) take the
@@ -1299,7 +1314,7 @@ __global__ void __launch_bounds__(256) k_wgrad(WGradJobs jobs) {
 // wave order. The block after the last tile sums the colour kernel's per-block variance partials in block order.
 constexpr uint32_t WR_CHUNKS = 1024 / 64;
 __global__ void __launch_bounds__(256) k_wgrad_reduce(WGradJobs jobs) {
-	if (jobs.n_valid && *jobs.n_valid == 0) return;
+	const bool none = jobs.n_valid && *jobs.n_valid == 0;  // no samples: the gradients are zero (k_wgrad wrote nothing)
 	__shared__ float s_part[4][64];
 	uint32_t b = blockIdx.x / WR_CHUNKS, ji = 0, tile_base = 0;
 	const uint32_t chunk = blockIdx.x % WR_CHUNKS;
@@ -1313,7 +1328,7 @@ __global__ void __launch_bounds__(256) k_wgrad_reduce(WGradJobs jobs) {
 		// fixed-order tree: thread t sums the partials t, t + 256, ..., then a pairwise tree over the threads
 		__shared__ float s_v[256];
 		float v = 0.f;
-		for (uint32_t k = threadIdx.x; k < jobs.var_blocks; k += 256) v += jobs.var_partial[k];
+		for (uint32_t k = threadIdx.x; k < jobs.var_blocks && !none; k += 256) v += jobs.var_partial[k];
 		s_v[threadIdx.x] = v;
 		__syncthreads();
 		for (uint32_t off = 128; off > 0; off >>= 1) {
@@ -1329,7 +1344,7 @@ __global__ void __launch_bounds__(256) k_wgrad_reduce(WGradJobs jobs) {
 	const uint32_t n_split = (J.ncols + jobs.split - 1) / jobs.split;
 	const uint32_t g = threadIdx.x >> 6, e = chunk * 64 + (threadIdx.x & 63);
 	float acc = 0.f;
-	for (uint32_t sp = g; sp < n_split; sp += 4) acc += jobs.partial[(size_t)(jobs.block_start[ji] + sp * tiles + tile) * 1024 + e];
+	for (uint32_t sp = g; sp < n_split && !none; sp += 4) acc += jobs.partial[(size_t)(jobs.block_start[ji] + sp * tiles + tile) * 1024 + e];
 	s_part[g][threadIdx.x & 63] = acc;
 	__syncthreads();
 	if (g == 0) {

@@ -973,9 +973,7 @@ struct NeusTestbed {
 		const bool get_loss = training_step % 16 == 0;
 		// ---- train_nerf_step (testbed_nerf.cu:3723-4001)
 		if (training_step == 0 || canonical_step == 0) HIP_CHECK(hipMemsetAsync(&st.p->n_rays_total, 0, 4, s));
-		HIP_CHECK(hipMemsetAsync(&st.p->n_kept, 0, 4, s));
-		HIP_CHECK(hipMemsetAsync(&st.p->n_rays_with_samples, 0, 4, s));
-		const DPInfo dp{rank, world};
+		const DPInfo dp{rank, world};  // (n_kept, n_rays_with_samples: zeroed by k_ray_gen)
 		mark(1);
 		launch_march_count(s, MAX_RAYS, max_samples, st.p, dp, ds, bitfield.p, bf_lin.p, rng.state, rng.inc, rays.p, startt.p, nreq.p, mwork);
 		launch_exclusive_scan(s, scan_tmp.p, scan_tmp_bytes, nreq.p, base.p, MAX_RAYS);
@@ -1016,7 +1014,9 @@ struct NeusTestbed {
 		launch_loss_ray(s, MAX_RAYS, st.p, dp, ds, lp, numsteps.p, ccount.p, cbase.p, w, loss.p, ek.p, mask.p);
 		launch_loss_grad(s, max_samples, st.p, dp, lp, coords.p, net_out.p, numsteps.p, w, coords_c.p, dL_dout.p);
 		launch_rollover(s, batch, st.p, coords_c.p, dL_dout.p);
-		HIP_CHECK(hipMemsetAsync(grads.p, 0, (size_t)lay.P * 4, s));
+		// the canonical backward writes every gradient entry (weight tiles and variance by k_wgrad_reduce, every grid
+		// entry by k_scatter_accum, zeros with no samples); the global-movement phase skips it: zero the buffer there
+		if (!(!dyn || train_canonical)) HIP_CHECK(hipMemsetAsync(grads.p, 0, (size_t)lay.P * 4, s));
 		mark(4);
 		if (use_delta) {
 			// the training forward runs on the deformed batch; dL/d(position) feeds the DeltaNetwork backward
@@ -1507,8 +1507,6 @@ static void time_kernel_impl(NeusTestbed* tb, int kernel, int variant, int iters
 		const uint32_t valid = t.valid_level_at((int)t.training_step);
 		const uint32_t* lin = t.bf_lin.p;
 		auto march = [&]() {
-			HIP_CHECK(hipMemsetAsync(&t.st.p->n_kept, 0, 4, s));
-			HIP_CHECK(hipMemsetAsync(&t.st.p->n_rays_with_samples, 0, 4, s));
 			launch_march_count(s, MAX_RAYS, t.max_samples, t.st.p, dp, t.ds, t.bitfield.p, lin, t.rng.state, t.rng.inc, t.rays.p, t.startt.p, t.nreq.p, t.mwork);
 			launch_exclusive_scan(s, t.scan_tmp.p, t.scan_tmp_bytes, t.nreq.p, t.base.p, MAX_RAYS);
 			launch_march_write(s, MAX_RAYS, t.st.p, t.ds, t.rays.p, t.mwork, t.nreq.p, t.base.p, t.numsteps.p, t.coords.p,
