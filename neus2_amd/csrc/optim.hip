@@ -141,14 +141,39 @@ __global__ void k_grid_to_bitfield(uint32_t n_bytes_total, uint32_t n_nonzero, c
 		bf[i] = bits;
 	}
 }
-__global__ void k_bitfield_max_pool(uint32_t n, const uint8_t* __restrict__ prev, uint8_t* __restrict__ next) {
-	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-		uint8_t bits = 0;
+
+// All mip levels' max pools in one launch (the reference runs bitfield_max_pool once per level, each reading the
+// previous level's final bytes; testbed_nerf.cu:3384-3392). A level-(m+1) bit in the inner region is set iff the
+// corresponding level-m byte is nonzero, so the fixpoint is an OR over the level tree. A wave takes 64 consecutive
+// bytes of a level (a 4x4x4-byte Morton block): the ballot of "byte nonzero" is exactly the 8 consecutive parent
+// bytes (one 64-bit atomic OR); the parent bytes this OR turned nonzero then set their own parent bit, and so on up
+// while a byte turns nonzero. Every byte that becomes nonzero is propagated by exactly the wave that made it so (or
+// by its own wave when its grid bits were set); OR is order-independent, so the bits are the level-by-level pool's.
+__global__ void k_bitfield_pool_all(uint32_t nbytes, uint8_t* __restrict__ bf) {
+	const uint32_t lane = threadIdx.x & 63, waves_per_level = nbytes / 64;
+	const uint32_t n_waves = waves_per_level * (NERF_CASCADES - 1);
+	for (uint32_t wg = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; wg < n_waves; wg += (gridDim.x * blockDim.x) >> 6) {
+		const uint32_t level0 = wg / waves_per_level, w = wg % waves_per_level;
+		const uint64_t M = __ballot(bf[(size_t)level0 * nbytes + 64 * w + lane] != 0);
+		if (M == 0 || lane != 0) continue;
+		// the 8 parent bytes: 8 morton(invert(w) + 8) .. + 7 at level0 + 1
+		uint32_t q0 = 8u * morton3D(morton3D_invert(w >> 0) + NERF_GRIDSIZE / 16, morton3D_invert(w >> 1) + NERF_GRIDSIZE / 16,
+		                             morton3D_invert(w >> 2) + NERF_GRIDSIZE / 16);
+		const uint64_t old = atomicOr((unsigned long long*)(bf + (size_t)(level0 + 1) * nbytes + q0), (unsigned long long)M);
+		uint32_t N = 0;  // parent bytes that turned nonzero
 #pragma unroll
-		for (uint8_t j = 0; j < 8; ++j) bits |= prev[i * 8 + j] > 0 ? ((uint8_t)1 << j) : 0;
-		const uint32_t x = morton3D_invert(i >> 0) + NERF_GRIDSIZE / 8, y = morton3D_invert(i >> 1) + NERF_GRIDSIZE / 8, z = morton3D_invert(i >> 2) + NERF_GRIDSIZE / 8;
-		// each destination byte is written by exactly one source thread of this level
-		next[morton3D(x, y, z)] |= bits;
+		for (int k = 0; k < 8; ++k) N |= (((old >> (8 * k)) & 0xffu) == 0 && ((M >> (8 * k)) & 0xffu) != 0) ? (1u << k) : 0u;
+		uint32_t level = level0 + 1, p = q0;  // bytes p .. p + 7 of `level`, N: which turned nonzero
+		while (N != 0 && level + 1 < NERF_CASCADES) {
+			const uint32_t i = p >> 3;
+			const uint32_t q = morton3D(morton3D_invert(i >> 0) + NERF_GRIDSIZE / 8, morton3D_invert(i >> 1) + NERF_GRIDSIZE / 8,
+			                            morton3D_invert(i >> 2) + NERF_GRIDSIZE / 8);
+			const size_t byte = (size_t)(level + 1) * nbytes + q;
+			const uint32_t sh = 8u * (uint32_t)(byte & 3);
+			const uint32_t o = atomicOr((uint32_t*)(bf + (byte & ~(size_t)3)), N << sh);
+			if (((o >> sh) & 0xffu) != 0) break;  // the parent byte was already nonzero: its propagation is someone else's
+			N = 1u << (q & 7); p = q & ~7u; ++level;
+		}
 	}
 }
 
@@ -185,8 +210,7 @@ void launch_grid_mean(hipStream_t s, const float* grid, float* partial, float* m
 void launch_bitfield(hipStream_t s, const float* grid, uint8_t* bitfield, const float* mean, uint32_t n_cascades) {
 	const uint32_t nbytes = GRID3 / 8;
 	k_grid_to_bitfield<<<nblk(nbytes * NERF_CASCADES), 256, 0, s>>>(nbytes * NERF_CASCADES, nbytes * n_cascades, grid, bitfield, mean);
-	for (uint32_t level = 1; level < NERF_CASCADES; ++level)
-		k_bitfield_max_pool<<<nblk(GRID3 / 64), 256, 0, s>>>(GRID3 / 64, bitfield + nbytes * (level - 1), bitfield + nbytes * level);
+	k_bitfield_pool_all<<<nblk((uint64_t)nbytes * (NERF_CASCADES - 1), 2048), 256, 0, s>>>(nbytes, bitfield);
 }
 
 } // namespace neus
