@@ -435,9 +435,9 @@ __global__ void __launch_bounds__(256) k_march_numsteps(uint32_t cap_rays, StepS
 // (b) block per WRITE_CHUNK consecutive output samples (balanced whatever the spread of samples over
 //     rays; kept rays form a prefix of the slot order since base is monotone). The block finds the
 //     ray slots overlapping its chunk by binary search over base, stages up to 256 of them (base, n,
-//     o, d) in LDS, and walks the chunk with consecutive threads on consecutive samples: ray by binary
-//     search over the staged bases, the ray's recorded t (contiguous per ray), NerfCoordinate with
-//     pos = o + t d exactly as the march computed it, warped dt, warped dir.
+//     o, d, record offsets) in LDS, maps each chunk sample to its run (one thread per run), then walks the
+//     chunk with consecutive threads on consecutive samples: t replayed from the run's first sample exactly
+//     as the march stepped it, NerfCoordinate with pos = o + t d, warped dt, warped dir.
 constexpr uint32_t WRITE_CHUNK = 4096;
 __device__ __forceinline__ uint32_t last_le(const uint32_t* __restrict__ a, uint32_t n, uint32_t q) {  // last k < n with a[k] <= q (a[0] <= q)
 	uint32_t lo = 0, hi = n;
@@ -449,8 +449,11 @@ __global__ void __launch_bounds__(256) k_march_write(uint32_t cap_rays, const St
                                                      const uint32_t* __restrict__ nreq, const uint32_t* __restrict__ base,
                                                      float* __restrict__ coords, uint32_t* __restrict__ sample_ray) {
 	__shared__ float s_ray[6][256];
-	__shared__ uint32_t s_b[256], s_n[256];
-	__shared__ uint32_t s_range[2];
+	__shared__ uint32_t s_b[256], s_n[256], s_roff[256];
+	__shared__ uint32_t s_range[3];
+	__shared__ uint32_t s_t0[WRITE_CHUNK];  // per chunk sample: t of its run's first sample (bits)
+	__shared__ uint16_t s_r[WRITE_CHUNK];   // its ray within the staged batch
+	__shared__ uint8_t s_u[WRITE_CHUNK];    // its step within the run
 	const uint32_t max_samples = st->max_inference;
 	const uint32_t tid = threadIdx.x;
 	const uint32_t q0 = blockIdx.x * WRITE_CHUNK;
@@ -477,16 +480,47 @@ __global__ void __launch_bounds__(256) k_march_write(uint32_t cap_rays, const St
 				for (int d = 0; d < 3; ++d) { s_ray[d][tid] = mr.o[d]; s_ray[3 + d][tid] = mr.dir[d]; }
 			}
 		}
+		// (1) one thread per sample RUN (record) of the batch's rays: for each of the run's samples in this chunk,
+		//     the run's first t, the sample's step within the run and its ray go to LDS maps (a binary search over
+		//     the ray's records per sample was a chain of dependent loads: waves waited ~75 % of the time)
+		s_roff[tid] = tid < nr ? (s_n[tid] ? mw.nrec[rb + tid] : 0u) : 0u;
 		__syncthreads();
-		// this batch's samples: up to the next batch's first base (or the chunk end)
+		if (tid < 64) {  // exclusive scan of the 256 record counts (one wave, 4 per lane)
+			uint32_t v[4], sum = 0;
+#pragma unroll
+			for (int k = 0; k < 4; ++k) { v[k] = s_roff[4 * tid + k]; sum += v[k]; }
+			uint32_t inc = sum;
+#pragma unroll
+			for (int off = 1; off < 64; off <<= 1) { const uint32_t o = (uint32_t)__shfl_up((int)inc, off); if ((int)tid >= off) inc += o; }
+			uint32_t ex = inc - sum;
+#pragma unroll
+			for (int k = 0; k < 4; ++k) { s_roff[4 * tid + k] = ex; ex += v[k]; }
+			if (tid == 63) s_range[2] = inc;  // records of the batch
+		}
+		__syncthreads();
+		const uint32_t n_rec = s_range[2];
+		for (uint32_t g = tid; g < n_rec; g += 256) {
+			const uint32_t r = last_le(s_roff, nr, g);
+			const uint32_t i = rb + r, k = g - s_roff[r];
+			const uint2 R = mw.rec[(size_t)i * NERF_STEPS + k];
+			const uint32_t qs = s_b[r] + (R.y >> 16), len = R.y & 0xffffu;
+			for (uint32_t u = 0; u < len; ++u) {
+				const uint32_t q = qs + u;
+				if (q >= q0 && q < q1) { s_t0[q - q0] = R.x; s_u[q - q0] = (uint8_t)u; s_r[q - q0] = (uint16_t)r; }
+			}
+		}
+		__syncthreads();
+		// (2) consecutive threads on the batch's consecutive samples: t replayed from the run's first sample
+		// (<= MARCH_RUN_MAX - 1 steps, exactly as the march stepped it), coalesced NerfCoordinate stores
 		const uint32_t qa = max(q0, s_b[0]);
 		const uint32_t qb = rb + nr > r_hi ? q1 : min(q1, base[rb + nr]);
 		for (uint32_t q = qa + tid; q < qb; q += 256) {
-			const uint32_t r = last_le(s_b, nr, q);
+			const uint32_t r = s_r[q - q0];
 			const uint32_t j = q - s_b[r];
-			if (j >= s_n[r]) continue;  // not a kept sample
+			if (j >= s_n[r]) continue;  // not a kept sample (no run wrote this slot)
 			const uint32_t i = rb + r;
-			const float t = ds.cone_angle == 0.0f ? run_sample_t<true>(mw, i, j, 0.0f) : run_sample_t<false>(mw, i, j, ds.cone_angle);
+			float t = __uint_as_float(s_t0[q - q0]);
+			for (uint32_t u = s_u[q - q0]; u > 0; --u) t += ds.cone_angle == 0.0f ? MIN_CONE_STEPSIZE : calc_dt(t, ds.cone_angle);
 			const float o[3] = {s_ray[0][r], s_ray[1][r], s_ray[2][r]}, dir[3] = {s_ray[3][r], s_ray[4][r], s_ray[5][r]};
 			float pos[3];
 #pragma unroll
