@@ -967,7 +967,7 @@ __device__ __forceinline__ void store_frag(half_t* buf, size_t ldc, uint32_t col
 //                         second-order front pass h1' = relu'(H0) . (W0 u)
 // They communicate through the weight-gradient operand buffers they write anyway (d1_delta, v).
 template <int L, int W>
-__global__ void __launch_bounds__(256) k_mlp_train_rgb(const uint32_t* __restrict__ n_valid_ptr, uint32_t n, uint32_t ld,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) k_mlp_train_rgb(const uint32_t* __restrict__ n_valid_ptr, uint32_t n, uint32_t ld,
                                                        const float* __restrict__ coords, const half_t* __restrict__ enc_h,
                                                        const float* __restrict__ dydx, const half_t* __restrict__ dL_dout,
                                                        MlpPtrs w, TrainBufs tb) {
@@ -1024,6 +1024,14 @@ __global__ void __launch_bounds__(256) k_mlp_train_rgb(const uint32_t* __restric
 		h8 rinB[3];
 		h8 H1B[HKS], H2B[HKS];
 		rgb_hidden_frag<W>(fw, D1B, x, wd, grad, r, h, rinB, H1B, H2B);
+		// weight-gradient operands stored as soon as they are final (shorter live ranges: this kernel runs at one
+		// wave per SIMD and spills its fragments to AGPRs when everything is stored at the end)
+		if (valid) {
+#pragma unroll
+			for (int ks = 0; ks < HKS; ++ks) { store_frag(tb.r1_x, ld, i, H1B[ks], ks, W, h); store_frag(tb.r2_x, ld, i, H2B[ks], ks, W, h); }
+#pragma unroll
+			for (int ks = 0; ks < 3; ++ks) store_frag(tb.r0_x, ld, i, rinB[ks], ks, 48, h);
+		}
 		// ---- colour backward
 		const h8 dlo = *(const h8*)(dL_dout + (size_t)ic * OUT_W + 8 * h);   // h=0: rows 0..7, h=1: rows 8..15
 		const h8 dlo_o = shfl_xor_h8(dlo, 32);
@@ -1040,6 +1048,11 @@ __global__ void __launch_bounds__(256) k_mlp_train_rgb(const uint32_t* __restric
 			dH2B[2 * mt] = mask_frag(acc, 0, H2B[2 * mt]);
 			if (2 * mt + 1 < HKS) dH2B[2 * mt + 1] = mask_frag(acc, 1, H2B[2 * mt + 1]);
 		}
+		if (valid) {
+#pragma unroll
+			for (int ks = 0; ks < HKS; ++ks) store_frag(tb.r1_delta, ld, i, dH2B[ks], ks, W, h);
+			store_frag(tb.r2_delta, ld, i, dOB, 0, 16, h);
+		}
 #pragma unroll
 		for (int mt = 0; mt < MT; ++mt) {
 			f16v acc = zero16();
@@ -1047,6 +1060,10 @@ __global__ void __launch_bounds__(256) k_mlp_train_rgb(const uint32_t* __restric
 			for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(bw.r1T, W, 32 * mt + r, 16 * ks, h), dH2B[ks], acc);
 			dH1B[2 * mt] = mask_frag(acc, 0, H1B[2 * mt]);
 			if (2 * mt + 1 < HKS) dH1B[2 * mt + 1] = mask_frag(acc, 1, H1B[2 * mt + 1]);
+		}
+		if (valid) {
+#pragma unroll
+			for (int ks = 0; ks < HKS; ++ks) store_frag(tb.r0_delta, ld, i, dH1B[ks], ks, W, h);
 		}
 		f16v dRin[2];
 #pragma unroll
@@ -1069,16 +1086,6 @@ __global__ void __launch_bounds__(256) k_mlp_train_rgb(const uint32_t* __restric
 		v[0] += (float)dlo_lo[4] / tb.indeed_batch; v[1] += (float)dlo_lo[5] / tb.indeed_batch; v[2] += (float)dlo_lo[6] / tb.indeed_batch;
 		v[0] += (float)dlo_hi[0]; v[1] += (float)dlo_hi[1]; v[2] += (float)dlo_hi[2];
 		if (valid) {
-#pragma unroll
-			for (int ks = 0; ks < HKS; ++ks) {
-				store_frag(tb.r0_delta, ld, i, dH1B[ks], ks, W, h);
-				store_frag(tb.r1_delta, ld, i, dH2B[ks], ks, W, h);
-				store_frag(tb.r1_x, ld, i, H1B[ks], ks, W, h);
-				store_frag(tb.r2_x, ld, i, H2B[ks], ks, W, h);
-			}
-#pragma unroll
-			for (int ks = 0; ks < 3; ++ks) store_frag(tb.r0_x, ld, i, rinB[ks], ks, 48, h);
-			store_frag(tb.r2_delta, ld, i, dOB, 0, 16, h);
 			store_acc(tb.d1_delta, ld2, i, dD1, 0, 16, h);
 			if (h == 0) tb.v[i] = make_float4(v[0], v[1], v[2], 0.f);
 			// dL/d(rgb input xyz rows 32..34) for the global-movement gradient (nerf_network.h:613-616)
@@ -1096,7 +1103,7 @@ __global__ void __launch_bounds__(256) k_mlp_train_rgb(const uint32_t* __restric
 }
 
 template <int L, int W>
-__global__ void __launch_bounds__(256) k_mlp_train_density(const uint32_t* __restrict__ n_valid_ptr, uint32_t n, uint32_t ld,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) k_mlp_train_density(const uint32_t* __restrict__ n_valid_ptr, uint32_t n, uint32_t ld,
                                                            const float* __restrict__ coords, const half_t* __restrict__ enc_h,
                                                            const float* __restrict__ dydx, MlpPtrs w, TrainBufs tb) {
 	constexpr int DIN = Dims<L>::DIN, DKS = Dims<L>::DKS, DMT = Dims<L>::DMT;
@@ -1126,6 +1133,28 @@ __global__ void __launch_bounds__(256) k_mlp_train_density(const uint32_t* __res
 		h8 H0B[HKS], D1B, GhB[HKS];
 		f16v Gi[DMT];
 		density_forward_frag<L, W>(fw, dinB, r, h, H0B, D1B, GhB, Gi);
+		// weight-gradient / scatter operands stored as soon as they are final (shorter live ranges)
+		if (valid) {
+#pragma unroll
+			for (int ks = 0; ks < HKS; ++ks) {
+				store_frag(tb.d1_x, ld2, i, H0B[ks], ks, W, h);
+				store_frag(tb.d0_delta, ld2, ld + i, GhB[ks], ks, W, h);
+			}
+#pragma unroll
+			for (int ks = 0; ks < DKS; ++ks) store_frag(tb.d0_x, ld2, i, dinB[ks], ks, DIN, h);
+			{
+				h8 e0 = (h8){0, 0, 0, 0, 0, 0, 0, 0};
+				if (h == 0) e0[0] = (half_t)1.0f;
+				store_frag(tb.d1_delta, ld2, ld + i, e0, 0, 16, h);
+			}
+#pragma unroll
+			for (int mt = 0; mt < DMT; ++mt)
+#pragma unroll
+				for (int reg = 0; reg < 16; ++reg) {
+					const int k = 32 * mt + acc_row(reg, h);
+					if (k >= 3 && k < 3 + 2 * L) tb.genc[((size_t)((k - 3) >> 1) * ld + i) * 2 + ((k - 3) & 1)] = (half_t)Gi[mt][reg];  // [L][ld] half2
+				}
+		}
 		// delta_D1 from the colour kernel (d1_delta column i), B fragment in pi order
 		h8 dD1B;
 #pragma unroll
@@ -1136,6 +1165,10 @@ __global__ void __launch_bounds__(256) k_mlp_train_density(const uint32_t* __res
 			const f16v acc = mfma(loadA(d1T, W, 32 * mt + r, 0, h), dD1B, zero16());
 			dH0B[2 * mt] = mask_frag(acc, 0, H0B[2 * mt]);
 			if (2 * mt + 1 < HKS) dH0B[2 * mt + 1] = mask_frag(acc, 1, H0B[2 * mt + 1]);
+		}
+		if (valid) {
+#pragma unroll
+			for (int ks = 0; ks < HKS; ++ks) store_frag(tb.d0_delta, ld2, i, dH0B[ks], ks, W, h);
 		}
 		f16v dDin[DMT];
 #pragma unroll
@@ -1197,38 +1230,20 @@ __global__ void __launch_bounds__(256) k_mlp_train_density(const uint32_t* __res
 		}
 		if (valid) {
 #pragma unroll
-			for (int ks = 0; ks < HKS; ++ks) {
-				store_frag(tb.d0_delta, ld2, i, dH0B[ks], ks, W, h);
-				store_frag(tb.d1_x, ld2, i, H0B[ks], ks, W, h);
-				store_frag(tb.d1_x, ld2, ld + i, H1pB[ks], ks, W, h);
-			}
+			for (int ks = 0; ks < HKS; ++ks) store_frag(tb.d1_x, ld2, ld + i, H1pB[ks], ks, W, h);
 #pragma unroll
-			for (int ks = 0; ks < HKS; ++ks) store_frag(tb.d0_delta, ld2, ld + i, GhB[ks], ks, W, h);
-#pragma unroll
-			for (int ks = 0; ks < DKS; ++ks) {
-				store_frag(tb.d0_x, ld2, i, dinB[ks], ks, DIN, h);
-				store_frag(tb.d0_x, ld2, ld + i, uB[ks], ks, DIN, h);
-			}
-			{
-				h8 e0 = (h8){0, 0, 0, 0, 0, 0, 0, 0};
-				if (h == 0) e0[0] = (half_t)1.0f;
-				store_frag(tb.d1_delta, ld2, ld + i, e0, 0, 16, h);
-			}
+			for (int ks = 0; ks < DKS; ++ks) store_frag(tb.d0_x, ld2, ld + i, uB[ks], ks, DIN, h);
 			if (tb.dpos && h == 0) {
 				const float4 rg = tb.dpos[i];
 				tb.dpos[i] = make_float4((pg[0] + rg.x) + pd[0], (pg[1] + rg.y) + pd[1], (pg[2] + rg.z) + pd[2], 0.f);
 			}
-			// ---- grid-scatter operands: dL/denc = dDin rows 3.., g = G_in rows 3..
+			// ---- grid-scatter operand dL/denc = dDin rows 3.. (g = G_in rows 3.. went out after the forward)
 #pragma unroll
 			for (int mt = 0; mt < DMT; ++mt)
 #pragma unroll
 				for (int reg = 0; reg < 16; ++reg) {
 					const int k = 32 * mt + acc_row(reg, h);
-					if (k >= 3 && k < 3 + 2 * L) {
-						const size_t e = ((size_t)((k - 3) >> 1) * ld + i) * 2 + ((k - 3) & 1);  // [L][ld] half2
-						tb.dLdenc[e] = (half_t)dDin[mt][reg];
-						tb.genc[e] = (half_t)Gi[mt][reg];
-					}
+					if (k >= 3 && k < 3 + 2 * L) tb.dLdenc[((size_t)((k - 3) >> 1) * ld + i) * 2 + ((k - 3) & 1)] = (half_t)dDin[mt][reg];
 				}
 		}
 	}
