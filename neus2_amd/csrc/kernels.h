@@ -266,6 +266,9 @@ void launch_grid_samples(hipStream_t s, uint32_t n, uint32_t i_begin, uint32_t i
 void launch_splat_max(hipStream_t s, uint32_t n, const uint32_t* indices, const float* density, float* grid_tmp);
 void launch_ema_grid(hipStream_t s, uint32_t n, float decay, float* grid, const float* tmp);
 void launch_grid_mean(hipStream_t s, const float* grid, float* partial, float* mean);
-void launch_bitfield(hipStream_t s, const float* grid, uint8_t* bitfield, const float* mean, uint32_t n_cascades);
+void launch_bitfield(hipStream_t s, const float* grid, uint8_t* bitfield, const float* mean, uint32_t n_cascades,
+                     uint32_t* lin = nullptr /* also the march's linear mip-0 words */);
+// EMA of the grid + its cascade-0 mean (n multiple of 1024)
+void launch_ema_mean(hipStream_t s, uint32_t n, float decay, float* grid, const float* tmp, float* partial, float* mean);
 
 } // namespace neus

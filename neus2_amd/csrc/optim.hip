@@ -130,6 +130,29 @@ __global__ void __launch_bounds__(256) k_grid_mean_final(const float* __restrict
 	if (threadIdx.x == 0) *mean = s[0];
 }
 
+// The EMA of the grid (k_ema_grid) with the mean partials of cascade 0 computed by the same blocks over the same
+// elements in the same order (k_grid_mean_partial's bits); k_grid_mean_final follows. (A last-block-done final sum
+// needs agent-scope fences, which write back the XCD L2s: 50 us here.)
+__global__ void __launch_bounds__(256) k_ema_mean(uint32_t n, float decay, float* __restrict__ grid, const float* __restrict__ tmp,
+                                                 float* __restrict__ partial) {
+	__shared__ float s[256];
+	const uint32_t b = blockIdx.x;  // n / 1024 blocks of 1024 cells
+	float acc = 0.f;
+#pragma unroll
+	for (int k = 0; k < 4; ++k) {
+		const uint32_t i = b * 1024 + k * 256 + threadIdx.x;
+		const float prev = grid[i];
+		const float v = (prev < 0.f) ? prev : fmaxf(prev * decay, tmp[i]);
+		grid[i] = v;
+		acc += fmaxf(v, 0.f) / (float)GRID3;
+	}
+	if (b >= GRID3 / 1024) return;  // the mean covers cascade 0 only
+	s[threadIdx.x] = acc;
+	__syncthreads();
+	for (int off = 128; off > 0; off >>= 1) { if (threadIdx.x < off) s[threadIdx.x] += s[threadIdx.x + off]; __syncthreads(); }
+	if (threadIdx.x == 0) partial[b] = s[0];
+}
+
 __global__ void k_grid_to_bitfield(uint32_t n_bytes_total, uint32_t n_nonzero, const float* __restrict__ grid, uint8_t* __restrict__ bf,
                                    const float* __restrict__ mean) {
 	const float thresh = fminf(NERF_MIN_OPTICAL_THICKNESS, *mean);
@@ -149,10 +172,23 @@ __global__ void k_grid_to_bitfield(uint32_t n_bytes_total, uint32_t n_nonzero, c
 // bytes (one 64-bit atomic OR); the parent bytes this OR turned nonzero then set their own parent bit, and so on up
 // while a byte turns nonzero. Every byte that becomes nonzero is propagated by exactly the wave that made it so (or
 // by its own wave when its grid bits were set); OR is order-independent, so the bits are the level-by-level pool's.
-__global__ void k_bitfield_pool_all(uint32_t nbytes, uint8_t* __restrict__ bf) {
+// The same launch converts mip 0 (which the pools only read) to the march's linear words (k_bitfield_linear) in
+// its last GRID3 / 32 / 64 waves.
+__global__ void k_bitfield_pool_all(uint32_t nbytes, uint8_t* __restrict__ bf, uint32_t* __restrict__ lin) {
 	const uint32_t lane = threadIdx.x & 63, waves_per_level = nbytes / 64;
-	const uint32_t n_waves = waves_per_level * (NERF_CASCADES - 1);
-	for (uint32_t wg = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; wg < n_waves; wg += (gridDim.x * blockDim.x) >> 6) {
+	const uint32_t n_waves = waves_per_level * (NERF_CASCADES - 1), n_lin_waves = lin ? GRID3 / 32 / 64 : 0u;
+	for (uint32_t wg = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; wg < n_waves + n_lin_waves; wg += (gridDim.x * blockDim.x) >> 6) {
+		if (wg >= n_waves) {
+			const uint32_t w = (wg - n_waves) * 64 + lane;
+			const uint32_t ix = w >> 9, iy = (w >> 2) & 127, iz0 = (w & 3) * 32;
+			uint32_t word = 0;
+			for (uint32_t b = 0; b < 32; ++b) {
+				const uint32_t idx = morton3D(ix, iy, iz0 + b);
+				word |= (uint32_t)((bf[idx / 8] >> (idx % 8)) & 1) << b;
+			}
+			lin[w] = word;
+			continue;
+		}
 		const uint32_t level0 = wg / waves_per_level, w = wg % waves_per_level;
 		const uint64_t M = __ballot(bf[(size_t)level0 * nbytes + 64 * w + lane] != 0);
 		if (M == 0 || lane != 0) continue;
@@ -207,10 +243,14 @@ void launch_grid_mean(hipStream_t s, const float* grid, float* partial, float* m
 	k_grid_mean_partial<<<GRID3 / 1024, 256, 0, s>>>(grid, partial);
 	k_grid_mean_final<<<1, 256, 0, s>>>(partial, GRID3 / 1024, mean);
 }
-void launch_bitfield(hipStream_t s, const float* grid, uint8_t* bitfield, const float* mean, uint32_t n_cascades) {
+void launch_bitfield(hipStream_t s, const float* grid, uint8_t* bitfield, const float* mean, uint32_t n_cascades, uint32_t* lin) {
 	const uint32_t nbytes = GRID3 / 8;
 	k_grid_to_bitfield<<<nblk(nbytes * NERF_CASCADES), 256, 0, s>>>(nbytes * NERF_CASCADES, nbytes * n_cascades, grid, bitfield, mean);
-	k_bitfield_pool_all<<<nblk((uint64_t)nbytes * (NERF_CASCADES - 1), 2048), 256, 0, s>>>(nbytes, bitfield);
+	k_bitfield_pool_all<<<nblk((uint64_t)nbytes * (NERF_CASCADES - 1), 2048), 256, 0, s>>>(nbytes, bitfield, lin);
+}
+void launch_ema_mean(hipStream_t s, uint32_t n, float decay, float* grid, const float* tmp, float* partial, float* mean) {
+	k_ema_mean<<<n / 1024, 256, 0, s>>>(n, decay, grid, tmp, partial);
+	k_grid_mean_final<<<1, 256, 0, s>>>(partial, GRID3 / 1024, mean);
 }
 
 } // namespace neus

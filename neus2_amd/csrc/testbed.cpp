@@ -761,11 +761,10 @@ struct NeusTestbed {
 			launch_splat_max(s, N, occ_idx.p, occ_density.p, density_tmp.p);
 		}
 		allreduce_f32(density_tmp.p, n_cells, true);
-		launch_ema_grid(s, n_cells, cfg.density_grid_decay, density_grid.p, density_tmp.p);
+		// EMA + mean partials (one launch), final mean, bitfield, mip pools + the march's linear words (one launch)
+		launch_ema_mean(s, n_cells, cfg.density_grid_decay, density_grid.p, density_tmp.p, grid_partial.p, grid_mean.p);
 		++density_grid_ema_step;
-		launch_grid_mean(s, density_grid.p, grid_partial.p, grid_mean.p);
-		launch_bitfield(s, density_grid.p, bitfield.p, grid_mean.p, max_cascade + 1);
-		launch_bitfield_linear(s, bitfield.p, bf_lin.p);
+		launch_bitfield(s, density_grid.p, bitfield.p, grid_mean.p, max_cascade + 1, bf_lin.p);
 	}
 
 	// ------------------------------------------------------------ optimizer (trainer.h:170-172)
