@@ -259,6 +259,7 @@ void launch_enc_ddLdoutput(hipStream_t s, uint32_t n, uint32_t ld, uint32_t L, c
 void launch_transpose_w(hipStream_t s, const TransposeJobs& jobs);
 struct DinPerm { int32_t p[48]; uint32_t din, W; };
 void launch_permute_din(hipStream_t s, const half_t* d0, half_t* d0p, half_t* d0Tp, const DinPerm& perm);
+void launch_transpose_permute(hipStream_t s, const TransposeJobs& jobs, const half_t* d0, half_t* d0p, half_t* d0Tp, const DinPerm& perm);
 // samples [i_begin, i_end) of an n-sample generate_grid_samples_nerf_nonuniform call, written from out_base
 void launch_grid_samples(hipStream_t s, uint32_t n, uint32_t i_begin, uint32_t i_end, uint32_t out_base, uint64_t rng_state, uint64_t rng_inc,
                          uint32_t step, const float* aabb_min, const float* aabb_max, const float* grid_in, float* pos, uint32_t* indices,

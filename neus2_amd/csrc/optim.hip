@@ -68,8 +68,21 @@ __global__ void k_permute_din(const half_t* __restrict__ d0, half_t* __restrict_
 	}
 }
 
-// dst[c][r] = src[r][c]  (all matrices are <= 64x64)
-__global__ void k_transpose_w(TransposeJobs jobs) {
+// dst[c][r] = src[r][c]  (all matrices are <= 64x64); with a DinPerm, the block after the last job does
+// k_permute_din's work (one launch for both)
+__global__ void k_transpose_w(TransposeJobs jobs, const half_t* __restrict__ d0, half_t* __restrict__ d0p, half_t* __restrict__ d0Tp,
+                              DinPerm perm) {
+	if (blockIdx.x == jobs.n) {
+		const uint32_t n = perm.W * perm.din;
+		for (uint32_t e = threadIdx.x; e < n; e += blockDim.x) {
+			const uint32_t row = e / perm.din, p = e % perm.din;
+			const int32_t k = perm.p[p];
+			const half_t v = k >= 0 ? d0[(size_t)row * perm.din + k] : (half_t)0.f;
+			d0p[(size_t)row * perm.din + p] = v;
+			d0Tp[(size_t)p * perm.W + row] = v;
+		}
+		return;
+	}
 	const TransposeJob J = jobs.j[blockIdx.x];
 	for (uint32_t e = threadIdx.x; e < J.rows * J.cols; e += blockDim.x) {
 		const uint32_t r = e / J.cols, c = e % J.cols;
@@ -223,7 +236,10 @@ void launch_add_f32(hipStream_t s, uint32_t n, const float* src, float* dst) {
 	if (n) k_add_f32<<<std::min<uint32_t>((n + 255) / 256, 8192), 256, 0, s>>>(n, src, dst);
 }
 void launch_cast_half(hipStream_t s, uint32_t n, const float* in, half_t* out) { k_cast_half<<<nblk(n), 256, 0, s>>>(n, in, out); }
-void launch_transpose_w(hipStream_t s, const TransposeJobs& jobs) { if (jobs.n) k_transpose_w<<<jobs.n, 256, 0, s>>>(jobs); }
+void launch_transpose_w(hipStream_t s, const TransposeJobs& jobs) { if (jobs.n) k_transpose_w<<<jobs.n, 256, 0, s>>>(jobs, nullptr, nullptr, nullptr, DinPerm{}); }
+void launch_transpose_permute(hipStream_t s, const TransposeJobs& jobs, const half_t* d0, half_t* d0p, half_t* d0Tp, const DinPerm& perm) {
+	k_transpose_w<<<jobs.n + 1, 256, 0, s>>>(jobs, d0, d0p, d0Tp, perm);
+}
 void launch_permute_din(hipStream_t s, const half_t* d0, half_t* d0p, half_t* d0Tp, const DinPerm& perm) {
 	k_permute_din<<<1, 256, 0, s>>>(d0, d0p, d0Tp, perm);
 }

@@ -638,8 +638,7 @@ struct NeusTestbed {
 		tj.j[3] = {mlp.r1, (half_t*)mlp.r1T, l.W, l.W};
 		tj.j[4] = {mlp.r2, (half_t*)mlp.r2T, 16, l.W};
 		tj.n = 5;
-		launch_transpose_w(stream, tj);
-		launch_permute_din(stream, mlp.d0, (half_t*)mlp.d0p, (half_t*)mlp.d0Tp, din_perm);
+		launch_transpose_permute(stream, tj, mlp.d0, (half_t*)mlp.d0p, (half_t*)mlp.d0Tp, din_perm);
 	}
 
 	// progressive levels (grid.h:2427-2440)
