@@ -39,6 +39,14 @@ def measured_traffic(kernel, levels):
     return None if e is None else e.get("bytes_per_launch")
 
 
+def line_traffic(traffic, ms, algorithmic):
+    if not traffic or not ms:
+        return None
+    gbs = traffic / (ms * 1e-3) / 1e9
+    return {"GBs": round(gbs, 1), "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4),
+            "traffic_over_algorithmic": round(traffic / algorithmic, 2) if algorithmic else None}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -184,6 +192,9 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": d["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": d["frac"], "traffic": measured_traffic(dom, levels), "bytes_per_launch": d["bytes"],
                      "units_per_launch": d["units"], "launch_ms": d["ms"], "levels_active": levels},
+        # memory-side line traffic (PMC, profiles/traffic.json) over the same launch: the hashed levels' 4-B corner
+        # gathers each move a 128-B line from the Infinity Cache, so this, not the algorithmic rate, is what binds
+        "line_traffic": line_traffic(measured_traffic(dom, levels), d["ms"], d["bytes"]),
         "non_rollover_fraction": round(real, 4),
         "kernels": kern,
         "loss": st["ray_loss"],

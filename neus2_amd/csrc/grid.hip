@@ -1,12 +1,13 @@
 // Multiresolution hash-grid encoding for gfx950.
 //
 //   k_grid_encode  : forward (enc, optional dy/dx) — restates kernel_grid (grid.h:174-369)
-//   k_grid_scatter : fused first-order (kernel_grid_backward, grid.h:371-500) and second-order
-//                    (kernel_grid_backward_input_backward_grid, grid.h:880-1007) parameter
-//                    gradients: ONE pass, one fp32 RMW per corner-feature instead of the
-//                    reference's two kernels x 24 corner atomics.
+//   k_scatter_hist / k_scatter_bin / k_scatter_accum : fused first-order (kernel_grid_backward,
+//                    grid.h:371-500) and second-order (kernel_grid_backward_input_backward_grid,
+//                    grid.h:880-1007) parameter gradients, binned by destination bucket and summed
+//                    in int64 fixed point (deterministic; see the scatter section below) instead of
+//                    the reference's two kernels x 8 corner fp16x2 atomics.
 //
-// Launch shape: blockIdx.y = level (level-major, like the reference): resident blocks work on
+// k_grid_encode launch shape: blockIdx.y = level (level-major, like the reference): resident blocks work on
 // one or two levels at a time, so the hashed level (2^19 x 4 B = 2 MiB) stays in the XCD's
 // 4 MiB L2 while the blocks of that level run. Samples are grid-strided and the active count is
 // read from device memory, so the host never syncs and the launch is graph-capturable.
@@ -153,6 +154,15 @@ __device__ __forceinline__ ScatterLevel scatter_level(const GridLevels& gl, uint
 	return L;
 }
 
+// Slot order of the blocks inside a bucket: blocks dispatched to the same XCD (blockIdx mod 8) are made
+// adjacent, so the short per-block runs that share a 128-B line of the record arrays are written through
+// one L2 (consecutive blockIdx land on different XCDs). A bijection on [0, n); the sum per bucket and
+// the bucket boundaries are unchanged, and k_scatter_accum is order-independent.
+__device__ __forceinline__ uint32_t xcd_slot(uint32_t blk, uint32_t n) {
+	const uint32_t q = n >> 3, r = n & 7, x = blk & 7, y = blk >> 3;
+	return x * q + min(x, r) + y;
+}
+
 __global__ void __launch_bounds__(256) k_scatter_hist(const uint32_t* __restrict__ n_ptr, uint32_t n_fixed, uint32_t ld,
                                                       const float* __restrict__ coords, uint32_t coord_stride, const GridLevels gl,
                                                       uint32_t valid_level, const uint32_t* __restrict__ dLdenc, const uint32_t* __restrict__ g,
@@ -181,15 +191,15 @@ __global__ void __launch_bounds__(256) k_scatter_hist(const uint32_t* __restrict
 		}
 	}
 	__syncthreads();
-	for (uint32_t b = threadIdx.x; b < w.n_buckets; b += blockDim.x) w.counts[(size_t)b * w.n_blocks + blk] = hist[b];
+	for (uint32_t b = threadIdx.x; b < w.n_buckets; b += blockDim.x) w.counts[(size_t)b * w.n_blocks + xcd_slot(blk, w.n_blocks)] = hist[b];
 }
 
-// Per wave and level: the wave's records (64 lanes x 8 corners) are staged in LDS in emission order
-// while their buckets are counted (as k_scatter_hist); each non-empty bucket then reserves its run with
-// one LDS atomic on the block's cursor for that bucket, and the staged records are written to their
-// run at a slot from a second per-bucket counter (lanes of one bucket get consecutive slots). The
-// block's cursors cover only the current level's buckets (one barrier pair per level), which keeps the
-// LDS footprint small enough for five workgroups per CU.
+// Per wave and level: each lane keeps its 8 records in registers while their buckets are counted (as
+// k_scatter_hist); each non-empty bucket then reserves its run with one LDS atomic on the block's cursor
+// for that bucket, the wave scans its bucket counts, and the records are counting-sorted by bucket into a
+// per-wave LDS stage. The stage is written out in order, so consecutive lanes store consecutive slots of
+// one bucket's run (coalesced segments instead of one scattered 2-B + 4-B store pair per lane). The
+// block's cursors cover only the current level's buckets (one barrier group per level).
 constexpr int SB_WSTAGE = 64 * 8;
 __global__ void __launch_bounds__(256) k_scatter_bin(const uint32_t* __restrict__ n_ptr, uint32_t n_fixed, uint32_t ld,
                                                      const float* __restrict__ coords, uint32_t coord_stride, const GridLevels gl,
@@ -197,9 +207,9 @@ __global__ void __launch_bounds__(256) k_scatter_bin(const uint32_t* __restrict_
                                                      const float4* __restrict__ v4, ScatterWork w) {
 	__shared__ uint32_t cursor[SB_LEVEL_BUCKETS];                // next global slot of this block in the level's buckets
 	__shared__ uint32_t carry_b, carry_v;                        // a bucket shared with the previous level
-	__shared__ uint32_t wcnt[4][SB_LEVEL_BUCKETS], wbase[4][SB_LEVEL_BUCKETS];
-	__shared__ float2 st_g[4][SB_WSTAGE];
-	__shared__ uint32_t st_e[4][SB_WSTAGE];                       // gidx of the record, or ~0u for none
+	__shared__ uint32_t wcnt[4][SB_LEVEL_BUCKETS], wbase[4][SB_LEVEL_BUCKETS], wloff[4][SB_LEVEL_BUCKETS];
+	__shared__ uint32_t st_g[4][SB_WSTAGE];                       // sorted stage: fp16x2 contribution
+	__shared__ uint32_t st_e[4][SB_WSTAGE];                       // sorted stage: entry in bucket | level-local bucket << 16
 	const uint32_t blk = blockIdx.x, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
 	const uint32_t n = load_n(n_ptr, n_fixed);
 	const uint32_t i = blk * blockDim.x + threadIdx.x;
@@ -210,42 +220,59 @@ __global__ void __launch_bounds__(256) k_scatter_bin(const uint32_t* __restrict_
 	const float4 vv = v4[ic];
 	uint32_t* cnt = wcnt[wv];
 	uint32_t* bas = wbase[wv];
-	float2* sg = st_g[wv];
+	uint32_t* loff = wloff[wv];
+	uint32_t* sg = st_g[wv];
 	uint32_t* se = st_e[wv];
 	if (threadIdx.x == 0) { carry_b = ~0u; carry_v = 0; }
 	for (uint32_t l = 0; l < gl.n_levels && l <= valid_level; ++l) {
 		const uint32_t b_first = gl.offset[l] >> SB_SHIFT, nlb = ((gl.offset[l + 1] - 1) >> SB_SHIFT) - b_first + 1;
-		__syncthreads();  // previous level's cursors are final (carry_b / carry_v written)
+		__syncthreads();  // previous level's cursors are final (carry_b / carry_v written), its stage drained
 		for (uint32_t k = threadIdx.x; k < nlb; k += blockDim.x) {
 			const uint32_t b = b_first + k;
-			cursor[k] = b == carry_b ? carry_v : w.offs[(size_t)b * w.n_blocks + blk];
+			cursor[k] = b == carry_b ? carry_v : w.offs[(size_t)b * w.n_blocks + xcd_slot(blk, w.n_blocks)];
 		}
 		for (uint32_t k = lane; k < nlb; k += 64) cnt[k] = 0;
+		__builtin_amdgcn_wave_barrier();
 		const ScatterLevel L = scatter_level(gl, l, x, y, z, ic, ld, dLdenc, g, vv);
+		uint32_t re[8], rg[8];
 #pragma unroll
 		for (uint32_t idx = 0; idx < 8; ++idx) {
 			uint32_t gidx; float a0, a1;
 			corner_contribution(L, idx, gidx, a0, a1);
 			const bool emit = wave_run_sum(gidx, a0, a1, ok);
 			if (emit) atomicAdd(&cnt[(gidx >> SB_SHIFT) - b_first], 1u);
-			sg[idx * 64 + lane] = make_float2(a0, a1);
-			se[idx * 64 + lane] = emit ? gidx : ~0u;
+			re[idx] = emit ? gidx : ~0u;
+			rg[idx] = __builtin_bit_cast(uint32_t, (h2){(half_t)a0, (half_t)a1});
 		}
-		__syncthreads();  // cursors loaded
-		for (uint32_t k = lane; k < nlb; k += 64) {
-			const uint32_t v = cnt[k];
-			bas[k] = v ? atomicAdd(&cursor[k], v) : 0u;
-			cnt[k] = 0;
+		__syncthreads();  // cursors loaded, bucket counts complete
+		// per bucket: the run reserved on the block cursor and the wave-local offset (exclusive scan of the counts)
+		uint32_t total = 0;
+		for (uint32_t k0 = 0; k0 < nlb; k0 += 64) {
+			const uint32_t k = k0 + lane;
+			const uint32_t v = k < nlb ? cnt[k] : 0u;
+			uint32_t incl = v;
+#pragma unroll
+			for (int d = 1; d < 64; d <<= 1) { const uint32_t t = (uint32_t)__shfl_up((int)incl, d); if ((int)lane >= d) incl += t; }
+			if (k < nlb) { bas[k] = v ? atomicAdd(&cursor[k], v) : 0u; loff[k] = total + incl - v; cnt[k] = 0; }
+			total += (uint32_t)__shfl((int)incl, 63);
 		}
-		for (uint32_t kk = 0; kk < 8; ++kk) {
-			const uint32_t e = se[kk * 64 + lane];
+		__syncthreads();  // offsets visible, counters cleared
+#pragma unroll
+		for (uint32_t idx = 0; idx < 8; ++idx) {
+			const uint32_t e = re[idx];
 			if (e != ~0u) {
 				const uint32_t lb = (e >> SB_SHIFT) - b_first;
-				const uint32_t gp = bas[lb] + atomicAdd(&cnt[lb], 1u);
-				w.rec_i[gp] = (uint16_t)(e & (SB_SIZE - 1));
-				const float2 v = sg[kk * 64 + lane];
-				w.rec_g[gp] = (h2){(half_t)v.x, (half_t)v.y};
+				const uint32_t pos = loff[lb] + atomicAdd(&cnt[lb], 1u);
+				se[pos] = (e & (SB_SIZE - 1)) | (lb << 16);
+				sg[pos] = rg[idx];
 			}
+		}
+		__syncthreads();  // stage complete
+		for (uint32_t r = lane; r < total; r += 64) {
+			const uint32_t u = se[r], lb = u >> 16;
+			const uint32_t gp = bas[lb] + (r - loff[lb]);
+			w.rec_i[gp] = (uint16_t)(u & 0xffffu);
+			w.rec_g[gp] = __builtin_bit_cast(h2, sg[r]);
 		}
 		__syncthreads();  // all reservations of this level done
 		if (threadIdx.x == 0) { carry_b = b_first + nlb - 1; carry_v = cursor[nlb - 1]; }

@@ -14,7 +14,8 @@
 // Pinning: the reference ships no golden vectors and cannot
 // be compiled here. The RNG is pinned against the published PCG32 known-answer
 // vectors; everything else is a line-by-line restatement cross-checked against
-// torch float64 autograd in tests/test_oracle_autograd.py. See DESIGN.md §Oracle.
+// torch float64 autograd (tests/torch_ref.py, used by tests/test_oracle.py and
+// tests/test_gpu_module.py). See DESIGN.md §Oracle.
 //
 // Determinism notes shared with the HIP path (both sides do exactly this):
 //  * no FMA contraction (-ffp-contract=off here and in the HIP march/loss files);

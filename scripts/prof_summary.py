@@ -85,6 +85,16 @@ def main():
         t0 = seq[0][1]
         lines.append("\nLaunch sequence of the final step (start us, duration us):\n")
         lines += [f"    {(st - t0) / 1e3:9.1f} {(en - st) / 1e3:8.1f}  {short(n)}" for n, st, en in seq]
+        # bench.py's per-kernel replays (kernel_rooflines) run after the last training step: their median launch is
+        # the `launch_ms` of the bench line's roofline / kernels entries
+        tail = {}
+        for n, st, en in ks[adam[-1] + 1:]:
+            tail.setdefault(short(n), []).append((en - st) / 1e3)
+        if tail:
+            lines.append("\nReplayed launches after the timed steps (bench.py kernel_rooflines): kernel, launches, median us\n")
+            for k, v in sorted(tail.items(), key=lambda kv: -sorted(kv[1])[len(kv[1]) // 2]):
+                v = sorted(v)
+                lines.append(f"    {k:28s} {len(v):4d} {v[len(v) // 2]:9.1f}")
     text = "\n".join(lines) + "\n"
     if len(sys.argv) > 2:
         open(sys.argv[2], "w").write(text)
