@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libneus2_hip.so")
+# NEUS2_HIP_LIB: development override (bitwise A/B of two builds, scripts/golden_params.py); unset in use
+LIB_PATH = os.environ.get("NEUS2_HIP_LIB") or os.path.join(_HERE, "libneus2_hip.so")
 
 
 class NeusNetworkConfig(C.Structure):

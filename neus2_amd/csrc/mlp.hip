@@ -1269,6 +1269,14 @@ __global__ void __launch_bounds__(256) k_wgrad(WGradJobs jobs) {
 	const WGradJob J = jobs.j[ji];
 	b -= jobs.block_start[ji];
 	const uint32_t tiles = J.tiles_m * J.tiles_k;
+	// XCD-aware order: the tiles of one sample split read the same D / X rows, so they go to blocks of one XCD
+	// (blockIdx mod 8; consecutive blockIdx land on different XCDs) and share its L2. The partial keeps its
+	// logical slot (split-major), so k_wgrad_reduce and its summation order are unchanged.
+	const uint32_t n_split = (J.ncols + jobs.split - 1) / jobs.split;
+	if (tiles > 1 && (n_split & 7) == 0 && (jobs.block_start[ji] & 7) == 0) {
+		const uint32_t x = b & 7, slot = b >> 3;
+		b = ((slot / tiles) * 8 + x) * tiles + slot % tiles;
+	}
 	const uint32_t tile = b % tiles, sp = b / tiles;
 	const uint32_t mt = tile / J.tiles_k, kt = tile % J.tiles_k;
 	const uint32_t n0 = sp * jobs.split, n1 = min(J.ncols, n0 + jobs.split);
@@ -1320,7 +1328,7 @@ __global__ void __launch_bounds__(256) k_wgrad(WGradJobs jobs) {
 #pragma unroll
 	for (int reg = 0; reg < 16; ++reg) red[wv][acc_row(reg, h) * 32 + r] = (acc[0][reg] + acc[1][reg]) + (acc[2][reg] + acc[3][reg]);
 	__syncthreads();
-	float* out = jobs.partial + (size_t)blockIdx.x * 1024;
+	float* out = jobs.partial + (size_t)(jobs.block_start[ji] + b) * 1024;
 	for (uint32_t e = threadIdx.x; e < 1024; e += 256) out[e] = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
 }
 

@@ -5,7 +5,7 @@ Follows the reference converter tools/data_format_from_neus.py (SURVEY.md §2.1,
   - load_K_Rt_from_P: P -> K (normalised by K[2,2]), pose = [R^T | C] (:12-33)
   - header {w, h, aabb_scale 1, scale 0.5, offset 0.5, from_na}        (:141-150, :177-186)
   - views 8,13,16,21,26,31,34,56 go to the test split, the rest train (:93, :170-171, :208-209)
-  - images: RGB from image/, alpha from mask/ (first channel), written as RGBA PNG (:120-135)
+  - images: RGB from image/, alpha from mask/ (luminance, as cv2.imread(path, 0)), written as RGBA PNG (:120-135)
 The reference decomposes P with cv2.decomposeProjectionMatrix (absent here); this is the same
 decomposition restated in numpy: M = K R with R a rotation (det +1), K upper triangular,
 K[0,0] > 0 and K[1,1] > 0 (OpenCV's RQDecomp3x3 convention), camera centre C = null(P).
@@ -73,7 +73,9 @@ def generate(base_dir, output_dir, copy_image=True, wrong_camera=(), test_views=
         if not copy_image:
             break
         rgb = np.asarray(Image.open(os.path.join(base_dir, "image", name)).convert("RGB"))
-        m = np.asarray(Image.open(os.path.join(base_dir, "mask", mname)).convert("RGB"))[..., 0]
+        # cv2.imread(path, 0) (reference :130) reads the mask as luminance; PIL's "L" is the same ITU-R 601 weighting
+        # (integer rounding may differ by one level from OpenCV's, which is not importable here: parity unpinned)
+        m = np.asarray(Image.open(os.path.join(base_dir, "mask", mname)).convert("L"))
         Image.fromarray(np.concatenate([rgb, m[..., None]], -1), "RGBA").save(os.path.join(out_img, name))
         H, W = rgb.shape[:2]
     names = sorted(os.listdir(out_img))
