@@ -192,12 +192,14 @@ void launch_march_write(hipStream_t s, uint32_t cap, StepState* st, const DevDat
                         const uint32_t* base, uint32_t* numsteps, float* coords, uint32_t* sample_ray, uint32_t sample_cap /* >= max_inference */);
 void debug_launch_march_stats(hipStream_t s, uint32_t n_rays, const float* rays, const float* tstart, const uint32_t* lin, const DevDataset& ds,
                               const uint8_t* bf, uint32_t* out);
+// dt_const: every sample's dt is MIN_CONE_STEPSIZE (cone angle 0, coordinates from k_march_write): the kernel
+// evaluates the same warp / unwarp instead of reading the coordinate record
 void launch_loss_alpha(hipStream_t s, uint32_t cap_samples, const StepState* st, const float* coords, const half_t* net_out, float cos_anneal,
-                       const LossWork& w);
+                       const LossWork& w, bool dt_const = false);
 void launch_loss_scan_ray(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, const LossWork& w, uint32_t* ccount);
 // progressive (cut-off-aware) inference rounds (march.hip)
 void launch_loss_alpha_list(hipStream_t s, uint32_t cap_samples, const uint32_t* n_ptr, const uint32_t* idx, const float* coords,
-                            const half_t* net_out, float cos_anneal, const LossWork& w);
+                            const half_t* net_out, float cos_anneal, const LossWork& w, bool dt_const = false);
 void launch_chunk_count(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, uint32_t e1, uint32_t* m, uint32_t* counters /* zeroed */,
                         uint32_t n_counters);
 void launch_chunk_write(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, const uint32_t* m, const uint32_t* pos /* exclusive scan of m */,

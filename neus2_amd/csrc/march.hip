@@ -580,14 +580,18 @@ __global__ void k_march_stats(uint32_t n_rays, const float* __restrict__ rays, c
 // n = min(*n_ptr, cap) samples; with idx, work item j is sample idx[j] (a progressive-inference round)
 __global__ void __launch_bounds__(256) k_loss_alpha(uint32_t cap, const uint32_t* __restrict__ n_ptr, const uint32_t* __restrict__ idx,
                                                     const float* __restrict__ coords, const half_t* __restrict__ net_out, float cos_anneal,
-                                                    float4* __restrict__ sa, float* __restrict__ ekt, uint32_t* __restrict__ n_long) {
+                                                    float4* __restrict__ sa, float* __restrict__ ekt, uint32_t* __restrict__ n_long,
+                                                    bool dt_const) {
 	if (n_long && blockIdx.x == 0 && threadIdx.x == 0) *n_long = 0u;  // the transmittance scan's long-ray list (next kernel)
 	const uint32_t n = min(*n_ptr, cap);
+	// cone angle 0: k_march_write stored warp_dt(MIN_CONE_STEPSIZE) in every record; the same round trip here
+	// (bit-identical) saves touching the 28-B records' lines for one float each
+	const float dt0 = unwarp_dt(warp_dt(MIN_CONE_STEPSIZE));
 	for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
 		const uint32_t s = idx ? idx[j] : j;
 		half_t lo[16]; load_out(net_out, s, lo);
 		float dir[3]; bent_dir(lo, dir);
-		const Alpha a = neus_alpha(lo, dir, unwarp_dt(coords[(size_t)s * COORD_W + 3]), cos_anneal);
+		const Alpha a = neus_alpha(lo, dir, dt_const ? dt0 : unwarp_dt(coords[(size_t)s * COORD_W + 3]), cos_anneal);
 		sa[s] = make_float4(a.alpha, det_logistic((float)lo[0]), det_logistic((float)lo[1]), det_logistic((float)lo[2]));
 		const float gn = grad_norm(lo);
 		ekt[s] = (gn - 1.0f) * (gn - 1.0f);
@@ -1102,12 +1106,13 @@ void debug_launch_march_stats(hipStream_t s, uint32_t n_rays, const float* rays,
 }
 static inline uint32_t sample_blocks(uint32_t cap) { return std::max<uint32_t>(1, std::min<uint32_t>((cap + 255) / 256, 16384)); }
 void launch_loss_alpha(hipStream_t s, uint32_t cap_samples, const StepState* st, const float* coords, const half_t* net_out, float cos_anneal,
-                       const LossWork& w) {
-	k_loss_alpha<<<sample_blocks(cap_samples), 256, 0, s>>>(cap_samples, &st->n_kept, nullptr, coords, net_out, cos_anneal, w.sa, w.ekt, w.n_long);
+                       const LossWork& w, bool dt_const) {
+	k_loss_alpha<<<sample_blocks(cap_samples), 256, 0, s>>>(cap_samples, &st->n_kept, nullptr, coords, net_out, cos_anneal, w.sa, w.ekt, w.n_long,
+	                                                        dt_const);
 }
 void launch_loss_alpha_list(hipStream_t s, uint32_t cap_samples, const uint32_t* n_ptr, const uint32_t* idx, const float* coords,
-                            const half_t* net_out, float cos_anneal, const LossWork& w) {
-	k_loss_alpha<<<sample_blocks(cap_samples), 256, 0, s>>>(cap_samples, n_ptr, idx, coords, net_out, cos_anneal, w.sa, w.ekt, nullptr);
+                            const half_t* net_out, float cos_anneal, const LossWork& w, bool dt_const) {
+	k_loss_alpha<<<sample_blocks(cap_samples), 256, 0, s>>>(cap_samples, n_ptr, idx, coords, net_out, cos_anneal, w.sa, w.ekt, nullptr, dt_const);
 }
 void launch_chunk_count(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, uint32_t e1, uint32_t* m, uint32_t* counters,
                         uint32_t n_counters) {

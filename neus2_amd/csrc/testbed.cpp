@@ -997,7 +997,7 @@ struct NeusTestbed {
 				const uint32_t e1 = k + 1 < nch ? chunk_ends[k] : 0xffffffffu;
 				const uint32_t e2 = k + 2 < nch ? chunk_ends[k + 1] : 0xffffffffu;
 				launch_nerf_infer(s, lay.L, lay.W, chunk_cnt.p + k, 0, c_in, gl, valid, params_h.p + lay.grid_off, mlp, net_out.p, 8192, chunk_list.p);
-				launch_loss_alpha_list(s, max_samples, chunk_cnt.p + k, chunk_list.p, coords.p, net_out.p, lp.cos_anneal, w);
+				launch_loss_alpha_list(s, max_samples, chunk_cnt.p + k, chunk_list.p, coords.p, net_out.p, lp.cos_anneal, w, ds.cone_angle == 0.0f);
 				launch_loss_scan_chunk(s, MAX_RAYS, numsteps.p, w, ccount.p, e0, e1, e2, k + 1 < nch ? chunk_list.p : nullptr, chunk_cnt.p + k + 1);
 				e0 = e1;
 			}
@@ -1005,7 +1005,7 @@ struct NeusTestbed {
 		} else {
 			launch_nerf_infer(s, lay.L, lay.W, &st.p->n_kept, 0, c_in, gl, valid, params_h.p + lay.grid_off, mlp, net_out.p, 8192);
 			mark(3);
-			launch_loss_alpha(s, max_samples, st.p, coords.p, net_out.p, lp.cos_anneal, w);
+			launch_loss_alpha(s, max_samples, st.p, coords.p, net_out.p, lp.cos_anneal, w, ds.cone_angle == 0.0f);
 			launch_loss_scan_ray(s, MAX_RAYS, numsteps.p, w, ccount.p);
 		}
 		launch_exclusive_scan(s, scan_tmp.p, scan_tmp_bytes, ccount.p, cbase.p, MAX_RAYS);
