@@ -143,6 +143,10 @@ struct NeusLocalGroup {
 struct NeusTestbed {
 	int device = 0;
 	hipStream_t stream = nullptr;
+	// side stream of the backward: the weight-gradient GEMM runs there beside the grid scatter (disjoint inputs and
+	// outputs; both deterministic), forked from and joined back into the step's stream by events
+	hipStream_t aux_stream = nullptr;
+	hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 	NeusNetworkConfig cfg{};
 	bool have_net = false, have_data = false;
 	Layout lay{};
@@ -262,6 +266,9 @@ struct NeusTestbed {
 	NeusTestbed(int dev) : device(dev) {
 		HIP_CHECK(hipSetDevice(device));
 		HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+		HIP_CHECK(hipStreamCreateWithFlags(&aux_stream, hipStreamNonBlocking));
+		HIP_CHECK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+		HIP_CHECK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
 		HIP_CHECK(hipHostMalloc((void**)&pinned, 64 * sizeof(float)));
 		for (auto& set : ev)
 			for (auto& e : set) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
@@ -286,6 +293,9 @@ struct NeusTestbed {
 		for (auto& e : ev_done) if (e) (void)hipEventDestroy(e);
 		if (prof_st) (void)hipHostFree(prof_st);
 		if (pinned) (void)hipHostFree(pinned);
+		if (aux_stream) { (void)hipStreamSynchronize(aux_stream); (void)hipStreamDestroy(aux_stream); }
+		if (ev_fork) (void)hipEventDestroy(ev_fork);
+		if (ev_join) (void)hipEventDestroy(ev_join);
 		if (stream) (void)hipStreamDestroy(stream);
 	}
 
@@ -696,10 +706,22 @@ struct NeusTestbed {
 		if (marks) mark(6);
 		if (!canonical) { if (marks) mark(7); return; }  // global-movement phase: canonical gradients unused
 		WGradJobs J = wgrad_jobs(n, ld, g, n_train_ptr);
-		launch_wgrad(s, J, J.block_start[5]);
-		if (marks) mark(7);
+		if (marks) {  // per-phase timing: in order on one stream
+			launch_wgrad(s, J, J.block_start[5]);
+			mark(7);
+			launch_grid_scatter(s, n_train_ptr, n, ld, c, COORD_W, gl, valid, tbuf.dLdenc, tbuf.genc, tbuf.v, g + lay.grid_off, swork, scan_tmp.p,
+			                    scan_tmp_bytes);
+			return;
+		}
+		// the weight-gradient GEMM (MLP gradients, variance) beside the grid scatter (grid gradients): neither reads
+		// what the other writes, so the side stream overlaps them; the step's stream waits for both
+		HIP_CHECK(hipEventRecord(ev_fork, s));
+		HIP_CHECK(hipStreamWaitEvent(aux_stream, ev_fork, 0));
+		launch_wgrad(aux_stream, J, J.block_start[5]);
+		HIP_CHECK(hipEventRecord(ev_join, aux_stream));
 		launch_grid_scatter(s, n_train_ptr, n, ld, c, COORD_W, gl, valid, tbuf.dLdenc, tbuf.genc, tbuf.v, g + lay.grid_off, swork, scan_tmp.p,
 		                    scan_tmp_bytes);
+		HIP_CHECK(hipStreamWaitEvent(s, ev_join, 0));
 	}
 
 	// ------------------------------------------------------------ collectives
