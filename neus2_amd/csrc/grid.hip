@@ -14,6 +14,7 @@
 #include "kernels.h"
 #include "grid_common.h"
 #include <algorithm>
+#include <vector>
 
 namespace neus {
 
@@ -279,12 +280,24 @@ __global__ void __launch_bounds__(256) k_scatter_bin(const uint32_t* __restrict_
 	}
 }
 
+// One workgroup per bucket, or `parts` workgroups for a bucket of a small dense level (one 4096-entry bucket can hold a
+// whole level's records): each part sums an equal slice of the bucket's records in LDS and adds its nonzero int64 sums
+// to the bucket's split slot with 64-bit integer atomics (exact, so the total is order-independent and bitwise the
+// one-workgroup sum); the last part to finish reads the slot back (exchanging it with zero for the next use) and
+// stores the fp32 gradient.
 __global__ void __launch_bounds__(256) k_scatter_accum(ScatterWork w, float* __restrict__ grads, uint32_t n_entries) {
 	__shared__ unsigned long long acc[2 * SB_SIZE];  // feature planes, int64 fixed point (2^-32)
-	const uint32_t b = blockIdx.x;
+	__shared__ uint32_t s_last;
+	const uint4 job = w.jobs[blockIdx.x];
+	const uint32_t b = job.x, part = job.y, parts = job.z, slot = job.w;
 	for (uint32_t k = threadIdx.x; k < 2 * SB_SIZE; k += blockDim.x) acc[k] = 0ull;
 	__syncthreads();
-	const uint32_t c0 = w.offs[(size_t)b * w.n_blocks], c1 = w.offs[(size_t)(b + 1) * w.n_blocks];
+	uint32_t c0 = w.offs[(size_t)b * w.n_blocks], c1 = w.offs[(size_t)(b + 1) * w.n_blocks];
+	if (parts > 1) {
+		const uint32_t len = c1 - c0;
+		c1 = c0 + (uint32_t)((uint64_t)len * (part + 1) / parts);
+		c0 = c0 + (uint32_t)((uint64_t)len * part / parts);
+	}
 	auto fix = [](float v) {  // |v| < 2^31 (clamped) -> int64 multiple of 2^-32
 		return (unsigned long long)__float2ll_rn(fminf(fmaxf(v, -2147483520.0f), 2147483520.0f) * SB_FIX_SCALE);
 	};
@@ -309,11 +322,30 @@ __global__ void __launch_bounds__(256) k_scatter_accum(ScatterWork w, float* __r
 		}
 	}
 	__syncthreads();
-	// the workgroup owns entries [b * SB_SIZE, +SB_SIZE): plain stores of the interleaved fp32 pairs
+	// the bucket owns entries [b * SB_SIZE, +SB_SIZE): plain stores of the interleaved fp32 pairs
 	const uint32_t e0 = b << SB_SHIFT;
 	const uint32_t ne = min(SB_SIZE, n_entries - e0);
-	for (uint32_t k = threadIdx.x; k < 2 * ne; k += blockDim.x)
-		grads[2 * (size_t)e0 + k] = (float)((double)(long long)acc[(k & 1) * SB_SIZE + (k >> 1)] * (1.0 / 4294967296.0));
+	if (parts == 1) {
+		for (uint32_t k = threadIdx.x; k < 2 * ne; k += blockDim.x)
+			grads[2 * (size_t)e0 + k] = (float)((double)(long long)acc[(k & 1) * SB_SIZE + (k >> 1)] * (1.0 / 4294967296.0));
+		return;
+	}
+	unsigned long long* H = w.split + (size_t)slot * 2 * SB_SIZE;
+	for (uint32_t k = threadIdx.x; k < 2 * SB_SIZE; k += blockDim.x) {
+		const unsigned long long v = acc[k];
+		if (v) atomicAdd(&H[k], v);
+	}
+	__threadfence();
+	__syncthreads();
+	if (threadIdx.x == 0) s_last = atomicAdd(&w.split_done[slot], 1u) == parts - 1 ? 1u : 0u;
+	__syncthreads();
+	if (!s_last) return;
+	__threadfence();
+	for (uint32_t k = threadIdx.x; k < 2 * ne; k += blockDim.x) {
+		const unsigned long long v = atomicExch(&H[(k & 1) * SB_SIZE + (k >> 1)], 0ull);
+		grads[2 * (size_t)e0 + k] = (float)((double)(long long)v * (1.0 / 4294967296.0));
+	}
+	if (threadIdx.x == 0) atomicExch(&w.split_done[slot], 0u);
 }
 
 // ---------------------------------------------------------------- operator-module helpers (neus_module_*)
@@ -371,6 +403,21 @@ void launch_grid_encode(hipStream_t s, const uint32_t* n_ptr, uint32_t n_fixed, 
 	k_grid_encode<<<dim3(grid_x, gl.n_levels), 256, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, grid, enc, dydx);
 }
 size_t scatter_records_capacity(uint32_t n_cap, uint32_t n_levels) { return (size_t)n_cap * n_levels * 8; }
+std::vector<uint32_t> scatter_accum_jobs(const GridLevels& gl, uint32_t n_buckets, uint32_t& n_split) {
+	// parts of a bucket ~ its records relative to a hashed level's bucket: 32 x 4096 / (entries of the smallest level
+	// overlapping it), clamped to [1, 32] (level 0 at 16^3: 32 parts; 23^3: 10; 33^3: 3; 48^3 and up: 1)
+	std::vector<uint32_t> jobs;
+	n_split = 0;
+	for (uint32_t b = 0; b < n_buckets; ++b) {
+		uint32_t smin = 0xffffffffu;
+		for (uint32_t l = 0; l < gl.n_levels; ++l)
+			if (gl.offset[l] < (b + 1) * SB_SIZE && gl.offset[l + 1] > b * SB_SIZE) smin = std::min(smin, gl.offset[l + 1] - gl.offset[l]);
+		const uint32_t parts = smin == 0xffffffffu ? 1u : std::max(1u, std::min(32u, (uint32_t)((32ull * SB_SIZE) / std::max(1u, smin))));
+		const uint32_t slot = parts > 1 ? n_split++ : 0u;
+		for (uint32_t p = 0; p < parts; ++p) { jobs.push_back(b); jobs.push_back(p); jobs.push_back(parts); jobs.push_back(slot); }
+	}
+	return jobs;
+}
 uint32_t scatter_n_buckets(const GridLevels& gl) {
 	for (uint32_t l = 0; l < gl.n_levels; ++l)
 		if (((gl.offset[l + 1] - 1) >> SB_SHIFT) - (gl.offset[l] >> SB_SHIFT) + 1 > SB_LEVEL_BUCKETS)
@@ -388,7 +435,7 @@ void launch_grid_scatter(hipStream_t s, const uint32_t* n_ptr, uint32_t n_fixed,
 	launch_exclusive_scan(s, scan_tmp, scan_tmp_bytes, w.counts, w.offs, (uint32_t)nb + 1);
 	k_scatter_bin<<<nblk, 256, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, (const uint32_t*)dLdenc, (const uint32_t*)g, v, w);
 	// every bucket (also one without records: its entries' gradient is zero) is written by its workgroup
-	k_scatter_accum<<<w.n_buckets, 256, 0, s>>>(w, grads, gl.offset[gl.n_levels]);
+	k_scatter_accum<<<w.n_jobs, 256, 0, s>>>(w, grads, gl.offset[gl.n_levels]);
 }
 
 } // namespace neus

@@ -1,6 +1,7 @@
 // Host-callable launchers of the gfx950 kernels (defined in the .hip files) and the structs
 // shared between the host orchestration (testbed.cpp) and the kernels.
 #pragma once
+#include <vector>
 #include "common.h"
 
 namespace neus {
@@ -102,7 +103,15 @@ struct ScatterWork {
 	h2* rec_g;          // [capacity] contribution (feature 0, feature 1), fp16 as the reference's per-corner half2 atomic operand
 	uint16_t* rec_i;    // [capacity] entry within the bucket
 	uint32_t n_buckets, n_blocks;
+	// accumulation workgroups (scatter_accum_jobs): {bucket, part, parts, split slot}; the buckets of the small dense
+	// levels collect most records, so they are split over `parts` workgroups whose int64 sums meet in `split`
+	const uint4* jobs;
+	unsigned long long* split;  // [n_split][2 * SB_SIZE] int64 partial sums (zero between uses)
+	uint32_t* split_done;       // [n_split] parts finished (reset by the last part)
+	uint32_t n_jobs;
 };
+// accumulation workgroups of the scatter (flattened uint4 {bucket, part, parts, split slot}); n_split = split buckets
+std::vector<uint32_t> scatter_accum_jobs(const GridLevels& gl, uint32_t n_buckets, uint32_t& n_split);
 
 // per-sample / per-ray scratch of the restructured loss (march.hip)
 struct LossWork {

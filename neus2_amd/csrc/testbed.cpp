@@ -213,7 +213,8 @@ struct NeusTestbed {
 	size_t scan_tmp_bytes = 0;
 	Dev<StepState> st;
 	ScatterWork swork{};
-	Dev<uint32_t> sc_counts, sc_offs;
+	Dev<uint32_t> sc_counts, sc_offs, sc_jobs, sc_split_done;
+	Dev<unsigned long long> sc_split;
 	Dev<h2> sc_rec_g;
 	Dev<uint16_t> sc_rec_i;
 	// restructured loss scratch (kernels.h LossWork)
@@ -483,6 +484,17 @@ struct NeusTestbed {
 		const size_t n_rec = scatter_records_capacity(swork.n_blocks * 256, l.L);
 		sc_rec_g.alloc(n_rec); sc_rec_i.alloc(n_rec);
 		swork.counts = sc_counts.p; swork.offs = sc_offs.p; swork.rec_g = sc_rec_g.p; swork.rec_i = sc_rec_i.p;
+		{
+			uint32_t n_split = 0;
+			const std::vector<uint32_t> jobs = scatter_accum_jobs(gl, swork.n_buckets, n_split);
+			sc_jobs.alloc(jobs.size());
+			HIP_CHECK(hipMemcpy(sc_jobs.p, jobs.data(), jobs.size() * 4, hipMemcpyHostToDevice));
+			sc_split.alloc(std::max<size_t>(1, (size_t)n_split * 2 * SB_SIZE)); sc_split_done.alloc(std::max(1u, n_split));
+			HIP_CHECK(hipMemset(sc_split.p, 0, sc_split.n * sizeof(unsigned long long)));
+			HIP_CHECK(hipMemset(sc_split_done.p, 0, sc_split_done.n * 4));
+			swork.jobs = (const uint4*)sc_jobs.p; swork.split = sc_split.p; swork.split_done = sc_split_done.p;
+			swork.n_jobs = (uint32_t)(jobs.size() / 4);
+		}
 		scan_tmp_bytes = std::max(scan_temp_bytes(MAX_RAYS), scan_temp_bytes((uint32_t)n_bins));
 		scan_tmp.alloc(scan_tmp_bytes + 256);
 		HIP_CHECK(hipStreamSynchronize(stream));
