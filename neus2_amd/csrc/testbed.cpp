@@ -215,6 +215,8 @@ struct NeusTestbed {
 	ScatterWork swork{};
 	Dev<uint32_t> sc_counts, sc_offs, sc_jobs, sc_split_done;
 	Dev<unsigned long long> sc_split;
+	std::vector<uint32_t> sc_jobs_before;  // [n_buckets + 1] accumulation jobs of the buckets below b
+	uint32_t sc_zero_from = 0;             // the grads' grid part is known zero from this bucket on
 	Dev<h2> sc_rec_g;
 	Dev<uint16_t> sc_rec_i;
 	// restructured loss scratch (kernels.h LossWork)
@@ -494,6 +496,10 @@ struct NeusTestbed {
 			HIP_CHECK(hipMemset(sc_split_done.p, 0, sc_split_done.n * 4));
 			swork.jobs = (const uint4*)sc_jobs.p; swork.split = sc_split.p; swork.split_done = sc_split_done.p;
 			swork.n_jobs = (uint32_t)(jobs.size() / 4);
+			sc_jobs_before.assign(swork.n_buckets + 1, 0u);
+			for (size_t j = 0; j < jobs.size() / 4; ++j) sc_jobs_before[jobs[4 * j] + 1] = (uint32_t)j + 1;
+			for (uint32_t b = 1; b <= swork.n_buckets; ++b) sc_jobs_before[b] = std::max(sc_jobs_before[b], sc_jobs_before[b - 1]);
+			sc_zero_from = swork.n_buckets;  // nothing assumed
 		}
 		scan_tmp_bytes = std::max(scan_temp_bytes(MAX_RAYS), scan_temp_bytes((uint32_t)n_bins));
 		scan_tmp.alloc(scan_tmp_bytes + 256);
@@ -706,6 +712,23 @@ struct NeusTestbed {
 		J.var_grad = g + lay.var_off;
 		return J;
 	}
+	// The grid-gradient buckets past the progressive valid level get no records: their gradient is zero. For the
+	// testbed's own gradient buffer the scatter skips them once they hold zeros (early in training ~2,500 of ~2,600
+	// buckets, each a 64 KB-LDS workgroup), zeroing first the range a lower valid level than the previous step's
+	// leaves stale (a reloaded network, a frame switch).
+	ScatterWork scatter_work_for(float* g_grid, uint32_t valid, hipStream_t s) {
+		if (g_grid != grads.p + lay.grid_off || sc_jobs_before.empty()) return swork;
+		const uint32_t L = gl.n_levels, n_entries = gl.offset[L];
+		const uint32_t sb = valid + 1 >= L ? swork.n_buckets : std::min(swork.n_buckets, (gl.offset[valid + 1] + SB_SIZE - 1) / SB_SIZE);
+		if (sc_zero_from > sb) {
+			const size_t e_lo = (size_t)sb * SB_SIZE, e_hi = std::min<size_t>((size_t)sc_zero_from * SB_SIZE, n_entries);
+			if (e_hi > e_lo) HIP_CHECK(hipMemsetAsync(g_grid + 2 * e_lo, 0, (e_hi - e_lo) * 2 * sizeof(float), s));
+		}
+		sc_zero_from = sb;
+		ScatterWork w = swork;
+		w.n_jobs = sc_jobs_before[sb];
+		return w;
+	}
 	// forward recompute + backward into g (fp32 [P], zeroed by the caller)
 	void net_backward(const uint32_t* n_valid_ptr, const uint32_t* n_train_ptr, uint32_t n, const float* c, uint32_t valid,
 	                  const half_t* dlo, float* g, hipStream_t s, bool marks = false, bool canonical = true) {
@@ -718,11 +741,11 @@ struct NeusTestbed {
 		if (marks) mark(6);
 		if (!canonical) { if (marks) mark(7); return; }  // global-movement phase: canonical gradients unused
 		WGradJobs J = wgrad_jobs(n, ld, g, n_train_ptr);
-		if (marks) {  // per-phase timing: in order on one stream
+		if (marks && profiling) {  // per-phase timing: in order on one stream
 			launch_wgrad(s, J, J.block_start[5]);
 			mark(7);
-			launch_grid_scatter(s, n_train_ptr, n, ld, c, COORD_W, gl, valid, tbuf.dLdenc, tbuf.genc, tbuf.v, g + lay.grid_off, swork, scan_tmp.p,
-			                    scan_tmp_bytes);
+			launch_grid_scatter(s, n_train_ptr, n, ld, c, COORD_W, gl, valid, tbuf.dLdenc, tbuf.genc, tbuf.v, g + lay.grid_off,
+			                    scatter_work_for(g + lay.grid_off, valid, s), scan_tmp.p, scan_tmp_bytes);
 			return;
 		}
 		// the weight-gradient GEMM (MLP gradients, variance) beside the grid scatter (grid gradients): neither reads
@@ -731,8 +754,8 @@ struct NeusTestbed {
 		HIP_CHECK(hipStreamWaitEvent(aux_stream, ev_fork, 0));
 		launch_wgrad(aux_stream, J, J.block_start[5]);
 		HIP_CHECK(hipEventRecord(ev_join, aux_stream));
-		launch_grid_scatter(s, n_train_ptr, n, ld, c, COORD_W, gl, valid, tbuf.dLdenc, tbuf.genc, tbuf.v, g + lay.grid_off, swork, scan_tmp.p,
-		                    scan_tmp_bytes);
+		launch_grid_scatter(s, n_train_ptr, n, ld, c, COORD_W, gl, valid, tbuf.dLdenc, tbuf.genc, tbuf.v, g + lay.grid_off,
+		                    scatter_work_for(g + lay.grid_off, valid, s), scan_tmp.p, scan_tmp_bytes);
 		HIP_CHECK(hipStreamWaitEvent(s, ev_join, 0));
 	}
 
