@@ -192,7 +192,7 @@ __global__ void __launch_bounds__(256) k_scatter_hist(const uint32_t* __restrict
 		}
 	}
 	__syncthreads();
-	for (uint32_t b = threadIdx.x; b < w.n_buckets; b += blockDim.x) w.counts[(size_t)b * w.n_blocks + xcd_slot(blk, w.n_blocks)] = hist[b];
+	for (uint32_t b = threadIdx.x; b < w.n_active; b += blockDim.x) w.counts[(size_t)b * w.n_blocks + xcd_slot(blk, w.n_blocks)] = hist[b];
 }
 
 // Per wave and level: each lane keeps its 8 records in registers while their buckets are counted (as
@@ -429,7 +429,7 @@ void launch_grid_scatter(hipStream_t s, const uint32_t* n_ptr, uint32_t n_fixed,
                          const ScatterWork& w, void* scan_tmp, size_t scan_tmp_bytes) {
 	// the grid always spans the workspace's sample capacity (w.n_blocks x 256 >= n, checked by the host)
 	const uint32_t nblk = w.n_blocks;
-	const size_t nb = (size_t)w.n_buckets * w.n_blocks;
+	const size_t nb = (size_t)w.n_active * w.n_blocks;  // buckets past n_active get no records (scatter_work_for)
 	k_scatter_hist<<<nblk, 256, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, (const uint32_t*)dLdenc, (const uint32_t*)g, v, w);
 	(void)hipMemsetAsync(w.counts + nb, 0, 4, s);
 	launch_exclusive_scan(s, scan_tmp, scan_tmp_bytes, w.counts, w.offs, (uint32_t)nb + 1);

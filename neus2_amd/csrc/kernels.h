@@ -109,6 +109,7 @@ struct ScatterWork {
 	unsigned long long* split;  // [n_split][2 * SB_SIZE] int64 partial sums (zero between uses)
 	uint32_t* split_done;       // [n_split] parts finished (reset by the last part)
 	uint32_t n_jobs;
+	uint32_t n_active;          // buckets counted / scanned (those below it hold every record of the step)
 };
 // accumulation workgroups of the scatter (flattened uint4 {bucket, part, parts, split slot}); n_split = split buckets
 std::vector<uint32_t> scatter_accum_jobs(const GridLevels& gl, uint32_t n_buckets, uint32_t& n_split);

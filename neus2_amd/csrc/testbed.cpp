@@ -496,6 +496,7 @@ struct NeusTestbed {
 			HIP_CHECK(hipMemset(sc_split_done.p, 0, sc_split_done.n * 4));
 			swork.jobs = (const uint4*)sc_jobs.p; swork.split = sc_split.p; swork.split_done = sc_split_done.p;
 			swork.n_jobs = (uint32_t)(jobs.size() / 4);
+			swork.n_active = swork.n_buckets;
 			sc_jobs_before.assign(swork.n_buckets + 1, 0u);
 			for (size_t j = 0; j < jobs.size() / 4; ++j) sc_jobs_before[jobs[4 * j] + 1] = (uint32_t)j + 1;
 			for (uint32_t b = 1; b <= swork.n_buckets; ++b) sc_jobs_before[b] = std::max(sc_jobs_before[b], sc_jobs_before[b - 1]);
@@ -727,6 +728,7 @@ struct NeusTestbed {
 		sc_zero_from = sb;
 		ScatterWork w = swork;
 		w.n_jobs = sc_jobs_before[sb];
+		w.n_active = sb;  // histogram and scan only the buckets that can receive records
 		return w;
 	}
 	// forward recompute + backward into g (fp32 [P], zeroed by the caller)
