@@ -1,4 +1,4 @@
-"""NeuS2 training throughput on MI355X (BASELINE.json metric: training samples/sec).
+"""NeuS2 training throughput on MI355X (BASELINE.json metric: training samples/sec + PSNR@20k).
 
 Workload (BASELINE.md §3 / SURVEY.md §8(d) "Config S"): DTU-scan24-shaped synthetic scene, 49 views of
 1600x1200 RGBA8 (analytic sphere; DTU itself is not reachable here), configs/nerf/base.json
@@ -7,35 +7,49 @@ rays per GPU per step (adaptation frozen), occupancy-grid updates at the referen
 A step = Testbed::train: occupancy update (when due) + sampling + pre-compaction forward + NeuS
 loss/compaction + forward/backward (1st + 2nd order) + RCCL gradient all-reduce + Ema(Adam).
 
-Usage: python bench.py --gpus N --steps K --warmup W  (N>1 via torch.distributed.run, one rank/GPU)
+The timed state is config 2 as labelled: before the W warm-up steps the network is trained `--prepare` steps
+(default 800) so that every hash-grid level is active (the progressive schedule of grid.h:2427-2440 enables the
+last level at step 660). The fresh-network number (W warm-up + K timed steps from step 0, 4 active levels) is
+reported beside it as the `early_steps` leg.
+
+Usage: python bench.py --gpus N --steps K --warmup W
+  N > 1: run under `torch.distributed.run` (one rank per GPU; WORLD_SIZE must equal N), or plainly, in which
+  case this process starts `torch.distributed.run` itself as a child (before touching the GPU) and exits with
+  its status.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-# Memory-side bytes per launch, measured by rocprofv3 PMC passes at HEAD (scripts/gpu_traffic.sh ->
-# profiles/traffic.json): reads = 128 B x TCC_EA0_RDREQ_128B + 64 B x the other read requests (FETCH_SIZE
-# tallies 128-B requests at 64 B, the gfx950 half-count), writes = WRITE_SIZE; L2-to-fabric traffic, so
-# Infinity Cache hits are included (an upper bound on DRAM bytes). Keyed by kernel and the number of
-# active hash-grid levels of the replayed state; `traffic` is null when no measurement of that state exists.
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
+MFMA_PEAK_TFLOPS = 2500.0  # MI355X dense fp16 MFMA (MI355X_MICROARCH.md)
+# Memory-side bytes per launch, measured by rocprofv3 PMC passes (scripts/gpu_traffic.sh -> profiles/traffic.json):
+# reads = 128 B x TCC_EA0_RDREQ_128B + 64 B x the other read requests (FETCH_SIZE tallies 128-B requests at 64 B,
+# the gfx950 half-count), writes = WRITE_SIZE; L2-to-fabric traffic, so Infinity Cache hits are included (an upper
+# bound on DRAM bytes). Keyed by kernel and the number of active hash-grid levels of the replayed state; `traffic`
+# is null when no measurement of that state exists. The file records the commit its passes ran at.
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
 
 
-def measured_traffic(kernel, levels):
+def traffic_table():
     try:
         with open(TRAFFIC_FILE) as f:
-            t = json.load(f)
+            return json.load(f)
     except (OSError, ValueError):
-        return None
-    e = t.get(f"{kernel}@L{levels}")
+        return {}
+
+
+def measured_traffic(kernel, levels):
+    e = traffic_table().get(f"{kernel}@L{levels}")
     return None if e is None else e.get("bytes_per_launch")
 
 
@@ -51,20 +65,24 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
-    p.add_argument("--warmup", type=int, default=800)  # past step ~660 every hash-grid level is active (valid_level schedule)
+    p.add_argument("--warmup", type=int, default=20)
+    # training steps before the warm-up: the all-levels state of config 2 (every level active from step 660)
+    p.add_argument("--prepare", type=int, default=800)
     p.add_argument("--views", type=int, default=49)
     p.add_argument("--width", type=int, default=1600)
     p.add_argument("--height", type=int, default=1200)
     p.add_argument("--batch", type=int, default=1 << 18)
     p.add_argument("--rays", type=int, default=1 << 18)
     p.add_argument("--cpu-baseline", type=int, default=1)
-    p.add_argument("--cpu-steps", type=int, default=8)
-    # quality half of the metric: PSNR after this many steps of the reference's (adaptive-R) training, N=1 only
+    p.add_argument("--cpu-steps", type=int, default=6)
+    p.add_argument("--cpu-config1-steps", type=int, default=100)
+    # quality half of the metric: PSNR after this many steps of the reference's (adaptive-R) training
     p.add_argument("--psnr-steps", type=int, default=20000)
-    # config 5: marching cubes at mc_res^3 over the PSNR leg's trained model (0 = skip)
+    # config 5: marching cubes at mc_res^3 over the PSNR leg's trained model (0 = skip), N = 1
     p.add_argument("--mc-res", type=int, default=1024)
     # BASELINE.json words config 2 as a 16-level grid (the reference's base.json has 14): the same step at L=16
     p.add_argument("--l16", type=int, default=1)
+    p.add_argument("--early", type=int, default=1)
     return p.parse_args()
 
 
@@ -77,9 +95,13 @@ def parse():
 #                  write (fused inference: 508 B) + 60 loss reads (loss kernels)
 #   unit "train" : 1496 B = 60 compacted coords + dL/dout write (loss) + 28 coords + 448 gather (training
 #                  encode: 476 B) + 32 output + 32 dL/dout (training MLP kernels: 32 B each) + 896 grid RMW (scatter)
-# The SURVEY's figures count the gathers as HBM bytes; the 21 MB table mostly hits L2 / Infinity Cache,
-# so `traffic` (PMC) is reported next to them. MFMA flops (SURVEY: 28,672 per pre-compaction sample,
-# 92,160 per compacted sample) are reported alongside for the MLP kernels.
+# MFMA flops per unit (SURVEY: 28,672 per pre-compaction sample, 92,160 per compacted sample), split over the
+# kernels that carry them (W = 64, DIN = 32):
+#   inference          : density fwd 6,144 + grad-SDF backward 6,144 + rgb fwd 16,384 = 28,672
+#   mlp_train_rgb      : density fwd 6,144 + grad SDF 6,144 + rgb hidden fwd 14,336 + rgb dL/dinput 16,384 = 43,008
+#   mlp_train_density  : density dL/dinput 6,144 + second-order front W0 u 4,096 = 10,240 (+ its recomputed
+#                        density forward, not algorithmic)
+#   weight gradients   : every layer's dW, first and second order = 28,672 (inside the training kernels, or k_wgrad)
 def kernel_table(levels):
     g = 8 * levels * 4
     return {
@@ -89,13 +111,10 @@ def kernel_table(levels):
         "inference": (3, 28 + g + 32, 28672),
         "loss_alpha": (4, 60, 0),
         "train_encode": (8, 28 + g, 0),
-        # the two training-MLP kernels (fwd recompute + 1st / 2nd-order backward; SURVEY: 92,160 - 28,672 flops per
-        # compacted sample between them): dL/dout read by the colour kernel, the output-side operands by the density one
-        "mlp_train_rgb": (9, 32, 0),
-        "mlp_train_density": (10, 32, 0),
+        "mlp_train_rgb": (9, 32, 43008),
+        "mlp_train_density": (10, 32, 10240),
         "grid_scatter": (7, 2 * g, 0),
     }
-MFMA_PEAK_TFLOPS = 2500.0  # MI355X dense fp16 (MI355X_MICROARCH.md)
 
 
 def kernel_rooflines(tb, levels, iters=9):
@@ -115,65 +134,157 @@ def kernel_rooflines(tb, levels, iters=9):
     return out
 
 
-def main():
-    args = parse()
-    import numpy as np
-    import torch
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+def step_roofline(d, levels, n_params, ms_per_step, steps):
+    """Whole-step roofline: B_step = 40 R + 596 Npre + 1496 Nc + 48 P + B_occ,
+    with the gather terms at L_active levels, from the counters of the timed steps (this rank). B_occ = (96 + 32 L)
+    bytes per occupancy sample + a 32 MB grid pass per update. F_step = 28,672 Npre + 92,160 Nc."""
+    g = 8 * levels * 4
+    R, npre, nc = d["rays"] / steps, d["pre"] / steps, d["train"] / steps
+    occ = (d["occ_samples"] * (96 + g) + d["occ_updates"] * 32e6) / steps
+    b = 40 * R + (28 + 28 + g + 32 + 60) * npre + (60 + 28 + g + 32 + 32 + 2 * g) * nc + 48 * n_params + occ
+    f = 28672 * npre + 92160 * nc
+    t = ms_per_step * 1e-3
+    return {"bound": "hbm", "achieved": round(b / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(b / t / 1e9 / HBM_PEAK_GBS, 4), "bytes_per_step": round(b), "flops_per_step": round(f),
+            "mfma_tflops": round(f / t / 1e12, 1), "mfma_frac": round(f / t / 1e12 / MFMA_PEAK_TFLOPS, 4),
+            "per_step": {"rays": round(R), "pre_samples": round(npre), "train_samples": round(nc),
+                         "occ_samples": round(d["occ_samples"] / steps), "params": n_params}}
+
+
+def work_counters(st):
+    return {"rays": st["rays_total"], "pre": st["pre_samples_total"], "occ_samples": st["occ_samples_total"],
+            "occ_updates": st["occ_updates"]}
+
+
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """One rank per GPU as fresh child processes (this process has not touched the GPU)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}", "--master-addr=127.0.0.1",
+           f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+class Group:
+    """The gloo control plane of the ranks (RCCL communicators are created inside each C++ Testbed)."""
+
+    def __init__(self, rank, world):
+        self.rank, self.world = rank, world
+        if world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo", init_method="env://")
+
+    def barrier(self):
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    def max(self, v):
+        if self.world == 1:
+            return v
+        import torch
         import torch.distributed as dist
-        dist.init_process_group("gloo", init_method="env://")
-    torch.cuda.set_device(local)
-    from neus2_amd import pyngp, scenes
-    sc = scenes.sphere_scene(args.views, args.width, args.height, principal=(823.2 / 1600, 619.1 / 1200))
-    tb = pyngp.Testbed(pyngp.TestbedMode.Nerf, device=local)
-    tb.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
-    tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=args.batch,
-                                fixed_rays_per_batch=args.rays)
-    if world > 1:
+        t = torch.tensor([v], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def attach(self, tb):
+        """Data-parallel Testbed: a fresh RCCL unique id from rank 0, broadcast over gloo."""
+        if self.world == 1:
+            return
         import torch.distributed as dist
-        obj = [pyngp.nccl_unique_id() if rank == 0 else None]
+        from neus2_amd import pyngp
+        obj = [pyngp.nccl_unique_id() if self.rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
-        tb.init_data_parallel(rank, world, obj[0])
+        tb.init_data_parallel(self.rank, self.world, obj[0])
+
+    def close(self):
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+
+
+def make_testbed(sc, grp, device, args, cfg=None, fixed_rays=True):
+    from neus2_amd import pyngp
+    tb = pyngp.Testbed(pyngp.TestbedMode.Nerf, device=device)
+    tb.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
+    kw = dict(batch_size=args.batch, fixed_rays_per_batch=args.rays) if fixed_rays else {}
+    if cfg is None:
+        tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), **kw)
+    else:
+        tb.reload_network_from_json(cfg, **kw)
+    grp.attach(tb)
+    return tb
+
+
+def timed_steps(tb, grp, warmup, steps, batch):
+    """W untimed warm-up steps, then exactly K steps bracketed by a barrier + device synchronisation on both
+    sides; the max over ranks. Returns (seconds, work counters of the timed steps)."""
+    import torch
 
     def barrier():
         tb.synchronize()
         torch.cuda.synchronize()
-        if world > 1:
-            import torch.distributed as dist
-            dist.barrier()
+        grp.barrier()
 
-    t0 = time.time()
-    tb.train_steps(args.warmup)
+    tb.train_steps(warmup)
     barrier()
-    warm_s = time.time() - t0
-    # timed region
-    tb.set_profiling(False)
-    barrier()
-    trained0 = tb.stats()["trained_samples_total"]
+    st0 = tb.stats()
     t1 = time.perf_counter()
-    tb.train_steps(args.steps)
+    tb.train_steps(steps)
     barrier()
-    elapsed = time.perf_counter() - t1
-    if world > 1:
-        import torch.distributed as dist
-        tt = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-    st = tb.stats()
+    elapsed = grp.max(time.perf_counter() - t1)
+    st1 = tb.stats()
+    w0, w1 = work_counters(st0), work_counters(st1)
+    d = {k: w1[k] - w0[k] for k in w0}
+    d["train"] = steps * batch
+    d["trained_real"] = st1["trained_samples_total"] - st0["trained_samples_total"]
+    return elapsed, d, st1
+
+
+def main():
+    args = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(world_env or "1")
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    grp = Group(rank, world)
+    torch.cuda.set_device(local)
+    from neus2_amd import scenes
+    sc = scenes.sphere_scene(args.views, args.width, args.height, principal=(823.2 / 1600, 619.1 / 1200))
+    tb = make_testbed(sc, grp, local, args)
+    t0 = time.time()
+    tb.train_steps(args.prepare)
+    tb.synchronize()
+    prepare_s = time.time() - t0
+    tb.set_profiling(False)
+    elapsed, d, st = timed_steps(tb, grp, args.warmup, args.steps, args.batch)
     batch = args.batch
     # every step trains on Nc = batch samples per GPU (the reference's m_training_batch_size; a short compaction
     # is rollover-padded, fill_rollover_and_rescale); the non-rollover share is reported next to it
-    samples = batch * world * args.steps
-    value = samples / elapsed
-    real = (st["trained_samples_total"] - trained0) / max(1, batch * args.steps)
-    levels = min(st["valid_level"] + 1, tb.layout()["n_levels"])
+    value = batch * world * args.steps / elapsed
+    ms_step = elapsed / args.steps * 1e3
+    lay = tb.layout()
+    levels = min(st["valid_level"] + 1, lay["n_levels"])
     # per-kernel timing after the timed region, on its final state (hipEvents on the testbed stream)
     kern = kernel_rooflines(tb, levels)
     dom = max(kern, key=lambda k: kern[k]["ms"])
-    d = kern[dom]
+    dk = kern[dom]
+    mlp = ("mlp_train_rgb", "mlp_train_density")
+    mlp_ms = sum(kern[k]["ms"] for k in mlp)
+    tr = traffic_table()
     out = {
         "metric": "training samples/sec (compacted NeuS2 training samples, DTU-scan24-shaped synthetic, base.json)",
         "value": value,
@@ -181,76 +292,91 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
+        "ms_per_step": ms_step,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "fp16 MFMA (fp32 accumulate) / fp32 optimizer",
         "data": "synthetic (analytic sphere, 49 x 1600x1200 RGBA8 views; DTU scan24 unavailable offline)",
-        "config": {"workload": "NeuS2 train step, Config S, base.json L=14 T=2^19 W=64, Nc=2^18/GPU, R=2^18/GPU fixed",
-                   "global_batch": batch * world, "rays_per_gpu": args.rays, "parallelism": f"dp{world}"},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": d["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": d["frac"], "traffic": measured_traffic(dom, levels), "bytes_per_launch": d["bytes"],
-                     "units_per_launch": d["units"], "launch_ms": d["ms"], "levels_active": levels},
+        "config": {"workload": "NeuS2 train step, Config S, base.json L=14 T=2^19 W=64, Nc=2^18/GPU, R=2^18/GPU fixed, "
+                               f"all {levels} levels active (network trained {args.prepare} steps before the warm-up)",
+                   "global_batch": batch * world, "rays_per_gpu": args.rays, "parallelism": f"dp{world}",
+                   "prepare_steps": args.prepare, "levels_active": levels},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": dk["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": dk["frac"], "traffic": measured_traffic(dom, levels), "bytes_per_launch": dk["bytes"],
+                     "units_per_launch": dk["units"], "launch_ms": dk["ms"], "levels_active": levels,
+                     "traffic_source": tr.get("_source")},
+        # the whole step against the HBM roofline and its MFMA rate
+        "roofline_step": step_roofline(d, levels, lay["n_params"], ms_step, args.steps),
+        # the training MLP kernels (fwd recompute + 1st / 2nd-order backward + weight gradients) against the MFMA peak
+        "mfma_mlp_train": {"flops_per_sample": 43008 + 10240 + 28672, "ms": round(mlp_ms, 4),
+                           "tflops": round((43008 + 10240 + 28672) * batch / (mlp_ms * 1e-3) / 1e12, 1),
+                           "frac": round((43008 + 10240 + 28672) * batch / (mlp_ms * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS, 4)},
         # memory-side line traffic (PMC, profiles/traffic.json) over the same launch: the hashed levels' 4-B corner
         # gathers each move a 128-B line from the Infinity Cache, so this, not the algorithmic rate, is what binds
-        "line_traffic": line_traffic(measured_traffic(dom, levels), d["ms"], d["bytes"]),
-        "non_rollover_fraction": round(real, 4),
+        "line_traffic": line_traffic(measured_traffic(dom, levels), dk["ms"], dk["bytes"]),
+        "non_rollover_fraction": round(d["trained_real"] / max(1, batch * args.steps), 4),
         "kernels": kern,
         "loss": st["ray_loss"],
-        "warmup_s": warm_s,
+        "prepare_s": round(prepare_s, 3),
     }
+    del tb
+    if args.early:
+        out["early_steps"] = early_leg(sc, grp, local, args)
     if world == 1 and args.l16:
-        out["levels16"] = l16_leg(sc, args)
-    if world == 1 and args.psnr_steps > 0:
-        del tb
-        out["psnr"], tb2 = psnr_leg(sc, args.psnr_steps)
-        if args.mc_res > 0:
+        out["levels16"] = l16_leg(sc, grp, local, args)
+    if args.psnr_steps > 0:
+        out["psnr"], tb2 = psnr_leg(sc, grp, local, args)
+        if world == 1 and args.mc_res > 0:
             out["marching_cubes"] = marching_cubes_leg(tb2, args.mc_res)
         del tb2
     if rank == 0 and args.cpu_baseline and world == 1:
-        out["cpu_baseline"] = cpu_baseline(sc, args.cpu_steps)
+        out["cpu_baseline"] = cpu_baseline(sc, args)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
-        import torch.distributed as dist
-        dist.destroy_process_group()
+    grp.close()
 
 
-def l16_leg(sc, args):
+def early_leg(sc, grp, device, args):
+    """The same step on a fresh network: W warm-up + K timed steps from step 0 (the first progressive levels,
+    occupancy updates every step): the driver-shaped transient."""
+    tb = make_testbed(sc, grp, device, args)
+    elapsed, d, st = timed_steps(tb, grp, args.warmup, args.steps, args.batch)
+    levels = min(st["valid_level"] + 1, tb.layout()["n_levels"])
+    del tb
+    return {"value": args.batch * grp.world * args.steps / elapsed, "unit": "samples/s", "ms_per_step": elapsed / args.steps * 1e3,
+            "steps": f"{args.warmup}..{args.warmup + args.steps}", "levels_active_at_end": levels}
+
+
+def l16_leg(sc, grp, device, args):
     """The timed step of the main measurement with a 16-level hash grid (base.json otherwise): same data, batch,
-    rays and warmup / steps, wall clock between synchronised points."""
-    from neus2_amd import config, pyngp
+    rays, preparation and warmup / steps."""
+    from neus2_amd import config
     cfg = config.load_json(os.path.join(ROOT, "configs", "nerf", "base.json"))
     cfg["encoding"]["n_levels"] = 16
-    tb = pyngp.Testbed(pyngp.TestbedMode.Nerf)
-    tb.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
-    tb.reload_network_from_json(cfg, batch_size=args.batch, fixed_rays_per_batch=args.rays)
-    tb.train_steps(args.warmup)
-    tb.synchronize()
-    t = time.perf_counter()
-    tb.train_steps(args.steps)
-    tb.synchronize()
-    dt = time.perf_counter() - t
-    st = tb.stats()
+    tb = make_testbed(sc, grp, device, args, cfg=cfg)
+    tb.train_steps(args.prepare)
+    elapsed, d, st = timed_steps(tb, grp, args.warmup, args.steps, args.batch)
     levels = min(st["valid_level"] + 1, 16)
+    ms_step = elapsed / args.steps * 1e3
     inf_ms, inf_units = tb.time_kernel(3, 9)
     g = 8 * levels * 4
+    n_params = tb.layout()["n_params"]
     del tb
-    return {"value": args.batch * args.steps / dt, "unit": "samples/s", "ms_per_step": dt / args.steps * 1e3,
-            "levels_active": levels,
+    return {"value": args.batch * grp.world * args.steps / elapsed, "unit": "samples/s", "ms_per_step": ms_step,
+            "levels_active": levels, "roofline_step": step_roofline(d, levels, n_params, ms_step, args.steps),
             "inference": {"ms": round(inf_ms, 4), "units": inf_units,
                           "achieved_GBs": round((28 + g + 32) * inf_units / (inf_ms * 1e-3) / 1e9, 1)}}
 
 
-def psnr_leg(sc, n_steps):
+def psnr_leg(sc, grp, device, args):
     """PSNR@n_steps (BASELINE.json metric, second half) with the reference's training (adaptive rays per
-    batch, Nc = 2^18) and evaluation protocol (render_utils.py:252-359: view 0, spp 8, black background,
-    pixel centres, min transmittance 1e-4, EMA weights); scripts/psnr_run.py is the standalone version."""
+    batch, Nc = 2^18 per GPU) and evaluation protocol (render_utils.py:252-359: view 0, spp 8, black background,
+    pixel centres, min transmittance 1e-4, EMA weights); at N > 1 every rank trains its ray shard (the global batch
+    is N x 2^18) and rank 0 renders. scripts/psnr_run.py is the standalone version."""
     from neus2_amd import pyngp
-    tb = pyngp.Testbed(pyngp.TestbedMode.Nerf)
-    tb.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
-    tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"))
+    n_steps = args.psnr_steps
+    tb = make_testbed(sc, grp, device, args, fixed_rays=False)
     t0 = time.perf_counter()
     done = 0
     while done < n_steps:
@@ -258,19 +384,23 @@ def psnr_leg(sc, n_steps):
         tb.train_steps(k)
         done += k
         tb.synchronize()  # also a progress point for long runs
-    train_s = time.perf_counter() - t0
-    tb.background_color = [0.0, 0.0, 0.0, 0.0]
-    tb.snap_to_pixel_centers = True
-    tb.nerf.rendering_min_transmittance = 1e-4
-    tb.set_camera_to_training_view(0)
-    gt = sc["images"][0]
-    t1 = time.perf_counter()
-    img = tb.render(gt.shape[1], gt.shape[0], spp=8)
-    render_s = time.perf_counter() - t1
-    psnr, _ = pyngp.eval_psnr(img, gt)
-    out = {"value": round(float(psnr), 3), "unit": "dB", "steps": n_steps, "train_wall_s": round(train_s, 2),
-           "render_s": round(render_s, 3), "protocol": "view 0, spp 8, black bg, snap_to_pixel_centers, min_T 1e-4, EMA weights",
-           "training": "reference schedule: adaptive rays/batch, Nc=2^18, base.json"}
+    grp.barrier()
+    train_s = grp.max(time.perf_counter() - t0)
+    out = {"unit": "dB", "steps": n_steps, "train_wall_s": round(train_s, 2), "n_gpus": grp.world,
+           "protocol": "view 0, spp 8, black bg, snap_to_pixel_centers, min_T 1e-4, EMA weights",
+           "training": f"reference schedule: adaptive rays/batch, Nc=2^18 per GPU, base.json, dp{grp.world}"}
+    if grp.rank == 0:
+        tb.background_color = [0.0, 0.0, 0.0, 0.0]
+        tb.snap_to_pixel_centers = True
+        tb.nerf.rendering_min_transmittance = 1e-4
+        tb.set_camera_to_training_view(0)
+        gt = sc["images"][0]
+        t1 = time.perf_counter()
+        img = tb.render(gt.shape[1], gt.shape[0], spp=8)
+        out["render_s"] = round(time.perf_counter() - t1, 3)
+        psnr, _ = pyngp.eval_psnr(img, gt)
+        out["value"] = round(float(psnr), 3)
+    grp.barrier()
     return out, tb
 
 
@@ -296,26 +426,7 @@ def marching_cubes_leg(tb, res=1024, reps=3):
             "achieved_GBs": round(n * (448 + 4 + 32) / best / 1e9, 1)}
 
 
-def cpu_baseline(sc, n_steps):
-    """The CPU oracle's train step (oracle/cpu_step.py) on the same Config S data at R = Nc = 4096
-    (BASELINE.md §2 'CS-small'), all host threads via OpenMP."""
-    import numpy as np
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as O
-    from cpu_step import CpuTrainer
-    from neus2_amd.pyngp import geometric_init_weights
-    cfg = O.make_cfg()
-    ds = O.Dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"])
-    p = O.init_params(cfg, geo=False)
-    geo = geometric_init_weights(14, 64)
-    p[: geo.size] = geo
-    tr = CpuTrainer(cfg, ds, p, batch=4096, rays_per_batch=4096, fixed_rays=True)
-    tr.step()  # step 0 includes the 2M-sample occupancy bootstrap; not timed
-    t = time.perf_counter()
-    for _ in range(n_steps):
-        tr.step()
-    dt = time.perf_counter() - t
-    import platform
+def host_cpu():
     cpu = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -325,9 +436,59 @@ def cpu_baseline(sc, n_steps):
                     break
     except OSError:
         pass
-    return {"value": 4096 * n_steps / dt, "unit": "samples/s", "cores": O.num_threads(), "kind": "port",
-            "sample": f"{n_steps} CPU-oracle train steps (incl. occupancy updates at cadence), Config S, R=Nc=4096; cpu={cpu}",
-            "ms_per_step": dt / n_steps * 1e3, "host": platform.node()}
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = None
+    return cpu, os.cpu_count(), aff
+
+
+def cpu_baseline(sc, args):
+    """The CPU oracle's train step (oracle/cpu_step.py, the reference's algorithm restated in C++ with OpenMP; the
+    reference has no CPU path) beside the GPU run:
+      * Config S at R = Nc = 4096 ('CS-small'), --cpu-steps steps after an untimed first step;
+      * config 1 in full: the 1-view 64x64 sphere, 1-level grid, width-16 MLPs, R = Nc = 4096, 100 steps from step 0
+        (occupancy updates at the reference cadence included).
+    Threads: OpenMP's count in this process (OMP_NUM_THREADS when set: the GPU pool sets it to the lease's CPU share)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from cpu_step import CpuTrainer
+    from neus2_amd import scenes
+    from neus2_amd.pyngp import geometric_init_weights
+    cfg = O.make_cfg()
+    ds = O.Dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"])
+    p = O.init_params(cfg, geo=False)
+    geo = geometric_init_weights(14, 64)
+    p[: geo.size] = geo
+    tr = CpuTrainer(cfg, ds, p, batch=4096, rays_per_batch=4096, fixed_rays=True)
+    tr.step()  # step 0 includes the 2M-sample occupancy bootstrap; not timed
+    t = time.perf_counter()
+    for _ in range(args.cpu_steps):
+        tr.step()
+    dt = time.perf_counter() - t
+    cpu, nproc, aff = host_cpu()
+    out = {"value": 4096 * args.cpu_steps / dt, "unit": "samples/s", "cores": O.num_threads(), "kind": "port",
+           "sample": f"{args.cpu_steps} CPU-oracle train steps (incl. occupancy updates at cadence), Config S, R=Nc=4096",
+           "ms_per_step": round(dt / args.cpu_steps * 1e3, 1),
+           "host": {"cpu": cpu, "nproc": nproc, "affinity_cpus": aff, "omp_threads": O.num_threads(),
+                    "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}}
+    if args.cpu_config1_steps > 0:
+        c1 = scenes.config1_scene()
+        cfg1 = O.make_cfg(n_levels=1, width=16, per_level_scale=2.0)
+        ds1 = O.Dataset(c1["images"], c1["focal"], c1["principal"], c1["xforms"])
+        p1 = O.init_params(cfg1, geo=False)
+        g1 = geometric_init_weights(1, 16)
+        p1[: g1.size] = g1
+        tr1 = CpuTrainer(cfg1, ds1, p1, batch=4096, rays_per_batch=4096, fixed_rays=True)
+        t = time.perf_counter()
+        for _ in range(args.cpu_config1_steps):
+            tr1.step()
+        dt1 = time.perf_counter() - t
+        out["config1"] = {"value": 4096 * args.cpu_config1_steps / dt1, "unit": "samples/s", "steps": args.cpu_config1_steps,
+                          "ms_per_step": round(dt1 / args.cpu_config1_steps * 1e3, 1),
+                          "sample": "config 1 in full: 1 view 64x64, L=1, W=16, R=Nc=4096, steps 0..99 incl. occupancy updates",
+                          "last_loss": round(float(tr1.last["loss"]), 6)}
+    return out
 
 
 if __name__ == "__main__":

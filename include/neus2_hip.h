@@ -116,6 +116,12 @@ typedef struct NeusTrainStats {
 	uint32_t kept_ray_extent;                 /* 1 + the last ray slot kept by the last step's sampler */
 	uint32_t nonfinite_loss;                  /* a logged loss sum was NaN / Inf (all-reduced, so every rank sees it) */
 	uint32_t training_aborted;                /* zero compacted samples (testbed_nerf.cu:3542-3548) or a non-finite loss */
+	/* work since the network was (re)loaded, this rank (the whole-step roofline of bench.py counts bytes from them) */
+	uint64_t pre_samples_total;               /* pre-compaction samples evaluated (sum of the kept samples per step) */
+	uint64_t rays_total;                      /* rays marched (sum of rays_per_batch) */
+	uint64_t occ_samples_total;               /* occupancy-grid samples evaluated by this rank (its shard of each update) */
+	uint32_t occ_updates;                     /* occupancy-grid updates (update_density_grid_nerf calls) */
+	uint32_t reserved_;
 } NeusTrainStats;
 
 /* Testbed::render_to_cpu (python_api.cu:123-169) after set_camera_to_training_view (testbed.cu:264-270). */
@@ -192,6 +198,20 @@ int neus_testbed_get_mesh(NeusTestbed* tb, float* verts, uint32_t* tris);
 int neus_testbed_mesh_vertex_colors(NeusTestbed* tb, float* rgb);
 /* The marching-cubes case table the kernels use: 256 rows x 19 int8 (edge triples, -1 terminated). */
 int neus_mc_table(int8_t* out);
+/* Training-image preparation of ngp::load_nerf (host side, in the reference's order), in place on w x h RGBA8:
+ *   alpha_rgba (nullable, w x h RGBA8: the frame's `<file_path>.alpha.<ext>` image): alpha := uint8(255 *
+ *     srgb_to_linear(red / 255)) (nerf_loader.cu:550-569);
+ *   mask_rgba (nullable, w x h RGBA8: the frame's `dynamic_mask_<basename>.png`): pixels whose mask red is nonzero
+ *     become the hot-pink key 0x00FF00FF, which read_rgba turns into a masked-away (negative) target
+ *     (nerf_loader.cu:571-590, common_device.cuh:635-667);
+ *   flags NEUS_IMAGE_WHITE_TRANSPARENT / NEUS_IMAGE_BLACK_TRANSPARENT (transforms.json `white_transparent` /
+ *     `black_transparent`): alpha := 0 on pure white / pure black rgb, then the mask key is re-applied
+ *     (convert_rgba32, nerf_loader.cu:59-81, applied by NerfDataset::set_training_image).
+ * Returns in *mask_color the key the image carries (0x00FF00FF with a mask, else 0). */
+#define NEUS_IMAGE_WHITE_TRANSPARENT 1u
+#define NEUS_IMAGE_BLACK_TRANSPARENT 2u
+int neus_prepare_image_rgba8(uint8_t* rgba, uint32_t width, uint32_t height, const uint8_t* alpha_rgba, const uint8_t* mask_rgba,
+                             uint32_t flags, uint32_t* mask_color);
 int neus_testbed_get_rng(NeusTestbed* tb, uint64_t* state_inc /*4: rng, density_grid_rng*/);
 /* Dynamic scenes. Testbed::training_network_next_frame (testbed.cu:2001-2082) with load_nerf(frame)
  * (testbed_nerf.cu:3096-3113): the next frame's images/cameras (same aabb), the frame's local movement folded
@@ -288,6 +308,19 @@ int neus_testbed_kernel_times(NeusTestbed* tb, float* ms_out /* NEUS_N_PHASES + 
 /* ------------------------------------------------------------------ data parallel (RCCL over xGMI) */
 int neus_nccl_unique_id(uint8_t* out /* 128 bytes */);
 int neus_testbed_init_data_parallel(NeusTestbed* tb, int rank, int world, const uint8_t* unique_id /* 128 bytes */);
+/* As neus_testbed_init_data_parallel; flags bit 0 (NEUS_DP_FORCE_COLLECTIVES): create the RCCL communicator and issue
+ * every collective of the step even at world 1 (a one-rank all-reduce is the identity: tests run the RCCL path with it). */
+#define NEUS_DP_FORCE_COLLECTIVES 1
+int neus_testbed_init_data_parallel_ex(NeusTestbed* tb, int rank, int world, const uint8_t* unique_id, uint32_t flags);
+typedef struct NeusDataParallelInfo {
+	uint32_t rank, world;
+	uint32_t has_communicator;       /* an RCCL communicator exists (world > 1, or forced) */
+	uint32_t local_group;            /* in-process group (host-staged collectives) */
+	uint64_t collective_calls;       /* all-reduce calls issued since init */
+	uint64_t allreduce_bytes;        /* bytes all-reduced since init (per rank, payload) */
+	uint64_t last_step_allreduce_bytes;
+} NeusDataParallelInfo;
+int neus_testbed_data_parallel_info(NeusTestbed* tb, NeusDataParallelInfo* out);
 /* In-process ranks: `world` testbeds driven from `world` host threads exchange through host staging buffers
  * (same step and collectives as the RCCL path: sharded occupancy update + max all-reduce, gradient / counter /
  * loss / DeltaNetwork sum all-reduces). For several ranks on one device (tests); collectives block until every

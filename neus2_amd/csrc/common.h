@@ -163,7 +163,11 @@ struct StepState {
 	unsigned long long trained_total; // real (non-rollover) training samples since step 0, this rank: sum of min(Nc measured, batch)
 	uint32_t march_total;             // samples requested by the first march pass's rays
 	uint32_t kept_extent;             // this step: 1 + the last kept ray slot (0 if none)
+	// work counters since step 0 (this rank), for the whole-step roofline (bench.py roofline_step)
+	unsigned long long pre_total;     // pre-compaction samples evaluated: sum of n_kept
+	unsigned long long rays_total;    // rays marched: sum of rays_per_batch
+	unsigned long long pad_[6];
 };
-static_assert(sizeof(StepState) == 64, "StepState is one 64-B record");
+static_assert(sizeof(StepState) == 128, "StepState is one 128-B record");
 
 } // namespace neus

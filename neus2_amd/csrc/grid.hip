@@ -390,7 +390,44 @@ __global__ void __launch_bounds__(256) k_enc_ddLdoutput(uint32_t n, uint32_t ld,
 	}
 }
 
+// Encoding output layouts of the operator module (tcnn GPUMatrix layouts): paired [L][n] half2 (this build's kernels)
+// <-> AoS [n][2L] (column-major: the cpp::Module view, cpp_api.cu:58-70) or SoA [2L][n] (GridEncoding's preferred
+// layout, grid.h:2357-2359). One thread per (sample, level).
+__global__ void __launch_bounds__(256) k_enc_relayout(uint32_t n, uint32_t L, const uint32_t* __restrict__ paired, half_t* __restrict__ dst,
+                                                      uint32_t layout, uint32_t to_paired, uint32_t* __restrict__ paired_out, const half_t* __restrict__ src) {
+	const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+	if (t >= n * L) return;
+	const uint32_t l = t / n, i = t % n;
+	const size_t a0 = layout == ENC_LAYOUT_AOS ? (size_t)i * 2 * L + 2 * l : (size_t)(2 * l) * n + i;
+	const size_t a1 = layout == ENC_LAYOUT_AOS ? a0 + 1 : a0 + n;
+	if (to_paired) {
+		h2 v = {src[a0], src[a1]};
+		paired_out[(size_t)l * n + i] = *(const uint32_t*)&v;
+	} else {
+		const uint32_t u = paired[(size_t)l * n + i];
+		const h2 v = *(const h2*)&u;
+		dst[a0] = v[0];
+		dst[a1] = v[1];
+	}
+}
+// fp32 parameter gradients -> the caller's fp16 buffer (tcnn's param-precision gradients, trainer.h:72-109): Overwrite
+// stores the rounded value, Accumulate adds into the fp16 value in fp32 and rounds once
+__global__ void __launch_bounds__(256) k_grad_to_half(uint32_t n, const float* __restrict__ g, half_t* __restrict__ out, uint32_t accumulate) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	out[i] = (half_t)(accumulate ? (float)out[i] + g[i] : g[i]);
+}
+
 // ---------------------------------------------------------------- host launchers
+void launch_enc_to_layout(hipStream_t s, uint32_t n, uint32_t L, const uint32_t* paired, half_t* dst, uint32_t layout) {
+	if (n) k_enc_relayout<<<(n * L + 255) / 256, 256, 0, s>>>(n, L, paired, dst, layout, 0u, nullptr, nullptr);
+}
+void launch_enc_from_layout(hipStream_t s, uint32_t n, uint32_t L, const half_t* src, uint32_t layout, uint32_t* paired) {
+	if (n) k_enc_relayout<<<(n * L + 255) / 256, 256, 0, s>>>(n, L, nullptr, nullptr, layout, 1u, paired, src);
+}
+void launch_grad_to_half(hipStream_t s, uint32_t n, const float* g, half_t* out, bool accumulate) {
+	if (n) k_grad_to_half<<<(n + 255) / 256, 256, 0, s>>>(n, g, out, accumulate ? 1u : 0u);
+}
 void launch_enc_input_grad(hipStream_t s, uint32_t n, uint32_t ld, uint32_t L, const half_t* dLdy, const float* dydx, float* dLdx, uint32_t stride) {
 	if (n) k_enc_input_grad<<<(n + 255) / 256, 256, 0, s>>>(n, ld, L, (const uint32_t*)dLdy, dydx, dLdx, stride);
 }

@@ -268,6 +268,11 @@ void launch_add_f32(hipStream_t s, uint32_t n, const float* src, float* dst);
 // operator-module encoding helpers (grid.hip)
 void launch_enc_input_grad(hipStream_t s, uint32_t n, uint32_t ld, uint32_t L, const half_t* dLdy, const float* dydx, float* dLdx, uint32_t stride);
 void launch_enc_ddLdoutput(hipStream_t s, uint32_t n, uint32_t ld, uint32_t L, const float* ddx, const float* dydx, half_t* out, float4* v4);
+// encoding output layouts of the operator module: paired [L][n] half2 <-> AoS [n][2L] / SoA [2L][n] fp16
+enum : uint32_t { ENC_LAYOUT_AOS = 0, ENC_LAYOUT_SOA = 1, ENC_LAYOUT_PAIRED = 2 };
+void launch_enc_to_layout(hipStream_t s, uint32_t n, uint32_t L, const uint32_t* paired, half_t* dst, uint32_t layout);
+void launch_enc_from_layout(hipStream_t s, uint32_t n, uint32_t L, const half_t* src, uint32_t layout, uint32_t* paired);
+void launch_grad_to_half(hipStream_t s, uint32_t n, const float* g, half_t* out, bool accumulate);
 void launch_transpose_w(hipStream_t s, const TransposeJobs& jobs);
 struct DinPerm { int32_t p[48]; uint32_t din, W; };
 void launch_permute_din(hipStream_t s, const half_t* d0, half_t* d0p, half_t* d0Tp, const DinPerm& perm);

@@ -1051,6 +1051,8 @@ __global__ void k_step_counters(StepState* st, uint32_t target_batch, uint32_t m
 	if (threadIdx.x != 0 || blockIdx.x != 0) return;
 	const uint32_t R = st->rays_per_batch;
 	st->n_rays_total += R * world;  // n_rays_total
+	st->pre_total += st->n_kept;
+	st->rays_total += R;
 	// next step's first march pass: the slots up to this step's kept extent plus a margin (all slots when every
 	// ray with samples fitted under this step's cap)
 	const bool fit = st->numsteps_counter <= st->max_inference;

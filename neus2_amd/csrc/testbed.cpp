@@ -113,14 +113,20 @@ struct NeusLocalGroup {
 	std::mutex mu;
 	std::condition_variable cv;
 	uint32_t arrived = 0, generation = 0;
+	bool failed = false;  // a rank timed out: every later collective fails fast instead of pairing the wrong ranks
 	std::vector<std::vector<uint8_t>> stage;
 	explicit NeusLocalGroup(uint32_t w) : world(w), stage(w) {}
 	void barrier() {
 		std::unique_lock<std::mutex> lk(mu);
+		if (failed) throw std::runtime_error("local group: a previous collective failed (the group is poisoned)");
 		const uint32_t gen = generation;
 		if (++arrived == world) { arrived = 0; ++generation; cv.notify_all(); return; }
-		if (!cv.wait_for(lk, std::chrono::seconds(120), [&] { return generation != gen; }))
+		if (!cv.wait_for(lk, std::chrono::seconds(120), [&] { return generation != gen || failed; }) || failed) {
+			if (generation == gen) --arrived;  // this rank's arrival is withdrawn
+			failed = true;
+			cv.notify_all();
 			throw std::runtime_error("local group: barrier timeout (a rank did not reach the collective)");
+		}
 	}
 	// in-place all-reduce of n elements of T on the device, on `s` (host-synchronous)
 	template <class T> void allreduce(uint32_t rank, T* dev, size_t n, Op op, hipStream_t s) {
@@ -199,6 +205,8 @@ struct NeusTestbed {
 	Dev<uint32_t> bf_lin;   // mip-0 occupancy in (x, y, z/32) word order for the constant-step march
 	Dev<PcgJump> pcg_tab;   // pcg32 jump-ahead table (common.h PcgJumpTable)
 	uint32_t density_grid_ema_step = 0;
+	uint64_t occ_samples = 0;  // occupancy-grid samples this rank evaluated since the network was loaded
+	uint32_t occ_updates = 0;
 	// step workspace
 	uint32_t batch = 0, max_samples = 0;
 	Dev<float> rays, startt, coords, coords_c, loss, ek, mask, loss_sum;
@@ -245,12 +253,15 @@ struct NeusTestbed {
 	float loss_scalar_ema = 0.f, last_loss = 0.f, ek_loss = 0.f, mask_loss = 0.f, ray_loss = 0.f;
 	uint32_t last_rays_with_samples = 0;
 	bool loss_ema_init = false;
-	float* pinned = nullptr;  // [0..3]: loss sum, ek sum, mask sum, grid mean ; [4..]: StepState copy
+	float* pinned = nullptr;  // [0..3]: loss sum, ek sum, mask sum, grid mean; [32..47] render / mesh counts; [64..]: StepState copy
 	bool loss_pending = false;
 	// data parallel: RCCL communicator (production) or an in-process group
 	ncclComm_t comm = nullptr;
 	NeusLocalGroup* group = nullptr;
 	uint32_t rank = 0, world = 1;
+	bool force_coll = false;  // issue the collectives at world 1 too (a forced one-rank communicator, tests)
+	uint64_t coll_calls = 0, coll_bytes = 0, coll_bytes_step = 0;
+	bool coll_on() const { return world > 1 || force_coll; }
 	// profiling
 	bool profiling = false;
 	static constexpr int N_PHASES = NEUS_N_PHASES;
@@ -272,7 +283,7 @@ struct NeusTestbed {
 		HIP_CHECK(hipStreamCreateWithFlags(&aux_stream, hipStreamNonBlocking));
 		HIP_CHECK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
 		HIP_CHECK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
-		HIP_CHECK(hipHostMalloc((void**)&pinned, 64 * sizeof(float)));
+		HIP_CHECK(hipHostMalloc((void**)&pinned, 128 * sizeof(float)));
 		for (auto& set : ev)
 			for (auto& e : set) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
 		for (auto& e : ev_done) HIP_CHECK(hipEventCreate(&e));
@@ -451,6 +462,7 @@ struct NeusTestbed {
 		density_grid_rng = make_pcg32(rng.next_uint());
 		(void)rng.next_uint();  // tv_loss_rng
 		training_step = 0; adam_step = 0; lr_factor = 1.f; density_grid_ema_step = 0; enc_step = 0;
+		occ_samples = 0; occ_updates = 0;
 		loss_ema_init = false; loss_scalar_ema = last_loss = ek_loss = mask_loss = 0.f; loss_pending = false;
 		nonfinite = aborted = false;
 		// forward + backward workspace of one training batch
@@ -765,13 +777,15 @@ struct NeusTestbed {
 	void coll_begin() { if (comm) NCCL_CHECK(ncclGroupStart()); }
 	void coll_end() { if (comm) NCCL_CHECK(ncclGroupEnd()); }
 	void allreduce_f32(float* p, size_t n, bool max_op = false) {
-		if (world == 1) return;
+		if (!coll_on() || n == 0) return;
+		++coll_calls; coll_bytes += n * 4; coll_bytes_step += n * 4;
 		if (comm) NCCL_CHECK(ncclAllReduce(p, p, n, ncclFloat32, max_op ? ncclMax : ncclSum, comm, stream));
 		else if (group) group->allreduce<float>(rank, p, n, max_op ? NeusLocalGroup::MAX : NeusLocalGroup::SUM, stream);
 		else throw std::runtime_error("data parallel: no communicator");
 	}
 	void allreduce_u32(uint32_t* p, size_t n) {
-		if (world == 1) return;
+		if (!coll_on() || n == 0) return;
+		++coll_calls; coll_bytes += n * 4; coll_bytes_step += n * 4;
 		if (comm) NCCL_CHECK(ncclAllReduce(p, p, n, ncclUint32, ncclSum, comm, stream));
 		else if (group) group->allreduce<uint32_t>(rank, p, n, NeusLocalGroup::SUM, stream);
 		else throw std::runtime_error("data parallel: no communicator");
@@ -792,6 +806,7 @@ struct NeusTestbed {
 		const uint32_t NT = n_uniform + n_nonuniform;
 		const uint32_t lo = (uint32_t)((uint64_t)NT * rank / world), hi = (uint32_t)((uint64_t)NT * (rank + 1) / world);
 		const uint32_t N = hi - lo;
+		occ_samples += N; ++occ_updates;
 		const pcg32 rng_u = density_grid_rng;
 		density_grid_rng.advance();
 		const pcg32 rng_nu = density_grid_rng;
@@ -1092,10 +1107,15 @@ struct NeusTestbed {
 			launch_sum_f32(s, scan_tmp.p, scan_tmp_bytes, ek.p, loss_sum.p + 1, MAX_RAYS);
 			launch_sum_f32(s, scan_tmp.p, scan_tmp_bytes, mask.p, loss_sum.p + 2, MAX_RAYS);
 		}
-		if (world > 1) {
-			// collective 1 (gradients; DeltaNetwork partials) and 3 (counters, loss scalars) of SURVEY §8(e), one group
+		if (coll_on()) {
+			// collective 1 (gradients; DeltaNetwork partials) and 3 (counters, loss scalars) of SURVEY §8(e), one group.
+			// The gradient of the grid levels past the progressive valid level is zero on every rank (no records; the
+			// scatter keeps that range zeroed), so only the MLP blocks, the active levels' tables and the variance move.
+			coll_bytes_step = 0;
+			const size_t grid_act = 2 * (size_t)gl.offset[std::min(valid + 1, gl.n_levels)];
 			coll_begin();
-			allreduce_f32(grads.p, lay.P);
+			allreduce_f32(grads.p, (size_t)lay.grid_off + grid_act);
+			allreduce_f32(grads.p + lay.var_off, lay.P - lay.var_off);
 			allreduce_u32(&st.p->compacted_counter, 1);
 			allreduce_u32(&st.p->n_rays_with_samples, 1);
 			if (use_delta) allreduce_f32(delta_partial.p, delta_partial_floats());
@@ -1104,7 +1124,7 @@ struct NeusTestbed {
 		}
 		if (get_loss) {
 			HIP_CHECK(hipMemcpyAsync(pinned, loss_sum.p, 3 * 4, hipMemcpyDeviceToHost, s));
-			HIP_CHECK(hipMemcpyAsync(pinned + 4, st.p, sizeof(StepState), hipMemcpyDeviceToHost, s));
+			HIP_CHECK(hipMemcpyAsync(pinned + 64, st.p, sizeof(StepState), hipMemcpyDeviceToHost, s));
 			loss_pending = true;
 		}
 		launch_step_counters(s, st.p, batch, max_samples, world, cfg.fixed_rays_per_batch);
@@ -1165,7 +1185,7 @@ struct NeusTestbed {
 	void consume_loss() {
 		if (!loss_pending) return;
 		HIP_CHECK(hipStreamSynchronize(stream));
-		const StepState* sst = (const StepState*)(pinned + 4);
+		const StepState* sst = (const StepState*)(pinned + 64);
 		const float measured = (float)sst->compacted_counter / (float)world;
 		const float scale = measured / (float)batch;
 		last_loss = pinned[0] * scale;
@@ -1244,6 +1264,8 @@ int neus_testbed_get_stats(NeusTestbed* tb, NeusTrainStats* o) {
 		o->march_first_pass_rays = s.march_est; o->kept_ray_extent = s.kept_extent;
 		o->nonfinite_loss = tb->nonfinite ? 1u : 0u;
 		o->training_aborted = (tb->aborted || (tb->training_step > 0 && s.zero_records)) ? 1u : 0u;
+		o->pre_samples_total = s.pre_total; o->rays_total = s.rays_total;
+		o->occ_samples_total = tb->occ_samples; o->occ_updates = tb->occ_updates; o->reserved_ = 0;
 	});
 }
 static int copy_param_vec(NeusTestbed* tb, const float* dev, float* host, uint64_t n) {
@@ -1418,6 +1440,38 @@ int neus_testbed_mesh_vertex_colors(NeusTestbed* tb, float* rgb) {
 	});
 }
 int neus_mc_table(int8_t* out) { return guard([&] { mc_table_host(out); }); }
+int neus_prepare_image_rgba8(uint8_t* rgba, uint32_t w, uint32_t h, const uint8_t* alpha_rgba, const uint8_t* mask_rgba, uint32_t flags,
+                             uint32_t* mask_color_out) {
+	return guard([&] {
+		if (!rgba) throw std::runtime_error("prepare_image: null image");
+		const uint64_t n = (uint64_t)w * h;
+		if (alpha_rgba) {
+			// srgb_to_linear (common_device.cuh:31-37) of the alpha image's red channel, as a 256-entry table
+			uint8_t lut[256];
+			for (int v = 0; v < 256; ++v) {
+				const float srgb = (float)v * (1.f / 255.f);
+				const float lin = srgb <= 0.04045f ? srgb / 12.92f : std::pow((srgb + 0.055f) / 1.055f, 2.4f);
+				lut[v] = (uint8_t)(255.0f * lin);
+			}
+			for (uint64_t i = 0; i < n; ++i) rgba[4 * i + 3] = lut[alpha_rgba[4 * i]];
+		}
+		const uint32_t key = mask_rgba ? 0x00FF00FFu : 0u;  // hot pink
+		if (mask_rgba)
+			for (uint64_t i = 0; i < n; ++i)
+				if (mask_rgba[4 * i] != 0) std::memcpy(rgba + 4 * i, &key, 4);
+		const bool wt = flags & NEUS_IMAGE_WHITE_TRANSPARENT, bt = flags & NEUS_IMAGE_BLACK_TRANSPARENT;
+		if (wt || bt || key)
+			for (uint64_t i = 0; i < n; ++i) {
+				uint8_t* p = rgba + 4 * i;
+				if (wt && p[0] == 255 && p[1] == 255 && p[2] == 255) p[3] = 0;
+				if (bt && p[0] == 0 && p[1] == 0 && p[2] == 0) p[3] = 0;
+				uint32_t v;
+				std::memcpy(&v, p, 4);
+				if (key != 0 && v == key) { p[0] = 0xFF; p[1] = 0x00; p[2] = 0xFF; p[3] = 0x00; }
+			}
+		if (mask_color_out) *mask_color_out = key;
+	});
+}
 int neus_testbed_next_frame(NeusTestbed* tb, uint32_t n_images, const NeusImage* images) {
 	return guard([&] {
 		HIP_CHECK(hipSetDevice(tb->device));
@@ -1651,17 +1705,31 @@ int neus_nccl_unique_id(uint8_t* out) {
 		std::memcpy(out, &id, 128);
 	});
 }
-int neus_testbed_init_data_parallel(NeusTestbed* tb, int rank, int world, const uint8_t* uid) {
+int neus_testbed_init_data_parallel_ex(NeusTestbed* tb, int rank, int world, const uint8_t* uid, uint32_t flags) {
 	return guard([&] {
 		if (world < 1 || rank < 0 || rank >= world) throw std::runtime_error("invalid rank/world");
+		if (tb->comm || tb->group) throw std::runtime_error("init_data_parallel: the testbed already has a communicator");
 		HIP_CHECK(hipSetDevice(tb->device));
 		tb->rank = (uint32_t)rank; tb->world = (uint32_t)world;
+		tb->force_coll = (flags & NEUS_DP_FORCE_COLLECTIVES) != 0;
 		tb->tbuf.indeed_batch = (float)tb->batch * (float)world;
-		if (world > 1) {
+		tb->coll_calls = tb->coll_bytes = tb->coll_bytes_step = 0;
+		if (world > 1 || tb->force_coll) {
+			if (!uid) throw std::runtime_error("init_data_parallel: no unique id");
 			ncclUniqueId id;
 			std::memcpy(&id, uid, 128);
 			NCCL_CHECK(ncclCommInitRank(&tb->comm, world, id, rank));
 		}
+	});
+}
+int neus_testbed_init_data_parallel(NeusTestbed* tb, int rank, int world, const uint8_t* uid) {
+	return neus_testbed_init_data_parallel_ex(tb, rank, world, uid, 0u);
+}
+int neus_testbed_data_parallel_info(NeusTestbed* tb, NeusDataParallelInfo* o) {
+	return guard([&] {
+		o->rank = tb->rank; o->world = tb->world;
+		o->has_communicator = tb->comm ? 1u : 0u; o->local_group = tb->group ? 1u : 0u;
+		o->collective_calls = tb->coll_calls; o->allreduce_bytes = tb->coll_bytes; o->last_step_allreduce_bytes = tb->coll_bytes_step;
 	});
 }
 

@@ -270,10 +270,29 @@ def ngp_matrix_to_nerf(m, scale, offset, from_na):
     return r
 
 
+def prepare_image(img, alpha=None, mask=None, white_transparent=False, black_transparent=False):
+    """ngp::load_nerf's training-image preparation (neus_prepare_image_rgba8): alpha image, dynamic mask (hot-pink
+    key), white / black transparency. Returns (prepared h x w x 4 uint8 copy, mask colour key or 0)."""
+    out = np.ascontiguousarray(img, np.uint8).copy()
+    h, w = out.shape[:2]
+    a = None if alpha is None else np.ascontiguousarray(alpha, np.uint8)
+    m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+    for x in (a, m):
+        if x is not None and x.shape[:2] != (h, w):
+            raise RuntimeError("prepare_image: alpha / mask resolution differs from the image")
+    key = C.c_uint32(0)
+    flags = (1 if white_transparent else 0) | (2 if black_transparent else 0)
+    check(lib().neus_prepare_image_rgba8(C.c_void_p(out.ctypes.data), C.c_uint32(w), C.c_uint32(h),
+                                         C.c_void_p(a.ctypes.data) if a is not None else None,
+                                         C.c_void_p(m.ctypes.data) if m is not None else None, C.c_uint32(flags), C.byref(key)))
+    return out, int(key.value)
+
+
 def load_transforms(path):
     """ngp::load_nerf (nerf_loader.cu:197-751) subset: from_na/scale/offset/aabb_scale, per-frame
     intrinsic_matrix or fl_x/fl_y/camera_angle_x, cx/cy; RGBA PNG images (alpha premultiplied on
-    the device by read_rgba)."""
+    the device by read_rgba), with the reference's image preparation (neus_prepare_image_rgba8): separate alpha
+    images, dynamic masks (the hot-pink key) and white_transparent / black_transparent."""
     from PIL import Image
     with open(path) as f:
         js = json.load(f)
@@ -290,13 +309,37 @@ def load_transforms(path):
         length = max(1e-6, float(np.max(np.abs(a[1] - a[0]))))
         scale = 1.0 / length
         offset = (a[1] + a[0]) * 0.5 * -scale + 0.5
-    images, focal, principal, xforms = [], [], [], []
+    white_t, black_t = bool(js.get("white_transparent", False)), bool(js.get("black_transparent", False))
+    flags = white_t or black_t
+    images, focal, principal, xforms, mask_colors = [], [], [], [], []
     for fr in js["frames"]:
-        p = os.path.join(base, fr["file_path"])
-        if not os.path.splitext(p)[1]:
+        fp = fr["file_path"]
+        p = os.path.join(base, fp)
+        name = os.path.basename(p)
+        if "." not in name:  # path.extension() == "" -> png (exr is not supported here)
             p = p + ".png"
-        img = np.asarray(Image.open(p).convert("RGBA"), np.uint8)
+            name += ".png"
+            if not os.path.exists(p):
+                raise RuntimeError("Could not find image file: " + p)
+        ext = name[name.rfind(".") + 1:]
+        img = np.ascontiguousarray(np.asarray(Image.open(p).convert("RGBA"), np.uint8)).copy()
         h, w = img.shape[:2]
+        # alpha image `<file_path>.alpha.<ext>` and dynamic mask `dynamic_mask_<basename>.png` (nerf_loader.cu:550-590)
+        alpha = mask = None
+        apath = os.path.join(base, fp + ".alpha." + ext)
+        if os.path.exists(apath):
+            alpha = np.ascontiguousarray(np.asarray(Image.open(apath).convert("RGBA"), np.uint8))
+            if alpha.shape[:2] != (h, w):
+                raise RuntimeError("Alpha image has wrong resolution: " + apath)
+        mpath = os.path.join(os.path.dirname(p), "dynamic_mask_" + name[: name.rfind(".")] + ".png")
+        if os.path.exists(mpath):
+            mask = np.ascontiguousarray(np.asarray(Image.open(mpath).convert("RGBA"), np.uint8))
+            if mask.shape[:2] != (h, w):
+                raise RuntimeError("Mask image has wrong resolution: " + mpath)
+        key = 0
+        if alpha is not None or mask is not None or flags:
+            img, key = prepare_image(img, alpha, mask, white_t, black_t)
+        mask_colors.append(key)
         pp = np.array([0.5, 0.5], np.float32)
         if "cx" in js:
             pp[0] = float(js["cx"]) / float(js["w"])
@@ -329,7 +372,8 @@ def load_transforms(path):
         focal.append(fl)
         principal.append(pp)
     return dict(images=images, focal=np.array(focal, np.float32), principal=np.array(principal, np.float32),
-                xforms=np.stack(xforms).astype(np.float32), aabb_scale=aabb_scale, scale=scale, offset=offset, from_na=from_na)
+                xforms=np.stack(xforms).astype(np.float32), aabb_scale=aabb_scale, scale=scale, offset=offset, from_na=from_na,
+                mask_colors=mask_colors, white_transparent=white_t, black_transparent=black_t)
 
 
 def geometric_init_weights(n_levels, width=64, seed=1337, path_hint=True):
@@ -1058,9 +1102,18 @@ class Testbed:
     def synchronize(self):
         check(lib().neus_testbed_synchronize(self._h))
 
-    def init_data_parallel(self, rank, world, unique_id: bytes):
+    def init_data_parallel(self, rank, world, unique_id: bytes, force_collectives=False):
+        """RCCL data parallelism over ray batches (one rank per GPU). force_collectives: create the communicator and
+        issue the step's collectives at world 1 as well (tests of the RCCL path on one GPU)."""
         buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
-        check(lib().neus_testbed_init_data_parallel(self._h, C.c_int(rank), C.c_int(world), buf))
+        check(lib().neus_testbed_init_data_parallel_ex(self._h, C.c_int(rank), C.c_int(world), buf,
+                                                       C.c_uint32(1 if force_collectives else 0)))
+
+    def data_parallel_info(self):
+        from ._lib import NeusDataParallelInfo
+        o = NeusDataParallelInfo()
+        check(lib().neus_testbed_data_parallel_info(self._h, C.byref(o)))
+        return {k: getattr(o, k) for k, _ in o._fields_}
 
     @property
     def handle(self):

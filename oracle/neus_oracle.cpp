@@ -1553,4 +1553,33 @@ uint64_t or_marching_cubes(const float* d, uint32_t rx, uint32_t ry, uint32_t rz
 	if (n_tris_out) *n_tris_out = nt;
 	return nv;
 }
+
+// ---------------------------------------------------------------- training-image preparation (ngp::load_nerf)
+// nerf_loader.cu:550-569 (alpha image: red channel through srgb_to_linear, common_device.cuh:31-37, truncated to
+// uint8), :571-590 (dynamic mask: mask red != 0 -> 0x00FF00FF), then convert_rgba32 (:59-81) as set_training_image
+// applies it: white / black rgb -> alpha 0, the mask colour re-keyed to hot pink.
+static float or_srgb_to_linear(float srgb) { return srgb <= 0.04045f ? srgb / 12.92f : std::pow((srgb + 0.055f) / 1.055f, 2.4f); }
+uint32_t or_prepare_image_rgba8(uint8_t* img, uint32_t w, uint32_t h, const uint8_t* alpha_img, const uint8_t* mask_img, int white_transparent,
+                                int black_transparent) {
+	const uint64_t n = (uint64_t)w * h;
+	if (alpha_img)
+		for (uint64_t i = 0; i < n; ++i) img[i * 4 + 3] = uint8_t(255.0f * or_srgb_to_linear(alpha_img[i * 4] * (1.f / 255.f)));
+	uint32_t mask_color = 0;
+	if (mask_img) {
+		mask_color = 0x00FF00FF;
+		for (uint64_t i = 0; i < n; ++i)
+			if (mask_img[i * 4] != 0) std::memcpy(img + i * 4, &mask_color, 4);
+	}
+	for (uint64_t i = 0; i < n; ++i) {
+		uint8_t rgba[4];
+		std::memcpy(rgba, img + i * 4, 4);
+		if (white_transparent && rgba[0] == 255 && rgba[1] == 255 && rgba[2] == 255) rgba[3] = 0;
+		if (black_transparent && rgba[0] == 0 && rgba[1] == 0 && rgba[2] == 0) rgba[3] = 0;
+		uint32_t v;
+		std::memcpy(&v, rgba, 4);
+		if (mask_color != 0 && mask_color == v) { rgba[0] = 0xFF; rgba[1] = 0x00; rgba[2] = 0xFF; rgba[3] = 0x00; }
+		std::memcpy(img + i * 4, rgba, 4);
+	}
+	return mask_color;
+}
 } // extern "C"

@@ -273,6 +273,18 @@ def det_expf(x):
     return lib().or_det_expf(float(x))
 
 
+def prepare_image(img, alpha=None, mask=None, white_transparent=False, black_transparent=False):
+    """ngp::load_nerf's image preparation (nerf_loader.cu:550-590 + convert_rgba32 :59-81); returns (rgba, mask_color)."""
+    out = np.ascontiguousarray(img, np.uint8).copy()
+    h, w = out.shape[:2]
+    a = None if alpha is None else np.ascontiguousarray(alpha, np.uint8)
+    m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+    lib().or_prepare_image_rgba8.restype = C.c_uint32
+    key = lib().or_prepare_image_rgba8(P(out), C.c_uint32(w), C.c_uint32(h), P(a) if a is not None else None,
+                                       P(m) if m is not None else None, C.c_int(int(white_transparent)), C.c_int(int(black_transparent)))
+    return out, int(key)
+
+
 def num_threads():
     return lib().or_num_threads()
 

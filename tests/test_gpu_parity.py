@@ -259,6 +259,72 @@ def test_loss_compaction_parity(env):
         np.testing.assert_allclose(loss.cpu().numpy(), ref["loss"], rtol=1e-4, atol=1e-9)
 
 
+def test_masked_dataset_sampling_and_loss_parity(env):
+    """Dynamic masks (nerf_loader.cu:571-590): views prepared with a mask (pyngp.prepare_image -> the hot-pink key
+    0x00FF00FF) read as negative targets (read_rgba, common_device.cuh:635-667), so the sampler drops 90 % of the rays
+    that hit them with an extra rng draw (testbed_nerf.cu:1310-1312) and the loss of the kept ones takes the masked
+    branch (rgb target from -1 texels, mask_gt 0). Sampling (rays, numsteps, coordinates) bit-exact and the loss /
+    compaction as test_loss_compaction_parity, against the oracle on the same prepared images."""
+    from neus2_amd import pyngp
+    t, O = env["t"], env["O"]
+    lib, check = L()
+    sc = env["sc"]
+    rng = np.random.default_rng(21)
+    images = []
+    n_masked = 0
+    for img in sc["images"]:
+        mask = np.zeros_like(img)
+        mask[..., 0] = (rng.random(img.shape[:2]) < 0.4) * 255
+        out, key = pyngp.prepare_image(img, mask=mask)
+        assert key == 0x00FF00FF
+        n_masked += int((out.view(np.uint32)[..., 0] == 0x00FF00FF).sum())
+        images.append(out)
+    assert n_masked > 0
+    tb = pyngp.Testbed(pyngp.TestbedMode.Nerf)
+    tb.set_dataset(images, sc["focal"], sc["principal"], sc["xforms"], 1)
+    tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=BATCH)
+    ds = O.Dataset(images, sc["focal"], sc["principal"], sc["xforms"])
+    bf = _bitfield(env)
+    n_rays, max_s = 4096, 4096 * 16
+    rs, ri = 0x2545F4914F6CDD1D, 0xDA3E39CB94B95BDB | 1
+    rays = t.zeros((n_rays, 6), dtype=t.float32, device="cuda")
+    ns = t.zeros((n_rays, 2), dtype=t.int32, device="cuda")
+    co = t.zeros((max_s, 7), dtype=t.float32, device="cuda")
+    cnt = (C.c_uint32 * 3)()
+    check(lib.neus_sample_rays(tb.handle, None, C.c_uint32(n_rays), C.c_uint32(0), C.c_uint32(1), C.c_uint32(0),
+                               C.c_uint64(rs), C.c_uint64(ri), C.c_uint32(max_s), ptr(dev(t, bf)), ptr(rays), ptr(ns), ptr(co), cnt))
+    r_rays, r_ns, r_co, r_cnt, r_nr = O.generate_samples(ds, bf, n_rays, 0, rs, ri, max_s)
+    np.testing.assert_array_equal(host(ns, np.uint32), r_ns)
+    np.testing.assert_array_equal(host(rays, np.uint32), r_rays.view(np.uint32))
+    nk = int(cnt[1])
+    assert nk == int(r_ns[:, 0].sum()) and nk > 0
+    np.testing.assert_array_equal(host(co, np.uint32)[:nk], r_co.view(np.uint32)[:nk])
+    # unmasked: more rays keep samples (the masked rays are dropped 9 times in 10)
+    _, r_ns_plain, _, _, _ = O.generate_samples(env["ds"], bf, n_rays, 0, rs, ri, max_s)
+    assert (r_ns[:, 0] > 0).sum() < (r_ns_plain[:, 0] > 0).sum()
+    net = O.network_forward(env["cfg"], tb.get_params(), r_co[:nk], 14).view(np.float16).copy()
+    net[:, 3] = rng.normal(0.0, 0.05, nk).astype(np.float16)
+    net[:, 7] = np.float16(0.35)
+    net = net.view(np.uint16)
+    nsd = dev(t, r_ns)
+    co_c = t.zeros((BATCH, 7), dtype=t.float32, device="cuda")
+    dlo = t.zeros((BATCH, 16), dtype=t.int16, device="cuda")
+    loss = t.zeros(n_rays, dtype=t.float32, device="cuda"); ek = t.zeros_like(loss); mk = t.zeros_like(loss)
+    c1 = (C.c_uint32 * 1)()
+    check(lib.neus_loss_compact(tb.handle, None, C.c_uint32(n_rays), C.c_uint32(0), C.c_uint32(1), C.c_uint32(0),
+                                C.c_uint64(rs), C.c_uint64(ri), C.c_uint32(BATCH), ptr(dev(t, r_rays)), ptr(nsd),
+                                ptr(dev(t, r_co)), ptr(dev(t, net)), ptr(co_c), ptr(dlo), ptr(loss), ptr(ek), ptr(mk), c1))
+    ref = O.compute_loss(ds, n_rays, 0, rs, ri, BATCH, r_rays, r_ns, r_co, net)
+    assert c1[0] == ref["counter"]
+    np.testing.assert_array_equal(host(nsd, np.uint32), ref["numsteps"])
+    nc = min(ref["counter"], BATCH)
+    np.testing.assert_array_equal(host(co_c, np.uint32)[:nc], ref["coords"].view(np.uint32)[:nc])
+    g = host(dlo, np.float16).astype(np.float32)[:nc, :11]
+    r = ref["dL_dout"].view(np.float16).astype(np.float32)[:nc, :11]
+    np.testing.assert_allclose(g, r, rtol=2e-3, atol=1e-6)
+    np.testing.assert_allclose(loss.cpu().numpy(), ref["loss"], rtol=1e-4, atol=1e-9)
+
+
 def test_loss_target_options_parity(env):
     """The loss targets under the reference's training options (testbed_nerf.cu:1642-1671): a fixed background
     (random_bg_color False, background_color) and the SRGB colour space / linear_colors target modes, against the
