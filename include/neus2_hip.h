@@ -360,6 +360,13 @@ typedef struct NeusModuleInfo {
 } NeusModuleInfo;
 int neus_module_create_network(const char* config_json, uint32_t batch_capacity, NeusModule** out);
 int neus_module_create_encoding(uint32_t n_input_dims, const char* encoding_json, uint32_t batch_capacity, NeusModule** out);
+/* create_network_with_input_encoding (cpp_api.h:108; network_with_input_encoding.h): HashGrid -> FullyFusedMLP (1 hidden ReLU
+ * layer of n_neurons 16 or 64, linear output padded to 16). Input [n][3] f32, output [n][16] fp16 (column-major, as
+ * cpp_api.cu:58-70), params [W x DE | 16 x W | grid] fp16 with DE = 2 n_levels padded to 16. backward_backward_input follows
+ * network_with_input_encoding.h:159-250 / fully_fused_mlp.cu:1088-1198 (parameter gradients only; dL_ddLdoutput and
+ * dL_dinput are not written, as in the reference). */
+int neus_module_create_network_with_input_encoding(uint32_t n_input_dims, uint32_t n_output_dims, const char* encoding_json,
+                                                   const char* network_json, uint32_t batch_capacity, NeusModule** out);
 int neus_module_destroy(NeusModule* m);
 int neus_context_destroy(NeusContext* ctx);
 int neus_module_info(const NeusModule* m, NeusModuleInfo* out);

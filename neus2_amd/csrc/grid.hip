@@ -280,6 +280,127 @@ __global__ void __launch_bounds__(256) k_scatter_bin(const uint32_t* __restrict_
 	}
 }
 
+// ---------------------------------------------------------------- wide-block binning (default)
+// The same records, slots and buckets as k_scatter_hist / k_scatter_bin, with one BS-thread workgroup per BS = 512
+// (default) or 1024 samples instead of 256: a (block, bucket) run of a hashed level holds ~32-64 records instead of ~16, so the
+// sorted stage leaves the workgroup as whole 128-B lines (the 256-sample runs were written in 32-64 B pieces), the
+// histogram has 2-4x fewer (bucket, block) counters to scan, and the per-level barriers are paid once per BS samples.
+// The wave groups (64 consecutive samples) and their run sums are unchanged, so the records - and the int64 sums -
+// are bitwise those of the 256-sample path.
+template <int BS>
+__global__ void __launch_bounds__(BS) k_scatter_hist_w(const uint32_t* __restrict__ n_ptr, uint32_t n_fixed, uint32_t ld,
+                                                         const float* __restrict__ coords, uint32_t coord_stride, const GridLevels gl,
+                                                         uint32_t valid_level, const uint32_t* __restrict__ dLdenc, const uint32_t* __restrict__ g,
+                                                         const float4* __restrict__ v4, ScatterWork w) {
+	__shared__ uint32_t hist[SB_MAX_BUCKETS];
+	for (uint32_t b = threadIdx.x; b < w.n_active; b += blockDim.x) hist[b] = 0;
+	__syncthreads();
+	const uint32_t n = load_n(n_ptr, n_fixed);
+	const uint32_t blk = blockIdx.x, i = blk * blockDim.x + threadIdx.x;
+	const bool ok = i < n;
+	const uint32_t ic = ok ? i : 0;
+	const float* c = coords + (size_t)ic * coord_stride;
+	const float x = c[0], y = c[1], z = c[2];
+	const float4 vv = v4[ic];
+	for (uint32_t l = 0; l < gl.n_levels && l <= valid_level; ++l) {
+		const ScatterLevel L = scatter_level(gl, l, x, y, z, ic, ld, dLdenc, g, vv);
+#pragma unroll
+		for (uint32_t idx = 0; idx < 8; ++idx) {
+			uint32_t gidx; float a0, a1;
+			corner_contribution(L, idx, gidx, a0, a1);
+			const bool emit = wave_run_sum(gidx, a0, a1, ok);
+			const uint32_t bkt = gidx >> SB_SHIFT;
+			if (L.s.hsize <= 4 * SB_SIZE) (void)wave_bucket_slot(hist, bkt, emit);
+			else if (emit) atomicAdd(&hist[bkt], 1u);
+		}
+	}
+	__syncthreads();
+	for (uint32_t b = threadIdx.x; b < w.n_active; b += blockDim.x) w.counts[(size_t)b * w.n_chunks + xcd_slot(blk, w.n_chunks)] = hist[b];
+}
+
+template <int BS>
+__global__ void __launch_bounds__(BS) k_scatter_bin_w(const uint32_t* __restrict__ n_ptr, uint32_t n_fixed, uint32_t ld,
+                                                        const float* __restrict__ coords, uint32_t coord_stride, const GridLevels gl,
+                                                        uint32_t valid_level, const uint32_t* __restrict__ dLdenc, const uint32_t* __restrict__ g,
+                                                        const float4* __restrict__ v4, ScatterWork w) {
+	__shared__ uint32_t cnt[SB_LEVEL_BUCKETS], cursor[SB_LEVEL_BUCKETS], base[SB_LEVEL_BUCKETS + 1];
+	__shared__ uint32_t carry_b, carry_v;  // a bucket shared with the previous level: the block's next slot in it
+	__shared__ uint16_t st_i[BS * 8];
+	__shared__ uint32_t st_g[BS * 8];
+	__shared__ uint8_t st_b[BS * 8];       // level-local bucket of each staged record
+	const uint32_t blk = blockIdx.x, lane = threadIdx.x & 63;
+	const uint32_t n = load_n(n_ptr, n_fixed);
+	const uint32_t i = blk * blockDim.x + threadIdx.x;
+	const bool ok = i < n;
+	const uint32_t ic = ok ? i : 0;
+	const float* c = coords + (size_t)ic * coord_stride;
+	const float x = c[0], y = c[1], z = c[2];
+	const float4 vv = v4[ic];
+	const uint32_t slot_blk = xcd_slot(blk, w.n_chunks);
+	if (threadIdx.x == 0) { carry_b = ~0u; carry_v = 0; }
+	for (uint32_t l = 0; l < gl.n_levels && l <= valid_level; ++l) {
+		const uint32_t b_first = gl.offset[l] >> SB_SHIFT, nlb = ((gl.offset[l + 1] - 1) >> SB_SHIFT) - b_first + 1;
+		const bool few = gl.offset[l + 1] - gl.offset[l] <= 4 * SB_SIZE;
+		__syncthreads();  // the previous level's stage is written out, carry_b / carry_v final
+		for (uint32_t k = threadIdx.x; k < nlb; k += blockDim.x) {
+			const uint32_t b = b_first + k;
+			cnt[k] = 0;
+			cursor[k] = b == carry_b ? carry_v : w.offs[(size_t)b * w.n_chunks + slot_blk];
+		}
+		__syncthreads();
+		const ScatterLevel L = scatter_level(gl, l, x, y, z, ic, ld, dLdenc, g, vv);
+		uint32_t re[8], rs[8], rg[8];
+#pragma unroll
+		for (uint32_t idx = 0; idx < 8; ++idx) {
+			uint32_t gidx; float a0, a1;
+			corner_contribution(L, idx, gidx, a0, a1);
+			const bool emit = wave_run_sum(gidx, a0, a1, ok);
+			const uint32_t lb = (gidx >> SB_SHIFT) - b_first;
+			uint32_t sl = 0;
+			if (few) sl = wave_bucket_slot(cnt, lb, emit);
+			else if (emit) sl = atomicAdd(&cnt[lb], 1u);
+			re[idx] = emit ? gidx : ~0u;
+			rs[idx] = sl;
+			rg[idx] = __builtin_bit_cast(uint32_t, (h2){(half_t)a0, (half_t)a1});
+		}
+		__syncthreads();  // bucket counts complete
+		if (threadIdx.x < 64) {  // exclusive scan of the counts (one wave)
+			uint32_t total = 0;
+			for (uint32_t k0 = 0; k0 < nlb; k0 += 64) {
+				const uint32_t k = k0 + lane;
+				const uint32_t v = k < nlb ? cnt[k] : 0u;
+				uint32_t incl = v;
+#pragma unroll
+				for (int d = 1; d < 64; d <<= 1) { const uint32_t t = (uint32_t)__shfl_up((int)incl, d); if ((int)lane >= d) incl += t; }
+				if (k < nlb) base[k] = total + incl - v;
+				total += (uint32_t)__shfl((int)incl, 63);
+			}
+			if (lane == 0) base[nlb] = total;
+		}
+		__syncthreads();
+#pragma unroll
+		for (uint32_t idx = 0; idx < 8; ++idx) {
+			const uint32_t e = re[idx];
+			if (e != ~0u) {
+				const uint32_t lb = (e >> SB_SHIFT) - b_first;
+				const uint32_t pos = base[lb] + rs[idx];
+				st_i[pos] = (uint16_t)(e & (SB_SIZE - 1));
+				st_g[pos] = rg[idx];
+				st_b[pos] = (uint8_t)lb;
+			}
+		}
+		__syncthreads();  // stage complete: consecutive threads store consecutive slots of a bucket's run
+		const uint32_t total = base[nlb];
+		for (uint32_t r = threadIdx.x; r < total; r += blockDim.x) {
+			const uint32_t lb = st_b[r];
+			const uint32_t gp = cursor[lb] + (r - base[lb]);
+			w.rec_i[gp] = st_i[r];
+			w.rec_g[gp] = __builtin_bit_cast(h2, st_g[r]);
+		}
+		if (threadIdx.x == 0) { carry_b = b_first + nlb - 1; carry_v = cursor[nlb - 1] + cnt[nlb - 1]; }
+	}
+}
+
 // One workgroup per bucket, or `parts` workgroups for a bucket of a small dense level (one 4096-entry bucket can hold a
 // whole level's records): each part sums an equal slice of the bucket's records in LDS and adds its nonzero int64 sums
 // to the bucket's split slot with 64-bit integer atomics (exact, so the total is order-independent and bitwise the
@@ -464,6 +585,28 @@ uint32_t scatter_n_buckets(const GridLevels& gl) {
 void launch_grid_scatter(hipStream_t s, const uint32_t* n_ptr, uint32_t n_fixed, uint32_t ld, const float* coords, uint32_t coord_stride,
                          const GridLevels& gl, uint32_t valid_level, const half_t* dLdenc, const half_t* g, const float4* v, float* grads,
                          const ScatterWork& w, void* scan_tmp, size_t scan_tmp_bytes) {
+	if (w.mode == 0) {
+		// the grid spans the workspace's sample capacity (w.n_chunks x w.chunk >= n)
+		const size_t nb = (size_t)w.n_active * w.n_chunks;
+		if (w.chunk == 1024)
+			k_scatter_hist_w<1024><<<w.n_chunks, 1024, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, (const uint32_t*)dLdenc,
+			                                                   (const uint32_t*)g, v, w);
+		else
+			k_scatter_hist_w<512><<<w.n_chunks, 512, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, (const uint32_t*)dLdenc,
+			                                                 (const uint32_t*)g, v, w);
+		(void)hipMemsetAsync(w.counts + nb, 0, 4, s);
+		launch_exclusive_scan(s, scan_tmp, scan_tmp_bytes, w.counts, w.offs, (uint32_t)nb + 1);
+		if (w.chunk == 1024)
+			k_scatter_bin_w<1024><<<w.n_chunks, 1024, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, (const uint32_t*)dLdenc,
+			                                                  (const uint32_t*)g, v, w);
+		else
+			k_scatter_bin_w<512><<<w.n_chunks, 512, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, (const uint32_t*)dLdenc,
+			                                                (const uint32_t*)g, v, w);
+		ScatterWork wa = w;
+		wa.n_blocks = w.n_chunks;  // bucket b's records start at offs[b * n_chunks]
+		k_scatter_accum<<<w.n_jobs, 256, 0, s>>>(wa, grads, gl.offset[gl.n_levels]);
+		return;
+	}
 	// the grid always spans the workspace's sample capacity (w.n_blocks x 256 >= n, checked by the host)
 	const uint32_t nblk = w.n_blocks;
 	const size_t nb = (size_t)w.n_active * w.n_blocks;  // buckets past n_active get no records (scatter_work_for)

@@ -17,18 +17,22 @@ struct MlpPtrs {
 };
 
 struct TrainBufs {
-	// weight-gradient operands, SoA [rows][cols] fp16; density layers have 2*ld columns
-	half_t* d0_delta; half_t* d0_x;   // [W][2ld], [DIN][2ld]
-	half_t* d1_delta; half_t* d1_x;   // [16][2ld], [W][2ld]
-	half_t* r0_delta; half_t* r0_x;   // [W][ld], [48][ld]
-	half_t* r1_delta; half_t* r1_x;   // [W][ld], [W][ld]
-	half_t* r2_delta; half_t* r2_x;   // [16][ld], [W][ld]
-	half_t* dLdenc; half_t* genc;     // [L][ld] half2 (features 2l, 2l+1)
+	half_t* d1_delta;                 // [16][ld] dL/d(density output) (colour kernel -> density kernel)
+	half_t* dLdenc; half_t* genc;     // [L][ld] half2 (features 2l, 2l+1): the grid scatter's operands
 	float4* v;                        // [ld]
-	float* var_grad;                  // variance gradient (written by the weight-gradient reduction)
+	float* var_grad;                  // variance gradient (written by the gradient reduction)
 	float* var_partial;               // [blocks of the colour kernel] per-block sums of dL/dout[7]
 	float indeed_batch;
 	float4* dpos;                     // [ld] dL/d(network input position), first order (null: not needed)
+	// MLP weight gradients, accumulated in registers by the training kernels: one row of n_matrix floats per block
+	// (the density kernel fills [0, n_density), the colour kernel [n_density, n_matrix)), summed over the blocks in
+	// a fixed order by k_mlp_grad_reduce
+	float* wpartial;
+	uint32_t n_matrix, off_d1, off_r0, off_r1, off_r2;
+};
+struct MlpGradReduce {
+	const float* partial; uint32_t n_blocks, n_matrix; float* g; const uint32_t* n_valid;
+	const float* var_partial; uint32_t var_blocks; float* var_grad;
 };
 
 // Dynamic scenes. DeltaNetwork parameters in the reference's order: transition[4] |
@@ -47,15 +51,6 @@ struct RayMotion { float R[9]; float t[3]; uint32_t on; };
 // Loss-target options; all-zero = the reference drivers' defaults (random background, colour space Linear,
 // linear_colors off: sRGB targets). mode: 0 Linear colour space, 1 SRGB colour space, 2 train in linear colours.
 struct TrainTarget { uint32_t fixed_bg; float bg[3]; uint32_t mode; };
-
-struct WGradJob { const half_t* D; const half_t* X; float* dW; uint32_t M, K, ncols, ldc; uint32_t tiles_m, tiles_k; };
-// Weight gradients without atomics: every (job, 32x32 tile, sample split) block writes its partial tile to
-// `partial` (block-major, 1024 floats each); k_wgrad_reduce sums the splits in a fixed order into dW, and the
-// colour kernel's per-block variance sums into var_grad (bitwise reproducible).
-struct WGradJobs {
-	WGradJob j[5]; uint32_t n_jobs; uint32_t split; uint32_t block_start[6]; const uint32_t* n_valid;
-	float* partial; const float* var_partial; uint32_t var_blocks; float* var_grad;
-};
 
 struct DevDataset {
 	const uint32_t* pixels;
@@ -110,7 +105,10 @@ struct ScatterWork {
 	uint32_t* split_done;       // [n_split] parts finished (reset by the last part)
 	uint32_t n_jobs;
 	uint32_t n_active;          // buckets counted / scanned (those below it hold every record of the step)
+	uint32_t n_chunks, chunk;   // workgroups of the wide-block binning (mode 0) and their samples (512 or 1024)
+	uint32_t mode;              // 0 wide-block binning (default), 1 the 256-sample hist / scan / bin path (A/B reference)
 };
+
 // accumulation workgroups of the scatter (flattened uint4 {bucket, part, parts, split slot}); n_split = split buckets
 std::vector<uint32_t> scatter_accum_jobs(const GridLevels& gl, uint32_t n_buckets, uint32_t& n_split);
 
@@ -177,9 +175,16 @@ void launch_sdf_grid(hipStream_t s, uint32_t L, uint32_t W, const uint32_t res[3
                      const half_t* grid, const MlpPtrs& w, float* sdf, const DeltaState* delta = nullptr);
 void launch_mlp_train(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_valid_ptr, uint32_t n, uint32_t ld, const float* coords,
                       const half_t* enc, const float* dydx, const half_t* dL_dout, const MlpPtrs& w, const TrainBufs& tb, int part = 0 /* 0 both, 1 colour, 2 density */);
-void launch_wgrad(hipStream_t s, const WGradJobs& jobs, uint32_t n_blocks);
+void launch_mlp_grad_reduce(hipStream_t s, const MlpGradReduce& r);  // MLP weight + variance gradients (fixed order)
 uint32_t mlp_train_blocks(uint32_t L, uint32_t W, uint32_t n);  // grid of the training MLP kernels (= the variance partial count)
 void launch_mfma_probe(hipStream_t s, const half_t* A, const half_t* B, float* C);
+// operator module: tcnn NetworkWithInputEncoding(HashGrid -> FullyFusedMLP 1 hidden ReLU layer -> 16 linear), mlp.hip k_dnet
+struct DNetLaunch {
+	const half_t* w0; const half_t* w1; const uint32_t* enc; const half_t* dL; const uint32_t* u; half_t* out; uint32_t* denc; float* wpartial;
+};
+bool dnet_supported(uint32_t L, uint32_t W);
+uint32_t dnet_blocks(uint32_t n);  // the grid of launch_dnet (= the partial rows of modes 1 and 2)
+void launch_dnet(hipStream_t s, uint32_t L, uint32_t W, int mode /* 0 fwd, 1 bwd, 2 bwd-bwd */, uint32_t n, const DNetLaunch& d);
 // march.hip
 void launch_bitfield_linear(hipStream_t s, const uint8_t* bitfield, uint32_t* lin /* LIN_WORDS */);
 // Sample runs of the march (march.hip): per ray slot up to NERF_STEPS records {t of the run's first sample,

@@ -938,10 +938,49 @@ template <int L, int W> struct TrainSmem {
 };
 
 // ------------------------------------------------------------------------------------------
-// Training forward-recompute + first- and second-order backward for 32 compacted samples per
-// wave. Writes the weight-gradient GEMM operands (SoA fp16), the grid-scatter operands
-// (dL/denc, dSDF/denc as [2L][ld] fp16, v as float4) and the variance-gradient partial sum.
+// Training forward-recompute + first- and second-order backward for 32 compacted samples per wave, with the
+// weight-gradient GEMMs fused in: dW = sum over samples of D X^T (fully_fused_mlp.cu:967-1085, the split-K
+// fc_multiply_split_k of :1007 / :1020, and the second-order terms of :1088-1198) accumulated in registers across
+// the persistent loop, one partial row per block at the end. The operands (activations and deltas, held as B
+// fragments with the sample on the MFMA column) are turned into "sample on the k dimension" fragments by an MFMA
+// with a 0/1 selection matrix (exact: one nonzero product per output), so the per-sample operands never leave the
+// registers (the split-K GEMM used to write ~340 MB of fp16 operands per step and read them back).
 // ------------------------------------------------------------------------------------------
+// The selection operand of transpose32: column 16 q + c (c < 16) picks k index kinv(c) = 8 ((c >> 2) & 1) + 4 (c >> 3)
+// + (c & 3), the slot of fragment row c (pi_row(j, h) = c); columns of the other half are zero.
+__device__ __forceinline__ h8 transpose_sel(int q) {
+	const int lane = threadIdx.x & 63, col = lane & 31, h = lane >> 5, c = col & 15;
+	const bool on = (col >> 4) == q && ((c >> 2) & 1) == h;
+	const int j = 4 * (c >> 3) + (c & 3);
+	h8 b;
+#pragma unroll
+	for (int k = 0; k < 8; ++k) b[k] = (on && k == j) ? (half_t)1.0f : (half_t)0.0f;
+	return b;
+}
+// 32 rows of B fragments (f0: rows 32t + [0, 16), f1: rows 32t + [16, 32) if has1) -> the two k-step fragments of
+// samples for the row on this lane's column: T[q][j] = row 32t + (lane & 31), sample acc_row(8q + j, lane >> 5).
+__device__ __forceinline__ void transpose32(const h8& f0, const h8& f1, bool has1, const h8& s0, const h8& s1, h8 T[2]) {
+	f16v acc = mfma(f0, s0, zero16());
+	if (has1) acc = mfma(f1, s1, acc);
+	T[0] = frag<false>(acc, 0);
+	T[1] = frag<false>(acc, 1);
+}
+// LDS of a kernel whose weight staging is reused by flush_tile at the end (4 waves x 1024 floats)
+constexpr int smem_halves(int staged) { return staged > 8192 ? staged : 8192; }
+// dW tile (rows of D's tile, columns of X's tile) += TD . TX^T over the 32 samples
+__device__ __forceinline__ f16v wg_acc(const h8 TD[2], const h8 TX[2], f16v a) { return mfma(TD[1], TX[1], mfma(TD[0], TX[0], a)); }
+// The block's dW tiles summed over its four waves in a fixed order into its partial row (`red`: 4 KB per wave of LDS)
+__device__ __forceinline__ void flush_tile(float* red, float* prow, const f16v& a, uint32_t off, int M, int K, int mt, int kt) {
+	const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5, wv = threadIdx.x >> 6;
+#pragma unroll
+	for (int reg = 0; reg < 16; ++reg) red[wv * 1024 + acc_row(reg, h) * 32 + r] = a[reg];
+	__syncthreads();
+	for (uint32_t e = threadIdx.x; e < 1024; e += blockDim.x) {
+		const int m = 32 * mt + (int)(e / 32), k = 32 * kt + (int)(e % 32);
+		if (m < M && k < K) prow[off + (uint32_t)(m * K + k)] = (red[e] + red[1024 + e]) + (red[2048 + e] + red[3072 + e]);
+	}
+	__syncthreads();
+}
 // store an accumulator tile (rows 32*mt + acc_row) into SoA [rows][ldc] at column col, rows < R
 __device__ __forceinline__ void store_acc(half_t* buf, size_t ldc, uint32_t col, const f16v& a, int mt, int R, int h) {
 #pragma unroll
@@ -950,31 +989,22 @@ __device__ __forceinline__ void store_acc(half_t* buf, size_t ldc, uint32_t col,
 		if (row < R) buf[(size_t)row * ldc + col] = (half_t)a[reg];
 	}
 }
-// store a B fragment (k-step ks, pi order) into SoA rows 16ks + pi
-__device__ __forceinline__ void store_frag(half_t* buf, size_t ldc, uint32_t col, const h8& b, int ks, int R, int h) {
-#pragma unroll
-	for (int j = 0; j < 8; ++j) {
-		const int row = 16 * ks + (h ? pi_row(j, 1) : pi_row(j, 0));
-		if (row < R) buf[(size_t)row * ldc + col] = b[j];
-	}
-}
 
-// Training is split in two kernels so that neither holds the whole forward + backward state
-// (one fused kernel spilled ~1 KB per lane):
-//   k_mlp_train_rgb     : forward recompute (density + grad SDF + colour hidden layers), colour
-//                         backward, dL/d(density output) and v = dL/d(grad SDF)
-//   k_mlp_train_density : density forward recompute, density backward (first order) and the
-//                         second-order front pass h1' = relu'(H0) . (W0 u)
-// They communicate through the weight-gradient operand buffers they write anyway (d1_delta, v).
+// Training is split in two kernels so that neither holds the whole forward + backward state:
+//   k_mlp_train_rgb     : forward recompute (density + grad SDF + colour hidden layers), colour backward,
+//                         dL/d(density output) and v = dL/d(grad SDF); dW of the three colour layers
+//   k_mlp_train_density : density forward recompute, density backward (first order) and the second-order
+//                         front pass h1' = relu'(H0) . (W0 u); dW of the two density layers, first + second order
+// They communicate through d1_delta and v.
 template <int L, int W>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) k_mlp_train_rgb(const uint32_t* __restrict__ n_valid_ptr, uint32_t n, uint32_t ld,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) k_mlp_train_rgb(const uint32_t* __restrict__ n_valid_ptr, uint32_t n, uint32_t ld,
                                                        const float* __restrict__ coords, const half_t* __restrict__ enc_h,
                                                        const float* __restrict__ dydx, const half_t* __restrict__ dL_dout,
                                                        MlpPtrs w, TrainBufs tb) {
 	constexpr int DKS = Dims<L>::DKS, DMT = Dims<L>::DMT;
 	constexpr int MT = (W + 31) / 32, HKS = W / 16;
-	if (n_valid_ptr && *n_valid_ptr == 0) return;  // zero compacted samples: nothing to train on
-	__shared__ half_t sm[TrainSmem<L, W>::END];
+	if (n_valid_ptr && *n_valid_ptr == 0) return;
+	__shared__ half_t sm[smem_halves(TrainSmem<L, W>::END)];  // (the end-of-kernel dW reduction reuses 16 KB of it)
 	using TS = TrainSmem<L, W>;
 	const FwdW fw0 = stage_fwd<L, W>(sm, w.d0, w.d0T, w);
 	stage_mat(sm + TS::R2T, w.r2T, W, 16);
@@ -985,7 +1015,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 	const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
 	const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
 	const uint32_t n_waves = (gridDim.x * blockDim.x) >> 6;
-	const size_t ld2 = 2 * (size_t)ld;
+	const h8 sel0 = transpose_sel(0), sel1 = transpose_sel(1);
+	const h8 z8 = (h8){0, 0, 0, 0, 0, 0, 0, 0};
+	// dW accumulators: r0 [W][48] (K tiles: rin rows 0..31, 32..47), r1 [W][W], r2 [16][W]
+	f16v aR0[MT][2], aR1[MT][MT], aR2[MT];
+#pragma unroll
+	for (int mt = 0; mt < MT; ++mt) {
+		aR0[mt][0] = zero16(); aR0[mt][1] = zero16(); aR2[mt] = zero16();
+#pragma unroll
+		for (int kt = 0; kt < MT; ++kt) aR1[mt][kt] = zero16();
+	}
 	float var_part = 0.f;
 	for (uint32_t base = wave * 32; base < n; base += n_waves * 32) {
 		const uint32_t z = opaque_zero();
@@ -1024,23 +1063,25 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 		h8 rinB[3];
 		h8 H1B[HKS], H2B[HKS];
 		rgb_hidden_frag<W>(fw, D1B, x, wd, grad, r, h, rinB, H1B, H2B);
-		// weight-gradient operands stored as soon as they are final (shorter live ranges: this kernel runs at one
-		// wave per SIMD and spills its fragments to AGPRs when everything is stored at the end)
-		if (valid) {
-#pragma unroll
-			for (int ks = 0; ks < HKS; ++ks) { store_frag(tb.r1_x, ld, i, H1B[ks], ks, W, h); store_frag(tb.r2_x, ld, i, H2B[ks], ks, W, h); }
-#pragma unroll
-			for (int ks = 0; ks < 3; ++ks) store_frag(tb.r0_x, ld, i, rinB[ks], ks, 48, h);
-		}
-		// ---- colour backward
-		const h8 dlo = *(const h8*)(dL_dout + (size_t)ic * OUT_W + 8 * h);   // h=0: rows 0..7, h=1: rows 8..15
+		// ---- colour backward (a lane without a sample gets dL/dout = 0: every delta, hence its dW share, is 0)
+		const h8 dlo = valid ? *(const h8*)(dL_dout + (size_t)ic * OUT_W + 8 * h) : z8;  // h=0: rows 0..7, h=1: rows 8..15
 		const h8 dlo_o = shfl_xor_h8(dlo, 32);
 		const h8 dlo_lo = h ? dlo_o : dlo;   // rows 0..7 on every lane
 		const h8 dlo_hi = h ? dlo : dlo_o;   // rows 8..15 on every lane
 		if (valid && h == 0) var_part += (float)dlo_lo[7];
 		// delta_o (rows 0..2 = dL/drgb): B fragment, pi order -> lane h=0 elements 0..2
-		h8 dOB = (h8){0, 0, 0, 0, 0, 0, 0, 0};
+		h8 dOB = z8;
 		if (h == 0) { dOB[0] = dlo_lo[0]; dOB[1] = dlo_lo[1]; dOB[2] = dlo_lo[2]; }
+		{  // dW_r2 += dO . H2^T
+			h8 TD[2];
+			transpose32(dOB, z8, false, sel0, sel1, TD);
+#pragma unroll
+			for (int kt = 0; kt < MT; ++kt) {
+				h8 TX[2];
+				transpose32(H2B[2 * kt], 2 * kt + 1 < HKS ? H2B[2 * kt + 1] : z8, 2 * kt + 1 < HKS, sel0, sel1, TX);
+				aR2[kt] = wg_acc(TD, TX, aR2[kt]);
+			}
+		}
 		h8 dH2B[HKS], dH1B[HKS];
 #pragma unroll
 		for (int mt = 0; mt < MT; ++mt) {
@@ -1048,10 +1089,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 			dH2B[2 * mt] = mask_frag(acc, 0, H2B[2 * mt]);
 			if (2 * mt + 1 < HKS) dH2B[2 * mt + 1] = mask_frag(acc, 1, H2B[2 * mt + 1]);
 		}
-		if (valid) {
+		{  // dW_r1 += dH2 . H1^T
+			h8 TD[MT][2];
 #pragma unroll
-			for (int ks = 0; ks < HKS; ++ks) store_frag(tb.r1_delta, ld, i, dH2B[ks], ks, W, h);
-			store_frag(tb.r2_delta, ld, i, dOB, 0, 16, h);
+			for (int mt = 0; mt < MT; ++mt) transpose32(dH2B[2 * mt], 2 * mt + 1 < HKS ? dH2B[2 * mt + 1] : z8, 2 * mt + 1 < HKS, sel0, sel1, TD[mt]);
+#pragma unroll
+			for (int kt = 0; kt < MT; ++kt) {
+				h8 TX[2];
+				transpose32(H1B[2 * kt], 2 * kt + 1 < HKS ? H1B[2 * kt + 1] : z8, 2 * kt + 1 < HKS, sel0, sel1, TX);
+#pragma unroll
+				for (int mt = 0; mt < MT; ++mt) aR1[mt][kt] = wg_acc(TD[mt], TX, aR1[mt][kt]);
+			}
 		}
 #pragma unroll
 		for (int mt = 0; mt < MT; ++mt) {
@@ -1061,9 +1109,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 			dH1B[2 * mt] = mask_frag(acc, 0, H1B[2 * mt]);
 			if (2 * mt + 1 < HKS) dH1B[2 * mt + 1] = mask_frag(acc, 1, H1B[2 * mt + 1]);
 		}
-		if (valid) {
+		{  // dW_r0 += dH1 . rin^T
+			h8 TD[MT][2];
 #pragma unroll
-			for (int ks = 0; ks < HKS; ++ks) store_frag(tb.r0_delta, ld, i, dH1B[ks], ks, W, h);
+			for (int mt = 0; mt < MT; ++mt) transpose32(dH1B[2 * mt], 2 * mt + 1 < HKS ? dH1B[2 * mt + 1] : z8, 2 * mt + 1 < HKS, sel0, sel1, TD[mt]);
+#pragma unroll
+			for (int kt = 0; kt < 2; ++kt) {
+				h8 TX[2];
+				transpose32(rinB[2 * kt], kt == 0 ? rinB[1] : z8, kt == 0, sel0, sel1, TX);
+#pragma unroll
+				for (int mt = 0; mt < MT; ++mt) aR0[mt][kt] = wg_acc(TD[mt], TX, aR0[mt][kt]);
+			}
 		}
 		f16v dRin[2];
 #pragma unroll
@@ -1086,30 +1142,40 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 		v[0] += (float)dlo_lo[4] / tb.indeed_batch; v[1] += (float)dlo_lo[5] / tb.indeed_batch; v[2] += (float)dlo_lo[6] / tb.indeed_batch;
 		v[0] += (float)dlo_hi[0]; v[1] += (float)dlo_hi[1]; v[2] += (float)dlo_hi[2];
 		if (valid) {
-			store_acc(tb.d1_delta, ld2, i, dD1, 0, 16, h);
+			store_acc(tb.d1_delta, ld, i, dD1, 0, 16, h);
 			if (h == 0) tb.v[i] = make_float4(v[0], v[1], v[2], 0.f);
 			// dL/d(rgb input xyz rows 32..34) for the global-movement gradient (nerf_network.h:613-616)
 			if (tb.dpos && h == 0) tb.dpos[i] = make_float4(dRin[1][0], dRin[1][1], dRin[1][2], 0.f);
 		}
 	}
 	// variance gradient: batch sum of dL/dout[7] (nerf_network.h:461-474); per block here, the blocks in a fixed
-	// order in k_wgrad_reduce
+	// order in k_mlp_grad_reduce
 #pragma unroll
 	for (int off = 32; off > 0; off >>= 1) var_part += __shfl_xor(var_part, off);
 	__shared__ float s_var[4];
 	if (lane == 0) s_var[threadIdx.x >> 6] = var_part;
-	__syncthreads();
+	__syncthreads();  // (also: every wave is done with the staged weights; their LDS holds the dW reduction now)
 	if (threadIdx.x == 0) tb.var_partial[blockIdx.x] = (s_var[0] + s_var[1]) + (s_var[2] + s_var[3]);
+	float* red = (float*)sm;
+	float* prow = tb.wpartial + (size_t)blockIdx.x * tb.n_matrix;
+#pragma unroll
+	for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+		for (int kt = 0; kt < 2; ++kt) flush_tile(red, prow, aR0[mt][kt], tb.off_r0, W, 48, mt, kt);
+#pragma unroll
+		for (int kt = 0; kt < MT; ++kt) flush_tile(red, prow, aR1[mt][kt], tb.off_r1, W, W, mt, kt);
+		flush_tile(red, prow, aR2[mt], tb.off_r2, 16, W, 0, mt);
+	}
 }
 
 template <int L, int W>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) k_mlp_train_density(const uint32_t* __restrict__ n_valid_ptr, uint32_t n, uint32_t ld,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) k_mlp_train_density(const uint32_t* __restrict__ n_valid_ptr, uint32_t n, uint32_t ld,
                                                            const float* __restrict__ coords, const half_t* __restrict__ enc_h,
                                                            const float* __restrict__ dydx, MlpPtrs w, TrainBufs tb) {
 	constexpr int DIN = Dims<L>::DIN, DKS = Dims<L>::DKS, DMT = Dims<L>::DMT;
 	constexpr int MT = (W + 31) / 32, HKS = W / 16;
 	if (n_valid_ptr && *n_valid_ptr == 0) return;
-	__shared__ half_t sm[TrainSmem<L, W>::END];
+	__shared__ half_t sm[smem_halves(TrainSmem<L, W>::END)];  // (the end-of-kernel dW reduction reuses 16 KB of it)
 	using TS = TrainSmem<L, W>;
 	const FwdW fw0 = stage_fwd<L, W>(sm, w.d0, w.d0T, w);
 	stage_mat(sm + TS::D1T, w.d1T, W, 16);
@@ -1118,7 +1184,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 	const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
 	const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
 	const uint32_t n_waves = (gridDim.x * blockDim.x) >> 6;
-	const size_t ld2 = 2 * (size_t)ld;
+	const h8 sel0 = transpose_sel(0), sel1 = transpose_sel(1);
+	const h8 z8 = (h8){0, 0, 0, 0, 0, 0, 0, 0};
+	// dW accumulators: d0 [W][DIN], d1 [16][W] (first + second order)
+	f16v aD0[MT][DMT], aD1[MT];
+#pragma unroll
+	for (int mt = 0; mt < MT; ++mt) {
+		aD1[mt] = zero16();
+#pragma unroll
+		for (int kt = 0; kt < DMT; ++kt) aD0[mt][kt] = zero16();
+	}
 	for (uint32_t base = wave * 32; base < n; base += n_waves * 32) {
 		const uint32_t z = opaque_zero();
 		const FwdW fw = fw0.at(z);
@@ -1133,20 +1208,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 		h8 H0B[HKS], D1B, GhB[HKS];
 		f16v Gi[DMT];
 		density_forward_frag<L, W>(fw, dinB, r, h, H0B, D1B, GhB, Gi);
-		// weight-gradient / scatter operands stored as soon as they are final (shorter live ranges)
 		if (valid) {
-#pragma unroll
-			for (int ks = 0; ks < HKS; ++ks) {
-				store_frag(tb.d1_x, ld2, i, H0B[ks], ks, W, h);
-				store_frag(tb.d0_delta, ld2, ld + i, GhB[ks], ks, W, h);
-			}
-#pragma unroll
-			for (int ks = 0; ks < DKS; ++ks) store_frag(tb.d0_x, ld2, i, dinB[ks], ks, DIN, h);
-			{
-				h8 e0 = (h8){0, 0, 0, 0, 0, 0, 0, 0};
-				if (h == 0) e0[0] = (half_t)1.0f;
-				store_frag(tb.d1_delta, ld2, ld + i, e0, 0, 16, h);
-			}
 #pragma unroll
 			for (int mt = 0; mt < DMT; ++mt)
 #pragma unroll
@@ -1155,10 +1217,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 					if (k >= 3 && k < 3 + 2 * L) tb.genc[((size_t)((k - 3) >> 1) * ld + i) * 2 + ((k - 3) & 1)] = (half_t)Gi[mt][reg];  // [L][ld] half2
 				}
 		}
-		// delta_D1 from the colour kernel (d1_delta column i), B fragment in pi order
+		// delta_D1 from the colour kernel (d1_delta column i), B fragment in pi order (0 without a sample)
 		h8 dD1B;
 #pragma unroll
-		for (int j = 0; j < 8; ++j) dD1B[j] = tb.d1_delta[(size_t)(h ? pi_row(j, 1) : pi_row(j, 0)) * ld2 + ic];
+		for (int j = 0; j < 8; ++j) dD1B[j] = valid ? tb.d1_delta[(size_t)(h ? pi_row(j, 1) : pi_row(j, 0)) * ld + ic] : (half_t)0.f;
+		{  // dW_d1 (first order) += dD1 . H0^T
+			h8 TD[2];
+			transpose32(dD1B, z8, false, sel0, sel1, TD);
+#pragma unroll
+			for (int kt = 0; kt < MT; ++kt) {
+				h8 TX[2];
+				transpose32(H0B[2 * kt], 2 * kt + 1 < HKS ? H0B[2 * kt + 1] : z8, 2 * kt + 1 < HKS, sel0, sel1, TX);
+				aD1[kt] = wg_acc(TD, TX, aD1[kt]);
+			}
+		}
 		h8 dH0B[HKS];
 #pragma unroll
 		for (int mt = 0; mt < MT; ++mt) {
@@ -1166,9 +1238,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 			dH0B[2 * mt] = mask_frag(acc, 0, H0B[2 * mt]);
 			if (2 * mt + 1 < HKS) dH0B[2 * mt + 1] = mask_frag(acc, 1, H0B[2 * mt + 1]);
 		}
-		if (valid) {
+		{  // dW_d0 (first order) += dH0 . din^T
+			h8 TD[MT][2];
 #pragma unroll
-			for (int ks = 0; ks < HKS; ++ks) store_frag(tb.d0_delta, ld2, i, dH0B[ks], ks, W, h);
+			for (int mt = 0; mt < MT; ++mt) transpose32(dH0B[2 * mt], 2 * mt + 1 < HKS ? dH0B[2 * mt + 1] : z8, 2 * mt + 1 < HKS, sel0, sel1, TD[mt]);
+#pragma unroll
+			for (int kt = 0; kt < DMT; ++kt) {
+				h8 TX[2];
+				transpose32(dinB[2 * kt], 2 * kt + 1 < DKS ? dinB[2 * kt + 1] : z8, 2 * kt + 1 < DKS, sel0, sel1, TX);
+#pragma unroll
+				for (int mt = 0; mt < MT; ++mt) aD0[mt][kt] = wg_acc(TD[mt], TX, aD0[mt][kt]);
+			}
 		}
 		f16v dDin[DMT];
 #pragma unroll
@@ -1228,11 +1308,36 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 			H1pB[2 * mt] = mask_frag(acc, 0, H0B[2 * mt]);
 			if (2 * mt + 1 < HKS) H1pB[2 * mt + 1] = mask_frag(acc, 1, H0B[2 * mt + 1]);
 		}
+		{  // second order (fully_fused_mlp.cu:1088-1198): dW_d0 += b2 . u^T with b2 = relu'(H0) . W1d^T e0 (= GhB)
+			h8 TD[MT][2];
+#pragma unroll
+			for (int mt = 0; mt < MT; ++mt) {
+				const h8 g0 = valid ? GhB[2 * mt] : z8;
+				const h8 g1 = (2 * mt + 1 < HKS && valid) ? GhB[2 * mt + 1] : z8;
+				transpose32(g0, g1, 2 * mt + 1 < HKS, sel0, sel1, TD[mt]);
+			}
+#pragma unroll
+			for (int kt = 0; kt < DMT; ++kt) {
+				h8 TX[2];
+				transpose32(uB[2 * kt], 2 * kt + 1 < DKS ? uB[2 * kt + 1] : z8, 2 * kt + 1 < DKS, sel0, sel1, TX);
+#pragma unroll
+				for (int mt = 0; mt < MT; ++mt) aD0[mt][kt] = wg_acc(TD[mt], TX, aD0[mt][kt]);
+			}
+		}
+		{  // and dW_d1 += e0 . h1'^T: row 0 (this lane's column 0) collects the samples' h1', one per valid sample
+			h8 TD[2];
+#pragma unroll
+			for (int q = 0; q < 2; ++q)
+#pragma unroll
+				for (int j = 0; j < 8; ++j) TD[q][j] = (r == 0 && base + acc_row(8 * q + j, h) < n) ? (half_t)1.0f : (half_t)0.0f;
+#pragma unroll
+			for (int kt = 0; kt < MT; ++kt) {
+				h8 TX[2];
+				transpose32(H1pB[2 * kt], 2 * kt + 1 < HKS ? H1pB[2 * kt + 1] : z8, 2 * kt + 1 < HKS, sel0, sel1, TX);
+				aD1[kt] = wg_acc(TD, TX, aD1[kt]);
+			}
+		}
 		if (valid) {
-#pragma unroll
-			for (int ks = 0; ks < HKS; ++ks) store_frag(tb.d1_x, ld2, ld + i, H1pB[ks], ks, W, h);
-#pragma unroll
-			for (int ks = 0; ks < DKS; ++ks) store_frag(tb.d0_x, ld2, ld + i, uB[ks], ks, DIN, h);
 			if (tb.dpos && h == 0) {
 				const float4 rg = tb.dpos[i];
 				tb.dpos[i] = make_float4((pg[0] + rg.x) + pd[0], (pg[1] + rg.y) + pd[1], (pg[2] + rg.z) + pd[2], 0.f);
@@ -1247,133 +1352,245 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 				}
 		}
 	}
+	__syncthreads();  // every wave is done with the staged weights: their LDS holds the dW reduction
+	float* red = (float*)sm;
+	float* prow = tb.wpartial + (size_t)blockIdx.x * tb.n_matrix;
+#pragma unroll
+	for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+		for (int kt = 0; kt < DMT; ++kt) flush_tile(red, prow, aD0[mt][kt], 0u, W, DIN, mt, kt);
+		flush_tile(red, prow, aD1[mt], tb.off_d1, 16, W, 0, mt);
+	}
 }
 
-// ------------------------------------------------------------------------------------------
-// Weight gradients: dW[M][K] += sum_n D[M][n] X[K][n] over the batch (split-K over samples),
-// MFMA with natural k order (k = sample), fp32 accumulation, one atomic flush per block.
-// ------------------------------------------------------------------------------------------
-
-// A chunk (64 samples) of a wave's D and X rows is fetched cooperatively, row-contiguous (lane l: row l / 8 + 8 q,
-// 16 B segment l % 8: 8 lines per load instruction) and staged in LDS; the MFMA operands (lane (r, h): row r, the
-// chunk's samples 32 h + 8 u .. + 7) are read back from LDS. Fetching them straight from global memory put 64 lines
-// behind every load instruction and kept the texture-address unit ~75 % busy. The next chunk's fetch is in flight
-// while the current one runs; four accumulators (k-step u into acc[u]) keep independent MFMAs in flight.
-__global__ void __launch_bounds__(256) k_wgrad(WGradJobs jobs) {
-	constexpr int LDR = 64 + 8;  // LDS row stride (halves)
-	__shared__ half_t s_op[4][2][32 * LDR];
-	float (*red)[32 * 32] = (float (*)[32 * 32])s_op;  // reused after the loop (4 x 4 KB <= 4 x 9 KB)
-	if (jobs.n_valid && *jobs.n_valid == 0) return;
-	uint32_t b = blockIdx.x, ji = 0;
-	while (ji + 1 < jobs.n_jobs && b >= jobs.block_start[ji + 1]) ++ji;
-	const WGradJob J = jobs.j[ji];
-	b -= jobs.block_start[ji];
-	const uint32_t tiles = J.tiles_m * J.tiles_k;
-	// XCD-aware order: the tiles of one sample split read the same D / X rows, so they go to blocks of one XCD
-	// (blockIdx mod 8; consecutive blockIdx land on different XCDs) and share its L2. The partial keeps its
-	// logical slot (split-major), so k_wgrad_reduce and its summation order are unchanged.
-	const uint32_t n_split = (J.ncols + jobs.split - 1) / jobs.split;
-	if (tiles > 1 && (n_split & 7) == 0 && (jobs.block_start[ji] & 7) == 0) {
-		const uint32_t x = b & 7, slot = b >> 3;
-		b = ((slot / tiles) * 8 + x) * tiles + slot % tiles;
-	}
-	const uint32_t tile = b % tiles, sp = b / tiles;
-	const uint32_t mt = tile / J.tiles_k, kt = tile % J.tiles_k;
-	const uint32_t n0 = sp * jobs.split, n1 = min(J.ncols, n0 + jobs.split);
-	const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
-	// loader view: rows lr + 8 q (q = 0..3), 16 B segment ls of the chunk's 128 B
-	const int lr = lane >> 3, ls = lane & 7;
-	const char* Db = (const char*)J.D;
-	const char* Xb = (const char*)J.X;
-	uint32_t offD[4], offX[4];
-	bool okD[4], okX[4];
-#pragma unroll
-	for (int q = 0; q < 4; ++q) {
-		const uint32_t rm = 32 * mt + lr + 8 * q, rk = 32 * kt + lr + 8 * q;
-		okD[q] = rm < J.M; okX[q] = rk < J.K;
-		offD[q] = (rm * J.ldc + 8 * ls) * 2;  // byte offsets (operand buffers < 4 GB)
-		offX[q] = (rk * J.ldc + 8 * ls) * 2;
-	}
-	const h8 z8 = (h8){0, 0, 0, 0, 0, 0, 0, 0};
-	auto fetch = [&](uint32_t nb, h8 (&d)[4], h8 (&x)[4]) {
-#pragma unroll
-		for (int q = 0; q < 4; ++q) {
-			d[q] = okD[q] ? *(const h8*)(Db + offD[q] + 2 * nb) : z8;
-			x[q] = okX[q] ? *(const h8*)(Xb + offX[q] + 2 * nb) : z8;
-		}
-	};
-	half_t* sD = s_op[wv][0];
-	half_t* sX = s_op[wv][1];
-	f16v acc[4] = {zero16(), zero16(), zero16(), zero16()};
-	uint32_t nb = n0 + 64 * wv;
-	h8 d[4], x[4];
-	if (nb + 64 <= n1) fetch(nb, d, x);
-	for (; nb + 64 <= n1; nb += 256) {
-		__builtin_amdgcn_wave_barrier();
-#pragma unroll
-		for (int q = 0; q < 4; ++q) {
-			*(h8*)(sD + (lr + 8 * q) * LDR + 8 * ls) = d[q];
-			*(h8*)(sX + (lr + 8 * q) * LDR + 8 * ls) = x[q];
-		}
-		__builtin_amdgcn_wave_barrier();
-		if (nb + 256 + 64 <= n1) fetch(nb + 256, d, x);
-#pragma unroll
-		for (int u = 0; u < 4; ++u) {
-			const h8 a = *(const h8*)(sD + r * LDR + 32 * h + 8 * u);
-			const h8 bb = *(const h8*)(sX + r * LDR + 32 * h + 8 * u);
-			acc[u] = mfma(a, bb, acc[u]);
-		}
-	}
-	__syncthreads();  // every wave is done with its staging rows before they hold the partials
-#pragma unroll
-	for (int reg = 0; reg < 16; ++reg) red[wv][acc_row(reg, h) * 32 + r] = (acc[0][reg] + acc[1][reg]) + (acc[2][reg] + acc[3][reg]);
-	__syncthreads();
-	float* out = jobs.partial + (size_t)(jobs.block_start[ji] + b) * 1024;
-	for (uint32_t e = threadIdx.x; e < 1024; e += 256) out[e] = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
-}
-
-// dW = each tile's split partials summed in a fixed order. Block = (job, tile, 64-element chunk of the tile);
-// its four waves sum the splits sp = g, g + 4, ... (g = wave) in order, then the four partial sums are added in
-// wave order. The block after the last tile sums the colour kernel's per-block variance partials in block order.
-constexpr uint32_t WR_CHUNKS = 1024 / 64;
-__global__ void __launch_bounds__(256) k_wgrad_reduce(WGradJobs jobs) {
-	const bool none = jobs.n_valid && *jobs.n_valid == 0;  // no samples: the gradients are zero (k_wgrad wrote nothing)
-	__shared__ float s_part[4][64];
-	uint32_t b = blockIdx.x / WR_CHUNKS, ji = 0, tile_base = 0;
-	const uint32_t chunk = blockIdx.x % WR_CHUNKS;
-	for (; ji < jobs.n_jobs; ++ji) {
-		const uint32_t t = jobs.j[ji].tiles_m * jobs.j[ji].tiles_k;
-		if (b < tile_base + t) break;
-		tile_base += t;
-	}
-	if (ji == jobs.n_jobs) {
-		if (chunk != 0) return;
+// dW = the blocks' partial rows summed in a fixed order: a workgroup owns 64 parameters, its four waves sum the rows
+// b = g, g + 4, ... (g = wave) with four interleaved chains each (16 independent loads in flight per lane), and the four
+// wave sums are added in wave order. The workgroup after the last one sums the colour kernel's per-block variance
+// partials in block order.
+__global__ void __launch_bounds__(256) k_mlp_grad_reduce(MlpGradReduce rd) {
+	const bool none = rd.n_valid && *rd.n_valid == 0;  // no samples: the gradients are zero (the training kernels wrote nothing)
+	const uint32_t nblk_p = (rd.n_matrix + 63) / 64;
+	if (blockIdx.x == nblk_p) {
 		// fixed-order tree: thread t sums the partials t, t + 256, ..., then a pairwise tree over the threads
 		__shared__ float s_v[256];
 		float v = 0.f;
-		for (uint32_t k = threadIdx.x; k < jobs.var_blocks && !none; k += 256) v += jobs.var_partial[k];
+		for (uint32_t k = threadIdx.x; k < rd.var_blocks && !none; k += 256) v += rd.var_partial[k];
 		s_v[threadIdx.x] = v;
 		__syncthreads();
 		for (uint32_t off = 128; off > 0; off >>= 1) {
 			if (threadIdx.x < off) s_v[threadIdx.x] += s_v[threadIdx.x + off];
 			__syncthreads();
 		}
-		if (threadIdx.x == 0) *jobs.var_grad = s_v[0];
+		if (threadIdx.x == 0 && rd.var_grad) *rd.var_grad = s_v[0];
 		return;
 	}
-	const WGradJob J = jobs.j[ji];
-	const uint32_t tiles = J.tiles_m * J.tiles_k, tile = b - tile_base;
-	const uint32_t mt = tile / J.tiles_k, kt = tile % J.tiles_k;
-	const uint32_t n_split = (J.ncols + jobs.split - 1) / jobs.split;
-	const uint32_t g = threadIdx.x >> 6, e = chunk * 64 + (threadIdx.x & 63);
-	float acc = 0.f;
-	for (uint32_t sp = g; sp < n_split && !none; sp += 4) acc += jobs.partial[(size_t)(jobs.block_start[ji] + sp * tiles + tile) * 1024 + e];
-	s_part[g][threadIdx.x & 63] = acc;
+	__shared__ float s_part[4][64];
+	const uint32_t p = blockIdx.x * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
+	float a[4] = {0.f, 0.f, 0.f, 0.f};
+	if (!none && p < rd.n_matrix) {
+		const float* src = rd.partial + p;
+		const size_t stride = rd.n_matrix;
+		uint32_t b = g;
+		for (; b + 12 < rd.n_blocks; b += 16) {
+#pragma unroll
+			for (int q = 0; q < 4; ++q) a[q] += src[(size_t)(b + 4 * q) * stride];
+		}
+		for (int q = 0; b < rd.n_blocks; b += 4, q = (q + 1) & 3) a[q] += src[(size_t)b * stride];
+	}
+	s_part[g][threadIdx.x & 63] = (a[0] + a[1]) + (a[2] + a[3]);
 	__syncthreads();
-	if (g == 0) {
-		const uint32_t m = 32 * mt + e / 32, k = 32 * kt + e % 32;
-		const uint32_t l = threadIdx.x & 63;
-		if (m < J.M && k < J.K) J.dW[(size_t)m * J.K + k] = (s_part[0][l] + s_part[1][l]) + (s_part[2][l] + s_part[3][l]);
+	if (g == 0 && p < rd.n_matrix) {
+		const uint32_t l = threadIdx.x;
+		rd.g[p] = (s_part[0][l] + s_part[1][l]) + (s_part[2][l] + s_part[3][l]);
+	}
+}
+
+// ------------------------------------------------------------------------------------------
+// tcnn NetworkWithInputEncoding(HashGrid -> FullyFusedMLP, 1 hidden ReLU layer, linear 16-wide output) for the
+// operator module (network_with_input_encoding.h:84-250; fully_fused_mlp.cu:678-812 forward, :967-1085 backward,
+// :1088-1198 backward_backward_input). The MLP input is the encoding alone, padded to DE = next multiple of 16 of 2L
+// (NetworkWithInputEncoding::set_alignment): logical row k = feature k of the paired encoding [L][n] half2.
+//   MODE 0 forward : out [n][16] fp16 (the cpp::Module column-major view)
+//   MODE 1 backward: dH0 = relu'(H0) . W1^T dL; dL/denc = W0^T dH0 -> paired; dW1 += dL H0^T, dW0 += dH0 din^T
+//   MODE 2 bwd-bwd : b2 = relu'(H0) . W1^T dL; h1' = relu'(H0) . W0 u (u = dy/dx . dL_ddLdinput, paired);
+//                    dW0 += b2 u^T, dW1 += dL h1'^T; g = W0^T b2 -> paired (the encoding's second-order operand)
+// Weight gradients as in the training kernels: in registers, one partial row per block (k_mlp_grad_reduce).
+// ------------------------------------------------------------------------------------------
+template <int L> struct DimsE {
+	static constexpr int DE = (2 * L + 15) / 16 * 16, DKS = DE / 16, DMT = (DE + 31) / 32;
+};
+template <int L, int W> struct DNetSmem {
+	static constexpr int DE = DimsE<L>::DE;
+	static constexpr int W0 = 0, W0T = W0 + W * (DE + 8), W1 = W0T + DE * (W + 8), W1T = W1 + 16 * (W + 8), END = W1T + W * (16 + 8);
+};
+template <int L>
+__device__ __forceinline__ void build_din_enc(h8* dinB, const uint32_t* __restrict__ enc, uint32_t ld, uint32_t i, int h) {
+	constexpr int DKS = DimsE<L>::DKS;
+#pragma unroll
+	for (int ks = 0; ks < DKS; ++ks)
+#pragma unroll
+		for (int j = 0; j < 8; ++j) {
+			const int k = 16 * ks + (h ? pi_row(j, 1) : pi_row(j, 0));
+			half_t v = (half_t)0.f;
+			if (k < 2 * L) { const uint32_t u = enc[(size_t)(k >> 1) * ld + i]; v = __builtin_bit_cast(h2, u)[k & 1]; }
+			dinB[ks][j] = v;
+		}
+}
+// a DE-row accumulator set (rows 32 mt + acc_row) -> paired [L][ld] half2, rows < 2L
+template <int L>
+__device__ __forceinline__ void store_paired(uint32_t* out, uint32_t ld, uint32_t i, const f16v* a, int h) {
+	constexpr int DMT = DimsE<L>::DMT;
+	half_t* o = (half_t*)out;
+#pragma unroll
+	for (int mt = 0; mt < DMT; ++mt)
+#pragma unroll
+		for (int reg = 0; reg < 16; ++reg) {
+			const int k = 32 * mt + acc_row(reg, h);
+			if (k < 2 * L) o[((size_t)(k >> 1) * ld + i) * 2 + (k & 1)] = (half_t)a[mt][reg];
+		}
+}
+struct DNetArgs {
+	const half_t* w0; const half_t* w1;     // [W][DE], [16][W] fp16 (the module's parameters)
+	const uint32_t* enc;                    // paired [L][n]
+	const half_t* dL;                       // [n][16] fp16 (modes 1, 2)
+	const uint32_t* u;                      // paired [L][n] (mode 2)
+	half_t* out;                            // [n][16] (mode 0)
+	uint32_t* denc;                         // paired [L][n] (modes 1, 2)
+	float* wpartial;                        // [blocks][W DE + 16 W] (modes 1, 2)
+};
+template <int L, int W, int MODE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) k_dnet(uint32_t n, DNetArgs a) {
+	constexpr int DE = DimsE<L>::DE, DKS = DimsE<L>::DKS, DMT = DimsE<L>::DMT;
+	constexpr int MT = (W + 31) / 32, HKS = W / 16;
+	using S = DNetSmem<L, W>;
+	__shared__ half_t sm[smem_halves(S::END)];
+	stage_mat(sm + S::W0, a.w0, W, DE);
+	stage_mat(sm + S::W1, a.w1, 16, W);
+	for (uint32_t e = threadIdx.x; e < (uint32_t)(W * DE); e += blockDim.x) {  // transposed copies
+		const uint32_t r = e / DE, c = e % DE;
+		sm[S::W0T + c * (W + 8) + r] = a.w0[e];
+	}
+	for (uint32_t e = threadIdx.x; e < (uint32_t)(16 * W); e += blockDim.x) {
+		const uint32_t r = e / W, c = e % W;
+		sm[S::W1T + c * (16 + 8) + r] = a.w1[e];
+	}
+	__syncthreads();
+	const MatRef W0r{sm + S::W0, DE + 8}, W0Tr{sm + S::W0T, W + 8}, W1r{sm + S::W1, W + 8}, W1Tr{sm + S::W1T, 16 + 8};
+	const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+	const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, n_waves = (gridDim.x * blockDim.x) >> 6;
+	const h8 sel0 = transpose_sel(0), sel1 = transpose_sel(1);
+	const h8 z8 = (h8){0, 0, 0, 0, 0, 0, 0, 0};
+	f16v aW0[MT][DMT], aW1[MT];
+#pragma unroll
+	for (int mt = 0; mt < MT; ++mt) {
+		aW1[mt] = zero16();
+#pragma unroll
+		for (int kt = 0; kt < DMT; ++kt) aW0[mt][kt] = zero16();
+	}
+	for (uint32_t base = wave * 32; base < n; base += n_waves * 32) {
+		const uint32_t z = opaque_zero();
+		const MatRef w0 = rebase(W0r, z), w0T = rebase(W0Tr, z), w1 = rebase(W1r, z), w1T = rebase(W1Tr, z);
+		const uint32_t i = base + r;
+		const bool valid = i < n;
+		const uint32_t ic = valid ? i : 0;
+		h8 dinB[DKS];
+		build_din_enc<L>(dinB, a.enc, n, ic, h);
+		h8 H0B[HKS];
+#pragma unroll
+		for (int mt = 0; mt < MT; ++mt) {
+			f16v acc = zero16();
+#pragma unroll
+			for (int ks = 0; ks < DKS; ++ks) acc = mfma(loadA(w0, W, 32 * mt + r, 16 * ks, h), dinB[ks], acc);
+			H0B[2 * mt] = frag<true>(acc, 0);
+			if (2 * mt + 1 < HKS) H0B[2 * mt + 1] = frag<true>(acc, 1);
+		}
+		if (MODE == 0) {
+			f16v acc = zero16();
+#pragma unroll
+			for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w1, 16, r, 16 * ks, h), H0B[ks], acc);
+			if (valid)
+#pragma unroll
+				for (int reg = 0; reg < 8; ++reg) a.out[(size_t)i * 16 + acc_row(reg, h)] = (half_t)acc[reg];
+			continue;
+		}
+		// dL [n][16] as a B fragment (rows pi_row(j, h)); 0 without a sample
+		h8 dLB;
+#pragma unroll
+		for (int j = 0; j < 8; ++j) dLB[j] = valid ? a.dL[(size_t)ic * 16 + (h ? pi_row(j, 1) : pi_row(j, 0))] : (half_t)0.f;
+		h8 dHB[HKS];  // relu'(H0) . W1^T dL (MODE 1: dH0; MODE 2: b2)
+#pragma unroll
+		for (int mt = 0; mt < MT; ++mt) {
+			const f16v acc = mfma(loadA(w1T, W, 32 * mt + r, 0, h), dLB, zero16());
+			dHB[2 * mt] = mask_frag(acc, 0, H0B[2 * mt]);
+			if (2 * mt + 1 < HKS) dHB[2 * mt + 1] = mask_frag(acc, 1, H0B[2 * mt + 1]);
+		}
+		// W0^T dHB -> paired (MODE 1: dL/denc; MODE 2: the encoding's second-order g)
+		f16v dDin[DMT];
+#pragma unroll
+		for (int mt = 0; mt < DMT; ++mt) {
+			f16v acc = zero16();
+#pragma unroll
+			for (int ks = 0; ks < HKS; ++ks) acc = mfma(loadA(w0T, DE, 32 * mt + r, 16 * ks, h), dHB[ks], acc);
+			dDin[mt] = acc;
+		}
+		if (valid) store_paired<L>(a.denc, n, i, dDin, h);
+		h8 TDL[2];
+		transpose32(dLB, z8, false, sel0, sel1, TDL);
+		h8 TDH[MT][2];
+#pragma unroll
+		for (int mt = 0; mt < MT; ++mt) transpose32(dHB[2 * mt], 2 * mt + 1 < HKS ? dHB[2 * mt + 1] : z8, 2 * mt + 1 < HKS, sel0, sel1, TDH[mt]);
+		if (MODE == 1) {
+			// dW1 += dL H0^T, dW0 += dH0 din^T
+#pragma unroll
+			for (int kt = 0; kt < MT; ++kt) {
+				h8 TX[2];
+				transpose32(H0B[2 * kt], 2 * kt + 1 < HKS ? H0B[2 * kt + 1] : z8, 2 * kt + 1 < HKS, sel0, sel1, TX);
+				aW1[kt] = wg_acc(TDL, TX, aW1[kt]);
+			}
+#pragma unroll
+			for (int kt = 0; kt < DMT; ++kt) {
+				h8 TX[2];
+				transpose32(dinB[2 * kt], 2 * kt + 1 < DKS ? dinB[2 * kt + 1] : z8, 2 * kt + 1 < DKS, sel0, sel1, TX);
+#pragma unroll
+				for (int mt = 0; mt < MT; ++mt) aW0[mt][kt] = wg_acc(TDH[mt], TX, aW0[mt][kt]);
+			}
+		} else {
+			h8 uB[DKS];
+			build_din_enc<L>(uB, a.u, n, ic, h);
+			h8 H1pB[HKS];
+#pragma unroll
+			for (int mt = 0; mt < MT; ++mt) {
+				f16v acc = zero16();
+#pragma unroll
+				for (int ks = 0; ks < DKS; ++ks) acc = mfma(loadA(w0, W, 32 * mt + r, 16 * ks, h), uB[ks], acc);
+				H1pB[2 * mt] = mask_frag(acc, 0, H0B[2 * mt]);
+				if (2 * mt + 1 < HKS) H1pB[2 * mt + 1] = mask_frag(acc, 1, H0B[2 * mt + 1]);
+			}
+			// dW0 += b2 u^T, dW1 += dL h1'^T
+#pragma unroll
+			for (int kt = 0; kt < DMT; ++kt) {
+				h8 TX[2];
+				transpose32(uB[2 * kt], 2 * kt + 1 < DKS ? uB[2 * kt + 1] : z8, 2 * kt + 1 < DKS, sel0, sel1, TX);
+#pragma unroll
+				for (int mt = 0; mt < MT; ++mt) aW0[mt][kt] = wg_acc(TDH[mt], TX, aW0[mt][kt]);
+			}
+#pragma unroll
+			for (int kt = 0; kt < MT; ++kt) {
+				h8 TX[2];
+				transpose32(H1pB[2 * kt], 2 * kt + 1 < HKS ? H1pB[2 * kt + 1] : z8, 2 * kt + 1 < HKS, sel0, sel1, TX);
+				aW1[kt] = wg_acc(TDL, TX, aW1[kt]);
+			}
+		}
+	}
+	if (MODE == 0) return;
+	__syncthreads();
+	float* red = (float*)sm;
+	float* prow = a.wpartial + (size_t)blockIdx.x * (W * DE + 16 * W);
+#pragma unroll
+	for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+		for (int kt = 0; kt < DMT; ++kt) flush_tile(red, prow, aW0[mt][kt], 0u, W, DE, mt, kt);
+		flush_tile(red, prow, aW1[mt], (uint32_t)(W * DE), 16, W, 0, mt);
 	}
 }
 
@@ -1471,12 +1688,8 @@ void launch_mlp_train(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_v
 	NEUS_MLP_CONFIGS(X)
 #undef X
 }
-void launch_wgrad(hipStream_t s, const WGradJobs& jobs, uint32_t n_blocks) {
-	if (!n_blocks) return;
-	k_wgrad<<<n_blocks, 256, 0, s>>>(jobs);
-	uint32_t tiles = 0;
-	for (uint32_t k = 0; k < jobs.n_jobs; ++k) tiles += jobs.j[k].tiles_m * jobs.j[k].tiles_k;
-	k_wgrad_reduce<<<(tiles + 1) * WR_CHUNKS, 256, 0, s>>>(jobs);
+void launch_mlp_grad_reduce(hipStream_t s, const MlpGradReduce& r) {
+	k_mlp_grad_reduce<<<(r.n_matrix + 63) / 64 + 1, 256, 0, s>>>(r);
 }
 // persistent grid: at most the resident capacity of the two training kernels, so the ~53 KB weight staging runs
 // once per block (one wave per SIMD: a grid of n / 128 blocks re-staged the weights for every 128 samples)
@@ -1491,5 +1704,27 @@ uint32_t mlp_train_blocks(uint32_t L, uint32_t W, uint32_t n) {
 	return std::max<uint32_t>(1, std::min<uint32_t>((n + 127) / 128, cap));
 }
 void launch_mfma_probe(hipStream_t s, const half_t* A, const half_t* B, float* C) { k_mfma_probe<<<1, 64, 0, s>>>(A, B, C); }
+
+#define NEUS_DNET_CONFIGS(X) X(1, 16) X(1, 64) X(2, 64) X(4, 64) X(8, 64) X(14, 64) X(16, 64)
+bool dnet_supported(uint32_t L, uint32_t W) {
+#define X(l, w) if (L == l && W == w) return true;
+	NEUS_DNET_CONFIGS(X)
+#undef X
+	return false;
+}
+uint32_t dnet_blocks(uint32_t n) { return std::max<uint32_t>(1, std::min<uint32_t>((n + 127) / 128, 512)); }
+void launch_dnet(hipStream_t s, uint32_t L, uint32_t W, int mode, uint32_t n, const DNetLaunch& d) {
+	if (n == 0) return;
+	DNetArgs a{d.w0, d.w1, d.enc, d.dL, d.u, d.out, d.denc, d.wpartial};
+	const uint32_t blocks = dnet_blocks(n);
+#define X(l, w_) if (L == l && W == w_) { \
+		if (mode == 0) k_dnet<l, w_, 0><<<blocks, 256, 0, s>>>(n, a); \
+		else if (mode == 1) k_dnet<l, w_, 1><<<blocks, 256, 0, s>>>(n, a); \
+		else k_dnet<l, w_, 2><<<blocks, 256, 0, s>>>(n, a); \
+		return; }
+	NEUS_DNET_CONFIGS(X)
+#undef X
+	throw std::runtime_error("density network module: unsupported (n_levels, n_neurons)");
+}
 
 } // namespace neus

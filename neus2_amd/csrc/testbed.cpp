@@ -216,7 +216,8 @@ struct NeusTestbed {
 	Dev<float> dydx;
 	Dev<half_t> net_out, dL_dout, trainbuf;
 	Dev<float4> vbuf;
-	Dev<float> wgrad_partial, var_partial;  // weight-gradient split partials, per-block variance sums
+	Dev<float> wgrad_partial, var_partial;  // per-block MLP weight-gradient rows, per-block variance sums
+	uint32_t mlp_blocks = 0;                // grid of the training MLP kernels at the batch capacity
 	Dev<uint8_t> scan_tmp;
 	size_t scan_tmp_bytes = 0;
 	Dev<StepState> st;
@@ -370,14 +371,17 @@ struct NeusTestbed {
 	// initial parameters (trainer.h:54-109): seed_seq{seed} -> pcg32; xavier MLPs (the density MLP replaced by
 	// `geo` when given), hash grid U(-1e-4, 1e-4), variance 0.3
 	std::vector<float> initial_params(uint32_t seed, const float* geo) const {
+		std::seed_seq seq{seed};
+		std::vector<uint32_t> seeds(2);
+		seq.generate(seeds.begin(), seeds.end());
+		return initial_params_rng(make_pcg32(seeds.front()), geo);
+	}
+	// NerfNetwork::initialize_params (nerf_network.h:741-886) drawing from `rnd`
+	std::vector<float> initial_params_rng(pcg32 rnd, const float* geo) const {
 		const Layout& l = lay;
 		const uint32_t P = l.P;
 		std::vector<float> h(P, 0.f);
 		{
-			std::seed_seq seq{seed};
-			std::vector<uint32_t> seeds(2);
-			seq.generate(seeds.begin(), seeds.end());
-			pcg32 rnd = make_pcg32(seeds.front());
 			auto xavier = [&](uint32_t off, uint32_t out, uint32_t in) {
 				const float scale = std::sqrt(6.0f / (float)(in + out));
 				for (uint32_t i = 0; i < out * in; ++i) h[off + i] = rnd.next_float() * 2.0f * scale - scale;
@@ -469,28 +473,32 @@ struct NeusTestbed {
 		batch = c.batch_size;
 		max_samples = batch * 16;  // testbed_nerf.cu:3725
 		enc.alloc((size_t)l.L * batch); dydx.alloc((size_t)6 * l.L * batch);  // training batch only: inference fuses the encode
-		const size_t ld = batch, ld2 = 2 * ld;
-		const size_t tb_elems = (size_t)l.W * ld2 + (size_t)l.din * ld2 + 16 * ld2 + (size_t)l.W * ld2 + (size_t)l.W * ld + 48 * ld +
-		                        2 * (size_t)l.W * ld + 16 * ld + (size_t)l.W * ld + 2 * (size_t)l.L * ld * 2 + 64;
-		trainbuf.alloc(tb_elems);
+		const size_t ld = batch;
+		trainbuf.alloc(16 * ld + 2 * (2 * (size_t)l.L * ld) + 64);
 		vbuf.alloc(batch);
 		half_t* q = trainbuf.p;
 		auto take = [&](size_t k) { half_t* r = q; q += (k + 7) / 8 * 8; return r; };
-		tbuf.d0_delta = take((size_t)l.W * ld2); tbuf.d0_x = take((size_t)l.din * ld2);
-		tbuf.d1_delta = take(16 * ld2); tbuf.d1_x = take((size_t)l.W * ld2);
-		tbuf.r0_delta = take((size_t)l.W * ld); tbuf.r0_x = take(48 * ld);
-		tbuf.r1_delta = take((size_t)l.W * ld); tbuf.r1_x = take((size_t)l.W * ld);
-		tbuf.r2_delta = take(16 * ld); tbuf.r2_x = take((size_t)l.W * ld);
+		tbuf = TrainBufs{};
+		tbuf.d1_delta = take(16 * ld);
 		tbuf.dLdenc = take(2 * (size_t)l.L * ld); tbuf.genc = take(2 * (size_t)l.L * ld);
 		tbuf.v = vbuf.p;
 		tbuf.var_grad = grads.p + l.var_off;
-		var_partial.alloc(mlp_train_blocks(l.L, l.W, batch));
+		mlp_blocks = mlp_train_blocks(l.L, l.W, batch);
+		var_partial.alloc(mlp_blocks);
 		tbuf.var_partial = var_partial.p;
-		wgrad_partial.alloc((size_t)wgrad_jobs(batch, batch, grads.p, nullptr).block_start[5] * 1024);
+		// one row of MLP weight-gradient partials per training-kernel block
+		wgrad_partial.alloc((size_t)mlp_blocks * l.n_matrix);
+		tbuf.wpartial = wgrad_partial.p;
+		tbuf.n_matrix = l.n_matrix; tbuf.off_d1 = l.off_d1; tbuf.off_r0 = l.off_r0; tbuf.off_r1 = l.off_r1; tbuf.off_r2 = l.off_r2;
 		tbuf.indeed_batch = (float)batch * (float)world;
 		// binned grid-gradient scatter workspace (grid.hip)
 		swork = ScatterWork{};
 		swork.n_blocks = (batch + 255) / 256;
+		// wide-block binning: 512-sample workgroups (NEUS_SCATTER_CHUNK=1024: 1024-sample ones)
+		{ const char* e = std::getenv("NEUS_SCATTER_CHUNK"); swork.chunk = (e && std::string(e) == "1024") ? 1024u : 512u; }
+		swork.n_chunks = (batch + swork.chunk - 1) / swork.chunk;
+		// NEUS_SCATTER=binned selects the 256-sample histogram / scan / bin path (bitwise A/B reference of the wide one)
+		{ const char* e = std::getenv("NEUS_SCATTER"); swork.mode = (e && std::string(e) == "binned") ? 1u : 0u; }
 		swork.n_buckets = scatter_n_buckets(gl);
 		if (swork.n_buckets > SB_MAX_BUCKETS) throw std::runtime_error("hash grid too large for the scatter buckets");
 		const size_t n_bins = (size_t)swork.n_buckets * swork.n_blocks + 1;
@@ -699,31 +707,12 @@ struct NeusTestbed {
 		const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((n_cap + 127) / 128, 8192));
 		launch_nerf_infer(s, lay.L, lay.W, n_ptr, n_fixed, c, gl, valid, params_h.p + lay.grid_off, mlp, out, blocks);
 	}
-	WGradJobs wgrad_jobs(uint32_t n, uint32_t ld, float* g, const uint32_t* n_valid) {
-		const Layout& l = lay;
-		WGradJobs J{};
-		auto job = [&](int k, const half_t* D, const half_t* X, uint32_t off, uint32_t M, uint32_t K, uint32_t ncols, uint32_t ldc) {
-			J.j[k] = {D, X, g + off, M, K, ncols, ldc, (M + 31) / 32, (K + 31) / 32};
-		};
-		job(0, tbuf.d0_delta, tbuf.d0_x, l.off_d0, l.W, l.din, 2 * ld, 2 * ld);
-		job(1, tbuf.d1_delta, tbuf.d1_x, l.off_d1, 16, l.W, 2 * ld, 2 * ld);
-		job(2, tbuf.r0_delta, tbuf.r0_x, l.off_r0, l.W, 48, ld, ld);
-		job(3, tbuf.r1_delta, tbuf.r1_x, l.off_r1, l.W, l.W, ld, ld);
-		job(4, tbuf.r2_delta, tbuf.r2_x, l.off_r2, 16, l.W, ld, ld);
-		J.n_jobs = 5;
-		J.split = 4096;
-		uint32_t b = 0;
-		for (int k = 0; k < 5; ++k) {
-			J.block_start[k] = b;
-			b += J.j[k].tiles_m * J.j[k].tiles_k * ((J.j[k].ncols + J.split - 1) / J.split);
-		}
-		J.block_start[5] = b;
-		J.n_valid = n_valid;
-		J.partial = wgrad_partial.p;
-		J.var_partial = var_partial.p;
-		J.var_blocks = mlp_train_blocks(lay.L, lay.W, n);
-		J.var_grad = g + lay.var_off;
-		return J;
+	// the reduction of the training kernels' per-block weight-gradient rows (and variance partials) into g
+	MlpGradReduce grad_reduce(uint32_t n, float* g, const uint32_t* n_valid) const {
+		MlpGradReduce r{};
+		r.partial = wgrad_partial.p; r.n_blocks = mlp_train_blocks(lay.L, lay.W, n); r.n_matrix = lay.n_matrix; r.g = g;
+		r.n_valid = n_valid; r.var_partial = var_partial.p; r.var_blocks = r.n_blocks; r.var_grad = g + lay.var_off;
+		return r;
 	}
 	// The grid-gradient buckets past the progressive valid level get no records: their gradient is zero. For the
 	// testbed's own gradient buffer the scatter skips them once they hold zeros (early in training ~2,500 of ~2,600
@@ -754,23 +743,11 @@ struct NeusTestbed {
 		launch_mlp_train(s, lay.L, lay.W, n_valid_ptr, n, ld, c, (const half_t*)enc.p, dydx.p, dlo, mlp, t);
 		if (marks) mark(6);
 		if (!canonical) { if (marks) mark(7); return; }  // global-movement phase: canonical gradients unused
-		WGradJobs J = wgrad_jobs(n, ld, g, n_train_ptr);
-		if (marks && profiling) {  // per-phase timing: in order on one stream
-			launch_wgrad(s, J, J.block_start[5]);
-			mark(7);
-			launch_grid_scatter(s, n_train_ptr, n, ld, c, COORD_W, gl, valid, tbuf.dLdenc, tbuf.genc, tbuf.v, g + lay.grid_off,
-			                    scatter_work_for(g + lay.grid_off, valid, s), scan_tmp.p, scan_tmp_bytes);
-			return;
-		}
-		// the weight-gradient GEMM (MLP gradients, variance) beside the grid scatter (grid gradients): neither reads
-		// what the other writes, so the side stream overlaps them; the step's stream waits for both
-		HIP_CHECK(hipEventRecord(ev_fork, s));
-		HIP_CHECK(hipStreamWaitEvent(aux_stream, ev_fork, 0));
-		launch_wgrad(aux_stream, J, J.block_start[5]);
-		HIP_CHECK(hipEventRecord(ev_join, aux_stream));
+		// the MLP weight gradients were accumulated inside the training kernels: one small fixed-order reduction
+		launch_mlp_grad_reduce(s, grad_reduce(n, g, n_train_ptr));
+		if (marks) mark(7);
 		launch_grid_scatter(s, n_train_ptr, n, ld, c, COORD_W, gl, valid, tbuf.dLdenc, tbuf.genc, tbuf.v, g + lay.grid_off,
 		                    scatter_work_for(g + lay.grid_off, valid, s), scan_tmp.p, scan_tmp_bytes);
-		HIP_CHECK(hipStreamWaitEvent(s, ev_join, 0));
 	}
 
 	// ------------------------------------------------------------ collectives
@@ -1650,9 +1627,12 @@ static void time_kernel_impl(NeusTestbed* tb, int kernel, int variant, int iters
 				                 kernel == 5 ? 0 : kernel - 8);
 				break;
 			}
-			case 6: { WGradJobs J = t.wgrad_jobs(t.batch, t.batch, t.grads.p, nullptr); launch_wgrad(s, J, J.block_start[5]); break; }
-			case 7: launch_grid_scatter(s, nullptr, t.batch, t.batch, t.coords_c.p, COORD_W, t.gl, valid, t.tbuf.dLdenc, t.tbuf.genc, t.tbuf.v,
-			                            t.grads.p + t.lay.grid_off, t.swork, t.scan_tmp.p, t.scan_tmp_bytes); break;
+			case 6: launch_mlp_grad_reduce(s, t.grad_reduce(t.batch, t.grads.p, nullptr)); break;
+			case 7:
+				launch_grid_scatter(s, nullptr, t.batch, t.batch, t.coords_c.p, COORD_W, t.gl, valid, t.tbuf.dLdenc, t.tbuf.genc, t.tbuf.v,
+				                    t.grads.p + t.lay.grid_off, t.swork, t.scan_tmp.p, t.scan_tmp_bytes);
+				t.sc_zero_from = t.swork.n_buckets;  // the replay wrote every bucket: nothing is known zero for the next step
+				break;
 			case 8: t.encode(nullptr, t.batch, t.batch, t.batch, t.coords_c.p, COORD_W, valid, true, s); break;
 			default: throw std::runtime_error("unknown kernel id");
 			}
@@ -1934,19 +1914,22 @@ int neus_mfma_probe(const uint16_t* A, const uint16_t* B, float* C) {
 // [L][n] half2 = features 2l, 2l+1 of level l adjacent).
 namespace {
 
-NeusNetworkConfig module_config(const JsonValue& enc, const JsonValue& net, const JsonValue& rgb, uint32_t batch) {
+std::string fmt_float(float v) { char b[32]; std::snprintf(b, sizeof(b), "%.9g", (double)v); return b; }
+// `standalone`: a HashGrid module (create_encoding): tcnn's defaults for the keys a config omits
+// (create_grid_encoding_templated, grid.h:2499-2525); otherwise the NeuS Testbed's (testbed.cu:2175-2187, base.json)
+NeusNetworkConfig module_config(const JsonValue& enc, const JsonValue& net, const JsonValue& rgb, uint32_t batch, bool standalone = false) {
 	NeusNetworkConfig c{};
 	const uint32_t nf = (uint32_t)enc.number("n_features_per_level", 2);
 	c.n_levels = enc.number("n_features", 0) > 0 ? (uint32_t)enc.number("n_features", 0) / nf : (uint32_t)enc.number("n_levels", 16);
 	c.n_features_per_level = nf;
-	c.log2_hashmap_size = (uint32_t)enc.number("log2_hashmap_size", 15);
-	c.base_resolution = (uint32_t)enc.number("base_resolution", 0);
+	c.log2_hashmap_size = (uint32_t)enc.number("log2_hashmap_size", standalone ? 19 : 15);
+	c.base_resolution = (uint32_t)enc.number("base_resolution", standalone ? 16 : 0);
 	if (!c.base_resolution) c.base_resolution = 1u << (c.log2_hashmap_size / 3);
-	c.per_level_scale = (float)enc.number("per_level_scale", 0.0);
+	c.per_level_scale = (float)enc.number("per_level_scale", standalone ? 2.0 : 0.0);
 	c.top_resolution = (float)enc.number("top_resolution", 2048.0);
-	c.valid_level_scale = (float)enc.number("valid_level_scale", 0.02);
-	c.base_valid_level_scale = (float)enc.number("base_valid_level_scale", 0.2);
-	c.base_training_step = (uint32_t)enc.number("base_training_step", 100);
+	c.valid_level_scale = (float)enc.number("valid_level_scale", standalone ? 0.01 : 0.02);
+	c.base_valid_level_scale = (float)enc.number("base_valid_level_scale", standalone ? 0.5 : 0.2);
+	c.base_training_step = (uint32_t)enc.number("base_training_step", standalone ? 200 : 100);
 	c.n_neurons = (uint32_t)net.number("n_neurons", 64);
 	if ((uint32_t)rgb.number("n_neurons", c.n_neurons) != c.n_neurons) throw std::runtime_error("density and rgb networks must share n_neurons");
 	c.n_density_hidden = (uint32_t)net.number("n_hidden_layers", 1);
@@ -1967,22 +1950,35 @@ struct StreamSwap {  // run a call's launches on the caller's stream (NULL: the 
 
 struct NeusContext {
 	uint32_t n = 0;
-	Dev<float> dydx;  // encoding: dy/dx [6L][n] of the forward (prepare_input_gradients)
+	Dev<float> dydx;     // encoding: dy/dx [6L][n] of the forward (prepare_input_gradients)
+	Dev<uint32_t> enc;   // network with input encoding: the forward's paired encoding [L][n] (the MLP input)
 };
 
 struct NeusModule {
-	enum Kind { Network = 0, Encoding = 1 } kind;
+	// Network: the NeuS NerfNetwork; Encoding: a HashGrid; DensityNet: tcnn's NetworkWithInputEncoding(HashGrid ->
+	// FullyFusedMLP with 1 hidden ReLU layer -> 16 linear outputs), the network whose backward_backward_input tcnn
+	// implements (network_with_input_encoding.h:159-250, fully_fused_mlp.cu:1088-1198)
+	enum Kind { Network = 0, Encoding = 1, DensityNet = 2 } kind;
+	uint32_t n_mlp = 0, dn_width = 0, dn_de = 0;  // DensityNet: MLP parameters W DE + 16 W ahead of the grid, width, padded input
+	Dev<uint32_t> u_tmp;                          // DensityNet: dy/dx . dL_ddLdinput, paired
+	Dev<float> dn_partial, dn_dummy;              // DensityNet: per-block weight-gradient rows
 	NeusTestbed core;
 	uint32_t capacity = 0, n_in = 0, n_out = 0;
 	int training_step = 0;              // GridEncoding::set_training_step (grid.h:2427-2437): 0 = every level
 	uint32_t indeed_batch = 0;          // NeuS backward normalisation of the eikonal entries; 0 = the call's n
 	std::string hyper;
-	Dev<float> gtmp;                    // gradients of an Accumulate call
+	// encoding output layout (ENC_LAYOUT_*): AoS [n][2L] = the column-major matrix tcnn's cpp::Module wraps around the
+	// caller's buffer (cpp_api.cu:58-70); SoA [2L][n] = GridEncoding::preferred_output_layout (grid.h:2357-2359);
+	// paired [L][n] half2 = this build's kernels
+	uint32_t layout = ENC_LAYOUT_AOS;
+	bool grad_fp16 = true;              // dL_dparams in param precision (fp16, trainer.h:72-109) or fp32
+	Dev<uint32_t> enc_tmp, denc_tmp;    // paired-layout staging of non-paired module I/O
+	Dev<float> gtmp;                    // gradients of an Accumulate call (and of every fp16-gradient call)
 	Dev<float4> dpos, v4;
 	Dev<half_t> zero_h;
 	Dev<float4> zero_v;
 	explicit NeusModule(int device) : core(device) {}
-	uint64_t n_params() const { return kind == Network ? core.lay.P : core.lay.n_grid; }
+	uint64_t n_params() const { return kind == Network ? core.lay.P : (kind == DensityNet ? n_mlp + core.lay.n_grid : core.lay.n_grid); }
 	uint32_t valid() const { return core.valid_level_at(training_step); }
 	void load_params(const void* params, hipStream_t s) {
 		if (!params) throw std::runtime_error("module: null params");
@@ -2002,21 +1998,48 @@ struct NeusModule {
 	float* grad_target(void* dL_dparams, int mode) {
 		if (mode == NEUS_GRADIENT_IGNORE) return nullptr;
 		if (!dL_dparams) throw std::runtime_error("module: dL_dparams is null with a gradient mode other than Ignore");
-		if (mode == NEUS_GRADIENT_OVERWRITE) return (float*)dL_dparams;
-		if (mode != NEUS_GRADIENT_ACCUMULATE) throw std::runtime_error("module: unknown gradient mode");
+		if (mode != NEUS_GRADIENT_OVERWRITE && mode != NEUS_GRADIENT_ACCUMULATE) throw std::runtime_error("module: unknown gradient mode");
+		if (mode == NEUS_GRADIENT_OVERWRITE && !grad_fp16) return (float*)dL_dparams;
 		return gtmp.p;
 	}
 	void finish_grad(void* dL_dparams, int mode, hipStream_t s) {
-		if (mode == NEUS_GRADIENT_ACCUMULATE) launch_add_f32(s, (uint32_t)n_params(), gtmp.p, (float*)dL_dparams);
+		if (grad_fp16) launch_grad_to_half(s, (uint32_t)n_params(), gtmp.p, (half_t*)dL_dparams, mode == NEUS_GRADIENT_ACCUMULATE);
+		else if (mode == NEUS_GRADIENT_ACCUMULATE) launch_add_f32(s, (uint32_t)n_params(), gtmp.p, (float*)dL_dparams);
+	}
+	// a caller-layout encoding tensor (dL_doutput) as the kernels' paired layout
+	const half_t* paired_in(const void* x, uint32_t n, hipStream_t s) {
+		if (layout == ENC_LAYOUT_PAIRED) return (const half_t*)x;
+		launch_enc_from_layout(s, n, core.lay.L, (const half_t*)x, layout, denc_tmp.p);
+		return (const half_t*)denc_tmp.p;
 	}
 };
 
+// module options (this build's keys, beside tcnn's): "gradient_precision": "fp16" (default, tcnn's param precision) |
+// "fp32"; encoding "output_layout": "AoS" (default: cpp::Module's column-major view) | "SoA" | "paired"
+static void module_options(NeusModule* m, const JsonValue& j) {
+	const std::string gp = j.string("gradient_precision", "fp16");
+	if (gp != "fp16" && gp != "fp32") throw std::runtime_error("module: gradient_precision must be fp16 or fp32");
+	m->grad_fp16 = gp == "fp16";
+	const std::string ol = j.string("output_layout", "AoS");
+	if (ol == "AoS") m->layout = ENC_LAYOUT_AOS;
+	else if (ol == "SoA") m->layout = ENC_LAYOUT_SOA;
+	else if (ol == "paired") m->layout = ENC_LAYOUT_PAIRED;
+	else throw std::runtime_error("encoding module: output_layout must be AoS, SoA or paired");
+}
 static void module_common_init(NeusModule* m, uint32_t capacity) {
 	m->capacity = capacity;
 	const size_t P = m->n_params();
 	m->gtmp.alloc(P);
 	m->dpos.alloc(capacity); m->v4.alloc(capacity);
 	m->zero_h.alloc((size_t)2 * m->core.lay.L * capacity); m->zero_v.alloc(capacity);
+	if ((m->kind == NeusModule::Encoding && m->layout != ENC_LAYOUT_PAIRED) || m->kind == NeusModule::DensityNet) {
+		m->enc_tmp.alloc((size_t)m->core.lay.L * capacity); m->denc_tmp.alloc((size_t)m->core.lay.L * capacity);
+	}
+	if (m->kind == NeusModule::DensityNet) {
+		m->u_tmp.alloc((size_t)m->core.lay.L * capacity);
+		m->dn_partial.alloc((size_t)dnet_blocks(capacity) * m->n_mlp);
+		m->dn_dummy.alloc(4);
+	}
 	HIP_CHECK(hipMemset(m->zero_h.p, 0, m->zero_h.n * sizeof(half_t)));
 	HIP_CHECK(hipMemset(m->zero_v.p, 0, m->zero_v.n * sizeof(float4)));
 	HIP_CHECK(hipStreamSynchronize(m->core.stream));
@@ -2032,11 +2055,14 @@ int neus_module_create_network(const char* config_json, uint32_t batch_capacity,
 		HIP_CHECK(hipGetDevice(&dev));
 		auto m = std::make_unique<NeusModule>(dev);
 		m->kind = NeusModule::Network;
+		module_options(m.get(), j);
+		m->layout = ENC_LAYOUT_AOS;
 		m->core.setup_network(module_config(j.object("encoding"), j.object("network"), j.object("rgb_network"), batch_capacity), nullptr);
 		m->n_in = COORD_W; m->n_out = OUT_W;
 		const NeusNetworkConfig& c = m->core.cfg;
 		m->hyper = "{\"otype\": \"NerfNetwork\", \"n_levels\": " + std::to_string(c.n_levels) + ", \"n_neurons\": " + std::to_string(c.n_neurons) +
-		           ", \"log2_hashmap_size\": " + std::to_string(c.log2_hashmap_size) + ", \"per_level_scale\": " + std::to_string(c.per_level_scale) + "}";
+		           ", \"log2_hashmap_size\": " + std::to_string(c.log2_hashmap_size) + ", \"per_level_scale\": " + fmt_float(c.per_level_scale) +
+		           ", \"gradient_precision\": \"" + (m->grad_fp16 ? "fp16" : "fp32") + "\"}";
 		module_common_init(m.get(), batch_capacity);
 		*out = m.release();
 	});
@@ -2055,13 +2081,56 @@ int neus_module_create_encoding(uint32_t n_input_dims, const char* encoding_json
 		HIP_CHECK(hipGetDevice(&dev));
 		auto m = std::make_unique<NeusModule>(dev);
 		m->kind = NeusModule::Encoding;
+		module_options(m.get(), j);
 		JsonValue none; none.kind = JsonValue::Object;
-		m->core.setup_network(module_config(j, none, none, batch_capacity), nullptr, false);
+		m->core.setup_network(module_config(j, none, none, batch_capacity, true), nullptr, false);
 		m->n_in = 3; m->n_out = 2 * m->core.lay.L;
 		const NeusNetworkConfig& c = m->core.cfg;
+		static const char* lay_names[3] = {"AoS", "SoA", "paired"};
 		m->hyper = "{\"otype\": \"HashGrid\", \"n_levels\": " + std::to_string(c.n_levels) + ", \"n_features_per_level\": 2, \"log2_hashmap_size\": " +
 		           std::to_string(c.log2_hashmap_size) + ", \"base_resolution\": " + std::to_string(c.base_resolution) + ", \"per_level_scale\": " +
-		           std::to_string(c.per_level_scale) + "}";
+		           fmt_float(c.per_level_scale) + ", \"valid_level_scale\": " + fmt_float(c.valid_level_scale) + ", \"base_valid_level_scale\": " +
+		           fmt_float(c.base_valid_level_scale) + ", \"base_training_step\": " + std::to_string(c.base_training_step) +
+		           ", \"output_layout\": \"" + lay_names[m->layout] + "\", \"gradient_precision\": \"" + (m->grad_fp16 ? "fp16" : "fp32") + "\"}";
+		module_common_init(m.get(), batch_capacity);
+		*out = m.release();
+	});
+}
+
+int neus_module_create_network_with_input_encoding(uint32_t n_input_dims, uint32_t n_output_dims, const char* encoding_json,
+                                                   const char* network_json, uint32_t batch_capacity, NeusModule** out) {
+	return guard([&] {
+		if (!encoding_json || !network_json || !out) throw std::runtime_error("neus_module_create_network_with_input_encoding: null argument");
+		if (n_input_dims != 3) throw std::runtime_error("network with input encoding: n_input_dims must be 3 (HashGrid)");
+		if (n_output_dims == 0 || n_output_dims > 16) throw std::runtime_error("network with input encoding: 1..16 outputs (padded to 16)");
+		if (batch_capacity == 0 || batch_capacity % 128 != 0 || batch_capacity > (1u << 24))
+			throw std::runtime_error("batch_capacity must be a positive multiple of 128 (<= 2^24)");
+		const JsonValue je = parse_json(encoding_json), jn = parse_json(network_json);
+		const std::string ot = je.string("otype", "HashGrid");
+		if (ot != "HashGrid" && ot != "Grid") throw std::runtime_error("network with input encoding: only the HashGrid encoding is implemented on gfx950");
+		if (jn.string("otype", "FullyFusedMLP") != "FullyFusedMLP" && jn.string("otype", "FullyFusedMLP") != "CutlassMLP")
+			throw std::runtime_error("network with input encoding: the network must be a FullyFusedMLP");
+		if (jn.string("activation", "ReLU") != "ReLU" || jn.string("output_activation", "None") != "None" || (uint32_t)jn.number("n_hidden_layers", 1) != 1)
+			throw std::runtime_error("network with input encoding: ReLU, 1 hidden layer, linear output supported on gfx950");
+		int dev = 0;
+		HIP_CHECK(hipGetDevice(&dev));
+		auto m = std::make_unique<NeusModule>(dev);
+		m->kind = NeusModule::DensityNet;
+		module_options(m.get(), jn);
+		m->layout = ENC_LAYOUT_AOS;
+		JsonValue none; none.kind = JsonValue::Object;
+		m->core.setup_network(module_config(je, none, none, batch_capacity, true), nullptr, false);
+		m->dn_width = (uint32_t)jn.number("n_neurons", 64);
+		if (!dnet_supported(m->core.lay.L, m->dn_width)) throw std::runtime_error("network with input encoding: unsupported (n_levels, n_neurons) on gfx950");
+		m->dn_de = (2 * m->core.lay.L + 15) / 16 * 16;
+		m->n_mlp = m->dn_width * m->dn_de + 16 * m->dn_width;
+		m->n_in = 3; m->n_out = 16;
+		const NeusNetworkConfig& c = m->core.cfg;
+		m->hyper = "{\"otype\": \"NetworkWithInputEncoding\", \"encoding\": {\"otype\": \"HashGrid\", \"n_levels\": " + std::to_string(c.n_levels) +
+		           ", \"log2_hashmap_size\": " + std::to_string(c.log2_hashmap_size) + ", \"base_resolution\": " + std::to_string(c.base_resolution) +
+		           ", \"per_level_scale\": " + fmt_float(c.per_level_scale) + "}, \"network\": {\"otype\": \"FullyFusedMLP\", \"n_neurons\": " +
+		           std::to_string(m->dn_width) + ", \"n_hidden_layers\": 1, \"activation\": \"ReLU\", \"output_activation\": \"None\"}, \"n_output_dims\": " +
+		           std::to_string(n_output_dims) + ", \"gradient_precision\": \"" + (m->grad_fp16 ? "fp16" : "fp32") + "\"}";
 		module_common_init(m.get(), batch_capacity);
 		*out = m.release();
 	});
@@ -2081,7 +2150,7 @@ int neus_module_info(const NeusModule* m, NeusModuleInfo* o) {
 		o->gradient_precision = NEUS_PRECISION_FP32;
 		o->batch_capacity = m->capacity;
 		o->n_levels = m->core.lay.L;
-		o->grid_offset = m->kind == NeusModule::Network ? m->core.lay.grid_off : 0;
+		o->grid_offset = m->kind == NeusModule::Network ? m->core.lay.grid_off : (m->kind == NeusModule::DensityNet ? m->n_mlp : 0);
 		o->per_level_scale = m->core.cfg.per_level_scale;
 	});
 }
@@ -2102,21 +2171,31 @@ int neus_module_initialize_params(NeusModule* m, uint64_t seed, float* params_fu
 		if (!m || !params_full_precision) throw std::runtime_error("neus_module_initialize_params: null argument");
 		HIP_CHECK(hipSetDevice(m->core.device));
 		std::vector<float> h;
+		// cpp::Module::initialize_params draws from pcg32{seed} (cpp_api.cu:162-165; the Trainer's seed_seq is not involved)
 		if (m->kind == NeusModule::Network) {
-			h = m->core.initial_params((uint32_t)seed, nullptr);
-		} else {  // a standalone GridEncoding draws from a fresh seed_seq{seed} generator (grid.h initialize_params)
-			h.assign(m->core.lay.n_grid, 0.f);
-			std::seed_seq seq{(uint32_t)seed};
-			std::vector<uint32_t> seeds(2);
-			seq.generate(seeds.begin(), seeds.end());
-			pcg32 rnd = make_pcg32(seeds.front());
-			const size_t N = h.size(), per = 4, n_threads = (N + per - 1) / per, n_pad = (n_threads + 127) / 128 * 128;
+			h = m->core.initial_params_rng(make_pcg32(seed), nullptr);
+		} else {  // [FullyFusedMLP xavier matrices (fully_fused_mlp.cu:1229-1256)] then GridEncoding::initialize_params:
+			      // generate_random_uniform(rnd, n_params, -1e-4, 1e-4) (grid.h:2375-2380)
+			h.assign(m->n_params(), 0.f);
+			pcg32 rnd = make_pcg32(seed);
+			size_t off = 0;
+			if (m->kind == NeusModule::DensityNet) {
+				auto xavier = [&](uint32_t out, uint32_t in) {
+					const float scale = std::sqrt(6.0f / (float)(in + out));
+					for (uint32_t i = 0; i < out * in; ++i) h[off + i] = rnd.next_float() * 2.0f * scale - scale;
+					off += (size_t)out * in;
+				};
+				xavier(m->dn_width, m->dn_de);
+				xavier(16, m->dn_width);
+			}
+			float* hg = h.data() + off;
+			const size_t N = h.size() - off, per = 4, n_threads = (N + per - 1) / per, n_pad = (n_threads + 127) / 128 * 128;
 			for (size_t i = 0; i < n_pad; ++i) {
 				pcg32 r = rnd; r.advance((int64_t)(i * per));
 				for (size_t k = 0; k < per; ++k) {
 					const size_t idx = i + n_pad * k;
 					if (idx >= N) break;
-					h[idx] = r.next_float() * (1e-4f - -1e-4f) + -1e-4f;
+					hg[idx] = r.next_float() * (1e-4f - -1e-4f) + -1e-4f;
 				}
 			}
 		}
@@ -2127,15 +2206,35 @@ int neus_module_initialize_params(NeusModule* m, uint64_t seed, float* params_fu
 static void module_forward(NeusModule* m, hipStream_t s, uint32_t n, const float* input, void* output, const void* params, NeusContext* ctx) {
 	if (!input || !output) throw std::runtime_error("module forward: null input / output");
 	m->check_n(n, false);
-	m->load_params(params, s);
 	NeusTestbed& t = m->core;
+	if (m->kind == NeusModule::DensityNet) {
+		// NetworkWithInputEncoding::forward (network_with_input_encoding.h:84-111): encoding, then the MLP on it
+		if (!params) throw std::runtime_error("module: null params");
+		const half_t* ph = (const half_t*)params;
+		float* dydx = nullptr;
+		uint32_t* enc = m->enc_tmp.p;
+		if (ctx) {
+			ctx->dydx.alloc((size_t)6 * t.lay.L * std::max(1u, n)); dydx = ctx->dydx.p;
+			ctx->enc.alloc((size_t)t.lay.L * std::max(1u, n)); enc = ctx->enc.p;
+		}
+		const uint32_t gx = std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, 4096));
+		launch_grid_encode(s, nullptr, n, n, input, 3, t.gl, m->valid(), ph + m->n_mlp, enc, dydx, gx);
+		DNetLaunch d{};
+		d.w0 = ph; d.w1 = ph + (size_t)m->dn_width * m->dn_de; d.enc = enc; d.out = (half_t*)output;
+		launch_dnet(s, t.lay.L, m->dn_width, 0, n, d);
+		HIP_CHECK(hipGetLastError());
+		return;
+	}
+	m->load_params(params, s);
 	if (m->kind == NeusModule::Network) {
 		t.net_forward(nullptr, n, n, input, m->valid(), (half_t*)output, s);
 	} else {
 		float* dydx = nullptr;
 		if (ctx) { ctx->dydx.alloc((size_t)6 * t.lay.L * std::max(1u, n)); dydx = ctx->dydx.p; }
 		const uint32_t gx = std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, 4096));
-		launch_grid_encode(s, nullptr, n, n, input, 3, t.gl, m->valid(), t.params_h.p + t.lay.grid_off, (uint32_t*)output, dydx, gx);
+		uint32_t* enc = m->layout == ENC_LAYOUT_PAIRED ? (uint32_t*)output : m->enc_tmp.p;
+		launch_grid_encode(s, nullptr, n, n, input, 3, t.gl, m->valid(), t.params_h.p + t.lay.grid_off, enc, dydx, gx);
+		if (m->layout != ENC_LAYOUT_PAIRED) launch_enc_to_layout(s, n, t.lay.L, enc, (half_t*)output, m->layout);
 	}
 	HIP_CHECK(hipGetLastError());
 }
@@ -2156,9 +2255,9 @@ int neus_module_forward(NeusModule* m, void* stream, uint32_t n, const float* in
 		StreamSwap sw(m->core, stream);
 		auto ctx = std::make_unique<NeusContext>();
 		ctx->n = n;
-		// the network's backward recomputes its forward; the encoding keeps dy/dx for dL_dinput and second order
+		// the NerfNetwork's backward recomputes its forward; the encodings keep dy/dx for dL_dinput and second order
 		(void)prepare_input_gradients;
-		module_forward(m, m->core.stream, n, input, output, params, m->kind == NeusModule::Encoding ? ctx.get() : nullptr);
+		module_forward(m, m->core.stream, n, input, output, params, m->kind != NeusModule::Network ? ctx.get() : nullptr);
 		*ctx_out = ctx.release();
 	});
 }
@@ -2176,8 +2275,28 @@ int neus_module_backward(NeusModule* m, void* stream, const NeusContext* ctx, ui
 		hipStream_t s = t.stream;
 		float* g = m->grad_target(dL_dparams, gradient_mode);
 		if (!g && !dL_dinput) return;
-		m->load_params(params, s);
 		const uint32_t valid = m->valid();
+		if (m->kind == NeusModule::DensityNet) {
+			// NetworkWithInputEncoding::backward (network_with_input_encoding.h:113-156): the MLP backward gives its weight
+			// gradients and dL/d(encoding); the encoding's backward the grid gradients and dL_dinput
+			if (!params) throw std::runtime_error("module: null params");
+			if (!ctx->enc.p || !ctx->dydx.p) throw std::runtime_error("module backward: the context is not from this module's forward");
+			const half_t* ph = (const half_t*)params;
+			DNetLaunch d{};
+			d.w0 = ph; d.w1 = ph + (size_t)m->dn_width * m->dn_de; d.enc = ctx->enc.p; d.dL = (const half_t*)dL_doutput;
+			d.denc = m->denc_tmp.p; d.wpartial = m->dn_partial.p;
+			launch_dnet(s, t.lay.L, m->dn_width, 1, n, d);
+			if (g) {
+				launch_mlp_grad_reduce(s, MlpGradReduce{m->dn_partial.p, dnet_blocks(n), m->n_mlp, g, nullptr, nullptr, 0, m->dn_dummy.p});
+				launch_grid_scatter(s, nullptr, n, n, input, 3, t.gl, valid, (const half_t*)m->denc_tmp.p, m->zero_h.p, m->zero_v.p, g + m->n_mlp,
+				                    t.swork, t.scan_tmp.p, t.scan_tmp_bytes);
+			}
+			if (dL_dinput) launch_enc_input_grad(s, n, n, t.lay.L, (const half_t*)m->denc_tmp.p, ctx->dydx.p, dL_dinput, 3);
+			if (g) m->finish_grad(dL_dparams, gradient_mode, s);
+			HIP_CHECK(hipGetLastError());
+			return;
+		}
+		m->load_params(params, s);
 		if (m->kind == NeusModule::Network) {
 			// NerfNetwork::backward (nerf_network.h:330-601): first and second order in one pass; the Testbed's
 			// forward-recompute + backward writes every parameter gradient (Overwrite) into g
@@ -2194,12 +2313,13 @@ int neus_module_backward(NeusModule* m, void* stream, const NeusContext* ctx, ui
 				HIP_CHECK(hipMemcpy2DAsync(dL_dinput, COORD_W * 4, m->dpos.p, 16, 12, n, hipMemcpyDeviceToDevice, s));
 			}
 		} else {
+			const half_t* dly = m->paired_in(dL_doutput, n, s);
 			if (dL_dinput) {
 				if (!ctx->dydx.p) throw std::runtime_error("encoding backward: dL_dinput needs the forward's dy/dx");
-				launch_enc_input_grad(s, n, n, t.lay.L, (const half_t*)dL_doutput, ctx->dydx.p, dL_dinput, 3);
+				launch_enc_input_grad(s, n, n, t.lay.L, dly, ctx->dydx.p, dL_dinput, 3);
 			}
 			if (g)  // kernel_grid_backward (grid.h:371-500) through the fused binned scatter, second-order term zero
-				launch_grid_scatter(s, nullptr, n, n, input, 3, t.gl, valid, (const half_t*)dL_doutput, m->zero_h.p, m->zero_v.p, g, t.swork,
+				launch_grid_scatter(s, nullptr, n, n, input, 3, t.gl, valid, dly, m->zero_h.p, m->zero_v.p, g, t.swork,
 				                    t.scan_tmp.p, t.scan_tmp_bytes);
 		}
 		if (g) m->finish_grad(dL_dparams, gradient_mode, s);
@@ -2213,7 +2333,35 @@ int neus_module_backward_backward_input(NeusModule* m, void* stream, const NeusC
 	return guard([&] {
 		if (m->kind == NeusModule::Network)
 			throw std::runtime_error("NerfNetwork: the eikonal second-order term is part of backward (nerf_network.h:330-601); "
-			                         "backward_backward_input is provided by the HashGrid encoding module");
+			                         "backward_backward_input is provided by the HashGrid and network-with-input-encoding modules "
+			                         "(the reference's NerfNetwork does not implement it either: object.h:222-232)");
+		if (m->kind == NeusModule::DensityNet) {
+			// NetworkWithInputEncoding::backward_backward_input (network_with_input_encoding.h:159-250): u = dy/dx . dL_ddLdinput
+			// (kernel_grid_backward_input_backward_dLdoutput), the MLP's backward-backward (fully_fused_mlp.cu:1088-1198: b2 =
+			// relu'(H0) W1^T dL, h1' = relu'(H0) W0 u; dW0 = b2 u^T, dW1 = dL h1'^T) and the encoding's second-order grid
+			// gradient with dL/d(encoding) = W0^T b2. Like the reference, dL_ddLdoutput and dL_dinput are not produced.
+			if (!ctx || ctx->n != n || !ctx->dydx.p || !ctx->enc.p) throw std::runtime_error("backward_backward_input: needs the forward's context");
+			if (!input || !dL_ddLdinput || !dL_doutput || !params) throw std::runtime_error("backward_backward_input: null input");
+			m->check_n(n, true);
+			HIP_CHECK(hipSetDevice(m->core.device));
+			StreamSwap sw(m->core, stream);
+			NeusTestbed& t = m->core;
+			hipStream_t s = t.stream;
+			float* g = m->grad_target(dL_dparams, gradient_mode);
+			if (!g) return;
+			const half_t* ph = (const half_t*)params;
+			launch_enc_ddLdoutput(s, n, n, t.lay.L, dL_ddLdinput, ctx->dydx.p, (half_t*)m->u_tmp.p, m->v4.p);
+			DNetLaunch d{};
+			d.w0 = ph; d.w1 = ph + (size_t)m->dn_width * m->dn_de; d.enc = ctx->enc.p; d.dL = (const half_t*)dL_doutput; d.u = m->u_tmp.p;
+			d.denc = m->denc_tmp.p; d.wpartial = m->dn_partial.p;
+			launch_dnet(s, t.lay.L, m->dn_width, 2, n, d);
+			launch_mlp_grad_reduce(s, MlpGradReduce{m->dn_partial.p, dnet_blocks(n), m->n_mlp, g, nullptr, nullptr, 0, m->dn_dummy.p});
+			launch_grid_scatter(s, nullptr, n, n, input, 3, t.gl, m->valid(), m->zero_h.p, (const half_t*)m->denc_tmp.p, m->v4.p, g + m->n_mlp,
+			                    t.swork, t.scan_tmp.p, t.scan_tmp_bytes);
+			m->finish_grad(dL_dparams, gradient_mode, s);
+			HIP_CHECK(hipGetLastError());
+			return;
+		}
 		if (dL_dinput) throw std::runtime_error("HashGrid backward_backward_input: dL_dinput (second derivative in x) is not provided");
 		if (!ctx || ctx->n != n || !ctx->dydx.p) throw std::runtime_error("backward_backward_input: needs the forward's context (dy/dx)");
 		if (!input || !dL_ddLdinput || !dL_doutput) throw std::runtime_error("backward_backward_input: null input");
@@ -2224,12 +2372,15 @@ int neus_module_backward_backward_input(NeusModule* m, void* stream, const NeusC
 		hipStream_t s = t.stream;
 		float* g = m->grad_target(dL_dparams, gradient_mode);
 		// dL_ddLdoutput (kernel_grid_backward_input_backward_dLdoutput) and dL_ddLdinput as float4 for the scatter
-		launch_enc_ddLdoutput(s, n, n, t.lay.L, dL_ddLdinput, ctx->dydx.p, (half_t*)dL_ddLdoutput, m->v4.p);
+		const bool relay = m->layout != ENC_LAYOUT_PAIRED && dL_ddLdoutput;
+		launch_enc_ddLdoutput(s, n, n, t.lay.L, dL_ddLdinput, ctx->dydx.p, relay ? (half_t*)m->enc_tmp.p : (half_t*)dL_ddLdoutput, m->v4.p);
+		if (relay) launch_enc_to_layout(s, n, t.lay.L, m->enc_tmp.p, (half_t*)dL_ddLdoutput, m->layout);
 		if (g) {
 			m->load_params(params, s);
+			const half_t* dly = m->paired_in(dL_doutput, n, s);
 			// kernel_grid_backward_input_backward_grid (grid.h:880-1007): the fused scatter's second-order term with
 			// g = dL_doutput, v = dL_ddLdinput, first-order term zero
-			launch_grid_scatter(s, nullptr, n, n, input, 3, t.gl, m->valid(), m->zero_h.p, (const half_t*)dL_doutput, m->v4.p, g, t.swork,
+			launch_grid_scatter(s, nullptr, n, n, input, 3, t.gl, m->valid(), m->zero_h.p, dly, m->v4.p, g, t.swork,
 			                    t.scan_tmp.p, t.scan_tmp_bytes);
 			m->finish_grad(dL_dparams, gradient_mode, s);
 		}

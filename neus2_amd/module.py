@@ -41,13 +41,19 @@ class Context:
 
 class Module:
     """tcnn::cpp::Module. kind 'network' = the NeuS NerfNetwork (input [n, 7] f32, output [n, 16] fp16),
-    'encoding' = the HashGrid encoding (input [n, 3] f32, output [L, n] half2 -> tensor [L, n, 2] fp16)."""
+    'encoding' = the HashGrid encoding (input [n, 3] f32; output layout by the config's "output_layout": "AoS" [n, 2L]
+    (default: the column-major view cpp::Module gives its caller, cpp_api.cu:58-70), "SoA" [2L, n] (GridEncoding's
+    preferred layout, grid.h:2357-2359) or "paired" [L, n, 2] (this build's kernels)). dL_dparams is fp16 (tcnn's param
+    precision) unless the config says "gradient_precision": "fp32"."""
 
     def __init__(self, handle, kind):
         self._h, self.kind = handle, kind
         info = NeusModuleInfo()
         check(lib().neus_module_info(self._h, C.byref(info)))
         self.info = {k: getattr(info, k) for k, _ in info._fields_}
+        hp = self.hyperparams()
+        self.output_layout = hp.get("output_layout", "AoS")
+        self.gradient_precision = hp.get("gradient_precision", "fp16")
 
     @classmethod
     def create_network(cls, config, batch_capacity=1 << 18):
@@ -57,6 +63,18 @@ class Module:
         h = C.c_void_p()
         check(lib().neus_module_create_network(text.encode(), C.c_uint32(batch_capacity), C.byref(h)))
         return cls(h, "network")
+
+    @classmethod
+    def create_network_with_input_encoding(cls, n_input_dims, n_output_dims, encoding, network, batch_capacity=1 << 18):
+        """tcnn create_network_with_input_encoding (cpp_api.h:108): HashGrid -> FullyFusedMLP (1 hidden ReLU layer), input
+        [n, 3] f32, output [n, 16] fp16, params [W x DE | 16 x W | grid]; backward_backward_input as
+        network_with_input_encoding.h:159-250."""
+        te = encoding if isinstance(encoding, str) else json.dumps(encoding)
+        tn = network if isinstance(network, str) else json.dumps(network)
+        h = C.c_void_p()
+        check(lib().neus_module_create_network_with_input_encoding(C.c_uint32(n_input_dims), C.c_uint32(n_output_dims), te.encode(),
+                                                                   tn.encode(), C.c_uint32(batch_capacity), C.byref(h)))
+        return cls(h, "network_with_input_encoding")
 
     @classmethod
     def create_encoding(cls, encoding, batch_capacity=1 << 18, n_input_dims=3):
@@ -108,9 +126,19 @@ class Module:
         import torch
         if output is not None:
             return output
-        if self.kind == "network":
-            return torch.empty((n, 16), dtype=torch.float16, device="cuda")
-        return torch.empty((self.info["n_levels"], n, 2), dtype=torch.float16, device="cuda")
+        return torch.empty(self.output_shape(n), dtype=torch.float16, device="cuda")
+
+    def output_shape(self, n):
+        if self.kind != "encoding":
+            return (n, 16)
+        L = self.info["n_levels"]
+        return {"AoS": (n, 2 * L), "SoA": (2 * L, n), "paired": (L, n, 2)}[self.output_layout]
+
+    def gradient_buffer(self):
+        """A zeroed dL_dparams tensor of the module's gradient precision."""
+        import torch
+        dt = torch.float16 if self.gradient_precision == "fp16" else torch.float32
+        return torch.zeros(self.n_params, dtype=dt, device="cuda")
 
     def inference(self, x, params, output=None):
         n = x.shape[0]
@@ -133,7 +161,7 @@ class Module:
 
     def backward_backward_input(self, ctx, x, dL_ddLdinput, dL_doutput, params, dL_dparams=None, dL_ddLdoutput=None,
                                 mode=GradientMode.Overwrite):
-        if self.kind != "encoding":
+        if self.kind == "network":
             raise NeusError("backward_backward_input: the NerfNetwork's second order is inside backward")
         check(lib().neus_module_backward_backward_input(self._h, _stream(), ctx._h, C.c_uint32(ctx.n), _p(dL_ddLdinput), _p(x),
                                                         _p(dL_doutput), _p(dL_dparams), _p(dL_ddLdoutput), None, _p(params),
@@ -147,3 +175,7 @@ def create_network(config, batch_capacity=1 << 18):
 
 def create_encoding(encoding, batch_capacity=1 << 18, n_input_dims=3):
     return Module.create_encoding(encoding, batch_capacity, n_input_dims)
+
+
+def create_network_with_input_encoding(n_input_dims, n_output_dims, encoding, network, batch_capacity=1 << 18):
+    return Module.create_network_with_input_encoding(n_input_dims, n_output_dims, encoding, network, batch_capacity)

@@ -663,15 +663,35 @@ void or_net_layout(const OrNetCfg* c, uint32_t* out) {
 // Parameter initialisation (trainer.h:54-109, fully_fused_mlp.cu:1229-1249, gpu_matrix.h:292-306,
 // grid.h:2375-2380, random.h:67-91, nerf_network.h:815-886). `geo_init` (n_density floats) replaces the
 // density MLP (the reference loads utils/mlp_weights*.txt).
+static void init_params_from(const OrNetCfg* c, pcg32 rnd, const float* geo_init, float* params);
+// Trainer (trainer.h:54-109): std::seed_seq{seed}.generate(2 values) -> pcg32{seeds[0]} -> model->initialize_params
 void or_init_params(const OrNetCfg* c, uint32_t seed, const float* geo_init, float* params) {
-	Net n(*c);
-	std::fill(params, params + n.n_params, 0.0f);
-	// std::seed_seq{seed}.generate(2 values) -> pcg32{seeds[0]}: computed by the caller-independent routine below
 	std::seed_seq seq{seed};
 	std::vector<uint32_t> seeds(2);
 	seq.generate(seeds.begin(), seeds.end());
-	const uint32_t seeds0 = seeds.front();
-	pcg32 rnd(seeds0);
+	init_params_from(c, pcg32(seeds.front()), geo_init, params);
+}
+// tcnn::cpp::Module::initialize_params (cpp_api.cu:162-165): pcg32{seed} -> model->initialize_params
+void or_init_params_pcg(const OrNetCfg* c, uint64_t seed, const float* geo_init, float* params) {
+	init_params_from(c, pcg32(seed), geo_init, params);
+}
+// GridEncoding::initialize_params alone (grid.h:2375-2380) from pcg32{seed}: generate_random_uniform(rnd, n, -1e-4,
+// 1e-4) with random.h:67-91's thread mapping (thread i draws 4 values for i + n_threads_padded * j)
+void or_grid_init_pcg(uint64_t n, uint64_t seed, float* out) {
+	pcg32 rnd(seed);
+	const size_t N_TO_GEN = 4, n_threads = (n + N_TO_GEN - 1) / N_TO_GEN, n_pad = (n_threads + 127) / 128 * 128;
+	for (size_t i = 0; i < n_pad; ++i) {
+		pcg32 r = rnd; r.advance((int64_t)(i * N_TO_GEN));
+		for (size_t j = 0; j < N_TO_GEN; ++j) {
+			const size_t idx = i + n_pad * j;
+			if (idx >= n) break;
+			out[idx] = r.next_float() * (1e-4f - -1e-4f) + -1e-4f;
+		}
+	}
+}
+static void init_params_from(const OrNetCfg* c, pcg32 rnd, const float* geo_init, float* params) {
+	Net n(*c);
+	std::fill(params, params + n.n_params, 0.0f);
 	auto xavier = [&](uint32_t off, uint32_t out, uint32_t in) {
 		float scale = std::sqrt(6.0f / (float)(in + out));
 		for (uint32_t i = 0; i < out * in; ++i) params[off + i] = rnd.next_float() * 2.0f * scale - scale;

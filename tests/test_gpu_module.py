@@ -54,15 +54,20 @@ def test_network_module(torch_cuda):
     tb.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
     tb.reload_network_from_json(cfg_dict, batch_size=4096)
     lay = tb.layout()
-    m = Module.create_network(cfg_dict, batch_capacity=4096)
+    m = Module.create_network(dict(cfg_dict, gradient_precision="fp32"), batch_capacity=4096)
+    m16 = Module.create_network(cfg_dict, batch_capacity=4096)  # default: fp16 dL_dparams (tcnn's param precision)
     assert m.n_params == lay["n_params"] and m.n_input_dims == 7 and m.n_output_dims == 16
     assert m.name() == "NerfNetwork" and m.info["grid_offset"] == lay["grid_offset"]
     assert abs(m.info["per_level_scale"] - lay["per_level_scale"]) < 1e-6
-    # initialize_params: the Trainer's init (seed 1337); the Testbed replaces the density block by the geometric init
+    assert m.gradient_precision == "fp32" and m16.gradient_precision == "fp16"
+    # initialize_params: cpp::Module draws from pcg32{seed} (cpp_api.cu:162-165), not the Trainer's seed_seq
     p0 = m.initialize_params(1337).cpu().numpy()
+    ocfg = O.make_cfg(per_level_scale=lay["per_level_scale"])
+    ref0 = np.zeros(p0.size, np.float32)
+    O.lib().or_init_params_pcg(C.byref(ocfg), C.c_uint64(1337), None, O.P(ref0))
+    np.testing.assert_array_equal(p0, ref0)
     tp = tb.get_params()
     nd = lay["n_density"]
-    np.testing.assert_array_equal(p0[nd:], tp[nd:])
     # perturbed parameters that exercise every path, shared as fp16 by the module call and the Testbed
     rng = np.random.default_rng(3)
     p = tp.copy()
@@ -114,6 +119,16 @@ def test_network_module(torch_cuda):
         rel, cos = _rel_cos(gm[a:b], gref[a:b])
         _record("module_network_backward_" + name, rel=rel, cos=cos)
         assert rel <= 2e-2 and cos >= 0.999, (name, rel, cos)
+    # fp16 dL_dparams (the default): the fp32 gradient rounded once; Accumulate adds in fp32 and rounds once
+    ctx16, _ = m16.forward(x, params)
+    m16.set_indeed_batch_size(N)
+    g16 = m16.gradient_buffer()
+    assert g16.dtype == t.float16
+    m16.backward(ctx16, x, dlt, params, dL_dparams=g16, mode=GradientMode.Overwrite)
+    h16 = gm.astype(np.float16)
+    np.testing.assert_array_equal(g16.cpu().numpy().view(np.uint16), h16.view(np.uint16))
+    m16.backward(ctx16, x, dlt, params, dL_dparams=g16, mode=GradientMode.Accumulate)
+    np.testing.assert_array_equal(g16.cpu().numpy().view(np.uint16), (h16.astype(np.float32) + gm).astype(np.float16).view(np.uint16))
     # Accumulate adds the same gradient; Ignore leaves dL_dparams untouched
     m.backward(ctx, x, dlt, params, dL_dparams=g, mode=GradientMode.Accumulate)
     np.testing.assert_array_equal(g.cpu().numpy(), gm * 2)
@@ -126,30 +141,57 @@ def test_network_module(torch_cuda):
     assert not t.equal(m.inference(x, params2).view(t.int16), ref)
 
 
-def test_encoding_module(torch_cuda):
+def _to_nf(a, layout, n, L):
+    """An encoding-shaped module tensor (host) as [n][2L] (feature 2l + k of level l)."""
+    a = np.asarray(a)
+    return {"AoS": lambda: a.reshape(n, 2 * L), "SoA": lambda: a.reshape(2 * L, n).T,
+            "paired": lambda: a.reshape(L, n, 2).transpose(1, 0, 2).reshape(n, 2 * L)}[layout]()
+
+
+def _from_nf(a, layout, n, L):
+    return np.ascontiguousarray({"AoS": lambda: a, "SoA": lambda: a.T,
+                                 "paired": lambda: a.reshape(n, L, 2).transpose(1, 0, 2)}[layout]())
+
+
+@pytest.mark.parametrize("layout", ["AoS", "SoA", "paired"])
+def test_encoding_module(torch_cuda, layout):
+    """The HashGrid module in each output layout: AoS [n][2L] (the cpp::Module view, cpp_api.cu:58-70, the default),
+    SoA [2L][n] (grid.h:2357-2359), paired [L][n] half2: forward bit-exact vs the oracle, backward and double backward
+    vs float64 autograd; pcg32{seed} initialisation (cpp_api.cu:162-165) bit-exact; tcnn's defaults for omitted keys."""
     import torch
     import oracle as O
     from torch_ref import grid_tables, hash_grid
     from neus2_amd.module import GradientMode, Module
     t = torch_cuda
     enc_cfg = {"otype": "HashGrid", "n_levels": 8, "n_features_per_level": 2, "log2_hashmap_size": 14, "base_resolution": 16,
-               "per_level_scale": 1.5}
+               "per_level_scale": 1.5, "gradient_precision": "fp32"}
+    if layout != "AoS":
+        enc_cfg["output_layout"] = layout
     m = Module.create_encoding(enc_cfg, batch_capacity=N)
+    assert m.output_layout == layout
     L = 8
     off, res = grid_tables(L, 14, 16, 1.5)
     assert m.n_params == 2 * off[-1] and m.n_output_dims == 2 * L and m.name() == "HashGrid"
+    hp = m.hyperparams()
+    # omitted progressive-level keys take tcnn's create_grid_encoding defaults (grid.h:2518-2525)
+    assert hp["valid_level_scale"] == pytest.approx(0.01) and hp["base_valid_level_scale"] == pytest.approx(0.5)
+    assert hp["base_training_step"] == 200 and hp["per_level_scale"] == 1.5
     p0 = m.initialize_params(1337).cpu().numpy()
     assert np.abs(p0).max() <= 1e-4 and np.abs(p0).max() > 0
+    oinit = np.zeros(m.n_params, np.float32)
+    O.lib().or_grid_init_pcg(C.c_uint64(m.n_params), C.c_uint64(1337), O.P(oinit))
+    np.testing.assert_array_equal(p0, oinit)
+    ocfg = O.make_cfg(n_levels=L, log2_hashmap_size=14, base_resolution=16, per_level_scale=1.5)
+    olay = O.layout(ocfg)
     rng = np.random.default_rng(9)
     ph = rng.uniform(-1, 1, m.n_params).astype(np.float16)
     params = t.from_numpy(ph.view(np.int16).copy()).cuda()
     pos = rng.uniform(0.02, 0.98, (N, 3)).astype(np.float32)
     x = t.from_numpy(pos).cuda()
     ctx, y = m.forward(x, params, prepare_input_gradients=True)
-    got = y.float().cpu().numpy().transpose(1, 0, 2).reshape(N, 2 * L)
+    assert tuple(y.shape) == m.output_shape(N)
+    got = _to_nf(y.float().cpu().numpy(), layout, N, L)
     # oracle: a 8-level config with the same tables, parameters in the grid block
-    ocfg = O.make_cfg(n_levels=L, log2_hashmap_size=14, base_resolution=16, per_level_scale=1.5)
-    olay = O.layout(ocfg)
     op = np.zeros(olay["n_params"], np.float32)
     op[olay["grid_off"]:olay["grid_off"] + m.n_params] = ph.astype(np.float32)
     renc, _ = O.grid_forward(ocfg, op, pos, L)
@@ -158,8 +200,9 @@ def test_encoding_module(torch_cuda):
     tab = torch.tensor(ph.astype(np.float64).reshape(-1, 2), requires_grad=True)
     xt = torch.tensor(pos.astype(np.float64), requires_grad=True)
     e = hash_grid(xt, tab, off, res)
-    dly = rng.normal(0, 1, (L, N, 2)).astype(np.float16)
-    dly_t = torch.tensor(dly.astype(np.float64).transpose(1, 0, 2).reshape(N, 2 * L), requires_grad=True)
+    dly_nf = rng.normal(0, 1, (N, 2 * L)).astype(np.float16)
+    dly = _from_nf(dly_nf, layout, N, L)
+    dly_t = torch.tensor(dly_nf.astype(np.float64), requires_grad=True)
     S = (e * dly_t).sum()
     g_tab, g_x = torch.autograd.grad(S, (tab, xt), create_graph=True)
     v = rng.normal(0, 1, (N, 3)).astype(np.float32)
@@ -174,12 +217,12 @@ def test_encoding_module(torch_cuda):
     rel_x, cos_x = _rel_cos(dx.cpu().numpy(), g_x.detach().numpy())
     # backward_backward_input: second-order dL_dparams and dL_ddLdoutput
     g2 = t.zeros(m.n_params, dtype=t.float32, device="cuda")
-    ddo = t.zeros((L, N, 2), dtype=t.float16, device="cuda")
+    ddo = t.zeros(m.output_shape(N), dtype=t.float16, device="cuda")
     m.backward_backward_input(ctx, x, t.from_numpy(v).cuda(), dly_dev, params, dL_dparams=g2, dL_ddLdoutput=ddo)
     rel_p2, cos_p2 = _rel_cos(g2.cpu().numpy(), g2_tab.numpy().ravel())
-    ddo_np = ddo.float().cpu().numpy().transpose(1, 0, 2).reshape(N, 2 * L)
+    ddo_np = _to_nf(ddo.float().cpu().numpy(), layout, N, L)
     rel_o2, cos_o2 = _rel_cos(ddo_np, g2_dly.numpy())
-    _record("module_encoding", rel_params=rel_p, rel_dinput=rel_x, rel_params_2nd=rel_p2, rel_ddLdoutput=rel_o2)
+    _record("module_encoding_" + layout, rel_params=rel_p, rel_dinput=rel_x, rel_params_2nd=rel_p2, rel_ddLdoutput=rel_o2)
     assert rel_p <= 2e-3 and cos_p >= 0.99999, (rel_p, cos_p)
     assert rel_x <= 1e-4, rel_x
     assert rel_p2 <= 2e-3 and cos_p2 >= 0.99999, (rel_p2, cos_p2)
@@ -188,7 +231,102 @@ def test_encoding_module(torch_cuda):
     acc = g.clone()
     m.backward_backward_input(ctx, x, t.from_numpy(v).cuda(), dly_dev, params, dL_dparams=acc, mode=GradientMode.Accumulate)
     np.testing.assert_allclose(acc.cpu().numpy(), g.cpu().numpy() + g2.cpu().numpy(), rtol=1e-6, atol=1e-6)
-    # progressive levels: set_training_step(1) -> ceil(0.2 * 8) = 2 -> levels 0..2 active, the rest 0
+    # progressive levels with tcnn's defaults: set_training_step(1) -> valid level ceil(0.5 * 8) = 4 -> levels 0..4 active
     m.set_training_step(1)
-    y3 = m.inference(x, params).float().cpu().numpy()
-    assert not y3[3:].any() and np.array_equal(y3[:3], y.float().cpu().numpy()[:3])
+    y3 = _to_nf(m.inference(x, params).float().cpu().numpy(), layout, N, L)
+    assert not y3[:, 10:].any() and np.array_equal(y3[:, :10], got[:, :10])
+    # fp16 dL_dparams (default gradient precision): the fp32 first-order gradient rounded once
+    enc16 = dict(enc_cfg)
+    del enc16["gradient_precision"]
+    m16 = Module.create_encoding(enc16, batch_capacity=N)
+    ctx16, _ = m16.forward(x, params, prepare_input_gradients=True)
+    g16 = m16.gradient_buffer()
+    m16.backward(ctx16, x, dly_dev, params, dL_dparams=g16, mode=GradientMode.Overwrite)
+    np.testing.assert_array_equal(g16.cpu().numpy().view(np.uint16), g.cpu().numpy().astype(np.float16).view(np.uint16))
+
+
+@pytest.mark.parametrize("n_levels,width", [(8, 64), (14, 64), (1, 16)])
+def test_network_with_input_encoding_module(torch_cuda, n_levels, width):
+    """create_network_with_input_encoding (cpp_api.h:108): HashGrid -> FullyFusedMLP (1 hidden ReLU layer) on the MFMA
+    kernel k_dnet, against a float64 autograd restatement (tests/torch_ref.hash_grid + the MLP):
+    * forward: the fp16 output within fp16 rounding of the float64 value;
+    * backward (network_with_input_encoding.h:113-156): dL_dparams (MLP and grid blocks) and dL_dinput;
+    * backward_backward_input (network_with_input_encoding.h:159-250, fully_fused_mlp.cu:1088-1198): the second-order
+      parameter gradient = d/dtheta of sum(dL_ddLdinput . dL/dx) (ReLU'' = 0), MLP and grid blocks;
+    * Accumulate adds; pcg32{seed} initialisation = xavier(W0), xavier(W1), then the grid (cpp_api.cu:162-165)."""
+    import torch
+    from torch_ref import grid_tables, hash_grid
+    from neus2_amd.module import GradientMode, Module
+    t = torch_cuda
+    L, W = n_levels, width
+    log2t = 14
+    enc_cfg = {"otype": "HashGrid", "n_levels": L, "n_features_per_level": 2, "log2_hashmap_size": log2t, "base_resolution": 16,
+               "per_level_scale": 1.5}
+    net_cfg = {"otype": "FullyFusedMLP", "activation": "ReLU", "output_activation": "None", "n_neurons": W, "n_hidden_layers": 1,
+               "gradient_precision": "fp32"}
+    m = Module.create_network_with_input_encoding(3, 16, enc_cfg, net_cfg, batch_capacity=N)
+    DE = (2 * L + 15) // 16 * 16
+    off, res = grid_tables(L, log2t, 16, 1.5)
+    n_mlp = W * DE + 16 * W
+    assert m.n_params == n_mlp + 2 * off[-1] and m.n_output_dims == 16 and m.info["grid_offset"] == n_mlp
+    assert m.name() == "NetworkWithInputEncoding"
+    # initialisation from pcg32{1337}: the two xavier matrices, then the grid block continues the same generator
+    p0 = m.initialize_params(1337).cpu().numpy()
+    s0, s1 = np.sqrt(6.0 / (W + DE)), np.sqrt(6.0 / (16 + W))
+    assert np.abs(p0[: W * DE]).max() <= s0 and np.abs(p0[W * DE:n_mlp]).max() <= s1 and np.abs(p0[n_mlp:]).max() <= 1e-4
+    rng = np.random.default_rng(L)
+    ph = np.concatenate([rng.normal(0, 0.3, W * DE), rng.normal(0, 0.3, 16 * W),
+                         rng.uniform(-1, 1, 2 * off[-1])]).astype(np.float16)
+    params = t.from_numpy(ph.view(np.int16).copy()).cuda()
+    pos = rng.uniform(0.02, 0.98, (N, 3)).astype(np.float32)
+    x = t.from_numpy(pos).cuda()
+    ctx, y = m.forward(x, params, prepare_input_gradients=True)
+    # float64 reference
+    pd = torch.tensor(ph.astype(np.float64))
+    w0 = pd[: W * DE].reshape(W, DE).clone().requires_grad_(True)
+    w1 = pd[W * DE:n_mlp].reshape(16, W).clone().requires_grad_(True)
+    tab = pd[n_mlp:].reshape(-1, 2).clone().requires_grad_(True)
+    xt = torch.tensor(pos.astype(np.float64), requires_grad=True)
+    e = hash_grid(xt, tab, off, res)
+    ein = torch.nn.functional.pad(e, (0, DE - 2 * L))
+    pre = ein @ w0.T
+    hid = torch.relu(pre)
+    out = hid @ w1.T
+    yo = y.float().cpu().numpy()
+    ro = out.detach().numpy()
+    err = np.abs(yo - ro)
+    assert np.mean(err <= 4e-3 + 4e-3 * np.abs(ro)) >= 0.995, np.max(err)
+    dlo = rng.normal(0, 1, (N, 16)).astype(np.float16)
+    # A pre-activation within fp16 rounding of 0 may take the other ReLU branch on the device (its encoding is fp16):
+    # one such flip moves a float64 gradient by ~1% (a whole W1^T dL entry). Those samples get dL = 0, which removes
+    # them from every first- and second-order term on both sides.
+    ambiguous = (np.abs(pre.detach().numpy()) < 2e-3).any(axis=1)
+    assert ambiguous.mean() < 0.5
+    dlo[ambiguous] = 0
+    dlo_t = torch.tensor(dlo.astype(np.float64))
+    S = (out * dlo_t).sum()
+    gw0, gw1, gtab, gx = torch.autograd.grad(S, (w0, w1, tab, xt), create_graph=True)
+    v = rng.normal(0, 1, (N, 3)).astype(np.float32)
+    S2 = (gx * torch.tensor(v.astype(np.float64))).sum()
+    g2w0, g2w1, g2tab = torch.autograd.grad(S2, (w0, w1, tab))
+    dlo_dev = t.from_numpy(dlo.view(np.int16).copy()).cuda()
+    g = t.zeros(m.n_params, dtype=t.float32, device="cuda")
+    dx = t.zeros((N, 3), dtype=t.float32, device="cuda")
+    m.backward(ctx, x, dlo_dev, params, dL_dparams=g, dL_dinput=dx, mode=GradientMode.Overwrite)
+    gm = g.cpu().numpy()
+    blocks1 = {"W0": (gm[: W * DE], gw0), "W1": (gm[W * DE:n_mlp], gw1), "grid": (gm[n_mlp:], gtab), "dinput": (dx.cpu().numpy(), gx)}
+    g2 = t.zeros(m.n_params, dtype=t.float32, device="cuda")
+    m.backward_backward_input(ctx, x, t.from_numpy(v).cuda(), dlo_dev, params, dL_dparams=g2, mode=GradientMode.Overwrite)
+    g2m = g2.cpu().numpy()
+    blocks2 = {"W0_2nd": (g2m[: W * DE], g2w0), "W1_2nd": (g2m[W * DE:n_mlp], g2w1), "grid_2nd": (g2m[n_mlp:], g2tab)}
+    res_ = {}
+    for name, (a, b) in {**blocks1, **blocks2}.items():
+        res_[name] = _rel_cos(a, b.detach().numpy())
+    _record(f"module_network_with_input_encoding_L{L}_W{W}", **{f"rel_{k}": v_[0] for k, v_ in res_.items()},
+            **{f"cos_{k}": v_[1] for k, v_ in res_.items()})
+    for name, (rel, cos) in res_.items():
+        assert rel <= 5e-3 and cos >= 0.9999, (name, rel, cos)
+    # Accumulate: the second-order gradient added onto the first-order one
+    acc = g.clone()
+    m.backward_backward_input(ctx, x, t.from_numpy(v).cuda(), dlo_dev, params, dL_dparams=acc, mode=GradientMode.Accumulate)
+    np.testing.assert_allclose(acc.cpu().numpy(), gm + g2m, rtol=1e-6, atol=1e-6)

@@ -1,0 +1,93 @@
+"""The wide-block hash-grid gradient scatter (k_scatter_hist_w + k_scatter_bin_w: 1024-sample workgroups, grid.hip)
+against the 256-sample binned one (NEUS_SCATTER=binned): both bin the same fp16x2 corner contributions (first +
+second order, grid.h:371-500 and 880-1007) and sum them in int64 fixed point, so the grid gradient must be bitwise equal, for a
+backward on perturbed parameters (every level active, dense and hashed levels, the heavy split buckets of the small
+dense levels), for a backward at a low progressive level (inactive levels untouched), and over 40 training steps."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+from gpu_util import dev, ptr
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _testbed(sc, mode, batch):
+    """mode: "seg" (wide-block binning, 512-sample workgroups), "seg1024" (1024-sample ones) or "binned" (256)."""
+    from neus2_amd import pyngp
+    env = {"NEUS_SCATTER": "binned" if mode == "binned" else None, "NEUS_SCATTER_CHUNK": "1024" if mode == "seg1024" else None}
+    old = {k: os.environ.get(k) for k in env}
+    for k, v in env.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
+    try:
+        tb = pyngp.Testbed(pyngp.TestbedMode.Nerf)
+        tb.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
+        tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=batch)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    return tb
+
+
+@pytest.fixture(scope="module")
+def scene(torch_cuda):
+    from neus2_amd import scenes
+    return scenes.small_scene(n_views=8, width=64, height=48)
+
+
+def test_wide_scatter_bitwise_equals_binned(scene, torch_cuda):
+    from neus2_amd._lib import check, lib
+    t = torch_cuda
+    n = 1 << 14
+    seg, seg1k, binned = _testbed(scene, "seg", n), _testbed(scene, "seg1024", n), _testbed(scene, "binned", n)
+    lay = seg.layout()
+    rng = np.random.default_rng(17)
+    p = seg.get_params().copy()
+    din, L = lay["density_input_width"], lay["n_levels"]
+    w0 = p[: 64 * din].reshape(64, din)
+    w0[:, 3:3 + 2 * L] = rng.normal(0, 0.3, (64, 2 * L))
+    p[: 64 * din] = w0.reshape(-1)
+    p[lay["grid_offset"]:lay["variance_offset"]] = rng.uniform(-0.1, 0.1, lay["variance_offset"] - lay["grid_offset"])
+    for tb in (seg, seg1k, binned):
+        tb.set_params(p)
+    c = np.zeros((n, 7), np.float32)
+    c[:, :3] = rng.uniform(0.02, 0.98, (n, 3))
+    # runs of samples along "rays" (consecutive lanes sharing coarse cells: the wave run merge)
+    c[n // 2:, :3] = np.repeat(rng.uniform(0.1, 0.9, (n // 64, 3)), 32, axis=0) + np.tile(np.linspace(0, 0.02, 32), n // 64)[:, None]
+    d = rng.normal(size=(n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    c[:, 4:] = (d + 1) * 0.5
+    dl = np.zeros((n, 16), np.float32)
+    dl[:, :4] = rng.normal(0, 1e-2, (n, 4))
+    dl[:, 4:7] = rng.normal(0, 1.0, (n, 3))
+    dl[:, 7] = rng.normal(0, 1e-2, n)
+    dl16 = dl.astype(np.float16)
+    for valid in (L, 3):
+        grads = []
+        for tb in (seg, seg1k, binned):
+            g = t.zeros(lay["n_params"], dtype=t.float32, device="cuda")
+            check(lib().neus_net_backward(tb.handle, None, C.c_uint32(n), ptr(dev(t, c)), C.c_uint32(valid), ptr(dev(t, dl16)),
+                                          C.c_uint32(n), ptr(g)))
+            t.cuda.synchronize()
+            grads.append(g.cpu().numpy())
+        a, a1k, b = grads
+        g0, g1 = lay["grid_offset"], lay["variance_offset"]
+        assert np.any(a[g0:g1])
+        np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
+        np.testing.assert_array_equal(a1k.view(np.uint32), b.view(np.uint32))
+    # training: 40 steps (progressive levels 3 -> 3, occupancy updates) bitwise equal
+    seg2, bin2 = _testbed(scene, "seg", 4096), _testbed(scene, "binned", 4096)
+    seg2.train_steps(40)
+    bin2.train_steps(40)
+    np.testing.assert_array_equal(seg2.get_params().view(np.uint32), bin2.get_params().view(np.uint32))
+    np.testing.assert_array_equal(seg2.get_gradients().view(np.uint32), bin2.get_gradients().view(np.uint32))
