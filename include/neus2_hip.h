@@ -292,6 +292,10 @@ int neus_testbed_time_kernel(NeusTestbed* tb, int kernel, int iters, float* ms_o
 // Development statistic of the last step's march: per ray {march_step calls, skip-loop additions,
 // samples} (3 x u32 per ray, n rays; cone_angle 0 only).
 int neus_debug_march_stats(NeusTestbed* tb, uint32_t n, uint32_t* out);
+/* Development check of the single-pass exclusive scan the step's compactions use (scan.hip): device buffers in / out
+ * of n u32 on `hip_stream`, `reps` launches on one fresh state (the epoch re-arm), synchronous; failures = bounded-wait
+ * give-ups (0 expected). */
+int neus_debug_exclusive_scan(void* hip_stream, const uint32_t* in, uint32_t* out, uint32_t n, int reps, uint32_t* failures);
 int neus_testbed_stream(NeusTestbed* tb, void** hip_stream);
 int neus_testbed_synchronize(NeusTestbed* tb);
 /* Per-phase step timing with hipEvents recorded on the testbed stream (profiling on), mean ms per step:

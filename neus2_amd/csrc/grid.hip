@@ -193,6 +193,7 @@ __global__ void __launch_bounds__(256) k_scatter_hist(const uint32_t* __restrict
 	}
 	__syncthreads();
 	for (uint32_t b = threadIdx.x; b < w.n_active; b += blockDim.x) w.counts[(size_t)b * w.n_blocks + xcd_slot(blk, w.n_blocks)] = hist[b];
+	if (blk == 0 && threadIdx.x == 0) w.counts[(size_t)w.n_active * w.n_blocks] = 0u;  // the scan's extra element: offs[end] = total
 }
 
 // Per wave and level: each lane keeps its 8 records in registers while their buckets are counted (as
@@ -316,6 +317,7 @@ __global__ void __launch_bounds__(BS) k_scatter_hist_w(const uint32_t* __restric
 	}
 	__syncthreads();
 	for (uint32_t b = threadIdx.x; b < w.n_active; b += blockDim.x) w.counts[(size_t)b * w.n_chunks + xcd_slot(blk, w.n_chunks)] = hist[b];
+	if (blk == 0 && threadIdx.x == 0) w.counts[(size_t)w.n_active * w.n_chunks] = 0u;  // the scan's extra element: offs[end] = total
 }
 
 template <int BS>
@@ -594,7 +596,6 @@ void launch_grid_scatter(hipStream_t s, const uint32_t* n_ptr, uint32_t n_fixed,
 		else
 			k_scatter_hist_w<512><<<w.n_chunks, 512, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, (const uint32_t*)dLdenc,
 			                                                 (const uint32_t*)g, v, w);
-		(void)hipMemsetAsync(w.counts + nb, 0, 4, s);
 		launch_exclusive_scan(s, scan_tmp, scan_tmp_bytes, w.counts, w.offs, (uint32_t)nb + 1);
 		if (w.chunk == 1024)
 			k_scatter_bin_w<1024><<<w.n_chunks, 1024, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, (const uint32_t*)dLdenc,
@@ -611,7 +612,6 @@ void launch_grid_scatter(hipStream_t s, const uint32_t* n_ptr, uint32_t n_fixed,
 	const uint32_t nblk = w.n_blocks;
 	const size_t nb = (size_t)w.n_active * w.n_blocks;  // buckets past n_active get no records (scatter_work_for)
 	k_scatter_hist<<<nblk, 256, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, (const uint32_t*)dLdenc, (const uint32_t*)g, v, w);
-	(void)hipMemsetAsync(w.counts + nb, 0, 4, s);
 	launch_exclusive_scan(s, scan_tmp, scan_tmp_bytes, w.counts, w.offs, (uint32_t)nb + 1);
 	k_scatter_bin<<<nblk, 256, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, (const uint32_t*)dLdenc, (const uint32_t*)g, v, w);
 	// every bucket (also one without records: its entries' gradient is zero) is written by its workgroup

@@ -187,6 +187,10 @@ uint32_t dnet_blocks(uint32_t n);  // the grid of launch_dnet (= the partial row
 void launch_dnet(hipStream_t s, uint32_t L, uint32_t W, int mode /* 0 fwd, 1 bwd, 2 bwd-bwd */, uint32_t n, const DNetLaunch& d);
 // march.hip
 void launch_bitfield_linear(hipStream_t s, const uint8_t* bitfield, uint32_t* lin /* LIN_WORDS */);
+// world-space box of every occupied cell of every mip -> scratch[0..6) = {min xyz, max xyz} (optim.hip); the ray
+// generation culls rays that miss it. scratch: occ_bbox_scratch_floats() floats.
+size_t occ_bbox_scratch_floats();
+void launch_occ_bbox(hipStream_t s, const uint8_t* bitfield, float* scratch);
 // Sample runs of the march (march.hip): per ray slot up to NERF_STEPS records {t of the run's first sample,
 // (samples of the ray before the run) << 16 | run length}; a run's samples are t, t + dt(t), ... (the reference's
 // t += dt), at most MARCH_RUN_MAX of them. nrec: records per slot; counter: the persistent march's ray queue.
@@ -202,9 +206,17 @@ struct MarchWork {
 // Ray generation + the occupancy march: rays (6 f32 per slot), tstart (1 per slot), nreq (requested
 // samples per slot) and the sample runs (MarchWork).
 void launch_march_count(hipStream_t s, uint32_t cap, uint32_t max_samples /* global cap: 16 x batch */, StepState* st, DPInfo dp, const DevDataset& ds, const uint8_t* bitfield,
-                        const uint32_t* lin, uint64_t rng_state, uint64_t rng_inc, float* rays, float* tstart, uint32_t* nreq, const MarchWork& mw);
+                        const uint32_t* lin, uint64_t rng_state, uint64_t rng_inc, float* rays, float* tstart, uint32_t* nreq, const MarchWork& mw,
+                        uint32_t* zero_counters = nullptr, uint32_t n_zero = 0,
+                        const float* occ_bbox = nullptr /* launch_occ_bbox; null: no culling */);
+// Progressive round 0's work list, written by the march (the first min(n, e1) samples of every kept ray at the
+// exclusive scan c0 of those counts); counters[0] = its length, counters[1 .. n_counters) zeroed for the later rounds.
+struct Round0List { uint32_t e1; uint32_t* c0; uint32_t* list; uint32_t* counters; uint32_t n_counters; };
+// k_march_scan (the scan of the requested counts fused with numsteps, scan_temp = a scan_temp_bytes buffer) and
+// k_march_write; round0 nullable
 void launch_march_write(hipStream_t s, uint32_t cap, StepState* st, const DevDataset& ds, const float* rays, const MarchWork& mw, const uint32_t* nreq,
-                        const uint32_t* base, uint32_t* numsteps, float* coords, uint32_t* sample_ray, uint32_t sample_cap /* >= max_inference */);
+                        uint32_t* base, uint32_t* numsteps, float* coords, uint32_t* sample_ray, uint32_t sample_cap, void* scan_temp,
+                        const Round0List* round0 = nullptr);
 void debug_launch_march_stats(hipStream_t s, uint32_t n_rays, const float* rays, const float* tstart, const uint32_t* lin, const DevDataset& ds,
                               const uint8_t* bf, uint32_t* out);
 // dt_const: every sample's dt is MIN_CONE_STEPSIZE (cone angle 0, coordinates from k_march_write): the kernel
@@ -215,10 +227,6 @@ void launch_loss_scan_ray(hipStream_t s, uint32_t cap_rays, const uint32_t* nums
 // progressive (cut-off-aware) inference rounds (march.hip)
 void launch_loss_alpha_list(hipStream_t s, uint32_t cap_samples, const uint32_t* n_ptr, const uint32_t* idx, const float* coords,
                             const half_t* net_out, float cos_anneal, const LossWork& w, bool dt_const = false);
-void launch_chunk_count(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, uint32_t e1, uint32_t* m, uint32_t* counters /* zeroed */,
-                        uint32_t n_counters);
-void launch_chunk_write(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, const uint32_t* m, const uint32_t* pos /* exclusive scan of m */,
-                        uint32_t* list, uint32_t* counter);
 void launch_loss_scan_chunk(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, const LossWork& w, uint32_t* ccount, uint32_t e0,
                             uint32_t e1, uint32_t e2, uint32_t* list /* nullptr in the last round */, uint32_t* next_counter);
 void launch_loss_ray(hipStream_t s, uint32_t cap_rays, StepState* st, DPInfo dp, const DevDataset& ds, const LossParams& lp, uint32_t* numsteps,
@@ -263,6 +271,12 @@ size_t delta_partial_floats();
 void host_accumulate_movement(const float delta_p[DELTA_PARAMS], float accR[9], float acct[3]);
 // scan.hip
 size_t scan_temp_bytes(uint32_t n);
+// zero the look-back state at the start of a scan temp buffer once after allocating it; scan_failures reads its
+// bounded-wait failure count (0 unless the state was corrupted)
+void scan_temp_reset(hipStream_t s, void* temp);
+// the look-back tag of the next scan launch on this temp buffer (scan.hip; used by the fused scans of march.hip)
+uint32_t scan_next_tag(void* temp);
+uint32_t scan_failures(void* temp);
 void launch_exclusive_scan(hipStream_t s, void* temp, size_t temp_bytes, const uint32_t* in, uint32_t* out, uint32_t n);
 void launch_sum_f32(hipStream_t s, void* temp, size_t temp_bytes, const float* in, float* out, uint32_t n);
 // optim.hip

@@ -15,6 +15,7 @@
 // arithmetic are bit-identical to the CPU oracle (no FMA contraction, det_expf).
 #pragma clang fp contract(off)
 #include "march_common.h"
+#include "scan_lookback.h"
 #include <algorithm>
 
 namespace neus {
@@ -35,13 +36,35 @@ __global__ void k_bitfield_linear(const uint8_t* __restrict__ bf, uint32_t* __re
 	}
 	lin[w] = word;
 }
+// Conservative slab test of the ray o + t d, t >= 0, against the box bb = {min xyz, max xyz} (touching counts as a hit).
+__device__ __forceinline__ bool ray_hits_box(const float o[3], const float d[3], const float bb[6]) {
+	float tn = 0.0f, tf = 3.402823466e+38f;
+#pragma unroll
+	for (int k = 0; k < 3; ++k) {
+		if (fabsf(d[k]) < 1e-20f) {
+			if (o[k] < bb[k] || o[k] > bb[3 + k]) return false;
+			continue;
+		}
+		const float inv = 1.0f / d[k];
+		float a = (bb[k] - o[k]) * inv, b = (bb[3 + k] - o[k]) * inv;
+		if (a > b) { const float t = a; a = b; b = t; }
+		tn = fmaxf(tn, a); tf = fminf(tf, b);
+	}
+	return tn <= tf;
+}
 // ---------------------------------------------------------------- pass 0: ray generation
 // Thread per ray slot: pixel/image pick from the ray's pcg32 stream, pinhole ray, AABB entry and
 // jittered start (testbed_nerf.cu:1263-1375). rays: 6 floats (o, unnormalised d); tstart: the jittered
 // start t, or -1 for a dropped ray and for slots >= R (nothing to march).
 __global__ void __launch_bounds__(256) k_ray_gen(uint32_t cap_rays, const StepState* __restrict__ st_r, DPInfo dp, DevDataset ds,
                                                  uint64_t rng_state, uint64_t rng_inc, float* __restrict__ rays, float* __restrict__ tstart,
-                                                 uint32_t* __restrict__ march_queue, StepState* __restrict__ st_w, PcgJumpTable jt) {
+                                                 uint32_t* __restrict__ march_queue, StepState* __restrict__ st_w, PcgJumpTable jt,
+                                                 uint32_t* __restrict__ zero_counters, uint32_t n_zero, const float* __restrict__ occ_bbox) {
+	if (blockIdx.x == 0 && threadIdx.x < n_zero) zero_counters[threadIdx.x] = 0u;  // the progressive rounds' list lengths
+	float bb[6] = {-3.402823466e+38f, -3.402823466e+38f, -3.402823466e+38f, 3.402823466e+38f, 3.402823466e+38f, 3.402823466e+38f};
+	if (occ_bbox)
+#pragma unroll
+		for (int k = 0; k < 6; ++k) bb[k] = occ_bbox[k];
 	if (blockIdx.x == 0 && threadIdx.x == 0) {  // the march passes' ray queues and counters (next kernels on the stream)
 		march_queue[0] = 0; march_queue[1] = 0;
 		st_w->march_total = 0; st_w->kept_extent = 0;
@@ -89,6 +112,8 @@ __global__ void __launch_bounds__(256) k_ray_gen(uint32_t cap_rays, const StepSt
 				tmin = fmaxf(tmin, 0.0f);
 				startt = tmin;
 				startt += calc_dt(startt, ds.cone_angle) * rng.next_float();
+				// a ray (t >= 0) that misses the occupied cells' padded box samples nothing: not marched
+				if (occ_bbox && !ray_hits_box(o, dir, bb)) startt = -1.0f;
 			}
 		}
 		float* rr = rays + 6 * (size_t)i;
@@ -407,28 +432,69 @@ __device__ __forceinline__ float run_sample_t(const MarchWork& mw, uint32_t i, u
 }
 
 // ---------------------------------------------------------------- pass 2: write kept rays
-// (a) per ray slot: numsteps (n or 0, base), the requested total and the kept-sample extent / kept-ray
-//     count (one atomic pair per wave).
-__global__ void __launch_bounds__(256) k_march_numsteps(uint32_t cap_rays, StepState* __restrict__ st, const uint32_t* __restrict__ nreq,
-                                                        const uint32_t* __restrict__ base, uint32_t* __restrict__ numsteps) {
+// (a) k_march_scan, one launch (scan_lookback.h): the exclusive scan of the requested counts (base), and per ray slot
+//     numsteps (n or 0, base), the requested total, the kept-sample extent / kept-ray count (one atomic triple per
+//     4096-slot tile); with a round-0 list (progressive inference) also the exclusive scan of min(n, e1) (the slot of
+//     each kept ray's first chunk in the list: the rays before a kept ray with samples are all kept, so the dropped
+//     rays' terms never reach a kept ray's prefix) and the list's length (an atomic max per tile).
+__global__ void __launch_bounds__(SCAN_THREADS) k_march_scan(uint32_t cap_rays, StepState* __restrict__ st, const uint32_t* __restrict__ nreq,
+                                                             uint32_t* __restrict__ base, uint32_t* __restrict__ numsteps, ScanState* __restrict__ ss,
+                                                             uint32_t tag, Round0List r0) {
+	__shared__ uint32_t s_pre[2], s_wsum[2][SCAN_THREADS / 64], s_red[4][SCAN_THREADS / 64];
+	const ScanTile tl = scan_tile(tag);
 	const uint32_t max_samples = st->max_inference;
-	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-	const bool in_range = i < cap_rays;
-	const uint32_t n = in_range ? nreq[i] : 0, b = in_range ? base[i] : 0;
-	const bool keep = n > 0 && b + n <= max_samples;
-	if (in_range) {
-		if (i == cap_rays - 1) st->numsteps_counter = b + n;
-		numsteps[2 * i] = keep ? n : 0;
-		numsteps[2 * i + 1] = b;
-	}
-	uint32_t kmax = keep ? b + n : 0u, kcnt = keep ? 1u : 0u, kext = keep ? i + 1 : 0u;
-	if (__ballot(kcnt != 0)) {
+	const uint32_t i0 = tl.tile * SCAN_TILE + threadIdx.x * SCAN_ITEMS;
+	uint32_t v[SCAN_ITEMS];
+	scan_load16(nreq, i0, cap_rays, true, v);
+	uint32_t tsum = 0, tsum2 = 0;
 #pragma unroll
-		for (int off = 32; off > 0; off >>= 1) {
-			kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, off)); kcnt += (uint32_t)__shfl_xor((int)kcnt, off);
-			kext = max(kext, (uint32_t)__shfl_xor((int)kext, off));
+	for (int k = 0; k < (int)SCAN_ITEMS; ++k) { tsum += v[k]; tsum2 += min(v[k], r0.e1); }
+	uint32_t agg, agg2 = 0;
+	const uint32_t tex = scan_block(tsum, s_wsum[0], agg);
+	const uint32_t tex2 = r0.list ? scan_block(tsum2, s_wsum[1], agg2) : 0u;
+	if (threadIdx.x < 64) {
+		const uint32_t p = scan_lookback(ss, 0, tl, agg);
+		const uint32_t p2 = r0.list ? scan_lookback(ss, 1, tl, agg2) : 0u;
+		if (threadIdx.x == 0) { s_pre[0] = p; s_pre[1] = p2; }
+	}
+	__syncthreads();
+	uint32_t b = s_pre[0] + tex, c = s_pre[1] + tex2;
+	uint32_t bo[SCAN_ITEMS], ns[2 * SCAN_ITEMS], co[SCAN_ITEMS];
+	uint32_t kmax = 0, kcnt = 0, kext = 0, cmax = 0;
+#pragma unroll
+	for (int k = 0; k < (int)SCAN_ITEMS; ++k) {
+		const uint32_t n = v[k], i = i0 + k;
+		const bool keep = n > 0 && b + n <= max_samples && i < cap_rays;
+		if (i == cap_rays - 1) st->numsteps_counter = b + n;
+		bo[k] = b; ns[2 * k] = keep ? n : 0u; ns[2 * k + 1] = b; co[k] = c;
+		if (keep) { kmax = max(kmax, b + n); ++kcnt; kext = i + 1; cmax = max(cmax, c + min(n, r0.e1)); }
+		b += n; c += min(n, r0.e1);
+	}
+	scan_store16(base, i0, cap_rays, true, bo);
+	if (i0 + SCAN_ITEMS <= cap_rays) {
+		uint4* p = (uint4*)(numsteps + 2 * (size_t)i0);
+#pragma unroll
+		for (int q = 0; q < (int)SCAN_ITEMS / 2; ++q) p[q] = make_uint4(ns[4 * q], ns[4 * q + 1], ns[4 * q + 2], ns[4 * q + 3]);
+	} else {
+#pragma unroll
+		for (int k = 0; k < (int)SCAN_ITEMS; ++k) if (i0 + k < cap_rays) { numsteps[2 * (i0 + k)] = ns[2 * k]; numsteps[2 * (i0 + k) + 1] = ns[2 * k + 1]; }
+	}
+	if (r0.list) scan_store16(r0.c0, i0, cap_rays, true, co);
+	// the tile's kept maxima / count: one atomic each
+#pragma unroll
+	for (int off = 32; off > 0; off >>= 1) {
+		kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, off)); kcnt += (uint32_t)__shfl_xor((int)kcnt, off);
+		kext = max(kext, (uint32_t)__shfl_xor((int)kext, off)); cmax = max(cmax, (uint32_t)__shfl_xor((int)cmax, off));
+	}
+	const uint32_t wv = threadIdx.x >> 6;
+	if ((threadIdx.x & 63) == 0) { s_red[0][wv] = kmax; s_red[1][wv] = kcnt; s_red[2][wv] = kext; s_red[3][wv] = cmax; }
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		for (int w = 1; w < (int)(SCAN_THREADS / 64); ++w) {
+			kmax = max(kmax, s_red[0][w]); kcnt += s_red[1][w]; kext = max(kext, s_red[2][w]); cmax = max(cmax, s_red[3][w]);
 		}
-		if ((threadIdx.x & 63) == 0) { atomicMax(&st->n_kept, kmax); atomicAdd(&st->n_rays_with_samples, kcnt); atomicMax(&st->kept_extent, kext); }
+		if (kcnt) { atomicMax(&st->n_kept, kmax); atomicAdd(&st->n_rays_with_samples, kcnt); atomicMax(&st->kept_extent, kext); }
+		if (r0.list && cmax) atomicMax(&r0.counters[0], cmax);  // the round-0 list's length (counters zeroed by k_ray_gen)
 	}
 }
 
@@ -447,9 +513,9 @@ __device__ __forceinline__ uint32_t last_le(const uint32_t* __restrict__ a, uint
 __global__ void __launch_bounds__(256) k_march_write(uint32_t cap_rays, const StepState* __restrict__ st, DevDataset ds,
                                                      const float* __restrict__ rays, const MarchWork mw,
                                                      const uint32_t* __restrict__ nreq, const uint32_t* __restrict__ base,
-                                                     float* __restrict__ coords, uint32_t* __restrict__ sample_ray) {
+                                                     float* __restrict__ coords, uint32_t* __restrict__ sample_ray, Round0List r0) {
 	__shared__ float s_ray[6][256];
-	__shared__ uint32_t s_b[256], s_n[256], s_roff[256];
+	__shared__ uint32_t s_b[256], s_n[256], s_roff[256], s_c0[256];
 	__shared__ uint32_t s_range[3];
 	__shared__ uint32_t s_t0[WRITE_CHUNK];  // per chunk sample: t of its run's first sample (bits)
 	__shared__ uint16_t s_r[WRITE_CHUNK];   // its ray within the staged batch
@@ -473,6 +539,7 @@ __global__ void __launch_bounds__(256) k_march_write(uint32_t cap_rays, const St
 			const uint32_t n = nreq[i], b = base[i];
 			const bool keep = n > 0 && b + n <= max_samples;
 			s_b[tid] = b; s_n[tid] = keep ? n : 0u;
+			if (r0.list) s_c0[tid] = r0.c0[i];
 			if (keep) {
 				MarchRay mr;
 				load_march_ray(rays, i, mr, ds.motion.on != 0);
@@ -532,6 +599,7 @@ __global__ void __launch_bounds__(256) k_march_write(uint32_t cap_rays, const St
 			*(f4u*)cc = p4;
 			*(f3u*)(cc + 4) = (f3u){(dir[0] + 1.0f) * 0.5f, (dir[1] + 1.0f) * 0.5f, (dir[2] + 1.0f) * 0.5f};
 			sample_ray[q] = i;
+			if (r0.list && j < r0.e1) r0.list[s_c0[r] + j] = q;  // the first chunk of the ray: progressive round 0
 		}
 		__syncthreads();
 	}
@@ -599,16 +667,16 @@ __global__ void __launch_bounds__(256) k_loss_alpha(uint32_t cap, const uint32_t
 }
 
 // Transmittance recurrence state of a ray (reference order: w = a T; rgb += w c; ws += w; ek += e; T *= 1 - a).
-struct ScanState { float T, r0, r1, r2, ek; };
+struct RecState { float T, r0, r1, r2, ek; };
 constexpr uint32_t SCAN_CK = 8;  // checkpoint stride of the stored scan state (in global sample index)
 constexpr uint32_t LONG_RAY = 32; // rays with more samples go to k_loss_scan_list
 
 // Replays the recurrence from the last stored checkpoint at or before sample s (or the ray start)
 // through sample s; returns T before s in T_before, and the state after s.
-__device__ __forceinline__ ScanState scan_replay(uint32_t base, uint32_t s, const float4* __restrict__ sa, const float* __restrict__ ekt,
+__device__ __forceinline__ RecState scan_replay(uint32_t base, uint32_t s, const float4* __restrict__ sa, const float* __restrict__ ekt,
                                                  const float4* __restrict__ ck4, const float* __restrict__ cke, float& T_before) {
 	const uint32_t g = s & ~(SCAN_CK - 1);
-	ScanState st{1.f, 0.f, 0.f, 0.f, 0.f};
+	RecState st{1.f, 0.f, 0.f, 0.f, 0.f};
 	uint32_t k = base;
 	if (g > base) { const float4 c = ck4[g / SCAN_CK]; st = {c.x, c.y, c.z, c.w, cke[g / SCAN_CK]}; k = g; }
 	for (; k <= s; ++k) {
@@ -774,82 +842,120 @@ __global__ void __launch_bounds__(64) k_loss_scan_list(const uint32_t* __restric
 // samples past the cut are never evaluated. The work lists hold sample indices; their order is immaterial (each
 // work item writes its own sample's slots).
 
-// Round 0's list: the first min(ns, e1) samples of every ray, at the exclusive scan of those counts
-// (k_chunk_count -> scan -> k_chunk_write; no atomics: one counter hit per wave serialises on a single address).
-__global__ void __launch_bounds__(256) k_chunk_count(uint32_t cap_rays, const uint32_t* __restrict__ numsteps, uint32_t e1,
-                                                     uint32_t* __restrict__ m, uint32_t* __restrict__ counters, uint32_t n_counters) {
-	if (blockIdx.x == 0 && threadIdx.x < n_counters) counters[threadIdx.x] = 0u;  // the rounds' list sizes
-	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cap_rays; i += gridDim.x * blockDim.x) m[i] = min(numsteps[2 * i], e1);
-}
-__global__ void __launch_bounds__(256) k_chunk_write(uint32_t cap_rays, const uint32_t* __restrict__ numsteps, const uint32_t* __restrict__ m,
-                                                     const uint32_t* __restrict__ pos, uint32_t* __restrict__ list, uint32_t* __restrict__ counter) {
-	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cap_rays; i += gridDim.x * blockDim.x) {
-		const uint32_t k = m[i], p = pos[i], base = numsteps[2 * i + 1];
-		for (uint32_t j = 0; j < k; ++j) list[p + j] = base + j;
-		if (i == cap_rays - 1) *counter = p + k;
-	}
-}
-
 // Round k's recurrence over [e0, e1) of each ray still open (all rays with samples when e0 == 0), continuing from
 // the stored state; rays that stay open append their next chunk [e1, min(ns, e2)) to the next round's list.
-__global__ void __launch_bounds__(256) k_loss_scan_chunk(uint32_t cap_rays, const uint32_t* __restrict__ numsteps, const float4* __restrict__ sa,
-                                                         const float* __restrict__ ekt, float4* __restrict__ ck4, float* __restrict__ cke,
-                                                         uint32_t* __restrict__ ccount, float4* __restrict__ racc, float* __restrict__ rT,
-                                                         float* __restrict__ rek, uint32_t e0, uint32_t e1, uint32_t e2,
-                                                         uint32_t* __restrict__ list, uint32_t* __restrict__ next_counter) {
-	const uint32_t stride = gridDim.x * blockDim.x;
-	for (uint32_t k = threadIdx.x * gridDim.x + blockIdx.x; k < ((cap_rays + stride - 1) / stride) * stride; k += stride) {
-		const uint32_t i = k;
-		if (i >= cap_rays) continue;
-		const uint32_t ns = numsteps[2 * i], base = numsteps[2 * i + 1];
+// 64 consecutive rays to a one-wave block, one lane per ray, the loads made coalesced as in k_loss_scan_list: per
+// 16-sample group 16 lanes fetch one ray's 16 samples (4 rays per load instruction), staged through LDS, the next
+// group's fetches in flight while the current one runs through the recurrence (one lane loading its own ray's samples
+// put 64 lines behind every load instruction). The appends are one atomic per wave and a cooperative write of the
+// wave's concatenated chunks (consecutive lanes, consecutive list slots). Same float operation sequence per ray, so
+// the state is bitwise the one-thread-per-ray loop's.
+__global__ void __launch_bounds__(64) k_loss_scan_chunk(uint32_t cap_rays, const uint32_t* __restrict__ numsteps, const float4* __restrict__ sa,
+                                                        const float* __restrict__ ekt, float4* __restrict__ ck4, float* __restrict__ cke,
+                                                        uint32_t* __restrict__ ccount, float4* __restrict__ racc, float* __restrict__ rT,
+                                                        float* __restrict__ rek, uint32_t e0, uint32_t e1, uint32_t e2,
+                                                        uint32_t* __restrict__ list, uint32_t* __restrict__ next_counter) {
+	constexpr uint32_t U = 16, PAD = U + 1;
+	typedef float f4v __attribute__((ext_vector_type(4)));
+	__shared__ f4v s_q[64 * PAD];
+	__shared__ float s_e[64 * PAD];
+	__shared__ uint32_t s_pre[64], s_src[64];
+	const uint32_t lane = threadIdx.x, sub = lane >> 4, el = lane & 15;
+	const char* sab = (const char*)sa;
+	const char* ekb = (const char*)ekt;
+	for (uint32_t w0 = blockIdx.x * 64; w0 < cap_rays; w0 += gridDim.x * 64) {
+		const uint32_t i = w0 + lane;
+		const bool inr = i < cap_rays;
+		const uint32_t ns = inr ? numsteps[2 * i] : 0u, base = inr ? numsteps[2 * i + 1] : 0u;
 		RayScan S{1.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0u};
-		if (e0 > 0) {
+		bool open = inr && (e0 == 0 || ns > 0);  // this round runs (and stores) the ray's state
+		if (e0 > 0 && open) {
 			S.cn = ccount[i];
-			if (S.cn != e0 || e0 >= ns) continue;  // closed in an earlier round (or no samples)
-			S.T = rT[i];
-			if (S.T < 1e-4f) continue;
-			const float4 a = racc[i];
-			S.r0 = a.x; S.r1 = a.y; S.r2 = a.z; S.ws = a.w; S.ek = rek[i];
-		}
-		const uint32_t to = min(ns, e1);
-		if (to > e0) {
-			// the same software-pipelined loop as k_loss_scan_ray, over [e0, to)
-			constexpr uint32_t U = 16;
-			const uint32_t last = base + to - 1;
-			float4 qn[U]; float en[U];
-#pragma unroll
-			for (uint32_t u = 0; u < U; ++u) { const uint32_t s = min(base + e0 + u, last); qn[u] = sa[s]; en[u] = ekt[s]; }
-			bool done = false;
-			for (uint32_t c = e0; c < to && !done; c += U) {
-				float4 q[U]; float e[U];
-#pragma unroll
-				for (uint32_t u = 0; u < U; ++u) { q[u] = qn[u]; e[u] = en[u]; }
-				if (c + U < to) {
-#pragma unroll
-					for (uint32_t u = 0; u < U; ++u) { const uint32_t s = min(base + c + U + u, last); qn[u] = sa[s]; en[u] = ekt[s]; }
-				}
-#pragma unroll
-				for (uint32_t u = 0; u < U; ++u) {
-					if (c + u >= to || S.T < 1e-4f) { done = true; break; }
-					const uint32_t s = base + c + u;
-					if ((s & (SCAN_CK - 1)) == 0) { ck4[s / SCAN_CK] = make_float4(S.T, S.r0, S.r1, S.r2); cke[s / SCAN_CK] = S.ek; }
-					const float w = q[u].x * S.T;
-					S.r0 += w * q[u].y; S.r1 += w * q[u].z; S.r2 += w * q[u].w;
-					S.ws += w;
-					S.ek += e[u];
-					S.T *= (1.f - q[u].x);
-					++S.cn;
-				}
+			if (S.cn != e0 || e0 >= ns) open = false;  // closed in an earlier round (or no samples)
+			else {
+				S.T = rT[i];
+				if (S.T < 1e-4f) open = false;
+				else { const float4 a = racc[i]; S.r0 = a.x; S.r1 = a.y; S.r2 = a.z; S.ws = a.w; S.ek = rek[i]; }
 			}
 		}
-		ccount[i] = S.cn;
-		racc[i] = make_float4(S.r0, S.r1, S.r2, S.ws);
-		rT[i] = S.T;
-		rek[i] = S.ek;
-		if (list && S.cn == e1 && e1 < ns && S.T >= 1e-4f) {
-			const uint32_t m = min(ns, e2) - e1;
-			const uint32_t p = atomicAdd(next_counter, m);
-			for (uint32_t j = 0; j < m; ++j) list[p + j] = base + e1 + j;
+		const uint32_t to = min(ns, e1);
+		bool live = open && to > e0;
+		const uint32_t g0 = live ? base + e0 : 0u, gl = live ? base + to - 1u : 0u;  // the round's samples [g0, gl]
+		uint32_t lb[U], ll[U];
+#pragma unroll
+		for (uint32_t j = 0; j < U; ++j) { lb[j] = __shfl(g0, 4 * j + sub); ll[j] = __shfl(gl, 4 * j + sub); }
+		auto fetch = [&](f4v (&q)[U], float (&e)[U], uint32_t c) {
+#pragma unroll
+			for (uint32_t j = 0; j < U; ++j) {
+				const uint32_t g = min(lb[j] + c + el, ll[j]);
+				q[j] = *(const f4v*)(sab + ((size_t)g << 4));
+				e[j] = *(const float*)(ekb + ((size_t)g << 2));
+			}
+		};
+		auto group = [&](f4v (&qs)[U], float (&es)[U], uint32_t c) {
+			__builtin_amdgcn_wave_barrier();
+#pragma unroll
+			for (uint32_t j = 0; j < U; ++j) { s_q[(4 * j + sub) * PAD + el] = qs[j]; s_e[(4 * j + sub) * PAD + el] = es[j]; }
+			__builtin_amdgcn_wave_barrier();
+			fetch(qs, es, c + 2 * U);
+			f4v q[U]; float e[U];
+#pragma unroll
+			for (uint32_t u = 0; u < U; ++u) { q[u] = s_q[lane * PAD + u]; e[u] = s_e[lane * PAD + u]; }
+#pragma unroll
+			for (uint32_t u = 0; u < U; ++u) {
+				live = live && (e0 + c + u < to) && !(S.T < 1e-4f);
+				const uint32_t s = base + e0 + c + u;
+				if (live && (s & (SCAN_CK - 1)) == 0) { ck4[s / SCAN_CK] = make_float4(S.T, S.r0, S.r1, S.r2); cke[s / SCAN_CK] = S.ek; }
+				const float w = q[u][0] * S.T;
+				const float n0 = S.r0 + w * q[u][1], n1 = S.r1 + w * q[u][2], n2 = S.r2 + w * q[u][3];
+				const float nws = S.ws + w, nek = S.ek + e[u], nT = S.T * (1.f - q[u][0]);
+				S.r0 = live ? n0 : S.r0; S.r1 = live ? n1 : S.r1; S.r2 = live ? n2 : S.r2;
+				S.ws = live ? nws : S.ws; S.ek = live ? nek : S.ek; S.T = live ? nT : S.T;
+				S.cn += live ? 1u : 0u;
+			}
+			__builtin_amdgcn_wave_barrier();
+		};
+		if (__ballot(live)) {
+			f4v qa[U], qb[U]; float ea[U], eb[U];
+			fetch(qa, ea, 0);
+			fetch(qb, eb, U);
+			for (uint32_t c = 0;; c += 2 * U) {
+				if (__ballot(live && e0 + c < to) == 0) break;
+				group(qa, ea, c);
+				if (__ballot(live && e0 + c + U < to) == 0) break;
+				group(qb, eb, c + U);
+			}
+		}
+		if (open) {
+			ccount[i] = S.cn;
+			racc[i] = make_float4(S.r0, S.r1, S.r2, S.ws);
+			rT[i] = S.T;
+			rek[i] = S.ek;
+		}
+		if (list) {
+			// the next round's chunk of every ray still open: one reservation per wave, written lane-contiguously
+			const uint32_t m = (open && S.cn == e1 && e1 < ns && S.T >= 1e-4f) ? min(ns, e2) - e1 : 0u;
+			uint32_t incl = m;
+#pragma unroll
+			for (int d = 1; d < 64; d <<= 1) { const uint32_t y = (uint32_t)__shfl_up((int)incl, d); if ((int)lane >= d) incl += y; }
+			const uint32_t total = (uint32_t)__shfl((int)incl, 63);
+			if (total) {
+				uint32_t p0 = 0;
+				if (lane == 0) p0 = atomicAdd(next_counter, total);
+				p0 = (uint32_t)__shfl((int)p0, 0);
+				__builtin_amdgcn_wave_barrier();
+				s_pre[lane] = incl - m;
+				s_src[lane] = base + e1;
+				__builtin_amdgcn_wave_barrier();
+				for (uint32_t r = lane; r < total; r += 64) {
+					// the owner: the last lane whose chunk starts at or before r (zero-length lanes share its start)
+					uint32_t o = 0;
+#pragma unroll
+					for (uint32_t step = 32; step > 0; step >>= 1) if (s_pre[o + step] <= r) o += step;
+					list[p0 + r] = s_src[o] + (r - s_pre[o]);
+				}
+				__builtin_amdgcn_wave_barrier();
+			}
 		}
 	}
 }
@@ -919,7 +1025,7 @@ __global__ void __launch_bounds__(256) k_loss_ray(uint32_t cap_rays, StepState* 
 		loss_out[i] = mean_loss / (float)n_rays_global;
 		mask_out[i] = -(mask_gt * logf(weight_sum) + (1 - mask_gt) * logf(1 - weight_sum));
 		float Tb;
-		const ScanState sc = scan_replay(base, base + comp - 1, sa, ekt, ck4, cke, Tb);
+		const RecState sc = scan_replay(base, base + comp - 1, sa, ekt, ck4, cke, Tb);
 		ek_out[i] = sc.ek / ((float)comp * (float)n_rays_global);
 		rgr[i] = make_float4(lgrad[0], lgrad[1], lgrad[2], gws * (1 - weight_sum));
 		racc[i] = make_float4(rgb_ray[0], rgb_ray[1], rgb_ray[2], 0.f);
@@ -951,7 +1057,7 @@ __global__ void __launch_bounds__(256) k_loss_grad(uint32_t cap, const StepState
 		float dir[3]; bent_dir(lo, dir);
 		const Alpha a = neus_alpha(lo, dir, unwarp_dt(ci[3]), lp.cos_anneal);
 		float Tb;
-		const ScanState P = scan_replay(rb, s, sa, ekt, ck4, cke, Tb);
+		const RecState P = scan_replay(rb, s, sa, ekt, ck4, cke, Tb);
 		const float4 G = rgr[r], A = racc[r];
 		const float lgrad[3] = {G.x, G.y, G.z}, rgb_ray[3] = {A.x, A.y, A.z}, rgb2[3] = {P.r0, P.r1, P.r2};
 		const float4 q = sa[s];
@@ -1080,8 +1186,11 @@ void launch_bitfield_linear(hipStream_t s, const uint8_t* bitfield, uint32_t* li
 	k_bitfield_linear<<<GRID3 / 32 / 256, 256, 0, s>>>(bitfield, lin);
 }
 void launch_march_count(hipStream_t s, uint32_t cap, uint32_t max_samples, StepState* st, DPInfo dp, const DevDataset& ds, const uint8_t* bitfield,
-                        const uint32_t* lin, uint64_t rng_state, uint64_t rng_inc, float* rays, float* tstart, uint32_t* nreq, const MarchWork& mw) {
-	k_ray_gen<<<ray_blocks(cap), 256, 0, s>>>(cap, st, dp, ds, rng_state, rng_inc, rays, tstart, mw.counter, st, mw.jt);
+                        const uint32_t* lin, uint64_t rng_state, uint64_t rng_inc, float* rays, float* tstart, uint32_t* nreq, const MarchWork& mw,
+                        uint32_t* zero_counters, uint32_t n_zero, const float* occ_bbox) {
+	if (n_zero > 256) throw std::runtime_error("launch_march_count: at most 256 counters to zero");
+	k_ray_gen<<<ray_blocks(cap), 256, 0, s>>>(cap, st, dp, ds, rng_state, rng_inc, rays, tstart, mw.counter, st, mw.jt, zero_counters,
+	                                          zero_counters ? n_zero : 0u, occ_bbox);
 	const uint32_t waves = mw.waves ? std::min(mw.waves, (cap + 63) / 64) : (cap + 63) / 64;
 	const uint32_t blocks = std::max<uint32_t>(1, (waves + 3) / 4);
 	for (uint32_t pass = 0; pass < 2; ++pass) {
@@ -1097,10 +1206,17 @@ void launch_march_count(hipStream_t s, uint32_t cap, uint32_t max_samples, StepS
 	}
 }
 void launch_march_write(hipStream_t s, uint32_t cap, StepState* st, const DevDataset& ds, const float* rays, const MarchWork& mw, const uint32_t* nreq,
-                        const uint32_t* base, uint32_t* numsteps, float* coords, uint32_t* sample_ray, uint32_t sample_cap) {
-	k_march_numsteps<<<(cap + 255) / 256, 256, 0, s>>>(cap, st, nreq, base, numsteps);
+                        uint32_t* base, uint32_t* numsteps, float* coords, uint32_t* sample_ray, uint32_t sample_cap, void* scan_temp,
+                        const Round0List* round0) {
+	const Round0List r0 = round0 ? *round0 : Round0List{0u, nullptr, nullptr, nullptr, 0u};
+	if (cap % 4 || ((uintptr_t)nreq | (uintptr_t)base | (uintptr_t)numsteps | (uintptr_t)r0.c0) & 15)
+		throw std::runtime_error("launch_march_write: ray buffers must be 16-B aligned, cap a multiple of 4");
+	const uint32_t tiles = (cap + SCAN_TILE - 1) / SCAN_TILE;
+	if (tiles > SCAN_MAX_TILES) throw std::runtime_error("launch_march_write: too many ray slots");
+	k_march_scan<<<tiles, SCAN_THREADS, 0, s>>>(cap, st, nreq, base, numsteps, (ScanState*)scan_temp, scan_next_tag(scan_temp), r0);
 	// one block per WRITE_CHUNK samples of the largest possible kept extent (max_inference <= sample_cap)
-	k_march_write<<<std::max<uint32_t>(1, (sample_cap + WRITE_CHUNK - 1) / WRITE_CHUNK), 256, 0, s>>>(cap, st, ds, rays, mw, nreq, base, coords, sample_ray);
+	k_march_write<<<std::max<uint32_t>(1, (sample_cap + WRITE_CHUNK - 1) / WRITE_CHUNK), 256, 0, s>>>(cap, st, ds, rays, mw, nreq, base, coords, sample_ray,
+	                                                                                                      r0);
 }
 void debug_launch_march_stats(hipStream_t s, uint32_t n_rays, const float* rays, const float* tstart, const uint32_t* lin, const DevDataset& ds,
                               const uint8_t* bf, uint32_t* out) {
@@ -1116,18 +1232,10 @@ void launch_loss_alpha_list(hipStream_t s, uint32_t cap_samples, const uint32_t*
                             const half_t* net_out, float cos_anneal, const LossWork& w, bool dt_const) {
 	k_loss_alpha<<<sample_blocks(cap_samples), 256, 0, s>>>(cap_samples, n_ptr, idx, coords, net_out, cos_anneal, w.sa, w.ekt, nullptr, dt_const);
 }
-void launch_chunk_count(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, uint32_t e1, uint32_t* m, uint32_t* counters,
-                        uint32_t n_counters) {
-	k_chunk_count<<<ray_blocks(cap_rays), 256, 0, s>>>(cap_rays, numsteps, e1, m, counters, n_counters);
-}
-void launch_chunk_write(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, const uint32_t* m, const uint32_t* pos, uint32_t* list,
-                        uint32_t* counter) {
-	k_chunk_write<<<ray_blocks(cap_rays), 256, 0, s>>>(cap_rays, numsteps, m, pos, list, counter);
-}
 void launch_loss_scan_chunk(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, const LossWork& w, uint32_t* ccount, uint32_t e0,
                             uint32_t e1, uint32_t e2, uint32_t* list, uint32_t* next_counter) {
-	k_loss_scan_chunk<<<ray_blocks(cap_rays), 256, 0, s>>>(cap_rays, numsteps, w.sa, w.ekt, w.ck4, w.cke, ccount, w.racc, w.rT, w.rek, e0, e1, e2,
-	                                                       list, next_counter);
+	k_loss_scan_chunk<<<std::max<uint32_t>(1, std::min<uint32_t>((cap_rays + 63) / 64, 8192)), 64, 0, s>>>(
+		cap_rays, numsteps, w.sa, w.ekt, w.ck4, w.cke, ccount, w.racc, w.rT, w.rek, e0, e1, e2, list, next_counter);
 }
 // w.n_long is zeroed by the k_loss_alpha launch before it
 void launch_loss_scan_ray(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, const LossWork& w, uint32_t* ccount) {

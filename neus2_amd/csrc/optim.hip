@@ -226,6 +226,68 @@ __global__ void k_bitfield_pool_all(uint32_t nbytes, uint8_t* __restrict__ bf, u
 	}
 }
 
+// World-space bounding box of every occupied cell of every mip (the union of the boxes the march's occupancy lookups can
+// land in: cell c of mip m covers 0.5 + (c / 128 - 0.5) 2^m .. 0.5 + ((c + 1) / 128 - 0.5) 2^m per axis), padded by
+// 1e-4 2^m for the float rounding of the lookup's index. A training ray that misses it cannot produce a sample
+// (k_ray_gen culls it: the march of such a ray returns zero samples anyway). Two stages: per-block min / max, then one
+// block; empty grid -> an empty box (+inf .. -inf).
+constexpr uint32_t OCC_BBOX_BLOCKS = 256;
+__global__ void __launch_bounds__(256) k_occ_bbox_partial(const uint8_t* __restrict__ bf, float* __restrict__ partial) {
+	float lo[3] = {3.402823466e+38f, 3.402823466e+38f, 3.402823466e+38f}, hi[3] = {-3.402823466e+38f, -3.402823466e+38f, -3.402823466e+38f};
+	const uint32_t nbytes = GRID3 / 8 * NERF_CASCADES;
+	for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < nbytes; b += gridDim.x * blockDim.x) {
+		uint32_t bits = bf[b];
+		if (!bits) continue;
+		const uint32_t mip = b / (GRID3 / 8);
+		const float sc = (float)(1u << mip), pad = 1e-4f * sc;
+		while (bits) {
+			const uint32_t k = (uint32_t)__builtin_ctz(bits);
+			bits &= bits - 1;
+			const uint32_t idx = (b % (GRID3 / 8)) * 8 + k;
+			const uint32_t c[3] = {morton3D_invert(idx >> 0), morton3D_invert(idx >> 1), morton3D_invert(idx >> 2)};
+#pragma unroll
+			for (int d = 0; d < 3; ++d) {
+				lo[d] = fminf(lo[d], 0.5f + ((float)c[d] / NERF_GRIDSIZE - 0.5f) * sc - pad);
+				hi[d] = fmaxf(hi[d], 0.5f + ((float)(c[d] + 1) / NERF_GRIDSIZE - 0.5f) * sc + pad);
+			}
+		}
+	}
+	__shared__ float s[6][4];
+#pragma unroll
+	for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+		for (int d = 0; d < 3; ++d) { lo[d] = fminf(lo[d], __shfl_xor(lo[d], off)); hi[d] = fmaxf(hi[d], __shfl_xor(hi[d], off)); }
+	const uint32_t wv = threadIdx.x >> 6;
+	if ((threadIdx.x & 63) == 0)
+		for (int d = 0; d < 3; ++d) { s[d][wv] = lo[d]; s[3 + d][wv] = hi[d]; }
+	__syncthreads();
+	if (threadIdx.x < 6) {
+		float v = s[threadIdx.x][0];
+		for (int w = 1; w < 4; ++w) v = threadIdx.x < 3 ? fminf(v, s[threadIdx.x][w]) : fmaxf(v, s[threadIdx.x][w]);
+		partial[blockIdx.x * 6 + threadIdx.x] = v;
+	}
+}
+__global__ void __launch_bounds__(256) k_occ_bbox_final(const float* __restrict__ partial, uint32_t n, float* __restrict__ bbox) {
+	float lo[3] = {3.402823466e+38f, 3.402823466e+38f, 3.402823466e+38f}, hi[3] = {-3.402823466e+38f, -3.402823466e+38f, -3.402823466e+38f};
+	for (uint32_t b = threadIdx.x; b < n; b += blockDim.x)
+#pragma unroll
+		for (int d = 0; d < 3; ++d) { lo[d] = fminf(lo[d], partial[b * 6 + d]); hi[d] = fmaxf(hi[d], partial[b * 6 + 3 + d]); }
+	__shared__ float s[6][4];
+#pragma unroll
+	for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+		for (int d = 0; d < 3; ++d) { lo[d] = fminf(lo[d], __shfl_xor(lo[d], off)); hi[d] = fmaxf(hi[d], __shfl_xor(hi[d], off)); }
+	const uint32_t wv = threadIdx.x >> 6;
+	if ((threadIdx.x & 63) == 0)
+		for (int d = 0; d < 3; ++d) { s[d][wv] = lo[d]; s[3 + d][wv] = hi[d]; }
+	__syncthreads();
+	if (threadIdx.x < 6) {
+		float v = s[threadIdx.x][0];
+		for (int w = 1; w < 4; ++w) v = threadIdx.x < 3 ? fminf(v, s[threadIdx.x][w]) : fmaxf(v, s[threadIdx.x][w]);
+		bbox[threadIdx.x] = v;
+	}
+}
+
 // ---------------------------------------------------------------- host launchers
 static inline uint32_t nblk(uint64_t n, uint32_t cap = 4096) { return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, cap)); }
 void launch_adam_ema(hipStream_t s, const AdamParams& p, float* weights_fp, half_t* weights_h, const float* grads, float* m1, float* m2,
@@ -263,6 +325,11 @@ void launch_bitfield(hipStream_t s, const float* grid, uint8_t* bitfield, const 
 	const uint32_t nbytes = GRID3 / 8;
 	k_grid_to_bitfield<<<nblk(nbytes * NERF_CASCADES), 256, 0, s>>>(nbytes * NERF_CASCADES, nbytes * n_cascades, grid, bitfield, mean);
 	k_bitfield_pool_all<<<nblk((uint64_t)nbytes * (NERF_CASCADES - 1), 2048), 256, 0, s>>>(nbytes, bitfield, lin);
+}
+size_t occ_bbox_scratch_floats() { return 6 + 6 * (size_t)OCC_BBOX_BLOCKS; }
+void launch_occ_bbox(hipStream_t s, const uint8_t* bitfield, float* scratch) {
+	k_occ_bbox_partial<<<OCC_BBOX_BLOCKS, 256, 0, s>>>(bitfield, scratch + 6);
+	k_occ_bbox_final<<<1, 256, 0, s>>>(scratch + 6, OCC_BBOX_BLOCKS, scratch);
 }
 void launch_ema_mean(hipStream_t s, uint32_t n, float decay, float* grid, const float* tmp, float* partial, float* mean) {
 	k_ema_mean<<<n / 1024, 256, 0, s>>>(n, decay, grid, tmp, partial);

@@ -203,6 +203,8 @@ struct NeusTestbed {
 	Dev<uint32_t> occ_idx;
 	Dev<uint8_t> bitfield;
 	Dev<uint32_t> bf_lin;   // mip-0 occupancy in (x, y, z/32) word order for the constant-step march
+	Dev<float> occ_bbox;    // world box of the occupied cells of every mip (+ stage-1 scratch): the ray generation's cull
+	bool ray_cull = true;   // NEUS_RAY_CULL=0: march every ray (A/B reference)
 	Dev<PcgJump> pcg_tab;   // pcg32 jump-ahead table (common.h PcgJumpTable)
 	uint32_t density_grid_ema_step = 0;
 	uint64_t occ_samples = 0;  // occupancy-grid samples this rank evaluated since the network was loaded
@@ -357,6 +359,9 @@ struct NeusTestbed {
 		HIP_CHECK(hipMemset(bitfield.p, 0xff, GRID3 / 8 * NERF_CASCADES));
 		bf_lin.alloc(LIN_WORDS);
 		launch_bitfield_linear(stream, bitfield.p, bf_lin.p);
+		occ_bbox.alloc(occ_bbox_scratch_floats());
+		launch_occ_bbox(stream, bitfield.p, occ_bbox.p);
+		{ const char* e = std::getenv("NEUS_RAY_CULL"); ray_cull = !(e && e[0] == '0'); }
 		grid_mean.alloc(4); grid_partial.alloc(GRID3 / 1024);
 		HIP_CHECK(hipMemset(grid_mean.p, 0, 16));
 	}
@@ -524,6 +529,7 @@ struct NeusTestbed {
 		}
 		scan_tmp_bytes = std::max(scan_temp_bytes(MAX_RAYS), scan_temp_bytes((uint32_t)n_bins));
 		scan_tmp.alloc(scan_tmp_bytes + 256);
+		scan_temp_reset(stream, scan_tmp.p);
 		HIP_CHECK(hipStreamSynchronize(stream));
 	}
 
@@ -815,6 +821,7 @@ struct NeusTestbed {
 		launch_ema_mean(s, n_cells, cfg.density_grid_decay, density_grid.p, density_tmp.p, grid_partial.p, grid_mean.p);
 		++density_grid_ema_step;
 		launch_bitfield(s, density_grid.p, bitfield.p, grid_mean.p, max_cascade + 1, bf_lin.p);
+		launch_occ_bbox(s, bitfield.p, occ_bbox.p);
 	}
 
 	// ------------------------------------------------------------ optimizer (trainer.h:170-172)
@@ -871,7 +878,7 @@ struct NeusTestbed {
 		r_out.alloc((size_t)n * MAX_STEPS_INBETWEEN_COMPACTION * OUT_W);
 		r_frame.alloc(n); r_accum.alloc(n);
 		const size_t sb = scan_temp_bytes(n);
-		if (sb > r_scan_bytes || !r_scan_tmp.p) { r_scan_tmp.alloc(sb + 256); r_scan_bytes = sb; }
+		if (sb > r_scan_bytes || !r_scan_tmp.p) { r_scan_tmp.alloc(sb + 256); r_scan_bytes = sb; scan_temp_reset(s, r_scan_tmp.p); }
 		const MlpPtrs& w = rq.use_ema ? mlp_ema : mlp;
 		const half_t* grid = (rq.use_ema ? ema_h.p : params_h.p) + lay.grid_off;
 		if (rq.use_ema) prepare_weights_for(mlp_ema);
@@ -950,7 +957,7 @@ struct NeusTestbed {
 		uint32_t *cv = mc_cnt.p, *ct = cv + nc, *ov = ct + nc, *ot = ov + nc;
 		launch_mc_count(s, res, amin, amax, thresh, d, cv, ct);
 		const size_t sb = scan_temp_bytes(nc);
-		if (sb > mc_scan_bytes || !mc_scan_tmp.p) { mc_scan_tmp.alloc(sb + 256); mc_scan_bytes = sb; }
+		if (sb > mc_scan_bytes || !mc_scan_tmp.p) { mc_scan_tmp.alloc(sb + 256); mc_scan_bytes = sb; scan_temp_reset(s, mc_scan_tmp.p); }
 		launch_exclusive_scan(s, mc_scan_tmp.p, mc_scan_bytes, cv, ov, nc);
 		launch_exclusive_scan(s, mc_scan_tmp.p, mc_scan_bytes, ct, ot, nc);
 		uint32_t last[4];
@@ -1024,9 +1031,15 @@ struct NeusTestbed {
 		if (training_step == 0 || canonical_step == 0) HIP_CHECK(hipMemsetAsync(&st.p->n_rays_total, 0, 4, s));
 		const DPInfo dp{rank, world};  // (n_kept, n_rays_with_samples: zeroed by k_ray_gen)
 		mark(1);
-		launch_march_count(s, MAX_RAYS, max_samples, st.p, dp, ds, bitfield.p, bf_lin.p, rng.state, rng.inc, rays.p, startt.p, nreq.p, mwork);
-		launch_exclusive_scan(s, scan_tmp.p, scan_tmp_bytes, nreq.p, base.p, MAX_RAYS);
-		launch_march_write(s, MAX_RAYS, st.p, ds, rays.p, mwork, nreq.p, base.p, numsteps.p, coords.p, sample_ray.p, max_samples);
+		// progressive (cut-off-aware) inference this step: its round-0 list is written by the march
+		const bool progressive = progressive_mode == 2 || (progressive_mode == 1 && last_keep_ratio < PROGRESSIVE_RATIO);
+		const uint32_t nch = (uint32_t)chunk_ends.size() + 1;
+		// round 0's list slots go through cbase (rewritten by the loss compaction before it is read again)
+		const Round0List r0{chunk_ends[0], cbase.p, chunk_list.p, chunk_cnt.p, nch + 1};
+		launch_march_count(s, MAX_RAYS, max_samples, st.p, dp, ds, bitfield.p, bf_lin.p, rng.state, rng.inc, rays.p, startt.p, nreq.p, mwork,
+		                   progressive ? chunk_cnt.p : nullptr, nch + 1, ray_cull ? occ_bbox.p : nullptr);
+		launch_march_write(s, MAX_RAYS, st.p, ds, rays.p, mwork, nreq.p, base.p, numsteps.p, coords.p, sample_ray.p, max_samples, scan_tmp.p,
+		                   progressive ? &r0 : nullptr);
 		mark(2);
 		// DeltaNetwork forward on the samples (nerf_network.h:162-182); the loss keeps the undeformed records
 		const float* c_in = coords.p;
@@ -1035,14 +1048,9 @@ struct NeusTestbed {
 		lp.loss_scale = LOSS_SCALE; lp.ek_w = cfg.ek_loss_weight; lp.mask_w = cfg.mask_loss_weight; lp.cos_anneal = cos_anneal();
 		lp.max_compacted = batch; lp.rng_state = rng.state; lp.rng_inc = rng.inc; lp.jt = jump_table();
 		const LossWork w = loss_work(base.p);
-		if (progressive_mode == 2 || (progressive_mode == 1 && last_keep_ratio < PROGRESSIVE_RATIO)) {
+		if (progressive) {
 			// rounds of per-ray chunks, each: network on the round's samples, alpha, the recurrence continued (march.hip);
 			// the "infer" phase mark then covers the composite as well
-			const uint32_t nch = (uint32_t)chunk_ends.size() + 1;
-			// round 0's list through ccount / cbase (both rewritten before they are read: round 0 does not read ccount)
-			launch_chunk_count(s, MAX_RAYS, numsteps.p, chunk_ends[0], ccount.p, chunk_cnt.p, nch + 1);
-			launch_exclusive_scan(s, scan_tmp.p, scan_tmp_bytes, ccount.p, cbase.p, MAX_RAYS);
-			launch_chunk_write(s, MAX_RAYS, numsteps.p, ccount.p, cbase.p, chunk_list.p, chunk_cnt.p);
 			uint32_t e0 = 0;
 			for (uint32_t k = 0; k < nch; ++k) {
 				const uint32_t e1 = k + 1 < nch ? chunk_ends[k] : 0xffffffffu;
@@ -1287,6 +1295,7 @@ int neus_testbed_set_density_grid(NeusTestbed* tb, const float* g, const uint8_t
 		if (bf) {
 			HIP_CHECK(hipMemcpy(tb->bitfield.p, bf, GRID3 / 8 * NERF_CASCADES, hipMemcpyHostToDevice));
 			launch_bitfield_linear(tb->stream, tb->bitfield.p, tb->bf_lin.p);
+			launch_occ_bbox(tb->stream, tb->bitfield.p, tb->occ_bbox.p);
 			HIP_CHECK(hipStreamSynchronize(tb->stream));
 		}
 	});
@@ -1320,6 +1329,7 @@ int neus_testbed_restore_state(NeusTestbed* tb, const NeusRestoreState* in) {
 			launch_grid_mean(tb->stream, tb->density_grid.p, tb->grid_partial.p, tb->grid_mean.p);
 			launch_bitfield(tb->stream, tb->density_grid.p, tb->bitfield.p, tb->grid_mean.p, tb->max_cascade + 1);
 			launch_bitfield_linear(tb->stream, tb->bitfield.p, tb->bf_lin.p);
+			launch_occ_bbox(tb->stream, tb->bitfield.p, tb->occ_bbox.p);
 		}
 		HIP_CHECK(hipStreamSynchronize(tb->stream));
 	});
@@ -1595,10 +1605,10 @@ static void time_kernel_impl(NeusTestbed* tb, int kernel, int variant, int iters
 		const uint32_t valid = t.valid_level_at((int)t.training_step);
 		const uint32_t* lin = t.bf_lin.p;
 		auto march = [&]() {
-			launch_march_count(s, MAX_RAYS, t.max_samples, t.st.p, dp, t.ds, t.bitfield.p, lin, t.rng.state, t.rng.inc, t.rays.p, t.startt.p, t.nreq.p, t.mwork);
-			launch_exclusive_scan(s, t.scan_tmp.p, t.scan_tmp_bytes, t.nreq.p, t.base.p, MAX_RAYS);
+			launch_march_count(s, MAX_RAYS, t.max_samples, t.st.p, dp, t.ds, t.bitfield.p, lin, t.rng.state, t.rng.inc, t.rays.p, t.startt.p, t.nreq.p, t.mwork,
+			                   nullptr, 0, t.ray_cull ? t.occ_bbox.p : nullptr);
 			launch_march_write(s, MAX_RAYS, t.st.p, t.ds, t.rays.p, t.mwork, t.nreq.p, t.base.p, t.numsteps.p, t.coords.p,
-			                   t.sample_ray.p, t.max_samples);
+			                   t.sample_ray.p, t.max_samples, t.scan_tmp.p);
 		};
 		const LossWork w = t.loss_work(t.base.p);
 		if (variant != 99) {  // 99: no re-preparation (counter runs: only the timed kernel is launched)
@@ -1613,9 +1623,10 @@ static void time_kernel_impl(NeusTestbed* tb, int kernel, int variant, int iters
 		for (int k = 0; k < iters; ++k) {
 			HIP_CHECK(hipEventRecord(evs[k], s));
 			switch (kernel) {
-			case 0: launch_march_count(s, MAX_RAYS, t.max_samples, t.st.p, dp, t.ds, t.bitfield.p, lin, t.rng.state, t.rng.inc, t.rays.p, t.startt.p, t.nreq.p, t.mwork); break;
+			case 0: launch_march_count(s, MAX_RAYS, t.max_samples, t.st.p, dp, t.ds, t.bitfield.p, lin, t.rng.state, t.rng.inc, t.rays.p, t.startt.p, t.nreq.p, t.mwork,
+			                   nullptr, 0, t.ray_cull ? t.occ_bbox.p : nullptr); break;
 			case 1: launch_march_write(s, MAX_RAYS, t.st.p, t.ds, t.rays.p, t.mwork, t.nreq.p, t.base.p, t.numsteps.p,
-			                           t.coords.p, t.sample_ray.p, t.max_samples); break;
+			                           t.coords.p, t.sample_ray.p, t.max_samples, t.scan_tmp.p); break;
 			case 2: debug_launch_loss_scan(s, variant, MAX_RAYS, t.numsteps.p, w, t.ccount.p); break;
 			case 3: launch_nerf_infer(s, t.lay.L, t.lay.W, &t.st.p->n_kept, 0, t.coords.p, t.gl, valid, t.params_h.p + t.lay.grid_off, t.mlp,
 			                          t.net_out.p, 8192); break;
@@ -1655,6 +1666,16 @@ int neus_debug_march_stats(NeusTestbed* tb, uint32_t n, uint32_t* out) {
 		debug_launch_march_stats(tb->stream, n, tb->rays.p, tb->startt.p, tb->bf_lin.p, tb->ds, tb->bitfield.p, o.p);
 		HIP_CHECK(hipStreamSynchronize(tb->stream));
 		HIP_CHECK(hipMemcpy(out, o.p, 12 * (size_t)n, hipMemcpyDeviceToHost));
+	});
+}
+int neus_debug_exclusive_scan(void* stream, const uint32_t* in, uint32_t* out, uint32_t n, int reps, uint32_t* failures) {
+	return guard([&] {
+		hipStream_t s = (hipStream_t)stream;
+		const size_t tb_ = scan_temp_bytes(std::max(1u, n));
+		Dev<uint8_t> tmp; tmp.alloc(tb_ + 256); scan_temp_reset(s, tmp.p);
+		for (int r = 0; r < std::max(1, reps); ++r) launch_exclusive_scan(s, tmp.p, tb_, in, out, n);
+		HIP_CHECK(hipStreamSynchronize(s));
+		if (failures) *failures = scan_failures(tmp.p);
 	});
 }
 int neus_testbed_stream(NeusTestbed* tb, void** s) { return guard([&] { *s = (void*)tb->stream; }); }
@@ -1816,13 +1837,16 @@ int neus_sample_rays(NeusTestbed* tb, void* stream, uint32_t n_rays, uint32_t ra
 		Dev<uint2> rec; rec.alloc((size_t)n_rays * NERF_STEPS);
 		Dev<uint2> seg; seg.alloc((size_t)n_rays * MARCH_SEG_RECS);
 		const MarchWork mw{rec.p, nrec.p, q.p, tb->mwork.waves, seg.p, tb->mwork.lanes_per_ray};
-		Dev<uint8_t> tmp; const size_t tb_ = scan_temp_bytes(n_rays); tmp.alloc(tb_ + 256);
+		Dev<uint8_t> tmp; const size_t tb_ = scan_temp_bytes(n_rays); tmp.alloc(tb_ + 256); scan_temp_reset(s, tmp.p);
 		Dev<uint32_t> lin; lin.alloc(LIN_WORDS);
 		launch_bitfield_linear(s, bitfield, lin.p);
-		launch_march_count(s, n_rays, max_samples, sst.p, DPInfo{rank, world}, tb->ds, bitfield, lin.p, rng_state, rng_inc, rays, st_t.p, nr.p, mw);
-		launch_exclusive_scan(s, tmp.p, tb_, nr.p, bs.p, n_rays);
+		// the occupied-box cull of the training step, from this bitfield (exact: culled rays march to zero samples)
+		Dev<float> bb; bb.alloc(occ_bbox_scratch_floats());
+		launch_occ_bbox(s, bitfield, bb.p);
+		launch_march_count(s, n_rays, max_samples, sst.p, DPInfo{rank, world}, tb->ds, bitfield, lin.p, rng_state, rng_inc, rays, st_t.p, nr.p, mw,
+		                   nullptr, 0, tb->ray_cull ? bb.p : nullptr);
 		Dev<uint32_t> sr; sr.alloc(std::max<uint32_t>(1, max_samples));
-		launch_march_write(s, n_rays, sst.p, tb->ds, rays, mw, nr.p, bs.p, numsteps, coords, sr.p, max_samples);
+		launch_march_write(s, n_rays, sst.p, tb->ds, rays, mw, nr.p, bs.p, numsteps, coords, sr.p, max_samples, tmp.p);
 		HIP_CHECK(hipMemcpyAsync(&h, sst.p, sizeof(h), hipMemcpyDeviceToHost, s));
 		HIP_CHECK(hipStreamSynchronize(s));
 		counters_out[0] = h.numsteps_counter; counters_out[1] = h.n_kept; counters_out[2] = h.n_rays_with_samples;
@@ -1848,7 +1872,7 @@ int neus_loss_compact(NeusTestbed* tb, void* stream, uint32_t n_rays, uint32_t r
 		Dev<uint32_t> cc, cb, rb, sr; cc.alloc(n_rays); cb.alloc(n_rays); rb.alloc(n_rays); sr.alloc(n_samples);
 		Dev<float4> sa, ck4, racc, rgr; sa.alloc(n_samples); ck4.alloc(n_samples / 8 + 1); racc.alloc(n_rays); rgr.alloc(n_rays);
 		Dev<float> ekt, cke, rT; ekt.alloc(n_samples); cke.alloc(n_samples / 8 + 1); rT.alloc(n_rays);
-		Dev<uint8_t> tmp; const size_t tb_ = scan_temp_bytes(n_rays); tmp.alloc(tb_ + 256);
+		Dev<uint8_t> tmp; const size_t tb_ = scan_temp_bytes(n_rays); tmp.alloc(tb_ + 256); scan_temp_reset(s, tmp.p);
 		LossParams lp{};
 		lp.loss_scale = LOSS_SCALE; lp.ek_w = tb->cfg.ek_loss_weight; lp.mask_w = tb->cfg.mask_loss_weight; lp.cos_anneal = tb->cos_anneal();
 		lp.max_compacted = max_compacted; lp.rng_state = rng_state; lp.rng_inc = rng_inc;

@@ -224,6 +224,35 @@ def test_sample_rays_bit_exact(env):
         assert nk > 0
 
 
+def test_sample_rays_culled_bit_exact(env):
+    """A small off-centre occupied blob: most rays miss the occupied cells' box and are culled by the ray generation
+    (k_ray_gen, launch_occ_bbox) instead of marched; rays, numsteps and coords stay bit-identical to the oracle's full
+    march, including the rays grazing the box."""
+    t, O, tb = env["t"], env["O"], env["tb"]
+    lib, check = L()
+    G = 128
+    c = (np.arange(G) + 0.5) / G
+    X, Y, Z = np.meshgrid(c, c, c, indexing="ij")
+    occ = (X - 0.62) ** 2 + (Y - 0.45) ** 2 + (Z - 0.55) ** 2 < 0.09 ** 2
+    bf = env["scenes"].bitfield_from_occupancy(occ)
+    n_rays, max_s = 4096, 4096 * 16
+    rays = t.zeros((n_rays, 6), dtype=t.float32, device="cuda")
+    ns = t.zeros((n_rays, 2), dtype=t.int32, device="cuda")
+    co = t.zeros((max_s, 7), dtype=t.float32, device="cuda")
+    cnt = (C.c_uint32 * 3)()
+    rs, ri = 0x0123456789ABCDEF, 0xDA3E39CB94B95BDB | 1
+    check(lib.neus_sample_rays(tb.handle, None, C.c_uint32(n_rays), C.c_uint32(0), C.c_uint32(1), C.c_uint32(0), C.c_uint64(rs), C.c_uint64(ri),
+                               C.c_uint32(max_s), ptr(dev(t, bf)), ptr(rays), ptr(ns), ptr(co), cnt))
+    r_rays, r_ns, r_co, r_cnt, r_nr = O.generate_samples(env["ds"], bf, n_rays, 0, rs, ri, max_s)
+    np.testing.assert_array_equal(host(ns, np.uint32), r_ns)
+    assert cnt[0] == r_cnt and cnt[2] == r_nr
+    np.testing.assert_array_equal(host(rays, np.uint32), r_rays.view(np.uint32))
+    nk = int(cnt[1])
+    np.testing.assert_array_equal(host(co, np.uint32)[:nk], r_co.view(np.uint32)[:nk])
+    # the blob is hit by a minority of the rays: the cull had most of them to skip
+    assert 0 < r_nr < n_rays // 2, r_nr
+
+
 def test_loss_compaction_parity(env):
     """Composite/loss/compaction on fixed network outputs: compaction bit-exact, dL/dout fp16-close."""
     t, O, tb = env["t"], env["O"], env["tb"]
