@@ -292,6 +292,11 @@ int neus_testbed_time_kernel(NeusTestbed* tb, int kernel, int iters, float* ms_o
 // Development statistic of the last step's march: per ray {march_step calls, skip-loop additions,
 // samples} (3 x u32 per ray, n rays; cone_angle 0 only).
 int neus_debug_march_stats(NeusTestbed* tb, uint32_t n, uint32_t* out);
+/* Development timing of the occupancy march (ray generation + both passes on the current state): per wave of the
+ * first pass, 8 u64 = wall-clock stamps (100 MHz) at start, slice start reached, segment marched, segments joined,
+ * samples counted, records written, then the wave's samples and its re-march rounds; pass 1 overwrites its waves'
+ * stamps only where it marches. */
+int neus_debug_march_profile(NeusTestbed* tb, unsigned long long* out, uint32_t max_waves, uint32_t* n_waves);
 /* Development check of the single-pass exclusive scan the step's compactions use (scan.hip): device buffers in / out
  * of n u32 on `hip_stream`, `reps` launches on one fresh state (the epoch re-arm), synchronous; failures = bounded-wait
  * give-ups (0 expected). */

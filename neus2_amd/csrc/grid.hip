@@ -143,6 +143,16 @@ __device__ __forceinline__ void corner_contribution(const ScatterLevel& L, uint3
 	const uint32_t gx = L.s.g[0] + (idx & 1), gy = L.s.g[1] + ((idx >> 1) & 1), gz = L.s.g[2] + ((idx >> 2) & 1);
 	gidx = L.off + grid_index(L.s.hsize, L.s.res, gx, gy, gz);
 }
+__device__ __forceinline__ ScatterLevel scatter_level_ab(const GridLevels& gl, uint32_t l, float x, float y, float z, uint32_t a, uint32_t b2,
+                                                         const float4 vv) {
+	ScatterLevel L;
+	L.s = level_setup(gl, l, x, y, z);
+	const h2 d1 = *(const h2*)&a, g2 = *(const h2*)&b2;
+	L.dl0 = (float)d1[0]; L.dl1 = (float)d1[1]; L.g0 = (float)g2[0]; L.g1 = (float)g2[1];
+	L.vin[0] = L.s.scale * vv.x; L.vin[1] = L.s.scale * vv.y; L.vin[2] = L.s.scale * vv.z;
+	L.off = gl.offset[l];
+	return L;
+}
 __device__ __forceinline__ ScatterLevel scatter_level(const GridLevels& gl, uint32_t l, float x, float y, float z, uint32_t ic, uint32_t ld,
                                                       const uint32_t* __restrict__ dLdenc, const uint32_t* __restrict__ g, const float4 vv) {
 	ScatterLevel L;
@@ -403,6 +413,184 @@ __global__ void __launch_bounds__(BS) k_scatter_bin_w(const uint32_t* __restrict
 	}
 }
 
+// ---------------------------------------------------------------- per-block record regions (default)
+// The same records as the binned paths, without the histogram pass and the device-wide slot scan: each BS-sample
+// workgroup counting-sorts its records of a level by level-local bucket (4096 entries of that level) in LDS and writes
+// them out as ONE contiguous region [level][block] (BS x 8 slots), whole 128-B lines, plus the bucket start offsets of
+// the region (rtab [level][block][bucket], u16). The accumulation of bucket (l, k) then reads the k-th segment of every
+// block's level-l region (~32 records each on a hashed level): the region reads are the only extra cost, against the
+// histogram pass, the ~1M-entry scan and the runs of 16-64 records the binned path writes to scattered slots. Records,
+// their int64 sums and so the gradient are bitwise the binned paths' (the sum per entry is order-independent).
+constexpr uint32_t RT_STRIDE = SB_LEVEL_BUCKETS + 1;
+template <int BS>
+__global__ void __launch_bounds__(BS) k_scatter_bin_r(const uint32_t* __restrict__ n_ptr, uint32_t n_fixed, uint32_t ld,
+                                                        const float* __restrict__ coords, uint32_t coord_stride, const GridLevels gl,
+                                                        uint32_t valid_level, const uint32_t* __restrict__ dLdenc, const uint32_t* __restrict__ g,
+                                                        const float4* __restrict__ v4, ScatterWork w) {
+	__shared__ uint32_t cnt[SB_LEVEL_BUCKETS], base[SB_LEVEL_BUCKETS + 1];
+	__shared__ uint16_t st_i[BS * 8];
+	__shared__ uint32_t st_g[BS * 8];
+	const uint32_t blk = blockIdx.x, lane = threadIdx.x & 63;
+	const uint32_t n = load_n(n_ptr, n_fixed);
+	const uint32_t i = blk * blockDim.x + threadIdx.x;
+	const bool ok = i < n;
+	const uint32_t ic = ok ? i : 0;
+	const float* c = coords + (size_t)ic * coord_stride;
+	const float x = c[0], y = c[1], z = c[2];
+	const float4 vv = v4[ic];
+	const uint32_t n_lv = min(gl.n_levels, valid_level + 1);
+	// the level's two per-sample operands, loaded one level ahead (the level loop's barriers would otherwise expose
+	// their latency once per level)
+	uint32_t a_cur = dLdenc[ic], g_cur = g[ic];
+	for (uint32_t l = 0; l < n_lv; ++l) {
+		const uint32_t ln = min(l + 1, n_lv - 1);
+		const uint32_t a_next = dLdenc[(size_t)ln * ld + ic], g_next = g[(size_t)ln * ld + ic];
+		const uint32_t off = gl.offset[l], size = gl.offset[l + 1] - off;
+		const uint32_t nlb = (size + SB_SIZE - 1) >> SB_SHIFT;
+		const bool few = size <= 4 * SB_SIZE;
+		for (uint32_t k = threadIdx.x; k < nlb; k += blockDim.x) cnt[k] = 0;
+		__syncthreads();
+		const ScatterLevel L = scatter_level_ab(gl, l, x, y, z, a_cur, g_cur, vv);
+		a_cur = a_next; g_cur = g_next;
+		uint32_t re[8], rs[8], rg[8];
+#pragma unroll
+		for (uint32_t idx = 0; idx < 8; ++idx) {
+			uint32_t gidx; float a0, a1;
+			corner_contribution(L, idx, gidx, a0, a1);
+			const bool emit = wave_run_sum(gidx, a0, a1, ok);
+			const uint32_t e = gidx - off, lb = e >> SB_SHIFT;
+			uint32_t sl = 0;
+			if (few) sl = wave_bucket_slot(cnt, lb, emit);
+			else if (emit) sl = atomicAdd(&cnt[lb], 1u);
+			re[idx] = emit ? e : ~0u;
+			rs[idx] = sl;
+			rg[idx] = __builtin_bit_cast(uint32_t, (h2){(half_t)a0, (half_t)a1});
+		}
+		__syncthreads();  // bucket counts complete
+		if (threadIdx.x < 64) {  // exclusive scan of the counts (one wave)
+			uint32_t total = 0;
+			for (uint32_t k0 = 0; k0 < nlb; k0 += 64) {
+				const uint32_t k = k0 + lane;
+				const uint32_t v = k < nlb ? cnt[k] : 0u;
+				uint32_t incl = v;
+#pragma unroll
+				for (int d = 1; d < 64; d <<= 1) { const uint32_t t = (uint32_t)__shfl_up((int)incl, d); if ((int)lane >= d) incl += t; }
+				if (k < nlb) base[k] = total + incl - v;
+				total += (uint32_t)__shfl((int)incl, 63);
+			}
+			if (lane == 0) base[nlb] = total;
+		}
+		__syncthreads();
+#pragma unroll
+		for (uint32_t idx = 0; idx < 8; ++idx) {
+			const uint32_t e = re[idx];
+			if (e != ~0u) {
+				const uint32_t pos = base[e >> SB_SHIFT] + rs[idx];
+				st_i[pos] = (uint16_t)(e & (SB_SIZE - 1));
+				st_g[pos] = rg[idx];
+			}
+		}
+		__syncthreads();  // stage complete: the region is written out contiguously
+		const size_t region = ((size_t)l * w.n_chunks + blk) * (BS * 8);
+		const uint32_t total = base[nlb];
+		for (uint32_t r = threadIdx.x; r < total; r += blockDim.x) {
+			w.rec_i[region + r] = st_i[r];
+			w.rec_g[region + r] = __builtin_bit_cast(h2, st_g[r]);
+		}
+		uint16_t* tab = w.rtab + ((size_t)l * w.n_chunks + blk) * RT_STRIDE;
+		for (uint32_t k = threadIdx.x; k <= nlb; k += blockDim.x) tab[k] = (uint16_t)base[k];
+		__syncthreads();  // LDS reused by the next level
+	}
+}
+
+// One workgroup per level-local bucket (l, k), or `parts` workgroups over slices of the blocks for the heavy buckets
+// of the small dense levels (int64 sums meeting in a split slot, as k_scatter_accum). A wave takes 64 of the slice's
+// blocks at a time (blocks wv, wv + 4, ... of the slice: every wave gets a share of a short slice): their segment
+// lengths, a wave scan, and the concatenated segments read lane-contiguously, SC_U batches of 64 records in flight
+// (the owner of each record by binary search over the 64 segment starts in LDS).
+constexpr int SC_U = 8;
+__global__ void __launch_bounds__(256) k_scatter_accum_r(ScatterWork w, const GridLevels gl, float* __restrict__ grads, uint32_t bs8) {
+	__shared__ unsigned long long acc[2 * SB_SIZE];
+	__shared__ uint32_t s_pre[4][65], s_src[4][64];
+	__shared__ uint32_t s_last;
+	const uint4 job = w.jobs2[blockIdx.x];
+	const uint32_t l = job.x, kb = job.y, part = job.z & 0xffffu, parts = job.z >> 16, slot = job.w;
+	const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+	for (uint32_t k = threadIdx.x; k < 2 * SB_SIZE; k += blockDim.x) acc[k] = 0ull;
+	__syncthreads();
+	auto fix = [](float v) {  // |v| < 2^31 (clamped) -> int64 multiple of 2^-32
+		return (unsigned long long)__float2ll_rn(fminf(fmaxf(v, -2147483520.0f), 2147483520.0f) * SB_FIX_SCALE);
+	};
+	const uint32_t nb = w.n_chunks;
+	const uint32_t b0 = (uint32_t)((uint64_t)nb * part / parts), b1 = (uint32_t)((uint64_t)nb * (part + 1) / parts);
+	uint32_t* pre = s_pre[wv];
+	uint32_t* src = s_src[wv];
+	for (uint32_t it = 0; b0 + wv + 4 * 64 * it < b1; ++it) {
+		const uint32_t b = b0 + wv + 4 * (64 * it + lane);
+		uint32_t s0 = 0, len = 0;
+		if (b < b1) {
+			const uint16_t* tab = w.rtab + ((size_t)l * nb + b) * RT_STRIDE;
+			s0 = tab[kb];
+			len = (uint32_t)tab[kb + 1] - s0;
+		}
+		uint32_t incl = len;
+#pragma unroll
+		for (int d = 1; d < 64; d <<= 1) { const uint32_t t = (uint32_t)__shfl_up((int)incl, d); if ((int)lane >= d) incl += t; }
+		const uint32_t total = (uint32_t)__shfl((int)incl, 63);
+		__builtin_amdgcn_wave_barrier();
+		pre[lane] = incl - len;
+		src[lane] = (uint32_t)(((size_t)l * nb + (b < b1 ? b : 0u)) * bs8) + s0;  // u32: < 2^32 records
+		__builtin_amdgcn_wave_barrier();
+		for (uint32_t r0 = 0; r0 < total; r0 += 64 * SC_U) {
+			uint32_t q[SC_U];
+#pragma unroll
+			for (int u = 0; u < SC_U; ++u) {
+				const uint32_t r = min(r0 + 64u * u + lane, total - 1u);
+				uint32_t o = 0;
+#pragma unroll
+				for (uint32_t step = 32; step > 0; step >>= 1) if (pre[o + step] <= r) o += step;
+				q[u] = src[o] + (r - pre[o]);
+			}
+			uint32_t ev[SC_U], gv[SC_U];
+#pragma unroll
+			for (int u = 0; u < SC_U; ++u) { ev[u] = w.rec_i[q[u]]; gv[u] = __builtin_bit_cast(uint32_t, w.rec_g[q[u]]); }
+#pragma unroll
+			for (int u = 0; u < SC_U; ++u) {
+				if (r0 + 64u * u + lane < total) {
+					const h2 g2 = __builtin_bit_cast(h2, gv[u]);
+					atomicAdd(&acc[ev[u]], fix((float)g2[0]));
+					atomicAdd(&acc[SB_SIZE + ev[u]], fix((float)g2[1]));
+				}
+			}
+		}
+		__builtin_amdgcn_wave_barrier();
+	}
+	__syncthreads();
+	const uint32_t off = gl.offset[l], size = gl.offset[l + 1] - off;
+	const uint32_t e0 = off + kb * SB_SIZE, ne = min(SB_SIZE, size - kb * SB_SIZE);
+	if (parts == 1) {
+		for (uint32_t k = threadIdx.x; k < 2 * ne; k += blockDim.x)
+			grads[2 * (size_t)e0 + k] = (float)((double)(long long)acc[(k & 1) * SB_SIZE + (k >> 1)] * (1.0 / 4294967296.0));
+		return;
+	}
+	unsigned long long* H = w.split + (size_t)slot * 2 * SB_SIZE;
+	for (uint32_t k = threadIdx.x; k < 2 * SB_SIZE; k += blockDim.x) {
+		const unsigned long long v = acc[k];
+		if (v) atomicAdd(&H[k], v);
+	}
+	__threadfence();
+	__syncthreads();
+	if (threadIdx.x == 0) s_last = atomicAdd(&w.split_done[slot], 1u) == parts - 1 ? 1u : 0u;
+	__syncthreads();
+	if (!s_last) return;
+	__threadfence();
+	for (uint32_t k = threadIdx.x; k < 2 * ne; k += blockDim.x) {
+		const unsigned long long v = atomicExch(&H[(k & 1) * SB_SIZE + (k >> 1)], 0ull);
+		grads[2 * (size_t)e0 + k] = (float)((double)(long long)v * (1.0 / 4294967296.0));
+	}
+	if (threadIdx.x == 0) atomicExch(&w.split_done[slot], 0u);
+}
+
 // One workgroup per bucket, or `parts` workgroups for a bucket of a small dense level (one 4096-entry bucket can hold a
 // whole level's records): each part sums an equal slice of the bucket's records in LDS and adds its nonzero int64 sums
 // to the bucket's split slot with 64-bit integer atomics (exact, so the total is order-independent and bitwise the
@@ -578,6 +766,23 @@ std::vector<uint32_t> scatter_accum_jobs(const GridLevels& gl, uint32_t n_bucket
 	}
 	return jobs;
 }
+std::vector<uint32_t> scatter_region_jobs(const GridLevels& gl, uint32_t& n_split, std::vector<uint32_t>& jobs_before_level) {
+	// level-local buckets; parts as scatter_accum_jobs: 32 x 4096 / the level's entries, clamped to [1, 32]
+	std::vector<uint32_t> jobs;
+	n_split = 0;
+	jobs_before_level.assign(gl.n_levels + 1, 0u);
+	for (uint32_t l = 0; l < gl.n_levels; ++l) {
+		const uint32_t size = gl.offset[l + 1] - gl.offset[l], nlb = (size + SB_SIZE - 1) / SB_SIZE;
+		if (nlb > SB_LEVEL_BUCKETS) throw std::runtime_error("hash-grid level table too large for the scatter's per-level buckets");
+		const uint32_t parts = std::max(1u, std::min(32u, (uint32_t)((32ull * SB_SIZE) / std::max(1u, size))));
+		for (uint32_t k = 0; k < nlb; ++k) {
+			const uint32_t slot = parts > 1 ? n_split++ : 0u;
+			for (uint32_t p = 0; p < parts; ++p) { jobs.push_back(l); jobs.push_back(k); jobs.push_back(p | (parts << 16)); jobs.push_back(slot); }
+		}
+		jobs_before_level[l + 1] = (uint32_t)(jobs.size() / 4);
+	}
+	return jobs;
+}
 uint32_t scatter_n_buckets(const GridLevels& gl) {
 	for (uint32_t l = 0; l < gl.n_levels; ++l)
 		if (((gl.offset[l + 1] - 1) >> SB_SHIFT) - (gl.offset[l] >> SB_SHIFT) + 1 > SB_LEVEL_BUCKETS)
@@ -587,6 +792,21 @@ uint32_t scatter_n_buckets(const GridLevels& gl) {
 void launch_grid_scatter(hipStream_t s, const uint32_t* n_ptr, uint32_t n_fixed, uint32_t ld, const float* coords, uint32_t coord_stride,
                          const GridLevels& gl, uint32_t valid_level, const half_t* dLdenc, const half_t* g, const float4* v, float* grads,
                          const ScatterWork& w, void* scan_tmp, size_t scan_tmp_bytes) {
+	if (w.mode == 2) {
+		// the grid spans the workspace's sample capacity (w.n_chunks x w.chunk >= n)
+		if (w.chunk == 1024)
+			k_scatter_bin_r<1024><<<w.n_chunks, 1024, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, (const uint32_t*)dLdenc,
+			                                                  (const uint32_t*)g, v, w);
+		else if (w.chunk == 256)
+			k_scatter_bin_r<256><<<w.n_chunks, 256, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, (const uint32_t*)dLdenc,
+			                                                (const uint32_t*)g, v, w);
+		else
+			k_scatter_bin_r<512><<<w.n_chunks, 512, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, (const uint32_t*)dLdenc,
+			                                                (const uint32_t*)g, v, w);
+		const uint32_t nj = std::min(w.n_jobs2, w.jobs2_before[std::min(valid_level + 1, gl.n_levels)]);
+		if (nj) k_scatter_accum_r<<<nj, 256, 0, s>>>(w, gl, grads, w.chunk * 8);
+		return;
+	}
 	if (w.mode == 0) {
 		// the grid spans the workspace's sample capacity (w.n_chunks x w.chunk >= n)
 		const size_t nb = (size_t)w.n_active * w.n_chunks;

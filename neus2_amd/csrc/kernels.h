@@ -105,12 +105,20 @@ struct ScatterWork {
 	uint32_t* split_done;       // [n_split] parts finished (reset by the last part)
 	uint32_t n_jobs;
 	uint32_t n_active;          // buckets counted / scanned (those below it hold every record of the step)
-	uint32_t n_chunks, chunk;   // workgroups of the wide-block binning (mode 0) and their samples (512 or 1024)
-	uint32_t mode;              // 0 wide-block binning (default), 1 the 256-sample hist / scan / bin path (A/B reference)
+	uint32_t n_chunks, chunk;   // workgroups of the wide-block / region binning (modes 0, 2) and their samples (512 or 1024)
+	uint32_t mode;              // 2 per-block record regions (default), 0 wide-block binning, 1 the 256-sample hist / scan / bin path
+	// mode 2: bucket starts of every [level][block] region (u16, SB_LEVEL_BUCKETS + 1 per region) and the accumulation
+	// jobs over level-local buckets {level, bucket, part | parts << 16, split slot}, level-major
+	uint16_t* rtab;
+	const uint4* jobs2;
+	uint32_t n_jobs2;
+	uint32_t jobs2_before[17];  // jobs of the levels below l (l <= 16): the launch takes those up to the valid level
 };
 
 // accumulation workgroups of the scatter (flattened uint4 {bucket, part, parts, split slot}); n_split = split buckets
 std::vector<uint32_t> scatter_accum_jobs(const GridLevels& gl, uint32_t n_buckets, uint32_t& n_split);
+// mode-2 jobs (flattened uint4) and the jobs of the levels below l (jobs_before_level[l], L + 1 entries)
+std::vector<uint32_t> scatter_region_jobs(const GridLevels& gl, uint32_t& n_split, std::vector<uint32_t>& jobs_before_level);
 
 // per-sample / per-ray scratch of the restructured loss (march.hip)
 struct LossWork {
@@ -149,9 +157,13 @@ void launch_grid_scatter(hipStream_t s, const uint32_t* n_ptr, uint32_t n_cap, u
 // mlp.hip
 bool mlp_supported(uint32_t n_levels, uint32_t width);
 void mlp_din_permutation(uint32_t L, int32_t* perm /* DIN entries: physical row -> logical din index or -1 */);
+// the loss's alpha pass fused into the inference epilogue (k_loss_alpha's per-sample terms of every evaluated sample):
+// sa / ekt of LossWork, the cosine anneal, dt_const (cone angle 0: every record's dt is the constant step) and the
+// long-ray counter to zero (nullable)
+struct InferAlpha { float4* sa; float* ekt; float cos_anneal; uint32_t dt_const; uint32_t* n_long; };
 void launch_nerf_infer(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_ptr, uint32_t n_fixed, const float* coords, const GridLevels& gl,
                        uint32_t valid_level, const half_t* grid, const MlpPtrs& w, half_t* out, uint32_t blocks,
-                       const uint32_t* idx = nullptr /* work item j -> sample idx[j] (progressive-inference rounds) */);
+                       const uint32_t* idx = nullptr /* work item j -> sample idx[j] (progressive-inference rounds) */, const InferAlpha* ia = nullptr);
 void launch_nerf_density(hipStream_t s, uint32_t L, uint32_t W, uint32_t n, const float* pos, const GridLevels& gl, uint32_t valid_level,
                          const half_t* grid, const MlpPtrs& w, float* density);
 // Occupancy-grid update, fused (MODE 2 of k_nerf_density): density-grid samples [lo, lo + n) of the update's
@@ -200,8 +212,9 @@ constexpr uint32_t MARCH_RUN_MAX = 16;
 constexpr uint32_t MARCH_SEG_RECS = NERF_STEPS + 64;
 struct MarchWork {
 	uint2* rec; uint32_t* nrec; uint32_t* counter /* 2: the two passes' ray queues */; uint32_t waves; /* 0 = one lane per ray */
-	uint2* seg; uint32_t lanes_per_ray;  /* 1, 4 or 8 */
+	uint2* seg; uint32_t lanes_per_ray;  /* 1, 4, 8 or 16 */
 	PcgJumpTable jt;                      /* jump-ahead of the ray generator's per-ray rng offsets */
+	unsigned long long* prof = nullptr;   /* development: per-wave phase timestamps of the march (8 per wave), or null */
 };
 // Ray generation + the occupancy march: rays (6 f32 per slot), tstart (1 per slot), nreq (requested
 // samples per slot) and the sample runs (MarchWork).

@@ -220,7 +220,8 @@ __device__ __forceinline__ bool march_event(const DevDataset& ds, const uint8_t*
 			tn = fminf(tn, (floorf(p + 0.5f + 0.5f * signf(mr.dir[d])) - p) * mr.idir[d]);
 		}
 		const float t_target = t + fmaxf(ldexpf(tn, -(int)(7 - mip)), 0.0f);
-		do { t += MIN_CONE_STEPSIZE; ++k; } while (t < t_target);
+		t += MIN_CONE_STEPSIZE; ++k;
+		step_until(t, k, t_target, 0xffffffffu, MIN_CONE_STEPSIZE);  // do { t += dt; ++k; } while (t < t_target)
 		return true;
 	} else {
 		float dt, pos[3];
@@ -294,6 +295,12 @@ __global__ void __launch_bounds__(256) k_march(uint32_t cap_rays, uint32_t pass,
 	const uint32_t lane = threadIdx.x & 63, g = lane % MG;
 	const uint32_t groups = (gridDim.x * blockDim.x) / MG;
 	uint32_t total = 0;
+	// development timing (MarchWork::prof): wall clock (100 MHz) at the phases of the wave's first ray group
+	unsigned long long* pw = mw.prof ? mw.prof + (size_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 8 : nullptr;
+	bool first = true;
+	uint32_t n_redo = 0;
+	auto stamp = [&](int ph) { if (pw && first && lane == 0) pw[ph] = wall_clock64(); };
+	stamp(0);
 	for (uint32_t i = lo + (blockIdx.x * blockDim.x + threadIdx.x) / MG; i - lo < ((hi - lo + groups - 1) / groups) * groups; i += groups) {
 		const bool have = i < hi;
 		const float t0 = have ? tstart[i] : -1.f;
@@ -317,8 +324,10 @@ __global__ void __launch_bounds__(256) k_march(uint32_t cap_rays, uint32_t pass,
 		const bool active = t0 >= 0.f && (g == 0 || split);
 		if (active && g > 0) {
 			const float t_g = t0 + span * ((float)g / (float)MG);
-			while (t < t_g && k < 4 * NERF_STEPS) { t += FAST ? MIN_CONE_STEPSIZE : calc_dt(t, ds.cone_angle); ++k; }
+			if (FAST) step_until(t, k, t_g, 4 * NERF_STEPS, MIN_CONE_STEPSIZE);
+			else while (t < t_g && k < 4 * NERF_STEPS) { t += calc_dt(t, ds.cone_angle); ++k; }
 		}
+		stamp(1);
 		uint32_t k_end = (uint32_t)__shfl((int)k, (int)((lane + 1) % 64));  // the next lane's start
 		if (g == MG - 1 || !split) k_end = FINISHED;
 		uint2* rec = mw.seg + ((size_t)i * MG + g) * SEG_CAP;
@@ -328,6 +337,7 @@ __global__ void __launch_bounds__(256) k_march(uint32_t cap_rays, uint32_t pass,
 		float et = t;
 		uint32_t ek = active ? k : FINISHED;
 		if (active) { march_segment<FAST>(ds, bitfield, lin, mr, et, ek, k_end, acc, vis, rec, SEG_CAP); }
+		stamp(2);
 		// segment order: lane g joins the exit of lane g - 1
 		uint32_t vk = k;   // first valid step of this segment
 		for (int q = 1; q < MG; ++q) {
@@ -346,6 +356,7 @@ __global__ void __launch_bounds__(256) k_march(uint32_t cap_rays, uint32_t pass,
 				}
 			}
 			if (__ballot(redo)) {
+				++n_redo;
 				if (redo) {
 					acc = SegAcc{0.f, 0u, 0u, 0u, 0u}; vis.n = 0;
 					et = pt; ek = pk; vk = pk;
@@ -353,6 +364,7 @@ __global__ void __launch_bounds__(256) k_march(uint32_t cap_rays, uint32_t pass,
 				}
 			}
 		}
+		stamp(3);
 		// samples of this segment at k >= vk (the first run may start before vk and is cut there)
 		uint32_t n_g = 0, r_first = 0;
 		float t_first = 0.f;
@@ -389,6 +401,7 @@ __global__ void __launch_bounds__(256) k_march(uint32_t cap_rays, uint32_t pass,
 			if ((uint32_t)q < g) rbefore += pw;
 			r_tot += pw;
 		}
+		stamp(4);
 		// final records: {t of the first sample, (samples of the ray before the run) << 16 | length}
 		uint2* out = mw.rec + (size_t)i * NERF_STEPS;
 		uint32_t written = 0, nr = rbefore;
@@ -411,6 +424,14 @@ __global__ void __launch_bounds__(256) k_march(uint32_t cap_rays, uint32_t pass,
 			mw.nrec[i] = t0 >= 0.f ? r_tot : 0u;
 			total += t0 >= 0.f ? n_tot : 0u;
 		}
+		if (pw && first) {
+			stamp(5);
+			uint32_t ws = g == 0 && have && t0 >= 0.f ? n_tot : 0u;
+#pragma unroll
+			for (int off = 32; off > 0; off >>= 1) ws += (uint32_t)__shfl_xor((int)ws, off);
+			if (lane == 0) { pw[6] = ws; pw[7] = n_redo; }
+		}
+		first = false;
 	}
 	if (pass == 0) {  // the pass's requested samples (one atomic per wave)
 #pragma unroll
@@ -658,11 +679,7 @@ __global__ void __launch_bounds__(256) k_loss_alpha(uint32_t cap, const uint32_t
 	for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
 		const uint32_t s = idx ? idx[j] : j;
 		half_t lo[16]; load_out(net_out, s, lo);
-		float dir[3]; bent_dir(lo, dir);
-		const Alpha a = neus_alpha(lo, dir, dt_const ? dt0 : unwarp_dt(coords[(size_t)s * COORD_W + 3]), cos_anneal);
-		sa[s] = make_float4(a.alpha, det_logistic((float)lo[0]), det_logistic((float)lo[1]), det_logistic((float)lo[2]));
-		const float gn = grad_norm(lo);
-		ekt[s] = (gn - 1.0f) * (gn - 1.0f);
+		loss_alpha_sample(lo, dt_const ? dt0 : unwarp_dt(coords[(size_t)s * COORD_W + 3]), cos_anneal, sa, ekt, s);
 	}
 }
 
@@ -1197,10 +1214,12 @@ void launch_march_count(hipStream_t s, uint32_t cap, uint32_t max_samples, StepS
 		if (ds.cone_angle == 0.0f) {
 			if (mw.lanes_per_ray == 1) k_march<true, 1><<<blocks, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, lin, rays, tstart, nreq, mw);
 			else if (mw.lanes_per_ray == 8) k_march<true, 8><<<blocks * 8, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, lin, rays, tstart, nreq, mw);
+			else if (mw.lanes_per_ray == 16) k_march<true, 16><<<blocks * 16, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, lin, rays, tstart, nreq, mw);
 			else k_march<true, 4><<<blocks * 4, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, lin, rays, tstart, nreq, mw);
 		} else {
 			if (mw.lanes_per_ray == 1) k_march<false, 1><<<blocks, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, nullptr, rays, tstart, nreq, mw);
 			else if (mw.lanes_per_ray == 8) k_march<false, 8><<<blocks * 8, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, nullptr, rays, tstart, nreq, mw);
+			else if (mw.lanes_per_ray == 16) k_march<false, 16><<<blocks * 16, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, nullptr, rays, tstart, nreq, mw);
 			else k_march<false, 4><<<blocks * 4, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, nullptr, rays, tstart, nreq, mw);
 		}
 	}

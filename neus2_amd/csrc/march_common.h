@@ -42,6 +42,29 @@ __device__ __forceinline__ int mip_from_dt(float dt, float px, float py, float p
 	int e; frexpf(dt, &e);
 	return min((int)NERF_CASCADES - 1, max(e, mip));
 }
+// Exactly `while (t < target && k < kmax) { t += dt; ++k; }` for a constant dt > 0 and a finite t >= 0, in a few
+// iterations per binade instead of one per step. Inside a binade [2^e, 2^(e+1)) every float is a multiple of its ulp,
+// so t + dt rounds to t plus a fixed number of ulps - once the parity of t's significand is settled: a tie
+// (dt / ulp = n + 1/2) rounds to the even neighbour, after which the increment stays fixed. Two exact steps that add the
+// same increment prove the stretch linear; it is then jumped in the integer domain (positive floats order as their
+// bit patterns) up to the first step at or past target, the step cap or the binade's end, whichever comes first.
+// Single exact steps cross binades and settle the parity.
+__device__ __forceinline__ void step_until(float& t, uint32_t& k, float target, uint32_t kmax, float dt) {
+	while (t < target && k < kmax) {
+		const float t2 = t + dt;
+		const uint32_t b = __float_as_uint(t), b2 = __float_as_uint(t2), ex = b & 0x7f800000u;
+		if (!(t2 < target) || k + 1u >= kmax || ex == 0u || (b2 & 0x7f800000u) != ex) { t = t2; ++k; continue; }
+		const float t3 = t2 + dt;
+		const uint32_t b3 = __float_as_uint(t3), inc = b2 - b;
+		if (b3 - b2 != inc || (b3 & 0x7f800000u) != ex) { t = t2; ++k; continue; }
+		const uint32_t e_end = ex + 0x00800000u;  // the next binade's first bit pattern
+		uint32_t j = (e_end - 1u - b) / inc;       // the last step inside the binade (>= 2: t3 is inside)
+		j = min(j, kmax - k);
+		j = min(j, (__float_as_uint(target) - b + inc - 1u) / inc);  // the first step at or past target (>= 2: t2 < target)
+		t = __uint_as_float(b + j * inc);
+		k += j;
+	}
+}
 __device__ __forceinline__ float signf(float x) { return copysignf(1.0f, x); }
 __device__ __forceinline__ float advance_to_next_voxel(float t, float cone, const float pos[3], const float dir[3], const float idir[3], uint32_t res) {
 	float p[3], tt[3];
@@ -185,6 +208,16 @@ __device__ __forceinline__ void bent_dir(const half_t* lo, float dir[3]) {
 __device__ __forceinline__ float grad_norm(const half_t* lo) {
 	const float pg[3] = {(float)lo[4], (float)lo[5], (float)lo[6]};
 	return sqrt((double)(pg[0] * pg[0] + pg[1] * pg[1] + pg[2] * pg[2]) + 1e-6);
+}
+// k_loss_alpha's per-sample work (compute_loss_kernel_train_nerf's alpha / colour / eikonal terms): {alpha, sigmoid(rgb)}
+// and (|grad sdf| - 1)^2 of sample s from its 16 network outputs; also the fused inference's epilogue
+__device__ __forceinline__ void loss_alpha_sample(const half_t* lo, float dt, float cos_anneal, float4* __restrict__ sa, float* __restrict__ ekt,
+                                                  uint32_t s) {
+	float dir[3]; bent_dir(lo, dir);
+	const Alpha a = neus_alpha(lo, dir, dt, cos_anneal);
+	sa[s] = make_float4(a.alpha, det_logistic((float)lo[0]), det_logistic((float)lo[1]), det_logistic((float)lo[2]));
+	const float gn = grad_norm(lo);
+	ekt[s] = (gn - 1.0f) * (gn - 1.0f);
 }
 __device__ __forceinline__ void load_out(const half_t* net_out, uint32_t s, half_t lo[16]) {
 	const h8* p = (const h8*)(net_out + (size_t)s * OUT_W);

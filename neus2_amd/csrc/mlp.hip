@@ -24,6 +24,11 @@
 #include "kernels.h"
 #include "grid_common.h"
 #include "occ_common.h"
+// the loss's alpha terms (fused inference epilogue) keep the march / loss files' arithmetic: no FMA contraction, so they
+// are bitwise k_loss_alpha's (march.hip) and the oracle's
+#pragma clang fp contract(off)
+#include "march_common.h"
+#pragma clang fp contract(fast)
 #include <algorithm>
 
 namespace neus {
@@ -619,7 +624,7 @@ __device__ __forceinline__ h8 mask_frag(const f16v& acc, int k, const h8& m) {
 template <int L, int W, bool IDX>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) k_nerf_infer(const uint32_t* __restrict__ n_ptr, uint32_t n_fixed, const float* __restrict__ coords,
                                                     const GridLevels gl, uint32_t valid_level, const half_t* __restrict__ grid,
-                                                    MlpPtrs wp, half_t* __restrict__ out, const uint32_t* __restrict__ idx) {
+                                                    MlpPtrs wp, half_t* __restrict__ out, const uint32_t* __restrict__ idx, InferAlpha ia) {
 	constexpr int DKS = Dims<L>::DKS, DMT = Dims<L>::DMT, HALF = Fused<L>::HALF, M0 = Fused<L>::M0;
 	constexpr int MT = (W + 31) / 32, HKS = W / 16;
 	__shared__ half_t sm[FwdSmem<L, W>::END];
@@ -633,6 +638,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))
 	const uint32_t n_waves = (gridDim.x * blockDim.x) >> 6;
 	const half_t var_h = wp.var[0];
 	const half_t bias_h = (half_t)wp.sdf_bias;
+	if (ia.n_long && blockIdx.x == 0 && threadIdx.x == 0) *ia.n_long = 0u;  // the transmittance scan's long-ray list
 	for (uint32_t base = wave * 32; base < n; base += n_waves * 32) {
 		const FwdW w = w0.at(opaque_zero());
 		const uint32_t j = base + r;
@@ -737,19 +743,32 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))
 #pragma unroll
 		for (int ks = 0; ks < HKS; ++ks) O = mfma(loadA(w.r2, 16, r, 16 * ks, h), H2B[ks], O);
 		const half_t row11 = (half_t)__shfl_xor(O[7], 32);  // lane h=0 holds row 11 in reg 7
-		if (valid) {
-			h8 o;
-			if (h == 0) {
-				o[0] = (half_t)O[0]; o[1] = (half_t)O[1]; o[2] = (half_t)O[2];
-				o[3] = D1B[0] + bias_h;                              // half add (common_operation.cuh:964)
-				o[4] = (half_t)grad[0]; o[5] = (half_t)grad[1]; o[6] = (half_t)grad[2];
-				o[7] = var_h;
-			} else {
-				o[0] = (half_t)wd[0]; o[1] = (half_t)wd[1]; o[2] = (half_t)wd[2];
-				o[3] = row11;
-				o[4] = (half_t)O[4]; o[5] = (half_t)O[5]; o[6] = (half_t)O[6]; o[7] = (half_t)O[7];
+		h8 o;
+		if (h == 0) {
+			o[0] = (half_t)O[0]; o[1] = (half_t)O[1]; o[2] = (half_t)O[2];
+			o[3] = D1B[0] + bias_h;                              // half add (common_operation.cuh:964)
+			o[4] = (half_t)grad[0]; o[5] = (half_t)grad[1]; o[6] = (half_t)grad[2];
+			o[7] = var_h;
+		} else {
+			o[0] = (half_t)wd[0]; o[1] = (half_t)wd[1]; o[2] = (half_t)wd[2];
+			o[3] = row11;
+			o[4] = (half_t)O[4]; o[5] = (half_t)O[5]; o[6] = (half_t)O[6]; o[7] = (half_t)O[7];
+		}
+		if (valid) *(h8*)(out + (size_t)i * OUT_W + 8 * h) = o;
+		if (ia.sa) {
+			// the loss's alpha terms of this sample from its 16 outputs (the h = 1 half arrives by shuffle)
+			half_t lo[16];
+#pragma unroll
+			for (int q = 0; q < 4; ++q) {
+				const uint32_t mine = __builtin_bit_cast(uint32_t, (h2){o[2 * q], o[2 * q + 1]});
+				const h2 other = __builtin_bit_cast(h2, (uint32_t)__shfl_xor((int)mine, 32));
+				lo[2 * q] = o[2 * q]; lo[2 * q + 1] = o[2 * q + 1];
+				lo[8 + 2 * q] = other[0]; lo[8 + 2 * q + 1] = other[1];
 			}
-			*(h8*)(out + (size_t)i * OUT_W + 8 * h) = o;
+			if (valid && h == 0) {
+				const float dt = ia.dt_const ? unwarp_dt(warp_dt(MIN_CONE_STEPSIZE)) : unwarp_dt(c[3]);
+				loss_alpha_sample(lo, dt, ia.cos_anneal, ia.sa, ia.ekt, i);
+			}
 		}
 	}
 }
@@ -1634,13 +1653,15 @@ bool mlp_supported(uint32_t L, uint32_t W) {
 }
 
 void launch_nerf_infer(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_ptr, uint32_t n_fixed, const float* coords, const GridLevels& gl,
-                       uint32_t valid_level, const half_t* grid, const MlpPtrs& w, half_t* out, uint32_t blocks, const uint32_t* idx) {
+                       uint32_t valid_level, const half_t* grid, const MlpPtrs& w, half_t* out, uint32_t blocks, const uint32_t* idx,
+                       const InferAlpha* ia) {
+	const InferAlpha a = ia ? *ia : InferAlpha{nullptr, nullptr, 0.f, 0u, nullptr};
 	// persistent grid: at most the resident capacity (weights are staged once per block; both variants run at the
 	// same 3 waves per SIMD, amdgpu_waves_per_eu)
 #define X(l, w_) if (L == l && W == w_) { \
 		static const uint32_t cap = resident_blocks((const void*)k_nerf_infer<l, w_, false>, 256); \
-		if (idx) k_nerf_infer<l, w_, true><<<std::min(blocks, cap), 256, 0, s>>>(n_ptr, n_fixed, coords, gl, valid_level, grid, w, out, idx); \
-		else k_nerf_infer<l, w_, false><<<std::min(blocks, cap), 256, 0, s>>>(n_ptr, n_fixed, coords, gl, valid_level, grid, w, out, nullptr); \
+		if (idx) k_nerf_infer<l, w_, true><<<std::min(blocks, cap), 256, 0, s>>>(n_ptr, n_fixed, coords, gl, valid_level, grid, w, out, idx, a); \
+		else k_nerf_infer<l, w_, false><<<std::min(blocks, cap), 256, 0, s>>>(n_ptr, n_fixed, coords, gl, valid_level, grid, w, out, nullptr, a); \
 		return; }
 	NEUS_MLP_CONFIGS(X)
 #undef X

@@ -228,6 +228,10 @@ struct NeusTestbed {
 	Dev<unsigned long long> sc_split;
 	std::vector<uint32_t> sc_jobs_before;  // [n_buckets + 1] accumulation jobs of the buckets below b
 	uint32_t sc_zero_from = 0;             // the grads' grid part is known zero from this bucket on
+	Dev<uint32_t> sc_jobs2;
+	Dev<uint16_t> sc_rtab;
+	std::vector<uint32_t> sc_jobs2_before;  // [L + 1] region-scatter jobs of the levels below l
+	uint32_t sc_zero_from_e = 0;            // region scatter: grid entries from here on hold zero gradients
 	Dev<h2> sc_rec_g;
 	Dev<uint16_t> sc_rec_i;
 	// restructured loss scratch (kernels.h LossWork)
@@ -500,15 +504,23 @@ struct NeusTestbed {
 		swork = ScatterWork{};
 		swork.n_blocks = (batch + 255) / 256;
 		// wide-block binning: 512-sample workgroups (NEUS_SCATTER_CHUNK=1024: 1024-sample ones)
-		{ const char* e = std::getenv("NEUS_SCATTER_CHUNK"); swork.chunk = (e && std::string(e) == "1024") ? 1024u : 512u; }
+		{
+			const char* e = std::getenv("NEUS_SCATTER_CHUNK");
+			swork.chunk = (e && std::string(e) == "1024") ? 1024u : (e && std::string(e) == "256") ? 256u : 512u;
+		}
 		swork.n_chunks = (batch + swork.chunk - 1) / swork.chunk;
-		// NEUS_SCATTER=binned selects the 256-sample histogram / scan / bin path (bitwise A/B reference of the wide one)
-		{ const char* e = std::getenv("NEUS_SCATTER"); swork.mode = (e && std::string(e) == "binned") ? 1u : 0u; }
+		// per-block record regions (mode 2); NEUS_SCATTER=wide / binned select the wide-block (0) or the 256-sample (1)
+		// histogram / scan / bin paths (bitwise A/B references)
+		{
+			const char* e = std::getenv("NEUS_SCATTER");
+			swork.mode = !e ? 2u : std::string(e) == "binned" ? 1u : std::string(e) == "wide" ? 0u : 2u;
+			if (swork.mode != 2 && swork.chunk == 256) { swork.chunk = 512; swork.n_chunks = (batch + 511) / 512; }  // wide binning: 512 / 1024
+		}
 		swork.n_buckets = scatter_n_buckets(gl);
 		if (swork.n_buckets > SB_MAX_BUCKETS) throw std::runtime_error("hash grid too large for the scatter buckets");
 		const size_t n_bins = (size_t)swork.n_buckets * swork.n_blocks + 1;
 		sc_counts.alloc(n_bins); sc_offs.alloc(n_bins);
-		const size_t n_rec = scatter_records_capacity(swork.n_blocks * 256, l.L);
+		const size_t n_rec = std::max(scatter_records_capacity(swork.n_blocks * 256, l.L), (size_t)l.L * swork.n_chunks * swork.chunk * 8);
 		sc_rec_g.alloc(n_rec); sc_rec_i.alloc(n_rec);
 		swork.counts = sc_counts.p; swork.offs = sc_offs.p; swork.rec_g = sc_rec_g.p; swork.rec_i = sc_rec_i.p;
 		{
@@ -516,6 +528,16 @@ struct NeusTestbed {
 			const std::vector<uint32_t> jobs = scatter_accum_jobs(gl, swork.n_buckets, n_split);
 			sc_jobs.alloc(jobs.size());
 			HIP_CHECK(hipMemcpy(sc_jobs.p, jobs.data(), jobs.size() * 4, hipMemcpyHostToDevice));
+			uint32_t n_split2 = 0;
+			const std::vector<uint32_t> jobs2 = scatter_region_jobs(gl, n_split2, sc_jobs2_before);
+			sc_jobs2.alloc(jobs2.size());
+			HIP_CHECK(hipMemcpy(sc_jobs2.p, jobs2.data(), jobs2.size() * 4, hipMemcpyHostToDevice));
+			swork.jobs2 = (const uint4*)sc_jobs2.p; swork.n_jobs2 = (uint32_t)(jobs2.size() / 4);
+			if (sc_jobs2_before.size() > 17) throw std::runtime_error("region scatter: at most 16 levels");
+			for (size_t k = 0; k < sc_jobs2_before.size(); ++k) swork.jobs2_before[k] = sc_jobs2_before[k];
+			sc_rtab.alloc((size_t)l.L * swork.n_chunks * (SB_LEVEL_BUCKETS + 1));
+			swork.rtab = sc_rtab.p;
+			n_split = std::max(n_split, n_split2);
 			sc_split.alloc(std::max<size_t>(1, (size_t)n_split * 2 * SB_SIZE)); sc_split_done.alloc(std::max(1u, n_split));
 			HIP_CHECK(hipMemset(sc_split.p, 0, sc_split.n * sizeof(unsigned long long)));
 			HIP_CHECK(hipMemset(sc_split_done.p, 0, sc_split_done.n * 4));
@@ -526,6 +548,7 @@ struct NeusTestbed {
 			for (size_t j = 0; j < jobs.size() / 4; ++j) sc_jobs_before[jobs[4 * j] + 1] = (uint32_t)j + 1;
 			for (uint32_t b = 1; b <= swork.n_buckets; ++b) sc_jobs_before[b] = std::max(sc_jobs_before[b], sc_jobs_before[b - 1]);
 			sc_zero_from = swork.n_buckets;  // nothing assumed
+			sc_zero_from_e = gl.offset[gl.n_levels];
 		}
 		scan_tmp_bytes = std::max(scan_temp_bytes(MAX_RAYS), scan_temp_bytes((uint32_t)n_bins));
 		scan_tmp.alloc(scan_tmp_bytes + 256);
@@ -661,7 +684,7 @@ struct NeusTestbed {
 	// lanes marching one ray (segments of its step sequence, see march.hip): 8 (NEUS_MARCH_LANES = 1 / 4 / 8).
 	// Measured on MI355X (Config S, R = 2^18, step 5): sampling 0.52 ms with 1 lane, 0.24 with 4, 0.21 with 8.
 	uint32_t march_lanes() const {
-		if (const char* e = std::getenv("NEUS_MARCH_LANES")) { const uint32_t v = (uint32_t)std::strtoul(e, nullptr, 10); return v == 1 || v == 4 ? v : 8u; }
+		if (const char* e = std::getenv("NEUS_MARCH_LANES")) { const uint32_t v = (uint32_t)std::strtoul(e, nullptr, 10); return v == 1 || v == 4 || v == 16 ? v : 8u; }
 		return 8;
 	}
 	uint32_t gm_steps() const { return cfg.predict_global_movement ? cfg.global_movement_steps : 0u; }
@@ -727,6 +750,15 @@ struct NeusTestbed {
 	ScatterWork scatter_work_for(float* g_grid, uint32_t valid, hipStream_t s) {
 		if (g_grid != grads.p + lay.grid_off || sc_jobs_before.empty()) return swork;
 		const uint32_t L = gl.n_levels, n_entries = gl.offset[L];
+		if (swork.mode == 2) {
+			// the accumulation writes exactly the entries of the levels up to the valid one
+			const uint32_t lv = std::min(valid + 1, L), e_end = gl.offset[lv];
+			if (sc_zero_from_e > e_end) HIP_CHECK(hipMemsetAsync(g_grid + 2 * (size_t)e_end, 0, (size_t)(sc_zero_from_e - e_end) * 2 * sizeof(float), s));
+			sc_zero_from_e = e_end;
+			ScatterWork w = swork;
+			w.n_jobs2 = sc_jobs2_before[lv];
+			return w;
+		}
 		const uint32_t sb = valid + 1 >= L ? swork.n_buckets : std::min(swork.n_buckets, (gl.offset[valid + 1] + SB_SIZE - 1) / SB_SIZE);
 		if (sc_zero_from > sb) {
 			const size_t e_lo = (size_t)sb * SB_SIZE, e_hi = std::min<size_t>((size_t)sc_zero_from * SB_SIZE, n_entries);
@@ -1055,16 +1087,21 @@ struct NeusTestbed {
 			for (uint32_t k = 0; k < nch; ++k) {
 				const uint32_t e1 = k + 1 < nch ? chunk_ends[k] : 0xffffffffu;
 				const uint32_t e2 = k + 2 < nch ? chunk_ends[k + 1] : 0xffffffffu;
-				launch_nerf_infer(s, lay.L, lay.W, chunk_cnt.p + k, 0, c_in, gl, valid, params_h.p + lay.grid_off, mlp, net_out.p, 8192, chunk_list.p);
-				launch_loss_alpha_list(s, max_samples, chunk_cnt.p + k, chunk_list.p, coords.p, net_out.p, lp.cos_anneal, w, ds.cone_angle == 0.0f);
+				// the loss's alpha terms in the inference epilogue (k_loss_alpha's work on the round's samples)
+				const InferAlpha ia{w.sa, w.ekt, lp.cos_anneal, ds.cone_angle == 0.0f ? 1u : 0u, nullptr};
+				launch_nerf_infer(s, lay.L, lay.W, chunk_cnt.p + k, 0, c_in, gl, valid, params_h.p + lay.grid_off, mlp, net_out.p, 8192, chunk_list.p,
+				                  use_delta ? nullptr : &ia);
+				if (use_delta) launch_loss_alpha_list(s, max_samples, chunk_cnt.p + k, chunk_list.p, coords.p, net_out.p, lp.cos_anneal, w, ds.cone_angle == 0.0f);
 				launch_loss_scan_chunk(s, MAX_RAYS, numsteps.p, w, ccount.p, e0, e1, e2, k + 1 < nch ? chunk_list.p : nullptr, chunk_cnt.p + k + 1);
 				e0 = e1;
 			}
 			mark(3);
 		} else {
-			launch_nerf_infer(s, lay.L, lay.W, &st.p->n_kept, 0, c_in, gl, valid, params_h.p + lay.grid_off, mlp, net_out.p, 8192);
+			const InferAlpha ia{w.sa, w.ekt, lp.cos_anneal, ds.cone_angle == 0.0f ? 1u : 0u, w.n_long};
+			launch_nerf_infer(s, lay.L, lay.W, &st.p->n_kept, 0, c_in, gl, valid, params_h.p + lay.grid_off, mlp, net_out.p, 8192, nullptr,
+			                  use_delta ? nullptr : &ia);
 			mark(3);
-			launch_loss_alpha(s, max_samples, st.p, coords.p, net_out.p, lp.cos_anneal, w, ds.cone_angle == 0.0f);
+			if (use_delta) launch_loss_alpha(s, max_samples, st.p, coords.p, net_out.p, lp.cos_anneal, w, ds.cone_angle == 0.0f);
 			launch_loss_scan_ray(s, MAX_RAYS, numsteps.p, w, ccount.p);
 		}
 		launch_exclusive_scan(s, scan_tmp.p, scan_tmp_bytes, ccount.p, cbase.p, MAX_RAYS);
@@ -1643,6 +1680,7 @@ static void time_kernel_impl(NeusTestbed* tb, int kernel, int variant, int iters
 				launch_grid_scatter(s, nullptr, t.batch, t.batch, t.coords_c.p, COORD_W, t.gl, valid, t.tbuf.dLdenc, t.tbuf.genc, t.tbuf.v,
 				                    t.grads.p + t.lay.grid_off, t.swork, t.scan_tmp.p, t.scan_tmp_bytes);
 				t.sc_zero_from = t.swork.n_buckets;  // the replay wrote every bucket: nothing is known zero for the next step
+				t.sc_zero_from_e = t.gl.offset[t.gl.n_levels];
 				break;
 			case 8: t.encode(nullptr, t.batch, t.batch, t.batch, t.coords_c.p, COORD_W, valid, true, s); break;
 			default: throw std::runtime_error("unknown kernel id");
@@ -1666,6 +1704,24 @@ int neus_debug_march_stats(NeusTestbed* tb, uint32_t n, uint32_t* out) {
 		debug_launch_march_stats(tb->stream, n, tb->rays.p, tb->startt.p, tb->bf_lin.p, tb->ds, tb->bitfield.p, o.p);
 		HIP_CHECK(hipStreamSynchronize(tb->stream));
 		HIP_CHECK(hipMemcpy(out, o.p, 12 * (size_t)n, hipMemcpyDeviceToHost));
+	});
+}
+int neus_debug_march_profile(NeusTestbed* tb, unsigned long long* out, uint32_t max_waves, uint32_t* n_waves) {
+	return guard([&] {
+		if (!tb->have_net) throw std::runtime_error("no network");
+		NeusTestbed& t = *tb;
+		hipStream_t s = t.stream;
+		const uint32_t waves = MAX_RAYS * t.mwork.lanes_per_ray / 64;
+		Dev<unsigned long long> buf; buf.alloc((size_t)waves * 8);
+		HIP_CHECK(hipMemsetAsync(buf.p, 0, (size_t)waves * 64, s));
+		MarchWork mw = t.mwork;
+		mw.prof = buf.p;
+		launch_march_count(s, MAX_RAYS, t.max_samples, t.st.p, DPInfo{t.rank, t.world}, t.ds, t.bitfield.p, t.bf_lin.p, t.rng.state, t.rng.inc,
+		                   t.rays.p, t.startt.p, t.nreq.p, mw, nullptr, 0, t.ray_cull ? t.occ_bbox.p : nullptr);
+		HIP_CHECK(hipStreamSynchronize(s));
+		const uint32_t n = std::min(waves, max_waves);
+		HIP_CHECK(hipMemcpy(out, buf.p, (size_t)n * 64, hipMemcpyDeviceToHost));
+		if (n_waves) *n_waves = n;
 	});
 }
 int neus_debug_exclusive_scan(void* stream, const uint32_t* in, uint32_t* out, uint32_t n, int reps, uint32_t* failures) {

@@ -25,6 +25,9 @@ for target in [int(x) for x in os.environ.get("STEPS", "100,800,2000").split(","
     print(f"step {target}: rays {n} outer mean {outer.mean():.1f} max {outer.max():.0f} p50 {np.median(outer):.0f} p99 {np.percentile(outer, 99):.0f}; "
           f"inner mean {inner.mean():.1f}; samples mean {ns.mean():.1f} max {ns.max():.0f}; wave SIMT eff {eff:.3f}; "
           f"sum wave-max {w.max(1).sum():.3e} vs sum/64 {outer.sum() / 64:.3e}", flush=True)
+    m = int(os.environ.get("FIRST", "22000"))
+    print(f"   first {m} rays: outer mean {outer[:m].mean():.1f} p99 {np.percentile(outer[:m], 99):.0f} max {outer[:m].max():.0f}; "
+          f"inner mean {inner[:m].mean():.1f} max {inner[:m].max():.0f}; samples mean {ns[:m].mean():.1f} max {ns[:m].max():.0f}", flush=True)
     for k in (1, 2, 4, 8):  # efficiency if waves took k*64 rays with perfect refill
         ww = outer.reshape(-1, 64 * k)
         print(f"   refill pool {64 * k}: max-lane-sum bound eff {(ww.sum(1) / 64).sum() / np.maximum(ww.max(1), ww.sum(1) / 64).sum():.3f}")

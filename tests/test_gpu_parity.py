@@ -902,7 +902,7 @@ def test_marching_cubes_64bit_grid_index(torch_cuda):
 
 
 def test_multilane_march_equals_single_lane(env):
-    """The 4- and 8-lanes-per-ray segmented march (march.hip k_march<.., MG>: lanes start at slices of the ray's step
+    """The 4-, 8- and 16-lanes-per-ray segmented march (march.hip k_march<.., MG>: lanes start at slices of the ray's step
     sequence, join the previous segment's exit, re-march when they missed it) against the one-lane march, bit for bit
     (rays, numsteps, coordinates, counters), on random occupancy grids from sparse to full (many empty-cell skips
     landing across segment starts, long sample runs, the NERF_STEPS cap on the full grid) and on the training bitfield."""
@@ -911,7 +911,7 @@ def test_multilane_march_equals_single_lane(env):
     from neus2_amd import pyngp
     sc = env["sc"]
     tbs = {}
-    for lanes in ("1", "4", "8"):
+    for lanes in ("1", "4", "8", "16"):
         os.environ["NEUS_MARCH_LANES"] = lanes
         tb = pyngp.Testbed(pyngp.TestbedMode.Nerf)
         tb.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)

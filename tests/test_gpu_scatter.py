@@ -1,5 +1,6 @@
-"""The wide-block hash-grid gradient scatter (k_scatter_hist_w + k_scatter_bin_w: 1024-sample workgroups, grid.hip)
-against the 256-sample binned one (NEUS_SCATTER=binned): both bin the same fp16x2 corner contributions (first +
+"""The hash-grid gradient scatter paths (grid.hip) against each other: per-block record regions (k_scatter_bin_r +
+k_scatter_accum_r, the default), the wide-block binning (k_scatter_hist_w + k_scatter_bin_w, NEUS_SCATTER=wide) and
+the 256-sample binned one (NEUS_SCATTER=binned), at 512- and 1024-sample workgroups: all bin the same fp16x2 corner contributions (first +
 second order, grid.h:371-500 and 880-1007) and sum them in int64 fixed point, so the grid gradient must be bitwise equal, for a
 backward on perturbed parameters (every level active, dense and hashed levels, the heavy split buckets of the small
 dense levels), for a backward at a low progressive level (inactive levels untouched), and over 40 training steps."""
@@ -17,9 +18,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _testbed(sc, mode, batch):
-    """mode: "seg" (wide-block binning, 512-sample workgroups), "seg1024" (1024-sample ones) or "binned" (256)."""
+    """mode: "regions" (per-block record regions, 512-sample workgroups: the default), "regions1024" (1024-sample
+    ones), "seg" (wide-block binning, 512), "seg1024" or "binned" (the 256-sample histogram / scan / bin path)."""
     from neus2_amd import pyngp
-    env = {"NEUS_SCATTER": "binned" if mode == "binned" else None, "NEUS_SCATTER_CHUNK": "1024" if mode == "seg1024" else None}
+    env = {"NEUS_SCATTER": {"binned": "binned", "seg": "wide", "seg1024": "wide"}.get(mode),
+           "NEUS_SCATTER_CHUNK": "1024" if mode.endswith("1024") else None}
     old = {k: os.environ.get(k) for k in env}
     for k, v in env.items():
         if v is None:
@@ -45,11 +48,13 @@ def scene(torch_cuda):
     return scenes.small_scene(n_views=8, width=64, height=48)
 
 
-def test_wide_scatter_bitwise_equals_binned(scene, torch_cuda):
+def test_scatter_paths_bitwise_equal(scene, torch_cuda):
     from neus2_amd._lib import check, lib
     t = torch_cuda
     n = 1 << 14
-    seg, seg1k, binned = _testbed(scene, "seg", n), _testbed(scene, "seg1024", n), _testbed(scene, "binned", n)
+    modes = ("regions", "regions1024", "seg", "seg1024", "binned")
+    tbs = [_testbed(scene, m, n) for m in modes]
+    seg = tbs[0]
     lay = seg.layout()
     rng = np.random.default_rng(17)
     p = seg.get_params().copy()
@@ -58,7 +63,7 @@ def test_wide_scatter_bitwise_equals_binned(scene, torch_cuda):
     w0[:, 3:3 + 2 * L] = rng.normal(0, 0.3, (64, 2 * L))
     p[: 64 * din] = w0.reshape(-1)
     p[lay["grid_offset"]:lay["variance_offset"]] = rng.uniform(-0.1, 0.1, lay["variance_offset"] - lay["grid_offset"])
-    for tb in (seg, seg1k, binned):
+    for tb in tbs:
         tb.set_params(p)
     c = np.zeros((n, 7), np.float32)
     c[:, :3] = rng.uniform(0.02, 0.98, (n, 3))
@@ -74,19 +79,19 @@ def test_wide_scatter_bitwise_equals_binned(scene, torch_cuda):
     dl16 = dl.astype(np.float16)
     for valid in (L, 3):
         grads = []
-        for tb in (seg, seg1k, binned):
+        for tb in tbs:
             g = t.zeros(lay["n_params"], dtype=t.float32, device="cuda")
             check(lib().neus_net_backward(tb.handle, None, C.c_uint32(n), ptr(dev(t, c)), C.c_uint32(valid), ptr(dev(t, dl16)),
                                           C.c_uint32(n), ptr(g)))
             t.cuda.synchronize()
             grads.append(g.cpu().numpy())
-        a, a1k, b = grads
+        b = grads[-1]
         g0, g1 = lay["grid_offset"], lay["variance_offset"]
-        assert np.any(a[g0:g1])
-        np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
-        np.testing.assert_array_equal(a1k.view(np.uint32), b.view(np.uint32))
+        assert np.any(b[g0:g1])
+        for m, a in zip(modes, grads):
+            np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32), err_msg=m)
     # training: 40 steps (progressive levels 3 -> 3, occupancy updates) bitwise equal
-    seg2, bin2 = _testbed(scene, "seg", 4096), _testbed(scene, "binned", 4096)
+    seg2, bin2 = _testbed(scene, "regions", 4096), _testbed(scene, "binned", 4096)
     seg2.train_steps(40)
     bin2.train_steps(40)
     np.testing.assert_array_equal(seg2.get_params().view(np.uint32), bin2.get_params().view(np.uint32))
