@@ -170,4 +170,33 @@ struct StepState {
 };
 static_assert(sizeof(StepState) == 128, "StepState is one 128-B record");
 
+// Counters::update_after_training (testbed_nerf.cu:3399-3438) at the end of a step: one thread (k_step_counters, or
+// the Adam launch's block 0)
+__device__ __forceinline__ void step_counters_update(StepState* st, uint32_t target_batch, uint32_t max_samples, uint32_t world, uint32_t fixed_rays) {
+	const uint32_t R = st->rays_per_batch;
+	st->n_rays_total += R * world;  // n_rays_total
+	st->pre_total += st->n_kept;
+	st->rays_total += R;
+	// next step's first march pass: the slots up to this step's kept extent plus a margin (all slots when every
+	// ray with samples fitted under this step's cap)
+	const bool fit = st->numsteps_counter <= st->max_inference;
+	const uint32_t ext = st->kept_extent + st->kept_extent / 4 + 1024;
+	st->march_est = fit ? 0u : (ext + 63u) / 64u * 64u;
+	// per rank: the cap on the next step's pre-compaction samples follows this rank's own request count
+	const uint32_t before = st->numsteps_counter;
+	const uint32_t measured = st->compacted_counter / world;
+	st->measured_before = before;
+	st->measured_batch_size = measured;
+	st->trained_total += min(measured, target_batch);  // real training samples (the rest of the batch is rollover)
+	if (before == 0 || measured == 0) { st->zero_records = 1; return; }
+	st->zero_records = 0;
+	uint32_t mi = min(before, max_samples);
+	st->max_inference = (mi + 127u) / 128u * 128u;
+	if (fixed_rays) { st->rays_per_batch = fixed_rays; return; }
+	uint32_t r = (uint32_t)((float)R * (float)target_batch / (float)measured);
+	r = (r + 127u) / 128u * 128u;
+	st->rays_per_batch = min(r, 1u << 18);
+}
+
+
 } // namespace neus

@@ -21,15 +21,30 @@ namespace neus {
 __device__ __forceinline__ uint32_t load_n(const uint32_t* n_ptr, uint32_t n_fixed) { return n_ptr ? *n_ptr : n_fixed; }
 
 // enc: [L][ld] packed half2 (features 2l, 2l+1); dydx: [L*6][ld] f32 (feature f, dim d at row 6l+3f+d)
+// With a rollover (EncodeRollover: the training batch), records i >= n_in = min(compacted, n_elements) are the
+// reference's fill_rollover_and_rescale copies (my_tcnn common_device.h:515-535): every level reads record i % n_in,
+// and the level-0 blocks write the copies (coordinates, and dL/doutput scaled by n_in / n_elements) for the kernels
+// after this one (k_rollover's work, without its launch).
 __global__ void __launch_bounds__(256) k_grid_encode(
 	const uint32_t* __restrict__ n_ptr, uint32_t n_fixed, uint32_t ld,
 	const float* __restrict__ coords, uint32_t coord_stride,
 	const GridLevels gl, uint32_t valid_level,
-	const half_t* __restrict__ grid, uint32_t* __restrict__ enc, float* __restrict__ dydx) {
+	const half_t* __restrict__ grid, uint32_t* __restrict__ enc, float* __restrict__ dydx, EncodeRollover ro) {
 	const uint32_t n = load_n(n_ptr, n_fixed);
 	const uint32_t l = blockIdx.y;
 	const half_t* gp = grid + (size_t)gl.offset[l] * 2;
+	const uint32_t n_in = ro.n_in_ptr ? min(*ro.n_in_ptr, ro.n_elements) : 0xffffffffu;
 	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+		const uint32_t src = i < n_in ? i : i % n_in;  // (n_in > 0 whenever n > 0: n_train is 0 without records)
+		if (l == 0 && i != src) {
+			float* cw = (float*)coords;
+			for (uint32_t k = 0; k < coord_stride; ++k) cw[(size_t)i * coord_stride + k] = coords[(size_t)src * coord_stride + k];
+#pragma unroll
+			for (int k = 0; k < OUT_W; ++k) {
+				const float r = (float)ro.dL_dout[(size_t)src * OUT_W + k];
+				ro.dL_dout[(size_t)i * OUT_W + k] = (half_t)(r * n_in / ro.n_elements);
+			}
+		}
 		if (l > valid_level) {
 			enc[(size_t)l * ld + i] = 0u;
 			if (dydx) {
@@ -38,7 +53,7 @@ __global__ void __launch_bounds__(256) k_grid_encode(
 			}
 			continue;
 		}
-		const float* c = coords + (size_t)i * coord_stride;
+		const float* c = coords + (size_t)src * coord_stride;
 		LevelSetup s = level_setup(gl, l, c[0], c[1], c[2]);
 		h2 v[8];
 		gather_corners(s, gp, v);
@@ -746,9 +761,11 @@ void launch_enc_ddLdoutput(hipStream_t s, uint32_t n, uint32_t ld, uint32_t L, c
 	if (n) k_enc_ddLdoutput<<<(n + 255) / 256, 256, 0, s>>>(n, ld, L, ddx, dydx, (uint32_t*)out, v4);
 }
 void launch_grid_encode(hipStream_t s, const uint32_t* n_ptr, uint32_t n_fixed, uint32_t ld, const float* coords, uint32_t coord_stride,
-                        const GridLevels& gl, uint32_t valid_level, const half_t* grid, uint32_t* enc, float* dydx, uint32_t grid_x) {
+                        const GridLevels& gl, uint32_t valid_level, const half_t* grid, uint32_t* enc, float* dydx, uint32_t grid_x,
+                        const EncodeRollover* ro) {
 	if (!grid_x) return;
-	k_grid_encode<<<dim3(grid_x, gl.n_levels), 256, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, grid, enc, dydx);
+	const EncodeRollover r = ro ? *ro : EncodeRollover{nullptr, 0u, nullptr};
+	k_grid_encode<<<dim3(grid_x, gl.n_levels), 256, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, grid, enc, dydx, r);
 }
 size_t scatter_records_capacity(uint32_t n_cap, uint32_t n_levels) { return (size_t)n_cap * n_levels * 8; }
 std::vector<uint32_t> scatter_accum_jobs(const GridLevels& gl, uint32_t n_buckets, uint32_t& n_split) {

@@ -143,12 +143,26 @@ struct AdamParams {
 	uint32_t optimize_matrix, optimize_non_matrix;
 };
 
+// The Adam launch's two riders (each optional): the step-end counters (k_step_counters' work, done by thread 0 of block
+// 0) and the transposed / permuted fp16 copies of the MLP matrices (prepare_weights), written by the threads that
+// update the matrix parameters (the launch after it no longer has to re-transpose)
+struct StepCounterArgs { StepState* st; uint32_t target_batch, max_samples, world, fixed_rays; };
+struct AdamTranspose {
+	uint32_t n;                                    // matrices (0: none)
+	uint32_t off[5], rows[5], cols[5];             // parameter offset and shape of matrix j
+	half_t* dst[5];                                // its transposed copy [cols][rows]
+	int32_t inv[48];                               // matrix 0 (the density input layer): logical column -> physical, -1 none
+	half_t* d0p; half_t* d0Tp; uint32_t din, W;    // its permuted copy [W][din] and transposed permuted copy [din][W]
+};
 struct TransposeJob { const half_t* src; half_t* dst; uint32_t rows, cols; };
 struct TransposeJobs { TransposeJob j[8]; uint32_t n; };
 
 // grid.hip
+// the training batch's rollover done by the encode (k_grid_encode): n_in = *n_in_ptr (compacted count) records are real,
+// the rest of the n_elements batch copies record i % n_in (coordinates in place, dL_dout rescaled)
+struct EncodeRollover { const uint32_t* n_in_ptr; uint32_t n_elements; half_t* dL_dout; };
 void launch_grid_encode(hipStream_t s, const uint32_t* n_ptr, uint32_t n_fixed, uint32_t ld, const float* coords, uint32_t coord_stride,
-                        const GridLevels& gl, uint32_t valid_level, const half_t* grid, uint32_t* enc, float* dydx, uint32_t grid_x);
+                        const GridLevels& gl, uint32_t valid_level, const half_t* grid, uint32_t* enc, float* dydx, uint32_t grid_x, const EncodeRollover* ro = nullptr);
 size_t scatter_records_capacity(uint32_t n_cap, uint32_t n_levels);
 uint32_t scatter_n_buckets(const GridLevels& gl);
 void launch_grid_scatter(hipStream_t s, const uint32_t* n_ptr, uint32_t n_cap, uint32_t ld, const float* coords, uint32_t coord_stride,
@@ -215,6 +229,7 @@ struct MarchWork {
 	uint2* seg; uint32_t lanes_per_ray;  /* 1, 4, 8 or 16 */
 	PcgJumpTable jt;                      /* jump-ahead of the ray generator's per-ray rng offsets */
 	unsigned long long* prof = nullptr;   /* development: per-wave phase timestamps of the march (8 per wave), or null */
+	uint32_t dbg = 0;                     /* development timing experiments (wrong results): 1 no record stores, 2 no occupancy loads */
 };
 // Ray generation + the occupancy march: rays (6 f32 per slot), tstart (1 per slot), nreq (requested
 // samples per slot) and the sample runs (MarchWork).
@@ -294,7 +309,8 @@ void launch_exclusive_scan(hipStream_t s, void* temp, size_t temp_bytes, const u
 void launch_sum_f32(hipStream_t s, void* temp, size_t temp_bytes, const float* in, float* out, uint32_t n);
 // optim.hip
 void launch_adam_ema(hipStream_t s, const AdamParams& p, float* weights_fp, half_t* weights_h, const float* grads, float* m1, float* m2,
-                     uint32_t* steps, float* ema_tmp, half_t* ema_h);
+                     uint32_t* steps, float* ema_tmp, half_t* ema_h,
+                     const StepCounterArgs* counters = nullptr, const AdamTranspose* tr = nullptr);
 void launch_cast_half(hipStream_t s, uint32_t n, const float* in, half_t* out);
 void launch_add_f32(hipStream_t s, uint32_t n, const float* src, float* dst);
 // operator-module encoding helpers (grid.hip)

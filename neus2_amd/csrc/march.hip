@@ -150,11 +150,15 @@ __device__ __forceinline__ void load_march_ray(const float* __restrict__ rays, u
 // step at or past it is the next segment's). Returns false once the ray is finished (left the AABB).
 // Sample runs go to `rec` as {t of the first sample, k_first << 8 | length} (segment-local records).
 struct SegAcc { float t0; uint32_t k0, len, nrec, n; };
-__device__ __forceinline__ void seg_flush(uint2* __restrict__ rec, SegAcc& a) {
-	if (a.len) { rec[a.nrec++] = make_uint2(__float_as_uint(a.t0), (a.k0 << 8) | a.len); a.len = 0; }
+// dbg: MarchWork::dbg (development timing experiments; 0 in production)
+__device__ __forceinline__ void seg_flush(uint2* __restrict__ rec, SegAcc& a, uint32_t dbg = 0) {
+	if (a.len) {
+		if (!(dbg & 1u)) rec[a.nrec] = make_uint2(__float_as_uint(a.t0), (a.k0 << 8) | a.len);
+		++a.nrec; a.len = 0;
+	}
 }
-__device__ __forceinline__ void seg_add(uint2* __restrict__ rec, SegAcc& a, float t, uint32_t k) {
-	if (a.len == MARCH_RUN_MAX) seg_flush(rec, a);
+__device__ __forceinline__ void seg_add(uint2* __restrict__ rec, SegAcc& a, float t, uint32_t k, uint32_t dbg = 0) {
+	if (a.len == MARCH_RUN_MAX) seg_flush(rec, a, dbg);
 	if (a.len == 0) { a.t0 = t; a.k0 = k; }
 	++a.len; ++a.n;
 }
@@ -174,7 +178,7 @@ __device__ __forceinline__ void visit(Visits& v, uint32_t kb, uint32_t ke) {
 template <bool FAST>
 __device__ __forceinline__ bool march_event(const DevDataset& ds, const uint8_t* __restrict__ bf, const uint32_t* __restrict__ lin,
                                             const MarchRay& mr, float& t, uint32_t& k, uint32_t k_end, SegAcc& acc, Visits& vis,
-                                            uint2* __restrict__ rec) {
+                                            uint2* __restrict__ rec, uint32_t dbg = 0) {
 	const uint32_t kb = k;
 	if (FAST) {
 		float pos[3];
@@ -187,7 +191,8 @@ __device__ __forceinline__ bool march_event(const DevDataset& ds, const uint8_t*
 		bool occ, interior = false;
 		if ((m > 0.0f) & (m < 0.5f)) {
 			mip0_cell(pos, c);
-			occ = (lin[((uint32_t)c[0] << 9) | ((uint32_t)c[1] << 2) | ((uint32_t)c[2] >> 5)] >> (c[2] & 31)) & 1;
+			const uint32_t wi = ((uint32_t)c[0] << 9) | ((uint32_t)c[1] << 2) | ((uint32_t)c[2] >> 5);
+			occ = ((dbg & 2u) ? (wi * 2654435761u) : lin[wi]) >> (c[2] & 31) & 1;
 			interior = (c[0] >= 1) & (c[0] <= NERF_GRIDSIZE - 2) & (c[1] >= 1) & (c[1] <= NERF_GRIDSIZE - 2) & (c[2] >= 1) &
 			           (c[2] <= NERF_GRIDSIZE - 2) & !((c[0] == NERF_GRIDSIZE / 2) & (c[1] == NERF_GRIDSIZE / 2) & (c[2] == NERF_GRIDSIZE / 2));
 		} else {
@@ -195,7 +200,7 @@ __device__ __forceinline__ bool march_event(const DevDataset& ds, const uint8_t*
 			occ = occupied(pos[0], pos[1], pos[2], bf, mip);
 		}
 		if (occ) {
-			seg_add(rec, acc, t, k); t += MIN_CONE_STEPSIZE; ++k;
+			seg_add(rec, acc, t, k, dbg); t += MIN_CONE_STEPSIZE; ++k;
 			if (interior) {
 				while (k < k_end) {
 					float p2[3];
@@ -203,13 +208,13 @@ __device__ __forceinline__ bool march_event(const DevDataset& ds, const uint8_t*
 					for (int d = 0; d < 3; ++d) p2[d] = mr.o[d] + t * mr.dir[d];
 					int c2[3]; mip0_cell(p2, c2);
 					if ((c2[0] != c[0]) | (c2[1] != c[1]) | (c2[2] != c[2])) break;
-					seg_add(rec, acc, t, k); t += MIN_CONE_STEPSIZE; ++k;
+					seg_add(rec, acc, t, k, dbg); t += MIN_CONE_STEPSIZE; ++k;
 				}
 			}
 			visit(vis, kb, k);
 			return true;
 		}
-		seg_flush(rec, acc);
+		seg_flush(rec, acc, dbg);
 		visit(vis, kb, kb + 1);
 		// advance_to_next_voxel with a constant step (march_step)
 		const uint32_t res = NERF_GRIDSIZE >> mip;
@@ -256,11 +261,12 @@ constexpr uint32_t FINISHED = 0xffffffffu;
 template <bool FAST>
 __device__ __forceinline__ void march_segment(const DevDataset& ds, const uint8_t* __restrict__ bf, const uint32_t* __restrict__ lin,
                                               const MarchRay& mr, float& t, uint32_t& k, uint32_t k_end, SegAcc& acc, Visits& vis,
-                                              uint2* __restrict__ rec, uint32_t rec_cap) {
+                                              uint2* __restrict__ rec, uint32_t rec_cap, uint32_t* n_ev = nullptr, uint32_t dbg = 0) {
 	while (k < k_end) {
-		if (acc.nrec + 1 >= rec_cap || !march_event<FAST>(ds, bf, lin, mr, t, k, k_end, acc, vis, rec)) { k = FINISHED; break; }
+		if (n_ev) ++*n_ev;
+		if (acc.nrec + 1 >= rec_cap || !march_event<FAST>(ds, bf, lin, mr, t, k, k_end, acc, vis, rec, dbg)) { k = FINISHED; break; }
 	}
-	seg_flush(rec, acc);
+	seg_flush(rec, acc, dbg);
 }
 
 // Two passes over the ray slots. Only a prefix of the slots can be kept: slot i is kept iff n_i > 0 and
@@ -336,7 +342,8 @@ __global__ void __launch_bounds__(256) k_march(uint32_t cap_rays, uint32_t pass,
 		vis.n = 0;
 		float et = t;
 		uint32_t ek = active ? k : FINISHED;
-		if (active) { march_segment<FAST>(ds, bitfield, lin, mr, et, ek, k_end, acc, vis, rec, SEG_CAP); }
+		uint32_t n_ev = 0;
+		if (active) { march_segment<FAST>(ds, bitfield, lin, mr, et, ek, k_end, acc, vis, rec, SEG_CAP, &n_ev, mw.dbg); }
 		stamp(2);
 		// segment order: lane g joins the exit of lane g - 1
 		uint32_t vk = k;   // first valid step of this segment
@@ -429,7 +436,10 @@ __global__ void __launch_bounds__(256) k_march(uint32_t cap_rays, uint32_t pass,
 			uint32_t ws = g == 0 && have && t0 >= 0.f ? n_tot : 0u;
 #pragma unroll
 			for (int off = 32; off > 0; off >>= 1) ws += (uint32_t)__shfl_xor((int)ws, off);
-			if (lane == 0) { pw[6] = ws; pw[7] = n_redo; }
+			uint32_t emax = n_ev, esum = n_ev;
+#pragma unroll
+			for (int off = 32; off > 0; off >>= 1) { emax = max(emax, (uint32_t)__shfl_xor((int)emax, off)); esum += (uint32_t)__shfl_xor((int)esum, off); }
+			if (lane == 0) { pw[6] = ws; pw[7] = ((unsigned long long)emax << 32) | ((unsigned long long)esum << 8) | n_redo; }
 		}
 		first = false;
 	}
@@ -988,7 +998,10 @@ __global__ void __launch_bounds__(256) k_loss_ray(uint32_t cap_rays, StepState* 
 	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cap_rays; i += gridDim.x * blockDim.x) {
 		const uint32_t ns = numsteps[2 * i], base = numsteps[2 * i + 1];
 		const uint32_t cn = ccount[i], cb = cbase[i];
-		if (i == cap_rays - 1) st->compacted_counter = cb + cn;
+		if (i == cap_rays - 1) {
+			st->compacted_counter = cb + cn;
+			st->n_train = min(cb + cn, lp.max_compacted) ? lp.max_compacted : 0u;  // the training batch (k_rollover sets it too)
+		}
 		loss_out[i] = 0.f; ek_out[i] = 0.f; mask_out[i] = 0.f;
 		if (ns == 0) { numsteps[2 * i] = 0; numsteps[2 * i + 1] = cb; continue; }
 		const float4 acc = racc[i];
@@ -1172,29 +1185,7 @@ __global__ void k_rollover(uint32_t n_elements, const StepState* __restrict__ st
 // all-reduced counters so every rank adapts R identically.
 __global__ void k_step_counters(StepState* st, uint32_t target_batch, uint32_t max_samples, uint32_t world, uint32_t fixed_rays) {
 	if (threadIdx.x != 0 || blockIdx.x != 0) return;
-	const uint32_t R = st->rays_per_batch;
-	st->n_rays_total += R * world;  // n_rays_total
-	st->pre_total += st->n_kept;
-	st->rays_total += R;
-	// next step's first march pass: the slots up to this step's kept extent plus a margin (all slots when every
-	// ray with samples fitted under this step's cap)
-	const bool fit = st->numsteps_counter <= st->max_inference;
-	const uint32_t ext = st->kept_extent + st->kept_extent / 4 + 1024;
-	st->march_est = fit ? 0u : (ext + 63u) / 64u * 64u;
-	// per rank: the cap on the next step's pre-compaction samples follows this rank's own request count
-	const uint32_t before = st->numsteps_counter;
-	const uint32_t measured = st->compacted_counter / world;
-	st->measured_before = before;
-	st->measured_batch_size = measured;
-	st->trained_total += min(measured, target_batch);  // real training samples (the rest of the batch is rollover)
-	if (before == 0 || measured == 0) { st->zero_records = 1; return; }
-	st->zero_records = 0;
-	uint32_t mi = min(before, max_samples);
-	st->max_inference = (mi + 127u) / 128u * 128u;
-	if (fixed_rays) { st->rays_per_batch = fixed_rays; return; }
-	uint32_t r = (uint32_t)((float)R * (float)target_batch / (float)measured);
-	r = (r + 127u) / 128u * 128u;
-	st->rays_per_batch = min(r, 1u << 18);
+	step_counters_update(st, target_batch, max_samples, world, fixed_rays);
 }
 
 // ---------------------------------------------------------------- host launchers

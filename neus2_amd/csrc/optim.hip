@@ -19,7 +19,9 @@ namespace neus {
 // used by every kernel; ema_tmp fp32 running EMA; ema_h fp16 inference weights.
 __global__ void __launch_bounds__(256) k_adam_ema(AdamParams p, float* __restrict__ weights_fp, half_t* __restrict__ weights_h,
                                                   const float* __restrict__ grads, float* __restrict__ m1, float* __restrict__ m2,
-                                                  uint32_t* __restrict__ steps, float* __restrict__ ema_tmp, half_t* __restrict__ ema_h) {
+                                                  uint32_t* __restrict__ steps, float* __restrict__ ema_tmp, half_t* __restrict__ ema_h,
+                                                  StepCounterArgs sc, AdamTranspose tr) {
+	if (sc.st && blockIdx.x == 0 && threadIdx.x == 0) step_counters_update(sc.st, sc.target_batch, sc.max_samples, sc.world, sc.fixed_rays);
 	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < p.n; i += gridDim.x * blockDim.x) {
 		float gradient = grads[i] / p.loss_scale;
 		const bool is_matrix = i < p.n_matrix;
@@ -43,6 +45,19 @@ __global__ void __launch_bounds__(256) k_adam_ema(AdamParams p, float* __restric
 		const float f = (ema_tmp[i] * p.ema_decay * p.ema_debias_old + wh * (1 - p.ema_decay)) * p.ema_debias_new;
 		ema_tmp[i] = f;
 		ema_h[i] = (half_t)f;
+		if (tr.n && is_matrix) {  // the MLP's transposed / permuted fp16 copies of this weight (prepare_weights)
+			const half_t hv = (half_t)wh;
+			for (uint32_t j = 0; j < tr.n; ++j) {
+				const uint32_t e = i - tr.off[j];
+				if (i < tr.off[j] || e >= tr.rows[j] * tr.cols[j]) continue;
+				const uint32_t r = e / tr.cols[j], c = e % tr.cols[j];
+				tr.dst[j][(size_t)c * tr.rows[j] + r] = hv;
+				if (j == 0 && tr.d0p) {
+					const int32_t q = c < 48 ? tr.inv[c] : -1;
+					if (q >= 0) { tr.d0p[(size_t)r * tr.din + q] = hv; tr.d0Tp[(size_t)q * tr.W + r] = hv; }
+				}
+			}
+		}
 	}
 }
 
@@ -291,8 +306,11 @@ __global__ void __launch_bounds__(256) k_occ_bbox_final(const float* __restrict_
 // ---------------------------------------------------------------- host launchers
 static inline uint32_t nblk(uint64_t n, uint32_t cap = 4096) { return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, cap)); }
 void launch_adam_ema(hipStream_t s, const AdamParams& p, float* weights_fp, half_t* weights_h, const float* grads, float* m1, float* m2,
-                     uint32_t* steps, float* ema_tmp, half_t* ema_h) {
-	k_adam_ema<<<nblk(p.n, 8192), 256, 0, s>>>(p, weights_fp, weights_h, grads, m1, m2, steps, ema_tmp, ema_h);
+                     uint32_t* steps, float* ema_tmp, half_t* ema_h, const StepCounterArgs* counters, const AdamTranspose* tr) {
+	const StepCounterArgs sc = counters ? *counters : StepCounterArgs{nullptr, 0u, 0u, 1u, 0u};
+	AdamTranspose t{};
+	if (tr) t = *tr;
+	k_adam_ema<<<nblk(p.n, 8192), 256, 0, s>>>(p, weights_fp, weights_h, grads, m1, m2, steps, ema_tmp, ema_h, sc, t);
 }
 void launch_add_f32(hipStream_t s, uint32_t n, const float* src, float* dst) {
 	if (n) k_add_f32<<<std::min<uint32_t>((n + 255) / 256, 8192), 256, 0, s>>>(n, src, dst);

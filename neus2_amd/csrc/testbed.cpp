@@ -728,9 +728,10 @@ struct NeusTestbed {
 	float cos_anneal() const { return cfg.anneal_end == 0 ? 1.0f : std::min(1.0f, (float)training_step / cfg.anneal_end); }
 
 	// ------------------------------------------------------------ network stages
-	void encode(const uint32_t* n_ptr, uint32_t n_fixed, uint32_t n_cap, uint32_t ld, const float* c, uint32_t stride, uint32_t valid, bool want_dydx, hipStream_t s) {
+	void encode(const uint32_t* n_ptr, uint32_t n_fixed, uint32_t n_cap, uint32_t ld, const float* c, uint32_t stride, uint32_t valid, bool want_dydx, hipStream_t s,
+	            const EncodeRollover* ro = nullptr) {
 		const uint32_t gx = std::max<uint32_t>(1, std::min<uint32_t>((n_cap + 255) / 256, 2048));
-		launch_grid_encode(s, n_ptr, n_fixed, ld, c, stride, gl, valid, params_h.p + lay.grid_off, enc.p, want_dydx ? dydx.p : nullptr, gx);
+		launch_grid_encode(s, n_ptr, n_fixed, ld, c, stride, gl, valid, params_h.p + lay.grid_off, enc.p, want_dydx ? dydx.p : nullptr, gx, ro);
 	}
 	void net_forward(const uint32_t* n_ptr, uint32_t n_fixed, uint32_t n_cap, const float* c, uint32_t valid, half_t* out, hipStream_t s) {
 		const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((n_cap + 127) / 128, 8192));
@@ -772,9 +773,9 @@ struct NeusTestbed {
 	}
 	// forward recompute + backward into g (fp32 [P], zeroed by the caller)
 	void net_backward(const uint32_t* n_valid_ptr, const uint32_t* n_train_ptr, uint32_t n, const float* c, uint32_t valid,
-	                  const half_t* dlo, float* g, hipStream_t s, bool marks = false, bool canonical = true) {
+	                  const half_t* dlo, float* g, hipStream_t s, bool marks = false, bool canonical = true, const EncodeRollover* ro = nullptr) {
 		const uint32_t ld = n;
-		encode(n_train_ptr, n, n, ld, c, COORD_W, valid, true, s);
+		encode(n_train_ptr, n, n, ld, c, COORD_W, valid, true, s, ro);
 		if (marks) mark(5);
 		TrainBufs t = tbuf;
 		t.var_grad = g + lay.var_off;
@@ -857,7 +858,7 @@ struct NeusTestbed {
 	}
 
 	// ------------------------------------------------------------ optimizer (trainer.h:170-172)
-	void optimizer_step(const float* g) {
+	void optimizer_step(const float* g, const StepCounterArgs* counters = nullptr) {
 		// ExponentialDecay (exponential_decay.h:61-80): evaluated with the nested step count before the Adam step
 		const uint32_t sb = adam_step;
 		if (sb == 0) lr_factor = 1.0f;
@@ -871,8 +872,21 @@ struct NeusTestbed {
 		p.ema_debias_old = 1 - (float)std::pow(cfg.ema_decay, adam_step - 1);
 		p.ema_debias_new = 1.0f / (1 - (float)std::pow(cfg.ema_decay, adam_step));
 		p.optimize_matrix = 1; p.optimize_non_matrix = 1;
-		launch_adam_ema(stream, p, params_fp.p, params_h.p, g, m1.p, m2.p, adam_steps.p, ema_tmp.p, ema_h.p);
-		prepare_weights();
+		// the transposed / permuted MLP copies are written by the Adam launch itself
+		const AdamTranspose tr = adam_transpose();
+		launch_adam_ema(stream, p, params_fp.p, params_h.p, g, m1.p, m2.p, adam_steps.p, ema_tmp.p, ema_h.p, counters, &tr);
+	}
+	AdamTranspose adam_transpose() const {
+		const Layout& l = lay;
+		AdamTranspose t{};
+		t.n = 5;
+		const uint32_t off[5] = {l.off_d0, l.off_d1, l.off_r0, l.off_r1, l.off_r2}, rows[5] = {l.W, 16, l.W, l.W, 16}, cols[5] = {l.din, l.W, 48, l.W, l.W};
+		half_t* dst[5] = {(half_t*)mlp.d0T, (half_t*)mlp.d1T, (half_t*)mlp.r0T, (half_t*)mlp.r1T, (half_t*)mlp.r2T};
+		for (int j = 0; j < 5; ++j) { t.off[j] = off[j]; t.rows[j] = rows[j]; t.cols[j] = cols[j]; t.dst[j] = dst[j]; }
+		for (int k = 0; k < 48; ++k) t.inv[k] = -1;
+		for (uint32_t q = 0; q < din_perm.din && q < 48; ++q) if (din_perm.p[q] >= 0 && din_perm.p[q] < 48) t.inv[din_perm.p[q]] = (int32_t)q;
+		t.d0p = (half_t*)mlp.d0p; t.d0Tp = (half_t*)mlp.d0Tp; t.din = din_perm.din; t.W = din_perm.W;
+		return t;
 	}
 
 	void mark(int i) { if (profiling) HIP_CHECK(hipEventRecord(ev[prof_par][i], stream)); }
@@ -1107,7 +1121,9 @@ struct NeusTestbed {
 		launch_exclusive_scan(s, scan_tmp.p, scan_tmp_bytes, ccount.p, cbase.p, MAX_RAYS);
 		launch_loss_ray(s, MAX_RAYS, st.p, dp, ds, lp, numsteps.p, ccount.p, cbase.p, w, loss.p, ek.p, mask.p);
 		launch_loss_grad(s, max_samples, st.p, dp, lp, coords.p, net_out.p, numsteps.p, w, coords_c.p, dL_dout.p);
-		launch_rollover(s, batch, st.p, coords_c.p, dL_dout.p);
+		// the rollover copies are made by the training encode (static scenes); the DeltaNetwork reads the whole batch first
+		if (use_delta) launch_rollover(s, batch, st.p, coords_c.p, dL_dout.p);
+		const EncodeRollover ro{&st.p->compacted_counter, batch, dL_dout.p};
 		// the canonical backward writes every gradient entry (weight tiles and variance by k_wgrad_reduce, every grid
 		// entry by k_scatter_accum, zeros with no samples); the global-movement phase skips it: zero the buffer there
 		if (!(!dyn || train_canonical)) HIP_CHECK(hipMemsetAsync(grads.p, 0, (size_t)lay.P * 4, s));
@@ -1119,7 +1135,7 @@ struct NeusTestbed {
 			net_backward(&st.p->compacted_counter, &st.p->n_train, batch, coords_cdef.p, valid, dL_dout.p, grads.p, s, true, train_canonical);
 			tbuf.dpos = nullptr;
 		} else {
-			net_backward(&st.p->compacted_counter, &st.p->n_train, batch, coords_c.p, valid, dL_dout.p, grads.p, s, true, train_canonical);
+			net_backward(&st.p->compacted_counter, &st.p->n_train, batch, coords_c.p, valid, dL_dout.p, grads.p, s, true, train_canonical, &ro);
 		}
 		// DeltaNetwork gradient partial sums (the first half of its backward; the Adam step follows the exchange)
 		if (use_delta) launch_delta_grad(s, &st.p->n_train, batch, coords_c.p, COORD_W, dpos.p, delta.p, delta_partial.p);
@@ -1149,11 +1165,14 @@ struct NeusTestbed {
 			HIP_CHECK(hipMemcpyAsync(pinned + 64, st.p, sizeof(StepState), hipMemcpyDeviceToHost, s));
 			loss_pending = true;
 		}
-		launch_step_counters(s, st.p, batch, max_samples, world, cfg.fixed_rays_per_batch);
+		// the step-end counters ride on the Adam launch when the canonical optimizer steps (k_step_counters otherwise)
+		const StepCounterArgs sca{st.p, batch, max_samples, world, cfg.fixed_rays_per_batch};
+		const bool canon_opt = !dyn || train_canonical;
+		if (!canon_opt) launch_step_counters(s, st.p, batch, max_samples, world, cfg.fixed_rays_per_batch);
 		rng.advance();
 		mark(9);
 		// ---- optimizers (testbed_nerf.cu:3503-3508): the canonical trainer, the global-move trainer
-		if (!dyn || train_canonical) optimizer_step(grads.p);
+		if (canon_opt) optimizer_step(grads.p, &sca);
 		if (use_delta) {
 			// ExponentialDecay of the globalmove optimizer (exponential_decay.h:61-80), its own step count
 			if (delta_step == 0) delta_lr_factor = 1.f;
@@ -1716,6 +1735,7 @@ int neus_debug_march_profile(NeusTestbed* tb, unsigned long long* out, uint32_t 
 		HIP_CHECK(hipMemsetAsync(buf.p, 0, (size_t)waves * 64, s));
 		MarchWork mw = t.mwork;
 		mw.prof = buf.p;
+		if (const char* e = std::getenv("NEUS_MARCH_DBG")) mw.dbg = (uint32_t)std::strtoul(e, nullptr, 10);
 		launch_march_count(s, MAX_RAYS, t.max_samples, t.st.p, DPInfo{t.rank, t.world}, t.ds, t.bitfield.p, t.bf_lin.p, t.rng.state, t.rng.inc,
 		                   t.rays.p, t.startt.p, t.nreq.p, mw, nullptr, 0, t.ray_cull ? t.occ_bbox.p : nullptr);
 		HIP_CHECK(hipStreamSynchronize(s));

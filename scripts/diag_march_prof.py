@@ -30,7 +30,8 @@ q = p[act]
 t0 = q[:, 0].min()
 st, en = (q[:, 0] - t0) / 100.0, (q[:, 5] - t0) / 100.0  # us
 ph = np.diff(q[:, :6], axis=1) / 100.0
-samples, redo = q[:, 6], q[:, 7]
+samples, redo = q[:, 6], q[:, 7] & 0xff
+ev_max, ev_sum = q[:, 7] >> 32, (q[:, 7] >> 8) & 0xffffff
 print(f"waves with stamps {act.sum()} of {nw}; kernel span {en.max():.1f} us (first start .. last end)")
 print(f"wave start: p50 {np.median(st):.1f} p99 {np.percentile(st, 99):.1f} max {st.max():.1f} us")
 print(f"wave duration: mean {(en - st).mean():.1f} p50 {np.median(en - st):.1f} p99 {np.percentile(en - st, 99):.1f} max {(en - st).max():.1f} us")
@@ -39,11 +40,13 @@ for k, nm in enumerate(names):
     print(f"  {nm:14s} mean {ph[:, k].mean():7.2f} p50 {np.median(ph[:, k]):7.2f} p99 {np.percentile(ph[:, k], 99):7.2f} max {ph[:, k].max():7.2f} us")
 busy = samples > 0
 print(f"waves with samples {busy.sum()}; samples per such wave mean {samples[busy].mean():.0f} max {samples.max()}; redo rounds mean {redo.mean():.2f} max {redo.max()}")
+print(f"segment events per wave: lane max mean {ev_max[busy].mean():.1f} p99 {np.percentile(ev_max[busy], 99):.0f}; lane mean {(ev_sum[busy] / 64).mean():.1f}; "
+      f"segment-march us per max-lane event {np.median(ph[busy, 1] / np.maximum(ev_max[busy], 1)):.3f}")
 crit = np.argmax(en)
-print(f"critical wave: start {st[crit]:.1f} dur {en[crit] - st[crit]:.1f} phases {np.round(ph[crit], 1).tolist()} samples {samples[crit]} redo {redo[crit]}")
+print(f"critical wave: start {st[crit]:.1f} dur {en[crit] - st[crit]:.1f} phases {np.round(ph[crit], 1).tolist()} samples {samples[crit]} redo {redo[crit]} events max {ev_max[crit]}")
 order = np.argsort(-(en - st))[:10]
 for i in order:
-    print(f"   long wave: start {st[i]:7.1f} dur {en[i] - st[i]:7.1f} phases {np.round(ph[i], 1).tolist()} samples {samples[i]} redo {redo[i]}")
+    print(f"   long wave: start {st[i]:7.1f} dur {en[i] - st[i]:7.1f} phases {np.round(ph[i], 1).tolist()} samples {samples[i]} redo {redo[i]} events max {ev_max[i]} sum {ev_sum[i]}")
 # concurrency over time: waves running at t
 ts = np.linspace(0, en.max(), 20)
 print("running waves over time:", [int(((st <= t) & (en > t)).sum()) for t in ts])
