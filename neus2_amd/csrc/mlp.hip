@@ -390,9 +390,11 @@ __device__ __forceinline__ float slot_dydx(int q, int h, int d, const float dy[]
 
 // fp16 B fragment (k-step s) of an accumulator tile, optionally through ReLU: (half)max(acc, 0) is the
 // reference's fp16 storage of the post-activation value. The ReLU runs after the packed conversion as a packed
-// fp16 max with 0 (rounding is monotone, so the values are those of rounding max(acc, 0); a NaN gives 0 as the
-// reference's `x > 0 ? x : 0`): one op per 2 values instead of an fp32 max per value plus the IEEE-mode
-// quieting max the compiler puts before it (MFMA results are not known canonical; conversion results are).
+// fp16 max with 0 (rounding is monotone, so the values are those of rounding max(acc, 0)): one op per 2 values
+// instead of an fp32 max per value plus the IEEE-mode quieting max the compiler puts before it (MFMA results are
+// not known canonical; conversion results are). Non-finite inputs differ from the reference: its ReLU is x * (x > 0)
+// (my_tcnn common_device.h:74, warp_activation), NaN for NaN and -inf, while the max gives 0 for both; a diverged
+// run is still caught by the non-finite loss check, which sees the other non-finite outputs.
 typedef _Float16 hh2v __attribute__((ext_vector_type(2)));
 template <bool RELU>
 __device__ __forceinline__ h8 frag(const f16v& acc, int s) {

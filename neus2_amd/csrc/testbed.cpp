@@ -232,6 +232,7 @@ struct NeusTestbed {
 	Dev<uint16_t> sc_rtab;
 	std::vector<uint32_t> sc_jobs2_before;  // [L + 1] region-scatter jobs of the levels below l
 	uint32_t sc_zero_from_e = 0;            // region scatter: grid entries from here on hold zero gradients
+	bool scatter_noskip = false;            // NEUS_SCATTER_NOSKIP=1: zero the grid gradient every step (A/B reference)
 	Dev<h2> sc_rec_g;
 	Dev<uint16_t> sc_rec_i;
 	// restructured loss scratch (kernels.h LossWork)
@@ -366,6 +367,7 @@ struct NeusTestbed {
 		occ_bbox.alloc(occ_bbox_scratch_floats());
 		launch_occ_bbox(stream, bitfield.p, occ_bbox.p);
 		{ const char* e = std::getenv("NEUS_RAY_CULL"); ray_cull = !(e && e[0] == '0'); }
+		{ const char* e = std::getenv("NEUS_SCATTER_NOSKIP"); scatter_noskip = e && e[0] == '1'; }
 		grid_mean.alloc(4); grid_partial.alloc(GRID3 / 1024);
 		HIP_CHECK(hipMemset(grid_mean.p, 0, 16));
 	}
@@ -751,6 +753,11 @@ struct NeusTestbed {
 	ScatterWork scatter_work_for(float* g_grid, uint32_t valid, hipStream_t s) {
 		if (g_grid != grads.p + lay.grid_off || sc_jobs_before.empty()) return swork;
 		const uint32_t L = gl.n_levels, n_entries = gl.offset[L];
+		if (scatter_noskip) {  // A/B reference: the whole grid gradient zeroed before every scatter
+			HIP_CHECK(hipMemsetAsync(g_grid, 0, (size_t)n_entries * 2 * sizeof(float), s));
+			sc_zero_from = swork.n_buckets; sc_zero_from_e = n_entries;
+			return swork;
+		}
 		if (swork.mode == 2) {
 			// the accumulation writes exactly the entries of the levels up to the valid one
 			const uint32_t lv = std::min(valid + 1, L), e_end = gl.offset[lv];

@@ -96,3 +96,41 @@ def test_scatter_paths_bitwise_equal(scene, torch_cuda):
     bin2.train_steps(40)
     np.testing.assert_array_equal(seg2.get_params().view(np.uint32), bin2.get_params().view(np.uint32))
     np.testing.assert_array_equal(seg2.get_gradients().view(np.uint32), bin2.get_gradients().view(np.uint32))
+
+
+def test_valid_level_drop_matches_zeroed_reference(scene, torch_cuda, tmp_path):
+    """The scatter writes only the grid levels up to the progressive valid level and zeroes the rest of the gradient
+    once when the valid level drops (scatter_work_for): train past several level increments, reload a snapshot of an
+    early step (the valid level falls back), train on, and compare parameters and gradients bitwise with a testbed that
+    zeroes the whole grid gradient before every scatter (NEUS_SCATTER_NOSKIP=1)."""
+    from neus2_amd import pyngp
+    out = []
+    for noskip in (False, True):
+        old = os.environ.get("NEUS_SCATTER_NOSKIP")
+        if noskip:
+            os.environ["NEUS_SCATTER_NOSKIP"] = "1"
+        else:
+            os.environ.pop("NEUS_SCATTER_NOSKIP", None)
+        try:
+            tb = pyngp.Testbed(pyngp.TestbedMode.Nerf)
+            tb.set_dataset(scene["images"], scene["focal"], scene["principal"], scene["xforms"], 1)
+            tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=4096)
+        finally:
+            if old is None:
+                os.environ.pop("NEUS_SCATTER_NOSKIP", None)
+            else:
+                os.environ["NEUS_SCATTER_NOSKIP"] = old
+        tb.train_steps(20)
+        snap = str(tmp_path / f"early_{int(noskip)}.msgpack")
+        tb.save_snapshot(snap, include_optimizer_state=True)
+        v_early = tb.stats()["valid_level"]
+        tb.train_steps(400)
+        v_late = tb.stats()["valid_level"]
+        assert v_late > v_early
+        tb.load_snapshot(snap)
+        tb.train_steps(15)
+        assert tb.stats()["valid_level"] < v_late
+        out.append((tb.get_params(), tb.get_gradients()))
+    (p0, g0), (p1, g1) = out
+    np.testing.assert_array_equal(p0.view(np.uint32), p1.view(np.uint32))
+    np.testing.assert_array_equal(g0.view(np.uint32), g1.view(np.uint32))
