@@ -455,10 +455,11 @@ __global__ void __launch_bounds__(BS) k_scatter_bin_r(const uint32_t* __restrict
 	const float4 vv = v4[ic];
 	const uint32_t n_lv = min(gl.n_levels, valid_level + 1);
 	// the level's two per-sample operands, loaded one level ahead (the level loop's barriers would otherwise expose
-	// their latency once per level)
-	uint32_t a_cur = dLdenc[ic], g_cur = g[ic];
-	for (uint32_t l = 0; l < n_lv; ++l) {
-		const uint32_t ln = min(l + 1, n_lv - 1);
+	// their latency once per level); workgroup (chunk, y) bins levels y, y + gridDim.y, ... of its chunk
+	const uint32_t lstep = gridDim.y;
+	uint32_t a_cur = dLdenc[(size_t)blockIdx.y * ld + ic], g_cur = g[(size_t)blockIdx.y * ld + ic];
+	for (uint32_t l = blockIdx.y; l < n_lv; l += lstep) {
+		const uint32_t ln = min(l + lstep, n_lv - 1);
 		const uint32_t a_next = dLdenc[(size_t)ln * ld + ic], g_next = g[(size_t)ln * ld + ic];
 		const uint32_t off = gl.offset[l], size = gl.offset[l + 1] - off;
 		const uint32_t nlb = (size + SB_SIZE - 1) >> SB_SHIFT;
@@ -811,15 +812,19 @@ void launch_grid_scatter(hipStream_t s, const uint32_t* n_ptr, uint32_t n_fixed,
                          const ScatterWork& w, void* scan_tmp, size_t scan_tmp_bytes) {
 	if (w.mode == 2) {
 		// the grid spans the workspace's sample capacity (w.n_chunks x w.chunk >= n)
+		// one workgroup per (chunk, level) by default: ~14x the workgroups of a level loop, so the phases (corner
+		// contributions, bucket count, scan, stage, region write) of different workgroups overlap on a CU
+		const uint32_t n_lv = std::min(gl.n_levels, valid_level + 1);
+		const dim3 grid(w.n_chunks, w.level_groups ? std::min(w.level_groups, n_lv) : n_lv);
 		if (w.chunk == 1024)
-			k_scatter_bin_r<1024><<<w.n_chunks, 1024, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, (const uint32_t*)dLdenc,
-			                                                  (const uint32_t*)g, v, w);
+			k_scatter_bin_r<1024><<<grid, 1024, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, (const uint32_t*)dLdenc,
+			                                            (const uint32_t*)g, v, w);
 		else if (w.chunk == 256)
-			k_scatter_bin_r<256><<<w.n_chunks, 256, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, (const uint32_t*)dLdenc,
-			                                                (const uint32_t*)g, v, w);
+			k_scatter_bin_r<256><<<grid, 256, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, (const uint32_t*)dLdenc,
+			                                          (const uint32_t*)g, v, w);
 		else
-			k_scatter_bin_r<512><<<w.n_chunks, 512, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, (const uint32_t*)dLdenc,
-			                                                (const uint32_t*)g, v, w);
+			k_scatter_bin_r<512><<<grid, 512, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, (const uint32_t*)dLdenc,
+			                                          (const uint32_t*)g, v, w);
 		const uint32_t nj = std::min(w.n_jobs2, w.jobs2_before[std::min(valid_level + 1, gl.n_levels)]);
 		if (nj) k_scatter_accum_r<<<nj, 256, 0, s>>>(w, gl, grads, w.chunk * 8);
 		return;

@@ -113,6 +113,7 @@ struct ScatterWork {
 	const uint4* jobs2;
 	uint32_t n_jobs2;
 	uint32_t jobs2_before[17];  // jobs of the levels below l (l <= 16): the launch takes those up to the valid level
+	uint32_t level_groups;      // mode 2: workgroups per sample chunk, each binning levels y, y + groups, ... (0: one per level)
 };
 
 // accumulation workgroups of the scatter (flattened uint4 {bucket, part, parts, split slot}); n_split = split buckets

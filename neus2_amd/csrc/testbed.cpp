@@ -204,6 +204,7 @@ struct NeusTestbed {
 	Dev<uint8_t> bitfield;
 	Dev<uint32_t> bf_lin;   // mip-0 occupancy in (x, y, z/32) word order for the constant-step march
 	Dev<float> occ_bbox;    // world box of the occupied cells of every mip (+ stage-1 scratch): the ray generation's cull
+	Dev<uint32_t> dbg_enc;  // debug timing only (neus_debug_time_kernel 11): [L][16 Nc] encodings of the inference samples
 	bool ray_cull = true;   // NEUS_RAY_CULL=0: march every ray (A/B reference)
 	Dev<PcgJump> pcg_tab;   // pcg32 jump-ahead table (common.h PcgJumpTable)
 	uint32_t density_grid_ema_step = 0;
@@ -517,6 +518,9 @@ struct NeusTestbed {
 			const char* e = std::getenv("NEUS_SCATTER");
 			swork.mode = !e ? 2u : std::string(e) == "binned" ? 1u : std::string(e) == "wide" ? 0u : 2u;
 			if (swork.mode != 2 && swork.chunk == 256) { swork.chunk = 512; swork.n_chunks = (batch + 511) / 512; }  // wide binning: 512 / 1024
+			// NEUS_SCATTER_LG=k: k workgroups per chunk each binning every k-th level (default: one per level)
+			const char* lg = std::getenv("NEUS_SCATTER_LG");
+			swork.level_groups = lg ? (uint32_t)std::max(0, std::atoi(lg)) : 0u;
 		}
 		swork.n_buckets = scatter_n_buckets(gl);
 		if (swork.n_buckets > SB_MAX_BUCKETS) throw std::runtime_error("hash grid too large for the scatter buckets");
@@ -1709,6 +1713,14 @@ static void time_kernel_impl(NeusTestbed* tb, int kernel, int variant, int iters
 				t.sc_zero_from_e = t.gl.offset[t.gl.n_levels];
 				break;
 			case 8: t.encode(nullptr, t.batch, t.batch, t.batch, t.coords_c.p, COORD_W, valid, true, s); break;
+			case 11: {
+				// level-partitioned gather experiment: the level-major encode (enc only, no dy/dx) over the
+				// inference's pre-compaction samples; variant = workgroups per level (0: 2048)
+				if (!t.dbg_enc.p) t.dbg_enc.alloc((size_t)t.lay.L * t.max_samples);
+				launch_grid_encode(s, &t.st.p->n_kept, 0, t.max_samples, t.coords.p, COORD_W, t.gl, valid, t.params_h.p + t.lay.grid_off,
+				                   t.dbg_enc.p, nullptr, variant > 0 && variant != 99 ? (uint32_t)variant : 2048u, nullptr);
+				break;
+			}
 			default: throw std::runtime_error("unknown kernel id");
 			}
 		}
