@@ -109,11 +109,12 @@ def kernel_table(levels):
         "march": (0, 40, 0),
         "march_write": (1, 28, 0),
         "inference": (3, 28 + g + 32, 28672),
-        "loss_alpha": (4, 60, 0),
         "train_encode": (8, 28 + g, 0),
         "mlp_train_rgb": (9, 32, 43008),
         "mlp_train_density": (10, 32, 10240),
         "grid_scatter": (7, 2 * g, 0),
+        # Adam + EMA over every parameter: 48 B; the replay advances the optimizer (after the timed steps)
+        "adam_ema": (12, 48, 0),
     }
 
 

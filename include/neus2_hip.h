@@ -279,15 +279,16 @@ int neus_testbed_set_progressive_inference(NeusTestbed* tb, int mode, const uint
  * the march, samples composited before transmittance < 1e-4, and numsteps = (compacted count, base). */
 int neus_testbed_ray_counts(NeusTestbed* tb, uint32_t n, uint32_t* nreq, uint32_t* ccount, uint32_t* numsteps /* 2n */);
 /* Development timing hook: regenerates the last step's samples and times `iters` launches of one
- * kernel (0 march count, 1 march write, 2 loss transmittance scan, 3 fused inference, 4 loss alpha)
- * in implementation `variant` (0 = production); mean ms per launch. */
+ * kernel (the ids of neus_testbed_time_kernel; 11 the level-major encode alone over the pre-compaction samples,
+ * variant = workgroups per level; 12 the Adam / EMA pass, which advances the optimizer) in implementation
+ * `variant` (0 = production; 99 = no re-preparation); median ms per launch. */
 int neus_debug_time_kernel(NeusTestbed* tb, int kernel, int variant, int iters, float* ms_out);
 /* Median launch duration (hipEvents on the testbed stream between `iters` back-to-back launches) of one hot-path
  * kernel replayed on the current training state, and the work units of one launch.
  * kernel: 0 ray generation + march (units: ray slots), 1 coordinate write, 2 loss transmittance scan,
  * 3 fused inference, 4 loss alpha (units: pre-compaction samples), 5 training MLP, 6 weight gradients,
  * 7 grid-gradient scatter, 8 training-batch grid encode, 9 / 10 the colour / density training-MLP kernel alone
- * (units: compacted samples). */
+ * (units: compacted samples), 12 the Adam / EMA pass (units: parameters; the replays advance the optimizer). */
 int neus_testbed_time_kernel(NeusTestbed* tb, int kernel, int iters, float* ms_out, uint32_t* units_out);
 // Development statistic of the last step's march: per ray {march_step calls, skip-loop additions,
 // samples} (3 x u32 per ray, n rays; cone_angle 0 only).
@@ -297,6 +298,9 @@ int neus_debug_march_stats(NeusTestbed* tb, uint32_t n, uint32_t* out);
  * samples counted, records written, then the wave's samples and its re-march rounds; pass 1 overwrites its waves'
  * stamps only where it marches. */
 int neus_debug_march_profile(NeusTestbed* tb, unsigned long long* out, uint32_t max_waves, uint32_t* n_waves);
+/* Development statistic of the last grid-gradient scatter (region mode): records written per level (out[L], after the
+ * wave run merge) and the largest per-(level, block) region. */
+int neus_debug_scatter_stats(NeusTestbed* tb, uint64_t* records_per_level, uint32_t* max_region);
 /* Development check of the single-pass exclusive scan the step's compactions use (scan.hip): device buffers in / out
  * of n u32 on `hip_stream`, `reps` launches on one fresh state (the epoch re-arm), synchronous; failures = bounded-wait
  * give-ups (0 expected). */

@@ -198,5 +198,42 @@ __device__ __forceinline__ void step_counters_update(StepState* st, uint32_t tar
 	st->rays_per_batch = min(r, 1u << 18);
 }
 
+// ---------------------------------------------------------------- wave64 cross-lane steps on DPP (gfx9 family)
+// Lane moves through the VALU's data-parallel-primitive operand modifier instead of ds_bpermute (an LDS-pipe op
+// with LDS latency per step of a scan chain). wave_shr:1 / wave_shl:1 shift across the whole wave; row_shr:n
+// within rows of 16 lanes; row_bcast:15 / :31 hand a row's last lane to the next row / to rows 2 and 3 (the wave64
+// scan pattern). A lane whose source is out of range, or whose row is masked off, keeps `old`. Every lane of the
+// wave must be active.
+constexpr int DPP_ROW_SHR = 0x110, DPP_WAVE_SHL1 = 0x130, DPP_WAVE_SHR1 = 0x138, DPP_BCAST15 = 0x142, DPP_BCAST31 = 0x143;
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t old, uint32_t x) {
+	return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)x, CTRL, ROW_MASK, 0xf, false);
+}
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ float dpp_f32(float old, float x) {
+	return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old), __builtin_bit_cast(int, x), CTRL, ROW_MASK, 0xf, false));
+}
+// inclusive prefix sum over the wave's 64 lanes (u32, exact)
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+	x += dpp_u32<DPP_ROW_SHR + 1>(0u, x);
+	x += dpp_u32<DPP_ROW_SHR + 2>(0u, x);
+	x += dpp_u32<DPP_ROW_SHR + 4>(0u, x);
+	x += dpp_u32<DPP_ROW_SHR + 8>(0u, x);
+	x += dpp_u32<DPP_BCAST15, 0xa>(0u, x);
+	x += dpp_u32<DPP_BCAST31, 0xc>(0u, x);
+	return x;
+}
+__device__ __forceinline__ uint32_t wave_lane_value(uint32_t x, int lane) { return (uint32_t)__builtin_amdgcn_readlane((int)x, lane); }
+// wave-wide sum / max (u32), the same value on every lane
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) { return wave_lane_value(wave_incl_sum(x), 63); }
+__device__ __forceinline__ uint32_t wave_max(uint32_t x) {
+	x = max(x, dpp_u32<DPP_ROW_SHR + 1>(0u, x));
+	x = max(x, dpp_u32<DPP_ROW_SHR + 2>(0u, x));
+	x = max(x, dpp_u32<DPP_ROW_SHR + 4>(0u, x));
+	x = max(x, dpp_u32<DPP_ROW_SHR + 8>(0u, x));
+	x = max(x, dpp_u32<DPP_BCAST15, 0xa>(0u, x));
+	x = max(x, dpp_u32<DPP_BCAST31, 0xc>(0u, x));
+	return wave_lane_value(x, 63);
+}
 
 } // namespace neus

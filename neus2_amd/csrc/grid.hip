@@ -79,24 +79,34 @@ __device__ __forceinline__ void atomic_add_f32(float* p, float v) {
 // carries the run's sum (the last lane of the run). All 64 lanes must call this; `ok` masks lanes
 // without a sample.
 __device__ __forceinline__ bool wave_run_sum(uint32_t e, float& a0, float& a1, bool ok) {
-	const int lane = threadIdx.x & 63;
+	const uint32_t lane = threadIdx.x & 63;
 	if (!ok) { e = 0xffffffffu; a0 = a1 = 0.f; }
-	const uint32_t e_prev = __shfl_up(e, 1);
-	const bool head = lane == 0 || e_prev != e;
-	if (__ballot(!head) != 0) {  // at least one run longer than one lane
-		int rs = head ? lane : 0;
-#pragma unroll
-		for (int off = 1; off < 64; off <<= 1) { const int t = __shfl_up(rs, off); if (lane >= off) rs = max(rs, t); }
-#pragma unroll
-		for (int off = 1; off < 64; off <<= 1) {
-			const float t0 = __shfl_up(a0, off), t1 = __shfl_up(a1, off);
-			if (lane - off >= rs) { a0 += t0; a1 += t1; }
-		}
-		const uint32_t e_next = __shfl_down(e, 1);
-		const bool tail = lane == 63 || e_next != e;
-		return ok && tail;
+	const uint32_t e_prev = dpp_u32<DPP_WAVE_SHR1>(~e, e);  // lane 0 keeps ~e: a head
+	const uint64_t heads = __ballot(e_prev != e);
+	if (heads == ~0ull) return ok;  // no run longer than one lane
+	// run start: the highest head at or below this lane (lane 0 is always one)
+	const uint32_t rs = 63u - (uint32_t)__clzll(heads & ((2ull << lane) - 1ull));
+	// segmented sums: Kogge-Stone within rows of 16 lanes, then across rows (a run reaching back past its row's
+	// start); a step no lane of the wave needs is skipped (fine levels: runs of 2-3 lanes)
+	const uint32_t r0 = lane & ~15u;
+#define NEUS_SEG_STEP(CTRL, MASK, COND)                                                                  \
+	{                                                                                                    \
+		const bool c = (COND);                                                                           \
+		if (__ballot(c)) {                                                                               \
+			const float t0 = dpp_f32<CTRL, MASK>(0.f, a0), t1 = dpp_f32<CTRL, MASK>(0.f, a1);             \
+			a0 = c ? a0 + t0 : a0;                                                                       \
+			a1 = c ? a1 + t1 : a1;                                                                       \
+		}                                                                                                \
 	}
-	return ok;
+	NEUS_SEG_STEP(DPP_ROW_SHR + 1, 0xf, lane - r0 >= 1u && lane - 1u >= rs)
+	NEUS_SEG_STEP(DPP_ROW_SHR + 2, 0xf, lane - r0 >= 2u && lane - 2u >= rs)
+	NEUS_SEG_STEP(DPP_ROW_SHR + 4, 0xf, lane - r0 >= 4u && lane - 4u >= rs)
+	NEUS_SEG_STEP(DPP_ROW_SHR + 8, 0xf, lane - r0 >= 8u && lane - 8u >= rs)
+	NEUS_SEG_STEP(DPP_BCAST15, 0xa, (r0 == 16u || r0 == 48u) && rs < r0)  // rows 1, 3 += the previous row's last lane
+	NEUS_SEG_STEP(DPP_BCAST31, 0xc, lane >= 32u && rs < 32u)              // rows 2, 3 += lane 31
+#undef NEUS_SEG_STEP
+	const bool tail = lane == 63u || ((heads >> (lane + 1u)) & 1ull);
+	return ok && tail;
 }
 
 // Slot of this lane's record in its bucket's per-block counter, with one LDS atomic per distinct
@@ -107,11 +117,11 @@ __device__ __forceinline__ uint32_t wave_bucket_slot(uint32_t* hist, uint32_t bk
 	uint32_t res = 0;
 	while (todo) {
 		const int leader = __ffsll((unsigned long long)todo) - 1;
-		const uint32_t lb = (uint32_t)__shfl((int)bkt, leader);
+		const uint32_t lb = wave_lane_value(bkt, leader);
 		const uint64_t m = __ballot(active && bkt == lb);
 		uint32_t base = 0;
 		if ((int)lane == leader) base = atomicAdd(&hist[lb], (uint32_t)__popcll(m));
-		base = (uint32_t)__shfl((int)base, leader);
+		base = wave_lane_value(base, leader);
 		if (active && bkt == lb) res = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
 		todo &= ~m;
 	}
@@ -277,11 +287,9 @@ __global__ void __launch_bounds__(256) k_scatter_bin(const uint32_t* __restrict_
 		for (uint32_t k0 = 0; k0 < nlb; k0 += 64) {
 			const uint32_t k = k0 + lane;
 			const uint32_t v = k < nlb ? cnt[k] : 0u;
-			uint32_t incl = v;
-#pragma unroll
-			for (int d = 1; d < 64; d <<= 1) { const uint32_t t = (uint32_t)__shfl_up((int)incl, d); if ((int)lane >= d) incl += t; }
+			const uint32_t incl = wave_incl_sum(v);
 			if (k < nlb) { bas[k] = v ? atomicAdd(&cursor[k], v) : 0u; loff[k] = total + incl - v; cnt[k] = 0; }
-			total += (uint32_t)__shfl((int)incl, 63);
+			total += wave_lane_value(incl, 63);
 		}
 		__syncthreads();  // offsets visible, counters cleared
 #pragma unroll
@@ -396,11 +404,9 @@ __global__ void __launch_bounds__(BS) k_scatter_bin_w(const uint32_t* __restrict
 			for (uint32_t k0 = 0; k0 < nlb; k0 += 64) {
 				const uint32_t k = k0 + lane;
 				const uint32_t v = k < nlb ? cnt[k] : 0u;
-				uint32_t incl = v;
-#pragma unroll
-				for (int d = 1; d < 64; d <<= 1) { const uint32_t t = (uint32_t)__shfl_up((int)incl, d); if ((int)lane >= d) incl += t; }
+				const uint32_t incl = wave_incl_sum(v);
 				if (k < nlb) base[k] = total + incl - v;
-				total += (uint32_t)__shfl((int)incl, 63);
+				total += wave_lane_value(incl, 63);
 			}
 			if (lane == 0) base[nlb] = total;
 		}
@@ -488,11 +494,9 @@ __global__ void __launch_bounds__(BS) k_scatter_bin_r(const uint32_t* __restrict
 			for (uint32_t k0 = 0; k0 < nlb; k0 += 64) {
 				const uint32_t k = k0 + lane;
 				const uint32_t v = k < nlb ? cnt[k] : 0u;
-				uint32_t incl = v;
-#pragma unroll
-				for (int d = 1; d < 64; d <<= 1) { const uint32_t t = (uint32_t)__shfl_up((int)incl, d); if ((int)lane >= d) incl += t; }
+				const uint32_t incl = wave_incl_sum(v);
 				if (k < nlb) base[k] = total + incl - v;
-				total += (uint32_t)__shfl((int)incl, 63);
+				total += wave_lane_value(incl, 63);
 			}
 			if (lane == 0) base[nlb] = total;
 		}
@@ -525,10 +529,15 @@ __global__ void __launch_bounds__(BS) k_scatter_bin_r(const uint32_t* __restrict
 // lengths, a wave scan, and the concatenated segments read lane-contiguously, SC_U batches of 64 records in flight
 // (the owner of each record by binary search over the 64 segment starts in LDS).
 constexpr int SC_U = 8;
-__global__ void __launch_bounds__(256) k_scatter_accum_r(ScatterWork w, const GridLevels gl, float* __restrict__ grads, uint32_t bs8) {
+constexpr int SC_WAVES = 4;  // (8 waves per workgroup measured slower: 93 -> 103 us at the bench state)
+__global__ void __launch_bounds__(64 * SC_WAVES) k_scatter_accum_r(ScatterWork w, const GridLevels gl, float* __restrict__ grads, uint32_t bs8,
+                                                                   uint32_t n_jobs) {
 	__shared__ unsigned long long acc[2 * SB_SIZE];
-	__shared__ uint32_t s_pre[4][65], s_src[4][64];
+	__shared__ uint32_t s_pre[SC_WAVES][65], s_src[SC_WAVES][64];
 	__shared__ uint32_t s_last;
+	// (jobs in list order: an XCD-contiguous mapping - each XCD taking an eighth of the list, so adjacent buckets'
+	// segments that share lines meet in one L2 - measured 93 -> 169 us at the bench state)
+	(void)n_jobs;
 	const uint4 job = w.jobs2[blockIdx.x];
 	const uint32_t l = job.x, kb = job.y, part = job.z & 0xffffu, parts = job.z >> 16, slot = job.w;
 	const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -541,18 +550,16 @@ __global__ void __launch_bounds__(256) k_scatter_accum_r(ScatterWork w, const Gr
 	const uint32_t b0 = (uint32_t)((uint64_t)nb * part / parts), b1 = (uint32_t)((uint64_t)nb * (part + 1) / parts);
 	uint32_t* pre = s_pre[wv];
 	uint32_t* src = s_src[wv];
-	for (uint32_t it = 0; b0 + wv + 4 * 64 * it < b1; ++it) {
-		const uint32_t b = b0 + wv + 4 * (64 * it + lane);
+	for (uint32_t it = 0; b0 + wv + SC_WAVES * 64 * it < b1; ++it) {
+		const uint32_t b = b0 + wv + SC_WAVES * (64 * it + lane);
 		uint32_t s0 = 0, len = 0;
 		if (b < b1) {
 			const uint16_t* tab = w.rtab + ((size_t)l * nb + b) * RT_STRIDE;
 			s0 = tab[kb];
 			len = (uint32_t)tab[kb + 1] - s0;
 		}
-		uint32_t incl = len;
-#pragma unroll
-		for (int d = 1; d < 64; d <<= 1) { const uint32_t t = (uint32_t)__shfl_up((int)incl, d); if ((int)lane >= d) incl += t; }
-		const uint32_t total = (uint32_t)__shfl((int)incl, 63);
+		const uint32_t incl = wave_incl_sum(len);
+		const uint32_t total = wave_lane_value(incl, 63);
 		__builtin_amdgcn_wave_barrier();
 		pre[lane] = incl - len;
 		src[lane] = (uint32_t)(((size_t)l * nb + (b < b1 ? b : 0u)) * bs8) + s0;  // u32: < 2^32 records
@@ -826,7 +833,7 @@ void launch_grid_scatter(hipStream_t s, const uint32_t* n_ptr, uint32_t n_fixed,
 			k_scatter_bin_r<512><<<grid, 512, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, (const uint32_t*)dLdenc,
 			                                          (const uint32_t*)g, v, w);
 		const uint32_t nj = std::min(w.n_jobs2, w.jobs2_before[std::min(valid_level + 1, gl.n_levels)]);
-		if (nj) k_scatter_accum_r<<<nj, 256, 0, s>>>(w, gl, grads, w.chunk * 8);
+		if (nj) k_scatter_accum_r<<<nj, 64 * SC_WAVES, 0, s>>>(w, gl, grads, w.chunk * 8, nj);
 		return;
 	}
 	if (w.mode == 0) {

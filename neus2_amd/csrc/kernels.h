@@ -137,12 +137,22 @@ struct LossWork {
 	float4* rgr;            // [rays] dL/drgb_ray (Huber'), gws * (1 - weight_sum)
 };
 
+// Adam's bias-correction factors by per-parameter step: tab[k] = sqrtf(1 - powf(beta2, k)) and
+// tab[ADAM_BIAS_TAB + k] = 1 - powf(beta1, k) for k < ADAM_BIAS_TAB, evaluated once by k_adam_bias_table with the
+// expressions of adam.h:137 (the two powf per parameter were ~3/4 of the Adam pass's VALU work); past the table both
+// are exactly 1.0f when `bias_converged` (beta^k below 2^-30 there), so lr = (lr * 1) / 1 = lr.
+constexpr uint32_t ADAM_BIAS_TAB = 4096;
 struct AdamParams {
 	uint32_t n, n_matrix;
 	float loss_scale, lr, beta1, beta2, eps, l2_reg;
 	float ema_decay, ema_debias_old, ema_debias_new;
 	uint32_t optimize_matrix, optimize_non_matrix;
+	const float* bias_tab;    // [2 * ADAM_BIAS_TAB] or null (powf per parameter)
+	uint32_t bias_converged;
+	float inv_loss_scale;     // 1 / loss_scale when that is a power of two (the product is then the exact quotient)
+	uint32_t pow2_scale;
 };
+void launch_adam_bias_table(hipStream_t s, float beta1, float beta2, float* tab);
 
 // The Adam launch's two riders (each optional): the step-end counters (k_step_counters' work, done by thread 0 of block
 // 0) and the transposed / permuted fp16 copies of the MLP matrices (prepare_weights), written by the threads that

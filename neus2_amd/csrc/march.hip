@@ -444,8 +444,7 @@ __global__ void __launch_bounds__(256) k_march(uint32_t cap_rays, uint32_t pass,
 		first = false;
 	}
 	if (pass == 0) {  // the pass's requested samples (one atomic per wave)
-#pragma unroll
-		for (int off = 32; off > 0; off >>= 1) total += (uint32_t)__shfl_xor((int)total, off);
+		total = wave_sum(total);
 		if (lane == 0 && total) atomicAdd(&st->march_total, total);
 	}
 }
@@ -512,11 +511,7 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_march_scan(uint32_t cap_rays, 
 	}
 	if (r0.list) scan_store16(r0.c0, i0, cap_rays, true, co);
 	// the tile's kept maxima / count: one atomic each
-#pragma unroll
-	for (int off = 32; off > 0; off >>= 1) {
-		kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, off)); kcnt += (uint32_t)__shfl_xor((int)kcnt, off);
-		kext = max(kext, (uint32_t)__shfl_xor((int)kext, off)); cmax = max(cmax, (uint32_t)__shfl_xor((int)cmax, off));
-	}
+	kmax = wave_max(kmax); kcnt = wave_sum(kcnt); kext = wave_max(kext); cmax = wave_max(cmax);
 	const uint32_t wv = threadIdx.x >> 6;
 	if ((threadIdx.x & 63) == 0) { s_red[0][wv] = kmax; s_red[1][wv] = kcnt; s_red[2][wv] = kext; s_red[3][wv] = cmax; }
 	__syncthreads();
@@ -587,9 +582,7 @@ __global__ void __launch_bounds__(256) k_march_write(uint32_t cap_rays, const St
 			uint32_t v[4], sum = 0;
 #pragma unroll
 			for (int k = 0; k < 4; ++k) { v[k] = s_roff[4 * tid + k]; sum += v[k]; }
-			uint32_t inc = sum;
-#pragma unroll
-			for (int off = 1; off < 64; off <<= 1) { const uint32_t o = (uint32_t)__shfl_up((int)inc, off); if ((int)tid >= off) inc += o; }
+			const uint32_t inc = wave_incl_sum(sum);
 			uint32_t ex = inc - sum;
 #pragma unroll
 			for (int k = 0; k < 4; ++k) { s_roff[4 * tid + k] = ex; ex += v[k]; }
@@ -882,12 +875,15 @@ __global__ void __launch_bounds__(64) k_loss_scan_chunk(uint32_t cap_rays, const
                                                         uint32_t* __restrict__ ccount, float4* __restrict__ racc, float* __restrict__ rT,
                                                         float* __restrict__ rek, uint32_t e0, uint32_t e1, uint32_t e2,
                                                         uint32_t* __restrict__ list, uint32_t* __restrict__ next_counter) {
-	constexpr uint32_t U = 16, PAD = U + 1;
+	// U samples per ray and group: U lanes load U consecutive samples of one ray (64 / U rays per load instruction),
+	// transposed through LDS to one ray per lane. U = 8 (was 16): half the LDS and registers per wave, so twice the
+	// waves per CU hide the per-ray state loads
+	constexpr uint32_t U = 8, PAD = U + 1, RPI = 64 / U;
 	typedef float f4v __attribute__((ext_vector_type(4)));
 	__shared__ f4v s_q[64 * PAD];
 	__shared__ float s_e[64 * PAD];
 	__shared__ uint32_t s_pre[64], s_src[64];
-	const uint32_t lane = threadIdx.x, sub = lane >> 4, el = lane & 15;
+	const uint32_t lane = threadIdx.x, sub = lane / U, el = lane % U;
 	const char* sab = (const char*)sa;
 	const char* ekb = (const char*)ekt;
 	for (uint32_t w0 = blockIdx.x * 64; w0 < cap_rays; w0 += gridDim.x * 64) {
@@ -896,21 +892,22 @@ __global__ void __launch_bounds__(64) k_loss_scan_chunk(uint32_t cap_rays, const
 		const uint32_t ns = inr ? numsteps[2 * i] : 0u, base = inr ? numsteps[2 * i + 1] : 0u;
 		RayScan S{1.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0u};
 		bool open = inr && (e0 == 0 || ns > 0);  // this round runs (and stores) the ray's state
-		if (e0 > 0 && open) {
-			S.cn = ccount[i];
-			if (S.cn != e0 || e0 >= ns) open = false;  // closed in an earlier round (or no samples)
-			else {
-				S.T = rT[i];
-				if (S.T < 1e-4f) open = false;
-				else { const float4 a = racc[i]; S.r0 = a.x; S.r1 = a.y; S.r2 = a.z; S.ws = a.w; S.ek = rek[i]; }
-			}
+		if (e0 > 0 && inr) {
+			// the stored state, loaded together with numsteps (one round trip; read for closed rays too)
+			const uint32_t cn = ccount[i];
+			const float T = rT[i];
+			const float4 a = racc[i];
+			const float ek = rek[i];
+			S.cn = cn;
+			if (!open || cn != e0 || e0 >= ns || T < 1e-4f) open = false;  // closed in an earlier round (or no samples)
+			else { S.T = T; S.r0 = a.x; S.r1 = a.y; S.r2 = a.z; S.ws = a.w; S.ek = ek; }
 		}
 		const uint32_t to = min(ns, e1);
 		bool live = open && to > e0;
 		const uint32_t g0 = live ? base + e0 : 0u, gl = live ? base + to - 1u : 0u;  // the round's samples [g0, gl]
 		uint32_t lb[U], ll[U];
 #pragma unroll
-		for (uint32_t j = 0; j < U; ++j) { lb[j] = __shfl(g0, 4 * j + sub); ll[j] = __shfl(gl, 4 * j + sub); }
+		for (uint32_t j = 0; j < U; ++j) { lb[j] = __shfl(g0, RPI * j + sub); ll[j] = __shfl(gl, RPI * j + sub); }
 		auto fetch = [&](f4v (&q)[U], float (&e)[U], uint32_t c) {
 #pragma unroll
 			for (uint32_t j = 0; j < U; ++j) {
@@ -922,7 +919,7 @@ __global__ void __launch_bounds__(64) k_loss_scan_chunk(uint32_t cap_rays, const
 		auto group = [&](f4v (&qs)[U], float (&es)[U], uint32_t c) {
 			__builtin_amdgcn_wave_barrier();
 #pragma unroll
-			for (uint32_t j = 0; j < U; ++j) { s_q[(4 * j + sub) * PAD + el] = qs[j]; s_e[(4 * j + sub) * PAD + el] = es[j]; }
+			for (uint32_t j = 0; j < U; ++j) { s_q[(RPI * j + sub) * PAD + el] = qs[j]; s_e[(RPI * j + sub) * PAD + el] = es[j]; }
 			__builtin_amdgcn_wave_barrier();
 			fetch(qs, es, c + 2 * U);
 			f4v q[U]; float e[U];
@@ -962,14 +959,12 @@ __global__ void __launch_bounds__(64) k_loss_scan_chunk(uint32_t cap_rays, const
 		if (list) {
 			// the next round's chunk of every ray still open: one reservation per wave, written lane-contiguously
 			const uint32_t m = (open && S.cn == e1 && e1 < ns && S.T >= 1e-4f) ? min(ns, e2) - e1 : 0u;
-			uint32_t incl = m;
-#pragma unroll
-			for (int d = 1; d < 64; d <<= 1) { const uint32_t y = (uint32_t)__shfl_up((int)incl, d); if ((int)lane >= d) incl += y; }
-			const uint32_t total = (uint32_t)__shfl((int)incl, 63);
+			const uint32_t incl = wave_incl_sum(m);
+			const uint32_t total = wave_lane_value(incl, 63);
 			if (total) {
 				uint32_t p0 = 0;
 				if (lane == 0) p0 = atomicAdd(next_counter, total);
-				p0 = (uint32_t)__shfl((int)p0, 0);
+				p0 = wave_lane_value(p0, 0);
 				__builtin_amdgcn_wave_barrier();
 				s_pre[lane] = incl - m;
 				s_src[lane] = base + e1;

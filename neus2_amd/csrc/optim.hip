@@ -15,6 +15,23 @@
 
 namespace neus {
 
+// adam.h:137's bias correction of step k: sqrtf(1 - beta2^k) and 1 - beta1^k (the table and the fallback share it)
+__device__ __forceinline__ void adam_bias_terms(float beta1, float beta2, uint32_t k, float& s2, float& d1) {
+	s2 = sqrtf(1 - powf(beta2, (float)k));
+	d1 = 1 - powf(beta1, (float)k);
+}
+__global__ void k_adam_bias_table(float beta1, float beta2, float* __restrict__ tab) {
+	const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+	if (k >= ADAM_BIAS_TAB) return;
+	float s2, d1;
+	adam_bias_terms(beta1, beta2, k, s2, d1);
+	tab[k] = s2;
+	tab[ADAM_BIAS_TAB + k] = d1;
+}
+void launch_adam_bias_table(hipStream_t s, float beta1, float beta2, float* tab) {
+	k_adam_bias_table<<<ADAM_BIAS_TAB / 256, 256, 0, s>>>(beta1, beta2, tab);
+}
+
 // grads fp32 (the reference keeps fp16 gradients); weights_fp fp32 master; weights_h fp16 copy
 // used by every kernel; ema_tmp fp32 running EMA; ema_h fp16 inference weights.
 __global__ void __launch_bounds__(256) k_adam_ema(AdamParams p, float* __restrict__ weights_fp, half_t* __restrict__ weights_h,
@@ -23,7 +40,7 @@ __global__ void __launch_bounds__(256) k_adam_ema(AdamParams p, float* __restric
                                                   StepCounterArgs sc, AdamTranspose tr) {
 	if (sc.st && blockIdx.x == 0 && threadIdx.x == 0) step_counters_update(sc.st, sc.target_batch, sc.max_samples, sc.world, sc.fixed_rays);
 	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < p.n; i += gridDim.x * blockDim.x) {
-		float gradient = grads[i] / p.loss_scale;
+		float gradient = p.pow2_scale ? grads[i] * p.inv_loss_scale : grads[i] / p.loss_scale;
 		const bool is_matrix = i < p.n_matrix;
 		bool skip = is_matrix ? !p.optimize_matrix : (!p.optimize_non_matrix || gradient == 0.f);
 		float w = weights_fp[i];
@@ -35,7 +52,10 @@ __global__ void __launch_bounds__(256) k_adam_ema(AdamParams p, float* __restric
 			m1[i] = fm; m2[i] = sm;
 			const uint32_t cs = steps[i] + 1;
 			steps[i] = cs;
-			const float lr = p.lr * sqrtf(1 - powf(p.beta2, (float)cs)) / (1 - powf(p.beta1, (float)cs));
+			float lr;
+			if (p.bias_tab && cs < ADAM_BIAS_TAB) lr = p.lr * p.bias_tab[cs] / p.bias_tab[ADAM_BIAS_TAB + cs];
+			else if (p.bias_tab && p.bias_converged) lr = p.lr;  // (lr * 1.0f) / 1.0f
+			else { float s2, d1; adam_bias_terms(p.beta1, p.beta2, cs, s2, d1); lr = p.lr * s2 / d1; }
 			const float elr = fminf(fmaxf(lr / (sqrtf(sm) + p.eps), 0.0f), 3.402823466e+38f);
 			w = w - elr * fm;
 			weights_fp[i] = w;

@@ -204,6 +204,9 @@ struct NeusTestbed {
 	Dev<uint8_t> bitfield;
 	Dev<uint32_t> bf_lin;   // mip-0 occupancy in (x, y, z/32) word order for the constant-step march
 	Dev<float> occ_bbox;    // world box of the occupied cells of every mip (+ stage-1 scratch): the ray generation's cull
+	Dev<float> adam_bias;   // Adam bias-correction table (AdamParams::bias_tab) for betas bias_b1 / bias_b2
+	float bias_b1 = -1.f, bias_b2 = -1.f;
+	bool bias_conv = false;
 	Dev<uint32_t> dbg_enc;  // debug timing only (neus_debug_time_kernel 11): [L][16 Nc] encodings of the inference samples
 	bool ray_cull = true;   // NEUS_RAY_CULL=0: march every ray (A/B reference)
 	Dev<PcgJump> pcg_tab;   // pcg32 jump-ahead table (common.h PcgJumpTable)
@@ -883,6 +886,22 @@ struct NeusTestbed {
 		p.ema_debias_old = 1 - (float)std::pow(cfg.ema_decay, adam_step - 1);
 		p.ema_debias_new = 1.0f / (1 - (float)std::pow(cfg.ema_decay, adam_step));
 		p.optimize_matrix = 1; p.optimize_non_matrix = 1;
+		int e2 = 0;
+		p.pow2_scale = std::frexp(p.loss_scale, &e2) == 0.5f ? 1u : 0u;
+		p.inv_loss_scale = 1.0f / p.loss_scale;
+		if (p.beta1 != bias_b1 || p.beta2 != bias_b2) {
+			// bias-correction table for these betas (rebuilt only when they change)
+			adam_bias.alloc(2 * ADAM_BIAS_TAB);
+			launch_adam_bias_table(stream, p.beta1, p.beta2, adam_bias.p);
+			float last[2];
+			HIP_CHECK(hipStreamSynchronize(stream));
+			HIP_CHECK(hipMemcpy(&last[0], adam_bias.p + ADAM_BIAS_TAB - 1, 4, hipMemcpyDeviceToHost));
+			HIP_CHECK(hipMemcpy(&last[1], adam_bias.p + 2 * ADAM_BIAS_TAB - 1, 4, hipMemcpyDeviceToHost));
+			const double k = ADAM_BIAS_TAB - 1;
+			bias_conv = last[0] == 1.0f && last[1] == 1.0f && std::pow((double)p.beta1, k) < 0x1p-30 && std::pow((double)p.beta2, k) < 0x1p-30;
+			bias_b1 = p.beta1; bias_b2 = p.beta2;
+		}
+		p.bias_tab = adam_bias.p; p.bias_converged = bias_conv ? 1u : 0u;
 		// the transposed / permuted MLP copies are written by the Adam launch itself
 		const AdamTranspose tr = adam_transpose();
 		launch_adam_ema(stream, p, params_fp.p, params_h.p, g, m1.p, m2.p, adam_steps.p, ema_tmp.p, ema_h.p, counters, &tr);
@@ -1659,8 +1678,8 @@ int neus_testbed_time_kernel(NeusTestbed* tb, int kernel, int iters, float* ms_o
 		StepState h{};
 		HIP_CHECK(hipMemcpy(&h, tb->st.p, sizeof(StepState), hipMemcpyDeviceToHost));
 		// work units of one launch: ray slots (march), pre-compaction samples (write, inference, loss),
-		// compacted training samples (encode, MLP, weight gradients, grid scatter)
-		*units_out = kernel == 0 ? MAX_RAYS : (kernel <= 4 ? h.n_kept : tb->batch);
+		// compacted training samples (encode, MLP, weight gradients, grid scatter), parameters (Adam / EMA)
+		*units_out = kernel == 0 ? MAX_RAYS : kernel <= 4 ? h.n_kept : kernel == 12 ? tb->lay.P : tb->batch;
 	});
 }
 static void time_kernel_impl(NeusTestbed* tb, int kernel, int variant, int iters, float* ms_out) {
@@ -1721,6 +1740,7 @@ static void time_kernel_impl(NeusTestbed* tb, int kernel, int variant, int iters
 				                   t.dbg_enc.p, nullptr, variant > 0 && variant != 99 ? (uint32_t)variant : 2048u, nullptr);
 				break;
 			}
+			case 12: t.optimizer_step(t.grads.p); break;  // the Adam / EMA pass on the last gradient (advances the optimizer)
 			default: throw std::runtime_error("unknown kernel id");
 			}
 		}
@@ -1742,6 +1762,26 @@ int neus_debug_march_stats(NeusTestbed* tb, uint32_t n, uint32_t* out) {
 		debug_launch_march_stats(tb->stream, n, tb->rays.p, tb->startt.p, tb->bf_lin.p, tb->ds, tb->bitfield.p, o.p);
 		HIP_CHECK(hipStreamSynchronize(tb->stream));
 		HIP_CHECK(hipMemcpy(out, o.p, 12 * (size_t)n, hipMemcpyDeviceToHost));
+	});
+}
+int neus_debug_scatter_stats(NeusTestbed* tb, uint64_t* records_per_level, uint32_t* max_region) {
+	return guard([&] {
+		if (!tb->have_net || tb->swork.mode != 2) throw std::runtime_error("scatter stats: region mode only");
+		HIP_CHECK(hipStreamSynchronize(tb->stream));
+		const uint32_t L = tb->lay.L, nb = tb->swork.n_chunks;
+		std::vector<uint16_t> h((size_t)L * nb * (SB_LEVEL_BUCKETS + 1));
+		HIP_CHECK(hipMemcpy(h.data(), tb->sc_rtab.p, h.size() * 2, hipMemcpyDeviceToHost));
+		uint32_t mx = 0;
+		for (uint32_t l = 0; l < L; ++l) {
+			const uint32_t size = tb->gl.offset[l + 1] - tb->gl.offset[l], nlb = (size + SB_SIZE - 1) / SB_SIZE;
+			uint64_t t = 0;
+			for (uint32_t b = 0; b < nb; ++b) {
+				const uint32_t r = h[((size_t)l * nb + b) * (SB_LEVEL_BUCKETS + 1) + nlb];
+				t += r; mx = std::max(mx, r);
+			}
+			if (records_per_level) records_per_level[l] = t;
+		}
+		if (max_region) *max_region = mx;
 	});
 }
 int neus_debug_march_profile(NeusTestbed* tb, unsigned long long* out, uint32_t max_waves, uint32_t* n_waves) {

@@ -37,12 +37,26 @@ def rows_from(path):
     return out
 
 
+def replay_start(ks):
+    """Index of the first launch of bench.py's kernel replays (kernel_rooflines): each replay regenerates the step's
+    samples with k_loss_alpha, which the static-scene training step no longer launches (its alpha terms are in the
+    inference epilogue); len(ks) when there are none."""
+    return next((i for i, r in enumerate(ks) if "k_loss_alpha" in r[0]), len(ks))
+
+
+def step_ends(ks):
+    """Indices of the training steps' optimizer launches (one k_adam_ema per step), before the replays (which replay
+    the optimizer too)."""
+    end = replay_start(ks)
+    return [i for i, r in enumerate(ks[:end]) if "k_adam_ema" in r[0]]
+
+
 def rows_last_steps(path, k):
-    """Kernels of the last k training steps: the launches after the (k+1)-th last k_adam_ema up to and
-    including the last one (one optimizer launch per step; bench.py's kernel replays have none)."""
+    """Kernels of the last k training steps: the launches after the (k+1)-th last k_adam_ema of the training up to and
+    including the last one."""
     con = sqlite3.connect(path)
     ks = list(con.execute("select name, start, end from kernels order by start"))
-    adam = [i for i, r in enumerate(ks) if "k_adam_ema" in r[0]]
+    adam = step_ends(ks)
     begin, last = adam[-k - 1] + 1, adam[-1]
     out = {}
     for name, st, en in ks[begin:last + 1]:
@@ -80,7 +94,7 @@ def main():
         # the launch sequence of the final step (start offset, duration), e.g. the progressive-inference rounds
         con = sqlite3.connect(sys.argv[1])
         ks = list(con.execute("select name, start, end from kernels order by start"))
-        adam = [i for i, r in enumerate(ks) if "k_adam_ema" in r[0]]
+        adam = step_ends(ks)
         seq = ks[adam[-2] + 1:adam[-1] + 1]
         t0 = seq[0][1]
         lines.append("\nLaunch sequence of the final step (start us, duration us):\n")

@@ -8,7 +8,9 @@ import os
 import re
 
 NAMES = {"k_nerf_infer": "inference", "k_march": "march", "k_grid_encode": "train_encode", "k_loss_alpha": "loss_alpha",
-         "k_mlp_train_rgb": "mlp_train_rgb", "k_mlp_train_density": "mlp_train_density", "k_march_write": "march_write"}
+         "k_mlp_train_rgb": "mlp_train_rgb", "k_mlp_train_density": "mlp_train_density", "k_march_write": "march_write",
+         "k_scatter_bin_r": "scatter_bin", "k_scatter_accum_r": "scatter_accum", "k_adam_ema": "adam_ema",
+         "k_mlp_grad_reduce": "mlp_grad_reduce"}
 
 
 def parse(path):
