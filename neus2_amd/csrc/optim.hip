@@ -32,52 +32,108 @@ void launch_adam_bias_table(hipStream_t s, float beta1, float beta2, float* tab)
 	k_adam_bias_table<<<ADAM_BIAS_TAB / 256, 256, 0, s>>>(beta1, beta2, tab);
 }
 
-// grads fp32 (the reference keeps fp16 gradients); weights_fp fp32 master; weights_h fp16 copy
-// used by every kernel; ema_tmp fp32 running EMA; ema_h fp16 inference weights.
+// One parameter's Adam step (adam.h:86-159) on registers: false when it is skipped (a zero gradient of a non-matrix
+// parameter, or a disabled parameter class), leaving w / m1 / m2 / step unchanged.
+__device__ __forceinline__ bool adam_param(const AdamParams& p, uint32_t i, float graw, float& w, float& m1v, float& m2v, uint32_t& st) {
+	float gradient = p.pow2_scale ? graw * p.inv_loss_scale : graw / p.loss_scale;
+	const bool is_matrix = i < p.n_matrix;
+	const bool skip = is_matrix ? !p.optimize_matrix : (!p.optimize_non_matrix || gradient == 0.f);
+	if (skip) return false;
+	if (is_matrix) gradient += p.l2_reg * w;
+	const float g2 = gradient * gradient;
+	m1v = p.beta1 * m1v + (1 - p.beta1) * gradient;
+	m2v = p.beta2 * m2v + (1 - p.beta2) * g2;
+	const uint32_t cs = ++st;
+	float lr;
+	if (p.bias_tab && cs < ADAM_BIAS_TAB) lr = p.lr * p.bias_tab[cs] / p.bias_tab[ADAM_BIAS_TAB + cs];
+	else if (p.bias_tab && p.bias_converged) lr = p.lr;  // (lr * 1.0f) / 1.0f
+	else { float s2, d1; adam_bias_terms(p.beta1, p.beta2, cs, s2, d1); lr = p.lr * s2 / d1; }
+	const float elr = fminf(fmaxf(lr / (sqrtf(m2v) + p.eps), 0.0f), 3.402823466e+38f);
+	w = w - elr * m1v;
+	return true;
+}
+// Ema(ExponentialDecay) of the fp16 weight (ema.h:45-110): the running fp32 EMA, debiased
+__device__ __forceinline__ float ema_param(const AdamParams& p, float ema, float wh) {
+	return (ema * p.ema_decay * p.ema_debias_old + wh * (1 - p.ema_decay)) * p.ema_debias_new;
+}
+// the MLP's transposed / permuted fp16 copies of matrix weight i (prepare_weights)
+__device__ __forceinline__ void adam_transpose_param(const AdamTranspose& tr, uint32_t i, half_t hv) {
+	for (uint32_t j = 0; j < tr.n; ++j) {
+		const uint32_t e = i - tr.off[j];
+		if (i < tr.off[j] || e >= tr.rows[j] * tr.cols[j]) continue;
+		const uint32_t r = e / tr.cols[j], c = e % tr.cols[j];
+		tr.dst[j][(size_t)c * tr.rows[j] + r] = hv;
+		if (j == 0 && tr.d0p) {
+			const int32_t q = c < 48 ? tr.inv[c] : -1;
+			if (q >= 0) { tr.d0p[(size_t)r * tr.din + q] = hv; tr.d0Tp[(size_t)q * tr.W + r] = hv; }
+		}
+	}
+}
+
+// grads fp32 (the reference keeps fp16 gradients); weights_fp fp32 master; weights_h fp16 copy used by every kernel;
+// ema_tmp fp32 running EMA; ema_h fp16 inference weights. Four consecutive parameters per thread with 16-B (8-B for
+// fp16) accesses; the optimizer state of a group is read and written only when one of its four parameters steps (a
+// skipped parameter's values are written back unchanged); the n % 4 tail by block 0.
 __global__ void __launch_bounds__(256) k_adam_ema(AdamParams p, float* __restrict__ weights_fp, half_t* __restrict__ weights_h,
                                                   const float* __restrict__ grads, float* __restrict__ m1, float* __restrict__ m2,
                                                   uint32_t* __restrict__ steps, float* __restrict__ ema_tmp, half_t* __restrict__ ema_h,
                                                   StepCounterArgs sc, AdamTranspose tr) {
 	if (sc.st && blockIdx.x == 0 && threadIdx.x == 0) step_counters_update(sc.st, sc.target_batch, sc.max_samples, sc.world, sc.fixed_rays);
-	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < p.n; i += gridDim.x * blockDim.x) {
-		float gradient = p.pow2_scale ? grads[i] * p.inv_loss_scale : grads[i] / p.loss_scale;
-		const bool is_matrix = i < p.n_matrix;
-		bool skip = is_matrix ? !p.optimize_matrix : (!p.optimize_non_matrix || gradient == 0.f);
-		float w = weights_fp[i];
-		if (!skip) {
-			if (is_matrix) gradient += p.l2_reg * w;
-			const float g2 = gradient * gradient;
-			const float fm = p.beta1 * m1[i] + (1 - p.beta1) * gradient;
-			const float sm = p.beta2 * m2[i] + (1 - p.beta2) * g2;
-			m1[i] = fm; m2[i] = sm;
-			const uint32_t cs = steps[i] + 1;
-			steps[i] = cs;
-			float lr;
-			if (p.bias_tab && cs < ADAM_BIAS_TAB) lr = p.lr * p.bias_tab[cs] / p.bias_tab[ADAM_BIAS_TAB + cs];
-			else if (p.bias_tab && p.bias_converged) lr = p.lr;  // (lr * 1.0f) / 1.0f
-			else { float s2, d1; adam_bias_terms(p.beta1, p.beta2, cs, s2, d1); lr = p.lr * s2 / d1; }
-			const float elr = fminf(fmaxf(lr / (sqrtf(sm) + p.eps), 0.0f), 3.402823466e+38f);
-			w = w - elr * fm;
-			weights_fp[i] = w;
-			weights_h[i] = (half_t)w;
+	const uint32_t ng = p.n / 4;
+	for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < ng; g += gridDim.x * blockDim.x) {
+		const uint32_t i0 = 4 * g;
+		const float4 G = ((const float4*)grads)[g];
+		float4 W = ((const float4*)weights_fp)[g];
+		const uint2 WHr = ((const uint2*)weights_h)[g];
+		float4 E = ((const float4*)ema_tmp)[g];
+		float gr[4] = {G.x, G.y, G.z, G.w}, w[4] = {W.x, W.y, W.z, W.w}, e[4] = {E.x, E.y, E.z, E.w};
+		half_t wh[4];
+		*(uint2*)wh = WHr;
+		// any parameter of the group steps? (the same skip test as adam_param)
+		bool any = false;
+#pragma unroll
+		for (int k = 0; k < 4; ++k) {
+			const float gk = p.pow2_scale ? gr[k] * p.inv_loss_scale : gr[k] / p.loss_scale;
+			any |= (i0 + k < p.n_matrix) ? p.optimize_matrix != 0u : (p.optimize_non_matrix != 0u && gk != 0.f);
+		}
+		if (any) {
+			float4 M1 = ((const float4*)m1)[g], M2 = ((const float4*)m2)[g];
+			uint4 S = ((const uint4*)steps)[g];
+			float a[4] = {M1.x, M1.y, M1.z, M1.w}, b[4] = {M2.x, M2.y, M2.z, M2.w};
+			uint32_t st[4] = {S.x, S.y, S.z, S.w};
+#pragma unroll
+			for (int k = 0; k < 4; ++k)
+				if (adam_param(p, i0 + k, gr[k], w[k], a[k], b[k], st[k])) wh[k] = (half_t)w[k];
+			((float4*)m1)[g] = make_float4(a[0], a[1], a[2], a[3]);
+			((float4*)m2)[g] = make_float4(b[0], b[1], b[2], b[3]);
+			((uint4*)steps)[g] = make_uint4(st[0], st[1], st[2], st[3]);
+			((float4*)weights_fp)[g] = make_float4(w[0], w[1], w[2], w[3]);
+			((uint2*)weights_h)[g] = *(const uint2*)wh;
+		}
+		half_t eh[4];
+#pragma unroll
+		for (int k = 0; k < 4; ++k) { e[k] = ema_param(p, e[k], (float)wh[k]); eh[k] = (half_t)e[k]; }
+		((float4*)ema_tmp)[g] = make_float4(e[0], e[1], e[2], e[3]);
+		((uint2*)ema_h)[g] = *(const uint2*)eh;
+		if (tr.n && i0 < p.n_matrix) {
+#pragma unroll
+			for (int k = 0; k < 4; ++k)
+				if (i0 + k < p.n_matrix) adam_transpose_param(tr, i0 + k, wh[k]);
+		}
+	}
+	// the tail
+	if (blockIdx.x == 0 && threadIdx.x < p.n - 4 * ng) {
+		const uint32_t i = 4 * ng + threadIdx.x;
+		float w = weights_fp[i], a = m1[i], b = m2[i];
+		uint32_t st = steps[i];
+		if (adam_param(p, i, grads[i], w, a, b, st)) {
+			m1[i] = a; m2[i] = b; steps[i] = st; weights_fp[i] = w; weights_h[i] = (half_t)w;
 		}
 		const float wh = (float)weights_h[i];
-		const float f = (ema_tmp[i] * p.ema_decay * p.ema_debias_old + wh * (1 - p.ema_decay)) * p.ema_debias_new;
+		const float f = ema_param(p, ema_tmp[i], wh);
 		ema_tmp[i] = f;
 		ema_h[i] = (half_t)f;
-		if (tr.n && is_matrix) {  // the MLP's transposed / permuted fp16 copies of this weight (prepare_weights)
-			const half_t hv = (half_t)wh;
-			for (uint32_t j = 0; j < tr.n; ++j) {
-				const uint32_t e = i - tr.off[j];
-				if (i < tr.off[j] || e >= tr.rows[j] * tr.cols[j]) continue;
-				const uint32_t r = e / tr.cols[j], c = e % tr.cols[j];
-				tr.dst[j][(size_t)c * tr.rows[j] + r] = hv;
-				if (j == 0 && tr.d0p) {
-					const int32_t q = c < 48 ? tr.inv[c] : -1;
-					if (q >= 0) { tr.d0p[(size_t)r * tr.din + q] = hv; tr.d0Tp[(size_t)q * tr.W + r] = hv; }
-				}
-			}
-		}
+		if (tr.n && i < p.n_matrix) adam_transpose_param(tr, i, (half_t)wh);
 	}
 }
 
@@ -330,7 +386,7 @@ void launch_adam_ema(hipStream_t s, const AdamParams& p, float* weights_fp, half
 	const StepCounterArgs sc = counters ? *counters : StepCounterArgs{nullptr, 0u, 0u, 1u, 0u};
 	AdamTranspose t{};
 	if (tr) t = *tr;
-	k_adam_ema<<<nblk(p.n, 8192), 256, 0, s>>>(p, weights_fp, weights_h, grads, m1, m2, steps, ema_tmp, ema_h, sc, t);
+	k_adam_ema<<<nblk(std::max<uint64_t>(1, p.n / 4), 16384), 256, 0, s>>>(p, weights_fp, weights_h, grads, m1, m2, steps, ema_tmp, ema_h, sc, t);
 }
 void launch_add_f32(hipStream_t s, uint32_t n, const float* src, float* dst) {
 	if (n) k_add_f32<<<std::min<uint32_t>((n + 255) / 256, 8192), 256, 0, s>>>(n, src, dst);
