@@ -249,10 +249,40 @@ __device__ __forceinline__ void level_addr(const LevelSmem& sl, uint32_t dense_b
 		}
 	}
 }
+#ifndef NEUS_GATHER
+#define NEUS_GATHER 0
+#endif
 __device__ __forceinline__ void level_gather(const half_t* __restrict__ grid, const LevelAddr& A, uint32_t v[8]) {
 	const char* base = (const char*)grid;
+#if NEUS_GATHER == 0
 #pragma unroll
 	for (int c = 0; c < 8; ++c) v[c] = *(const uint32_t*)(base + (A.e[c] << 2));
+#elif NEUS_GATHER == 1
+	// x-neighbour corners (c, c+1) share an aligned 8-B entry pair when e1 == e0 ^ 1 (a hashed level with even x, a
+	// dense level with even e0): one load for both; the other lanes load e1 by itself.
+#pragma unroll
+	for (int k = 0; k < 4; ++k) {
+		const uint32_t e0 = A.e[2 * k], e1 = A.e[2 * k + 1];
+		const uint2 w = *(const uint2*)(base + ((e0 & ~1u) << 2));
+		const bool odd = e0 & 1u;
+		v[2 * k] = odd ? w.y : w.x;
+		uint32_t o = odd ? w.x : w.y;
+		if ((e0 ^ e1) != 1u) o = *(const uint32_t*)(base + (e1 << 2));
+		v[2 * k + 1] = o;
+	}
+#else
+	// aligned 16-B entry quad holding e0; e1 from the same quad when it is there
+#pragma unroll
+	for (int k = 0; k < 4; ++k) {
+		const uint32_t e0 = A.e[2 * k], e1 = A.e[2 * k + 1];
+		const uint4 w = *(const uint4*)(base + ((e0 & ~3u) << 2));
+		const uint32_t s0 = e0 & 3u, s1 = e1 & 3u;
+		v[2 * k] = s0 & 2u ? (s0 & 1u ? w.w : w.z) : (s0 & 1u ? w.y : w.x);
+		uint32_t o = s1 & 2u ? (s1 & 1u ? w.w : w.z) : (s1 & 1u ? w.y : w.x);
+		if ((e0 ^ e1) > 3u) o = *(const uint32_t*)(base + (e1 << 2));
+		v[2 * k + 1] = o;
+	}
+#endif
 }
 __device__ __forceinline__ f2v h2f(uint32_t u) {
 	h2 hv = __builtin_bit_cast(h2, u);
