@@ -529,7 +529,10 @@ __global__ void __launch_bounds__(BS) k_scatter_bin_r(const uint32_t* __restrict
 // lengths, a wave scan, and the concatenated segments read lane-contiguously, SC_U batches of 64 records in flight
 // (the owner of each record by binary search over the 64 segment starts in LDS).
 constexpr int SC_U = 8;
-constexpr int SC_WAVES = 4;  // (8 waves per workgroup measured slower: 93 -> 103 us at the bench state)
+#ifndef NEUS_SC_WAVES
+#define NEUS_SC_WAVES 4
+#endif
+constexpr int SC_WAVES = NEUS_SC_WAVES;  // (8 waves per workgroup measured slower: 93 -> 103 us at the bench state)
 __global__ void __launch_bounds__(64 * SC_WAVES) k_scatter_accum_r(ScatterWork w, const GridLevels gl, float* __restrict__ grads, uint32_t bs8,
                                                                    uint32_t n_jobs) {
 	__shared__ unsigned long long acc[2 * SB_SIZE];

@@ -89,8 +89,13 @@ struct LossParams {
 };
 
 // binned hash-grid gradient scatter (grid.hip)
-constexpr uint32_t SB_SHIFT = 12, SB_SIZE = 1u << SB_SHIFT;   // bucket = 4096 grid entries (64 KB of int64 pairs in LDS)
-constexpr uint32_t SB_MAX_BUCKETS = 4096;                      // 16 levels x 2^19 entries / 4096 + level boundaries
+// bucket = 2048 grid entries: 32 KB of int64 pairs in LDS, four accumulation workgroups per CU (4096-entry buckets, two
+// per CU: 158 -> 148 us per step of scatter at the bench state; 1024 entries: 166 us, the region tables' reads grow)
+#ifndef NEUS_SB_SHIFT
+#define NEUS_SB_SHIFT 11
+#endif
+constexpr uint32_t SB_SHIFT = NEUS_SB_SHIFT, SB_SIZE = 1u << SB_SHIFT;
+constexpr uint32_t SB_MAX_BUCKETS = (1u << 24) / SB_SIZE;      // 16 levels x 2^19 entries / SB_SIZE (+ level boundaries: 4096 at 4096-entry buckets)
 constexpr uint32_t SB_LEVEL_BUCKETS = (1u << 19) / SB_SIZE + 2; // buckets one level can touch (2^19-entry tables)
 struct ScatterWork {
 	uint32_t* counts;   // [n_buckets * n_blocks + 1] contributions per (bucket, block), bucket-major

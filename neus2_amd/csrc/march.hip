@@ -287,7 +287,15 @@ __device__ __forceinline__ void march_segment(const DevDataset& ds, const uint8_
 // checks run in segment order. Samples past NERF_STEPS are cut (the reference's loop stops there). The result is the
 // single-lane march's, sample for sample (tests/test_gpu_parity.py::test_sample_rays_bit_exact).
 template <bool FAST, int MG>
-__global__ void __launch_bounds__(256) k_march(uint32_t cap_rays, uint32_t pass, uint32_t max_samples, StepState* __restrict__ st, DevDataset ds,
+#ifndef NEUS_MARCH_WPE
+#define NEUS_MARCH_WPE 0
+#endif
+#if NEUS_MARCH_WPE
+#define MARCH_OCC __attribute__((amdgpu_waves_per_eu(NEUS_MARCH_WPE, NEUS_MARCH_WPE)))
+#else
+#define MARCH_OCC
+#endif
+__global__ void __launch_bounds__(256) MARCH_OCC k_march(uint32_t cap_rays, uint32_t pass, uint32_t max_samples, StepState* __restrict__ st, DevDataset ds,
                                                const uint8_t* __restrict__ bitfield, const uint32_t* __restrict__ lin, const float* __restrict__ rays,
                                                const float* __restrict__ tstart, uint32_t* __restrict__ nreq, MarchWork mw) {
 	const uint32_t est = st->march_est ? min(st->march_est, cap_rays) : cap_rays;
