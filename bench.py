@@ -53,6 +53,14 @@ def measured_traffic(kernel, levels):
     return None if e is None else e.get("bytes_per_launch")
 
 
+def traffic_source(tr, kernel, levels):
+    """Where `roofline.traffic` comes from: a builder-run PMC pass (not this run), its summary file and commit."""
+    e = tr.get(f"{kernel}@L{levels}")
+    if e is None:
+        return None
+    return f"builder-run rocprofv3 PMC pass, profiles/{e.get('source')} at commit {e.get('commit')}"
+
+
 def line_traffic(traffic, ms, algorithmic):
     if not traffic or not ms:
         return None
@@ -306,7 +314,7 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": dk["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": dk["frac"], "traffic": measured_traffic(dom, levels), "bytes_per_launch": dk["bytes"],
                      "units_per_launch": dk["units"], "launch_ms": dk["ms"], "levels_active": levels,
-                     "traffic_source": tr.get("_source")},
+                     "traffic_source": traffic_source(tr, dom, levels)},
         # the whole step against the HBM roofline and its MFMA rate
         "roofline_step": step_roofline(d, levels, lay["n_params"], ms_step, args.steps),
         # the training MLP kernels (fwd recompute + 1st / 2nd-order backward + weight gradients) against the MFMA peak

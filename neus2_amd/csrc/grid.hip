@@ -362,7 +362,7 @@ __global__ void __launch_bounds__(BS) k_scatter_bin_w(const uint32_t* __restrict
 	__shared__ uint32_t carry_b, carry_v;  // a bucket shared with the previous level: the block's next slot in it
 	__shared__ uint16_t st_i[BS * 8];
 	__shared__ uint32_t st_g[BS * 8];
-	__shared__ uint8_t st_b[BS * 8];       // level-local bucket of each staged record
+	__shared__ uint16_t st_b[BS * 8];      // level-local bucket of each staged record (up to 257 per level at 2048-entry buckets)
 	const uint32_t blk = blockIdx.x, lane = threadIdx.x & 63;
 	const uint32_t n = load_n(n_ptr, n_fixed);
 	const uint32_t i = blk * blockDim.x + threadIdx.x;
@@ -419,7 +419,7 @@ __global__ void __launch_bounds__(BS) k_scatter_bin_w(const uint32_t* __restrict
 				const uint32_t pos = base[lb] + rs[idx];
 				st_i[pos] = (uint16_t)(e & (SB_SIZE - 1));
 				st_g[pos] = rg[idx];
-				st_b[pos] = (uint8_t)lb;
+				st_b[pos] = (uint16_t)lb;
 			}
 		}
 		__syncthreads();  // stage complete: consecutive threads store consecutive slots of a bucket's run

@@ -271,8 +271,12 @@ void launch_loss_scan_ray(hipStream_t s, uint32_t cap_rays, const uint32_t* nums
 // progressive (cut-off-aware) inference rounds (march.hip)
 void launch_loss_alpha_list(hipStream_t s, uint32_t cap_samples, const uint32_t* n_ptr, const uint32_t* idx, const float* coords,
                             const half_t* net_out, float cos_anneal, const LossWork& w, bool dt_const = false);
+// rays_in / *n_rays_in: the rays still open (rounds after the first; nullptr: every ray slot); rays_out / n_rays_out: the
+// rays that stay open, for the next round (nullptr in the last round, with list)
 void launch_loss_scan_chunk(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, const LossWork& w, uint32_t* ccount, uint32_t e0,
-                            uint32_t e1, uint32_t e2, uint32_t* list /* nullptr in the last round */, uint32_t* next_counter);
+                            uint32_t e1, uint32_t e2, uint32_t* list /* nullptr in the last round */, uint32_t* next_counter,
+                            const uint32_t* rays_in = nullptr, const uint32_t* n_rays_in = nullptr, uint32_t* rays_out = nullptr,
+                            uint32_t* n_rays_out = nullptr);
 void launch_loss_ray(hipStream_t s, uint32_t cap_rays, StepState* st, DPInfo dp, const DevDataset& ds, const LossParams& lp, uint32_t* numsteps,
                      const uint32_t* ccount, const uint32_t* cbase, const LossWork& w, float* loss, float* ek, float* mask);
 void launch_loss_grad(hipStream_t s, uint32_t cap_samples, const StepState* st, DPInfo dp, const LossParams& lp, const float* coords,

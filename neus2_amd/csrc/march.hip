@@ -554,7 +554,7 @@ __global__ void __launch_bounds__(256) k_march_write(uint32_t cap_rays, const St
 	__shared__ uint32_t s_t0[WRITE_CHUNK];  // per chunk sample: t of its run's first sample (bits)
 	__shared__ uint16_t s_r[WRITE_CHUNK];   // its ray within the staged batch
 	__shared__ uint8_t s_u[WRITE_CHUNK];    // its step within the run
-	const uint32_t max_samples = st->max_inference;
+	const uint32_t max_samples = st->max_inference, n_kept = st->n_kept;
 	const uint32_t tid = threadIdx.x;
 	const uint32_t q0 = blockIdx.x * WRITE_CHUNK;
 	if (q0 >= max_samples) return;
@@ -610,15 +610,22 @@ __global__ void __launch_bounds__(256) k_march_write(uint32_t cap_rays, const St
 		}
 		__syncthreads();
 		// (2) consecutive threads on the batch's consecutive samples: t replayed from the run's first sample
-		// (<= MARCH_RUN_MAX - 1 steps, exactly as the march stepped it), coalesced NerfCoordinate stores
+		// (<= MARCH_RUN_MAX - 1 steps, exactly as the march stepped it; 41 -> 39 us with the constant step's jumps),
+		// coalesced NerfCoordinate stores
+		// slots at or past n_kept belong to no kept ray (the first ray over the cap and every later one): none of its
+		// runs mapped them in (1), so their LDS map entries are stale and they are skipped
 		const uint32_t qa = max(q0, s_b[0]);
-		const uint32_t qb = rb + nr > r_hi ? q1 : min(q1, base[rb + nr]);
+		const uint32_t qb = min(rb + nr > r_hi ? q1 : min(q1, base[rb + nr]), n_kept);
 		for (uint32_t q = qa + tid; q < qb; q += 256) {
 			const uint32_t r = s_r[q - q0];
 			const uint32_t j = q - s_b[r];
 			if (j >= s_n[r]) continue;  // not a kept sample (no run wrote this slot)
 			const uint32_t i = rb + r;
 			float t = __uint_as_float(s_t0[q - q0]);
+			if (ds.cone_angle == 0.0f) {  // the run's u constant steps in a few integer-domain jumps (exact, step_until)
+				uint32_t kk = 0;
+				step_until(t, kk, __int_as_float(0x7f800000), s_u[q - q0], MIN_CONE_STEPSIZE);
+			} else
 			for (uint32_t u = s_u[q - q0]; u > 0; --u) t += ds.cone_angle == 0.0f ? MIN_CONE_STEPSIZE : calc_dt(t, ds.cone_angle);
 			const float o[3] = {s_ray[0][r], s_ray[1][r], s_ray[2][r]}, dir[3] = {s_ray[3][r], s_ray[4][r], s_ray[5][r]};
 			float pos[3];
@@ -871,8 +878,11 @@ __global__ void __launch_bounds__(64) k_loss_scan_list(const uint32_t* __restric
 // work item writes its own sample's slots).
 
 // Round k's recurrence over [e0, e1) of each ray still open (all rays with samples when e0 == 0), continuing from
-// the stored state; rays that stay open append their next chunk [e1, min(ns, e2)) to the next round's list.
-// 64 consecutive rays to a one-wave block, one lane per ray, the loads made coalesced as in k_loss_scan_list: per
+// the stored state; rays that stay open append their next chunk [e1, min(ns, e2)) to the next round's list and
+// themselves to the next round's ray list (rays_out), so a later round visits only the rays still open (rays_in,
+// *n_rays_in of them) instead of sweeping every ray slot for its stored state.
+// 64 rays to a one-wave block (consecutive slots in round 0, the open-ray list after it), one lane per ray, the loads
+// made coalesced as in k_loss_scan_list: per
 // 16-sample group 16 lanes fetch one ray's 16 samples (4 rays per load instruction), staged through LDS, the next
 // group's fetches in flight while the current one runs through the recurrence (one lane loading its own ray's samples
 // put 64 lines behind every load instruction). The appends are one atomic per wave and a cooperative write of the
@@ -882,7 +892,9 @@ __global__ void __launch_bounds__(64) k_loss_scan_chunk(uint32_t cap_rays, const
                                                         const float* __restrict__ ekt, float4* __restrict__ ck4, float* __restrict__ cke,
                                                         uint32_t* __restrict__ ccount, float4* __restrict__ racc, float* __restrict__ rT,
                                                         float* __restrict__ rek, uint32_t e0, uint32_t e1, uint32_t e2,
-                                                        uint32_t* __restrict__ list, uint32_t* __restrict__ next_counter) {
+                                                        uint32_t* __restrict__ list, uint32_t* __restrict__ next_counter,
+                                                        const uint32_t* __restrict__ rays_in, const uint32_t* __restrict__ n_rays_in,
+                                                        uint32_t* __restrict__ rays_out, uint32_t* __restrict__ n_rays_out) {
 	// U samples per ray and group: U lanes load U consecutive samples of one ray (64 / U rays per load instruction),
 	// transposed through LDS to one ray per lane. U = 8 (was 16): half the LDS and registers per wave, so twice the
 	// waves per CU hide the per-ray state loads
@@ -894,9 +906,10 @@ __global__ void __launch_bounds__(64) k_loss_scan_chunk(uint32_t cap_rays, const
 	const uint32_t lane = threadIdx.x, sub = lane / U, el = lane % U;
 	const char* sab = (const char*)sa;
 	const char* ekb = (const char*)ekt;
-	for (uint32_t w0 = blockIdx.x * 64; w0 < cap_rays; w0 += gridDim.x * 64) {
-		const uint32_t i = w0 + lane;
-		const bool inr = i < cap_rays;
+	const uint32_t n_slots = rays_in ? min(*n_rays_in, cap_rays) : cap_rays;
+	for (uint32_t w0 = blockIdx.x * 64; w0 < n_slots; w0 += gridDim.x * 64) {
+		const bool inr = w0 + lane < n_slots;
+		const uint32_t i = rays_in ? (inr ? rays_in[w0 + lane] : 0u) : w0 + lane;
 		const uint32_t ns = inr ? numsteps[2 * i] : 0u, base = inr ? numsteps[2 * i + 1] : 0u;
 		RayScan S{1.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0u};
 		bool open = inr && (e0 == 0 || ns > 0);  // this round runs (and stores) the ray's state
@@ -985,6 +998,13 @@ __global__ void __launch_bounds__(64) k_loss_scan_chunk(uint32_t cap_rays, const
 					list[p0 + r] = s_src[o] + (r - s_pre[o]);
 				}
 				__builtin_amdgcn_wave_barrier();
+				if (rays_out) {  // the open rays, one reservation per wave
+					const unsigned long long mk = __ballot(m > 0);
+					uint32_t q0 = 0;
+					if (lane == 0) q0 = atomicAdd(n_rays_out, (uint32_t)__popcll(mk));
+					q0 = wave_lane_value(q0, 0);
+					if (m > 0) rays_out[q0 + (uint32_t)__popcll(mk & ((1ull << lane) - 1ull))] = i;
+				}
 			}
 		}
 	}
@@ -1246,9 +1266,11 @@ void launch_loss_alpha_list(hipStream_t s, uint32_t cap_samples, const uint32_t*
 	k_loss_alpha<<<sample_blocks(cap_samples), 256, 0, s>>>(cap_samples, n_ptr, idx, coords, net_out, cos_anneal, w.sa, w.ekt, nullptr, dt_const);
 }
 void launch_loss_scan_chunk(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, const LossWork& w, uint32_t* ccount, uint32_t e0,
-                            uint32_t e1, uint32_t e2, uint32_t* list, uint32_t* next_counter) {
+                            uint32_t e1, uint32_t e2, uint32_t* list, uint32_t* next_counter, const uint32_t* rays_in, const uint32_t* n_rays_in,
+                            uint32_t* rays_out, uint32_t* n_rays_out) {
 	k_loss_scan_chunk<<<std::max<uint32_t>(1, std::min<uint32_t>((cap_rays + 63) / 64, 8192)), 64, 0, s>>>(
-		cap_rays, numsteps, w.sa, w.ekt, w.ck4, w.cke, ccount, w.racc, w.rT, w.rek, e0, e1, e2, list, next_counter);
+		cap_rays, numsteps, w.sa, w.ekt, w.ck4, w.cke, ccount, w.racc, w.rT, w.rek, e0, e1, e2, list, next_counter, rays_in, n_rays_in,
+		rays_out, n_rays_out);
 }
 // w.n_long is zeroed by the k_loss_alpha launch before it
 void launch_loss_scan_ray(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, const LossWork& w, uint32_t* ccount) {

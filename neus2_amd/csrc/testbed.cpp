@@ -246,10 +246,12 @@ struct NeusTestbed {
 	// progressive (cut-off-aware) inference: 0 off, 1 auto (when under PROGRESSIVE_RATIO of the kept samples were
 	// composited at the last loss readback), 2 always; chunk ends of the rounds before the last (march.hip)
 	int progressive_mode = 1;
-	std::vector<uint32_t> chunk_ends{32, 80};
+	std::vector<uint32_t> chunk_ends{32, 64, 96};  // NEUS_CHUNK_ENDS="e0,e1,..." at creation overrides (A/B of schedules)
 	float last_keep_ratio = 1.f;
 	static constexpr float PROGRESSIVE_RATIO = 0.7f;
-	Dev<uint32_t> chunk_list, chunk_cnt;
+	Dev<uint32_t> chunk_list, chunk_cnt;  // chunk_cnt: [k] round k's sample list length, [16] the long-ray list's, [32 + k] open rays
+	Dev<uint32_t> open_rays[2];          // the rays still open after a round (ping-pong: round k reads [(k - 1) & 1])
+	static constexpr uint32_t OPEN_CNT = 32;
 	Dev<uint32_t> long_rays;  // the loss scan's wave-per-ray list (+ its counter in chunk_cnt[16])
 	TrainBufs tbuf{};
 	// RNG + counters (testbed.cu:2087-2101)
@@ -371,6 +373,13 @@ struct NeusTestbed {
 		occ_bbox.alloc(occ_bbox_scratch_floats());
 		launch_occ_bbox(stream, bitfield.p, occ_bbox.p);
 		{ const char* e = std::getenv("NEUS_RAY_CULL"); ray_cull = !(e && e[0] == '0'); }
+		if (const char* e = std::getenv("NEUS_CHUNK_ENDS")) {
+			std::vector<uint32_t> v;
+			for (const char* p = e; *p;) { char* q = nullptr; const unsigned long x = std::strtoul(p, &q, 10); if (q == p) break; v.push_back((uint32_t)x); p = *q ? q + 1 : q; }
+			bool ok = !v.empty() && v.size() <= 14 && v[0] > 0;
+			for (size_t k = 1; k < v.size(); ++k) ok = ok && v[k] > v[k - 1];
+			if (ok) chunk_ends = v;
+		}
 		{ const char* e = std::getenv("NEUS_SCATTER_NOSKIP"); scatter_noskip = e && e[0] == '1'; }
 		grid_mean.alloc(4); grid_partial.alloc(GRID3 / 1024);
 		HIP_CHECK(hipMemset(grid_mean.p, 0, 16));
@@ -577,7 +586,8 @@ struct NeusTestbed {
 		l_sa.alloc(max_samples); l_ekt.alloc(max_samples); sample_ray.alloc(max_samples);
 		l_ck4.alloc(max_samples / 8 + 1); l_cke.alloc(max_samples / 8 + 1);
 		l_racc.alloc(MAX_RAYS); l_rgr.alloc(MAX_RAYS); l_rT.alloc(MAX_RAYS); l_rek.alloc(MAX_RAYS);
-		chunk_list.alloc(max_samples); chunk_cnt.alloc(17); long_rays.alloc(MAX_RAYS);
+		chunk_list.alloc(max_samples); chunk_cnt.alloc(64); long_rays.alloc(MAX_RAYS);
+		open_rays[0].alloc(MAX_RAYS); open_rays[1].alloc(MAX_RAYS);
 		loss.alloc(MAX_RAYS); ek.alloc(MAX_RAYS); mask.alloc(MAX_RAYS); loss_sum.alloc(4);
 		coords.alloc((size_t)max_samples * COORD_W); net_out.alloc((size_t)max_samples * OUT_W);
 		coords_c.alloc((size_t)batch * COORD_W); dL_dout.alloc((size_t)batch * OUT_W);
@@ -1113,7 +1123,7 @@ struct NeusTestbed {
 		// round 0's list slots go through cbase (rewritten by the loss compaction before it is read again)
 		const Round0List r0{chunk_ends[0], cbase.p, chunk_list.p, chunk_cnt.p, nch + 1};
 		launch_march_count(s, MAX_RAYS, max_samples, st.p, dp, ds, bitfield.p, bf_lin.p, rng.state, rng.inc, rays.p, startt.p, nreq.p, mwork,
-		                   progressive ? chunk_cnt.p : nullptr, nch + 1, ray_cull ? occ_bbox.p : nullptr);
+		                   progressive ? chunk_cnt.p : nullptr, OPEN_CNT + nch, ray_cull ? occ_bbox.p : nullptr);  // list lengths + open-ray counts
 		launch_march_write(s, MAX_RAYS, st.p, ds, rays.p, mwork, nreq.p, base.p, numsteps.p, coords.p, sample_ray.p, max_samples, scan_tmp.p,
 		                   progressive ? &r0 : nullptr);
 		mark(2);
@@ -1136,7 +1146,10 @@ struct NeusTestbed {
 				launch_nerf_infer(s, lay.L, lay.W, chunk_cnt.p + k, 0, c_in, gl, valid, params_h.p + lay.grid_off, mlp, net_out.p, 8192, chunk_list.p,
 				                  use_delta ? nullptr : &ia);
 				if (use_delta) launch_loss_alpha_list(s, max_samples, chunk_cnt.p + k, chunk_list.p, coords.p, net_out.p, lp.cos_anneal, w, ds.cone_angle == 0.0f);
-				launch_loss_scan_chunk(s, MAX_RAYS, numsteps.p, w, ccount.p, e0, e1, e2, k + 1 < nch ? chunk_list.p : nullptr, chunk_cnt.p + k + 1);
+				const bool more = k + 1 < nch;
+				launch_loss_scan_chunk(s, MAX_RAYS, numsteps.p, w, ccount.p, e0, e1, e2, more ? chunk_list.p : nullptr, chunk_cnt.p + k + 1,
+				                       k ? open_rays[(k - 1) & 1].p : nullptr, k ? chunk_cnt.p + OPEN_CNT + k - 1 : nullptr,
+				                       more ? open_rays[k & 1].p : nullptr, more ? chunk_cnt.p + OPEN_CNT + k : nullptr);
 				e0 = e1;
 			}
 			mark(3);

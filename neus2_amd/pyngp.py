@@ -678,7 +678,7 @@ class Testbed:
     def set_progressive_inference(self, mode, chunk_ends=None):
         """Training-step inference in rounds of per-ray sample chunks, skipping the samples past the T < 1e-4 cut
         (bit-identical to one pass; an option of this implementation). mode: 0 off, 1 auto (default), 2 always;
-        chunk_ends: the increasing round boundaries (default 32, 80)."""
+        chunk_ends: the increasing round boundaries (default 32, 64, 96)."""
         e = None if chunk_ends is None else np.ascontiguousarray(chunk_ends, np.uint32)
         check(lib().neus_testbed_set_progressive_inference(self._h, C.c_int(int(mode)),
                                                            None if e is None else C.c_void_p(e.ctypes.data),

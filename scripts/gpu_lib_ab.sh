@@ -22,5 +22,10 @@ d = json.loads([l for l in open(sys.argv[2]) if l.startswith("{")][-1])
 k = d["kernels"]
 print(sys.argv[1], "ms/step %.4f" % d["ms_per_step"], " ".join("%s=%.1f" % (n, 1000 * v["ms"]) for n, v in k.items()))
 EOF
+  if [ -n "$PROF" ]; then  # kernel-trace summary of the steady-state steps with this library
+    ( cd /tmp && export TMPDIR=/tmp && NEUS2_HIP_LIB="$LIB" timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_${TAG}_$L" -o run -- python3 "$R/bench.py" --steps 50 --warmup 5 --cpu-baseline 0 --psnr-steps 0 --mc-res 0 --l16 0 --early 0 > "$R/gpurun_out/prof_${TAG}_$L.log" 2>&1 ) || { echo "PROF_FAIL $L"; exit 1; }
+    python3 scripts/prof_summary.py "$R/gpurun_out/prof_${TAG}_$L" "$R/gpurun_out/prof_${TAG}_${L}_summary.md" --last-steps 50 > /dev/null && rm -rf "$R/gpurun_out/prof_${TAG}_$L"
+    grep -E "^\| k_|per step" "$R/gpurun_out/prof_${TAG}_${L}_summary.md" | head -${PROF_N:-14}
+  fi
 done
 echo AB_OK
