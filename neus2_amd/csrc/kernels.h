@@ -140,6 +140,7 @@ struct LossWork {
 	uint32_t* long_rays;    // [rays] rays the transmittance scan runs one wave per ray (nullable: one thread per ray)
 	uint32_t* n_long;       // their count (zeroed by k_loss_alpha)
 	float4* rgr;            // [rays] dL/drgb_ray (Huber'), gws * (1 - weight_sum)
+	uint32_t* cmap;         // [max_compacted] owning ray of each compacted sample (k_loss_ray; k_loss_grad's work items)
 };
 
 // Adam's bias-correction factors by per-parameter step: tab[k] = sqrtf(1 - powf(beta2, k)) and

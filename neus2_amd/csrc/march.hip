@@ -1015,7 +1015,8 @@ __global__ void __launch_bounds__(256) k_loss_ray(uint32_t cap_rays, StepState* 
                                                   const uint32_t* __restrict__ cbase, const float4* __restrict__ sa, const float* __restrict__ ekt,
                                                   const float4* __restrict__ ck4, const float* __restrict__ cke,
                                                   float4* __restrict__ racc, const float* __restrict__ rT, float4* __restrict__ rgr,
-                                                  float* __restrict__ loss_out, float* __restrict__ ek_out, float* __restrict__ mask_out) {
+                                                  float* __restrict__ loss_out, float* __restrict__ ek_out, float* __restrict__ mask_out,
+                                                  uint32_t* __restrict__ cmap) {
 	const uint32_t R = st->rays_per_batch;
 	const uint32_t n_rays_global = R * dp.world, n_rays_total = st->n_rays_total;
 	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cap_rays; i += gridDim.x * blockDim.x) {
@@ -1062,6 +1063,7 @@ __global__ void __launch_bounds__(256) k_loss_ray(uint32_t cap_rays, StepState* 
 		const uint32_t comp = min(lp.max_compacted - min(lp.max_compacted, cb), cn);
 		numsteps[2 * i] = comp; numsteps[2 * i + 1] = cb;
 		if (comp == 0) continue;
+		for (uint32_t j = 0; j < comp; ++j) cmap[cb + j] = i;
 		float lgrad[3], lloss[3];
 #pragma unroll
 		for (int k = 0; k < 3; ++k) {
@@ -1085,23 +1087,23 @@ __global__ void __launch_bounds__(256) k_loss_ray(uint32_t cap_rays, StepState* 
 	}
 }
 
-// gradient of one compacted sample (testbed_nerf.cu:1775-1959)
-__global__ void __launch_bounds__(256) k_loss_grad(uint32_t cap, const StepState* __restrict__ st, DPInfo dp, LossParams lp,
+// gradient of one compacted sample (testbed_nerf.cu:1775-1959): one thread per compacted sample cs (its ray from the
+// map k_loss_ray wrote; the pre-compaction samples past each ray's composited prefix are never visited)
+__global__ void __launch_bounds__(256) k_loss_grad(const StepState* __restrict__ st, DPInfo dp, LossParams lp,
                                                    const float* __restrict__ coords, const half_t* __restrict__ net_out,
-                                                   const uint32_t* __restrict__ numsteps, const uint32_t* __restrict__ sample_ray,
+                                                   const uint32_t* __restrict__ numsteps, const uint32_t* __restrict__ cmap,
                                                    const uint32_t* __restrict__ rbase, const float4* __restrict__ sa, const float* __restrict__ ekt,
                                                    const float4* __restrict__ ck4, const float* __restrict__ cke, const float4* __restrict__ racc,
                                                    const float4* __restrict__ rgr, float* __restrict__ coords_out, half_t* __restrict__ dL_dout) {
-	const uint32_t n = min(st->n_kept, cap);
+	const uint32_t n = min(st->compacted_counter, lp.max_compacted);
 	const uint32_t n_rays_global = st->rays_per_batch * dp.world;
 	const float loss_scale = lp.loss_scale / n_rays_global;
-	for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < n; s += gridDim.x * blockDim.x) {
-		const uint32_t r = sample_ray[s];
+	for (uint32_t cs = blockIdx.x * blockDim.x + threadIdx.x; cs < n; cs += gridDim.x * blockDim.x) {
+		const uint32_t r = cmap[cs];
 		const uint32_t rb = rbase[r];
-		const uint32_t j = s - rb;
-		const uint32_t comp = numsteps[2 * r];
-		if (j >= comp) continue;
 		const uint32_t cb = numsteps[2 * r + 1];
+		const uint32_t j = cs - cb;
+		const uint32_t s = rb + j;
 		const float* ci = coords + (size_t)s * COORD_W;
 		float* co = coords_out + (size_t)(cb + j) * COORD_W;
 #pragma unroll
@@ -1292,12 +1294,14 @@ void debug_launch_loss_scan(hipStream_t s, int variant, uint32_t cap_rays, const
 }
 void launch_loss_ray(hipStream_t s, uint32_t cap_rays, StepState* st, DPInfo dp, const DevDataset& ds, const LossParams& lp, uint32_t* numsteps,
                      const uint32_t* ccount, const uint32_t* cbase, const LossWork& w, float* loss, float* ek, float* mask) {
+	if (!w.cmap) throw std::runtime_error("launch_loss_ray: LossWork::cmap (max_compacted entries) is required");
 	k_loss_ray<<<ray_blocks(cap_rays), 256, 0, s>>>(cap_rays, st, dp, ds, lp, numsteps, ccount, cbase, w.sa, w.ekt, w.ck4, w.cke, w.racc, w.rT,
-	                                                  w.rgr, loss, ek, mask);
+	                                                  w.rgr, loss, ek, mask, w.cmap);
 }
 void launch_loss_grad(hipStream_t s, uint32_t cap_samples, const StepState* st, DPInfo dp, const LossParams& lp, const float* coords,
                       const half_t* net_out, const uint32_t* numsteps, const LossWork& w, float* coords_out, half_t* dL_dout) {
-	k_loss_grad<<<sample_blocks(cap_samples), 256, 0, s>>>(cap_samples, st, dp, lp, coords, net_out, numsteps, w.sample_ray, w.rbase, w.sa,
+	(void)cap_samples;  // (the compacted samples: at most lp.max_compacted)
+	k_loss_grad<<<sample_blocks(lp.max_compacted), 256, 0, s>>>(st, dp, lp, coords, net_out, numsteps, w.cmap, w.rbase, w.sa,
 	                                                         w.ekt, w.ck4, w.cke, w.racc, w.rgr, coords_out, dL_dout);
 }
 void launch_ray_index(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, StepState* st, uint32_t* sample_ray, uint32_t* rbase) {

@@ -243,6 +243,7 @@ struct NeusTestbed {
 	Dev<float4> l_sa, l_ck4, l_racc, l_rgr;
 	Dev<float> l_ekt, l_cke, l_rT, l_rek;
 	Dev<uint32_t> sample_ray;
+	Dev<uint32_t> cmap;  // compacted sample -> ray (LossWork::cmap)
 	// progressive (cut-off-aware) inference: 0 off, 1 auto (when under PROGRESSIVE_RATIO of the kept samples were
 	// composited at the last loss readback), 2 always; chunk ends of the rounds before the last (march.hip)
 	int progressive_mode = 1;
@@ -583,7 +584,7 @@ struct NeusTestbed {
 		mwork = MarchWork{march_rec.p, march_nrec.p, march_queue.p, march_waves(), march_seg.p, march_lanes(), jump_table()};
 		nreq.alloc(MAX_RAYS); base.alloc(MAX_RAYS);
 		numsteps.alloc(2 * (size_t)MAX_RAYS); ccount.alloc(MAX_RAYS); cbase.alloc(MAX_RAYS);
-		l_sa.alloc(max_samples); l_ekt.alloc(max_samples); sample_ray.alloc(max_samples);
+		l_sa.alloc(max_samples); l_ekt.alloc(max_samples); sample_ray.alloc(max_samples); cmap.alloc(batch);
 		l_ck4.alloc(max_samples / 8 + 1); l_cke.alloc(max_samples / 8 + 1);
 		l_racc.alloc(MAX_RAYS); l_rgr.alloc(MAX_RAYS); l_rT.alloc(MAX_RAYS); l_rek.alloc(MAX_RAYS);
 		chunk_list.alloc(max_samples); chunk_cnt.alloc(64); long_rays.alloc(MAX_RAYS);
@@ -1241,7 +1242,7 @@ struct NeusTestbed {
 
 	LossWork loss_work(const uint32_t* rbase) {
 		LossWork w{};
-		w.sa = l_sa.p; w.ck4 = l_ck4.p; w.cke = l_cke.p; w.ekt = l_ekt.p; w.sample_ray = sample_ray.p; w.rbase = rbase;
+		w.sa = l_sa.p; w.ck4 = l_ck4.p; w.cke = l_cke.p; w.ekt = l_ekt.p; w.sample_ray = sample_ray.p; w.rbase = rbase; w.cmap = cmap.p;
 		w.racc = l_racc.p; w.rT = l_rT.p; w.rgr = l_rgr.p; w.rek = l_rek.p;
 		w.long_rays = long_rays.p; w.n_long = chunk_cnt.p + 16;
 		return w;
@@ -2026,6 +2027,7 @@ int neus_loss_compact(NeusTestbed* tb, void* stream, uint32_t n_rays, uint32_t r
 		lp.max_compacted = max_compacted; lp.rng_state = rng_state; lp.rng_inc = rng_inc;
 		LossWork w{};
 		w.sa = sa.p; w.ck4 = ck4.p; w.cke = cke.p; w.ekt = ekt.p; w.sample_ray = sr.p; w.rbase = rb.p; w.racc = racc.p; w.rT = rT.p; w.rgr = rgr.p;
+		Dev<uint32_t> cm; cm.alloc(std::max(1u, max_compacted)); w.cmap = cm.p;
 		Dev<uint32_t> lr, nl; lr.alloc(n_rays); nl.alloc(1);
 		w.long_rays = lr.p; w.n_long = nl.p;
 		const DPInfo dp{rank, world};
