@@ -209,7 +209,15 @@ struct OccSampling {
 	float* grid_tmp;
 	PcgJumpTable jt;
 	uint32_t exclusive;   // the all-cells uniform pass over one cascade: index = cell (occ_common.h grid_sample_cell), plain stores
+	// the uniform samples of this rank in the order of their mip-0 cells (k_occ_uniform_list; nullable): work item k < n_ulist
+	// is uniform sample ulist[k], the rest are the nonuniform samples in index order
+	const uint32_t* ulist;
+	uint32_t n_ulist;
 };
+// Cell-ordered list of the uniform samples [lo, hi) (n_u <= 128^3): the uniform hash (the first try always taken) maps
+// sample i to cell ((i + step n_u) 56924617 + 96925573) mod 2^21 bijectively, so walking the cells in (Morton) order and
+// inverting gives the samples in spatially coherent order; one wave-compacted pass, list[] gets hi - lo entries
+void launch_occ_uniform_list(hipStream_t s, uint32_t n_u, uint32_t step, uint32_t lo, uint32_t hi, uint32_t* list, uint32_t* counter);
 void launch_occ_density(hipStream_t s, uint32_t L, uint32_t W, uint32_t n, const OccSampling& os, const GridLevels& gl, uint32_t valid_level,
                         const half_t* grid, const MlpPtrs& w);
 // raw SDF on a uniform grid (marching cubes input), grid points offset .. offset + n - 1 (x fastest)

@@ -850,7 +850,8 @@ __global__ void __launch_bounds__(256) k_nerf_density(uint32_t n, const float* _
 			cell = os.lo + ic;
 			grid_sample_cell(cell, os.rng_u_state, os.rng_u_inc, os.amin, os.diag, x, os.jt);
 		} else if (MODE == 2) {
-			const uint32_t g = os.lo + ic;
+			// cell-ordered uniform samples first (coherent gathers), then the nonuniform ones of the rank's range
+			const uint32_t g = os.ulist ? (ic < os.n_ulist ? os.ulist[ic] : max(os.lo, os.n_u) + (ic - os.n_ulist)) : os.lo + ic;
 			const bool uni = g < os.n_u;
 			grid_sample(uni ? os.n_u : os.n_nu, uni ? g : g - os.n_u, uni ? os.rng_u_state : os.rng_nu_state, uni ? os.rng_u_inc : os.rng_nu_inc,
 			            os.step, os.amin, os.diag, os.grid_in, os.n_cascades, uni ? -0.01f : os.thresh_nu, x, cell, os.jt);
@@ -1705,6 +1706,24 @@ void launch_nerf_density(hipStream_t s, uint32_t L, uint32_t W, uint32_t n, cons
 #define X(l, w_) if (L == l && W == w_) { k_nerf_density<l, w_, 0><<<blocks, 256, 0, s>>>(n, pos, UniformGrid{}, OccSampling{}, gl, valid_level, grid, w, density); return; }
 	NEUS_MLP_CONFIGS(X)
 #undef X
+}
+__global__ void __launch_bounds__(256) k_occ_uniform_list(uint32_t n_u, uint32_t step, uint32_t lo, uint32_t hi, uint32_t* __restrict__ list,
+                                                           uint32_t* __restrict__ counter) {
+	const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;  // < GRID3 (grid of GRID3 / 256 blocks)
+	const uint32_t lane = threadIdx.x & 63;
+	// sample of cell c: (i + step n_u) = (c - 96925573) 53369 mod 2^21 (53369 = 56924617^-1 mod 2^21)
+	const uint32_t i = (((c - 96925573u) * 53369u) - step * n_u) & (GRID3 - 1u);
+	const bool keep = i >= lo && i < hi;
+	const unsigned long long m = __ballot(keep);
+	uint32_t p0 = 0;
+	if (lane == 0 && m) p0 = atomicAdd(counter, (uint32_t)__popcll(m));
+	p0 = __shfl(p0, 0);
+	if (keep) list[p0 + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = i;
+}
+void launch_occ_uniform_list(hipStream_t s, uint32_t n_u, uint32_t step, uint32_t lo, uint32_t hi, uint32_t* list, uint32_t* counter) {
+	if (n_u > GRID3) throw std::runtime_error("launch_occ_uniform_list: more uniform samples than mip-0 cells");
+	(void)hipMemsetAsync(counter, 0, 4, s);
+	k_occ_uniform_list<<<GRID3 / 256, 256, 0, s>>>(n_u, step, lo, hi, list, counter);
 }
 void launch_occ_density(hipStream_t s, uint32_t L, uint32_t W, uint32_t n, const OccSampling& os, const GridLevels& gl, uint32_t valid_level,
                         const half_t* grid, const MlpPtrs& w) {

@@ -201,6 +201,8 @@ struct NeusTestbed {
 	// occupancy grid
 	Dev<float> density_grid, density_tmp, grid_mean, grid_partial, occ_pos, occ_density;
 	Dev<uint32_t> occ_idx;
+	Dev<uint32_t> occ_ulist;  // the cell-ordered uniform samples (+ counter), OccSampling::ulist
+	bool occ_sort = true;     // NEUS_OCC_SORT=0: uniform samples in index order (A/B reference)
 	Dev<uint8_t> bitfield;
 	Dev<uint32_t> bf_lin;   // mip-0 occupancy in (x, y, z/32) word order for the constant-step march
 	Dev<float> occ_bbox;    // world box of the occupied cells of every mip (+ stage-1 scratch): the ray generation's cull
@@ -374,6 +376,7 @@ struct NeusTestbed {
 		occ_bbox.alloc(occ_bbox_scratch_floats());
 		launch_occ_bbox(stream, bitfield.p, occ_bbox.p);
 		{ const char* e = std::getenv("NEUS_RAY_CULL"); ray_cull = !(e && e[0] == '0'); }
+		{ const char* e = std::getenv("NEUS_OCC_SORT"); occ_sort = !(e && e[0] == '0'); }
 		if (const char* e = std::getenv("NEUS_CHUNK_ENDS")) {
 			std::vector<uint32_t> v;
 			for (const char* p = e; *p;) { char* q = nullptr; const unsigned long x = std::strtoul(p, &q, 10); if (q == p) break; v.push_back((uint32_t)x); p = *q ? q + 1 : q; }
@@ -862,6 +865,14 @@ struct NeusTestbed {
 			os.grid_in = density_grid.p; os.grid_tmp = density_tmp.p;
 			os.jt = jump_table();
 			os.exclusive = exclusive ? 1u : 0u;
+			// the uniform part in cell order (spatially coherent gathers; the max splat is order-independent): one cascade
+			// of cells or fewer uniform samples, so the uniform hash is a bijection onto the cells
+			const uint32_t u_lo = std::min(lo, n_uniform), u_hi = std::min(hi, n_uniform);
+			if (!exclusive && occ_sort && u_hi > u_lo && n_uniform <= GRID3) {
+				if (!occ_ulist.p) occ_ulist.alloc(GRID3 + 1);
+				launch_occ_uniform_list(s, n_uniform, density_grid_ema_step, u_lo, u_hi, occ_ulist.p, occ_ulist.p + GRID3);
+				os.ulist = occ_ulist.p; os.n_ulist = u_hi - u_lo;
+			}
 			launch_occ_density(s, lay.L, lay.W, N, os, gl, valid, params_h.p + lay.grid_off, mlp);
 		} else {
 			launch_grid_samples(s, n_uniform, std::min(lo, n_uniform), std::min(hi, n_uniform), 0, rng_u.state, rng_u.inc, density_grid_ema_step,
