@@ -216,8 +216,9 @@ struct OccSampling {
 };
 // Cell-ordered list of the uniform samples [lo, hi) (n_u <= 128^3): the uniform hash (the first try always taken) maps
 // sample i to cell ((i + step n_u) 56924617 + 96925573) mod 2^21 bijectively, so walking the cells in (Morton) order and
-// inverting gives the samples in spatially coherent order; one wave-compacted pass, list[] gets hi - lo entries
-void launch_occ_uniform_list(hipStream_t s, uint32_t n_u, uint32_t step, uint32_t lo, uint32_t hi, uint32_t* list, uint32_t* counter);
+// inverting gives the samples in spatially coherent order; one look-back-scan pass (scan_tmp: a scan_temp_bytes state),
+// list[] gets hi - lo entries
+void launch_occ_uniform_list(hipStream_t s, uint32_t n_u, uint32_t step, uint32_t lo, uint32_t hi, uint32_t* list, void* scan_tmp);
 void launch_occ_density(hipStream_t s, uint32_t L, uint32_t W, uint32_t n, const OccSampling& os, const GridLevels& gl, uint32_t valid_level,
                         const half_t* grid, const MlpPtrs& w);
 // raw SDF on a uniform grid (marching cubes input), grid points offset .. offset + n - 1 (x fastest)

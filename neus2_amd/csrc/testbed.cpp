@@ -201,7 +201,7 @@ struct NeusTestbed {
 	// occupancy grid
 	Dev<float> density_grid, density_tmp, grid_mean, grid_partial, occ_pos, occ_density;
 	Dev<uint32_t> occ_idx;
-	Dev<uint32_t> occ_ulist;  // the cell-ordered uniform samples (+ counter), OccSampling::ulist
+	Dev<uint32_t> occ_ulist;  // the cell-ordered uniform samples, OccSampling::ulist
 	bool occ_sort = true;     // NEUS_OCC_SORT=0: uniform samples in index order (A/B reference)
 	Dev<uint8_t> bitfield;
 	Dev<uint32_t> bf_lin;   // mip-0 occupancy in (x, y, z/32) word order for the constant-step march
@@ -869,8 +869,8 @@ struct NeusTestbed {
 			// of cells or fewer uniform samples, so the uniform hash is a bijection onto the cells
 			const uint32_t u_lo = std::min(lo, n_uniform), u_hi = std::min(hi, n_uniform);
 			if (!exclusive && occ_sort && u_hi > u_lo && n_uniform <= GRID3) {
-				if (!occ_ulist.p) occ_ulist.alloc(GRID3 + 1);
-				launch_occ_uniform_list(s, n_uniform, density_grid_ema_step, u_lo, u_hi, occ_ulist.p, occ_ulist.p + GRID3);
+				if (!occ_ulist.p) occ_ulist.alloc(GRID3);
+				launch_occ_uniform_list(s, n_uniform, density_grid_ema_step, u_lo, u_hi, occ_ulist.p, scan_tmp.p);
 				os.ulist = occ_ulist.p; os.n_ulist = u_hi - u_lo;
 			}
 			launch_occ_density(s, lay.L, lay.W, N, os, gl, valid, params_h.p + lay.grid_off, mlp);
