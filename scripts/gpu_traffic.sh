@@ -5,7 +5,7 @@
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-traffic}
 export WARM=${WARM:-800} ITERS=3 V=99 K=${K:-3,7,0,5,8,1,4}
-RX="k_nerf_infer|k_scatter|k_march|k_ray_gen|k_mlp_train|k_grid_encode|k_loss_alpha|rocprim"
+RX=${RX:-"k_nerf_infer|k_scatter|k_march|k_ray_gen|k_mlp_train|k_grid_encode|k_loss_alpha|k_adam_ema|rocprim"}
 i=0
 for CNT in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_128B_sum" "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
