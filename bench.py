@@ -126,6 +126,24 @@ def kernel_table(levels):
     }
 
 
+INFER_STEPS = 10
+
+
+def step_inference(it, levels):
+    """The pre-compaction network pass as the training step runs it (progressive rounds of k_nerf_infer over their
+    work lists): bytes = (28 coords + 32 L gather + 32 output) per evaluated sample, time = the launches' summed
+    hipEvent durations; reported per launch (the rocprofv3 kernel-trace average of k_nerf_infer over the same steps)."""
+    g = 8 * levels * 4
+    n = max(1, it["launches"])
+    ms = it["ms"] / n
+    b = (28 + g + 32) * it["evaluated"] / n
+    return {"ms": round(ms, 4), "units": round(it["evaluated"] / n), "bytes": round(b), "achieved": round(b / (ms * 1e-3) / 1e9, 1),
+            "frac": round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "launches_per_step": round(it["launches"] / max(1, it["steps"]), 2),
+            "evaluated_per_step": round(it["evaluated"] / max(1, it["steps"])), "ms_per_step": round(it["ms"] / max(1, it["steps"]), 4),
+            "steps": it["steps"], "tflops": round(28672 * it["evaluated"] / (it["ms"] * 1e-3) / 1e12, 1),
+            "note": "the step's own k_nerf_infer launches (progressive rounds), hipEvents around each, timed over the steps after the timed region"}
+
+
 def kernel_rooflines(tb, levels, iters=9):
     """Per-kernel median launch duration (hipEvents on the testbed stream between `iters` back-to-back
     launches replayed on the final training state, neus_testbed_time_kernel) and the algorithmic HBM
@@ -144,25 +162,28 @@ def kernel_rooflines(tb, levels, iters=9):
 
 
 def step_roofline(d, levels, n_params, ms_per_step, steps):
-    """Whole-step roofline: B_step = 40 R + 596 Npre + 1496 Nc + 48 P + B_occ,
-    with the gather terms at L_active levels, from the counters of the timed steps (this rank). B_occ = (96 + 32 L)
-    bytes per occupancy sample + a 32 MB grid pass per update. F_step = 28,672 Npre + 92,160 Nc."""
+    """Whole-step roofline: B_step = 40 R + 28 Npre + 568 Nev + 1496 Nc + 48 P + B_occ,
+    with the gather terms at L_active levels, from the counters of the timed steps (this rank): every kept sample's
+    coordinates are written (28 B), the pre-compaction network pass reads, gathers and writes only the samples it
+    evaluates (Nev <= Npre: progressive inference skips samples past the transmittance cut-off) and the loss reads their
+    outputs (28 + 32 L + 32 + 60 B). B_occ = (96 + 32 L) bytes per occupancy sample + a 32 MB grid pass per update.
+    F_step = 28,672 Nev + 92,160 Nc."""
     g = 8 * levels * 4
-    R, npre, nc = d["rays"] / steps, d["pre"] / steps, d["train"] / steps
+    R, npre, nev, nc = d["rays"] / steps, d["pre"] / steps, d["evaluated"] / steps, d["train"] / steps
     occ = (d["occ_samples"] * (96 + g) + d["occ_updates"] * 32e6) / steps
-    b = 40 * R + (28 + 28 + g + 32 + 60) * npre + (60 + 28 + g + 32 + 32 + 2 * g) * nc + 48 * n_params + occ
-    f = 28672 * npre + 92160 * nc
+    b = 40 * R + 28 * npre + (28 + g + 32 + 60) * nev + (60 + 28 + g + 32 + 32 + 2 * g) * nc + 48 * n_params + occ
+    f = 28672 * nev + 92160 * nc
     t = ms_per_step * 1e-3
     return {"bound": "hbm", "achieved": round(b / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(b / t / 1e9 / HBM_PEAK_GBS, 4), "bytes_per_step": round(b), "flops_per_step": round(f),
             "mfma_tflops": round(f / t / 1e12, 1), "mfma_frac": round(f / t / 1e12 / MFMA_PEAK_TFLOPS, 4),
-            "per_step": {"rays": round(R), "pre_samples": round(npre), "train_samples": round(nc),
+            "per_step": {"rays": round(R), "pre_samples": round(npre), "evaluated_samples": round(nev), "train_samples": round(nc),
                          "occ_samples": round(d["occ_samples"] / steps), "params": n_params}}
 
 
 def work_counters(st):
-    return {"rays": st["rays_total"], "pre": st["pre_samples_total"], "occ_samples": st["occ_samples_total"],
-            "occ_updates": st["occ_updates"]}
+    return {"rays": st["rays_total"], "pre": st["pre_samples_total"], "evaluated": st["evaluated_samples_total"],
+            "occ_samples": st["occ_samples_total"], "occ_updates": st["occ_updates"], "progressive": st["progressive_steps"]}
 
 
 def free_port():
@@ -287,10 +308,17 @@ def main():
     ms_step = elapsed / args.steps * 1e3
     lay = tb.layout()
     levels = min(st["valid_level"] + 1, lay["n_levels"])
-    # per-kernel timing after the timed region, on its final state (hipEvents on the testbed stream)
+    # the dominant kernel as the training step runs it: after the timed region, INFER_STEPS more steps with hipEvents
+    # around each pre-compaction network launch (the progressive rounds' k_nerf_infer), the samples they evaluated
+    # from the device counter
+    it = tb.infer_timing(INFER_STEPS)
+    inf = step_inference(it, levels)
+    # per-kernel timing of the other kernels after that, on the final state (hipEvents on the testbed stream)
     kern = kernel_rooflines(tb, levels)
-    dom = max(kern, key=lambda k: kern[k]["ms"])
-    dk = kern[dom]
+    per_step = {k: v["ms"] for k, v in kern.items() if k != "inference"}
+    per_step["inference_step"] = inf["ms_per_step"]
+    dom = max(per_step, key=per_step.get)
+    dk = inf if dom == "inference_step" else kern[dom]
     mlp = ("mlp_train_rgb", "mlp_train_density")
     mlp_ms = sum(kern[k]["ms"] for k in mlp)
     tr = traffic_table()
@@ -314,7 +342,9 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": dk["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": dk["frac"], "traffic": measured_traffic(dom, levels), "bytes_per_launch": dk["bytes"],
                      "units_per_launch": dk["units"], "launch_ms": dk["ms"], "levels_active": levels,
-                     "traffic_source": traffic_source(tr, dom, levels)},
+                     "traffic_source": traffic_source(tr, dom, levels),
+                     **({k: inf[k] for k in ("launches_per_step", "evaluated_per_step", "ms_per_step", "steps", "note")}
+                        if dom == "inference_step" else {})},
         # the whole step against the HBM roofline and its MFMA rate
         "roofline_step": step_roofline(d, levels, lay["n_params"], ms_step, args.steps),
         # the training MLP kernels (fwd recompute + 1st / 2nd-order backward + weight gradients) against the MFMA peak
@@ -324,6 +354,7 @@ def main():
         # memory-side line traffic (PMC, profiles/traffic.json) over the same launch: the hashed levels' 4-B corner
         # gathers each move a 128-B line from the Infinity Cache, so this, not the algorithmic rate, is what binds
         "line_traffic": line_traffic(measured_traffic(dom, levels), dk["ms"], dk["bytes"]),
+        "progressive_steps_timed": d["progressive"],
         "non_rollover_fraction": round(d["trained_real"] / max(1, batch * args.steps), 4),
         "kernels": kern,
         "loss": st["ray_loss"],

@@ -121,6 +121,12 @@ typedef struct NeusTrainStats {
 	uint64_t rays_total;                      /* rays marched (sum of rays_per_batch) */
 	uint64_t occ_samples_total;               /* occupancy-grid samples evaluated by this rank (its shard of each update) */
 	uint32_t occ_updates;                     /* occupancy-grid updates (update_density_grid_nerf calls) */
+	uint32_t health_flags;                    /* device health bits (sticky): 1 the occupancy march met a non-finite / negative t,
+	                                           * 2 a look-back scan gave up waiting; either makes neus_testbed_train fail */
+	uint64_t evaluated_samples_total;         /* samples the pre-compaction network pass evaluated (progressive inference: the
+	                                           * rounds' work lists, a subset of the kept samples) */
+	uint64_t progressive_steps;               /* steps that ran progressive (multi-round) inference */
+	uint32_t evaluated_samples_last;          /* samples the last step's pre-compaction pass evaluated */
 	uint32_t reserved_;
 } NeusTrainStats;
 
@@ -305,6 +311,20 @@ int neus_debug_scatter_stats(NeusTestbed* tb, uint64_t* records_per_level, uint3
  * of n u32 on `hip_stream`, `reps` launches on one fresh state (the epoch re-arm), synchronous; failures = bounded-wait
  * give-ups (0 expected). */
 int neus_debug_exclusive_scan(void* hip_stream, const uint32_t* in, uint32_t* out, uint32_t n, int reps, uint32_t* failures);
+/* Test hook of the scan's bounded wait: the same scan with its first tile never run, so every later tile gives up
+ * waiting (n > 4096 elements); failures = the give-ups counted (nonzero expected). */
+int neus_debug_scan_giveup(void* hip_stream, const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* failures);
+/* Test hook of the training step's health check: raises device health bits (1 march t, 2 scan give-up) in the
+ * testbed's step state / scan state, as the kernels would; the next loss readback makes neus_testbed_train fail. */
+int neus_debug_inject_health(NeusTestbed* tb, uint32_t flags);
+/* Test hook: every training step fills every CU's LDS with `pattern` (0: off) before its march write kernel. */
+int neus_debug_set_lds_fill(NeusTestbed* tb, uint32_t pattern);
+/* neus_sample_rays (rank 0 of 1) plus the progressive round-0 work list the training step's march writes (the first
+ * min(n, chunk_end) samples of every kept ray, in ray order; list: device, max_samples u32, list_len: host u32), with
+ * lds_fill != 0 every CU's LDS filled with that pattern between the scan and the write kernel (stale-LDS test). */
+int neus_debug_sample_rays_round0(NeusTestbed* tb, void* stream, uint32_t n_rays, uint32_t n_rays_total, uint64_t rng_state, uint64_t rng_inc,
+                                  uint32_t max_samples, const uint8_t* bitfield, float* rays, uint32_t* numsteps, float* coords,
+                                  uint32_t* counters_out, uint32_t chunk_end, uint32_t* list, uint32_t* list_len, uint32_t lds_fill);
 int neus_testbed_stream(NeusTestbed* tb, void** hip_stream);
 int neus_testbed_synchronize(NeusTestbed* tb);
 /* Per-phase step timing with hipEvents recorded on the testbed stream (profiling on), mean ms per step:
@@ -317,6 +337,12 @@ int neus_testbed_synchronize(NeusTestbed* tb);
 #define NEUS_N_PHASES 10
 int neus_testbed_set_profiling(NeusTestbed* tb, int on);
 int neus_testbed_kernel_times(NeusTestbed* tb, float* ms_out /* NEUS_N_PHASES + 3 entries */);
+/* Inference timing of the training step as it runs: with it on, every pre-compaction network launch of a step (the
+ * one pass, or each progressive round's k_nerf_infer) is bracketed by hipEvents on the testbed stream and the host
+ * waits for them after the step (a measurement pass, not for timed runs). Totals since it was turned on: summed launch
+ * ms, launches, steps; the samples those launches evaluated are NeusTrainStats::evaluated_samples_total's growth. */
+int neus_testbed_set_infer_timing(NeusTestbed* tb, int on);
+int neus_testbed_infer_timing(NeusTestbed* tb, double* ms_total, uint64_t* launches, uint64_t* steps);
 
 /* ------------------------------------------------------------------ data parallel (RCCL over xGMI) */
 int neus_nccl_unique_id(uint8_t* out /* 128 bytes */);

@@ -166,17 +166,34 @@ struct StepState {
 	// work counters since step 0 (this rank), for the whole-step roofline (bench.py roofline_step)
 	unsigned long long pre_total;     // pre-compaction samples evaluated: sum of n_kept
 	unsigned long long rays_total;    // rays marched: sum of rays_per_batch
-	unsigned long long pad_[6];
+	unsigned long long eval_total;    // samples the pre-compaction network pass evaluated (progressive rounds: their lists)
+	uint32_t fail_flags;              // device health: STEP_FAIL_* bits (sticky; the host raises on the next readback)
+	uint32_t eval_last;               // samples evaluated by the last step's pre-compaction pass
+	unsigned long long prog_steps;    // steps that ran progressive (multi-round) inference
+	unsigned long long pad_[3];
 };
 static_assert(sizeof(StepState) == 128, "StepState is one 128-B record");
+// fail_flags bits: a march step saw a non-finite or negative t (step_until's precondition; the ray is ended there);
+// a look-back scan gave up waiting (set by the host from the scan state's counter)
+constexpr uint32_t STEP_FAIL_MARCH_T = 1u, STEP_FAIL_SCAN = 2u;
 
 // Counters::update_after_training (testbed_nerf.cu:3399-3438) at the end of a step: one thread (k_step_counters, or
-// the Adam launch's block 0)
-__device__ __forceinline__ void step_counters_update(StepState* st, uint32_t target_batch, uint32_t max_samples, uint32_t world, uint32_t fixed_rays) {
+// the Adam launch's block 0). eval_cnt: the progressive rounds' list lengths (n_eval of them; null: one pass over the
+// kept samples)
+__device__ __forceinline__ void step_counters_update(StepState* st, uint32_t target_batch, uint32_t max_samples, uint32_t world, uint32_t fixed_rays,
+                                                     const uint32_t* eval_cnt = nullptr, uint32_t n_eval = 0) {
 	const uint32_t R = st->rays_per_batch;
 	st->n_rays_total += R * world;  // n_rays_total
 	st->pre_total += st->n_kept;
 	st->rays_total += R;
+	uint32_t ev = st->n_kept;
+	if (eval_cnt) {
+		ev = 0;
+		for (uint32_t k = 0; k < n_eval; ++k) ev += eval_cnt[k];
+		++st->prog_steps;
+	}
+	st->eval_last = ev;
+	st->eval_total += ev;
 	// next step's first march pass: the slots up to this step's kept extent plus a margin (all slots when every
 	// ray with samples fitted under this step's cap)
 	const bool fit = st->numsteps_counter <= st->max_inference;

@@ -163,7 +163,7 @@ void launch_adam_bias_table(hipStream_t s, float beta1, float beta2, float* tab)
 // The Adam launch's two riders (each optional): the step-end counters (k_step_counters' work, done by thread 0 of block
 // 0) and the transposed / permuted fp16 copies of the MLP matrices (prepare_weights), written by the threads that
 // update the matrix parameters (the launch after it no longer has to re-transpose)
-struct StepCounterArgs { StepState* st; uint32_t target_batch, max_samples, world, fixed_rays; };
+struct StepCounterArgs { StepState* st; uint32_t target_batch, max_samples, world, fixed_rays; const uint32_t* eval_cnt; uint32_t n_eval; };
 struct AdamTranspose {
 	uint32_t n;                                    // matrices (0: none)
 	uint32_t off[5], rows[5], cols[5];             // parameter offset and shape of matrix j
@@ -270,7 +270,9 @@ struct Round0List { uint32_t e1; uint32_t* c0; uint32_t* list; uint32_t* counter
 // k_march_write; round0 nullable
 void launch_march_write(hipStream_t s, uint32_t cap, StepState* st, const DevDataset& ds, const float* rays, const MarchWork& mw, const uint32_t* nreq,
                         uint32_t* base, uint32_t* numsteps, float* coords, uint32_t* sample_ray, uint32_t sample_cap, void* scan_temp,
-                        const Round0List* round0 = nullptr);
+                        const Round0List* round0 = nullptr, uint32_t lds_fill = 0 /* tests: garbage-fill LDS before the write kernel */);
+constexpr uint32_t FILL_LDS_BYTES = 40 * 1024;
+void launch_fill_lds(hipStream_t s, uint32_t pattern);
 void debug_launch_march_stats(hipStream_t s, uint32_t n_rays, const float* rays, const float* tstart, const uint32_t* lin, const DevDataset& ds,
                               const uint8_t* bf, uint32_t* out);
 // dt_const: every sample's dt is MIN_CONE_STEPSIZE (cone angle 0, coordinates from k_march_write): the kernel
@@ -294,7 +296,8 @@ void launch_loss_grad(hipStream_t s, uint32_t cap_samples, const StepState* st, 
 void debug_launch_loss_scan(hipStream_t s, int variant, uint32_t cap_rays, const uint32_t* numsteps, const LossWork& w, uint32_t* ccount);
 void launch_ray_index(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, StepState* st, uint32_t* sample_ray, uint32_t* rbase);
 void launch_rollover(hipStream_t s, uint32_t n_elements, const StepState* st, float* coords, half_t* dL_dout);
-void launch_step_counters(hipStream_t s, StepState* st, uint32_t target_batch, uint32_t max_samples, uint32_t world, uint32_t fixed_rays);
+void launch_step_counters(hipStream_t s, StepState* st, uint32_t target_batch, uint32_t max_samples, uint32_t world, uint32_t fixed_rays,
+                          const uint32_t* eval_cnt = nullptr, uint32_t n_eval = 0);
 // render.hip (rays: RenderRay records, render_ray_bytes() each)
 size_t render_ray_bytes();
 void launch_render_init(hipStream_t s, const RenderCamera& cam, uint32_t sample_index, const DevDataset& ds, const uint8_t* bf, const uint32_t* lin,
@@ -335,6 +338,9 @@ void scan_temp_reset(hipStream_t s, void* temp);
 // the look-back tag of the next scan launch on this temp buffer (scan.hip; used by the fused scans of march.hip)
 uint32_t scan_next_tag(void* temp);
 uint32_t scan_failures(void* temp);
+void scan_temp_release(void* temp);  // forget the buffer's tag counter (it is being freed)
+// tests: the scan with its first tile never published, so every later tile's look-back gives up (a failure count)
+void debug_scan_skip_first_tile(hipStream_t s, void* temp, const uint32_t* in, uint32_t* out, uint32_t n);
 void launch_exclusive_scan(hipStream_t s, void* temp, size_t temp_bytes, const uint32_t* in, uint32_t* out, uint32_t n);
 void launch_sum_f32(hipStream_t s, void* temp, size_t temp_bytes, const float* in, float* out, uint32_t n);
 // optim.hip

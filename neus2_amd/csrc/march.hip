@@ -178,7 +178,7 @@ __device__ __forceinline__ void visit(Visits& v, uint32_t kb, uint32_t ke) {
 template <bool FAST>
 __device__ __forceinline__ bool march_event(const DevDataset& ds, const uint8_t* __restrict__ bf, const uint32_t* __restrict__ lin,
                                             const MarchRay& mr, float& t, uint32_t& k, uint32_t k_end, SegAcc& acc, Visits& vis,
-                                            uint2* __restrict__ rec, uint32_t dbg = 0) {
+                                            uint2* __restrict__ rec, uint32_t dbg = 0, uint32_t* fail = nullptr) {
 	const uint32_t kb = k;
 	if (FAST) {
 		float pos[3];
@@ -226,7 +226,9 @@ __device__ __forceinline__ bool march_event(const DevDataset& ds, const uint8_t*
 		}
 		const float t_target = t + fmaxf(ldexpf(tn, -(int)(7 - mip)), 0.0f);
 		t += MIN_CONE_STEPSIZE; ++k;
-		step_until(t, k, t_target, 0xffffffffu, MIN_CONE_STEPSIZE);  // do { t += dt; ++k; } while (t < t_target)
+		// do { t += dt; ++k; } while (t < t_target); bounded: at cone angle 0 the box diagonal is NERF_STEPS steps, so
+		// no skip spans 4 NERF_STEPS and the bound only ends a corrupted t (the ray is ended, the step reports it)
+		if (!step_until(t, k, t_target, k + 4 * NERF_STEPS, MIN_CONE_STEPSIZE)) { step_fail(fail, STEP_FAIL_MARCH_T); return false; }
 		return true;
 	} else {
 		float dt, pos[3];
@@ -261,10 +263,11 @@ constexpr uint32_t FINISHED = 0xffffffffu;
 template <bool FAST>
 __device__ __forceinline__ void march_segment(const DevDataset& ds, const uint8_t* __restrict__ bf, const uint32_t* __restrict__ lin,
                                               const MarchRay& mr, float& t, uint32_t& k, uint32_t k_end, SegAcc& acc, Visits& vis,
-                                              uint2* __restrict__ rec, uint32_t rec_cap, uint32_t* n_ev = nullptr, uint32_t dbg = 0) {
+                                              uint2* __restrict__ rec, uint32_t rec_cap, uint32_t* n_ev = nullptr, uint32_t dbg = 0,
+                                              uint32_t* fail = nullptr) {
 	while (k < k_end) {
 		if (n_ev) ++*n_ev;
-		if (acc.nrec + 1 >= rec_cap || !march_event<FAST>(ds, bf, lin, mr, t, k, k_end, acc, vis, rec, dbg)) { k = FINISHED; break; }
+		if (acc.nrec + 1 >= rec_cap || !march_event<FAST>(ds, bf, lin, mr, t, k, k_end, acc, vis, rec, dbg, fail)) { k = FINISHED; break; }
 	}
 	seg_flush(rec, acc, dbg);
 }
@@ -338,7 +341,7 @@ __global__ void __launch_bounds__(256) MARCH_OCC k_march(uint32_t cap_rays, uint
 		const bool active = t0 >= 0.f && (g == 0 || split);
 		if (active && g > 0) {
 			const float t_g = t0 + span * ((float)g / (float)MG);
-			if (FAST) step_until(t, k, t_g, 4 * NERF_STEPS, MIN_CONE_STEPSIZE);
+			if (FAST && !step_until(t, k, t_g, 4 * NERF_STEPS, MIN_CONE_STEPSIZE)) step_fail(&st->fail_flags, STEP_FAIL_MARCH_T);
 			else while (t < t_g && k < 4 * NERF_STEPS) { t += calc_dt(t, ds.cone_angle); ++k; }
 		}
 		stamp(1);
@@ -351,7 +354,7 @@ __global__ void __launch_bounds__(256) MARCH_OCC k_march(uint32_t cap_rays, uint
 		float et = t;
 		uint32_t ek = active ? k : FINISHED;
 		uint32_t n_ev = 0;
-		if (active) { march_segment<FAST>(ds, bitfield, lin, mr, et, ek, k_end, acc, vis, rec, SEG_CAP, &n_ev, mw.dbg); }
+		if (active) { march_segment<FAST>(ds, bitfield, lin, mr, et, ek, k_end, acc, vis, rec, SEG_CAP, &n_ev, mw.dbg, &st->fail_flags); }
 		stamp(2);
 		// segment order: lane g joins the exit of lane g - 1
 		uint32_t vk = k;   // first valid step of this segment
@@ -375,7 +378,7 @@ __global__ void __launch_bounds__(256) MARCH_OCC k_march(uint32_t cap_rays, uint
 				if (redo) {
 					acc = SegAcc{0.f, 0u, 0u, 0u, 0u}; vis.n = 0;
 					et = pt; ek = pk; vk = pk;
-					march_segment<FAST>(ds, bitfield, lin, mr, et, ek, k_end, acc, vis, rec, SEG_CAP);
+					march_segment<FAST>(ds, bitfield, lin, mr, et, ek, k_end, acc, vis, rec, SEG_CAP, nullptr, 0, &st->fail_flags);
 				}
 			}
 		}
@@ -544,7 +547,7 @@ __device__ __forceinline__ uint32_t last_le(const uint32_t* __restrict__ a, uint
 	while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (a[mid] <= q) lo = mid; else hi = mid; }
 	return lo;
 }
-__global__ void __launch_bounds__(256) k_march_write(uint32_t cap_rays, const StepState* __restrict__ st, DevDataset ds,
+__global__ void __launch_bounds__(256) k_march_write(uint32_t cap_rays, StepState* __restrict__ st, DevDataset ds,
                                                      const float* __restrict__ rays, const MarchWork mw,
                                                      const uint32_t* __restrict__ nreq, const uint32_t* __restrict__ base,
                                                      float* __restrict__ coords, uint32_t* __restrict__ sample_ray, Round0List r0) {
@@ -624,7 +627,7 @@ __global__ void __launch_bounds__(256) k_march_write(uint32_t cap_rays, const St
 			float t = __uint_as_float(s_t0[q - q0]);
 			if (ds.cone_angle == 0.0f) {  // the run's u constant steps in a few integer-domain jumps (exact, step_until)
 				uint32_t kk = 0;
-				step_until(t, kk, __int_as_float(0x7f800000), s_u[q - q0], MIN_CONE_STEPSIZE);
+				if (!step_until(t, kk, __int_as_float(0x7f800000), s_u[q - q0], MIN_CONE_STEPSIZE)) step_fail(&st->fail_flags, STEP_FAIL_MARCH_T);
 			} else
 			for (uint32_t u = s_u[q - q0]; u > 0; --u) t += ds.cone_angle == 0.0f ? MIN_CONE_STEPSIZE : calc_dt(t, ds.cone_angle);
 			const float o[3] = {s_ray[0][r], s_ray[1][r], s_ray[2][r]}, dir[3] = {s_ray[3][r], s_ray[4][r], s_ray[5][r]};
@@ -1208,9 +1211,10 @@ __global__ void k_rollover(uint32_t n_elements, const StepState* __restrict__ st
 // Counters::update_after_training (testbed_nerf.cu:3399-3438) + the next step's max_inference
 // (testbed_nerf.cu:3771-3776) + n_rays_total (testbed_nerf.cu:3784-3790). `world` divides the
 // all-reduced counters so every rank adapts R identically.
-__global__ void k_step_counters(StepState* st, uint32_t target_batch, uint32_t max_samples, uint32_t world, uint32_t fixed_rays) {
+__global__ void k_step_counters(StepState* st, uint32_t target_batch, uint32_t max_samples, uint32_t world, uint32_t fixed_rays,
+                                const uint32_t* eval_cnt, uint32_t n_eval) {
 	if (threadIdx.x != 0 || blockIdx.x != 0) return;
-	step_counters_update(st, target_batch, max_samples, world, fixed_rays);
+	step_counters_update(st, target_batch, max_samples, world, fixed_rays, eval_cnt, n_eval);
 }
 
 // ---------------------------------------------------------------- host launchers
@@ -1240,15 +1244,28 @@ void launch_march_count(hipStream_t s, uint32_t cap, uint32_t max_samples, StepS
 		}
 	}
 }
+// Test hook: every CU's LDS filled with `pattern` by resident workgroups (volatile stores: kept), so that a kernel that
+// reads LDS it never wrote sees garbage, not the zeros of a fresh device
+__global__ void __launch_bounds__(256) k_fill_lds(uint32_t pattern) {
+	extern __shared__ uint32_t s_fill[];
+	volatile uint32_t* v = s_fill;
+	for (uint32_t i = threadIdx.x; i < FILL_LDS_BYTES / 4; i += 256) v[i] = pattern;
+}
+void launch_fill_lds(hipStream_t s, uint32_t pattern) {
+	// 40 KB per workgroup, 4 resident per CU: the whole 160 KB of every CU (256 CUs), twice over
+	k_fill_lds<<<2048, 256, FILL_LDS_BYTES, s>>>(pattern);
+}
+
 void launch_march_write(hipStream_t s, uint32_t cap, StepState* st, const DevDataset& ds, const float* rays, const MarchWork& mw, const uint32_t* nreq,
                         uint32_t* base, uint32_t* numsteps, float* coords, uint32_t* sample_ray, uint32_t sample_cap, void* scan_temp,
-                        const Round0List* round0) {
+                        const Round0List* round0, uint32_t lds_fill) {
 	const Round0List r0 = round0 ? *round0 : Round0List{0u, nullptr, nullptr, nullptr, 0u};
 	if (cap % 4 || ((uintptr_t)nreq | (uintptr_t)base | (uintptr_t)numsteps | (uintptr_t)r0.c0) & 15)
 		throw std::runtime_error("launch_march_write: ray buffers must be 16-B aligned, cap a multiple of 4");
 	const uint32_t tiles = (cap + SCAN_TILE - 1) / SCAN_TILE;
 	if (tiles > SCAN_MAX_TILES) throw std::runtime_error("launch_march_write: too many ray slots");
 	k_march_scan<<<tiles, SCAN_THREADS, 0, s>>>(cap, st, nreq, base, numsteps, (ScanState*)scan_temp, scan_next_tag(scan_temp), r0);
+	if (lds_fill) launch_fill_lds(s, lds_fill);  // tests: the write kernel finds garbage in every CU's LDS
 	// one block per WRITE_CHUNK samples of the largest possible kept extent (max_inference <= sample_cap)
 	k_march_write<<<std::max<uint32_t>(1, (sample_cap + WRITE_CHUNK - 1) / WRITE_CHUNK), 256, 0, s>>>(cap, st, ds, rays, mw, nreq, base, coords, sample_ray,
 	                                                                                                      r0);
@@ -1310,8 +1327,9 @@ void launch_ray_index(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps
 void launch_rollover(hipStream_t s, uint32_t n_elements, const StepState* st, float* coords, half_t* dL_dout) {
 	k_rollover<<<std::max<uint32_t>(1, std::min<uint32_t>((n_elements + 255) / 256, 2048)), 256, 0, s>>>(n_elements, st, coords, dL_dout);
 }
-void launch_step_counters(hipStream_t s, StepState* st, uint32_t target_batch, uint32_t max_samples, uint32_t world, uint32_t fixed_rays) {
-	k_step_counters<<<1, 64, 0, s>>>(st, target_batch, max_samples, world, fixed_rays);
+void launch_step_counters(hipStream_t s, StepState* st, uint32_t target_batch, uint32_t max_samples, uint32_t world, uint32_t fixed_rays,
+                          const uint32_t* eval_cnt, uint32_t n_eval) {
+	k_step_counters<<<1, 64, 0, s>>>(st, target_batch, max_samples, world, fixed_rays, eval_cnt, n_eval);
 }
 
 } // namespace neus

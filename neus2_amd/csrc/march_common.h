@@ -49,7 +49,13 @@ __device__ __forceinline__ int mip_from_dt(float dt, float px, float py, float p
 // same increment prove the stretch linear; it is then jumped in the integer domain (positive floats order as their
 // bit patterns) up to the first step at or past target, the step cap or the binade's end, whichever comes first.
 // Single exact steps cross binades and settle the parity.
-__device__ __forceinline__ void step_until(float& t, uint32_t& k, float target, uint32_t kmax, float dt) {
+// Precondition checked: with t negative or not finite (or dt <= 0) the jumps' integer arithmetic is meaningless, so the
+// plain loop runs instead (bounded by kmax) and false is returned; the caller ends the ray and raises STEP_FAIL_MARCH_T.
+__device__ __forceinline__ bool step_until(float& t, uint32_t& k, float target, uint32_t kmax, float dt) {
+	if (!(t >= 0.0f) || !(t < __builtin_huge_valf()) || !(dt > 0.0f)) {
+		while (t < target && k < kmax) { t += dt; ++k; }
+		return false;
+	}
 	while (t < target && k < kmax) {
 		const float t2 = t + dt;
 		const uint32_t b = __float_as_uint(t), b2 = __float_as_uint(t2), ex = b & 0x7f800000u;
@@ -64,6 +70,11 @@ __device__ __forceinline__ void step_until(float& t, uint32_t& k, float target, 
 		t = __uint_as_float(b + j * inc);
 		k += j;
 	}
+	return true;
+}
+// raises a device health bit (vector atomic on the step state; rare path)
+__device__ __forceinline__ void step_fail(uint32_t* flags, uint32_t bit) {
+	if (flags) atomicOr(flags, bit);
 }
 __device__ __forceinline__ float signf(float x) { return copysignf(1.0f, x); }
 __device__ __forceinline__ float advance_to_next_voxel(float t, float cone, const float pos[3], const float dir[3], const float idir[3], uint32_t res) {

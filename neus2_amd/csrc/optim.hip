@@ -78,7 +78,7 @@ __global__ void __launch_bounds__(256) k_adam_ema(AdamParams p, float* __restric
                                                   const float* __restrict__ grads, float* __restrict__ m1, float* __restrict__ m2,
                                                   uint32_t* __restrict__ steps, float* __restrict__ ema_tmp, half_t* __restrict__ ema_h,
                                                   StepCounterArgs sc, AdamTranspose tr) {
-	if (sc.st && blockIdx.x == 0 && threadIdx.x == 0) step_counters_update(sc.st, sc.target_batch, sc.max_samples, sc.world, sc.fixed_rays);
+	if (sc.st && blockIdx.x == 0 && threadIdx.x == 0) step_counters_update(sc.st, sc.target_batch, sc.max_samples, sc.world, sc.fixed_rays, sc.eval_cnt, sc.n_eval);
 	const uint32_t ng = p.n / 4;
 	for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < ng; g += gridDim.x * blockDim.x) {
 		const uint32_t i0 = 4 * g;
@@ -383,7 +383,7 @@ __global__ void __launch_bounds__(256) k_occ_bbox_final(const float* __restrict_
 static inline uint32_t nblk(uint64_t n, uint32_t cap = 4096) { return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, cap)); }
 void launch_adam_ema(hipStream_t s, const AdamParams& p, float* weights_fp, half_t* weights_h, const float* grads, float* m1, float* m2,
                      uint32_t* steps, float* ema_tmp, half_t* ema_h, const StepCounterArgs* counters, const AdamTranspose* tr) {
-	const StepCounterArgs sc = counters ? *counters : StepCounterArgs{nullptr, 0u, 0u, 1u, 0u};
+	const StepCounterArgs sc = counters ? *counters : StepCounterArgs{nullptr, 0u, 0u, 1u, 0u, nullptr, 0u};
 	AdamTranspose t{};
 	if (tr) t = *tr;
 	k_adam_ema<<<nblk(std::max<uint64_t>(1, p.n / 4), 16384), 256, 0, s>>>(p, weights_fp, weights_h, grads, m1, m2, steps, ema_tmp, ema_h, sc, t);

@@ -10,14 +10,16 @@
 #include "scan_lookback.h"
 #include <hipcub/hipcub.hpp>
 #include <mutex>
+#include <stdexcept>
 #include <unordered_map>
 
 namespace neus {
 
 __global__ void __launch_bounds__(SCAN_THREADS) k_scan_lookback(const uint32_t* in, uint32_t* out, uint32_t n, ScanState* __restrict__ st, uint32_t vec,
-                                                                uint32_t tag) {
+                                                                uint32_t tag, uint32_t tile_base) {
 	__shared__ uint32_t s_prefix, s_wsum[SCAN_THREADS / 64];
-	const ScanTile tl = scan_tile(tag);
+	ScanTile tl = scan_tile(tag);
+	tl.tile += tile_base;  // 0 (tests: 1, the first tile never runs)
 	const size_t b0 = (size_t)tl.tile * SCAN_TILE + (size_t)threadIdx.x * SCAN_ITEMS;
 	uint32_t v[SCAN_ITEMS];
 	scan_load16(in, b0, n, vec != 0, v);
@@ -63,12 +65,21 @@ uint32_t scan_failures(void* temp) {
 	if (temp) (void)hipMemcpy(&f, (const char*)temp + offsetof(ScanState, fail), 4, hipMemcpyDeviceToHost);
 	return f;
 }
+void scan_temp_release(void* temp) {
+	std::lock_guard<std::mutex> g(g_tag_mu);
+	g_tags.erase(temp);
+}
+void debug_scan_skip_first_tile(hipStream_t s, void* temp, const uint32_t* in, uint32_t* out, uint32_t n) {
+	const uint32_t tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+	if (tiles < 2 || tiles > SCAN_MAX_TILES) throw std::runtime_error("debug_scan_skip_first_tile: needs 2 .. SCAN_MAX_TILES tiles");
+	k_scan_lookback<<<tiles - 1, SCAN_THREADS, 0, s>>>(in, out, n, (ScanState*)temp, 0u, scan_next_tag(temp), 1u);
+}
 void launch_exclusive_scan(hipStream_t s, void* temp, size_t temp_bytes, const uint32_t* in, uint32_t* out, uint32_t n) {
 	if (n == 0) return;
 	const uint32_t tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
 	if (tiles <= SCAN_MAX_TILES) {
 		const uint32_t vec = ((((uintptr_t)in) | ((uintptr_t)out)) & 15u) == 0 ? 1u : 0u;
-		k_scan_lookback<<<tiles, SCAN_THREADS, 0, s>>>(in, out, n, (ScanState*)temp, vec, scan_next_tag(temp));
+		k_scan_lookback<<<tiles, SCAN_THREADS, 0, s>>>(in, out, n, (ScanState*)temp, vec, scan_next_tag(temp), 0u);
 		return;
 	}
 	size_t tb = temp_bytes - SCAN_STATE_BYTES;

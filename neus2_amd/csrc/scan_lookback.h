@@ -3,10 +3,11 @@
 // A launch scans 4096-element tiles (256 threads x 16 consecutive elements), tile = blockIdx.x. Each tile publishes an
 // 8-byte {flag, tag, value} word with an agent-scope atomic store (the data is the flag: no fence pairs); its first
 // wave reads up to 64 predecessors' words per pass, relaxed, until every word of the window carries this launch's tag,
-// and sums back to the nearest inclusive prefix. The launch's blocks are dispatched in order after the previous kernel
-// on the stream has drained, and a scan launch of up to SCAN_MAX_TILES 256-thread blocks is resident at once, so a
-// predecessor is never waiting for a slot; the spin is bounded anyway (a corrupted state gives a wrong scan and a
-// failure count, not a hang). The tag is a per-state launch counter kept on the host (scan_next_tag), so a word left by
+// and sums back to the nearest inclusive prefix. Forward progress rests on in-order workgroup dispatch: the blocks of a
+// launch are dispatched in blockIdx order, so every predecessor of a spinning tile has been dispatched (it is running or
+// done) and none waits for the spinning tile's slot. (Residency is not the argument: SCAN_MAX_TILES blocks need not all
+// fit at once.) The spin is bounded anyway: a give-up counts in ScanState::fail, which the training step reads back and
+// raises as an error (testbed.cpp health_raise), so a wrong scan never passes silently. The tag is a per-state launch counter kept on the host (scan_next_tag), so a word left by
 // an earlier launch never matches and the state needs no per-call memset: it is zeroed once after allocation
 // (scan_temp_reset). Every shared word is a global-address-space agent-scope access (sc1).
 #pragma once

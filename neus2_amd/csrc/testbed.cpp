@@ -8,6 +8,7 @@
 //   * fp32 gradients and master weights, fp16 weights for the kernels (the reference keeps fp16
 //     gradients), RCCL all-reduce of the gradient buffer for data parallelism over ray batches.
 #include "kernels.h"
+#include "scan_lookback.h"
 #include "json_lite.h"
 #include "../../include/neus2_hip.h"
 
@@ -55,6 +56,13 @@ template <class T> struct Dev {
 	}
 	void release() { if (p) (void)hipFree(p); p = nullptr; n = 0; }
 	~Dev() { release(); }
+};
+// A scan temp buffer (scan_temp_bytes: look-back state + hipCUB scratch): its host-side launch tag (scan.hip) is dropped
+// with the buffer
+struct ScanTemp : Dev<uint8_t> {
+	void alloc(size_t k) { if (k <= n && p) return; release(); Dev<uint8_t>::alloc(k); }
+	void release() { if (p) scan_temp_release(p); Dev<uint8_t>::release(); }
+	~ScanTemp() { release(); }
 };
 
 constexpr uint32_t MAX_RAYS = 1u << 18;  // testbed_nerf.cu:3435 cap on rays_per_batch
@@ -174,7 +182,8 @@ struct NeusTestbed {
 	Dev<half_t> wT_ema;
 	MlpPtrs mlp_ema{};
 	// renderer workspace (NerfTracer, testbed_nerf.cu:2397-2630)
-	Dev<uint8_t> r_rays[2], r_scan_tmp;
+	Dev<uint8_t> r_rays[2];
+	ScanTemp r_scan_tmp;
 	Dev<uint32_t> r_flags, r_base, r_alive;
 	Dev<float> r_coords, r_coords_def;
 	Dev<half_t> r_out;
@@ -183,7 +192,7 @@ struct NeusTestbed {
 	// marching cubes workspace and the last mesh (Testbed::m_mesh, testbed.h:596-610)
 	Dev<float> mc_density, mesh_v;
 	Dev<uint32_t> mc_vidx, mc_cnt, mesh_f;
-	Dev<uint8_t> mc_scan_tmp;
+	ScanTemp mc_scan_tmp;
 	size_t mc_scan_bytes = 0;
 	uint32_t mesh_nv = 0, mesh_nt = 0;
 	// dynamic scenes (testbed.h:455-477, 889-890): frame, phase flags, the DeltaNetwork state on the device,
@@ -211,6 +220,7 @@ struct NeusTestbed {
 	bool bias_conv = false;
 	Dev<uint32_t> dbg_enc;  // debug timing only (neus_debug_time_kernel 11): [L][16 Nc] encodings of the inference samples
 	bool ray_cull = true;   // NEUS_RAY_CULL=0: march every ray (A/B reference)
+	uint32_t dbg_lds_fill = 0;  // tests (neus_debug_set_lds_fill): garbage-fill every CU's LDS before the step's march write
 	Dev<PcgJump> pcg_tab;   // pcg32 jump-ahead table (common.h PcgJumpTable)
 	uint32_t density_grid_ema_step = 0;
 	uint64_t occ_samples = 0;  // occupancy-grid samples this rank evaluated since the network was loaded
@@ -226,7 +236,7 @@ struct NeusTestbed {
 	Dev<float4> vbuf;
 	Dev<float> wgrad_partial, var_partial;  // per-block MLP weight-gradient rows, per-block variance sums
 	uint32_t mlp_blocks = 0;                // grid of the training MLP kernels at the batch capacity
-	Dev<uint8_t> scan_tmp;
+	ScanTemp scan_tmp;
 	size_t scan_tmp_bytes = 0;
 	Dev<StepState> st;
 	ScatterWork swork{};
@@ -270,8 +280,10 @@ struct NeusTestbed {
 	float loss_scalar_ema = 0.f, last_loss = 0.f, ek_loss = 0.f, mask_loss = 0.f, ray_loss = 0.f;
 	uint32_t last_rays_with_samples = 0;
 	bool loss_ema_init = false;
-	float* pinned = nullptr;  // [0..3]: loss sum, ek sum, mask sum, grid mean; [32..47] render / mesh counts; [64..]: StepState copy
+	float* pinned = nullptr;  // [0..3]: loss sum, ek sum, mask sum, grid mean; [32..47] render / mesh counts; [48]: the step scans'
+	                          // give-up count; [64..]: StepState copy
 	bool loss_pending = false;
+	hipEvent_t ev_loss = nullptr;  // after the logged step's readback copies (consume_loss waits on it, not on the stream)
 	// data parallel: RCCL communicator (production) or an in-process group
 	ncclComm_t comm = nullptr;
 	NeusLocalGroup* group = nullptr;
@@ -300,6 +312,7 @@ struct NeusTestbed {
 		HIP_CHECK(hipStreamCreateWithFlags(&aux_stream, hipStreamNonBlocking));
 		HIP_CHECK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
 		HIP_CHECK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+		HIP_CHECK(hipEventCreateWithFlags(&ev_loss, hipEventDisableTiming));
 		HIP_CHECK(hipHostMalloc((void**)&pinned, 128 * sizeof(float)));
 		for (auto& set : ev)
 			for (auto& e : set) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
@@ -327,6 +340,8 @@ struct NeusTestbed {
 		if (aux_stream) { (void)hipStreamSynchronize(aux_stream); (void)hipStreamDestroy(aux_stream); }
 		if (ev_fork) (void)hipEventDestroy(ev_fork);
 		if (ev_join) (void)hipEventDestroy(ev_join);
+		if (ev_loss) (void)hipEventDestroy(ev_loss);
+		for (auto& e : it_ev) if (e) (void)hipEventDestroy(e);
 		if (stream) (void)hipStreamDestroy(stream);
 	}
 
@@ -942,6 +957,32 @@ struct NeusTestbed {
 	}
 
 	void mark(int i) { if (profiling) HIP_CHECK(hipEventRecord(ev[prof_par][i], stream)); }
+	// Inference timing (neus_testbed_set_infer_timing): hipEvents around every pre-compaction network launch of the step
+	// (the one pass, or each progressive round's k_nerf_infer), summed per step after the step (host waits: timing passes
+	// only, never the bench's timed region)
+	bool infer_timing = false;
+	static constexpr int IT_MAX = 16;
+	hipEvent_t it_ev[2 * IT_MAX] = {};
+	int it_n = 0;
+	double it_ms = 0.0;
+	uint64_t it_launches = 0, it_steps = 0;
+	void it_mark() {
+		if (!infer_timing || it_n >= 2 * IT_MAX) return;
+		if (!it_ev[it_n]) HIP_CHECK(hipEventCreateWithFlags(&it_ev[it_n], hipEventDisableSystemFence));
+		HIP_CHECK(hipEventRecord(it_ev[it_n++], stream));
+	}
+	void it_collect() {
+		if (!infer_timing || it_n < 2) { it_n = 0; return; }
+		HIP_CHECK(hipEventSynchronize(it_ev[it_n - 1]));
+		for (int i = 0; i + 1 < it_n; i += 2) {
+			float ms = 0.f;
+			HIP_CHECK(hipEventElapsedTime(&ms, it_ev[i], it_ev[i + 1]));
+			it_ms += ms;
+			++it_launches;
+		}
+		++it_steps;
+		it_n = 0;
+	}
 
 	// ------------------------------------------------------------ rendering (render_to_cpu, python_api.cu:123-169)
 	// NerfTracer::init_rays_from_camera + trace (testbed_nerf.cu:2397-2600) once per spp, accumulated in linear
@@ -1137,7 +1178,7 @@ struct NeusTestbed {
 		launch_march_count(s, MAX_RAYS, max_samples, st.p, dp, ds, bitfield.p, bf_lin.p, rng.state, rng.inc, rays.p, startt.p, nreq.p, mwork,
 		                   progressive ? chunk_cnt.p : nullptr, OPEN_CNT + nch, ray_cull ? occ_bbox.p : nullptr);  // list lengths + open-ray counts
 		launch_march_write(s, MAX_RAYS, st.p, ds, rays.p, mwork, nreq.p, base.p, numsteps.p, coords.p, sample_ray.p, max_samples, scan_tmp.p,
-		                   progressive ? &r0 : nullptr);
+		                   progressive ? &r0 : nullptr, dbg_lds_fill);
 		mark(2);
 		// DeltaNetwork forward on the samples (nerf_network.h:162-182); the loss keeps the undeformed records
 		const float* c_in = coords.p;
@@ -1155,8 +1196,10 @@ struct NeusTestbed {
 				const uint32_t e2 = k + 2 < nch ? chunk_ends[k + 1] : 0xffffffffu;
 				// the loss's alpha terms in the inference epilogue (k_loss_alpha's work on the round's samples)
 				const InferAlpha ia{w.sa, w.ekt, lp.cos_anneal, ds.cone_angle == 0.0f ? 1u : 0u, nullptr};
+				it_mark();
 				launch_nerf_infer(s, lay.L, lay.W, chunk_cnt.p + k, 0, c_in, gl, valid, params_h.p + lay.grid_off, mlp, net_out.p, 8192, chunk_list.p,
 				                  use_delta ? nullptr : &ia);
+				it_mark();
 				if (use_delta) launch_loss_alpha_list(s, max_samples, chunk_cnt.p + k, chunk_list.p, coords.p, net_out.p, lp.cos_anneal, w, ds.cone_angle == 0.0f);
 				const bool more = k + 1 < nch;
 				launch_loss_scan_chunk(s, MAX_RAYS, numsteps.p, w, ccount.p, e0, e1, e2, more ? chunk_list.p : nullptr, chunk_cnt.p + k + 1,
@@ -1167,8 +1210,10 @@ struct NeusTestbed {
 			mark(3);
 		} else {
 			const InferAlpha ia{w.sa, w.ekt, lp.cos_anneal, ds.cone_angle == 0.0f ? 1u : 0u, w.n_long};
+			it_mark();
 			launch_nerf_infer(s, lay.L, lay.W, &st.p->n_kept, 0, c_in, gl, valid, params_h.p + lay.grid_off, mlp, net_out.p, 8192, nullptr,
 			                  use_delta ? nullptr : &ia);
+			it_mark();
 			mark(3);
 			if (use_delta) launch_loss_alpha(s, max_samples, st.p, coords.p, net_out.p, lp.cos_anneal, w, ds.cone_angle == 0.0f);
 			launch_loss_scan_ray(s, MAX_RAYS, numsteps.p, w, ccount.p);
@@ -1216,14 +1261,20 @@ struct NeusTestbed {
 			coll_end();
 		}
 		if (get_loss) {
+			// the previous readback (16 steps back, long done on the device) is checked first: a health failure then
+			// surfaces as this train call's error, while the host stays at most 16 steps ahead of the device
+			if (loss_pending) consume_loss();
 			HIP_CHECK(hipMemcpyAsync(pinned, loss_sum.p, 3 * 4, hipMemcpyDeviceToHost, s));
 			HIP_CHECK(hipMemcpyAsync(pinned + 64, st.p, sizeof(StepState), hipMemcpyDeviceToHost, s));
+			HIP_CHECK(hipMemcpyAsync(pinned + 48, scan_tmp.p + offsetof(ScanState, fail), 4, hipMemcpyDeviceToHost, s));
+			HIP_CHECK(hipEventRecord(ev_loss, s));
 			loss_pending = true;
 		}
 		// the step-end counters ride on the Adam launch when the canonical optimizer steps (k_step_counters otherwise)
-		const StepCounterArgs sca{st.p, batch, max_samples, world, cfg.fixed_rays_per_batch};
+		// (progressive inference: the samples evaluated are the rounds' list lengths chunk_cnt[0, nch))
+		const StepCounterArgs sca{st.p, batch, max_samples, world, cfg.fixed_rays_per_batch, progressive ? chunk_cnt.p : nullptr, nch};
 		const bool canon_opt = !dyn || train_canonical;
-		if (!canon_opt) launch_step_counters(s, st.p, batch, max_samples, world, cfg.fixed_rays_per_batch);
+		if (!canon_opt) launch_step_counters(s, st.p, batch, max_samples, world, cfg.fixed_rays_per_batch, sca.eval_cnt, sca.n_eval);
 		rng.advance();
 		mark(9);
 		// ---- optimizers (testbed_nerf.cu:3503-3508): the canonical trainer, the global-move trainer
@@ -1249,6 +1300,7 @@ struct NeusTestbed {
 			prof_par ^= 1;
 			if (prof_pending[prof_par]) accumulate_phases(prof_par);  // the previous step
 		}
+		it_collect();
 	}
 
 	LossWork loss_work(const uint32_t* rbase) {
@@ -1280,7 +1332,7 @@ struct NeusTestbed {
 
 	void consume_loss() {
 		if (!loss_pending) return;
-		HIP_CHECK(hipStreamSynchronize(stream));
+		HIP_CHECK(hipEventSynchronize(ev_loss));
 		const StepState* sst = (const StepState*)(pinned + 64);
 		const float measured = (float)sst->compacted_counter / (float)world;
 		const float scale = measured / (float)batch;
@@ -1301,6 +1353,21 @@ struct NeusTestbed {
 			aborted = true;
 		}
 		loss_pending = false;
+		// device health (sticky): a march that met a non-finite / negative t, a look-back scan that gave up waiting. Either
+		// means corrupted sampling or compaction bases: training stops with an error instead of continuing on bad data.
+		uint32_t scan_fail = 0;
+		std::memcpy(&scan_fail, pinned + 48, 4);
+		health_raise(sst->fail_flags | (scan_fail ? STEP_FAIL_SCAN : 0u));
+	}
+	uint32_t fail_seen = 0;
+	void health_raise(uint32_t flags) {
+		if (!flags) return;
+		fail_seen |= flags;
+		aborted = true;
+		std::string m = "training step: device health check failed:";
+		if (flags & STEP_FAIL_MARCH_T) m += " the occupancy march met a non-finite or negative t (corrupted sampling state);";
+		if (flags & STEP_FAIL_SCAN) m += " a look-back scan gave up waiting for a predecessor tile (compaction bases are wrong);";
+		throw std::runtime_error(m);
 	}
 };
 
@@ -1362,6 +1429,8 @@ int neus_testbed_get_stats(NeusTestbed* tb, NeusTrainStats* o) {
 		o->training_aborted = (tb->aborted || (tb->training_step > 0 && s.zero_records)) ? 1u : 0u;
 		o->pre_samples_total = s.pre_total; o->rays_total = s.rays_total;
 		o->occ_samples_total = tb->occ_samples; o->occ_updates = tb->occ_updates; o->reserved_ = 0;
+		o->health_flags = s.fail_flags | tb->fail_seen | (scan_failures(tb->scan_tmp.p) ? STEP_FAIL_SCAN : 0u);
+		o->evaluated_samples_total = s.eval_total; o->progressive_steps = s.prog_steps; o->evaluated_samples_last = s.eval_last;
 	});
 }
 static int copy_param_vec(NeusTestbed* tb, const float* dev, float* host, uint64_t n) {
@@ -1832,7 +1901,7 @@ int neus_debug_exclusive_scan(void* stream, const uint32_t* in, uint32_t* out, u
 	return guard([&] {
 		hipStream_t s = (hipStream_t)stream;
 		const size_t tb_ = scan_temp_bytes(std::max(1u, n));
-		Dev<uint8_t> tmp; tmp.alloc(tb_ + 256); scan_temp_reset(s, tmp.p);
+		ScanTemp tmp; tmp.alloc(tb_ + 256); scan_temp_reset(s, tmp.p);
 		for (int r = 0; r < std::max(1, reps); ++r) launch_exclusive_scan(s, tmp.p, tb_, in, out, n);
 		HIP_CHECK(hipStreamSynchronize(s));
 		if (failures) *failures = scan_failures(tmp.p);
@@ -1846,6 +1915,19 @@ int neus_testbed_set_profiling(NeusTestbed* tb, int on) {
 		tb->profiling = on != 0;
 		for (auto& m : tb->phase_ms) m = 0;
 		tb->phase_steps = 0; tb->phase_npre = tb->phase_ntrain = 0;
+	});
+}
+int neus_testbed_set_infer_timing(NeusTestbed* tb, int on) {
+	return guard([&] {
+		tb->infer_timing = on != 0;
+		tb->it_n = 0; tb->it_ms = 0.0; tb->it_launches = 0; tb->it_steps = 0;
+	});
+}
+int neus_testbed_infer_timing(NeusTestbed* tb, double* ms_total, uint64_t* launches, uint64_t* steps) {
+	return guard([&] {
+		if (ms_total) *ms_total = tb->it_ms;
+		if (launches) *launches = tb->it_launches;
+		if (steps) *steps = tb->it_steps;
 	});
 }
 int neus_testbed_kernel_times(NeusTestbed* tb, float* ms) {
@@ -1983,10 +2065,56 @@ int neus_delta_backward(NeusTestbed* tb, void* stream, uint32_t n, uint32_t stri
 		std::memcpy(grads12, h.grad, DELTA_PARAMS * 4);
 	});
 }
+static void sample_rays_impl(NeusTestbed* tb, void* stream, uint32_t n_rays, uint32_t rank, uint32_t world, uint32_t n_rays_total,
+                             uint64_t rng_state, uint64_t rng_inc, uint32_t max_samples, const uint8_t* bitfield, float* rays, uint32_t* numsteps,
+                             float* coords, uint32_t* counters_out, uint32_t e1, uint32_t* list, uint32_t* list_len, uint32_t lds_fill);
 int neus_sample_rays(NeusTestbed* tb, void* stream, uint32_t n_rays, uint32_t rank, uint32_t world, uint32_t n_rays_total,
                      uint64_t rng_state, uint64_t rng_inc, uint32_t max_samples, const uint8_t* bitfield, float* rays, uint32_t* numsteps,
                      float* coords, uint32_t* counters_out) {
 	return guard([&] {
+		sample_rays_impl(tb, stream, n_rays, rank, world, n_rays_total, rng_state, rng_inc, max_samples, bitfield, rays, numsteps, coords, counters_out,
+		                 0u, nullptr, nullptr, 0u);
+	});
+}
+int neus_debug_sample_rays_round0(NeusTestbed* tb, void* stream, uint32_t n_rays, uint32_t n_rays_total, uint64_t rng_state, uint64_t rng_inc,
+                                  uint32_t max_samples, const uint8_t* bitfield, float* rays, uint32_t* numsteps, float* coords, uint32_t* counters_out,
+                                  uint32_t chunk_end, uint32_t* list, uint32_t* list_len, uint32_t lds_fill) {
+	return guard([&] {
+		if (chunk_end == 0 || !list || !list_len) throw std::runtime_error("sample_rays_round0: chunk_end > 0, list and list_len required");
+		sample_rays_impl(tb, stream, n_rays, 0u, 1u, n_rays_total, rng_state, rng_inc, max_samples, bitfield, rays, numsteps, coords, counters_out,
+		                 chunk_end, list, list_len, lds_fill);
+	});
+}
+int neus_debug_scan_giveup(void* stream, const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* failures) {
+	return guard([&] {
+		hipStream_t s = (hipStream_t)stream;
+		ScanTemp tmp; tmp.alloc(scan_temp_bytes(n) + 256); scan_temp_reset(s, tmp.p);
+		debug_scan_skip_first_tile(s, tmp.p, in, out, n);
+		HIP_CHECK(hipStreamSynchronize(s));
+		*failures = scan_failures(tmp.p);
+	});
+}
+int neus_debug_set_lds_fill(NeusTestbed* tb, uint32_t pattern) { return guard([&] { tb->dbg_lds_fill = pattern; }); }
+int neus_debug_inject_health(NeusTestbed* tb, uint32_t flags) {
+	return guard([&] {
+		if (!tb->have_net) throw std::runtime_error("no network");
+		HIP_CHECK(hipStreamSynchronize(tb->stream));
+		if (flags & STEP_FAIL_MARCH_T) {
+			StepState h{};
+			HIP_CHECK(hipMemcpy(&h, tb->st.p, sizeof(h), hipMemcpyDeviceToHost));
+			h.fail_flags |= STEP_FAIL_MARCH_T;
+			HIP_CHECK(hipMemcpy(tb->st.p, &h, sizeof(h), hipMemcpyHostToDevice));
+		}
+		if (flags & STEP_FAIL_SCAN) {
+			const uint32_t one = 1;
+			HIP_CHECK(hipMemcpy(tb->scan_tmp.p + offsetof(ScanState, fail), &one, 4, hipMemcpyHostToDevice));
+		}
+	});
+}
+static void sample_rays_impl(NeusTestbed* tb, void* stream, uint32_t n_rays, uint32_t rank, uint32_t world, uint32_t n_rays_total,
+                             uint64_t rng_state, uint64_t rng_inc, uint32_t max_samples, const uint8_t* bitfield, float* rays, uint32_t* numsteps,
+                             float* coords, uint32_t* counters_out, uint32_t e1, uint32_t* list, uint32_t* list_len, uint32_t lds_fill) {
+	{
 		if (!tb->have_data || !tb->have_net) throw std::runtime_error("no dataset/network");
 		if (n_rays == 0 || n_rays > MAX_RAYS) throw std::runtime_error("n_rays out of range");
 		hipStream_t s = as_stream(tb, stream);
@@ -1997,20 +2125,27 @@ int neus_sample_rays(NeusTestbed* tb, void* stream, uint32_t n_rays, uint32_t ra
 		Dev<uint2> rec; rec.alloc((size_t)n_rays * NERF_STEPS);
 		Dev<uint2> seg; seg.alloc((size_t)n_rays * MARCH_SEG_RECS);
 		const MarchWork mw{rec.p, nrec.p, q.p, tb->mwork.waves, seg.p, tb->mwork.lanes_per_ray};
-		Dev<uint8_t> tmp; const size_t tb_ = scan_temp_bytes(n_rays); tmp.alloc(tb_ + 256); scan_temp_reset(s, tmp.p);
+		ScanTemp tmp; const size_t tb_ = scan_temp_bytes(n_rays); tmp.alloc(tb_ + 256); scan_temp_reset(s, tmp.p);
 		Dev<uint32_t> lin; lin.alloc(LIN_WORDS);
 		launch_bitfield_linear(s, bitfield, lin.p);
 		// the occupied-box cull of the training step, from this bitfield (exact: culled rays march to zero samples)
 		Dev<float> bb; bb.alloc(occ_bbox_scratch_floats());
 		launch_occ_bbox(s, bitfield, bb.p);
+		// progressive round 0's list (the training step's, written by the march): its slots and counters
+		Dev<uint32_t> c0, cnt;
+		if (list) { c0.alloc(n_rays); cnt.alloc(2); }
+		const Round0List r0{e1, c0.p, list, cnt.p, 2u};
 		launch_march_count(s, n_rays, max_samples, sst.p, DPInfo{rank, world}, tb->ds, bitfield, lin.p, rng_state, rng_inc, rays, st_t.p, nr.p, mw,
-		                   nullptr, 0, tb->ray_cull ? bb.p : nullptr);
+		                   list ? cnt.p : nullptr, list ? 2u : 0u, tb->ray_cull ? bb.p : nullptr);
 		Dev<uint32_t> sr; sr.alloc(std::max<uint32_t>(1, max_samples));
-		launch_march_write(s, n_rays, sst.p, tb->ds, rays, mw, nr.p, bs.p, numsteps, coords, sr.p, max_samples, tmp.p);
+		launch_march_write(s, n_rays, sst.p, tb->ds, rays, mw, nr.p, bs.p, numsteps, coords, sr.p, max_samples, tmp.p, list ? &r0 : nullptr, lds_fill);
 		HIP_CHECK(hipMemcpyAsync(&h, sst.p, sizeof(h), hipMemcpyDeviceToHost, s));
+		if (list) HIP_CHECK(hipMemcpyAsync(list_len, cnt.p, 4, hipMemcpyDeviceToHost, s));
 		HIP_CHECK(hipStreamSynchronize(s));
+		if (h.fail_flags) throw std::runtime_error("sample_rays: the march met a non-finite or negative t");
+		if (scan_failures(tmp.p)) throw std::runtime_error("sample_rays: the look-back scan gave up");
 		counters_out[0] = h.numsteps_counter; counters_out[1] = h.n_kept; counters_out[2] = h.n_rays_with_samples;
-	});
+	}
 }
 int neus_loss_compact(NeusTestbed* tb, void* stream, uint32_t n_rays, uint32_t rank, uint32_t world, uint32_t n_rays_total,
                       uint64_t rng_state, uint64_t rng_inc, uint32_t max_compacted, const float* rays, uint32_t* numsteps,
@@ -2032,7 +2167,7 @@ int neus_loss_compact(NeusTestbed* tb, void* stream, uint32_t n_rays, uint32_t r
 		Dev<uint32_t> cc, cb, rb, sr; cc.alloc(n_rays); cb.alloc(n_rays); rb.alloc(n_rays); sr.alloc(n_samples);
 		Dev<float4> sa, ck4, racc, rgr; sa.alloc(n_samples); ck4.alloc(n_samples / 8 + 1); racc.alloc(n_rays); rgr.alloc(n_rays);
 		Dev<float> ekt, cke, rT; ekt.alloc(n_samples); cke.alloc(n_samples / 8 + 1); rT.alloc(n_rays);
-		Dev<uint8_t> tmp; const size_t tb_ = scan_temp_bytes(n_rays); tmp.alloc(tb_ + 256); scan_temp_reset(s, tmp.p);
+		ScanTemp tmp; const size_t tb_ = scan_temp_bytes(n_rays); tmp.alloc(tb_ + 256); scan_temp_reset(s, tmp.p);
 		LossParams lp{};
 		lp.loss_scale = LOSS_SCALE; lp.ek_w = tb->cfg.ek_loss_weight; lp.mask_w = tb->cfg.mask_loss_weight; lp.cos_anneal = tb->cos_anneal();
 		lp.max_compacted = max_compacted; lp.rng_state = rng_state; lp.rng_inc = rng_inc;

@@ -1008,6 +1008,22 @@ class Testbed:
         check(lib().neus_testbed_time_kernel(self._h, C.c_int(kernel), C.c_int(iters), C.byref(ms), C.byref(units)))
         return float(ms.value), int(units.value)
 
+    def infer_timing(self, steps):
+        """Trains `steps` steps with the step's own pre-compaction network launches timed (hipEvents around each
+        k_nerf_infer launch: the one pass or the progressive rounds): dict of summed launch ms, launches, steps and the
+        samples those launches evaluated (neus_testbed_set_infer_timing)."""
+        s0 = self.stats()["evaluated_samples_total"]
+        check(lib().neus_testbed_set_infer_timing(self._h, C.c_int(1)))
+        try:
+            self.train_steps(steps)
+            self.synchronize()
+            ms, n, k = C.c_double(), C.c_uint64(), C.c_uint64()
+            check(lib().neus_testbed_infer_timing(self._h, C.byref(ms), C.byref(n), C.byref(k)))
+        finally:
+            check(lib().neus_testbed_set_infer_timing(self._h, C.c_int(0)))
+        return {"ms": float(ms.value), "launches": int(n.value), "steps": int(k.value),
+                "evaluated": int(self.stats()["evaluated_samples_total"] - s0)}
+
     def phase_times(self):
         """Mean ms per profiled step for each of PHASES, plus (n_steps, mean Npre, mean Ntrain)."""
         n = len(PHASES)

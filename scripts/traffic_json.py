@@ -13,14 +13,14 @@ NAMES = {"k_nerf_infer": "inference", "k_march": "march", "k_grid_encode": "trai
          "k_mlp_grad_reduce": "mlp_grad_reduce"}
 
 
-def parse(path):
+def parse(path, names=NAMES):
     cur, out = None, {}
     for line in open(path):
         m = re.match(r"\s+(\S.*?) dispatches=\d+ grid=\d+", line)
         if m:
             name = m.group(1)
             # k_march is the templated march itself ("k_march<"), not k_march_numsteps / k_march_write
-            cur = next((v for k, v in NAMES.items() if (k + "<" in name if k == "k_march" else k in name)), None)
+            cur = next((v for k, v in names.items() if (k + "<" in name if k == "k_march" else k in name)), None)
             continue
         m = re.match(r"\s+(\w+)\s+([-+0-9.eE]+)$", line)
         if m and cur:
@@ -33,13 +33,19 @@ def main():
     ap.add_argument("table")
     ap.add_argument("levels", type=int)
     ap.add_argument("--commit", default="")
+    # kernel=key overrides of the traffic.json key (e.g. k_nerf_infer=inference_step for the training step's own rounds)
+    ap.add_argument("--name", action="append", default=[])
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "traffic.json"))
     a = ap.parse_args()
     try:
         db = json.load(open(a.out))
     except (OSError, ValueError):
         db = {}
-    for k, c in parse(a.table).items():
+    names = dict(NAMES)
+    for kv in a.name:
+        k, v = kv.split("=", 1)
+        names[k] = v
+    for k, c in parse(a.table, names).items():
         if "TCC_EA0_RDREQ_sum" not in c or "WRITE_SIZE" not in c:
             continue
         r128, r32 = c.get("TCC_EA0_RDREQ_128B_sum", 0.0), c.get("TCC_EA0_RDREQ_32B_sum", 0.0)

@@ -56,7 +56,8 @@ int main(void) {
   O(NeusImage, rgba8) O(NeusImage, xform)
   O(NeusTrainStats, ray_loss) O(NeusTrainStats, n_rays_with_samples) O(NeusTrainStats, trained_samples_total)
   O(NeusNetLayout, per_level_scale) O(NeusNetLayout, n_levels)
-  O(NeusTrainStats, pre_samples_total) O(NeusTrainStats, occ_updates)
+  O(NeusTrainStats, pre_samples_total) O(NeusTrainStats, occ_updates) O(NeusTrainStats, evaluated_samples_total)
+  O(NeusTrainStats, evaluated_samples_last)
   O(NeusDataParallelInfo, collective_calls) O(NeusDataParallelInfo, last_step_allreduce_bytes)
   printf("NEUS_N_PHASES %d\n", NEUS_N_PHASES);
   return 0;

@@ -268,6 +268,90 @@ def test_teacher_forced_steps_vs_oracle(scene, torch_cuda):
         assert cos >= 0.9999 and rel <= 2e-3, (name, cos, rel)
 
 
+def test_teacher_forced_all_levels_vs_oracle(scene, torch_cuda):
+    """Teacher-forced training at the bench's state: the device trains 700 free-running steps first, so
+    all 14 levels are active (hashed levels 5-13: 2^19-entry tables, the 2048-entry region scatter of hashed buckets),
+    the occupancy grid is shaped by hundreds of updates and progressive inference is on by its auto rule (checked: the
+    steps ran the chunk rounds and later rounds had work). Then 14 consecutive steps, each compared with the oracle's
+    step from the device's state before it (as test_teacher_forced_steps_vs_oracle). One step runs with half the rays,
+    so its compacted count is below the batch and the rollover fused into k_grid_encode fills the rest
+    (fill_rollover_and_rescale, common_device.h:515-535). Per step: the march bit-exact, the compacted count equal up to
+    fp16-moved cut-offs, every gradient block cos >= 0.9999 and rel-L2 <= 2e-3; per hash level the worst rel-L2 is
+    recorded (profiles/, parity metrics). Reference: testbed_nerf.cu:3723-4001, grid.h:371-500, 880-1007, 2427-2440."""
+    import ctypes as C
+    import oracle as O
+    from cpu_step import CpuTrainer
+    from neus2_amd._lib import NeusRestoreState, check, lib
+    tb = _testbed(scene)
+    tb.train_steps(700)
+    lay = tb.layout()
+    cfg = O.make_cfg(per_level_scale=tb._net_cfg.per_level_scale)
+    assert tb.stats()["valid_level"] + 1 >= cfg.n_levels, "not every level is active"
+    ds = O.Dataset(scene["images"], scene["focal"], scene["principal"], scene["xforms"])
+    tr = CpuTrainer(cfg, ds, tb.get_params(), batch=BATCH, rays_per_batch=BATCH)
+    blocks = {"density": (0, lay["n_density"]), "rgb": (lay["n_density"], lay["n_matrix"]),
+              "grid": (lay["grid_offset"], lay["variance_offset"]), "variance": (lay["variance_offset"], lay["variance_offset"] + 1)}
+    off, _, _, _ = O.grid_tables(cfg)
+    g0 = lay["grid_offset"]
+    worst = {k: [1.0, 0.0] for k in blocks}
+    lev_rel = np.zeros(cfg.n_levels)
+    prog0 = tb.stats()["progressive_steps"]
+    n_steps, short_step, short_seen, n_comp_equal, later_rounds = 14, 5, False, 0, 0
+    for k in range(n_steps):
+        st = tb.stats()
+        if k == short_step:  # half the rays for this step: the compaction falls short of the batch
+            rs = NeusRestoreState(training_step=st["training_step"], rays_per_batch=max(128, st["rays_per_batch"] // 256 * 128),
+                                  measured_batch_size=st["measured_batch_size"],
+                                  measured_batch_size_before_compaction=st["measured_batch_size_before_compaction"], loss=st["loss"],
+                                  rebuild_bitfield=0)
+            check(lib().neus_testbed_restore_state(tb.handle, C.byref(rs)))
+            st = tb.stats()
+        rng = tb.get_rng()
+        tr.params = tb.get_params().copy()
+        tr.R = st["rays_per_batch"]
+        tr.training_step = st["training_step"]
+        tr.n_rays_total = st["n_rays_total"]
+        tr.rng_state, tr.rng_inc = rng[0], rng[1]
+        before = st["measured_batch_size_before_compaction"]
+        tr.max_inference = (min(before, tr.max_samples) + 127) // 128 * 128 if before else tr.max_samples
+        assert tr.valid_level(tr.training_step) == cfg.n_levels
+        tb.train_steps(1)
+        g = tb.get_gradients().astype(np.float64)
+        grid, bf = tb.get_density_grid()
+        st1 = tb.stats()
+        _, cc, _ = tb.ray_counts(1 << 18)
+        later_rounds += int((cc > 32).sum())
+        tr.density_grid[:] = grid
+        tr.bitfield[:] = bf
+        gr = tr.grads(skip_occupancy=True).astype(np.float64)
+        assert st1["measured_batch_size_before_compaction"] == tr.last["numsteps_counter"], k
+        comp_d, comp_o = st1["measured_batch_size"], tr.last["compacted"]
+        n_comp_equal += comp_d == comp_o
+        assert abs(comp_d - comp_o) <= max(2, 1e-3 * comp_o), (k, comp_d, comp_o)
+        short_seen |= comp_o < BATCH
+        for name, (a, b) in blocks.items():
+            x, y = g[a:b], gr[a:b]
+            cos = x @ y / max(np.linalg.norm(x) * np.linalg.norm(y), 1e-30)
+            rel = np.linalg.norm(x - y) / max(np.linalg.norm(y), 1e-30)
+            worst[name][0] = min(worst[name][0], cos)
+            worst[name][1] = max(worst[name][1], rel)
+        for l in range(cfg.n_levels):
+            a, b = g0 + 2 * int(off[l]), g0 + 2 * int(off[l + 1])
+            y = gr[a:b]
+            if np.linalg.norm(y) > 0:
+                lev_rel[l] = max(lev_rel[l], np.linalg.norm(g[a:b] - y) / np.linalg.norm(y))
+    prog = tb.stats()["progressive_steps"] - prog0
+    _record("teacher_forced_all_levels", steps=n_steps, start_step=700, compacted_equal_steps=n_comp_equal, progressive_steps=prog,
+            later_round_rays=later_rounds, short_step_compacted_below_batch=short_seen,
+            **{f"min_cos_{k}": v[0] for k, v in worst.items()}, **{f"max_rel_{k}": v[1] for k, v in worst.items()},
+            **{f"max_rel_grid_L{l}": lev_rel[l] for l in range(cfg.n_levels)})
+    assert prog >= n_steps - 1, f"progressive inference ran on {prog} of {n_steps} steps"
+    assert later_rounds > 0, "no ray composited past the first chunk: the later rounds had no work"
+    assert short_seen, "no step compacted fewer samples than the batch: the rollover did not run"
+    for name, (cos, rel) in worst.items():
+        assert cos >= 0.9999 and rel <= 2e-3, (name, cos, rel)
+
+
 def test_training_is_bitwise_reproducible(scene, torch_cuda):
     """Two testbeds, same seed and data, 50 free-running steps each: parameters, EMA weights, occupancy grid and
     losses are bitwise equal. Every reduction of the step is fixed-order (scan compaction, int64 fixed-point grid
