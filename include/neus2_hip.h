@@ -250,7 +250,9 @@ int neus_testbed_saved_transform(NeusTestbed* tb, float* out12);
  *   color_space          testbed.color_space: 0 Linear (default), 1 SRGB (testbed_nerf.cu:1657-1671)
  *   linear_colors        nerf.training.linear_colors: targets and rendering stay linear
  *   cone_angle_constant  nerf.cone_angle_constant (load_nerf sets 0 for aabb_scale 1, else 1/256)
- *   near_distance        nerf.training.near_distance (stored; the NeuS sampler does not read it) */
+ *   near_distance        nerf.training.near_distance (stored; the NeuS sampler does not read it)
+ *   depth_supervision_lambda  nerf.training.depth_supervision_lambda (python_api.cu:555; stored: the reference computes
+ *                        the depth term, testbed_nerf.cu:1697-1698 / 1836, and adds it to no gradient or loss) */
 typedef struct NeusTrainingOptions {
 	int32_t random_bg_color;
 	float background_color[3];
@@ -258,6 +260,7 @@ typedef struct NeusTrainingOptions {
 	int32_t linear_colors;
 	float cone_angle_constant;
 	float near_distance;
+	float depth_supervision_lambda;
 } NeusTrainingOptions;
 int neus_testbed_get_training_options(NeusTestbed* tb, NeusTrainingOptions* out);
 /* Trainer::serialize(include_optimizer_state) / deserialize (trainer.h:281-305): the Ema(ExponentialDecay(Adam))

@@ -87,6 +87,7 @@ class NeusTrainingOptions(C.Structure):
     _fields_ = [
         ("random_bg_color", C.c_int32), ("background_color", C.c_float * 3), ("color_space", C.c_int32),
         ("linear_colors", C.c_int32), ("cone_angle_constant", C.c_float), ("near_distance", C.c_float),
+        ("depth_supervision_lambda", C.c_float),
     ]
 
 

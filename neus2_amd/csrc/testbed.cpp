@@ -202,6 +202,10 @@ struct NeusTestbed {
 	bool nonfinite = false, aborted = false;  // training health (consume_loss); cleared by reset_network
 	bool render_delta = false;     // prepare_for_test (testbed.cu:1987-1999): render / mesh through the DeltaNetwork
 	float near_distance = 0.f;     // nerf.training.near_distance: stored; the NeuS sampler does not read it (testbed_nerf.cu:1525)
+	// nerf.training.depth_supervision_lambda (testbed.h:649): stored. The reference's loss kernel computes the depth term
+	// (testbed_nerf.cu:1697-1698, 1836) but adds it to no gradient and no loss output, so it never changes training; the
+	// step here keeps that (no depth term; tests/test_gpu_depth.py checks a lambda > 0 run against lambda = 0 bitwise)
+	float depth_lambda = 0.f;
 	int32_t color_space_when_linear = 0;  // color_space as set while linear_colors overrides it
 	float delta_lr_factor = 1.f;
 	Dev<DeltaState> delta;
@@ -1681,6 +1685,7 @@ int neus_testbed_get_training_options(NeusTestbed* tb, NeusTrainingOptions* o) {
 		if (t.mode == 2) o->color_space = tb->color_space_when_linear;
 		o->cone_angle_constant = tb->ds.cone_angle;
 		o->near_distance = tb->near_distance;
+		o->depth_supervision_lambda = tb->depth_lambda;
 	});
 }
 int neus_testbed_set_progressive_inference(NeusTestbed* tb, int mode, const uint32_t* chunk_ends, uint32_t n_ends) {
@@ -1711,6 +1716,8 @@ int neus_testbed_set_training_options(NeusTestbed* tb, const NeusTrainingOptions
 		tb->ds.target = t;
 		tb->ds.cone_angle = o->cone_angle_constant;
 		tb->near_distance = o->near_distance;
+		if (!(o->depth_supervision_lambda >= 0.f)) throw std::runtime_error("depth_supervision_lambda must be >= 0");
+		tb->depth_lambda = o->depth_supervision_lambda;
 	});
 }
 int neus_testbed_get_movement(NeusTestbed* tb, float* global12, float* local12) {

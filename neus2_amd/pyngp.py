@@ -311,7 +311,12 @@ def load_transforms(path):
         offset = (a[1] + a[0]) * 0.5 * -scale + 0.5
     white_t, black_t = bool(js.get("white_transparent", False)), bool(js.get("black_transparent", False))
     flags = white_t or black_t
-    images, focal, principal, xforms, mask_colors = [], [], [], [], []
+    # depth maps (nerf_loader.cu:321-393, 599-612): frames' `depth_path` 16-bit images, loaded when the dataset sets
+    # `integer_depth_scale` > 0 and `enable_depth_loading` is not false; metres = value x integer_depth_scale x scale
+    # (set_training_image(..., depth_scale * result.scale), copy_depth :91-99)
+    enable_depth = bool(js.get("enable_depth_loading", True))
+    int_depth_scale = float(js.get("integer_depth_scale", -1.0))
+    images, focal, principal, xforms, mask_colors, depths = [], [], [], [], [], []
     for fr in js["frames"]:
         fp = fr["file_path"]
         p = os.path.join(base, fp)
@@ -340,6 +345,15 @@ def load_transforms(path):
         if alpha is not None or mask is not None or flags:
             img, key = prepare_image(img, alpha, mask, white_t, black_t)
         mask_colors.append(key)
+        depth = None
+        if enable_depth and int_depth_scale > 0 and "depth_path" in fr:
+            dpath = os.path.join(base, str(fr["depth_path"]))
+            if os.path.exists(dpath):
+                d16 = read_depth_u16(dpath)
+                if d16.shape != (h, w):
+                    raise RuntimeError("Depth image has wrong resolution: " + dpath)
+                depth = (d16.astype(np.float32) * np.float32(int_depth_scale * scale)).astype(np.float32)
+        depths.append(depth)
         pp = np.array([0.5, 0.5], np.float32)
         if "cx" in js:
             pp[0] = float(js["cx"]) / float(js["w"])
@@ -373,7 +387,23 @@ def load_transforms(path):
         principal.append(pp)
     return dict(images=images, focal=np.array(focal, np.float32), principal=np.array(principal, np.float32),
                 xforms=np.stack(xforms).astype(np.float32), aabb_scale=aabb_scale, scale=scale, offset=offset, from_na=from_na,
-                mask_colors=mask_colors, white_transparent=white_t, black_transparent=black_t)
+                mask_colors=mask_colors, white_transparent=white_t, black_transparent=black_t, depths=depths)
+
+
+def read_depth_u16(path):
+    """stbi_load_16(path, ..., 1) as nerf_loader.cu:603 calls it: one 16-bit channel; 8-bit images are widened by
+    x 257, colour images reduced to stbi's luma (77 r + 150 g + 29 b) >> 8 (stbi__compute_y_16)."""
+    from PIL import Image
+    im = Image.open(path)
+    if im.mode in ("I;16", "I;16B", "I;16L", "I"):
+        a = np.asarray(im).astype(np.int64)
+        if a.ndim == 3:
+            a = a[..., 0]
+        return np.clip(a, 0, 65535).astype(np.uint16)
+    if im.mode in ("L", "P", "1"):
+        return (np.asarray(im.convert("L"), np.uint16) * 257).astype(np.uint16)
+    rgb = np.asarray(im.convert("RGB"), np.uint32) * 257
+    return ((rgb[..., 0] * 77 + rgb[..., 1] * 150 + rgb[..., 2] * 29) >> 8).astype(np.uint16)
 
 
 def geometric_init_weights(n_levels, width=64, seed=1337, path_hint=True):
@@ -451,6 +481,14 @@ class _Dataset:
         return BoundingBox(*self._tb._aabb)
 
     @property
+    def has_depth(self):
+        return any(d is not None for d in (getattr(self._tb, "_depths", None) or []))
+
+    def depth(self, image):
+        """The depth map of a training image (scene units) or None."""
+        return self._tb._depths[image]
+
+    @property
     def transforms(self):
         return [np.asarray(x, np.float32).reshape(3, 4).copy() for x in (self._tb._dataset_meta or {}).get("xforms", [])]
 
@@ -461,6 +499,10 @@ class _Training:
     random_bg_color = _opt_property("random_bg_color", bool)
     linear_colors = _opt_property("linear_colors", bool)
     near_distance = _opt_property("near_distance", float)
+    # nerf.training.depth_supervision_lambda (python_api.cu:555; default 0, testbed.h:649). The reference's loss kernel
+    # computes the depth term (testbed_nerf.cu:1697-1698, 1836) but never adds it to dL/dalpha or any output, so in
+    # zbqq/neus2 it does not change training; stored and passed to the device step, which keeps those semantics.
+    depth_supervision_lambda = _opt_property("depth_supervision_lambda", float)
 
     def __init__(self, tb):
         self._tb = tb
@@ -556,6 +598,9 @@ class Testbed:
             files = [path]
         d = load_transforms(files[0])
         self.set_dataset(d["images"], d["focal"], d["principal"], d["xforms"], d["aabb_scale"])
+        for i, dep in enumerate(d.get("depths") or []):
+            if dep is not None:
+                self.set_depth(i, dep)
         self._scale, self._offset, self._from_na = float(d["scale"]), np.asarray(d["offset"], np.float32), bool(d["from_na"])
         self._frames = files  # all_json_paths (testbed_nerf.cu:2967-2994): one transforms file per time frame
 
@@ -661,12 +706,23 @@ class Testbed:
         check(lib().neus_testbed_set_movement(self._h, C.c_void_p(g.ctypes.data) if g is not None else None,
                                               C.c_void_p(l.ctypes.data) if l is not None else None))
 
+    def set_depth(self, image, depth):
+        """NerfDataset::set_training_image's depth (nerf_loader.cu:753-790): a float depth map (scene units) of training
+        image `image` at its resolution, kept with the dataset (metadata[img].depth). The reference's training step does
+        not use it (see _Training.depth_supervision_lambda)."""
+        h, w = self._images[image].shape[:2]
+        d = np.ascontiguousarray(depth, np.float32)
+        if d.shape != (h, w):
+            raise NeusError(f"depth map of image {image} must be {h} x {w}, got {d.shape}")
+        self._depths[image] = d
+
     def set_dataset(self, images, focal, principal, xforms, aabb_scale=1):
         imgs = [np.ascontiguousarray(im, np.uint8) for im in images]
         arr = _images_array(imgs, focal, principal, xforms)
         self._frames = None
         check(lib().neus_testbed_set_dataset(self._h, C.c_uint32(len(imgs)), arr, C.c_float(aabb_scale)))
         self._images = imgs
+        self._depths = [None] * len(imgs)
         self._n_images = len(imgs)
         self._dataset_meta = {"xforms": list(xforms), "focal": list(focal), "principal": list(principal),
                               "aabb_scale": float(aabb_scale)}

@@ -51,7 +51,8 @@ PROBE = r"""
 #define S(T) printf(#T " %zu\n", sizeof(T));
 #define O(T, f) printf(#T "." #f " %zu\n", offsetof(T, f));
 int main(void) {
-  S(NeusNetworkConfig) S(NeusImage) S(NeusTrainStats) S(NeusNetLayout) S(NeusDataParallelInfo)
+  S(NeusNetworkConfig) S(NeusImage) S(NeusTrainStats) S(NeusNetLayout) S(NeusDataParallelInfo) S(NeusTrainingOptions)
+  O(NeusTrainingOptions, depth_supervision_lambda)
   O(NeusNetworkConfig, fixed_rays_per_batch) O(NeusNetworkConfig, seed) O(NeusNetworkConfig, batch_size)
   O(NeusImage, rgba8) O(NeusImage, xform)
   O(NeusTrainStats, ray_loss) O(NeusTrainStats, n_rays_with_samples) O(NeusTrainStats, trained_samples_total)
@@ -72,7 +73,7 @@ def test_struct_layouts_match_header(tmp_path):
     exe = tmp_path / "probe"
     subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     vals = dict(l.rsplit(" ", 1) for l in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.splitlines())
-    for name in ("NeusNetworkConfig", "NeusImage", "NeusTrainStats", "NeusNetLayout", "NeusDataParallelInfo"):
+    for name in ("NeusNetworkConfig", "NeusImage", "NeusTrainStats", "NeusNetLayout", "NeusDataParallelInfo", "NeusTrainingOptions"):
         T = getattr(_lib, name)
         assert C.sizeof(T) == int(vals[name]), name
         for key, v in vals.items():

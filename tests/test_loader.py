@@ -94,3 +94,73 @@ def test_plain_dataset_unchanged(tmp_path):
     for i, (img, _, _) in enumerate(raw):
         np.testing.assert_array_equal(ds["images"][i], img)
         assert ds["mask_colors"][i] == 0
+
+
+def _depth_scene(tmp_path, scale_int=1e-3, enable=None, n=3, w=20, h=12, seed=5, missing=(), wrong=()):
+    """Frames with `depth_path` 16-bit PNGs (nerf_loader.cu:599-612); frame indices in `missing` name a file that does
+    not exist, those in `wrong` one of the wrong resolution."""
+    from PIL import Image
+    _scene(tmp_path, n=n, w=w, h=h)
+    js = json.load(open(tmp_path / "transforms.json"))
+    rng = np.random.default_rng(seed)
+    raw = []
+    for i, fr in enumerate(js["frames"]):
+        d = rng.integers(0, 65536, (h, w), dtype=np.uint16)
+        if i in wrong:
+            d = d[:-1]
+        name = f"depth/{i:03d}.png"
+        os.makedirs(tmp_path / "depth", exist_ok=True)
+        if i not in missing:
+            Image.fromarray(d).save(tmp_path / name)
+        fr["depth_path"] = name
+        raw.append(d)
+    if scale_int is not None:
+        js["integer_depth_scale"] = scale_int
+    if enable is not None:
+        js["enable_depth_loading"] = enable
+    with open(tmp_path / "transforms.json", "w") as f:
+        json.dump(js, f)
+    return raw, js["scale"]
+
+
+def test_depth_maps_loaded_as_reference(tmp_path):
+    """depth = uint16 x integer_depth_scale x scale (set_training_image(..., depth_scale * result.scale), copy_depth
+    nerf_loader.cu:91-99, 736); a frame whose depth file does not exist has none (the reference skips it)."""
+    from neus2_amd import pyngp
+    raw, scale = _depth_scene(tmp_path, scale_int=2.5e-4, missing=(1,))
+    ds = pyngp.load_transforms(str(tmp_path / "transforms.json"))
+    assert ds["depths"][1] is None
+    for i in (0, 2):
+        expect = raw[i].astype(np.float32) * np.float32(2.5e-4 * scale)
+        np.testing.assert_array_equal(ds["depths"][i], expect)
+        assert ds["depths"][i].dtype == np.float32
+
+
+@pytest.mark.parametrize("scale_int,enable", [(None, None), (-1.0, None), (1e-3, False)])
+def test_depth_loading_gated(tmp_path, scale_int, enable):
+    """No `integer_depth_scale` (default -1), a non-positive one, or enable_depth_loading false: no depth is loaded
+    (nerf_loader.cu:321-339, 392-393, 599)."""
+    from neus2_amd import pyngp
+    _depth_scene(tmp_path, scale_int=scale_int, enable=enable)
+    ds = pyngp.load_transforms(str(tmp_path / "transforms.json"))
+    assert all(d is None for d in ds["depths"])
+
+
+def test_depth_resolution_checked(tmp_path):
+    from neus2_amd import pyngp
+    _depth_scene(tmp_path, wrong=(2,))
+    with pytest.raises(RuntimeError, match="Depth image has wrong resolution"):
+        pyngp.load_transforms(str(tmp_path / "transforms.json"))
+
+
+def test_read_depth_u16_formats(tmp_path):
+    """stbi_load_16(..., 1): 16-bit grey as is, 8-bit grey widened x 257, colour reduced to stbi's 16-bit luma."""
+    from PIL import Image
+    from neus2_amd import pyngp
+    g8 = np.arange(60, dtype=np.uint8).reshape(6, 10)
+    Image.fromarray(g8, "L").save(tmp_path / "g8.png")
+    np.testing.assert_array_equal(pyngp.read_depth_u16(str(tmp_path / "g8.png")), g8.astype(np.uint16) * 257)
+    rgb = np.stack([g8, g8[::-1], g8 // 2], -1)
+    Image.fromarray(rgb, "RGB").save(tmp_path / "rgb.png")
+    r, g, b = [rgb[..., k].astype(np.uint32) * 257 for k in range(3)]
+    np.testing.assert_array_equal(pyngp.read_depth_u16(str(tmp_path / "rgb.png")), ((r * 77 + g * 150 + b * 29) >> 8).astype(np.uint16))
