@@ -154,7 +154,7 @@ def test_ctypes_options_struct_matches_header():
     body = re.search(r"typedef struct NeusTrainingOptions \{(.*?)\} NeusTrainingOptions;", hdr, re.S).group(1)
     names = re.findall(r"(\w+)(?:\[\d+\])?;", body)
     assert names == [f for f, _ in pyngp._lib.NeusTrainingOptions._fields_]
-    assert C.sizeof(pyngp._lib.NeusTrainingOptions) == 32
+    assert C.sizeof(pyngp._lib.NeusTrainingOptions) == 36
 
 
 @pytest.mark.parametrize("val", [True])
