@@ -375,18 +375,27 @@ int neus_testbed_init_local_group(NeusTestbed* tb, NeusLocalGroup* group, int ra
 /* ------------------------------------------------------------------ tcnn-shaped operator modules
  * tcnn::cpp::Module (dependencies/my_tcnn/include/tiny-cuda-nn/cpp_api.h:66-110) over the gfx950 kernels, with
  * explicit parameter pointers, a forward context and EGradientMode (object.h:90-94). Device buffers throughout;
- * `stream` is the hipStream_t the call runs on (NULL: the null stream).
- *   neus_module_create_network   the NeuS NerfNetwork (nerf_network.h; the full config object with "encoding",
+ * `stream` is the hipStream_t the call runs on (NULL: the null stream). Factories, named as tcnn's (cpp_api.h:108-110):
+ *   neus_module_create_network   create_network(n_input_dims, n_output_dims, network) (cpp_api.cu:170-172): an Identity
+ *                                encoding (inputs padded to 16 with ones) in front of a FullyFusedMLP (n_neurons 16 / 32 /
+ *                                64 / 128, n_hidden_layers >= 1, activation / output_activation None, ReLU, Exponential,
+ *                                Sigmoid, Squareplus, Softplus); input [n][n_input_dims] f32, output [n][padded out] fp16,
+ *                                params [W x in_pad | (N - 1) x W x W | out_pad x W] fp16 (fully_fused_mlp.cu:816-879);
+ *                                n must be a multiple of 128 (fully_fused_mlp.cu:779-781).
+ *   neus_module_create_encoding  create_encoding (HashGrid, grid.h): input [n][3] f32; output layout from the config's
+ *                                "output_layout": "AoS" [n][2L] fp16 (default: the column-major matrix cpp::Module wraps,
+ *                                cpp_api.cu:58-70), "SoA" [2L][n] (GridEncoding::preferred_output_layout, grid.h:2357-2359) or
+ *                                "paired" [L][n] half2 (this build's kernels); params [n_grid] fp16.
+ *   neus_module_create_network_with_input_encoding  HashGrid -> FullyFusedMLP with one hidden ReLU layer (below).
+ *   neus_module_create_nerf_network  the NeuS NerfNetwork (nerf_network.h; the full config object with "encoding",
  *                                "network", "rgb_network"): input NerfCoordinate [n][7] f32 (pos, dt, dir), output
- *                                [n][16] fp16; params [n_params] fp16 in the layout of neus_testbed_layout.
- *   neus_module_create_encoding  the HashGrid encoding (create_encoding, grid.h): input [n][3] f32, output [L][n]
- *                                half2 (features 2l, 2l+1 of level l adjacent; tcnn's SoA has them in separate rows),
- *                                params [n_grid] fp16.
- * Parameter gradients are fp32 (the reference's are param-precision fp16). Network backward needs n % 128 == 0;
- * its dL_dinput ([n][7] f32) carries the position columns (dt / direction columns written 0). The network's
- * eikonal second order is inside backward (as nerf_network.h:330-601); backward_backward_input is the encoding's
- * (grid.h:1697-1800, without the dL_dinput term). Progressive levels follow set_training_step (grid.h:2427-2437;
- * 0 = all levels). */
+ *                                [n][16] fp16; params [n_params] fp16 in the layout of neus_testbed_layout. Its backward
+ *                                needs n % 128 == 0 and includes the eikonal second order (as nerf_network.h:330-601); its
+ *                                dL_dinput ([n][7] f32) carries the position columns (dt / direction columns written 0).
+ * Parameter gradients dL_dparams are param precision (fp16, tcnn's trainer.h:72-109) unless the config sets
+ * "gradient_precision": "fp32". backward_backward_input is the encoding's (grid.h:1697-1800, without the dL_dinput term),
+ * the network-with-input-encoding's and create_network's (fully_fused_mlp.cu:1088-1198: parameter gradients only).
+ * Progressive levels follow set_training_step (grid.h:2427-2437; 0 = all levels). */
 typedef struct NeusModule NeusModule;
 typedef struct NeusContext NeusContext;
 enum { NEUS_GRADIENT_IGNORE = 0, NEUS_GRADIENT_OVERWRITE = 1, NEUS_GRADIENT_ACCUMULATE = 2 };
@@ -400,7 +409,8 @@ typedef struct NeusModuleInfo {
 	uint64_t grid_offset;   /* first hash-grid parameter (network modules) */
 	float per_level_scale;
 } NeusModuleInfo;
-int neus_module_create_network(const char* config_json, uint32_t batch_capacity, NeusModule** out);
+int neus_module_create_network(uint32_t n_input_dims, uint32_t n_output_dims, const char* network_json, uint32_t batch_capacity, NeusModule** out);
+int neus_module_create_nerf_network(const char* config_json, uint32_t batch_capacity, NeusModule** out);
 int neus_module_create_encoding(uint32_t n_input_dims, const char* encoding_json, uint32_t batch_capacity, NeusModule** out);
 /* create_network_with_input_encoding (cpp_api.h:108; network_with_input_encoding.h): HashGrid -> FullyFusedMLP (1 hidden ReLU
  * layer of n_neurons 16 or 64, linear output padded to 16). Input [n][3] f32, output [n][16] fp16 (column-major, as

@@ -122,7 +122,7 @@ EXPORTS = [
     "neus_testbed_change_frame", "neus_testbed_prepare_for_test", "neus_testbed_get_training_options",
     "neus_testbed_set_training_options", "neus_testbed_saved_transform", "neus_testbed_get_optimizer_state",
     "neus_testbed_set_optimizer_state", "neus_testbed_set_progressive_inference",
-    "neus_module_create_network", "neus_module_create_encoding", "neus_module_create_network_with_input_encoding", "neus_module_destroy", "neus_context_destroy",
+    "neus_module_create_network", "neus_module_create_nerf_network", "neus_module_create_encoding", "neus_module_create_network_with_input_encoding", "neus_module_destroy", "neus_context_destroy",
     "neus_module_info", "neus_module_hyperparams", "neus_module_set_training_step", "neus_module_set_indeed_batch_size",
     "neus_module_initialize_params", "neus_module_inference", "neus_module_forward", "neus_module_backward",
     "neus_module_backward_backward_input",

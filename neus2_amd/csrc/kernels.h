@@ -237,6 +237,27 @@ struct DNetLaunch {
 bool dnet_supported(uint32_t L, uint32_t W);
 uint32_t dnet_blocks(uint32_t n);  // the grid of launch_dnet (= the partial rows of modes 1 and 2)
 void launch_dnet(hipStream_t s, uint32_t L, uint32_t W, int mode /* 0 fwd, 1 bwd, 2 bwd-bwd */, uint32_t n, const DNetLaunch& d);
+// ffmlp.hip: tcnn FullyFusedMLP behind the Identity encoding (cpp_api.cu:170-172, the network of create_network)
+enum : uint32_t { FF_NONE = 0, FF_RELU = 1, FF_EXP = 2, FF_SIGMOID = 3, FF_SQUAREPLUS = 4, FF_SOFTPLUS = 5 };
+enum : uint32_t { FF_MODE_ACT = 0, FF_MODE_DACT = 1, FF_MODE_F32 = 2 };
+struct FfLayer {
+	const half_t* W; uint32_t O, K; uint32_t trans;  // A = W [O][K] or (trans) W^T of W [K][O]
+	const half_t* in; uint32_t ldi;                    // [n][ldi] fp16
+	half_t* out; float* out_f; uint32_t ldo, o_lim;    // [n][ldo] fp16 (modes ACT, DACT) or f32 (mode F32, o < o_lim)
+	const half_t* aux; uint32_t ldx;                   // mode DACT: forward post-activation values [n][ldx]
+	uint32_t mode, act, n;
+};
+struct FfWgrad {
+	const half_t* D; uint32_t ldd, O;                  // [n][ldd] deltas
+	const half_t* X; uint32_t ldx, I;                  // [n][ldx] layer inputs
+	float* partial; uint32_t ld_partial, off;          // partial rows [blocks][ld_partial], this matrix at off (O x I)
+	uint32_t n;
+};
+void launch_ff_layer(hipStream_t s, const FfLayer& L);
+uint32_t ff_wgrad_blocks(uint32_t n);  // blocks (= partial rows) of launch_ff_wgrad for n samples
+void launch_ff_wgrad(hipStream_t s, const FfWgrad& G);
+void launch_ff_input(hipStream_t s, uint32_t n, uint32_t n_in, uint32_t ld, const float* in, float scale, float offset, half_t* x, bool grad);
+void launch_ff_out_delta(hipStream_t s, uint32_t n, uint32_t ld, uint32_t act, const half_t* dL, const half_t* out, half_t* d);
 // march.hip
 void launch_bitfield_linear(hipStream_t s, const uint8_t* bitfield, uint32_t* lin /* LIN_WORDS */);
 // world-space box of every occupied cell of every mip -> scratch[0..6) = {min xyz, max xyz} (optim.hip); the ray

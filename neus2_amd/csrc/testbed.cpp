@@ -2279,13 +2279,43 @@ struct NeusContext {
 	uint32_t n = 0;
 	Dev<float> dydx;     // encoding: dy/dx [6L][n] of the forward (prepare_input_gradients)
 	Dev<uint32_t> enc;   // network with input encoding: the forward's paired encoding [L][n] (the MLP input)
+	Dev<half_t> acts;    // FullyFusedMLP: the forward's input X0 [n][in_pad] and hidden outputs [N][n][W] (post-activation)
+};
+
+// tcnn FullyFusedMLP shape (fully_fused_mlp.cu:816-879): weight matrices [W][in_pad], (N - 1) x [W][W], [out_pad][W]
+struct FfNet {
+	uint32_t W = 0, N = 0, n_in = 0, in_pad = 0, n_out = 0, out_pad = 0, act = FF_RELU, out_act = FF_NONE;
+	std::vector<uint32_t> off, rows, cols;
+	uint32_t P = 0;
+	void build() {
+		off.clear(); rows.clear(); cols.clear(); P = 0;
+		for (uint32_t l = 0; l <= N; ++l) {
+			const uint32_t r = l == N ? out_pad : W, c = l == 0 ? in_pad : W;
+			off.push_back(P); rows.push_back(r); cols.push_back(c); P += r * c;
+		}
+	}
+	size_t acts_halves(uint32_t n) const { return (size_t)n * (in_pad + (size_t)N * W); }
+	static uint32_t activation(const std::string& s) {
+		if (s == "None") return FF_NONE;
+		if (s == "ReLU") return FF_RELU;
+		if (s == "Exponential") return FF_EXP;
+		if (s == "Sigmoid") return FF_SIGMOID;
+		if (s == "Squareplus") return FF_SQUAREPLUS;
+		if (s == "Softplus") return FF_SOFTPLUS;
+		throw std::runtime_error("FullyFusedMLP: activation '" + s + "' is not supported on gfx950 (None, ReLU, Exponential, Sigmoid, Squareplus, "
+		                         "Softplus; Sine has no backward in tcnn's fully fused MLP)");
+	}
 };
 
 struct NeusModule {
 	// Network: the NeuS NerfNetwork; Encoding: a HashGrid; DensityNet: tcnn's NetworkWithInputEncoding(HashGrid ->
 	// FullyFusedMLP with 1 hidden ReLU layer -> 16 linear outputs), the network whose backward_backward_input tcnn
 	// implements (network_with_input_encoding.h:159-250, fully_fused_mlp.cu:1088-1198)
-	enum Kind { Network = 0, Encoding = 1, DensityNet = 2 } kind;
+	// Mlp: tcnn::cpp::create_network = NetworkWithInputEncoding(Identity -> FullyFusedMLP) (cpp_api.cu:170-172), ffmlp.hip
+	enum Kind { Network = 0, Encoding = 1, DensityNet = 2, Mlp = 3 } kind;
+	FfNet ff;
+	Dev<half_t> ff_acts, ff_front, ff_d[2];  // Mlp: inference activations, backward-backward fronts, delta ping-pong
+	Dev<float> ff_partial, ff_dummy;         // Mlp: per-block weight-gradient rows
 	uint32_t n_mlp = 0, dn_width = 0, dn_de = 0;  // DensityNet: MLP parameters W DE + 16 W ahead of the grid, width, padded input
 	Dev<uint32_t> u_tmp;                          // DensityNet: dy/dx . dL_ddLdinput, paired
 	Dev<float> dn_partial, dn_dummy;              // DensityNet: per-block weight-gradient rows
@@ -2305,7 +2335,10 @@ struct NeusModule {
 	Dev<half_t> zero_h;
 	Dev<float4> zero_v;
 	explicit NeusModule(int device) : core(device) {}
-	uint64_t n_params() const { return kind == Network ? core.lay.P : (kind == DensityNet ? n_mlp + core.lay.n_grid : core.lay.n_grid); }
+	uint64_t n_params() const {
+		if (kind == Mlp) return ff.P;
+		return kind == Network ? core.lay.P : (kind == DensityNet ? n_mlp + core.lay.n_grid : core.lay.n_grid);
+	}
 	uint32_t valid() const { return core.valid_level_at(training_step); }
 	void load_params(const void* params, hipStream_t s) {
 		if (!params) throw std::runtime_error("module: null params");
@@ -2320,6 +2353,7 @@ struct NeusModule {
 		if (n > capacity) throw std::runtime_error("module: n_elements exceeds the module's batch capacity");
 		if (backward && kind == Network && (n == 0 || n % 128 != 0))
 			throw std::runtime_error("module backward: n_elements must be a positive multiple of 128 (fully_fused_mlp.cu:779-781)");
+		if (kind == Mlp && n % 128 != 0) throw std::runtime_error("FullyFusedMLP: batch size must be a multiple of 128 (fully_fused_mlp.cu:779-781)");
 	}
 	// the destination of this call's parameter gradients (Overwrite: dL_dparams itself; Accumulate: a scratch buffer)
 	float* grad_target(void* dL_dparams, int mode) {
@@ -2372,9 +2406,9 @@ static void module_common_init(NeusModule* m, uint32_t capacity) {
 	HIP_CHECK(hipStreamSynchronize(m->core.stream));
 }
 
-int neus_module_create_network(const char* config_json, uint32_t batch_capacity, NeusModule** out) {
+int neus_module_create_nerf_network(const char* config_json, uint32_t batch_capacity, NeusModule** out) {
 	return guard([&] {
-		if (!config_json || !out) throw std::runtime_error("neus_module_create_network: null argument");
+		if (!config_json || !out) throw std::runtime_error("neus_module_create_nerf_network: null argument");
 		if (batch_capacity == 0 || batch_capacity % 128 != 0 || batch_capacity > (1u << 24))
 			throw std::runtime_error("batch_capacity must be a positive multiple of 128 (<= 2^24)");
 		const JsonValue j = parse_json(config_json);
@@ -2463,6 +2497,98 @@ int neus_module_create_network_with_input_encoding(uint32_t n_input_dims, uint32
 	});
 }
 
+// tcnn::cpp::create_network(n_input_dims, n_output_dims, network) (cpp_api.cu:170-172): NetworkWithInputEncoding with an
+// Identity encoding (scale 1, offset 0; padded to 16 inputs with ones, identity.h:44-70) and a FullyFusedMLP
+// (fully_fused_mlp.cu:816-879: n_neurons 16 / 32 / 64 / 128, n_hidden_layers >= 1, output padded to 16)
+int neus_module_create_network(uint32_t n_input_dims, uint32_t n_output_dims, const char* network_json, uint32_t batch_capacity, NeusModule** out) {
+	return guard([&] {
+		if (!network_json || !out) throw std::runtime_error("neus_module_create_network: null argument");
+		if (batch_capacity == 0 || batch_capacity % 128 != 0 || batch_capacity > (1u << 24))
+			throw std::runtime_error("batch_capacity must be a positive multiple of 128 (<= 2^24)");
+		const JsonValue j = parse_json(network_json);
+		const std::string ot = j.string("otype", "FullyFusedMLP");
+		if (ot != "FullyFusedMLP" && ot != "MegakernelMLP" && ot != "CutlassMLP")
+			throw std::runtime_error("create_network: only FullyFusedMLP networks are implemented on gfx950");
+		FfNet f;
+		f.W = (uint32_t)j.number("n_neurons", 64);
+		if (f.W != 16 && f.W != 32 && f.W != 64 && f.W != 128)
+			throw std::runtime_error("FullyFusedMLP only supports 16, 32, 64, and 128 neurons, but got " + std::to_string(f.W));
+		const double nh = j.number("n_hidden_layers", 1);
+		if (nh < 1 || nh > 32) throw std::runtime_error("FullyFusedMLP requires at least 1 hidden layer (3 layers in total).");
+		f.N = (uint32_t)nh;
+		if (n_input_dims == 0 || n_input_dims > 128) throw std::runtime_error("create_network: 1..128 input dims on gfx950");
+		if (n_output_dims == 0 || n_output_dims > 128) throw std::runtime_error("create_network: 1..128 output dims on gfx950");
+		f.n_in = n_input_dims; f.in_pad = (n_input_dims + 15) / 16 * 16;
+		f.n_out = n_output_dims; f.out_pad = (n_output_dims + 15) / 16 * 16;
+		f.act = FfNet::activation(j.string("activation", "ReLU"));
+		f.out_act = FfNet::activation(j.string("output_activation", "None"));
+		f.build();
+		int dev = 0;
+		HIP_CHECK(hipGetDevice(&dev));
+		auto m = std::make_unique<NeusModule>(dev);
+		m->kind = NeusModule::Mlp;
+		module_options(m.get(), j);
+		m->ff = f;
+		m->n_in = f.n_in; m->n_out = f.out_pad;  // cpp::Module::n_output_dims = the padded output width
+		m->capacity = batch_capacity;
+		m->gtmp.alloc(f.P);
+		m->ff_acts.alloc(f.acts_halves(batch_capacity));
+		m->ff_front.alloc((size_t)batch_capacity * (f.in_pad + (size_t)f.N * f.W));
+		const uint32_t dmax = std::max(std::max(f.W, f.out_pad), f.in_pad);
+		m->ff_d[0].alloc((size_t)batch_capacity * dmax); m->ff_d[1].alloc((size_t)batch_capacity * dmax);
+		m->ff_partial.alloc((size_t)ff_wgrad_blocks(batch_capacity) * f.P);
+		m->ff_dummy.alloc(4);
+		static const char* an[6] = {"None", "ReLU", "Exponential", "Sigmoid", "Squareplus", "Softplus"};
+		m->hyper = "{\"otype\": \"NetworkWithInputEncoding\", \"encoding\": {\"otype\": \"Identity\", \"scale\": 1, \"offset\": 0}, "
+		           "\"network\": {\"otype\": \"FullyFusedMLP\", \"n_neurons\": " + std::to_string(f.W) + ", \"n_hidden_layers\": " +
+		           std::to_string(f.N) + ", \"activation\": \"" + an[f.act] + "\", \"output_activation\": \"" + an[f.out_act] +
+		           "\"}, \"n_input_dims\": " + std::to_string(f.n_in) + ", \"n_output_dims\": " + std::to_string(f.n_out) +
+		           ", \"gradient_precision\": \"" + (m->grad_fp16 ? "fp16" : "fp32") + "\"}";
+		HIP_CHECK(hipStreamSynchronize(m->core.stream));
+		*out = m.release();
+	});
+}
+
+namespace {
+// FullyFusedMLP passes (ffmlp.hip). acts: X0 [n][in_pad] then hidden l at n (in_pad + l W), each [n][W].
+const half_t* ff_mat(const FfNet& f, const void* params, uint32_t l) { return (const half_t*)params + f.off[l]; }
+half_t* ff_hidden(const FfNet& f, half_t* acts, uint32_t n, uint32_t l) { return acts + (size_t)n * f.in_pad + (size_t)l * n * f.W; }
+FfLayer ff_layer(const half_t* W, uint32_t O, uint32_t K, bool trans, const half_t* in, uint32_t ldi, uint32_t n) {
+	FfLayer L{};
+	L.W = W; L.O = O; L.K = K; L.trans = trans ? 1u : 0u; L.in = in; L.ldi = ldi; L.n = n;
+	return L;
+}
+// forward (mlp_fused_forward, fully_fused_mlp.cu:678-812): hidden layers act(W x), output out_act(W_N h)
+void ff_forward(const FfNet& f, hipStream_t s, uint32_t n, const float* input, const void* params, half_t* acts, half_t* output) {
+	launch_ff_input(s, n, f.n_in, f.in_pad, input, 1.f, 0.f, acts, false);
+	const half_t* x = acts;
+	uint32_t ldx = f.in_pad;
+	for (uint32_t l = 0; l <= f.N; ++l) {
+		FfLayer L = ff_layer(ff_mat(f, params, l), f.rows[l], f.cols[l], false, x, ldx, n);
+		L.mode = FF_MODE_ACT;
+		L.act = l == f.N ? f.out_act : f.act;
+		L.out = l == f.N ? output : ff_hidden(f, acts, n, l);
+		L.ldo = l == f.N ? f.out_pad : f.W;
+		launch_ff_layer(s, L);
+		x = L.out; ldx = f.W;
+	}
+}
+// delta through layer l (l >= 1) to the input of layer l: act'(h_{l-1}) (W_l^T d)
+void ff_back_through(const FfNet& f, hipStream_t s, uint32_t n, const void* params, uint32_t l, const half_t* d, uint32_t ldd, const half_t* acts_fwd,
+                     half_t* out) {
+	FfLayer L = ff_layer(ff_mat(f, params, l), f.cols[l], f.rows[l], true, d, ldd, n);
+	L.mode = FF_MODE_DACT; L.act = f.act; L.out = out; L.ldo = f.W;
+	L.aux = ff_hidden(f, const_cast<half_t*>(acts_fwd), n, l - 1); L.ldx = f.W;
+	launch_ff_layer(s, L);
+}
+void ff_wgrad(const FfNet& f, hipStream_t s, uint32_t n, uint32_t l, const half_t* d, uint32_t ldd, const half_t* x, uint32_t ldx, float* partial) {
+	FfWgrad G{};
+	G.D = d; G.ldd = ldd; G.O = f.rows[l]; G.X = x; G.ldx = ldx; G.I = f.cols[l];
+	G.partial = partial; G.ld_partial = f.P; G.off = f.off[l]; G.n = n;
+	launch_ff_wgrad(s, G);
+}
+}  // namespace
+
 int neus_module_destroy(NeusModule* m) { return guard([&] { delete m; }); }
 int neus_context_destroy(NeusContext* c) { return guard([&] { delete c; }); }
 
@@ -2478,6 +2604,7 @@ int neus_module_info(const NeusModule* m, NeusModuleInfo* o) {
 		o->batch_capacity = m->capacity;
 		o->n_levels = m->core.lay.L;
 		o->grid_offset = m->kind == NeusModule::Network ? m->core.lay.grid_off : (m->kind == NeusModule::DensityNet ? m->n_mlp : 0);
+		if (m->kind == NeusModule::Mlp) { o->n_levels = 0; o->grid_offset = m->ff.P; }  // no encoding parameters
 		o->per_level_scale = m->core.cfg.per_level_scale;
 	});
 }
@@ -2499,7 +2626,17 @@ int neus_module_initialize_params(NeusModule* m, uint64_t seed, float* params_fu
 		HIP_CHECK(hipSetDevice(m->core.device));
 		std::vector<float> h;
 		// cpp::Module::initialize_params draws from pcg32{seed} (cpp_api.cu:162-165; the Trainer's seed_seq is not involved)
-		if (m->kind == NeusModule::Network) {
+		if (m->kind == NeusModule::Mlp) {
+			// NetworkWithInputEncoding::initialize_params: Identity has none; FullyFusedMLP::initialize_params
+			// (fully_fused_mlp.cu:1229-1256): every matrix xavier-uniform in order, U(+-sqrt(6 / (fan_in + fan_out)))
+			// (gpu_matrix.h:292-306) from pcg32{seed} (cpp_api.cu:162-165)
+			h.assign(m->ff.P, 0.f);
+			pcg32 rnd = make_pcg32(seed);
+			for (uint32_t l = 0; l <= m->ff.N; ++l) {
+				const float scale = std::sqrt(6.0f / (float)(m->ff.rows[l] + m->ff.cols[l]));
+				for (uint32_t i = 0; i < m->ff.rows[l] * m->ff.cols[l]; ++i) h[m->ff.off[l] + i] = rnd.next_float() * 2.0f * scale - scale;
+			}
+		} else if (m->kind == NeusModule::Network) {
 			h = m->core.initial_params_rng(make_pcg32(seed), nullptr);
 		} else {  // [FullyFusedMLP xavier matrices (fully_fused_mlp.cu:1229-1256)] then GridEncoding::initialize_params:
 			      // generate_random_uniform(rnd, n_params, -1e-4, 1e-4) (grid.h:2375-2380)
@@ -2534,6 +2671,13 @@ static void module_forward(NeusModule* m, hipStream_t s, uint32_t n, const float
 	if (!input || !output) throw std::runtime_error("module forward: null input / output");
 	m->check_n(n, false);
 	NeusTestbed& t = m->core;
+	if (m->kind == NeusModule::Mlp) {
+		if (!params) throw std::runtime_error("module: null params");
+		if (ctx) ctx->acts.alloc(std::max<size_t>(1, m->ff.acts_halves(n)));
+		ff_forward(m->ff, s, n, input, params, ctx ? ctx->acts.p : m->ff_acts.p, (half_t*)output);
+		HIP_CHECK(hipGetLastError());
+		return;
+	}
 	if (m->kind == NeusModule::DensityNet) {
 		// NetworkWithInputEncoding::forward (network_with_input_encoding.h:84-111): encoding, then the MLP on it
 		if (!params) throw std::runtime_error("module: null params");
@@ -2602,6 +2746,37 @@ int neus_module_backward(NeusModule* m, void* stream, const NeusContext* ctx, ui
 		hipStream_t s = t.stream;
 		float* g = m->grad_target(dL_dparams, gradient_mode);
 		if (!g && !dL_dinput) return;
+		if (m->kind == NeusModule::Mlp) {
+			// FullyFusedMLP::backward_impl (fully_fused_mlp.cu:967-1085): the output activation's backward on dL/doutput, the
+			// deltas through the hidden layers (activation derivative from the stored outputs), dW = D^T x per layer and
+			// dL/dinput = W_0^T D_0 through the Identity encoding's backward (identity.h:86-104: x scale = 1)
+			const FfNet& f = m->ff;
+			if (!params) throw std::runtime_error("module: null params");
+			if (!ctx->acts.p) throw std::runtime_error("module backward: the context is not from this module's forward");
+			if (f.out_act != FF_NONE && !output) throw std::runtime_error("FullyFusedMLP backward: the forward output is needed for its output activation");
+			const half_t* d = (const half_t*)dL_doutput;
+			int pp = 0;
+			if (f.out_act != FF_NONE) { launch_ff_out_delta(s, n, f.out_pad, f.out_act, d, (const half_t*)output, m->ff_d[0].p); d = m->ff_d[0].p; pp = 1; }
+			uint32_t ldd = f.out_pad;
+			for (uint32_t l = f.N + 1; l-- > 0;) {
+				const half_t* x = l == 0 ? ctx->acts.p : ff_hidden(f, ctx->acts.p, n, l - 1);
+				if (g) ff_wgrad(f, s, n, l, d, ldd, x, l == 0 ? f.in_pad : f.W, m->ff_partial.p);
+				if (l > 0) {
+					ff_back_through(f, s, n, params, l, d, ldd, ctx->acts.p, m->ff_d[pp].p);
+					d = m->ff_d[pp].p; pp ^= 1; ldd = f.W;
+				} else if (dL_dinput) {
+					FfLayer L = ff_layer(ff_mat(f, params, 0), f.in_pad, f.W, true, d, ldd, n);
+					L.mode = FF_MODE_F32; L.out_f = dL_dinput; L.ldo = f.n_in; L.o_lim = f.n_in;
+					launch_ff_layer(s, L);
+				}
+			}
+			if (g) {
+				launch_mlp_grad_reduce(s, MlpGradReduce{m->ff_partial.p, ff_wgrad_blocks(n), f.P, g, nullptr, nullptr, 0, m->ff_dummy.p});
+				m->finish_grad(dL_dparams, gradient_mode, s);
+			}
+			HIP_CHECK(hipGetLastError());
+			return;
+		}
 		const uint32_t valid = m->valid();
 		if (m->kind == NeusModule::DensityNet) {
 			// NetworkWithInputEncoding::backward (network_with_input_encoding.h:113-156): the MLP backward gives its weight
@@ -2662,6 +2837,46 @@ int neus_module_backward_backward_input(NeusModule* m, void* stream, const NeusC
 			throw std::runtime_error("NerfNetwork: the eikonal second-order term is part of backward (nerf_network.h:330-601); "
 			                         "backward_backward_input is provided by the HashGrid and network-with-input-encoding modules "
 			                         "(the reference's NerfNetwork does not implement it either: object.h:222-232)");
+		if (m->kind == NeusModule::Mlp) {
+			// NetworkWithInputEncoding::backward_backward_input (network_with_input_encoding.h:159-250) with the Identity
+			// encoding: its backward_backward_input (identity.h:182-206) turns dL_ddLdinput into the network's dL_ddLdinput
+			// (x scale; the padded rows, which the reference leaves uninitialised, are 0: the constant padding has no input
+			// gradient); FullyFusedMLP::backward_backward_input_impl (fully_fused_mlp.cu:1088-1198): fronts f_0 = u,
+			// f_i = act'(h_{i-1}) (W_{i-1} f_{i-1}); backs b_{N+2} = dL_doutput, b_i = act'(h_{i-2}) (W_{i-1}^T b_{i+1});
+			// dW_{i-1} = b_{i+1} f_{i-1}^T. Like the reference, dL_ddLdoutput and dL_dinput are not produced.
+			if (!ctx || ctx->n != n || !ctx->acts.p) throw std::runtime_error("backward_backward_input: needs the forward's context");
+			if (!dL_ddLdinput || !dL_doutput || !params) throw std::runtime_error("backward_backward_input: null input");
+			m->check_n(n, true);
+			HIP_CHECK(hipSetDevice(m->core.device));
+			StreamSwap sw(m->core, stream);
+			hipStream_t s = m->core.stream;
+			float* g = m->grad_target(dL_dparams, gradient_mode);
+			if (!g) return;
+			const FfNet& f = m->ff;
+			half_t* fr = m->ff_front.p;
+			auto front = [&](uint32_t i) { return i == 0 ? fr : fr + (size_t)n * f.in_pad + (size_t)(i - 1) * n * f.W; };
+			launch_ff_input(s, n, f.n_in, f.in_pad, dL_ddLdinput, 1.f, 0.f, fr, true);
+			for (uint32_t i = 1; i <= f.N; ++i) {
+				FfLayer L = ff_layer(ff_mat(f, params, i - 1), f.rows[i - 1], f.cols[i - 1], false, front(i - 1), i == 1 ? f.in_pad : f.W, n);
+				L.mode = FF_MODE_DACT; L.act = f.act; L.out = front(i); L.ldo = f.W;
+				L.aux = ff_hidden(f, ctx->acts.p, n, i - 1); L.ldx = f.W;
+				launch_ff_layer(s, L);
+			}
+			const half_t* b = (const half_t*)dL_doutput;
+			uint32_t ldb = f.out_pad;
+			int pp = 0;
+			for (uint32_t l = f.N + 1; l-- > 0;) {  // dW_l = b_{l+2} f_l^T, then b_{l+1} through W_l
+				ff_wgrad(f, s, n, l, b, ldb, front(l), l == 0 ? f.in_pad : f.W, m->ff_partial.p);
+				if (l > 0) {
+					ff_back_through(f, s, n, params, l, b, ldb, ctx->acts.p, m->ff_d[pp].p);
+					b = m->ff_d[pp].p; pp ^= 1; ldb = f.W;
+				}
+			}
+			launch_mlp_grad_reduce(s, MlpGradReduce{m->ff_partial.p, ff_wgrad_blocks(n), f.P, g, nullptr, nullptr, 0, m->ff_dummy.p});
+			m->finish_grad(dL_dparams, gradient_mode, s);
+			HIP_CHECK(hipGetLastError());
+			return;
+		}
 		if (m->kind == NeusModule::DensityNet) {
 			// NetworkWithInputEncoding::backward_backward_input (network_with_input_encoding.h:159-250): u = dy/dx . dL_ddLdinput
 			// (kernel_grid_backward_input_backward_dLdoutput), the MLP's backward-backward (fully_fused_mlp.cu:1088-1198: b2 =

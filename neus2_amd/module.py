@@ -1,7 +1,8 @@
 """tcnn-shaped operator modules over the gfx950 kernels (include/neus2_hip.h neus_module_*), mirroring
 tiny-cuda-nn's C++ API (dependencies/my_tcnn/include/tiny-cuda-nn/cpp_api.h:66-110) the reference's bindings wrap:
-create_network / create_encoding, n_params, initialize_params, inference, forward (-> Context), backward,
-backward_backward_input with explicit parameter pointers and EGradientMode (object.h:90-94).
+create_network(n_input_dims, n_output_dims, network) / create_encoding / create_network_with_input_encoding (the names
+mean what tcnn's mean) plus create_nerf_network (the NeuS NerfNetwork), n_params, initialize_params, inference, forward
+(-> Context), backward, backward_backward_input with explicit parameter pointers and EGradientMode (object.h:90-94).
 
 Arguments are torch CUDA tensors (device memory + the current stream); outputs are allocated here unless given.
 """
@@ -40,7 +41,8 @@ class Context:
 
 
 class Module:
-    """tcnn::cpp::Module. kind 'network' = the NeuS NerfNetwork (input [n, 7] f32, output [n, 16] fp16),
+    """tcnn::cpp::Module. kind 'mlp' = create_network's Identity -> FullyFusedMLP (input [n, n_input_dims] f32, output
+    [n, padded output] fp16), 'network' = the NeuS NerfNetwork (input [n, 7] f32, output [n, 16] fp16),
     'encoding' = the HashGrid encoding (input [n, 3] f32; output layout by the config's "output_layout": "AoS" [n, 2L]
     (default: the column-major view cpp::Module gives its caller, cpp_api.cu:58-70), "SoA" [2L, n] (GridEncoding's
     preferred layout, grid.h:2357-2359) or "paired" [L, n, 2] (this build's kernels)). dL_dparams is fp16 (tcnn's param
@@ -56,12 +58,23 @@ class Module:
         self.gradient_precision = hp.get("gradient_precision", "fp16")
 
     @classmethod
-    def create_network(cls, config, batch_capacity=1 << 18):
-        """create_network_with_input_encoding for the NeuS network: `config` is the configs/nerf/*.json object
-        (or its text) with "encoding", "network" and "rgb_network"."""
+    def create_network(cls, n_input_dims, n_output_dims, network, batch_capacity=1 << 18):
+        """tcnn create_network (cpp_api.h:109; cpp_api.cu:170-172): NetworkWithInputEncoding with an Identity encoding and
+        a FullyFusedMLP (`network`: {"otype": "FullyFusedMLP", "n_neurons", "n_hidden_layers", "activation",
+        "output_activation"})."""
+        text = network if isinstance(network, str) else json.dumps(network)
+        h = C.c_void_p()
+        check(lib().neus_module_create_network(C.c_uint32(n_input_dims), C.c_uint32(n_output_dims), text.encode(),
+                                               C.c_uint32(batch_capacity), C.byref(h)))
+        return cls(h, "mlp")
+
+    @classmethod
+    def create_nerf_network(cls, config, batch_capacity=1 << 18):
+        """The NeuS NerfNetwork (nerf_network.h): `config` is the configs/nerf/*.json object (or its text) with
+        "encoding", "network" and "rgb_network"."""
         text = config if isinstance(config, str) else json.dumps(config)
         h = C.c_void_p()
-        check(lib().neus_module_create_network(text.encode(), C.c_uint32(batch_capacity), C.byref(h)))
+        check(lib().neus_module_create_nerf_network(text.encode(), C.c_uint32(batch_capacity), C.byref(h)))
         return cls(h, "network")
 
     @classmethod
@@ -129,6 +142,8 @@ class Module:
         return torch.empty(self.output_shape(n), dtype=torch.float16, device="cuda")
 
     def output_shape(self, n):
+        if self.kind == "mlp":
+            return (n, self.n_output_dims)
         if self.kind != "encoding":
             return (n, 16)
         L = self.info["n_levels"]
@@ -169,8 +184,12 @@ class Module:
         return dL_dparams, dL_ddLdoutput
 
 
-def create_network(config, batch_capacity=1 << 18):
-    return Module.create_network(config, batch_capacity)
+def create_network(n_input_dims, n_output_dims, network, batch_capacity=1 << 18):
+    return Module.create_network(n_input_dims, n_output_dims, network, batch_capacity)
+
+
+def create_nerf_network(config, batch_capacity=1 << 18):
+    return Module.create_nerf_network(config, batch_capacity)
 
 
 def create_encoding(encoding, batch_capacity=1 << 18, n_input_dims=3):

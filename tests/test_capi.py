@@ -95,3 +95,22 @@ def test_mc_table_matches_oracle_restatement():
     out = np.zeros((256, 19), np.int8)
     check(lib().neus_mc_table(C.c_void_p(out.ctypes.data)))
     np.testing.assert_array_equal(out, mc_table.build_table())
+
+
+@pytest.mark.parametrize("n_in,n_out,net,msg", [
+    (32, 3, '{"otype": "FullyFusedMLP", "n_neurons": 48, "n_hidden_layers": 2}', "only supports 16, 32, 64, and 128 neurons"),
+    (32, 3, '{"otype": "FullyFusedMLP", "n_neurons": 64, "n_hidden_layers": 0}', "at least 1 hidden layer"),
+    (32, 3, '{"otype": "FullyFusedMLP", "n_neurons": 64, "activation": "Sine"}', "Sine has no backward"),
+    (32, 3, '{"otype": "CutlassResNet"}', "only FullyFusedMLP"),
+    (0, 3, '{"otype": "FullyFusedMLP"}', "input dims"),
+])
+def test_create_network_validates_config(n_in, n_out, net, msg):
+    """tcnn create_network's FullyFusedMLP checks (fully_fused_mlp.cu:816-879, network.cu:111-120) run before any device
+    call: a bad config is an error status with tcnn's message (no GPU needed)."""
+    from neus2_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libneus2_hip.so not built")
+    lib = _lib.lib()
+    h = C.c_void_p()
+    rc = lib.neus_module_create_network(C.c_uint32(n_in), C.c_uint32(n_out), net.encode(), C.c_uint32(1024), C.byref(h))
+    assert rc != 0 and msg in lib.neus_last_error().decode()

@@ -54,8 +54,8 @@ def test_network_module(torch_cuda):
     tb.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
     tb.reload_network_from_json(cfg_dict, batch_size=4096)
     lay = tb.layout()
-    m = Module.create_network(dict(cfg_dict, gradient_precision="fp32"), batch_capacity=4096)
-    m16 = Module.create_network(cfg_dict, batch_capacity=4096)  # default: fp16 dL_dparams (tcnn's param precision)
+    m = Module.create_nerf_network(dict(cfg_dict, gradient_precision="fp32"), batch_capacity=4096)
+    m16 = Module.create_nerf_network(cfg_dict, batch_capacity=4096)  # default: fp16 dL_dparams (tcnn's param precision)
     assert m.n_params == lay["n_params"] and m.n_input_dims == 7 and m.n_output_dims == 16
     assert m.name() == "NerfNetwork" and m.info["grid_offset"] == lay["grid_offset"]
     assert abs(m.info["per_level_scale"] - lay["per_level_scale"]) < 1e-6
