@@ -363,6 +363,10 @@ typedef struct NeusDataParallelInfo {
 	uint64_t last_step_allreduce_bytes;
 } NeusDataParallelInfo;
 int neus_testbed_data_parallel_info(NeusTestbed* tb, NeusDataParallelInfo* out);
+/* Overlapped gradient exchange (default on): the MLP blocks are all-reduced after the weight-gradient reduction and the
+ * hash-grid levels in three groups as the scatter finishes them, on a communication stream beside the rest of the
+ * backward; off: one grouped exchange after the backward (the same elementwise sums). */
+int neus_testbed_set_exchange_overlap(NeusTestbed* tb, int on);
 /* In-process ranks: `world` testbeds driven from `world` host threads exchange through host staging buffers
  * (same step and collectives as the RCCL path: sharded occupancy update + max all-reduce, gradient / counter /
  * loss / DeltaNetwork sum all-reduces). For several ranks on one device (tests); collectives block until every

@@ -534,14 +534,13 @@ constexpr int SC_U = 8;
 #endif
 constexpr int SC_WAVES = NEUS_SC_WAVES;  // (8 waves per workgroup measured slower: 93 -> 103 us at the bench state)
 __global__ void __launch_bounds__(64 * SC_WAVES) k_scatter_accum_r(ScatterWork w, const GridLevels gl, float* __restrict__ grads, uint32_t bs8,
-                                                                   uint32_t n_jobs) {
+                                                                   uint32_t job0) {
 	__shared__ unsigned long long acc[2 * SB_SIZE];
 	__shared__ uint32_t s_pre[SC_WAVES][65], s_src[SC_WAVES][64];
 	__shared__ uint32_t s_last;
 	// (jobs in list order: an XCD-contiguous mapping - each XCD taking an eighth of the list, so adjacent buckets'
 	// segments that share lines meet in one L2 - measured 93 -> 169 us at the bench state)
-	(void)n_jobs;
-	const uint4 job = w.jobs2[blockIdx.x];
+	const uint4 job = w.jobs2[job0 + blockIdx.x];
 	const uint32_t l = job.x, kb = job.y, part = job.z & 0xffffu, parts = job.z >> 16, slot = job.w;
 	const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
 	for (uint32_t k = threadIdx.x; k < 2 * SB_SIZE; k += blockDim.x) acc[k] = 0ull;
@@ -819,7 +818,7 @@ uint32_t scatter_n_buckets(const GridLevels& gl) {
 }
 void launch_grid_scatter(hipStream_t s, const uint32_t* n_ptr, uint32_t n_fixed, uint32_t ld, const float* coords, uint32_t coord_stride,
                          const GridLevels& gl, uint32_t valid_level, const half_t* dLdenc, const half_t* g, const float4* v, float* grads,
-                         const ScatterWork& w, void* scan_tmp, size_t scan_tmp_bytes) {
+                         const ScatterWork& w, void* scan_tmp, size_t scan_tmp_bytes, const ScatterSplit* split) {
 	if (w.mode == 2) {
 		// the grid spans the workspace's sample capacity (w.n_chunks x w.chunk >= n)
 		// one workgroup per (chunk, level) by default: ~14x the workgroups of a level loop, so the phases (corner
@@ -835,8 +834,21 @@ void launch_grid_scatter(hipStream_t s, const uint32_t* n_ptr, uint32_t n_fixed,
 		else
 			k_scatter_bin_r<512><<<grid, 512, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, (const uint32_t*)dLdenc,
 			                                          (const uint32_t*)g, v, w);
-		const uint32_t nj = std::min(w.n_jobs2, w.jobs2_before[std::min(valid_level + 1, gl.n_levels)]);
-		if (nj) k_scatter_accum_r<<<nj, 64 * SC_WAVES, 0, s>>>(w, gl, grads, w.chunk * 8, nj);
+		const uint32_t n_act = std::min(valid_level + 1, gl.n_levels);
+		if (!split) {
+			const uint32_t nj = std::min(w.n_jobs2, w.jobs2_before[n_act]);
+			if (nj) k_scatter_accum_r<<<nj, 64 * SC_WAVES, 0, s>>>(w, gl, grads, w.chunk * 8, 0u);
+			return;
+		}
+		uint32_t lo = 0;
+		for (uint32_t gi = 0; gi < split->n_groups && lo < n_act; ++gi) {
+			const uint32_t hi = gi + 1 == split->n_groups ? n_act : std::min(split->level_end[gi], n_act);
+			if (hi <= lo) continue;
+			const uint32_t j0 = std::min(w.n_jobs2, w.jobs2_before[lo]), j1 = std::min(w.n_jobs2, w.jobs2_before[hi]);
+			if (j1 > j0) k_scatter_accum_r<<<j1 - j0, 64 * SC_WAVES, 0, s>>>(w, gl, grads, w.chunk * 8, j0);
+			if (split->done) split->done(lo, hi);
+			lo = hi;
+		}
 		return;
 	}
 	if (w.mode == 0) {

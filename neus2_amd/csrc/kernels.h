@@ -1,6 +1,7 @@
 // Host-callable launchers of the gfx950 kernels (defined in the .hip files) and the structs
 // shared between the host orchestration (testbed.cpp) and the kernels.
 #pragma once
+#include <functional>
 #include <vector>
 #include "common.h"
 
@@ -182,9 +183,13 @@ void launch_grid_encode(hipStream_t s, const uint32_t* n_ptr, uint32_t n_fixed, 
                         const GridLevels& gl, uint32_t valid_level, const half_t* grid, uint32_t* enc, float* dydx, uint32_t grid_x, const EncodeRollover* ro = nullptr);
 size_t scatter_records_capacity(uint32_t n_cap, uint32_t n_levels);
 uint32_t scatter_n_buckets(const GridLevels& gl);
+// Level groups of the accumulation (region mode): the accumulation runs group by group, level-major, and after the
+// launch of the levels [lo, hi) `done(lo, hi)` is called (their gradient range is final once that launch completes on
+// the stream): the data-parallel step all-reduces it beside the accumulation of the next group
+struct ScatterSplit { uint32_t n_groups; uint32_t level_end[8]; std::function<void(uint32_t, uint32_t)> done; };
 void launch_grid_scatter(hipStream_t s, const uint32_t* n_ptr, uint32_t n_cap, uint32_t ld, const float* coords, uint32_t coord_stride,
                          const GridLevels& gl, uint32_t valid_level, const half_t* dLdenc, const half_t* g, const float4* v, float* grads,
-                         const ScatterWork& w, void* scan_tmp, size_t scan_tmp_bytes);
+                         const ScatterWork& w, void* scan_tmp, size_t scan_tmp_bytes, const ScatterSplit* split = nullptr);
 // mlp.hip
 bool mlp_supported(uint32_t n_levels, uint32_t width);
 void mlp_din_permutation(uint32_t L, int32_t* perm /* DIN entries: physical row -> logical din index or -1 */);

@@ -293,6 +293,55 @@ struct NeusTestbed {
 	NeusLocalGroup* group = nullptr;
 	uint32_t rank = 0, world = 1;
 	bool force_coll = false;  // issue the collectives at world 1 too (a forced one-rank communicator, tests)
+	// Overlapped gradient exchange: each finished gradient range is all-reduced as soon as its producer
+	// finishes - the MLP blocks after the weight-gradient reduction, the grid levels group by group beside the scatter's
+	// accumulation of the later groups - on comm_stream (RCCL; one stream keeps every rank's collectives in one order),
+	// which the step's stream joins before the optimizer. Off (NEUS_EXCHANGE_OVERLAP=0, neus_testbed_set_exchange_overlap):
+	// one grouped exchange after the backward. Elementwise sums are the same either way (bitwise with two ranks).
+	bool exchange_overlap = true;
+	hipStream_t comm_stream = nullptr;
+	hipEvent_t ev_x[16] = {};
+	uint32_t ev_x_n = 0;
+	hipEvent_t ev_xdone = nullptr;
+	bool x_pending = false;
+	static constexpr uint32_t X_GROUPS = 3;   // grid level groups of the overlapped exchange (~equal bytes at L=14)
+	// on comm_stream after the work queued so far on the step's stream (RCCL); the in-process group stages on the host
+	hipStream_t x_stream() {
+		if (!comm) return stream;
+		if (!comm_stream) {
+			HIP_CHECK(hipStreamCreateWithFlags(&comm_stream, hipStreamNonBlocking));
+			HIP_CHECK(hipEventCreateWithFlags(&ev_xdone, hipEventDisableTiming));
+		}
+		hipEvent_t& e = ev_x[ev_x_n++ % 16];
+		if (!e) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+		HIP_CHECK(hipEventRecord(e, stream));
+		HIP_CHECK(hipStreamWaitEvent(comm_stream, e, 0));
+		x_pending = true;
+		return comm_stream;
+	}
+	void x_join() {  // the step's stream waits for every exchange issued on comm_stream
+		if (!x_pending) return;
+		HIP_CHECK(hipEventRecord(ev_xdone, comm_stream));
+		HIP_CHECK(hipStreamWaitEvent(stream, ev_xdone, 0));
+		x_pending = false;
+	}
+	// level groups of the overlapped exchange: the active levels cut where the cumulative parameter count passes 1/3, 2/3
+	ScatterSplit x_split(uint32_t valid, float* grid_grads) {
+		ScatterSplit sp{};
+		const uint32_t n_act = std::min(valid + 1, gl.n_levels);
+		sp.n_groups = X_GROUPS;
+		const uint64_t tot = gl.offset[n_act];
+		uint32_t gi = 0;
+		for (uint32_t l = 1; l < n_act && gi + 1 < X_GROUPS; ++l)
+			if ((uint64_t)gl.offset[l] * X_GROUPS >= tot * (gi + 1)) sp.level_end[gi++] = l;
+		for (; gi + 1 < X_GROUPS; ++gi) sp.level_end[gi] = n_act;
+		sp.level_end[X_GROUPS - 1] = n_act;
+		sp.done = [this, grid_grads](uint32_t lo, uint32_t hi) {
+			hipStream_t xs = x_stream();
+			allreduce_f32(grid_grads + 2 * (size_t)gl.offset[lo], 2 * (size_t)(gl.offset[hi] - gl.offset[lo]), false, xs);
+		};
+		return sp;
+	}
 	uint64_t coll_calls = 0, coll_bytes = 0, coll_bytes_step = 0;
 	bool coll_on() const { return world > 1 || force_coll; }
 	// profiling
@@ -345,6 +394,9 @@ struct NeusTestbed {
 		if (ev_fork) (void)hipEventDestroy(ev_fork);
 		if (ev_join) (void)hipEventDestroy(ev_join);
 		if (ev_loss) (void)hipEventDestroy(ev_loss);
+		if (comm_stream) { (void)hipStreamSynchronize(comm_stream); (void)hipStreamDestroy(comm_stream); }
+		for (auto& e : ev_x) if (e) (void)hipEventDestroy(e);
+		if (ev_xdone) (void)hipEventDestroy(ev_xdone);
 		for (auto& e : it_ev) if (e) (void)hipEventDestroy(e);
 		if (stream) (void)hipStreamDestroy(stream);
 	}
@@ -395,6 +447,7 @@ struct NeusTestbed {
 		occ_bbox.alloc(occ_bbox_scratch_floats());
 		launch_occ_bbox(stream, bitfield.p, occ_bbox.p);
 		{ const char* e = std::getenv("NEUS_RAY_CULL"); ray_cull = !(e && e[0] == '0'); }
+		{ const char* e = std::getenv("NEUS_EXCHANGE_OVERLAP"); exchange_overlap = !(e && e[0] == '0'); }
 		{ const char* e = std::getenv("NEUS_OCC_SORT"); occ_sort = !(e && e[0] == '0'); }
 		if (const char* e = std::getenv("NEUS_CHUNK_ENDS")) {
 			std::vector<uint32_t> v;
@@ -820,7 +873,8 @@ struct NeusTestbed {
 	}
 	// forward recompute + backward into g (fp32 [P], zeroed by the caller)
 	void net_backward(const uint32_t* n_valid_ptr, const uint32_t* n_train_ptr, uint32_t n, const float* c, uint32_t valid,
-	                  const half_t* dlo, float* g, hipStream_t s, bool marks = false, bool canonical = true, const EncodeRollover* ro = nullptr) {
+	                  const half_t* dlo, float* g, hipStream_t s, bool marks = false, bool canonical = true, const EncodeRollover* ro = nullptr,
+	                  bool exchange = false) {
 		const uint32_t ld = n;
 		encode(n_train_ptr, n, n, ld, c, COORD_W, valid, true, s, ro);
 		if (marks) mark(5);
@@ -831,25 +885,36 @@ struct NeusTestbed {
 		if (!canonical) { if (marks) mark(7); return; }  // global-movement phase: canonical gradients unused
 		// the MLP weight gradients were accumulated inside the training kernels: one small fixed-order reduction
 		launch_mlp_grad_reduce(s, grad_reduce(n, g, n_train_ptr));
+		if (exchange) {  // the MLP blocks and the variance are final: their exchange runs beside the grid scatter
+			hipStream_t xs = x_stream();
+			allreduce_f32(g, lay.grid_off, false, xs);
+			allreduce_f32(g + lay.var_off, lay.P - lay.var_off, false, xs);
+		}
 		if (marks) mark(7);
-		launch_grid_scatter(s, n_train_ptr, n, ld, c, COORD_W, gl, valid, tbuf.dLdenc, tbuf.genc, tbuf.v, g + lay.grid_off,
-		                    scatter_work_for(g + lay.grid_off, valid, s), scan_tmp.p, scan_tmp_bytes);
+		const ScatterWork sw = scatter_work_for(g + lay.grid_off, valid, s);
+		const ScatterSplit sp = exchange && sw.mode == 2 ? x_split(valid, g + lay.grid_off) : ScatterSplit{};
+		launch_grid_scatter(s, n_train_ptr, n, ld, c, COORD_W, gl, valid, tbuf.dLdenc, tbuf.genc, tbuf.v, g + lay.grid_off, sw, scan_tmp.p,
+		                    scan_tmp_bytes, exchange && sw.mode == 2 ? &sp : nullptr);
+		if (exchange && sw.mode != 2) {  // other scatter modes: the grid exchange after the whole scatter
+			const size_t grid_act = 2 * (size_t)gl.offset[std::min(valid + 1, gl.n_levels)];
+			allreduce_f32(g + lay.grid_off, grid_act, false, x_stream());
+		}
 	}
 
 	// ------------------------------------------------------------ collectives
 	void coll_begin() { if (comm) NCCL_CHECK(ncclGroupStart()); }
 	void coll_end() { if (comm) NCCL_CHECK(ncclGroupEnd()); }
-	void allreduce_f32(float* p, size_t n, bool max_op = false) {
+	void allreduce_f32(float* p, size_t n, bool max_op = false, hipStream_t on = nullptr) {
 		if (!coll_on() || n == 0) return;
 		++coll_calls; coll_bytes += n * 4; coll_bytes_step += n * 4;
-		if (comm) NCCL_CHECK(ncclAllReduce(p, p, n, ncclFloat32, max_op ? ncclMax : ncclSum, comm, stream));
+		if (comm) NCCL_CHECK(ncclAllReduce(p, p, n, ncclFloat32, max_op ? ncclMax : ncclSum, comm, on ? on : stream));
 		else if (group) group->allreduce<float>(rank, p, n, max_op ? NeusLocalGroup::MAX : NeusLocalGroup::SUM, stream);
 		else throw std::runtime_error("data parallel: no communicator");
 	}
-	void allreduce_u32(uint32_t* p, size_t n) {
+	void allreduce_u32(uint32_t* p, size_t n, hipStream_t on = nullptr) {
 		if (!coll_on() || n == 0) return;
 		++coll_calls; coll_bytes += n * 4; coll_bytes_step += n * 4;
-		if (comm) NCCL_CHECK(ncclAllReduce(p, p, n, ncclUint32, ncclSum, comm, stream));
+		if (comm) NCCL_CHECK(ncclAllReduce(p, p, n, ncclUint32, ncclSum, comm, on ? on : stream));
 		else if (group) group->allreduce<uint32_t>(rank, p, n, NeusLocalGroup::SUM, stream);
 		else throw std::runtime_error("data parallel: no communicator");
 	}
@@ -1232,14 +1297,17 @@ struct NeusTestbed {
 		// entry by k_scatter_accum, zeros with no samples); the global-movement phase skips it: zero the buffer there
 		if (!(!dyn || train_canonical)) HIP_CHECK(hipMemsetAsync(grads.p, 0, (size_t)lay.P * 4, s));
 		mark(4);
+		// the overlapped exchange (coll_on): the canonical backward all-reduces its gradient ranges as they finish
+		const bool xo = coll_on() && exchange_overlap && (!dyn || train_canonical);
+		coll_bytes_step = 0;
 		if (use_delta) {
 			// the training forward runs on the deformed batch; dL/d(position) feeds the DeltaNetwork backward
 			launch_delta_apply(s, nullptr, batch, COORD_W, coords_c.p, coords_cdef.p, delta.p);
 			tbuf.dpos = dpos.p;
-			net_backward(&st.p->compacted_counter, &st.p->n_train, batch, coords_cdef.p, valid, dL_dout.p, grads.p, s, true, train_canonical);
+			net_backward(&st.p->compacted_counter, &st.p->n_train, batch, coords_cdef.p, valid, dL_dout.p, grads.p, s, true, train_canonical, nullptr, xo);
 			tbuf.dpos = nullptr;
 		} else {
-			net_backward(&st.p->compacted_counter, &st.p->n_train, batch, coords_c.p, valid, dL_dout.p, grads.p, s, true, train_canonical, &ro);
+			net_backward(&st.p->compacted_counter, &st.p->n_train, batch, coords_c.p, valid, dL_dout.p, grads.p, s, true, train_canonical, &ro, xo);
 		}
 		// DeltaNetwork gradient partial sums (the first half of its backward; the Adam step follows the exchange)
 		if (use_delta) launch_delta_grad(s, &st.p->n_train, batch, coords_c.p, COORD_W, dpos.p, delta.p, delta_partial.p);
@@ -1250,19 +1318,24 @@ struct NeusTestbed {
 			launch_sum_f32(s, scan_tmp.p, scan_tmp_bytes, mask.p, loss_sum.p + 2, MAX_RAYS);
 		}
 		if (coll_on()) {
-			// collective 1 (gradients; DeltaNetwork partials) and 3 (counters, loss scalars) of SURVEY §8(e), one group.
-			// The gradient of the grid levels past the progressive valid level is zero on every rank (no records; the
-			// scatter keeps that range zeroed), so only the MLP blocks, the active levels' tables and the variance move.
-			coll_bytes_step = 0;
+			// collective 1 (gradients; DeltaNetwork partials) and 3 (counters, loss scalars) of SURVEY §8(e). The gradient
+			// of the grid levels past the progressive valid level is zero on every rank: the scatter writes no records there
+			// and keeps that range zeroed (scatter_work_for's sc_zero_from / sc_zero_from_e invariant: every grid entry from
+			// gl.offset[valid + 1] on holds 0 after the backward, on every rank), so only the MLP blocks, the active levels'
+			// tables and the variance move. Overlapped: the gradients went out during the backward (net_backward).
 			const size_t grid_act = 2 * (size_t)gl.offset[std::min(valid + 1, gl.n_levels)];
+			hipStream_t xs = xo ? x_stream() : stream;
 			coll_begin();
-			allreduce_f32(grads.p, (size_t)lay.grid_off + grid_act);
-			allreduce_f32(grads.p + lay.var_off, lay.P - lay.var_off);
-			allreduce_u32(&st.p->compacted_counter, 1);
-			allreduce_u32(&st.p->n_rays_with_samples, 1);
-			if (use_delta) allreduce_f32(delta_partial.p, delta_partial_floats());
-			if (get_loss) allreduce_f32(loss_sum.p, 3);
+			if (!xo) {
+				allreduce_f32(grads.p, (size_t)lay.grid_off + grid_act);
+				allreduce_f32(grads.p + lay.var_off, lay.P - lay.var_off);
+			}
+			allreduce_u32(&st.p->compacted_counter, 1, xs);
+			allreduce_u32(&st.p->n_rays_with_samples, 1, xs);
+			if (use_delta) allreduce_f32(delta_partial.p, delta_partial_floats(), false, xs);
+			if (get_loss) allreduce_f32(loss_sum.p, 3, false, xs);
 			coll_end();
+			x_join();
 		}
 		if (get_loss) {
 			// the previous readback (16 steps back, long done on the device) is checked first: a health failure then
@@ -1970,6 +2043,12 @@ int neus_testbed_init_data_parallel_ex(NeusTestbed* tb, int rank, int world, con
 			std::memcpy(&id, uid, 128);
 			NCCL_CHECK(ncclCommInitRank(&tb->comm, world, id, rank));
 		}
+	});
+}
+int neus_testbed_set_exchange_overlap(NeusTestbed* tb, int on) {
+	return guard([&] {
+		HIP_CHECK(hipStreamSynchronize(tb->stream));
+		tb->exchange_overlap = on != 0;
 	});
 }
 int neus_testbed_init_data_parallel(NeusTestbed* tb, int rank, int world, const uint8_t* uid) {

@@ -1181,6 +1181,10 @@ class Testbed:
         check(lib().neus_testbed_init_data_parallel_ex(self._h, C.c_int(rank), C.c_int(world), buf,
                                                        C.c_uint32(1 if force_collectives else 0)))
 
+    def set_exchange_overlap(self, on=True):
+        """Overlapped gradient exchange of the data-parallel step (default on; off: one exchange after the backward)."""
+        check(lib().neus_testbed_set_exchange_overlap(self._h, C.c_int(1 if on else 0)))
+
     def data_parallel_info(self):
         from ._lib import NeusDataParallelInfo
         o = NeusDataParallelInfo()

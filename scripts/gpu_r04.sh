@@ -28,7 +28,7 @@ if [ "${PMC:-1}" = "1" ]; then
   bash scripts/gpu_traffic_steps.sh ${TAG}_steps 20 || exit 1
 fi
 if [ "${ANCHOR:-1}" = "1" ]; then
-  timeout -k 10 300 python -u scripts/psnr_anchor.py --side gpu --steps 1000 --checkpoints 250,500 > gpurun_out/psnr_anchor_gpu_$TAG.jsonl 2>&1 || { echo ANCHOR_FAIL; exit 1; }
+  timeout -k 10 300 python -u scripts/psnr_anchor.py --side gpu --steps 2000 --checkpoints 250,500,1000,1500 > gpurun_out/psnr_anchor_gpu_$TAG.jsonl 2>&1 || { echo ANCHOR_FAIL; exit 1; }
   cat gpurun_out/psnr_anchor_gpu_$TAG.jsonl
 fi
 echo ALL_OK

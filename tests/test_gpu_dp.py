@@ -179,11 +179,35 @@ def test_dp_step_gradient_matches_oracle_and_ranks_stay_identical(scene):
     del group
 
 
+def test_dp_overlapped_exchange_bitwise(scene):
+    """The overlapped gradient exchange (MLP blocks after the weight-gradient reduction, the grid levels in three
+    groups as the scatter finishes them) against the one grouped exchange after the backward: two world-2 groups from
+    the same init train 20 steps (crossing progressive-level changes and occupancy updates); every rank of both groups
+    holds bitwise the same parameters, gradients and EMA weights, and the overlapped ranks issued more (split)
+    collective calls for the same bytes."""
+    R = 2048
+    ga, (a0, a1) = _ranks(scene, fixed_rays=R)
+    gb, (b0, b1) = _ranks(scene, fixed_rays=R)
+    for tb in (b0, b1):
+        tb.set_exchange_overlap(False)
+    _parallel(lambda: a0.train_steps(20), lambda: a1.train_steps(20))
+    _parallel(lambda: b0.train_steps(20), lambda: b1.train_steps(20))
+    for x in (a1, b0, b1):
+        np.testing.assert_array_equal(a0.get_params().view(np.uint32), x.get_params().view(np.uint32))
+        np.testing.assert_array_equal(a0.get_gradients().view(np.uint32), x.get_gradients().view(np.uint32))
+        np.testing.assert_array_equal(a0.get_ema_params().view(np.uint32), x.get_ema_params().view(np.uint32))
+    ia, ib = a0.data_parallel_info(), b0.data_parallel_info()
+    assert ia["allreduce_bytes"] == ib["allreduce_bytes"]
+    assert ia["collective_calls"] > ib["collective_calls"]
+    del ga, gb
+
+
 def test_rccl_world1_matches_no_communicator(scene):
     """The RCCL path of the data-parallel step with a world-1 communicator (neus_nccl_unique_id ->
     neus_testbed_init_data_parallel(0, 1, id): ncclCommInitRank, and the grouped ncclAllReduce calls of every step
     forced on although one rank would skip them): 12 steps are bitwise identical to the testbed without a
-    communicator (a one-rank all-reduce is the identity)."""
+    communicator (a one-rank all-reduce is the identity). The default overlapped exchange runs its all-reduces on the
+    communication stream, joined by events; the non-overlapped grouped exchange is checked the same way."""
     from neus2_amd import pyngp
     R = 2048
     plain = _testbed(scene, fixed_rays=R)
@@ -198,6 +222,11 @@ def test_rccl_world1_matches_no_communicator(scene):
     for k in ("training_step", "rays_per_batch", "measured_batch_size", "n_rays_total", "loss"):
         assert sp[k] == sc[k], k
     assert comm.data_parallel_info()["collective_calls"] > 0
+    grouped = _testbed(scene, fixed_rays=R)
+    grouped.init_data_parallel(0, 1, pyngp.nccl_unique_id(), force_collectives=True)
+    grouped.set_exchange_overlap(False)
+    grouped.train_steps(12)
+    np.testing.assert_array_equal(plain.get_params(), grouped.get_params())
 
 
 def test_dp_dynamic_frame_movement_identical(torch_cuda):
