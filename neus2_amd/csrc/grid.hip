@@ -37,8 +37,8 @@ __global__ void __launch_bounds__(256) k_grid_encode(
 	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
 		const uint32_t src = i < n_in ? i : i % n_in;  // (n_in > 0 whenever n > 0: n_train is 0 without records)
 		if (l == 0 && i != src) {
-			float* cw = (float*)coords;
-			for (uint32_t k = 0; k < coord_stride; ++k) cw[(size_t)i * coord_stride + k] = coords[(size_t)src * coord_stride + k];
+			// rows i >= n_in are written, rows src < n_in read: the const input view and ro.coords never meet on an element
+			for (uint32_t k = 0; k < coord_stride; ++k) ro.coords[(size_t)i * coord_stride + k] = coords[(size_t)src * coord_stride + k];
 #pragma unroll
 			for (int k = 0; k < OUT_W; ++k) {
 				const float r = (float)ro.dL_dout[(size_t)src * OUT_W + k];
@@ -774,7 +774,7 @@ void launch_grid_encode(hipStream_t s, const uint32_t* n_ptr, uint32_t n_fixed, 
                         const GridLevels& gl, uint32_t valid_level, const half_t* grid, uint32_t* enc, float* dydx, uint32_t grid_x,
                         const EncodeRollover* ro) {
 	if (!grid_x) return;
-	const EncodeRollover r = ro ? *ro : EncodeRollover{nullptr, 0u, nullptr};
+	const EncodeRollover r = ro ? *ro : EncodeRollover{nullptr, 0u, nullptr, nullptr};
 	k_grid_encode<<<dim3(grid_x, gl.n_levels), 256, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, grid, enc, dydx, r);
 }
 size_t scatter_records_capacity(uint32_t n_cap, uint32_t n_levels) { return (size_t)n_cap * n_levels * 8; }

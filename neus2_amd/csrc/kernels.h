@@ -177,8 +177,9 @@ struct TransposeJobs { TransposeJob j[8]; uint32_t n; };
 
 // grid.hip
 // the training batch's rollover done by the encode (k_grid_encode): n_in = *n_in_ptr (compacted count) records are real,
-// the rest of the n_elements batch copies record i % n_in (coordinates in place, dL_dout rescaled)
-struct EncodeRollover { const uint32_t* n_in_ptr; uint32_t n_elements; half_t* dL_dout; };
+// the rest of the n_elements batch copies record i % n_in (coordinates in place through `coords`, the writable view of
+// the encode's coordinate input; dL_dout rescaled)
+struct EncodeRollover { const uint32_t* n_in_ptr; uint32_t n_elements; half_t* dL_dout; float* coords; };
 void launch_grid_encode(hipStream_t s, const uint32_t* n_ptr, uint32_t n_fixed, uint32_t ld, const float* coords, uint32_t coord_stride,
                         const GridLevels& gl, uint32_t valid_level, const half_t* grid, uint32_t* enc, float* dydx, uint32_t grid_x, const EncodeRollover* ro = nullptr);
 size_t scatter_records_capacity(uint32_t n_cap, uint32_t n_levels);

@@ -1292,7 +1292,7 @@ struct NeusTestbed {
 		launch_loss_grad(s, max_samples, st.p, dp, lp, coords.p, net_out.p, numsteps.p, w, coords_c.p, dL_dout.p);
 		// the rollover copies are made by the training encode (static scenes); the DeltaNetwork reads the whole batch first
 		if (use_delta) launch_rollover(s, batch, st.p, coords_c.p, dL_dout.p);
-		const EncodeRollover ro{&st.p->compacted_counter, batch, dL_dout.p};
+		const EncodeRollover ro{&st.p->compacted_counter, batch, dL_dout.p, coords_c.p};
 		// the canonical backward writes every gradient entry (weight tiles and variance by k_wgrad_reduce, every grid
 		// entry by k_scatter_accum, zeros with no samples); the global-movement phase skips it: zero the buffer there
 		if (!(!dyn || train_canonical)) HIP_CHECK(hipMemsetAsync(grads.p, 0, (size_t)lay.P * 4, s));

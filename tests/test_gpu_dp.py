@@ -196,6 +196,16 @@ def test_dp_overlapped_exchange_bitwise(scene):
         np.testing.assert_array_equal(a0.get_params().view(np.uint32), x.get_params().view(np.uint32))
         np.testing.assert_array_equal(a0.get_gradients().view(np.uint32), x.get_gradients().view(np.uint32))
         np.testing.assert_array_equal(a0.get_ema_params().view(np.uint32), x.get_ema_params().view(np.uint32))
+    # the exchange skips the grid range past the progressive valid level: it must be zero on every rank (the scatter's
+    # sc_zero_from invariant the reduced range relies on, testbed.cpp collective 1)
+    import oracle as O
+    lay = a0.layout()
+    off, _, _, _ = O.grid_tables(O.make_cfg(per_level_scale=a0._net_cfg.per_level_scale))
+    act = a0.stats()["valid_level"] + 1
+    assert act < lay["n_levels"]
+    for x in (a0, a1):
+        tail = x.get_gradients()[lay["grid_offset"] + 2 * int(off[act]): lay["variance_offset"]]
+        assert tail.size > 0 and not np.any(tail)
     ia, ib = a0.data_parallel_info(), b0.data_parallel_info()
     assert ia["allreduce_bytes"] == ib["allreduce_bytes"]
     assert ia["collective_calls"] > ib["collective_calls"]

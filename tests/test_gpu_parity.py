@@ -938,7 +938,7 @@ def test_multilane_march_equals_single_lane(env):
             out[lanes] = (host(rays, np.uint32).copy(), host(ns, np.uint32).copy(), host(co, np.uint32).copy(), tuple(cnt))
         a = out["1"]
         nk = int(a[3][1])
-        for lanes in ("4", "8"):
+        for lanes in ("4", "8", "16"):
             b = out[lanes]
             assert a[3] == b[3], (k, lanes, a[3], b[3])
             np.testing.assert_array_equal(a[0], b[0])
