@@ -178,7 +178,7 @@ __device__ __forceinline__ void visit(Visits& v, uint32_t kb, uint32_t ke) {
 template <bool FAST>
 __device__ __forceinline__ bool march_event(const DevDataset& ds, const uint8_t* __restrict__ bf, const uint32_t* __restrict__ lin,
                                             const MarchRay& mr, float& t, uint32_t& k, uint32_t k_end, SegAcc& acc, Visits& vis,
-                                            uint2* __restrict__ rec, uint32_t dbg = 0, uint32_t* fail = nullptr) {
+                                            uint2* __restrict__ rec, uint32_t dbg = 0) {
 	const uint32_t kb = k;
 	if (FAST) {
 		float pos[3];
@@ -228,7 +228,7 @@ __device__ __forceinline__ bool march_event(const DevDataset& ds, const uint8_t*
 		t += MIN_CONE_STEPSIZE; ++k;
 		// do { t += dt; ++k; } while (t < t_target); bounded: at cone angle 0 the box diagonal is NERF_STEPS steps, so
 		// no skip spans 4 NERF_STEPS and the bound only ends a corrupted t (the ray is ended, the step reports it)
-		if (!step_until(t, k, t_target, k + 4 * NERF_STEPS, MIN_CONE_STEPSIZE)) { step_fail(fail, STEP_FAIL_MARCH_T); return false; }
+		if (!step_until(t, k, t_target, k + 4 * NERF_STEPS, MIN_CONE_STEPSIZE)) return false;
 		return true;
 	} else {
 		float dt, pos[3];
@@ -263,11 +263,10 @@ constexpr uint32_t FINISHED = 0xffffffffu;
 template <bool FAST>
 __device__ __forceinline__ void march_segment(const DevDataset& ds, const uint8_t* __restrict__ bf, const uint32_t* __restrict__ lin,
                                               const MarchRay& mr, float& t, uint32_t& k, uint32_t k_end, SegAcc& acc, Visits& vis,
-                                              uint2* __restrict__ rec, uint32_t rec_cap, uint32_t* n_ev = nullptr, uint32_t dbg = 0,
-                                              uint32_t* fail = nullptr) {
+                                              uint2* __restrict__ rec, uint32_t rec_cap, uint32_t* n_ev = nullptr, uint32_t dbg = 0) {
 	while (k < k_end) {
 		if (n_ev) ++*n_ev;
-		if (acc.nrec + 1 >= rec_cap || !march_event<FAST>(ds, bf, lin, mr, t, k, k_end, acc, vis, rec, dbg, fail)) { k = FINISHED; break; }
+		if (acc.nrec + 1 >= rec_cap || !march_event<FAST>(ds, bf, lin, mr, t, k, k_end, acc, vis, rec, dbg)) { k = FINISHED; break; }
 	}
 	seg_flush(rec, acc, dbg);
 }
@@ -341,7 +340,7 @@ __global__ void __launch_bounds__(256) MARCH_OCC k_march(uint32_t cap_rays, uint
 		const bool active = t0 >= 0.f && (g == 0 || split);
 		if (active && g > 0) {
 			const float t_g = t0 + span * ((float)g / (float)MG);
-			if (FAST && !step_until(t, k, t_g, 4 * NERF_STEPS, MIN_CONE_STEPSIZE)) step_fail(&st->fail_flags, STEP_FAIL_MARCH_T);
+			if (FAST) step_until(t, k, t_g, 4 * NERF_STEPS, MIN_CONE_STEPSIZE);  // (a bad t ends the ray at its first event)
 			else while (t < t_g && k < 4 * NERF_STEPS) { t += calc_dt(t, ds.cone_angle); ++k; }
 		}
 		stamp(1);
@@ -354,7 +353,10 @@ __global__ void __launch_bounds__(256) MARCH_OCC k_march(uint32_t cap_rays, uint
 		float et = t;
 		uint32_t ek = active ? k : FINISHED;
 		uint32_t n_ev = 0;
-		if (active) { march_segment<FAST>(ds, bitfield, lin, mr, et, ek, k_end, acc, vis, rec, SEG_CAP, &n_ev, mw.dbg, &st->fail_flags); }
+		if (active) { march_segment<FAST>(ds, bitfield, lin, mr, et, ek, k_end, acc, vis, rec, SEG_CAP, &n_ev, mw.dbg); }
+		// health: an active lane whose walk ends on a negative or non-finite t was handed a corrupted state
+		if (__builtin_expect(__ballot(active && !((et >= 0.f) & (et < __builtin_huge_valf()))) != 0ull, 0) && lane == 0)
+			atomicOr(&st->fail_flags, STEP_FAIL_MARCH_T);
 		stamp(2);
 		// segment order: lane g joins the exit of lane g - 1
 		uint32_t vk = k;   // first valid step of this segment
@@ -378,7 +380,7 @@ __global__ void __launch_bounds__(256) MARCH_OCC k_march(uint32_t cap_rays, uint
 				if (redo) {
 					acc = SegAcc{0.f, 0u, 0u, 0u, 0u}; vis.n = 0;
 					et = pt; ek = pk; vk = pk;
-					march_segment<FAST>(ds, bitfield, lin, mr, et, ek, k_end, acc, vis, rec, SEG_CAP, nullptr, 0, &st->fail_flags);
+					march_segment<FAST>(ds, bitfield, lin, mr, et, ek, k_end, acc, vis, rec, SEG_CAP);
 				}
 			}
 		}
@@ -627,7 +629,7 @@ __global__ void __launch_bounds__(256) k_march_write(uint32_t cap_rays, StepStat
 			float t = __uint_as_float(s_t0[q - q0]);
 			if (ds.cone_angle == 0.0f) {  // the run's u constant steps in a few integer-domain jumps (exact, step_until)
 				uint32_t kk = 0;
-				if (!step_until(t, kk, __int_as_float(0x7f800000), s_u[q - q0], MIN_CONE_STEPSIZE)) step_fail(&st->fail_flags, STEP_FAIL_MARCH_T);
+				if (!step_until(t, kk, __int_as_float(0x7f800000), s_u[q - q0], MIN_CONE_STEPSIZE)) atomicOr(&st->fail_flags, STEP_FAIL_MARCH_T);
 			} else
 			for (uint32_t u = s_u[q - q0]; u > 0; --u) t += ds.cone_angle == 0.0f ? MIN_CONE_STEPSIZE : calc_dt(t, ds.cone_angle);
 			const float o[3] = {s_ray[0][r], s_ray[1][r], s_ray[2][r]}, dir[3] = {s_ray[3][r], s_ray[4][r], s_ray[5][r]};

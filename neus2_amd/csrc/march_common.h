@@ -49,13 +49,11 @@ __device__ __forceinline__ int mip_from_dt(float dt, float px, float py, float p
 // same increment prove the stretch linear; it is then jumped in the integer domain (positive floats order as their
 // bit patterns) up to the first step at or past target, the step cap or the binade's end, whichever comes first.
 // Single exact steps cross binades and settle the parity.
-// Precondition checked: with t negative or not finite (or dt <= 0) the jumps' integer arithmetic is meaningless, so the
-// plain loop runs instead (bounded by kmax) and false is returned; the caller ends the ray and raises STEP_FAIL_MARCH_T.
+// Precondition checked: with t negative or not finite the jumps' integer arithmetic is meaningless (and the plain loop
+// could spin without end), so nothing is stepped and false is returned: the caller ends the ray, and the march's exit
+// check (a non-finite / negative t at a segment's end) raises STEP_FAIL_MARCH_T. dt: the constant step (> 0).
 __device__ __forceinline__ bool step_until(float& t, uint32_t& k, float target, uint32_t kmax, float dt) {
-	if (!(t >= 0.0f) || !(t < __builtin_huge_valf()) || !(dt > 0.0f)) {
-		while (t < target && k < kmax) { t += dt; ++k; }
-		return false;
-	}
+	if (!(t >= 0.0f) || !(t < __builtin_huge_valf())) return false;
 	while (t < target && k < kmax) {
 		const float t2 = t + dt;
 		const uint32_t b = __float_as_uint(t), b2 = __float_as_uint(t2), ex = b & 0x7f800000u;
@@ -71,10 +69,6 @@ __device__ __forceinline__ bool step_until(float& t, uint32_t& k, float target, 
 		k += j;
 	}
 	return true;
-}
-// raises a device health bit (vector atomic on the step state; rare path)
-__device__ __forceinline__ void step_fail(uint32_t* flags, uint32_t bit) {
-	if (flags) atomicOr(flags, bit);
 }
 __device__ __forceinline__ float signf(float x) { return copysignf(1.0f, x); }
 __device__ __forceinline__ float advance_to_next_voxel(float t, float cone, const float pos[3], const float dir[3], const float idir[3], uint32_t res) {

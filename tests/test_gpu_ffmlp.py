@@ -57,14 +57,32 @@ def _mats(c, p):
     return out
 
 
+def _r16_fn(torch):
+    class R16(torch.autograd.Function):
+        """fp16 storage of a value and of the gradient flowing back through it (the kernels store activations and
+        deltas in fp16); differentiable, so double backward works."""
+
+        @staticmethod
+        def forward(ctx, v):
+            return v.to(torch.float16).to(torch.float64)
+
+        @staticmethod
+        def backward(ctx, g):
+            return R16.apply(g)
+    return R16.apply
+
+
 def _ref_forward(c, mats, x, torch):
-    """float64 restatement on the fp16 parameters and fp16-rounded input (no intermediate rounding)."""
+    """float64 restatement on the fp16 parameters and fp16-rounded input; every layer's sum and output, and the deltas
+    flowing back through them, are rounded to fp16 as the kernels store them."""
     _, in_pad, _ = _shapes(c)
     n = x.shape[0]
+    r16 = _r16_fn(torch)
+
     h = torch.cat([x, torch.ones(n, in_pad - c["n_in"], dtype=torch.float64)], 1)
     for l, Wm in enumerate(mats):
-        z = h @ Wm.T
-        h = _act(c["out_act"] if l == len(mats) - 1 else c["act"], z, torch)
+        z = r16(h @ Wm.T)
+        h = r16(_act(c["out_act"] if l == len(mats) - 1 else c["act"], z, torch))
     return h
 
 

@@ -268,26 +268,28 @@ def test_teacher_forced_steps_vs_oracle(scene, torch_cuda):
         assert cos >= 0.9999 and rel <= 2e-3, (name, cos, rel)
 
 
-def test_teacher_forced_all_levels_vs_oracle(scene, torch_cuda):
-    """Teacher-forced training at the bench's state: the device trains 700 free-running steps first, so
-    all 14 levels are active (hashed levels 5-13: 2^19-entry tables, the 2048-entry region scatter of hashed buckets),
-    the occupancy grid is shaped by hundreds of updates and progressive inference is on by its auto rule (checked: the
-    steps ran the chunk rounds and later rounds had work). Then 14 consecutive steps, each compared with the oracle's
-    step from the device's state before it (as test_teacher_forced_steps_vs_oracle). One step runs with half the rays,
-    so its compacted count is below the batch and the rollover fused into k_grid_encode fills the rest
+def _teacher_forced_all_levels(sc, tag, progressive, n_steps=14, prepare=700, short_step=5):
+    """Teacher-forced training at the all-levels state: the device trains `prepare` free-running steps
+    first, so all 14 levels are active (hashed levels 5-13: 2^19-entry tables, the 2048-entry region scatter of hashed
+    buckets) and the occupancy grid is shaped by hundreds of updates. Then n_steps consecutive steps, each compared with
+    the oracle's step from the device's state before it (as test_teacher_forced_steps_vs_oracle). One step runs with half
+    the rays, so its compacted count is below the batch and the rollover fused into k_grid_encode fills the rest
     (fill_rollover_and_rescale, common_device.h:515-535). Per step: the march bit-exact, the compacted count equal up to
     fp16-moved cut-offs, every gradient block cos >= 0.9999 and rel-L2 <= 2e-3; per hash level the worst rel-L2 is
-    recorded (profiles/, parity metrics). Reference: testbed_nerf.cu:3723-4001, grid.h:371-500, 880-1007, 2427-2440."""
+    recorded. progressive: None leaves the auto rule on (asserted to have run the rounds), 2 forces the rounds.
+    Reference: testbed_nerf.cu:3723-4001, grid.h:371-500, 880-1007, 2427-2440."""
     import ctypes as C
     import oracle as O
     from cpu_step import CpuTrainer
     from neus2_amd._lib import NeusRestoreState, check, lib
-    tb = _testbed(scene)
-    tb.train_steps(700)
+    tb = _testbed(sc)
+    if progressive is not None:
+        tb.set_progressive_inference(progressive, (32, 64, 96))
+    tb.train_steps(prepare)
     lay = tb.layout()
     cfg = O.make_cfg(per_level_scale=tb._net_cfg.per_level_scale)
     assert tb.stats()["valid_level"] + 1 >= cfg.n_levels, "not every level is active"
-    ds = O.Dataset(scene["images"], scene["focal"], scene["principal"], scene["xforms"])
+    ds = O.Dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"])
     tr = CpuTrainer(cfg, ds, tb.get_params(), batch=BATCH, rays_per_batch=BATCH)
     blocks = {"density": (0, lay["n_density"]), "rgb": (lay["n_density"], lay["n_matrix"]),
               "grid": (lay["grid_offset"], lay["variance_offset"]), "variance": (lay["variance_offset"], lay["variance_offset"] + 1)}
@@ -296,7 +298,7 @@ def test_teacher_forced_all_levels_vs_oracle(scene, torch_cuda):
     worst = {k: [1.0, 0.0] for k in blocks}
     lev_rel = np.zeros(cfg.n_levels)
     prog0 = tb.stats()["progressive_steps"]
-    n_steps, short_step, short_seen, n_comp_equal, later_rounds = 14, 5, False, 0, 0
+    short_seen, n_comp_equal, later_rounds, evaluated, kept = False, 0, 0, 0, 0
     for k in range(n_steps):
         st = tb.stats()
         if k == short_step:  # half the rays for this step: the compaction falls short of the batch
@@ -321,9 +323,11 @@ def test_teacher_forced_all_levels_vs_oracle(scene, torch_cuda):
         st1 = tb.stats()
         _, cc, _ = tb.ray_counts(1 << 18)
         later_rounds += int((cc > 32).sum())
+        evaluated += st1["evaluated_samples_last"]
         tr.density_grid[:] = grid
         tr.bitfield[:] = bf
         gr = tr.grads(skip_occupancy=True).astype(np.float64)
+        kept += tr.last["n_kept"]
         assert st1["measured_batch_size_before_compaction"] == tr.last["numsteps_counter"], k
         comp_d, comp_o = st1["measured_batch_size"], tr.last["compacted"]
         n_comp_equal += comp_d == comp_o
@@ -341,15 +345,31 @@ def test_teacher_forced_all_levels_vs_oracle(scene, torch_cuda):
             if np.linalg.norm(y) > 0:
                 lev_rel[l] = max(lev_rel[l], np.linalg.norm(g[a:b] - y) / np.linalg.norm(y))
     prog = tb.stats()["progressive_steps"] - prog0
-    _record("teacher_forced_all_levels", steps=n_steps, start_step=700, compacted_equal_steps=n_comp_equal, progressive_steps=prog,
-            later_round_rays=later_rounds, short_step_compacted_below_batch=short_seen,
+    _record(f"teacher_forced_all_levels_{tag}", steps=n_steps, start_step=prepare, compacted_equal_steps=n_comp_equal, progressive_steps=prog,
+            evaluated_over_kept=evaluated / max(kept, 1), later_round_rays=later_rounds, short_step_compacted_below_batch=short_seen,
             **{f"min_cos_{k}": v[0] for k, v in worst.items()}, **{f"max_rel_{k}": v[1] for k, v in worst.items()},
             **{f"max_rel_grid_L{l}": lev_rel[l] for l in range(cfg.n_levels)})
     assert prog >= n_steps - 1, f"progressive inference ran on {prog} of {n_steps} steps"
+    assert evaluated < kept, "the rounds evaluated every kept sample: the cut-off never skipped work"
     assert later_rounds > 0, "no ray composited past the first chunk: the later rounds had no work"
     assert short_seen, "no step compacted fewer samples than the batch: the rollover did not run"
     for name, (cos, rel) in worst.items():
         assert cos >= 0.9999 and rel <= 2e-3, (name, cos, rel)
+
+
+def test_teacher_forced_all_levels_vs_oracle(scene, torch_cuda):
+    """_teacher_forced_all_levels on the 8-view 64x48 scene with the progressive rounds forced on: the auto rule keeps
+    this small scene one-pass (over 70 % of its kept samples are composited at step 700), so the rounds are forced with
+    the same kernels the auto rule runs."""
+    _teacher_forced_all_levels(scene, "small_forced", progressive=2)
+
+
+def test_teacher_forced_all_levels_config_s_auto(torch_cuda):
+    """_teacher_forced_all_levels on the bench's scene (Config S: 49 views of 1600x1200, DTU-scan24 intrinsics) at a
+    4096-sample batch, progressive inference left on its auto rule, which turns the rounds on there."""
+    from neus2_amd import scenes
+    sc = scenes.sphere_scene(49, 1600, 1200, principal=(823.2 / 1600, 619.1 / 1200))
+    _teacher_forced_all_levels(sc, "config_s_auto", progressive=None)
 
 
 def test_training_is_bitwise_reproducible(scene, torch_cuda):
