@@ -41,10 +41,12 @@ def main():
         db = json.load(open(a.out))
     except (OSError, ValueError):
         db = {}
-    names = dict(NAMES)
-    for kv in a.name:
+    names = {}
+    for kv in a.name:  # overrides first: the first key contained in a kernel's name wins
         k, v = kv.split("=", 1)
         names[k] = v
+    for k, v in NAMES.items():
+        names.setdefault(k, v)
     for k, c in parse(a.table, names).items():
         if "TCC_EA0_RDREQ_sum" not in c or "WRITE_SIZE" not in c:
             continue
