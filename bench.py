@@ -82,7 +82,7 @@ def parse():
     p.add_argument("--batch", type=int, default=1 << 18)
     p.add_argument("--rays", type=int, default=1 << 18)
     p.add_argument("--cpu-baseline", type=int, default=1)
-    p.add_argument("--cpu-steps", type=int, default=6)
+    p.add_argument("--cpu-steps", type=int, default=20)
     p.add_argument("--cpu-config1-steps", type=int, default=100)
     # quality half of the metric: PSNR after this many steps of the reference's (adaptive-R) training
     p.add_argument("--psnr-steps", type=int, default=20000)

@@ -83,10 +83,9 @@ __global__ void __launch_bounds__(256) k_adam_ema(AdamParams p, float* __restric
 	for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < ng; g += gridDim.x * blockDim.x) {
 		const uint32_t i0 = 4 * g;
 		const float4 G = ((const float4*)grads)[g];
-		float4 W = ((const float4*)weights_fp)[g];
 		const uint2 WHr = ((const uint2*)weights_h)[g];
 		float4 E = ((const float4*)ema_tmp)[g];
-		float gr[4] = {G.x, G.y, G.z, G.w}, w[4] = {W.x, W.y, W.z, W.w}, e[4] = {E.x, E.y, E.z, E.w};
+		float gr[4] = {G.x, G.y, G.z, G.w}, e[4] = {E.x, E.y, E.z, E.w};
 		half_t wh[4];
 		*(uint2*)wh = WHr;
 		// any parameter of the group steps? (the same skip test as adam_param)
@@ -96,7 +95,9 @@ __global__ void __launch_bounds__(256) k_adam_ema(AdamParams p, float* __restric
 			const float gk = p.pow2_scale ? gr[k] * p.inv_loss_scale : gr[k] / p.loss_scale;
 			any |= (i0 + k < p.n_matrix) ? p.optimize_matrix != 0u : (p.optimize_non_matrix != 0u && gk != 0.f);
 		}
-		if (any) {
+		if (any) {  // (a skipped group reads neither its optimizer state nor its fp32 master weights: the EMA reads the fp16 copy)
+			const float4 W = ((const float4*)weights_fp)[g];
+			float w[4] = {W.x, W.y, W.z, W.w};
 			float4 M1 = ((const float4*)m1)[g], M2 = ((const float4*)m2)[g];
 			uint4 S = ((const uint4*)steps)[g];
 			float a[4] = {M1.x, M1.y, M1.z, M1.w}, b[4] = {M2.x, M2.y, M2.z, M2.w};
