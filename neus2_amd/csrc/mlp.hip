@@ -919,30 +919,21 @@ __global__ void __launch_bounds__(256) k_nerf_density(uint32_t n, const float* _
 // ------------------------------------------------------------------------------------------
 // Training path: encodings and dy/dx come from k_grid_encode (logical din order).
 // ------------------------------------------------------------------------------------------
-// Forward state kept in registers for one 32-sample chunk.
-template <int L, int W> struct Fwd {
-	static constexpr int MT = (W + 31) / 32;   // hidden tiles
-	static constexpr int HKS = W / 16;          // hidden k-steps
-	h8 dinB[Dims<L>::DKS];
-	f16v H0[MT];          // density hidden (post-ReLU, fp16-rounded)
-	f16v D1;              // density output (fp16-rounded), rows 0..15 in regs 0..7
-	h8 GhB[HKS];          // relu'(H0) . W1d[0]  (also b2 of the double backward)
-	f16v Gi[Dims<L>::DMT];// dSDF/d(density input) (fp16-rounded)
-	float grad[3];        // dSDF/dx
-	h8 rinB[3];           // rgb input fragments
-	f16v H1[MT], H2[MT];  // rgb hidden (post-ReLU, fp16)
-	f16v O;               // rgb output (fp16-rounded)
-};
-
 // Reads this lane's encoding features and builds the density-input B fragments (logical order).
 template <int L>
-__device__ __forceinline__ void build_din(h8* dinB, const float x[3], const half_t* __restrict__ enc_h /*[L][ld] half2*/, uint32_t ld, uint32_t i, int h) {
+__device__ __forceinline__ void load_enc(uint32_t ev[L], const half_t* __restrict__ enc_h /*[L][ld] half2*/, uint32_t ld, uint32_t i) {
+#pragma unroll
+	for (int l = 0; l < L; ++l) ev[l] = ((const uint32_t*)enc_h)[(size_t)l * ld + i];
+}
+// (split from the loads, so a kernel can issue its other loads of the chunk in between)
+template <int L>
+__device__ __forceinline__ void build_din(h8* dinB, const float x[3], const uint32_t ev[L], int h) {
 	constexpr int DIN = Dims<L>::DIN;
 	float dv[DIN];
 #pragma unroll
 	for (int k = 0; k < DIN; ++k) {
 		if (k < 3) dv[k] = rh(rh(x[k]) - 0.5f);
-		else if (k < 3 + 2 * L) dv[k] = (float)enc_h[((size_t)((k - 3) >> 1) * ld + i) * 2 + ((k - 3) & 1)];  // [L][ld] half2
+		else if (k < 3 + 2 * L) dv[k] = (float)__builtin_bit_cast(h2, ev[(k - 3) >> 1])[(k - 3) & 1];
 		else dv[k] = 0.f;
 	}
 #pragma unroll
@@ -951,36 +942,15 @@ __device__ __forceinline__ void build_din(h8* dinB, const float x[3], const half
 		for (int j = 0; j < 8; ++j) dinB[ks][j] = (half_t)hsel(h, dv[16 * ks + pi_row(j, 1)], dv[16 * ks + pi_row(j, 0)]);
 }
 
-// Full NerfNetwork forward for this lane's sample from stored encodings (r = lane & 31, h = lane >> 5).
-// Every lane of the wave must call this (MFMA), valid or not.
-template <int L, int W>
-__device__ __forceinline__ void forward_chunk(Fwd<L, W>& F, const FwdW& w, const float x[3], const float wd[3],
-                                              const half_t* __restrict__ enc_h, const float* __restrict__ dydx, uint32_t ld,
-                                              uint32_t i, bool valid, int r, int h) {
-	constexpr int DMT = Dims<L>::DMT;
-	build_din<L>(F.dinB, x, enc_h, ld, valid ? i : 0, h);
-	density_forward<L, W>(w, F.dinB, r, h, F.H0, F.D1, F.GhB, F.Gi);
-	// dSDF/dx = sum_k G_in[k] dy/dx[k] (+ identity rows 0..2), split over the two lane halves
-	float part[3] = {0.f, 0.f, 0.f};
-	const uint32_t ii = valid ? i : 0;
-#pragma unroll
-	for (int mt = 0; mt < DMT; ++mt)
-#pragma unroll
-		for (int reg = 0; reg < 16; ++reg) {
-			const int k = 32 * mt + acc_row(reg, h);
-			const float gv = F.Gi[mt][reg];
-			if (k < 3) {
-				part[0] += (k == 0) ? gv : 0.f; part[1] += (k == 1) ? gv : 0.f; part[2] += (k == 2) ? gv : 0.f;
-			} else if (k < 3 + 2 * L) {
-				const float* dp = dydx + (size_t)(3 * (k - 3)) * ld + ii;
-				part[0] += gv * dp[0];
-				part[1] += gv * dp[ld];
-				part[2] += gv * dp[2 * (size_t)ld];
-			}
-		}
-#pragma unroll
-	for (int d = 0; d < 3; ++d) F.grad[d] = part[d] + __shfl_xor(part[d], 32);
-	F.O = rgb_forward<W>(w, F.D1, x, wd, F.grad, r, h, F.rinB, F.H1, F.H2);
+// dy/dx of density-input slot k (k = 3 + 2 l + f: feature f of level l) for sample i, [6L][ld] f32 rows 3 (k - 3) + d.
+// Slots outside the features read a clamped row; the caller masks them. The loads are unconditional on purpose: the
+// slot depends on the lane half, and a lane-dependent branch around each load group made the compiler wait for
+// every group before issuing the next (14 serial memory round trips per 32-sample chunk in the colour kernel).
+template <int L>
+__device__ __forceinline__ void load_dydx(const float* __restrict__ dydx, uint32_t ld, uint32_t i, int k, float dy[3]) {
+	const int q = min(max(k - 3, 0), 2 * L - 1);
+	const float* dp = dydx + (size_t)(3 * q) * ld + i;
+	dy[0] = dp[0]; dy[1] = dp[ld]; dy[2] = dp[2 * (size_t)ld];
 }
 
 // backward weight set: transposed copies, staged after the forward set
@@ -1089,11 +1059,25 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 		const float* c = coords + (size_t)ic * COORD_W;
 		const float x[3] = {c[0], c[1], c[2]}, wd[3] = {c[4], c[5], c[6]};
 		// ---- forward recompute up to the colour hidden layers
+		uint32_t ev[L];
+		load_enc<L>(ev, enc_h, ld, ic);
+		// all of the chunk's dy/dx loads (and dL/dout) are issued right after the encoding's, before the density forward:
+		// one memory round trip per chunk, the dy/dx part overlapped with the forward's MFMAs (loads complete in order,
+		// so the forward waits for the encoding only; the sched_barrier keeps them up front)
+		float dyv[DMT * 16][3];
+#pragma unroll
+		for (int mt = 0; mt < DMT; ++mt)
+#pragma unroll
+			for (int reg = 0; reg < 16; ++reg) load_dydx<L>(dydx, ld, ic, 32 * mt + acc_row(reg, h), dyv[16 * mt + reg]);
+		const h8 dlo_ld = *(const h8*)(dL_dout + (size_t)ic * OUT_W + 8 * h);  // h=0: rows 0..7, h=1: rows 8..15
+		__builtin_amdgcn_sched_barrier(0);
 		h8 dinB[DKS];
-		build_din<L>(dinB, x, enc_h, ld, ic, h);
+		build_din<L>(dinB, x, ev, h);
 		h8 H0B[HKS], D1B, GhB[HKS];
 		f16v Gi[DMT];
 		density_forward_frag<L, W>(fw, dinB, r, h, H0B, D1B, GhB, Gi);
+		// (feature slots: part += G dy/dx as one fma each; xyz slots: the fma adds 0 * dy, then the identity term -
+		// the values of the former branchy form, bit for bit)
 		float part[3] = {0.f, 0.f, 0.f};
 #pragma unroll
 		for (int mt = 0; mt < DMT; ++mt)
@@ -1101,14 +1085,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 			for (int reg = 0; reg < 16; ++reg) {
 				const int k = 32 * mt + acc_row(reg, h);
 				const float gv = Gi[mt][reg];
-				if (k < 3) {
-					part[0] += (k == 0) ? gv : 0.f; part[1] += (k == 1) ? gv : 0.f; part[2] += (k == 2) ? gv : 0.f;
-				} else if (k < 3 + 2 * L) {
-					const float* dp = dydx + (size_t)(3 * (k - 3)) * ld + ic;
-					part[0] += gv * dp[0];
-					part[1] += gv * dp[ld];
-					part[2] += gv * dp[2 * (size_t)ld];
-				}
+				const float gf = (k >= 3 && k < 3 + 2 * L) ? gv : 0.f;
+#pragma unroll
+				for (int d = 0; d < 3; ++d) part[d] = fmaf(gf, dyv[16 * mt + reg][d], part[d]) + ((k == d) ? gv : 0.f);
 			}
 		float grad[3];
 #pragma unroll
@@ -1117,7 +1096,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 		h8 H1B[HKS], H2B[HKS];
 		rgb_hidden_frag<W>(fw, D1B, x, wd, grad, r, h, rinB, H1B, H2B);
 		// ---- colour backward (a lane without a sample gets dL/dout = 0: every delta, hence its dW share, is 0)
-		const h8 dlo = valid ? *(const h8*)(dL_dout + (size_t)ic * OUT_W + 8 * h) : z8;  // h=0: rows 0..7, h=1: rows 8..15
+		const h8 dlo = valid ? dlo_ld : z8;
 		const h8 dlo_o = shfl_xor_h8(dlo, 32);
 		const h8 dlo_lo = h ? dlo_o : dlo;   // rows 0..7 on every lane
 		const h8 dlo_hi = h ? dlo : dlo_o;   // rows 8..15 on every lane
@@ -1256,8 +1235,24 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 		const uint32_t ic = valid ? i : 0;
 		const float* c = coords + (size_t)ic * COORD_W;
 		const float x[3] = {c[0], c[1], c[2]};
+		// the chunk's loads up front (as the colour kernel): encoding, then dy/dx of this lane's density-input slots (the
+		// accumulator rows k = 32 mt + acc_row(reg, h); fragment j of k-step ks is register 8 (ks & 1) + j of tile ks >> 1),
+		// delta_D1 and v
+		uint32_t ev[L];
+		load_enc<L>(ev, enc_h, ld, ic);
+		__builtin_amdgcn_sched_barrier(0);  // (the encoding's loads first: in-order completion lets the forward wait for them alone)
+		float dyv[DMT * 16][3];
+#pragma unroll
+		for (int mt = 0; mt < DMT; ++mt)
+#pragma unroll
+			for (int reg = 0; reg < 16; ++reg) load_dydx<L>(dydx, ld, ic, 32 * mt + acc_row(reg, h), dyv[16 * mt + reg]);
+		half_t d1v[8];
+#pragma unroll
+		for (int j = 0; j < 8; ++j) d1v[j] = tb.d1_delta[(size_t)(h ? pi_row(j, 1) : pi_row(j, 0)) * ld + ic];
+		const float4 v4 = tb.v[ic];
+		__builtin_amdgcn_sched_barrier(0);
 		h8 dinB[DKS];
-		build_din<L>(dinB, x, enc_h, ld, ic, h);
+		build_din<L>(dinB, x, ev, h);
 		h8 H0B[HKS], D1B, GhB[HKS];
 		f16v Gi[DMT];
 		density_forward_frag<L, W>(fw, dinB, r, h, H0B, D1B, GhB, Gi);
@@ -1273,7 +1268,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 		// delta_D1 from the colour kernel (d1_delta column i), B fragment in pi order (0 without a sample)
 		h8 dD1B;
 #pragma unroll
-		for (int j = 0; j < 8; ++j) dD1B[j] = valid ? tb.d1_delta[(size_t)(h ? pi_row(j, 1) : pi_row(j, 0)) * ld + ic] : (half_t)0.f;
+		for (int j = 0; j < 8; ++j) dD1B[j] = valid ? d1v[j] : (half_t)0.f;
 		{  // dW_d1 (first order) += dD1 . H0^T
 			h8 TD[2];
 			transpose32(dD1B, z8, false, sel0, sel1, TD);
@@ -1322,19 +1317,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 				for (int reg = 0; reg < 16; ++reg) {
 					const int k = 32 * mt + acc_row(reg, h);
 					const float gv = dDin[mt][reg];
-					if (k < 3) {
-						pd[0] += (k == 0) ? gv : 0.f; pd[1] += (k == 1) ? gv : 0.f; pd[2] += (k == 2) ? gv : 0.f;
-					} else if (k < 3 + 2 * L) {
-						const float* dp = dydx + (size_t)(3 * (k - 3)) * ld + ic;
-						pg[0] += gv * dp[0];
-						pg[1] += gv * dp[ld];
-						pg[2] += gv * dp[2 * (size_t)ld];
+					const float gf = (k >= 3 && k < 3 + 2 * L) ? gv : 0.f;
+#pragma unroll
+					for (int d = 0; d < 3; ++d) {
+						pd[d] += (k == d) ? gv : 0.f;
+						pg[d] = fmaf(gf, dyv[16 * mt + reg][d], pg[d]);
 					}
 				}
 #pragma unroll
 			for (int d = 0; d < 3; ++d) { pg[d] += __shfl_xor(pg[d], 32); pd[d] += __shfl_xor(pd[d], 32); }
 		}
-		const float4 v4 = tb.v[ic];
 		const float v[3] = {v4.x, v4.y, v4.z};
 		// u = [v, dy/dx . v, 0] (grid.h:1182-1207), B fragments in pi order
 		h8 uB[DKS];
@@ -1343,13 +1335,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 #pragma unroll
 			for (int j = 0; j < 8; ++j) {
 				const int k = 16 * ks + (h ? pi_row(j, 1) : pi_row(j, 0));
-				float val = 0.f;
-				if (k < 3) val = v[k];
-				else if (k < 3 + 2 * L) {
-					const float* dp = dydx + (size_t)(3 * (k - 3)) * ld + ic;
-					val = dp[0] * v[0] + dp[ld] * v[1] + dp[2 * (size_t)ld] * v[2];
-				}
-				uB[ks][j] = (half_t)val;
+				const float* dy = dyv[16 * (ks >> 1) + 8 * (ks & 1) + j];
+				const float du = dy[0] * v[0] + dy[1] * v[1] + dy[2] * v[2];
+				const float vk = k == 0 ? v[0] : (k == 1 ? v[1] : v[2]);
+				uB[ks][j] = (half_t)(k < 3 ? vk : (k < 3 + 2 * L ? du : 0.f));
 			}
 		// h1' = relu'(H0) . (W0d u)
 		h8 H1pB[HKS];

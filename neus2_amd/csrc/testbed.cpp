@@ -7,6 +7,7 @@
 //   * deterministic count -> scan -> write compaction instead of atomic appends;
 //   * fp32 gradients and master weights, fp16 weights for the kernels (the reference keeps fp16
 //     gradients), RCCL all-reduce of the gradient buffer for data parallelism over ray batches.
+#include <rocprofiler-sdk-roctx/roctx.h>
 #include "kernels.h"
 #include "scan_lookback.h"
 #include "json_lite.h"
@@ -1025,7 +1026,17 @@ struct NeusTestbed {
 		return t;
 	}
 
-	void mark(int i) { if (profiling) HIP_CHECK(hipEventRecord(ev[prof_par][i], stream)); }
+	// each phase mark also closes the previous roctx range and opens the phase's (host enqueue spans of the step's kernel
+	// groups in `rocprofv3 --marker-trace`; the calls are no-ops without a tool attached)
+	int rx_open = -1;
+	void mark(int i) {
+		static const char* const names[N_PHASES] = {"neus:occupancy", "neus:march", "neus:inference", "neus:loss", "neus:encode",
+		                                            "neus:mlp", "neus:wgrad", "neus:scatter", "neus:exchange", "neus:optimizer"};
+		if (profiling) HIP_CHECK(hipEventRecord(ev[prof_par][i], stream));
+		if (rx_open >= 0) roctxRangePop();
+		rx_open = i < N_PHASES ? i : -1;
+		if (rx_open >= 0) roctxRangePushA(names[i]);
+	}
 	// Inference timing (neus_testbed_set_infer_timing): hipEvents around every pre-compaction network launch of the step
 	// (the one pass, or each progressive round's k_nerf_infer), summed per step after the step (host waits: timing passes
 	// only, never the bench's timed region)
