@@ -330,7 +330,14 @@ def _teacher_forced_all_levels(sc, tag, progressive, n_steps=14, prepare=700, sh
         tr.bitfield[:] = bf
         gr = tr.grads(skip_occupancy=True).astype(np.float64)
         kept += tr.last["n_kept"]
-        assert st1["measured_batch_size_before_compaction"] == tr.last["numsteps_counter"], k
+        # the requested-sample counter: equal below the cap; past it the device's prefix-limited march (k_march's
+        # second pass skipped once the first pass's rays request max_samples) reads some value >= the cap, which is
+        # all the reference uses of it (min(counter, max_samples), testbed_nerf.cu:3036-3039)
+        req_d, req_o = st1["measured_batch_size_before_compaction"], tr.last["numsteps_counter"]
+        if req_o >= tr.max_samples:
+            assert req_d >= tr.max_samples, (k, req_d, req_o)
+        else:
+            assert req_d == req_o, (k, req_d, req_o)
         comp_d, comp_o = st1["measured_batch_size"], tr.last["compacted"]
         n_comp_equal += comp_d == comp_o
         assert abs(comp_d - comp_o) <= max(2, 1e-3 * comp_o), (k, comp_d, comp_o)
