@@ -32,9 +32,6 @@ constexpr float NERF_MIN_OPTICAL_THICKNESS = 0.1f;
 constexpr uint32_t GRID3 = NERF_GRIDSIZE * NERF_GRIDSIZE * NERF_GRIDSIZE;
 // Linear mip-0 occupancy for the constant-step march: GRID3 / 32 words in (x, y, z/32) order.
 constexpr uint32_t LIN_WORDS = GRID3 / 32;
-// ... followed by a 16^3 coarse occupancy (one byte per cell of 8^3 mip-0 cells: any bit set) for the march order
-constexpr uint32_t COARSE_RES = 16, COARSE3 = COARSE_RES * COARSE_RES * COARSE_RES;
-constexpr uint32_t LIN_ALLOC_WORDS = LIN_WORDS + COARSE3 / 4;
 constexpr uint32_t MAX_LEVELS = 16;
 constexpr uint32_t OUT_W = 16;      // padded network output width (nerf_network.h:935)
 constexpr uint32_t COORD_W = 7;     // NerfCoordinate floats (nerf.h:76-102)

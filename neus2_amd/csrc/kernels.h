@@ -265,7 +265,7 @@ void launch_ff_wgrad(hipStream_t s, const FfWgrad& G);
 void launch_ff_input(hipStream_t s, uint32_t n, uint32_t n_in, uint32_t ld, const float* in, float scale, float offset, half_t* x, bool grad);
 void launch_ff_out_delta(hipStream_t s, uint32_t n, uint32_t ld, uint32_t act, const half_t* dL, const half_t* out, half_t* d);
 // march.hip
-void launch_bitfield_linear(hipStream_t s, const uint8_t* bitfield, uint32_t* lin /* LIN_ALLOC_WORDS: words + coarse bytes */);
+void launch_bitfield_linear(hipStream_t s, const uint8_t* bitfield, uint32_t* lin /* LIN_WORDS */);
 // world-space box of every occupied cell of every mip -> scratch[0..6) = {min xyz, max xyz} (optim.hip); the ray
 // generation culls rays that miss it. scratch: occ_bbox_scratch_floats() floats.
 size_t occ_bbox_scratch_floats();
@@ -278,13 +278,11 @@ void launch_occ_bbox(hipStream_t s, const uint8_t* bitfield, float* scratch);
 constexpr uint32_t MARCH_RUN_MAX = 16;
 constexpr uint32_t MARCH_SEG_RECS = NERF_STEPS + 64;
 struct MarchWork {
-	uint2* rec; uint32_t* nrec; uint32_t* counter /* 4: the march order's slot counters (zeroed by the ray generation) */; uint32_t waves; /* 0 = one lane per ray */
+	uint2* rec; uint32_t* nrec; uint32_t* counter /* 2: the two passes' ray queues */; uint32_t waves; /* 0 = one lane per ray */
 	uint2* seg; uint32_t lanes_per_ray;  /* 1, 4, 8 or 16 */
 	PcgJumpTable jt;                      /* jump-ahead of the ray generator's per-ray rng offsets */
 	unsigned long long* prof = nullptr;   /* development: per-wave phase timestamps of the march (8 per wave), or null */
 	uint32_t dbg = 0;                     /* development timing experiments (wrong results): 1 no record stores, 2 no occupancy loads */
-	uint32_t* order = nullptr;            /* march order (k_ray_order): per pass range, the slots whose ray crosses occupied coarse
-	                                         cells first; null: slot order (FAST march only) */
 };
 // Ray generation + the occupancy march: rays (6 f32 per slot), tstart (1 per slot), nreq (requested
 // samples per slot) and the sample runs (MarchWork).

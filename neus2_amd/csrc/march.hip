@@ -36,17 +36,6 @@ __global__ void k_bitfield_linear(const uint8_t* __restrict__ bf, uint32_t* __re
 	}
 	lin[w] = word;
 }
-// Coarse occupancy after the linear words (lin + LIN_WORDS, bytes): cell (X, Y, Z) of 16^3 covers mip-0 cells
-// [8X, 8X + 8) x [8Y, 8Y + 8) x [8Z, 8Z + 8), i.e. bits 8 (Z & 3) .. + 7 of the words (x, y, Z >> 2)
-__global__ void k_bitfield_coarse(const uint32_t* __restrict__ lin, uint8_t* __restrict__ coarse) {
-	const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-	if (c >= COARSE3) return;
-	const uint32_t X = c >> 8, Y = (c >> 4) & 15, Z = c & 15, sh = 8 * (Z & 3);
-	uint32_t any = 0;
-	for (uint32_t x = 8 * X; x < 8 * X + 8; ++x)
-		for (uint32_t y = 8 * Y; y < 8 * Y + 8; ++y) any |= (lin[(x << 9) | (y << 2) | (Z >> 2)] >> sh) & 0xffu;
-	coarse[c] = any ? 1 : 0;
-}
 // Conservative slab test of the ray o + t d, t >= 0, against the box bb = {min xyz, max xyz} (touching counts as a hit).
 __device__ __forceinline__ bool ray_hits_box(const float o[3], const float d[3], const float bb[6]) {
 	float tn = 0.0f, tf = 3.402823466e+38f;
@@ -77,7 +66,7 @@ __global__ void __launch_bounds__(256) k_ray_gen(uint32_t cap_rays, const StepSt
 #pragma unroll
 		for (int k = 0; k < 6; ++k) bb[k] = occ_bbox[k];
 	if (blockIdx.x == 0 && threadIdx.x == 0) {  // the march passes' ray queues and counters (next kernels on the stream)
-		march_queue[0] = 0; march_queue[1] = 0; march_queue[2] = 0; march_queue[3] = 0;
+		march_queue[0] = 0; march_queue[1] = 0;
 		st_w->march_total = 0; st_w->kept_extent = 0;
 		st_w->n_kept = 0; st_w->n_rays_with_samples = 0;  // this step's march maxima / counts (k_march, k_march_write)
 	}
@@ -143,71 +132,6 @@ __device__ __forceinline__ void load_march_ray(const float* __restrict__ rays, u
 		mr.o[d] = rr[d];
 		mr.dir[d] = unit ? du[d] : (nrm > 0.f ? du[d] / nrm : du[d]);
 		mr.idir[d] = 1.0f / mr.dir[d];
-	}
-}
-
-// ---------------------------------------------------------------- march order
-// A ray's march costs from a few events (empty space, large skips) to ~40 per lane (the occupied shell), and a wave
-// lasts as long as its slowest lanes. In slot order the few rays with samples (~6 % of the slots at the bench's late
-// state) are spread over ~40 % of the waves, each of which then runs as long as a full one. k_ray_order sorts the
-// slots of each march pass range ([0, est), [est, cap): the passes of k_march) into the rays whose path crosses an
-// occupied coarse cell (16^3, k_bitfield_coarse) first and the others after, so the expensive rays share waves and are
-// dispatched first. Only the assignment of slots to lanes changes: every output of the march is indexed by slot, so
-// the result is the slot-order march's, bit for bit (the order within a class follows the atomics and is immaterial).
-// cnt: 4 counters zeroed by k_ray_gen (heavy / light, per pass range).
-__global__ void __launch_bounds__(256) k_ray_order(uint32_t cap, const StepState* __restrict__ st, DevDataset ds, const float* __restrict__ rays,
-                                                   const float* __restrict__ tstart, const uint8_t* __restrict__ coarse, uint32_t* __restrict__ order,
-                                                   uint32_t* __restrict__ cnt) {
-	const uint32_t est = st->march_est ? min(st->march_est, cap) : cap;
-	const uint32_t lane = threadIdx.x & 63;
-	for (uint32_t i0 = (blockIdx.x * blockDim.x + threadIdx.x) & ~63u; i0 < cap; i0 += gridDim.x * blockDim.x) {
-		const uint32_t i = i0 + lane;
-		const bool have = i < cap;
-		const float t0 = have ? tstart[i] : -1.f;
-		bool heavy = false;
-		if (t0 >= 0.f) {
-			MarchRay mr;
-			load_march_ray(rays, i, mr, ds.motion.on != 0);
-			float t_exit = 3.402823466e+38f;
-#pragma unroll
-			for (int d = 0; d < 3; ++d)
-				t_exit = fminf(t_exit, fmaxf((ds.aabb_min[d] - mr.o[d]) * mr.idir[d], (ds.aabb_max[d] - mr.o[d]) * mr.idir[d]));
-			// points every half coarse cell along the ray inside the AABB; the first in an occupied coarse cell decides
-			constexpr float H = 0.5f / COARSE_RES;
-			for (uint32_t s = 0; s < 4 * COARSE_RES && !heavy; ++s) {
-				const float t = t0 + ((float)s + 0.5f) * H;
-				if (!(t < t_exit)) break;
-				int c[3];
-				bool in = true;
-#pragma unroll
-				for (int d = 0; d < 3; ++d) {
-					const float p = mr.o[d] + t * mr.dir[d];
-					in &= (p >= 0.f) & (p < 1.f);
-					c[d] = min((int)(p * (float)COARSE_RES), (int)COARSE_RES - 1);
-				}
-				if (in) heavy = coarse[(c[0] * COARSE_RES + c[1]) * COARSE_RES + c[2]] != 0;
-			}
-		}
-		// slot -> position: heavy rays from the range's start upward, the others from its end downward (one atomic per
-		// class per wave)
-#pragma unroll
-		for (uint32_t r = 0; r < 2; ++r) {
-			const bool mine = have && ((i < est) == (r == 0));
-			const uint64_t mh = __ballot(mine && heavy), ml = __ballot(mine && !heavy);
-			if (!(mh | ml)) continue;
-			uint32_t bh = 0, bl = 0;
-			if (lane == 0) {
-				if (mh) bh = atomicAdd(&cnt[2 * r], (uint32_t)__popcll(mh));
-				if (ml) bl = atomicAdd(&cnt[2 * r + 1], (uint32_t)__popcll(ml));
-			}
-			bh = (uint32_t)__shfl((int)bh, 0);
-			bl = (uint32_t)__shfl((int)bl, 0);
-			if (mine) {
-				const uint32_t lo = r == 0 ? 0u : est, hi = r == 0 ? est : cap;
-				const uint64_t below = (1ull << lane) - 1ull;
-				order[heavy ? lo + bh + (uint32_t)__popcll(mh & below) : hi - 1u - (bl + (uint32_t)__popcll(ml & below))] = i;
-			}
-		}
 	}
 }
 
@@ -393,9 +317,8 @@ __global__ void __launch_bounds__(256) MARCH_OCC k_march(uint32_t cap_rays, uint
 	uint32_t n_redo = 0;
 	auto stamp = [&](int ph) { if (pw && first && lane == 0) pw[ph] = wall_clock64(); };
 	stamp(0);
-	for (uint32_t j = lo + (blockIdx.x * blockDim.x + threadIdx.x) / MG; j - lo < ((hi - lo + groups - 1) / groups) * groups; j += groups) {
-		const bool have = j < hi;
-		const uint32_t i = (have && mw.order) ? mw.order[j] : j;  // the ray slot marched at position j (k_ray_order)
+	for (uint32_t i = lo + (blockIdx.x * blockDim.x + threadIdx.x) / MG; i - lo < ((hi - lo + groups - 1) / groups) * groups; i += groups) {
+		const bool have = i < hi;
 		const float t0 = have ? tstart[i] : -1.f;
 		MarchRay mr;
 		float t_exit = t0;
@@ -1300,7 +1223,6 @@ __global__ void k_step_counters(StepState* st, uint32_t target_batch, uint32_t m
 static inline uint32_t ray_blocks(uint32_t cap) { return std::max<uint32_t>(1, std::min<uint32_t>((cap + 255) / 256, 2048)); }
 void launch_bitfield_linear(hipStream_t s, const uint8_t* bitfield, uint32_t* lin) {
 	k_bitfield_linear<<<GRID3 / 32 / 256, 256, 0, s>>>(bitfield, lin);
-	k_bitfield_coarse<<<COARSE3 / 256, 256, 0, s>>>(lin, (uint8_t*)(lin + LIN_WORDS));
 }
 void launch_march_count(hipStream_t s, uint32_t cap, uint32_t max_samples, StepState* st, DPInfo dp, const DevDataset& ds, const uint8_t* bitfield,
                         const uint32_t* lin, uint64_t rng_state, uint64_t rng_inc, float* rays, float* tstart, uint32_t* nreq, const MarchWork& mw,
@@ -1308,22 +1230,19 @@ void launch_march_count(hipStream_t s, uint32_t cap, uint32_t max_samples, StepS
 	if (n_zero > 256) throw std::runtime_error("launch_march_count: at most 256 counters to zero");
 	k_ray_gen<<<ray_blocks(cap), 256, 0, s>>>(cap, st, dp, ds, rng_state, rng_inc, rays, tstart, mw.counter, st, mw.jt, zero_counters,
 	                                          zero_counters ? n_zero : 0u, occ_bbox);
-	MarchWork mwo = mw;
-	if (ds.cone_angle != 0.0f || !lin) mwo.order = nullptr;  // (the order's coarse cells come with the constant-step march's words)
-	if (mwo.order) k_ray_order<<<ray_blocks(cap), 256, 0, s>>>(cap, st, ds, rays, tstart, (const uint8_t*)(lin + LIN_WORDS), mwo.order, mw.counter);
 	const uint32_t waves = mw.waves ? std::min(mw.waves, (cap + 63) / 64) : (cap + 63) / 64;
 	const uint32_t blocks = std::max<uint32_t>(1, (waves + 3) / 4);
 	for (uint32_t pass = 0; pass < 2; ++pass) {
 		if (ds.cone_angle == 0.0f) {
-			if (mw.lanes_per_ray == 1) k_march<true, 1><<<blocks, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, lin, rays, tstart, nreq, mwo);
-			else if (mw.lanes_per_ray == 8) k_march<true, 8><<<blocks * 8, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, lin, rays, tstart, nreq, mwo);
-			else if (mw.lanes_per_ray == 16) k_march<true, 16><<<blocks * 16, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, lin, rays, tstart, nreq, mwo);
-			else k_march<true, 4><<<blocks * 4, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, lin, rays, tstart, nreq, mwo);
+			if (mw.lanes_per_ray == 1) k_march<true, 1><<<blocks, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, lin, rays, tstart, nreq, mw);
+			else if (mw.lanes_per_ray == 8) k_march<true, 8><<<blocks * 8, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, lin, rays, tstart, nreq, mw);
+			else if (mw.lanes_per_ray == 16) k_march<true, 16><<<blocks * 16, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, lin, rays, tstart, nreq, mw);
+			else k_march<true, 4><<<blocks * 4, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, lin, rays, tstart, nreq, mw);
 		} else {
-			if (mw.lanes_per_ray == 1) k_march<false, 1><<<blocks, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, nullptr, rays, tstart, nreq, mwo);
-			else if (mw.lanes_per_ray == 8) k_march<false, 8><<<blocks * 8, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, nullptr, rays, tstart, nreq, mwo);
-			else if (mw.lanes_per_ray == 16) k_march<false, 16><<<blocks * 16, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, nullptr, rays, tstart, nreq, mwo);
-			else k_march<false, 4><<<blocks * 4, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, nullptr, rays, tstart, nreq, mwo);
+			if (mw.lanes_per_ray == 1) k_march<false, 1><<<blocks, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, nullptr, rays, tstart, nreq, mw);
+			else if (mw.lanes_per_ray == 8) k_march<false, 8><<<blocks * 8, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, nullptr, rays, tstart, nreq, mw);
+			else if (mw.lanes_per_ray == 16) k_march<false, 16><<<blocks * 16, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, nullptr, rays, tstart, nreq, mw);
+			else k_march<false, 4><<<blocks * 4, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, nullptr, rays, tstart, nreq, mw);
 		}
 	}
 }

@@ -233,7 +233,7 @@ struct NeusTestbed {
 	// step workspace
 	uint32_t batch = 0, max_samples = 0;
 	Dev<float> rays, startt, coords, coords_c, loss, ek, mask, loss_sum;
-	Dev<uint32_t> nreq, base, numsteps, ccount, cbase, enc, march_nrec, march_queue, march_order;
+	Dev<uint32_t> nreq, base, numsteps, ccount, cbase, enc, march_nrec, march_queue;
 	Dev<uint2> march_rec, march_seg;
 	MarchWork mwork{};
 	Dev<float> dydx;
@@ -443,7 +443,7 @@ struct NeusTestbed {
 		HIP_CHECK(hipMemset(density_grid.p, 0, n_cells * 4));
 		bitfield.alloc(GRID3 / 8 * NERF_CASCADES);
 		HIP_CHECK(hipMemset(bitfield.p, 0xff, GRID3 / 8 * NERF_CASCADES));
-		bf_lin.alloc(LIN_ALLOC_WORDS);
+		bf_lin.alloc(LIN_WORDS);
 		launch_bitfield_linear(stream, bitfield.p, bf_lin.p);
 		occ_bbox.alloc(occ_bbox_scratch_floats());
 		launch_occ_bbox(stream, bitfield.p, occ_bbox.p);
@@ -655,11 +655,9 @@ struct NeusTestbed {
 	// MAX_RAYS rays and 16 x batch samples), occupancy-update scratch, device counters, dynamic-scene state.
 	void alloc_step_workspace() {
 		rays.alloc(6 * (size_t)MAX_RAYS); startt.alloc((size_t)MAX_RAYS);
-		march_rec.alloc((size_t)MAX_RAYS * NERF_STEPS); march_nrec.alloc(MAX_RAYS); march_queue.alloc(4);
-		march_order.alloc(MAX_RAYS);
+		march_rec.alloc((size_t)MAX_RAYS * NERF_STEPS); march_nrec.alloc(MAX_RAYS); march_queue.alloc(2);
 		march_seg.alloc((size_t)MAX_RAYS * MARCH_SEG_RECS);
 		mwork = MarchWork{march_rec.p, march_nrec.p, march_queue.p, march_waves(), march_seg.p, march_lanes(), jump_table()};
-		{ const char* e = std::getenv("NEUS_MARCH_ORDER"); if (!(e && e[0] == '0')) mwork.order = march_order.p; }
 		nreq.alloc(MAX_RAYS); base.alloc(MAX_RAYS);
 		numsteps.alloc(2 * (size_t)MAX_RAYS); ccount.alloc(MAX_RAYS); cbase.alloc(MAX_RAYS);
 		l_sa.alloc(max_samples); l_ekt.alloc(max_samples); sample_ray.alloc(max_samples); cmap.alloc(batch);
@@ -2220,14 +2218,12 @@ static void sample_rays_impl(NeusTestbed* tb, void* stream, uint32_t n_rays, uin
 		Dev<StepState> sst; sst.alloc(1);
 		StepState h{}; h.rays_per_batch = n_rays; h.max_inference = max_samples; h.n_rays_total = n_rays_total;
 		HIP_CHECK(hipMemcpyAsync(sst.p, &h, sizeof(h), hipMemcpyHostToDevice, s));
-		Dev<float> st_t; st_t.alloc(n_rays); Dev<uint32_t> nr, bs, nrec, q; nr.alloc(n_rays); bs.alloc(n_rays); nrec.alloc(n_rays); q.alloc(4);
-		Dev<uint32_t> order; order.alloc(n_rays);
+		Dev<float> st_t; st_t.alloc(n_rays); Dev<uint32_t> nr, bs, nrec, q; nr.alloc(n_rays); bs.alloc(n_rays); nrec.alloc(n_rays); q.alloc(2);
 		Dev<uint2> rec; rec.alloc((size_t)n_rays * NERF_STEPS);
 		Dev<uint2> seg; seg.alloc((size_t)n_rays * MARCH_SEG_RECS);
-		MarchWork mw{rec.p, nrec.p, q.p, tb->mwork.waves, seg.p, tb->mwork.lanes_per_ray};
-		if (tb->mwork.order) mw.order = order.p;
+		const MarchWork mw{rec.p, nrec.p, q.p, tb->mwork.waves, seg.p, tb->mwork.lanes_per_ray};
 		ScanTemp tmp; const size_t tb_ = scan_temp_bytes(n_rays); tmp.alloc(tb_ + 256); scan_temp_reset(s, tmp.p);
-		Dev<uint32_t> lin; lin.alloc(LIN_ALLOC_WORDS);
+		Dev<uint32_t> lin; lin.alloc(LIN_WORDS);
 		launch_bitfield_linear(s, bitfield, lin.p);
 		// the occupied-box cull of the training step, from this bitfield (exact: culled rays march to zero samples)
 		Dev<float> bb; bb.alloc(occ_bbox_scratch_floats());
