@@ -277,14 +277,14 @@ def _teacher_forced_all_levels(sc, tag, progressive, n_steps=14, prepare=700, sh
     (fill_rollover_and_rescale, common_device.h:515-535). Per step: the march bit-exact, the compacted count equal up to
     fp16-moved cut-offs, every gradient block cos >= 0.9999 and rel-L2 <= 2e-3; per hash level the worst rel-L2 is
     recorded. progressive: None leaves the auto rule on (asserted to have run the rounds), 2 forces the rounds.
-    fixed_rays: R = the batch every step (the bench's shape, fixed_rays_per_batch; no short step there: R = Nc rays
-    always composite more than Nc samples).
+    fixed_rays: R fixed at this many rays every step (fixed_rays_per_batch; no short step there: the rays composite
+    more than Nc samples).
     Reference: testbed_nerf.cu:3723-4001, grid.h:371-500, 880-1007, 2427-2440."""
     import ctypes as C
     import oracle as O
     from cpu_step import CpuTrainer
     from neus2_amd._lib import NeusRestoreState, check, lib
-    tb = _testbed(sc, fixed_rays_per_batch=BATCH) if fixed_rays else _testbed(sc)
+    tb = _testbed(sc, fixed_rays_per_batch=fixed_rays) if fixed_rays else _testbed(sc)
     if progressive is not None:
         tb.set_progressive_inference(progressive, (32, 64, 96))
     tb.train_steps(prepare)
@@ -292,7 +292,7 @@ def _teacher_forced_all_levels(sc, tag, progressive, n_steps=14, prepare=700, sh
     cfg = O.make_cfg(per_level_scale=tb._net_cfg.per_level_scale)
     assert tb.stats()["valid_level"] + 1 >= cfg.n_levels, "not every level is active"
     ds = O.Dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"])
-    tr = CpuTrainer(cfg, ds, tb.get_params(), batch=BATCH, rays_per_batch=BATCH, fixed_rays=fixed_rays)
+    tr = CpuTrainer(cfg, ds, tb.get_params(), batch=BATCH, rays_per_batch=fixed_rays or BATCH, fixed_rays=bool(fixed_rays))
     blocks = {"density": (0, lay["n_density"]), "rgb": (lay["n_density"], lay["n_matrix"]),
               "grid": (lay["grid_offset"], lay["variance_offset"]), "variance": (lay["variance_offset"], lay["variance_offset"] + 1)}
     off, _, _, _ = O.grid_tables(cfg)
@@ -358,7 +358,9 @@ def _teacher_forced_all_levels(sc, tag, progressive, n_steps=14, prepare=700, sh
             evaluated_over_kept=evaluated / max(kept, 1), later_round_rays=later_rounds, short_step_compacted_below_batch=short_seen,
             **{f"min_cos_{k}": v[0] for k, v in worst.items()}, **{f"max_rel_{k}": v[1] for k, v in worst.items()},
             **{f"max_rel_grid_L{l}": lev_rel[l] for l in range(cfg.n_levels)})
-    assert prog >= n_steps - 1, f"progressive inference ran on {prog} of {n_steps} steps"
+    st = tb.stats()
+    assert prog >= n_steps - 1, (f"progressive inference ran on {prog} of {n_steps} steps (last step: {st['measured_batch_size']} "
+                                 f"compacted of {st['measured_batch_size_before_compaction']} requested)")
     assert evaluated < kept, "the rounds evaluated every kept sample: the cut-off never skipped work"
     assert later_rounds > 0, "no ray composited past the first chunk: the later rounds had no work"
     assert short_seen or short_step is None, "no step compacted fewer samples than the batch: the rollover did not run"
@@ -375,11 +377,13 @@ def test_teacher_forced_all_levels_vs_oracle(scene, torch_cuda):
 
 def test_teacher_forced_all_levels_config_s_auto(torch_cuda):
     """_teacher_forced_all_levels on the bench's scene (Config S: 49 views of 1600x1200, DTU-scan24 intrinsics) at a
-    4096-sample batch and the bench's ray shape (R = Nc fixed), progressive inference left on its auto rule, which
-    turns the rounds on there (under 70 % of the kept samples composited)."""
+    4096-sample batch with R fixed at 4 Nc, progressive inference left on its auto rule. The auto rule turns the rounds
+    on when under 70 % of the kept samples are composited; at the bench state (R = Nc = 2^18 rays of a network trained
+    on 64x the samples) the 16 Nc sample cap cuts the kept rays to those whose early samples composite; at 4096 samples
+    per step the network is less converged and R = Nc stays above the ratio, R = 4 Nc reproduces the cut."""
     from neus2_amd import scenes
     sc = scenes.sphere_scene(49, 1600, 1200, principal=(823.2 / 1600, 619.1 / 1200))
-    _teacher_forced_all_levels(sc, "config_s_auto", progressive=None, short_step=None, fixed_rays=True)
+    _teacher_forced_all_levels(sc, "config_s_auto", progressive=None, short_step=None, fixed_rays=4 * BATCH)
 
 
 def test_training_is_bitwise_reproducible(scene, torch_cuda):
