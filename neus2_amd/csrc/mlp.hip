@@ -963,7 +963,9 @@ __device__ __forceinline__ void load_dydx(const float* __restrict__ dydx, uint32
 typedef __attribute__((address_space(3))) void* lds_vptr;
 __device__ __forceinline__ void glds16(const void* g, const uint32_t* lds_dst) {
 	const uint32_t a = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_vptr)lds_dst);
-	asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(a) : "memory", "m0");
+	uint32_t keep;  // m0 is reserved by the compiler: saved and restored around the copy
+	asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+	             : "=&s"(keep) : "v"(g), "s"(a) : "memory");
 }
 // n16 pieces of 16 B, contiguous at src -> dst
 template <int N16>
