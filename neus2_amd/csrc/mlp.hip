@@ -953,45 +953,6 @@ __device__ __forceinline__ void load_dydx(const float* __restrict__ dydx, uint32
 	dy[0] = dp[0]; dy[1] = dp[ld]; dy[2] = dp[2 * (size_t)ld];
 }
 
-// ---- LDS-DMA staging of a 32-sample chunk's inputs (global_load_lds, 16 B per lane, destination = the wave-uniform
-// base + 16 B x lane). The training kernels run one wave per SIMD, so a chunk's loads cannot hide behind other waves:
-// each wave issues the next chunk's copies as soon as it has read the current chunk's, and they land during the
-// current chunk's compute without holding VGPRs. The staging buffers are their own __shared__ arrays, apart from the
-// weights. The copies are issued by inline asm, so the compiler does not track them: with the builtin it waited for them
-// (vmcnt(0)) before the first weight reads of the chunk, which serialised the copies with the compute again. The
-// kernels wait for them themselves (wait_vm_all before reading the staging buffer; no other global loads in the loop).
-typedef __attribute__((address_space(3))) void* lds_vptr;
-__device__ __forceinline__ void glds16(const void* g, const uint32_t* lds_dst) {
-	const uint32_t a = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_vptr)lds_dst);
-	uint32_t keep;  // m0 is reserved by the compiler: saved and restored around the copy
-	asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-	             : "=&s"(keep) : "v"(g), "s"(a) : "memory");
-}
-// n16 pieces of 16 B, contiguous at src -> dst
-template <int N16>
-__device__ __forceinline__ void stage_bytes(const void* src, uint32_t* dst, int lane) {
-#pragma unroll
-	for (int q = 0; q < (N16 + 63) / 64; ++q)
-		if (64 * q + lane < N16)
-			glds16((const uint8_t*)src + (size_t)(64 * q + lane) * 16, dst + 256 * q);
-}
-// ROWS rows of RB bytes (RB = 64 or 128: 32 samples of 2 or 4 B), row k at src + k * stride bytes -> dst rows of RB bytes
-template <int ROWS, int RB>
-__device__ __forceinline__ void stage_rows(const void* src, size_t stride, uint32_t* dst, int lane) {
-	constexpr int LPR = RB / 16, RPI = 64 / LPR;  // lanes per row, rows per wave instruction
-	const int rr = lane / LPR, cc = (lane % LPR) * 16;
-#pragma unroll
-	for (int q = 0; q < (ROWS + RPI - 1) / RPI; ++q)
-		if (RPI * q + rr < ROWS)
-			glds16((const uint8_t*)src + (size_t)(RPI * q + rr) * stride + cc, dst + 256 * q);
-}
-__device__ __forceinline__ void wait_vm_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-__device__ __forceinline__ void wait_lgkm_all() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-// staging layouts (words per wave): colour kernel {coords 32 x 7 f32, dL/dout 32 x 16 fp16, enc [L][32], dy/dx [6L][32]},
-// density kernel {coords, enc, dy/dx, delta_D1 [16][32] fp16, v 32 x float4}
-template <int L> struct StgRgb { static constexpr int C = 0, D = 224, E = 480, Y = E + 32 * L, N = Y + 192 * L; };
-template <int L> struct StgDen { static constexpr int C = 0, E = 224, Y = E + 32 * L, D1 = Y + 192 * L, V = D1 + 256, N = V + 128; };
-
 // backward weight set: transposed copies, staged after the forward set
 struct BwdW { MatRef r2T, r1T, r0T, d1T; };
 template <int L, int W> struct TrainSmem {
@@ -1088,43 +1049,28 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 		for (int kt = 0; kt < MT; ++kt) aR1[mt][kt] = zero16();
 	}
 	float var_part = 0.f;
-	// the chunk's inputs through the wave's staging buffer (n % 32 == 0: every chunk is whole)
-	using SG = StgRgb<L>;
-	__shared__ uint32_t stg[4][SG::N];
-	uint32_t* my = stg[threadIdx.x >> 6];
-	auto stage = [&](uint32_t b) {
-		stage_bytes<32 * COORD_W * 4 / 16>(coords + (size_t)b * COORD_W, my + SG::C, lane);
-		stage_bytes<32 * OUT_W * 2 / 16>(dL_dout + (size_t)b * OUT_W, my + SG::D, lane);
-		stage_rows<L, 128>(enc_h + (size_t)b * 2, (size_t)ld * 4, my + SG::E, lane);
-		stage_rows<6 * L, 128>(dydx + b, (size_t)ld * 4, my + SG::Y, lane);
-	};
-	if (wave * 32 < n) stage(wave * 32);
 	for (uint32_t base = wave * 32; base < n; base += n_waves * 32) {
 		const uint32_t z = opaque_zero();
 		const FwdW fw = fw0.at(z);
 		const BwdW bw{rebase(bw0.r2T, z), rebase(bw0.r1T, z), rebase(bw0.r0T, z), rebase(bw0.d1T, z)};
 		const uint32_t i = base + r;
 		const bool valid = i < n;
-		// ---- this chunk's inputs from the staging buffer, then the next chunk's copies are issued
-		wait_vm_all();
-		const float* sc = (const float*)(my + SG::C) + r * COORD_W;
-		const float x[3] = {sc[0], sc[1], sc[2]}, wd[3] = {sc[4], sc[5], sc[6]};
+		const uint32_t ic = valid ? i : 0;
+		const float* c = coords + (size_t)ic * COORD_W;
+		const float x[3] = {c[0], c[1], c[2]}, wd[3] = {c[4], c[5], c[6]};
+		// ---- forward recompute up to the colour hidden layers
 		uint32_t ev[L];
-#pragma unroll
-		for (int l = 0; l < L; ++l) ev[l] = my[SG::E + 32 * l + r];
-		float dyv[DMT * 16][3];  // dy/dx of this lane's density-input slots (clamped rows outside the features)
+		load_enc<L>(ev, enc_h, ld, ic);
+		// all of the chunk's dy/dx loads (and dL/dout) are issued right after the encoding's, before the density forward:
+		// one memory round trip per chunk, the dy/dx part overlapped with the forward's MFMAs (loads complete in order,
+		// so the forward waits for the encoding only; the sched_barrier keeps them up front)
+		float dyv[DMT * 16][3];
 #pragma unroll
 		for (int mt = 0; mt < DMT; ++mt)
 #pragma unroll
-			for (int reg = 0; reg < 16; ++reg) {
-				const int q = min(max(32 * mt + acc_row(reg, h) - 3, 0), 2 * L - 1);
-#pragma unroll
-				for (int d = 0; d < 3; ++d) dyv[16 * mt + reg][d] = __uint_as_float(my[SG::Y + (3 * q + d) * 32 + r]);
-			}
-		const h8 dlo_ld = *(const h8*)(my + SG::D + r * 8 + 4 * h);  // h=0: rows 0..7, h=1: rows 8..15
-		wait_lgkm_all();
-		if (base + n_waves * 32 < n) stage(base + n_waves * 32);
-		// ---- forward recompute up to the colour hidden layers
+			for (int reg = 0; reg < 16; ++reg) load_dydx<L>(dydx, ld, ic, 32 * mt + acc_row(reg, h), dyv[16 * mt + reg]);
+		const h8 dlo_ld = *(const h8*)(dL_dout + (size_t)ic * OUT_W + 8 * h);  // h=0: rows 0..7, h=1: rows 8..15
+		__builtin_amdgcn_sched_barrier(0);
 		h8 dinB[DKS];
 		build_din<L>(dinB, x, ev, h);
 		h8 H0B[HKS], D1B, GhB[HKS];
@@ -1280,17 +1226,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 #pragma unroll
 		for (int kt = 0; kt < DMT; ++kt) aD0[mt][kt] = zero16();
 	}
-	using SG = StgDen<L>;
-	__shared__ uint32_t stg[4][SG::N];
-	uint32_t* my = stg[threadIdx.x >> 6];
-	auto stage = [&](uint32_t b) {
-		stage_bytes<32 * COORD_W * 4 / 16>(coords + (size_t)b * COORD_W, my + SG::C, lane);
-		stage_rows<L, 128>(enc_h + (size_t)b * 2, (size_t)ld * 4, my + SG::E, lane);
-		stage_rows<6 * L, 128>(dydx + b, (size_t)ld * 4, my + SG::Y, lane);
-		stage_rows<16, 64>(tb.d1_delta + b, (size_t)ld * 2, my + SG::D1, lane);
-		stage_bytes<32>(tb.v + b, my + SG::V, lane);
-	};
-	if (wave * 32 < n) stage(wave * 32);
 	for (uint32_t base = wave * 32; base < n; base += n_waves * 32) {
 		const uint32_t z = opaque_zero();
 		const FwdW fw = fw0.at(z);
@@ -1298,31 +1233,24 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
 		const uint32_t i = base + r;
 		const bool valid = i < n;
 		const uint32_t ic = valid ? i : 0;
-		// this chunk's inputs from the staging buffer (as the colour kernel): coordinates, encoding, dy/dx of this lane's
-		// density-input slots (the accumulator rows k = 32 mt + acc_row(reg, h); fragment j of k-step ks is register
-		// 8 (ks & 1) + j of tile ks >> 1), delta_D1 and v; then the next chunk's copies
-		wait_vm_all();
-		const float* sc = (const float*)(my + SG::C) + r * COORD_W;
-		const float x[3] = {sc[0], sc[1], sc[2]};
+		const float* c = coords + (size_t)ic * COORD_W;
+		const float x[3] = {c[0], c[1], c[2]};
+		// the chunk's loads up front (as the colour kernel): encoding, then dy/dx of this lane's density-input slots (the
+		// accumulator rows k = 32 mt + acc_row(reg, h); fragment j of k-step ks is register 8 (ks & 1) + j of tile ks >> 1),
+		// delta_D1 and v
 		uint32_t ev[L];
-#pragma unroll
-		for (int l = 0; l < L; ++l) ev[l] = my[SG::E + 32 * l + r];
+		load_enc<L>(ev, enc_h, ld, ic);
+		__builtin_amdgcn_sched_barrier(0);  // (the encoding's loads first: in-order completion lets the forward wait for them alone)
 		float dyv[DMT * 16][3];
 #pragma unroll
 		for (int mt = 0; mt < DMT; ++mt)
 #pragma unroll
-			for (int reg = 0; reg < 16; ++reg) {
-				const int q = min(max(32 * mt + acc_row(reg, h) - 3, 0), 2 * L - 1);
-#pragma unroll
-				for (int d = 0; d < 3; ++d) dyv[16 * mt + reg][d] = __uint_as_float(my[SG::Y + (3 * q + d) * 32 + r]);
-			}
+			for (int reg = 0; reg < 16; ++reg) load_dydx<L>(dydx, ld, ic, 32 * mt + acc_row(reg, h), dyv[16 * mt + reg]);
 		half_t d1v[8];
-		const half_t* sd1 = (const half_t*)(my + SG::D1);
 #pragma unroll
-		for (int j = 0; j < 8; ++j) d1v[j] = sd1[(h ? pi_row(j, 1) : pi_row(j, 0)) * 32 + r];
-		const float4 v4 = ((const float4*)(my + SG::V))[r];
-		wait_lgkm_all();
-		if (base + n_waves * 32 < n) stage(base + n_waves * 32);
+		for (int j = 0; j < 8; ++j) d1v[j] = tb.d1_delta[(size_t)(h ? pi_row(j, 1) : pi_row(j, 0)) * ld + ic];
+		const float4 v4 = tb.v[ic];
+		__builtin_amdgcn_sched_barrier(0);
 		h8 dinB[DKS];
 		build_din<L>(dinB, x, ev, h);
 		h8 H0B[HKS], D1B, GhB[HKS];
@@ -1833,9 +1761,6 @@ void launch_mlp_train(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_v
                       const half_t* enc, const float* dydx, const half_t* dL_dout, const MlpPtrs& w, const TrainBufs& tb, int part) {
 	const uint32_t blocks = mlp_train_blocks(L, W, n);
 	if (n == 0) return;
-	// whole 32-sample chunks staged by 16-B LDS-DMA copies: n and ld multiples of 32, the buffers 16-B aligned
-	if (n % 32 || ld % 32 || ((uintptr_t)coords | (uintptr_t)enc | (uintptr_t)dydx | (uintptr_t)dL_dout | (uintptr_t)tb.d1_delta | (uintptr_t)tb.v) & 15)
-		throw std::runtime_error("launch_mlp_train: n and ld must be multiples of 32 and the buffers 16-B aligned");
 #define X(l, w_) if (L == l && W == w_) { \
 		if (part != 2) k_mlp_train_rgb<l, w_><<<blocks, 256, 0, s>>>(n_valid_ptr, n, ld, coords, enc, dydx, dL_dout, w, tb); \
 		if (part != 1) k_mlp_train_density<l, w_><<<blocks, 256, 0, s>>>(n_valid_ptr, n, ld, coords, enc, dydx, w, tb); return; }
