@@ -268,7 +268,7 @@ def test_teacher_forced_steps_vs_oracle(scene, torch_cuda):
         assert cos >= 0.9999 and rel <= 2e-3, (name, cos, rel)
 
 
-def _teacher_forced_all_levels(sc, tag, progressive, n_steps=14, prepare=700, short_step=5, fixed_rays=False):
+def _teacher_forced_all_levels(sc, tag, progressive, n_steps=14, prepare=700, short_step=5, fixed_rays=False, prepare_batch=None):
     """Teacher-forced training at the all-levels state: the device trains `prepare` free-running steps
     first, so all 14 levels are active (hashed levels 5-13: 2^19-entry tables, the 2048-entry region scatter of hashed
     buckets) and the occupancy grid is shaped by hundreds of updates. Then n_steps consecutive steps, each compared with
@@ -278,7 +278,9 @@ def _teacher_forced_all_levels(sc, tag, progressive, n_steps=14, prepare=700, sh
     fp16-moved cut-offs, every gradient block cos >= 0.9999 and rel-L2 <= 2e-3; per hash level the worst rel-L2 is
     recorded. progressive: None leaves the auto rule on (asserted to have run the rounds), 2 forces the rounds.
     fixed_rays: R fixed at this many rays every step (fixed_rays_per_batch; no short step there: the rays composite
-    more than Nc samples).
+    more than Nc samples). prepare_batch: the `prepare` steps run in a second testbed at this batch (and as many fixed
+    rays), whose parameters, optimizer state, occupancy grid and step count are then moved into the 4096-sample one:
+    a state as converged as the bench's.
     Reference: testbed_nerf.cu:3723-4001, grid.h:371-500, 880-1007, 2427-2440."""
     import ctypes as C
     import oracle as O
@@ -287,7 +289,21 @@ def _teacher_forced_all_levels(sc, tag, progressive, n_steps=14, prepare=700, sh
     tb = _testbed(sc, fixed_rays_per_batch=fixed_rays) if fixed_rays else _testbed(sc)
     if progressive is not None:
         tb.set_progressive_inference(progressive, (32, 64, 96))
-    tb.train_steps(prepare)
+    if prepare_batch:
+        big = _testbed(sc, batch=prepare_batch, fixed_rays_per_batch=prepare_batch)
+        big.train_steps(prepare)
+        tb.set_params(big.get_params())
+        tb.set_optimizer_state(big.get_optimizer_state())
+        grid, bf = big.get_density_grid()
+        tb.set_density_grid(grid, bf)
+        st = big.stats()
+        rs = NeusRestoreState(training_step=st["training_step"], rays_per_batch=fixed_rays or BATCH, measured_batch_size=BATCH,
+                              measured_batch_size_before_compaction=16 * BATCH, loss=st["loss"], rebuild_bitfield=0)
+        check(lib().neus_testbed_restore_state(tb.handle, C.byref(rs)))
+        del big
+        tb.train_steps(2)  # the auto rule reads the previous step's composited / kept ratio
+    else:
+        tb.train_steps(prepare)
     lay = tb.layout()
     cfg = O.make_cfg(per_level_scale=tb._net_cfg.per_level_scale)
     assert tb.stats()["valid_level"] + 1 >= cfg.n_levels, "not every level is active"
@@ -377,13 +393,14 @@ def test_teacher_forced_all_levels_vs_oracle(scene, torch_cuda):
 
 def test_teacher_forced_all_levels_config_s_auto(torch_cuda):
     """_teacher_forced_all_levels on the bench's scene (Config S: 49 views of 1600x1200, DTU-scan24 intrinsics) at a
-    4096-sample batch with R fixed at 4 Nc, progressive inference left on its auto rule. The auto rule turns the rounds
-    on when under 70 % of the kept samples are composited; at the bench state (R = Nc = 2^18 rays of a network trained
-    on 64x the samples) the 16 Nc sample cap cuts the kept rays to those whose early samples composite; at 4096 samples
-    per step the network is less converged and R = Nc stays above the ratio, R = 4 Nc reproduces the cut."""
+    4096-sample batch and the bench's ray shape (R = Nc fixed), from a state trained 800 steps at 2^16 samples per step
+    (the bench trains at 2^18; a network trained on 4096-sample steps is far less opaque and composites nearly every
+    kept sample: measured 65120 of 65536), with progressive inference left on its auto rule, which turns the rounds on
+    when under 70 % of the kept samples are composited."""
     from neus2_amd import scenes
     sc = scenes.sphere_scene(49, 1600, 1200, principal=(823.2 / 1600, 619.1 / 1200))
-    _teacher_forced_all_levels(sc, "config_s_auto", progressive=None, short_step=None, fixed_rays=4 * BATCH)
+    _teacher_forced_all_levels(sc, "config_s_auto", progressive=None, prepare=800, short_step=None, fixed_rays=BATCH,
+                               prepare_batch=1 << 16)
 
 
 def test_training_is_bitwise_reproducible(scene, torch_cuda):
