@@ -467,17 +467,26 @@ static void sh4(const float wd[3], float* out) {
 	out[15] = 0.59004358992664352f * x * (-x2 + 3.0f * y2);
 }
 
+// Summation order of the layer products (or_set_sum_order): 0 = index order (the oracle), 1 = reversed. Test-only: the
+// reversed oracle measures how far the fp32 accumulation order alone moves a training step (fp16 activations flipping
+// at rounding boundaries), the noise floor against which the device's MFMA-ordered sums are compared.
+static int g_sum_reverse = 0;
 // y = W x with W RM [out][in] (fp16-rounded weights), fp32 accumulation.
 static inline void matvec(const float* W, uint32_t out, uint32_t in, const float* x, float* y) {
 	for (uint32_t o = 0; o < out; ++o) {
 		float s = 0; const float* w = W + (size_t)o * in;
-		for (uint32_t i = 0; i < in; ++i) s += w[i] * x[i];
+		if (g_sum_reverse) for (uint32_t i = in; i-- > 0;) s += w[i] * x[i];
+		else for (uint32_t i = 0; i < in; ++i) s += w[i] * x[i];
 		y[o] = s;
 	}
 }
 // y = W^T d
 static inline void matvec_t(const float* W, uint32_t out, uint32_t in, const float* d, float* y) {
 	for (uint32_t i = 0; i < in; ++i) y[i] = 0;
+	if (g_sum_reverse) {
+		for (uint32_t o = out; o-- > 0;) { const float* w = W + (size_t)o * in; for (uint32_t i = 0; i < in; ++i) y[i] += w[i] * d[o]; }
+		return;
+	}
 	for (uint32_t o = 0; o < out; ++o) { const float* w = W + (size_t)o * in; for (uint32_t i = 0; i < in; ++i) y[i] += w[i] * d[o]; }
 }
 
@@ -655,6 +664,7 @@ struct SampleRay { float o[3], d[3]; };  // Ray (unnormalized direction)
 extern "C" {
 
 uint32_t or_net_n_params(const OrNetCfg* c) { Net n(*c); return n.n_params; }
+void or_set_sum_order(int reverse) { g_sum_reverse = reverse ? 1 : 0; }
 void or_net_layout(const OrNetCfg* c, uint32_t* out) {
 	Net n(*c);
 	out[0] = n.n_density; out[1] = n.n_rgb; out[2] = n.grid_off; out[3] = n.n_grid_params; out[4] = n.var_off; out[5] = n.n_params; out[6] = n.n_matrix;

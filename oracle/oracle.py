@@ -289,6 +289,12 @@ def num_threads():
     return lib().or_num_threads()
 
 
+def set_sum_order(reverse: bool):
+    """Layer products summed in reversed index order (True) or index order (False, the default): test-only, to measure
+    how much the fp32 accumulation order alone moves a step (the noise floor of the fp16 network)."""
+    lib().or_set_sum_order(C.c_int(1 if reverse else 0))
+
+
 class OrRenderCamera(C.Structure):
     _fields_ = [("xform", C.c_float * 12), ("focal", C.c_float * 2), ("screen_center", C.c_float * 2),
                 ("width", C.c_uint32), ("height", C.c_uint32)]

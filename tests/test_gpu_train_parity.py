@@ -314,7 +314,8 @@ def _teacher_forced_all_levels(sc, tag, progressive, n_steps=14, prepare=700, sh
     off, _, _, _ = O.grid_tables(cfg)
     g0 = lay["grid_offset"]
     worst = {k: [1.0, 0.0] for k in blocks}
-    lev_rel = np.zeros(cfg.n_levels)
+    floor = {k: 0.0 for k in blocks}
+    lev_rel, lev_floor = np.zeros(cfg.n_levels), np.zeros(cfg.n_levels)
     prog0 = tb.stats()["progressive_steps"]
     short_seen, n_comp_equal, later_rounds, evaluated, kept = False, 0, 0, 0, 0
     for k in range(n_steps):
@@ -345,6 +346,15 @@ def _teacher_forced_all_levels(sc, tag, progressive, n_steps=14, prepare=700, sh
         tr.density_grid[:] = grid
         tr.bitfield[:] = bf
         gr = tr.grads(skip_occupancy=True).astype(np.float64)
+        # the noise floor: the same oracle step with its layer products summed in reversed order (fp16 activations
+        # flip at rounding boundaries; the device's MFMA sums are a third order)
+        last = tr.last
+        O.set_sum_order(True)
+        try:
+            gr_rev = tr.grads(skip_occupancy=True).astype(np.float64)
+        finally:
+            O.set_sum_order(False)
+        tr.last = last
         kept += tr.last["n_kept"]
         # the requested-sample counter: equal below the cap; past it the device's prefix-limited march (k_march's
         # second pass skipped once the first pass's rays request max_samples) reads some value >= the cap, which is
@@ -364,24 +374,29 @@ def _teacher_forced_all_levels(sc, tag, progressive, n_steps=14, prepare=700, sh
             rel = np.linalg.norm(x - y) / max(np.linalg.norm(y), 1e-30)
             worst[name][0] = min(worst[name][0], cos)
             worst[name][1] = max(worst[name][1], rel)
+            floor[name] = max(floor[name], np.linalg.norm(gr_rev[a:b] - y) / max(np.linalg.norm(y), 1e-30))
         for l in range(cfg.n_levels):
             a, b = g0 + 2 * int(off[l]), g0 + 2 * int(off[l + 1])
             y = gr[a:b]
             if np.linalg.norm(y) > 0:
                 lev_rel[l] = max(lev_rel[l], np.linalg.norm(g[a:b] - y) / np.linalg.norm(y))
+                lev_floor[l] = max(lev_floor[l], np.linalg.norm(gr_rev[a:b] - y) / np.linalg.norm(y))
     prog = tb.stats()["progressive_steps"] - prog0
     _record(f"teacher_forced_all_levels_{tag}", steps=n_steps, start_step=prepare, compacted_equal_steps=n_comp_equal, progressive_steps=prog,
             evaluated_over_kept=evaluated / max(kept, 1), later_round_rays=later_rounds, short_step_compacted_below_batch=short_seen,
             **{f"min_cos_{k}": v[0] for k, v in worst.items()}, **{f"max_rel_{k}": v[1] for k, v in worst.items()},
-            **{f"max_rel_grid_L{l}": lev_rel[l] for l in range(cfg.n_levels)})
+            **{f"max_rel_grid_L{l}": lev_rel[l] for l in range(cfg.n_levels)},
+            **{f"floor_rel_{k}": v for k, v in floor.items()}, **{f"floor_rel_grid_L{l}": lev_floor[l] for l in range(cfg.n_levels)})
     st = tb.stats()
     assert prog >= n_steps - 1, (f"progressive inference ran on {prog} of {n_steps} steps (last step: {st['measured_batch_size']} "
                                  f"compacted of {st['measured_batch_size_before_compaction']} requested)")
     assert evaluated < kept, "the rounds evaluated every kept sample: the cut-off never skipped work"
     assert later_rounds > 0, "no ray composited past the first chunk: the later rounds had no work"
     assert short_seen or short_step is None, "no step compacted fewer samples than the batch: the rollover did not run"
+    # per block: cos >= 0.9999 and rel-L2 <= 2e-3, or within 3x of the oracle's own spread under a reversed summation
+    # order (a converged state's gradients are sums of nearly cancelling fp16 terms: their rel-L2 floor rises above 2e-3)
     for name, (cos, rel) in worst.items():
-        assert cos >= 0.9999 and rel <= 2e-3, (name, cos, rel)
+        assert cos >= 0.9999 and rel <= max(2e-3, 3.0 * floor[name]), (name, cos, rel, floor[name])
 
 
 def test_teacher_forced_all_levels_vs_oracle(scene, torch_cuda):
