@@ -567,13 +567,18 @@ constexpr int SC_U = 8;
 #endif
 constexpr int SC_WAVES = NEUS_SC_WAVES;  // (8 waves per workgroup measured slower: 93 -> 103 us at the bench state)
 __global__ void __launch_bounds__(64 * SC_WAVES) k_scatter_accum_r(ScatterWork w, const GridLevels gl, float* __restrict__ grads, uint32_t bs8,
-                                                                   uint32_t job0) {
+                                                                   uint32_t job0, uint32_t n_jobs, uint32_t xg) {
 	__shared__ unsigned long long acc[2 * SB_SIZE];
 	__shared__ uint32_t s_pre[SC_WAVES][65], s_src[SC_WAVES][64];
 	__shared__ uint32_t s_last;
-	// (jobs in list order: an XCD-contiguous mapping - each XCD taking an eighth of the list, so adjacent buckets'
-	// segments that share lines meet in one L2 - measured 93 -> 169 us at the bench state)
-	const uint4 job = w.jobs2[job0 + blockIdx.x];
+	// Workgroup -> job: groups of xg consecutive jobs (adjacent buckets of a level, whose record segments share 128-B
+	// lines of every block's region) go to one XCD (workgroups are dispatched to the XCDs round-robin: XCD = blockIdx
+	// mod 8), so a shared line is fetched into one L2 instead of two; xg = 1 is list order. (An XCD-contiguous mapping,
+	// each XCD an eighth of the list, measured 93 -> 169 us at the bench state.)
+	const uint32_t bx = blockIdx.x & 7u, bk = blockIdx.x >> 3;
+	const uint32_t jl = ((bk / xg) * 8u + bx) * xg + bk % xg;
+	if (jl >= n_jobs) return;
+	const uint4 job = w.jobs2[job0 + jl];
 	const uint32_t l = job.x, kb = job.y, part = job.z & 0xffffu, parts = job.z >> 16, slot = job.w;
 	const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
 	for (uint32_t k = threadIdx.x; k < 2 * SB_SIZE; k += blockDim.x) acc[k] = 0ull;
@@ -849,6 +854,8 @@ uint32_t scatter_n_buckets(const GridLevels& gl) {
 			throw std::runtime_error("hash-grid level table too large for the scatter's per-level buckets");
 	return (gl.offset[gl.n_levels] + SB_SIZE - 1) >> SB_SHIFT;
 }
+// the accumulation grid: n jobs rounded up to whole rounds of 8 XCD groups (the remap's domain)
+static inline uint32_t accum_blocks(uint32_t n, uint32_t xg) { return (n + 8 * xg - 1) / (8 * xg) * (8 * xg); }
 void launch_grid_scatter(hipStream_t s, const uint32_t* n_ptr, uint32_t n_fixed, uint32_t ld, const float* coords, uint32_t coord_stride,
                          const GridLevels& gl, uint32_t valid_level, const half_t* dLdenc, const half_t* g, const float4* v, float* grads,
                          const ScatterWork& w, void* scan_tmp, size_t scan_tmp_bytes, const ScatterSplit* split) {
@@ -870,7 +877,7 @@ void launch_grid_scatter(hipStream_t s, const uint32_t* n_ptr, uint32_t n_fixed,
 		const uint32_t n_act = std::min(valid_level + 1, gl.n_levels);
 		if (!split) {
 			const uint32_t nj = std::min(w.n_jobs2, w.jobs2_before[n_act]);
-			if (nj) k_scatter_accum_r<<<nj, 64 * SC_WAVES, 0, s>>>(w, gl, grads, w.chunk * 8, 0u);
+			if (nj) k_scatter_accum_r<<<accum_blocks(nj, w.xcd_group), 64 * SC_WAVES, 0, s>>>(w, gl, grads, w.chunk * 8, 0u, nj, w.xcd_group);
 			return;
 		}
 		uint32_t lo = 0;
@@ -878,7 +885,8 @@ void launch_grid_scatter(hipStream_t s, const uint32_t* n_ptr, uint32_t n_fixed,
 			const uint32_t hi = gi + 1 == split->n_groups ? n_act : std::min(split->level_end[gi], n_act);
 			if (hi <= lo) continue;
 			const uint32_t j0 = std::min(w.n_jobs2, w.jobs2_before[lo]), j1 = std::min(w.n_jobs2, w.jobs2_before[hi]);
-			if (j1 > j0) k_scatter_accum_r<<<j1 - j0, 64 * SC_WAVES, 0, s>>>(w, gl, grads, w.chunk * 8, j0);
+			if (j1 > j0)
+				k_scatter_accum_r<<<accum_blocks(j1 - j0, w.xcd_group), 64 * SC_WAVES, 0, s>>>(w, gl, grads, w.chunk * 8, j0, j1 - j0, w.xcd_group);
 			if (split->done) split->done(lo, hi);
 			lo = hi;
 		}

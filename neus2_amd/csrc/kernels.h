@@ -118,6 +118,7 @@ struct ScatterWork {
 	uint16_t* rtab;
 	const uint4* jobs2;
 	uint32_t n_jobs2;
+	uint32_t xcd_group = 1;     // the region accumulation's jobs per XCD group (k_scatter_accum_r; 1 = list order)
 	uint32_t jobs2_before[17];  // jobs of the levels below l (l <= 16): the launch takes those up to the valid level
 	uint32_t level_groups;      // mode 2: workgroups per sample chunk, each binning levels y, y + groups, ... (0: one per level)
 };

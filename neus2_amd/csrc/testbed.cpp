@@ -628,6 +628,8 @@ struct NeusTestbed {
 			sc_jobs2.alloc(jobs2.size());
 			HIP_CHECK(hipMemcpy(sc_jobs2.p, jobs2.data(), jobs2.size() * 4, hipMemcpyHostToDevice));
 			swork.jobs2 = (const uint4*)sc_jobs2.p; swork.n_jobs2 = (uint32_t)(jobs2.size() / 4);
+			swork.xcd_group = 4;
+			if (const char* e = std::getenv("NEUS_SC_XCD_GROUP")) swork.xcd_group = std::max(1u, (uint32_t)std::strtoul(e, nullptr, 10));
 			if (sc_jobs2_before.size() > 17) throw std::runtime_error("region scatter: at most 16 levels");
 			for (size_t k = 0; k < sc_jobs2_before.size(); ++k) swork.jobs2_before[k] = sc_jobs2_before[k];
 			sc_rtab.alloc((size_t)l.L * swork.n_chunks * (SB_LEVEL_BUCKETS + 1));
