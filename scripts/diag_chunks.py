@@ -16,14 +16,13 @@ sc = scenes.sphere_scene(49, 1600, 1200, principal=(823.2 / 1600, 619.1 / 1200))
 tb = pyngp.Testbed(pyngp.TestbedMode.Nerf)
 tb.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
 tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=1 << 18, fixed_rays_per_batch=1 << 18)
-CANDS = [(32, 64, 96), (64, 128), (56, 112), (48, 96), (24, 48, 96), (32, 64), (40, 80), (32, 64, 128)]
+CANDS = [(32, 64, 96), (24, 48), (32, 64), (40, 80), (48, 96), (56, 112), (64, 128), (80, 160)]
 done = 0
 for warm in [int(x) for x in os.environ.get("STATES", "400,800,1200,1600,2400").split(",")]:
     tb.train_steps(warm - done)
     done = warm
     st = tb.stats()
-    _, cc, nsb = tb.ray_counts(1 << 18)
-    ns = nsb[0::2]  # kept samples per ray slot (0: no samples or dropped past the cap)
+    _, cc, ns = tb.ray_counts(1 << 18)  # ns: kept samples per ray slot (0: no samples or dropped past the cap)
     m = ns > 0
     ns, cc = ns[m].astype(np.int64), cc[m].astype(np.int64)
     q = np.percentile(cc, [25, 50, 75, 90, 99])
