@@ -281,8 +281,10 @@ int neus_testbed_set_training_options(NeusTestbed* tb, const NeusTrainingOptions
  * [0, e_0), [e_0, e_1), ..., [e_last, end) and a ray's next chunk only while its transmittance is >= 1e-4, so samples
  * past the cut-off (never read by the loss) are not evaluated; bit-identical to one pass. mode 0 off, 1 auto (on when
  * under 70 % of the kept samples were composited at the last loss readback; the default), 2 always. chunk_ends
- * (strictly increasing, at most 14; nullable to keep the current ones, default 32, 64, 96). A performance option
- * of this implementation (no reference counterpart: testbed_nerf.cu:3802-3811 infers every kept sample). */
+ * (strictly increasing, at most 14; nullable to keep the current ones): given, they are fixed from then on; by default
+ * they follow the training state (three rounds {e, 2e, rest}, e from the mean composited samples per ray at each loss
+ * readback). A performance option of this implementation (no reference counterpart:
+ * testbed_nerf.cu:3802-3811 infers every kept sample). */
 int neus_testbed_set_progressive_inference(NeusTestbed* tb, int mode, const uint32_t* chunk_ends, uint32_t n_ends);
 /* Per-ray counters of the last step (first n rays, host buffers, each nullable): samples requested by
  * the march, samples composited before transmittance < 1e-4, and numsteps = (compacted count, base). */

@@ -265,6 +265,19 @@ struct NeusTestbed {
 	// composited at the last loss readback), 2 always; chunk ends of the rounds before the last (march.hip)
 	int progressive_mode = 1;
 	std::vector<uint32_t> chunk_ends{32, 64, 96};  // NEUS_CHUNK_ENDS="e0,e1,..." at creation overrides (A/B of schedules)
+	// Chunk ends chosen from the training state (chunk_auto: no explicit ends given): at each loss readback the mean
+	// composited samples per ray with samples, mc (all-reduced counters: the same on every rank), sets three rounds
+	// {e, 2e, rest} with e = 0.5 mc + 12 rounded to 8 in [24, 128]. Measured at the bench workload (Config S, R = Nc =
+	// 2^18, profiles/r04fg_chunk_ends_sweep.txt, r04hi_*): step 800 (mc ~117) best at e = 64 (1.237 ms vs 1.283 for
+	// {32, 64, 96}), step 1600 (mc ~39) best at e = 32 (1.203 ms vs 1.308 for e = 64). The rounds only change which
+	// samples are evaluated, never a result (bit-identical to the one pass).
+	bool chunk_auto = true;
+	void choose_chunk_ends(uint32_t composited, uint32_t rays_with_samples) {
+		if (!chunk_auto || rays_with_samples == 0) return;
+		const float mc = (float)composited / (float)rays_with_samples;
+		const uint32_t e = std::min(128u, std::max(24u, 8u * (uint32_t)std::lround((0.5f * mc + 12.f) / 8.f)));
+		chunk_ends.assign({e, 2 * e});
+	}
 	float last_keep_ratio = 1.f;
 	static constexpr float PROGRESSIVE_RATIO = 0.7f;
 	Dev<uint32_t> chunk_list, chunk_cnt;  // chunk_cnt: [k] round k's sample list length, [16] the long-ray list's, [32 + k] open rays
@@ -455,7 +468,7 @@ struct NeusTestbed {
 			for (const char* p = e; *p;) { char* q = nullptr; const unsigned long x = std::strtoul(p, &q, 10); if (q == p) break; v.push_back((uint32_t)x); p = *q ? q + 1 : q; }
 			bool ok = !v.empty() && v.size() <= 14 && v[0] > 0;
 			for (size_t k = 1; k < v.size(); ++k) ok = ok && v[k] > v[k - 1];
-			if (ok) chunk_ends = v;
+			if (ok) { chunk_ends = v; chunk_auto = false; }
 		}
 		{ const char* e = std::getenv("NEUS_SCATTER_NOSKIP"); scatter_noskip = e && e[0] == '1'; }
 		grid_mean.alloc(4); grid_partial.alloc(GRID3 / 1024);
@@ -1431,6 +1444,7 @@ struct NeusTestbed {
 		mask_loss = pinned[2] * scale;
 		last_rays_with_samples = sst->n_rays_with_samples;
 		last_keep_ratio = sst->n_kept ? measured / (float)sst->n_kept : 1.f;  // composited / kept (progressive inference)
+		choose_chunk_ends(sst->compacted_counter, sst->n_rays_with_samples);
 		ray_loss = sst->n_rays_with_samples ? pinned[0] * (float)(sst->rays_per_batch * world) / (float)sst->n_rays_with_samples : 0.f;
 		if (!loss_ema_init) { loss_scalar_ema = last_loss; loss_ema_init = true; }
 		else loss_scalar_ema = 0.99f * loss_scalar_ema + 0.01f * last_loss;
@@ -1782,6 +1796,7 @@ int neus_testbed_set_progressive_inference(NeusTestbed* tb, int mode, const uint
 			for (uint32_t k = 0; k < n_ends; ++k)
 				if (chunk_ends[k] == 0 || (k && chunk_ends[k] <= chunk_ends[k - 1])) throw std::runtime_error("chunk ends must increase from >= 1");
 			tb->chunk_ends.assign(chunk_ends, chunk_ends + n_ends);
+			tb->chunk_auto = false;
 		}
 		tb->progressive_mode = mode;
 	});
