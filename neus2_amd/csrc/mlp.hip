@@ -332,7 +332,7 @@ __device__ __forceinline__ void level_interp(const LevelAddr& A, const uint32_t 
 			}
 	}
 }
-template <int L, bool DYDX>
+template <int L, bool DYDX, bool ALL = false>
 __device__ __forceinline__ void fused_levels(const LevelSmem& sl, uint32_t dense_bits, uint32_t valid_level, const half_t* __restrict__ grid,
                                              const float x[3], int h, h2 ev[], float dy[][2][3]) {
 	constexpr int M0 = Fused<L>::M0;
@@ -340,16 +340,20 @@ __device__ __forceinline__ void fused_levels(const LevelSmem& sl, uint32_t dense
 	uint32_t v[2][8];
 	// Level pair m (levels 2m, 2m+1) is skipped when both are beyond valid_level (kernel-uniform branch):
 	// the reference outputs zeros there without a lookup (grid.h:198-215), so no gather is issued.
+	// ALL (every level active, the caller checked): no per-level branch, and a scheduling barrier between level
+	// m+1's gathers and level m's interpolation. The branches split the unrolled loop into blocks, and the gathers were
+	// then sunk to their use after the previous level's interpolation: one exposed memory round trip per level.
 	level_addr<L>(sl, dense_bits, valid_level, x, h, 0, A[0]);
 	level_gather(grid, A[0], v[0]);
 #pragma unroll
 	for (int m = 0; m < M0; ++m) {
 		const int cur = m & 1, nxt = cur ^ 1;
-		if (m + 1 < M0 && (uint32_t)(2 * (m + 1)) <= valid_level) {
+		if (m + 1 < M0 && (ALL || (uint32_t)(2 * (m + 1)) <= valid_level)) {
 			level_addr<L>(sl, dense_bits, valid_level, x, h, m + 1, A[nxt]);
 			level_gather(grid, A[nxt], v[nxt]);
 		}
-		if (m > 0 && (uint32_t)(2 * m) > valid_level) {
+		if (ALL) __builtin_amdgcn_sched_barrier(0);
+		if (!ALL && m > 0 && (uint32_t)(2 * m) > valid_level) {
 			ev[m] = (h2){(half_t)0.f, (half_t)0.f};
 			if (DYDX)
 #pragma unroll
@@ -654,8 +658,13 @@ __device__ __forceinline__ h8 mask_frag(const f16v& acc, int k, const h8& m) {
 // (their storage precision), not fp32 tiles. n from device memory; 32 samples per wave-iteration,
 // grid-strided.
 // ------------------------------------------------------------------------------------------
-template <int L, int W, bool IDX>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) k_nerf_infer(const uint32_t* __restrict__ n_ptr, uint32_t n_fixed, const float* __restrict__ coords,
+#ifndef NEUS_INFER_ALL_WPE
+#define NEUS_INFER_ALL_WPE 2
+#endif
+// ALL: every level active (the launch checks valid_level): the gathers of level pair m+1 are pinned in flight during
+// level pair m's interpolation (fused_levels ALL); that needs more registers than 3 waves per SIMD allow without spills
+template <int L, int W, bool IDX, bool ALL = false>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ALL ? NEUS_INFER_ALL_WPE : 3, ALL ? NEUS_INFER_ALL_WPE : 3))) k_nerf_infer(const uint32_t* __restrict__ n_ptr, uint32_t n_fixed, const float* __restrict__ coords,
                                                     const GridLevels gl, uint32_t valid_level, const half_t* __restrict__ grid,
                                                     MlpPtrs wp, half_t* __restrict__ out, const uint32_t* __restrict__ idx, InferAlpha ia) {
 	constexpr int DKS = Dims<L>::DKS, DMT = Dims<L>::DMT, HALF = Fused<L>::HALF, M0 = Fused<L>::M0;
@@ -682,7 +691,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))
 		// ---- encode this lane's levels
 		h2 ev[M0];
 		float dy[M0][2][3];
-		fused_levels<L, true>(s_lvl, gl.dense_bits, valid_level, grid, x, h, ev, dy);
+		fused_levels<L, true, ALL>(s_lvl, gl.dense_bits, valid_level, grid, x, h, ev, dy);
 		__builtin_amdgcn_sched_barrier(0);  // keep the MLP's LDS weight reads out of the encode region
 		float ov[3], ovd[3][3];
 		overflow_values<L>(h, ev, ov);
@@ -1681,8 +1690,15 @@ void launch_nerf_infer(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_
 	const InferAlpha a = ia ? *ia : InferAlpha{nullptr, nullptr, 0.f, 0u, nullptr};
 	// persistent grid: at most the resident capacity (weights are staged once per block; both variants run at the
 	// same 3 waves per SIMD, amdgpu_waves_per_eu)
+	static const bool pipe = [] { const char* e = std::getenv("NEUS_INFER_PIPE"); return !(e && e[0] == '0'); }();
+	const bool all = pipe && valid_level + 1 >= L;
 #define X(l, w_) if (L == l && W == w_) { \
 		static const uint32_t cap = resident_blocks((const void*)k_nerf_infer<l, w_, false>, 256); \
+		static const uint32_t cap_all = resident_blocks((const void*)k_nerf_infer<l, w_, false, true>, 256); \
+		if (all) { \
+			if (idx) k_nerf_infer<l, w_, true, true><<<std::min(blocks, cap_all), 256, 0, s>>>(n_ptr, n_fixed, coords, gl, valid_level, grid, w, out, idx, a); \
+			else k_nerf_infer<l, w_, false, true><<<std::min(blocks, cap_all), 256, 0, s>>>(n_ptr, n_fixed, coords, gl, valid_level, grid, w, out, nullptr, a); \
+			return; } \
 		if (idx) k_nerf_infer<l, w_, true><<<std::min(blocks, cap), 256, 0, s>>>(n_ptr, n_fixed, coords, gl, valid_level, grid, w, out, idx, a); \
 		else k_nerf_infer<l, w_, false><<<std::min(blocks, cap), 256, 0, s>>>(n_ptr, n_fixed, coords, gl, valid_level, grid, w, out, nullptr, a); \
 		return; }
