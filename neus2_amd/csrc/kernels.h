@@ -284,6 +284,8 @@ struct MarchWork {
 	PcgJumpTable jt;                      /* jump-ahead of the ray generator's per-ray rng offsets */
 	unsigned long long* prof = nullptr;   /* development: per-wave phase timestamps of the march (8 per wave), or null */
 	uint32_t dbg = 0;                     /* development timing experiments (wrong results): 1 no record stores, 2 no occupancy loads */
+	uint32_t balanced = 0;                /* 8 lanes per ray on average, shared by the 8 rays of a wave by length (k_march_bal, constant-step
+	                                         march only) */
 };
 // Ray generation + the occupancy march: rays (6 f32 per slot), tstart (1 per slot), nreq (requested
 // samples per slot) and the sample runs (MarchWork).

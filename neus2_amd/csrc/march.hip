@@ -462,6 +462,221 @@ __global__ void __launch_bounds__(256) MARCH_OCC k_march(uint32_t cap_rays, uint
 	}
 }
 
+constexpr uint32_t MARCH_BAL_MAX = 16;  // lanes of one ray at most (k_march_bal)
+// Balanced lanes (MarchWork::balanced, constant-step march): a wave takes 8 consecutive ray slots and shares its 64
+// lanes among them in proportion to the mip-0 cells each crosses inside the AABB (span x (|dx| + |dy| + |dz|): one march
+// event per cell crossed), every active ray at least one lane and a ray's lanes contiguous. With 8 lanes per ray a wave
+// lasted as long as its longest ray's slices while the lanes of short, dropped and culled rays idled (lane event mean
+// 20.5 vs max 28.9 at the step-1600 state). The slices, joins and outputs are k_march's with a per-ray lane count m:
+// where a lane starts never changes a result (the join keeps only samples of the true trajectory), so the output is
+// the single-lane march's, bit for bit.
+__global__ void __launch_bounds__(256) MARCH_OCC k_march_bal(uint32_t cap_rays, uint32_t pass, uint32_t max_samples, StepState* __restrict__ st,
+                                                   DevDataset ds, const uint8_t* __restrict__ bitfield, const uint32_t* __restrict__ lin,
+                                                   const float* __restrict__ rays, const float* __restrict__ tstart, uint32_t* __restrict__ nreq,
+                                                   MarchWork mw) {
+	constexpr bool FAST = true;
+	const uint32_t est = st->march_est ? min(st->march_est, cap_rays) : cap_rays;
+	const uint32_t lo = pass == 0 ? 0u : est, hi = pass == 0 ? est : cap_rays;
+	if (lo >= hi) return;
+	if (pass == 1 && st->march_total >= max_samples) {
+		for (uint32_t k = lo + blockIdx.x * blockDim.x + threadIdx.x; k < hi; k += gridDim.x * blockDim.x) { nreq[k] = 1; mw.nrec[k] = 0; }
+		return;
+	}
+	const uint32_t lane = threadIdx.x & 63;
+	const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, n_waves = (gridDim.x * blockDim.x) >> 6;
+	uint32_t total = 0;
+	unsigned long long* pw = mw.prof ? mw.prof + (size_t)wave * 8 : nullptr;
+	bool first = true;
+	uint32_t n_redo = 0;
+	auto stamp = [&](int ph) { if (pw && first && lane == 0) pw[ph] = wall_clock64(); };
+	stamp(0);
+	for (uint32_t b = lo + 8 * wave; b < hi; b += 8 * n_waves) {
+		// ---- the group's rays on lanes 0..7: start, exit, weight
+		float t0r = -1.f, wr = 0.f;
+		if (lane < 8 && b + lane < hi) {
+			t0r = tstart[b + lane];
+			if (t0r >= 0.f) {
+				MarchRay m;
+				load_march_ray(rays, b + lane, m, ds.motion.on != 0);
+				float te = 3.402823466e+38f;
+#pragma unroll
+				for (int d = 0; d < 3; ++d) te = fminf(te, fmaxf((ds.aabb_min[d] - m.o[d]) * m.idir[d], (ds.aabb_max[d] - m.o[d]) * m.idir[d]));
+				const float span = te - t0r;
+				if (span > 0.f && span < 1e4f) wr = span * (fabsf(m.dir[0]) + fabsf(m.dir[1]) + fabsf(m.dir[2]));
+			}
+		}
+		// ---- lanes per ray (wave-uniform): 1 per active ray, the rest by weight, the remainder to the heaviest ray; at
+		// most 16 per ray (the segment scratch of a ray, MARCH_SEG_RECS runs, is split over its lanes: at 16 a lane holds
+		// 68 runs for its at most 1024 / 16 + 2 steps), lanes beyond that idle
+		uint32_t mr[8], Lr[8];
+		float W = 0.f, wmax = -1.f;
+		uint32_t n_act = 0, heavy = 0;
+		float wv[8];
+#pragma unroll
+		for (int r = 0; r < 8; ++r) {
+			wv[r] = __shfl(wr, r);
+			const bool act = __shfl(t0r, r) >= 0.f;
+			mr[r] = act ? 1u : 0u;
+			n_act += act ? 1u : 0u;
+			W += wv[r];
+			if (act && wv[r] > wmax) { wmax = wv[r]; heavy = (uint32_t)r; }
+		}
+		uint32_t used = n_act;
+		if (W > 0.f) {
+			const float extra = (float)(64u - n_act);
+#pragma unroll
+			for (int r = 0; r < 8; ++r) {
+				const uint32_t add = mr[r] ? min((uint32_t)(extra * (wv[r] / W)), MARCH_BAL_MAX - 1u) : 0u;
+				mr[r] += add;
+				used += add;
+			}
+			if (used < 64u && wv[heavy] > 0.f) { const uint32_t add = min(64u - used, MARCH_BAL_MAX - mr[heavy]); mr[heavy] += add; used += add; }
+		}
+		uint32_t acc_l = 0, maxm = 1;
+#pragma unroll
+		for (int r = 0; r < 8; ++r) { Lr[r] = acc_l; acc_l += mr[r]; maxm = max(maxm, mr[r]); }
+		// this lane's ray and segment
+		int rr = -1;
+#pragma unroll
+		for (int r = 0; r < 8; ++r) if (mr[r] && lane >= Lr[r] && lane < Lr[r] + mr[r]) rr = r;
+		const bool have = rr >= 0;
+		const uint32_t MG = have ? mr[rr] : 1u, g = have ? lane - Lr[rr] : 0u;
+		const uint32_t i = have ? b + (uint32_t)rr : b;
+		const float t0 = __shfl(t0r, have ? rr : 0);
+		MarchRay mr_{};
+		float t_exit = t0;
+		if (have && t0 >= 0.f) {
+			load_march_ray(rays, i, mr_, ds.motion.on != 0);
+			float tx[3];
+#pragma unroll
+			for (int d = 0; d < 3; ++d) {
+				const float a = (ds.aabb_min[d] - mr_.o[d]) * mr_.idir[d], c = (ds.aabb_max[d] - mr_.o[d]) * mr_.idir[d];
+				tx[d] = fmaxf(a, c);
+			}
+			t_exit = fminf(fminf(tx[0], tx[1]), tx[2]);
+		}
+		const float span = t_exit - t0;
+		const bool split = have && t0 >= 0.f && span > 0.f && span < 1e4f;
+		float t = t0;
+		uint32_t k = 0;
+		const bool active = have && t0 >= 0.f && (g == 0 || split);
+		if (active && g > 0) step_until(t, k, t0 + span * ((float)g / (float)MG), 4 * NERF_STEPS, MIN_CONE_STEPSIZE);
+		stamp(1);
+		uint32_t k_end = (uint32_t)__shfl((int)k, (int)((lane + 1) & 63));  // the next lane's start
+		if (g + 1 == MG || !split) k_end = FINISHED;
+		const uint32_t seg_cap = MARCH_SEG_RECS / MG;
+		uint2* rec = mw.seg + (size_t)i * MARCH_SEG_RECS + (size_t)g * seg_cap;
+		SegAcc acc{0.f, 0u, 0u, 0u, 0u};
+		Visits vis{};
+		vis.n = 0;
+		float et = t;
+		uint32_t ek = active ? k : FINISHED;
+		uint32_t n_ev = 0;
+		if (active) march_segment<FAST>(ds, bitfield, lin, mr_, et, ek, k_end, acc, vis, rec, seg_cap, &n_ev, mw.dbg);
+		if (__builtin_expect(__ballot(active && !((et >= 0.f) & (et < __builtin_huge_valf()))) != 0ull, 0) && lane == 0)
+			atomicOr(&st->fail_flags, STEP_FAIL_MARCH_T);
+		stamp(2);
+		// segment order: lane g joins the exit of lane g - 1 (the lanes of a ray are contiguous)
+		uint32_t vk = k;
+		for (uint32_t q = 1; q < maxm; ++q) {
+			const uint32_t pk = (uint32_t)__shfl((int)ek, (int)((lane - 1) & 63));
+			const float pt = __shfl(et, (int)((lane - 1) & 63));
+			bool redo = false;
+			if (g == q && active) {
+				if (pk == FINISHED || pk >= k_end) {
+					acc.n = 0; acc.nrec = 0; vk = pk; ek = pk; et = pt;
+				} else {
+					bool seen = false;
+#pragma unroll
+					for (int w = 0; w < VQ; ++w) seen |= (w < (int)vis.n) && pk >= vis.b[w] && pk < vis.e[w];
+					if (seen) vk = pk;
+					else redo = true;
+				}
+			}
+			if (__ballot(redo)) {
+				++n_redo;
+				if (redo) {
+					acc = SegAcc{0.f, 0u, 0u, 0u, 0u}; vis.n = 0;
+					et = pt; ek = pk; vk = pk;
+					march_segment<FAST>(ds, bitfield, lin, mr_, et, ek, k_end, acc, vis, rec, seg_cap);
+				}
+			}
+		}
+		stamp(3);
+		uint32_t n_g = 0, r_first = 0, cut = 0;
+		if (active && vk != FINISHED) {
+			for (uint32_t r = 0; r < acc.nrec; ++r) {
+				const uint2 R = rec[r];
+				const uint32_t k0 = R.y >> 8, len = R.y & 0xff;
+				if (k0 + len <= vk) { r_first = r + 1; continue; }
+				if (r == r_first && k0 < vk) { cut = vk - k0; }
+				n_g += len - (r == r_first ? cut : 0u);
+			}
+		}
+		if (!active || vk == FINISHED) { n_g = 0; r_first = acc.nrec; }
+		// prefix over the ray's lanes (in segment order) of the samples, NERF_STEPS cap
+		const uint32_t L0 = lane - g;
+		uint32_t before = 0;
+		for (uint32_t q = 0; q + 1 < maxm; ++q) {
+			const uint32_t pn = (uint32_t)__shfl((int)n_g, (int)((L0 + q) & 63));
+			if (q < g) before += pn;
+		}
+		const uint32_t keep = before >= NERF_STEPS ? 0u : min(n_g, NERF_STEPS - before);
+		uint32_t w_g = 0;
+		{
+			uint32_t got = 0;
+			for (uint32_t r = r_first; r < acc.nrec && got < keep; ++r) {
+				const uint32_t len = (rec[r].y & 0xff) - (r == r_first ? cut : 0u);
+				got += len; ++w_g;
+			}
+		}
+		uint32_t rbefore = 0, r_tot = 0;
+		for (uint32_t q = 0; q < maxm; ++q) {
+			const uint32_t pwg = (uint32_t)__shfl((int)w_g, (int)((L0 + q) & 63));
+			if (q < g) rbefore += pwg;
+			if (q < MG) r_tot += pwg;
+		}
+		stamp(4);
+		uint2* out = mw.rec + (size_t)i * NERF_STEPS;
+		uint32_t written = 0, nr = rbefore;
+		for (uint32_t r = r_first; r < acc.nrec && written < keep; ++r) {
+			const uint2 R = rec[r];
+			uint32_t len = R.y & 0xff;
+			float tr = __uint_as_float(R.x);
+			if (r == r_first && cut) {
+				for (uint32_t c = 0; c < cut; ++c) tr += MIN_CONE_STEPSIZE;
+				len -= cut;
+			}
+			len = min(len, keep - written);
+			out[nr++] = make_uint2(__float_as_uint(tr), ((before + written) << 16) | len);
+			written += len;
+		}
+		const uint32_t n_tot = (uint32_t)__shfl((int)(before + keep), (int)((L0 + MG - 1) & 63));
+		if (have && g == 0) {
+			nreq[i] = t0 >= 0.f ? n_tot : 0u;
+			mw.nrec[i] = t0 >= 0.f ? r_tot : 0u;
+			total += t0 >= 0.f ? n_tot : 0u;
+		}
+		// slots of the group without a lane (b + r < hi, no samples: t0 < 0) report 0 from lanes 0..7
+		if (lane < 8 && b + lane < hi && !(t0r >= 0.f)) { nreq[b + lane] = 0u; mw.nrec[b + lane] = 0u; }
+		if (pw && first) {
+			stamp(5);
+			uint32_t ws = g == 0 && have && t0 >= 0.f ? n_tot : 0u;
+#pragma unroll
+			for (int off = 32; off > 0; off >>= 1) ws += (uint32_t)__shfl_xor((int)ws, off);
+			uint32_t emax = n_ev, esum = n_ev;
+#pragma unroll
+			for (int off = 32; off > 0; off >>= 1) { emax = max(emax, (uint32_t)__shfl_xor((int)emax, off)); esum += (uint32_t)__shfl_xor((int)esum, off); }
+			if (lane == 0) { pw[6] = ws; pw[7] = ((unsigned long long)emax << 32) | ((unsigned long long)esum << 8) | n_redo; }
+		}
+		first = false;
+	}
+	if (pass == 0) {
+		total = wave_sum(total);
+		if (lane == 0 && total) atomicAdd(&st->march_total, total);
+	}
+}
+
 // t of local sample j of ray slot i from its runs: the run holding j, then the run's t += dt replayed
 template <bool FAST>
 __device__ __forceinline__ float run_sample_t(const MarchWork& mw, uint32_t i, uint32_t j, float cone) {
@@ -1235,6 +1450,7 @@ void launch_march_count(hipStream_t s, uint32_t cap, uint32_t max_samples, StepS
 	for (uint32_t pass = 0; pass < 2; ++pass) {
 		if (ds.cone_angle == 0.0f) {
 			if (mw.lanes_per_ray == 1) k_march<true, 1><<<blocks, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, lin, rays, tstart, nreq, mw);
+			else if (mw.lanes_per_ray == 8 && mw.balanced) k_march_bal<<<blocks * 8, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, lin, rays, tstart, nreq, mw);
 			else if (mw.lanes_per_ray == 8) k_march<true, 8><<<blocks * 8, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, lin, rays, tstart, nreq, mw);
 			else if (mw.lanes_per_ray == 16) k_march<true, 16><<<blocks * 16, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, lin, rays, tstart, nreq, mw);
 			else k_march<true, 4><<<blocks * 4, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, lin, rays, tstart, nreq, mw);

@@ -673,6 +673,7 @@ struct NeusTestbed {
 		march_rec.alloc((size_t)MAX_RAYS * NERF_STEPS); march_nrec.alloc(MAX_RAYS); march_queue.alloc(2);
 		march_seg.alloc((size_t)MAX_RAYS * MARCH_SEG_RECS);
 		mwork = MarchWork{march_rec.p, march_nrec.p, march_queue.p, march_waves(), march_seg.p, march_lanes(), jump_table()};
+		{ const char* e = std::getenv("NEUS_MARCH_BALANCE"); mwork.balanced = !(e && e[0] == '0') ? 1u : 0u; }
 		nreq.alloc(MAX_RAYS); base.alloc(MAX_RAYS);
 		numsteps.alloc(2 * (size_t)MAX_RAYS); ccount.alloc(MAX_RAYS); cbase.alloc(MAX_RAYS);
 		l_sa.alloc(max_samples); l_ekt.alloc(max_samples); sample_ray.alloc(max_samples); cmap.alloc(batch);
@@ -2238,7 +2239,8 @@ static void sample_rays_impl(NeusTestbed* tb, void* stream, uint32_t n_rays, uin
 		Dev<float> st_t; st_t.alloc(n_rays); Dev<uint32_t> nr, bs, nrec, q; nr.alloc(n_rays); bs.alloc(n_rays); nrec.alloc(n_rays); q.alloc(2);
 		Dev<uint2> rec; rec.alloc((size_t)n_rays * NERF_STEPS);
 		Dev<uint2> seg; seg.alloc((size_t)n_rays * MARCH_SEG_RECS);
-		const MarchWork mw{rec.p, nrec.p, q.p, tb->mwork.waves, seg.p, tb->mwork.lanes_per_ray};
+		MarchWork mw{rec.p, nrec.p, q.p, tb->mwork.waves, seg.p, tb->mwork.lanes_per_ray};
+		mw.balanced = tb->mwork.balanced;
 		ScanTemp tmp; const size_t tb_ = scan_temp_bytes(n_rays); tmp.alloc(tb_ + 256); scan_temp_reset(s, tmp.p);
 		Dev<uint32_t> lin; lin.alloc(LIN_WORDS);
 		launch_bitfield_linear(s, bitfield, lin.p);

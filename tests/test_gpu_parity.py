@@ -903,21 +903,25 @@ def test_marching_cubes_64bit_grid_index(torch_cuda):
 
 def test_multilane_march_equals_single_lane(env):
     """The 4-, 8- and 16-lanes-per-ray segmented march (march.hip k_march<.., MG>: lanes start at slices of the ray's step
-    sequence, join the previous segment's exit, re-march when they missed it) against the one-lane march, bit for bit
-    (rays, numsteps, coordinates, counters), on random occupancy grids from sparse to full (many empty-cell skips
-    landing across segment starts, long sample runs, the NERF_STEPS cap on the full grid) and on the training bitfield."""
+    sequence, join the previous segment's exit, re-march when they missed it) and the balanced march (k_march_bal, the
+    default: a wave's 64 lanes shared by its 8 rays by length, 1-16 per ray; "8" below, "8u" the fixed 8 lanes) against the
+    one-lane march, bit for bit (rays, numsteps, coordinates, counters), on random occupancy grids from sparse to full
+    (many empty-cell skips landing across segment starts, long sample runs, the NERF_STEPS cap on the full grid) and on
+    the training bitfield."""
     t = env["t"]
     lib, check = L()
     from neus2_amd import pyngp
     sc = env["sc"]
     tbs = {}
-    for lanes in ("1", "4", "8", "16"):
+    for key, lanes, bal in (("1", "1", "1"), ("4", "4", "1"), ("8", "8", "1"), ("8u", "8", "0"), ("16", "16", "1")):
         os.environ["NEUS_MARCH_LANES"] = lanes
+        os.environ["NEUS_MARCH_BALANCE"] = bal
         tb = pyngp.Testbed(pyngp.TestbedMode.Nerf)
         tb.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
         tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=BATCH)
-        tbs[lanes] = tb
+        tbs[key] = tb
     os.environ.pop("NEUS_MARCH_LANES", None)
+    os.environ.pop("NEUS_MARCH_BALANCE", None)
     rng = np.random.default_rng(17)
     n_rays, max_s = 8192, 8192 * 64
     bfs = [_bitfield(env)]
@@ -938,7 +942,7 @@ def test_multilane_march_equals_single_lane(env):
             out[lanes] = (host(rays, np.uint32).copy(), host(ns, np.uint32).copy(), host(co, np.uint32).copy(), tuple(cnt))
         a = out["1"]
         nk = int(a[3][1])
-        for lanes in ("4", "8", "16"):
+        for lanes in ("4", "8", "8u", "16"):
             b = out[lanes]
             assert a[3] == b[3], (k, lanes, a[3], b[3])
             np.testing.assert_array_equal(a[0], b[0])
