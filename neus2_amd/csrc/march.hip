@@ -139,8 +139,8 @@ __device__ __forceinline__ void load_march_ray(const float* __restrict__ rays, u
 // The reference marches every ray twice inside one thread (count, then write after an atomicAdd). Here the march
 // runs once and records, per ray, runs of consecutive samples {t of the first sample, count} (MarchWork); the
 // write pass rebuilds each sample's t by replaying the run's t += dt, the same float additions.
-// Work distribution: persistent waves pull ray slots from a queue and refill idle lanes as their rays finish,
-// so a wave does not wait on its longest ray (path lengths through the occupancy grid vary ~10x).
+// Work distribution: a ray's step sequence is split over several lanes (8 per ray, or k_march_bal's 1-16 by length),
+// which join in segment order (below), so a wave does not wait on one lane walking its longest ray alone.
 // FAST (cone_angle 0, constant dt): inside an occupied interior cell every further step is a sample for as long
 // as the cell index stays the same (same occupancy bit, inside the AABB, mip 0), so the run continues on the
 // position and cell index alone (no bitfield read, no store per sample). Cells with an index 0 / 127 (a position
