@@ -1,4 +1,4 @@
-"""The single-pass exclusive scan (scan.hip: decoupled look-back, ticketed tiles, epoch-tagged state) that every
+"""The single-pass exclusive scan (scan.hip: decoupled look-back, tile = blockIdx.x (in-order dispatch), epoch-tagged state) that every
 deterministic compaction of the step runs on (the march's sample bases, the progressive rounds' chunk lists, the loss
 compaction, the scatter's bucket x block slots), against numpy's cumsum: exact for ragged sizes around the 4096-element
 tile, look-back windows longer than one wave (> 64 tiles), counts near the u32 range, aligned and unaligned buffers,
