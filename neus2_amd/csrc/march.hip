@@ -170,8 +170,12 @@ __device__ __forceinline__ void mip0_cell(const float pos[3], int c[3]) {  // ca
 constexpr int VQ = 4;
 struct Visits { uint32_t b[VQ], e[VQ]; uint32_t n; };
 __device__ __forceinline__ void visit(Visits& v, uint32_t kb, uint32_t ke) {
+	// (branch, not selects: past its first VQ events a lane records nothing, and a wave whose lanes all are past them
+	// skips the ~40 select instructions per event)
+	if (v.n < (uint32_t)VQ) {
 #pragma unroll
-	for (int q = 0; q < VQ; ++q) if (v.n == (uint32_t)q) { v.b[q] = kb; v.e[q] = ke; }
+		for (int q = 0; q < VQ; ++q) if (v.n == (uint32_t)q) { v.b[q] = kb; v.e[q] = ke; }
+	}
 	++v.n;
 }
 
