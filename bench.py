@@ -355,6 +355,7 @@ def main():
         # gathers each move a 128-B line from the Infinity Cache, so this, not the algorithmic rate, is what binds
         "line_traffic": line_traffic(measured_traffic(dom, levels), dk["ms"], dk["bytes"]),
         "progressive_steps_timed": d["progressive"],
+        "progressive_chunk_end": st["progressive_chunk_end"],
         "non_rollover_fraction": round(d["trained_real"] / max(1, batch * args.steps), 4),
         "kernels": kern,
         "loss": st["ray_loss"],

@@ -127,7 +127,8 @@ typedef struct NeusTrainStats {
 	                                           * rounds' work lists, a subset of the kept samples) */
 	uint64_t progressive_steps;               /* steps that ran progressive (multi-round) inference */
 	uint32_t evaluated_samples_last;          /* samples the last step's pre-compaction pass evaluated */
-	uint32_t reserved_;
+	uint32_t progressive_chunk_end;           /* end of the progressive inference's first chunk (the rounds are [0, e), [e, 2e), ...
+	                                           * by default; neus_testbed_set_progressive_inference) */
 } NeusTrainStats;
 
 /* Testbed::render_to_cpu (python_api.cu:123-169) after set_camera_to_training_view (testbed.cu:264-270). */

@@ -48,7 +48,7 @@ class NeusTrainStats(C.Structure):
         ("training_aborted", C.c_uint32), ("pre_samples_total", C.c_uint64), ("rays_total", C.c_uint64),
         ("occ_samples_total", C.c_uint64), ("occ_updates", C.c_uint32), ("health_flags", C.c_uint32),
         ("evaluated_samples_total", C.c_uint64), ("progressive_steps", C.c_uint64), ("evaluated_samples_last", C.c_uint32),
-        ("reserved_", C.c_uint32),
+        ("progressive_chunk_end", C.c_uint32),
     ]
 
 

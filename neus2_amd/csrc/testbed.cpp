@@ -1533,7 +1533,8 @@ int neus_testbed_get_stats(NeusTestbed* tb, NeusTrainStats* o) {
 		o->nonfinite_loss = tb->nonfinite ? 1u : 0u;
 		o->training_aborted = (tb->aborted || (tb->training_step > 0 && s.zero_records)) ? 1u : 0u;
 		o->pre_samples_total = s.pre_total; o->rays_total = s.rays_total;
-		o->occ_samples_total = tb->occ_samples; o->occ_updates = tb->occ_updates; o->reserved_ = 0;
+		o->occ_samples_total = tb->occ_samples; o->occ_updates = tb->occ_updates;
+		o->progressive_chunk_end = tb->chunk_ends.empty() ? 0u : tb->chunk_ends[0];
 		o->health_flags = s.fail_flags | tb->fail_seen | (scan_failures(tb->scan_tmp.p) ? STEP_FAIL_SCAN : 0u);
 		o->evaluated_samples_total = s.eval_total; o->progressive_steps = s.prog_steps; o->evaluated_samples_last = s.eval_last;
 	});
