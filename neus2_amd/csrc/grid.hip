@@ -34,71 +34,38 @@ __global__ void __launch_bounds__(256) k_grid_encode(
 	const uint32_t l = blockIdx.y;
 	const half_t* gp = grid + (size_t)gl.offset[l] * 2;
 	const uint32_t n_in = ro.n_in_ptr ? min(*ro.n_in_ptr, ro.n_elements) : 0xffffffffu;
-	const uint32_t stride = gridDim.x * blockDim.x;
-	// two samples per thread and pass (i, i + stride), their loads issued together: each sample is two dependent memory
-	// round trips (coordinates, then the corners), so pairing them halves the exposed latency per sample
-	for (uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += 2 * stride) {
-		uint32_t ii[2] = {i0, i0 + stride}, src[2];
-		bool have[2];
+	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+		const uint32_t src = i < n_in ? i : i % n_in;  // (n_in > 0 whenever n > 0: n_train is 0 without records)
+		if (l == 0 && i != src) {
+			// rows i >= n_in are written, rows src < n_in read: the const input view and ro.coords never meet on an element
+			for (uint32_t k = 0; k < coord_stride; ++k) ro.coords[(size_t)i * coord_stride + k] = coords[(size_t)src * coord_stride + k];
 #pragma unroll
-		for (int q = 0; q < 2; ++q) {
-			have[q] = ii[q] < n;
-			src[q] = !have[q] ? 0u : (ii[q] < n_in ? ii[q] : ii[q] % n_in);  // (n_in > 0 whenever n > 0: n_train is 0 without records)
-		}
-		if (l == 0) {
-#pragma unroll
-			for (int q = 0; q < 2; ++q) {
-				const uint32_t i = ii[q], s0 = src[q];
-				if (!have[q] || i == s0) continue;
-				// rows i >= n_in are written, rows src < n_in read: the const input view and ro.coords never meet on an element
-				for (uint32_t k = 0; k < coord_stride; ++k) ro.coords[(size_t)i * coord_stride + k] = coords[(size_t)s0 * coord_stride + k];
-#pragma unroll
-				for (int k = 0; k < OUT_W; ++k) {
-					const float r = (float)ro.dL_dout[(size_t)s0 * OUT_W + k];
-					ro.dL_dout[(size_t)i * OUT_W + k] = (half_t)(r * n_in / ro.n_elements);
-				}
+			for (int k = 0; k < OUT_W; ++k) {
+				const float r = (float)ro.dL_dout[(size_t)src * OUT_W + k];
+				ro.dL_dout[(size_t)i * OUT_W + k] = (half_t)(r * n_in / ro.n_elements);
 			}
 		}
 		if (l > valid_level) {
+			enc[(size_t)l * ld + i] = 0u;
+			if (dydx) {
 #pragma unroll
-			for (int q = 0; q < 2; ++q) {
-				if (!have[q]) continue;
-				enc[(size_t)l * ld + ii[q]] = 0u;
-				if (dydx) {
-#pragma unroll
-					for (int k = 0; k < 6; ++k) dydx[(size_t)(6 * l + k) * ld + ii[q]] = 0.0f;
-				}
+				for (int k = 0; k < 6; ++k) dydx[(size_t)(6 * l + k) * ld + i] = 0.0f;
 			}
 			continue;
 		}
-		float cx[2][3];
+		const float* c = coords + (size_t)src * coord_stride;
+		LevelSetup s = level_setup(gl, l, c[0], c[1], c[2]);
+		h2 v[8];
+		gather_corners(s, gp, v);
+		const h2 out = interp_features(s, v);
+		enc[(size_t)l * ld + i] = *(const uint32_t*)&out;
+		if (dydx) {
+			float gr[2][3];
+			interp_dydx(s, v, gr);
 #pragma unroll
-		for (int q = 0; q < 2; ++q) {
-			const float* c = coords + (size_t)src[q] * coord_stride;
+			for (int f = 0; f < 2; ++f)
 #pragma unroll
-			for (int d = 0; d < 3; ++d) cx[q][d] = c[d];
-		}
-		LevelSetup s[2];
-		h2 v[2][8];
-#pragma unroll
-		for (int q = 0; q < 2; ++q) {
-			s[q] = level_setup(gl, l, cx[q][0], cx[q][1], cx[q][2]);
-			gather_corners(s[q], gp, v[q]);
-		}
-#pragma unroll
-		for (int q = 0; q < 2; ++q) {
-			if (!have[q]) continue;
-			const uint32_t i = ii[q];
-			const h2 out = interp_features(s[q], v[q]);
-			enc[(size_t)l * ld + i] = *(const uint32_t*)&out;
-			if (dydx) {
-				float gr[2][3];
-				interp_dydx(s[q], v[q], gr);
-#pragma unroll
-				for (int f = 0; f < 2; ++f)
-#pragma unroll
-					for (int d = 0; d < 3; ++d) dydx[(size_t)(6 * l + 3 * f + d) * ld + i] = gr[f][d];
-			}
+				for (int d = 0; d < 3; ++d) dydx[(size_t)(6 * l + 3 * f + d) * ld + i] = gr[f][d];
 		}
 	}
 }

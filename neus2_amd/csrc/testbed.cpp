@@ -842,7 +842,7 @@ struct NeusTestbed {
 	// ------------------------------------------------------------ network stages
 	void encode(const uint32_t* n_ptr, uint32_t n_fixed, uint32_t n_cap, uint32_t ld, const float* c, uint32_t stride, uint32_t valid, bool want_dydx, hipStream_t s,
 	            const EncodeRollover* ro = nullptr) {
-		const uint32_t gx = std::max<uint32_t>(1, std::min<uint32_t>((n_cap + 511) / 512, 2048));  // (two samples per thread and pass)
+		const uint32_t gx = std::max<uint32_t>(1, std::min<uint32_t>((n_cap + 255) / 256, 2048));
 		launch_grid_encode(s, n_ptr, n_fixed, ld, c, stride, gl, valid, params_h.p + lay.grid_off, enc.p, want_dydx ? dydx.p : nullptr, gx, ro);
 	}
 	void net_forward(const uint32_t* n_ptr, uint32_t n_fixed, uint32_t n_cap, const float* c, uint32_t valid, half_t* out, hipStream_t s) {
