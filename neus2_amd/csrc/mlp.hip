@@ -832,9 +832,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ALL ? 
 //         DeltaNetwork first: x' = R (x + t), as k_delta_apply.
 struct UniformGrid { uint32_t res[3]; float inv_res[3], rmin[3], rdiag[3], tmin[3], tdiag[3]; uint64_t offset; const DeltaState* delta; };
 
-// ALL: the all-levels gather pipeline (fused_levels ALL) at 3 waves per SIMD (4 would spill)
-template <int L, int W, int MODE, bool ALL = false>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ALL ? 3 : 1))) k_nerf_density(uint32_t n, const float* __restrict__ pos, const UniformGrid ug, const OccSampling os,
+template <int L, int W, int MODE>
+__global__ void __launch_bounds__(256) k_nerf_density(uint32_t n, const float* __restrict__ pos, const UniformGrid ug, const OccSampling os,
                                                       const GridLevels gl, uint32_t valid_level, const half_t* __restrict__ grid, MlpPtrs wp,
                                                       float* __restrict__ density) {
 	constexpr int DKS = Dims<L>::DKS, M0 = Fused<L>::M0, MT = (W + 31) / 32, HKS = W / 16;
@@ -887,7 +886,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ALL ? 
 		}
 		h2 ev[M0];
 		float dy[1][2][3];
-		fused_levels<L, false, ALL>(s_lvl, gl.dense_bits, valid_level, grid, x, h, ev, dy);
+		fused_levels<L, false>(s_lvl, gl.dense_bits, valid_level, grid, x, h, ev, dy);
 		float ov[3];
 		overflow_values<L>(h, ev, ov);
 		const float xm[3] = {rh(rh(x[0]) - 0.5f), rh(rh(x[1]) - 0.5f), rh(rh(x[2]) - 0.5f)};
@@ -1685,15 +1684,14 @@ bool mlp_supported(uint32_t L, uint32_t W) {
 	return false;
 }
 
-// the all-levels instantiations of the fused encode (fused_levels ALL) unless NEUS_INFER_PIPE=0
-static bool infer_pipe() { static const bool on = [] { const char* e = std::getenv("NEUS_INFER_PIPE"); return !(e && e[0] == '0'); }(); return on; }
 void launch_nerf_infer(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_ptr, uint32_t n_fixed, const float* coords, const GridLevels& gl,
                        uint32_t valid_level, const half_t* grid, const MlpPtrs& w, half_t* out, uint32_t blocks, const uint32_t* idx,
                        const InferAlpha* ia) {
 	const InferAlpha a = ia ? *ia : InferAlpha{nullptr, nullptr, 0.f, 0u, nullptr};
 	// persistent grid: at most the resident capacity (weights are staged once per block; both variants run at the
 	// same 3 waves per SIMD, amdgpu_waves_per_eu)
-	const bool all = infer_pipe() && valid_level + 1 >= L;
+	static const bool pipe = [] { const char* e = std::getenv("NEUS_INFER_PIPE"); return !(e && e[0] == '0'); }();
+	const bool all = pipe && valid_level + 1 >= L;
 #define X(l, w_) if (L == l && W == w_) { \
 		static const uint32_t cap = resident_blocks((const void*)k_nerf_infer<l, w_, false>, 256); \
 		static const uint32_t cap_all = resident_blocks((const void*)k_nerf_infer<l, w_, false, true>, 256); \
@@ -1711,10 +1709,7 @@ void launch_nerf_density(hipStream_t s, uint32_t L, uint32_t W, uint32_t n, cons
                          const half_t* grid, const MlpPtrs& w, float* density) {
 	const uint32_t blocks = std::min<uint32_t>((n + 127) / 128, 8192);
 	if (n == 0) return;
-#define X(l, w_) if (L == l && W == w_) { \
-		if (infer_pipe() && valid_level + 1 >= L) k_nerf_density<l, w_, 0, true><<<blocks, 256, 0, s>>>(n, pos, UniformGrid{}, OccSampling{}, gl, valid_level, grid, w, density); \
-		else k_nerf_density<l, w_, 0><<<blocks, 256, 0, s>>>(n, pos, UniformGrid{}, OccSampling{}, gl, valid_level, grid, w, density); \
-		return; }
+#define X(l, w_) if (L == l && W == w_) { k_nerf_density<l, w_, 0><<<blocks, 256, 0, s>>>(n, pos, UniformGrid{}, OccSampling{}, gl, valid_level, grid, w, density); return; }
 	NEUS_MLP_CONFIGS(X)
 #undef X
 }
@@ -1757,10 +1752,7 @@ void launch_occ_density(hipStream_t s, uint32_t L, uint32_t W, uint32_t n, const
                         const half_t* grid, const MlpPtrs& w) {
 	const uint32_t blocks = std::min<uint32_t>((n + 127) / 128, 8192);
 	if (n == 0) return;
-#define X(l, w_) if (L == l && W == w_) { \
-		if (infer_pipe() && valid_level + 1 >= L) k_nerf_density<l, w_, 2, true><<<blocks, 256, 0, s>>>(n, nullptr, UniformGrid{}, os, gl, valid_level, grid, w, nullptr); \
-		else k_nerf_density<l, w_, 2><<<blocks, 256, 0, s>>>(n, nullptr, UniformGrid{}, os, gl, valid_level, grid, w, nullptr); \
-		return; }
+#define X(l, w_) if (L == l && W == w_) { k_nerf_density<l, w_, 2><<<blocks, 256, 0, s>>>(n, nullptr, UniformGrid{}, os, gl, valid_level, grid, w, nullptr); return; }
 	NEUS_MLP_CONFIGS(X)
 #undef X
 }
@@ -1777,10 +1769,7 @@ void launch_sdf_grid(hipStream_t s, uint32_t L, uint32_t W, const uint32_t res[3
 	}
 	ug.offset = offset;
 	const uint32_t blocks = std::min<uint32_t>((n + 127) / 128, 16384);
-#define X(l, w_) if (L == l && W == w_) { \
-		if (infer_pipe() && valid_level + 1 >= L) k_nerf_density<l, w_, 1, true><<<blocks, 256, 0, s>>>(n, nullptr, ug, OccSampling{}, gl, valid_level, grid, w, sdf); \
-		else k_nerf_density<l, w_, 1><<<blocks, 256, 0, s>>>(n, nullptr, ug, OccSampling{}, gl, valid_level, grid, w, sdf); \
-		return; }
+#define X(l, w_) if (L == l && W == w_) { k_nerf_density<l, w_, 1><<<blocks, 256, 0, s>>>(n, nullptr, ug, OccSampling{}, gl, valid_level, grid, w, sdf); return; }
 	NEUS_MLP_CONFIGS(X)
 #undef X
 }
