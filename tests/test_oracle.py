@@ -407,3 +407,24 @@ def test_mc_edge_cases():
     V, F = O.marching_cubes(d, 0.0)
     assert len(V) == 3 and len(F) == 1
     np.testing.assert_allclose(sorted(map(tuple, V)), sorted([(0.25, 0, 0), (0, 0.25, 0), (0, 0, 0.25)]), atol=1e-7)
+
+
+def test_oracle_sum_order_switch():
+    """or_set_sum_order (the all-levels parity test's noise floor): the reversed summation order moves the fp16 outputs
+    by at most a few ulps, and switching back restores the index-order results bit for bit."""
+    cfg = O.make_cfg(n_levels=4, log2_hashmap_size=12, base_resolution=8, per_level_scale=2.0)
+    lay = O.layout(cfg)
+    rng = np.random.default_rng(5)
+    p = O.init_params(cfg)
+    p[lay["grid_off"]:lay["var_off"]] = rng.uniform(-0.1, 0.1, lay["n_grid_params"])
+    c = _coords(512, seed=2)
+    a = O.network_forward(cfg, p, c, 4)
+    try:
+        O.set_sum_order(True)
+        b = O.network_forward(cfg, p, c, 4)
+    finally:
+        O.set_sum_order(False)
+    a2 = O.network_forward(cfg, p, c, 4)
+    np.testing.assert_array_equal(a, a2)
+    fa, fb = a.view(np.float16).astype(np.float64), b.view(np.float16).astype(np.float64)
+    assert np.abs(fa - fb).max() <= 1e-2 * max(1.0, np.abs(fa).max())
