@@ -166,17 +166,18 @@ __device__ __forceinline__ void mip0_cell(const float pos[3], int c[3]) {  // ca
 #pragma unroll
 	for (int d = 0; d < 3; ++d) c[d] = clampi((int)(((pos[d] - 0.5f) + 0.5f) * NERF_GRIDSIZE), 0, NERF_GRIDSIZE - 1);
 }
-// the first VQ event intervals [k_first, k_after) of a segment (the visited steps where the true trajectory may join)
-constexpr int VQ = 4;
-struct Visits { uint32_t b[VQ], e[VQ]; uint32_t n; };
+// the visited steps k0 .. k0 + 63 of a segment as bits (where the true trajectory may join it; a join further on
+// is not seen and re-marches, which costs time, never a result). One event marks [kb, ke): a few instructions on
+// both paths of the event where the first-events list it replaces took ~40 (a select chain under a branch).
+struct Visits { unsigned long long m; uint32_t k0; };
 __device__ __forceinline__ void visit(Visits& v, uint32_t kb, uint32_t ke) {
-	// (branch, not selects: past its first VQ events a lane records nothing, and a wave whose lanes all are past them
-	// skips the ~40 select instructions per event)
-	if (v.n < (uint32_t)VQ) {
-#pragma unroll
-		for (int q = 0; q < VQ; ++q) if (v.n == (uint32_t)q) { v.b[q] = kb; v.e[q] = ke; }
-	}
-	++v.n;
+	const uint32_t a = kb - v.k0, n = ke - kb;   // kb >= k0, n >= 1
+	const unsigned long long run = n >= 64u ? ~0ull : (1ull << n) - 1ull;
+	v.m |= a < 64u ? run << a : 0ull;
+}
+__device__ __forceinline__ bool visited(const Visits& v, uint32_t k) {
+	const uint32_t a = k - v.k0;
+	return a < 64u && ((v.m >> a) & 1ull);
 }
 
 template <bool FAST>
@@ -231,8 +232,13 @@ __device__ __forceinline__ bool march_event(const DevDataset& ds, const uint8_t*
 		const float t_target = t + fmaxf(ldexpf(tn, -(int)(7 - mip)), 0.0f);
 		t += MIN_CONE_STEPSIZE; ++k;
 		// do { t += dt; ++k; } while (t < t_target); bounded: at cone angle 0 the box diagonal is NERF_STEPS steps, so
-		// no skip spans 4 NERF_STEPS and the bound only ends a corrupted t (the ray is ended, the step reports it)
-		if (!step_until(t, k, t_target, k + 4 * NERF_STEPS, MIN_CONE_STEPSIZE)) return false;
+		// no skip spans 4 NERF_STEPS and the bound only ends a corrupted t (the ray is ended, the step reports it).
+		// A mip-0 skip (to the next cell boundary, <= sqrt(3) / 128 away) spans at most 8 steps: plain steps first (the
+		// loop itself), the exact integer-domain jump (two divisions) only for what remains (mip >= 1 skips)
+#pragma unroll
+		for (int s = 0; s < 8; ++s)
+			if (t < t_target) { t += MIN_CONE_STEPSIZE; ++k; }
+		if (t < t_target && !step_until(t, k, t_target, k + 4 * NERF_STEPS, MIN_CONE_STEPSIZE)) return false;
 		return true;
 	} else {
 		float dt, pos[3];
@@ -352,8 +358,7 @@ __global__ void __launch_bounds__(256) MARCH_OCC k_march(uint32_t cap_rays, uint
 		if (g == MG - 1 || !split) k_end = FINISHED;
 		uint2* rec = mw.seg + ((size_t)i * MG + g) * SEG_CAP;
 		SegAcc acc{0.f, 0u, 0u, 0u, 0u};
-		Visits vis{};
-		vis.n = 0;
+		Visits vis{0ull, k};
 		float et = t;
 		uint32_t ek = active ? k : FINISHED;
 		uint32_t n_ev = 0;
@@ -372,17 +377,14 @@ __global__ void __launch_bounds__(256) MARCH_OCC k_march(uint32_t cap_rays, uint
 				if (pk == FINISHED || pk >= k_end) {  // the ray ended (or jumped past this segment) before it
 					acc.n = 0; acc.nrec = 0; vk = pk; ek = pk; et = pt;
 				} else {
-					bool seen = false;
-#pragma unroll
-					for (int w = 0; w < VQ; ++w) seen |= (w < (int)vis.n) && pk >= vis.b[w] && pk < vis.e[w];
-					if (seen) vk = pk;
+					if (visited(vis, pk)) vk = pk;
 					else redo = true;
 				}
 			}
 			if (__ballot(redo)) {
 				++n_redo;
 				if (redo) {
-					acc = SegAcc{0.f, 0u, 0u, 0u, 0u}; vis.n = 0;
+					acc = SegAcc{0.f, 0u, 0u, 0u, 0u}; vis = Visits{0ull, pk};
 					et = pt; ek = pk; vk = pk;
 					march_segment<FAST>(ds, bitfield, lin, mr, et, ek, k_end, acc, vis, rec, SEG_CAP);
 				}
@@ -571,8 +573,7 @@ __global__ void __launch_bounds__(256) MARCH_OCC k_march_bal(uint32_t cap_rays, 
 		const uint32_t seg_cap = MARCH_SEG_RECS / MG;
 		uint2* rec = mw.seg + (size_t)i * MARCH_SEG_RECS + (size_t)g * seg_cap;
 		SegAcc acc{0.f, 0u, 0u, 0u, 0u};
-		Visits vis{};
-		vis.n = 0;
+		Visits vis{0ull, k};
 		float et = t;
 		uint32_t ek = active ? k : FINISHED;
 		uint32_t n_ev = 0;
@@ -590,17 +591,14 @@ __global__ void __launch_bounds__(256) MARCH_OCC k_march_bal(uint32_t cap_rays, 
 				if (pk == FINISHED || pk >= k_end) {
 					acc.n = 0; acc.nrec = 0; vk = pk; ek = pk; et = pt;
 				} else {
-					bool seen = false;
-#pragma unroll
-					for (int w = 0; w < VQ; ++w) seen |= (w < (int)vis.n) && pk >= vis.b[w] && pk < vis.e[w];
-					if (seen) vk = pk;
+					if (visited(vis, pk)) vk = pk;
 					else redo = true;
 				}
 			}
 			if (__ballot(redo)) {
 				++n_redo;
 				if (redo) {
-					acc = SegAcc{0.f, 0u, 0u, 0u, 0u}; vis.n = 0;
+					acc = SegAcc{0.f, 0u, 0u, 0u, 0u}; vis = Visits{0ull, pk};
 					et = pt; ek = pk; vk = pk;
 					march_segment<FAST>(ds, bitfield, lin, mr_, et, ek, k_end, acc, vis, rec, seg_cap);
 				}
