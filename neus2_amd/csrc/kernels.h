@@ -198,7 +198,10 @@ void mlp_din_permutation(uint32_t L, int32_t* perm /* DIN entries: physical row 
 // the loss's alpha pass fused into the inference epilogue (k_loss_alpha's per-sample terms of every evaluated sample):
 // sa / ekt of LossWork, the cosine anneal, dt_const (cone angle 0: every record's dt is the constant step) and the
 // long-ray counter to zero (nullable)
-struct InferAlpha { float4* sa; float* ekt; float cos_anneal; uint32_t dt_const; uint32_t* n_long; };
+struct InferAlpha {
+	float4* sa; float* ekt; float cos_anneal; uint32_t dt_const; uint32_t* n_long;
+	uint32_t xcd_parts = 0;  // 8: the work items cut into 8 contiguous parts, part x run by the blocks of XCD x (blockIdx mod 8)
+};
 void launch_nerf_infer(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_ptr, uint32_t n_fixed, const float* coords, const GridLevels& gl,
                        uint32_t valid_level, const half_t* grid, const MlpPtrs& w, half_t* out, uint32_t blocks,
                        const uint32_t* idx = nullptr /* work item j -> sample idx[j] (progressive-inference rounds) */, const InferAlpha* ia = nullptr);
@@ -296,6 +299,15 @@ void launch_march_count(hipStream_t s, uint32_t cap, uint32_t max_samples /* glo
 // Progressive round 0's work list, written by the march (the first min(n, e1) samples of every kept ray at the
 // exclusive scan c0 of those counts); counters[0] = its length, counters[1 .. n_counters) zeroed for the later rounds.
 struct Round0List { uint32_t e1; uint32_t* c0; uint32_t* list; uint32_t* counters; uint32_t n_counters; };
+// Spatial ray order of the progressive rounds (march.hip k_ray_hist, a scan, k_ray_sort_place): hist and off are
+// [2][RS_BINS + 1][ray_sort_blocks(cap)] (per block of slots: ray count and round-0 chunk samples per 8^3 Morton cell;
+// bin RS_BINS = slots without kept samples) and its exclusive scan; key [cap] per ray slot; perm [cap] the slots in
+// order, *n_perm of them
+constexpr uint32_t RS_BINS = 512;
+struct RaySort { uint32_t* hist; uint32_t* off; uint16_t* key; uint32_t* perm; uint32_t* n_perm; };
+uint32_t ray_sort_blocks(uint32_t cap);
+void launch_ray_sort(hipStream_t s, uint32_t cap, const uint32_t* numsteps, const float* coords, uint32_t e1, const RaySort& rs, uint32_t* list,
+                     uint32_t* list_len, void* scan_temp, size_t scan_temp_bytes);
 // k_march_scan (the scan of the requested counts fused with numsteps, scan_temp = a scan_temp_bytes buffer) and
 // k_march_write; round0 nullable
 void launch_march_write(hipStream_t s, uint32_t cap, StepState* st, const DevDataset& ds, const float* rays, const MarchWork& mw, const uint32_t* nreq,

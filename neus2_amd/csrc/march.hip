@@ -866,6 +866,104 @@ __global__ void __launch_bounds__(256) k_march_write(uint32_t cap_rays, StepStat
 	}
 }
 
+// ---------------------------------------------------------------- spatial ray order (progressive rounds)
+// k_nerf_infer's hash-grid gathers miss an XCD's 4 MB L2 on a list in ray-slot order (random pixels of random views:
+// every wave touches the whole surface). With round 0's list in Morton order of 8^3 cells of each ray's first kept
+// sample, and the rays in that order through k_loss_scan_chunk (so later rounds' lists follow it), the inference takes
+// the list as 8 contiguous eighths, eighth x on XCD x (InferAlpha::xcd_parts): each XCD gathers from one eighth of the
+// surface. A counting sort over the ray slots in RS_RPB-slot blocks: per-block LDS histograms into a [2][bin][block]
+// matrix, one device-wide exclusive scan of it (scan.hip), placement with LDS cursors (global per-ray atomics on the
+// ~300 rays of an occupied cell serialised at the memory side: ~50 us). Order within a cell is immaterial (every work
+// item writes its own sample's slots, every ray's recurrence is its own), so results are unchanged.
+constexpr uint32_t RS_RPB = 1024, RS_NB = RS_BINS + 1;
+__device__ __forceinline__ uint32_t spread4(uint32_t v) {
+	v &= 15u;
+	v = (v | (v << 4)) & 0x0C3u;
+	return (v | (v << 2)) & 0x249u;
+}
+__device__ __forceinline__ uint32_t ray_cell_key(const float* __restrict__ c) {  // Morton index of the 8^3 cell
+	uint32_t k = 0;
+#pragma unroll
+	for (int d = 0; d < 3; ++d) k |= spread4((uint32_t)clampi((int)(c[d] * 8.0f), 0, 7)) << d;
+	return k;
+}
+// block b, slots [b RS_RPB, (b + 1) RS_RPB), one per thread: per slot with kept samples its cell (first kept sample);
+// the block's ray count and round-0 chunk samples per cell (bin RS_BINS: slots without samples) -> hist [2][RS_NB][nblk]
+__global__ void __launch_bounds__(RS_RPB) k_ray_hist(uint32_t cap, const uint32_t* __restrict__ numsteps, const float* __restrict__ coords,
+                                                     uint32_t e1, RaySort rs) {
+	__shared__ uint32_t h[2][RS_NB];
+	const uint32_t nblk = gridDim.x, blk = blockIdx.x, t = threadIdx.x;
+	for (uint32_t b = t; b < 2 * RS_NB; b += RS_RPB) (&h[0][0])[b] = 0u;
+	__syncthreads();
+	const uint32_t i = blk * RS_RPB + t;
+	const bool in = i < cap;
+	const uint32_t ns = in ? numsteps[2 * i] : 0u;
+	if (ns) {
+		const uint32_t key = ray_cell_key(coords + (size_t)numsteps[2 * i + 1] * COORD_W);
+		rs.key[i] = (uint16_t)key;
+		atomicAdd(&h[0][key], 1u);
+		atomicAdd(&h[1][key], min(ns, e1));
+	}
+	const unsigned long long m = __ballot(in && !ns);
+	if ((t & 63) == 0 && m) atomicAdd(&h[0][RS_BINS], (uint32_t)__popcll(m));
+	__syncthreads();
+	for (uint32_t b = t; b < RS_NB; b += RS_RPB) {
+		rs.hist[(size_t)b * nblk + blk] = h[0][b];
+		rs.hist[((size_t)RS_NB + b) * nblk + blk] = h[1][b];
+	}
+}
+// each slot to its place in the order (LDS cursors from the scanned matrix); a ray with samples also writes its round-0
+// chunk [0, min(n, e1)) into its cell's part of the list, each wave's chunks written lane-contiguously. Block 0 writes
+// the ordered slot count and the round-0 list length.
+__global__ void __launch_bounds__(RS_RPB) k_ray_sort_place(uint32_t cap, const uint32_t* __restrict__ numsteps, uint32_t e1, RaySort rs,
+                                                           uint32_t* __restrict__ list, uint32_t* __restrict__ list_len) {
+	__shared__ uint32_t cur[2][RS_NB];
+	__shared__ uint32_t s_pre[RS_RPB / 64][64], s_dst[RS_RPB / 64][64], s_src[RS_RPB / 64][64];
+	const uint32_t nblk = gridDim.x, blk = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+	const size_t n = 2 * (size_t)RS_NB * nblk, h1 = (size_t)RS_NB * nblk;
+	const uint32_t h0_total = rs.off[h1];  // every slot (h0 counts them all)
+	for (uint32_t b = t; b < RS_NB; b += RS_RPB) {
+		cur[0][b] = rs.off[(size_t)b * nblk + blk];
+		cur[1][b] = rs.off[h1 + (size_t)b * nblk + blk] - h0_total;
+	}
+	if (blk == 0 && t == 0) { *rs.n_perm = h0_total; *list_len = rs.off[n - 1] + rs.hist[n - 1] - h0_total; }
+	__syncthreads();
+	const uint32_t i = blk * RS_RPB + t;
+	const bool in = i < cap;
+	const uint32_t ns = in ? numsteps[2 * i] : 0u, base = in ? numsteps[2 * i + 1] : 0u;
+	uint32_t w = 0, dst = 0;
+	if (ns) {
+		const uint32_t key = rs.key[i];
+		rs.perm[atomicAdd(&cur[0][key], 1u)] = i;
+		w = min(ns, e1);
+		dst = atomicAdd(&cur[1][key], w);
+	}
+	const unsigned long long m = __ballot(in && !ns);
+	if (m) {
+		uint32_t p0 = 0;
+		if (lane == 0) p0 = atomicAdd(&cur[0][RS_BINS], (uint32_t)__popcll(m));
+		p0 = wave_lane_value(p0, 0);
+		if (in && !ns) rs.perm[p0 + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = i;
+	}
+	const uint32_t incl = wave_incl_sum(w), total = wave_lane_value(incl, 63);
+	s_pre[wv][lane] = incl - w; s_dst[wv][lane] = dst; s_src[wv][lane] = base;
+	__builtin_amdgcn_wave_barrier();
+	for (uint32_t r = lane; r < total; r += 64) {
+		uint32_t o = 0;  // the last lane whose chunk starts at or before r (zero-length lanes share its start)
+#pragma unroll
+		for (uint32_t step = 32; step > 0; step >>= 1) if (s_pre[wv][o + step] <= r) o += step;
+		list[s_dst[wv][o] + (r - s_pre[wv][o])] = s_src[wv][o] + (r - s_pre[wv][o]);
+	}
+}
+uint32_t ray_sort_blocks(uint32_t cap) { return std::max<uint32_t>(1, (cap + RS_RPB - 1) / RS_RPB); }
+void launch_ray_sort(hipStream_t s, uint32_t cap, const uint32_t* numsteps, const float* coords, uint32_t e1, const RaySort& rs, uint32_t* list,
+                     uint32_t* list_len, void* scan_temp, size_t scan_temp_bytes) {
+	const uint32_t nblk = ray_sort_blocks(cap);
+	k_ray_hist<<<nblk, RS_RPB, 0, s>>>(cap, numsteps, coords, e1, rs);
+	launch_exclusive_scan(s, scan_temp, scan_temp_bytes, rs.hist, rs.off, 2 * RS_NB * nblk);
+	k_ray_sort_place<<<nblk, RS_RPB, 0, s>>>(cap, numsteps, e1, rs, list, list_len);
+}
+
 // Development statistic: per ray, march_step calls and skip-loop additions of the march
 // (SIMT-efficiency analysis; neus_debug_march_stats).
 __global__ void k_march_stats(uint32_t n_rays, const float* __restrict__ rays, const float* __restrict__ tstart, const uint32_t* __restrict__ lin,

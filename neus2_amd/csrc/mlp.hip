@@ -676,15 +676,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ALL ? 
 	__syncthreads();
 	const uint32_t n = n_ptr ? *n_ptr : n_fixed;
 	const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-	const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-	const uint32_t n_waves = (gridDim.x * blockDim.x) >> 6;
+	uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+	uint32_t n_waves = (gridDim.x * blockDim.x) >> 6;
+	uint32_t lo = 0, hi = n;
+	if (ia.xcd_parts == 8u) {  // (grid a multiple of 8: the launch rounds it)
+		const uint32_t x = blockIdx.x & 7u, wpb = blockDim.x >> 6;
+		lo = (uint32_t)((uint64_t)n * x / 8u); hi = (uint32_t)((uint64_t)n * (x + 1u) / 8u);
+		wave = (blockIdx.x >> 3) * wpb + (threadIdx.x >> 6); n_waves = (gridDim.x >> 3) * wpb;
+	}
 	const half_t var_h = wp.var[0];
 	const half_t bias_h = (half_t)wp.sdf_bias;
 	if (ia.n_long && blockIdx.x == 0 && threadIdx.x == 0) *ia.n_long = 0u;  // the transmittance scan's long-ray list
-	for (uint32_t base = wave * 32; base < n; base += n_waves * 32) {
+	for (uint32_t base = lo + wave * 32; base < hi; base += n_waves * 32) {
 		const FwdW w = w0.at(opaque_zero());
 		const uint32_t j = base + r;
-		const bool valid = j < n;
+		const bool valid = j < hi;
 		const uint32_t i = valid ? (IDX ? idx[j] : j) : 0;
 		const float* c = coords + (size_t)i * COORD_W;
 		const float x[3] = {c[0], c[1], c[2]}, wd[3] = {c[4], c[5], c[6]};
@@ -1687,20 +1693,23 @@ bool mlp_supported(uint32_t L, uint32_t W) {
 void launch_nerf_infer(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_ptr, uint32_t n_fixed, const float* coords, const GridLevels& gl,
                        uint32_t valid_level, const half_t* grid, const MlpPtrs& w, half_t* out, uint32_t blocks, const uint32_t* idx,
                        const InferAlpha* ia) {
-	const InferAlpha a = ia ? *ia : InferAlpha{nullptr, nullptr, 0.f, 0u, nullptr};
+	InferAlpha a = ia ? *ia : InferAlpha{nullptr, nullptr, 0.f, 0u, nullptr};
+	static const bool xcd_parts = [] { const char* e = std::getenv("NEUS_INFER_XCD_PARTS"); return e && e[0] == '1'; }();
+	if (xcd_parts) a.xcd_parts = 8u;
 	// persistent grid: at most the resident capacity (weights are staged once per block; both variants run at the
 	// same 3 waves per SIMD, amdgpu_waves_per_eu)
 	static const bool pipe = [] { const char* e = std::getenv("NEUS_INFER_PIPE"); return !(e && e[0] == '0'); }();
 	const bool all = pipe && valid_level + 1 >= L;
+	auto xg = [&](uint32_t b) { return a.xcd_parts ? std::max(8u, b & ~7u) : b; };
 #define X(l, w_) if (L == l && W == w_) { \
 		static const uint32_t cap = resident_blocks((const void*)k_nerf_infer<l, w_, false>, 256); \
 		static const uint32_t cap_all = resident_blocks((const void*)k_nerf_infer<l, w_, false, true>, 256); \
 		if (all) { \
-			if (idx) k_nerf_infer<l, w_, true, true><<<std::min(blocks, cap_all), 256, 0, s>>>(n_ptr, n_fixed, coords, gl, valid_level, grid, w, out, idx, a); \
-			else k_nerf_infer<l, w_, false, true><<<std::min(blocks, cap_all), 256, 0, s>>>(n_ptr, n_fixed, coords, gl, valid_level, grid, w, out, nullptr, a); \
+			if (idx) k_nerf_infer<l, w_, true, true><<<xg(std::min(blocks, cap_all)), 256, 0, s>>>(n_ptr, n_fixed, coords, gl, valid_level, grid, w, out, idx, a); \
+			else k_nerf_infer<l, w_, false, true><<<xg(std::min(blocks, cap_all)), 256, 0, s>>>(n_ptr, n_fixed, coords, gl, valid_level, grid, w, out, nullptr, a); \
 			return; } \
-		if (idx) k_nerf_infer<l, w_, true><<<std::min(blocks, cap), 256, 0, s>>>(n_ptr, n_fixed, coords, gl, valid_level, grid, w, out, idx, a); \
-		else k_nerf_infer<l, w_, false><<<std::min(blocks, cap), 256, 0, s>>>(n_ptr, n_fixed, coords, gl, valid_level, grid, w, out, nullptr, a); \
+		if (idx) k_nerf_infer<l, w_, true><<<xg(std::min(blocks, cap)), 256, 0, s>>>(n_ptr, n_fixed, coords, gl, valid_level, grid, w, out, idx, a); \
+		else k_nerf_infer<l, w_, false><<<xg(std::min(blocks, cap)), 256, 0, s>>>(n_ptr, n_fixed, coords, gl, valid_level, grid, w, out, nullptr, a); \
 		return; }
 	NEUS_MLP_CONFIGS(X)
 #undef X

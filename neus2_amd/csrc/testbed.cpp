@@ -282,7 +282,12 @@ struct NeusTestbed {
 	static constexpr float PROGRESSIVE_RATIO = 0.7f;
 	Dev<uint32_t> chunk_list, chunk_cnt;  // chunk_cnt: [k] round k's sample list length, [16] the long-ray list's, [32 + k] open rays
 	Dev<uint32_t> open_rays[2];          // the rays still open after a round (ping-pong: round k reads [(k - 1) & 1])
+	// spatial ray order of the progressive rounds (RaySort; NEUS_RAY_SORT=0: slot order, one-XCD-agnostic lists)
+	Dev<uint32_t> rs_hist, rs_off, rs_perm;
+	Dev<uint16_t> rs_key;
+	bool ray_sort = [] { const char* e = std::getenv("NEUS_RAY_SORT"); return !(e && e[0] == '0'); }();
 	static constexpr uint32_t OPEN_CNT = 32;
+	static constexpr uint32_t RS_N_PERM = 48;  // chunk_cnt slot: the ray order's length (k_ray_sort_scan)
 	Dev<uint32_t> long_rays;  // the loss scan's wave-per-ray list (+ its counter in chunk_cnt[16])
 	TrainBufs tbuf{};
 	// RNG + counters (testbed.cu:2087-2101)
@@ -660,7 +665,8 @@ struct NeusTestbed {
 			sc_zero_from = swork.n_buckets;  // nothing assumed
 			sc_zero_from_e = gl.offset[gl.n_levels];
 		}
-		scan_tmp_bytes = std::max(scan_temp_bytes(MAX_RAYS), scan_temp_bytes((uint32_t)n_bins));
+		scan_tmp_bytes = std::max({scan_temp_bytes(MAX_RAYS), scan_temp_bytes((uint32_t)n_bins),
+		                           scan_temp_bytes(2 * (RS_BINS + 1) * ray_sort_blocks(MAX_RAYS))});
 		scan_tmp.alloc(scan_tmp_bytes + 256);
 		scan_temp_reset(stream, scan_tmp.p);
 		HIP_CHECK(hipStreamSynchronize(stream));
@@ -681,6 +687,8 @@ struct NeusTestbed {
 		l_racc.alloc(MAX_RAYS); l_rgr.alloc(MAX_RAYS); l_rT.alloc(MAX_RAYS); l_rek.alloc(MAX_RAYS);
 		chunk_list.alloc(max_samples); chunk_cnt.alloc(64); long_rays.alloc(MAX_RAYS);
 		open_rays[0].alloc(MAX_RAYS); open_rays[1].alloc(MAX_RAYS);
+		rs_hist.alloc(2 * (size_t)(RS_BINS + 1) * ray_sort_blocks(MAX_RAYS)); rs_off.alloc(rs_hist.n);
+		rs_perm.alloc(MAX_RAYS); rs_key.alloc(MAX_RAYS);
 		loss.alloc(MAX_RAYS); ek.alloc(MAX_RAYS); mask.alloc(MAX_RAYS); loss_sum.alloc(4);
 		coords.alloc((size_t)max_samples * COORD_W); net_out.alloc((size_t)max_samples * OUT_W);
 		coords_c.alloc((size_t)batch * COORD_W); dL_dout.alloc((size_t)batch * OUT_W);
@@ -1271,10 +1279,13 @@ struct NeusTestbed {
 		const uint32_t nch = (uint32_t)chunk_ends.size() + 1;
 		// round 0's list slots go through cbase (rewritten by the loss compaction before it is read again)
 		const Round0List r0{chunk_ends[0], cbase.p, chunk_list.p, chunk_cnt.p, nch + 1};
+		const bool sorted_rays = progressive && ray_sort;  // round 0's list by k_ray_sort_place instead of the march write
 		launch_march_count(s, MAX_RAYS, max_samples, st.p, dp, ds, bitfield.p, bf_lin.p, rng.state, rng.inc, rays.p, startt.p, nreq.p, mwork,
 		                   progressive ? chunk_cnt.p : nullptr, OPEN_CNT + nch, ray_cull ? occ_bbox.p : nullptr);  // list lengths + open-ray counts
 		launch_march_write(s, MAX_RAYS, st.p, ds, rays.p, mwork, nreq.p, base.p, numsteps.p, coords.p, sample_ray.p, max_samples, scan_tmp.p,
-		                   progressive ? &r0 : nullptr, dbg_lds_fill);
+		                   progressive && !sorted_rays ? &r0 : nullptr, dbg_lds_fill);
+		const RaySort rsort{rs_hist.p, rs_off.p, rs_key.p, rs_perm.p, chunk_cnt.p + RS_N_PERM};
+		if (sorted_rays) launch_ray_sort(s, MAX_RAYS, numsteps.p, coords.p, chunk_ends[0], rsort, chunk_list.p, chunk_cnt.p, scan_tmp.p, scan_tmp_bytes);
 		mark(2);
 		// DeltaNetwork forward on the samples (nerf_network.h:162-182); the loss keeps the undeformed records
 		const float* c_in = coords.p;
@@ -1291,7 +1302,7 @@ struct NeusTestbed {
 				const uint32_t e1 = k + 1 < nch ? chunk_ends[k] : 0xffffffffu;
 				const uint32_t e2 = k + 2 < nch ? chunk_ends[k + 1] : 0xffffffffu;
 				// the loss's alpha terms in the inference epilogue (k_loss_alpha's work on the round's samples)
-				const InferAlpha ia{w.sa, w.ekt, lp.cos_anneal, ds.cone_angle == 0.0f ? 1u : 0u, nullptr};
+				const InferAlpha ia{w.sa, w.ekt, lp.cos_anneal, ds.cone_angle == 0.0f ? 1u : 0u, nullptr, sorted_rays ? 8u : 0u};
 				it_mark();
 				launch_nerf_infer(s, lay.L, lay.W, chunk_cnt.p + k, 0, c_in, gl, valid, params_h.p + lay.grid_off, mlp, net_out.p, 8192, chunk_list.p,
 				                  use_delta ? nullptr : &ia);
@@ -1299,7 +1310,8 @@ struct NeusTestbed {
 				if (use_delta) launch_loss_alpha_list(s, max_samples, chunk_cnt.p + k, chunk_list.p, coords.p, net_out.p, lp.cos_anneal, w, ds.cone_angle == 0.0f);
 				const bool more = k + 1 < nch;
 				launch_loss_scan_chunk(s, MAX_RAYS, numsteps.p, w, ccount.p, e0, e1, e2, more ? chunk_list.p : nullptr, chunk_cnt.p + k + 1,
-				                       k ? open_rays[(k - 1) & 1].p : nullptr, k ? chunk_cnt.p + OPEN_CNT + k - 1 : nullptr,
+				                       k ? open_rays[(k - 1) & 1].p : (sorted_rays ? rs_perm.p : nullptr),
+				                       k ? chunk_cnt.p + OPEN_CNT + k - 1 : (sorted_rays ? rsort.n_perm : nullptr),
 				                       more ? open_rays[k & 1].p : nullptr, more ? chunk_cnt.p + OPEN_CNT + k : nullptr);
 				e0 = e1;
 			}
