@@ -3,7 +3,9 @@ network evaluated in rounds of per-ray sample chunks, a ray's next chunk only wh
 The composited samples, the recurrence and therefore every output must be bit-identical to the one-pass step
 (testbed_nerf.cu:3802-3811 infers every kept sample): two testbeds from the same init, one forced progressive, one
 forced one-pass, trained side by side and compared bitwise (parameters, optimizer state, occupancy grid, per-ray
-counts, loss). The variance parameter is raised so the initial sphere is opaque and rays end mid-march (checked)."""
+counts, loss). The variance parameter is raised so the initial sphere is opaque and rays end mid-march (checked).
+The progressive testbed runs the rounds in the spatial ray order (k_ray_sort_place, one list eighth per XCD) unless
+NEUS_RAY_SORT=0 at its creation; both orders are compared with the one-pass step."""
 import numpy as np
 import pytest
 
@@ -54,3 +56,11 @@ def test_progressive_inference_bit_identical(torch_cuda, chunk_ends):
     sa, sb = a.stats(), b.stats()
     for k in ("loss", "measured_batch_size", "measured_batch_size_before_compaction"):
         assert sa[k] == sb[k], (k, sa[k], sb[k])
+
+
+def test_progressive_slot_order_bit_identical(torch_cuda, monkeypatch):
+    """The rounds in ray-slot order (NEUS_RAY_SORT=0, no XCD eighths): the same bitwise equality."""
+    monkeypatch.setenv("NEUS_RAY_SORT", "0")
+    a, b, cut = _pair((32, 80), steps=8)
+    assert cut > 0
+    np.testing.assert_array_equal(a.get_params().view(np.uint32), b.get_params().view(np.uint32))
