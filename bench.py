@@ -91,6 +91,11 @@ def parse():
     # BASELINE.json words config 2 as a 16-level grid (the reference's base.json has 14): the same step at L=16
     p.add_argument("--l16", type=int, default=1)
     p.add_argument("--early", type=int, default=1)
+    # data-parallel backend: "rccl" (one rank per GPU over xGMI, the production path) or "host" (the host-staged TCP
+    # group, include/neus2_hip.h neus_host_group_create: ranks that cannot form an RCCL communicator, e.g. several on
+    # one GPU with --same-device; a bring-up / test path whose exchange runs through host memory, not a scaling number)
+    p.add_argument("--dp-backend", choices=("rccl", "host"), default="rccl")
+    p.add_argument("--same-device", type=int, default=0, help="every rank on GPU 0 (with --dp-backend host)")
     return p.parse_args()
 
 
@@ -204,8 +209,9 @@ def launch_ranks(n):
 class Group:
     """The gloo control plane of the ranks (RCCL communicators are created inside each C++ Testbed)."""
 
-    def __init__(self, rank, world):
-        self.rank, self.world = rank, world
+    def __init__(self, rank, world, backend="rccl"):
+        self.rank, self.world, self.backend = rank, world, backend
+        self.hgroups = []  # host groups outlive their testbeds' training (kept until close)
         if world > 1:
             import torch.distributed as dist
             dist.init_process_group("gloo", init_method="env://")
@@ -225,11 +231,19 @@ class Group:
         return float(t.item())
 
     def attach(self, tb):
-        """Data-parallel Testbed: a fresh RCCL unique id from rank 0, broadcast over gloo."""
+        """Data-parallel Testbed: a fresh RCCL unique id from rank 0, broadcast over gloo (or, with the host backend, rank
+        0's TCP port for a fresh host group)."""
         if self.world == 1:
             return
         import torch.distributed as dist
         from neus2_amd import pyngp
+        if self.backend == "host":
+            obj = [free_port() if self.rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            g = pyngp.HostGroup(self.rank, self.world, "127.0.0.1", obj[0])
+            g.join(tb)
+            self.hgroups.append(g)
+            return
         obj = [pyngp.nccl_unique_id() if self.rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         tb.init_data_parallel(self.rank, self.world, obj[0])
@@ -289,8 +303,13 @@ def main():
         sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.same_device:
+        if args.dp_backend != "host" and world > 1:
+            print("bench.py: --same-device needs --dp-backend host (RCCL refuses two ranks on one GPU)", file=sys.stderr)
+            sys.exit(2)
+        local = 0
     import torch
-    grp = Group(rank, world)
+    grp = Group(rank, world, args.dp_backend)
     torch.cuda.set_device(local)
     from neus2_amd import scenes
     sc = scenes.sphere_scene(args.views, args.width, args.height, principal=(823.2 / 1600, 619.1 / 1200))
@@ -338,6 +357,8 @@ def main():
         "config": {"workload": "NeuS2 train step, Config S, base.json L=14 T=2^19 W=64, Nc=2^18/GPU, R=2^18/GPU fixed, "
                                f"all {levels} levels active (network trained {args.prepare} steps before the warm-up)",
                    "global_batch": batch * world, "rays_per_gpu": args.rays, "parallelism": f"dp{world}",
+                   "dp_backend": args.dp_backend if world > 1 else None,
+                   **({"same_device": True} if args.same_device and world > 1 else {}),
                    "prepare_steps": args.prepare, "levels_active": levels},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": dk["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": dk["frac"], "traffic": measured_traffic(dom, levels), "bytes_per_launch": dk["bytes"],

@@ -151,6 +151,12 @@ typedef struct NeusNetLayout {
 	uint32_t n_levels;
 } NeusNetLayout;
 
+/* ABI version of this header (bumped on any incompatible signature or struct change; version 2: neus_module_create_network
+ * became tcnn's create_network(n_input_dims, n_output_dims, network), the NerfNetwork factory neus_module_create_nerf_network;
+ * version 3: NeusDataParallelInfo gained host_group).
+ * Bindings compare it on load so that a stale library or binding fails loudly instead of misreading arguments. */
+#define NEUS_ABI_VERSION 3u
+int neus_abi_version(uint32_t* out);
 const char* neus_last_error(void);
 int neus_device_count(int* count);
 int neus_device_synchronize(void);
@@ -313,6 +319,9 @@ int neus_debug_march_profile(NeusTestbed* tb, unsigned long long* out, uint32_t 
 /* Development statistic of the last grid-gradient scatter (region mode): records written per level (out[L], after the
  * wave run merge) and the largest per-(level, block) region. */
 int neus_debug_scatter_stats(NeusTestbed* tb, uint64_t* records_per_level, uint32_t* max_region);
+/* The region scatter's job plan: per level, the workgroups one level-local bucket is split over (1: not split; the heavy
+ * buckets of the small dense levels meet through 64-bit integer atomics). */
+int neus_debug_scatter_parts(NeusTestbed* tb, uint32_t* parts_per_level /* n_levels */);
 /* Development check of the single-pass exclusive scan the step's compactions use (scan.hip): device buffers in / out
  * of n u32 on `hip_stream`, `reps` launches on one fresh state (the epoch re-arm), synchronous; failures = bounded-wait
  * give-ups (0 expected). */
@@ -364,6 +373,7 @@ typedef struct NeusDataParallelInfo {
 	uint64_t collective_calls;       /* all-reduce calls issued since init */
 	uint64_t allreduce_bytes;        /* bytes all-reduced since init (per rank, payload) */
 	uint64_t last_step_allreduce_bytes;
+	uint32_t host_group;             /* cross-process host-staged group (neus_host_group_create) */
 } NeusDataParallelInfo;
 int neus_testbed_data_parallel_info(NeusTestbed* tb, NeusDataParallelInfo* out);
 /* Overlapped gradient exchange (default on): the MLP blocks are all-reduced after the weight-gradient reduction and the
@@ -378,6 +388,19 @@ typedef struct NeusLocalGroup NeusLocalGroup;
 int neus_local_group_create(int world, NeusLocalGroup** out);
 int neus_local_group_destroy(NeusLocalGroup* group);
 int neus_testbed_init_local_group(NeusTestbed* tb, NeusLocalGroup* group, int rank);
+/* Cross-process host-staged collectives (hostgroup.h): ranks in separate processes (e.g. several on one GPU, which RCCL
+ * refuses) exchange over TCP, rank 0 at host:port (IPv4) reducing in rank order (bitwise the in-process group's sums).
+ * Each collective is staged on the testbed's communication stream (device -> pinned host, a host function for the
+ * exchange, host -> device), gated by the same events as the RCCL collectives, so the overlapped exchange runs beside the
+ * backward. Every rank creates its group (rank 0 listens, the others connect; 120 s timeouts) and attaches its testbed;
+ * the ranks must issue the same collectives (a mismatch fails loudly). The group must outlive its testbed's training. */
+typedef struct NeusHostGroup NeusHostGroup;
+int neus_host_group_create(int rank, int world, const char* host, int port, NeusHostGroup** out);
+int neus_host_group_destroy(NeusHostGroup* group);
+int neus_testbed_init_host_group(NeusTestbed* tb, NeusHostGroup* group);
+/* Test hook (no GPU): one collective of the group's protocol on a host buffer of n 4-byte elements, type 0 f32 / 1 u32,
+ * op 0 sum / 1 max; a failed exchange poisons the group and returns its error. */
+int neus_debug_host_group_allreduce(NeusHostGroup* group, void* host, uint64_t n, int type, int op);
 
 /* ------------------------------------------------------------------ tcnn-shaped operator modules
  * tcnn::cpp::Module (dependencies/my_tcnn/include/tiny-cuda-nn/cpp_api.h:66-110) over the gfx950 kernels, with

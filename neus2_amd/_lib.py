@@ -56,6 +56,7 @@ class NeusDataParallelInfo(C.Structure):
     _fields_ = [
         ("rank", C.c_uint32), ("world", C.c_uint32), ("has_communicator", C.c_uint32), ("local_group", C.c_uint32),
         ("collective_calls", C.c_uint64), ("allreduce_bytes", C.c_uint64), ("last_step_allreduce_bytes", C.c_uint64),
+        ("host_group", C.c_uint32),
     ]
 
 
@@ -105,17 +106,17 @@ class NeusModuleInfo(C.Structure):
 
 # Every symbol declared in include/neus2_hip.h (checked by tests/test_capi.py).
 EXPORTS = [
-    "neus_last_error", "neus_device_count", "neus_device_synchronize",
+    "neus_last_error", "neus_abi_version", "neus_device_count", "neus_device_synchronize",
     "neus_testbed_create", "neus_testbed_destroy", "neus_testbed_set_dataset", "neus_testbed_reload_network",
     "neus_testbed_layout", "neus_testbed_train", "neus_testbed_get_stats", "neus_testbed_get_params",
     "neus_testbed_set_params", "neus_testbed_get_gradients", "neus_testbed_get_ema_params",
     "neus_testbed_get_half_params",
     "neus_testbed_get_density_grid", "neus_testbed_set_density_grid", "neus_testbed_restore_state", "neus_testbed_get_rng", "neus_testbed_render", "neus_testbed_sdf_on_grid",
-    "neus_testbed_marching_cubes", "neus_testbed_mc_density", "neus_testbed_get_mesh", "neus_testbed_mesh_vertex_colors", "neus_mc_table", "neus_prepare_image_rgba8", "neus_testbed_ray_counts", "neus_debug_time_kernel", "neus_debug_march_stats", "neus_debug_exclusive_scan", "neus_debug_scan_giveup", "neus_debug_inject_health", "neus_debug_set_lds_fill", "neus_debug_sample_rays_round0", "neus_debug_march_profile", "neus_debug_scatter_stats", "neus_testbed_time_kernel", "neus_testbed_stream",
+    "neus_testbed_marching_cubes", "neus_testbed_mc_density", "neus_testbed_get_mesh", "neus_testbed_mesh_vertex_colors", "neus_mc_table", "neus_prepare_image_rgba8", "neus_testbed_ray_counts", "neus_debug_time_kernel", "neus_debug_march_stats", "neus_debug_exclusive_scan", "neus_debug_scan_giveup", "neus_debug_inject_health", "neus_debug_set_lds_fill", "neus_debug_sample_rays_round0", "neus_debug_march_profile", "neus_debug_scatter_stats", "neus_debug_scatter_parts", "neus_testbed_time_kernel", "neus_testbed_stream",
     "neus_testbed_synchronize", "neus_testbed_set_profiling", "neus_testbed_kernel_times", "neus_testbed_set_infer_timing", "neus_testbed_infer_timing",
     "neus_nccl_unique_id", "neus_testbed_init_data_parallel", "neus_testbed_init_data_parallel_ex",
     "neus_testbed_data_parallel_info", "neus_testbed_set_exchange_overlap", "neus_local_group_create", "neus_local_group_destroy",
-    "neus_testbed_init_local_group",
+    "neus_testbed_init_local_group", "neus_host_group_create", "neus_host_group_destroy", "neus_testbed_init_host_group", "neus_debug_host_group_allreduce",
     "neus_grid_encode", "neus_net_forward", "neus_net_backward", "neus_sample_rays", "neus_loss_compact",
     "neus_optimizer_step", "neus_fill_rollover", "neus_occ_update", "neus_mfma_probe",
     "neus_testbed_next_frame", "neus_testbed_get_movement", "neus_testbed_set_movement", "neus_testbed_frame_state",
@@ -128,6 +129,9 @@ EXPORTS = [
     "neus_module_backward_backward_input",
     "neus_net_backward_pos", "neus_delta_apply", "neus_delta_backward",
 ]
+
+# include/neus2_hip.h's NEUS_ABI_VERSION this binding was written against: a library of another ABI fails to load
+ABI_VERSION = 3
 
 _lib = None
 
@@ -145,6 +149,9 @@ def lib():
         f = getattr(l, name)
         if name != "neus_last_error":
             f.restype = C.c_int
+    v = C.c_uint32(0)
+    if l.neus_abi_version(C.byref(v)) != 0 or v.value != ABI_VERSION:
+        raise RuntimeError(f"{LIB_PATH}: C-ABI version {v.value}, this binding needs {ABI_VERSION} (rebuild the library)")
     _lib = l
     return l
 

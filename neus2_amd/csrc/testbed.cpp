@@ -11,6 +11,7 @@
 #include "kernels.h"
 #include "scan_lookback.h"
 #include "json_lite.h"
+#include "hostgroup.h"
 #include "../../include/neus2_hip.h"
 
 #include <rccl/rccl.h>
@@ -233,6 +234,7 @@ struct NeusTestbed {
 	// step workspace
 	uint32_t batch = 0, max_samples = 0;
 	Dev<float> rays, startt, coords, coords_c, loss, ek, mask, loss_sum;
+	Dev<uint32_t> health_buf;  // [0] march fail flags, [1] scan give-ups (all-reduced at every loss readback); [2..3] setting checks
 	Dev<uint32_t> nreq, base, numsteps, ccount, cbase, enc, march_nrec, march_queue;
 	Dev<uint2> march_rec, march_seg;
 	MarchWork mwork{};
@@ -310,7 +312,14 @@ struct NeusTestbed {
 	// data parallel: RCCL communicator (production) or an in-process group
 	ncclComm_t comm = nullptr;
 	NeusLocalGroup* group = nullptr;
+	// cross-process host-staged group (hostgroup.h): every collective staged on comm_stream through a pinned buffer
+	NeusHostGroup* hgroup = nullptr;
+	uint8_t* hg_stage = nullptr;
+	size_t hg_stage_bytes = 0;
 	uint32_t rank = 0, world = 1;
+	// the exchange setting must be the same on every rank (the overlapped and grouped exchanges issue different
+	// collective sequences): checked by an all-reduce at the first step after init or a change
+	bool overlap_verified = false;
 	bool force_coll = false;  // issue the collectives at world 1 too (a forced one-rank communicator, tests)
 	// Overlapped gradient exchange: each finished gradient range is all-reduced as soon as its producer
 	// finishes - the MLP blocks after the weight-gradient reduction, the grid levels group by group beside the scatter's
@@ -326,7 +335,7 @@ struct NeusTestbed {
 	static constexpr uint32_t X_GROUPS = 3;   // grid level groups of the overlapped exchange (~equal bytes at L=14)
 	// on comm_stream after the work queued so far on the step's stream (RCCL); the in-process group stages on the host
 	hipStream_t x_stream() {
-		if (!comm) return stream;
+		if (!comm && !hgroup) return stream;
 		if (!comm_stream) {
 			HIP_CHECK(hipStreamCreateWithFlags(&comm_stream, hipStreamNonBlocking));
 			HIP_CHECK(hipEventCreateWithFlags(&ev_xdone, hipEventDisableTiming));
@@ -414,6 +423,7 @@ struct NeusTestbed {
 		if (ev_join) (void)hipEventDestroy(ev_join);
 		if (ev_loss) (void)hipEventDestroy(ev_loss);
 		if (comm_stream) { (void)hipStreamSynchronize(comm_stream); (void)hipStreamDestroy(comm_stream); }
+		if (hg_stage) (void)hipHostFree(hg_stage);
 		for (auto& e : ev_x) if (e) (void)hipEventDestroy(e);
 		if (ev_xdone) (void)hipEventDestroy(ev_xdone);
 		for (auto& e : it_ev) if (e) (void)hipEventDestroy(e);
@@ -689,7 +699,7 @@ struct NeusTestbed {
 		open_rays[0].alloc(MAX_RAYS); open_rays[1].alloc(MAX_RAYS);
 		rs_hist.alloc(2 * (size_t)(RS_BINS + 1) * ray_sort_blocks(MAX_RAYS)); rs_off.alloc(rs_hist.n);
 		rs_perm.alloc(MAX_RAYS); rs_key.alloc(MAX_RAYS);
-		loss.alloc(MAX_RAYS); ek.alloc(MAX_RAYS); mask.alloc(MAX_RAYS); loss_sum.alloc(4);
+		loss.alloc(MAX_RAYS); ek.alloc(MAX_RAYS); mask.alloc(MAX_RAYS); loss_sum.alloc(4); health_buf.alloc(4);
 		coords.alloc((size_t)max_samples * COORD_W); net_out.alloc((size_t)max_samples * OUT_W);
 		coords_c.alloc((size_t)batch * COORD_W); dL_dout.alloc((size_t)batch * OUT_W);
 		const NeusNetworkConfig& c = cfg;
@@ -933,6 +943,7 @@ struct NeusTestbed {
 		if (!coll_on() || n == 0) return;
 		++coll_calls; coll_bytes += n * 4; coll_bytes_step += n * 4;
 		if (comm) NCCL_CHECK(ncclAllReduce(p, p, n, ncclFloat32, max_op ? ncclMax : ncclSum, comm, on ? on : stream));
+		else if (hgroup) hg_allreduce(p, n * 4, NeusHostGroup::F32, max_op ? NeusHostGroup::MAX : NeusHostGroup::SUM, on);
 		else if (group) group->allreduce<float>(rank, p, n, max_op ? NeusLocalGroup::MAX : NeusLocalGroup::SUM, stream);
 		else throw std::runtime_error("data parallel: no communicator");
 	}
@@ -940,8 +951,48 @@ struct NeusTestbed {
 		if (!coll_on() || n == 0) return;
 		++coll_calls; coll_bytes += n * 4; coll_bytes_step += n * 4;
 		if (comm) NCCL_CHECK(ncclAllReduce(p, p, n, ncclUint32, ncclSum, comm, on ? on : stream));
+		else if (hgroup) hg_allreduce(p, n * 4, NeusHostGroup::U32, NeusHostGroup::SUM, on);
 		else if (group) group->allreduce<uint32_t>(rank, p, n, NeusLocalGroup::SUM, stream);
 		else throw std::runtime_error("data parallel: no communicator");
+	}
+	// A host-group collective on comm_stream: device -> pinned stage, the socket exchange in a host function, stage ->
+	// device. Issued from the step's stream (on == nullptr / stream), it is gated after the work queued there and the step's
+	// stream waits for it; issued on comm_stream (the overlapped exchange), the stream order is the gate.
+	void hg_allreduce(void* dev, size_t bytes, uint32_t type, uint32_t op, hipStream_t on) {
+		const bool own = !(on && on == comm_stream);
+		hipStream_t cs = own ? x_stream() : on;
+		if (bytes > hg_stage_bytes) {  // grow: the queued collectives still read the old stage
+			if (comm_stream) HIP_CHECK(hipStreamSynchronize(comm_stream));
+			if (hg_stage) HIP_CHECK(hipHostFree(hg_stage));
+			hg_stage_bytes = std::max(bytes, (size_t)1 << 20);
+			HIP_CHECK(hipHostMalloc((void**)&hg_stage, hg_stage_bytes));
+		}
+		HIP_CHECK(hipMemcpyAsync(hg_stage, dev, bytes, hipMemcpyDeviceToHost, cs));
+		HostCollCall* c = new HostCollCall{hgroup, hg_stage, bytes, type, op};
+		HIP_CHECK(hipLaunchHostFunc(cs, [](void* a) {
+			HostCollCall* c = (HostCollCall*)a;
+			c->g->allreduce_host(c->host, c->bytes, c->type, c->op);
+			delete c;
+		}, c));
+		HIP_CHECK(hipMemcpyAsync(dev, hg_stage, bytes, hipMemcpyHostToDevice, cs));
+		if (own) x_join();
+	}
+	// every rank must run the same exchange (overlapped or grouped): sum of the setting over the ranks is 0 or world
+	void verify_uniform_exchange() {
+		if (overlap_verified || !coll_on()) return;
+		health_buf.alloc(4);
+		const uint32_t v[2] = {exchange_overlap ? 1u : 0u, 1u};
+		HIP_CHECK(hipMemcpyAsync(health_buf.p + 2, v, 8, hipMemcpyHostToDevice, stream));
+		allreduce_u32(health_buf.p + 2, 2);
+		uint32_t h[2] = {0, 0};
+		HIP_CHECK(hipMemcpyAsync(h, health_buf.p + 2, 8, hipMemcpyDeviceToHost, stream));
+		HIP_CHECK(hipStreamSynchronize(stream));
+		if (hgroup) hgroup->check();
+		if (h[1] != world) throw std::runtime_error("data parallel: the exchange-setting check saw " + std::to_string(h[1]) + " of " + std::to_string(world) + " ranks");
+		if (h[0] != 0 && h[0] != world)
+			throw std::runtime_error("data parallel: the exchange overlap is on for " + std::to_string(h[0]) + " of " + std::to_string(world) +
+			                         " ranks (neus_testbed_set_exchange_overlap / NEUS_EXCHANGE_OVERLAP must be the same on every rank)");
+		overlap_verified = true;
 	}
 
 	// ------------------------------------------------------------ occupancy grid (testbed_nerf.cu:3293-3397, 4003-4016)
@@ -1246,6 +1297,12 @@ struct NeusTestbed {
 	void train_step() {
 		if (!have_net) throw std::runtime_error("train: no network (reload_network first)");
 		hipStream_t s = stream;
+		if (hgroup) hgroup->check();
+		verify_uniform_exchange();
+		// the readback of 16 steps back (long done on the device) is checked at this step boundary, before anything of
+		// this step is queued: a health failure (all-reduced, so every rank sees it) stops every rank on the same step
+		// with no collective half-issued and no step half-applied; the host stays at most 16 steps ahead of the device
+		if (training_step % 16 == 0 && loss_pending) consume_loss();
 		// dynamic scenes (testbed.cu:2651-2712): progressive levels count from the end of the global-movement
 		// phase; at its end canonical training starts (and the movement keeps training when finetuned)
 		const bool dyn = cur_frame >= 1;
@@ -1355,6 +1412,9 @@ struct NeusTestbed {
 			launch_sum_f32(s, scan_tmp.p, scan_tmp_bytes, loss.p, loss_sum.p + 0, MAX_RAYS);
 			launch_sum_f32(s, scan_tmp.p, scan_tmp_bytes, ek.p, loss_sum.p + 1, MAX_RAYS);
 			launch_sum_f32(s, scan_tmp.p, scan_tmp_bytes, mask.p, loss_sum.p + 2, MAX_RAYS);
+			// this rank's health words, summed over the ranks with the loss sums (any rank's failure stops all of them)
+			HIP_CHECK(hipMemcpyAsync(health_buf.p, &st.p->fail_flags, 4, hipMemcpyDeviceToDevice, s));
+			HIP_CHECK(hipMemcpyAsync(health_buf.p + 1, scan_tmp.p + offsetof(ScanState, fail), 4, hipMemcpyDeviceToDevice, s));
 		}
 		if (coll_on()) {
 			// collective 1 (gradients; DeltaNetwork partials) and 3 (counters, loss scalars) of SURVEY §8(e). The gradient
@@ -1372,15 +1432,14 @@ struct NeusTestbed {
 			allreduce_u32(&st.p->compacted_counter, 1, xs);
 			allreduce_u32(&st.p->n_rays_with_samples, 1, xs);
 			if (use_delta) allreduce_f32(delta_partial.p, delta_partial_floats(), false, xs);
-			if (get_loss) allreduce_f32(loss_sum.p, 3, false, xs);
+			if (get_loss) { allreduce_f32(loss_sum.p, 3, false, xs); allreduce_u32(health_buf.p, 2, xs); }
 			coll_end();
 			x_join();
 		}
 		if (get_loss) {
-			// the previous readback (16 steps back, long done on the device) is checked first: a health failure then
-			// surfaces as this train call's error, while the host stays at most 16 steps ahead of the device
-			if (loss_pending) consume_loss();
+			if (loss_pending) consume_loss();  // (consumed at this step's start already; a restored state may leave one)
 			HIP_CHECK(hipMemcpyAsync(pinned, loss_sum.p, 3 * 4, hipMemcpyDeviceToHost, s));
+			HIP_CHECK(hipMemcpyAsync(pinned + 52, health_buf.p, 8, hipMemcpyDeviceToHost, s));
 			HIP_CHECK(hipMemcpyAsync(pinned + 64, st.p, sizeof(StepState), hipMemcpyDeviceToHost, s));
 			HIP_CHECK(hipMemcpyAsync(pinned + 48, scan_tmp.p + offsetof(ScanState, fail), 4, hipMemcpyDeviceToHost, s));
 			HIP_CHECK(hipEventRecord(ev_loss, s));
@@ -1446,7 +1505,8 @@ struct NeusTestbed {
 		if (prof_pending[prof_par ^ 1]) accumulate_phases(prof_par ^ 1);
 	}
 
-	void consume_loss() {
+	// raise = false (stats): record the health bits and the abort without throwing
+	void consume_loss(bool raise = true) {
 		if (!loss_pending) return;
 		HIP_CHECK(hipEventSynchronize(ev_loss));
 		const StepState* sst = (const StepState*)(pinned + 64);
@@ -1472,16 +1532,20 @@ struct NeusTestbed {
 		loss_pending = false;
 		// device health (sticky): a march that met a non-finite / negative t, a look-back scan that gave up waiting. Either
 		// means corrupted sampling or compaction bases: training stops with an error instead of continuing on bad data.
-		uint32_t scan_fail = 0;
+		uint32_t scan_fail = 0, all[2] = {0, 0};
 		std::memcpy(&scan_fail, pinned + 48, 4);
-		health_raise(sst->fail_flags | (scan_fail ? STEP_FAIL_SCAN : 0u));
+		std::memcpy(all, pinned + 52, 8);  // the health words summed over the ranks (this rank's alone at world 1)
+		const uint32_t local = sst->fail_flags | (scan_fail ? STEP_FAIL_SCAN : 0u);
+		const uint32_t global = (all[0] ? (all[0] & STEP_FAIL_MARCH_T ? STEP_FAIL_MARCH_T : all[0]) : 0u) | (all[1] ? STEP_FAIL_SCAN : 0u);
+		health_raise(local | (coll_on() ? global : 0u), local == 0 && coll_on() && global != 0, raise);
 	}
 	uint32_t fail_seen = 0;
-	void health_raise(uint32_t flags) {
+	void health_raise(uint32_t flags, bool other_rank = false, bool raise = true) {
 		if (!flags) return;
 		fail_seen |= flags;
 		aborted = true;
-		std::string m = "training step: device health check failed:";
+		if (!raise) return;
+		std::string m = other_rank ? "training step: device health check failed on another rank:" : "training step: device health check failed:";
 		if (flags & STEP_FAIL_MARCH_T) m += " the occupancy march met a non-finite or negative t (corrupted sampling state);";
 		if (flags & STEP_FAIL_SCAN) m += " a look-back scan gave up waiting for a predecessor tile (compaction bases are wrong);";
 		throw std::runtime_error(m);
@@ -1500,6 +1564,11 @@ hipStream_t as_stream(NeusTestbed* tb, void* s) { return s ? (hipStream_t)s : tb
 extern "C" {
 
 const char* neus_last_error(void) { return g_err.c_str(); }
+int neus_abi_version(uint32_t* out) {
+	if (!out) return 1;
+	*out = NEUS_ABI_VERSION;
+	return 0;
+}
 int neus_device_count(int* count) { return guard([&] { HIP_CHECK(hipGetDeviceCount(count)); }); }
 int neus_device_synchronize(void) { return guard([&] { HIP_CHECK(hipDeviceSynchronize()); }); }
 
@@ -1528,7 +1597,7 @@ int neus_testbed_train(NeusTestbed* tb, uint32_t n_steps) {
 }
 int neus_testbed_get_stats(NeusTestbed* tb, NeusTrainStats* o) {
 	return guard([&] {
-		tb->consume_loss();
+		tb->consume_loss(false);  // health bits and the abort are reported below, not raised
 		HIP_CHECK(hipStreamSynchronize(tb->stream));
 		StepState s{};
 		HIP_CHECK(hipMemcpy(&s, tb->st.p, sizeof(s), hipMemcpyDeviceToHost));
@@ -2000,6 +2069,15 @@ int neus_debug_scatter_stats(NeusTestbed* tb, uint64_t* records_per_level, uint3
 		if (max_region) *max_region = mx;
 	});
 }
+int neus_debug_scatter_parts(NeusTestbed* tb, uint32_t* parts_per_level) {
+	return guard([&] {
+		if (!tb->have_net || tb->swork.mode != 2) throw std::runtime_error("scatter parts: region mode only");
+		std::vector<uint32_t> jobs(4 * (size_t)tb->swork.n_jobs2);
+		HIP_CHECK(hipMemcpy(jobs.data(), tb->sc_jobs2.p, jobs.size() * 4, hipMemcpyDeviceToHost));
+		for (uint32_t l = 0; l < tb->lay.L; ++l) parts_per_level[l] = 0;
+		for (size_t j = 0; j < jobs.size() / 4; ++j) parts_per_level[jobs[4 * j]] = std::max(parts_per_level[jobs[4 * j]], jobs[4 * j + 2] >> 16);
+	});
+}
 int neus_debug_march_profile(NeusTestbed* tb, unsigned long long* out, uint32_t max_waves, uint32_t* n_waves) {
 	return guard([&] {
 		if (!tb->have_net) throw std::runtime_error("no network");
@@ -2073,10 +2151,11 @@ int neus_nccl_unique_id(uint8_t* out) {
 int neus_testbed_init_data_parallel_ex(NeusTestbed* tb, int rank, int world, const uint8_t* uid, uint32_t flags) {
 	return guard([&] {
 		if (world < 1 || rank < 0 || rank >= world) throw std::runtime_error("invalid rank/world");
-		if (tb->comm || tb->group) throw std::runtime_error("init_data_parallel: the testbed already has a communicator");
+		if (tb->comm || tb->group || tb->hgroup) throw std::runtime_error("init_data_parallel: the testbed already has a communicator");
 		HIP_CHECK(hipSetDevice(tb->device));
 		tb->rank = (uint32_t)rank; tb->world = (uint32_t)world;
 		tb->force_coll = (flags & NEUS_DP_FORCE_COLLECTIVES) != 0;
+		tb->overlap_verified = false;
 		tb->tbuf.indeed_batch = (float)tb->batch * (float)world;
 		tb->coll_calls = tb->coll_bytes = tb->coll_bytes_step = 0;
 		if (world > 1 || tb->force_coll) {
@@ -2091,6 +2170,7 @@ int neus_testbed_set_exchange_overlap(NeusTestbed* tb, int on) {
 	return guard([&] {
 		HIP_CHECK(hipStreamSynchronize(tb->stream));
 		tb->exchange_overlap = on != 0;
+		tb->overlap_verified = false;
 	});
 }
 int neus_testbed_init_data_parallel(NeusTestbed* tb, int rank, int world, const uint8_t* uid) {
@@ -2099,7 +2179,7 @@ int neus_testbed_init_data_parallel(NeusTestbed* tb, int rank, int world, const 
 int neus_testbed_data_parallel_info(NeusTestbed* tb, NeusDataParallelInfo* o) {
 	return guard([&] {
 		o->rank = tb->rank; o->world = tb->world;
-		o->has_communicator = tb->comm ? 1u : 0u; o->local_group = tb->group ? 1u : 0u;
+		o->has_communicator = tb->comm ? 1u : 0u; o->local_group = tb->group ? 1u : 0u; o->host_group = tb->hgroup ? 1u : 0u;
 		o->collective_calls = tb->coll_calls; o->allreduce_bytes = tb->coll_bytes; o->last_step_allreduce_bytes = tb->coll_bytes_step;
 	});
 }
@@ -2117,6 +2197,34 @@ int neus_testbed_init_local_group(NeusTestbed* tb, NeusLocalGroup* g, int rank) 
 		if (tb->comm) throw std::runtime_error("testbed already has an RCCL communicator");
 		tb->group = g; tb->rank = (uint32_t)rank; tb->world = g->world;
 		tb->tbuf.indeed_batch = (float)tb->batch * (float)tb->world;
+		tb->overlap_verified = false;
+	});
+}
+
+int neus_host_group_create(int rank, int world, const char* host, int port, NeusHostGroup** out) {
+	return guard([&] {
+		if (world < 1 || world > 64 || rank < 0 || rank >= world) throw std::runtime_error("host group: world must be 1..64, 0 <= rank < world");
+		if (port <= 0 || port > 65535) throw std::runtime_error("host group: invalid port");
+		*out = new NeusHostGroup(rank, world, host ? host : "127.0.0.1", port);
+	});
+}
+int neus_host_group_destroy(NeusHostGroup* g) { return guard([&] { delete g; }); }
+int neus_debug_host_group_allreduce(NeusHostGroup* g, void* host, uint64_t n, int type, int op) {
+	return guard([&] {
+		if (!g) throw std::runtime_error("invalid host group");
+		g->allreduce_host(host, (size_t)n * 4, type ? NeusHostGroup::U32 : NeusHostGroup::F32, op ? NeusHostGroup::MAX : NeusHostGroup::SUM);
+		g->check();
+	});
+}
+int neus_testbed_init_host_group(NeusTestbed* tb, NeusHostGroup* g) {
+	return guard([&] {
+		if (!g) throw std::runtime_error("invalid host group");
+		if (tb->comm || tb->group || tb->hgroup) throw std::runtime_error("init_host_group: the testbed already has a communicator");
+		HIP_CHECK(hipSetDevice(tb->device));
+		tb->hgroup = g; tb->rank = (uint32_t)g->rank; tb->world = (uint32_t)g->world;
+		tb->tbuf.indeed_batch = (float)tb->batch * (float)tb->world;
+		tb->coll_calls = tb->coll_bytes = tb->coll_bytes_step = 0;
+		tb->overlap_verified = false;
 	});
 }
 

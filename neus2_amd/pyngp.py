@@ -1214,6 +1214,25 @@ class LocalGroup:
             self._h = None
 
 
+class HostGroup:
+    """Cross-process data-parallel group (neus_host_group_create): one per rank process; rank 0 listens on host:port, the
+    others connect. The testbed's collectives are staged on its communication stream through pinned host memory and
+    exchanged over TCP (several ranks on one GPU, where RCCL refuses duplicate devices). Keep it alive while training."""
+
+    def __init__(self, rank: int, world: int, host: str = "127.0.0.1", port: int = 29533):
+        self._h = C.c_void_p()
+        check(lib().neus_host_group_create(C.c_int(rank), C.c_int(world), host.encode(), C.c_int(port), C.byref(self._h)))
+        self.rank, self.world = rank, world
+
+    def join(self, tb):
+        check(lib().neus_testbed_init_host_group(tb.handle, self._h))
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().neus_host_group_destroy(self._h)
+            self._h = None
+
+
 def nccl_unique_id() -> bytes:
     buf = (C.c_uint8 * 128)()
     check(lib().neus_nccl_unique_id(buf))

@@ -61,18 +61,26 @@ class CpuTrainer:
         self.ema_step += 1
         return mean
 
-    def grads(self, skip_occupancy=False):
-        """Everything of one step up to (not including) the optimizer; returns fp32 gradients."""
+    def march(self, skip_occupancy=False):
+        """The step's occupancy update (at the reference cadence) and generate_training_samples_nerf: the rays, per-ray
+        sample counts and NerfCoordinates the network then evaluates (no network arithmetic: independent of the sum order)."""
         step = self.training_step
         n_prep = min(16, max(1, step // 16))
         if not skip_occupancy and step % n_prep == 0:
             self.occupancy()
         if step == 0:
             self.n_rays_total = 0
-        vl = self.valid_level(step)
         R, W = self.R, self.world
         rays, ns, co, counter, nr = O.generate_samples(self.ds, self.bitfield, R, self.n_rays_total, self.rng_state, self.rng_inc,
                                                        self.max_inference, ray_offset=self.rank * R, n_rays_global=W * R)
+        return dict(rays=rays, numsteps=ns, coords=co, counter=counter, n_rays_with_samples=nr)
+
+    def grads_from_march(self, m):
+        """Network forward over every kept sample, the NeuS loss / compaction, the rollover and the network backward for
+        the samples `march` produced; returns fp32 gradients."""
+        vl = self.valid_level(self.training_step)
+        R, W = self.R, self.world
+        rays, ns, co = m["rays"], m["numsteps"], m["coords"]
         nk = int(ns[:, 0].sum())
         net = O.network_forward(self.cfg, self.params, co[:nk], vl)
         full = np.zeros((max(nk, 1), 16), np.uint16)
@@ -83,10 +91,27 @@ class CpuTrainer:
         coords_c, dout = res["coords"], res["dL_dout"]
         O.fill_rollover(self.batch, ncomp, coords_c, dout)
         g = O.network_backward(self.cfg, self.params, coords_c, vl, dout, self.batch * W) if ncomp > 0 else np.zeros_like(self.params)
-        self.last = dict(numsteps_counter=counter, compacted=res["counter"], n_kept=nk, n_rays_with_samples=nr,
+        self.last = dict(numsteps_counter=m["counter"], compacted=res["counter"], n_kept=nk, n_rays_with_samples=m["n_rays_with_samples"],
                          loss=float(res["loss"].sum()), rays=rays, numsteps=ns, coords=co[:nk], compacted_coords=coords_c[:ncomp],
-                         dL_dout=dout[:ncomp])
+                         dL_dout=dout[:ncomp], ray_ncomp=res["numsteps"][:, 0])
         return g
+
+    def grads(self, skip_occupancy=False):
+        """Everything of one step up to (not including) the optimizer; returns fp32 gradients."""
+        return self.grads_from_march(self.march(skip_occupancy))
+
+    def grads_alt_orders(self, m, orders=("reversed", "pairwise", "blocked")):
+        """The same step's gradients with the network's layer products summed in each alternative order (the oracle's own
+        spread: the noise floor of the fp16 network). self.last is left as the index-order step set it."""
+        last, out = self.last, {}
+        try:
+            for o in orders:
+                O.set_sum_order(o)
+                out[o] = self.grads_from_march(m)
+        finally:
+            O.set_sum_order("index")
+            self.last = last
+        return out
 
     def finish(self, g, counters_sum=None):
         """Counters update (testbed_nerf.cu:3399-3438), RNG advance and the Ema(Adam) step."""

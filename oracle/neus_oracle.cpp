@@ -32,51 +32,16 @@
 #include <vector>
 #ifdef _OPENMP
 #include <omp.h>
+#include <immintrin.h>
 #endif
 
 namespace {
 
 // ---------------------------------------------------------------- half helpers
-static inline uint16_t f2h(float f) {
-	uint32_t x; std::memcpy(&x, &f, 4);
-	uint32_t sign = (x >> 16) & 0x8000u;
-	uint32_t exp = (x >> 23) & 0xffu;
-	uint32_t man = x & 0x7fffffu;
-	if (exp == 0xff) return (uint16_t)(sign | 0x7c00u | (man ? 0x200u : 0u));
-	int e = (int)exp - 127 + 15;
-	if (e >= 31) return (uint16_t)(sign | 0x7c00u);
-	if (e <= 0) {
-		if (e < -10) return (uint16_t)sign;
-		man |= 0x800000u;
-		uint32_t shift = (uint32_t)(14 - e);
-		uint32_t hm = man >> shift;
-		uint32_t rem = man & ((1u << shift) - 1u);
-		uint32_t half = 1u << (shift - 1u);
-		if (rem > half || (rem == half && (hm & 1u))) ++hm;
-		return (uint16_t)(sign | hm);
-	}
-	uint32_t hm = man >> 13;
-	uint32_t rem = man & 0x1fffu;
-	uint32_t out = sign | ((uint32_t)e << 10) | hm;
-	if (rem > 0x1000u || (rem == 0x1000u && (hm & 1u))) ++out;
-	return (uint16_t)out;
-}
-static inline float h2f(uint16_t h) {
-	uint32_t sign = (uint32_t)(h & 0x8000u) << 16;
-	uint32_t exp = (h >> 10) & 0x1fu;
-	uint32_t man = h & 0x3ffu;
-	uint32_t x;
-	if (exp == 0) {
-		if (man == 0) x = sign;
-		else {
-			int e = -1;
-			do { man <<= 1; ++e; } while (!(man & 0x400u));
-			x = sign | ((uint32_t)(127 - 15 - e) << 23) | ((man & 0x3ffu) << 13);
-		}
-	} else if (exp == 31) x = sign | 0x7f800000u | (man << 13);
-	else x = sign | ((exp + 127 - 15) << 23) | (man << 13);
-	float f; std::memcpy(&f, &x, 4); return f;
-}
+// F16C conversions (round to nearest even, subnormals kept): the same results as a bit-level IEEE restatement, and
+// the oracle's hottest operation (every fp16 storage point of the reference is a round trip through them).
+static inline uint16_t f2h(float f) { return (uint16_t)_cvtss_sh(f, _MM_FROUND_TO_NEAREST_INT); }
+static inline float h2f(uint16_t h) { return _cvtsh_ss(h); }
 static inline float rh(float f) { return h2f(f2h(f)); }
 
 // --------------------------------------------- pcg32 (my_tcnn pcg32.h:43-170)
@@ -467,27 +432,81 @@ static void sh4(const float wd[3], float* out) {
 	out[15] = 0.59004358992664352f * x * (-x2 + 3.0f * y2);
 }
 
-// Summation order of the layer products (or_set_sum_order): 0 = index order (the oracle), 1 = reversed. Test-only: the
-// reversed oracle measures how far the fp32 accumulation order alone moves a training step (fp16 activations flipping
-// at rounding boundaries), the noise floor against which the device's MFMA-ordered sums are compared.
-static int g_sum_reverse = 0;
+// Summation order of the layer products (or_set_sum_order). Test-only: 0 = index order (the oracle); 1 = reversed,
+// 2 = pairwise (recursive halves), 3 = blocked (sequential blocks of 8, then the block sums in order). The alternative
+// orders measure how far the fp32 accumulation order alone moves a training step (fp16 activations flipping at
+// rounding boundaries): the noise floor against which the device's MFMA-ordered sums are compared.
+static int g_sum_order = 0;
+static float sum_pairwise(const float* p, uint32_t n) {
+	if (n == 1) return p[0];
+	if (n == 2) return p[0] + p[1];
+	const uint32_t h = n / 2;
+	return sum_pairwise(p, h) + sum_pairwise(p + h, n - h);
+}
+// sum of the products p[0..n) in the active alternative order (g_sum_order != 0)
+static float sum_ordered(const float* p, uint32_t n) {
+	if (n == 0) return 0.0f;
+	float s = 0;
+	switch (g_sum_order) {
+	case 1: for (uint32_t i = n; i-- > 0;) s += p[i]; return s;
+	case 2: return sum_pairwise(p, n);
+	case 3: {
+		for (uint32_t b0 = 0; b0 < n; b0 += 8) {
+			float bs = 0;
+			for (uint32_t i = b0; i < std::min(n, b0 + 8); ++i) bs += p[i];
+			s += bs;
+		}
+		return s;
+	}
+	default: for (uint32_t i = 0; i < n; ++i) s += p[i]; return s;
+	}
+}
 // y = W x with W RM [out][in] (fp16-rounded weights), fp32 accumulation.
 static inline void matvec(const float* W, uint32_t out, uint32_t in, const float* x, float* y) {
 	for (uint32_t o = 0; o < out; ++o) {
-		float s = 0; const float* w = W + (size_t)o * in;
-		if (g_sum_reverse) for (uint32_t i = in; i-- > 0;) s += w[i] * x[i];
-		else for (uint32_t i = 0; i < in; ++i) s += w[i] * x[i];
+		const float* w = W + (size_t)o * in;
+		if (g_sum_order) {
+			float p[64];
+			for (uint32_t i = 0; i < in; ++i) p[i] = w[i] * x[i];
+			y[o] = sum_ordered(p, in);
+			continue;
+		}
+		if (o + 8 <= out) {  // eight independent index-order chains (the same sums, not latency-bound)
+			float s8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+			for (uint32_t i = 0; i < in; ++i)
+				for (int j = 0; j < 8; ++j) s8[j] += w[(size_t)j * in + i] * x[i];
+			for (int j = 0; j < 8; ++j) y[o + j] = s8[j];
+			o += 7;
+			continue;
+		}
+		float s = 0;
+		for (uint32_t i = 0; i < in; ++i) s += w[i] * x[i];
 		y[o] = s;
 	}
 }
 // y = W^T d
 static inline void matvec_t(const float* W, uint32_t out, uint32_t in, const float* d, float* y) {
-	for (uint32_t i = 0; i < in; ++i) y[i] = 0;
-	if (g_sum_reverse) {
-		for (uint32_t o = out; o-- > 0;) { const float* w = W + (size_t)o * in; for (uint32_t i = 0; i < in; ++i) y[i] += w[i] * d[o]; }
+	if (g_sum_order) {
+		for (uint32_t i = 0; i < in; ++i) {
+			float p[64];
+			for (uint32_t o = 0; o < out; ++o) p[o] = W[(size_t)o * in + i] * d[o];
+			y[i] = sum_ordered(p, out);
+		}
 		return;
 	}
+	for (uint32_t i = 0; i < in; ++i) y[i] = 0;
 	for (uint32_t o = 0; o < out; ++o) { const float* w = W + (size_t)o * in; for (uint32_t i = 0; i < in; ++i) y[i] += w[i] * d[o]; }
+}
+// sum_k a[k] * b[stride * k] over n terms (the grid-input gradients' sums over the 2L features)
+static inline float dot_strided(const float* a, const float* b, uint32_t stride, uint32_t n) {
+	if (g_sum_order) {
+		float p[64];
+		for (uint32_t k = 0; k < n; ++k) p[k] = a[k] * b[stride * k];
+		return sum_ordered(p, n);
+	}
+	float s = 0;
+	for (uint32_t k = 0; k < n; ++k) s += a[k] * b[stride * k];
+	return s;
 }
 
 // Per-sample forward context (NerfNetwork::ForwardContext, nerf_network.h:1297-1315).
@@ -533,8 +552,7 @@ static void net_forward_one(const Net& n, const float* P, const float* coord, ui
 	{ float t[64]; matvec_t(P + n.dl[0].offset, nout, c.density_in, dcur, t); for (uint32_t i = 0; i < c.density_in; ++i) cx.gin[i] = rh(t[i]); }
 	// kernel_grid_backward_input (grid.h:803-830) then identity path add (nerf_network.h:249-251)
 	for (int d = 0; d < 3; ++d) {
-		float s = 0;
-		for (uint32_t k = 0; k < 2 * L; ++k) s += cx.gin[3 + k] * cx.dydx[3 * k + d];
+		const float s = dot_strided(cx.gin + 3, cx.dydx + d, 3, 2 * L);
 		cx.grad_sdf[d] = s + cx.gin[d];
 	}
 	// rgb input: [density_out(16), SH(16), xyz(3), grad_sdf(3), 0...] (nerf_network.h:262-280)
@@ -563,8 +581,10 @@ static void net_forward_one(const Net& n, const float* P, const float* coord, ui
 
 // Weight-gradient accumulation target: double per param.
 // NerfNetwork::backward_impl (nerf_network.h:330-601) for one sample.
+// G: the matrix-parameter gradients, private to the calling thread (plain adds); Ggrid: the shared grid gradient (atomic)
 static void net_backward_one(const Net& n, const float* P, const float* coord, uint32_t valid_level, const Ctx& cx,
-                             const uint16_t* dout16, float indeed_batch, double* G, double* var_grad_acc, float* dpos_out = nullptr) {
+                             const uint16_t* dout16, float indeed_batch, double* G, double* Ggrid, double* var_grad_acc,
+                             float* dpos_out = nullptr) {
 	const OrNetCfg& c = n.c;
 	const uint32_t W = c.width, L = c.n_levels;
 	float dLo[16]; for (int k = 0; k < 16; ++k) dLo[k] = h2f(dout16[k]);
@@ -577,7 +597,7 @@ static void net_backward_one(const Net& n, const float* P, const float* coord, u
 		for (uint32_t o = 0; o < ly.out; ++o) {
 			if (dcur[o] == 0.0f) continue;
 			double* g = G + ly.offset + (size_t)o * ly.in;
-			for (uint32_t i = 0; i < ly.in; ++i) atomic_add_d(&g[i], (double)dcur[o] * act[i]);
+			for (uint32_t i = 0; i < ly.in; ++i) g[i] += (double)dcur[o] * act[i];
 		}
 		float t[64]; matvec_t(P + ly.offset, nout, ly.in, dcur, t);
 		if (li > 0) { for (uint32_t i = 0; i < W; ++i) dcur[i] = rh(cx.rh_[li - 1][i] > 0 ? t[i] : 0.0f); nout = W; }
@@ -595,20 +615,19 @@ static void net_backward_one(const Net& n, const float* P, const float* coord, u
 		for (uint32_t o = 0; o < ly.out; ++o) {
 			if (dcur[o] == 0.0f) continue;
 			double* g = G + ly.offset + (size_t)o * ly.in;
-			for (uint32_t i = 0; i < ly.in; ++i) atomic_add_d(&g[i], (double)dcur[o] * act[i]);
+			for (uint32_t i = 0; i < ly.in; ++i) g[i] += (double)dcur[o] * act[i];
 		}
 		float t[64]; matvec_t(P + ly.offset, nout, ly.in, dcur, t);
 		if (li > 0) { for (uint32_t i = 0; i < W; ++i) dcur[i] = rh(cx.dh[li - 1][i] > 0 ? t[i] : 0.0f); nout = W; }
 		else { for (uint32_t i = 0; i < ly.in; ++i) dL_ddin[i] = rh(t[i]); }
 	}
 	// variance gradient = batch sum of dL_dout[7] (nerf_network.h:461-474)
-	atomic_add_d(var_grad_acc, (double)dLo[7]);
+	*var_grad_acc += (double)dLo[7];
 	// dL/d(position) for the DeltaNetwork (nerf_network.h:602-631): grid input gradient (kernel_grid_backward_input
 	// of dL/denc) + rgb input xyz rows + density input xyz rows
 	if (dpos_out)
 		for (int d = 0; d < 3; ++d) {
-			float s = 0;
-			for (uint32_t k = 0; k < 2 * L; ++k) s += dL_ddin[3 + k] * cx.dydx[3 * k + d];
+			const float s = dot_strided(dL_ddin + 3, cx.dydx + d, 3, 2 * L);
 			dpos_out[d] = (s + dL_drin[32 + d]) + dL_ddin[d];
 		}
 	// v = dL/d(grad_sdf): rgb-input rows 35..37 + eikonal/indeed_batch + bent-dir rows 8..10 (nerf_network.h:478-504)
@@ -619,7 +638,7 @@ static void net_backward_one(const Net& n, const float* P, const float* coord, u
 		v[d] += dLo[8 + d];
 	}
 	// grid gradients: first order (dL/denc) + second order (g = dSDF/denc, v) (nerf_network.h:423-442, 547-557)
-	grid_scatter_one(n, coord, valid_level, dL_ddin + 3, cx.gin + 3, v, G + n.grid_off);
+	grid_scatter_one(n, coord, valid_level, dL_ddin + 3, cx.gin + 3, v, Ggrid);
 	// pos_encoding_dy = dy/dx . v (grid.h:1182-1207), stored half
 	float u[64]; for (uint32_t k = 0; k < c.density_in; ++k) u[k] = 0;
 	for (int d = 0; d < 3; ++d) u[d] = rh(v[d]);
@@ -629,30 +648,28 @@ static void net_backward_one(const Net& n, const float* P, const float* coord, u
 	}
 	// FullyFusedMLP::backward_backward_input (fully_fused_mlp.cu:1088-1198), 1 hidden layer form
 	// front: hf_i = relu'(h_{i-1}) . (W_{i-1} hf_{i-1}), hf_0 = u ; back: b_i = relu'(h) . (W^T b_{i+1}), b_top = e0
-	std::vector<std::vector<float>> front(n.dl.size());
-	front[0].assign(u, u + c.density_in);
+	constexpr size_t MAXL = 8;  // density layers (n_density_hidden + 1)
+	float front[MAXL][64], back[MAXL + 1][64];
+	std::copy(u, u + c.density_in, front[0]);
 	for (size_t li = 1; li < n.dl.size(); ++li) {
 		const auto& ly = n.dl[li - 1];
-		float t[64]; matvec(P + ly.offset, ly.out, ly.in, front[li - 1].data(), t);
-		front[li].resize(ly.out);
+		float t[64]; matvec(P + ly.offset, ly.out, ly.in, front[li - 1], t);
 		for (uint32_t o = 0; o < ly.out; ++o) front[li][o] = rh(cx.dh[li - 1][o] > 0 ? t[o] : 0.0f);
 	}
-	std::vector<std::vector<float>> back(n.dl.size() + 1);
-	back[n.dl.size()].assign(16, 0.0f); back[n.dl.size()][0] = 1.0f;
+	std::fill(back[n.dl.size()], back[n.dl.size()] + 16, 0.0f); back[n.dl.size()][0] = 1.0f;
 	for (int li = (int)n.dl.size() - 1; li >= 1; --li) {
 		const auto& ly = n.dl[li];
-		float t[64]; matvec_t(P + ly.offset, ly.out, ly.in, back[li + 1].data(), t);
-		back[li].resize(ly.in);
+		float t[64]; matvec_t(P + ly.offset, ly.out, ly.in, back[li + 1], t);
 		for (uint32_t i = 0; i < ly.in; ++i) back[li][i] = rh(cx.dh[li - 1][i] > 0 ? t[i] : 0.0f);
 	}
 	for (size_t li = 0; li < n.dl.size(); ++li) {
 		const auto& ly = n.dl[li];
-		const std::vector<float>& bk = back[li + 1];
-		const std::vector<float>& fr = front[li];
+		const float* bk = back[li + 1];
+		const float* fr = front[li];
 		for (uint32_t o = 0; o < ly.out; ++o) {
 			if (bk[o] == 0.0f) continue;
 			double* g = G + ly.offset + (size_t)o * ly.in;
-			for (uint32_t i = 0; i < ly.in; ++i) atomic_add_d(&g[i], (double)bk[o] * fr[i]);
+			for (uint32_t i = 0; i < ly.in; ++i) g[i] += (double)bk[o] * fr[i];
 		}
 	}
 }
@@ -664,7 +681,7 @@ struct SampleRay { float o[3], d[3]; };  // Ray (unnormalized direction)
 extern "C" {
 
 uint32_t or_net_n_params(const OrNetCfg* c) { Net n(*c); return n.n_params; }
-void or_set_sum_order(int reverse) { g_sum_reverse = reverse ? 1 : 0; }
+void or_set_sum_order(int order) { g_sum_order = order; }
 void or_net_layout(const OrNetCfg* c, uint32_t* out) {
 	Net n(*c);
 	out[0] = n.n_density; out[1] = n.n_rgb; out[2] = n.grid_off; out[3] = n.n_grid_params; out[4] = n.var_off; out[5] = n.n_params; out[6] = n.n_matrix;
@@ -792,41 +809,50 @@ void or_network_forward_debug(const OrNetCfg* c, const float* params, const floa
 	for (int k = 0; k < 16; ++k) { dout16[k] = cx.dout[k]; rout16[k] = cx.rout[k]; }
 }
 
+// The matrix gradients accumulate per thread in double (plain adds) and are summed in thread order; the grid gradient
+// (10 M entries) is shared, with atomic double adds.
+static void network_backward_impl(const OrNetCfg* c, const float* params, uint32_t n_el, const float* coords, uint32_t valid_level,
+                                  const uint16_t* dL_dout, uint32_t indeed_batch_size, float* grads, float* dpos) {
+	Net n(*c);
+	std::vector<float> P = half_params(n, params);
+	std::vector<double> G(n.n_params, 0.0);
+	const int nt = omp_get_max_threads();
+	std::vector<std::vector<double>> Gm(nt);
+	std::vector<double> var_acc(nt, 0.0);
+#pragma omp parallel
+	{
+		const int tid = omp_get_thread_num();
+		Gm[tid].assign(n.n_matrix, 0.0);
+#pragma omp for schedule(dynamic, 64)
+		for (int64_t i = 0; i < (int64_t)n_el; ++i) {
+			Ctx cx; net_forward_one(n, P.data(), coords + 7 * i, valid_level, cx, nullptr);
+			if (dpos) dpos[4 * i + 3] = 0.f;
+			net_backward_one(n, P.data(), coords + 7 * i, valid_level, cx, dL_dout + 16 * i, (float)indeed_batch_size, Gm[tid].data(),
+			                 G.data() + n.grid_off, &var_acc[tid], dpos ? dpos + 4 * i : nullptr);
+		}
+	}
+	double var = 0.0;
+	for (int t = 0; t < nt; ++t) {
+		var += var_acc[t];
+		if (Gm[t].empty()) continue;
+		for (uint32_t i = 0; i < n.n_matrix; ++i) G[i] += Gm[t][i];
+	}
+	for (uint32_t i = 0; i < n.n_params; ++i) grads[i] = (float)G[i];
+	grads[n.var_off] = rh((float)var);
+	for (int k = 1; k < 4; ++k) grads[n.var_off + k] = 0.0f;
+}
+
 // NerfNetwork::forward + backward (Overwrite) on n compacted coords with dL/doutput (AoS 16 halves).
 // grads (n_params floats) is overwritten; variance grad = half(sum dL_dout[7]) (nerf_network.h:461-474).
 void or_network_backward(const OrNetCfg* c, const float* params, uint32_t n_el, const float* coords, uint32_t valid_level,
                          const uint16_t* dL_dout, uint32_t indeed_batch_size, float* grads) {
-	Net n(*c);
-	std::vector<float> P = half_params(n, params);
-	std::vector<double> G(n.n_params, 0.0);
-	double var_acc = 0.0;
-	const float inv_b = (float)indeed_batch_size;
-#pragma omp parallel for schedule(dynamic, 64)
-	for (int64_t i = 0; i < (int64_t)n_el; ++i) {
-		Ctx cx; net_forward_one(n, P.data(), coords + 7 * i, valid_level, cx, nullptr);
-		net_backward_one(n, P.data(), coords + 7 * i, valid_level, cx, dL_dout + 16 * i, inv_b, G.data(), &var_acc);
-	}
-	for (uint32_t i = 0; i < n.n_params; ++i) grads[i] = (float)G[i];
-	grads[n.var_off] = rh((float)var_acc);
-	for (int k = 1; k < 4; ++k) grads[n.var_off + k] = 0.0f;
+	network_backward_impl(c, params, n_el, coords, valid_level, dL_dout, indeed_batch_size, grads, nullptr);
 }
 
 // or_network_backward plus dL/d(position) per sample (dpos: 4 floats per sample, the 4th 0).
 void or_network_backward_pos(const OrNetCfg* c, const float* params, uint32_t n_el, const float* coords, uint32_t valid_level,
                              const uint16_t* dL_dout, uint32_t indeed_batch_size, float* grads, float* dpos) {
-	Net n(*c);
-	std::vector<float> P = half_params(n, params);
-	std::vector<double> G(n.n_params, 0.0);
-	double var_acc = 0.0;
-#pragma omp parallel for schedule(dynamic, 64)
-	for (int64_t i = 0; i < (int64_t)n_el; ++i) {
-		Ctx cx; net_forward_one(n, P.data(), coords + 7 * i, valid_level, cx, nullptr);
-		dpos[4 * i + 3] = 0.f;
-		net_backward_one(n, P.data(), coords + 7 * i, valid_level, cx, dL_dout + 16 * i, (float)indeed_batch_size, G.data(), &var_acc, dpos + 4 * i);
-	}
-	for (uint32_t i = 0; i < n.n_params; ++i) grads[i] = (float)G[i];
-	grads[n.var_off] = rh((float)var_acc);
-	for (int k = 1; k < 4; ++k) grads[n.var_off + k] = 0.0f;
+	network_backward_impl(c, params, n_el, coords, valid_level, dL_dout, indeed_batch_size, grads, dpos);
 }
 
 // -------------------------------------------------------------------------------------------

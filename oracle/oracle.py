@@ -289,10 +289,16 @@ def num_threads():
     return lib().or_num_threads()
 
 
-def set_sum_order(reverse: bool):
-    """Layer products summed in reversed index order (True) or index order (False, the default): test-only, to measure
-    how much the fp32 accumulation order alone moves a step (the noise floor of the fp16 network)."""
-    lib().or_set_sum_order(C.c_int(1 if reverse else 0))
+SUM_ORDERS = {"index": 0, "reversed": 1, "pairwise": 2, "blocked": 3}
+
+
+def set_sum_order(order):
+    """Order in which the layer products are summed: "index" (the default), "reversed", "pairwise" (recursive halves) or
+    "blocked" (blocks of 8, then the block sums); True / False mean reversed / index. Test-only: the alternative orders
+    measure how much the fp32 accumulation order alone moves a step (the noise floor of the fp16 network)."""
+    if isinstance(order, bool):
+        order = "reversed" if order else "index"
+    lib().or_set_sum_order(C.c_int(SUM_ORDERS[order] if isinstance(order, str) else int(order)))
 
 
 class OrRenderCamera(C.Structure):
