@@ -334,6 +334,10 @@ int neus_debug_scan_giveup(void* hip_stream, const uint32_t* in, uint32_t* out, 
 int neus_debug_inject_health(NeusTestbed* tb, uint32_t flags);
 /* Test hook: every training step fills every CU's LDS with `pattern` (0: off) before its march write kernel. */
 int neus_debug_set_lds_fill(NeusTestbed* tb, uint32_t pattern);
+/* Test hook: every training step fills every CU's LDS with `pattern` (its complement on odd steps; 0: off) before each of
+ * the step's kernels, so a kernel that read LDS it had not written in its own launch would change the results (the
+ * determinism test of the whole step: tests/test_gpu_determinism.py). */
+int neus_debug_set_lds_fill_all(NeusTestbed* tb, uint32_t pattern);
 /* neus_sample_rays (rank 0 of 1) plus the progressive round-0 work list the training step's march writes (the first
  * min(n, chunk_end) samples of every kept ray, in ray order; list: device, max_samples u32, list_len: host u32), with
  * lds_fill != 0 every CU's LDS filled with that pattern between the scan and the write kernel (stale-LDS test). */

@@ -780,6 +780,7 @@ void launch_grid_encode(hipStream_t s, const uint32_t* n_ptr, uint32_t n_fixed, 
                         const EncodeRollover* ro) {
 	if (!grid_x) return;
 	const EncodeRollover r = ro ? *ro : EncodeRollover{nullptr, 0u, nullptr, nullptr};
+	dbg_lds_gate(s);
 	k_grid_encode<<<dim3(grid_x, gl.n_levels), 256, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, grid, enc, dydx, r);
 }
 size_t scatter_records_capacity(uint32_t n_cap, uint32_t n_levels) { return (size_t)n_cap * n_levels * 8; }
@@ -832,6 +833,7 @@ void launch_grid_scatter(hipStream_t s, const uint32_t* n_ptr, uint32_t n_fixed,
 		// contributions, bucket count, scan, stage, region write) of different workgroups overlap on a CU
 		const uint32_t n_lv = std::min(gl.n_levels, valid_level + 1);
 		const dim3 grid(w.n_chunks, w.level_groups ? std::min(w.level_groups, n_lv) : n_lv);
+		dbg_lds_gate(s);
 		if (w.chunk == 1024)
 			k_scatter_bin_r<1024><<<grid, 1024, 0, s>>>(n_ptr, n_fixed, ld, coords, coord_stride, gl, valid_level, (const uint32_t*)dLdenc,
 			                                            (const uint32_t*)g, v, w);
@@ -844,6 +846,7 @@ void launch_grid_scatter(hipStream_t s, const uint32_t* n_ptr, uint32_t n_fixed,
 		const uint32_t n_act = std::min(valid_level + 1, gl.n_levels);
 		if (!split) {
 			const uint32_t nj = std::min(w.n_jobs2, w.jobs2_before[n_act]);
+			dbg_lds_gate(s);
 			if (nj) k_scatter_accum_r<<<accum_blocks(nj, w.xcd_group), 64 * SC_WAVES, 0, s>>>(w, gl, grads, w.chunk * 8, 0u, nj, w.xcd_group);
 			return;
 		}
@@ -852,6 +855,7 @@ void launch_grid_scatter(hipStream_t s, const uint32_t* n_ptr, uint32_t n_fixed,
 			const uint32_t hi = gi + 1 == split->n_groups ? n_act : std::min(split->level_end[gi], n_act);
 			if (hi <= lo) continue;
 			const uint32_t j0 = std::min(w.n_jobs2, w.jobs2_before[lo]), j1 = std::min(w.n_jobs2, w.jobs2_before[hi]);
+			dbg_lds_gate(s);
 			if (j1 > j0)
 				k_scatter_accum_r<<<accum_blocks(j1 - j0, w.xcd_group), 64 * SC_WAVES, 0, s>>>(w, gl, grads, w.chunk * 8, j0, j1 - j0, w.xcd_group);
 			if (split->done) split->done(lo, hi);

@@ -315,6 +315,14 @@ void launch_march_write(hipStream_t s, uint32_t cap, StepState* st, const DevDat
                         const Round0List* round0 = nullptr, uint32_t lds_fill = 0 /* tests: garbage-fill LDS before the write kernel */);
 constexpr uint32_t FILL_LDS_BYTES = 40 * 1024;
 void launch_fill_lds(hipStream_t s, uint32_t pattern);
+// Determinism test hook (neus_debug_set_lds_fill_all): while the calling host thread runs a training step with it set,
+// every CU's LDS is filled with this pattern before each kernel of the step (the launchers call dbg_lds_gate before their
+// launches), so a kernel that read LDS it had not written in this launch would read garbage and change the step's
+// results. 0 (always, outside the tests): no fill.
+extern thread_local uint32_t g_dbg_lds_fill;
+inline void dbg_lds_gate(hipStream_t s) {
+	if (g_dbg_lds_fill) launch_fill_lds(s, g_dbg_lds_fill);
+}
 void debug_launch_march_stats(hipStream_t s, uint32_t n_rays, const float* rays, const float* tstart, const uint32_t* lin, const DevDataset& ds,
                               const uint8_t* bf, uint32_t* out);
 // dt_const: every sample's dt is MIN_CONE_STEPSIZE (cone angle 0, coordinates from k_march_write): the kernel

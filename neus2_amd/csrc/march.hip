@@ -959,8 +959,10 @@ uint32_t ray_sort_blocks(uint32_t cap) { return std::max<uint32_t>(1, (cap + RS_
 void launch_ray_sort(hipStream_t s, uint32_t cap, const uint32_t* numsteps, const float* coords, uint32_t e1, const RaySort& rs, uint32_t* list,
                      uint32_t* list_len, void* scan_temp, size_t scan_temp_bytes) {
 	const uint32_t nblk = ray_sort_blocks(cap);
+	dbg_lds_gate(s);
 	k_ray_hist<<<nblk, RS_RPB, 0, s>>>(cap, numsteps, coords, e1, rs);
 	launch_exclusive_scan(s, scan_temp, scan_temp_bytes, rs.hist, rs.off, 2 * RS_NB * nblk);
+	dbg_lds_gate(s);
 	k_ray_sort_place<<<nblk, RS_RPB, 0, s>>>(cap, numsteps, e1, rs, list, list_len);
 }
 
@@ -1543,11 +1545,13 @@ void launch_march_count(hipStream_t s, uint32_t cap, uint32_t max_samples, StepS
                         const uint32_t* lin, uint64_t rng_state, uint64_t rng_inc, float* rays, float* tstart, uint32_t* nreq, const MarchWork& mw,
                         uint32_t* zero_counters, uint32_t n_zero, const float* occ_bbox) {
 	if (n_zero > 256) throw std::runtime_error("launch_march_count: at most 256 counters to zero");
+	dbg_lds_gate(s);
 	k_ray_gen<<<ray_blocks(cap), 256, 0, s>>>(cap, st, dp, ds, rng_state, rng_inc, rays, tstart, mw.counter, st, mw.jt, zero_counters,
 	                                          zero_counters ? n_zero : 0u, occ_bbox);
 	const uint32_t waves = mw.waves ? std::min(mw.waves, (cap + 63) / 64) : (cap + 63) / 64;
 	const uint32_t blocks = std::max<uint32_t>(1, (waves + 3) / 4);
 	for (uint32_t pass = 0; pass < 2; ++pass) {
+		dbg_lds_gate(s);
 		if (ds.cone_angle == 0.0f) {
 			if (mw.lanes_per_ray == 1) k_march<true, 1><<<blocks, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, lin, rays, tstart, nreq, mw);
 			else if (mw.lanes_per_ray == 8 && mw.balanced) k_march_bal<<<blocks * 8, 256, 0, s>>>(cap, pass, max_samples, st, ds, bitfield, lin, rays, tstart, nreq, mw);
@@ -1569,6 +1573,7 @@ __global__ void __launch_bounds__(256) k_fill_lds(uint32_t pattern) {
 	volatile uint32_t* v = s_fill;
 	for (uint32_t i = threadIdx.x; i < FILL_LDS_BYTES / 4; i += 256) v[i] = pattern;
 }
+thread_local uint32_t g_dbg_lds_fill = 0;
 void launch_fill_lds(hipStream_t s, uint32_t pattern) {
 	// 40 KB per workgroup, 4 resident per CU: the whole 160 KB of every CU (256 CUs), twice over
 	k_fill_lds<<<2048, 256, FILL_LDS_BYTES, s>>>(pattern);
@@ -1582,8 +1587,10 @@ void launch_march_write(hipStream_t s, uint32_t cap, StepState* st, const DevDat
 		throw std::runtime_error("launch_march_write: ray buffers must be 16-B aligned, cap a multiple of 4");
 	const uint32_t tiles = (cap + SCAN_TILE - 1) / SCAN_TILE;
 	if (tiles > SCAN_MAX_TILES) throw std::runtime_error("launch_march_write: too many ray slots");
+	dbg_lds_gate(s);
 	k_march_scan<<<tiles, SCAN_THREADS, 0, s>>>(cap, st, nreq, base, numsteps, (ScanState*)scan_temp, scan_next_tag(scan_temp), r0);
 	if (lds_fill) launch_fill_lds(s, lds_fill);  // tests: the write kernel finds garbage in every CU's LDS
+	else dbg_lds_gate(s);
 	// one block per WRITE_CHUNK samples of the largest possible kept extent (max_inference <= sample_cap)
 	k_march_write<<<std::max<uint32_t>(1, (sample_cap + WRITE_CHUNK - 1) / WRITE_CHUNK), 256, 0, s>>>(cap, st, ds, rays, mw, nreq, base, coords, sample_ray,
 	                                                                                                      r0);
@@ -1595,16 +1602,19 @@ void debug_launch_march_stats(hipStream_t s, uint32_t n_rays, const float* rays,
 static inline uint32_t sample_blocks(uint32_t cap) { return std::max<uint32_t>(1, std::min<uint32_t>((cap + 255) / 256, 16384)); }
 void launch_loss_alpha(hipStream_t s, uint32_t cap_samples, const StepState* st, const float* coords, const half_t* net_out, float cos_anneal,
                        const LossWork& w, bool dt_const) {
+	dbg_lds_gate(s);
 	k_loss_alpha<<<sample_blocks(cap_samples), 256, 0, s>>>(cap_samples, &st->n_kept, nullptr, coords, net_out, cos_anneal, w.sa, w.ekt, w.n_long,
 	                                                        dt_const);
 }
 void launch_loss_alpha_list(hipStream_t s, uint32_t cap_samples, const uint32_t* n_ptr, const uint32_t* idx, const float* coords,
                             const half_t* net_out, float cos_anneal, const LossWork& w, bool dt_const) {
+	dbg_lds_gate(s);
 	k_loss_alpha<<<sample_blocks(cap_samples), 256, 0, s>>>(cap_samples, n_ptr, idx, coords, net_out, cos_anneal, w.sa, w.ekt, nullptr, dt_const);
 }
 void launch_loss_scan_chunk(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, const LossWork& w, uint32_t* ccount, uint32_t e0,
                             uint32_t e1, uint32_t e2, uint32_t* list, uint32_t* next_counter, const uint32_t* rays_in, const uint32_t* n_rays_in,
                             uint32_t* rays_out, uint32_t* n_rays_out) {
+	dbg_lds_gate(s);
 	k_loss_scan_chunk<<<std::max<uint32_t>(1, std::min<uint32_t>((cap_rays + 63) / 64, 8192)), 64, 0, s>>>(
 		cap_rays, numsteps, w.sa, w.ekt, w.ck4, w.cke, ccount, w.racc, w.rT, w.rek, e0, e1, e2, list, next_counter, rays_in, n_rays_in,
 		rays_out, n_rays_out);
@@ -1612,8 +1622,10 @@ void launch_loss_scan_chunk(hipStream_t s, uint32_t cap_rays, const uint32_t* nu
 // w.n_long is zeroed by the k_loss_alpha launch before it
 void launch_loss_scan_ray(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, const LossWork& w, uint32_t* ccount) {
 	const uint32_t blocks = ray_blocks(cap_rays);
+	dbg_lds_gate(s);
 	k_loss_scan_ray<true><<<blocks, 256, 0, s>>>(cap_rays, numsteps, w.sa, w.ekt, w.ck4, w.cke, ccount, w.racc, w.rT, w.long_rays, w.n_long);
 	// the long rays, 64 to a one-wave block
+	if (w.long_rays) dbg_lds_gate(s);
 	if (w.long_rays) k_loss_scan_list<<<std::max<uint32_t>(1, std::min<uint32_t>((cap_rays + 63) / 64, 4096)), 64, 0, s>>>(
 		numsteps, w.sa, w.ekt, w.ck4, w.cke, ccount, w.racc, w.rT, w.long_rays, w.n_long);
 }
@@ -1630,12 +1642,14 @@ void debug_launch_loss_scan(hipStream_t s, int variant, uint32_t cap_rays, const
 void launch_loss_ray(hipStream_t s, uint32_t cap_rays, StepState* st, DPInfo dp, const DevDataset& ds, const LossParams& lp, uint32_t* numsteps,
                      const uint32_t* ccount, const uint32_t* cbase, const LossWork& w, float* loss, float* ek, float* mask) {
 	if (!w.cmap) throw std::runtime_error("launch_loss_ray: LossWork::cmap (max_compacted entries) is required");
+	dbg_lds_gate(s);
 	k_loss_ray<<<ray_blocks(cap_rays), 256, 0, s>>>(cap_rays, st, dp, ds, lp, numsteps, ccount, cbase, w.sa, w.ekt, w.ck4, w.cke, w.racc, w.rT,
 	                                                  w.rgr, loss, ek, mask, w.cmap);
 }
 void launch_loss_grad(hipStream_t s, uint32_t cap_samples, const StepState* st, DPInfo dp, const LossParams& lp, const float* coords,
                       const half_t* net_out, const uint32_t* numsteps, const LossWork& w, float* coords_out, half_t* dL_dout) {
 	(void)cap_samples;  // (the compacted samples: at most lp.max_compacted)
+	dbg_lds_gate(s);
 	k_loss_grad<<<sample_blocks(lp.max_compacted), 256, 0, s>>>(st, dp, lp, coords, net_out, numsteps, w.cmap, w.rbase, w.sa,
 	                                                         w.ekt, w.ck4, w.cke, w.racc, w.rgr, coords_out, dL_dout);
 }
@@ -1647,6 +1661,7 @@ void launch_rollover(hipStream_t s, uint32_t n_elements, const StepState* st, fl
 }
 void launch_step_counters(hipStream_t s, StepState* st, uint32_t target_batch, uint32_t max_samples, uint32_t world, uint32_t fixed_rays,
                           const uint32_t* eval_cnt, uint32_t n_eval) {
+	dbg_lds_gate(s);
 	k_step_counters<<<1, 64, 0, s>>>(st, target_batch, max_samples, world, fixed_rays, eval_cnt, n_eval);
 }
 

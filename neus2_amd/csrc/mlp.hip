@@ -1701,6 +1701,7 @@ void launch_nerf_infer(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_
 	static const bool pipe = [] { const char* e = std::getenv("NEUS_INFER_PIPE"); return !(e && e[0] == '0'); }();
 	const bool all = pipe && valid_level + 1 >= L;
 	auto xg = [&](uint32_t b) { return a.xcd_parts ? std::max(8u, b & ~7u) : b; };
+	dbg_lds_gate(s);
 #define X(l, w_) if (L == l && W == w_) { \
 		static const uint32_t cap = resident_blocks((const void*)k_nerf_infer<l, w_, false>, 256); \
 		static const uint32_t cap_all = resident_blocks((const void*)k_nerf_infer<l, w_, false, true>, 256); \
@@ -1755,12 +1756,14 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_occ_uniform_list(uint32_t n_u,
 void launch_occ_uniform_list(hipStream_t s, uint32_t n_u, uint32_t step, uint32_t lo, uint32_t hi, uint32_t* list, void* scan_tmp) {
 	if (n_u > GRID3) throw std::runtime_error("launch_occ_uniform_list: more uniform samples than mip-0 cells");
 	static_assert(GRID3 % SCAN_TILE == 0 && GRID3 / SCAN_TILE <= SCAN_MAX_TILES, "uniform list tiles");
+	dbg_lds_gate(s);
 	k_occ_uniform_list<<<GRID3 / SCAN_TILE, SCAN_THREADS, 0, s>>>(n_u, step, lo, hi, list, (ScanState*)scan_tmp, scan_next_tag(scan_tmp));
 }
 void launch_occ_density(hipStream_t s, uint32_t L, uint32_t W, uint32_t n, const OccSampling& os, const GridLevels& gl, uint32_t valid_level,
                         const half_t* grid, const MlpPtrs& w) {
 	const uint32_t blocks = std::min<uint32_t>((n + 127) / 128, 8192);
 	if (n == 0) return;
+	dbg_lds_gate(s);
 #define X(l, w_) if (L == l && W == w_) { k_nerf_density<l, w_, 2><<<blocks, 256, 0, s>>>(n, nullptr, UniformGrid{}, os, gl, valid_level, grid, w, nullptr); return; }
 	NEUS_MLP_CONFIGS(X)
 #undef X
@@ -1787,12 +1790,15 @@ void launch_mlp_train(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_v
 	const uint32_t blocks = mlp_train_blocks(L, W, n);
 	if (n == 0) return;
 #define X(l, w_) if (L == l && W == w_) { \
+		dbg_lds_gate(s); \
 		if (part != 2) k_mlp_train_rgb<l, w_><<<blocks, 256, 0, s>>>(n_valid_ptr, n, ld, coords, enc, dydx, dL_dout, w, tb); \
+		dbg_lds_gate(s); \
 		if (part != 1) k_mlp_train_density<l, w_><<<blocks, 256, 0, s>>>(n_valid_ptr, n, ld, coords, enc, dydx, w, tb); return; }
 	NEUS_MLP_CONFIGS(X)
 #undef X
 }
 void launch_mlp_grad_reduce(hipStream_t s, const MlpGradReduce& r) {
+	dbg_lds_gate(s);
 	k_mlp_grad_reduce<<<(r.n_matrix + 63) / 64 + 1, 256, 0, s>>>(r);
 }
 // persistent grid: at most the resident capacity of the two training kernels, so the ~53 KB weight staging runs

@@ -387,6 +387,7 @@ void launch_adam_ema(hipStream_t s, const AdamParams& p, float* weights_fp, half
 	const StepCounterArgs sc = counters ? *counters : StepCounterArgs{nullptr, 0u, 0u, 1u, 0u, nullptr, 0u};
 	AdamTranspose t{};
 	if (tr) t = *tr;
+	dbg_lds_gate(s);
 	k_adam_ema<<<nblk(std::max<uint64_t>(1, p.n / 4), 16384), 256, 0, s>>>(p, weights_fp, weights_h, grads, m1, m2, steps, ema_tmp, ema_h, sc, t);
 }
 void launch_add_f32(hipStream_t s, uint32_t n, const float* src, float* dst) {
@@ -411,23 +412,31 @@ void launch_grid_samples(hipStream_t s, uint32_t n, uint32_t i_begin, uint32_t i
 void launch_splat_max(hipStream_t s, uint32_t n, const uint32_t* indices, const float* density, float* grid_tmp) {
 	if (n) k_splat_max<<<nblk(n), 256, 0, s>>>(n, indices, density, grid_tmp);
 }
-void launch_ema_grid(hipStream_t s, uint32_t n, float decay, float* grid, const float* tmp) { k_ema_grid<<<nblk(n), 256, 0, s>>>(n, decay, grid, tmp); }
+void launch_ema_grid(hipStream_t s, uint32_t n, float decay, float* grid, const float* tmp) { dbg_lds_gate(s); k_ema_grid<<<nblk(n), 256, 0, s>>>(n, decay, grid, tmp); }
 void launch_grid_mean(hipStream_t s, const float* grid, float* partial, float* mean) {
+	dbg_lds_gate(s);
 	k_grid_mean_partial<<<GRID3 / 1024, 256, 0, s>>>(grid, partial);
+	dbg_lds_gate(s);
 	k_grid_mean_final<<<1, 256, 0, s>>>(partial, GRID3 / 1024, mean);
 }
 void launch_bitfield(hipStream_t s, const float* grid, uint8_t* bitfield, const float* mean, uint32_t n_cascades, uint32_t* lin) {
 	const uint32_t nbytes = GRID3 / 8;
+	dbg_lds_gate(s);
 	k_grid_to_bitfield<<<nblk(nbytes * NERF_CASCADES), 256, 0, s>>>(nbytes * NERF_CASCADES, nbytes * n_cascades, grid, bitfield, mean);
+	dbg_lds_gate(s);
 	k_bitfield_pool_all<<<nblk((uint64_t)nbytes * (NERF_CASCADES - 1), 2048), 256, 0, s>>>(nbytes, bitfield, lin);
 }
 size_t occ_bbox_scratch_floats() { return 6 + 6 * (size_t)OCC_BBOX_BLOCKS; }
 void launch_occ_bbox(hipStream_t s, const uint8_t* bitfield, float* scratch) {
+	dbg_lds_gate(s);
 	k_occ_bbox_partial<<<OCC_BBOX_BLOCKS, 256, 0, s>>>(bitfield, scratch + 6);
+	dbg_lds_gate(s);
 	k_occ_bbox_final<<<1, 256, 0, s>>>(scratch + 6, OCC_BBOX_BLOCKS, scratch);
 }
 void launch_ema_mean(hipStream_t s, uint32_t n, float decay, float* grid, const float* tmp, float* partial, float* mean) {
+	dbg_lds_gate(s);
 	k_ema_mean<<<n / 1024, 256, 0, s>>>(n, decay, grid, tmp, partial);
+	dbg_lds_gate(s);
 	k_grid_mean_final<<<1, 256, 0, s>>>(partial, GRID3 / 1024, mean);
 }
 

@@ -79,6 +79,7 @@ void launch_exclusive_scan(hipStream_t s, void* temp, size_t temp_bytes, const u
 	const uint32_t tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
 	if (tiles <= SCAN_MAX_TILES) {
 		const uint32_t vec = ((((uintptr_t)in) | ((uintptr_t)out)) & 15u) == 0 ? 1u : 0u;
+		dbg_lds_gate(s);
 		k_scan_lookback<<<tiles, SCAN_THREADS, 0, s>>>(in, out, n, (ScanState*)temp, vec, scan_next_tag(temp), 0u);
 		return;
 	}
@@ -86,6 +87,7 @@ void launch_exclusive_scan(hipStream_t s, void* temp, size_t temp_bytes, const u
 	(void)hipcub::DeviceScan::ExclusiveSum((char*)temp + SCAN_STATE_BYTES, tb, in, out, (int)n, s);
 }
 void launch_sum_f32(hipStream_t s, void* temp, size_t temp_bytes, const float* in, float* out, uint32_t n) {
+	dbg_lds_gate(s);
 	size_t tb = temp_bytes - SCAN_STATE_BYTES;
 	(void)hipcub::DeviceReduce::Sum((char*)temp + SCAN_STATE_BYTES, tb, in, out, (int)n, s);
 }

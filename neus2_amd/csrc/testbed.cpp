@@ -227,6 +227,7 @@ struct NeusTestbed {
 	Dev<uint32_t> dbg_enc;  // debug timing only (neus_debug_time_kernel 11): [L][16 Nc] encodings of the inference samples
 	bool ray_cull = true;   // NEUS_RAY_CULL=0: march every ray (A/B reference)
 	uint32_t dbg_lds_fill = 0;  // tests (neus_debug_set_lds_fill): garbage-fill every CU's LDS before the step's march write
+	uint32_t dbg_lds_fill_all = 0;  // tests (neus_debug_set_lds_fill_all): ... before every kernel of the step (g_dbg_lds_fill)
 	Dev<PcgJump> pcg_tab;   // pcg32 jump-ahead table (common.h PcgJumpTable)
 	uint32_t density_grid_ema_step = 0;
 	uint64_t occ_samples = 0;  // occupancy-grid samples this rank evaluated since the network was loaded
@@ -1592,7 +1593,13 @@ int neus_testbed_layout(NeusTestbed* tb, NeusNetLayout* o) {
 int neus_testbed_train(NeusTestbed* tb, uint32_t n_steps) {
 	return guard([&] {
 		HIP_CHECK(hipSetDevice(tb->device));
-		for (uint32_t i = 0; i < n_steps; ++i) tb->train_step();
+		// the LDS-garbage test hook is this thread's while its steps are queued (other testbeds / threads unaffected);
+		// the pattern alternates with its complement from step to step
+		struct FillScope { ~FillScope() { g_dbg_lds_fill = 0; } } fill_scope;
+		for (uint32_t i = 0; i < n_steps; ++i) {
+			g_dbg_lds_fill = tb->dbg_lds_fill_all ? ((tb->training_step & 1) ? ~tb->dbg_lds_fill_all : tb->dbg_lds_fill_all) : 0u;
+			tb->train_step();
+		}
 	});
 }
 int neus_testbed_get_stats(NeusTestbed* tb, NeusTrainStats* o) {
@@ -2331,6 +2338,7 @@ int neus_debug_scan_giveup(void* stream, const uint32_t* in, uint32_t* out, uint
 	});
 }
 int neus_debug_set_lds_fill(NeusTestbed* tb, uint32_t pattern) { return guard([&] { tb->dbg_lds_fill = pattern; }); }
+int neus_debug_set_lds_fill_all(NeusTestbed* tb, uint32_t pattern) { return guard([&] { tb->dbg_lds_fill_all = pattern; }); }
 int neus_debug_inject_health(NeusTestbed* tb, uint32_t flags) {
 	return guard([&] {
 		if (!tb->have_net) throw std::runtime_error("no network");
