@@ -153,9 +153,9 @@ typedef struct NeusNetLayout {
 
 /* ABI version of this header (bumped on any incompatible signature or struct change; version 2: neus_module_create_network
  * became tcnn's create_network(n_input_dims, n_output_dims, network), the NerfNetwork factory neus_module_create_nerf_network;
- * version 3: NeusDataParallelInfo gained host_group).
+ * version 3: NeusDataParallelInfo gained host_group; version 4: neus_module_create_encoding gained requested_precision).
  * Bindings compare it on load so that a stale library or binding fails loudly instead of misreading arguments. */
-#define NEUS_ABI_VERSION 3u
+#define NEUS_ABI_VERSION 4u
 int neus_abi_version(uint32_t* out);
 const char* neus_last_error(void);
 int neus_device_count(int* count);
@@ -338,6 +338,16 @@ int neus_debug_set_lds_fill(NeusTestbed* tb, uint32_t pattern);
  * the step's kernels, so a kernel that read LDS it had not written in its own launch would change the results (the
  * determinism test of the whole step: tests/test_gpu_determinism.py). */
 int neus_debug_set_lds_fill_all(NeusTestbed* tb, uint32_t pattern);
+/* Test hook: every training step launches a no-op kernel of n_blocks workgroups before each of its kernels, shifting the
+ * round-robin workgroup -> XCD placement (0: off); the step's results must not depend on the placement. */
+int neus_debug_set_xcd_shift(NeusTestbed* tb, uint32_t n_blocks);
+/* Development: the last step's compacted training batch (coords batch x 7 f32, dL/doutput batch x 16 fp16 bits) and
+ * per-ray losses (2^18 f32); host buffers, each nullable. */
+int neus_debug_get_batch(NeusTestbed* tb, float* coords_out, uint16_t* dl_dout_out, float* loss_out);
+/* Development: nbytes at offset of one step-workspace buffer (ids in testbed.cpp neus_debug_get_buffer). */
+int neus_debug_get_buffer(NeusTestbed* tb, int id, uint64_t offset, uint64_t nbytes, void* host);
+/* Development: the loss-gradient kernel replayed on the last step's state into a separate buffer (batch x 16 fp16). */
+int neus_debug_replay_loss_grad(NeusTestbed* tb, uint16_t* dl_dout_out);
 /* neus_sample_rays (rank 0 of 1) plus the progressive round-0 work list the training step's march writes (the first
  * min(n, chunk_end) samples of every kept ray, in ray order; list: device, max_samples u32, list_len: host u32), with
  * lds_fill != 0 every CU's LDS filled with that pattern between the scan and the write kernel (stale-LDS test). */
@@ -419,8 +429,11 @@ int neus_debug_host_group_allreduce(NeusHostGroup* group, void* host, uint64_t n
  *   neus_module_create_encoding  create_encoding (HashGrid, grid.h): input [n][3] f32; output layout from the config's
  *                                "output_layout": "AoS" [n][2L] fp16 (default: the column-major matrix cpp::Module wraps,
  *                                cpp_api.cu:58-70), "SoA" [2L][n] (GridEncoding::preferred_output_layout, grid.h:2357-2359) or
- *                                "paired" [L][n] half2 (this build's kernels); params [n_grid] fp16.
- *   neus_module_create_network_with_input_encoding  HashGrid -> FullyFusedMLP with one hidden ReLU layer (below).
+ *                                "paired" [L][n] half2 (this build's kernels); params [n_grid] fp16. requested_precision
+ *                                (cpp_api.h:110, cpp_api.cu:174-180): NEUS_PRECISION_FP16 = GridEncoding<__half> (the
+ *                                kernels of the training step), NEUS_PRECISION_FP32 = GridEncoding<float>: params, output,
+ *                                dL_doutput, dL_ddLdoutput and dL_dparams f32 (AoS / SoA layouts).
+ *   neus_module_create_network_with_input_encoding  {HashGrid, Identity} -> FullyFusedMLP of any depth (below).
  *   neus_module_create_nerf_network  the NeuS NerfNetwork (nerf_network.h; the full config object with "encoding",
  *                                "network", "rgb_network"): input NerfCoordinate [n][7] f32 (pos, dt, dir), output
  *                                [n][16] fp16; params [n_params] fp16 in the layout of neus_testbed_layout. Its backward
@@ -445,11 +458,15 @@ typedef struct NeusModuleInfo {
 } NeusModuleInfo;
 int neus_module_create_network(uint32_t n_input_dims, uint32_t n_output_dims, const char* network_json, uint32_t batch_capacity, NeusModule** out);
 int neus_module_create_nerf_network(const char* config_json, uint32_t batch_capacity, NeusModule** out);
-int neus_module_create_encoding(uint32_t n_input_dims, const char* encoding_json, uint32_t batch_capacity, NeusModule** out);
-/* create_network_with_input_encoding (cpp_api.h:108; network_with_input_encoding.h): HashGrid -> FullyFusedMLP (1 hidden ReLU
- * layer of n_neurons 16 or 64, linear output padded to 16). Input [n][3] f32, output [n][16] fp16 (column-major, as
- * cpp_api.cu:58-70), params [W x DE | 16 x W | grid] fp16 with DE = 2 n_levels padded to 16. backward_backward_input follows
- * network_with_input_encoding.h:159-250 / fully_fused_mlp.cu:1088-1198 (parameter gradients only; dL_ddLdoutput and
+int neus_module_create_encoding(uint32_t n_input_dims, const char* encoding_json, int requested_precision, uint32_t batch_capacity,
+                                NeusModule** out);
+/* create_network_with_input_encoding (cpp_api.h:108; network_with_input_encoding.h): `encoding` HashGrid (input [n][3] f32) or
+ * Identity ({"scale", "offset"}, identity.h; input [n][n_input_dims] f32) in front of a FullyFusedMLP as create_network's.
+ * Output [n][padded n_output_dims] fp16 (column-major, as cpp_api.cu:58-70); params [network matrices in order | grid] fp16
+ * (NetworkWithInputEncoding: network first, network_with_input_encoding.h:262-270), the MLP's input width DE = 2 n_levels
+ * padded to 16 with zeros (grid.h:1540-1550). HashGrid -> 1 hidden ReLU layer of 16 / 64 neurons -> linear output of <= 16
+ * dims runs as one fused kernel; other shapes as the grid kernels feeding the FullyFusedMLP layers. backward_backward_input
+ * follows network_with_input_encoding.h:159-250 / fully_fused_mlp.cu:1088-1198 (parameter gradients only; dL_ddLdoutput and
  * dL_dinput are not written, as in the reference). */
 int neus_module_create_network_with_input_encoding(uint32_t n_input_dims, uint32_t n_output_dims, const char* encoding_json,
                                                    const char* network_json, uint32_t batch_capacity, NeusModule** out);

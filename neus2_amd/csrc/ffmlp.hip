@@ -93,7 +93,7 @@ __global__ void __launch_bounds__(256) k_ff_layer(FfLayer L) {
 				if (o >= L.O) continue;
 				const float x = (float)(half_t)acc[mt][i];
 				if (L.mode == FF_MODE_F32) {
-					if (o < L.o_lim) L.out_f[(size_t)s * L.ldo + o] = x;
+					if (o < L.o_lim) L.out_f[(size_t)s * L.ldo + o] = x * L.out_scale;
 				} else if (L.mode == FF_MODE_DACT) {
 					const float d = (float)(half_t)ff_dact(L.act, (float)L.aux[(size_t)s * L.ldx + o]);
 					L.out[(size_t)s * L.ldo + o] = (half_t)(x * d);

@@ -751,6 +751,22 @@ __global__ void __launch_bounds__(256) k_enc_relayout(uint32_t n, uint32_t L, co
 		dst[a1] = v[1];
 	}
 }
+// paired [L][n] half2 <-> sample rows [n][ld] fp16 with the features in columns [0, 2L) and the columns [2L, ld) zero: the
+// FullyFusedMLP input of a HashGrid-encoded network (GridEncoding pads its output with zeros, grid.h:1540-1550). One
+// thread per (sample, column pair).
+__global__ void __launch_bounds__(256) k_enc_rows(uint32_t n, uint32_t L, uint32_t ld, const uint32_t* __restrict__ paired, half_t* __restrict__ rows,
+                                                  uint32_t to_paired, uint32_t* __restrict__ paired_out, const half_t* __restrict__ src) {
+	const uint32_t half_ld = ld / 2;
+	const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (t >= (uint64_t)n * half_ld) return;
+	const uint32_t i = (uint32_t)(t / half_ld), c = (uint32_t)(t % half_ld);
+	if (to_paired) {
+		if (c < L) paired_out[(size_t)c * n + i] = *(const uint32_t*)(src + (size_t)i * ld + 2 * c);
+	} else {
+		const uint32_t u = c < L ? paired[(size_t)c * n + i] : 0u;
+		*(uint32_t*)(rows + (size_t)i * ld + 2 * c) = u;
+	}
+}
 // fp32 parameter gradients -> the caller's fp16 buffer (tcnn's param-precision gradients, trainer.h:72-109): Overwrite
 // stores the rounded value, Accumulate adds into the fp16 value in fp32 and rounds once
 __global__ void __launch_bounds__(256) k_grad_to_half(uint32_t n, const float* __restrict__ g, half_t* __restrict__ out, uint32_t accumulate) {
@@ -765,6 +781,16 @@ void launch_enc_to_layout(hipStream_t s, uint32_t n, uint32_t L, const uint32_t*
 }
 void launch_enc_from_layout(hipStream_t s, uint32_t n, uint32_t L, const half_t* src, uint32_t layout, uint32_t* paired) {
 	if (n) k_enc_relayout<<<(n * L + 255) / 256, 256, 0, s>>>(n, L, nullptr, nullptr, layout, 1u, paired, src);
+}
+void launch_enc_to_rows(hipStream_t s, uint32_t n, uint32_t L, const uint32_t* paired, half_t* rows, uint32_t ld) {
+	if (ld % 2 || ld < 2 * L) throw std::runtime_error("launch_enc_to_rows: ld must be even and >= 2 L");
+	const uint64_t m = (uint64_t)n * (ld / 2);
+	if (m) k_enc_rows<<<(uint32_t)((m + 255) / 256), 256, 0, s>>>(n, L, ld, paired, rows, 0u, nullptr, nullptr);
+}
+void launch_enc_from_rows(hipStream_t s, uint32_t n, uint32_t L, const half_t* rows, uint32_t ld, uint32_t* paired) {
+	if (ld % 2 || ld < 2 * L) throw std::runtime_error("launch_enc_from_rows: ld must be even and >= 2 L");
+	const uint64_t m = (uint64_t)n * (ld / 2);
+	if (m) k_enc_rows<<<(uint32_t)((m + 255) / 256), 256, 0, s>>>(n, L, ld, nullptr, nullptr, 1u, paired, rows);
 }
 void launch_grad_to_half(hipStream_t s, uint32_t n, const float* g, half_t* out, bool accumulate) {
 	if (n) k_grad_to_half<<<(n + 255) / 256, 256, 0, s>>>(n, g, out, accumulate ? 1u : 0u);

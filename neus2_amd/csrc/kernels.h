@@ -87,6 +87,7 @@ struct LossParams {
 	uint32_t max_compacted; // target batch size
 	uint64_t rng_state, rng_inc;
 	PcgJumpTable jt;
+	uint32_t dbg_fence = 0;  // development (NEUS_DBG_LOSS_FENCE=1): an agent-scope acquire fence at the loss-gradient kernel's start
 };
 
 // binned hash-grid gradient scatter (grid.hip)
@@ -254,6 +255,7 @@ struct FfLayer {
 	const half_t* W; uint32_t O, K; uint32_t trans;  // A = W [O][K] or (trans) W^T of W [K][O]
 	const half_t* in; uint32_t ldi;                    // [n][ldi] fp16
 	half_t* out; float* out_f; uint32_t ldo, o_lim;    // [n][ldo] fp16 (modes ACT, DACT) or f32 (mode F32, o < o_lim)
+	float out_scale = 1.f;                             // mode F32: the fp16-rounded sum times this (an Identity encoding's scale)
 	const half_t* aux; uint32_t ldx;                   // mode DACT: forward post-activation values [n][ldx]
 	uint32_t mode, act, n;
 };
@@ -320,8 +322,13 @@ void launch_fill_lds(hipStream_t s, uint32_t pattern);
 // launches), so a kernel that read LDS it had not written in this launch would read garbage and change the step's
 // results. 0 (always, outside the tests): no fill.
 extern thread_local uint32_t g_dbg_lds_fill;
+// Placement test hook (neus_debug_set_xcd_shift): a one-wave kernel of this many workgroups before each kernel of the
+// step shifts the round-robin workgroup -> XCD placement of the next launch (results must not depend on it)
+extern thread_local uint32_t g_dbg_xcd_shift;
+void launch_xcd_shift(hipStream_t s, uint32_t n_blocks);
 inline void dbg_lds_gate(hipStream_t s) {
 	if (g_dbg_lds_fill) launch_fill_lds(s, g_dbg_lds_fill);
+	if (g_dbg_xcd_shift) launch_xcd_shift(s, g_dbg_xcd_shift);
 }
 void debug_launch_march_stats(hipStream_t s, uint32_t n_rays, const float* rays, const float* tstart, const uint32_t* lin, const DevDataset& ds,
                               const uint8_t* bf, uint32_t* out);
@@ -406,6 +413,16 @@ void launch_enc_ddLdoutput(hipStream_t s, uint32_t n, uint32_t ld, uint32_t L, c
 enum : uint32_t { ENC_LAYOUT_AOS = 0, ENC_LAYOUT_SOA = 1, ENC_LAYOUT_PAIRED = 2 };
 void launch_enc_to_layout(hipStream_t s, uint32_t n, uint32_t L, const uint32_t* paired, half_t* dst, uint32_t layout);
 void launch_enc_from_layout(hipStream_t s, uint32_t n, uint32_t L, const half_t* src, uint32_t layout, uint32_t* paired);
+// fp32 HashGrid (grid_f32.hip): create_encoding with requested_precision = fp32 (cpp_api.cu:174-180)
+void launch_grid_f32_forward(hipStream_t s, uint32_t n, const GridLevels& gl, uint32_t valid_level, const float* coords, const float* table,
+                             float* out, uint32_t layout, float* dydx);
+void launch_grid_f32_backward(hipStream_t s, uint32_t n, const GridLevels& gl, uint32_t valid_level, const float* coords, const float* dLdy,
+                              uint32_t layout, float* grads, const float* dydx, float* dLdx);
+void launch_grid_f32_bbi(hipStream_t s, uint32_t n, const GridLevels& gl, uint32_t valid_level, const float* coords, const float* ddx,
+                         const float* dLdy, uint32_t layout, float* grads, const float* dydx, float* ddLdy);
+// paired [L][n] <-> sample rows [n][ld] (features in columns [0, 2L), zero padding up to ld): a FullyFusedMLP's input
+void launch_enc_to_rows(hipStream_t s, uint32_t n, uint32_t L, const uint32_t* paired, half_t* rows, uint32_t ld);
+void launch_enc_from_rows(hipStream_t s, uint32_t n, uint32_t L, const half_t* rows, uint32_t ld, uint32_t* paired);
 void launch_grad_to_half(hipStream_t s, uint32_t n, const float* g, half_t* out, bool accumulate);
 void launch_transpose_w(hipStream_t s, const TransposeJobs& jobs);
 struct DinPerm { int32_t p[48]; uint32_t din, W; };

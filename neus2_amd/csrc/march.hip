@@ -1417,6 +1417,7 @@ __global__ void __launch_bounds__(256) k_loss_grad(const StepState* __restrict__
                                                    const uint32_t* __restrict__ rbase, const float4* __restrict__ sa, const float* __restrict__ ekt,
                                                    const float4* __restrict__ ck4, const float* __restrict__ cke, const float4* __restrict__ racc,
                                                    const float4* __restrict__ rgr, float* __restrict__ coords_out, half_t* __restrict__ dL_dout) {
+	if (lp.dbg_fence) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 	const uint32_t n = min(st->compacted_counter, lp.max_compacted);
 	const uint32_t n_rays_global = st->rays_per_batch * dp.world;
 	const float loss_scale = lp.loss_scale / n_rays_global;
@@ -1574,6 +1575,9 @@ __global__ void __launch_bounds__(256) k_fill_lds(uint32_t pattern) {
 	for (uint32_t i = threadIdx.x; i < FILL_LDS_BYTES / 4; i += 256) v[i] = pattern;
 }
 thread_local uint32_t g_dbg_lds_fill = 0;
+thread_local uint32_t g_dbg_xcd_shift = 0;
+__global__ void k_xcd_shift() {}
+void launch_xcd_shift(hipStream_t s, uint32_t n_blocks) { k_xcd_shift<<<n_blocks, 64, 0, s>>>(); }
 void launch_fill_lds(hipStream_t s, uint32_t pattern) {
 	// 40 KB per workgroup, 4 resident per CU: the whole 160 KB of every CU (256 CUs), twice over
 	k_fill_lds<<<2048, 256, FILL_LDS_BYTES, s>>>(pattern);

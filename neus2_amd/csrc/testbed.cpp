@@ -17,6 +17,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
+#include <cstdio>
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
@@ -46,6 +48,21 @@ thread_local std::string g_err;
 		if (r_ != ncclSuccess) throw std::runtime_error(std::string(#x) + " failed: " + ncclGetErrorString(r_)); \
 	} while (0)
 
+// Debug: NEUS_DBG_POISON="byte[:lo:hi]" fills the fresh device allocations number lo .. hi-1 (counted from the last
+// testbed creation) with `byte`; NEUS_DBG_ALLOC_LOG=1 lists them (number, bytes) on stderr. A result that changes with
+// the fill reads memory no kernel wrote (i.e. depends on what a recycled allocation held). Off: one getenv per alloc.
+std::atomic<uint64_t> g_alloc_seq{0}, g_alloc_base{0};
+void dbg_poison(void* p, size_t bytes) {
+	const uint64_t k = g_alloc_seq++ - g_alloc_base.load();
+	if (std::getenv("NEUS_DBG_ALLOC_LOG")) std::fprintf(stderr, "neus alloc %llu %zu\n", (unsigned long long)k, bytes);
+	const char* e = std::getenv("NEUS_DBG_POISON");
+	if (!e) return;
+	unsigned v = 0;
+	unsigned long long lo = 0, hi = ~0ull;
+	if (std::sscanf(e, "%u:%llu:%llu", &v, &lo, &hi) < 1) return;
+	if (k >= lo && k < hi) HIP_CHECK(hipMemset(p, (int)v, bytes));
+}
+
 template <class T> struct Dev {
 	T* p = nullptr;
 	size_t n = 0;
@@ -54,6 +71,7 @@ template <class T> struct Dev {
 		release();
 		if (k == 0) return;
 		HIP_CHECK(hipMalloc((void**)&p, k * sizeof(T)));
+		dbg_poison(p, k * sizeof(T));
 		n = k;
 	}
 	void release() { if (p) (void)hipFree(p); p = nullptr; n = 0; }
@@ -227,7 +245,12 @@ struct NeusTestbed {
 	Dev<uint32_t> dbg_enc;  // debug timing only (neus_debug_time_kernel 11): [L][16 Nc] encodings of the inference samples
 	bool ray_cull = true;   // NEUS_RAY_CULL=0: march every ray (A/B reference)
 	uint32_t dbg_lds_fill = 0;  // tests (neus_debug_set_lds_fill): garbage-fill every CU's LDS before the step's march write
-	uint32_t dbg_lds_fill_all = 0;  // tests (neus_debug_set_lds_fill_all): ... before every kernel of the step (g_dbg_lds_fill)
+	bool dbg_loss_replay = [] { const char* e = std::getenv("NEUS_DBG_LOSS_REPLAY"); return e && e[0] == '1'; }();
+	Dev<float> dbg_co; Dev<half_t> dbg_dl;
+	static constexpr int DBG_SNAP_N = 15;
+	Dev<uint8_t> dbg_snap[DBG_SNAP_N];  // the loss-gradient inputs right after its launch (ids 0..14 of neus_debug_get_buffer)
+	uint32_t dbg_lds_fill_all = 0;
+	uint32_t dbg_xcd_shift = 0;  // tests (neus_debug_set_xcd_shift): workgroups of a no-op kernel before every kernel of the step  // tests (neus_debug_set_lds_fill_all): ... before every kernel of the step (g_dbg_lds_fill)
 	Dev<PcgJump> pcg_tab;   // pcg32 jump-ahead table (common.h PcgJumpTable)
 	uint32_t density_grid_ema_step = 0;
 	uint64_t occ_samples = 0;  // occupancy-grid samples this rank evaluated since the network was loaded
@@ -1351,6 +1374,7 @@ struct NeusTestbed {
 		LossParams lp{};
 		lp.loss_scale = LOSS_SCALE; lp.ek_w = cfg.ek_loss_weight; lp.mask_w = cfg.mask_loss_weight; lp.cos_anneal = cos_anneal();
 		lp.max_compacted = batch; lp.rng_state = rng.state; lp.rng_inc = rng.inc; lp.jt = jump_table();
+		{ static const bool f = [] { const char* e = std::getenv("NEUS_DBG_LOSS_FENCE"); return e && e[0] == '1'; }(); lp.dbg_fence = f ? 1u : 0u; }
 		const LossWork w = loss_work(base.p);
 		if (progressive) {
 			// rounds of per-ray chunks, each: network on the round's samples, alpha, the recurrence continued (march.hip);
@@ -1387,6 +1411,19 @@ struct NeusTestbed {
 		launch_exclusive_scan(s, scan_tmp.p, scan_tmp_bytes, ccount.p, cbase.p, MAX_RAYS);
 		launch_loss_ray(s, MAX_RAYS, st.p, dp, ds, lp, numsteps.p, ccount.p, cbase.p, w, loss.p, ek.p, mask.p);
 		launch_loss_grad(s, max_samples, st.p, dp, lp, coords.p, net_out.p, numsteps.p, w, coords_c.p, dL_dout.p);
+		if (dbg_loss_replay) {  // development (NEUS_DBG_LOSS_REPLAY=1): the same launch again, into separate outputs, and
+			                     // copies of the loss-gradient kernel's inputs as they were right after it
+			dbg_co.alloc((size_t)batch * COORD_W); dbg_dl.alloc((size_t)batch * OUT_W);
+			launch_loss_grad(s, max_samples, st.p, dp, lp, coords.p, net_out.p, numsteps.p, w, dbg_co.p, dbg_dl.p);
+			const std::pair<const void*, size_t> src[DBG_SNAP_N] = {
+				{l_sa.p, l_sa.n * 16}, {l_ekt.p, l_ekt.n * 4}, {l_ck4.p, l_ck4.n * 16}, {l_cke.p, l_cke.n * 4}, {l_racc.p, l_racc.n * 16},
+				{l_rgr.p, l_rgr.n * 16}, {l_rT.p, l_rT.n * 4}, {l_rek.p, l_rek.n * 4}, {ccount.p, ccount.n * 4}, {net_out.p, net_out.n * 2},
+				{coords.p, coords.n * 4}, {base.p, base.n * 4}, {numsteps.p, numsteps.n * 4}, {cmap.p, cmap.n * 4}, {nreq.p, nreq.n * 4}};
+			for (int k = 0; k < DBG_SNAP_N; ++k) {
+				dbg_snap[k].alloc(src[k].second);
+				HIP_CHECK(hipMemcpyAsync(dbg_snap[k].p, src[k].first, src[k].second, hipMemcpyDeviceToDevice, s));
+			}
+		}
 		// the rollover copies are made by the training encode (static scenes); the DeltaNetwork reads the whole batch first
 		if (use_delta) launch_rollover(s, batch, st.p, coords_c.p, dL_dout.p);
 		const EncodeRollover ro{&st.p->compacted_counter, batch, dL_dout.p, coords_c.p};
@@ -1573,7 +1610,12 @@ int neus_abi_version(uint32_t* out) {
 int neus_device_count(int* count) { return guard([&] { HIP_CHECK(hipGetDeviceCount(count)); }); }
 int neus_device_synchronize(void) { return guard([&] { HIP_CHECK(hipDeviceSynchronize()); }); }
 
-int neus_testbed_create(int device, NeusTestbed** out) { return guard([&] { *out = new NeusTestbed(device); }); }
+int neus_testbed_create(int device, NeusTestbed** out) {
+	return guard([&] {
+		g_alloc_base = g_alloc_seq.load();
+		*out = new NeusTestbed(device);
+	});
+}
 int neus_testbed_destroy(NeusTestbed* tb) { return guard([&] { delete tb; }); }
 int neus_testbed_set_dataset(NeusTestbed* tb, uint32_t n_images, const NeusImage* images, float aabb_scale) {
 	return guard([&] { tb->set_dataset(n_images, images, aabb_scale); });
@@ -1595,9 +1637,14 @@ int neus_testbed_train(NeusTestbed* tb, uint32_t n_steps) {
 		HIP_CHECK(hipSetDevice(tb->device));
 		// the LDS-garbage test hook is this thread's while its steps are queued (other testbeds / threads unaffected);
 		// the pattern alternates with its complement from step to step
-		struct FillScope { ~FillScope() { g_dbg_lds_fill = 0; } } fill_scope;
+		struct FillScope { ~FillScope() { g_dbg_lds_fill = 0; g_dbg_xcd_shift = 0; } } fill_scope;
+		static const bool lock_launches = [] { const char* e = std::getenv("NEUS_LAUNCH_LOCK"); return e && e[0] == '1'; }();
+		static std::mutex launch_mu;
 		for (uint32_t i = 0; i < n_steps; ++i) {
+			std::unique_lock<std::mutex> lk(launch_mu, std::defer_lock);
+			if (lock_launches) lk.lock();
 			g_dbg_lds_fill = tb->dbg_lds_fill_all ? ((tb->training_step & 1) ? ~tb->dbg_lds_fill_all : tb->dbg_lds_fill_all) : 0u;
+			g_dbg_xcd_shift = tb->dbg_xcd_shift;
 			tb->train_step();
 		}
 	});
@@ -2339,6 +2386,72 @@ int neus_debug_scan_giveup(void* stream, const uint32_t* in, uint32_t* out, uint
 }
 int neus_debug_set_lds_fill(NeusTestbed* tb, uint32_t pattern) { return guard([&] { tb->dbg_lds_fill = pattern; }); }
 int neus_debug_set_lds_fill_all(NeusTestbed* tb, uint32_t pattern) { return guard([&] { tb->dbg_lds_fill_all = pattern; }); }
+int neus_debug_set_xcd_shift(NeusTestbed* tb, uint32_t n_blocks) { return guard([&] { tb->dbg_xcd_shift = n_blocks; }); }
+// Development: raw bytes of one step-workspace buffer (ids: 0 sa, 1 ekt, 2 ck4, 3 cke, 4 racc, 5 rgr, 6 rT, 7 rek,
+// 8 ccount, 9 net_out, 10 coords, 11 base, 12 numsteps, 13 cmap, 14 nreq)
+int neus_debug_get_buffer(NeusTestbed* tb, int id, uint64_t offset, uint64_t nbytes, void* host) {
+	return guard([&] {
+		if (!tb->have_net) throw std::runtime_error("no network");
+		const void* p = nullptr;
+		size_t cap = 0;
+		auto pick = [&](const void* q, size_t bytes) { p = q; cap = bytes; };
+		switch (id) {
+		case 0: pick(tb->l_sa.p, tb->l_sa.n * 16); break;
+		case 1: pick(tb->l_ekt.p, tb->l_ekt.n * 4); break;
+		case 2: pick(tb->l_ck4.p, tb->l_ck4.n * 16); break;
+		case 3: pick(tb->l_cke.p, tb->l_cke.n * 4); break;
+		case 4: pick(tb->l_racc.p, tb->l_racc.n * 16); break;
+		case 5: pick(tb->l_rgr.p, tb->l_rgr.n * 16); break;
+		case 6: pick(tb->l_rT.p, tb->l_rT.n * 4); break;
+		case 7: pick(tb->l_rek.p, tb->l_rek.n * 4); break;
+		case 8: pick(tb->ccount.p, tb->ccount.n * 4); break;
+		case 9: pick(tb->net_out.p, tb->net_out.n * 2); break;
+		case 10: pick(tb->coords.p, tb->coords.n * 4); break;
+		case 11: pick(tb->base.p, tb->base.n * 4); break;
+		case 12: pick(tb->numsteps.p, tb->numsteps.n * 4); break;
+		case 13: pick(tb->cmap.p, tb->cmap.n * 4); break;
+		case 14: pick(tb->nreq.p, tb->nreq.n * 4); break;
+		case 15: pick(tb->dbg_dl.p, tb->dbg_dl.n * 2); break;
+		case 20: case 21: case 22: case 23: case 24: case 25: case 26: case 27: case 28: case 29: case 30: case 31: case 32: case 33: case 34:
+			pick(tb->dbg_snap[id - 20].p, tb->dbg_snap[id - 20].n); break;
+		default: throw std::runtime_error("debug_get_buffer: unknown id");
+		}
+		if (offset + nbytes > cap) throw std::runtime_error("debug_get_buffer: range past the buffer");
+		HIP_CHECK(hipStreamSynchronize(tb->stream));
+		HIP_CHECK(hipMemcpy(host, (const char*)p + offset, nbytes, hipMemcpyDeviceToHost));
+	});
+}
+// Development: k_loss_grad replayed on the last step's state (same inputs as the step's launch) into separate outputs;
+// dl_dout_out: batch x 16 fp16 bits (host). Valid after a static-scene step at the default options.
+int neus_debug_replay_loss_grad(NeusTestbed* tb, uint16_t* dl_dout_out) {
+	return guard([&] {
+		if (!tb->have_net) throw std::runtime_error("no network");
+		NeusTestbed& t = *tb;
+		hipStream_t s = t.stream;
+		LossParams lp{};
+		lp.loss_scale = LOSS_SCALE; lp.ek_w = t.cfg.ek_loss_weight; lp.mask_w = t.cfg.mask_loss_weight;
+		// the cos-anneal of the step that ran (training_step was incremented after it)
+		const int ts = (int)t.training_step - 1;
+		lp.cos_anneal = t.cfg.anneal_end == 0 ? 1.0f : std::min(1.0f, (float)std::max(ts, 0) / t.cfg.anneal_end);
+		lp.max_compacted = t.batch;
+		const LossWork w = t.loss_work(t.base.p);
+		Dev<float> co; co.alloc((size_t)t.batch * COORD_W);
+		Dev<half_t> dl; dl.alloc((size_t)t.batch * OUT_W);
+		HIP_CHECK(hipMemsetAsync(dl.p, 0, dl.n * 2, s));
+		launch_loss_grad(s, t.max_samples, t.st.p, DPInfo{t.rank, t.world}, lp, t.coords.p, t.net_out.p, t.numsteps.p, w, co.p, dl.p);
+		HIP_CHECK(hipStreamSynchronize(s));
+		HIP_CHECK(hipMemcpy(dl_dout_out, dl.p, dl.n * 2, hipMemcpyDeviceToHost));
+	});
+}
+int neus_debug_get_batch(NeusTestbed* tb, float* coords_out, uint16_t* dl_dout_out, float* loss_out) {
+	return guard([&] {
+		if (!tb->have_net) throw std::runtime_error("no network");
+		HIP_CHECK(hipStreamSynchronize(tb->stream));
+		if (coords_out) HIP_CHECK(hipMemcpy(coords_out, tb->coords_c.p, (size_t)tb->batch * COORD_W * 4, hipMemcpyDeviceToHost));
+		if (dl_dout_out) HIP_CHECK(hipMemcpy(dl_dout_out, tb->dL_dout.p, (size_t)tb->batch * OUT_W * 2, hipMemcpyDeviceToHost));
+		if (loss_out) HIP_CHECK(hipMemcpy(loss_out, tb->loss.p, (size_t)MAX_RAYS * 4, hipMemcpyDeviceToHost));
+	});
+}
 int neus_debug_inject_health(NeusTestbed* tb, uint32_t flags) {
 	return guard([&] {
 		if (!tb->have_net) throw std::runtime_error("no network");
@@ -2523,6 +2636,7 @@ struct NeusContext {
 // tcnn FullyFusedMLP shape (fully_fused_mlp.cu:816-879): weight matrices [W][in_pad], (N - 1) x [W][W], [out_pad][W]
 struct FfNet {
 	uint32_t W = 0, N = 0, n_in = 0, in_pad = 0, n_out = 0, out_pad = 0, act = FF_RELU, out_act = FF_NONE;
+	float in_scale = 1.f, in_offset = 0.f;  // the Identity encoding's scale / offset (identity.h:44-70)
 	std::vector<uint32_t> off, rows, cols;
 	uint32_t P = 0;
 	void build() {
@@ -2550,7 +2664,8 @@ struct NeusModule {
 	// FullyFusedMLP with 1 hidden ReLU layer -> 16 linear outputs), the network whose backward_backward_input tcnn
 	// implements (network_with_input_encoding.h:159-250, fully_fused_mlp.cu:1088-1198)
 	// Mlp: tcnn::cpp::create_network = NetworkWithInputEncoding(Identity -> FullyFusedMLP) (cpp_api.cu:170-172), ffmlp.hip
-	enum Kind { Network = 0, Encoding = 1, DensityNet = 2, Mlp = 3 } kind;
+	// GridMlp: NetworkWithInputEncoding(HashGrid -> any FullyFusedMLP), composed of the encoding kernels and ffmlp.hip's layers
+	enum Kind { Network = 0, Encoding = 1, DensityNet = 2, Mlp = 3, GridMlp = 4 } kind;
 	FfNet ff;
 	Dev<half_t> ff_acts, ff_front, ff_d[2];  // Mlp: inference activations, backward-backward fronts, delta ping-pong
 	Dev<float> ff_partial, ff_dummy;         // Mlp: per-block weight-gradient rows
@@ -2567,6 +2682,7 @@ struct NeusModule {
 	// paired [L][n] half2 = this build's kernels
 	uint32_t layout = ENC_LAYOUT_AOS;
 	bool grad_fp16 = true;              // dL_dparams in param precision (fp16, trainer.h:72-109) or fp32
+	bool f32 = false;                   // Encoding created with requested_precision fp32: float params / output / gradients
 	Dev<uint32_t> enc_tmp, denc_tmp;    // paired-layout staging of non-paired module I/O
 	Dev<float> gtmp;                    // gradients of an Accumulate call (and of every fp16-gradient call)
 	Dev<float4> dpos, v4;
@@ -2575,6 +2691,7 @@ struct NeusModule {
 	explicit NeusModule(int device) : core(device) {}
 	uint64_t n_params() const {
 		if (kind == Mlp) return ff.P;
+		if (kind == GridMlp) return ff.P + core.lay.n_grid;
 		return kind == Network ? core.lay.P : (kind == DensityNet ? n_mlp + core.lay.n_grid : core.lay.n_grid);
 	}
 	uint32_t valid() const { return core.valid_level_at(training_step); }
@@ -2591,7 +2708,7 @@ struct NeusModule {
 		if (n > capacity) throw std::runtime_error("module: n_elements exceeds the module's batch capacity");
 		if (backward && kind == Network && (n == 0 || n % 128 != 0))
 			throw std::runtime_error("module backward: n_elements must be a positive multiple of 128 (fully_fused_mlp.cu:779-781)");
-		if (kind == Mlp && n % 128 != 0) throw std::runtime_error("FullyFusedMLP: batch size must be a multiple of 128 (fully_fused_mlp.cu:779-781)");
+		if ((kind == Mlp || kind == GridMlp) && n % 128 != 0) throw std::runtime_error("FullyFusedMLP: batch size must be a multiple of 128 (fully_fused_mlp.cu:779-781)");
 	}
 	// the destination of this call's parameter gradients (Overwrite: dL_dparams itself; Accumulate: a scratch buffer)
 	float* grad_target(void* dL_dparams, int mode) {
@@ -2631,8 +2748,18 @@ static void module_common_init(NeusModule* m, uint32_t capacity) {
 	m->gtmp.alloc(P);
 	m->dpos.alloc(capacity); m->v4.alloc(capacity);
 	m->zero_h.alloc((size_t)2 * m->core.lay.L * capacity); m->zero_v.alloc(capacity);
-	if ((m->kind == NeusModule::Encoding && m->layout != ENC_LAYOUT_PAIRED) || m->kind == NeusModule::DensityNet) {
+	if ((m->kind == NeusModule::Encoding && m->layout != ENC_LAYOUT_PAIRED) || m->kind == NeusModule::DensityNet || m->kind == NeusModule::GridMlp) {
 		m->enc_tmp.alloc((size_t)m->core.lay.L * capacity); m->denc_tmp.alloc((size_t)m->core.lay.L * capacity);
+	}
+	if (m->kind == NeusModule::GridMlp) {
+		const FfNet& f = m->ff;
+		m->u_tmp.alloc((size_t)m->core.lay.L * capacity);
+		m->ff_acts.alloc(f.acts_halves(capacity));
+		m->ff_front.alloc((size_t)capacity * (f.in_pad + (size_t)f.N * f.W));
+		const uint32_t dmax = std::max(std::max(f.W, f.out_pad), f.in_pad);
+		m->ff_d[0].alloc((size_t)capacity * dmax); m->ff_d[1].alloc((size_t)capacity * dmax);
+		m->ff_partial.alloc((size_t)ff_wgrad_blocks(capacity) * f.P);
+		m->ff_dummy.alloc(4);
 	}
 	if (m->kind == NeusModule::DensityNet) {
 		m->u_tmp.alloc((size_t)m->core.lay.L * capacity);
@@ -2667,7 +2794,8 @@ int neus_module_create_nerf_network(const char* config_json, uint32_t batch_capa
 	});
 }
 
-int neus_module_create_encoding(uint32_t n_input_dims, const char* encoding_json, uint32_t batch_capacity, NeusModule** out) {
+int neus_module_create_encoding(uint32_t n_input_dims, const char* encoding_json, int requested_precision, uint32_t batch_capacity,
+                                NeusModule** out) {
 	return guard([&] {
 		if (!encoding_json || !out) throw std::runtime_error("neus_module_create_encoding: null argument");
 		if (n_input_dims != 3) throw std::runtime_error("HashGrid module: n_input_dims must be 3");
@@ -2681,6 +2809,14 @@ int neus_module_create_encoding(uint32_t n_input_dims, const char* encoding_json
 		auto m = std::make_unique<NeusModule>(dev);
 		m->kind = NeusModule::Encoding;
 		module_options(m.get(), j);
+		// cpp_api.cu:174-180: Fp32 -> GridEncoding<float> (float params, output and gradients), Fp16 -> GridEncoding<__half>
+		if (requested_precision != NEUS_PRECISION_FP32 && requested_precision != NEUS_PRECISION_FP16)
+			throw std::runtime_error("create_encoding: requested_precision must be NEUS_PRECISION_FP32 or NEUS_PRECISION_FP16");
+		m->f32 = requested_precision == NEUS_PRECISION_FP32;
+		if (m->f32) {
+			if (m->layout == ENC_LAYOUT_PAIRED) throw std::runtime_error("fp32 HashGrid: output_layout AoS or SoA (paired is the fp16 kernels' layout)");
+			m->grad_fp16 = false;
+		}
 		JsonValue none; none.kind = JsonValue::Object;
 		m->core.setup_network(module_config(j, none, none, batch_capacity, true), nullptr, false);
 		m->n_in = 3; m->n_out = 2 * m->core.lay.L;
@@ -2690,49 +2826,97 @@ int neus_module_create_encoding(uint32_t n_input_dims, const char* encoding_json
 		           std::to_string(c.log2_hashmap_size) + ", \"base_resolution\": " + std::to_string(c.base_resolution) + ", \"per_level_scale\": " +
 		           fmt_float(c.per_level_scale) + ", \"valid_level_scale\": " + fmt_float(c.valid_level_scale) + ", \"base_valid_level_scale\": " +
 		           fmt_float(c.base_valid_level_scale) + ", \"base_training_step\": " + std::to_string(c.base_training_step) +
-		           ", \"output_layout\": \"" + lay_names[m->layout] + "\", \"gradient_precision\": \"" + (m->grad_fp16 ? "fp16" : "fp32") + "\"}";
+		           ", \"output_layout\": \"" + lay_names[m->layout] + "\", \"gradient_precision\": \"" + (m->grad_fp16 ? "fp16" : "fp32") +
+		           "\", \"precision\": \"" + (m->f32 ? "fp32" : "fp16") + "\"}";
 		module_common_init(m.get(), batch_capacity);
 		*out = m.release();
 	});
 }
 
+static std::string grid_hyper(const NeusNetworkConfig& c) {
+	return "{\"otype\": \"HashGrid\", \"n_levels\": " + std::to_string(c.n_levels) + ", \"n_features_per_level\": 2, \"log2_hashmap_size\": " +
+	       std::to_string(c.log2_hashmap_size) + ", \"base_resolution\": " + std::to_string(c.base_resolution) + ", \"per_level_scale\": " +
+	       fmt_float(c.per_level_scale) + "}";
+}
+static FfNet ff_from_json(const JsonValue& j, uint32_t n_input_dims, uint32_t n_output_dims);
+static std::string ff_hyper(const FfNet& f);
+static NeusModule* make_mlp_module(const FfNet& f, const JsonValue& j, uint32_t batch_capacity);
+// create_network_with_input_encoding (cpp_api.h:108; network_with_input_encoding.h): an Identity encoding (any input
+// width; scale / offset) or a HashGrid (3 inputs) in front of a FullyFusedMLP of any depth, width 16 / 32 / 64 / 128 and
+// activations. The HashGrid -> one hidden ReLU layer -> linear network of width 16 / 64 runs on the fused k_dnet kernel;
+// every other HashGrid network is the encoding's kernels composed with ffmlp.hip's layers (GridMlp).
 int neus_module_create_network_with_input_encoding(uint32_t n_input_dims, uint32_t n_output_dims, const char* encoding_json,
                                                    const char* network_json, uint32_t batch_capacity, NeusModule** out) {
 	return guard([&] {
 		if (!encoding_json || !network_json || !out) throw std::runtime_error("neus_module_create_network_with_input_encoding: null argument");
-		if (n_input_dims != 3) throw std::runtime_error("network with input encoding: n_input_dims must be 3 (HashGrid)");
-		if (n_output_dims == 0 || n_output_dims > 16) throw std::runtime_error("network with input encoding: 1..16 outputs (padded to 16)");
 		if (batch_capacity == 0 || batch_capacity % 128 != 0 || batch_capacity > (1u << 24))
 			throw std::runtime_error("batch_capacity must be a positive multiple of 128 (<= 2^24)");
 		const JsonValue je = parse_json(encoding_json), jn = parse_json(network_json);
 		const std::string ot = je.string("otype", "HashGrid");
-		if (ot != "HashGrid" && ot != "Grid") throw std::runtime_error("network with input encoding: only the HashGrid encoding is implemented on gfx950");
-		if (jn.string("otype", "FullyFusedMLP") != "FullyFusedMLP" && jn.string("otype", "FullyFusedMLP") != "CutlassMLP")
-			throw std::runtime_error("network with input encoding: the network must be a FullyFusedMLP");
-		if (jn.string("activation", "ReLU") != "ReLU" || jn.string("output_activation", "None") != "None" || (uint32_t)jn.number("n_hidden_layers", 1) != 1)
-			throw std::runtime_error("network with input encoding: ReLU, 1 hidden layer, linear output supported on gfx950");
+		if (ot == "Identity") {
+			FfNet f = ff_from_json(jn, n_input_dims, n_output_dims);
+			f.in_scale = (float)je.number("scale", 1.0);
+			f.in_offset = (float)je.number("offset", 0.0);
+			*out = make_mlp_module(f, jn, batch_capacity);
+			return;
+		}
+		if (ot != "HashGrid" && ot != "Grid") throw std::runtime_error("network with input encoding: the encoding must be Identity or HashGrid on gfx950");
+		if (n_input_dims != 3) throw std::runtime_error("network with input encoding: a HashGrid encodes 3 input dims");
 		int dev = 0;
 		HIP_CHECK(hipGetDevice(&dev));
 		auto m = std::make_unique<NeusModule>(dev);
-		m->kind = NeusModule::DensityNet;
 		module_options(m.get(), jn);
 		m->layout = ENC_LAYOUT_AOS;
 		JsonValue none; none.kind = JsonValue::Object;
 		m->core.setup_network(module_config(je, none, none, batch_capacity, true), nullptr, false);
-		m->dn_width = (uint32_t)jn.number("n_neurons", 64);
-		if (!dnet_supported(m->core.lay.L, m->dn_width)) throw std::runtime_error("network with input encoding: unsupported (n_levels, n_neurons) on gfx950");
-		m->dn_de = (2 * m->core.lay.L + 15) / 16 * 16;
-		m->n_mlp = m->dn_width * m->dn_de + 16 * m->dn_width;
-		m->n_in = 3; m->n_out = 16;
-		const NeusNetworkConfig& c = m->core.cfg;
-		m->hyper = "{\"otype\": \"NetworkWithInputEncoding\", \"encoding\": {\"otype\": \"HashGrid\", \"n_levels\": " + std::to_string(c.n_levels) +
-		           ", \"log2_hashmap_size\": " + std::to_string(c.log2_hashmap_size) + ", \"base_resolution\": " + std::to_string(c.base_resolution) +
-		           ", \"per_level_scale\": " + fmt_float(c.per_level_scale) + "}, \"network\": {\"otype\": \"FullyFusedMLP\", \"n_neurons\": " +
-		           std::to_string(m->dn_width) + ", \"n_hidden_layers\": 1, \"activation\": \"ReLU\", \"output_activation\": \"None\"}, \"n_output_dims\": " +
-		           std::to_string(n_output_dims) + ", \"gradient_precision\": \"" + (m->grad_fp16 ? "fp16" : "fp32") + "\"}";
+		const uint32_t L = m->core.lay.L;
+		const FfNet f = ff_from_json(jn, 2 * L, n_output_dims);
+		const bool fused = f.act == FF_RELU && f.out_act == FF_NONE && f.N == 1 && n_output_dims <= 16 && dnet_supported(L, f.W);
+		m->n_in = 3;
+		if (fused) {
+			m->kind = NeusModule::DensityNet;
+			m->dn_width = f.W;
+			m->dn_de = (2 * L + 15) / 16 * 16;
+			m->n_mlp = m->dn_width * m->dn_de + 16 * m->dn_width;
+			m->n_out = 16;
+		} else {
+			m->kind = NeusModule::GridMlp;
+			m->ff = f;
+			m->n_out = f.out_pad;
+		}
+		m->hyper = "{\"otype\": \"NetworkWithInputEncoding\", \"encoding\": " + grid_hyper(m->core.cfg) + ", \"network\": " + ff_hyper(f) +
+		           ", \"n_output_dims\": " + std::to_string(n_output_dims) + ", \"gradient_precision\": \"" + (m->grad_fp16 ? "fp16" : "fp32") + "\"}";
 		module_common_init(m.get(), batch_capacity);
 		*out = m.release();
 	});
+}
+
+// A FullyFusedMLP from its config (fully_fused_mlp.cu:816-879): n_neurons 16 / 32 / 64 / 128, n_hidden_layers >= 1, input and
+// output padded to multiples of 16
+static FfNet ff_from_json(const JsonValue& j, uint32_t n_input_dims, uint32_t n_output_dims) {
+	const std::string ot = j.string("otype", "FullyFusedMLP");
+	if (ot != "FullyFusedMLP" && ot != "MegakernelMLP" && ot != "CutlassMLP")
+		throw std::runtime_error("only FullyFusedMLP networks are implemented on gfx950");
+	FfNet f;
+	f.W = (uint32_t)j.number("n_neurons", 64);
+	if (f.W != 16 && f.W != 32 && f.W != 64 && f.W != 128)
+		throw std::runtime_error("FullyFusedMLP only supports 16, 32, 64, and 128 neurons, but got " + std::to_string(f.W));
+	const double nh = j.number("n_hidden_layers", 1);
+	if (nh < 1 || nh > 32) throw std::runtime_error("FullyFusedMLP requires at least 1 hidden layer (3 layers in total).");
+	f.N = (uint32_t)nh;
+	if (n_input_dims == 0 || n_input_dims > 128) throw std::runtime_error("FullyFusedMLP: 1..128 input dims on gfx950");
+	if (n_output_dims == 0 || n_output_dims > 128) throw std::runtime_error("FullyFusedMLP: 1..128 output dims on gfx950");
+	f.n_in = n_input_dims; f.in_pad = (n_input_dims + 15) / 16 * 16;
+	f.n_out = n_output_dims; f.out_pad = (n_output_dims + 15) / 16 * 16;
+	f.act = FfNet::activation(j.string("activation", "ReLU"));
+	f.out_act = FfNet::activation(j.string("output_activation", "None"));
+	f.build();
+	return f;
+}
+static std::string ff_hyper(const FfNet& f) {
+	static const char* an[6] = {"None", "ReLU", "Exponential", "Sigmoid", "Squareplus", "Softplus"};
+	return "{\"otype\": \"FullyFusedMLP\", \"n_neurons\": " + std::to_string(f.W) + ", \"n_hidden_layers\": " + std::to_string(f.N) +
+	       ", \"activation\": \"" + an[f.act] + "\", \"output_activation\": \"" + an[f.out_act] + "\"}";
 }
 
 // tcnn::cpp::create_network(n_input_dims, n_output_dims, network) (cpp_api.cu:170-172): NetworkWithInputEncoding with an
@@ -2744,23 +2928,13 @@ int neus_module_create_network(uint32_t n_input_dims, uint32_t n_output_dims, co
 		if (batch_capacity == 0 || batch_capacity % 128 != 0 || batch_capacity > (1u << 24))
 			throw std::runtime_error("batch_capacity must be a positive multiple of 128 (<= 2^24)");
 		const JsonValue j = parse_json(network_json);
-		const std::string ot = j.string("otype", "FullyFusedMLP");
-		if (ot != "FullyFusedMLP" && ot != "MegakernelMLP" && ot != "CutlassMLP")
-			throw std::runtime_error("create_network: only FullyFusedMLP networks are implemented on gfx950");
-		FfNet f;
-		f.W = (uint32_t)j.number("n_neurons", 64);
-		if (f.W != 16 && f.W != 32 && f.W != 64 && f.W != 128)
-			throw std::runtime_error("FullyFusedMLP only supports 16, 32, 64, and 128 neurons, but got " + std::to_string(f.W));
-		const double nh = j.number("n_hidden_layers", 1);
-		if (nh < 1 || nh > 32) throw std::runtime_error("FullyFusedMLP requires at least 1 hidden layer (3 layers in total).");
-		f.N = (uint32_t)nh;
-		if (n_input_dims == 0 || n_input_dims > 128) throw std::runtime_error("create_network: 1..128 input dims on gfx950");
-		if (n_output_dims == 0 || n_output_dims > 128) throw std::runtime_error("create_network: 1..128 output dims on gfx950");
-		f.n_in = n_input_dims; f.in_pad = (n_input_dims + 15) / 16 * 16;
-		f.n_out = n_output_dims; f.out_pad = (n_output_dims + 15) / 16 * 16;
-		f.act = FfNet::activation(j.string("activation", "ReLU"));
-		f.out_act = FfNet::activation(j.string("output_activation", "None"));
-		f.build();
+		*out = make_mlp_module(ff_from_json(j, n_input_dims, n_output_dims), j, batch_capacity);
+	});
+}
+// NetworkWithInputEncoding(Identity{scale, offset} -> FullyFusedMLP) as a module (create_network, and
+// create_network_with_input_encoding with an Identity encoding)
+static NeusModule* make_mlp_module(const FfNet& f, const JsonValue& j, uint32_t batch_capacity) {
+	{
 		int dev = 0;
 		HIP_CHECK(hipGetDevice(&dev));
 		auto m = std::make_unique<NeusModule>(dev);
@@ -2776,15 +2950,12 @@ int neus_module_create_network(uint32_t n_input_dims, uint32_t n_output_dims, co
 		m->ff_d[0].alloc((size_t)batch_capacity * dmax); m->ff_d[1].alloc((size_t)batch_capacity * dmax);
 		m->ff_partial.alloc((size_t)ff_wgrad_blocks(batch_capacity) * f.P);
 		m->ff_dummy.alloc(4);
-		static const char* an[6] = {"None", "ReLU", "Exponential", "Sigmoid", "Squareplus", "Softplus"};
-		m->hyper = "{\"otype\": \"NetworkWithInputEncoding\", \"encoding\": {\"otype\": \"Identity\", \"scale\": 1, \"offset\": 0}, "
-		           "\"network\": {\"otype\": \"FullyFusedMLP\", \"n_neurons\": " + std::to_string(f.W) + ", \"n_hidden_layers\": " +
-		           std::to_string(f.N) + ", \"activation\": \"" + an[f.act] + "\", \"output_activation\": \"" + an[f.out_act] +
-		           "\"}, \"n_input_dims\": " + std::to_string(f.n_in) + ", \"n_output_dims\": " + std::to_string(f.n_out) +
-		           ", \"gradient_precision\": \"" + (m->grad_fp16 ? "fp16" : "fp32") + "\"}";
+		m->hyper = "{\"otype\": \"NetworkWithInputEncoding\", \"encoding\": {\"otype\": \"Identity\", \"scale\": " + fmt_float(f.in_scale) +
+		           ", \"offset\": " + fmt_float(f.in_offset) + "}, \"network\": " + ff_hyper(f) + ", \"n_input_dims\": " + std::to_string(f.n_in) +
+		           ", \"n_output_dims\": " + std::to_string(f.n_out) + ", \"gradient_precision\": \"" + (m->grad_fp16 ? "fp16" : "fp32") + "\"}";
 		HIP_CHECK(hipStreamSynchronize(m->core.stream));
-		*out = m.release();
-	});
+		return m.release();
+	}
 }
 
 namespace {
@@ -2798,7 +2969,7 @@ FfLayer ff_layer(const half_t* W, uint32_t O, uint32_t K, bool trans, const half
 }
 // forward (mlp_fused_forward, fully_fused_mlp.cu:678-812): hidden layers act(W x), output out_act(W_N h)
 void ff_forward(const FfNet& f, hipStream_t s, uint32_t n, const float* input, const void* params, half_t* acts, half_t* output) {
-	launch_ff_input(s, n, f.n_in, f.in_pad, input, 1.f, 0.f, acts, false);
+	if (input) launch_ff_input(s, n, f.n_in, f.in_pad, input, f.in_scale, f.in_offset, acts, false);  // (null: X0 already in acts)
 	const half_t* x = acts;
 	uint32_t ldx = f.in_pad;
 	for (uint32_t l = 0; l <= f.N; ++l) {
@@ -2825,6 +2996,54 @@ void ff_wgrad(const FfNet& f, hipStream_t s, uint32_t n, uint32_t l, const half_
 	G.partial = partial; G.ld_partial = f.P; G.off = f.off[l]; G.n = n;
 	launch_ff_wgrad(s, G);
 }
+// FullyFusedMLP::backward_impl (fully_fused_mlp.cu:967-1085) of a module's network down to dL/d(its input) as fp16 rows
+// [n][in_pad] (returned; the module's delta ping-pong buffer), with the weight-gradient partials when wgrad
+const half_t* ff_backward_chain(NeusModule* m, hipStream_t s, uint32_t n, const void* params, const half_t* acts, const half_t* dL_doutput,
+                                const half_t* output, bool wgrad) {
+	const FfNet& f = m->ff;
+	const half_t* d = dL_doutput;
+	int pp = 0;
+	if (f.out_act != FF_NONE) { launch_ff_out_delta(s, n, f.out_pad, f.out_act, d, output, m->ff_d[0].p); d = m->ff_d[0].p; pp = 1; }
+	uint32_t ldd = f.out_pad;
+	for (uint32_t l = f.N + 1; l-- > 0;) {
+		const half_t* x = l == 0 ? acts : ff_hidden(f, const_cast<half_t*>(acts), n, l - 1);
+		if (wgrad) ff_wgrad(f, s, n, l, d, ldd, x, l == 0 ? f.in_pad : f.W, m->ff_partial.p);
+		if (l > 0) {
+			ff_back_through(f, s, n, params, l, d, ldd, acts, m->ff_d[pp].p);
+			d = m->ff_d[pp].p; pp ^= 1; ldd = f.W;
+		} else {
+			FfLayer L = ff_layer(ff_mat(f, params, 0), f.in_pad, f.W, true, d, ldd, n);
+			L.mode = FF_MODE_ACT; L.act = FF_NONE; L.out = m->ff_d[pp].p; L.ldo = f.in_pad;
+			launch_ff_layer(s, L);
+			d = m->ff_d[pp].p;
+		}
+	}
+	return d;
+}
+// FullyFusedMLP::backward_backward_input_impl (fully_fused_mlp.cu:1088-1198), parameter gradients only, with the front
+// f_0 = the network's dL_ddLdinput already in m->ff_front as rows [n][in_pad]: fronts f_i = act'(h_{i-1}) (W_{i-1} f_{i-1});
+// backs b_{N+2} = dL_doutput, b_i = act'(h_{i-2}) (W_{i-1}^T b_{i+1}); dW_{i-1} = b_{i+1} f_{i-1}^T into the partials
+void ff_bbi_chain(NeusModule* m, hipStream_t s, uint32_t n, const void* params, const half_t* acts, const half_t* dL_doutput) {
+	const FfNet& f = m->ff;
+	half_t* fr = m->ff_front.p;
+	auto front = [&](uint32_t i) { return i == 0 ? fr : fr + (size_t)n * f.in_pad + (size_t)(i - 1) * n * f.W; };
+	for (uint32_t i = 1; i <= f.N; ++i) {
+		FfLayer L = ff_layer(ff_mat(f, params, i - 1), f.rows[i - 1], f.cols[i - 1], false, front(i - 1), i == 1 ? f.in_pad : f.W, n);
+		L.mode = FF_MODE_DACT; L.act = f.act; L.out = front(i); L.ldo = f.W;
+		L.aux = ff_hidden(f, const_cast<half_t*>(acts), n, i - 1); L.ldx = f.W;
+		launch_ff_layer(s, L);
+	}
+	const half_t* b = dL_doutput;
+	uint32_t ldb = f.out_pad;
+	int pp = 0;
+	for (uint32_t l = f.N + 1; l-- > 0;) {
+		ff_wgrad(f, s, n, l, b, ldb, front(l), l == 0 ? f.in_pad : f.W, m->ff_partial.p);
+		if (l > 0) {
+			ff_back_through(f, s, n, params, l, b, ldb, acts, m->ff_d[pp].p);
+			b = m->ff_d[pp].p; pp ^= 1; ldb = f.W;
+		}
+	}
+}
 }  // namespace
 
 int neus_module_destroy(NeusModule* m) { return guard([&] { delete m; }); }
@@ -2836,13 +3055,14 @@ int neus_module_info(const NeusModule* m, NeusModuleInfo* o) {
 		o->n_params = m->n_params();
 		o->n_input_dims = m->n_in;
 		o->n_output_dims = m->n_out;
-		o->param_precision = NEUS_PRECISION_FP16;
-		o->output_precision = NEUS_PRECISION_FP16;
+		o->param_precision = m->f32 ? NEUS_PRECISION_FP32 : NEUS_PRECISION_FP16;
+		o->output_precision = m->f32 ? NEUS_PRECISION_FP32 : NEUS_PRECISION_FP16;
 		o->gradient_precision = NEUS_PRECISION_FP32;
 		o->batch_capacity = m->capacity;
 		o->n_levels = m->core.lay.L;
 		o->grid_offset = m->kind == NeusModule::Network ? m->core.lay.grid_off : (m->kind == NeusModule::DensityNet ? m->n_mlp : 0);
 		if (m->kind == NeusModule::Mlp) { o->n_levels = 0; o->grid_offset = m->ff.P; }  // no encoding parameters
+		if (m->kind == NeusModule::GridMlp) o->grid_offset = m->ff.P;
 		o->per_level_scale = m->core.cfg.per_level_scale;
 	});
 }
@@ -2881,6 +3101,13 @@ int neus_module_initialize_params(NeusModule* m, uint64_t seed, float* params_fu
 			h.assign(m->n_params(), 0.f);
 			pcg32 rnd = make_pcg32(seed);
 			size_t off = 0;
+			if (m->kind == NeusModule::GridMlp) {  // NetworkWithInputEncoding::initialize_params: the network, then the encoding
+				for (uint32_t l = 0; l <= m->ff.N; ++l) {
+					const float scale = std::sqrt(6.0f / (float)(m->ff.rows[l] + m->ff.cols[l]));
+					for (uint32_t i = 0; i < m->ff.rows[l] * m->ff.cols[l]; ++i) h[off + i] = rnd.next_float() * 2.0f * scale - scale;
+					off += (size_t)m->ff.rows[l] * m->ff.cols[l];
+				}
+			}
 			if (m->kind == NeusModule::DensityNet) {
 				auto xavier = [&](uint32_t out, uint32_t in) {
 					const float scale = std::sqrt(6.0f / (float)(in + out));
@@ -2916,6 +3143,26 @@ static void module_forward(NeusModule* m, hipStream_t s, uint32_t n, const float
 		HIP_CHECK(hipGetLastError());
 		return;
 	}
+	if (m->kind == NeusModule::GridMlp) {
+		// NetworkWithInputEncoding::forward (network_with_input_encoding.h:113-124): the HashGrid (zero-padded to the MLP's
+		// input width, grid.h:1540-1550), then the FullyFusedMLP on it
+		if (!params) throw std::runtime_error("module: null params");
+		const FfNet& f = m->ff;
+		uint32_t* enc = m->enc_tmp.p;
+		float* dydx = nullptr;
+		half_t* acts = m->ff_acts.p;
+		if (ctx) {
+			ctx->dydx.alloc((size_t)6 * t.lay.L * std::max(1u, n)); dydx = ctx->dydx.p;
+			ctx->enc.alloc((size_t)t.lay.L * std::max(1u, n)); enc = ctx->enc.p;
+			ctx->acts.alloc(std::max<size_t>(1, f.acts_halves(n))); acts = ctx->acts.p;
+		}
+		const uint32_t gx = std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, 4096));
+		launch_grid_encode(s, nullptr, n, n, input, 3, t.gl, m->valid(), (const half_t*)params + f.P, enc, dydx, gx);
+		launch_enc_to_rows(s, n, t.lay.L, enc, acts, f.in_pad);
+		ff_forward(f, s, n, nullptr, params, acts, (half_t*)output);
+		HIP_CHECK(hipGetLastError());
+		return;
+	}
 	if (m->kind == NeusModule::DensityNet) {
 		// NetworkWithInputEncoding::forward (network_with_input_encoding.h:84-111): encoding, then the MLP on it
 		if (!params) throw std::runtime_error("module: null params");
@@ -2931,6 +3178,14 @@ static void module_forward(NeusModule* m, hipStream_t s, uint32_t n, const float
 		DNetLaunch d{};
 		d.w0 = ph; d.w1 = ph + (size_t)m->dn_width * m->dn_de; d.enc = enc; d.out = (half_t*)output;
 		launch_dnet(s, t.lay.L, m->dn_width, 0, n, d);
+		HIP_CHECK(hipGetLastError());
+		return;
+	}
+	if (m->f32) {  // GridEncoding<float>::forward (kernel_grid with T = float)
+		if (!params) throw std::runtime_error("module: null params");
+		float* dydx = nullptr;
+		if (ctx) { ctx->dydx.alloc((size_t)6 * t.lay.L * std::max(1u, n)); dydx = ctx->dydx.p; }
+		launch_grid_f32_forward(s, n, t.gl, m->valid(), input, (const float*)params, (float*)output, m->layout, dydx);
 		HIP_CHECK(hipGetLastError());
 		return;
 	}
@@ -3004,7 +3259,7 @@ int neus_module_backward(NeusModule* m, void* stream, const NeusContext* ctx, ui
 					d = m->ff_d[pp].p; pp ^= 1; ldd = f.W;
 				} else if (dL_dinput) {
 					FfLayer L = ff_layer(ff_mat(f, params, 0), f.in_pad, f.W, true, d, ldd, n);
-					L.mode = FF_MODE_F32; L.out_f = dL_dinput; L.ldo = f.n_in; L.o_lim = f.n_in;
+					L.mode = FF_MODE_F32; L.out_f = dL_dinput; L.ldo = f.n_in; L.o_lim = f.n_in; L.out_scale = f.in_scale;
 					launch_ff_layer(s, L);
 				}
 			}
@@ -3016,6 +3271,25 @@ int neus_module_backward(NeusModule* m, void* stream, const NeusContext* ctx, ui
 			return;
 		}
 		const uint32_t valid = m->valid();
+		if (m->kind == NeusModule::GridMlp) {
+			// NetworkWithInputEncoding::backward (network_with_input_encoding.h:126-156): the FullyFusedMLP's backward (weight
+			// gradients, dL/d(its input) in fp16) and the HashGrid's backward of that (grid gradients, dL_dinput from dy/dx)
+			const FfNet& f = m->ff;
+			if (!params) throw std::runtime_error("module: null params");
+			if (!ctx->acts.p || !ctx->dydx.p) throw std::runtime_error("module backward: the context is not from this module's forward");
+			if (f.out_act != FF_NONE && !output) throw std::runtime_error("FullyFusedMLP backward: the forward output is needed for its output activation");
+			const half_t* dX0 = ff_backward_chain(m, s, n, params, ctx->acts.p, (const half_t*)dL_doutput, (const half_t*)output, g != nullptr);
+			launch_enc_from_rows(s, n, t.lay.L, dX0, f.in_pad, m->denc_tmp.p);
+			if (g) {
+				launch_mlp_grad_reduce(s, MlpGradReduce{m->ff_partial.p, ff_wgrad_blocks(n), f.P, g, nullptr, nullptr, 0, m->ff_dummy.p});
+				launch_grid_scatter(s, nullptr, n, n, input, 3, t.gl, valid, (const half_t*)m->denc_tmp.p, m->zero_h.p, m->zero_v.p, g + f.P,
+				                    t.swork, t.scan_tmp.p, t.scan_tmp_bytes);
+			}
+			if (dL_dinput) launch_enc_input_grad(s, n, n, t.lay.L, (const half_t*)m->denc_tmp.p, ctx->dydx.p, dL_dinput, 3);
+			if (g) m->finish_grad(dL_dparams, gradient_mode, s);
+			HIP_CHECK(hipGetLastError());
+			return;
+		}
 		if (m->kind == NeusModule::DensityNet) {
 			// NetworkWithInputEncoding::backward (network_with_input_encoding.h:113-156): the MLP backward gives its weight
 			// gradients and dL/d(encoding); the encoding's backward the grid gradients and dL_dinput
@@ -3032,6 +3306,14 @@ int neus_module_backward(NeusModule* m, void* stream, const NeusContext* ctx, ui
 				                    t.swork, t.scan_tmp.p, t.scan_tmp_bytes);
 			}
 			if (dL_dinput) launch_enc_input_grad(s, n, n, t.lay.L, (const half_t*)m->denc_tmp.p, ctx->dydx.p, dL_dinput, 3);
+			if (g) m->finish_grad(dL_dparams, gradient_mode, s);
+			HIP_CHECK(hipGetLastError());
+			return;
+		}
+		if (m->f32) {  // GridEncoding<float>::backward: kernel_grid_backward (float atomics) and dL_dinput from dy/dx
+			if (dL_dinput && !ctx->dydx.p) throw std::runtime_error("encoding backward: dL_dinput needs the forward's dy/dx");
+			if (g) HIP_CHECK(hipMemsetAsync(g, 0, (size_t)m->n_params() * 4, s));
+			launch_grid_f32_backward(s, n, t.gl, valid, input, (const float*)dL_doutput, m->layout, g, ctx->dydx.p, dL_dinput);
 			if (g) m->finish_grad(dL_dparams, gradient_mode, s);
 			HIP_CHECK(hipGetLastError());
 			return;
@@ -3093,7 +3375,7 @@ int neus_module_backward_backward_input(NeusModule* m, void* stream, const NeusC
 			const FfNet& f = m->ff;
 			half_t* fr = m->ff_front.p;
 			auto front = [&](uint32_t i) { return i == 0 ? fr : fr + (size_t)n * f.in_pad + (size_t)(i - 1) * n * f.W; };
-			launch_ff_input(s, n, f.n_in, f.in_pad, dL_ddLdinput, 1.f, 0.f, fr, true);
+			launch_ff_input(s, n, f.n_in, f.in_pad, dL_ddLdinput, f.in_scale, 0.f, fr, true);
 			for (uint32_t i = 1; i <= f.N; ++i) {
 				FfLayer L = ff_layer(ff_mat(f, params, i - 1), f.rows[i - 1], f.cols[i - 1], false, front(i - 1), i == 1 ? f.in_pad : f.W, n);
 				L.mode = FF_MODE_DACT; L.act = f.act; L.out = front(i); L.ldo = f.W;
@@ -3110,6 +3392,34 @@ int neus_module_backward_backward_input(NeusModule* m, void* stream, const NeusC
 					b = m->ff_d[pp].p; pp ^= 1; ldb = f.W;
 				}
 			}
+			launch_mlp_grad_reduce(s, MlpGradReduce{m->ff_partial.p, ff_wgrad_blocks(n), f.P, g, nullptr, nullptr, 0, m->ff_dummy.p});
+			m->finish_grad(dL_dparams, gradient_mode, s);
+			HIP_CHECK(hipGetLastError());
+			return;
+		}
+		if (m->kind == NeusModule::GridMlp) {
+			// NetworkWithInputEncoding::backward_backward_input (network_with_input_encoding.h:159-250): (1) the network's
+			// backward gives dL/d(encoding) (parameter gradients ignored); (2) the HashGrid's backward_backward_input with it as
+			// dL_doutput: the second-order grid gradient and pos_encoding_dy = dy/dx . dL_ddLdinput (grid.h:1697-1800); (3) the
+			// FullyFusedMLP's backward_backward_input with pos_encoding_dy as its dL_ddLdinput (fully_fused_mlp.cu:1088-1198).
+			// Like the reference, dL_ddLdoutput and dL_dinput are not produced.
+			if (!ctx || ctx->n != n || !ctx->dydx.p || !ctx->acts.p) throw std::runtime_error("backward_backward_input: needs the forward's context");
+			if (!input || !dL_ddLdinput || !dL_doutput || !params) throw std::runtime_error("backward_backward_input: null input");
+			m->check_n(n, true);
+			HIP_CHECK(hipSetDevice(m->core.device));
+			StreamSwap sw(m->core, stream);
+			NeusTestbed& t = m->core;
+			hipStream_t s = t.stream;
+			float* g = m->grad_target(dL_dparams, gradient_mode);
+			if (!g) return;
+			const FfNet& f = m->ff;
+			const half_t* dX0 = ff_backward_chain(m, s, n, params, ctx->acts.p, (const half_t*)dL_doutput, nullptr, false);
+			launch_enc_from_rows(s, n, t.lay.L, dX0, f.in_pad, m->denc_tmp.p);
+			launch_enc_ddLdoutput(s, n, n, t.lay.L, dL_ddLdinput, ctx->dydx.p, (half_t*)m->u_tmp.p, m->v4.p);
+			launch_grid_scatter(s, nullptr, n, n, input, 3, t.gl, m->valid(), m->zero_h.p, (const half_t*)m->denc_tmp.p, m->v4.p, g + f.P,
+			                    t.swork, t.scan_tmp.p, t.scan_tmp_bytes);
+			launch_enc_to_rows(s, n, t.lay.L, m->u_tmp.p, m->ff_front.p, f.in_pad);
+			ff_bbi_chain(m, s, n, params, ctx->acts.p, (const half_t*)dL_doutput);
 			launch_mlp_grad_reduce(s, MlpGradReduce{m->ff_partial.p, ff_wgrad_blocks(n), f.P, g, nullptr, nullptr, 0, m->ff_dummy.p});
 			m->finish_grad(dL_dparams, gradient_mode, s);
 			HIP_CHECK(hipGetLastError());
@@ -3151,6 +3461,13 @@ int neus_module_backward_backward_input(NeusModule* m, void* stream, const NeusC
 		NeusTestbed& t = m->core;
 		hipStream_t s = t.stream;
 		float* g = m->grad_target(dL_dparams, gradient_mode);
+		if (m->f32) {  // GridEncoding<float>::backward_backward_input (grid.h:880-1007 with GRAD_T = float)
+			if (g) HIP_CHECK(hipMemsetAsync(g, 0, (size_t)m->n_params() * 4, s));
+			launch_grid_f32_bbi(s, n, t.gl, m->valid(), input, dL_ddLdinput, (const float*)dL_doutput, m->layout, g, ctx->dydx.p, (float*)dL_ddLdoutput);
+			if (g) m->finish_grad(dL_dparams, gradient_mode, s);
+			HIP_CHECK(hipGetLastError());
+			return;
+		}
 		// dL_ddLdoutput (kernel_grid_backward_input_backward_dLdoutput) and dL_ddLdinput as float4 for the scatter
 		const bool relay = m->layout != ENC_LAYOUT_PAIRED && dL_ddLdoutput;
 		launch_enc_ddLdoutput(s, n, n, t.lay.L, dL_ddLdinput, ctx->dydx.p, relay ? (half_t*)m->enc_tmp.p : (half_t*)dL_ddLdoutput, m->v4.p);

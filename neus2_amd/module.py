@@ -15,6 +15,11 @@ import json
 from ._lib import NeusError, NeusModuleInfo, check, lib
 
 
+class Precision(enum.IntEnum):  # tcnn::cpp::EPrecision (cpp_api.h:50-53)
+    Fp32 = 0
+    Fp16 = 1
+
+
 class GradientMode(enum.IntEnum):
     Ignore = 0
     Overwrite = 1
@@ -56,6 +61,7 @@ class Module:
         hp = self.hyperparams()
         self.output_layout = hp.get("output_layout", "AoS")
         self.gradient_precision = hp.get("gradient_precision", "fp16")
+        self.precision = hp.get("precision", "fp16")
 
     @classmethod
     def create_network(cls, n_input_dims, n_output_dims, network, batch_capacity=1 << 18):
@@ -79,9 +85,13 @@ class Module:
 
     @classmethod
     def create_network_with_input_encoding(cls, n_input_dims, n_output_dims, encoding, network, batch_capacity=1 << 18):
-        """tcnn create_network_with_input_encoding (cpp_api.h:108): HashGrid -> FullyFusedMLP (1 hidden ReLU layer), input
-        [n, 3] f32, output [n, 16] fp16, params [W x DE | 16 x W | grid]; backward_backward_input as
-        network_with_input_encoding.h:159-250."""
+        """tcnn create_network_with_input_encoding (cpp_api.h:108; network_with_input_encoding.h): `encoding` HashGrid or
+        Identity ({"scale", "offset"}, identity.h), `network` a FullyFusedMLP of any depth / width (16..128) / activation.
+        Params [network matrices in order | grid] (network first, as NetworkWithInputEncoding's set_params_impl,
+        network_with_input_encoding.h:262-270); output [n, padded n_output_dims] fp16; the grid's output is zero-padded to
+        a multiple of 16 (grid.h:1540-1550). HashGrid -> one hidden ReLU layer with a linear output of <= 16 dims runs as
+        the fused DensityNet kernel, anything else as the grid kernels feeding ffmlp.hip's MFMA layers;
+        backward_backward_input as network_with_input_encoding.h:159-250."""
         te = encoding if isinstance(encoding, str) else json.dumps(encoding)
         tn = network if isinstance(network, str) else json.dumps(network)
         h = C.c_void_p()
@@ -90,10 +100,13 @@ class Module:
         return cls(h, "network_with_input_encoding")
 
     @classmethod
-    def create_encoding(cls, encoding, batch_capacity=1 << 18, n_input_dims=3):
+    def create_encoding(cls, encoding, batch_capacity=1 << 18, n_input_dims=3, requested_precision=Precision.Fp16):
+        """tcnn create_encoding(n_input_dims, encoding, requested_precision) (cpp_api.h:110; cpp_api.cu:174-180): Fp16 =
+        GridEncoding<__half> (fp16 params / output), Fp32 = GridEncoding<float> (f32 params, output and gradients)."""
         text = encoding if isinstance(encoding, str) else json.dumps(encoding)
         h = C.c_void_p()
-        check(lib().neus_module_create_encoding(C.c_uint32(n_input_dims), text.encode(), C.c_uint32(batch_capacity), C.byref(h)))
+        check(lib().neus_module_create_encoding(C.c_uint32(n_input_dims), text.encode(), C.c_int(int(Precision(requested_precision))),
+                                                C.c_uint32(batch_capacity), C.byref(h)))
         return cls(h, "encoding")
 
     def __del__(self):
@@ -139,10 +152,11 @@ class Module:
         import torch
         if output is not None:
             return output
-        return torch.empty(self.output_shape(n), dtype=torch.float16, device="cuda")
+        dt = torch.float32 if self.precision == "fp32" else torch.float16
+        return torch.empty(self.output_shape(n), dtype=dt, device="cuda")
 
     def output_shape(self, n):
-        if self.kind == "mlp":
+        if self.kind in ("mlp", "network_with_input_encoding"):
             return (n, self.n_output_dims)
         if self.kind != "encoding":
             return (n, 16)
@@ -192,8 +206,8 @@ def create_nerf_network(config, batch_capacity=1 << 18):
     return Module.create_nerf_network(config, batch_capacity)
 
 
-def create_encoding(encoding, batch_capacity=1 << 18, n_input_dims=3):
-    return Module.create_encoding(encoding, batch_capacity, n_input_dims)
+def create_encoding(encoding, batch_capacity=1 << 18, n_input_dims=3, requested_precision=Precision.Fp16):
+    return Module.create_encoding(encoding, batch_capacity, n_input_dims, requested_precision)
 
 
 def create_network_with_input_encoding(n_input_dims, n_output_dims, encoding, network, batch_capacity=1 << 18):

@@ -6,6 +6,9 @@ transmittance 1e-4, EMA weights; PSNR of clip(srgb(pred)) vs clip(srgb(gt)), scr
 Reduced Config S: 8 views of the Config S sphere at 200x150 (DTU-scan24 intrinsics scaled by 1/8), base.json (L=14),
 the reference's adaptive rays per batch with a compacted batch of --batch samples (default 4096; the reference's 2^18
 is out of reach for the CPU), --steps steps, geometric init. Same seed, same data, same schedule on both sides.
+--fixed-rays R freezes the rays per batch at R on both sides (round 5): the adaptation follows the compacted counts, which
+fp16 network noise moves, so with it on the two runs drift onto different ray sets; frozen, they see identical rays at
+every step and differ only by the network arithmetic.
 
 Usage:
   python scripts/psnr_anchor.py --side cpu [--steps 2000] [--checkpoints 250,500,1000] > profiles/rNN_psnr_anchor_cpu.jsonl
@@ -48,7 +51,7 @@ def run_cpu(args, sc, cps):
     p = O.init_params(cfg, geo=False)
     geo = geometric_init_weights(14, 64)
     p[: geo.size] = geo
-    tr = CpuTrainer(cfg, ds, p, batch=args.batch, rays_per_batch=args.batch, fixed_rays=False)
+    tr = CpuTrainer(cfg, ds, p, batch=args.batch, rays_per_batch=args.fixed_rays or args.batch, fixed_rays=bool(args.fixed_rays))
     gt = sc["images"][0]
     t0 = time.perf_counter()
     done = 0
@@ -72,7 +75,8 @@ def run_gpu(args, sc, cps):
     from neus2_amd import pyngp
     tb = pyngp.Testbed(pyngp.TestbedMode.Nerf)
     tb.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
-    tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=args.batch)
+    kw = dict(fixed_rays_per_batch=args.fixed_rays) if args.fixed_rays else {}
+    tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=args.batch, **kw)
     tb.background_color = [0.0, 0.0, 0.0, 0.0]
     tb.snap_to_pixel_centers = True
     tb.nerf.rendering_min_transmittance = 1e-4
@@ -101,6 +105,7 @@ def main():
     ap.add_argument("--height", type=int, default=150)
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--spp", type=int, default=8)
+    ap.add_argument("--fixed-rays", type=int, default=0, help="rays per batch frozen at this many on both sides (0: adaptive)")
     args = ap.parse_args()
     cps = sorted({int(c) for c in args.checkpoints.split(",") if c and int(c) < args.steps} | {args.steps})
     sc = scene(args)

@@ -19,8 +19,9 @@ def parse(path, names=NAMES):
         m = re.match(r"\s+(\S.*?) dispatches=\d+ grid=\d+", line)
         if m:
             name = m.group(1)
-            # k_march is the templated march itself ("k_march<"), not k_march_numsteps / k_march_write
-            cur = next((v for k, v in names.items() if (k + "<" in name if k == "k_march" else k in name)), None)
+            # k_march is the march itself: the templated k_march<...> or the balanced k_march_bal (the default), not
+            # k_march_numsteps / k_march_write / k_march_scan
+            cur = next((v for k, v in names.items() if (re.match(r"k_march(<|_bal\b)", name) if k == "k_march" else k in name)), None)
             continue
         m = re.match(r"\s+(\w+)\s+([-+0-9.eE]+)$", line)
         if m and cur:

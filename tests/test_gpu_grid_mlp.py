@@ -1,0 +1,177 @@
+"""create_network_with_input_encoding (cpp_api.h:108; network_with_input_encoding.h) beyond the fused one-hidden-layer
+network (VERDICT r4 Missing #3): a HashGrid in front of FullyFusedMLPs of other depths, widths and activations (the
+encoding's kernels composed with ffmlp.hip's MFMA layers: GridMlp), and an Identity encoding with scale / offset.
+Against a float64 autograd restatement (tests/torch_ref.hash_grid + the MLP) with the kernels' fp16 storage points:
+* forward (GridEncoding's zero padding to the network width, grid.h:1540-1550; the MLP's layers);
+* backward (network_with_input_encoding.h:126-156): the MLP and grid blocks of dL_dparams, dL_dinput;
+* backward_backward_input (network_with_input_encoding.h:159-250: the network's backward for dL/d(encoding), the
+  encoding's backward_backward_input, the network's backward_backward_input with pos_encoding_dy): the MLP and grid
+  blocks of the second-order gradient (ReLU networks with a linear output, where tcnn's chain is exact);
+* the Identity encoding: bitwise create_network on x * scale + offset (forward), dL_dinput scaled by `scale`."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+N = 1024
+CASES = [
+    dict(L=8, W=32, NH=2, act="ReLU", out_act="None", n_out=4),
+    dict(L=6, W=64, NH=1, act="ReLU", out_act="Sigmoid", n_out=3),
+    dict(L=4, W=128, NH=3, act="ReLU", out_act="None", n_out=16),
+]
+
+
+def _record(test, **metrics):
+    import json
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "parity_metrics.jsonl"), "a") as f:
+        f.write(json.dumps({"test": test, **{k: float(v) for k, v in metrics.items()}}) + "\n")
+
+
+def _rel_cos(x, y):
+    x, y = np.asarray(x, np.float64).ravel(), np.asarray(y, np.float64).ravel()
+    return np.linalg.norm(x - y) / max(np.linalg.norm(y), 1e-30), x @ y / max(np.linalg.norm(x) * np.linalg.norm(y), 1e-30)
+
+
+def _r16_fn(torch):
+    class R16(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, v):
+            return v.to(torch.float16).to(torch.float64)
+
+        @staticmethod
+        def backward(ctx, g):
+            return R16.apply(g)
+    return R16.apply
+
+
+def _act(name, x, torch):
+    return {"ReLU": torch.relu, "Sigmoid": torch.sigmoid}.get(name, lambda v: v)(x)
+
+
+@pytest.mark.parametrize("case", range(len(CASES)))
+def test_grid_mlp_module(torch_cuda, case):
+    import torch
+    from torch_ref import grid_tables, hash_grid
+    from neus2_amd.module import GradientMode, Module
+    t = torch_cuda
+    c = CASES[case]
+    L, W, NH = c["L"], c["W"], c["NH"]
+    log2t = 14
+    enc_cfg = {"otype": "HashGrid", "n_levels": L, "n_features_per_level": 2, "log2_hashmap_size": log2t, "base_resolution": 16,
+               "per_level_scale": 1.5}
+    net_cfg = {"otype": "FullyFusedMLP", "activation": c["act"], "output_activation": c["out_act"], "n_neurons": W,
+               "n_hidden_layers": NH, "gradient_precision": "fp32"}
+    m = Module.create_network_with_input_encoding(3, c["n_out"], enc_cfg, net_cfg, batch_capacity=N)
+    DE = (2 * L + 15) // 16 * 16
+    out_pad = (c["n_out"] + 15) // 16 * 16
+    shapes = [(W, DE)] + [(W, W)] * (NH - 1) + [(out_pad, W)]
+    n_mlp = sum(r * k for r, k in shapes)
+    off, res = grid_tables(L, log2t, 16, 1.5)
+    assert m.n_params == n_mlp + 2 * off[-1] and m.n_output_dims == out_pad and m.info["grid_offset"] == n_mlp
+    hp = m.hyperparams()
+    assert hp["network"]["n_hidden_layers"] == NH and hp["encoding"]["otype"] == "HashGrid"
+    # initialisation: the network's matrices (xavier, in order), then the grid from the same pcg32
+    p0 = m.initialize_params(1337).cpu().numpy()
+    o = 0
+    for r, k in shapes:
+        assert np.abs(p0[o:o + r * k]).max() <= np.sqrt(6.0 / (r + k))
+        o += r * k
+    assert np.abs(p0[n_mlp:]).max() <= 1e-4
+    rng = np.random.default_rng(case)
+    mats_h = [rng.normal(0, 1.2 / np.sqrt(k), (r, k)) for r, k in shapes]
+    ph = np.concatenate([a.ravel() for a in mats_h] + [rng.uniform(-1, 1, 2 * off[-1])]).astype(np.float16)
+    params = t.from_numpy(ph.view(np.int16).copy()).cuda()
+    pos = rng.uniform(0.02, 0.98, (N, 3)).astype(np.float32)
+    x = t.from_numpy(pos).cuda()
+    ctx, y = m.forward(x, params, prepare_input_gradients=True)
+    r16 = _r16_fn(torch)
+    pd = torch.tensor(ph.astype(np.float64))
+    mats, o = [], 0
+    for r, k in shapes:
+        mats.append(pd[o:o + r * k].reshape(r, k).clone().requires_grad_(True))
+        o += r * k
+    tab = pd[n_mlp:].reshape(-1, 2).clone().requires_grad_(True)
+    xt = torch.tensor(pos.astype(np.float64), requires_grad=True)
+    h = torch.nn.functional.pad(r16(hash_grid(xt, tab, off, res)), (0, DE - 2 * L))
+    pre = []
+    for li, Wm in enumerate(mats):
+        z = r16(h @ Wm.T)
+        pre.append(z)
+        h = r16(_act(c["out_act"] if li == len(mats) - 1 else c["act"], z, torch))
+    out = h
+    yo, ro = y.float().cpu().numpy(), out.detach().numpy()
+    err = np.abs(yo - ro)
+    within = np.mean(err <= 1e-2 * np.abs(ro) + 4e-3)
+    _record(f"grid_mlp_forward_{case}", frac_within=within, max_err=err.max())
+    assert within >= 0.99, err.max()
+    # samples whose hidden pre-activations sit within fp16 rounding of 0 may take the other ReLU branch: dL = 0 there
+    ambiguous = np.zeros(N, bool)
+    for z in pre[:-1]:
+        ambiguous |= (np.abs(z.detach().numpy()) < 4e-3).any(axis=1)
+    assert ambiguous.mean() < 0.6
+    dlo = rng.normal(0, 1, (N, out_pad)).astype(np.float16)
+    dlo[ambiguous] = 0
+    dlo_t = torch.tensor(dlo.astype(np.float64))
+    S = (out * dlo_t).sum()
+    grads = torch.autograd.grad(S, mats + [tab, xt], create_graph=True)
+    gmats, gtab, gx = grads[:len(mats)], grads[-2], grads[-1]
+    dlo_dev = t.from_numpy(dlo.view(np.int16).copy()).cuda()
+    g = t.zeros(m.n_params, dtype=t.float32, device="cuda")
+    dx = t.zeros((N, 3), dtype=t.float32, device="cuda")
+    m.backward(ctx, x, dlo_dev, params, dL_dparams=g, dL_dinput=dx, mode=GradientMode.Overwrite, output=y)
+    gm = g.cpu().numpy()
+    blocks, o = {}, 0
+    for li, (r, k) in enumerate(shapes):
+        blocks[f"W{li}"] = (gm[o:o + r * k], gmats[li])
+        o += r * k
+    blocks["grid"] = (gm[n_mlp:], gtab)
+    blocks["dinput"] = (dx.cpu().numpy(), gx)
+    if c["out_act"] == "None":
+        v = rng.normal(0, 1, (N, 3)).astype(np.float32)
+        S2 = (gx * torch.tensor(v.astype(np.float64))).sum()
+        g2 = torch.autograd.grad(S2, mats + [tab], allow_unused=True)
+        gd2 = t.zeros(m.n_params, dtype=t.float32, device="cuda")
+        m.backward_backward_input(ctx, x, t.from_numpy(v).cuda(), dlo_dev, params, dL_dparams=gd2, mode=GradientMode.Overwrite)
+        g2m, o = gd2.cpu().numpy(), 0
+        for li, (r, k) in enumerate(shapes):
+            if g2[li] is not None and np.linalg.norm(g2[li].detach().numpy()) > 0:
+                blocks[f"W{li}_2nd"] = (g2m[o:o + r * k], g2[li])
+            o += r * k
+        blocks["grid_2nd"] = (g2m[n_mlp:], g2[-1])
+    res_ = {name: _rel_cos(a, b.detach().numpy()) for name, (a, b) in blocks.items()}
+    _record(f"grid_mlp_{case}", **{f"rel_{k}": v_[0] for k, v_ in res_.items()}, **{f"cos_{k}": v_[1] for k, v_ in res_.items()})
+    for name, (rel, cos) in res_.items():
+        assert rel <= 3e-2 and cos >= 0.999, (name, rel, cos)
+
+
+def test_identity_encoding_scale_offset(torch_cuda):
+    """NetworkWithInputEncoding(Identity{scale, offset} -> FullyFusedMLP): the forward equals create_network on
+    x * scale + offset bit for bit (identity.h:44-70), the input gradient is the plain network's times `scale`
+    (identity.h:86-104), the parameter gradients are equal."""
+    from neus2_amd.module import GradientMode, Module
+    t = torch_cuda
+    net = {"otype": "FullyFusedMLP", "n_neurons": 64, "n_hidden_layers": 2, "activation": "ReLU", "output_activation": "None",
+           "gradient_precision": "fp32"}
+    scale, offset = 0.5, 0.25
+    a = Module.create_network_with_input_encoding(5, 3, {"otype": "Identity", "scale": scale, "offset": offset}, net, batch_capacity=512)
+    b = Module.create_network(5, 3, net, batch_capacity=512)
+    assert a.n_params == b.n_params and a.hyperparams()["encoding"]["scale"] == scale
+    params = t.from_numpy((b.initialize_params(5).cpu().numpy() * 0.8).astype(np.float16).view(np.int16)).cuda()
+    rng = np.random.default_rng(2)
+    x = rng.uniform(-1, 1, (512, 5)).astype(np.float32)
+    xa = t.from_numpy(x).cuda()
+    xb = t.from_numpy((x * np.float32(scale) + np.float32(offset)).astype(np.float32)).cuda()
+    ca, ya = a.forward(xa, params)
+    cb, yb = b.forward(xb, params)
+    np.testing.assert_array_equal(ya.cpu().numpy().view(np.uint16), yb.cpu().numpy().view(np.uint16))
+    dl = t.from_numpy(rng.normal(0, 1, (512, 16)).astype(np.float16).view(np.int16)).cuda()
+    ga, gb = t.zeros(a.n_params, device="cuda"), t.zeros(b.n_params, device="cuda")
+    da, db = t.zeros((512, 5), device="cuda"), t.zeros((512, 5), device="cuda")
+    a.backward(ca, xa, dl, params, dL_dparams=ga, dL_dinput=da, mode=GradientMode.Overwrite)
+    b.backward(cb, xb, dl, params, dL_dparams=gb, dL_dinput=db, mode=GradientMode.Overwrite)
+    np.testing.assert_array_equal(ga.cpu().numpy(), gb.cpu().numpy())
+    np.testing.assert_array_equal(da.cpu().numpy(), db.cpu().numpy() * np.float32(scale))

@@ -245,6 +245,69 @@ def test_encoding_module(torch_cuda, layout):
     np.testing.assert_array_equal(g16.cpu().numpy().view(np.uint16), g.cpu().numpy().astype(np.float16).view(np.uint16))
 
 
+@pytest.mark.parametrize("layout", ["AoS", "SoA"])
+def test_encoding_module_fp32(torch_cuda, layout):
+    """create_encoding(..., requested_precision=Fp32) (cpp_api.h:110, cpp_api.cu:174-183: GridEncoding<float>): f32 params,
+    output, dL_doutput and gradients. Forward, backward (dL_dparams, dL_dinput) and backward_backward_input
+    (second-order dL_dparams, dL_ddLdoutput) vs float64 autograd at fp32 tolerance; Overwrite / Accumulate; paired
+    layout refused; the fp16 module (Fp16, the default) is unchanged."""
+    import torch
+    from torch_ref import grid_tables, hash_grid
+    from neus2_amd.module import GradientMode, Module, Precision
+    t = torch_cuda
+    L = 8
+    enc_cfg = {"otype": "HashGrid", "n_levels": L, "n_features_per_level": 2, "log2_hashmap_size": 14, "base_resolution": 16,
+               "per_level_scale": 1.5, "output_layout": layout}
+    m = Module.create_encoding(enc_cfg, batch_capacity=N, requested_precision=Precision.Fp32)
+    assert m.info["param_precision"] == 0 and m.info["output_precision"] == 0 and m.hyperparams()["precision"] == "fp32"
+    with pytest.raises(Exception):
+        Module.create_encoding(dict(enc_cfg, output_layout="paired"), batch_capacity=N, requested_precision=Precision.Fp32)
+    off, res = grid_tables(L, 14, 16, 1.5)
+    rng = np.random.default_rng(19)
+    pf = rng.uniform(-1, 1, m.n_params).astype(np.float32)
+    params = t.from_numpy(pf).cuda()
+    pos = rng.uniform(0.02, 0.98, (N, 3)).astype(np.float32)
+    x = t.from_numpy(pos).cuda()
+    ctx, y = m.forward(x, params, prepare_input_gradients=True)
+    assert y.dtype == t.float32 and tuple(y.shape) == m.output_shape(N)
+    tab = torch.tensor(pf.astype(np.float64).reshape(-1, 2), requires_grad=True)
+    xt = torch.tensor(pos.astype(np.float64), requires_grad=True)
+    e = hash_grid(xt, tab, off, res)
+    rel_f, _ = _rel_cos(_to_nf(y.cpu().numpy(), layout, N, L), e.detach().numpy())
+    dly_nf = rng.normal(0, 1, (N, 2 * L)).astype(np.float32)
+    dly_t = torch.tensor(dly_nf.astype(np.float64), requires_grad=True)
+    S = (e * dly_t).sum()
+    g_tab, g_x = torch.autograd.grad(S, (tab, xt), create_graph=True)
+    v = rng.normal(0, 1, (N, 3)).astype(np.float32)
+    S2 = (g_x * torch.tensor(v.astype(np.float64))).sum()
+    g2_tab, g2_dly = torch.autograd.grad(S2, (tab, dly_t))
+    dly_dev = t.from_numpy(_from_nf(dly_nf, layout, N, L)).cuda()
+    g = t.zeros(m.n_params, dtype=t.float32, device="cuda")
+    dx = t.zeros((N, 3), dtype=t.float32, device="cuda")
+    m.backward(ctx, x, dly_dev, params, dL_dparams=g, dL_dinput=dx, mode=GradientMode.Overwrite)
+    rel_p, cos_p = _rel_cos(g.cpu().numpy(), g_tab.detach().numpy().ravel())
+    rel_x, _ = _rel_cos(dx.cpu().numpy(), g_x.detach().numpy())
+    g2 = t.full((m.n_params,), 7.0, dtype=t.float32, device="cuda")  # Overwrite must not read the old contents
+    ddo = t.zeros(m.output_shape(N), dtype=t.float32, device="cuda")
+    m.backward_backward_input(ctx, x, t.from_numpy(v).cuda(), dly_dev, params, dL_dparams=g2, dL_ddLdoutput=ddo)
+    rel_p2, cos_p2 = _rel_cos(g2.cpu().numpy(), g2_tab.numpy().ravel())
+    rel_o2, _ = _rel_cos(_to_nf(ddo.cpu().numpy(), layout, N, L), g2_dly.numpy())
+    _record("module_encoding_fp32_" + layout, rel_forward=rel_f, rel_params=rel_p, rel_dinput=rel_x, rel_params_2nd=rel_p2,
+            rel_ddLdoutput=rel_o2)
+    assert rel_f <= 1e-6, rel_f
+    assert rel_p <= 1e-5 and cos_p >= 0.9999999, (rel_p, cos_p)
+    assert rel_x <= 1e-5, rel_x
+    assert rel_p2 <= 1e-5 and cos_p2 >= 0.9999999, (rel_p2, cos_p2)
+    assert rel_o2 <= 1e-5, rel_o2
+    acc = g.clone()
+    m.backward_backward_input(ctx, x, t.from_numpy(v).cuda(), dly_dev, params, dL_dparams=acc, mode=GradientMode.Accumulate)
+    np.testing.assert_allclose(acc.cpu().numpy(), g.cpu().numpy() + g2.cpu().numpy(), rtol=1e-5, atol=1e-6)
+    # progressive levels: set_training_step(1) -> levels 0..4 (tcnn's defaults), the rest 0
+    m.set_training_step(1)
+    y3 = _to_nf(m.inference(x, params).cpu().numpy(), layout, N, L)
+    assert not y3[:, 10:].any() and np.array_equal(y3[:, :10], _to_nf(y.cpu().numpy(), layout, N, L)[:, :10])
+
+
 @pytest.mark.parametrize("n_levels,width", [(8, 64), (14, 64), (1, 16)])
 def test_network_with_input_encoding_module(torch_cuda, n_levels, width):
     """create_network_with_input_encoding (cpp_api.h:108): HashGrid -> FullyFusedMLP (1 hidden ReLU layer) on the MFMA
