@@ -344,6 +344,10 @@ int neus_debug_set_xcd_shift(NeusTestbed* tb, uint32_t n_blocks);
 /* Development: the last step's compacted training batch (coords batch x 7 f32, dL/doutput batch x 16 fp16 bits) and
  * per-ray losses (2^18 f32); host buffers, each nullable. */
 int neus_debug_get_batch(NeusTestbed* tb, float* coords_out, uint16_t* dl_dout_out, float* loss_out);
+/* Diagnostic: `launches` launches of an fp32-denormal arithmetic probe (march.hip k_denorm_probe) over n threads on a
+ * stream of its own, every value compared with the CPU's bits. stats[10]: launches, mismatches, mismatches by 16-lane row
+ * of the wave (4), values flushed to zero, distinct MODE register values (1 or 2), the first MODE, a differing MODE. */
+int neus_debug_denorm_probe(int device, uint32_t n, uint32_t launches, uint64_t* stats);
 /* Development: nbytes at offset of one step-workspace buffer (ids in testbed.cpp neus_debug_get_buffer). */
 int neus_debug_get_buffer(NeusTestbed* tb, int id, uint64_t offset, uint64_t nbytes, void* host);
 /* Development: the loss-gradient kernel replayed on the last step's state into a separate buffer (batch x 16 fp16). */

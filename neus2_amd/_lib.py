@@ -112,7 +112,7 @@ EXPORTS = [
     "neus_testbed_set_params", "neus_testbed_get_gradients", "neus_testbed_get_ema_params",
     "neus_testbed_get_half_params",
     "neus_testbed_get_density_grid", "neus_testbed_set_density_grid", "neus_testbed_restore_state", "neus_testbed_get_rng", "neus_testbed_render", "neus_testbed_sdf_on_grid",
-    "neus_testbed_marching_cubes", "neus_testbed_mc_density", "neus_testbed_get_mesh", "neus_testbed_mesh_vertex_colors", "neus_mc_table", "neus_prepare_image_rgba8", "neus_testbed_ray_counts", "neus_debug_time_kernel", "neus_debug_march_stats", "neus_debug_exclusive_scan", "neus_debug_scan_giveup", "neus_debug_inject_health", "neus_debug_set_lds_fill", "neus_debug_set_lds_fill_all", "neus_debug_set_xcd_shift", "neus_debug_get_batch", "neus_debug_get_buffer", "neus_debug_replay_loss_grad", "neus_debug_sample_rays_round0", "neus_debug_march_profile", "neus_debug_scatter_stats", "neus_debug_scatter_parts", "neus_testbed_time_kernel", "neus_testbed_stream",
+    "neus_testbed_marching_cubes", "neus_testbed_mc_density", "neus_testbed_get_mesh", "neus_testbed_mesh_vertex_colors", "neus_mc_table", "neus_prepare_image_rgba8", "neus_testbed_ray_counts", "neus_debug_time_kernel", "neus_debug_march_stats", "neus_debug_exclusive_scan", "neus_debug_scan_giveup", "neus_debug_inject_health", "neus_debug_set_lds_fill", "neus_debug_set_lds_fill_all", "neus_debug_set_xcd_shift", "neus_debug_denorm_probe", "neus_debug_get_batch", "neus_debug_get_buffer", "neus_debug_replay_loss_grad", "neus_debug_sample_rays_round0", "neus_debug_march_profile", "neus_debug_scatter_stats", "neus_debug_scatter_parts", "neus_testbed_time_kernel", "neus_testbed_stream",
     "neus_testbed_synchronize", "neus_testbed_set_profiling", "neus_testbed_kernel_times", "neus_testbed_set_infer_timing", "neus_testbed_infer_timing",
     "neus_nccl_unique_id", "neus_testbed_init_data_parallel", "neus_testbed_init_data_parallel_ex",
     "neus_testbed_data_parallel_info", "neus_testbed_set_exchange_overlap", "neus_local_group_create", "neus_local_group_destroy",

@@ -17,6 +17,8 @@
 #include "march_common.h"
 #include "scan_lookback.h"
 #include <algorithm>
+#include <cstring>
+#include <vector>
 
 namespace neus {
 
@@ -1581,6 +1583,66 @@ void launch_xcd_shift(hipStream_t s, uint32_t n_blocks) { k_xcd_shift<<<n_blocks
 void launch_fill_lds(hipStream_t s, uint32_t pattern) {
 	// 40 KB per workgroup, 4 resident per CU: the whole 160 KB of every CU (256 CUs), twice over
 	k_fill_lds<<<2048, 256, FILL_LDS_BYTES, s>>>(pattern);
+}
+
+// Diagnostic (scripts/diag_denorm.py): fp32 denormal arithmetic per lane — det_expf into the denormal range, a product
+// of denormal results, ldexpf below FLT_MIN, a product that passes through a denormal and is scaled back — plus the
+// wave's MODE register (denormal / rounding controls, s_getreg: a register read). The host compares every launch's bits
+// with the same expressions evaluated on the CPU (denormals kept, as the kernels' code objects request).
+NEUS_HD void denorm_probe_values(uint32_t i, float v[4]) {
+	v[0] = det_expf(-87.0f - (float)(i & 1023u) * 0.015f);
+	v[1] = v[0] * 3.7f;
+	v[2] = ldexpf(1.5f, -127 - (int)(i % 20u));
+	const float a = 1e-20f * (float)(1u + (i & 7u));
+	const float b = a * 1e-19f;
+	v[3] = b * 1e20f;
+}
+__global__ void __launch_bounds__(256) k_denorm_probe(uint32_t n, uint32_t* __restrict__ out) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	float v[4];
+	denorm_probe_values(i, v);
+	uint32_t* o = out + (size_t)i * 5;
+#pragma unroll
+	for (int k = 0; k < 4; ++k) o[k] = __float_as_uint(v[k]);
+	o[4] = (uint32_t)__builtin_amdgcn_s_getreg(1 | (31 << 11));  // HW_REG_MODE, bits 0..31
+}
+// stats: [0] launches, [1] mismatching values, [2..5] mismatches by 16-lane row of the wave, [6] values flushed to 0,
+// [7] distinct MODE values seen, [8] first MODE, [9] a MODE differing from the first (0 if none)
+void debug_denorm_probe(hipStream_t s, uint32_t n, uint32_t launches, uint64_t* stats) {
+	uint32_t* d = nullptr;
+	if (hipMalloc((void**)&d, (size_t)n * 5 * 4) != hipSuccess) throw std::runtime_error("denorm probe: hipMalloc");
+	std::vector<uint32_t> h((size_t)n * 5), want((size_t)n * 4);
+	for (uint32_t i = 0; i < n; ++i) {
+		float v[4];
+		denorm_probe_values(i, v);
+		for (int k = 0; k < 4; ++k) std::memcpy(&want[(size_t)i * 4 + k], &v[k], 4);
+	}
+	for (int k = 0; k < 10; ++k) stats[k] = 0;
+	uint32_t mode0 = 0;
+	bool have_mode = false;
+	for (uint32_t l = 0; l < launches; ++l) {
+		k_denorm_probe<<<(n + 255) / 256, 256, 0, s>>>(n, d);
+		if (hipMemcpyAsync(h.data(), d, h.size() * 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
+			(void)hipFree(d);
+			throw std::runtime_error("denorm probe: copy");
+		}
+		++stats[0];
+		for (uint32_t i = 0; i < n; ++i) {
+			for (int k = 0; k < 4; ++k) {
+				const uint32_t g = h[(size_t)i * 5 + k], w = want[(size_t)i * 4 + k];
+				if (g != w) {
+					++stats[1];
+					++stats[2 + ((i & 63u) >> 4)];
+					if ((g & 0x7fffffffu) == 0) ++stats[6];
+				}
+			}
+			const uint32_t m = h[(size_t)i * 5 + 4];
+			if (!have_mode) { mode0 = m; have_mode = true; stats[7] = 1; stats[8] = m; }
+			else if (m != mode0 && stats[9] == 0) { stats[9] = m; stats[7] = 2; }
+		}
+	}
+	(void)hipFree(d);
 }
 
 void launch_march_write(hipStream_t s, uint32_t cap, StepState* st, const DevDataset& ds, const float* rays, const MarchWork& mw, const uint32_t* nreq,

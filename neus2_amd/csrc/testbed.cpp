@@ -1638,11 +1638,7 @@ int neus_testbed_train(NeusTestbed* tb, uint32_t n_steps) {
 		// the LDS-garbage test hook is this thread's while its steps are queued (other testbeds / threads unaffected);
 		// the pattern alternates with its complement from step to step
 		struct FillScope { ~FillScope() { g_dbg_lds_fill = 0; g_dbg_xcd_shift = 0; } } fill_scope;
-		static const bool lock_launches = [] { const char* e = std::getenv("NEUS_LAUNCH_LOCK"); return e && e[0] == '1'; }();
-		static std::mutex launch_mu;
 		for (uint32_t i = 0; i < n_steps; ++i) {
-			std::unique_lock<std::mutex> lk(launch_mu, std::defer_lock);
-			if (lock_launches) lk.lock();
 			g_dbg_lds_fill = tb->dbg_lds_fill_all ? ((tb->training_step & 1) ? ~tb->dbg_lds_fill_all : tb->dbg_lds_fill_all) : 0u;
 			g_dbg_xcd_shift = tb->dbg_xcd_shift;
 			tb->train_step();
@@ -2387,6 +2383,18 @@ int neus_debug_scan_giveup(void* stream, const uint32_t* in, uint32_t* out, uint
 int neus_debug_set_lds_fill(NeusTestbed* tb, uint32_t pattern) { return guard([&] { tb->dbg_lds_fill = pattern; }); }
 int neus_debug_set_lds_fill_all(NeusTestbed* tb, uint32_t pattern) { return guard([&] { tb->dbg_lds_fill_all = pattern; }); }
 int neus_debug_set_xcd_shift(NeusTestbed* tb, uint32_t n_blocks) { return guard([&] { tb->dbg_xcd_shift = n_blocks; }); }
+// Diagnostic: `launches` launches of the fp32-denormal probe on a stream of its own (device `device`), each compared with
+// the CPU's bits; stats as debug_denorm_probe (march.hip)
+int neus_debug_denorm_probe(int device, uint32_t n, uint32_t launches, uint64_t* stats) {
+	return guard([&] {
+		if (!stats || n == 0) throw std::runtime_error("neus_debug_denorm_probe: bad argument");
+		HIP_CHECK(hipSetDevice(device));
+		hipStream_t s = nullptr;
+		HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+		try { debug_denorm_probe(s, n, launches, stats); } catch (...) { (void)hipStreamDestroy(s); throw; }
+		HIP_CHECK(hipStreamDestroy(s));
+	});
+}
 // Development: raw bytes of one step-workspace buffer (ids: 0 sa, 1 ekt, 2 ck4, 3 cke, 4 racc, 5 rgr, 6 rT, 7 rek,
 // 8 ccount, 9 net_out, 10 coords, 11 base, 12 numsteps, 13 cmap, 14 nreq)
 int neus_debug_get_buffer(NeusTestbed* tb, int id, uint64_t offset, uint64_t nbytes, void* host) {

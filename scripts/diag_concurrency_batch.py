@@ -43,6 +43,10 @@ def main():
         check(lib().neus_debug_get_batch(tb.handle, C.c_void_p(co.ctypes.data), C.c_void_p(dl.ctypes.data), C.c_void_p(lo.ctypes.data)))
         nreq, cc, ns = tb.ray_counts(R)
         out = {"coords": co, "dl": dl, "loss": lo, "nreq": nreq, "cc": cc, "ns": ns, "grads": tb.get_gradients(), "params": tb.get_params()}
+        if os.environ.get("NEUS_DBG_LOSS_VALS") == "1":
+            dv = np.zeros((B, 8), np.float32)
+            check(lib().neus_debug_get_buffer(tb.handle, C.c_int(16), C.c_uint64(0), C.c_uint64(B * 32), C.c_void_p(dv.ctypes.data)))
+            out["dbg_vals"] = dv
         rdl = np.zeros((B, 16), np.uint16)
         check(lib().neus_debug_replay_loss_grad(tb.handle, C.c_void_p(rdl.ctypes.data)))
         out["replay_dl"] = rdl
@@ -101,7 +105,7 @@ def main():
         for i in range(2):
             out = {"trial": trial, "testbed": i}
             for k, (a, b) in enumerate(zip(rr, recs[i])):
-                diff = [key for key in a if not key.startswith("snapdiff_") and not np.array_equal(a[key].view(np.uint8), b[key].view(np.uint8))]
+                diff = [key for key in a if not key.startswith("snapdiff_") and key != "dbg_vals" and not np.array_equal(a[key].view(np.uint8), b[key].view(np.uint8))]
                 if not diff:
                     continue
                 out["step"] = k + 1
@@ -113,6 +117,17 @@ def main():
                     out["dl_n_rows"] = int(rows.size)
                     out["dl_cols"] = [int(x) for x in cols]
                     r0 = rows[0]
+                    lanes = np.bincount(rows % 64, minlength=64)
+                    out["dl_row_lanes"] = {int(k): int(v) for k, v in enumerate(lanes) if v}
+                    if "dbg_vals" in a:
+                        names = ["inv_s", "dloss_dalpha", "dadem", "dem_dinvs", "dadpe", "dpe_dinvs", "dloss_dinvs", "dloss_dvar"]
+                        va, vb = a["dbg_vals"][rows], b["dbg_vals"][rows]
+                        out["vals_differ_in_dl_rows"] = {nm: int((va[:, k].view(np.uint32) != vb[:, k].view(np.uint32)).sum()) for k, nm in enumerate(names)}
+                        allr = np.nonzero((a["dbg_vals"].view(np.uint32) != b["dbg_vals"].view(np.uint32)).any(1))[0]
+                        out["vals_rows_differ_total"] = int(allr.size)
+                        out["vals_rows_lanes"] = {int(k): int(v) for k, v in enumerate(np.bincount(allr % 64, minlength=64)) if v}
+                        r0_ = rows[0]
+                        out["vals_first"] = {"ref": a["dbg_vals"][r0_].tolist(), "got": b["dbg_vals"][r0_].tolist()}
                     out["dl_first"] = {"ref": a["dl"][r0].view(np.float16).astype(float).tolist(), "got": b["dl"][r0].view(np.float16).astype(float).tolist(),
                                        "coords": a["coords"][r0].tolist()}
                 for key in ("loss", "cc", "nreq", "ns"):

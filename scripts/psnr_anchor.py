@@ -47,6 +47,8 @@ def run_cpu(args, sc, cps):
     from cpu_step import CpuTrainer
     from neus2_amd.pyngp import geometric_init_weights
     cfg = O.make_cfg()
+    if args.sum_order != "index":
+        O.set_sum_order(args.sum_order)
     ds = O.Dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"])
     p = O.init_params(cfg, geo=False)
     geo = geometric_init_weights(14, 64)
@@ -67,7 +69,7 @@ def run_cpu(args, sc, cps):
         img, _ = O.render(cfg, ema, tr.valid_level(tr.training_step), ds, tr.bitfield, sc["xforms"][0], sc["focal"][0],
                           sc["principal"][0], gt.shape[1], gt.shape[0], spp=args.spp, snap=True, min_transmittance=1e-4, cos_anneal=1.0)
         psnr, mse = psnr_of(img, gt)
-        print(json.dumps({"side": "cpu", "step": cp, "psnr": psnr, "mse": mse, "wall_s": round(time.perf_counter() - t0, 1),
+        print(json.dumps({"side": "cpu", "sum_order": args.sum_order, "step": cp, "psnr": psnr, "mse": mse, "wall_s": round(time.perf_counter() - t0, 1),
                           "rays_per_batch": int(tr.R), "compacted": int(tr.last["compacted"]), "threads": O.num_threads()}), flush=True)
 
 
@@ -77,6 +79,15 @@ def run_gpu(args, sc, cps):
     tb.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
     kw = dict(fixed_rays_per_batch=args.fixed_rays) if args.fixed_rays else {}
     tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=args.batch, **kw)
+    if args.perturb:
+        # ensemble member: the lowest mantissa bit of a random 1 % of the initial fp32 parameters flipped (a change far
+        # below the fp16 rounding the network computes with), to measure how far fp16-level noise alone moves the PSNR
+        import numpy as np
+        p = tb.get_params().copy()
+        rng = np.random.default_rng(args.perturb)
+        idx = rng.choice(p.size, p.size // 100, replace=False)
+        p.view(np.uint32)[idx] ^= np.uint32(1)
+        tb.set_params(p)
     tb.background_color = [0.0, 0.0, 0.0, 0.0]
     tb.snap_to_pixel_centers = True
     tb.nerf.rendering_min_transmittance = 1e-4
@@ -91,7 +102,7 @@ def run_gpu(args, sc, cps):
         img = tb.render(gt.shape[1], gt.shape[0], spp=args.spp)
         psnr, mse = psnr_of(img, gt)
         st = tb.stats()
-        print(json.dumps({"side": "gpu", "step": cp, "psnr": psnr, "mse": mse, "wall_s": round(time.perf_counter() - t0, 2),
+        print(json.dumps({"side": "gpu", "perturb": args.perturb, "step": cp, "psnr": psnr, "mse": mse, "wall_s": round(time.perf_counter() - t0, 2),
                           "rays_per_batch": st["rays_per_batch"], "compacted": st["measured_batch_size"]}), flush=True)
 
 
@@ -106,10 +117,19 @@ def main():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--spp", type=int, default=8)
     ap.add_argument("--fixed-rays", type=int, default=0, help="rays per batch frozen at this many on both sides (0: adaptive)")
+    ap.add_argument("--sum-order", default="index", help="cpu: the oracle's fp32 summation order (oracle.SUM_ORDERS)")
+    ap.add_argument("--perturb", type=int, default=0, help="gpu: seed of a 1-ulp flip of 1 %% of the initial parameters (0: none)")
+    ap.add_argument("--ensemble", type=int, default=0, help="gpu: also run perturb seeds 1..N")
     args = ap.parse_args()
     cps = sorted({int(c) for c in args.checkpoints.split(",") if c and int(c) < args.steps} | {args.steps})
     sc = scene(args)
-    (run_cpu if args.side == "cpu" else run_gpu)(args, sc, cps)
+    if args.side == "cpu":
+        run_cpu(args, sc, cps)
+        return
+    run_gpu(args, sc, cps)
+    for k in range(1, args.ensemble + 1):
+        args.perturb = k
+        run_gpu(args, sc, cps)
 
 
 if __name__ == "__main__":

@@ -11,7 +11,11 @@ order with its atomic within-cell order, and the region scatter's split heavy bu
   (neus_debug_set_lds_fill_all): a kernel that read LDS it had not written in its own launch would change the result;
 * concurrency: two testbeds trained at the same time from two host threads on the same GPU (the situation of round 4's
   r04d run, whose two-rank test found 5,096 parameters differing), so the atomics' orders and the CU sharing differ.
-After 800 + 16 steps all four hold bitwise the same parameters, gradients, EMA weights and occupancy grid."""
+After 800 + 16 steps all four hold bitwise the same parameters, gradients, EMA weights and occupancy grid.
+Round 5 found what broke the concurrent case: with kernels of two testbeds of one process co-resident on
+a SIMD, a packed-fp32 instruction's upper-half result was read stale in lanes 48-63 (k_loss_grad's dL/doutput column 7;
+6-8 of 12 concurrent pairs differing, 0 of 12 once no object uses packed fp32: profiles/r05i_*, r05j_*). The library is
+built without packed fp32 since; this test passed with that build (profiles/r05j_pytest_determinism.log)."""
 import ctypes as C
 import os
 import threading

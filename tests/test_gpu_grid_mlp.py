@@ -96,7 +96,17 @@ def test_grid_mlp_module(torch_cuda, case):
         o += r * k
     tab = pd[n_mlp:].reshape(-1, 2).clone().requires_grad_(True)
     xt = torch.tensor(pos.astype(np.float64), requires_grad=True)
-    h = torch.nn.functional.pad(r16(hash_grid(xt, tab, off, res)), (0, DE - 2 * L))
+    # GridEncoding<__half> accumulates the features in fp16 (grid.h:275-297): the forward values are the oracle's
+    # bit-exact features, the gradients those of the float64 interpolation (the device's backward works in fp32)
+    import oracle as O
+    ocfg = O.make_cfg(n_levels=L, log2_hashmap_size=log2t, base_resolution=16, per_level_scale=1.5)
+    olay = O.layout(ocfg)
+    op = np.zeros(olay["n_params"], np.float32)
+    op[olay["grid_off"]:olay["grid_off"] + 2 * off[-1]] = ph[n_mlp:].astype(np.float32)
+    renc, _ = O.grid_forward(ocfg, op, pos, L)
+    e = hash_grid(xt, tab, off, res)
+    e = e + (torch.tensor(np.asarray(renc, np.float64)) - e).detach()
+    h = torch.nn.functional.pad(e, (0, DE - 2 * L))
     pre = []
     for li, Wm in enumerate(mats):
         z = r16(h @ Wm.T)
@@ -108,11 +118,12 @@ def test_grid_mlp_module(torch_cuda, case):
     within = np.mean(err <= 1e-2 * np.abs(ro) + 4e-3)
     _record(f"grid_mlp_forward_{case}", frac_within=within, max_err=err.max())
     assert within >= 0.99, err.max()
-    # samples whose hidden pre-activations sit within fp16 rounding of 0 may take the other ReLU branch: dL = 0 there
+    # both sides round the same fp16 inputs; a hidden pre-activation whose fp32 sum sits within the accumulation-order
+    # error of 0 may take the other ReLU branch on the device: dL = 0 for those samples
     ambiguous = np.zeros(N, bool)
     for z in pre[:-1]:
-        ambiguous |= (np.abs(z.detach().numpy()) < 4e-3).any(axis=1)
-    assert ambiguous.mean() < 0.6
+        ambiguous |= (np.abs(z.detach().numpy()) < 1e-4).any(axis=1)
+    assert ambiguous.mean() < 0.3
     dlo = rng.normal(0, 1, (N, out_pad)).astype(np.float16)
     dlo[ambiguous] = 0
     dlo_t = torch.tensor(dlo.astype(np.float64))
@@ -145,7 +156,7 @@ def test_grid_mlp_module(torch_cuda, case):
     res_ = {name: _rel_cos(a, b.detach().numpy()) for name, (a, b) in blocks.items()}
     _record(f"grid_mlp_{case}", **{f"rel_{k}": v_[0] for k, v_ in res_.items()}, **{f"cos_{k}": v_[1] for k, v_ in res_.items()})
     for name, (rel, cos) in res_.items():
-        assert rel <= 3e-2 and cos >= 0.999, (name, rel, cos)
+        assert rel <= 2e-3 and cos >= 0.99999, (name, rel, cos)
 
 
 def test_identity_encoding_scale_offset(torch_cuda):
