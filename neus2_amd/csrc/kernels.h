@@ -65,6 +65,7 @@ struct DevDataset {
 	float cone_angle;
 	RayMotion motion;         // frames >= 1 of a dynamic scene: o' = R o + t, d' = R d (normalized d)
 	TrainTarget target;       // background / colour space of the loss targets (testbed_nerf.cu:1642-1671)
+	const float* lin_lut;     // 256 entries: srgb_to_linear(b / 255) as the device computes it (read_rgba's byte path)
 };
 
 struct DPInfo { uint32_t rank, world; };
@@ -347,6 +348,7 @@ void launch_loss_scan_chunk(hipStream_t s, uint32_t cap_rays, const uint32_t* nu
                             uint32_t e1, uint32_t e2, uint32_t* list /* nullptr in the last round */, uint32_t* next_counter,
                             const uint32_t* rays_in = nullptr, const uint32_t* n_rays_in = nullptr, uint32_t* rays_out = nullptr,
                             uint32_t* n_rays_out = nullptr);
+void launch_srgb_lut(hipStream_t s, float* lut);
 void launch_loss_ray(hipStream_t s, uint32_t cap_rays, StepState* st, DPInfo dp, const DevDataset& ds, const LossParams& lp, uint32_t* numsteps,
                      const uint32_t* ccount, const uint32_t* cbase, const LossWork& w, float* loss, float* ek, float* mask);
 void launch_loss_grad(hipStream_t s, uint32_t cap_samples, const StepState* st, DPInfo dp, const LossParams& lp, const float* coords,

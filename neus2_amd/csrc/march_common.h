@@ -99,9 +99,11 @@ __device__ __forceinline__ void read_rgba(const DevDataset& ds, uint32_t img, fl
 	const uint32_t v = ds.pixels[ds.pix_off[img] + (uint64_t)px + (uint64_t)py * rx];
 	if (v == 0x00FF00FFu) { o[0] = o[1] = o[2] = o[3] = -1.0f; return; }
 	const float a = (float)((v >> 24) & 0xff) * (1.0f / 255.0f);
-	o[0] = srgb_to_linear((float)(v & 0xff) * (1.0f / 255.0f)) * a;
-	o[1] = srgb_to_linear((float)((v >> 8) & 0xff) * (1.0f / 255.0f)) * a;
-	o[2] = srgb_to_linear((float)((v >> 16) & 0xff) * (1.0f / 255.0f)) * a;
+	// srgb_to_linear((float)byte * (1 / 255)) from the dataset's 256-entry table (the same expression, evaluated once
+	// per value by k_srgb_lut: bit-identical, without a powf per channel)
+	o[0] = ds.lin_lut[v & 0xff] * a;
+	o[1] = ds.lin_lut[(v >> 8) & 0xff] * a;
+	o[2] = ds.lin_lut[(v >> 16) & 0xff] * a;
 	o[3] = a;
 }
 __device__ __forceinline__ bool aabb_contains(const DevDataset& ds, const float p[3]) {

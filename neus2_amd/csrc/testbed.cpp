@@ -188,6 +188,7 @@ struct NeusTestbed {
 	// dataset
 	Dev<uint32_t> pixels; Dev<uint64_t> pix_off; Dev<int32_t> res; Dev<float> focal, pp, xform;
 	DevDataset ds{};
+	Dev<float> srgb_lut;  // read_rgba's byte -> linear table
 	std::vector<float> host_focal, host_pp, host_xform;
 	std::vector<int32_t> host_res;
 	uint32_t max_cascade = 0;
@@ -482,6 +483,10 @@ struct NeusTestbed {
 		HIP_CHECK(hipMemcpy(pp.p, p.data(), p.size() * 4, hipMemcpyHostToDevice));
 		HIP_CHECK(hipMemcpy(xform.p, x.data(), x.size() * 4, hipMemcpyHostToDevice));
 		ds.pixels = pixels.p; ds.pix_off = pix_off.p; ds.res = res.p; ds.focal = focal.p; ds.pp = pp.p; ds.xform = xform.p;
+		srgb_lut.alloc(256);
+		launch_srgb_lut(stream, srgb_lut.p);
+		HIP_CHECK(hipStreamSynchronize(stream));
+		ds.lin_lut = srgb_lut.p;
 		ds.n_images = n_images;
 		host_focal = f; host_pp = p; host_xform = x; host_res = r;
 		const float infl = 0.5f * (float)std::min(1 << (NERF_CASCADES - 1), s);
