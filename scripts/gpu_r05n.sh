@@ -4,4 +4,4 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export PYTHONPATH=$PWD
 mkdir -p gpurun_out
-timeout -k 10 1100 python -u scripts/psnr_anchor_segments.py --starts ${STARTS:-1000,1500} --length 500 > gpurun_out/r05_psnr_anchor_segments.jsonl 2> gpurun_out/r05_psnr_anchor_segments.err
+timeout -k 10 1100 python -u scripts/psnr_anchor_segments.py --starts ${STARTS:-250,500,750,1000,1250,1500,1750} --length ${LEN:-250} > gpurun_out/r05_psnr_anchor_segments.jsonl 2> gpurun_out/r05_psnr_anchor_segments.err

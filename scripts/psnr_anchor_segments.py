@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--fixed-rays", type=int, default=512)
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--spp", type=int, default=8)
+    ap.add_argument("--alt-order", default="reversed", help="also continue the oracle in this summation order ('' : no)")
     args = ap.parse_args()
     import oracle as O
     from cpu_step import CpuTrainer
@@ -89,6 +90,19 @@ def main():
         done = start
         tb.synchronize()
         p_start = gpu_psnr(tb)
+        # the oracle's own spread over the segment: the same state continued with its layer products summed in reversed
+        # order (the noise floor any fp32 accumulation order adds to an fp16 network)
+        p_cpu_alt = None
+        if args.alt_order:
+            tr2 = cpu_from(tb)
+            O.set_sum_order(args.alt_order)
+            try:
+                for _ in range(args.length):
+                    tr2.step()
+            finally:
+                O.set_sum_order("index")
+            p_cpu_alt = cpu_psnr(tr2)
+            del tr2
         tr = cpu_from(tb)
         t0 = time.perf_counter()
         lock = []
@@ -106,6 +120,8 @@ def main():
         p_gpu = gpu_psnr(tb)
         print(json.dumps({"segment_start": start, "segment_end": start + args.length, "psnr_start": round(p_start, 3),
                           "psnr_cpu_oracle": round(p_cpu, 3), "psnr_gpu": round(p_gpu, 3), "delta_db": round(p_gpu - p_cpu, 3),
+                          "psnr_cpu_alt_order": None if p_cpu_alt is None else round(p_cpu_alt, 3),
+                          "delta_cpu_alt_db": None if p_cpu_alt is None else round(p_cpu_alt - p_cpu, 3),
                           "cpu_s": round(time.perf_counter() - t0, 1), "threads": O.num_threads(),
                           "rays_per_batch": args.fixed_rays, "batch": args.batch, "lockstep_compacted_gpu_cpu": lock}), flush=True)
 
