@@ -161,6 +161,7 @@ struct AdamParams {
 	uint32_t bias_converged;
 	float inv_loss_scale;     // 1 / loss_scale when that is a power of two (the product is then the exact quotient)
 	uint32_t pow2_scale;
+	uint32_t skip_ema_h;      // leave the fp16 EMA copy to a later cast of the fp32 EMA (NeusTestbed::sync_ema_h)
 };
 void launch_adam_bias_table(hipStream_t s, float beta1, float beta2, float* tab);
 

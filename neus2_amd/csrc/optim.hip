@@ -83,11 +83,9 @@ __global__ void __launch_bounds__(256) k_adam_ema(AdamParams p, float* __restric
 	for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < ng; g += gridDim.x * blockDim.x) {
 		const uint32_t i0 = 4 * g;
 		const float4 G = ((const float4*)grads)[g];
-		const uint2 WHr = ((const uint2*)weights_h)[g];
 		float4 E = ((const float4*)ema_tmp)[g];
 		float gr[4] = {G.x, G.y, G.z, G.w}, e[4] = {E.x, E.y, E.z, E.w};
 		half_t wh[4];
-		*(uint2*)wh = WHr;
 		// any parameter of the group steps? (the same skip test as adam_param)
 		bool any = false;
 #pragma unroll
@@ -102,20 +100,26 @@ __global__ void __launch_bounds__(256) k_adam_ema(AdamParams p, float* __restric
 			uint4 S = ((const uint4*)steps)[g];
 			float a[4] = {M1.x, M1.y, M1.z, M1.w}, b[4] = {M2.x, M2.y, M2.z, M2.w};
 			uint32_t st[4] = {S.x, S.y, S.z, S.w};
+			// the fp16 copy of every parameter of the group is the cast of its fp32 master (weights_h == half(weights_fp)
+			// wherever either is written), so a stepping group needs no read of the fp16 copy: 2 B per parameter less
 #pragma unroll
-			for (int k = 0; k < 4; ++k)
-				if (adam_param(p, i0 + k, gr[k], w[k], a[k], b[k], st[k])) wh[k] = (half_t)w[k];
+			for (int k = 0; k < 4; ++k) {
+				adam_param(p, i0 + k, gr[k], w[k], a[k], b[k], st[k]);
+				wh[k] = (half_t)w[k];
+			}
 			((float4*)m1)[g] = make_float4(a[0], a[1], a[2], a[3]);
 			((float4*)m2)[g] = make_float4(b[0], b[1], b[2], b[3]);
 			((uint4*)steps)[g] = make_uint4(st[0], st[1], st[2], st[3]);
 			((float4*)weights_fp)[g] = make_float4(w[0], w[1], w[2], w[3]);
 			((uint2*)weights_h)[g] = *(const uint2*)wh;
+		} else {
+			*(uint2*)wh = ((const uint2*)weights_h)[g];  // (the EMA of a skipped group reads the fp16 copy)
 		}
 		half_t eh[4];
 #pragma unroll
 		for (int k = 0; k < 4; ++k) { e[k] = ema_param(p, e[k], (float)wh[k]); eh[k] = (half_t)e[k]; }
 		((float4*)ema_tmp)[g] = make_float4(e[0], e[1], e[2], e[3]);
-		((uint2*)ema_h)[g] = *(const uint2*)eh;
+		if (!p.skip_ema_h) ((uint2*)ema_h)[g] = *(const uint2*)eh;
 		if (tr.n && i0 < p.n_matrix) {
 #pragma unroll
 			for (int k = 0; k < 4; ++k)
@@ -133,7 +137,7 @@ __global__ void __launch_bounds__(256) k_adam_ema(AdamParams p, float* __restric
 		const float wh = (float)weights_h[i];
 		const float f = ema_param(p, ema_tmp[i], wh);
 		ema_tmp[i] = f;
-		ema_h[i] = (half_t)f;
+		if (!p.skip_ema_h) ema_h[i] = (half_t)f;
 		if (tr.n && i < p.n_matrix) adam_transpose_param(tr, i, (half_t)wh);
 	}
 }

@@ -201,6 +201,17 @@ struct NeusTestbed {
 	DinPerm din_perm{};
 	// inference params (EMA weights, the reference's Ema::custom_weights) for rendering
 	Dev<half_t> wT_ema;
+	// The fp16 EMA (inference) weights are only read outside the training step (render, SDF grid, mesh colours, snapshots,
+	// the frame restart), so the step updates the fp32 EMA alone and the fp16 copy is cast from it when first read: the
+	// same bits the Adam kernel would have written (ema_h = half(ema_tmp) after every step), 2 B per parameter less per step
+	bool ema_h_stale = false;
+	void sync_ema_h() {
+		if (!ema_h_stale) return;
+		launch_cast_half(stream, lay.P, ema_tmp.p, ema_h.p);
+		HIP_CHECK(hipGetLastError());
+		HIP_CHECK(hipStreamSynchronize(stream));  // (readers may use another stream or the host)
+		ema_h_stale = false;
+	}
 	MlpPtrs mlp_ema{};
 	// renderer workspace (NerfTracer, testbed_nerf.cu:2397-2630)
 	Dev<uint8_t> r_rays[2];
@@ -616,6 +627,7 @@ struct NeusTestbed {
 		HIP_CHECK(hipMemset(m1.p, 0, (size_t)P * 4)); HIP_CHECK(hipMemset(m2.p, 0, (size_t)P * 4));
 		HIP_CHECK(hipMemset(ema_tmp.p, 0, (size_t)P * 4)); HIP_CHECK(hipMemset(adam_steps.p, 0, (size_t)P * 4));
 		HIP_CHECK(hipMemset(ema_h.p, 0, (size_t)P * 2)); HIP_CHECK(hipMemset(grads.p, 0, (size_t)P * 4));
+		ema_h_stale = false;
 		launch_cast_half(stream, P, params_fp.p, params_h.p);
 		setup_mlp_ptrs();
 		prepare_weights();
@@ -784,6 +796,7 @@ struct NeusTestbed {
 		const uint32_t P = lay.P;
 		{
 			std::vector<half_t> eh(P);
+			sync_ema_h();
 			HIP_CHECK(hipMemcpy(eh.data(), ema_h.p, (size_t)P * 2, hipMemcpyDeviceToHost));
 			std::vector<float> ef(P);
 			for (uint32_t i = 0; i < P; ++i) ef[i] = (float)eh[i];
@@ -825,6 +838,7 @@ struct NeusTestbed {
 		HIP_CHECK(hipMemset(adam_steps.p, 0, (size_t)P * 4));
 		{  // the fp32 EMA restarts from the inference weights (weighted by 0 at the next EMA step)
 			std::vector<half_t> eh(P);
+			sync_ema_h();
 			HIP_CHECK(hipMemcpy(eh.data(), ema_h.p, (size_t)P * 2, hipMemcpyDeviceToHost));
 			std::vector<float> ef(P);
 			for (uint32_t i = 0; i < P; ++i) ef[i] = (float)eh[i];
@@ -1115,7 +1129,9 @@ struct NeusTestbed {
 		p.bias_tab = adam_bias.p; p.bias_converged = bias_conv ? 1u : 0u;
 		// the transposed / permuted MLP copies are written by the Adam launch itself
 		const AdamTranspose tr = adam_transpose();
+		{ static const bool eager = [] { const char* e = std::getenv("NEUS_EAGER_EMA_H"); return e && e[0] == '1'; }(); p.skip_ema_h = eager ? 0u : 1u; }
 		launch_adam_ema(stream, p, params_fp.p, params_h.p, g, m1.p, m2.p, adam_steps.p, ema_tmp.p, ema_h.p, counters, &tr);
+		if (p.skip_ema_h) ema_h_stale = true;
 	}
 	AdamTranspose adam_transpose() const {
 		const Layout& l = lay;
@@ -1204,7 +1220,7 @@ struct NeusTestbed {
 		if (sb > r_scan_bytes || !r_scan_tmp.p) { r_scan_tmp.alloc(sb + 256); r_scan_bytes = sb; scan_temp_reset(s, r_scan_tmp.p); }
 		const MlpPtrs& w = rq.use_ema ? mlp_ema : mlp;
 		const half_t* grid = (rq.use_ema ? ema_h.p : params_h.p) + lay.grid_off;
-		if (rq.use_ema) prepare_weights_for(mlp_ema);
+		if (rq.use_ema) { sync_ema_h(); prepare_weights_for(mlp_ema); }
 		const uint32_t valid = valid_level_at(enc_step);
 		const uint32_t spp = std::max(1u, rq.spp);
 		// m_use_delta (prepare_for_test): the network sees the sample positions through the DeltaNetwork
@@ -1247,7 +1263,7 @@ struct NeusTestbed {
 	// get_density_on_grid: raw SDF of the inference (EMA) weights at every grid point, written to dst.
 	void sdf_on_grid(const uint32_t res[3], const float amin[3], const float amax[3], float* dst) {
 		if (!have_net) throw std::runtime_error("sdf_on_grid: no network");
-		prepare_weights_for(mlp_ema);
+		sync_ema_h(); prepare_weights_for(mlp_ema);
 		const uint64_t n = (uint64_t)res[0] * res[1] * res[2];
 		const uint32_t valid = valid_level_at(enc_step);
 		const bool use_delta = render_delta && cur_frame >= 1;
@@ -1305,7 +1321,7 @@ struct NeusTestbed {
 	// looking outward from the aabb centre; sRGB (the network is trained on sRGB targets).
 	void mesh_colors(float* host_rgb) {
 		if (!mesh_nv) return;
-		prepare_weights_for(mlp_ema);
+		sync_ema_h(); prepare_weights_for(mlp_ema);
 		Dev<float> c; Dev<half_t> o;
 		c.alloc((size_t)mesh_nv * COORD_W); o.alloc((size_t)mesh_nv * OUT_W);
 		launch_mesh_coords(stream, mesh_nv, mesh_v.p, ds, c.p);
@@ -1689,6 +1705,7 @@ int neus_testbed_get_half_params(NeusTestbed* tb, int which, uint16_t* o, uint64
 	return guard([&] {
 		if (!tb->have_net || n != tb->lay.P) throw std::runtime_error("parameter count mismatch");
 		if (which != 0 && which != 1) throw std::runtime_error("get_half_params: which must be 0 (training) or 1 (inference)");
+		if (which) tb->sync_ema_h();
 		HIP_CHECK(hipStreamSynchronize(tb->stream));
 		HIP_CHECK(hipMemcpy(o, which ? tb->ema_h.p : tb->params_h.p, n * 2, hipMemcpyDeviceToHost));
 	});
@@ -1745,6 +1762,7 @@ int neus_testbed_restore_state(NeusTestbed* tb, const NeusRestoreState* in) {
 		tb->loss_scalar_ema = tb->last_loss = in->loss;
 		tb->loss_ema_init = true;
 		HIP_CHECK(hipMemcpy(tb->ema_h.p, tb->params_h.p, (size_t)tb->lay.P * 2, hipMemcpyDeviceToDevice));
+		tb->ema_h_stale = false;
 		// the fp32 EMA follows the loaded inference weights (the first EMA step after a reload weighs it by 0)
 		HIP_CHECK(hipMemcpy(tb->ema_tmp.p, tb->params_fp.p, (size_t)tb->lay.P * 4, hipMemcpyDeviceToDevice));
 		if (in->rebuild_bitfield) {
@@ -1759,6 +1777,7 @@ int neus_testbed_restore_state(NeusTestbed* tb, const NeusRestoreState* in) {
 int neus_testbed_get_optimizer_state(NeusTestbed* tb, NeusOptimizerState* st, float* m1, float* m2, uint32_t* steps, uint16_t* ema_half) {
 	return guard([&] {
 		if (!tb->have_net) throw std::runtime_error("optimizer state: no network");
+		tb->sync_ema_h();
 		HIP_CHECK(hipStreamSynchronize(tb->stream));
 		const size_t P = tb->lay.P;
 		if (st) {
@@ -1789,12 +1808,13 @@ int neus_testbed_set_optimizer_state(NeusTestbed* tb, const NeusOptimizerState* 
 		else HIP_CHECK(hipMemset(tb->adam_steps.p, 0, P * 4));
 		// Ema::deserialize (ema.h:189-194): the EMA weights, and the fp32 accumulator cast from them
 		HIP_CHECK(hipMemcpy(tb->ema_h.p, ema_half, P * 2, hipMemcpyHostToDevice));
+		tb->ema_h_stale = false;
 		std::vector<float> f(P);
 		for (size_t i = 0; i < P; ++i) { half_t h; std::memcpy(&h, &ema_half[i], 2); f[i] = (float)h; }
 		HIP_CHECK(hipMemcpy(tb->ema_tmp.p, f.data(), P * 4, hipMemcpyHostToDevice));
 		tb->adam_step = st->current_step;
 		tb->lr_factor = st->learning_rate_factor;
-		tb->prepare_weights_for(tb->mlp_ema);
+		tb->sync_ema_h(); tb->prepare_weights_for(tb->mlp_ema);
 		HIP_CHECK(hipStreamSynchronize(tb->stream));
 	});
 }

@@ -17,6 +17,7 @@ for name, steps, extra in (("early", 12, None), ("late", 300, None)):
     tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=1 << 16)
     tb.train_steps(steps)
     res[name + "_params"] = tb.get_params()
+    res[name + "_ema_h"] = tb.get_half_params(True).view(np.uint16)
     g, bf = tb.get_density_grid()
     res[name + "_grid"] = g
     res[name + "_counts"] = np.concatenate(tb.ray_counts(1 << 16)[:2])
