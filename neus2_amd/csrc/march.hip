@@ -861,7 +861,7 @@ __global__ void __launch_bounds__(256) k_march_write(uint32_t cap_rays, StepStat
 			const f4u p4 = {(pos[0] - ds.aabb_min[0]) / diag[0], (pos[1] - ds.aabb_min[1]) / diag[1], (pos[2] - ds.aabb_min[2]) / diag[2], warp_dt(dt)};
 			*(f4u*)cc = p4;
 			*(f3u*)(cc + 4) = (f3u){(dir[0] + 1.0f) * 0.5f, (dir[1] + 1.0f) * 0.5f, (dir[2] + 1.0f) * 0.5f};
-			sample_ray[q] = i;
+			if (sample_ray) sample_ray[q] = i;  // (operator path only: the training step maps compacted samples by cmap)
 			if (r0.list && j < r0.e1) r0.list[s_c0[r] + j] = q;  // the first chunk of the ray: progressive round 0
 		}
 		__syncthreads();

@@ -1384,7 +1384,7 @@ struct NeusTestbed {
 		const bool sorted_rays = progressive && ray_sort;  // round 0's list by k_ray_sort_place instead of the march write
 		launch_march_count(s, MAX_RAYS, max_samples, st.p, dp, ds, bitfield.p, bf_lin.p, rng.state, rng.inc, rays.p, startt.p, nreq.p, mwork,
 		                   progressive ? chunk_cnt.p : nullptr, OPEN_CNT + nch, ray_cull ? occ_bbox.p : nullptr);  // list lengths + open-ray counts
-		launch_march_write(s, MAX_RAYS, st.p, ds, rays.p, mwork, nreq.p, base.p, numsteps.p, coords.p, sample_ray.p, max_samples, scan_tmp.p,
+		launch_march_write(s, MAX_RAYS, st.p, ds, rays.p, mwork, nreq.p, base.p, numsteps.p, coords.p, nullptr, max_samples, scan_tmp.p,
 		                   progressive && !sorted_rays ? &r0 : nullptr, dbg_lds_fill);
 		const RaySort rsort{rs_hist.p, rs_off.p, rs_key.p, rs_perm.p, chunk_cnt.p + RS_N_PERM};
 		if (sorted_rays) launch_ray_sort(s, MAX_RAYS, numsteps.p, coords.p, chunk_ends[0], rsort, chunk_list.p, chunk_cnt.p, scan_tmp.p, scan_tmp_bytes);
