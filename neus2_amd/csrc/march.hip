@@ -17,6 +17,7 @@
 #include "march_common.h"
 #include "scan_lookback.h"
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -920,8 +921,7 @@ __global__ void __launch_bounds__(RS_RPB) k_ray_hist(uint32_t cap, const uint32_
 __global__ void __launch_bounds__(RS_RPB) k_ray_sort_place(uint32_t cap, const uint32_t* __restrict__ numsteps, uint32_t e1, RaySort rs,
                                                            uint32_t* __restrict__ list, uint32_t* __restrict__ list_len) {
 	__shared__ uint32_t cur[2][RS_NB];
-	__shared__ uint32_t s_pre[RS_RPB / 64][64], s_dst[RS_RPB / 64][64], s_src[RS_RPB / 64][64];
-	const uint32_t nblk = gridDim.x, blk = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+	const uint32_t nblk = gridDim.x, blk = blockIdx.x, t = threadIdx.x, lane = t & 63;
 	const size_t n = 2 * (size_t)RS_NB * nblk, h1 = (size_t)RS_NB * nblk;
 	const uint32_t h0_total = rs.off[h1];  // every slot (h0 counts them all)
 	for (uint32_t b = t; b < RS_NB; b += RS_RPB) {
@@ -947,14 +947,13 @@ __global__ void __launch_bounds__(RS_RPB) k_ray_sort_place(uint32_t cap, const u
 		p0 = wave_lane_value(p0, 0);
 		if (in && !ns) rs.perm[p0 + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = i;
 	}
-	const uint32_t incl = wave_incl_sum(w), total = wave_lane_value(incl, 63);
-	s_pre[wv][lane] = incl - w; s_dst[wv][lane] = dst; s_src[wv][lane] = base;
-	__builtin_amdgcn_wave_barrier();
-	for (uint32_t r = lane; r < total; r += 64) {
-		uint32_t o = 0;  // the last lane whose chunk starts at or before r (zero-length lanes share its start)
-#pragma unroll
-		for (uint32_t step = 32; step > 0; step >>= 1) if (s_pre[wv][o + step] <= r) o += step;
-		list[s_dst[wv][o] + (r - s_pre[wv][o])] = s_src[wv][o] + (r - s_pre[wv][o]);
+	// each ray's chunk written by the whole wave, one ray at a time (consecutive lanes, consecutive slots)
+	unsigned long long todo = __ballot(w > 0);
+	while (todo) {
+		const int o = __ffsll(todo) - 1;
+		todo &= todo - 1ull;
+		const uint32_t w_o = wave_lane_value(w, o), d_o = wave_lane_value(dst, o), s_o = wave_lane_value(base, o);
+		for (uint32_t j = lane; j < w_o; j += 64) list[d_o + j] = s_o + j;
 	}
 }
 uint32_t ray_sort_blocks(uint32_t cap) { return std::max<uint32_t>(1, (cap + RS_RPB - 1) / RS_RPB); }
@@ -1221,12 +1220,12 @@ __global__ void __launch_bounds__(64) k_loss_scan_chunk(uint32_t cap_rays, const
                                                         uint32_t* __restrict__ rays_out, uint32_t* __restrict__ n_rays_out) {
 	// U samples per ray and group: U lanes load U consecutive samples of one ray (64 / U rays per load instruction),
 	// transposed through LDS to one ray per lane. U = 8 (was 16): half the LDS and registers per wave, so twice the
-	// waves per CU hide the per-ray state loads
-	constexpr uint32_t U = 8, PAD = U + 1, RPI = 64 / U;
+	// waves per CU hide the per-ray state loads. Two groups are in flight (a 4-deep fetch in the later rounds, whose few
+	// waves each wait on their own loads, measured the same: profiles/r05q_scan_ab.txt)
+	constexpr uint32_t U = 8, PAD = U + 1, RPI = 64 / U, NB = 2;
 	typedef float f4v __attribute__((ext_vector_type(4)));
 	__shared__ f4v s_q[64 * PAD];
 	__shared__ float s_e[64 * PAD];
-	__shared__ uint32_t s_pre[64], s_src[64];
 	const uint32_t lane = threadIdx.x, sub = lane / U, el = lane % U;
 	const char* sab = (const char*)sa;
 	const char* ekb = (const char*)ekt;
@@ -1266,7 +1265,7 @@ __global__ void __launch_bounds__(64) k_loss_scan_chunk(uint32_t cap_rays, const
 #pragma unroll
 			for (uint32_t j = 0; j < U; ++j) { s_q[(RPI * j + sub) * PAD + el] = qs[j]; s_e[(RPI * j + sub) * PAD + el] = es[j]; }
 			__builtin_amdgcn_wave_barrier();
-			fetch(qs, es, c + 2 * U);
+			fetch(qs, es, c + NB * U);
 			f4v q[U]; float e[U];
 #pragma unroll
 			for (uint32_t u = 0; u < U; ++u) { q[u] = s_q[lane * PAD + u]; e[u] = s_e[lane * PAD + u]; }
@@ -1285,14 +1284,17 @@ __global__ void __launch_bounds__(64) k_loss_scan_chunk(uint32_t cap_rays, const
 			__builtin_amdgcn_wave_barrier();
 		};
 		if (__ballot(live)) {
-			f4v qa[U], qb[U]; float ea[U], eb[U];
-			fetch(qa, ea, 0);
-			fetch(qb, eb, U);
-			for (uint32_t c = 0;; c += 2 * U) {
-				if (__ballot(live && e0 + c < to) == 0) break;
-				group(qa, ea, c);
-				if (__ballot(live && e0 + c + U < to) == 0) break;
-				group(qb, eb, c + U);
+			f4v qs[NB][U]; float es[NB][U];
+#pragma unroll
+			for (uint32_t bf = 0; bf < NB; ++bf) fetch(qs[bf], es[bf], bf * U);
+			for (uint32_t c = 0;; c += NB * U) {
+				bool more = true;
+#pragma unroll
+				for (uint32_t bf = 0; bf < NB; ++bf) {
+					if (more && __ballot(live && e0 + c + bf * U < to) == 0) more = false;
+					if (more) group(qs[bf], es[bf], c + bf * U);
+				}
+				if (!more) break;
 			}
 		}
 		if (open) {
@@ -1310,18 +1312,16 @@ __global__ void __launch_bounds__(64) k_loss_scan_chunk(uint32_t cap_rays, const
 				uint32_t p0 = 0;
 				if (lane == 0) p0 = atomicAdd(next_counter, total);
 				p0 = wave_lane_value(p0, 0);
-				__builtin_amdgcn_wave_barrier();
-				s_pre[lane] = incl - m;
-				s_src[lane] = base + e1;
-				__builtin_amdgcn_wave_barrier();
-				for (uint32_t r = lane; r < total; r += 64) {
-					// the owner: the last lane whose chunk starts at or before r (zero-length lanes share its start)
-					uint32_t o = 0;
-#pragma unroll
-					for (uint32_t step = 32; step > 0; step >>= 1) if (s_pre[o + step] <= r) o += step;
-					list[p0 + r] = s_src[o] + (r - s_pre[o]);
+				// each open ray's next chunk written by the whole wave, one ray at a time (consecutive lanes, consecutive
+				// slots: the same list as each lane writing its own, in the same positions)
+				const uint32_t pre = incl - m, src = base + e1;
+				unsigned long long todo = __ballot(m > 0);
+				while (todo) {
+					const int o = __ffsll(todo) - 1;
+					todo &= todo - 1ull;
+					const uint32_t m_o = wave_lane_value(m, o), p_o = p0 + wave_lane_value(pre, o), s_o = wave_lane_value(src, o);
+					for (uint32_t j = lane; j < m_o; j += 64) list[p_o + j] = s_o + j;
 				}
-				__builtin_amdgcn_wave_barrier();
 				if (rays_out) {  // the open rays, one reservation per wave
 					const unsigned long long mk = __ballot(m > 0);
 					uint32_t q0 = 0;
