@@ -406,7 +406,7 @@ void launch_exclusive_scan(hipStream_t s, void* temp, size_t temp_bytes, const u
 void launch_sum_f32(hipStream_t s, void* temp, size_t temp_bytes, const float* in, float* out, uint32_t n);
 // optim.hip
 void launch_adam_ema(hipStream_t s, const AdamParams& p, float* weights_fp, half_t* weights_h, const float* grads, float* m1, float* m2,
-                     uint32_t* steps, float* ema_tmp, half_t* ema_h,
+                     uint16_t* steps, float* ema_tmp, half_t* ema_h,
                      const StepCounterArgs* counters = nullptr, const AdamTranspose* tr = nullptr);
 void launch_cast_half(hipStream_t s, uint32_t n, const float* in, half_t* out);
 void launch_add_f32(hipStream_t s, uint32_t n, const float* src, float* dst);

@@ -195,7 +195,7 @@ struct NeusTestbed {
 	float aabb_scale = 1.f;
 	// parameters
 	Dev<float> params_fp, grads, m1, m2, ema_tmp;
-	Dev<uint32_t> adam_steps;
+	Dev<uint16_t> adam_steps;  // per-parameter Adam steps, saturating at 65535 (optim.hip adam_step16)
 	Dev<half_t> params_h, ema_h, wT;
 	MlpPtrs mlp{};
 	DinPerm din_perm{};
@@ -625,7 +625,7 @@ struct NeusTestbed {
 		const std::vector<float> h = initial_params(c.seed, geo);
 		HIP_CHECK(hipMemcpy(params_fp.p, h.data(), (size_t)P * 4, hipMemcpyHostToDevice));
 		HIP_CHECK(hipMemset(m1.p, 0, (size_t)P * 4)); HIP_CHECK(hipMemset(m2.p, 0, (size_t)P * 4));
-		HIP_CHECK(hipMemset(ema_tmp.p, 0, (size_t)P * 4)); HIP_CHECK(hipMemset(adam_steps.p, 0, (size_t)P * 4));
+		HIP_CHECK(hipMemset(ema_tmp.p, 0, (size_t)P * 4)); HIP_CHECK(hipMemset(adam_steps.p, 0, (size_t)P * 2));
 		HIP_CHECK(hipMemset(ema_h.p, 0, (size_t)P * 2)); HIP_CHECK(hipMemset(grads.p, 0, (size_t)P * 4));
 		ema_h_stale = false;
 		launch_cast_half(stream, P, params_fp.p, params_h.p);
@@ -804,7 +804,7 @@ struct NeusTestbed {
 			HIP_CHECK(hipMemcpy(params_h.p, eh.data(), (size_t)P * 2, hipMemcpyHostToDevice));
 		}
 		HIP_CHECK(hipMemset(m1.p, 0, (size_t)P * 4)); HIP_CHECK(hipMemset(m2.p, 0, (size_t)P * 4));
-		HIP_CHECK(hipMemset(adam_steps.p, 0, (size_t)P * 4));
+		HIP_CHECK(hipMemset(adam_steps.p, 0, (size_t)P * 2));
 		// the fp32 EMA starts at the loaded weights: the first EMA step weighs it by 1 - decay^0 = 0, and until the
 		// canonical optimizer steps (after the global-movement phase) it is what get_ema_params reports
 		HIP_CHECK(hipMemcpy(ema_tmp.p, params_fp.p, (size_t)P * 4, hipMemcpyDeviceToDevice));
@@ -835,7 +835,7 @@ struct NeusTestbed {
 		training_step = 0; canonical_step = 0;
 		const uint32_t P = lay.P;
 		HIP_CHECK(hipMemset(m1.p, 0, (size_t)P * 4)); HIP_CHECK(hipMemset(m2.p, 0, (size_t)P * 4));
-		HIP_CHECK(hipMemset(adam_steps.p, 0, (size_t)P * 4));
+		HIP_CHECK(hipMemset(adam_steps.p, 0, (size_t)P * 2));
 		{  // the fp32 EMA restarts from the inference weights (weighted by 0 at the next EMA step)
 			std::vector<half_t> eh(P);
 			sync_ema_h();
@@ -1788,7 +1788,11 @@ int neus_testbed_get_optimizer_state(NeusTestbed* tb, NeusOptimizerState* st, fl
 		}
 		if (m1) HIP_CHECK(hipMemcpy(m1, tb->m1.p, P * 4, hipMemcpyDeviceToHost));
 		if (m2) HIP_CHECK(hipMemcpy(m2, tb->m2.p, P * 4, hipMemcpyDeviceToHost));
-		if (steps) HIP_CHECK(hipMemcpy(steps, tb->adam_steps.p, P * 4, hipMemcpyDeviceToHost));
+		if (steps) {  // (stored in 16 bits, saturating at 65535: optim.hip adam_step16)
+			std::vector<uint16_t> h(P);
+			HIP_CHECK(hipMemcpy(h.data(), tb->adam_steps.p, P * 2, hipMemcpyDeviceToHost));
+			for (size_t i = 0; i < P; ++i) steps[i] = h[i];
+		}
 		if (ema_half) HIP_CHECK(hipMemcpy(ema_half, tb->ema_h.p, P * 2, hipMemcpyDeviceToHost));
 	});
 }
@@ -1804,8 +1808,11 @@ int neus_testbed_set_optimizer_state(NeusTestbed* tb, const NeusOptimizerState* 
 		HIP_CHECK(hipMemcpy(tb->m1.p, m1, P * 4, hipMemcpyHostToDevice));
 		HIP_CHECK(hipMemcpy(tb->m2.p, m2, P * 4, hipMemcpyHostToDevice));
 		// Adam::deserialize: param_steps absent -> zeros (adam.h:437-442)
-		if (steps) HIP_CHECK(hipMemcpy(tb->adam_steps.p, steps, P * 4, hipMemcpyHostToDevice));
-		else HIP_CHECK(hipMemset(tb->adam_steps.p, 0, P * 4));
+		if (steps) {
+			std::vector<uint16_t> h(P);
+			for (size_t i = 0; i < P; ++i) h[i] = (uint16_t)std::min<uint32_t>(steps[i], 0xffffu);
+			HIP_CHECK(hipMemcpy(tb->adam_steps.p, h.data(), P * 2, hipMemcpyHostToDevice));
+		} else HIP_CHECK(hipMemset(tb->adam_steps.p, 0, P * 2));
 		// Ema::deserialize (ema.h:189-194): the EMA weights, and the fp32 accumulator cast from them
 		HIP_CHECK(hipMemcpy(tb->ema_h.p, ema_half, P * 2, hipMemcpyHostToDevice));
 		tb->ema_h_stale = false;
