@@ -62,9 +62,12 @@ __device__ __forceinline__ bool step_until(float& t, uint32_t& k, float target, 
 		const uint32_t b3 = __float_as_uint(t3), inc = b2 - b;
 		if (b3 - b2 != inc || (b3 & 0x7f800000u) != ex) { t = t2; ++k; continue; }
 		const uint32_t e_end = ex + 0x00800000u;  // the next binade's first bit pattern
-		uint32_t j = (e_end - 1u - b) / inc;       // the last step inside the binade (>= 2: t3 is inside)
+		const uint32_t tb = __float_as_uint(target);
+		// j = min(the first step at or past target, the last step inside the binade) (both >= 2: t2 < target, t3 is inside),
+		// with one division when the first is inside the binade
+		uint32_t j = tb < e_end ? (tb - b + inc - 1u) / inc : 0xffffffffu;
+		if (j == 0xffffffffu || b + j * inc >= e_end) j = (e_end - 1u - b) / inc;
 		j = min(j, kmax - k);
-		j = min(j, (__float_as_uint(target) - b + inc - 1u) / inc);  // the first step at or past target (>= 2: t2 < target)
 		t = __uint_as_float(b + j * inc);
 		k += j;
 	}

@@ -253,6 +253,35 @@ def test_sample_rays_culled_bit_exact(env):
     assert 0 < r_nr < n_rays // 2, r_nr
 
 
+def test_sample_rays_block_grid_bit_exact(env):
+    """The exact empty-block skip (march.hip macro_skip: a 4^3-cell block without an occupied cell is crossed in one
+    event) against the oracle's cell-by-cell march: single occupied cells in 3 % of the blocks, so most rays enter and
+    leave many empty blocks beside occupied ones; rays, numsteps and coords bit-identical."""
+    t, O, tb = env["t"], env["O"], env["tb"]
+    lib, check = L()
+    G = 128
+    rng = np.random.default_rng(5)
+    occ = np.zeros((G, G, G), bool)
+    bi = np.argwhere(rng.random((G // 4,) * 3) < 0.03)
+    occ[tuple((4 * bi + rng.integers(0, 4, size=bi.shape)).T)] = True
+    bf = env["scenes"].bitfield_from_occupancy(occ)
+    n_rays, max_s = 16384, 16384 * 16
+    rays = t.zeros((n_rays, 6), dtype=t.float32, device="cuda")
+    ns = t.zeros((n_rays, 2), dtype=t.int32, device="cuda")
+    co = t.zeros((max_s, 7), dtype=t.float32, device="cuda")
+    cnt = (C.c_uint32 * 3)()
+    rs, ri = 0x0F1E2D3C4B5A6978, 0xDA3E39CB94B95BDB | 1
+    check(lib.neus_sample_rays(tb.handle, None, C.c_uint32(n_rays), C.c_uint32(0), C.c_uint32(1), C.c_uint32(0), C.c_uint64(rs), C.c_uint64(ri),
+                               C.c_uint32(max_s), ptr(dev(t, bf)), ptr(rays), ptr(ns), ptr(co), cnt))
+    r_rays, r_ns, r_co, r_cnt, r_nr = O.generate_samples(env["ds"], bf, n_rays, 0, rs, ri, max_s)
+    np.testing.assert_array_equal(host(ns, np.uint32), r_ns)
+    assert cnt[0] == r_cnt and cnt[2] == r_nr
+    np.testing.assert_array_equal(host(rays, np.uint32), r_rays.view(np.uint32))
+    nk = int(cnt[1])
+    np.testing.assert_array_equal(host(co, np.uint32)[:nk], r_co.view(np.uint32)[:nk])
+    assert nk > 1000, nk
+
+
 def test_loss_compaction_parity(env):
     """Composite/loss/compaction on fixed network outputs: compaction bit-exact, dL/dout fp16-close."""
     t, O, tb = env["t"], env["O"], env["tb"]
@@ -906,22 +935,26 @@ def test_multilane_march_equals_single_lane(env):
     sequence, join the previous segment's exit, re-march when they missed it) and the balanced march (k_march_bal, the
     default: a wave's 64 lanes shared by its 8 rays by length, 1-16 per ray; "8" below, "8u" the fixed 8 lanes) against the
     one-lane march, bit for bit (rays, numsteps, coordinates, counters), on random occupancy grids from sparse to full
-    (many empty-cell skips landing across segment starts, long sample runs, the NERF_STEPS cap on the full grid) and on
-    the training bitfield."""
+    (many empty-cell skips landing across segment starts, long sample runs, the NERF_STEPS cap on the full grid), on
+    the training bitfield and on grids of empty 4^3 blocks beside occupied ones; "1n" / "8n" run without the exact
+    empty-block skip (march.hip macro_skip), so the skip is checked against the cell-by-cell march as well."""
     t = env["t"]
     lib, check = L()
     from neus2_amd import pyngp
     sc = env["sc"]
     tbs = {}
-    for key, lanes, bal in (("1", "1", "1"), ("4", "4", "1"), ("8", "8", "1"), ("8u", "8", "0"), ("16", "16", "1")):
+    # "1n" / "8n": the one-lane and balanced marches without the exact empty-block skip (NEUS_MARCH_MACRO=0)
+    for key, lanes, bal, mac in (("1", "1", "1", "1"), ("4", "4", "1", "1"), ("8", "8", "1", "1"), ("8u", "8", "0", "1"),
+                                 ("16", "16", "1", "1"), ("1n", "1", "1", "0"), ("8n", "8", "1", "0")):
         os.environ["NEUS_MARCH_LANES"] = lanes
         os.environ["NEUS_MARCH_BALANCE"] = bal
+        os.environ["NEUS_MARCH_MACRO"] = mac
         tb = pyngp.Testbed(pyngp.TestbedMode.Nerf)
         tb.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
         tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=BATCH)
         tbs[key] = tb
-    os.environ.pop("NEUS_MARCH_LANES", None)
-    os.environ.pop("NEUS_MARCH_BALANCE", None)
+    for v in ("NEUS_MARCH_LANES", "NEUS_MARCH_BALANCE", "NEUS_MARCH_MACRO"):
+        os.environ.pop(v, None)
     rng = np.random.default_rng(17)
     n_rays, max_s = 8192, 8192 * 64
     bfs = [_bitfield(env)]
@@ -929,6 +962,18 @@ def test_multilane_march_equals_single_lane(env):
         bf = np.zeros(128 ** 3 // 8 * 8, np.uint8)
         bf[: 128 ** 3 // 8] = np.packbits(rng.random(128 ** 3) < p, bitorder="little")
         bfs.append(bf)
+    # empty 4^3 blocks beside occupied ones (the block skip's entries and exits everywhere): a blob, and single cells in
+    # 3 % of the blocks
+    G = 128
+    c = (np.arange(G) + 0.5) / G
+    X, Y, Z = np.meshgrid(c, c, c, indexing="ij")
+    bfs.append(env["scenes"].bitfield_from_occupancy((X - 0.62) ** 2 + (Y - 0.45) ** 2 + (Z - 0.55) ** 2 < 0.09 ** 2))
+    occ = np.zeros((G, G, G), bool)
+    blk = rng.random((G // 4,) * 3) < 0.03
+    bi = np.argwhere(blk)
+    off = rng.integers(0, 4, size=bi.shape)
+    occ[tuple((4 * bi + off).T)] = True
+    bfs.append(env["scenes"].bitfield_from_occupancy(occ))
     for k, bf in enumerate(bfs):
         out = {}
         for lanes, tb in tbs.items():
@@ -942,7 +987,7 @@ def test_multilane_march_equals_single_lane(env):
             out[lanes] = (host(rays, np.uint32).copy(), host(ns, np.uint32).copy(), host(co, np.uint32).copy(), tuple(cnt))
         a = out["1"]
         nk = int(a[3][1])
-        for lanes in ("4", "8", "8u", "16"):
+        for lanes in ("4", "8", "8u", "16", "1n", "8n"):
             b = out[lanes]
             assert a[3] == b[3], (k, lanes, a[3], b[3])
             np.testing.assert_array_equal(a[0], b[0])
