@@ -30,12 +30,8 @@ constexpr float MAX_CONE_STEPSIZE = STEPSIZE * (1 << (NERF_CASCADES - 1)) * NERF
 constexpr uint32_t N_MAX_RANDOM_SAMPLES_PER_RAY = 8;
 constexpr float NERF_MIN_OPTICAL_THICKNESS = 0.1f;
 constexpr uint32_t GRID3 = NERF_GRIDSIZE * NERF_GRIDSIZE * NERF_GRIDSIZE;
-// The constant-step march's occupancy words: mip 0 linear, GRID3 / 32 words in (x, y, z/32) order, then the block
-// map at MACRO_OFF: one bit per 4^3-cell block in (x, y) words of 32 z-blocks, set when the block cannot be skipped
-// whole (an occupied cell, a block on the grid's faces, the centre block; occ_common.h macro_wave).
-constexpr uint32_t MACRO_B = 4, MACRO_N = NERF_GRIDSIZE / MACRO_B, MACRO_WORDS = MACRO_N * MACRO_N * MACRO_N / 32;
-constexpr uint32_t MACRO_OFF = GRID3 / 32;
-constexpr uint32_t LIN_WORDS = GRID3 / 32 + MACRO_WORDS;
+// Linear mip-0 occupancy for the constant-step march: GRID3 / 32 words in (x, y, z/32) order.
+constexpr uint32_t LIN_WORDS = GRID3 / 32;
 constexpr uint32_t MAX_LEVELS = 16;
 constexpr uint32_t OUT_W = 16;      // padded network output width (nerf_network.h:935)
 constexpr uint32_t COORD_W = 7;     // NerfCoordinate floats (nerf.h:76-102)

@@ -293,9 +293,6 @@ struct MarchWork {
 	uint32_t dbg = 0;                     /* development timing experiments (wrong results): 1 no record stores, 2 no occupancy loads */
 	uint32_t balanced = 0;                /* 8 lanes per ray on average, shared by the 8 rays of a wave by length (k_march_bal, constant-step
 	                                         march only) */
-	uint32_t macro = 1;                   /* exact skips of empty 4^3-cell blocks (constant-step march; march.hip macro_landing_ok) */
-	float prof_w = 4.f;                   /* k_march_bal's work profile: weight of a point in a block that is not skipped whole (1: an
-	                                         empty block's) */
 };
 // Ray generation + the occupancy march: rays (6 f32 per slot), tstart (1 per slot), nreq (requested
 // samples per slot) and the sample runs (MarchWork).

@@ -16,7 +16,6 @@
 #pragma clang fp contract(off)
 #include "march_common.h"
 #include "scan_lookback.h"
-#include "occ_common.h"
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -39,9 +38,6 @@ __global__ void k_bitfield_linear(const uint8_t* __restrict__ bf, uint32_t* __re
 		word |= (uint32_t)((bf[idx / 8] >> (idx % 8)) & 1) << b;
 	}
 	lin[w] = word;
-}
-__global__ void k_bitfield_macro(const uint8_t* __restrict__ bf, uint32_t* __restrict__ lin) {
-	macro_wave(bf, lin, (blockIdx.x * blockDim.x + threadIdx.x) >> 6, threadIdx.x & 63);
 }
 // Conservative slab test of the ray o + t d, t >= 0, against the box bb = {min xyz, max xyz} (touching counts as a hit).
 __device__ __forceinline__ bool ray_hits_box(const float o[3], const float d[3], const float bb[6]) {
@@ -187,56 +183,10 @@ __device__ __forceinline__ bool visited(const Visits& v, uint32_t k) {
 	return a < 64u && ((v.m >> a) & 1ull);
 }
 
-// Exact skip of an empty 4^3-cell block (MarchWork::macro; the block map of common.h MACRO_OFF). From a landing (t, k) in
-// unoccupied interior cell c whose block B is empty, the reference's march goes cell by cell through B without a sample
-// and lands on the first step past B. That landing is computed directly when it is certain:
-//  * every position function here (pos = o + t dir, the cell index ((pos - 0.5) + 0.5) * 128, P = 128 pos) is a chain of
-//    monotone float operations, so along the ray each axis' cell index and P are monotone in t. With the position at t_lo
-//    inside the AABB and classified in B (and the current one too), every step in between lands in B: inside the AABB,
-//    mip 0, unoccupied;
-//  * a landing L in B (t_L < t_lo) has its next target min_d t_L + (floor(P + 0.5 + 0.5 sgn) - P) idir / 128 at most the
-//    term of an axis x whose floor is at most the block face F (P(t_lo) 2^-12 cells short of it: the two rounded half
-//    additions cannot reach F + 1). That term is the exact plane crossing t_F = (F / 128 - o) / dir up to the rounding
-//    of pos (<= 1.01 u (|t dir| + 1), divided by |dir|) and of the three operations after it; the estimate `est`, the
-//    same expression at the current landing, is as close, so every target of the chain is <= est + E with
-//    E = u (16 |est| + 8 / |dir| + 4) (a margin of > 3 over the two bounds; u = 2^-24);
-//  * K, the first step at or past t_lo (exact stepping), with T_K >= est + E is then where every landing of the chain
-//    goes next once it is the last in B: the chain lands exactly on K, whatever landing in B it starts from.
-// Otherwise (a step within the window, a near-parallel axis, the position at t_lo not classified in B) the cell-by-cell
-// skip runs from the same landing: a speed difference, never a result. Steps k .. K - 1 may be taken as visited by the
-// segment join (a previous segment's exit there continues to K as well). macro_landing_ok: the checks at t_lo.
-__device__ __forceinline__ bool macro_landing_ok(const DevDataset& ds, const MarchRay& mr, const int c[3], int dx, float face, float t_lo) {
-	float p[3];
-#pragma unroll
-	for (int d = 0; d < 3; ++d) p[d] = mr.o[d] + t_lo * mr.dir[d];
-	int cl[3];
-	mip0_cell(p, cl);
-	bool ok = aabb_contains(ds, p) & ((cl[0] >> 2) == (c[0] >> 2)) & ((cl[1] >> 2) == (c[1] >> 2)) & ((cl[2] >> 2) == (c[2] >> 2));
-	constexpr float M = 2.44140625e-4f;  // 2^-12 cells
-#pragma unroll
-	for (int d = 0; d < 3; ++d)
-		if (d == dx) {
-			const float P = NERF_GRIDSIZE * p[d];
-			ok &= mr.dir[d] > 0.0f ? (P <= face - M) : (P >= face + M);
-		}
-	return ok;
-}
-// The constant-step skip loop do { t += dt; ++k; } while (t < target); bounded: at cone angle 0 the box diagonal is
-// NERF_STEPS steps, so no skip spans 4 NERF_STEPS and the bound only ends a corrupted t (the ray is ended, the step
-// reports it). A mip-0 cell skip (to the next cell boundary, <= sqrt(3) / 128 away) spans at most 8 steps: plain steps
-// first, the exact integer-domain jump only for what remains (block and mip >= 1 skips).
-__device__ __forceinline__ bool skip_to(float& t, uint32_t& k, float target) {
-	t += MIN_CONE_STEPSIZE; ++k;
-#pragma unroll
-	for (int s = 0; s < 8; ++s)
-		if (t < target) { t += MIN_CONE_STEPSIZE; ++k; }
-	return !(t < target) || step_until(t, k, target, k + 4 * NERF_STEPS, MIN_CONE_STEPSIZE);
-}
-
 template <bool FAST>
 __device__ __forceinline__ bool march_event(const DevDataset& ds, const uint8_t* __restrict__ bf, const uint32_t* __restrict__ lin,
                                             const MarchRay& mr, float& t, uint32_t& k, uint32_t k_end, SegAcc& acc, Visits& vis,
-                                            uint2* __restrict__ rec, uint32_t dbg = 0, const uint32_t* __restrict__ mac = nullptr) {
+                                            uint2* __restrict__ rec, uint32_t dbg = 0) {
 	const uint32_t kb = k;
 	if (FAST) {
 		float pos[3];
@@ -273,41 +223,25 @@ __device__ __forceinline__ bool march_event(const DevDataset& ds, const uint8_t*
 			return true;
 		}
 		seg_flush(rec, acc, dbg);
-		// advance_to_next_voxel with a constant step (march_step), or past an empty 4^3 block (macro_landing_ok)
-		bool blk = mac && c[0] >= 0 && !((mac[((uint32_t)(c[0] >> 2) << 5) | (uint32_t)(c[1] >> 2)] >> (c[2] >> 2)) & 1u);
+		visit(vis, kb, kb + 1);
+		// advance_to_next_voxel with a constant step (march_step)
 		const uint32_t res = NERF_GRIDSIZE >> mip;
-		float tn = 3.402823466e+38f, tnb = 3.402823466e+38f, face = 0.f, aid = 0.f;
-		int dx = -1;
+		float tn = 3.402823466e+38f;
 #pragma unroll
 		for (int d = 0; d < 3; ++d) {
 			const float p = res * pos[d];
 			tn = fminf(tn, (floorf(p + 0.5f + 0.5f * signf(mr.dir[d])) - p) * mr.idir[d]);
-			const float f = (float)(int)(MACRO_B * ((c[d] >> 2) + (mr.dir[d] > 0.0f ? 1 : 0)));
-			const float tb = (f - p) * mr.idir[d];  // (dir 0: +inf or NaN, never the minimum)
-			if (tb < tnb) { tnb = tb; face = f; aid = fabsf(mr.idir[d]); dx = d; }
 		}
 		const float t_target = t + fmaxf(ldexpf(tn, -(int)(7 - mip)), 0.0f);
-		float target = t_target, t_hi = 0.f;
-		if (blk) {
-			const float est = t + ldexpf(tnb, -7);
-			const float E = 5.9604644775390625e-8f * (16.0f * fabsf(est) + 8.0f * aid + 4.0f);
-			const float t_lo = est - E - 3.814697265625e-6f * aid;  // 2^-18 / |dir|: twice the 2^-12-cell margin in t
-			t_hi = est + E;
-			blk = dx >= 0 && aid < 1024.0f && est < 1.0e6f && t < t_lo;
-			if (blk) target = t_lo;
-		}
-		const float ts = t;
-		const uint32_t ks = k;
-		if (!skip_to(t, k, target)) return false;
-		if (blk) {
-			if ((t >= t_hi) && macro_landing_ok(ds, mr, c, dx, face, target)) {
-				visit(vis, kb, k);
-				return true;
-			}
-			t = ts; k = ks;  // not certain: the cell skip
-			if (!skip_to(t, k, t_target)) return false;
-		}
-		visit(vis, kb, kb + 1);
+		t += MIN_CONE_STEPSIZE; ++k;
+		// do { t += dt; ++k; } while (t < t_target); bounded: at cone angle 0 the box diagonal is NERF_STEPS steps, so
+		// no skip spans 4 NERF_STEPS and the bound only ends a corrupted t (the ray is ended, the step reports it).
+		// A mip-0 skip (to the next cell boundary, <= sqrt(3) / 128 away) spans at most 8 steps: plain steps first (the
+		// loop itself), the exact integer-domain jump (two divisions) only for what remains (mip >= 1 skips)
+#pragma unroll
+		for (int s = 0; s < 8; ++s)
+			if (t < t_target) { t += MIN_CONE_STEPSIZE; ++k; }
+		if (t < t_target && !step_until(t, k, t_target, k + 4 * NERF_STEPS, MIN_CONE_STEPSIZE)) return false;
 		return true;
 	} else {
 		float dt, pos[3];
@@ -342,19 +276,12 @@ constexpr uint32_t FINISHED = 0xffffffffu;
 template <bool FAST>
 __device__ __forceinline__ void march_segment(const DevDataset& ds, const uint8_t* __restrict__ bf, const uint32_t* __restrict__ lin,
                                               const MarchRay& mr, float& t, uint32_t& k, uint32_t k_end, SegAcc& acc, Visits& vis,
-                                              uint2* __restrict__ rec, uint32_t rec_cap, uint32_t* n_ev = nullptr, uint32_t dbg = 0,
-                                              const uint32_t* __restrict__ mac = nullptr) {
+                                              uint2* __restrict__ rec, uint32_t rec_cap, uint32_t* n_ev = nullptr, uint32_t dbg = 0) {
 	while (k < k_end) {
 		if (n_ev) ++*n_ev;
-		if (acc.nrec + 1 >= rec_cap || !march_event<FAST>(ds, bf, lin, mr, t, k, k_end, acc, vis, rec, dbg, mac)) { k = FINISHED; break; }
+		if (acc.nrec + 1 >= rec_cap || !march_event<FAST>(ds, bf, lin, mr, t, k, k_end, acc, vis, rec, dbg)) { k = FINISHED; break; }
 	}
 	seg_flush(rec, acc, dbg);
-}
-
-// The block map to LDS (4 KB); off: all ones (no block skipped whole). Block-uniform call (a barrier).
-__device__ __forceinline__ void stage_macro(uint32_t* s_mac, const uint32_t* __restrict__ lin, bool on) {
-	for (uint32_t w = threadIdx.x; w < MACRO_WORDS; w += blockDim.x) s_mac[w] = on ? lin[MACRO_OFF + w] : 0xffffffffu;
-	__syncthreads();
 }
 
 // Two passes over the ray slots. Only a prefix of the slots can be kept: slot i is kept iff n_i > 0 and
@@ -393,8 +320,6 @@ __global__ void __launch_bounds__(256) MARCH_OCC k_march(uint32_t cap_rays, uint
 		for (uint32_t k = lo + blockIdx.x * blockDim.x + threadIdx.x; k < hi; k += gridDim.x * blockDim.x) { nreq[k] = 1; mw.nrec[k] = 0; }
 		return;
 	}
-	__shared__ uint32_t s_mac[MACRO_WORDS];
-	stage_macro(s_mac, lin, FAST && mw.macro && !mw.dbg);
 	constexpr uint32_t SEG_CAP = MARCH_SEG_RECS / MG;  // segment-local records per lane
 	const uint32_t lane = threadIdx.x & 63, g = lane % MG;
 	const uint32_t groups = (gridDim.x * blockDim.x) / MG;
@@ -440,7 +365,7 @@ __global__ void __launch_bounds__(256) MARCH_OCC k_march(uint32_t cap_rays, uint
 		float et = t;
 		uint32_t ek = active ? k : FINISHED;
 		uint32_t n_ev = 0;
-		if (active) { march_segment<FAST>(ds, bitfield, lin, mr, et, ek, k_end, acc, vis, rec, SEG_CAP, &n_ev, mw.dbg, s_mac); }
+		if (active) { march_segment<FAST>(ds, bitfield, lin, mr, et, ek, k_end, acc, vis, rec, SEG_CAP, &n_ev, mw.dbg); }
 		// health: an active lane whose walk ends on a negative or non-finite t was handed a corrupted state
 		if (__builtin_expect(__ballot(active && !((et >= 0.f) & (et < __builtin_huge_valf()))) != 0ull, 0) && lane == 0)
 			atomicOr(&st->fail_flags, STEP_FAIL_MARCH_T);
@@ -464,7 +389,7 @@ __global__ void __launch_bounds__(256) MARCH_OCC k_march(uint32_t cap_rays, uint
 				if (redo) {
 					acc = SegAcc{0.f, 0u, 0u, 0u, 0u}; vis = Visits{0ull, pk};
 					et = pt; ek = pk; vk = pk;
-					march_segment<FAST>(ds, bitfield, lin, mr, et, ek, k_end, acc, vis, rec, SEG_CAP, nullptr, 0u, s_mac);
+					march_segment<FAST>(ds, bitfield, lin, mr, et, ek, k_end, acc, vis, rec, SEG_CAP);
 				}
 			}
 		}
@@ -554,8 +479,7 @@ constexpr uint32_t MARCH_BAL_MAX = 16;  // lanes of one ray at most (k_march_bal
 // 20.5 vs max 28.9 at the step-1600 state). The slices, joins and outputs are k_march's with a per-ray lane count m:
 // where a lane starts never changes a result (the join keeps only samples of the true trajectory), so the output is
 // the single-lane march's, bit for bit.
-// (5 waves per SIMD: 96 VGPRs without scratch; the compiler's own choice, 111, leaves 4)
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) k_march_bal(uint32_t cap_rays, uint32_t pass, uint32_t max_samples, StepState* __restrict__ st,
+__global__ void __launch_bounds__(256) MARCH_OCC k_march_bal(uint32_t cap_rays, uint32_t pass, uint32_t max_samples, StepState* __restrict__ st,
                                                    DevDataset ds, const uint8_t* __restrict__ bitfield, const uint32_t* __restrict__ lin,
                                                    const float* __restrict__ rays, const float* __restrict__ tstart, uint32_t* __restrict__ nreq,
                                                    MarchWork mw) {
@@ -567,10 +491,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))
 		for (uint32_t k = lo + blockIdx.x * blockDim.x + threadIdx.x; k < hi; k += gridDim.x * blockDim.x) { nreq[k] = 1; mw.nrec[k] = 0; }
 		return;
 	}
-	__shared__ uint32_t s_mac[MACRO_WORDS];
-	__shared__ float s_cum[4][8][32];  // per wave, per ray: cumulative work of the 32 profile points
-	__shared__ float s_ray[4][8][10];  // per wave, per ray: o, dir, 1 / dir (load_march_ray) and the box exit
-	stage_macro(s_mac, lin, mw.macro && !mw.dbg);
 	const uint32_t lane = threadIdx.x & 63;
 	const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, n_waves = (gridDim.x * blockDim.x) >> 6;
 	uint32_t total = 0;
@@ -580,69 +500,30 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))
 	auto stamp = [&](int ph) { if (pw && first && lane == 0) pw[ph] = wall_clock64(); };
 	stamp(0);
 	for (uint32_t b = lo + 8 * wave; b < hi; b += 8 * n_waves) {
-		// ---- the group's rays: start on lanes 0..7; each ray's work profile on the 8 lanes 8 r .. 8 r + 7: the block map
-		// at 32 points of its span (4 per lane), a point in a block that cannot be skipped whole weighing 4 (an event per
-		// cell crossed) and one in an empty block 1 (an event per 4^3 block), as cumulative weights in LDS
-		float t0r = -1.f;
-		if (lane < 8 && b + lane < hi) t0r = tstart[b + lane];
-		float wr = 0.f;  // lane 8 r: the ray's weight (cells crossed x mean point weight)
-		{
-			const uint32_t rs = lane >> 3, js = lane & 7;
-			float w4[4] = {0.f, 0.f, 0.f, 0.f}, cells = 0.f;
-			if (b + rs < hi) {
-				// the ray and its start loaded together (no dependent round trip); the ray and its box exit go to LDS for
-				// the marching lanes below
-				const float t0s = tstart[b + rs];
+		// ---- the group's rays on lanes 0..7: start, exit, weight
+		float t0r = -1.f, wr = 0.f;
+		if (lane < 8 && b + lane < hi) {
+			t0r = tstart[b + lane];
+			if (t0r >= 0.f) {
 				MarchRay m;
-				load_march_ray(rays, b + rs, m, ds.motion.on != 0);
-				float tx[3];
+				load_march_ray(rays, b + lane, m, ds.motion.on != 0);
+				float te = 3.402823466e+38f;
 #pragma unroll
-				for (int d = 0; d < 3; ++d) tx[d] = fmaxf((ds.aabb_min[d] - m.o[d]) * m.idir[d], (ds.aabb_max[d] - m.o[d]) * m.idir[d]);
-				const float te = fminf(fminf(tx[0], tx[1]), tx[2]);
-				if (js == 0) {
-					float* sr = s_ray[threadIdx.x >> 6][rs];
-#pragma unroll
-					for (int d = 0; d < 3; ++d) { sr[d] = m.o[d]; sr[3 + d] = m.dir[d]; sr[6 + d] = m.idir[d]; }
-					sr[9] = te;
-				}
-				const float span = te - t0s;
-				if (t0s >= 0.f && span > 0.f && span < 1e4f) {
-					cells = span * (fabsf(m.dir[0]) + fabsf(m.dir[1]) + fabsf(m.dir[2]));
-#pragma unroll
-					for (int q = 0; q < 4; ++q) {
-						const float tq = t0s + span * (((float)(4 * js + q) + 0.5f) * (1.0f / 32.0f));
-						int bq[3];
-#pragma unroll
-						for (int d = 0; d < 3; ++d) bq[d] = clampi((int)((m.o[d] + tq * m.dir[d]) * (float)MACRO_N), 0, (int)MACRO_N - 1);
-						const bool full = (s_mac[((uint32_t)bq[0] << 5) | (uint32_t)bq[1]] >> bq[2]) & 1u;
-						w4[q] = (q ? w4[q - 1] : 0.f) + (full ? mw.prof_w : 1.f);
-					}
-				}
+				for (int d = 0; d < 3; ++d) te = fminf(te, fmaxf((ds.aabb_min[d] - m.o[d]) * m.idir[d], (ds.aabb_max[d] - m.o[d]) * m.idir[d]));
+				const float span = te - t0r;
+				if (span > 0.f && span < 1e4f) wr = span * (fabsf(m.dir[0]) + fabsf(m.dir[1]) + fabsf(m.dir[2]));
 			}
-			// inclusive scan of the lanes' sums over the ray's 8 lanes
-			float pre = w4[3];
-#pragma unroll
-			for (int off = 1; off < 8; off <<= 1) {
-				const float v = __shfl(pre, (int)((lane - off) & 63));
-				if (js >= (uint32_t)off) pre += v;
-			}
-			const float excl = pre - w4[3];
-#pragma unroll
-			for (int q = 0; q < 4; ++q) s_cum[threadIdx.x >> 6][rs][4 * js + q] = excl + w4[q];
-			const float W = __shfl(pre, (int)(lane | 7));
-			wr = cells * W;
 		}
-		__builtin_amdgcn_wave_barrier();
 		// ---- lanes per ray (wave-uniform): 1 per active ray, the rest by weight, the remainder to the heaviest ray; at
-		// most 16 per ray (the segment scratch of a ray, MARCH_SEG_RECS runs, is split over its lanes by steps with 2
-		// spare per lane), lanes beyond that idle
+		// most 16 per ray (the segment scratch of a ray, MARCH_SEG_RECS runs, is split over its lanes: at 16 a lane holds
+		// 68 runs for its at most 1024 / 16 + 2 steps), lanes beyond that idle
 		uint32_t mr[8], Lr[8];
 		float W = 0.f, wmax = -1.f;
 		uint32_t n_act = 0, heavy = 0;
 		float wv[8];
 #pragma unroll
 		for (int r = 0; r < 8; ++r) {
-			wv[r] = __shfl(wr, 8 * r);
+			wv[r] = __shfl(wr, r);
 			const bool act = __shfl(t0r, r) >= 0.f;
 			mr[r] = act ? 1u : 0u;
 			n_act += act ? 1u : 0u;
@@ -674,49 +555,32 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))
 		MarchRay mr_{};
 		float t_exit = t0;
 		if (have && t0 >= 0.f) {
-			const float* sr = s_ray[threadIdx.x >> 6][rr];
+			load_march_ray(rays, i, mr_, ds.motion.on != 0);
+			float tx[3];
 #pragma unroll
-			for (int d = 0; d < 3; ++d) { mr_.o[d] = sr[d]; mr_.dir[d] = sr[3 + d]; mr_.idir[d] = sr[6 + d]; }
-			t_exit = sr[9];
+			for (int d = 0; d < 3; ++d) {
+				const float a = (ds.aabb_min[d] - mr_.o[d]) * mr_.idir[d], c = (ds.aabb_max[d] - mr_.o[d]) * mr_.idir[d];
+				tx[d] = fmaxf(a, c);
+			}
+			t_exit = fminf(fminf(tx[0], tx[1]), tx[2]);
 		}
 		const float span = t_exit - t0;
 		const bool split = have && t0 >= 0.f && span > 0.f && span < 1e4f;
 		float t = t0;
 		uint32_t k = 0;
 		const bool active = have && t0 >= 0.f && (g == 0 || split);
-		if (active && g > 0) {
-			// lane g starts where the ray's cumulative work reaches g / MG of its total (any start gives the same result;
-			// this one shares the events evenly), linear within the profile's bin
-			const float* cum = s_cum[threadIdx.x >> 6][rr];
-			const float Wt = cum[31], c = Wt * ((float)g / (float)MG);
-			float fr = (float)g / (float)MG;
-			if (Wt > 0.f) {
-				uint32_t pos = 0;
-#pragma unroll
-				for (uint32_t st2 = 16; st2 > 0; st2 >>= 1)
-					if (cum[pos + st2 - 1] <= c) pos += st2;
-				const uint32_t bin = min(pos, 31u);
-				const float prev = bin ? cum[bin - 1] : 0.f, wb = cum[bin] - prev;
-				fr = ((float)bin + (wb > 0.f ? fminf(fmaxf((c - prev) / wb, 0.f), 1.f) : 0.f)) * (1.0f / 32.0f);
-			}
-			step_until(t, k, t0 + span * fr, 4 * NERF_STEPS, MIN_CONE_STEPSIZE);
-		}
+		if (active && g > 0) step_until(t, k, t0 + span * ((float)g / (float)MG), 4 * NERF_STEPS, MIN_CONE_STEPSIZE);
 		stamp(1);
-		const uint32_t k_next = (uint32_t)__shfl((int)k, (int)((lane + 1) & 63));  // the next lane's start
-		uint32_t k_end = k_next;
+		uint32_t k_end = (uint32_t)__shfl((int)k, (int)((lane + 1) & 63));  // the next lane's start
 		if (g + 1 == MG || !split) k_end = FINISHED;
-		// the ray's run scratch split by steps: lane g's slice [k, k_next) holds at most k_next - k runs (a run is >= 1
-		// step); the offsets k + 2 g leave the join's margin, and the last lane's <= 1025 - k steps fit the rest
-		// (k <= 1026: the span is at most the box diagonal, 1024 steps, plus the start's jitter and t's rounding; g < 16)
-		const uint32_t seg_off = k + 2u * g;
-		const uint32_t seg_cap = k_end == FINISHED ? MARCH_SEG_RECS - seg_off : k_next - k + 2u;
-		uint2* rec = mw.seg + (size_t)i * MARCH_SEG_RECS + seg_off;
+		const uint32_t seg_cap = MARCH_SEG_RECS / MG;
+		uint2* rec = mw.seg + (size_t)i * MARCH_SEG_RECS + (size_t)g * seg_cap;
 		SegAcc acc{0.f, 0u, 0u, 0u, 0u};
 		Visits vis{0ull, k};
 		float et = t;
 		uint32_t ek = active ? k : FINISHED;
 		uint32_t n_ev = 0;
-		if (active) march_segment<FAST>(ds, bitfield, lin, mr_, et, ek, k_end, acc, vis, rec, seg_cap, &n_ev, mw.dbg, s_mac);
+		if (active) march_segment<FAST>(ds, bitfield, lin, mr_, et, ek, k_end, acc, vis, rec, seg_cap, &n_ev, mw.dbg);
 		if (__builtin_expect(__ballot(active && !((et >= 0.f) & (et < __builtin_huge_valf()))) != 0ull, 0) && lane == 0)
 			atomicOr(&st->fail_flags, STEP_FAIL_MARCH_T);
 		stamp(2);
@@ -739,7 +603,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))
 				if (redo) {
 					acc = SegAcc{0.f, 0u, 0u, 0u, 0u}; vis = Visits{0ull, pk};
 					et = pt; ek = pk; vk = pk;
-					march_segment<FAST>(ds, bitfield, lin, mr_, et, ek, k_end, acc, vis, rec, seg_cap, nullptr, 0u, s_mac);
+					march_segment<FAST>(ds, bitfield, lin, mr_, et, ek, k_end, acc, vis, rec, seg_cap);
 				}
 			}
 		}
@@ -1698,7 +1562,6 @@ __global__ void k_step_counters(StepState* st, uint32_t target_batch, uint32_t m
 static inline uint32_t ray_blocks(uint32_t cap) { return std::max<uint32_t>(1, std::min<uint32_t>((cap + 255) / 256, 2048)); }
 void launch_bitfield_linear(hipStream_t s, const uint8_t* bitfield, uint32_t* lin) {
 	k_bitfield_linear<<<GRID3 / 32 / 256, 256, 0, s>>>(bitfield, lin);
-	k_bitfield_macro<<<MACRO_N * MACRO_N * MACRO_N / 256, 256, 0, s>>>(bitfield, lin);
 }
 void launch_march_count(hipStream_t s, uint32_t cap, uint32_t max_samples, StepState* st, DPInfo dp, const DevDataset& ds, const uint8_t* bitfield,
                         const uint32_t* lin, uint64_t rng_state, uint64_t rng_inc, float* rays, float* tstart, uint32_t* nreq, const MarchWork& mw,

@@ -58,17 +58,4 @@ __device__ __forceinline__ void grid_sample_cell(uint32_t c, uint64_t rng_state,
 	pos[2] = (pz - amin[2]) / diag[2];
 }
 
-// The march's block map (common.h MACRO_OFF): wave q covers blocks 64 q .. 64 q + 63, (x, y, z) = (q' >> 10, q' >> 5 & 31,
-// q' & 31). A 4^3-aligned block of mip 0 is 64 consecutive Morton bits, i.e. one 8-byte word of the bitfield. A bit is
-// 1 (never skipped whole) for a block with an occupied cell, a block holding a face cell (index 0 / 127 takes mip 1 at
-// the face itself) and the block of the centre cell (the centre point takes mip 1).
-__device__ __forceinline__ void macro_wave(const uint8_t* __restrict__ bf, uint32_t* __restrict__ lin, uint32_t q, uint32_t lane) {
-	const uint32_t b = q * 64u + lane, bx = b >> 10, by = (b >> 5) & 31u, bz = b & 31u;
-	const uint64_t v = reinterpret_cast<const uint64_t*>(bf)[morton3D(bx, by, bz)];
-	const bool face = bx == 0 || by == 0 || bz == 0 || bx == MACRO_N - 1 || by == MACRO_N - 1 || bz == MACRO_N - 1;
-	const bool centre = bx == MACRO_N / 2 && by == MACRO_N / 2 && bz == MACRO_N / 2;
-	const unsigned long long m = __ballot(v != 0ull || face || centre);
-	if ((lane & 31u) == 0u) lin[MACRO_OFF + (b >> 5)] = (uint32_t)(m >> (lane & 32u));
-}
-
 } // namespace neus

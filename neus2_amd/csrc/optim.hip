@@ -285,14 +285,12 @@ __global__ void k_grid_to_bitfield(uint32_t n_bytes_total, uint32_t n_nonzero, c
 // bytes (one 64-bit atomic OR); the parent bytes this OR turned nonzero then set their own parent bit, and so on up
 // while a byte turns nonzero. Every byte that becomes nonzero is propagated by exactly the wave that made it so (or
 // by its own wave when its grid bits were set); OR is order-independent, so the bits are the level-by-level pool's.
-// The same launch converts mip 0 (which the pools only read) to the march's linear words (k_bitfield_linear) and its
-// block map (macro_wave) in its last GRID3 / 32 / 64 + 512 waves.
+// The same launch converts mip 0 (which the pools only read) to the march's linear words (k_bitfield_linear) in
+// its last GRID3 / 32 / 64 waves.
 __global__ void k_bitfield_pool_all(uint32_t nbytes, uint8_t* __restrict__ bf, uint32_t* __restrict__ lin) {
 	const uint32_t lane = threadIdx.x & 63, waves_per_level = nbytes / 64;
 	const uint32_t n_waves = waves_per_level * (NERF_CASCADES - 1), n_lin_waves = lin ? GRID3 / 32 / 64 : 0u;
-	const uint32_t n_mac_waves = lin ? MACRO_N * MACRO_N * MACRO_N / 64 : 0u;
-	for (uint32_t wg = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; wg < n_waves + n_lin_waves + n_mac_waves; wg += (gridDim.x * blockDim.x) >> 6) {
-		if (wg >= n_waves + n_lin_waves) { macro_wave(bf, lin, wg - n_waves - n_lin_waves, lane); continue; }
+	for (uint32_t wg = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; wg < n_waves + n_lin_waves; wg += (gridDim.x * blockDim.x) >> 6) {
 		if (wg >= n_waves) {
 			const uint32_t w = (wg - n_waves) * 64 + lane;
 			const uint32_t ix = w >> 9, iy = (w >> 2) & 127, iz0 = (w & 3) * 32;

@@ -731,8 +731,6 @@ struct NeusTestbed {
 		march_seg.alloc((size_t)MAX_RAYS * MARCH_SEG_RECS);
 		mwork = MarchWork{march_rec.p, march_nrec.p, march_queue.p, march_waves(), march_seg.p, march_lanes(), jump_table()};
 		{ const char* e = std::getenv("NEUS_MARCH_BALANCE"); mwork.balanced = !(e && e[0] == '0') ? 1u : 0u; }
-		{ const char* e = std::getenv("NEUS_MARCH_MACRO"); mwork.macro = !(e && e[0] == '0') ? 1u : 0u; }
-		{ const char* e = std::getenv("NEUS_MARCH_PROF_W"); if (e && std::atof(e) > 0.0) mwork.prof_w = (float)std::atof(e); }
 		nreq.alloc(MAX_RAYS); base.alloc(MAX_RAYS);
 		numsteps.alloc(2 * (size_t)MAX_RAYS); ccount.alloc(MAX_RAYS); cbase.alloc(MAX_RAYS);
 		l_sa.alloc(max_samples); l_ekt.alloc(max_samples); sample_ray.alloc(max_samples); cmap.alloc(batch);
@@ -2525,8 +2523,6 @@ static void sample_rays_impl(NeusTestbed* tb, void* stream, uint32_t n_rays, uin
 		Dev<uint2> seg; seg.alloc((size_t)n_rays * MARCH_SEG_RECS);
 		MarchWork mw{rec.p, nrec.p, q.p, tb->mwork.waves, seg.p, tb->mwork.lanes_per_ray};
 		mw.balanced = tb->mwork.balanced;
-		mw.macro = tb->mwork.macro;
-		mw.prof_w = tb->mwork.prof_w;
 		ScanTemp tmp; const size_t tb_ = scan_temp_bytes(n_rays); tmp.alloc(tb_ + 256); scan_temp_reset(s, tmp.p);
 		Dev<uint32_t> lin; lin.alloc(LIN_WORDS);
 		launch_bitfield_linear(s, bitfield, lin.p);
