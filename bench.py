@@ -162,6 +162,9 @@ def kernel_rooflines(tb, levels, iters=9):
         if fpu:
             r["tflops"] = round(fpu * units / (ms * 1e-3) / 1e12, 1)
             r["mfma_frac"] = round(r["tflops"] / MFMA_PEAK_TFLOPS, 4)
+        if name == "adam_ema":
+            r["note"] = ("bytes: the reference's 48 B per parameter (SURVEY §8(d)); the kernel reads and writes the fp32 weight, moments "
+                         "and step count only for groups with a nonzero gradient, so it moves fewer and frac can exceed 1")
         out[name] = r
     return out
 
