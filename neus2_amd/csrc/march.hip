@@ -1211,7 +1211,20 @@ __global__ void __launch_bounds__(64) k_loss_scan_list(const uint32_t* __restric
 // put 64 lines behind every load instruction). The appends are one atomic per wave and a cooperative write of the
 // wave's concatenated chunks (consecutive lanes, consecutive list slots). Same float operation sequence per ray, so
 // the state is bitwise the one-thread-per-ray loop's.
-__global__ void __launch_bounds__(64) k_loss_scan_chunk(uint32_t cap_rays, const uint32_t* __restrict__ numsteps, const float4* __restrict__ sa,
+// groups in flight: 1 (130 VGPRs, 3 waves per SIMD) measured 2 us/step faster than 2 (170 VGPRs, 2 waves), 1 at 4 waves
+// per SIMD (5 spilled dwords) slower (profiles/r05nb_scan_groups_ab.txt)
+#ifndef NEUS_SCAN_NB
+#define NEUS_SCAN_NB 1
+#endif
+#ifndef NEUS_SCAN_WPE
+#define NEUS_SCAN_WPE 0
+#endif
+#if NEUS_SCAN_WPE
+#define SCAN_OCC __attribute__((amdgpu_waves_per_eu(NEUS_SCAN_WPE, NEUS_SCAN_WPE)))
+#else
+#define SCAN_OCC
+#endif
+__global__ void __launch_bounds__(64) SCAN_OCC k_loss_scan_chunk(uint32_t cap_rays, const uint32_t* __restrict__ numsteps, const float4* __restrict__ sa,
                                                         const float* __restrict__ ekt, float4* __restrict__ ck4, float* __restrict__ cke,
                                                         uint32_t* __restrict__ ccount, float4* __restrict__ racc, float* __restrict__ rT,
                                                         float* __restrict__ rek, uint32_t e0, uint32_t e1, uint32_t e2,
@@ -1220,9 +1233,10 @@ __global__ void __launch_bounds__(64) k_loss_scan_chunk(uint32_t cap_rays, const
                                                         uint32_t* __restrict__ rays_out, uint32_t* __restrict__ n_rays_out) {
 	// U samples per ray and group: U lanes load U consecutive samples of one ray (64 / U rays per load instruction),
 	// transposed through LDS to one ray per lane. U = 8 (was 16): half the LDS and registers per wave, so twice the
-	// waves per CU hide the per-ray state loads. Two groups are in flight (a 4-deep fetch in the later rounds, whose few
-	// waves each wait on their own loads, measured the same: profiles/r05q_scan_ab.txt)
-	constexpr uint32_t U = 8, PAD = U + 1, RPI = 64 / U, NB = 2;
+	// waves per CU hide the per-ray state loads. NB groups are in flight, the next group's fetch issued before the
+	// current one runs through the recurrence (a 4-deep fetch in the later rounds measured the same as 2:
+	// profiles/r05q_scan_ab.txt; 1 is the default, above)
+	constexpr uint32_t U = 8, PAD = U + 1, RPI = 64 / U, NB = NEUS_SCAN_NB;
 	typedef float f4v __attribute__((ext_vector_type(4)));
 	__shared__ f4v s_q[64 * PAD];
 	__shared__ float s_e[64 * PAD];
