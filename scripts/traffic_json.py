@@ -21,7 +21,8 @@ def parse(path, names=NAMES):
             name = m.group(1)
             # k_march is the march itself: the templated k_march<...> or the balanced k_march_bal (the default), not
             # k_march_numsteps / k_march_write / k_march_scan
-            cur = next((v for k, v in names.items() if (re.match(r"k_march(<|_bal\b)", name) if k == "k_march" else k in name)), None)
+            # (names come mangled or demangled: "neus::k_march_bal", "void neus::k_scatter_bin_r<512>")
+            cur = next((v for k, v in names.items() if (re.search(r"(^|::)k_march(<|_bal\b)", name) if k == "k_march" else k in name)), None)
             continue
         m = re.match(r"\s+(\w+)\s+([-+0-9.eE]+)$", line)
         if m and cur:
