@@ -181,6 +181,14 @@ struct NeusTestbed {
 	// outputs; both deterministic), forked from and joined back into the step's stream by events
 	hipStream_t aux_stream = nullptr;
 	hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+	// Lookahead (NEUS_LOOKAHEAD): the next step's ray sampling (ray generation, march, march write, ray sort) issued on
+	// la_stream right after this step's loss, beside its backward and optimizer, which read none of its outputs. Only
+	// between steps of one neus_testbed_train call (nothing pending between calls), at one rank, on static scenes, and
+	// not before a step that starts with an occupancy update or a loss readback (train_step: la_go).
+	bool la_on = [] { const char* e = std::getenv("NEUS_LOOKAHEAD"); return !(e && e[0] == '0'); }();
+	bool la_pending = false, la_next_in_call = false;
+	hipStream_t la_stream = nullptr;
+	hipEvent_t ev_la_start = nullptr, ev_la_done = nullptr;
 	NeusNetworkConfig cfg{};
 	bool have_net = false, have_data = false;
 	Layout lay{};
@@ -279,7 +287,7 @@ struct NeusTestbed {
 	Dev<float4> vbuf;
 	Dev<float> wgrad_partial, var_partial;  // per-block MLP weight-gradient rows, per-block variance sums
 	uint32_t mlp_blocks = 0;                // grid of the training MLP kernels at the batch capacity
-	ScanTemp scan_tmp;
+	ScanTemp scan_tmp, scan_tmp_la;  // (scan_tmp_la: the lookahead's march scans, on la_stream)
 	size_t scan_tmp_bytes = 0;
 	Dev<StepState> st;
 	ScatterWork swork{};
@@ -455,6 +463,9 @@ struct NeusTestbed {
 		if (prof_st) (void)hipHostFree(prof_st);
 		if (pinned) (void)hipHostFree(pinned);
 		if (aux_stream) { (void)hipStreamSynchronize(aux_stream); (void)hipStreamDestroy(aux_stream); }
+		if (la_stream) { (void)hipStreamSynchronize(la_stream); (void)hipStreamDestroy(la_stream); }
+		if (ev_la_start) (void)hipEventDestroy(ev_la_start);
+		if (ev_la_done) (void)hipEventDestroy(ev_la_done);
 		if (ev_fork) (void)hipEventDestroy(ev_fork);
 		if (ev_join) (void)hipEventDestroy(ev_join);
 		if (ev_loss) (void)hipEventDestroy(ev_loss);
@@ -1360,6 +1371,8 @@ struct NeusTestbed {
 			}
 		}
 		const bool use_delta = dyn && train_delta;
+		const bool la_have = la_pending;
+		la_pending = false;
 		render_delta = use_delta;  // m_nerf_network->m_use_delta follows the training step (testbed.cu:2704-2710)
 		enc_step = dyn ? (int)training_step - (int)gm_steps() : (int)training_step;
 		const uint32_t valid = valid_level_at(enc_step);
@@ -1371,7 +1384,6 @@ struct NeusTestbed {
 			if (training_step < 256) occ_update(nc, 0, valid, use_delta);
 			else occ_update(nc / 4, nc / 4, valid, use_delta);
 		}
-		const bool get_loss = training_step % 16 == 0;
 		// ---- train_nerf_step (testbed_nerf.cu:3723-4001)
 		if (training_step == 0 || canonical_step == 0) HIP_CHECK(hipMemsetAsync(&st.p->n_rays_total, 0, 4, s));
 		const DPInfo dp{rank, world};  // (n_kept, n_rays_with_samples: zeroed by k_ray_gen)
@@ -1382,12 +1394,13 @@ struct NeusTestbed {
 		// round 0's list slots go through cbase (rewritten by the loss compaction before it is read again)
 		const Round0List r0{chunk_ends[0], cbase.p, chunk_list.p, chunk_cnt.p, nch + 1};
 		const bool sorted_rays = progressive && ray_sort;  // round 0's list by k_ray_sort_place instead of the march write
-		launch_march_count(s, MAX_RAYS, max_samples, st.p, dp, ds, bitfield.p, bf_lin.p, rng.state, rng.inc, rays.p, startt.p, nreq.p, mwork,
-		                   progressive ? chunk_cnt.p : nullptr, OPEN_CNT + nch, ray_cull ? occ_bbox.p : nullptr);  // list lengths + open-ray counts
-		launch_march_write(s, MAX_RAYS, st.p, ds, rays.p, mwork, nreq.p, base.p, numsteps.p, coords.p, nullptr, max_samples, scan_tmp.p,
-		                   progressive && !sorted_rays ? &r0 : nullptr, dbg_lds_fill);
 		const RaySort rsort{rs_hist.p, rs_off.p, rs_key.p, rs_perm.p, chunk_cnt.p + RS_N_PERM};
-		if (sorted_rays) launch_ray_sort(s, MAX_RAYS, numsteps.p, coords.p, chunk_ends[0], rsort, chunk_list.p, chunk_cnt.p, scan_tmp.p, scan_tmp_bytes);
+		if (la_have) {
+			if (canonical_step % n_prep == 0) throw std::runtime_error("train: lookahead issued before an occupancy update");
+			HIP_CHECK(hipStreamWaitEvent(s, ev_la_done, 0));  // this step's samples came from the previous step's lookahead
+		} else {
+			issue_march(s, dp, rng, progressive, scan_tmp.p);
+		}
 		mark(2);
 		// DeltaNetwork forward on the samples (nerf_network.h:162-182); the loss keeps the undeformed records
 		const float* c_in = coords.p;
@@ -1445,6 +1458,49 @@ struct NeusTestbed {
 				HIP_CHECK(hipMemcpyAsync(dbg_snap[k].p, src[k].first, src[k].second, hipMemcpyDeviceToDevice, s));
 			}
 		}
+		// ---- lookahead: the next step's ray sampling beside this step's backward (la_on; see the members)
+		const bool get_loss = training_step % 16 == 0;
+		const StepCounterArgs sca{st.p, batch, max_samples, world, cfg.fixed_rays_per_batch, progressive ? chunk_cnt.p : nullptr, nch};
+		bool counters_done = false;
+		{
+			const uint32_t cs1 = training_step + 1;  // the next step's canonical step (static scenes)
+			const uint32_t n_prep1 = std::min(16u, std::max(1u, cs1 / 16u));
+			const bool la_go = la_on && la_next_in_call && world == 1 && !coll_on() && !dyn && !use_delta && !profiling && !dbg_loss_replay &&
+			                   !dbg_lds_fill && g_dbg_lds_fill == 0 && g_dbg_xcd_shift == 0 && cs1 % 16 != 0 && cs1 % n_prep1 != 0 &&
+			                   !(get_loss && loss_pending);
+			if (la_go) {
+				// the host's StepState readback first (its place in the step without the lookahead: nothing writes these
+				// fields between here and there at one rank), then the step counters the next step's sampling reads
+				if (get_loss) HIP_CHECK(hipMemcpyAsync(pinned + 64, st.p, sizeof(StepState), hipMemcpyDeviceToHost, s));
+				launch_step_counters(s, st.p, batch, max_samples, world, cfg.fixed_rays_per_batch, sca.eval_cnt, sca.n_eval);
+				counters_done = true;
+				if (!la_stream) {
+					// the lookahead stream at the lowest priority: the backward's workgroups are dispatched first and the march's
+					// fill what they leave (1.154 -> 1.107 ms/step at the bench state; the default priority 1.139, the highest
+					// 1.141: profiles/r05lap_lookahead_priority_ab.txt). NEUS_LA_PRIO: -1 lowest, 0 default, 1 highest.
+					const char* e = std::getenv("NEUS_LA_PRIO");
+					const int want = e ? std::atoi(e) : -1;
+					int lo = 0, hi = 0;
+					HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));  // (lo: least urgent, hi: most urgent; hi <= lo numerically)
+					if (want == 0) HIP_CHECK(hipStreamCreateWithFlags(&la_stream, hipStreamNonBlocking));
+					else HIP_CHECK(hipStreamCreateWithPriority(&la_stream, hipStreamNonBlocking, want > 0 ? hi : lo));
+					HIP_CHECK(hipEventCreateWithFlags(&ev_la_start, hipEventDisableTiming));
+					HIP_CHECK(hipEventCreateWithFlags(&ev_la_done, hipEventDisableTiming));
+				}
+				if (!scan_tmp_la.p || scan_tmp_la.n < scan_tmp_bytes + 256) {
+					scan_tmp_la.alloc(scan_tmp_bytes + 256);
+					scan_temp_reset(s, scan_tmp_la.p);
+				}
+				HIP_CHECK(hipEventRecord(ev_la_start, s));
+				HIP_CHECK(hipStreamWaitEvent(la_stream, ev_la_start, 0));
+				pcg32 r1 = rng;
+				r1.advance();
+				const bool prog1 = progressive_mode == 2 || (progressive_mode == 1 && last_keep_ratio < PROGRESSIVE_RATIO);
+				issue_march(la_stream, dp, r1, prog1, scan_tmp_la.p);
+				HIP_CHECK(hipEventRecord(ev_la_done, la_stream));
+				la_pending = true;
+			}
+		}
 		// the rollover copies are made by the training encode (static scenes); the DeltaNetwork reads the whole batch first
 		if (use_delta) launch_rollover(s, batch, st.p, coords_c.p, dL_dout.p);
 		const EncodeRollover ro{&st.p->compacted_counter, batch, dL_dout.p, coords_c.p};
@@ -1499,20 +1555,19 @@ struct NeusTestbed {
 			if (loss_pending) consume_loss();  // (consumed at this step's start already; a restored state may leave one)
 			HIP_CHECK(hipMemcpyAsync(pinned, loss_sum.p, 3 * 4, hipMemcpyDeviceToHost, s));
 			HIP_CHECK(hipMemcpyAsync(pinned + 52, health_buf.p, 8, hipMemcpyDeviceToHost, s));
-			HIP_CHECK(hipMemcpyAsync(pinned + 64, st.p, sizeof(StepState), hipMemcpyDeviceToHost, s));
+			if (!counters_done) HIP_CHECK(hipMemcpyAsync(pinned + 64, st.p, sizeof(StepState), hipMemcpyDeviceToHost, s));
 			HIP_CHECK(hipMemcpyAsync(pinned + 48, scan_tmp.p + offsetof(ScanState, fail), 4, hipMemcpyDeviceToHost, s));
 			HIP_CHECK(hipEventRecord(ev_loss, s));
 			loss_pending = true;
 		}
 		// the step-end counters ride on the Adam launch when the canonical optimizer steps (k_step_counters otherwise)
 		// (progressive inference: the samples evaluated are the rounds' list lengths chunk_cnt[0, nch))
-		const StepCounterArgs sca{st.p, batch, max_samples, world, cfg.fixed_rays_per_batch, progressive ? chunk_cnt.p : nullptr, nch};
 		const bool canon_opt = !dyn || train_canonical;
-		if (!canon_opt) launch_step_counters(s, st.p, batch, max_samples, world, cfg.fixed_rays_per_batch, sca.eval_cnt, sca.n_eval);
+		if (!canon_opt && !counters_done) launch_step_counters(s, st.p, batch, max_samples, world, cfg.fixed_rays_per_batch, sca.eval_cnt, sca.n_eval);
 		rng.advance();
 		mark(9);
 		// ---- optimizers (testbed_nerf.cu:3503-3508): the canonical trainer, the global-move trainer
-		if (canon_opt) optimizer_step(grads.p, &sca);
+		if (canon_opt) optimizer_step(grads.p, counters_done ? nullptr : &sca);
 		if (use_delta) {
 			// ExponentialDecay of the globalmove optimizer (exponential_decay.h:61-80), its own step count
 			if (delta_step == 0) delta_lr_factor = 1.f;
@@ -1535,6 +1590,21 @@ struct NeusTestbed {
 			if (prof_pending[prof_par]) accumulate_phases(prof_par);  // the previous step
 		}
 		it_collect();
+	}
+
+	// A step's ray sampling: ray generation + the march's two passes, the coordinate write (and round 0's list, unsorted
+	// progressive), the spatial ray sort (sorted progressive); rng / progressive: the step's own (train_step, or the
+	// lookahead for the next step), scan: the look-back state of the stream it runs on.
+	void issue_march(hipStream_t s, const DPInfo& dp, const pcg32& r, bool progressive, uint8_t* scan) {
+		const uint32_t nch = (uint32_t)chunk_ends.size() + 1;
+		const Round0List r0{chunk_ends[0], cbase.p, chunk_list.p, chunk_cnt.p, nch + 1};
+		const bool sorted_rays = progressive && ray_sort;
+		launch_march_count(s, MAX_RAYS, max_samples, st.p, dp, ds, bitfield.p, bf_lin.p, r.state, r.inc, rays.p, startt.p, nreq.p, mwork,
+		                   progressive ? chunk_cnt.p : nullptr, OPEN_CNT + nch, ray_cull ? occ_bbox.p : nullptr);  // list lengths + open-ray counts
+		launch_march_write(s, MAX_RAYS, st.p, ds, rays.p, mwork, nreq.p, base.p, numsteps.p, coords.p, nullptr, max_samples, scan,
+		                   progressive && !sorted_rays ? &r0 : nullptr, dbg_lds_fill);
+		const RaySort rsort{rs_hist.p, rs_off.p, rs_key.p, rs_perm.p, chunk_cnt.p + RS_N_PERM};
+		if (sorted_rays) launch_ray_sort(s, MAX_RAYS, numsteps.p, coords.p, chunk_ends[0], rsort, chunk_list.p, chunk_cnt.p, scan, scan_tmp_bytes);
 	}
 
 	LossWork loss_work(const uint32_t* rbase) {
@@ -1659,9 +1729,12 @@ int neus_testbed_train(NeusTestbed* tb, uint32_t n_steps) {
 		// the LDS-garbage test hook is this thread's while its steps are queued (other testbeds / threads unaffected);
 		// the pattern alternates with its complement from step to step
 		struct FillScope { ~FillScope() { g_dbg_lds_fill = 0; g_dbg_xcd_shift = 0; } } fill_scope;
+		// (a lookahead left pending by a step that threw is dropped: the next step marches again, the same samples)
+		struct LaScope { NeusTestbed* t; ~LaScope() { if (t->la_pending) { (void)hipStreamSynchronize(t->la_stream); t->la_pending = false; } t->la_next_in_call = false; } } la_scope{tb};
 		for (uint32_t i = 0; i < n_steps; ++i) {
 			g_dbg_lds_fill = tb->dbg_lds_fill_all ? ((tb->training_step & 1) ? ~tb->dbg_lds_fill_all : tb->dbg_lds_fill_all) : 0u;
 			g_dbg_xcd_shift = tb->dbg_xcd_shift;
+			tb->la_next_in_call = i + 1 < n_steps;
 			tb->train_step();
 		}
 	});

@@ -87,3 +87,29 @@ def test_bench_step_bitwise_under_lds_garbage_and_concurrency(torch_cuda):
         got = _state(tb)
         for k, v in want.items():
             np.testing.assert_array_equal(got[k].view(np.uint8), v.view(np.uint8), err_msg=f"concurrent testbed {i}: {k}")
+
+
+def test_lookahead_sampling_bitwise(torch_cuda):
+    """The next step's ray sampling issued beside the current step's backward (the default; NEUS_LOOKAHEAD=0 turns it
+    off, testbed.cpp la_go) gives the step the same samples: from one initialisation, 300 steps in one call (occupancy
+    updates and loss readbacks, where the lookahead pauses, included) end with bitwise equal parameters, EMA weights,
+    occupancy grid and per-ray counts, with and without it."""
+    from neus2_amd import pyngp, scenes
+    sc = scenes.sphere_scene(16, 400, 300, principal=(0.51, 0.52))
+    out = {}
+    for la in ("0", "1"):
+        os.environ["NEUS_LOOKAHEAD"] = la
+        try:
+            tb = pyngp.Testbed(pyngp.TestbedMode.Nerf)
+            tb.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
+            tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=1 << 16)
+            tb.train_steps(300)
+            grid, bf = tb.get_density_grid()
+            out[la] = {"params": tb.get_params(), "ema": tb.get_ema_params(), "grid": grid, "bitfield": bf,
+                       "counts": np.concatenate(tb.ray_counts(1 << 16)[:2]), "step": tb.stats()["training_step"]}
+            del tb
+        finally:
+            os.environ.pop("NEUS_LOOKAHEAD", None)
+    assert out["0"]["step"] == out["1"]["step"] == 300
+    for k in ("params", "ema", "grid", "bitfield", "counts"):
+        np.testing.assert_array_equal(out["0"][k], out["1"][k], err_msg=k)
