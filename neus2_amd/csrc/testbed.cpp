@@ -187,6 +187,7 @@ struct NeusTestbed {
 	// not before a step that starts with an occupancy update or a loss readback (train_step: la_go).
 	bool la_on = [] { const char* e = std::getenv("NEUS_LOOKAHEAD"); return !(e && e[0] == '0'); }();
 	bool la_pending = false, la_next_in_call = false;
+	int main_prio = 0;  // the step's streams' priority (0: created without one; the communication stream follows it)
 	hipStream_t la_stream = nullptr;
 	hipEvent_t ev_la_start = nullptr, ev_la_done = nullptr;
 	NeusNetworkConfig cfg{};
@@ -381,7 +382,8 @@ struct NeusTestbed {
 	hipStream_t x_stream() {
 		if (!comm && !hgroup) return stream;
 		if (!comm_stream) {
-			HIP_CHECK(hipStreamCreateWithFlags(&comm_stream, hipStreamNonBlocking));
+			if (main_prio) HIP_CHECK(hipStreamCreateWithPriority(&comm_stream, hipStreamNonBlocking, main_prio));
+			else HIP_CHECK(hipStreamCreateWithFlags(&comm_stream, hipStreamNonBlocking));
 			HIP_CHECK(hipEventCreateWithFlags(&ev_xdone, hipEventDisableTiming));
 		}
 		hipEvent_t& e = ev_x[ev_x_n++ % 16];
@@ -433,8 +435,25 @@ struct NeusTestbed {
 
 	NeusTestbed(int dev) : device(dev) {
 		HIP_CHECK(hipSetDevice(device));
-		HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-		HIP_CHECK(hipStreamCreateWithFlags(&aux_stream, hipStreamNonBlocking));
+		{
+			// The step's streams at the highest priority, the lookahead's at the lowest (train_step). With the step's
+			// streams at the default priority, a testbed created after another one was destroyed ran the 16-level bench leg
+			// at 1.91 ms/step instead of 1.27 with the lookahead at the lowest priority (profiles/r05l16_priorities_ab.txt),
+			// presumably from how the runtime maps the streams onto its few hardware queues; explicit priorities on every
+			// stream keep it at 1.24. NEUS_MAIN_PRIO=0: the default priority.
+			const char* e = std::getenv("NEUS_MAIN_PRIO");
+			int lo = 0, hi = 0;
+			HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+			main_prio = hi;
+			if (!(e && e[0] == '0')) {
+				HIP_CHECK(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, hi));
+				HIP_CHECK(hipStreamCreateWithPriority(&aux_stream, hipStreamNonBlocking, hi));
+			} else {
+				main_prio = 0;
+				HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+				HIP_CHECK(hipStreamCreateWithFlags(&aux_stream, hipStreamNonBlocking));
+			}
+		}
 		HIP_CHECK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
 		HIP_CHECK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
 		HIP_CHECK(hipEventCreateWithFlags(&ev_loss, hipEventDisableTiming));
