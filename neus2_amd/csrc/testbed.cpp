@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
+#include <functional>
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
@@ -187,9 +188,46 @@ struct NeusTestbed {
 	// not before a step that starts with an occupancy update or a loss readback (train_step: la_go).
 	bool la_on = [] { const char* e = std::getenv("NEUS_LOOKAHEAD"); return !(e && e[0] == '0'); }();
 	bool la_pending = false, la_next_in_call = false;
+	const bool la_stat = [] { const char* e = std::getenv("NEUS_LA_STAT"); return e && e[0] == '1'; }();
+	// development (NEUS_LA_AT): where in the backward the lookahead is issued. 0 right after the loss (the default), 1 after
+	// the training encode, 2 after the training MLP kernels, 3 after the weight-gradient reduction, 4 after the scatter
+	// (profiles/r05la_issue_point_ab.txt: 1 as 0, 2 and 3 slower)
+	const int la_at = [] { const char* e = std::getenv("NEUS_LA_AT"); return e ? std::atoi(e) : 0; }();
+	std::function<void()> la_deferred;
+	void la_fire(int at) {
+		if (la_deferred && at >= la_at) { auto f = std::move(la_deferred); la_deferred = nullptr; f(); }
+	}
 	int main_prio = 0;  // the step's streams' priority (0: created without one; the communication stream follows it)
 	hipStream_t la_stream = nullptr;
 	hipEvent_t ev_la_start = nullptr, ev_la_done = nullptr;
+	// development (NEUS_LA_STAT=1): per lookahead, timing events around its sampling (la stream) and around the next
+	// step's wait for it (main stream); summed and printed at the end of each neus_testbed_train call
+	std::vector<hipEvent_t> la_stat_ev;
+	size_t la_stat_used = 0;
+	hipEvent_t la_stat_next() {
+		if (la_stat_used == la_stat_ev.size()) {
+			hipEvent_t e;
+			HIP_CHECK(hipEventCreate(&e));
+			la_stat_ev.push_back(e);
+		}
+		return la_stat_ev[la_stat_used++];
+	}
+	void la_stat_report() {
+		if (la_stat_used < 4) { la_stat_used = 0; return; }
+		HIP_CHECK(hipDeviceSynchronize());
+		// groups of 4: la begin, la end (previous step), wait begin, wait end (this step)
+		double wait = 0, dur = 0, slack = 0;
+		size_t n = 0;
+		for (size_t k = 0; k + 4 <= la_stat_used; k += 4, ++n) {
+			float a = 0, b = 0, c = 0;
+			HIP_CHECK(hipEventElapsedTime(&a, la_stat_ev[k + 2], la_stat_ev[k + 3]));
+			HIP_CHECK(hipEventElapsedTime(&b, la_stat_ev[k], la_stat_ev[k + 1]));
+			HIP_CHECK(hipEventElapsedTime(&c, la_stat_ev[k + 1], la_stat_ev[k + 2]));
+			wait += a; dur += b; slack += c;
+		}
+		std::fprintf(stderr, "la_stat n=%zu wait_us=%.1f sampling_us=%.1f slack_us=%.1f\n", n, 1e3 * wait / n, 1e3 * dur / n, 1e3 * slack / n);
+		la_stat_used = 0;
+	}
 	NeusNetworkConfig cfg{};
 	bool have_net = false, have_data = false;
 	Layout lay{};
@@ -485,6 +523,7 @@ struct NeusTestbed {
 		if (la_stream) { (void)hipStreamSynchronize(la_stream); (void)hipStreamDestroy(la_stream); }
 		if (ev_la_start) (void)hipEventDestroy(ev_la_start);
 		if (ev_la_done) (void)hipEventDestroy(ev_la_done);
+		for (hipEvent_t e : la_stat_ev) (void)hipEventDestroy(e);
 		if (ev_fork) (void)hipEventDestroy(ev_fork);
 		if (ev_join) (void)hipEventDestroy(ev_join);
 		if (ev_loss) (void)hipEventDestroy(ev_loss);
@@ -985,14 +1024,17 @@ struct NeusTestbed {
 	                  bool exchange = false) {
 		const uint32_t ld = n;
 		encode(n_train_ptr, n, n, ld, c, COORD_W, valid, true, s, ro);
+		la_fire(1);
 		if (marks) mark(5);
 		TrainBufs t = tbuf;
 		t.var_grad = g + lay.var_off;
 		launch_mlp_train(s, lay.L, lay.W, n_valid_ptr, n, ld, c, (const half_t*)enc.p, dydx.p, dlo, mlp, t);
+		la_fire(2);
 		if (marks) mark(6);
 		if (!canonical) { if (marks) mark(7); return; }  // global-movement phase: canonical gradients unused
 		// the MLP weight gradients were accumulated inside the training kernels: one small fixed-order reduction
 		launch_mlp_grad_reduce(s, grad_reduce(n, g, n_train_ptr));
+		la_fire(3);
 		if (exchange) {  // the MLP blocks and the variance are final: their exchange runs beside the grid scatter
 			hipStream_t xs = x_stream();
 			allreduce_f32(g, lay.grid_off, false, xs);
@@ -1416,7 +1458,9 @@ struct NeusTestbed {
 		const RaySort rsort{rs_hist.p, rs_off.p, rs_key.p, rs_perm.p, chunk_cnt.p + RS_N_PERM};
 		if (la_have) {
 			if (canonical_step % n_prep == 0) throw std::runtime_error("train: lookahead issued before an occupancy update");
+			if (la_stat && la_stat_used % 4 == 2) HIP_CHECK(hipEventRecord(la_stat_next(), s));
 			HIP_CHECK(hipStreamWaitEvent(s, ev_la_done, 0));  // this step's samples came from the previous step's lookahead
+			if (la_stat && la_stat_used % 4 == 3) HIP_CHECK(hipEventRecord(la_stat_next(), s));
 		} else {
 			issue_march(s, dp, rng, progressive, scan_tmp.p);
 		}
@@ -1510,13 +1554,18 @@ struct NeusTestbed {
 					scan_tmp_la.alloc(scan_tmp_bytes + 256);
 					scan_temp_reset(s, scan_tmp_la.p);
 				}
-				HIP_CHECK(hipEventRecord(ev_la_start, s));
-				HIP_CHECK(hipStreamWaitEvent(la_stream, ev_la_start, 0));
 				pcg32 r1 = rng;
 				r1.advance();
 				const bool prog1 = progressive_mode == 2 || (progressive_mode == 1 && last_keep_ratio < PROGRESSIVE_RATIO);
-				issue_march(la_stream, dp, r1, prog1, scan_tmp_la.p);
-				HIP_CHECK(hipEventRecord(ev_la_done, la_stream));
+				la_deferred = [this, s, dp, r1, prog1] {
+					HIP_CHECK(hipEventRecord(ev_la_start, s));
+					HIP_CHECK(hipStreamWaitEvent(la_stream, ev_la_start, 0));
+					if (la_stat) { la_stat_used -= la_stat_used % 4; HIP_CHECK(hipEventRecord(la_stat_next(), la_stream)); }
+					issue_march(la_stream, dp, r1, prog1, scan_tmp_la.p);
+					if (la_stat) HIP_CHECK(hipEventRecord(la_stat_next(), la_stream));
+					HIP_CHECK(hipEventRecord(ev_la_done, la_stream));
+				};
+				la_fire(0);
 				la_pending = true;
 			}
 		}
@@ -1539,6 +1588,7 @@ struct NeusTestbed {
 		} else {
 			net_backward(&st.p->compacted_counter, &st.p->n_train, batch, coords_c.p, valid, dL_dout.p, grads.p, s, true, train_canonical, &ro, xo);
 		}
+		la_fire(99);  // (issued by now in any case)
 		// DeltaNetwork gradient partial sums (the first half of its backward; the Adam step follows the exchange)
 		if (use_delta) launch_delta_grad(s, &st.p->n_train, batch, coords_c.p, COORD_W, dpos.p, delta.p, delta_partial.p);
 		mark(8);
@@ -1749,7 +1799,7 @@ int neus_testbed_train(NeusTestbed* tb, uint32_t n_steps) {
 		// the pattern alternates with its complement from step to step
 		struct FillScope { ~FillScope() { g_dbg_lds_fill = 0; g_dbg_xcd_shift = 0; } } fill_scope;
 		// (a lookahead left pending by a step that threw is dropped: the next step marches again, the same samples)
-		struct LaScope { NeusTestbed* t; ~LaScope() { if (t->la_pending) { (void)hipStreamSynchronize(t->la_stream); t->la_pending = false; } t->la_next_in_call = false; } } la_scope{tb};
+		struct LaScope { NeusTestbed* t; ~LaScope() { if (t->la_pending) { (void)hipStreamSynchronize(t->la_stream); t->la_pending = false; } t->la_next_in_call = false; if (t->la_stat) t->la_stat_report(); } } la_scope{tb};
 		for (uint32_t i = 0; i < n_steps; ++i) {
 			g_dbg_lds_fill = tb->dbg_lds_fill_all ? ((tb->training_step & 1) ? ~tb->dbg_lds_fill_all : tb->dbg_lds_fill_all) : 0u;
 			g_dbg_xcd_shift = tb->dbg_xcd_shift;

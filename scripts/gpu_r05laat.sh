@@ -1,0 +1,17 @@
+#!/bin/bash
+# Where the lookahead is issued (NEUS_LA_AT 0-4), alternating on one box, at the bench state (main leg only).
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R" && mkdir -p gpurun_out
+F="--cpu-baseline 0 --psnr-steps 0 --mc-res 0 --l16 0 --early 0 --steps 200 --warmup 20"
+: > gpurun_out/ab_r05laat.txt
+for rep in 1 2; do for at in 0 1 2 3; do
+  NEUS_LA_STAT=1 NEUS_LA_AT=$at timeout -k 10 300 python -u bench.py $F > gpurun_out/laat_${at}_$rep.log 2>&1 || exit 1
+  python3 - "$at" "$rep" gpurun_out/laat_${at}_$rep.log >> gpurun_out/ab_r05laat.txt <<'PY'
+import json, sys
+lines = open(sys.argv[3]).read().splitlines()
+d = json.loads(lines[-1]); st = [l for l in lines if l.startswith("la_stat n=1")]
+print("at", sys.argv[1], "rep", sys.argv[2], "ms", round(d["ms_per_step"], 4), st[-1] if st else "")
+PY
+  tail -1 gpurun_out/ab_r05laat.txt
+done; done
+echo ALL_OK
