@@ -137,7 +137,7 @@ INFER_STEPS = 10
 def step_inference(it, levels):
     """The pre-compaction network pass as the training step runs it (progressive rounds of k_nerf_infer over their
     work lists): bytes = (28 coords + 32 L gather + 32 output) per evaluated sample, time = the launches' summed
-    hipEvent durations; reported per launch (the rocprofv3 kernel-trace average of k_nerf_infer over the same steps)."""
+    kernel durations (start/stop hipEvents given to hipExtLaunchKernelGGL); reported per launch (the rocprofv3 kernel-trace average of k_nerf_infer over the same steps)."""
     g = 8 * levels * 4
     n = max(1, it["launches"])
     ms = it["ms"] / n
@@ -146,7 +146,7 @@ def step_inference(it, levels):
             "frac": round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "launches_per_step": round(it["launches"] / max(1, it["steps"]), 2),
             "evaluated_per_step": round(it["evaluated"] / max(1, it["steps"])), "ms_per_step": round(it["ms"] / max(1, it["steps"]), 4),
             "steps": it["steps"], "tflops": round(28672 * it["evaluated"] / (it["ms"] * 1e-3) / 1e12, 1),
-            "note": "the step's own k_nerf_infer launches (progressive rounds), hipEvents around each, timed over the steps after the timed region"}
+            "note": "the step's own k_nerf_infer launches (progressive rounds), each launched with start/stop hipEvents (hipExtLaunchKernelGGL), timed over the steps after the timed region"}
 
 
 def kernel_rooflines(tb, levels, iters=9):

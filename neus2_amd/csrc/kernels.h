@@ -327,6 +327,9 @@ extern thread_local uint32_t g_dbg_lds_fill;
 // Placement test hook (neus_debug_set_xcd_shift): a one-wave kernel of this many workgroups before each kernel of the
 // step shifts the round-robin workgroup -> XCD placement of the next launch (results must not depend on it)
 extern thread_local uint32_t g_dbg_xcd_shift;
+// inference timing (testbed.cpp it_arm): when set, the next launch_nerf_infer launch records these two events at its
+// kernel's start and end (hipExtLaunchKernelGGL), then clears them
+extern thread_local hipEvent_t g_infer_ev[2];
 void debug_denorm_probe(hipStream_t s, uint32_t n, uint32_t launches, uint64_t* stats);
 void launch_xcd_shift(hipStream_t s, uint32_t n_blocks);
 inline void dbg_lds_gate(hipStream_t s) {

@@ -21,6 +21,7 @@
 //   backward     nerf_network.h:330-601, FullyFusedMLP::backward_backward_input (:1088-1198)
 // Storage rounding points (fp16) follow the reference: hidden activations, deltas, the
 // density output, dSDF/d(input), the network output and dL/doutput.
+#include <hip/hip_ext.h>
 #include "kernels.h"
 #include "scan_lookback.h"
 #include "grid_common.h"
@@ -1702,19 +1703,27 @@ void launch_nerf_infer(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_
 	const bool all = pipe && valid_level + 1 >= L;
 	auto xg = [&](uint32_t b) { return a.xcd_parts ? std::max(8u, b & ~7u) : b; };
 	dbg_lds_gate(s);
+	const hipEvent_t ev0 = g_infer_ev[0], ev1 = g_infer_ev[1];
+	g_infer_ev[0] = g_infer_ev[1] = nullptr;
+	// (with timing events: the same launch through hipExtLaunchKernelGGL, which records them at the kernel's start and end)
+	auto go = [&](auto kern, uint32_t nb, const uint32_t* ix) {
+		if (ev0) hipExtLaunchKernelGGL(kern, dim3(nb), dim3(256), 0, s, ev0, ev1, 0, n_ptr, n_fixed, coords, gl, valid_level, grid, w, out, ix, a);
+		else kern<<<nb, 256, 0, s>>>(n_ptr, n_fixed, coords, gl, valid_level, grid, w, out, ix, a);
+	};
 #define X(l, w_) if (L == l && W == w_) { \
 		static const uint32_t cap = resident_blocks((const void*)k_nerf_infer<l, w_, false>, 256); \
 		static const uint32_t cap_all = resident_blocks((const void*)k_nerf_infer<l, w_, false, true>, 256); \
 		if (all) { \
-			if (idx) k_nerf_infer<l, w_, true, true><<<xg(std::min(blocks, cap_all)), 256, 0, s>>>(n_ptr, n_fixed, coords, gl, valid_level, grid, w, out, idx, a); \
-			else k_nerf_infer<l, w_, false, true><<<xg(std::min(blocks, cap_all)), 256, 0, s>>>(n_ptr, n_fixed, coords, gl, valid_level, grid, w, out, nullptr, a); \
+			if (idx) go(k_nerf_infer<l, w_, true, true>, xg(std::min(blocks, cap_all)), idx); \
+			else go(k_nerf_infer<l, w_, false, true>, xg(std::min(blocks, cap_all)), nullptr); \
 			return; } \
-		if (idx) k_nerf_infer<l, w_, true><<<xg(std::min(blocks, cap)), 256, 0, s>>>(n_ptr, n_fixed, coords, gl, valid_level, grid, w, out, idx, a); \
-		else k_nerf_infer<l, w_, false><<<xg(std::min(blocks, cap)), 256, 0, s>>>(n_ptr, n_fixed, coords, gl, valid_level, grid, w, out, nullptr, a); \
+		if (idx) go(k_nerf_infer<l, w_, true>, xg(std::min(blocks, cap)), idx); \
+		else go(k_nerf_infer<l, w_, false>, xg(std::min(blocks, cap)), nullptr); \
 		return; }
 	NEUS_MLP_CONFIGS(X)
 #undef X
 }
+thread_local hipEvent_t g_infer_ev[2] = {nullptr, nullptr};
 void launch_nerf_density(hipStream_t s, uint32_t L, uint32_t W, uint32_t n, const float* pos, const GridLevels& gl, uint32_t valid_level,
                          const half_t* grid, const MlpPtrs& w, float* density) {
 	const uint32_t blocks = std::min<uint32_t>((n + 127) / 128, 8192);

@@ -1229,19 +1229,24 @@ struct NeusTestbed {
 		rx_open = i < N_PHASES ? i : -1;
 		if (rx_open >= 0) roctxRangePushA(names[i]);
 	}
-	// Inference timing (neus_testbed_set_infer_timing): hipEvents around every pre-compaction network launch of the step
-	// (the one pass, or each progressive round's k_nerf_infer), summed per step after the step (host waits: timing passes
-	// only, never the bench's timed region)
+	// Inference timing (neus_testbed_set_infer_timing): every pre-compaction network launch of the step (the one pass, or
+	// each progressive round's k_nerf_infer) records a pair of hipEvents at its kernel's start and end (launched through
+	// hipExtLaunchKernelGGL: events recorded between launches also counted the dispatch gap and overlapped the previous
+	// kernel's tail, 182 against the kernel trace's 146 us per launch), summed per step after the step (host waits: timing
+	// passes only, never the bench's timed region)
 	bool infer_timing = false;
 	static constexpr int IT_MAX = 16;
 	hipEvent_t it_ev[2 * IT_MAX] = {};
 	int it_n = 0;
 	double it_ms = 0.0;
 	uint64_t it_launches = 0, it_steps = 0;
-	void it_mark() {
-		if (!infer_timing || it_n >= 2 * IT_MAX) return;
-		if (!it_ev[it_n]) HIP_CHECK(hipEventCreateWithFlags(&it_ev[it_n], hipEventDisableSystemFence));
-		HIP_CHECK(hipEventRecord(it_ev[it_n++], stream));
+	void it_arm() {
+		if (!infer_timing || it_n + 2 > 2 * IT_MAX) return;
+		for (int k = 0; k < 2; ++k)
+			if (!it_ev[it_n + k]) HIP_CHECK(hipEventCreate(&it_ev[it_n + k]));
+		g_infer_ev[0] = it_ev[it_n];
+		g_infer_ev[1] = it_ev[it_n + 1];
+		it_n += 2;
 	}
 	void it_collect() {
 		if (!infer_timing || it_n < 2) { it_n = 0; return; }
@@ -1482,10 +1487,9 @@ struct NeusTestbed {
 				const uint32_t e2 = k + 2 < nch ? chunk_ends[k + 1] : 0xffffffffu;
 				// the loss's alpha terms in the inference epilogue (k_loss_alpha's work on the round's samples)
 				const InferAlpha ia{w.sa, w.ekt, lp.cos_anneal, ds.cone_angle == 0.0f ? 1u : 0u, nullptr, sorted_rays ? 8u : 0u};
-				it_mark();
+				it_arm();
 				launch_nerf_infer(s, lay.L, lay.W, chunk_cnt.p + k, 0, c_in, gl, valid, params_h.p + lay.grid_off, mlp, net_out.p, 8192, chunk_list.p,
 				                  use_delta ? nullptr : &ia);
-				it_mark();
 				if (use_delta) launch_loss_alpha_list(s, max_samples, chunk_cnt.p + k, chunk_list.p, coords.p, net_out.p, lp.cos_anneal, w, ds.cone_angle == 0.0f);
 				const bool more = k + 1 < nch;
 				launch_loss_scan_chunk(s, MAX_RAYS, numsteps.p, w, ccount.p, e0, e1, e2, more ? chunk_list.p : nullptr, chunk_cnt.p + k + 1,
@@ -1497,10 +1501,9 @@ struct NeusTestbed {
 			mark(3);
 		} else {
 			const InferAlpha ia{w.sa, w.ekt, lp.cos_anneal, ds.cone_angle == 0.0f ? 1u : 0u, w.n_long};
-			it_mark();
+			it_arm();
 			launch_nerf_infer(s, lay.L, lay.W, &st.p->n_kept, 0, c_in, gl, valid, params_h.p + lay.grid_off, mlp, net_out.p, 8192, nullptr,
 			                  use_delta ? nullptr : &ia);
-			it_mark();
 			mark(3);
 			if (use_delta) launch_loss_alpha(s, max_samples, st.p, coords.p, net_out.p, lp.cos_anneal, w, ds.cone_angle == 0.0f);
 			launch_loss_scan_ray(s, MAX_RAYS, numsteps.p, w, ccount.p);
