@@ -96,6 +96,8 @@ def parse():
     # one GPU with --same-device; a bring-up / test path whose exchange runs through host memory, not a scaling number)
     p.add_argument("--dp-backend", choices=("rccl", "host"), default="rccl")
     p.add_argument("--same-device", type=int, default=0, help="every rank on GPU 0 (with --dp-backend host)")
+    p.add_argument("--rccl-info", type=int, default=1, help="N > 1 over RCCL: record RCCL's setup and algorithm / protocol "
+                                                            "choices (NCCL_DEBUG=INFO into a file) in the bench line")
     return p.parse_args()
 
 
@@ -126,7 +128,8 @@ def kernel_table(levels):
         "mlp_train_rgb": (9, 32, 43008),
         "mlp_train_density": (10, 32, 10240),
         "grid_scatter": (7, 2 * g, 0),
-        # Adam + EMA over every parameter: 48 B; the replay advances the optimizer (after the timed steps)
+        # Adam + EMA: 14 B per parameter + 34 B per stepped parameter (adam_bytes); the replay advances the optimizer
+        # (after the timed steps)
         "adam_ema": (12, 48, 0),
     }
 
@@ -149,37 +152,54 @@ def step_inference(it, levels):
             "note": "the step's own k_nerf_infer launches (progressive rounds), each launched with start/stop hipEvents (hipExtLaunchKernelGGL), timed over the steps after the timed region"}
 
 
+def adam_bytes(tb):
+    """The bytes the reference's optimizer step moves over the last step's gradient (adam.h:51-160 + ema.h:45-110):
+    every parameter reads its fp16 gradient (2 B) and takes the EMA step (fp16 weight read, fp32 EMA read + write, fp16
+    EMA write: 12 B); a parameter that steps (every matrix weight; the others only with a nonzero gradient, adam.h:
+    107-110) also reads and writes its fp32 master weight, both moments and its step count and writes its fp16 weight
+    (34 B): 14 P + 34 P_stepped. Returns (bytes, P, P_stepped)."""
+    import numpy as np
+    g = tb.get_gradients()
+    n_matrix = tb.layout()["n_matrix"]
+    stepped = n_matrix + int(np.count_nonzero(g[n_matrix:]))
+    return 14 * g.size + 34 * stepped, int(g.size), stepped
+
+
 def kernel_rooflines(tb, levels, iters=9):
     """Per-kernel median launch duration (hipEvents on the testbed stream between `iters` back-to-back
     launches replayed on the final training state, neus_testbed_time_kernel) and the algorithmic HBM
     roofline of each launch with `levels` active hash-grid levels."""
     out = {}
+    ab = adam_bytes(tb)  # (the gradient the Adam replays run on)
     for name, (kid, bpu, fpu) in kernel_table(levels).items():
         ms, units = tb.time_kernel(kid, iters)
-        b = bpu * units
+        b = bpu * units if name != "adam_ema" else ab[0]
         r = {"ms": round(ms, 4), "units": units, "bytes": b, "achieved": round(b / (ms * 1e-3) / 1e9, 1), "unit": "GB/s",
              "frac": round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
         if fpu:
             r["tflops"] = round(fpu * units / (ms * 1e-3) / 1e12, 1)
             r["mfma_frac"] = round(r["tflops"] / MFMA_PEAK_TFLOPS, 4)
         if name == "adam_ema":
-            r["note"] = ("bytes: the reference's 48 B per parameter (SURVEY §8(d)); the kernel reads and writes the fp32 weight, moments "
-                         "and step count only for groups with a nonzero gradient, so it moves fewer and frac can exceed 1")
+            r["params_stepped"] = ab[2]
+            r["note"] = ("bytes: what the reference's adam_step + Ema move for this gradient: 14 B per parameter (fp16 gradient "
+                         "read and early-out, EMA step) + 34 B per stepped parameter (fp32 master weight, moments, step count, "
+                         "fp16 weight); a parameter steps when it is a matrix weight or its gradient is nonzero (adam.h:107-110)")
         out[name] = r
     return out
 
 
-def step_roofline(d, levels, n_params, ms_per_step, steps):
+def step_roofline(d, levels, n_params, ms_per_step, steps, adam_b=None):
     """Whole-step roofline: B_step = 40 R + 28 Npre + 568 Nev + 1496 Nc + 48 P + B_occ,
     with the gather terms at L_active levels, from the counters of the timed steps (this rank): every kept sample's
     coordinates are written (28 B), the pre-compaction network pass reads, gathers and writes only the samples it
     evaluates (Nev <= Npre: progressive inference skips samples past the transmittance cut-off) and the loss reads their
     outputs (28 + 32 L + 32 + 60 B). B_occ = (96 + 32 L) bytes per occupancy sample + a 32 MB grid pass per update.
+    The optimizer term is adam_bytes of the last step (14 P + 34 P_stepped), or the upper bound 48 P without it.
     F_step = 28,672 Nev + 92,160 Nc."""
     g = 8 * levels * 4
     R, npre, nev, nc = d["rays"] / steps, d["pre"] / steps, d["evaluated"] / steps, d["train"] / steps
     occ = (d["occ_samples"] * (96 + g) + d["occ_updates"] * 32e6) / steps
-    b = 40 * R + 28 * npre + (28 + g + 32 + 60) * nev + (60 + 28 + g + 32 + 32 + 2 * g) * nc + 48 * n_params + occ
+    b = 40 * R + 28 * npre + (28 + g + 32 + 60) * nev + (60 + 28 + g + 32 + 32 + 2 * g) * nc + (adam_b or 48 * n_params) + occ
     f = 28672 * nev + 92160 * nc
     t = ms_per_step * 1e-3
     return {"bound": "hbm", "achieved": round(b / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -207,6 +227,44 @@ def launch_ranks(n):
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     return subprocess.call(cmd, env=env)
+
+
+RCCL_LOG = "/tmp/neus_bench_rccl.%h.%p.log"
+
+
+def rccl_env(args, world):
+    """RCCL's own report of its setup (NCCL_DEBUG=INFO, subsystems INIT / GRAPH / TUNING) into a per-process file, read
+    back by rccl_info; never to stdout, which carries the bench line. Set before the communicator exists; a caller's own
+    NCCL_DEBUG wins."""
+    if world > 1 and args.dp_backend == "rccl" and args.rccl_info and "NCCL_DEBUG" not in os.environ:
+        os.environ.update(NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="INIT,GRAPH,TUNING", NCCL_DEBUG_FILE=RCCL_LOG)
+        return True
+    return False
+
+
+def rccl_info(args, rank):
+    """What RCCL reported about this rank's communicator (rccl_env): the channel / ring / tree setup lines of init and
+    the algorithm / protocol it chose per message size (its TUNING lines), summarised; {} without a log."""
+    import glob
+    import re
+    if os.environ.get("NCCL_DEBUG_FILE") != RCCL_LOG:
+        return {}
+    try:
+        paths = [p for p in glob.glob(RCCL_LOG.replace("%h", "*").replace("%p", str(os.getpid())))]
+        if not paths:
+            return {"rccl_log": "missing"}
+        init, choices = [], {}
+        with open(paths[0], errors="replace") as f:
+            for line in f:
+                m = re.search(r"(\d+) Bytes -> Algo (\w+) proto (\w+)", line)
+                if m:
+                    choices.setdefault(f"algo {m.group(2)} proto {m.group(3)}", []).append(int(m.group(1)))
+                elif len(init) < 24 and re.search(r"Init COMPLETE|nchannels|Channel 00|Trees|Pattern|NCCL_ALGO|NCCL_PROTO|Using", line):
+                    init.append(line.strip()[-160:])
+        return {"rccl": {"rank": rank, "init": init,
+                         "choices": {k: {"calls": len(v), "min_bytes": min(v), "max_bytes": max(v)} for k, v in choices.items()}}}
+    except Exception as e:  # the report is informational: never fail the bench over it
+        return {"rccl_log_error": repr(e)[:200]}
 
 
 class Group:
@@ -241,9 +299,9 @@ class Group:
         import torch.distributed as dist
         from neus2_amd import pyngp
         if self.backend == "host":
-            obj = [free_port() if self.rank == 0 else None]
+            obj = [(free_port(), int.from_bytes(os.urandom(8), "little")) if self.rank == 0 else None]
             dist.broadcast_object_list(obj, src=0)
-            g = pyngp.HostGroup(self.rank, self.world, "127.0.0.1", obj[0])
+            g = pyngp.HostGroup(self.rank, self.world, "127.0.0.1", obj[0][0], token=obj[0][1])
             g.join(tb)
             self.hgroups.append(g)
             return
@@ -283,6 +341,8 @@ def timed_steps(tb, grp, warmup, steps, batch):
     tb.train_steps(warmup)
     barrier()
     st0 = tb.stats()
+    if grp.world > 1:  # per step: the join before Adam waiting for the collectives (events, no host wait per step)
+        tb.set_exchange_timing(True)
     t1 = time.perf_counter()
     tb.train_steps(steps)
     barrier()
@@ -290,6 +350,17 @@ def timed_steps(tb, grp, warmup, steps, batch):
     st1 = tb.stats()
     w0, w1 = work_counters(st0), work_counters(st1)
     d = {k: w1[k] - w0[k] for k in w0}
+    if grp.world > 1:
+        x = tb.exchange_timing()
+        tb.set_exchange_timing(False)
+        info = tb.data_parallel_info()
+        k = max(1, x["steps"])
+        d["exchange"] = {"exposed_us_per_step": round(grp.max(x["exposed_ms"] / k) * 1e3, 1),
+                         "span_us_per_step": round(grp.max(x["span_ms"] / k) * 1e3, 1), "steps": x["steps"],
+                         "allreduce_bytes_last_step": int(info["last_step_allreduce_bytes"]),
+                         "note": "exposed = max over ranks of the mean per-step wait of the join before Adam for the "
+                                 "collectives (end of the last collective - end of the backward, hipEvents); span = end of "
+                                 "the last collective - end of the loss (the counters' all-reduce starts there)"}
     d["train"] = steps * batch
     d["trained_real"] = st1["trained_samples_total"] - st0["trained_samples_total"]
     return elapsed, d, st1
@@ -311,6 +382,7 @@ def main():
             print("bench.py: --same-device needs --dp-backend host (RCCL refuses two ranks on one GPU)", file=sys.stderr)
             sys.exit(2)
         local = 0
+    rccl_env(args, world)
     import torch
     grp = Group(rank, world, args.dp_backend)
     torch.cuda.set_device(local)
@@ -370,7 +442,7 @@ def main():
                      **({k: inf[k] for k in ("launches_per_step", "evaluated_per_step", "ms_per_step", "steps", "note")}
                         if dom == "inference_step" else {})},
         # the whole step against the HBM roofline and its MFMA rate
-        "roofline_step": step_roofline(d, levels, lay["n_params"], ms_step, args.steps),
+        "roofline_step": step_roofline(d, levels, lay["n_params"], ms_step, args.steps, kern["adam_ema"]["bytes"]),
         # the training MLP kernels (fwd recompute + 1st / 2nd-order backward + weight gradients) against the MFMA peak
         "mfma_mlp_train": {"flops_per_sample": 43008 + 10240 + 28672, "ms": round(mlp_ms, 4),
                            "tflops": round((43008 + 10240 + 28672) * batch / (mlp_ms * 1e-3) / 1e12, 1),
@@ -381,6 +453,7 @@ def main():
         "progressive_steps_timed": d["progressive"],
         "progressive_chunk_end": st["progressive_chunk_end"],
         "non_rollover_fraction": round(d["trained_real"] / max(1, batch * args.steps), 4),
+        **({"exchange": {**d["exchange"], **rccl_info(args, rank)}} if "exchange" in d else {}),
         "kernels": kern,
         "loss": st["ray_loss"],
         "prepare_s": round(prepare_s, 3),

@@ -129,6 +129,8 @@ typedef struct NeusTrainStats {
 	uint32_t evaluated_samples_last;          /* samples the last step's pre-compaction pass evaluated */
 	uint32_t progressive_chunk_end;           /* end of the progressive inference's first chunk (the rounds are [0, e), [e, 2e), ...
 	                                           * by default; neus_testbed_set_progressive_inference) */
+	uint64_t lookahead_steps;                 /* (ABI 5) steps whose ray sampling was issued beside the step before them */
+	uint64_t adam_split_steps;                /* (ABI 5) steps whose optimizer ran in pieces beside the scatter (adam_overlap) */
 } NeusTrainStats;
 
 /* Testbed::render_to_cpu (python_api.cu:123-169) after set_camera_to_training_view (testbed.cu:264-270). */
@@ -153,9 +155,10 @@ typedef struct NeusNetLayout {
 
 /* ABI version of this header (bumped on any incompatible signature or struct change; version 2: neus_module_create_network
  * became tcnn's create_network(n_input_dims, n_output_dims, network), the NerfNetwork factory neus_module_create_nerf_network;
- * version 3: NeusDataParallelInfo gained host_group; version 4: neus_module_create_encoding gained requested_precision).
+ * version 3: NeusDataParallelInfo gained host_group; version 4: neus_module_create_encoding gained requested_precision;
+ * version 5: neus_testbed_{set_,}exchange_timing, neus_host_group_create gained job_token).
  * Bindings compare it on load so that a stale library or binding fails loudly instead of misreading arguments. */
-#define NEUS_ABI_VERSION 4u
+#define NEUS_ABI_VERSION 5u
 int neus_abi_version(uint32_t* out);
 const char* neus_last_error(void);
 int neus_device_count(int* count);
@@ -273,7 +276,11 @@ int neus_testbed_get_training_options(NeusTestbed* tb, NeusTrainingOptions* out)
 /* Trainer::serialize(include_optimizer_state) / deserialize (trainer.h:281-305): the Ema(ExponentialDecay(Adam))
  * state - Adam current_step, first / second moments, per-parameter steps (adam.h:424-445), the decay's learning
  * rate and factor (exponential_decay.h:128-140), the fp16 EMA weights (ema.h:182-194; the fp32 accumulator is
- * rebuilt from them on set). Arrays are n_params long, host memory, nullable on get; steps nullable on set. */
+ * rebuilt from them on set). Arrays are n_params long, host memory, nullable on get; steps nullable on set.
+ * Per-parameter steps (uint32 in the reference): when the betas' bias correction has converged to 1.0f by step 4096
+ * (beta^4095 < 2^-30: the default betas 0.9 / 0.99), the device keeps them in 16 bits and they saturate at 65535 - every
+ * count past 4095 gives the same update, so training is unchanged, but a count above 65535 reads back as 65535. With
+ * betas whose correction has not converged there, they are kept in 32 bits and round-trip exactly. */
 typedef struct NeusOptimizerState {
 	uint32_t n_params;
 	uint32_t current_step;
@@ -376,6 +383,13 @@ int neus_testbed_kernel_times(NeusTestbed* tb, float* ms_out /* NEUS_N_PHASES + 
  * ms, launches, steps; the samples those launches evaluated are NeusTrainStats::evaluated_samples_total's growth. */
 int neus_testbed_set_infer_timing(NeusTestbed* tb, int on);
 int neus_testbed_infer_timing(NeusTestbed* tb, double* ms_total, uint64_t* launches, uint64_t* steps);
+/* Exchange timing of the data-parallel step (ABI 5; no effect without collectives): per step, hipEvents where the
+ * backward is done on the step's stream and where the last collective ends on the exchange stream. Totals since it was
+ * turned on: exposed_ms = sum of max(0, exchange end - backward end), the time the join before the optimizer waits;
+ * span_ms = sum of (exchange end - loss end), the exchange's whole window (the counters' all-reduce starts after the
+ * loss); steps. Collected without a per-step host wait, so it may run inside a timed region. */
+int neus_testbed_set_exchange_timing(NeusTestbed* tb, int on);
+int neus_testbed_exchange_timing(NeusTestbed* tb, double* exposed_ms_total, double* span_ms_total, uint64_t* steps);
 
 /* ------------------------------------------------------------------ data parallel (RCCL over xGMI) */
 int neus_nccl_unique_id(uint8_t* out /* 128 bytes */);
@@ -411,9 +425,12 @@ int neus_testbed_init_local_group(NeusTestbed* tb, NeusLocalGroup* group, int ra
  * Each collective is staged on the testbed's communication stream (device -> pinned host, a host function for the
  * exchange, host -> device), gated by the same events as the RCCL collectives, so the overlapped exchange runs beside the
  * backward. Every rank creates its group (rank 0 listens, the others connect; 120 s timeouts) and attaches its testbed;
- * the ranks must issue the same collectives (a mismatch fails loudly). The group must outlive its testbed's training. */
+ * the ranks must issue the same collectives (a mismatch fails loudly). The group must outlive its testbed's training.
+ * job_token (ABI 5): a per-job value every rank passes alike (e.g. random, broadcast by the launcher with the port); rank 0
+ * drops connections whose hello carries another token or an already-joined rank and keeps waiting. It keeps stray and
+ * foreign processes out, it does not authenticate: keep host at 127.0.0.1 unless the port's network is trusted. */
 typedef struct NeusHostGroup NeusHostGroup;
-int neus_host_group_create(int rank, int world, const char* host, int port, NeusHostGroup** out);
+int neus_host_group_create(int rank, int world, const char* host, int port, uint64_t job_token, NeusHostGroup** out);
 int neus_host_group_destroy(NeusHostGroup* group);
 int neus_testbed_init_host_group(NeusTestbed* tb, NeusHostGroup* group);
 /* Test hook (no GPU): one collective of the group's protocol on a host buffer of n 4-byte elements, type 0 f32 / 1 u32,

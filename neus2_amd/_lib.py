@@ -48,7 +48,7 @@ class NeusTrainStats(C.Structure):
         ("training_aborted", C.c_uint32), ("pre_samples_total", C.c_uint64), ("rays_total", C.c_uint64),
         ("occ_samples_total", C.c_uint64), ("occ_updates", C.c_uint32), ("health_flags", C.c_uint32),
         ("evaluated_samples_total", C.c_uint64), ("progressive_steps", C.c_uint64), ("evaluated_samples_last", C.c_uint32),
-        ("progressive_chunk_end", C.c_uint32),
+        ("progressive_chunk_end", C.c_uint32), ("lookahead_steps", C.c_uint64), ("adam_split_steps", C.c_uint64),
     ]
 
 
@@ -114,6 +114,7 @@ EXPORTS = [
     "neus_testbed_get_density_grid", "neus_testbed_set_density_grid", "neus_testbed_restore_state", "neus_testbed_get_rng", "neus_testbed_render", "neus_testbed_sdf_on_grid",
     "neus_testbed_marching_cubes", "neus_testbed_mc_density", "neus_testbed_get_mesh", "neus_testbed_mesh_vertex_colors", "neus_mc_table", "neus_prepare_image_rgba8", "neus_testbed_ray_counts", "neus_debug_time_kernel", "neus_debug_march_stats", "neus_debug_exclusive_scan", "neus_debug_scan_giveup", "neus_debug_inject_health", "neus_debug_set_lds_fill", "neus_debug_set_lds_fill_all", "neus_debug_set_xcd_shift", "neus_debug_denorm_probe", "neus_debug_get_batch", "neus_debug_get_buffer", "neus_debug_replay_loss_grad", "neus_debug_sample_rays_round0", "neus_debug_march_profile", "neus_debug_scatter_stats", "neus_debug_scatter_parts", "neus_testbed_time_kernel", "neus_testbed_stream",
     "neus_testbed_synchronize", "neus_testbed_set_profiling", "neus_testbed_kernel_times", "neus_testbed_set_infer_timing", "neus_testbed_infer_timing",
+    "neus_testbed_set_exchange_timing", "neus_testbed_exchange_timing",
     "neus_nccl_unique_id", "neus_testbed_init_data_parallel", "neus_testbed_init_data_parallel_ex",
     "neus_testbed_data_parallel_info", "neus_testbed_set_exchange_overlap", "neus_local_group_create", "neus_local_group_destroy",
     "neus_testbed_init_local_group", "neus_host_group_create", "neus_host_group_destroy", "neus_testbed_init_host_group", "neus_debug_host_group_allreduce",
@@ -131,7 +132,7 @@ EXPORTS = [
 ]
 
 # include/neus2_hip.h's NEUS_ABI_VERSION this binding was written against: a library of another ABI fails to load
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _lib = None
 

@@ -170,7 +170,12 @@ struct StepState {
 	uint32_t fail_flags;              // device health: STEP_FAIL_* bits (sticky; the host raises on the next readback)
 	uint32_t eval_last;               // samples evaluated by the last step's pre-compaction pass
 	unsigned long long prog_steps;    // steps that ran progressive (multi-round) inference
-	unsigned long long pad_[3];
+	// the step's compacted count and rays with samples summed over the ranks (k_loss_ray writes this rank's; the data-
+	// parallel exchange all-reduces the pair right after the loss, so compacted_counter stays this rank's training batch
+	// for the backward while the counters update and the next step's sampling can start before the backward ends)
+	uint32_t compacted_global;
+	uint32_t rays_ws_global;
+	unsigned long long pad_[2];
 };
 static_assert(sizeof(StepState) == 128, "StepState is one 128-B record");
 // fail_flags bits: a march step saw a non-finite or negative t (step_until's precondition; the ray is ended there);
@@ -201,7 +206,7 @@ __device__ __forceinline__ void step_counters_update(StepState* st, uint32_t tar
 	st->march_est = fit ? 0u : (ext + 63u) / 64u * 64u;
 	// per rank: the cap on the next step's pre-compaction samples follows this rank's own request count
 	const uint32_t before = st->numsteps_counter;
-	const uint32_t measured = st->compacted_counter / world;
+	const uint32_t measured = st->compacted_global / world;
 	st->measured_before = before;
 	st->measured_batch_size = measured;
 	st->trained_total += min(measured, target_batch);  // real training samples (the rest of the batch is rollover)

@@ -3,8 +3,9 @@
 // the operator-API variant a caller asks for with requested_precision = fp32.
 //   k_grid_f32_forward : kernel_grid (grid.h:174-369) with T = float: result[f] += weight * value in fp32, dy/dx kept
 //                        for dL_dinput / second order
-//   k_grid_f32_backward: kernel_grid_backward (grid.h:371-500; float atomicAdd per feature, as GRAD_T = float) and
-//                        dL_dinput = sum_(l,f) dL_dy . dy/dx (kernel_grid_backward_input)
+//   k_grid_f32_backward: kernel_grid_backward (grid.h:371-500; float atomicAdd per feature, as GRAD_T = float)
+//   k_grid_f32_input_grad: dL_dinput = sum over the 2L features, in feature order, of dL_dy . dy/dx (kernel_grid_
+//                        backward_input, grid.h:804-830: one thread per sample, so the sum is run-to-run deterministic)
 //   k_grid_f32_bbi     : kernel_grid_backward_input_backward_grid (grid.h:880-1007) and dL_ddLdoutput = dy/dx .
 //                        dL_ddLdinput (kernel_grid_backward_input_backward_dLdoutput)
 // One thread per (sample, level) (blockIdx.y = level, as the reference's launch): a level's table stays in the XCD's L2
@@ -87,31 +88,36 @@ __global__ void __launch_bounds__(256) k_grid_f32_forward(uint32_t n, const Grid
 	}
 }
 
-// grads may be null (dL_dinput only); dL_dinput accumulates over levels with float atomics (zeroed by the host)
 __global__ void __launch_bounds__(256) k_grid_f32_backward(uint32_t n, const GridLevels gl, uint32_t valid_level, const float* __restrict__ coords,
-                                                           const float* __restrict__ dLdy, uint32_t layout, float* __restrict__ grads,
-                                                           const float* __restrict__ dydx, float* __restrict__ dLdx) {
+                                                           const float* __restrict__ dLdy, uint32_t layout, float* __restrict__ grads) {
 	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x, l = blockIdx.y, L = gl.n_levels;
 	if (i >= n || l > valid_level) return;
 	const float g0 = dLdy[enc_addr(layout, n, L, i, 2 * l)], g1 = dLdy[enc_addr(layout, n, L, i, 2 * l + 1)];
-	if (grads) {
-		const LevelSetup s = level_setup(gl, l, coords[(size_t)i * 3], coords[(size_t)i * 3 + 1], coords[(size_t)i * 3 + 2]);
-		float* gp = grads + (size_t)gl.offset[l] * 2;
+	const LevelSetup s = level_setup(gl, l, coords[(size_t)i * 3], coords[(size_t)i * 3 + 1], coords[(size_t)i * 3 + 2]);
+	float* gp = grads + (size_t)gl.offset[l] * 2;
 #pragma unroll
-		for (uint32_t idx = 0; idx < 8; ++idx) {
-			const uint32_t e = grid_index(s.hsize, s.res, s.g[0] + (idx & 1), s.g[1] + ((idx >> 1) & 1), s.g[2] + ((idx >> 2) & 1));
-			const float w = corner_weight(s, idx);
-			atomicAdd(gp + 2 * (size_t)e, w * g0);
-			atomicAdd(gp + 2 * (size_t)e + 1, w * g1);
-		}
+	for (uint32_t idx = 0; idx < 8; ++idx) {
+		const uint32_t e = grid_index(s.hsize, s.res, s.g[0] + (idx & 1), s.g[1] + ((idx >> 1) & 1), s.g[2] + ((idx >> 2) & 1));
+		const float w = corner_weight(s, idx);
+		atomicAdd(gp + 2 * (size_t)e, w * g0);
+		atomicAdd(gp + 2 * (size_t)e + 1, w * g1);
 	}
-	if (dLdx) {
+}
+
+// dL/dx[i][d] = sum over features k = 2l + f, in k order, of dL_dy[k][i] * dy_dx[k][d][i] (result[dim] += ..., nvcc
+// contracted to an FMA); the features of levels past valid_level have dy/dx = 0 (the forward wrote zeros)
+__global__ void __launch_bounds__(256) k_grid_f32_input_grad(uint32_t n, uint32_t L, const float* __restrict__ dLdy, uint32_t layout,
+                                                             const float* __restrict__ dydx, float* __restrict__ dLdx) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	float r[3] = {0.f, 0.f, 0.f};
+	for (uint32_t k = 0; k < 2 * L; ++k) {
+		const float g = dLdy[enc_addr(layout, n, L, i, k)];
 #pragma unroll
-		for (int d = 0; d < 3; ++d) {
-			const float a = g0 * dydx[(size_t)(6 * l + d) * n + i] + g1 * dydx[(size_t)(6 * l + 3 + d) * n + i];
-			atomicAdd(dLdx + (size_t)i * 3 + d, a);
-		}
+		for (int d = 0; d < 3; ++d) r[d] = __builtin_fmaf(g, dydx[(size_t)(3 * k + d) * n + i], r[d]);
 	}
+#pragma unroll
+	for (int d = 0; d < 3; ++d) dLdx[(size_t)i * 3 + d] = r[d];
 }
 
 __global__ void __launch_bounds__(256) k_grid_f32_bbi(uint32_t n, const GridLevels gl, uint32_t valid_level, const float* __restrict__ coords,
@@ -171,8 +177,9 @@ void launch_grid_f32_backward(hipStream_t s, uint32_t n, const GridLevels& gl, u
                               uint32_t layout, float* grads, const float* dydx, float* dLdx) {
 	check_layout(layout);
 	if (dLdx && !dydx) throw std::runtime_error("fp32 HashGrid backward: dL_dinput needs the forward's dy/dx");
-	if (dLdx && hipMemsetAsync(dLdx, 0, (size_t)n * 3 * sizeof(float), s) != hipSuccess) throw std::runtime_error("fp32 HashGrid backward: memset");
-	if (n) k_grid_f32_backward<<<dim3((n + 255) / 256, gl.n_levels), 256, 0, s>>>(n, gl, valid_level, coords, dLdy, layout, grads, dydx, dLdx);
+	if (!n) return;
+	if (grads) k_grid_f32_backward<<<dim3((n + 255) / 256, gl.n_levels), 256, 0, s>>>(n, gl, valid_level, coords, dLdy, layout, grads);
+	if (dLdx) k_grid_f32_input_grad<<<(n + 255) / 256, 256, 0, s>>>(n, gl.n_levels, dLdy, layout, dydx, dLdx);
 }
 void launch_grid_f32_bbi(hipStream_t s, uint32_t n, const GridLevels& gl, uint32_t valid_level, const float* coords, const float* ddx,
                          const float* dLdy, uint32_t layout, float* grads, const float* dydx, float* ddLdy) {

@@ -13,6 +13,12 @@
 // instead of pairing the wrong buffers), reduces in rank order (v0 + v1 + ... as NeusLocalGroup, so the result is bitwise
 // the in-process group's), and sends the result back. A host-function failure cannot throw through the HIP runtime: it
 // poisons the group (sockets shut down, so the peers fail too) and the next step boundary raises.
+//
+// Joining: every rank's hello carries {magic, rank, job token}. The token is a per-job 64-bit value the launcher hands
+// every rank (bench.py draws it at random on rank 0 and broadcasts it with the port); rank 0 drops a connection whose
+// hello is malformed, carries another token or names a rank already joined, and keeps waiting for the real ranks. The
+// token is a guard against stray or foreign connections, not authentication against an attacker who can read the
+// launcher's traffic: the default address is 127.0.0.1, and a non-loopback address exposes the port to its network.
 #pragma once
 
 #include <arpa/inet.h>
@@ -36,8 +42,10 @@ struct NeusHostGroup {
 	enum Op : uint32_t { SUM = 0, MAX = 1 };
 	enum Type : uint32_t { F32 = 0, U32 = 1 };
 	struct Header { uint32_t magic, op, type, pad; uint64_t seq, bytes; };
+	struct Hello { uint32_t magic; int32_t rank; uint64_t token; };
 	static constexpr uint32_t MAGIC = 0x4e484731u;  // "NHG1"
 	static constexpr int TIMEOUT_MS = 120000;
+	static constexpr int HELLO_TIMEOUT_MS = 5000;    // a connection that sends no hello this long is dropped
 
 	int rank = 0, world = 1;
 	std::vector<int> fd;           // rank 0: fd[r] = socket of rank r (r >= 1); others: fd[0] = socket of rank 0
@@ -47,7 +55,7 @@ struct NeusHostGroup {
 	std::mutex err_mu;
 	std::string err;
 
-	NeusHostGroup(int r, int w, const char* host, int port) : rank(r), world(w) {
+	NeusHostGroup(int r, int w, const char* host, int port, uint64_t token) : rank(r), world(w) {
 		if (w < 1 || r < 0 || r >= w) throw std::runtime_error("host group: invalid rank / world");
 		fd.assign(w, -1);
 		if (w == 1) return;
@@ -64,16 +72,26 @@ struct NeusHostGroup {
 				close(ls);
 				throw std::runtime_error("host group: rank 0 cannot listen on " + std::string(host) + ":" + std::to_string(port));
 			}
-			for (int k = 1; k < w; ++k) {
+			const auto t0 = std::chrono::steady_clock::now();
+			int joined = 0, dropped = 0;
+			while (joined < w - 1) {
+				const int left = TIMEOUT_MS - (int)std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
 				pollfd p{ls, POLLIN, 0};
-				if (poll(&p, 1, TIMEOUT_MS) <= 0) { close(ls); shutdown_all(); throw std::runtime_error("host group: ranks did not connect in time"); }
+				if (left <= 0 || poll(&p, 1, left) <= 0) {
+					close(ls); shutdown_all();
+					throw std::runtime_error("host group: " + std::to_string(joined) + " of " + std::to_string(w - 1) + " ranks joined in time (" +
+					                         std::to_string(dropped) + " connections dropped: wrong job token, rank or hello)");
+				}
 				const int s = accept(ls, nullptr, nullptr);
-				if (s < 0) { close(ls); shutdown_all(); throw std::runtime_error("host group: accept"); }
-				int32_t peer = -1;
-				recv_all(s, &peer, 4);
-				if (peer < 1 || peer >= w || fd[peer] >= 0) { close(s); close(ls); shutdown_all(); throw std::runtime_error("host group: bad rank hello"); }
+				if (s < 0) continue;
+				Hello hi{};
+				bool ok = true;
+				try { recv_all(s, &hi, sizeof(hi), HELLO_TIMEOUT_MS); } catch (const std::exception&) { ok = false; }
+				ok = ok && hi.magic == MAGIC && hi.token == token && hi.rank >= 1 && hi.rank < w && fd[hi.rank] < 0;
+				if (!ok) { close(s); ++dropped; continue; }
 				tune(s);
-				fd[peer] = s;
+				fd[hi.rank] = s;
+				++joined;
 			}
 			close(ls);
 		} else {
@@ -89,8 +107,8 @@ struct NeusHostGroup {
 				std::this_thread::sleep_for(std::chrono::milliseconds(20));
 			}
 			tune(s);
-			const int32_t me = r;
-			send_all(s, &me, 4);
+			const Hello me{MAGIC, r, token};
+			send_all(s, &me, sizeof(me));
 			fd[0] = s;
 		}
 	}
@@ -114,11 +132,11 @@ struct NeusHostGroup {
 			b += k; n -= (size_t)k;
 		}
 	}
-	static void recv_all(int s, void* p, size_t n) {
+	static void recv_all(int s, void* p, size_t n, int timeout_ms = TIMEOUT_MS) {
 		uint8_t* b = (uint8_t*)p;
 		while (n) {
 			pollfd q{s, POLLIN, 0};
-			if (poll(&q, 1, TIMEOUT_MS) <= 0) throw std::runtime_error("host group: receive timeout (a rank did not reach the collective)");
+			if (poll(&q, 1, timeout_ms) <= 0) throw std::runtime_error("host group: receive timeout (a rank did not reach the collective)");
 			const ssize_t k = ::recv(s, b, n, 0);
 			if (k <= 0) throw std::runtime_error("host group: peer closed (receive)");
 			b += k; n -= (size_t)k;

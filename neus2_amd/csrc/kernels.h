@@ -409,8 +409,12 @@ void launch_exclusive_scan(hipStream_t s, void* temp, size_t temp_bytes, const u
 void launch_sum_f32(hipStream_t s, void* temp, size_t temp_bytes, const float* in, float* out, uint32_t n);
 // optim.hip
 void launch_adam_ema(hipStream_t s, const AdamParams& p, float* weights_fp, half_t* weights_h, const float* grads, float* m1, float* m2,
-                     uint16_t* steps, float* ema_tmp, half_t* ema_h,
+                     void* steps, bool steps32, float* ema_tmp, half_t* ema_h,
                      const StepCounterArgs* counters = nullptr, const AdamTranspose* tr = nullptr);
+// Ema(Adam) over the parameters [lo, hi) of a p.n-parameter vector (lo % 4 == 0): the optimizer step in pieces, each as
+// soon as its gradient range is final (NeusTestbed::adam_overlap); no step counters on these launches
+void launch_adam_ema_range(hipStream_t s, AdamParams p, uint32_t lo, uint32_t hi, float* weights_fp, half_t* weights_h, const float* grads,
+                           float* m1, float* m2, void* steps, bool steps32, float* ema_tmp, half_t* ema_h, const AdamTranspose* tr);
 void launch_cast_half(hipStream_t s, uint32_t n, const float* in, half_t* out);
 void launch_add_f32(hipStream_t s, uint32_t n, const float* src, float* dst);
 // operator-module encoding helpers (grid.hip)

@@ -1348,10 +1348,11 @@ __global__ void __launch_bounds__(64) SCAN_OCC k_loss_scan_chunk(uint32_t cap_ra
 	}
 }
 
-// One thread per ray; cap_rays % 64 == 0, so a wave's lanes run the grid-stride loop together and fill the sample ->
-// ray map of their 64 consecutive rays cooperatively at the end of each iteration: each ray's range is written by
-// consecutive lanes (coalesced stores) instead of every lane storing its own range one element per instruction (64
-// scattered lines per store).
+// One thread per ray. The grid-stride loop runs to cap_rays rounded up to 64, so a wave's lanes run it together and
+// fill the sample -> ray map of their 64 consecutive rays cooperatively at the end of each iteration: each ray's range
+// is written by consecutive lanes (coalesced stores) instead of every lane storing its own range one element per
+// instruction (64 scattered lines per store). Lanes past cap_rays (any ray count: neus_loss_compact takes 1..2^18)
+// take part in the fill with an empty range.
 __global__ void __launch_bounds__(256) k_loss_ray(uint32_t cap_rays, StepState* __restrict__ st, DPInfo dp, DevDataset ds, LossParams lp,
                                                   uint32_t* __restrict__ numsteps, const uint32_t* __restrict__ ccount,
                                                   const uint32_t* __restrict__ cbase, const float4* __restrict__ sa, const float* __restrict__ ekt,
@@ -1362,73 +1363,79 @@ __global__ void __launch_bounds__(256) k_loss_ray(uint32_t cap_rays, StepState* 
 	const uint32_t lane = threadIdx.x & 63;
 	const uint32_t R = st->rays_per_batch;
 	const uint32_t n_rays_global = R * dp.world, n_rays_total = st->n_rays_total;
-	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cap_rays; i += gridDim.x * blockDim.x) {
-		const uint32_t ns = numsteps[2 * i], base = numsteps[2 * i + 1];
-		const uint32_t cn = ccount[i], cb = cbase[i];
-		if (i == cap_rays - 1) {
-			st->compacted_counter = cb + cn;
-			st->n_train = min(cb + cn, lp.max_compacted) ? lp.max_compacted : 0u;  // the training batch (k_rollover sets it too)
-		}
-		loss_out[i] = 0.f; ek_out[i] = 0.f; mask_out[i] = 0.f;
-		uint32_t comp = 0;
-		if (ns == 0) {
-			numsteps[2 * i] = 0; numsteps[2 * i + 1] = cb;
-		} else {
-			const float4 acc = racc[i];
-			float rgb_ray[3] = {acc.x, acc.y, acc.z}, weight_sum = acc.w;
-			const float T = rT[i];
-			// target pixel and background (same RNG stream as the sampler; testbed_nerf.cu:1632-1660)
-			const uint32_t ig = dp.rank * R + i;
-			pcg32 rng(lp.rng_state, lp.rng_inc);
-			pcg_advance(rng, (uint64_t)(uint32_t)(ig * N_MAX_RANDOM_SAMPLES_PER_RAY), lp.jt);
-			const uint32_t img = image_idx(ig, n_rays_global, n_rays_total, ds.n_images);
-			const int rx = ds.res[2 * img], ry = ds.res[2 * img + 1];
-			float xx, yy; random_image_pos(rng, rx, ry, xx, yy);
-			float bg[3];
-			if (ds.target.fixed_bg) { bg[0] = ds.target.bg[0]; bg[1] = ds.target.bg[1]; bg[2] = ds.target.bg[2]; }
-			else { bg[0] = rng.next_float(); bg[1] = rng.next_float(); bg[2] = rng.next_float(); }
-#pragma unroll
-			for (int k = 0; k < 3; ++k) bg[k] = srgb_to_linear(bg[k]);
-			float tex[4]; read_rgba(ds, img, xx, yy, tex);
-			float target[3];
-			const uint32_t tmode = ds.target.mode;
-#pragma unroll
-			for (int k = 0; k < 3; ++k) {
-				if (tmode != 1) {  // Linear colour space (sRGB targets unless linear_colors) (:1658-1663)
-					target[k] = 1.0f * tex[k] + (1.0f - tex[3]) * bg[k];
-					if (tmode == 0) { target[k] = linear_to_srgb(target[k]); bg[k] = linear_to_srgb(bg[k]); }
-				} else {           // SRGB colour space (:1664-1670)
-					bg[k] = linear_to_srgb(bg[k]);
-					target[k] = tex[3] > 0.0f ? linear_to_srgb(1.0f * tex[k] / tex[3]) * tex[3] + (1.0f - tex[3]) * bg[k] : bg[k];
-				}
+	const uint32_t cap64 = (cap_rays + 63u) & ~63u;
+	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cap64; i += gridDim.x * blockDim.x) {
+		uint32_t comp = 0, cb = 0;
+		if (i < cap_rays) {
+			const uint32_t ns = numsteps[2 * i], base = numsteps[2 * i + 1];
+			const uint32_t cn = ccount[i];
+			cb = cbase[i];
+			if (i == cap_rays - 1) {
+				st->compacted_counter = cb + cn;
+				st->compacted_global = cb + cn;                     // (all-reduced by the data-parallel exchange)
+				st->rays_ws_global = st->n_rays_with_samples;
+				st->n_train = min(cb + cn, lp.max_compacted) ? lp.max_compacted : 0u;  // the training batch (k_rollover sets it too)
 			}
-			if (cn == ns) {
-#pragma unroll
-				for (int k = 0; k < 3; ++k) rgb_ray[k] += T * bg[k];
-			}
-			comp = min(lp.max_compacted - min(lp.max_compacted, cb), cn);
-			numsteps[2 * i] = comp; numsteps[2 * i + 1] = cb;
-			if (comp > 0) {
-				float lgrad[3], lloss[3];
-#pragma unroll
+			loss_out[i] = 0.f; ek_out[i] = 0.f; mask_out[i] = 0.f;
+			if (ns == 0) {
+				numsteps[2 * i] = 0; numsteps[2 * i + 1] = cb;
+			} else {
+				const float4 acc = racc[i];
+				float rgb_ray[3] = {acc.x, acc.y, acc.z}, weight_sum = acc.w;
+				const float T = rT[i];
+				// target pixel and background (same RNG stream as the sampler; testbed_nerf.cu:1632-1660)
+				const uint32_t ig = dp.rank * R + i;
+				pcg32 rng(lp.rng_state, lp.rng_inc);
+				pcg_advance(rng, (uint64_t)(uint32_t)(ig * N_MAX_RANDOM_SAMPLES_PER_RAY), lp.jt);
+				const uint32_t img = image_idx(ig, n_rays_global, n_rays_total, ds.n_images);
+				const int rx = ds.res[2 * img], ry = ds.res[2 * img + 1];
+				float xx, yy; random_image_pos(rng, rx, ry, xx, yy);
+				float bg[3];
+				if (ds.target.fixed_bg) { bg[0] = ds.target.bg[0]; bg[1] = ds.target.bg[1]; bg[2] = ds.target.bg[2]; }
+				else { bg[0] = rng.next_float(); bg[1] = rng.next_float(); bg[2] = rng.next_float(); }
+	#pragma unroll
+				for (int k = 0; k < 3; ++k) bg[k] = srgb_to_linear(bg[k]);
+				float tex[4]; read_rgba(ds, img, xx, yy, tex);
+				float target[3];
+				const uint32_t tmode = ds.target.mode;
+	#pragma unroll
 				for (int k = 0; k < 3; ++k) {
-					const float diff = rgb_ray[k] - target[k], ad = fabsf(diff), sq = 0.5f / 0.1f * diff * diff;
-					lloss[k] = (ad > 0.1f ? (ad - 0.5f * 0.1f) : sq) / 5.0f;
-					lgrad[k] = (ad > 0.1f ? (diff > 0 ? 1.0f : -1.0f) : (diff / 0.1f)) / 5.0f;
+					if (tmode != 1) {  // Linear colour space (sRGB targets unless linear_colors) (:1658-1663)
+						target[k] = 1.0f * tex[k] + (1.0f - tex[3]) * bg[k];
+						if (tmode == 0) { target[k] = linear_to_srgb(target[k]); bg[k] = linear_to_srgb(bg[k]); }
+					} else {           // SRGB colour space (:1664-1670)
+						bg[k] = linear_to_srgb(bg[k]);
+						target[k] = tex[3] > 0.0f ? linear_to_srgb(1.0f * tex[k] / tex[3]) * tex[3] + (1.0f - tex[3]) * bg[k] : bg[k];
+					}
 				}
-				const float mask_gt = (float)(tex[3] > 0.9999f);
-				float gws;
-				if (weight_sum >= 1.0 - 1e-4) { weight_sum = 1.0 - 1e-4; gws = 0.0f; }
-				else if (weight_sum <= 1e-4) { weight_sum = 1e-4; gws = 0.0f; }
-				else { const float sws = 1.0f / (1.0f + exp(-(double)weight_sum)); gws = (mask_gt - sws) * weight_sum * lp.mask_w; }
-				const float mean_loss = ((lloss[0] + lloss[1]) + lloss[2]) / 3.0f;
-				loss_out[i] = mean_loss / (float)n_rays_global;
-				mask_out[i] = -(mask_gt * logf(weight_sum) + (1 - mask_gt) * logf(1 - weight_sum));
-				float Tb;
-				const RecState sc = scan_replay(base, base + comp - 1, sa, ekt, ck4, cke, Tb);
-				ek_out[i] = sc.ek / ((float)comp * (float)n_rays_global);
-				rgr[i] = make_float4(lgrad[0], lgrad[1], lgrad[2], gws * (1 - weight_sum));
-				racc[i] = make_float4(rgb_ray[0], rgb_ray[1], rgb_ray[2], 0.f);
+				if (cn == ns) {
+	#pragma unroll
+					for (int k = 0; k < 3; ++k) rgb_ray[k] += T * bg[k];
+				}
+				comp = min(lp.max_compacted - min(lp.max_compacted, cb), cn);
+				numsteps[2 * i] = comp; numsteps[2 * i + 1] = cb;
+				if (comp > 0) {
+					float lgrad[3], lloss[3];
+	#pragma unroll
+					for (int k = 0; k < 3; ++k) {
+						const float diff = rgb_ray[k] - target[k], ad = fabsf(diff), sq = 0.5f / 0.1f * diff * diff;
+						lloss[k] = (ad > 0.1f ? (ad - 0.5f * 0.1f) : sq) / 5.0f;
+						lgrad[k] = (ad > 0.1f ? (diff > 0 ? 1.0f : -1.0f) : (diff / 0.1f)) / 5.0f;
+					}
+					const float mask_gt = (float)(tex[3] > 0.9999f);
+					float gws;
+					if (weight_sum >= 1.0 - 1e-4) { weight_sum = 1.0 - 1e-4; gws = 0.0f; }
+					else if (weight_sum <= 1e-4) { weight_sum = 1e-4; gws = 0.0f; }
+					else { const float sws = 1.0f / (1.0f + exp(-(double)weight_sum)); gws = (mask_gt - sws) * weight_sum * lp.mask_w; }
+					const float mean_loss = ((lloss[0] + lloss[1]) + lloss[2]) / 3.0f;
+					loss_out[i] = mean_loss / (float)n_rays_global;
+					mask_out[i] = -(mask_gt * logf(weight_sum) + (1 - mask_gt) * logf(1 - weight_sum));
+					float Tb;
+					const RecState sc = scan_replay(base, base + comp - 1, sa, ekt, ck4, cke, Tb);
+					ek_out[i] = sc.ek / ((float)comp * (float)n_rays_global);
+					rgr[i] = make_float4(lgrad[0], lgrad[1], lgrad[2], gws * (1 - weight_sum));
+					racc[i] = make_float4(rgb_ray[0], rgb_ray[1], rgb_ray[2], 0.f);
+				}
 			}
 		}
 		// cmap[cb + j] = i for j < comp, by the whole wave: one lane's range at a time (wave-uniform loop over the lanes
@@ -1746,7 +1753,6 @@ void launch_srgb_lut(hipStream_t s, float* lut) { k_srgb_lut<<<1, 256, 0, s>>>(l
 void launch_loss_ray(hipStream_t s, uint32_t cap_rays, StepState* st, DPInfo dp, const DevDataset& ds, const LossParams& lp, uint32_t* numsteps,
                      const uint32_t* ccount, const uint32_t* cbase, const LossWork& w, float* loss, float* ek, float* mask) {
 	if (!w.cmap) throw std::runtime_error("launch_loss_ray: LossWork::cmap (max_compacted entries) is required");
-	if (cap_rays % 64) throw std::runtime_error("launch_loss_ray: cap_rays must be a multiple of 64 (the wave fills the sample map)");
 	dbg_lds_gate(s);
 	k_loss_ray<<<ray_blocks(cap_rays), 256, 0, s>>>(cap_rays, st, dp, ds, lp, numsteps, ccount, cbase, w.sa, w.ekt, w.ck4, w.cke, w.racc, w.rT,
 	                                                  w.rgr, loss, ek, mask, w.cmap);

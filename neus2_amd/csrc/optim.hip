@@ -52,10 +52,29 @@ __device__ __forceinline__ bool adam_param(const AdamParams& p, uint32_t i, floa
 	w = w - elr * m1v;
 	return true;
 }
-// The per-parameter step count is stored in 16 bits, saturating at 65535: it only enters the bias correction, which is
-// exactly 1.0f from step ADAM_BIAS_TAB on when bias_converged (beta^k below 2^-30 there), so every later count gives the
-// same update. (Without a converged table a parameter stepped more than 65535 times would see its correction at 65536.)
-__device__ __forceinline__ uint32_t adam_step16(uint32_t st) { return st < 0xffffu ? st : 0xffffu; }
+// The per-parameter step count (adam.h:106, uint32 in the reference) is stored in 16 bits, saturating at 65535, when the
+// bias table is converged: the count only enters the bias correction, which is exactly 1.0f from step ADAM_BIAS_TAB on
+// (beta^k below 2^-30 there), so every later count gives the same update. Otherwise (betas whose correction has not
+// converged by ADAM_BIAS_TAB) the counts are kept in 32 bits and never saturate (AdamSteps<uint32_t>).
+template <class ST> struct AdamSteps;
+template <> struct AdamSteps<uint16_t> {
+	static __device__ __forceinline__ uint32_t sat(uint32_t st) { return st < 0xffffu ? st : 0xffffu; }
+	static __device__ __forceinline__ void load4(const uint16_t* p, uint32_t g, uint32_t st[4]) {
+		const uint2 S = ((const uint2*)p)[g];
+		st[0] = S.x & 0xffffu; st[1] = S.x >> 16; st[2] = S.y & 0xffffu; st[3] = S.y >> 16;
+	}
+	static __device__ __forceinline__ void store4(uint16_t* p, uint32_t g, const uint32_t st[4]) {
+		((uint2*)p)[g] = make_uint2(sat(st[0]) | (sat(st[1]) << 16), sat(st[2]) | (sat(st[3]) << 16));
+	}
+};
+template <> struct AdamSteps<uint32_t> {
+	static __device__ __forceinline__ uint32_t sat(uint32_t st) { return st; }
+	static __device__ __forceinline__ void load4(const uint32_t* p, uint32_t g, uint32_t st[4]) {
+		const uint4 S = ((const uint4*)p)[g];
+		st[0] = S.x; st[1] = S.y; st[2] = S.z; st[3] = S.w;
+	}
+	static __device__ __forceinline__ void store4(uint32_t* p, uint32_t g, const uint32_t st[4]) { ((uint4*)p)[g] = make_uint4(st[0], st[1], st[2], st[3]); }
+};
 // Ema(ExponentialDecay) of the fp16 weight (ema.h:45-110): the running fp32 EMA, debiased
 __device__ __forceinline__ float ema_param(const AdamParams& p, float ema, float wh) {
 	return (ema * p.ema_decay * p.ema_debias_old + wh * (1 - p.ema_decay)) * p.ema_debias_new;
@@ -78,9 +97,10 @@ __device__ __forceinline__ void adam_transpose_param(const AdamTranspose& tr, ui
 // ema_tmp fp32 running EMA; ema_h fp16 inference weights. Four consecutive parameters per thread with 16-B (8-B for
 // fp16) accesses; the optimizer state of a group is read and written only when one of its four parameters steps (a
 // skipped parameter's values are written back unchanged); the n % 4 tail by block 0.
+template <class ST>
 __global__ void __launch_bounds__(256) k_adam_ema(AdamParams p, float* __restrict__ weights_fp, half_t* __restrict__ weights_h,
                                                   const float* __restrict__ grads, float* __restrict__ m1, float* __restrict__ m2,
-                                                  uint16_t* __restrict__ steps, float* __restrict__ ema_tmp, half_t* __restrict__ ema_h,
+                                                  ST* __restrict__ steps, float* __restrict__ ema_tmp, half_t* __restrict__ ema_h,
                                                   StepCounterArgs sc, AdamTranspose tr) {
 	if (sc.st && blockIdx.x == 0 && threadIdx.x == 0) step_counters_update(sc.st, sc.target_batch, sc.max_samples, sc.world, sc.fixed_rays, sc.eval_cnt, sc.n_eval);
 	const uint32_t ng = p.n / 4;
@@ -101,9 +121,9 @@ __global__ void __launch_bounds__(256) k_adam_ema(AdamParams p, float* __restric
 			const float4 W = ((const float4*)weights_fp)[g];
 			float w[4] = {W.x, W.y, W.z, W.w};
 			float4 M1 = ((const float4*)m1)[g], M2 = ((const float4*)m2)[g];
-			const uint2 S = ((const uint2*)steps)[g];
 			float a[4] = {M1.x, M1.y, M1.z, M1.w}, b[4] = {M2.x, M2.y, M2.z, M2.w};
-			uint32_t st[4] = {S.x & 0xffffu, S.x >> 16, S.y & 0xffffu, S.y >> 16};
+			uint32_t st[4];
+			AdamSteps<ST>::load4(steps, g, st);
 			// the fp16 copy of every parameter of the group is the cast of its fp32 master (weights_h == half(weights_fp)
 			// wherever either is written), so a stepping group needs no read of the fp16 copy: 2 B per parameter less
 #pragma unroll
@@ -113,7 +133,7 @@ __global__ void __launch_bounds__(256) k_adam_ema(AdamParams p, float* __restric
 			}
 			((float4*)m1)[g] = make_float4(a[0], a[1], a[2], a[3]);
 			((float4*)m2)[g] = make_float4(b[0], b[1], b[2], b[3]);
-			((uint2*)steps)[g] = make_uint2(adam_step16(st[0]) | (adam_step16(st[1]) << 16), adam_step16(st[2]) | (adam_step16(st[3]) << 16));
+			AdamSteps<ST>::store4(steps, g, st);
 			((float4*)weights_fp)[g] = make_float4(w[0], w[1], w[2], w[3]);
 			((uint2*)weights_h)[g] = *(const uint2*)wh;
 		} else {
@@ -136,7 +156,7 @@ __global__ void __launch_bounds__(256) k_adam_ema(AdamParams p, float* __restric
 		float w = weights_fp[i], a = m1[i], b = m2[i];
 		uint32_t st = steps[i];
 		if (adam_param(p, i, grads[i], w, a, b, st)) {
-			m1[i] = a; m2[i] = b; steps[i] = (uint16_t)adam_step16(st); weights_fp[i] = w; weights_h[i] = (half_t)w;
+			m1[i] = a; m2[i] = b; steps[i] = (ST)AdamSteps<ST>::sat(st); weights_fp[i] = w; weights_h[i] = (half_t)w;
 		}
 		const float wh = (float)weights_h[i];
 		const float f = ema_param(p, ema_tmp[i], wh);
@@ -391,12 +411,25 @@ __global__ void __launch_bounds__(256) k_occ_bbox_final(const float* __restrict_
 // ---------------------------------------------------------------- host launchers
 static inline uint32_t nblk(uint64_t n, uint32_t cap = 4096) { return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, cap)); }
 void launch_adam_ema(hipStream_t s, const AdamParams& p, float* weights_fp, half_t* weights_h, const float* grads, float* m1, float* m2,
-                     uint16_t* steps, float* ema_tmp, half_t* ema_h, const StepCounterArgs* counters, const AdamTranspose* tr) {
+                     void* steps, bool steps32, float* ema_tmp, half_t* ema_h, const StepCounterArgs* counters, const AdamTranspose* tr) {
 	const StepCounterArgs sc = counters ? *counters : StepCounterArgs{nullptr, 0u, 0u, 1u, 0u, nullptr, 0u};
 	AdamTranspose t{};
 	if (tr) t = *tr;
 	dbg_lds_gate(s);
-	k_adam_ema<<<nblk(std::max<uint64_t>(1, p.n / 4), 16384), 256, 0, s>>>(p, weights_fp, weights_h, grads, m1, m2, steps, ema_tmp, ema_h, sc, t);
+	const uint32_t nb = nblk(std::max<uint64_t>(1, p.n / 4), 16384);
+	if (steps32) k_adam_ema<uint32_t><<<nb, 256, 0, s>>>(p, weights_fp, weights_h, grads, m1, m2, (uint32_t*)steps, ema_tmp, ema_h, sc, t);
+	else k_adam_ema<uint16_t><<<nb, 256, 0, s>>>(p, weights_fp, weights_h, grads, m1, m2, (uint16_t*)steps, ema_tmp, ema_h, sc, t);
+}
+void launch_adam_ema_range(hipStream_t s, AdamParams p, uint32_t lo, uint32_t hi, float* weights_fp, half_t* weights_h, const float* grads,
+                           float* m1, float* m2, void* steps, bool steps32, float* ema_tmp, half_t* ema_h, const AdamTranspose* tr) {
+	// parameters [lo, hi): 16-B group accesses need lo % 4 == 0; the transposed MLP copies index parameters from 0
+	if (lo % 4 || hi < lo || hi > p.n) throw std::runtime_error("launch_adam_ema_range: lo must be a multiple of 4 and lo <= hi <= n");
+	if (tr && tr->n && lo != 0) throw std::runtime_error("launch_adam_ema_range: the transposed copies need the range to start at 0");
+	if (hi == lo) return;
+	p.n_matrix = p.n_matrix > lo ? std::min(p.n_matrix - lo, hi - lo) : 0u;
+	p.n = hi - lo;
+	void* st = (uint8_t*)steps + (size_t)lo * (steps32 ? 4 : 2);
+	launch_adam_ema(s, p, weights_fp + lo, weights_h + lo, grads + lo, m1 + lo, m2 + lo, st, steps32, ema_tmp + lo, ema_h + lo, nullptr, tr);
 }
 void launch_add_f32(hipStream_t s, uint32_t n, const float* src, float* dst) {
 	if (n) k_add_f32<<<std::min<uint32_t>((n + 255) / 256, 8192), 256, 0, s>>>(n, src, dst);

@@ -187,7 +187,9 @@ struct NeusTestbed {
 	// between steps of one neus_testbed_train call (nothing pending between calls), at one rank, on static scenes, and
 	// not before a step that starts with an occupancy update or a loss readback (train_step: la_go).
 	bool la_on = [] { const char* e = std::getenv("NEUS_LOOKAHEAD"); return !(e && e[0] == '0'); }();
+	struct AdamSplit { AdamParams p; uint32_t next; };  // adam_overlap: the step's Adam parameters; next: first parameter not issued
 	bool la_pending = false, la_next_in_call = false;
+	uint64_t la_steps = 0, adam_split_steps = 0;  // (stats: lookahead_steps, adam_split_steps)
 	const bool la_stat = [] { const char* e = std::getenv("NEUS_LA_STAT"); return e && e[0] == '1'; }();
 	// development (NEUS_LA_AT): where in the backward the lookahead is issued. 0 right after the loss (the default), 1 after
 	// the training encode, 2 after the training MLP kernels, 3 after the weight-gradient reduction, 4 after the scatter
@@ -242,7 +244,10 @@ struct NeusTestbed {
 	float aabb_scale = 1.f;
 	// parameters
 	Dev<float> params_fp, grads, m1, m2, ema_tmp;
-	Dev<uint16_t> adam_steps;  // per-parameter Adam steps, saturating at 65535 (optim.hip adam_step16)
+	// per-parameter Adam steps: u16 [P] saturating at 65535 while the bias table is converged (optim.hip AdamSteps), else
+	// u32 [P] (steps32); P x 4 B either way
+	Dev<uint32_t> adam_steps;
+	bool steps32 = false;
 	Dev<half_t> params_h, ema_h, wT;
 	MlpPtrs mlp{};
 	DinPerm din_perm{};
@@ -523,6 +528,10 @@ struct NeusTestbed {
 		if (la_stream) { (void)hipStreamSynchronize(la_stream); (void)hipStreamDestroy(la_stream); }
 		if (ev_la_start) (void)hipEventDestroy(ev_la_start);
 		if (ev_la_done) (void)hipEventDestroy(ev_la_done);
+		if (ad_stream) { (void)hipStreamSynchronize(ad_stream); (void)hipStreamDestroy(ad_stream); }
+		for (auto& e : ad_ev) if (e) (void)hipEventDestroy(e);
+		if (ad_done) (void)hipEventDestroy(ad_done);
+		for (auto& e : xt_ev) for (auto& x : e) if (x) (void)hipEventDestroy(x);
 		for (hipEvent_t e : la_stat_ev) (void)hipEventDestroy(e);
 		if (ev_fork) (void)hipEventDestroy(ev_fork);
 		if (ev_join) (void)hipEventDestroy(ev_join);
@@ -694,7 +703,7 @@ struct NeusTestbed {
 		const std::vector<float> h = initial_params(c.seed, geo);
 		HIP_CHECK(hipMemcpy(params_fp.p, h.data(), (size_t)P * 4, hipMemcpyHostToDevice));
 		HIP_CHECK(hipMemset(m1.p, 0, (size_t)P * 4)); HIP_CHECK(hipMemset(m2.p, 0, (size_t)P * 4));
-		HIP_CHECK(hipMemset(ema_tmp.p, 0, (size_t)P * 4)); HIP_CHECK(hipMemset(adam_steps.p, 0, (size_t)P * 2));
+		HIP_CHECK(hipMemset(ema_tmp.p, 0, (size_t)P * 4)); HIP_CHECK(hipMemset(adam_steps.p, 0, (size_t)P * 4));
 		HIP_CHECK(hipMemset(ema_h.p, 0, (size_t)P * 2)); HIP_CHECK(hipMemset(grads.p, 0, (size_t)P * 4));
 		ema_h_stale = false;
 		launch_cast_half(stream, P, params_fp.p, params_h.p);
@@ -873,7 +882,7 @@ struct NeusTestbed {
 			HIP_CHECK(hipMemcpy(params_h.p, eh.data(), (size_t)P * 2, hipMemcpyHostToDevice));
 		}
 		HIP_CHECK(hipMemset(m1.p, 0, (size_t)P * 4)); HIP_CHECK(hipMemset(m2.p, 0, (size_t)P * 4));
-		HIP_CHECK(hipMemset(adam_steps.p, 0, (size_t)P * 2));
+		HIP_CHECK(hipMemset(adam_steps.p, 0, (size_t)P * 4));
 		// the fp32 EMA starts at the loaded weights: the first EMA step weighs it by 1 - decay^0 = 0, and until the
 		// canonical optimizer steps (after the global-movement phase) it is what get_ema_params reports
 		HIP_CHECK(hipMemcpy(ema_tmp.p, params_fp.p, (size_t)P * 4, hipMemcpyDeviceToDevice));
@@ -904,7 +913,7 @@ struct NeusTestbed {
 		training_step = 0; canonical_step = 0;
 		const uint32_t P = lay.P;
 		HIP_CHECK(hipMemset(m1.p, 0, (size_t)P * 4)); HIP_CHECK(hipMemset(m2.p, 0, (size_t)P * 4));
-		HIP_CHECK(hipMemset(adam_steps.p, 0, (size_t)P * 2));
+		HIP_CHECK(hipMemset(adam_steps.p, 0, (size_t)P * 4));
 		{  // the fp32 EMA restarts from the inference weights (weighted by 0 at the next EMA step)
 			std::vector<half_t> eh(P);
 			sync_ema_h();
@@ -1021,7 +1030,7 @@ struct NeusTestbed {
 	// forward recompute + backward into g (fp32 [P], zeroed by the caller)
 	void net_backward(const uint32_t* n_valid_ptr, const uint32_t* n_train_ptr, uint32_t n, const float* c, uint32_t valid,
 	                  const half_t* dlo, float* g, hipStream_t s, bool marks = false, bool canonical = true, const EncodeRollover* ro = nullptr,
-	                  bool exchange = false) {
+	                  bool exchange = false, AdamSplit* as = nullptr) {
 		const uint32_t ld = n;
 		encode(n_train_ptr, n, n, ld, c, COORD_W, valid, true, s, ro);
 		la_fire(1);
@@ -1035,6 +1044,7 @@ struct NeusTestbed {
 		// the MLP weight gradients were accumulated inside the training kernels: one small fixed-order reduction
 		launch_mlp_grad_reduce(s, grad_reduce(n, g, n_train_ptr));
 		la_fire(3);
+		if (as) adam_issue(*as, lay.grid_off, g, true);  // the MLP blocks (and their transposed copies) beside the scatter
 		if (exchange) {  // the MLP blocks and the variance are final: their exchange runs beside the grid scatter
 			hipStream_t xs = x_stream();
 			allreduce_f32(g, lay.grid_off, false, xs);
@@ -1042,9 +1052,14 @@ struct NeusTestbed {
 		}
 		if (marks) mark(7);
 		const ScatterWork sw = scatter_work_for(g + lay.grid_off, valid, s);
-		const ScatterSplit sp = exchange && sw.mode == 2 ? x_split(valid, g + lay.grid_off) : ScatterSplit{};
+		ScatterSplit sp = exchange && sw.mode == 2 ? x_split(valid, g + lay.grid_off) : ScatterSplit{};
+		const bool a_split = as && !exchange && sw.mode == 2;
+		if (a_split) {  // the level groups of the overlapped exchange; each group's Adam once its accumulation is queued
+			sp = x_split(valid, g + lay.grid_off);
+			sp.done = [this, as, g](uint32_t, uint32_t hi) { adam_issue(*as, lay.grid_off + 2 * gl.offset[hi], g, false); };
+		}
 		launch_grid_scatter(s, n_train_ptr, n, ld, c, COORD_W, gl, valid, tbuf.dLdenc, tbuf.genc, tbuf.v, g + lay.grid_off, sw, scan_tmp.p,
-		                    scan_tmp_bytes, exchange && sw.mode == 2 ? &sp : nullptr);
+		                    scan_tmp_bytes, (exchange || a_split) && sw.mode == 2 ? &sp : nullptr);
 		if (exchange && sw.mode != 2) {  // other scatter modes: the grid exchange after the whole scatter
 			const size_t grid_act = 2 * (size_t)gl.offset[std::min(valid + 1, gl.n_levels)];
 			allreduce_f32(g + lay.grid_off, grid_act, false, x_stream());
@@ -1170,6 +1185,13 @@ struct NeusTestbed {
 
 	// ------------------------------------------------------------ optimizer (trainer.h:170-172)
 	void optimizer_step(const float* g, const StepCounterArgs* counters = nullptr) {
+		const AdamParams p = adam_params();
+		const AdamTranspose tr = adam_transpose();  // the transposed / permuted MLP copies are written by the Adam launch itself
+		launch_adam_ema(stream, p, params_fp.p, params_h.p, g, m1.p, m2.p, adam_steps.p, steps32, ema_tmp.p, ema_h.p, counters, &tr);
+		if (p.skip_ema_h) ema_h_stale = true;
+	}
+	// The host side of one optimizer step (advances the step count and the learning-rate decay): call once per step
+	AdamParams adam_params() {
 		// ExponentialDecay (exponential_decay.h:61-80): evaluated with the nested step count before the Adam step
 		const uint32_t sb = adam_step;
 		if (sb == 0) lr_factor = 1.0f;
@@ -1186,24 +1208,76 @@ struct NeusTestbed {
 		int e2 = 0;
 		p.pow2_scale = std::frexp(p.loss_scale, &e2) == 0.5f ? 1u : 0u;
 		p.inv_loss_scale = 1.0f / p.loss_scale;
-		if (p.beta1 != bias_b1 || p.beta2 != bias_b2) {
-			// bias-correction table for these betas (rebuilt only when they change)
-			adam_bias.alloc(2 * ADAM_BIAS_TAB);
-			launch_adam_bias_table(stream, p.beta1, p.beta2, adam_bias.p);
-			float last[2];
-			HIP_CHECK(hipStreamSynchronize(stream));
-			HIP_CHECK(hipMemcpy(&last[0], adam_bias.p + ADAM_BIAS_TAB - 1, 4, hipMemcpyDeviceToHost));
-			HIP_CHECK(hipMemcpy(&last[1], adam_bias.p + 2 * ADAM_BIAS_TAB - 1, 4, hipMemcpyDeviceToHost));
-			const double k = ADAM_BIAS_TAB - 1;
-			bias_conv = last[0] == 1.0f && last[1] == 1.0f && std::pow((double)p.beta1, k) < 0x1p-30 && std::pow((double)p.beta2, k) < 0x1p-30;
-			bias_b1 = p.beta1; bias_b2 = p.beta2;
-		}
+		ensure_bias_table();
 		p.bias_tab = adam_bias.p; p.bias_converged = bias_conv ? 1u : 0u;
-		// the transposed / permuted MLP copies are written by the Adam launch itself
-		const AdamTranspose tr = adam_transpose();
 		{ static const bool eager = [] { const char* e = std::getenv("NEUS_EAGER_EMA_H"); return e && e[0] == '1'; }(); p.skip_ema_h = eager ? 0u : 1u; }
-		launch_adam_ema(stream, p, params_fp.p, params_h.p, g, m1.p, m2.p, adam_steps.p, ema_tmp.p, ema_h.p, counters, &tr);
-		if (p.skip_ema_h) ema_h_stale = true;
+		return p;
+	}
+	// Adam in pieces beside the backward (adam_overlap; one rank, static scenes): the MLP blocks once the weight-gradient
+	// reduction is done (beside the grid scatter), each grid level group once its accumulation launch is done (beside the
+	// next group's), on ad_stream; the step's stream joins it where the one Adam launch used to be. Elementwise, so the
+	// parameters are bitwise those of the one launch. Cut points are rounded down to 4 parameters (the kernel's 16-B
+	// groups): a range may start with the last few parameters of the level before it, whose gradient is final already.
+	bool adam_overlap = [] { const char* e = std::getenv("NEUS_ADAM_OVERLAP"); return e && e[0] == '1'; }();
+	hipStream_t ad_stream = nullptr;
+	hipEvent_t ad_ev[8] = {}, ad_done = nullptr;
+	int ad_n = 0;
+	void adam_issue(AdamSplit& a, uint32_t hi, const float* g, bool with_tr) {
+		if (!ad_stream) {
+			if (main_prio) HIP_CHECK(hipStreamCreateWithPriority(&ad_stream, hipStreamNonBlocking, main_prio));
+			else HIP_CHECK(hipStreamCreateWithFlags(&ad_stream, hipStreamNonBlocking));
+			for (auto& e : ad_ev) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+			HIP_CHECK(hipEventCreateWithFlags(&ad_done, hipEventDisableTiming));
+		}
+		hi = hi >= lay.P ? lay.P : hi / 4 * 4;
+		if (hi <= a.next) return;
+		hipEvent_t e = ad_ev[ad_n++ % 8];
+		HIP_CHECK(hipEventRecord(e, stream));
+		HIP_CHECK(hipStreamWaitEvent(ad_stream, e, 0));
+		const AdamTranspose tr = with_tr ? adam_transpose() : AdamTranspose{};
+		launch_adam_ema_range(ad_stream, a.p, a.next, hi, params_fp.p, params_h.p, g, m1.p, m2.p, adam_steps.p, steps32, ema_tmp.p, ema_h.p,
+		                      with_tr ? &tr : nullptr);
+		a.next = hi;
+	}
+	void adam_join(AdamSplit& a, const float* g) {
+		adam_issue(a, lay.P, g, false);  // (whatever is left: the levels past the valid one, the variance)
+		HIP_CHECK(hipEventRecord(ad_done, ad_stream));
+		HIP_CHECK(hipStreamWaitEvent(stream, ad_done, 0));
+		if (a.p.skip_ema_h) ema_h_stale = true;
+	}
+	// bias-correction table for the config's betas (rebuilt only when they change), and the step counts' width for it:
+	// u16 while the table is converged, u32 otherwise (moved through the host when the betas change)
+	void ensure_bias_table() {
+		const float b1 = cfg.beta1, b2 = cfg.beta2;
+		if (b1 == bias_b1 && b2 == bias_b2) return;
+		adam_bias.alloc(2 * ADAM_BIAS_TAB);
+		launch_adam_bias_table(stream, b1, b2, adam_bias.p);
+		float last[2];
+		HIP_CHECK(hipStreamSynchronize(stream));
+		HIP_CHECK(hipMemcpy(&last[0], adam_bias.p + ADAM_BIAS_TAB - 1, 4, hipMemcpyDeviceToHost));
+		HIP_CHECK(hipMemcpy(&last[1], adam_bias.p + 2 * ADAM_BIAS_TAB - 1, 4, hipMemcpyDeviceToHost));
+		const double k = ADAM_BIAS_TAB - 1;
+		bias_conv = last[0] == 1.0f && last[1] == 1.0f && std::pow((double)b1, k) < 0x1p-30 && std::pow((double)b2, k) < 0x1p-30;
+		bias_b1 = b1; bias_b2 = b2;
+		if (steps32 == bias_conv) {
+			std::vector<uint32_t> h(lay.P);
+			get_steps(h.data());
+			steps32 = !bias_conv;
+			put_steps(h.data());
+		}
+	}
+	void get_steps(uint32_t* out) {
+		if (steps32) { HIP_CHECK(hipMemcpy(out, adam_steps.p, lay.P * 4, hipMemcpyDeviceToHost)); return; }
+		std::vector<uint16_t> h(lay.P);
+		HIP_CHECK(hipMemcpy(h.data(), adam_steps.p, lay.P * 2, hipMemcpyDeviceToHost));
+		for (size_t i = 0; i < lay.P; ++i) out[i] = h[i];
+	}
+	void put_steps(const uint32_t* in) {  // in = nullptr: zeros
+		if (!in) { HIP_CHECK(hipMemset(adam_steps.p, 0, lay.P * 4)); return; }
+		if (steps32) { HIP_CHECK(hipMemcpy(adam_steps.p, in, lay.P * 4, hipMemcpyHostToDevice)); return; }
+		std::vector<uint16_t> h(lay.P);
+		for (size_t i = 0; i < lay.P; ++i) h[i] = (uint16_t)std::min<uint32_t>(in[i], 0xffffu);
+		HIP_CHECK(hipMemcpy(adam_steps.p, h.data(), lay.P * 2, hipMemcpyHostToDevice));
 	}
 	AdamTranspose adam_transpose() const {
 		const Layout& l = lay;
@@ -1260,6 +1334,40 @@ struct NeusTestbed {
 		++it_steps;
 		it_n = 0;
 	}
+
+	// Exchange timing (neus_testbed_set_exchange_timing, data parallel): per step, an event on the step's stream where the
+	// backward is done (the gradients' last use before the join) and one on the exchange's stream after its last
+	// collective. exposed = max(0, done - backward done): what the join before Adam waits for; span = done - the loss's end
+	// (the counters' exchange starts there). A ring of event sets collected lazily (the oldest has long completed when the
+	// ring wraps, the host running at most 16 steps ahead), so timing runs inside timed regions without a per-step sync.
+	bool xt_on = false;
+	static constexpr int XT_RING = 64;
+	hipEvent_t xt_ev[XT_RING][3] = {};  // [loss end (step stream), backward done (step stream), exchange done (exchange stream)]
+	int xt_head = 0, xt_n = 0;
+	double xt_exposed_ms = 0.0, xt_span_ms = 0.0;
+	uint64_t xt_steps = 0;
+	hipEvent_t* xt_slot() {
+		if (xt_n == XT_RING) xt_collect_one();
+		hipEvent_t* e = xt_ev[(xt_head + xt_n) % XT_RING];
+		for (int k = 0; k < 3; ++k)
+			if (!e[k]) HIP_CHECK(hipEventCreate(&e[k]));
+		++xt_n;
+		return e;
+	}
+	void xt_collect_one() {
+		hipEvent_t* e = xt_ev[xt_head];
+		HIP_CHECK(hipEventSynchronize(e[2]));
+		HIP_CHECK(hipEventSynchronize(e[1]));
+		float exposed = 0.f, span = 0.f;
+		HIP_CHECK(hipEventElapsedTime(&exposed, e[1], e[2]));
+		HIP_CHECK(hipEventElapsedTime(&span, e[0], e[2]));
+		xt_exposed_ms += std::max(0.f, exposed);
+		xt_span_ms += span;
+		++xt_steps;
+		xt_head = (xt_head + 1) % XT_RING;
+		--xt_n;
+	}
+	void xt_collect_all() { while (xt_n) xt_collect_one(); }
 
 	// ------------------------------------------------------------ rendering (render_to_cpu, python_api.cu:123-169)
 	// NerfTracer::init_rays_from_camera + trace (testbed_nerf.cu:2397-2600) once per spp, accumulated in linear
@@ -1463,6 +1571,7 @@ struct NeusTestbed {
 		const RaySort rsort{rs_hist.p, rs_off.p, rs_key.p, rs_perm.p, chunk_cnt.p + RS_N_PERM};
 		if (la_have) {
 			if (canonical_step % n_prep == 0) throw std::runtime_error("train: lookahead issued before an occupancy update");
+			++la_steps;
 			if (la_stat && la_stat_used % 4 == 2) HIP_CHECK(hipEventRecord(la_stat_next(), s));
 			HIP_CHECK(hipStreamWaitEvent(s, ev_la_done, 0));  // this step's samples came from the previous step's lookahead
 			if (la_stat && la_stat_used % 4 == 3) HIP_CHECK(hipEventRecord(la_stat_next(), s));
@@ -1524,6 +1633,21 @@ struct NeusTestbed {
 				HIP_CHECK(hipMemcpyAsync(dbg_snap[k].p, src[k].first, src[k].second, hipMemcpyDeviceToDevice, s));
 			}
 		}
+		// ---- the step's counters over the ranks (data parallel): the compacted count and the rays with samples, summed
+		// right after the loss into StepState::compacted_global / rays_ws_global (compacted_counter stays this rank's
+		// training batch for the backward). On the communication stream with the overlapped exchange, so the backward
+		// does not wait for it; the gradients' collectives follow on the same stream, in the same order on every rank.
+		const bool xo = coll_on() && exchange_overlap && (!dyn || train_canonical);
+		coll_bytes_step = 0;
+		hipStream_t cs = s;  // the stream the counters (and the lookahead's start) are ordered on
+		hipEvent_t* xt = coll_on() && xt_on ? xt_slot() : nullptr;
+		if (xt) HIP_CHECK(hipEventRecord(xt[0], s));
+		if (coll_on()) {
+			cs = xo ? x_stream() : stream;
+			coll_begin();
+			allreduce_u32(&st.p->compacted_global, 2, cs);
+			coll_end();
+		}
 		// ---- lookahead: the next step's ray sampling beside this step's backward (la_on; see the members)
 		const bool get_loss = training_step % 16 == 0;
 		const StepCounterArgs sca{st.p, batch, max_samples, world, cfg.fixed_rays_per_batch, progressive ? chunk_cnt.p : nullptr, nch};
@@ -1531,14 +1655,15 @@ struct NeusTestbed {
 		{
 			const uint32_t cs1 = training_step + 1;  // the next step's canonical step (static scenes)
 			const uint32_t n_prep1 = std::min(16u, std::max(1u, cs1 / 16u));
-			const bool la_go = la_on && la_next_in_call && world == 1 && !coll_on() && !dyn && !use_delta && !profiling && !dbg_loss_replay &&
+			const bool la_go = la_on && la_next_in_call && !dyn && !use_delta && !profiling && !dbg_loss_replay &&
 			                   !dbg_lds_fill && g_dbg_lds_fill == 0 && g_dbg_xcd_shift == 0 && cs1 % 16 != 0 && cs1 % n_prep1 != 0 &&
 			                   !(get_loss && loss_pending);
 			if (la_go) {
-				// the host's StepState readback first (its place in the step without the lookahead: nothing writes these
-				// fields between here and there at one rank), then the step counters the next step's sampling reads
-				if (get_loss) HIP_CHECK(hipMemcpyAsync(pinned + 64, st.p, sizeof(StepState), hipMemcpyDeviceToHost, s));
-				launch_step_counters(s, st.p, batch, max_samples, world, cfg.fixed_rays_per_batch, sca.eval_cnt, sca.n_eval);
+				// the host's StepState readback first (its place in the step without the lookahead: nothing it reads is
+				// written between here and there - the ranks' counts are already summed), then the step counters the next
+				// step's sampling reads; both behind the counters' exchange (cs)
+				if (get_loss) HIP_CHECK(hipMemcpyAsync(pinned + 64, st.p, sizeof(StepState), hipMemcpyDeviceToHost, cs));
+				launch_step_counters(cs, st.p, batch, max_samples, world, cfg.fixed_rays_per_batch, sca.eval_cnt, sca.n_eval);
 				counters_done = true;
 				if (!la_stream) {
 					// the lookahead stream at the lowest priority: the backward's workgroups are dispatched first and the march's
@@ -1560,14 +1685,15 @@ struct NeusTestbed {
 				pcg32 r1 = rng;
 				r1.advance();
 				const bool prog1 = progressive_mode == 2 || (progressive_mode == 1 && last_keep_ratio < PROGRESSIVE_RATIO);
-				la_deferred = [this, s, dp, r1, prog1] {
-					HIP_CHECK(hipEventRecord(ev_la_start, s));
+				la_deferred = [this, cs, dp, r1, prog1] {
+					HIP_CHECK(hipEventRecord(ev_la_start, cs));
 					HIP_CHECK(hipStreamWaitEvent(la_stream, ev_la_start, 0));
 					if (la_stat) { la_stat_used -= la_stat_used % 4; HIP_CHECK(hipEventRecord(la_stat_next(), la_stream)); }
 					issue_march(la_stream, dp, r1, prog1, scan_tmp_la.p);
 					if (la_stat) HIP_CHECK(hipEventRecord(la_stat_next(), la_stream));
 					HIP_CHECK(hipEventRecord(ev_la_done, la_stream));
 				};
+				if (cs != s) la_fire(0x7fffffff);  // (the communication stream: issued now, before the gradients' collectives queue there)
 				la_fire(0);
 				la_pending = true;
 			}
@@ -1579,9 +1705,11 @@ struct NeusTestbed {
 		// entry by k_scatter_accum, zeros with no samples); the global-movement phase skips it: zero the buffer there
 		if (!(!dyn || train_canonical)) HIP_CHECK(hipMemsetAsync(grads.p, 0, (size_t)lay.P * 4, s));
 		mark(4);
-		// the overlapped exchange (coll_on): the canonical backward all-reduces its gradient ranges as they finish
-		const bool xo = coll_on() && exchange_overlap && (!dyn || train_canonical);
-		coll_bytes_step = 0;
+		// the overlapped exchange (xo): the canonical backward all-reduces its gradient ranges as they finish; adam_overlap
+		// (one rank, static scenes): the optimizer step in pieces beside the scatter
+		AdamSplit asp{};
+		const bool a_over = adam_overlap && !coll_on() && !dyn;
+		if (a_over) asp.p = adam_params();
 		if (use_delta) {
 			// the training forward runs on the deformed batch; dL/d(position) feeds the DeltaNetwork backward
 			launch_delta_apply(s, nullptr, batch, COORD_W, coords_c.p, coords_cdef.p, delta.p);
@@ -1589,7 +1717,8 @@ struct NeusTestbed {
 			net_backward(&st.p->compacted_counter, &st.p->n_train, batch, coords_cdef.p, valid, dL_dout.p, grads.p, s, true, train_canonical, nullptr, xo);
 			tbuf.dpos = nullptr;
 		} else {
-			net_backward(&st.p->compacted_counter, &st.p->n_train, batch, coords_c.p, valid, dL_dout.p, grads.p, s, true, train_canonical, &ro, xo);
+			net_backward(&st.p->compacted_counter, &st.p->n_train, batch, coords_c.p, valid, dL_dout.p, grads.p, s, true, train_canonical, &ro, xo,
+			             a_over ? &asp : nullptr);
 		}
 		la_fire(99);  // (issued by now in any case)
 		// DeltaNetwork gradient partial sums (the first half of its backward; the Adam step follows the exchange)
@@ -1610,17 +1739,17 @@ struct NeusTestbed {
 			// gl.offset[valid + 1] on holds 0 after the backward, on every rank), so only the MLP blocks, the active levels'
 			// tables and the variance move. Overlapped: the gradients went out during the backward (net_backward).
 			const size_t grid_act = 2 * (size_t)gl.offset[std::min(valid + 1, gl.n_levels)];
+			if (xt) HIP_CHECK(hipEventRecord(xt[1], s));  // the backward is done (and the loss sums, when logged)
 			hipStream_t xs = xo ? x_stream() : stream;
 			coll_begin();
 			if (!xo) {
 				allreduce_f32(grads.p, (size_t)lay.grid_off + grid_act);
 				allreduce_f32(grads.p + lay.var_off, lay.P - lay.var_off);
 			}
-			allreduce_u32(&st.p->compacted_counter, 1, xs);
-			allreduce_u32(&st.p->n_rays_with_samples, 1, xs);
 			if (use_delta) allreduce_f32(delta_partial.p, delta_partial_floats(), false, xs);
 			if (get_loss) { allreduce_f32(loss_sum.p, 3, false, xs); allreduce_u32(health_buf.p, 2, xs); }
 			coll_end();
+			if (xt) HIP_CHECK(hipEventRecord(xt[2], xs));
 			x_join();
 		}
 		if (get_loss) {
@@ -1639,7 +1768,13 @@ struct NeusTestbed {
 		rng.advance();
 		mark(9);
 		// ---- optimizers (testbed_nerf.cu:3503-3508): the canonical trainer, the global-move trainer
-		if (canon_opt) optimizer_step(grads.p, counters_done ? nullptr : &sca);
+		if (canon_opt && a_over) {
+			++adam_split_steps;
+			if (!counters_done) launch_step_counters(s, st.p, batch, max_samples, world, cfg.fixed_rays_per_batch, sca.eval_cnt, sca.n_eval);
+			adam_join(asp, grads.p);
+		} else if (canon_opt) {
+			optimizer_step(grads.p, counters_done ? nullptr : &sca);
+		}
 		if (use_delta) {
 			// ExponentialDecay of the globalmove optimizer (exponential_decay.h:61-80), its own step count
 			if (delta_step == 0) delta_lr_factor = 1.f;
@@ -1696,7 +1831,7 @@ struct NeusTestbed {
 		}
 		const StepState& h = prof_st[par];
 		phase_npre += h.n_kept;
-		phase_ntrain += std::min(h.compacted_counter / std::max(1u, world), batch);
+		phase_ntrain += std::min(h.compacted_global / std::max(1u, world), batch);
 		++phase_steps;
 		prof_pending[par] = false;
 	}
@@ -1711,22 +1846,22 @@ struct NeusTestbed {
 		if (!loss_pending) return;
 		HIP_CHECK(hipEventSynchronize(ev_loss));
 		const StepState* sst = (const StepState*)(pinned + 64);
-		const float measured = (float)sst->compacted_counter / (float)world;
+		const float measured = (float)sst->compacted_global / (float)world;
 		const float scale = measured / (float)batch;
 		last_loss = pinned[0] * scale;
 		ek_loss = pinned[1] * scale;
 		mask_loss = pinned[2] * scale;
-		last_rays_with_samples = sst->n_rays_with_samples;
+		last_rays_with_samples = sst->rays_ws_global;
 		last_keep_ratio = sst->n_kept ? measured / (float)sst->n_kept : 1.f;  // composited / kept (progressive inference)
-		choose_chunk_ends(sst->compacted_counter, sst->n_rays_with_samples);
-		ray_loss = sst->n_rays_with_samples ? pinned[0] * (float)(sst->rays_per_batch * world) / (float)sst->n_rays_with_samples : 0.f;
+		choose_chunk_ends(sst->compacted_global, sst->rays_ws_global);
+		ray_loss = sst->rays_ws_global ? pinned[0] * (float)(sst->rays_per_batch * world) / (float)sst->rays_ws_global : 0.f;
 		if (!loss_ema_init) { loss_scalar_ema = last_loss; loss_ema_init = true; }
 		else loss_scalar_ema = 0.99f * loss_scalar_ema + 0.01f * last_loss;
 		// health: a non-finite loss sum (a NaN / Inf flag on the loss; the sums are all-reduced, so every
 		// rank raises it on the same step), and the zero-sample guard (testbed_nerf.cu:3542-3548: loss scalars 0,
 		// training stops - the Python frame() loop reads training_aborted)
 		if (!std::isfinite(pinned[0]) || !std::isfinite(pinned[1]) || !std::isfinite(pinned[2])) { nonfinite = true; aborted = true; }
-		if (sst->compacted_counter == 0) {
+		if (sst->compacted_global == 0) {
 			loss_scalar_ema = last_loss = ek_loss = mask_loss = 0.f;
 			aborted = true;
 		}
@@ -1737,7 +1872,9 @@ struct NeusTestbed {
 		std::memcpy(&scan_fail, pinned + 48, 4);
 		std::memcpy(all, pinned + 52, 8);  // the health words summed over the ranks (this rank's alone at world 1)
 		const uint32_t local = sst->fail_flags | (scan_fail ? STEP_FAIL_SCAN : 0u);
-		const uint32_t global = (all[0] ? (all[0] & STEP_FAIL_MARCH_T ? STEP_FAIL_MARCH_T : all[0]) : 0u) | (all[1] ? STEP_FAIL_SCAN : 0u);
+		// the words are sums over the ranks, not bit sets: word 0 sums the ranks' fail_flags (the march sets only
+		// STEP_FAIL_MARCH_T there), word 1 the scans' give-up counters; any nonzero sum names its cause
+		const uint32_t global = (all[0] ? STEP_FAIL_MARCH_T : 0u) | (all[1] ? STEP_FAIL_SCAN : 0u);
 		health_raise(local | (coll_on() ? global : 0u), local == 0 && coll_on() && global != 0, raise);
 	}
 	uint32_t fail_seen = 0;
@@ -1832,6 +1969,8 @@ int neus_testbed_get_stats(NeusTestbed* tb, NeusTrainStats* o) {
 		o->pre_samples_total = s.pre_total; o->rays_total = s.rays_total;
 		o->occ_samples_total = tb->occ_samples; o->occ_updates = tb->occ_updates;
 		o->progressive_chunk_end = tb->chunk_ends.empty() ? 0u : tb->chunk_ends[0];
+		o->lookahead_steps = tb->la_steps;
+		o->adam_split_steps = tb->adam_split_steps;
 		o->health_flags = s.fail_flags | tb->fail_seen | (scan_failures(tb->scan_tmp.p) ? STEP_FAIL_SCAN : 0u);
 		o->evaluated_samples_total = s.eval_total; o->progressive_steps = s.prog_steps; o->evaluated_samples_last = s.eval_last;
 	});
@@ -1933,11 +2072,7 @@ int neus_testbed_get_optimizer_state(NeusTestbed* tb, NeusOptimizerState* st, fl
 		}
 		if (m1) HIP_CHECK(hipMemcpy(m1, tb->m1.p, P * 4, hipMemcpyDeviceToHost));
 		if (m2) HIP_CHECK(hipMemcpy(m2, tb->m2.p, P * 4, hipMemcpyDeviceToHost));
-		if (steps) {  // (stored in 16 bits, saturating at 65535: optim.hip adam_step16)
-			std::vector<uint16_t> h(P);
-			HIP_CHECK(hipMemcpy(h.data(), tb->adam_steps.p, P * 2, hipMemcpyDeviceToHost));
-			for (size_t i = 0; i < P; ++i) steps[i] = h[i];
-		}
+		if (steps) tb->get_steps(steps);  // (saturated at 65535 while the bias table is converged: optim.hip AdamSteps)
 		if (ema_half) HIP_CHECK(hipMemcpy(ema_half, tb->ema_h.p, P * 2, hipMemcpyDeviceToHost));
 	});
 }
@@ -1953,11 +2088,8 @@ int neus_testbed_set_optimizer_state(NeusTestbed* tb, const NeusOptimizerState* 
 		HIP_CHECK(hipMemcpy(tb->m1.p, m1, P * 4, hipMemcpyHostToDevice));
 		HIP_CHECK(hipMemcpy(tb->m2.p, m2, P * 4, hipMemcpyHostToDevice));
 		// Adam::deserialize: param_steps absent -> zeros (adam.h:437-442)
-		if (steps) {
-			std::vector<uint16_t> h(P);
-			for (size_t i = 0; i < P; ++i) h[i] = (uint16_t)std::min<uint32_t>(steps[i], 0xffffu);
-			HIP_CHECK(hipMemcpy(tb->adam_steps.p, h.data(), P * 2, hipMemcpyHostToDevice));
-		} else HIP_CHECK(hipMemset(tb->adam_steps.p, 0, P * 2));
+		tb->ensure_bias_table();  // (the counts' width follows the betas' bias table)
+		tb->put_steps(steps);
 		// Ema::deserialize (ema.h:189-194): the EMA weights, and the fp32 accumulator cast from them
 		HIP_CHECK(hipMemcpy(tb->ema_h.p, ema_half, P * 2, hipMemcpyHostToDevice));
 		tb->ema_h_stale = false;
@@ -2357,6 +2489,22 @@ int neus_testbed_infer_timing(NeusTestbed* tb, double* ms_total, uint64_t* launc
 		if (steps) *steps = tb->it_steps;
 	});
 }
+int neus_testbed_set_exchange_timing(NeusTestbed* tb, int on) {
+	return guard([&] {
+		tb->xt_collect_all();
+		tb->xt_on = on != 0;
+		tb->xt_exposed_ms = tb->xt_span_ms = 0.0; tb->xt_steps = 0;
+	});
+}
+int neus_testbed_exchange_timing(NeusTestbed* tb, double* exposed_ms_total, double* span_ms_total, uint64_t* steps) {
+	return guard([&] {
+		HIP_CHECK(hipSetDevice(tb->device));
+		tb->xt_collect_all();
+		if (exposed_ms_total) *exposed_ms_total = tb->xt_exposed_ms;
+		if (span_ms_total) *span_ms_total = tb->xt_span_ms;
+		if (steps) *steps = tb->xt_steps;
+	});
+}
 int neus_testbed_kernel_times(NeusTestbed* tb, float* ms) {
 	return guard([&] {
 		tb->flush_phases();
@@ -2428,11 +2576,11 @@ int neus_testbed_init_local_group(NeusTestbed* tb, NeusLocalGroup* g, int rank) 
 	});
 }
 
-int neus_host_group_create(int rank, int world, const char* host, int port, NeusHostGroup** out) {
+int neus_host_group_create(int rank, int world, const char* host, int port, uint64_t job_token, NeusHostGroup** out) {
 	return guard([&] {
 		if (world < 1 || world > 64 || rank < 0 || rank >= world) throw std::runtime_error("host group: world must be 1..64, 0 <= rank < world");
 		if (port <= 0 || port > 65535) throw std::runtime_error("host group: invalid port");
-		*out = new NeusHostGroup(rank, world, host ? host : "127.0.0.1", port);
+		*out = new NeusHostGroup(rank, world, host ? host : "127.0.0.1", port, job_token);
 	});
 }
 int neus_host_group_destroy(NeusHostGroup* g) { return guard([&] { delete g; }); }

@@ -1080,6 +1080,17 @@ class Testbed:
         return {"ms": float(ms.value), "launches": int(n.value), "steps": int(k.value),
                 "evaluated": int(self.stats()["evaluated_samples_total"] - s0)}
 
+    def set_exchange_timing(self, on=True):
+        """Data-parallel exchange timing (neus_testbed_set_exchange_timing): per step, how long the join before the
+        optimizer waits for the collectives (exposed) and the exchange's whole window; totals restart here."""
+        check(lib().neus_testbed_set_exchange_timing(self._h, C.c_int(1 if on else 0)))
+
+    def exchange_timing(self):
+        """dict of exposed_ms / span_ms totals and the steps they cover since set_exchange_timing(True)."""
+        e, sp, k = C.c_double(), C.c_double(), C.c_uint64()
+        check(lib().neus_testbed_exchange_timing(self._h, C.byref(e), C.byref(sp), C.byref(k)))
+        return {"exposed_ms": float(e.value), "span_ms": float(sp.value), "steps": int(k.value)}
+
     def phase_times(self):
         """Mean ms per profiled step for each of PHASES, plus (n_steps, mean Npre, mean Ntrain)."""
         n = len(PHASES)
@@ -1217,11 +1228,14 @@ class LocalGroup:
 class HostGroup:
     """Cross-process data-parallel group (neus_host_group_create): one per rank process; rank 0 listens on host:port, the
     others connect. The testbed's collectives are staged on its communication stream through pinned host memory and
-    exchanged over TCP (several ranks on one GPU, where RCCL refuses duplicate devices). Keep it alive while training."""
+    exchanged over TCP (several ranks on one GPU, where RCCL refuses duplicate devices). Keep it alive while training.
+    token: the per-job value every rank passes alike (rank 0 drops connections with another one; draw it at random and
+    hand it to the ranks with the port)."""
 
-    def __init__(self, rank: int, world: int, host: str = "127.0.0.1", port: int = 29533):
+    def __init__(self, rank: int, world: int, host: str = "127.0.0.1", port: int = 29533, token: int = 0):
         self._h = C.c_void_p()
-        check(lib().neus_host_group_create(C.c_int(rank), C.c_int(world), host.encode(), C.c_int(port), C.byref(self._h)))
+        check(lib().neus_host_group_create(C.c_int(rank), C.c_int(world), host.encode(), C.c_int(port), C.c_uint64(token),
+                                           C.byref(self._h)))
         self.rank, self.world = rank, world
 
     def join(self, tb):

@@ -113,6 +113,18 @@ class CpuTrainer:
             self.last = last
         return out
 
+    def grads_grid_mode(self, m, mode="ref_operand"):
+        """The same step's gradients with the hash-grid gradient summed under another semantics (oracle.set_grid_grad_mode:
+        "ref_operand" = each corner contribution rounded to fp16 as the reference's atomicAdd(__half2) operand,
+        grid.h:418-421). self.last is left as the exact step set it."""
+        last = self.last
+        try:
+            O.set_grid_grad_mode(mode)
+            return self.grads_from_march(m)
+        finally:
+            O.set_grid_grad_mode("exact")
+            self.last = last
+
     def finish(self, g, counters_sum=None):
         """Counters update (testbed_nerf.cu:3399-3438), RNG advance and the Ema(Adam) step."""
         W = self.world

@@ -370,12 +370,36 @@ static inline void atomic_add_d(double* p, double v) {
 	*p += v;
 }
 
+// Grid-gradient semantics (or_set_grid_grad_mode; test-only, used to bound the device's record rounding):
+//  0 = exact (default): every corner contribution summed unrounded in double;
+//  1 = the reference's atomic operand: each contribution rounded to fp16, `(__half)((float)grad[f] * weight)`
+//      (grid.h:418-421 for the first order, the same lambda at grid.h:926-929 for the second order with weight = -/+w),
+//      summed in double;
+//  2 = operand and accumulator in fp16: grad_t = __half (grid.h:1433), atomicAdd(__half2) - the adds land in the
+//      thread schedule's order, as the reference's atomics do, so this mode is not reproducible run to run.
+static int g_grid_grad_mode = 0;
+static uint16_t* g_grid_half = nullptr;  // mode 2: the fp16 grid gradient (the grid's parameter index space)
+static inline void half_atomic_add(uint16_t* p, uint16_t op) {
+	uint16_t old = __atomic_load_n(p, __ATOMIC_RELAXED);
+	for (;;) {
+		const uint16_t nv = f2h(h2f(old) + h2f(op));
+		if (__atomic_compare_exchange_n(p, &old, nv, true, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) return;
+	}
+}
+// one contribution `op32` (the reference's float product) to entry i of the level at parameter offset `off`
+static inline void grid_add(double* gg, size_t off, uint32_t i, double exact, float op32) {
+	if (g_grid_grad_mode == 0) atomic_add_d(&gg[i], exact);
+	else if (g_grid_grad_mode == 1) atomic_add_d(&gg[i], (double)rh(op32));
+	else half_atomic_add(g_grid_half + off + i, f2h(op32));
+}
+
 // kernel_grid_backward (grid.h:371-500) + kernel_grid_backward_input_backward_grid (grid.h:880-1007):
 // first-order dL/denc * w_corner, plus second-order g_f * (+/- scale * v_d * prod w_other).
 static void grid_scatter_one(const Net& n, const float x[3], uint32_t valid_level, const float* dL_denc, const float* g, const float* v, double* grad) {
 	for (uint32_t l = 0; l < n.c.n_levels && l <= valid_level; ++l) {
 		LevelPos lp = level_pos(n, l, x);
-		double* gg = grad + (size_t)lp.off * 2;
+		const size_t go = (size_t)lp.off * 2;
+		double* gg = grad + go;
 		if (dL_denc) {
 			for (uint32_t idx = 0; idx < 8; ++idx) {
 				float w = 1; uint32_t pl[3];
@@ -384,8 +408,8 @@ static void grid_scatter_one(const Net& n, const float x[3], uint32_t valid_leve
 					else { w *= lp.pos[d]; pl[d] = lp.grid[d] + 1; }
 				}
 				uint32_t i = grid_index(lp.hsize, lp.res, pl);
-				atomic_add_d(&gg[i], (double)dL_denc[2 * l] * w);
-				atomic_add_d(&gg[i + 1], (double)dL_denc[2 * l + 1] * w);
+				grid_add(gg, go, i, (double)dL_denc[2 * l] * w, dL_denc[2 * l] * w);
+				grid_add(gg, go, i + 1, (double)dL_denc[2 * l + 1] * w, dL_denc[2 * l + 1] * w);
 			}
 		}
 		if (g && v) {
@@ -399,11 +423,11 @@ static void grid_scatter_one(const Net& n, const float x[3], uint32_t valid_leve
 						else { w *= lp.pos[d]; pl[d] = lp.grid[d] + 1; }
 					}
 					pl[gd] = lp.grid[gd]; uint32_t il = grid_index(lp.hsize, lp.res, pl);
-					atomic_add_d(&gg[il], -(double)g[2 * l] * w);
-					atomic_add_d(&gg[il + 1], -(double)g[2 * l + 1] * w);
+					grid_add(gg, go, il, -(double)g[2 * l] * w, g[2 * l] * -w);
+					grid_add(gg, go, il + 1, -(double)g[2 * l + 1] * w, g[2 * l + 1] * -w);
 					pl[gd] = lp.grid[gd] + 1; uint32_t ir = grid_index(lp.hsize, lp.res, pl);
-					atomic_add_d(&gg[ir], (double)g[2 * l] * w);
-					atomic_add_d(&gg[ir + 1], (double)g[2 * l + 1] * w);
+					grid_add(gg, go, ir, (double)g[2 * l] * w, g[2 * l] * w);
+					grid_add(gg, go, ir + 1, (double)g[2 * l + 1] * w, g[2 * l + 1] * w);
 				}
 			}
 		}
@@ -682,6 +706,7 @@ extern "C" {
 
 uint32_t or_net_n_params(const OrNetCfg* c) { Net n(*c); return n.n_params; }
 void or_set_sum_order(int order) { g_sum_order = order; }
+void or_set_grid_grad_mode(int mode) { g_grid_grad_mode = mode; }
 void or_net_layout(const OrNetCfg* c, uint32_t* out) {
 	Net n(*c);
 	out[0] = n.n_density; out[1] = n.n_rgb; out[2] = n.grid_off; out[3] = n.n_grid_params; out[4] = n.var_off; out[5] = n.n_params; out[6] = n.n_matrix;
@@ -819,6 +844,8 @@ static void network_backward_impl(const OrNetCfg* c, const float* params, uint32
 	const int nt = omp_get_max_threads();
 	std::vector<std::vector<double>> Gm(nt);
 	std::vector<double> var_acc(nt, 0.0);
+	std::vector<uint16_t> Ghalf(g_grid_grad_mode == 2 ? n.n_grid_params : 0, (uint16_t)0);
+	g_grid_half = Ghalf.data();
 #pragma omp parallel
 	{
 		const int tid = omp_get_thread_num();
@@ -837,6 +864,9 @@ static void network_backward_impl(const OrNetCfg* c, const float* params, uint32
 		if (Gm[t].empty()) continue;
 		for (uint32_t i = 0; i < n.n_matrix; ++i) G[i] += Gm[t][i];
 	}
+	if (g_grid_grad_mode == 2)
+		for (uint32_t i = 0; i < n.n_grid_params; ++i) G[n.grid_off + i] = h2f(Ghalf[i]);
+	g_grid_half = nullptr;
 	for (uint32_t i = 0; i < n.n_params; ++i) grads[i] = (float)G[i];
 	grads[n.var_off] = rh((float)var);
 	for (int k = 1; k < 4; ++k) grads[n.var_off + k] = 0.0f;

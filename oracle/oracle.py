@@ -301,6 +301,18 @@ def set_sum_order(order):
     lib().or_set_sum_order(C.c_int(SUM_ORDERS[order] if isinstance(order, str) else int(order)))
 
 
+GRID_GRAD_MODES = {"exact": 0, "ref_operand": 1, "ref_half": 2}
+
+
+def set_grid_grad_mode(mode):
+    """Semantics of the hash-grid gradient sum (neus_oracle.cpp, or_set_grid_grad_mode). "exact" (the default): corner
+    contributions summed unrounded in double. "ref_operand": each contribution rounded to fp16 as the reference's
+    atomicAdd(__half2) operand (grid.h:418-421), summed in double. "ref_half": operand and accumulator in fp16
+    (grad_t = __half, grid.h:1433), adds in thread-schedule order like the reference's atomics (not reproducible).
+    Test-only: bounds how far the reference's own fp16 gradient path sits from the exact sum."""
+    lib().or_set_grid_grad_mode(C.c_int(GRID_GRAD_MODES[mode] if isinstance(mode, str) else int(mode)))
+
+
 class OrRenderCamera(C.Structure):
     _fields_ = [("xform", C.c_float * 12), ("focal", C.c_float * 2), ("screen_center", C.c_float * 2),
                 ("width", C.c_uint32), ("height", C.c_uint32)]

@@ -18,7 +18,7 @@ def main():
     tb = pyngp.Testbed(pyngp.TestbedMode.Nerf, device=0)
     tb.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
     tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=4096, fixed_rays_per_batch=rays)
-    group = pyngp.HostGroup(rank, world, "127.0.0.1", port)
+    group = pyngp.HostGroup(rank, world, "127.0.0.1", port, token=(port * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF)
     group.join(tb)
     tb.set_exchange_overlap(bool(overlap))
     tb.train_steps(steps)

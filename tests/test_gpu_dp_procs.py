@@ -138,3 +138,26 @@ def test_health_failure_on_one_rank_stops_every_rank(scene):
     assert s0["training_step"] == s1["training_step"] and s0["training_step"] % 16 == 0, (s0["training_step"], s1["training_step"])
     assert s0["training_aborted"] and s1["training_aborted"] and s1["health_flags"] & 1
     del tbs, group
+
+
+def test_health_failure_on_every_rank_names_its_cause(scene):
+    """the health words are summed over the ranks. The same march fault (STEP_FAIL_MARCH_T = 1) on both ranks
+    sums to 2, which read as a bit set would have named the look-back scan; both ranks must report the march."""
+    import ctypes as C
+    from neus2_amd import pyngp
+    from neus2_amd._lib import check, lib
+    group = pyngp.LocalGroup(2)
+    tbs = [_testbed(scene) for _ in range(2)]
+    for r, tb in enumerate(tbs):
+        group.join(tb, r)
+    errs = _parallel(lambda: tbs[0].train_steps(3), lambda: tbs[1].train_steps(3))
+    assert not any(errs), errs
+    for tb in tbs:
+        check(lib().neus_debug_inject_health(tb.handle, C.c_uint32(1)))
+    errs = _parallel(lambda: tbs[0].train_steps(40), lambda: tbs[1].train_steps(40))
+    for e in errs:
+        assert e is not None and "non-finite or negative t" in str(e) and "look-back scan" not in str(e), errs
+    s0, s1 = tbs[0].stats(), tbs[1].stats()
+    assert s0["training_step"] == s1["training_step"], (s0["training_step"], s1["training_step"])
+    assert s0["health_flags"] == s1["health_flags"] == 1, (s0["health_flags"], s1["health_flags"])
+    del tbs, group

@@ -285,6 +285,11 @@ def test_encoding_module_fp32(torch_cuda, layout):
     g = t.zeros(m.n_params, dtype=t.float32, device="cuda")
     dx = t.zeros((N, 3), dtype=t.float32, device="cuda")
     m.backward(ctx, x, dly_dev, params, dL_dparams=g, dL_dinput=dx, mode=GradientMode.Overwrite)
+    # dL_dinput summed per sample in feature order (kernel_grid_backward_input, grid.h:804-830): bitwise the same on a
+    # second call (it was a float-atomic sum over the levels)
+    dx2 = t.full((N, 3), 3.0, dtype=t.float32, device="cuda")
+    m.backward(ctx, x, dly_dev, params, dL_dinput=dx2, mode=GradientMode.Ignore)
+    np.testing.assert_array_equal(dx2.cpu().numpy(), dx.cpu().numpy())
     rel_p, cos_p = _rel_cos(g.cpu().numpy(), g_tab.detach().numpy().ravel())
     rel_x, _ = _rel_cos(dx.cpu().numpy(), g_x.detach().numpy())
     g2 = t.full((m.n_params,), 7.0, dtype=t.float32, device="cuda")  # Overwrite must not read the old contents

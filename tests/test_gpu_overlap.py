@@ -1,0 +1,130 @@
+"""Work issued beside the backward must not change a bit (round 6):
+* the next step's ray sampling (the lookahead) with a data-parallel group: the step's counters are all-reduced right
+  after the loss (StepState::compacted_global), so the sampling no longer waits for the whole exchange;
+* the optimizer in pieces beside the grid scatter (NEUS_ADAM_OVERLAP=1): the MLP blocks after the weight-gradient
+  reduction, each grid level group after its accumulation launch.
+Each is compared bitwise with the same training without it. Reference: testbed_nerf.cu:3723-4001 (the step),
+adam.h:51-160 (elementwise Adam)."""
+import contextlib
+import os
+import sys
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+BATCH = 4096
+
+
+@contextlib.contextmanager
+def _env(**kv):
+    old = {k: os.environ.get(k) for k in kv}
+    os.environ.update({k: str(v) for k, v in kv.items()})
+    try:
+        yield
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def _testbed(sc, fixed_rays=0):
+    from neus2_amd import pyngp
+    tb = pyngp.Testbed(pyngp.TestbedMode.Nerf)
+    tb.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
+    tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=BATCH, fixed_rays_per_batch=fixed_rays)
+    return tb
+
+
+def _parallel(*fns):
+    errs = []
+
+    def run(f):
+        try:
+            f()
+        except Exception as e:  # noqa: BLE001 - re-raised below
+            errs.append(e)
+
+    ts = [threading.Thread(target=run, args=(f,)) for f in fns]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=300)
+    assert not any(t.is_alive() for t in ts), "a rank did not finish"
+    if errs:
+        raise errs[0]
+
+
+def _same(a, b):
+    np.testing.assert_array_equal(a.get_params().view(np.uint32), b.get_params().view(np.uint32))
+    np.testing.assert_array_equal(a.get_gradients().view(np.uint32), b.get_gradients().view(np.uint32))
+    np.testing.assert_array_equal(a.get_ema_params().view(np.uint32), b.get_ema_params().view(np.uint32))
+    np.testing.assert_array_equal(a.get_density_grid()[0].view(np.uint32), b.get_density_grid()[0].view(np.uint32))
+    sa, sb = a.stats(), b.stats()
+    for k in ("training_step", "rays_per_batch", "measured_batch_size", "n_rays_total", "loss"):
+        assert sa[k] == sb[k], (k, sa[k], sb[k])
+
+
+@pytest.fixture(scope="module")
+def scene(torch_cuda):
+    from neus2_amd import scenes
+    return scenes.small_scene(n_views=8, width=64, height=48)
+
+
+def test_adam_overlap_bitwise(scene):
+    """300 steps in one call (the progressive level changes, the occupancy updates and their cadence change at step 256,
+    the lookahead) with the optimizer split beside the scatter and without: bitwise the same parameters, gradients, EMA
+    weights, occupancy grid and counters."""
+    with _env(NEUS_ADAM_OVERLAP=1):
+        a = _testbed(scene)
+    with _env(NEUS_ADAM_OVERLAP=0):
+        b = _testbed(scene)
+    a.train_steps(300)
+    b.train_steps(300)
+    assert a.stats()["adam_split_steps"] == 300 and b.stats()["adam_split_steps"] == 0
+    assert a.stats()["lookahead_steps"] > 0
+    _same(a, b)
+
+
+def test_dp_lookahead_bitwise(scene):
+    """Two ranks (in-process group, host-staged collectives) with the lookahead on - it now runs beside the backward at
+    any world size - against two ranks with it off (NEUS_LOOKAHEAD=0): 40 steps in one call each, bitwise the same on
+    every rank; the lookahead ran."""
+    from neus2_amd import pyngp
+    R = 2048
+    ga = pyngp.LocalGroup(2)
+    a = [_testbed(scene, R) for _ in range(2)]
+    with _env(NEUS_LOOKAHEAD=0):
+        gb = pyngp.LocalGroup(2)
+        b = [_testbed(scene, R) for _ in range(2)]
+    for r in range(2):
+        ga.join(a[r], r)
+        gb.join(b[r], r)
+    _parallel(lambda: a[0].train_steps(40), lambda: a[1].train_steps(40))
+    _parallel(lambda: b[0].train_steps(40), lambda: b[1].train_steps(40))
+    assert a[0].stats()["lookahead_steps"] > 0 and a[1].stats()["lookahead_steps"] > 0
+    assert b[0].stats()["lookahead_steps"] == 0
+    for x in (a[1], b[0], b[1]):
+        _same(a[0], x)
+    del ga, gb
+
+
+def test_rccl_world1_lookahead_bitwise(scene):
+    """A world-1 RCCL communicator (collectives forced on) now takes the lookahead too, its counters all-reduced on the
+    communication stream before the sampling starts: bitwise the testbed without a communicator."""
+    from neus2_amd import pyngp
+    R = 2048
+    plain = _testbed(scene, R)
+    comm = _testbed(scene, R)
+    comm.init_data_parallel(0, 1, pyngp.nccl_unique_id(), force_collectives=True)
+    plain.train_steps(40)
+    comm.train_steps(40)
+    assert comm.stats()["lookahead_steps"] > 0
+    _same(plain, comm)

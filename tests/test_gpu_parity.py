@@ -282,12 +282,15 @@ def test_sample_rays_block_grid_bit_exact(env):
     assert nk > 1000, nk
 
 
-def test_loss_compaction_parity(env):
-    """Composite/loss/compaction on fixed network outputs: compaction bit-exact, dL/dout fp16-close."""
+@pytest.mark.parametrize("n_rays", [4096, 1000])
+def test_loss_compaction_parity(env, n_rays):
+    """Composite/loss/compaction on fixed network outputs: compaction bit-exact, dL/dout fp16-close. 1000 rays: a ray
+    count that is not a multiple of the wave (k_loss_ray's wave-wide sample-map fill masks the lanes past
+    the last ray instead of refusing the call)."""
     t, O, tb = env["t"], env["O"], env["tb"]
     lib, check = L()
     bf = _bitfield(env)
-    n_rays, max_s = 4096, 4096 * 16
+    max_s = n_rays * 16
     rs, ri = 0x0BADF00D12345678, 0xDA3E39CB94B95BDB | 1
     r_rays, r_ns, r_co, r_cnt, _ = O.generate_samples(env["ds"], bf, n_rays, 0, rs, ri, max_s)
     nk = int(r_ns[:, 0].sum())

@@ -41,6 +41,50 @@ def scene(torch_cuda):
     return scenes.small_scene(n_views=8, width=64, height=48)
 
 
+@pytest.mark.parametrize("beta2", [0.99999, 0.99])
+def test_optimizer_step_counts_width(scene, torch_cuda, beta2):
+    """per-parameter Adam step counts (uint32 in the reference, adam.h:106). With betas whose bias correction has
+    not converged by step 4096 (beta2 = 0.99999) the device keeps them in 32 bits: a state with counts far above 65535
+    round-trips exactly, and one step at those counts matches the oracle's Adam (bias correction at the true count). With
+    the default betas (0.99: converged) they are 16-bit and read back saturated at 65535, and the step still matches the
+    oracle at the true counts, since every count past 4095 gives the same update."""
+    import oracle as O
+    from neus2_amd import config as _config
+    from neus2_amd import pyngp
+    t = torch_cuda
+    lib, check = _lib()
+    cfg = _config.load_json(os.path.join(ROOT, "configs", "nerf", "base.json"))
+    cfg["optimizer"]["nested"]["nested"]["beta2"] = beta2
+    tb = pyngp.Testbed(pyngp.TestbedMode.Nerf)
+    tb.set_dataset(scene["images"], scene["focal"], scene["principal"], scene["xforms"], 1)
+    tb.reload_network_from_json(cfg, batch_size=BATCH)
+    lay = tb.layout()
+    P, n_matrix = lay["n_params"], lay["n_matrix"]
+    rng = np.random.default_rng(4)
+    st = tb.get_optimizer_state()
+    steps = rng.integers(0, 200000, P).astype(np.uint32)
+    steps[:64] = 65535 + np.arange(64, dtype=np.uint32)
+    # moments of a unit-variance gradient (the step's gradient / loss scale below): updates of O(lr)
+    m1 = rng.normal(0, 0.1, P).astype(np.float32)
+    m2 = rng.uniform(0.5, 1.5, P).astype(np.float32)
+    st.update(current_step=10, param_steps=steps, m1=m1, m2=m2)
+    tb.set_optimizer_state(st)
+    back = tb.get_optimizer_state()["param_steps"]
+    wide = beta2 == 0.99999
+    np.testing.assert_array_equal(back, steps if wide else np.minimum(steps, 65535))
+    w = tb.get_params().copy()
+    g = rng.normal(0, 1.0, P).astype(np.float32) * 128.0
+    g[rng.random(P) < 0.3] = 0.0
+    check(lib.neus_optimizer_step(tb.handle, None, ptr(dev(t, g))))
+    s_o, e_tmp, e_out = steps.copy(), np.zeros(P, np.float32), np.zeros(P, np.float32)
+    O.adam_ema_step(w, g, m1, m2, s_o, e_tmp, e_out, n_matrix, 11, lr=1e-3, beta1=0.9, beta2=beta2, eps=1e-15, l2=1e-6)
+    got = tb.get_params()
+    dw = np.abs(got - w) / np.maximum(np.abs(w), 1e-3)
+    assert dw.max() <= 2e-6, (dw.argmax(), got[dw.argmax()], w[dw.argmax()])
+    back = tb.get_optimizer_state()["param_steps"]
+    np.testing.assert_array_equal(back, s_o if wide else np.minimum(s_o, 65535))
+
+
 def test_optimizer_step_parity(scene, torch_cuda):
     """Trainer::optimizer_step = Ema(ExponentialDecay(Adam)) (adam.h:51-160, ema.h:45-110) for three steps
     against or_adam_ema_step: fp32 master weights and the fp32 EMA within 2e-6 relative to max(|w|, lr) (device
@@ -280,7 +324,7 @@ FLOOR_ORDERS = ("reversed", "pairwise", "blocked")
 
 
 def _teacher_forced_all_levels(sc, tag, progressive, n_steps=14, prepare=700, short_step=5, fixed_rays=False, prepare_batch=None,
-                               batch=BATCH, floor_factor=1.5):
+                               batch=BATCH, floor_factor=1.5, level_bar=True):
     """Teacher-forced training at the all-levels state: the device trains `prepare` free-running steps
     first, so all 14 levels are active (hashed levels 5-13: 2^19-entry tables, the 2048-entry region scatter of hashed
     buckets) and the occupancy grid is shaped by hundreds of updates. Then n_steps consecutive steps, each compared with
@@ -288,7 +332,9 @@ def _teacher_forced_all_levels(sc, tag, progressive, n_steps=14, prepare=700, sh
     the rays, so its compacted count is below the batch and the rollover fused into k_grid_encode fills the rest
     (fill_rollover_and_rescale, common_device.h:515-535). Per step: the march bit-exact, the compacted count equal up to
     fp16-moved cut-offs, every gradient block cos >= 0.9999 and rel-L2 <= max(2e-3, floor_factor x the noise floor); per
-    hash level the worst rel-L2 is recorded. The noise floor of a block is the largest rel-L2 between the oracle's step and
+    hash level the worst rel-L2 is asserted the same way against that level's floor (round 6; level_bar) and recorded beside
+    the distance of the reference's own fp16 operand (each corner contribution rounded to fp16, grid.h:418-421: the
+    oracle's "ref_operand" mode) from the exact sum. The noise floor of a block is the largest rel-L2 between the oracle's step and
     the same oracle step with the network's layer products summed in another order (reversed, pairwise, blocked): the
     spread any fp32 accumulation order has on a network with fp16 activations. progressive: None leaves the auto rule on
     (asserted to have run the rounds), 2 forces the rounds. fixed_rays: R fixed at this many rays every step
@@ -331,7 +377,8 @@ def _teacher_forced_all_levels(sc, tag, progressive, n_steps=14, prepare=700, sh
     worst = {k: [1.0, 0.0] for k in blocks}
     floor = {k: 0.0 for k in blocks}
     floor_by_order = {o: {k: 0.0 for k in blocks} for o in FLOOR_ORDERS}
-    lev_rel, lev_floor = np.zeros(cfg.n_levels), np.zeros(cfg.n_levels)
+    lev_rel, lev_floor, lev_refop = np.zeros(cfg.n_levels), np.zeros(cfg.n_levels), np.zeros(cfg.n_levels)
+    var_cond = 0.0  # the variance gradient's conditioning bar (below)
     prog0 = tb.stats()["progressive_steps"]
     short_seen, n_comp_equal, later_rounds, evaluated, kept = False, 0, 0, 0, 0
     records = []
@@ -369,6 +416,12 @@ def _teacher_forced_all_levels(sc, tag, progressive, n_steps=14, prepare=700, sh
         m = tr.march(skip_occupancy=True)
         gr = tr.grads_from_march(m).astype(np.float64)
         alt = {o: v.astype(np.float64) for o, v in tr.grads_alt_orders(m).items()}
+        g_refop = tr.grads_grid_mode(m, "ref_operand").astype(np.float64)
+        # the variance gradient is one batch sum of the fp16 dL/doutput[7] (nerf_network.h:461-474): each term is rounded
+        # to fp16 from an fp32 value that the network outputs' fp16 noise moves, so two implementations can differ by an
+        # fp16 ulp (2^-10 relative) per term; relative to the sum that is 2^-10 sum|x| / |sum x|, large when the terms cancel
+        dl7 = tr.last["dL_dout"].view(np.float16)[:, 7].astype(np.float64)
+        var_cond = max(var_cond, 2.0 ** -10 * np.abs(dl7).sum() / max(abs(dl7.sum()), 1e-30))
         _progress(f"{tag}: step {k + 1}/{n_steps} compared")
         kept += tr.last["n_kept"]
         # per-ray sample counts of the march, bit-exact over the kept ray slots (canonical ray order; past the kept extent
@@ -410,6 +463,7 @@ def _teacher_forced_all_levels(sc, tag, progressive, n_steps=14, prepare=700, sh
             if np.linalg.norm(y) > 0:
                 lev_rel[l] = max(lev_rel[l], np.linalg.norm(g[a:b] - y) / np.linalg.norm(y))
                 lev_floor[l] = max(lev_floor[l], max(np.linalg.norm(ga[a:b] - y) for ga in alt.values()) / np.linalg.norm(y))
+                lev_refop[l] = max(lev_refop[l], np.linalg.norm(g_refop[a:b] - y) / np.linalg.norm(y))
         records.append(rec)
     prog = tb.stats()["progressive_steps"] - prog0
     _record(f"teacher_forced_all_levels_{tag}", steps=n_steps, start_step=prepare, batch=batch, compacted_equal_steps=n_comp_equal,
@@ -419,7 +473,8 @@ def _teacher_forced_all_levels(sc, tag, progressive, n_steps=14, prepare=700, sh
             **{f"max_rel_grid_L{l}": lev_rel[l] for l in range(cfg.n_levels)},
             **{f"floor_rel_{k}": v for k, v in floor.items()},
             **{f"floor_{o}_{k}": v for o, d in floor_by_order.items() for k, v in d.items()},
-            **{f"floor_rel_grid_L{l}": lev_floor[l] for l in range(cfg.n_levels)})
+            **{f"floor_rel_grid_L{l}": lev_floor[l] for l in range(cfg.n_levels)},
+            **{f"ref_operand_rel_grid_L{l}": lev_refop[l] for l in range(cfg.n_levels)}, variance_conditioning_bar=var_cond)
     st = tb.stats()
     assert prog >= n_steps - 1, (f"progressive inference ran on {prog} of {n_steps} steps (last step: {st['measured_batch_size']} "
                                  f"compacted of {st['measured_batch_size_before_compaction']} requested)")
@@ -430,7 +485,14 @@ def _teacher_forced_all_levels(sc, tag, progressive, n_steps=14, prepare=700, sh
     # alternative summation orders (a converged state's gradients are sums of nearly cancelling fp16 terms: their rel-L2
     # floor rises above 2e-3)
     for name, (cos, rel) in worst.items():
-        assert cos >= 0.9999 and rel <= max(2e-3, floor_factor * floor[name]), (name, cos, rel, floor[name])
+        bar = max(2e-3, floor_factor * floor[name], var_cond if name == "variance" else 0.0)
+        assert cos >= 0.9999 and rel <= bar, (name, cos, rel, floor[name], bar)
+    # per hash level: the fine levels' gradient is a sum of contributions far below fp16's normal range
+    # at small loss scales; the device's scaled records (grid.hip, record format) must keep each level at the floor
+    if level_bar:
+        bad = [(l, float(lev_rel[l]), float(lev_floor[l])) for l in range(cfg.n_levels)
+               if lev_rel[l] > max(2e-3, floor_factor * lev_floor[l])]
+        assert not bad, f"per-level grid rel-L2 above max(2e-3, {floor_factor} x floor): {bad}"
     return tb, records
 
 
