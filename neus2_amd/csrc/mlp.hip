@@ -1821,7 +1821,7 @@ uint32_t mlp_train_blocks(uint32_t L, uint32_t W, uint32_t n) {
 	NEUS_MLP_CONFIGS(X)
 #undef X
 	static const uint32_t pct = [] { const char* e = std::getenv("NEUS_MLP_BLOCKS_PCT"); return e ? (uint32_t)std::atoi(e) : 100u; }();
-	if (pct > 0 && pct < 100) cap = std::max<uint32_t>(1, cap * pct / 100);  // development: a smaller persistent grid
+	if (pct > 0 && pct != 100) cap = std::max<uint32_t>(1, cap * pct / 100);  // development: a smaller (or over-decomposed) grid
 	return std::max<uint32_t>(1, std::min<uint32_t>((n + 127) / 128, cap));
 }
 void launch_mfma_probe(hipStream_t s, const half_t* A, const half_t* B, float* C) { k_mfma_probe<<<1, 64, 0, s>>>(A, B, C); }

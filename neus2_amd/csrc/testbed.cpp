@@ -187,7 +187,9 @@ struct NeusTestbed {
 	// between steps of one neus_testbed_train call (nothing pending between calls), at one rank, on static scenes, and
 	// not before a step that starts with an occupancy update or a loss readback (train_step: la_go).
 	bool la_on = [] { const char* e = std::getenv("NEUS_LOOKAHEAD"); return !(e && e[0] == '0'); }();
-	struct AdamSplit { AdamParams p; uint32_t next; };  // adam_overlap: the step's Adam parameters; next: first parameter not issued
+	// adam_overlap: the step's Adam parameters; next: the first parameter not issued; on: the exchange stream the pieces
+	// follow their ranges' all-reduces on (data parallel), or null (one rank: ad_stream, behind the step's stream)
+	struct AdamSplit { AdamParams p; uint32_t next; hipStream_t on; };
 	bool la_pending = false, la_next_in_call = false;
 	uint64_t la_steps = 0, adam_split_steps = 0;  // (stats: lookahead_steps, adam_split_steps)
 	const bool la_stat = [] { const char* e = std::getenv("NEUS_LA_STAT"); return e && e[0] == '1'; }();
@@ -528,7 +530,6 @@ struct NeusTestbed {
 		if (la_stream) { (void)hipStreamSynchronize(la_stream); (void)hipStreamDestroy(la_stream); }
 		if (ev_la_start) (void)hipEventDestroy(ev_la_start);
 		if (ev_la_done) (void)hipEventDestroy(ev_la_done);
-		if (ad_stream) { (void)hipStreamSynchronize(ad_stream); (void)hipStreamDestroy(ad_stream); }
 		for (auto& e : ad_ev) if (e) (void)hipEventDestroy(e);
 		if (ad_done) (void)hipEventDestroy(ad_done);
 		for (auto& e : xt_ev) for (auto& x : e) if (x) (void)hipEventDestroy(x);
@@ -1044,19 +1045,24 @@ struct NeusTestbed {
 		// the MLP weight gradients were accumulated inside the training kernels: one small fixed-order reduction
 		launch_mlp_grad_reduce(s, grad_reduce(n, g, n_train_ptr));
 		la_fire(3);
-		if (as) adam_issue(*as, lay.grid_off, g, true);  // the MLP blocks (and their transposed copies) beside the scatter
 		if (exchange) {  // the MLP blocks and the variance are final: their exchange runs beside the grid scatter
 			hipStream_t xs = x_stream();
 			allreduce_f32(g, lay.grid_off, false, xs);
 			allreduce_f32(g + lay.var_off, lay.P - lay.var_off, false, xs);
+			if (as) as->on = xs;  // (the optimizer's pieces follow their ranges' all-reduces on the exchange stream)
 		}
+		if (as) adam_issue(*as, lay.grid_off, g, true);  // the MLP blocks (and their transposed copies) beside the scatter
 		if (marks) mark(7);
 		const ScatterWork sw = scatter_work_for(g + lay.grid_off, valid, s);
 		ScatterSplit sp = exchange && sw.mode == 2 ? x_split(valid, g + lay.grid_off) : ScatterSplit{};
-		const bool a_split = as && !exchange && sw.mode == 2;
-		if (a_split) {  // the level groups of the overlapped exchange; each group's Adam once its accumulation is queued
-			sp = x_split(valid, g + lay.grid_off);
-			sp.done = [this, as, g](uint32_t, uint32_t hi) { adam_issue(*as, lay.grid_off + 2 * gl.offset[hi], g, false); };
+		const bool a_split = as && sw.mode == 2;
+		if (a_split) {  // the level groups of the overlapped exchange; each group's Adam once its accumulation (and exchange) is queued
+			if (!exchange) sp = x_split(valid, g + lay.grid_off);
+			auto xdone = exchange ? sp.done : std::function<void(uint32_t, uint32_t)>();
+			sp.done = [this, as, g, xdone](uint32_t lo, uint32_t hi) {
+				if (xdone) xdone(lo, hi);
+				adam_issue(*as, lay.grid_off + 2 * gl.offset[hi], g, false);
+			};
 		}
 		launch_grid_scatter(s, n_train_ptr, n, ld, c, COORD_W, gl, valid, tbuf.dLdenc, tbuf.genc, tbuf.v, g + lay.grid_off, sw, scan_tmp.p,
 		                    scan_tmp_bytes, (exchange || a_split) && sw.mode == 2 ? &sp : nullptr);
@@ -1219,30 +1225,38 @@ struct NeusTestbed {
 	// parameters are bitwise those of the one launch. Cut points are rounded down to 4 parameters (the kernel's 16-B
 	// groups): a range may start with the last few parameters of the level before it, whose gradient is final already.
 	bool adam_overlap = [] { const char* e = std::getenv("NEUS_ADAM_OVERLAP"); return e && e[0] == '1'; }();
+	// ad_stream is the step's side stream (aux_stream, created with the step's stream at its priority): a stream of its own
+	// would be a fifth HIP stream of the process over GPU_MAX_HW_QUEUES = 4 hardware queues and share one - measured
+	// 1.12 -> 1.99 ms/step when it landed behind the lookahead's low-priority march (profiles/r06b_adam_overlap_ab.txt)
 	hipStream_t ad_stream = nullptr;
 	hipEvent_t ad_ev[8] = {}, ad_done = nullptr;
 	int ad_n = 0;
 	void adam_issue(AdamSplit& a, uint32_t hi, const float* g, bool with_tr) {
 		if (!ad_stream) {
-			if (main_prio) HIP_CHECK(hipStreamCreateWithPriority(&ad_stream, hipStreamNonBlocking, main_prio));
-			else HIP_CHECK(hipStreamCreateWithFlags(&ad_stream, hipStreamNonBlocking));
+			ad_stream = aux_stream;
 			for (auto& e : ad_ev) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
 			HIP_CHECK(hipEventCreateWithFlags(&ad_done, hipEventDisableTiming));
 		}
 		hi = hi >= lay.P ? lay.P : hi / 4 * 4;
 		if (hi <= a.next) return;
-		hipEvent_t e = ad_ev[ad_n++ % 8];
-		HIP_CHECK(hipEventRecord(e, stream));
-		HIP_CHECK(hipStreamWaitEvent(ad_stream, e, 0));
+		hipStream_t on = a.on;
+		if (!on) {
+			hipEvent_t e = ad_ev[ad_n++ % 8];
+			HIP_CHECK(hipEventRecord(e, stream));
+			HIP_CHECK(hipStreamWaitEvent(ad_stream, e, 0));
+			on = ad_stream;
+		}
 		const AdamTranspose tr = with_tr ? adam_transpose() : AdamTranspose{};
-		launch_adam_ema_range(ad_stream, a.p, a.next, hi, params_fp.p, params_h.p, g, m1.p, m2.p, adam_steps.p, steps32, ema_tmp.p, ema_h.p,
+		launch_adam_ema_range(on, a.p, a.next, hi, params_fp.p, params_h.p, g, m1.p, m2.p, adam_steps.p, steps32, ema_tmp.p, ema_h.p,
 		                      with_tr ? &tr : nullptr);
 		a.next = hi;
 	}
 	void adam_join(AdamSplit& a, const float* g) {
 		adam_issue(a, lay.P, g, false);  // (whatever is left: the levels past the valid one, the variance)
-		HIP_CHECK(hipEventRecord(ad_done, ad_stream));
-		HIP_CHECK(hipStreamWaitEvent(stream, ad_done, 0));
+		if (!a.on) {  // (on the exchange stream the step's x_join has waited for every piece already)
+			HIP_CHECK(hipEventRecord(ad_done, ad_stream));
+			HIP_CHECK(hipStreamWaitEvent(stream, ad_done, 0));
+		}
 		if (a.p.skip_ema_h) ema_h_stale = true;
 	}
 	// bias-correction table for the config's betas (rebuilt only when they change), and the step counts' width for it:
@@ -1708,7 +1722,7 @@ struct NeusTestbed {
 		// the overlapped exchange (xo): the canonical backward all-reduces its gradient ranges as they finish; adam_overlap
 		// (one rank, static scenes): the optimizer step in pieces beside the scatter
 		AdamSplit asp{};
-		const bool a_over = adam_overlap && !coll_on() && !dyn;
+		const bool a_over = adam_overlap && !dyn && (!coll_on() || xo);
 		if (a_over) asp.p = adam_params();
 		if (use_delta) {
 			// the training forward runs on the deformed batch; dL/d(position) feeds the DeltaNetwork backward
@@ -1749,6 +1763,7 @@ struct NeusTestbed {
 			if (use_delta) allreduce_f32(delta_partial.p, delta_partial_floats(), false, xs);
 			if (get_loss) { allreduce_f32(loss_sum.p, 3, false, xs); allreduce_u32(health_buf.p, 2, xs); }
 			coll_end();
+			if (a_over) adam_issue(asp, lay.P, grads.p, false);  // the optimizer's last piece, behind the exchange
 			if (xt) HIP_CHECK(hipEventRecord(xt[2], xs));
 			x_join();
 		}

@@ -81,7 +81,17 @@ def group_stats(pos, ray, n_levels, off, res, scale, grid_byte0, rng):
             "lines_per_gather_instruction_by_pair": [round(v, 2) for v in pairs], "lines_per_gather_instruction": round(float(np.mean(pairs)), 2)}
 
 
-def state(tb, cfg, off, res, scale, grid_byte0, rng):
+def kept_views(step_n_rays_total, extent, n_img, xforms, R=1 << 18):
+    """The training views of the kept ray prefix: image_idx (march_common.h, the reference's uint32 arithmetic,
+    testbed_nerf.cu:1291) of the slots [0, extent), with each view's forward direction (-z column of its camera-to-world)."""
+    i = np.arange(extent, dtype=np.uint64)
+    v = ((((i + np.uint64(step_n_rays_total)) * np.uint64(n_img)) & np.uint64(0xFFFFFFFF)) // np.uint64(R) % np.uint64(n_img)).astype(int)
+    ims, cnt = np.unique(v, return_counts=True)
+    X = np.asarray(xforms, np.float64).reshape(n_img, 3, 4)
+    return [{"view": int(k), "rays": int(c), "forward": (-X[k][:, 2]).round(3).tolist()} for k, c in zip(ims, cnt)]
+
+
+def state(tb, cfg, off, res, scale, grid_byte0, rng, sc=None):
     R = 1 << 18
     st = tb.stats()
     nreq, cc, _ = tb.ray_counts(R)
@@ -111,7 +121,15 @@ def state(tb, cfg, off, res, scale, grid_byte0, rng):
     step = d < 1.5 * dt
     out["consecutive"] = {"frac_constant_step": round(float(step.mean()), 4), "runs_per_ray": round(float((~step).sum() + m.sum()) / max(1, m.sum()), 2),
                           "mean_run_samples": round(n_kept / float((~step).sum() + m.sum()), 2),
-                          "median_jump": round(float(np.median(d[~step])) if (~step).any() else 0.0, 5)}
+                          "median_jump": round(float(np.median(d[~step])) if (~step).any() else 0.0, 5),
+                          "step_over_dt_percentiles_1_10_50_90": [round(float(v), 4) for v in np.percentile(d[step] / dt, [1, 10, 50, 90])],
+                          "frac_step_below_half_dt": round(float((d[step] < 0.5 * dt).mean()), 4),
+                          "frac_zero_step": round(float((d == 0).mean()), 4),
+                          # the grid axis the rays step along (mean |delta| per axis of a constant step, warped coordinates):
+                          # the hash's x prime is 1, so steps along x stay inside a 128-B line of a hashed table
+                          "mean_abs_step_xyz_over_dt": (np.abs(co[1:, :3] - co[:-1, :3])[same][step].mean(0) / dt).round(3).tolist()}
+    if sc is not None:  # the last step's views (its n_rays_total: the counter before that step's update)
+        out["kept_views"] = kept_views(int(st["n_rays_total"]) - R, extent, len(sc["xforms"]), sc["xforms"])
     out["march_order"] = group_stats(co[:, :3], ray, cfg.n_levels, off, res, scale, grid_byte0, rng)
     # round 0 of the progressive rounds: the first e samples of every kept ray, rays by the Morton key of the 8^3 cell of
     # their first sample (k_ray_hist / k_ray_sort_place)
@@ -143,7 +161,7 @@ def main():
         tb.train_steps(s - done)
         tb.synchronize()
         done = s
-        r = state(tb, cfg, off, res, scale, grid_byte0, rng)
+        r = state(tb, cfg, off, res, scale, grid_byte0, rng, sc)
         res_all.append(r)
         print(json.dumps(r), flush=True)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)

@@ -128,3 +128,26 @@ def test_rccl_world1_lookahead_bitwise(scene):
     comm.train_steps(40)
     assert comm.stats()["lookahead_steps"] > 0
     _same(plain, comm)
+
+
+def test_dp_adam_overlap_bitwise(scene):
+    """Data parallel with the optimizer in pieces, each behind its range's all-reduce on the exchange stream (the MLP blocks,
+    then every grid level group, the rest after the last collective), against the one Adam launch after the exchange:
+    two world-2 groups, 40 steps, bitwise the same on every rank."""
+    from neus2_amd import pyngp
+    R = 2048
+    with _env(NEUS_ADAM_OVERLAP=1):
+        ga = pyngp.LocalGroup(2)
+        a = [_testbed(scene, R) for _ in range(2)]
+    with _env(NEUS_ADAM_OVERLAP=0):
+        gb = pyngp.LocalGroup(2)
+        b = [_testbed(scene, R) for _ in range(2)]
+    for r in range(2):
+        ga.join(a[r], r)
+        gb.join(b[r], r)
+    _parallel(lambda: a[0].train_steps(40), lambda: a[1].train_steps(40))
+    _parallel(lambda: b[0].train_steps(40), lambda: b[1].train_steps(40))
+    assert a[0].stats()["adam_split_steps"] == 40 and b[0].stats()["adam_split_steps"] == 0
+    for x in (a[1], b[0], b[1]):
+        _same(a[0], x)
+    del ga, gb
