@@ -211,7 +211,8 @@ def step_roofline(d, levels, n_params, ms_per_step, steps, adam_b=None):
 
 def work_counters(st):
     return {"rays": st["rays_total"], "pre": st["pre_samples_total"], "evaluated": st["evaluated_samples_total"],
-            "occ_samples": st["occ_samples_total"], "occ_updates": st["occ_updates"], "progressive": st["progressive_steps"]}
+            "occ_samples": st["occ_samples_total"], "occ_updates": st["occ_updates"], "progressive": st["progressive_steps"],
+            "cut": st["cut_steps"]}
 
 
 def free_port():
@@ -451,6 +452,9 @@ def main():
         # gathers each move a 128-B line from the Infinity Cache, so this, not the algorithmic rate, is what binds
         "line_traffic": line_traffic(measured_traffic(dom, levels), dk["ms"], dk["bytes"]),
         "progressive_steps_timed": d["progressive"],
+        # steps whose later progressive rounds skipped the rays past the compaction cut (their network outputs
+        # feed no training sample; the trained parameters are bitwise those without the cut, NEUS_PROG_CUT=0)
+        "compaction_cut_steps_timed": d["cut"],
         "progressive_chunk_end": st["progressive_chunk_end"],
         "non_rollover_fraction": round(d["trained_real"] / max(1, batch * args.steps), 4),
         **({"exchange": {**d["exchange"], **rccl_info(args, rank)}} if "exchange" in d else {}),

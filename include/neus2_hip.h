@@ -131,6 +131,8 @@ typedef struct NeusTrainStats {
 	                                           * by default; neus_testbed_set_progressive_inference) */
 	uint64_t lookahead_steps;                 /* (ABI 5) steps whose ray sampling was issued beside the step before them */
 	uint64_t adam_split_steps;                /* (ABI 5) steps whose optimizer ran in pieces beside the scatter (adam_overlap) */
+	uint64_t cut_steps;                       /* (ABI 5) steps whose later progressive rounds skipped the rays past the
+	                                           * compaction cut (fixed rays per batch; never a step the host reads back) */
 } NeusTrainStats;
 
 /* Testbed::render_to_cpu (python_api.cu:123-169) after set_camera_to_training_view (testbed.cu:264-270). */

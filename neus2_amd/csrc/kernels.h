@@ -309,9 +309,16 @@ struct Round0List { uint32_t e1; uint32_t* c0; uint32_t* list; uint32_t* counter
 // order, *n_perm of them
 constexpr uint32_t RS_BINS = 512;
 struct RaySort { uint32_t* hist; uint32_t* off; uint16_t* key; uint32_t* perm; uint32_t* n_perm; };
+// The split of round 0 for the compaction cut (est != null; NeusTestbed::prog_cut): the rays of the slots below *est first
+// (pass A: perm [0, n_perm), list [0, list_len)), the rest apart (pass B: perm from perm_b, list from list_b, their counts in
+// cutw[CW_NB] / cutw[CW_LENB]); ccount zeroed for the slots without samples or past *est (pass A's cut reads it); rays
+// without samples are left out of both passes. hist / off then hold [2][2 RS_BINS + 1][blocks].
+struct RaySplit { const uint32_t* est; uint32_t* ccount; uint32_t* cutw; uint32_t perm_b, list_b; };
+// cutw words (march.hip k_prog_cut)
+constexpr uint32_t CW_CUT = 0, CW_LENB_EFF = 1, CW_NB_EFF = 2, CW_CUT_A = 3, CW_LENB = 4, CW_NB = 5, CW_EST = 6, CW_WORDS = 16;
 uint32_t ray_sort_blocks(uint32_t cap);
 void launch_ray_sort(hipStream_t s, uint32_t cap, const uint32_t* numsteps, const float* coords, uint32_t e1, const RaySort& rs, uint32_t* list,
-                     uint32_t* list_len, void* scan_temp, size_t scan_temp_bytes);
+                     uint32_t* list_len, void* scan_temp, size_t scan_temp_bytes, const RaySplit* split = nullptr);
 // k_march_scan (the scan of the requested counts fused with numsteps, scan_temp = a scan_temp_bytes buffer) and
 // k_march_write; round0 nullable
 void launch_march_write(hipStream_t s, uint32_t cap, StepState* st, const DevDataset& ds, const float* rays, const MarchWork& mw, const uint32_t* nreq,
@@ -348,6 +355,14 @@ void launch_loss_alpha_list(hipStream_t s, uint32_t cap_samples, const uint32_t*
                             const half_t* net_out, float cos_anneal, const LossWork& w, bool dt_const = false);
 // rays_in / *n_rays_in: the rays still open (rounds after the first; nullptr: every ray slot); rays_out / n_rays_out: the
 // rays that stay open, for the next round (nullptr in the last round, with list)
+// the compaction cut of the progressive rounds (march.hip k_prog_cut / k_prog_next)
+// mode 0: after round 0's pass A (split sort): cutw[CW_CUT_A], and pass B's counts cutw[CW_LENB_EFF] / [CW_NB_EFF] (0 when the
+// cut lies in pass A's slots); mode 1: the final cut cutw[CW_CUT], the next step's split estimate cutw[CW_EST], and pass B's
+// evaluated samples added to *eval0 (null: none)
+void launch_prog_cut(hipStream_t s, uint32_t cap_rays, const uint32_t* ccount, const uint32_t* excl, uint32_t batch, uint32_t* cutw, int mode,
+                     uint32_t* eval0);
+void launch_prog_next(hipStream_t s, uint32_t cap_rays, const uint32_t* rays_in, const uint32_t* n_in, const uint32_t* numsteps, const uint32_t* cut,
+                      uint32_t e1, uint32_t e2, uint32_t* list, uint32_t* list_counter, uint32_t* rays_out, uint32_t* n_out);
 void launch_loss_scan_chunk(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, const LossWork& w, uint32_t* ccount, uint32_t e0,
                             uint32_t e1, uint32_t e2, uint32_t* list /* nullptr in the last round */, uint32_t* next_counter,
                             const uint32_t* rays_in = nullptr, const uint32_t* n_rays_in = nullptr, uint32_t* rays_out = nullptr,

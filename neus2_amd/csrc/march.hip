@@ -878,7 +878,7 @@ __global__ void __launch_bounds__(256) k_march_write(uint32_t cap_rays, StepStat
 // matrix, one device-wide exclusive scan of it (scan.hip), placement with LDS cursors (global per-ray atomics on the
 // ~300 rays of an occupied cell serialised at the memory side: ~50 us). Order within a cell is immaterial (every work
 // item writes its own sample's slots, every ray's recurrence is its own), so results are unchanged.
-constexpr uint32_t RS_RPB = 1024, RS_NB = RS_BINS + 1;
+constexpr uint32_t RS_RPB = 1024, RS_NB = RS_BINS + 1, RS_NB2 = 2 * RS_BINS + 1;
 __device__ __forceinline__ uint32_t spread4(uint32_t v) {
 	v &= 15u;
 	v = (v | (v << 4)) & 0x0C3u;
@@ -892,43 +892,61 @@ __device__ __forceinline__ uint32_t ray_cell_key(const float* __restrict__ c) { 
 }
 // block b, slots [b RS_RPB, (b + 1) RS_RPB), one per thread: per slot with kept samples its cell (first kept sample);
 // the block's ray count and round-0 chunk samples per cell (bin RS_BINS: slots without samples) -> hist [2][RS_NB][nblk]
+// Split (RaySplit, sp.est != null): bin = cell + RS_BINS for the slots at or past *est (pass B), the no-sample bin is 2 RS_BINS.
 __global__ void __launch_bounds__(RS_RPB) k_ray_hist(uint32_t cap, const uint32_t* __restrict__ numsteps, const float* __restrict__ coords,
-                                                     uint32_t e1, RaySort rs) {
-	__shared__ uint32_t h[2][RS_NB];
+                                                     uint32_t e1, RaySort rs, RaySplit sp) {
+	__shared__ uint32_t h[2][RS_NB2];
 	const uint32_t nblk = gridDim.x, blk = blockIdx.x, t = threadIdx.x;
-	for (uint32_t b = t; b < 2 * RS_NB; b += RS_RPB) (&h[0][0])[b] = 0u;
+	const uint32_t nbins = sp.est ? 2 * RS_BINS : RS_BINS, NB = nbins + 1;
+	const uint32_t est = sp.est ? min(*sp.est, cap) : cap;
+	for (uint32_t b = t; b < 2 * RS_NB2; b += RS_RPB) (&h[0][0])[b] = 0u;
 	__syncthreads();
 	const uint32_t i = blk * RS_RPB + t;
 	const bool in = i < cap;
 	const uint32_t ns = in ? numsteps[2 * i] : 0u;
 	if (ns) {
-		const uint32_t key = ray_cell_key(coords + (size_t)numsteps[2 * i + 1] * COORD_W);
+		const uint32_t key = ray_cell_key(coords + (size_t)numsteps[2 * i + 1] * COORD_W) + (i >= est ? RS_BINS : 0u);
 		rs.key[i] = (uint16_t)key;
 		atomicAdd(&h[0][key], 1u);
 		atomicAdd(&h[1][key], min(ns, e1));
 	}
+	if (sp.est && in && (!ns || i >= est)) sp.ccount[i] = 0u;  // (pass A's cut: the slots it does not scan count 0)
 	const unsigned long long m = __ballot(in && !ns);
-	if ((t & 63) == 0 && m) atomicAdd(&h[0][RS_BINS], (uint32_t)__popcll(m));
+	if ((t & 63) == 0 && m) atomicAdd(&h[0][nbins], (uint32_t)__popcll(m));
 	__syncthreads();
-	for (uint32_t b = t; b < RS_NB; b += RS_RPB) {
+	for (uint32_t b = t; b < NB; b += RS_RPB) {
 		rs.hist[(size_t)b * nblk + blk] = h[0][b];
-		rs.hist[((size_t)RS_NB + b) * nblk + blk] = h[1][b];
+		rs.hist[((size_t)NB + b) * nblk + blk] = h[1][b];
 	}
 }
 // each slot to its place in the order (LDS cursors from the scanned matrix); a ray with samples also writes its round-0
 // chunk [0, min(n, e1)) into its cell's part of the list, each wave's chunks written lane-contiguously. Block 0 writes
 // the ordered slot count and the round-0 list length.
+// Split: pass A's rays and chunks at perm [0, nA) / list [0, lenA), pass B's at perm [perm_b, +nB) / list [list_b, +lenB);
+// the rays without samples are placed nowhere (neither pass scans them; k_ray_hist zeroed their ccount).
 __global__ void __launch_bounds__(RS_RPB) k_ray_sort_place(uint32_t cap, const uint32_t* __restrict__ numsteps, uint32_t e1, RaySort rs,
-                                                           uint32_t* __restrict__ list, uint32_t* __restrict__ list_len) {
-	__shared__ uint32_t cur[2][RS_NB];
+                                                           uint32_t* __restrict__ list, uint32_t* __restrict__ list_len, RaySplit sp) {
+	__shared__ uint32_t cur[2][RS_NB2];
 	const uint32_t nblk = gridDim.x, blk = blockIdx.x, t = threadIdx.x, lane = t & 63;
-	const size_t n = 2 * (size_t)RS_NB * nblk, h1 = (size_t)RS_NB * nblk;
+	const uint32_t nbins = sp.est ? 2 * RS_BINS : RS_BINS, NB = nbins + 1;
+	const size_t n = 2 * (size_t)NB * nblk, h1 = (size_t)NB * nblk;
 	const uint32_t h0_total = rs.off[h1];  // every slot (h0 counts them all)
-	for (uint32_t b = t; b < RS_NB; b += RS_RPB) {
+	for (uint32_t b = t; b < NB; b += RS_RPB) {
 		cur[0][b] = rs.off[(size_t)b * nblk + blk];
 		cur[1][b] = rs.off[h1 + (size_t)b * nblk + blk] - h0_total;
 	}
-	if (blk == 0 && t == 0) { *rs.n_perm = h0_total; *list_len = rs.off[n - 1] + rs.hist[n - 1] - h0_total; }
+	// split: the start of the B bins (rays, round-0 samples) and of the no-sample bin
+	const uint32_t nA = sp.est ? rs.off[(size_t)RS_BINS * nblk] : 0u, nAB = sp.est ? rs.off[(size_t)2 * RS_BINS * nblk] : 0u;
+	const uint32_t lenA = sp.est ? rs.off[h1 + (size_t)RS_BINS * nblk] - h0_total : 0u;
+	const uint32_t len = (uint32_t)(rs.off[n - 1] + rs.hist[n - 1] - h0_total);
+	if (blk == 0 && t == 0) {
+		if (sp.est) {
+			*rs.n_perm = nA; *list_len = lenA;
+			sp.cutw[CW_NB] = nAB - nA; sp.cutw[CW_LENB] = len - lenA;
+		} else {
+			*rs.n_perm = h0_total; *list_len = len;
+		}
+	}
 	__syncthreads();
 	const uint32_t i = blk * RS_RPB + t;
 	const bool in = i < cap;
@@ -936,14 +954,17 @@ __global__ void __launch_bounds__(RS_RPB) k_ray_sort_place(uint32_t cap, const u
 	uint32_t w = 0, dst = 0;
 	if (ns) {
 		const uint32_t key = rs.key[i];
-		rs.perm[atomicAdd(&cur[0][key], 1u)] = i;
+		const uint32_t p = atomicAdd(&cur[0][key], 1u);
+		const bool b = sp.est && key >= RS_BINS;
+		rs.perm[b ? sp.perm_b + (p - nA) : p] = i;
 		w = min(ns, e1);
 		dst = atomicAdd(&cur[1][key], w);
+		if (b) dst = sp.list_b + (dst - lenA);
 	}
 	const unsigned long long m = __ballot(in && !ns);
-	if (m) {
+	if (m && !sp.est) {
 		uint32_t p0 = 0;
-		if (lane == 0) p0 = atomicAdd(&cur[0][RS_BINS], (uint32_t)__popcll(m));
+		if (lane == 0) p0 = atomicAdd(&cur[0][nbins], (uint32_t)__popcll(m));
 		p0 = wave_lane_value(p0, 0);
 		if (in && !ns) rs.perm[p0 + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = i;
 	}
@@ -958,13 +979,15 @@ __global__ void __launch_bounds__(RS_RPB) k_ray_sort_place(uint32_t cap, const u
 }
 uint32_t ray_sort_blocks(uint32_t cap) { return std::max<uint32_t>(1, (cap + RS_RPB - 1) / RS_RPB); }
 void launch_ray_sort(hipStream_t s, uint32_t cap, const uint32_t* numsteps, const float* coords, uint32_t e1, const RaySort& rs, uint32_t* list,
-                     uint32_t* list_len, void* scan_temp, size_t scan_temp_bytes) {
+                     uint32_t* list_len, void* scan_temp, size_t scan_temp_bytes, const RaySplit* split) {
 	const uint32_t nblk = ray_sort_blocks(cap);
+	const RaySplit sp = split ? *split : RaySplit{nullptr, nullptr, nullptr, 0u, 0u};
+	if (sp.est && (!sp.ccount || !sp.cutw)) throw std::runtime_error("launch_ray_sort: the split needs ccount and the cut words");
 	dbg_lds_gate(s);
-	k_ray_hist<<<nblk, RS_RPB, 0, s>>>(cap, numsteps, coords, e1, rs);
-	launch_exclusive_scan(s, scan_temp, scan_temp_bytes, rs.hist, rs.off, 2 * RS_NB * nblk);
+	k_ray_hist<<<nblk, RS_RPB, 0, s>>>(cap, numsteps, coords, e1, rs, sp);
+	launch_exclusive_scan(s, scan_temp, scan_temp_bytes, rs.hist, rs.off, 2 * (sp.est ? RS_NB2 : RS_NB) * nblk);
 	dbg_lds_gate(s);
-	k_ray_sort_place<<<nblk, RS_RPB, 0, s>>>(cap, numsteps, e1, rs, list, list_len);
+	k_ray_sort_place<<<nblk, RS_RPB, 0, s>>>(cap, numsteps, e1, rs, list, list_len, sp);
 }
 
 // Development statistic: per ray, march_step calls and skip-loop additions of the march
@@ -1317,24 +1340,27 @@ __global__ void __launch_bounds__(64) SCAN_OCC k_loss_scan_chunk(uint32_t cap_ra
 			rT[i] = S.T;
 			rek[i] = S.ek;
 		}
-		if (list) {
-			// the next round's chunk of every ray still open: one reservation per wave, written lane-contiguously
+		if (list || rays_out) {
+			// the next round's chunk of every ray still open: one reservation per wave, written lane-contiguously (no list:
+			// the open rays only - k_prog_next builds the next list from them, past the compaction cut)
 			const uint32_t m = (open && S.cn == e1 && e1 < ns && S.T >= 1e-4f) ? min(ns, e2) - e1 : 0u;
 			const uint32_t incl = wave_incl_sum(m);
 			const uint32_t total = wave_lane_value(incl, 63);
 			if (total) {
-				uint32_t p0 = 0;
-				if (lane == 0) p0 = atomicAdd(next_counter, total);
-				p0 = wave_lane_value(p0, 0);
-				// each open ray's next chunk written by the whole wave, one ray at a time (consecutive lanes, consecutive
-				// slots: the same list as each lane writing its own, in the same positions)
-				const uint32_t pre = incl - m, src = base + e1;
-				unsigned long long todo = __ballot(m > 0);
-				while (todo) {
-					const int o = __ffsll(todo) - 1;
-					todo &= todo - 1ull;
-					const uint32_t m_o = wave_lane_value(m, o), p_o = p0 + wave_lane_value(pre, o), s_o = wave_lane_value(src, o);
-					for (uint32_t j = lane; j < m_o; j += 64) list[p_o + j] = s_o + j;
+				if (list) {
+					uint32_t p0 = 0;
+					if (lane == 0) p0 = atomicAdd(next_counter, total);
+					p0 = wave_lane_value(p0, 0);
+					// each open ray's next chunk written by the whole wave, one ray at a time (consecutive lanes, consecutive
+					// slots: the same list as each lane writing its own, in the same positions)
+					const uint32_t pre = incl - m, src = base + e1;
+					unsigned long long todo = __ballot(m > 0);
+					while (todo) {
+						const int o = __ffsll(todo) - 1;
+						todo &= todo - 1ull;
+						const uint32_t m_o = wave_lane_value(m, o), p_o = p0 + wave_lane_value(pre, o), s_o = wave_lane_value(src, o);
+						for (uint32_t j = lane; j < m_o; j += 64) list[p_o + j] = s_o + j;
+					}
 				}
 				if (rays_out) {  // the open rays, one reservation per wave
 					const unsigned long long mk = __ballot(m > 0);
@@ -1345,6 +1371,71 @@ __global__ void __launch_bounds__(64) SCAN_OCC k_loss_scan_chunk(uint32_t cap_ra
 				}
 			}
 		}
+	}
+}
+
+// ---- the compaction cut of the progressive rounds (fixed rays per batch; NeusTestbed::prog_cut)
+// The loss compacts the composited samples in ray-slot order and keeps the first `batch` (compute_loss_kernel_train_nerf,
+// testbed_nerf.cu:1682-1688: a ray whose compacted base is past the batch contributes nothing). After a round, ccount[i] is
+// the ray's composited count so far - exact if it is closed, a lower bound if it is open - and counts only grow in later
+// rounds. So once the inclusive prefix of ccount over the slots reaches the batch at slot c, every slot after c has a
+// compaction base of at least the batch whatever its remaining samples hold: the later rounds skip those rays. `excl` is
+// the exclusive scan of ccount; exactly one thread writes the cut (the crossing slot, or cap_rays when the prefix never
+// reaches the batch).
+// mode 0 (after pass A of a split round 0, the slots it did not scan counting 0): when the prefix reaches the batch in pass
+// A's slots, pass B has nothing to do (its counts 0), else pass B runs on everything the sort gave it. mode 1 (the cut the
+// later rounds use): also the next step's split estimate (the cut + 1/4 + 1024, whole waves) and pass B's samples added to
+// the round-0 evaluated count.
+__global__ void __launch_bounds__(256) k_prog_cut(uint32_t cap_rays, const uint32_t* __restrict__ ccount, const uint32_t* __restrict__ excl,
+                                                  uint32_t batch, uint32_t* __restrict__ cutw, int mode, uint32_t* __restrict__ eval0) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= cap_rays) return;
+	const uint32_t e = excl[i], incl = e + ccount[i];
+	const bool cross = e < batch && incl >= batch, none = i == cap_rays - 1 && incl < batch;
+	if (!cross && !none) return;
+	const uint32_t c = cross ? i : cap_rays;
+	if (mode == 0) {
+		cutw[CW_CUT_A] = c;
+		cutw[CW_LENB_EFF] = cross ? 0u : cutw[CW_LENB];
+		cutw[CW_NB_EFF] = cross ? 0u : cutw[CW_NB];
+	} else {
+		cutw[CW_CUT] = c;
+		cutw[CW_EST] = min(cap_rays, (c + c / 4u + 1024u + 63u) & ~63u);
+		if (eval0) *eval0 += cutw[CW_LENB_EFF];
+	}
+}
+// The next round's work from the rays still open (rays_in: the scan's rays_out), the rays at or before the cut only: the
+// ray to rays_out and its next chunk [e1, min(ns, e2)) to the sample list; one reservation per wave for each (the list
+// order differs from the scan's own append, which changes no result: every sample and every ray is independent).
+__global__ void __launch_bounds__(256) k_prog_next(const uint32_t* __restrict__ rays_in, const uint32_t* __restrict__ n_in,
+                                                   const uint32_t* __restrict__ numsteps, const uint32_t* __restrict__ cut, uint32_t e1, uint32_t e2,
+                                                   uint32_t* __restrict__ list, uint32_t* __restrict__ list_counter,
+                                                   uint32_t* __restrict__ rays_out, uint32_t* __restrict__ n_out) {
+	const uint32_t lane = threadIdx.x & 63;
+	const uint32_t n = *n_in, c = *cut, n64 = (n + 63u) & ~63u;
+	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n64; k += gridDim.x * blockDim.x) {
+		const uint32_t i = k < n ? rays_in[k] : 0u;
+		const uint32_t ns = k < n ? numsteps[2 * i] : 0u, base = k < n ? numsteps[2 * i + 1] : 0u;
+		const uint32_t m = (k < n && i <= c && ns > e1) ? min(ns, e2) - e1 : 0u;
+		const uint32_t incl = wave_incl_sum(m);
+		const uint32_t total = wave_lane_value(incl, 63);
+		if (!total) continue;
+		uint32_t p0 = 0;
+		if (lane == 0) p0 = atomicAdd(list_counter, total);
+		p0 = wave_lane_value(p0, 0);
+		const uint32_t pre = incl - m, src = base + e1;
+		unsigned long long todo = __ballot(m > 0);
+		while (todo) {
+			const int o = __ffsll(todo) - 1;
+			todo &= todo - 1ull;
+			const uint32_t m_o = wave_lane_value(m, o), p_o = p0 + wave_lane_value(pre, o), s_o = wave_lane_value(src, o);
+			for (uint32_t j = lane; j < m_o; j += 64) list[p_o + j] = s_o + j;
+		}
+		const unsigned long long mk = __ballot(m > 0);
+		uint32_t q0 = 0;
+		if (lane == 0) q0 = atomicAdd(n_out, (uint32_t)__popcll(mk));
+		q0 = wave_lane_value(q0, 0);
+		if (m > 0) rays_out[q0 + (uint32_t)__popcll(mk & ((1ull << lane) - 1ull))] = i;
 	}
 }
 
@@ -1724,6 +1815,15 @@ void launch_loss_scan_chunk(hipStream_t s, uint32_t cap_rays, const uint32_t* nu
 	k_loss_scan_chunk<<<std::max<uint32_t>(1, std::min<uint32_t>((cap_rays + 63) / 64, 8192)), 64, 0, s>>>(
 		cap_rays, numsteps, w.sa, w.ekt, w.ck4, w.cke, ccount, w.racc, w.rT, w.rek, e0, e1, e2, list, next_counter, rays_in, n_rays_in,
 		rays_out, n_rays_out);
+}
+void launch_prog_cut(hipStream_t s, uint32_t cap_rays, const uint32_t* ccount, const uint32_t* excl, uint32_t batch, uint32_t* cutw, int mode,
+                     uint32_t* eval0) {
+	k_prog_cut<<<(cap_rays + 255) / 256, 256, 0, s>>>(cap_rays, ccount, excl, batch, cutw, mode, eval0);
+}
+void launch_prog_next(hipStream_t s, uint32_t cap_rays, const uint32_t* rays_in, const uint32_t* n_in, const uint32_t* numsteps, const uint32_t* cut,
+                      uint32_t e1, uint32_t e2, uint32_t* list, uint32_t* list_counter, uint32_t* rays_out, uint32_t* n_out) {
+	k_prog_next<<<std::max<uint32_t>(1, std::min<uint32_t>((cap_rays + 255) / 256, 1024)), 256, 0, s>>>(rays_in, n_in, numsteps, cut, e1, e2, list,
+	                                                                                                   list_counter, rays_out, n_out);
 }
 // w.n_long is zeroed by the k_loss_alpha launch before it
 void launch_loss_scan_ray(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, const LossWork& w, uint32_t* ccount) {

@@ -380,6 +380,24 @@ struct NeusTestbed {
 	bool ray_sort = [] { const char* e = std::getenv("NEUS_RAY_SORT"); return !(e && e[0] == '0'); }();
 	static constexpr uint32_t OPEN_CNT = 32;
 	static constexpr uint32_t RS_N_PERM = 48;  // chunk_cnt slot: the ray order's length (k_ray_sort_scan)
+	static constexpr uint32_t RAW_CNT = 49;    // chunk_cnt [49 + k]: rays open after round k, before the compaction cut (k = 0)
+	// The compaction cut (march.hip k_prog_cut): with fixed rays per batch the later progressive rounds skip the rays whose
+	// compaction base is already past the batch after a round. Training is bitwise the same; what changes is the summed
+	// composited count of such a step (a lower bound, still >= the batch), which with fixed rays feeds no result - only the
+	// logged loss scale, the chunk-end rule and the stats. So a step that the host reads back (a loss readback step, the last
+	// step of a train call) never cuts, and every value the host sees is the uncut one. NEUS_PROG_CUT=0 turns it off.
+	bool prog_cut = [] { const char* e = std::getenv("NEUS_PROG_CUT"); return !(e && e[0] == '0'); }();
+	// With the spatial ray order, round 0 itself is split too: the sort puts the rays of the slots below the previous step's
+	// cut (+ 1/4, + 1024: cutw[CW_EST]) first (pass A); once pass A is scanned the cut is known whenever the prefix reaches
+	// the batch in those slots, and pass B (the rest of round 0) then has nothing to do.
+	Dev<uint32_t> open_raw, cutw;  // the rays open after round 0, before the cut; the cut words (kernels.h CW_*)
+	uint64_t cut_steps = 0;
+	uint32_t call_left = 0;        // steps of the current train call after the current one
+	bool la_cut = false;           // the pending lookahead's step cuts (its sort was split)
+	bool cut_for(uint32_t step, bool progressive, bool last_in_call, bool dyn) const {
+		const uint32_t nch = (uint32_t)chunk_ends.size() + 1;
+		return prog_cut && progressive && cfg.fixed_rays_per_batch && !dyn && step % 16 != 0 && !last_in_call && nch >= 2 && nch <= 15;
+	}
 	Dev<uint32_t> long_rays;  // the loss scan's wave-per-ray list (+ its counter in chunk_cnt[16])
 	TrainBufs tbuf{};
 	// RNG + counters (testbed.cu:2087-2101)
@@ -796,7 +814,7 @@ struct NeusTestbed {
 			sc_zero_from_e = gl.offset[gl.n_levels];
 		}
 		scan_tmp_bytes = std::max({scan_temp_bytes(MAX_RAYS), scan_temp_bytes((uint32_t)n_bins),
-		                           scan_temp_bytes(2 * (RS_BINS + 1) * ray_sort_blocks(MAX_RAYS))});
+		                           scan_temp_bytes(2 * (2 * RS_BINS + 1) * ray_sort_blocks(MAX_RAYS))});
 		scan_tmp.alloc(scan_tmp_bytes + 256);
 		scan_temp_reset(stream, scan_tmp.p);
 		HIP_CHECK(hipStreamSynchronize(stream));
@@ -815,10 +833,12 @@ struct NeusTestbed {
 		l_sa.alloc(max_samples); l_ekt.alloc(max_samples); sample_ray.alloc(max_samples); cmap.alloc(batch);
 		l_ck4.alloc(max_samples / 8 + 1); l_cke.alloc(max_samples / 8 + 1);
 		l_racc.alloc(MAX_RAYS); l_rgr.alloc(MAX_RAYS); l_rT.alloc(MAX_RAYS); l_rek.alloc(MAX_RAYS);
-		chunk_list.alloc(max_samples); chunk_cnt.alloc(64); long_rays.alloc(MAX_RAYS);
-		open_rays[0].alloc(MAX_RAYS); open_rays[1].alloc(MAX_RAYS);
-		rs_hist.alloc(2 * (size_t)(RS_BINS + 1) * ray_sort_blocks(MAX_RAYS)); rs_off.alloc(rs_hist.n);
-		rs_perm.alloc(MAX_RAYS); rs_key.alloc(MAX_RAYS);
+		// (the split round 0 of the compaction cut: pass B's list from max_samples, its rays from MAX_RAYS)
+		chunk_list.alloc(2 * (size_t)max_samples); chunk_cnt.alloc(64); long_rays.alloc(MAX_RAYS);
+		open_rays[0].alloc(MAX_RAYS); open_rays[1].alloc(MAX_RAYS); open_raw.alloc(MAX_RAYS); cutw.alloc(CW_WORDS);
+		{ uint32_t w[CW_WORDS] = {}; w[CW_EST] = MAX_RAYS; HIP_CHECK(hipMemcpy(cutw.p, w, sizeof(w), hipMemcpyHostToDevice)); }
+		rs_hist.alloc(2 * (size_t)(2 * RS_BINS + 1) * ray_sort_blocks(MAX_RAYS)); rs_off.alloc(rs_hist.n);
+		rs_perm.alloc(2 * (size_t)MAX_RAYS); rs_key.alloc(MAX_RAYS);
 		loss.alloc(MAX_RAYS); ek.alloc(MAX_RAYS); mask.alloc(MAX_RAYS); loss_sum.alloc(4); health_buf.alloc(4);
 		coords.alloc((size_t)max_samples * COORD_W); net_out.alloc((size_t)max_samples * OUT_W);
 		coords_c.alloc((size_t)batch * COORD_W); dL_dout.alloc((size_t)batch * OUT_W);
@@ -1590,8 +1610,11 @@ struct NeusTestbed {
 			HIP_CHECK(hipStreamWaitEvent(s, ev_la_done, 0));  // this step's samples came from the previous step's lookahead
 			if (la_stat && la_stat_used % 4 == 3) HIP_CHECK(hipEventRecord(la_stat_next(), s));
 		} else {
-			issue_march(s, dp, rng, progressive, scan_tmp.p);
+			issue_march(s, dp, rng, progressive, scan_tmp.p, cut_for(training_step, progressive, call_left == 0, dyn));
 		}
+		const bool cut = la_have ? la_cut : cut_for(training_step, progressive, call_left == 0, dyn);
+		const bool split = cut && sorted_rays;
+		if (cut) ++cut_steps;
 		mark(2);
 		// DeltaNetwork forward on the samples (nerf_network.h:162-182); the loss keeps the undeformed records
 		const float* c_in = coords.p;
@@ -1605,6 +1628,8 @@ struct NeusTestbed {
 			// rounds of per-ray chunks, each: network on the round's samples, alpha, the recurrence continued (march.hip);
 			// the "infer" phase mark then covers the composite as well
 			uint32_t e0 = 0;
+			// the compaction cut (prog_cut, cut_for): fixed rays per batch, not a step the host reads back (the loss readback
+			// steps, the last step of a train call), one rank's own batch
 			for (uint32_t k = 0; k < nch; ++k) {
 				const uint32_t e1 = k + 1 < nch ? chunk_ends[k] : 0xffffffffu;
 				const uint32_t e2 = k + 2 < nch ? chunk_ends[k + 1] : 0xffffffffu;
@@ -1615,10 +1640,33 @@ struct NeusTestbed {
 				                  use_delta ? nullptr : &ia);
 				if (use_delta) launch_loss_alpha_list(s, max_samples, chunk_cnt.p + k, chunk_list.p, coords.p, net_out.p, lp.cos_anneal, w, ds.cone_angle == 0.0f);
 				const bool more = k + 1 < nch;
-				launch_loss_scan_chunk(s, MAX_RAYS, numsteps.p, w, ccount.p, e0, e1, e2, more ? chunk_list.p : nullptr, chunk_cnt.p + k + 1,
+				// the cut after round 0 (the rays of the later rounds are then all at or before it: each round continues
+				// only the rays of the round before it)
+				const bool cut_k = cut && k == 0 && more;
+				launch_loss_scan_chunk(s, MAX_RAYS, numsteps.p, w, ccount.p, e0, e1, e2, more && !cut_k ? chunk_list.p : nullptr, chunk_cnt.p + k + 1,
 				                       k ? open_rays[(k - 1) & 1].p : (sorted_rays ? rs_perm.p : nullptr),
 				                       k ? chunk_cnt.p + OPEN_CNT + k - 1 : (sorted_rays ? rsort.n_perm : nullptr),
-				                       more ? open_rays[k & 1].p : nullptr, more ? chunk_cnt.p + OPEN_CNT + k : nullptr);
+				                       more ? (cut_k ? open_raw.p : open_rays[k & 1].p) : nullptr,
+				                       more ? chunk_cnt.p + (cut_k ? RAW_CNT : OPEN_CNT) + k : nullptr);
+				if (cut_k) {
+					// the cut after this round (cbase as the scan's scratch: the compaction rewrites it after the rounds), then
+					// the next round's rays and samples from the open rays at or before it
+					if (split) {
+						// pass A was the rays below the estimate: its cut, then pass B (empty when the cut lies in pass A's slots)
+						launch_exclusive_scan(s, scan_tmp.p, scan_tmp_bytes, ccount.p, cbase.p, MAX_RAYS);
+						launch_prog_cut(s, MAX_RAYS, ccount.p, cbase.p, batch, cutw.p, 0, nullptr);
+						const InferAlpha iab{w.sa, w.ekt, lp.cos_anneal, ds.cone_angle == 0.0f ? 1u : 0u, nullptr, 8u};
+						it_arm();
+						launch_nerf_infer(s, lay.L, lay.W, cutw.p + CW_LENB_EFF, 0, c_in, gl, valid, params_h.p + lay.grid_off, mlp, net_out.p, 8192,
+						                  chunk_list.p + max_samples, &iab);
+						launch_loss_scan_chunk(s, MAX_RAYS, numsteps.p, w, ccount.p, 0, e1, e2, nullptr, nullptr, rs_perm.p + MAX_RAYS,
+						                       cutw.p + CW_NB_EFF, open_raw.p, chunk_cnt.p + RAW_CNT + k);
+					}
+					launch_exclusive_scan(s, scan_tmp.p, scan_tmp_bytes, ccount.p, cbase.p, MAX_RAYS);
+					launch_prog_cut(s, MAX_RAYS, ccount.p, cbase.p, batch, cutw.p, 1, split ? chunk_cnt.p : nullptr);
+					launch_prog_next(s, MAX_RAYS, open_raw.p, chunk_cnt.p + RAW_CNT + k, numsteps.p, cutw.p + CW_CUT, e1, e2, chunk_list.p,
+					                 chunk_cnt.p + k + 1, open_rays[k & 1].p, chunk_cnt.p + OPEN_CNT + k);
+				}
 				e0 = e1;
 			}
 			mark(3);
@@ -1699,11 +1747,13 @@ struct NeusTestbed {
 				pcg32 r1 = rng;
 				r1.advance();
 				const bool prog1 = progressive_mode == 2 || (progressive_mode == 1 && last_keep_ratio < PROGRESSIVE_RATIO);
-				la_deferred = [this, cs, dp, r1, prog1] {
+				la_cut = cut_for(training_step + 1, prog1, call_left <= 1, false);
+				const bool cut1 = la_cut;
+				la_deferred = [this, cs, dp, r1, prog1, cut1] {
 					HIP_CHECK(hipEventRecord(ev_la_start, cs));
 					HIP_CHECK(hipStreamWaitEvent(la_stream, ev_la_start, 0));
 					if (la_stat) { la_stat_used -= la_stat_used % 4; HIP_CHECK(hipEventRecord(la_stat_next(), la_stream)); }
-					issue_march(la_stream, dp, r1, prog1, scan_tmp_la.p);
+					issue_march(la_stream, dp, r1, prog1, scan_tmp_la.p, cut1);
 					if (la_stat) HIP_CHECK(hipEventRecord(la_stat_next(), la_stream));
 					HIP_CHECK(hipEventRecord(ev_la_done, la_stream));
 				};
@@ -1817,16 +1867,18 @@ struct NeusTestbed {
 	// A step's ray sampling: ray generation + the march's two passes, the coordinate write (and round 0's list, unsorted
 	// progressive), the spatial ray sort (sorted progressive); rng / progressive: the step's own (train_step, or the
 	// lookahead for the next step), scan: the look-back state of the stream it runs on.
-	void issue_march(hipStream_t s, const DPInfo& dp, const pcg32& r, bool progressive, uint8_t* scan) {
+	void issue_march(hipStream_t s, const DPInfo& dp, const pcg32& r, bool progressive, uint8_t* scan, bool cut = false) {
 		const uint32_t nch = (uint32_t)chunk_ends.size() + 1;
 		const Round0List r0{chunk_ends[0], cbase.p, chunk_list.p, chunk_cnt.p, nch + 1};
 		const bool sorted_rays = progressive && ray_sort;
 		launch_march_count(s, MAX_RAYS, max_samples, st.p, dp, ds, bitfield.p, bf_lin.p, r.state, r.inc, rays.p, startt.p, nreq.p, mwork,
-		                   progressive ? chunk_cnt.p : nullptr, OPEN_CNT + nch, ray_cull ? occ_bbox.p : nullptr);  // list lengths + open-ray counts
+		                   progressive ? chunk_cnt.p : nullptr, RAW_CNT + nch, ray_cull ? occ_bbox.p : nullptr);  // list lengths + open-ray counts
 		launch_march_write(s, MAX_RAYS, st.p, ds, rays.p, mwork, nreq.p, base.p, numsteps.p, coords.p, nullptr, max_samples, scan,
 		                   progressive && !sorted_rays ? &r0 : nullptr, dbg_lds_fill);
 		const RaySort rsort{rs_hist.p, rs_off.p, rs_key.p, rs_perm.p, chunk_cnt.p + RS_N_PERM};
-		if (sorted_rays) launch_ray_sort(s, MAX_RAYS, numsteps.p, coords.p, chunk_ends[0], rsort, chunk_list.p, chunk_cnt.p, scan, scan_tmp_bytes);
+		const RaySplit split{cutw.p + CW_EST, ccount.p, cutw.p, MAX_RAYS, max_samples};
+		if (sorted_rays)
+			launch_ray_sort(s, MAX_RAYS, numsteps.p, coords.p, chunk_ends[0], rsort, chunk_list.p, chunk_cnt.p, scan, scan_tmp_bytes, cut ? &split : nullptr);
 	}
 
 	LossWork loss_work(const uint32_t* rbase) {
@@ -1959,6 +2011,7 @@ int neus_testbed_train(NeusTestbed* tb, uint32_t n_steps) {
 			g_dbg_lds_fill = tb->dbg_lds_fill_all ? ((tb->training_step & 1) ? ~tb->dbg_lds_fill_all : tb->dbg_lds_fill_all) : 0u;
 			g_dbg_xcd_shift = tb->dbg_xcd_shift;
 			tb->la_next_in_call = i + 1 < n_steps;
+			tb->call_left = n_steps - i - 1;
 			tb->train_step();
 		}
 	});
@@ -1985,6 +2038,7 @@ int neus_testbed_get_stats(NeusTestbed* tb, NeusTrainStats* o) {
 		o->occ_samples_total = tb->occ_samples; o->occ_updates = tb->occ_updates;
 		o->progressive_chunk_end = tb->chunk_ends.empty() ? 0u : tb->chunk_ends[0];
 		o->lookahead_steps = tb->la_steps;
+		o->cut_steps = tb->cut_steps;
 		o->adam_split_steps = tb->adam_split_steps;
 		o->health_flags = s.fail_flags | tb->fail_seen | (scan_failures(tb->scan_tmp.p) ? STEP_FAIL_SCAN : 0u);
 		o->evaluated_samples_total = s.eval_total; o->progressive_steps = s.prog_steps; o->evaluated_samples_last = s.eval_last;

@@ -35,11 +35,11 @@ def _env(**kv):
                 os.environ[k] = v
 
 
-def _testbed(sc, fixed_rays=0):
+def _testbed(sc, fixed_rays=0, batch=BATCH):
     from neus2_amd import pyngp
     tb = pyngp.Testbed(pyngp.TestbedMode.Nerf)
     tb.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
-    tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=BATCH, fixed_rays_per_batch=fixed_rays)
+    tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=batch, fixed_rays_per_batch=fixed_rays)
     return tb
 
 
@@ -151,3 +151,26 @@ def test_dp_adam_overlap_bitwise(scene):
     for x in (a[1], b[0], b[1]):
         _same(a[0], x)
     del ga, gb
+
+
+def test_compaction_cut_bitwise(scene):
+    """The compaction cut (march.hip k_prog_cut): with fixed rays per batch, the progressive rounds after round 0 skip the
+    rays whose compaction base is already past the batch, and round 0 itself runs the rays below the previous step's cut first
+    (the split sort), the rest only when the cut is not reached there. 300 steps in one call with progressive inference
+    forced on, a 1024-sample batch and R = 8192 fixed rays (the composited samples far exceed the batch), with the cut and
+    without (NEUS_PROG_CUT=0): bitwise the same parameters, gradients, EMA weights, occupancy grid and - the last step of a
+    call never cuts - the same counters; the cut ran and evaluated fewer samples."""
+    with _env(NEUS_PROG_CUT=1):
+        a = _testbed(scene, 8192, batch=1024)
+    with _env(NEUS_PROG_CUT=0):
+        b = _testbed(scene, 8192, batch=1024)
+    for tb in (a, b):
+        tb.set_progressive_inference(2, (2, 4, 8, 16))  # (short chunks: most rays are still open after round 0)
+        tb.train_steps(300)
+    sa, sb = a.stats(), b.stats()
+    assert sa["cut_steps"] > 200 and sb["cut_steps"] == 0, (sa["cut_steps"], sb["cut_steps"])
+    assert sa["measured_batch_size"] > 2 * 1024  # the composited samples exceed the batch: the cut has rays to skip
+    assert sa["evaluated_samples_total"] < sb["evaluated_samples_total"], (sa["evaluated_samples_total"], sb["evaluated_samples_total"])
+    for k in ("measured_batch_size", "measured_batch_size_before_compaction", "n_rays_with_samples", "progressive_steps"):
+        assert sa[k] == sb[k], (k, sa[k], sb[k])
+    _same(a, b)
