@@ -1,7 +1,7 @@
 """Turn the per-kernel PMC table of scripts/gpu_traffic.sh (pmc_table.py output) into profiles/traffic.json
 entries: memory-side bytes per launch, corrected as MI355X_MICROARCH.md prescribes for gfx950 (FETCH_SIZE
 tallies 128-B requests at 64 B, so reads are recomputed from the request-size breakdown; WRITE_SIZE is KB).
-Usage: traffic_json.py TABLE LEVELS [--commit SHA] [--out profiles/traffic.json]"""
+Usage: traffic_json.py TABLE LEVELS [--commit SHA] [--only-named] [--name KERNEL=KEY] [--out profiles/traffic.json]"""
 import argparse
 import json
 import os
@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--commit", default="")
     # kernel=key overrides of the traffic.json key (e.g. k_nerf_infer=inference_step for the training step's own rounds)
     ap.add_argument("--name", action="append", default=[])
+    # only the --name overrides (the table's other kernels and template variants are left out of the file)
+    ap.add_argument("--only-named", action="store_true")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "traffic.json"))
     a = ap.parse_args()
     try:
@@ -47,8 +49,9 @@ def main():
     for kv in a.name:  # overrides first: the first key contained in a kernel's name wins
         k, v = kv.split("=", 1)
         names[k] = v
-    for k, v in NAMES.items():
-        names.setdefault(k, v)
+    if not a.only_named:
+        for k, v in NAMES.items():
+            names.setdefault(k, v)
     for k, c in parse(a.table, names).items():
         if "TCC_EA0_RDREQ_sum" not in c or "WRITE_SIZE" not in c:
             continue
