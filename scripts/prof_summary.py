@@ -68,6 +68,11 @@ def rows_last_steps(path, k):
 def main():
     args = [a for a in sys.argv[1:]]
     last = None
+    back = [1]
+    if "--seq-back" in args:  # also print the launch sequences of these steps counted from the end (1 = the final step)
+        i = args.index("--seq-back")
+        back = [int(x) for x in args[i + 1].split(",")]
+        del args[i:i + 2]
     if "--last-steps" in args:
         i = args.index("--last-steps")
         last = int(args[i + 1])
@@ -95,10 +100,13 @@ def main():
         con = sqlite3.connect(sys.argv[1])
         ks = list(con.execute("select name, start, end from kernels order by start"))
         adam = step_ends(ks)
-        seq = ks[adam[-2] + 1:adam[-1] + 1]
-        t0 = seq[0][1]
-        lines.append("\nLaunch sequence of the final step (start us, duration us):\n")
-        lines += [f"    {(st - t0) / 1e3:9.1f} {(en - st) / 1e3:8.1f}  {short(n)}" for n, st, en in seq]
+        for j in back:
+            # from the end of the previous step's optimizer launch: the kernels that started after it (the lookahead's
+            # sampling for this step, issued beside that step's backward, started before it and is listed there)
+            seq = ks[adam[-j - 1] + 1:adam[-j] + 1]
+            t0 = ks[adam[-j - 1]][2]
+            lines.append(f"\nLaunch sequence of step -{j} (start us after the previous step's optimizer ended, end us, duration us):\n")
+            lines += [f"    {(st - t0) / 1e3:9.1f} {(en - t0) / 1e3:9.1f} {(en - st) / 1e3:8.1f}  {short(n)}" for n, st, en in seq]
         # bench.py's per-kernel replays (kernel_rooflines) run after the last training step: their median launch is
         # the `launch_ms` of the bench line's roofline / kernels entries
         tail = {}
