@@ -133,6 +133,10 @@ typedef struct NeusTrainStats {
 	uint64_t adam_split_steps;                /* (ABI 5) steps whose optimizer ran in pieces beside the scatter (adam_overlap) */
 	uint64_t cut_steps;                       /* (ABI 5) steps whose later progressive rounds skipped the rays past the
 	                                           * compaction cut (fixed rays per batch; never a step the host reads back) */
+	uint64_t march_cut_steps;                 /* (ABI 6) steps whose ray sampling marched only the slots below the compaction cut's
+	                                           * estimate (NEUS_MARCH_CUT) */
+	uint64_t march_cut_reruns;                /* (ABI 6) steps run again with the full march because the witness of a cut march failed
+	                                           * (nothing of the first run was applied) */
 } NeusTrainStats;
 
 /* Testbed::render_to_cpu (python_api.cu:123-169) after set_camera_to_training_view (testbed.cu:264-270). */
@@ -158,9 +162,10 @@ typedef struct NeusNetLayout {
 /* ABI version of this header (bumped on any incompatible signature or struct change; version 2: neus_module_create_network
  * became tcnn's create_network(n_input_dims, n_output_dims, network), the NerfNetwork factory neus_module_create_nerf_network;
  * version 3: NeusDataParallelInfo gained host_group; version 4: neus_module_create_encoding gained requested_precision;
- * version 5: neus_testbed_{set_,}exchange_timing, neus_host_group_create gained job_token).
+ * version 5: neus_testbed_{set_,}exchange_timing, neus_host_group_create gained job_token; version 6: NeusTrainStats gained
+ * march_cut_steps and march_cut_reruns).
  * Bindings compare it on load so that a stale library or binding fails loudly instead of misreading arguments. */
-#define NEUS_ABI_VERSION 5u
+#define NEUS_ABI_VERSION 6u
 int neus_abi_version(uint32_t* out);
 const char* neus_last_error(void);
 int neus_device_count(int* count);

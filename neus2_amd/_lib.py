@@ -49,7 +49,7 @@ class NeusTrainStats(C.Structure):
         ("occ_samples_total", C.c_uint64), ("occ_updates", C.c_uint32), ("health_flags", C.c_uint32),
         ("evaluated_samples_total", C.c_uint64), ("progressive_steps", C.c_uint64), ("evaluated_samples_last", C.c_uint32),
         ("progressive_chunk_end", C.c_uint32), ("lookahead_steps", C.c_uint64), ("adam_split_steps", C.c_uint64),
-        ("cut_steps", C.c_uint64),
+        ("cut_steps", C.c_uint64), ("march_cut_steps", C.c_uint64), ("march_cut_reruns", C.c_uint64),
     ]
 
 
@@ -133,7 +133,7 @@ EXPORTS = [
 ]
 
 # include/neus2_hip.h's NEUS_ABI_VERSION this binding was written against: a library of another ABI fails to load
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 _lib = None
 

@@ -175,7 +175,17 @@ struct StepState {
 	// for the backward while the counters update and the next step's sampling can start before the backward ends)
 	uint32_t compacted_global;
 	uint32_t rays_ws_global;
-	unsigned long long pad_[2];
+	// the march cut (testbed.cpp march_cut_for): cut_abort - this step's training is not provably the full
+	// march's (k_loss_grad copies it from the loss's abort word; all-reduced with the two counters above, so every rank
+	// sees the same); while set, the optimizer and the step counters leave every state untouched and the host re-runs the
+	// step with the full march. march_cut - this step's march covered only the slots below the cut estimate. mi_lb - a lower
+	// bound of the reference's cap on this step's pre-compaction samples, max_inference = next_multiple(min(the last step's
+	// requested count, max_samples)), when the last step's march was cut (its requested count is then known only for the
+	// marched slots; max_inference is max_samples then, an upper bound); 0 when max_inference is exact.
+	uint32_t cut_abort;
+	uint32_t march_cut;
+	uint32_t mi_lb;
+	uint32_t pad32_;
 };
 static_assert(sizeof(StepState) == 128, "StepState is one 128-B record");
 // fail_flags bits: a march step saw a non-finite or negative t (step_until's precondition; the ray is ended there);
@@ -187,7 +197,9 @@ constexpr uint32_t STEP_FAIL_MARCH_T = 1u, STEP_FAIL_SCAN = 2u;
 // kept samples)
 __device__ __forceinline__ void step_counters_update(StepState* st, uint32_t target_batch, uint32_t max_samples, uint32_t world, uint32_t fixed_rays,
                                                      const uint32_t* eval_cnt = nullptr, uint32_t n_eval = 0) {
+	if (st->cut_abort) return;  // the step is re-run with the full march (the march cut): no counter moves
 	const uint32_t R = st->rays_per_batch;
+	const bool mc = st->march_cut != 0;
 	st->n_rays_total += R * world;  // n_rays_total
 	st->pre_total += st->n_kept;
 	st->rays_total += R;
@@ -201,19 +213,23 @@ __device__ __forceinline__ void step_counters_update(StepState* st, uint32_t tar
 	st->eval_total += ev;
 	// next step's first march pass: the slots up to this step's kept extent plus a margin (all slots when every
 	// ray with samples fitted under this step's cap)
+	// (a cut march's kept extent is that of its marched slots: the estimate stays the last full march's)
 	const bool fit = st->numsteps_counter <= st->max_inference;
 	const uint32_t ext = st->kept_extent + st->kept_extent / 4 + 1024;
-	st->march_est = fit ? 0u : (ext + 63u) / 64u * 64u;
+	if (!mc) st->march_est = fit ? 0u : (ext + 63u) / 64u * 64u;
 	// per rank: the cap on the next step's pre-compaction samples follows this rank's own request count
 	const uint32_t before = st->numsteps_counter;
 	const uint32_t measured = st->compacted_global / world;
 	st->measured_before = before;
 	st->measured_batch_size = measured;
 	st->trained_total += min(measured, target_batch);  // real training samples (the rest of the batch is rollover)
-	if (before == 0 || measured == 0) { st->zero_records = 1; return; }
+	if (before == 0 || measured == 0) { st->zero_records = 1; st->mi_lb = 0; return; }
 	st->zero_records = 0;
 	uint32_t mi = min(before, max_samples);
 	st->max_inference = (mi + 127u) / 128u * 128u;
+	// a cut march requested past max_samples (its drop marker), so max_inference is max_samples; the reference's is at
+	// least the marched slots' count, rounded the same way
+	st->mi_lb = mc ? max((min(st->march_total, max_samples) + 127u) / 128u * 128u, 1u) : 0u;
 	if (fixed_rays) { st->rays_per_batch = fixed_rays; return; }
 	uint32_t r = (uint32_t)((float)R * (float)target_batch / (float)measured);
 	r = (r + 127u) / 128u * 128u;

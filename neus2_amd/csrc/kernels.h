@@ -89,6 +89,11 @@ struct LossParams {
 	uint64_t rng_state, rng_inc;
 	PcgJumpTable jt;
 	uint32_t dbg_fence = 0;  // development (NEUS_DBG_LOSS_FENCE=1): an agent-scope acquire fence at the loss-gradient kernel's start
+	// the march cut's witness (k_loss_ray): abort_w[abort_slot] set when this step's training is not provably the full
+	// march's, abort_w[abort_slot ^ 1] cleared for the next step; k_loss_grad copies the word to StepState::cut_abort.
+	// Null: no witness (cut_abort stays 0)
+	uint32_t* abort_w = nullptr;
+	uint32_t abort_slot = 0;
 };
 
 // binned hash-grid gradient scatter (grid.hip)
@@ -162,6 +167,7 @@ struct AdamParams {
 	float inv_loss_scale;     // 1 / loss_scale when that is a power of two (the product is then the exact quotient)
 	uint32_t pow2_scale;
 	uint32_t skip_ema_h;      // leave the fp16 EMA copy to a later cast of the fp32 EMA (NeusTestbed::sync_ema_h)
+	const uint32_t* abort;    // StepState::cut_abort, or null: while set the launch changes nothing (the step is re-run)
 };
 void launch_adam_bias_table(hipStream_t s, float beta1, float beta2, float* tab);
 
@@ -293,6 +299,11 @@ struct MarchWork {
 	uint32_t dbg = 0;                     /* development timing experiments (wrong results): 1 no record stores, 2 no occupancy loads */
 	uint32_t balanced = 0;                /* 8 lanes per ray on average, shared by the 8 rays of a wave by length (k_march_bal, constant-step
 	                                         march only) */
+	const uint32_t* est_cut = nullptr;    /* the march cut (k_ray_gen, k_march_bal): when this device word (the compaction cut's split
+	                                         estimate, cutw[CW_EST]) is below the first pass's slots, only the slots below it are generated
+	                                         and marched, the rest dropped behind one marker over the cap (StepState::march_cut) */
+	uint32_t est_div = 1;                 /* test hook (NEUS_DBG_MARCH_CUT_DIV): the march cut's estimate divided by this, so that its
+	                                         witness fails and the host's re-run path runs */
 };
 // Ray generation + the occupancy march: rays (6 f32 per slot), tstart (1 per slot), nreq (requested
 // samples per slot) and the sample runs (MarchWork).
@@ -315,7 +326,8 @@ struct RaySort { uint32_t* hist; uint32_t* off; uint16_t* key; uint32_t* perm; u
 // without samples are left out of both passes. hist / off then hold [2][2 RS_BINS + 1][blocks].
 struct RaySplit { const uint32_t* est; uint32_t* ccount; uint32_t* cutw; uint32_t perm_b, list_b; };
 // cutw words (march.hip k_prog_cut)
-constexpr uint32_t CW_CUT = 0, CW_LENB_EFF = 1, CW_NB_EFF = 2, CW_CUT_A = 3, CW_LENB = 4, CW_NB = 5, CW_EST = 6, CW_WORDS = 16;
+constexpr uint32_t CW_CUT = 0, CW_LENB_EFF = 1, CW_NB_EFF = 2, CW_CUT_A = 3, CW_LENB = 4, CW_NB = 5, CW_EST = 6, CW_ABORT = 8 /* 2 words */,
+                   CW_WORDS = 16;
 uint32_t ray_sort_blocks(uint32_t cap);
 void launch_ray_sort(hipStream_t s, uint32_t cap, const uint32_t* numsteps, const float* coords, uint32_t e1, const RaySort& rs, uint32_t* list,
                      uint32_t* list_len, void* scan_temp, size_t scan_temp_bytes, const RaySplit* split = nullptr);
@@ -370,7 +382,7 @@ void launch_loss_scan_chunk(hipStream_t s, uint32_t cap_rays, const uint32_t* nu
 void launch_srgb_lut(hipStream_t s, float* lut);
 void launch_loss_ray(hipStream_t s, uint32_t cap_rays, StepState* st, DPInfo dp, const DevDataset& ds, const LossParams& lp, uint32_t* numsteps,
                      const uint32_t* ccount, const uint32_t* cbase, const LossWork& w, float* loss, float* ek, float* mask);
-void launch_loss_grad(hipStream_t s, uint32_t cap_samples, const StepState* st, DPInfo dp, const LossParams& lp, const float* coords,
+void launch_loss_grad(hipStream_t s, uint32_t cap_samples, StepState* st, DPInfo dp, const LossParams& lp, const float* coords,
                       const half_t* net_out, const uint32_t* numsteps, const LossWork& w, float* coords_out, half_t* dL_dout);
 void debug_launch_loss_scan(hipStream_t s, int variant, uint32_t cap_rays, const uint32_t* numsteps, const LossWork& w, uint32_t* ccount);
 void launch_ray_index(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, StepState* st, uint32_t* sample_ray, uint32_t* rbase);

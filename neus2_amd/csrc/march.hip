@@ -62,8 +62,15 @@ __device__ __forceinline__ bool ray_hits_box(const float o[3], const float d[3],
 __global__ void __launch_bounds__(256) k_ray_gen(uint32_t cap_rays, const StepState* __restrict__ st_r, DPInfo dp, DevDataset ds,
                                                  uint64_t rng_state, uint64_t rng_inc, float* __restrict__ rays, float* __restrict__ tstart,
                                                  uint32_t* __restrict__ march_queue, StepState* __restrict__ st_w, PcgJumpTable jt,
-                                                 uint32_t* __restrict__ zero_counters, uint32_t n_zero, const float* __restrict__ occ_bbox) {
+                                                 uint32_t* __restrict__ zero_counters, uint32_t n_zero, const float* __restrict__ occ_bbox,
+                                                 const uint32_t* __restrict__ est_cut, uint32_t est_div) {
 	if (blockIdx.x == 0 && threadIdx.x < n_zero) zero_counters[threadIdx.x] = 0u;  // the progressive rounds' list lengths
+	// the march cut (MarchWork::est_cut): the same test as k_march_bal's; the slots past the estimate are not marched, so
+	// they get no ray
+	const uint32_t est0 = st_r->march_est ? min(st_r->march_est, cap_rays) : cap_rays;
+	const uint32_t ec = est_cut ? *est_cut / est_div : 0u;
+	const bool mcut = est_cut && ec < est0;
+	const uint32_t lim = mcut ? ec : cap_rays;
 	float bb[6] = {-3.402823466e+38f, -3.402823466e+38f, -3.402823466e+38f, 3.402823466e+38f, 3.402823466e+38f, 3.402823466e+38f};
 	if (occ_bbox)
 #pragma unroll
@@ -72,12 +79,13 @@ __global__ void __launch_bounds__(256) k_ray_gen(uint32_t cap_rays, const StepSt
 		march_queue[0] = 0; march_queue[1] = 0;
 		st_w->march_total = 0; st_w->kept_extent = 0;
 		st_w->n_kept = 0; st_w->n_rays_with_samples = 0;  // this step's march maxima / counts (k_march, k_march_write)
+		st_w->march_cut = mcut ? 1u : 0u;
 	}
 	const uint32_t R = st_r->rays_per_batch;
 	const uint32_t n_rays_global = R * dp.world, n_rays_total = st_r->n_rays_total;
 	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cap_rays; i += gridDim.x * blockDim.x) {
 		float o[3] = {0, 0, 0}, du[3] = {0, 0, 0}, startt = -1.0f;
-		if (i < R) {
+		if (i < R && i < lim) {
 			const uint32_t ig = dp.rank * R + i;
 			pcg32 rng(rng_state, rng_inc);
 			const uint32_t img = image_idx(ig, n_rays_global, n_rays_total, ds.n_images);
@@ -484,11 +492,18 @@ __global__ void __launch_bounds__(256) MARCH_OCC k_march_bal(uint32_t cap_rays, 
                                                    const float* __restrict__ rays, const float* __restrict__ tstart, uint32_t* __restrict__ nreq,
                                                    MarchWork mw) {
 	constexpr bool FAST = true;
-	const uint32_t est = st->march_est ? min(st->march_est, cap_rays) : cap_rays;
+	uint32_t est = st->march_est ? min(st->march_est, cap_rays) : cap_rays;
+	bool mcut = false;  // the march cut: pass 0 marches the slots below the estimate; pass 1 drops the rest behind one marker
+	if (mw.est_cut && *mw.est_cut / mw.est_div < est) { est = *mw.est_cut / mw.est_div; mcut = true; }
 	const uint32_t lo = pass == 0 ? 0u : est, hi = pass == 0 ? est : cap_rays;
 	if (lo >= hi) return;
-	if (pass == 1 && st->march_total >= max_samples) {
-		for (uint32_t k = lo + blockIdx.x * blockDim.x + threadIdx.x; k < hi; k += gridDim.x * blockDim.x) { nreq[k] = 1; mw.nrec[k] = 0; }
+	if (pass == 1 && (mcut || st->march_total >= max_samples)) {
+		for (uint32_t k = lo + blockIdx.x * blockDim.x + threadIdx.x; k < hi; k += gridDim.x * blockDim.x) {
+			// (a cut march: the first dropped slot requests past the cap - nothing after it is kept, and the requested count
+			// reads above max_samples, the next step's max_inference then max_samples - and the rest request nothing)
+			nreq[k] = mcut ? (k == lo ? max_samples + 1u : 0u) : 1u;
+			mw.nrec[k] = 0;
+		}
 		return;
 	}
 	const uint32_t lane = threadIdx.x & 63;
@@ -1455,6 +1470,12 @@ __global__ void __launch_bounds__(256) k_loss_ray(uint32_t cap_rays, StepState* 
 	const uint32_t R = st->rays_per_batch;
 	const uint32_t n_rays_global = R * dp.world, n_rays_total = st->n_rays_total;
 	const uint32_t cap64 = (cap_rays + 63u) & ~63u;
+	// the march cut's witness: the next step's abort word cleared; this step's set when (a) the march was cut
+	// and its slots do not fill the batch (the full march's later rays would have), or (b) a contributing ray ends past
+	// mi_lb (the last step's march was cut, so the reference's cap on this step's samples is known only to be at least
+	// mi_lb: a contributing ray past it might not have been kept there)
+	const uint32_t mi_lb = st->mi_lb;
+	if (lp.abort_w && blockIdx.x == 0 && threadIdx.x == 0) lp.abort_w[lp.abort_slot ^ 1u] = 0u;
 	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cap64; i += gridDim.x * blockDim.x) {
 		uint32_t comp = 0, cb = 0;
 		if (i < cap_rays) {
@@ -1462,6 +1483,7 @@ __global__ void __launch_bounds__(256) k_loss_ray(uint32_t cap_rays, StepState* 
 			const uint32_t cn = ccount[i];
 			cb = cbase[i];
 			if (i == cap_rays - 1) {
+				if (lp.abort_w && st->march_cut && cb + cn < lp.max_compacted) lp.abort_w[lp.abort_slot] = 1u;
 				st->compacted_counter = cb + cn;
 				st->compacted_global = cb + cn;                     // (all-reduced by the data-parallel exchange)
 				st->rays_ws_global = st->n_rays_with_samples;
@@ -1504,6 +1526,7 @@ __global__ void __launch_bounds__(256) k_loss_ray(uint32_t cap_rays, StepState* 
 					for (int k = 0; k < 3; ++k) rgb_ray[k] += T * bg[k];
 				}
 				comp = min(lp.max_compacted - min(lp.max_compacted, cb), cn);
+				if (lp.abort_w && mi_lb && comp > 0 && base + ns > mi_lb) lp.abort_w[lp.abort_slot] = 1u;
 				numsteps[2 * i] = comp; numsteps[2 * i + 1] = cb;
 				if (comp > 0) {
 					float lgrad[3], lloss[3];
@@ -1544,13 +1567,14 @@ __global__ void __launch_bounds__(256) k_loss_ray(uint32_t cap_rays, StepState* 
 
 // gradient of one compacted sample (testbed_nerf.cu:1775-1959): one thread per compacted sample cs (its ray from the
 // map k_loss_ray wrote; the pre-compaction samples past each ray's composited prefix are never visited)
-__global__ void __launch_bounds__(256) k_loss_grad(const StepState* __restrict__ st, DPInfo dp, LossParams lp,
+__global__ void __launch_bounds__(256) k_loss_grad(StepState* __restrict__ st, DPInfo dp, LossParams lp,
                                                    const float* __restrict__ coords, const half_t* __restrict__ net_out,
                                                    const uint32_t* __restrict__ numsteps, const uint32_t* __restrict__ cmap,
                                                    const uint32_t* __restrict__ rbase, const float4* __restrict__ sa, const float* __restrict__ ekt,
                                                    const float4* __restrict__ ck4, const float* __restrict__ cke, const float4* __restrict__ racc,
                                                    const float4* __restrict__ rgr, float* __restrict__ coords_out, half_t* __restrict__ dL_dout) {
 	if (lp.dbg_fence) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+	if (lp.abort_w && blockIdx.x == 0 && threadIdx.x == 0) st->cut_abort = lp.abort_w[lp.abort_slot];  // (k_loss_ray's witness)
 	const uint32_t n = min(st->compacted_counter, lp.max_compacted);
 	const uint32_t n_rays_global = st->rays_per_batch * dp.world;
 	const float loss_scale = lp.loss_scale / n_rays_global;
@@ -1680,8 +1704,10 @@ void launch_march_count(hipStream_t s, uint32_t cap, uint32_t max_samples, StepS
                         uint32_t* zero_counters, uint32_t n_zero, const float* occ_bbox) {
 	if (n_zero > 256) throw std::runtime_error("launch_march_count: at most 256 counters to zero");
 	dbg_lds_gate(s);
+	if (mw.est_cut && !(ds.cone_angle == 0.0f && mw.lanes_per_ray == 8 && mw.balanced))
+		throw std::runtime_error("launch_march_count: the march cut needs the balanced constant-step march");
 	k_ray_gen<<<ray_blocks(cap), 256, 0, s>>>(cap, st, dp, ds, rng_state, rng_inc, rays, tstart, mw.counter, st, mw.jt, zero_counters,
-	                                          zero_counters ? n_zero : 0u, occ_bbox);
+	                                          zero_counters ? n_zero : 0u, occ_bbox, mw.est_cut, std::max(1u, mw.est_div));
 	const uint32_t waves = mw.waves ? std::min(mw.waves, (cap + 63) / 64) : (cap + 63) / 64;
 	const uint32_t blocks = std::max<uint32_t>(1, (waves + 3) / 4);
 	for (uint32_t pass = 0; pass < 2; ++pass) {
@@ -1857,7 +1883,7 @@ void launch_loss_ray(hipStream_t s, uint32_t cap_rays, StepState* st, DPInfo dp,
 	k_loss_ray<<<ray_blocks(cap_rays), 256, 0, s>>>(cap_rays, st, dp, ds, lp, numsteps, ccount, cbase, w.sa, w.ekt, w.ck4, w.cke, w.racc, w.rT,
 	                                                  w.rgr, loss, ek, mask, w.cmap);
 }
-void launch_loss_grad(hipStream_t s, uint32_t cap_samples, const StepState* st, DPInfo dp, const LossParams& lp, const float* coords,
+void launch_loss_grad(hipStream_t s, uint32_t cap_samples, StepState* st, DPInfo dp, const LossParams& lp, const float* coords,
                       const half_t* net_out, const uint32_t* numsteps, const LossWork& w, float* coords_out, half_t* dL_dout) {
 	(void)cap_samples;  // (the compacted samples: at most lp.max_compacted)
 	dbg_lds_gate(s);

@@ -102,6 +102,7 @@ __global__ void __launch_bounds__(256) k_adam_ema(AdamParams p, float* __restric
                                                   const float* __restrict__ grads, float* __restrict__ m1, float* __restrict__ m2,
                                                   ST* __restrict__ steps, float* __restrict__ ema_tmp, half_t* __restrict__ ema_h,
                                                   StepCounterArgs sc, AdamTranspose tr) {
+	if (p.abort && *p.abort) return;  // (the step is re-run: nothing of it is applied)
 	if (sc.st && blockIdx.x == 0 && threadIdx.x == 0) step_counters_update(sc.st, sc.target_batch, sc.max_samples, sc.world, sc.fixed_rays, sc.eval_cnt, sc.n_eval);
 	const uint32_t ng = p.n / 4;
 	for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < ng; g += gridDim.x * blockDim.x) {

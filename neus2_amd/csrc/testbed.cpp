@@ -394,9 +394,44 @@ struct NeusTestbed {
 	uint64_t cut_steps = 0;
 	uint32_t call_left = 0;        // steps of the current train call after the current one
 	bool la_cut = false;           // the pending lookahead's step cuts (its sort was split)
+	bool la_mcut = false;          // the pending lookahead's march was cut (march_cut_for)
 	bool cut_for(uint32_t step, bool progressive, bool last_in_call, bool dyn) const {
 		const uint32_t nch = (uint32_t)chunk_ends.size() + 1;
 		return prog_cut && progressive && cfg.fixed_rays_per_batch && !dyn && step % 16 != 0 && !last_in_call && nch >= 2 && nch <= 15;
+	}
+	// The march cut: on a cut step the compaction cut lies, nearly always, well inside the slots below the
+	// split estimate (cutw[CW_EST]: at the bench's step 800, 5.6 K of the 41 K kept slots), and no ray past it contributes a
+	// training sample. So such a step generates and marches only those slots (MarchWork::est_cut). Two things make that
+	// step's training differ from the full march's, and k_loss_ray checks both (the witness): the marched slots may not
+	// fill the batch, and - on the step after - the reference's cap on the pre-compaction samples (max_inference, from the
+	// cut step's requested count) is then known only to be at least the marched slots' count, so a contributing ray past
+	// that bound might have been dropped there. Either sets StepState::cut_abort (all-reduced with the step's counters):
+	// the optimizer and the step counters of that step then change nothing, the host sees the word before it queues the
+	// next step, restores its own state to the step's start and runs the step again with the full march (after recounting
+	// the step before it in full when that one was cut, which makes its cap exact). The trained parameters are those of
+	// the full march in every case. A step the host reads back, one with (or before) an occupancy update, and the last two
+	// steps of a train call never cut the march, so the loss readback and the end of a call need no extra wait.
+	// NEUS_MARCH_CUT=0 turns it off.
+	bool march_cut_on = [] { const char* e = std::getenv("NEUS_MARCH_CUT"); return !(e && e[0] == '0'); }();
+	bool force_full = false;      // the step being re-run marches every slot
+	uint32_t mcut_div = [] { const char* e = std::getenv("NEUS_DBG_MARCH_CUT_DIV"); return e ? (uint32_t)std::max(1, std::atoi(e)) : 1u; }();  // test hook
+	bool mc_hist[2] = {false, false};  // the march of the last issued step / of the one before it was cut
+	struct StepSnap {
+		uint32_t training_step = 0, canonical_step = 0, adam_step = 0, call_left = 0;
+		int enc_step = 0;
+		float lr_factor = 1.f;
+		pcg32 rng{};
+		uint64_t la_steps = 0, cut_steps = 0, adam_split_steps = 0, mcut_steps = 0;
+	};
+	StepSnap snap[2];             // the host's step state at the start of the last issued step / of the one before it
+	bool abort_pending = false;   // the last issued step's abort word is on its way to pinned[100] (ev_abort)
+	hipEvent_t ev_abort = nullptr, ev_abort_src = nullptr;
+	uint64_t mcut_steps = 0, mcut_reruns = 0;
+	Dev<StepState> st_recount;
+	static bool occ_at(uint32_t cs) { const uint32_t n_prep = std::min(16u, std::max(1u, cs / 16u)); return cs % n_prep == 0; }
+	bool march_cut_for(uint32_t step, bool cut, uint32_t left_at_step) const {
+		if (!march_cut_on || force_full || !cut || profiling || !mwork.balanced || mwork.lanes_per_ray != 8 || ds.cone_angle != 0.0f) return false;
+		return (step + 1) % 16 != 0 && left_at_step >= 2 && !occ_at(step) && !occ_at(step + 1);
 	}
 	Dev<uint32_t> long_rays;  // the loss scan's wave-per-ray list (+ its counter in chunk_cnt[16])
 	TrainBufs tbuf{};
@@ -1237,6 +1272,7 @@ struct NeusTestbed {
 		ensure_bias_table();
 		p.bias_tab = adam_bias.p; p.bias_converged = bias_conv ? 1u : 0u;
 		{ static const bool eager = [] { const char* e = std::getenv("NEUS_EAGER_EMA_H"); return e && e[0] == '1'; }(); p.skip_ema_h = eager ? 0u : 1u; }
+		p.abort = &st.p->cut_abort;  // (the march cut's witness: a step that is re-run applies nothing)
 		return p;
 	}
 	// Adam in pieces beside the backward (adam_overlap; one rank, static scenes): the MLP blocks once the weight-gradient
@@ -1559,8 +1595,66 @@ struct NeusTestbed {
 
 	// ------------------------------------------------------------ one Testbed::train step (testbed.cu:2640-2736)
 	void train_step() {
+		if (abort_pending) check_abort();
+		train_step_body();
+	}
+	// The last issued step's march-cut witness (march_cut_on): when it aborted, its state changes were withheld on the
+	// device; the host state goes back to its start and the step runs again with the full march.
+	void check_abort() {
+		abort_pending = false;
+		HIP_CHECK(hipEventSynchronize(ev_abort));
+		uint32_t a = 0;
+		std::memcpy(&a, pinned + 100, 4);
+		if (!a) return;
+		// this testbed's streams drained (not the device's: another rank of an in-process group may share it)
+		for (hipStream_t q : {stream, aux_stream, la_stream, comm_stream})
+			if (q) HIP_CHECK(hipStreamSynchronize(q));
+		la_pending = false;
+		la_deferred = nullptr;
+		const uint32_t left = call_left;
+		const StepSnap s0 = snap[0], s1 = snap[1];
+		const bool prev_mc = mc_hist[1];
+		training_step = s0.training_step; canonical_step = s0.canonical_step; adam_step = s0.adam_step; call_left = s0.call_left;
+		enc_step = s0.enc_step; lr_factor = s0.lr_factor; rng = s0.rng;
+		la_steps = s0.la_steps; cut_steps = s0.cut_steps; adam_split_steps = s0.adam_split_steps; mcut_steps = s0.mcut_steps;
+		StepState h{};
+		HIP_CHECK(hipMemcpy(&h, st.p, sizeof(h), hipMemcpyDeviceToHost));
+		if (prev_mc) {
+			// the step before was cut too: its requested count in full (its rays again, from its rng and its n_rays_total), so
+			// that this step's cap is the reference's exactly (the bitfield is the one it marched: no occupancy update since)
+			StepState t = h;
+			t.n_rays_total = h.n_rays_total - h.rays_per_batch * world;
+			st_recount.alloc(1);
+			HIP_CHECK(hipMemcpy(st_recount.p, &t, sizeof(t), hipMemcpyHostToDevice));
+			launch_march_count(stream, MAX_RAYS, max_samples, st_recount.p, DPInfo{rank, world}, ds, bitfield.p, bf_lin.p, s1.rng.state, s1.rng.inc,
+			                   rays.p, startt.p, nreq.p, mwork, nullptr, 0, ray_cull ? occ_bbox.p : nullptr);
+			launch_march_write(stream, MAX_RAYS, st_recount.p, ds, rays.p, mwork, nreq.p, base.p, numsteps.p, coords.p, nullptr, max_samples,
+			                   scan_tmp.p, nullptr, 0);
+			HIP_CHECK(hipStreamSynchronize(stream));
+			HIP_CHECK(hipMemcpy(&t, st_recount.p, sizeof(t), hipMemcpyDeviceToHost));
+			const uint32_t before = t.numsteps_counter;
+			h.measured_before = before;
+			h.max_inference = (std::min(before, max_samples) + 127u) / 128u * 128u;
+		}
+		h.mi_lb = 0;
+		h.cut_abort = 0;
+		HIP_CHECK(hipMemcpy(st.p, &h, sizeof(h), hipMemcpyHostToDevice));
+		HIP_CHECK(hipMemset(cutw.p + CW_ABORT, 0, 2 * sizeof(uint32_t)));
+		snap[0] = s1;
+		mc_hist[0] = prev_mc;
+		++mcut_reruns;
+		force_full = true;
+		try { train_step_body(); } catch (...) { force_full = false; throw; }
+		force_full = false;
+		call_left = left;
+	}
+	void train_step_body() {
 		if (!have_net) throw std::runtime_error("train: no network (reload_network first)");
 		hipStream_t s = stream;
+		snap[1] = snap[0];
+		snap[0] = StepSnap{training_step, canonical_step, adam_step, call_left, enc_step, lr_factor, rng, la_steps, cut_steps, adam_split_steps, mcut_steps};
+		mc_hist[1] = mc_hist[0];
+		mc_hist[0] = false;
 		if (hgroup) hgroup->check();
 		verify_uniform_exchange();
 		// the readback of 16 steps back (long done on the device) is checked at this step boundary, before anything of
@@ -1609,12 +1703,16 @@ struct NeusTestbed {
 			if (la_stat && la_stat_used % 4 == 2) HIP_CHECK(hipEventRecord(la_stat_next(), s));
 			HIP_CHECK(hipStreamWaitEvent(s, ev_la_done, 0));  // this step's samples came from the previous step's lookahead
 			if (la_stat && la_stat_used % 4 == 3) HIP_CHECK(hipEventRecord(la_stat_next(), s));
-		} else {
-			issue_march(s, dp, rng, progressive, scan_tmp.p, cut_for(training_step, progressive, call_left == 0, dyn));
 		}
 		const bool cut = la_have ? la_cut : cut_for(training_step, progressive, call_left == 0, dyn);
+		const bool mcut = la_have ? la_mcut : march_cut_for(training_step, cut && sorted_rays, call_left);
+		if (!la_have) issue_march(s, dp, rng, progressive, scan_tmp.p, cut, mcut);
+		mc_hist[0] = mcut;
+		static const bool dbg_nowait = [] { const char* e = std::getenv("NEUS_DBG_ABORT_NOWAIT"); return e && e[0] == '1'; }();  // timing experiment (unsafe)
+		const bool risky = (mc_hist[0] || mc_hist[1]) && !dbg_nowait;  // (this step's witness can fail: the host waits for its word)
 		const bool split = cut && sorted_rays;
 		if (cut) ++cut_steps;
+		if (mcut) ++mcut_steps;
 		mark(2);
 		// DeltaNetwork forward on the samples (nerf_network.h:162-182); the loss keeps the undeformed records
 		const float* c_in = coords.p;
@@ -1622,6 +1720,7 @@ struct NeusTestbed {
 		LossParams lp{};
 		lp.loss_scale = LOSS_SCALE; lp.ek_w = cfg.ek_loss_weight; lp.mask_w = cfg.mask_loss_weight; lp.cos_anneal = cos_anneal();
 		lp.max_compacted = batch; lp.rng_state = rng.state; lp.rng_inc = rng.inc; lp.jt = jump_table();
+		lp.abort_w = cutw.p + CW_ABORT; lp.abort_slot = training_step & 1u;
 		{ static const bool f = [] { const char* e = std::getenv("NEUS_DBG_LOSS_FENCE"); return e && e[0] == '1'; }(); lp.dbg_fence = f ? 1u : 0u; }
 		const LossWork w = loss_work(base.p);
 		if (progressive) {
@@ -1707,8 +1806,20 @@ struct NeusTestbed {
 		if (coll_on()) {
 			cs = xo ? x_stream() : stream;
 			coll_begin();
-			allreduce_u32(&st.p->compacted_global, 2, cs);
+			allreduce_u32(&st.p->compacted_global, 3, cs);  // (+ cut_abort: every rank re-runs the step, or none)
 			coll_end();
+		}
+		if (risky) {
+			// the abort word to the host, off the step's stream (the backward starts at once)
+			if (!ev_abort) {
+				HIP_CHECK(hipEventCreateWithFlags(&ev_abort, hipEventDisableTiming));
+				HIP_CHECK(hipEventCreateWithFlags(&ev_abort_src, hipEventDisableTiming));
+			}
+			HIP_CHECK(hipEventRecord(ev_abort_src, cs));
+			HIP_CHECK(hipStreamWaitEvent(aux_stream, ev_abort_src, 0));
+			HIP_CHECK(hipMemcpyAsync(pinned + 100, &st.p->cut_abort, 4, hipMemcpyDeviceToHost, aux_stream));
+			HIP_CHECK(hipEventRecord(ev_abort, aux_stream));
+			abort_pending = true;
 		}
 		// ---- lookahead: the next step's ray sampling beside this step's backward (la_on; see the members)
 		const bool get_loss = training_step % 16 == 0;
@@ -1748,12 +1859,13 @@ struct NeusTestbed {
 				r1.advance();
 				const bool prog1 = progressive_mode == 2 || (progressive_mode == 1 && last_keep_ratio < PROGRESSIVE_RATIO);
 				la_cut = cut_for(training_step + 1, prog1, call_left <= 1, false);
-				const bool cut1 = la_cut;
-				la_deferred = [this, cs, dp, r1, prog1, cut1] {
+				la_mcut = march_cut_for(training_step + 1, la_cut && ray_sort, call_left - 1);
+				const bool cut1 = la_cut, mcut1 = la_mcut;
+				la_deferred = [this, cs, dp, r1, prog1, cut1, mcut1] {
 					HIP_CHECK(hipEventRecord(ev_la_start, cs));
 					HIP_CHECK(hipStreamWaitEvent(la_stream, ev_la_start, 0));
 					if (la_stat) { la_stat_used -= la_stat_used % 4; HIP_CHECK(hipEventRecord(la_stat_next(), la_stream)); }
-					issue_march(la_stream, dp, r1, prog1, scan_tmp_la.p, cut1);
+					issue_march(la_stream, dp, r1, prog1, scan_tmp_la.p, cut1, mcut1);
 					if (la_stat) HIP_CHECK(hipEventRecord(la_stat_next(), la_stream));
 					HIP_CHECK(hipEventRecord(ev_la_done, la_stream));
 				};
@@ -1867,13 +1979,16 @@ struct NeusTestbed {
 	// A step's ray sampling: ray generation + the march's two passes, the coordinate write (and round 0's list, unsorted
 	// progressive), the spatial ray sort (sorted progressive); rng / progressive: the step's own (train_step, or the
 	// lookahead for the next step), scan: the look-back state of the stream it runs on.
-	void issue_march(hipStream_t s, const DPInfo& dp, const pcg32& r, bool progressive, uint8_t* scan, bool cut = false) {
+	void issue_march(hipStream_t s, const DPInfo& dp, const pcg32& r, bool progressive, uint8_t* scan, bool cut = false, bool mcut = false) {
 		const uint32_t nch = (uint32_t)chunk_ends.size() + 1;
 		const Round0List r0{chunk_ends[0], cbase.p, chunk_list.p, chunk_cnt.p, nch + 1};
 		const bool sorted_rays = progressive && ray_sort;
-		launch_march_count(s, MAX_RAYS, max_samples, st.p, dp, ds, bitfield.p, bf_lin.p, r.state, r.inc, rays.p, startt.p, nreq.p, mwork,
+		MarchWork mw = mwork;
+		if (mcut) mw.est_cut = cutw.p + CW_EST;  // (the split sort's estimate: pass A's slots are the marched ones)
+		mw.est_div = mcut_div;
+		launch_march_count(s, MAX_RAYS, max_samples, st.p, dp, ds, bitfield.p, bf_lin.p, r.state, r.inc, rays.p, startt.p, nreq.p, mw,
 		                   progressive ? chunk_cnt.p : nullptr, RAW_CNT + nch, ray_cull ? occ_bbox.p : nullptr);  // list lengths + open-ray counts
-		launch_march_write(s, MAX_RAYS, st.p, ds, rays.p, mwork, nreq.p, base.p, numsteps.p, coords.p, nullptr, max_samples, scan,
+		launch_march_write(s, MAX_RAYS, st.p, ds, rays.p, mw, nreq.p, base.p, numsteps.p, coords.p, nullptr, max_samples, scan,
 		                   progressive && !sorted_rays ? &r0 : nullptr, dbg_lds_fill);
 		const RaySort rsort{rs_hist.p, rs_off.p, rs_key.p, rs_perm.p, chunk_cnt.p + RS_N_PERM};
 		const RaySplit split{cutw.p + CW_EST, ccount.p, cutw.p, MAX_RAYS, max_samples};
@@ -2039,6 +2154,8 @@ int neus_testbed_get_stats(NeusTestbed* tb, NeusTrainStats* o) {
 		o->progressive_chunk_end = tb->chunk_ends.empty() ? 0u : tb->chunk_ends[0];
 		o->lookahead_steps = tb->la_steps;
 		o->cut_steps = tb->cut_steps;
+		o->march_cut_steps = tb->mcut_steps;
+		o->march_cut_reruns = tb->mcut_reruns;
 		o->adam_split_steps = tb->adam_split_steps;
 		o->health_flags = s.fail_flags | tb->fail_seen | (scan_failures(tb->scan_tmp.p) ? STEP_FAIL_SCAN : 0u);
 		o->evaluated_samples_total = s.eval_total; o->progressive_steps = s.prog_steps; o->evaluated_samples_last = s.eval_last;

@@ -27,7 +27,8 @@ sha = lambda a: hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 res = {"params": sha(tb.get_params()), "ema_h": sha(tb.get_half_params(True)), "grid": sha(g), "bitfield": sha(bf),
        "counters": {k: st[k] for k in ("training_step", "rays_per_batch", "measured_batch_size", "measured_batch_size_before_compaction",
                                        "n_rays_total", "loss")},
-       "work": {k: st[k] for k in ("evaluated_samples_total", "cut_steps", "lookahead_steps", "progressive_steps")},
+       "work": {k: st[k] for k in ("evaluated_samples_total", "cut_steps", "lookahead_steps", "progressive_steps", "march_cut_steps",
+                                   "march_cut_reruns")},
        "env": {k: v for k, v in os.environ.items() if k.startswith("NEUS_")}}
 json.dump(res, open(sys.argv[1], "w"), indent=1)
 print(json.dumps(res))

@@ -2,7 +2,9 @@
 * the next step's ray sampling (the lookahead) with a data-parallel group: the step's counters are all-reduced right
   after the loss (StepState::compacted_global), so the sampling no longer waits for the whole exchange (VERDICT r5 #2);
 * the optimizer in pieces beside the grid scatter (NEUS_ADAM_OVERLAP=1): the MLP blocks after the weight-gradient
-  reduction, each grid level group after its accumulation launch.
+  reduction, each grid level group after its accumulation launch;
+* the compaction cut and the march cut (the march of a cut step limited to the slots below the cut's estimate, with its
+  witness and the host's re-run of a step whose witness failed).
 Each is compared bitwise with the same training without it. Reference: testbed_nerf.cu:3723-4001 (the step),
 adam.h:51-160 (elementwise Adam)."""
 import contextlib
@@ -153,6 +155,84 @@ def test_dp_adam_overlap_bitwise(scene):
     del ga, gb
 
 
+def _bench_shape_runs(configs, steps):
+    """Config S at the bench's shape (base.json, R = Nc = 2^18 fixed, progressive inference forced on), one testbed per
+    environment in `configs`, each trained `steps` steps in one call: (stats, params, grads, EMA, occupancy grid)."""
+    from neus2_amd import pyngp, scenes
+    sc = scenes.sphere_scene(49, 1600, 1200, principal=(823.2 / 1600, 619.1 / 1200))
+    n = 1 << 18
+    res = []
+    for env in configs:
+        with _env(**env):
+            tb = pyngp.Testbed(pyngp.TestbedMode.Nerf)
+            tb.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
+            tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=n, fixed_rays_per_batch=n)
+            tb.set_progressive_inference(2)
+            tb.train_steps(steps)
+            res.append((tb.stats(), tb.get_params(), tb.get_gradients(), tb.get_ema_params(), tb.get_density_grid()[0]))
+        del tb
+    return res
+
+
+STAT_KEYS = ("training_step", "rays_per_batch", "measured_batch_size", "measured_batch_size_before_compaction", "n_rays_total",
+             "n_rays_with_samples", "progressive_steps", "loss")
+
+
+def _same_run(a, b):
+    for k in STAT_KEYS:
+        assert a[0][k] == b[0][k], (k, a[0][k], b[0][k])
+    for x, y in zip(a[1:], b[1:]):
+        np.testing.assert_array_equal(x.view(np.uint32), y.view(np.uint32))
+
+
+def test_march_cut_bitwise(torch_cuda):
+    """The march cut (testbed.cpp march_cut_for): a cut step generates and marches only the ray slots below
+    the compaction cut's estimate. At the bench's shape, 600 steps in one call with it (the default), without it
+    (NEUS_MARCH_CUT=0) and with neither it nor the compaction cut (NEUS_PROG_CUT=0): bitwise the same parameters,
+    gradients, EMA weights, occupancy grid and last-step counters; the march was cut on most steps; a failed witness
+    (the re-run path) is counted."""
+    a, b, c = _bench_shape_runs([{"NEUS_MARCH_CUT": 1}, {"NEUS_MARCH_CUT": 0}, {"NEUS_PROG_CUT": 0, "NEUS_MARCH_CUT": 0}], 600)
+    assert a[0]["march_cut_steps"] > 300 and b[0]["march_cut_steps"] == 0, (a[0]["march_cut_steps"], b[0]["march_cut_steps"])
+    assert a[0]["cut_steps"] > 400 and c[0]["cut_steps"] == 0
+    _same_run(a, b)
+    _same_run(a, c)
+
+
+def test_march_cut_rerun_bitwise(torch_cuda):
+    """The re-run path of the march cut: with the test hook NEUS_DBG_MARCH_CUT_DIV=8 the cut march covers an eighth of the
+    estimate, so its slots often do not fill the batch (witness a) and the step after a cut one often has contributing rays
+    past the marched count's bound (witness b, which first recounts the step before in full). Every such step is run again
+    with the full march, nothing of its first run applied: 300 steps bitwise those without the march cut."""
+    a, b = _bench_shape_runs([{"NEUS_MARCH_CUT": 1, "NEUS_DBG_MARCH_CUT_DIV": 8}, {"NEUS_MARCH_CUT": 0}], 300)
+    assert a[0]["march_cut_reruns"] > 10, a[0]["march_cut_reruns"]
+    _same_run(a, b)
+
+
+def test_dp_march_cut_rerun_bitwise(scene):
+    """Two ranks (in-process group) with the march cut and the re-run hook (NEUS_DBG_MARCH_CUT_DIV=8, progressive inference
+    forced on): a failed witness on either rank is all-reduced with the step's counters, so both ranks withhold the step and
+    run it again together. 60 steps, bitwise two ranks without the march cut, on every rank."""
+    from neus2_amd import pyngp
+    R = 2048
+
+    def group(env):
+        with _env(**env):
+            g = pyngp.LocalGroup(2)
+            tbs = [_testbed(scene, R) for _ in range(2)]
+        for r in range(2):
+            tbs[r].set_progressive_inference(2)
+            g.join(tbs[r], r)
+        _parallel(lambda: tbs[0].train_steps(60), lambda: tbs[1].train_steps(60))
+        return g, tbs
+    ga, a = group({"NEUS_MARCH_CUT": 1, "NEUS_DBG_MARCH_CUT_DIV": 8})
+    gb, b = group({"NEUS_MARCH_CUT": 0})
+    sa = [t.stats() for t in a]
+    assert sa[0]["march_cut_steps"] > 0 and sa[0]["march_cut_reruns"] == sa[1]["march_cut_reruns"], sa
+    for x in (a[1], b[0], b[1]):
+        _same(a[0], x)
+    del ga, gb
+
+
 def test_compaction_cut_bitwise(torch_cuda):
     """The compaction cut (march.hip k_prog_cut): with fixed rays per batch, the progressive rounds after round 0 skip the
     rays whose compaction base is already past the batch, and round 0 itself runs the rays below the previous step's cut first
@@ -174,7 +254,7 @@ def test_compaction_cut_bitwise(torch_cuda):
         return tb
     res = {}
     for cut in (1, 0):
-        with _env(NEUS_PROG_CUT=cut):
+        with _env(NEUS_PROG_CUT=cut, NEUS_MARCH_CUT=0):
             tb = tb_()
         tb.train_steps(600)
         res[cut] = (tb.stats(), tb.get_params(), tb.get_gradients(), tb.get_ema_params(), tb.get_density_grid()[0])
