@@ -94,6 +94,7 @@ struct LossParams {
 	// Null: no witness (cut_abort stays 0)
 	uint32_t* abort_w = nullptr;
 	uint32_t abort_slot = 0;
+	uint32_t* abort_host = nullptr;  // (one rank) host-coherent pinned word the copy is also stored to, system scope
 };
 
 // binned hash-grid gradient scatter (grid.hip)

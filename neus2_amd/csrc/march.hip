@@ -1574,7 +1574,11 @@ __global__ void __launch_bounds__(256) k_loss_grad(StepState* __restrict__ st, D
                                                    const float4* __restrict__ ck4, const float* __restrict__ cke, const float4* __restrict__ racc,
                                                    const float4* __restrict__ rgr, float* __restrict__ coords_out, half_t* __restrict__ dL_dout) {
 	if (lp.dbg_fence) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-	if (lp.abort_w && blockIdx.x == 0 && threadIdx.x == 0) st->cut_abort = lp.abort_w[lp.abort_slot];  // (k_loss_ray's witness)
+	if (lp.abort_w && blockIdx.x == 0 && threadIdx.x == 0) {  // (k_loss_ray's witness)
+		const uint32_t a = lp.abort_w[lp.abort_slot];
+		st->cut_abort = a;
+		if (lp.abort_host) __hip_atomic_store(lp.abort_host, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+	}
 	const uint32_t n = min(st->compacted_counter, lp.max_compacted);
 	const uint32_t n_rays_global = st->rays_per_batch * dp.world;
 	const float loss_scale = lp.loss_scale / n_rays_global;

@@ -414,6 +414,8 @@ struct NeusTestbed {
 	// NEUS_MARCH_CUT=0 turns it off.
 	bool march_cut_on = [] { const char* e = std::getenv("NEUS_MARCH_CUT"); return !(e && e[0] == '0'); }();
 	bool force_full = false;      // the step being re-run marches every slot
+	bool abort_direct = false;            // the last risky step's word comes through abort_word (one rank)
+	volatile uint32_t* abort_word = nullptr;  // host-coherent pinned word k_loss_grad stores the witness to (one rank)
 	uint32_t mcut_div = [] { const char* e = std::getenv("NEUS_DBG_MARCH_CUT_DIV"); return e ? (uint32_t)std::max(1, std::atoi(e)) : 1u; }();  // test hook
 	bool mc_hist[2] = {false, false};  // the march of the last issued step / of the one before it was cut
 	struct StepSnap {
@@ -579,6 +581,7 @@ struct NeusTestbed {
 		for (auto& e : ev_done) if (e) (void)hipEventDestroy(e);
 		if (prof_st) (void)hipHostFree(prof_st);
 		if (pinned) (void)hipHostFree(pinned);
+		if (abort_word) (void)hipHostFree((void*)abort_word);
 		if (aux_stream) { (void)hipStreamSynchronize(aux_stream); (void)hipStreamDestroy(aux_stream); }
 		if (la_stream) { (void)hipStreamSynchronize(la_stream); (void)hipStreamDestroy(la_stream); }
 		if (ev_la_start) (void)hipEventDestroy(ev_la_start);
@@ -1602,9 +1605,19 @@ struct NeusTestbed {
 	// device; the host state goes back to its start and the step runs again with the full march.
 	void check_abort() {
 		abort_pending = false;
-		HIP_CHECK(hipEventSynchronize(ev_abort));
 		uint32_t a = 0;
-		std::memcpy(&a, pinned + 100, 4);
+		if (abort_direct) {
+			// one rank: k_loss_grad stored the word to host-coherent memory (sentinel ~0 before the step): poll it, and
+			// after a bounded spin wait for the step's stream (the kernel has then run)
+			const volatile uint32_t* w = abort_word;
+			for (uint32_t k = 0; k < (1u << 22) && *w == ~0u; ++k) __builtin_ia32_pause();
+			if (*w == ~0u) HIP_CHECK(hipStreamSynchronize(stream));
+			a = *w;
+			if (a == ~0u) throw std::runtime_error("march cut: the witness word was not written");
+		} else {
+			HIP_CHECK(hipEventSynchronize(ev_abort));
+			std::memcpy(&a, pinned + 100, 4);
+		}
 		if (!a) return;
 		// this testbed's streams drained (not the device's: another rank of an in-process group may share it)
 		for (hipStream_t q : {stream, aux_stream, la_stream, comm_stream})
@@ -1708,8 +1721,7 @@ struct NeusTestbed {
 		const bool mcut = la_have ? la_mcut : march_cut_for(training_step, cut && sorted_rays, call_left);
 		if (!la_have) issue_march(s, dp, rng, progressive, scan_tmp.p, cut, mcut);
 		mc_hist[0] = mcut;
-		static const bool dbg_nowait = [] { const char* e = std::getenv("NEUS_DBG_ABORT_NOWAIT"); return e && e[0] == '1'; }();  // timing experiment (unsafe)
-		const bool risky = (mc_hist[0] || mc_hist[1]) && !dbg_nowait;  // (this step's witness can fail: the host waits for its word)
+		const bool risky = mc_hist[0] || mc_hist[1];  // (this step's witness can fail: the host waits for its word)
 		const bool split = cut && sorted_rays;
 		if (cut) ++cut_steps;
 		if (mcut) ++mcut_steps;
@@ -1721,6 +1733,16 @@ struct NeusTestbed {
 		lp.loss_scale = LOSS_SCALE; lp.ek_w = cfg.ek_loss_weight; lp.mask_w = cfg.mask_loss_weight; lp.cos_anneal = cos_anneal();
 		lp.max_compacted = batch; lp.rng_state = rng.state; lp.rng_inc = rng.inc; lp.jt = jump_table();
 		lp.abort_w = cutw.p + CW_ABORT; lp.abort_slot = training_step & 1u;
+		if (risky && !coll_on()) {
+			// one rank: the word goes straight from k_loss_grad to host memory (no copy, no event on the step's streams)
+			if (!abort_word) {
+				void* p = nullptr;
+				HIP_CHECK(hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped));
+				abort_word = (volatile uint32_t*)p;
+			}
+			*abort_word = ~0u;
+			lp.abort_host = (uint32_t*)abort_word;
+		}
 		{ static const bool f = [] { const char* e = std::getenv("NEUS_DBG_LOSS_FENCE"); return e && e[0] == '1'; }(); lp.dbg_fence = f ? 1u : 0u; }
 		const LossWork w = loss_work(base.p);
 		if (progressive) {
@@ -1809,14 +1831,17 @@ struct NeusTestbed {
 			allreduce_u32(&st.p->compacted_global, 3, cs);  // (+ cut_abort: every rank re-runs the step, or none)
 			coll_end();
 		}
-		if (risky) {
-			// the abort word to the host, off the step's stream (the backward starts at once)
+		abort_direct = risky && !coll_on();
+		if (abort_direct) abort_pending = true;
+		if (risky && !abort_direct) {
+			// the all-reduced abort word to the host, off the step's stream (the backward starts at once)
 			if (!ev_abort) {
 				HIP_CHECK(hipEventCreateWithFlags(&ev_abort, hipEventDisableTiming));
 				HIP_CHECK(hipEventCreateWithFlags(&ev_abort_src, hipEventDisableTiming));
 			}
 			HIP_CHECK(hipEventRecord(ev_abort_src, cs));
 			HIP_CHECK(hipStreamWaitEvent(aux_stream, ev_abort_src, 0));
+			*(volatile uint32_t*)(pinned + 100) = ~0u;
 			HIP_CHECK(hipMemcpyAsync(pinned + 100, &st.p->cut_abort, 4, hipMemcpyDeviceToHost, aux_stream));
 			HIP_CHECK(hipEventRecord(ev_abort, aux_stream));
 			abort_pending = true;

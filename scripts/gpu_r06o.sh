@@ -5,7 +5,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" && mkdir -p gpurun_out
 TAG=${1:-r06o}
 for P in 800 1600; do
-for E in NEUS_DBG_ABORT_NOWAIT=0 NEUS_DBG_ABORT_NOWAIT=1 NEUS_DBG_ABORT_NOWAIT=0 NEUS_DBG_ABORT_NOWAIT=1; do
+for E in ${VARS:-NEUS_DBG_ABORT_NOWAIT=0 NEUS_DBG_ABORT_NOWAIT=1 NEUS_DBG_ABORT_NOWAIT=0 NEUS_DBG_ABORT_NOWAIT=1}; do
   env $E timeout -k 10 300 python -u bench.py --prepare $P --steps 100 --warmup 5 --cpu-baseline 0 --psnr-steps 0 --mc-res 0 --l16 0 --early 0 > "gpurun_out/bench_${TAG}_${P}_$E.log" 2>&1 || { echo "BENCH_FAIL $E"; exit 1; }
   python3 - "$E" "$P" "gpurun_out/bench_${TAG}_${P}_$E.log" <<'PY'
 import json, sys
