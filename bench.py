@@ -212,7 +212,7 @@ def step_roofline(d, levels, n_params, ms_per_step, steps, adam_b=None):
 def work_counters(st):
     return {"rays": st["rays_total"], "pre": st["pre_samples_total"], "evaluated": st["evaluated_samples_total"],
             "occ_samples": st["occ_samples_total"], "occ_updates": st["occ_updates"], "progressive": st["progressive_steps"],
-            "cut": st["cut_steps"]}
+            "cut": st["cut_steps"], "mcut": st["march_cut_steps"], "mcut_reruns": st["march_cut_reruns"]}
 
 
 def free_port():
@@ -455,6 +455,9 @@ def main():
         # steps whose later progressive rounds skipped the rays past the compaction cut (their network outputs
         # feed no training sample; the trained parameters are bitwise those without the cut, NEUS_PROG_CUT=0)
         "compaction_cut_steps_timed": d["cut"],
+        # steps whose sampling marched only the slots below the cut's estimate, and steps run again with the full march
+        # because the cut march's witness failed (nothing of the first run is applied)
+        "march_cut_steps_timed": d["mcut"], "march_cut_reruns_timed": d["mcut_reruns"],
         "progressive_chunk_end": st["progressive_chunk_end"],
         "non_rollover_fraction": round(d["trained_real"] / max(1, batch * args.steps), 4),
         **({"exchange": {**d["exchange"], **rccl_info(args, rank)}} if "exchange" in d else {}),

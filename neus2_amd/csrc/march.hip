@@ -63,7 +63,8 @@ __global__ void __launch_bounds__(256) k_ray_gen(uint32_t cap_rays, const StepSt
                                                  uint64_t rng_state, uint64_t rng_inc, float* __restrict__ rays, float* __restrict__ tstart,
                                                  uint32_t* __restrict__ march_queue, StepState* __restrict__ st_w, PcgJumpTable jt,
                                                  uint32_t* __restrict__ zero_counters, uint32_t n_zero, const float* __restrict__ occ_bbox,
-                                                 const uint32_t* __restrict__ est_cut, uint32_t est_div) {
+                                                 const uint32_t* __restrict__ est_cut, uint32_t est_div, uint32_t* __restrict__ nreq,
+                                                 uint32_t* __restrict__ nrec, uint32_t max_samples) {
 	if (blockIdx.x == 0 && threadIdx.x < n_zero) zero_counters[threadIdx.x] = 0u;  // the progressive rounds' list lengths
 	// the march cut (MarchWork::est_cut): the same test as k_march_bal's; the slots past the estimate are not marched, so
 	// they get no ray
@@ -84,8 +85,15 @@ __global__ void __launch_bounds__(256) k_ray_gen(uint32_t cap_rays, const StepSt
 	const uint32_t R = st_r->rays_per_batch;
 	const uint32_t n_rays_global = R * dp.world, n_rays_total = st_r->n_rays_total;
 	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cap_rays; i += gridDim.x * blockDim.x) {
+		if (i >= lim) {
+			// a cut march's dropped slots (k_march_bal's pass 1 leaves them): the first requests past the cap, the rest
+			// nothing; no ray
+			nreq[i] = i == lim ? max_samples + 1u : 0u;
+			nrec[i] = 0u;
+			continue;
+		}
 		float o[3] = {0, 0, 0}, du[3] = {0, 0, 0}, startt = -1.0f;
-		if (i < R && i < lim) {
+		if (i < R) {
 			const uint32_t ig = dp.rank * R + i;
 			pcg32 rng(rng_state, rng_inc);
 			const uint32_t img = image_idx(ig, n_rays_global, n_rays_total, ds.n_images);
@@ -497,13 +505,11 @@ __global__ void __launch_bounds__(256) MARCH_OCC k_march_bal(uint32_t cap_rays, 
 	if (mw.est_cut && *mw.est_cut / mw.est_div < est) { est = *mw.est_cut / mw.est_div; mcut = true; }
 	const uint32_t lo = pass == 0 ? 0u : est, hi = pass == 0 ? est : cap_rays;
 	if (lo >= hi) return;
-	if (pass == 1 && (mcut || st->march_total >= max_samples)) {
-		for (uint32_t k = lo + blockIdx.x * blockDim.x + threadIdx.x; k < hi; k += gridDim.x * blockDim.x) {
-			// (a cut march: the first dropped slot requests past the cap - nothing after it is kept, and the requested count
-			// reads above max_samples, the next step's max_inference then max_samples - and the rest request nothing)
-			nreq[k] = mcut ? (k == lo ? max_samples + 1u : 0u) : 1u;
-			mw.nrec[k] = 0;
-		}
+	// (a cut march: k_ray_gen marked the dropped slots - the first requests past the cap, so nothing after it is kept and
+	// the requested count reads above max_samples, the next step's max_inference then max_samples; the rest nothing)
+	if (pass == 1 && mcut) return;
+	if (pass == 1 && st->march_total >= max_samples) {
+		for (uint32_t k = lo + blockIdx.x * blockDim.x + threadIdx.x; k < hi; k += gridDim.x * blockDim.x) { nreq[k] = 1; mw.nrec[k] = 0; }
 		return;
 	}
 	const uint32_t lane = threadIdx.x & 63;
@@ -1402,7 +1408,8 @@ __global__ void __launch_bounds__(64) SCAN_OCC k_loss_scan_chunk(uint32_t cap_ra
 // later rounds use): also the next step's split estimate (the cut + 1/4 + 1024, whole waves) and pass B's samples added to
 // the round-0 evaluated count.
 __global__ void __launch_bounds__(256) k_prog_cut(uint32_t cap_rays, const uint32_t* __restrict__ ccount, const uint32_t* __restrict__ excl,
-                                                  uint32_t batch, uint32_t* __restrict__ cutw, int mode, uint32_t* __restrict__ eval0) {
+                                                  uint32_t batch, uint32_t* __restrict__ cutw, int mode, uint32_t* __restrict__ eval0,
+                                                  uint32_t* __restrict__ abort_if_none) {
 	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
 	if (i >= cap_rays) return;
 	const uint32_t e = excl[i], incl = e + ccount[i];
@@ -1417,6 +1424,9 @@ __global__ void __launch_bounds__(256) k_prog_cut(uint32_t cap_rays, const uint3
 		cutw[CW_CUT] = c;
 		cutw[CW_EST] = min(cap_rays, (c + c / 4u + 1024u + 63u) & ~63u);
 		if (eval0) *eval0 += cutw[CW_LENB_EFF];
+		// (a split round 0 whose pass B was not run - a cut march's step: pass A's slots must reach the batch, or the step
+		// is re-run; the march cut's witness word)
+		if (abort_if_none && !cross) *abort_if_none = 1u;
 	}
 }
 // The next round's work from the rays still open (rays_in: the scan's rays_out), the rays at or before the cut only: the
@@ -1711,7 +1721,7 @@ void launch_march_count(hipStream_t s, uint32_t cap, uint32_t max_samples, StepS
 	if (mw.est_cut && !(ds.cone_angle == 0.0f && mw.lanes_per_ray == 8 && mw.balanced))
 		throw std::runtime_error("launch_march_count: the march cut needs the balanced constant-step march");
 	k_ray_gen<<<ray_blocks(cap), 256, 0, s>>>(cap, st, dp, ds, rng_state, rng_inc, rays, tstart, mw.counter, st, mw.jt, zero_counters,
-	                                          zero_counters ? n_zero : 0u, occ_bbox, mw.est_cut, std::max(1u, mw.est_div));
+	                                          zero_counters ? n_zero : 0u, occ_bbox, mw.est_cut, std::max(1u, mw.est_div), nreq, mw.nrec, max_samples);
 	const uint32_t waves = mw.waves ? std::min(mw.waves, (cap + 63) / 64) : (cap + 63) / 64;
 	const uint32_t blocks = std::max<uint32_t>(1, (waves + 3) / 4);
 	for (uint32_t pass = 0; pass < 2; ++pass) {
@@ -1847,8 +1857,8 @@ void launch_loss_scan_chunk(hipStream_t s, uint32_t cap_rays, const uint32_t* nu
 		rays_out, n_rays_out);
 }
 void launch_prog_cut(hipStream_t s, uint32_t cap_rays, const uint32_t* ccount, const uint32_t* excl, uint32_t batch, uint32_t* cutw, int mode,
-                     uint32_t* eval0) {
-	k_prog_cut<<<(cap_rays + 255) / 256, 256, 0, s>>>(cap_rays, ccount, excl, batch, cutw, mode, eval0);
+                     uint32_t* eval0, uint32_t* abort_if_none) {
+	k_prog_cut<<<(cap_rays + 255) / 256, 256, 0, s>>>(cap_rays, ccount, excl, batch, cutw, mode, eval0, abort_if_none);
 }
 void launch_prog_next(hipStream_t s, uint32_t cap_rays, const uint32_t* rays_in, const uint32_t* n_in, const uint32_t* numsteps, const uint32_t* cut,
                       uint32_t e1, uint32_t e2, uint32_t* list, uint32_t* list_counter, uint32_t* rays_out, uint32_t* n_out) {

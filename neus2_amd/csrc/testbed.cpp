@@ -1721,7 +1721,9 @@ struct NeusTestbed {
 		const bool mcut = la_have ? la_mcut : march_cut_for(training_step, cut && sorted_rays, call_left);
 		if (!la_have) issue_march(s, dp, rng, progressive, scan_tmp.p, cut, mcut);
 		mc_hist[0] = mcut;
-		const bool risky = mc_hist[0] || mc_hist[1];  // (this step's witness can fail: the host waits for its word)
+		// (this step's witness can fail: the host waits for its word; a re-run step is exact by construction - not cut, and
+		// the step before it recounted when that one was cut)
+		const bool risky = (mc_hist[0] || mc_hist[1]) && !force_full;
 		const bool split = cut && sorted_rays;
 		if (cut) ++cut_steps;
 		if (mcut) ++mcut_steps;
@@ -1772,7 +1774,10 @@ struct NeusTestbed {
 				if (cut_k) {
 					// the cut after this round (cbase as the scan's scratch: the compaction rewrites it after the rounds), then
 					// the next round's rays and samples from the open rays at or before it
-					if (split) {
+					// a cut march's step: pass B (the slots past the estimate) was not marched, so it is skipped; pass A's
+					// slots must reach the batch, or the step is re-run (the witness word, set by the cut below)
+					const bool split_b = split && !mcut;
+					if (split_b) {
 						// pass A was the rays below the estimate: its cut, then pass B (empty when the cut lies in pass A's slots)
 						launch_exclusive_scan(s, scan_tmp.p, scan_tmp_bytes, ccount.p, cbase.p, MAX_RAYS);
 						launch_prog_cut(s, MAX_RAYS, ccount.p, cbase.p, batch, cutw.p, 0, nullptr);
@@ -1784,7 +1789,8 @@ struct NeusTestbed {
 						                       cutw.p + CW_NB_EFF, open_raw.p, chunk_cnt.p + RAW_CNT + k);
 					}
 					launch_exclusive_scan(s, scan_tmp.p, scan_tmp_bytes, ccount.p, cbase.p, MAX_RAYS);
-					launch_prog_cut(s, MAX_RAYS, ccount.p, cbase.p, batch, cutw.p, 1, split ? chunk_cnt.p : nullptr);
+					launch_prog_cut(s, MAX_RAYS, ccount.p, cbase.p, batch, cutw.p, 1, split_b ? chunk_cnt.p : nullptr,
+					                mcut ? cutw.p + CW_ABORT + (training_step & 1u) : nullptr);
 					launch_prog_next(s, MAX_RAYS, open_raw.p, chunk_cnt.p + RAW_CNT + k, numsteps.p, cutw.p + CW_CUT, e1, e2, chunk_list.p,
 					                 chunk_cnt.p + k + 1, open_rays[k & 1].p, chunk_cnt.p + OPEN_CNT + k);
 				}
@@ -1831,8 +1837,10 @@ struct NeusTestbed {
 			allreduce_u32(&st.p->compacted_global, 3, cs);  // (+ cut_abort: every rank re-runs the step, or none)
 			coll_end();
 		}
-		abort_direct = risky && !coll_on();
-		if (abort_direct) abort_pending = true;
+		if (risky) {
+			abort_pending = true;
+			abort_direct = !coll_on();
+		}
 		if (risky && !abort_direct) {
 			// the all-reduced abort word to the host, off the step's stream (the backward starts at once)
 			if (!ev_abort) {

@@ -155,7 +155,7 @@ def test_dp_adam_overlap_bitwise(scene):
     del ga, gb
 
 
-def _bench_shape_runs(configs, steps):
+def _bench_shape_runs(configs, steps, call=None):
     """Config S at the bench's shape (base.json, R = Nc = 2^18 fixed, progressive inference forced on), one testbed per
     environment in `configs`, each trained `steps` steps in one call: (stats, params, grads, EMA, occupancy grid)."""
     from neus2_amd import pyngp, scenes
@@ -168,7 +168,8 @@ def _bench_shape_runs(configs, steps):
             tb.set_dataset(sc["images"], sc["focal"], sc["principal"], sc["xforms"], 1)
             tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), batch_size=n, fixed_rays_per_batch=n)
             tb.set_progressive_inference(2)
-            tb.train_steps(steps)
+            for k in range(0, steps, call or steps):
+                tb.train_steps(min(call or steps, steps - k))
             res.append((tb.stats(), tb.get_params(), tb.get_gradients(), tb.get_ema_params(), tb.get_density_grid()[0]))
         del tb
     return res
@@ -206,6 +207,10 @@ def test_march_cut_rerun_bitwise(torch_cuda):
     a, b = _bench_shape_runs([{"NEUS_MARCH_CUT": 1, "NEUS_DBG_MARCH_CUT_DIV": 8}, {"NEUS_MARCH_CUT": 0}], 300)
     assert a[0]["march_cut_reruns"] > 10, a[0]["march_cut_reruns"]
     _same_run(a, b)
+    # the same in train calls of 23 steps (the re-runs land next to call ends, loss readbacks and occupancy updates)
+    c, = _bench_shape_runs([{"NEUS_MARCH_CUT": 1, "NEUS_DBG_MARCH_CUT_DIV": 8}], 300, call=23)
+    assert c[0]["march_cut_reruns"] > 10
+    _same_run(c, b)
 
 
 def test_dp_march_cut_rerun_bitwise(scene):
