@@ -374,6 +374,9 @@ void launch_loss_alpha_list(hipStream_t s, uint32_t cap_samples, const uint32_t*
 // evaluated samples added to *eval0 (null: none)
 void launch_prog_cut(hipStream_t s, uint32_t cap_rays, const uint32_t* ccount, const uint32_t* excl, uint32_t batch, uint32_t* cutw, int mode,
                      uint32_t* eval0, uint32_t* abort_if_none = nullptr);
+// launch_exclusive_scan(ccount -> excl) and launch_prog_cut in one launch (the look-back scan's state in scan_temp)
+void launch_scan_prog_cut(hipStream_t s, void* scan_temp, const uint32_t* ccount, uint32_t* excl, uint32_t n, uint32_t batch, uint32_t* cutw, int mode,
+                          uint32_t* eval0, uint32_t* abort_if_none = nullptr);
 void launch_prog_next(hipStream_t s, uint32_t cap_rays, const uint32_t* rays_in, const uint32_t* n_in, const uint32_t* numsteps, const uint32_t* cut,
                       uint32_t e1, uint32_t e2, uint32_t* list, uint32_t* list_counter, uint32_t* rays_out, uint32_t* n_out);
 void launch_loss_scan_chunk(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, const LossWork& w, uint32_t* ccount, uint32_t e0,

@@ -1429,6 +1429,60 @@ __global__ void __launch_bounds__(256) k_prog_cut(uint32_t cap_rays, const uint3
 		if (abort_if_none && !cross) *abort_if_none = 1u;
 	}
 }
+// The exclusive scan of ccount (k_scan_lookback's single pass) with k_prog_cut fused into its epilogue: the thread holding
+// the crossing slot (or the last slot, when the prefix never reaches the batch) writes the cut words. One launch instead
+// of two on the step's critical path; the scan and the words are those of the pair.
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan_prog_cut(const uint32_t* __restrict__ ccount, uint32_t* __restrict__ excl, uint32_t n,
+                                                                ScanState* __restrict__ ss, uint32_t tag, uint32_t batch, uint32_t* __restrict__ cutw,
+                                                                int mode, uint32_t* __restrict__ eval0, uint32_t* __restrict__ abort_if_none) {
+	__shared__ uint32_t s_prefix, s_wsum[SCAN_THREADS / 64];
+	const ScanTile tl = scan_tile(tag);
+	const size_t b0 = (size_t)tl.tile * SCAN_TILE + (size_t)threadIdx.x * SCAN_ITEMS;
+	uint32_t v[SCAN_ITEMS];
+	scan_load16(ccount, b0, n, true, v);
+	uint32_t tsum = 0;
+#pragma unroll
+	for (int k = 0; k < (int)SCAN_ITEMS; ++k) tsum += v[k];
+	uint32_t agg;
+	const uint32_t texcl = scan_block(tsum, s_wsum, agg);
+	if (threadIdx.x < 64) {
+		const uint32_t pre = scan_lookback(ss, 0, tl, agg);
+		if (threadIdx.x == 0) s_prefix = pre;
+	}
+	__syncthreads();
+	uint32_t run = s_prefix + texcl;
+#pragma unroll
+	for (int k = 0; k < (int)SCAN_ITEMS; ++k) {
+		const uint32_t x = v[k], i = (uint32_t)b0 + (uint32_t)k;
+		v[k] = run;
+		const bool cross = run < batch && run + x >= batch, none = i == n - 1 && run + x < batch;
+		run += x;
+		if ((cross || none) && i < n) {
+			const uint32_t c = cross ? i : n;
+			if (mode == 0) {
+				cutw[CW_CUT_A] = c;
+				cutw[CW_LENB_EFF] = cross ? 0u : cutw[CW_LENB];
+				cutw[CW_NB_EFF] = cross ? 0u : cutw[CW_NB];
+			} else {
+				cutw[CW_CUT] = c;
+				cutw[CW_EST] = min(n, (c + c / 4u + 1024u + 63u) & ~63u);
+				if (eval0) *eval0 += cutw[CW_LENB_EFF];
+				if (abort_if_none && !cross) *abort_if_none = 1u;
+			}
+		}
+	}
+	scan_store16(excl, b0, n, true, v);
+}
+void launch_scan_prog_cut(hipStream_t s, void* scan_temp, const uint32_t* ccount, uint32_t* excl, uint32_t n, uint32_t batch, uint32_t* cutw, int mode,
+                          uint32_t* eval0, uint32_t* abort_if_none) {
+	const uint32_t tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+	if (n == 0 || tiles > SCAN_MAX_TILES || (((uintptr_t)ccount | (uintptr_t)excl) & 15u))
+		throw std::runtime_error("launch_scan_prog_cut: 1 .. SCAN_MAX_TILES tiles of 16-B aligned counts");
+	dbg_lds_gate(s);
+	k_scan_prog_cut<<<tiles, SCAN_THREADS, 0, s>>>(ccount, excl, n, (ScanState*)scan_temp, scan_next_tag(scan_temp), batch, cutw, mode, eval0,
+	                                               abort_if_none);
+}
+
 // The next round's work from the rays still open (rays_in: the scan's rays_out), the rays at or before the cut only: the
 // ray to rays_out and its next chunk [e1, min(ns, e2)) to the sample list; one reservation per wave for each (the list
 // order differs from the scan's own append, which changes no result: every sample and every ray is independent).

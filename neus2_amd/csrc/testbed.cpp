@@ -357,6 +357,8 @@ struct NeusTestbed {
 	// composited at the last loss readback), 2 always; chunk ends of the rounds before the last (march.hip)
 	int progressive_mode = 1;
 	std::vector<uint32_t> chunk_ends{32, 64, 96};  // NEUS_CHUNK_ENDS="e0,e1,..." at creation overrides (A/B of schedules)
+	std::vector<uint32_t> chunk_ends_cut;          // the chunk ends of a cut step (chosen with chunk_ends; empty: chunk_ends)
+	const std::vector<uint32_t>& ends_for(bool cut) const { return cut && !chunk_ends_cut.empty() ? chunk_ends_cut : chunk_ends; }
 	// Chunk ends chosen from the training state (chunk_auto: no explicit ends given): at each loss readback the mean
 	// composited samples per ray with samples, mc (all-reduced counters: the same on every rank), sets three rounds
 	// {e, 2e, rest} with e = 0.5 mc + 12 rounded to 8 in [24, 128]. Measured at the bench workload (Config S, R = Nc =
@@ -369,6 +371,15 @@ struct NeusTestbed {
 		const float mc = (float)composited / (float)rays_with_samples;
 		const uint32_t e = std::min(128u, std::max(24u, 8u * (uint32_t)std::lround((0.5f * mc + 12.f) / 8.f)));
 		chunk_ends.assign({e, 2 * e});
+		// With the compaction cut (and the march cut) the later rounds see only the rays before the cut (a few thousand at
+		// the bench's shape), so their fixed cost - launches, scans, the cut - outweighs the samples a third round saves:
+		// two rounds, the first twice as long (steps 800 / 1600: 0.815 / 0.895 -> 0.773 / 0.878 ms/step,
+		// profiles/r06y_chunk_ends_cut_sweep.txt). NEUS_CHUNK_SCALE / NEUS_CHUNK_ROUNDS (2 or 3) override, for sweeps.
+		static const float scale = [] { const char* v = std::getenv("NEUS_CHUNK_SCALE"); return v ? (float)std::atof(v) : 2.f; }();
+		static const int rounds = [] { const char* v = std::getenv("NEUS_CHUNK_ROUNDS"); return v ? std::atoi(v) : 2; }();
+		const uint32_t ec = std::min(256u, std::max(24u, 8u * (uint32_t)std::lround(scale * (0.5f * mc + 12.f) / 8.f)));
+		if (rounds == 2) chunk_ends_cut.assign({ec});
+		else chunk_ends_cut.assign({ec, 2 * ec});
 	}
 	float last_keep_ratio = 1.f;
 	static constexpr float PROGRESSIVE_RATIO = 0.7f;
@@ -658,7 +669,7 @@ struct NeusTestbed {
 			for (const char* p = e; *p;) { char* q = nullptr; const unsigned long x = std::strtoul(p, &q, 10); if (q == p) break; v.push_back((uint32_t)x); p = *q ? q + 1 : q; }
 			bool ok = !v.empty() && v.size() <= 14 && v[0] > 0;
 			for (size_t k = 1; k < v.size(); ++k) ok = ok && v[k] > v[k - 1];
-			if (ok) { chunk_ends = v; chunk_auto = false; }
+			if (ok) { chunk_ends = v; chunk_auto = false; chunk_ends_cut.clear(); }
 		}
 		{ const char* e = std::getenv("NEUS_SCATTER_NOSKIP"); scatter_noskip = e && e[0] == '1'; }
 		grid_mean.alloc(4); grid_partial.alloc(GRID3 / 1024);
@@ -1705,9 +1716,6 @@ struct NeusTestbed {
 		mark(1);
 		// progressive (cut-off-aware) inference this step: its round-0 list is written by the march
 		const bool progressive = progressive_mode == 2 || (progressive_mode == 1 && last_keep_ratio < PROGRESSIVE_RATIO);
-		const uint32_t nch = (uint32_t)chunk_ends.size() + 1;
-		// round 0's list slots go through cbase (rewritten by the loss compaction before it is read again)
-		const Round0List r0{chunk_ends[0], cbase.p, chunk_list.p, chunk_cnt.p, nch + 1};
 		const bool sorted_rays = progressive && ray_sort;  // round 0's list by k_ray_sort_place instead of the march write
 		const RaySort rsort{rs_hist.p, rs_off.p, rs_key.p, rs_perm.p, chunk_cnt.p + RS_N_PERM};
 		if (la_have) {
@@ -1718,6 +1726,8 @@ struct NeusTestbed {
 			if (la_stat && la_stat_used % 4 == 3) HIP_CHECK(hipEventRecord(la_stat_next(), s));
 		}
 		const bool cut = la_have ? la_cut : cut_for(training_step, progressive, call_left == 0, dyn);
+		const std::vector<uint32_t>& ce = ends_for(cut);  // (a cut step's rounds: chunk_ends_cut)
+		const uint32_t nch = (uint32_t)ce.size() + 1;
 		const bool mcut = la_have ? la_mcut : march_cut_for(training_step, cut && sorted_rays, call_left);
 		if (!la_have) issue_march(s, dp, rng, progressive, scan_tmp.p, cut, mcut);
 		mc_hist[0] = mcut;
@@ -1754,8 +1764,8 @@ struct NeusTestbed {
 			// the compaction cut (prog_cut, cut_for): fixed rays per batch, not a step the host reads back (the loss readback
 			// steps, the last step of a train call), one rank's own batch
 			for (uint32_t k = 0; k < nch; ++k) {
-				const uint32_t e1 = k + 1 < nch ? chunk_ends[k] : 0xffffffffu;
-				const uint32_t e2 = k + 2 < nch ? chunk_ends[k + 1] : 0xffffffffu;
+				const uint32_t e1 = k + 1 < nch ? ce[k] : 0xffffffffu;
+				const uint32_t e2 = k + 2 < nch ? ce[k + 1] : 0xffffffffu;
 				// the loss's alpha terms in the inference epilogue (k_loss_alpha's work on the round's samples)
 				const InferAlpha ia{w.sa, w.ekt, lp.cos_anneal, ds.cone_angle == 0.0f ? 1u : 0u, nullptr, sorted_rays ? 8u : 0u};
 				it_arm();
@@ -1779,8 +1789,7 @@ struct NeusTestbed {
 					const bool split_b = split && !mcut;
 					if (split_b) {
 						// pass A was the rays below the estimate: its cut, then pass B (empty when the cut lies in pass A's slots)
-						launch_exclusive_scan(s, scan_tmp.p, scan_tmp_bytes, ccount.p, cbase.p, MAX_RAYS);
-						launch_prog_cut(s, MAX_RAYS, ccount.p, cbase.p, batch, cutw.p, 0, nullptr);
+						launch_scan_prog_cut(s, scan_tmp.p, ccount.p, cbase.p, MAX_RAYS, batch, cutw.p, 0, nullptr);
 						const InferAlpha iab{w.sa, w.ekt, lp.cos_anneal, ds.cone_angle == 0.0f ? 1u : 0u, nullptr, 8u};
 						it_arm();
 						launch_nerf_infer(s, lay.L, lay.W, cutw.p + CW_LENB_EFF, 0, c_in, gl, valid, params_h.p + lay.grid_off, mlp, net_out.p, 8192,
@@ -1788,9 +1797,8 @@ struct NeusTestbed {
 						launch_loss_scan_chunk(s, MAX_RAYS, numsteps.p, w, ccount.p, 0, e1, e2, nullptr, nullptr, rs_perm.p + MAX_RAYS,
 						                       cutw.p + CW_NB_EFF, open_raw.p, chunk_cnt.p + RAW_CNT + k);
 					}
-					launch_exclusive_scan(s, scan_tmp.p, scan_tmp_bytes, ccount.p, cbase.p, MAX_RAYS);
-					launch_prog_cut(s, MAX_RAYS, ccount.p, cbase.p, batch, cutw.p, 1, split_b ? chunk_cnt.p : nullptr,
-					                mcut ? cutw.p + CW_ABORT + (training_step & 1u) : nullptr);
+					launch_scan_prog_cut(s, scan_tmp.p, ccount.p, cbase.p, MAX_RAYS, batch, cutw.p, 1, split_b ? chunk_cnt.p : nullptr,
+					                     mcut ? cutw.p + CW_ABORT + (training_step & 1u) : nullptr);
 					launch_prog_next(s, MAX_RAYS, open_raw.p, chunk_cnt.p + RAW_CNT + k, numsteps.p, cutw.p + CW_CUT, e1, e2, chunk_list.p,
 					                 chunk_cnt.p + k + 1, open_rays[k & 1].p, chunk_cnt.p + OPEN_CNT + k);
 				}
@@ -1881,8 +1889,12 @@ struct NeusTestbed {
 					HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));  // (lo: least urgent, hi: most urgent; hi <= lo numerically)
 					if (want == 0) HIP_CHECK(hipStreamCreateWithFlags(&la_stream, hipStreamNonBlocking));
 					else HIP_CHECK(hipStreamCreateWithPriority(&la_stream, hipStreamNonBlocking, want > 0 ? hi : lo));
-					HIP_CHECK(hipEventCreateWithFlags(&ev_la_start, hipEventDisableTiming));
-					HIP_CHECK(hipEventCreateWithFlags(&ev_la_done, hipEventDisableTiming));
+					// (device-side hand-offs between the step's and the lookahead's kernels: no system-scope fence - its
+					// L2 write-back held the step's stream ~6 us at the record; NEUS_EV_SYSFENCE=1 keeps it, for A/B)
+					const char* f = std::getenv("NEUS_EV_SYSFENCE");
+					const unsigned fl = hipEventDisableTiming | (f && f[0] == '1' ? 0u : hipEventDisableSystemFence);
+					HIP_CHECK(hipEventCreateWithFlags(&ev_la_start, fl));
+					HIP_CHECK(hipEventCreateWithFlags(&ev_la_done, fl));
 				}
 				if (!scan_tmp_la.p || scan_tmp_la.n < scan_tmp_bytes + 256) {
 					scan_tmp_la.alloc(scan_tmp_bytes + 256);
@@ -2013,8 +2025,9 @@ struct NeusTestbed {
 	// progressive), the spatial ray sort (sorted progressive); rng / progressive: the step's own (train_step, or the
 	// lookahead for the next step), scan: the look-back state of the stream it runs on.
 	void issue_march(hipStream_t s, const DPInfo& dp, const pcg32& r, bool progressive, uint8_t* scan, bool cut = false, bool mcut = false) {
-		const uint32_t nch = (uint32_t)chunk_ends.size() + 1;
-		const Round0List r0{chunk_ends[0], cbase.p, chunk_list.p, chunk_cnt.p, nch + 1};
+		const std::vector<uint32_t>& ce = ends_for(cut);
+		const uint32_t nch = (uint32_t)ce.size() + 1;
+		const Round0List r0{ce[0], cbase.p, chunk_list.p, chunk_cnt.p, nch + 1};
 		const bool sorted_rays = progressive && ray_sort;
 		MarchWork mw = mwork;
 		if (mcut) mw.est_cut = cutw.p + CW_EST;  // (the split sort's estimate: pass A's slots are the marched ones)
@@ -2026,7 +2039,7 @@ struct NeusTestbed {
 		const RaySort rsort{rs_hist.p, rs_off.p, rs_key.p, rs_perm.p, chunk_cnt.p + RS_N_PERM};
 		const RaySplit split{cutw.p + CW_EST, ccount.p, cutw.p, MAX_RAYS, max_samples};
 		if (sorted_rays)
-			launch_ray_sort(s, MAX_RAYS, numsteps.p, coords.p, chunk_ends[0], rsort, chunk_list.p, chunk_cnt.p, scan, scan_tmp_bytes, cut ? &split : nullptr);
+			launch_ray_sort(s, MAX_RAYS, numsteps.p, coords.p, ce[0], rsort, chunk_list.p, chunk_cnt.p, scan, scan_tmp_bytes, cut ? &split : nullptr);
 	}
 
 	LossWork loss_work(const uint32_t* rbase) {
@@ -2457,6 +2470,7 @@ int neus_testbed_set_progressive_inference(NeusTestbed* tb, int mode, const uint
 			for (uint32_t k = 0; k < n_ends; ++k)
 				if (chunk_ends[k] == 0 || (k && chunk_ends[k] <= chunk_ends[k - 1])) throw std::runtime_error("chunk ends must increase from >= 1");
 			tb->chunk_ends.assign(chunk_ends, chunk_ends + n_ends);
+			tb->chunk_ends_cut.clear();
 			tb->chunk_auto = false;
 		}
 		tb->progressive_mode = mode;

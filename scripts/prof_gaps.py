@@ -1,7 +1,7 @@
 """Gaps between consecutive kernels of one queue in a rocprofv3 kernel trace (development tool): for every (previous,
 next) kernel pair on the same queue over the final K training steps, the number of transitions and the median idle gap
 between the previous kernel's end and the next one's start.
-Usage: prof_gaps.py <trace dir or .db> [--last-steps K]"""
+Usage: prof_gaps.py <trace dir or .db> [--last-steps K | --all]"""
 import glob
 import os
 import sqlite3
@@ -19,15 +19,18 @@ def main():
         i = args.index("--last-steps")
         k = int(args[i + 1])
         del args[i:i + 2]
-    path = args[0]
+    path = [a for a in args if not a.startswith("--")][0]
     if os.path.isdir(path):
         path = glob.glob(os.path.join(path, "**", "*.db"), recursive=True)[0]
     con = sqlite3.connect(path)
     cols = [r[1] for r in con.execute("pragma table_info(kernels)")]
     qcol = next((c for c in ("queue_id", "stream_id", "queue") if c in cols), None)
     ks = list(con.execute(f"select name, start, end, {qcol or 0} from kernels order by start"))
-    adam = step_ends([(n, s, e) for n, s, e, _ in ks])
-    t0, t1 = ks[adam[-k - 1]][2], ks[adam[-1]][2]
+    if "--all" in args:  # every kernel of the trace (replays, diagnostics)
+        t0, t1, k = ks[0][1], ks[-1][2], 1
+    else:
+        adam = step_ends([(n, s, e) for n, s, e, _ in ks])
+        t0, t1 = ks[adam[-k - 1]][2], ks[adam[-1]][2]
     byq = defaultdict(list)
     for n, s, e, q in ks:
         if t0 <= s <= t1:
