@@ -392,7 +392,7 @@ void debug_launch_loss_scan(hipStream_t s, int variant, uint32_t cap_rays, const
 void launch_ray_index(hipStream_t s, uint32_t cap_rays, const uint32_t* numsteps, StepState* st, uint32_t* sample_ray, uint32_t* rbase);
 void launch_rollover(hipStream_t s, uint32_t n_elements, const StepState* st, float* coords, half_t* dL_dout);
 void launch_step_counters(hipStream_t s, StepState* st, uint32_t target_batch, uint32_t max_samples, uint32_t world, uint32_t fixed_rays,
-                          const uint32_t* eval_cnt = nullptr, uint32_t n_eval = 0);
+                          const uint32_t* eval_cnt = nullptr, uint32_t n_eval = 0, uint32_t* abort_host = nullptr);
 // render.hip (rays: RenderRay records, render_ray_bytes() each)
 size_t render_ray_bytes();
 void launch_render_init(hipStream_t s, const RenderCamera& cam, uint32_t sample_index, const DevDataset& ds, const uint8_t* bf, const uint32_t* lin,

@@ -1757,8 +1757,10 @@ __global__ void k_rollover(uint32_t n_elements, const StepState* __restrict__ st
 // (testbed_nerf.cu:3771-3776) + n_rays_total (testbed_nerf.cu:3784-3790). `world` divides the
 // all-reduced counters so every rank adapts R identically.
 __global__ void k_step_counters(StepState* st, uint32_t target_batch, uint32_t max_samples, uint32_t world, uint32_t fixed_rays,
-                                const uint32_t* eval_cnt, uint32_t n_eval) {
+                                const uint32_t* eval_cnt, uint32_t n_eval, uint32_t* abort_host) {
 	if (threadIdx.x != 0 || blockIdx.x != 0) return;
+	// (the march cut's all-reduced witness word to the host, system scope: the host polls it before its next step)
+	if (abort_host) __hip_atomic_store(abort_host, st->cut_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 	step_counters_update(st, target_batch, max_samples, world, fixed_rays, eval_cnt, n_eval);
 }
 
@@ -1965,9 +1967,9 @@ void launch_rollover(hipStream_t s, uint32_t n_elements, const StepState* st, fl
 	k_rollover<<<std::max<uint32_t>(1, std::min<uint32_t>((n_elements + 255) / 256, 2048)), 256, 0, s>>>(n_elements, st, coords, dL_dout);
 }
 void launch_step_counters(hipStream_t s, StepState* st, uint32_t target_batch, uint32_t max_samples, uint32_t world, uint32_t fixed_rays,
-                          const uint32_t* eval_cnt, uint32_t n_eval) {
+                          const uint32_t* eval_cnt, uint32_t n_eval, uint32_t* abort_host) {
 	dbg_lds_gate(s);
-	k_step_counters<<<1, 64, 0, s>>>(st, target_batch, max_samples, world, fixed_rays, eval_cnt, n_eval);
+	k_step_counters<<<1, 64, 0, s>>>(st, target_batch, max_samples, world, fixed_rays, eval_cnt, n_eval, abort_host);
 }
 
 } // namespace neus

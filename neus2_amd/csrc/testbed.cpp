@@ -193,10 +193,12 @@ struct NeusTestbed {
 	bool la_pending = false, la_next_in_call = false;
 	uint64_t la_steps = 0, adam_split_steps = 0;  // (stats: lookahead_steps, adam_split_steps)
 	const bool la_stat = [] { const char* e = std::getenv("NEUS_LA_STAT"); return e && e[0] == '1'; }();
-	// development (NEUS_LA_AT): where in the backward the lookahead is issued. 0 right after the loss (the default), 1 after
-	// the training encode, 2 after the training MLP kernels, 3 after the weight-gradient reduction, 4 after the scatter
-	// (profiles/r05la_issue_point_ab.txt: 1 as 0, 2 and 3 slower)
-	const int la_at = [] { const char* e = std::getenv("NEUS_LA_AT"); return e ? std::atoi(e) : 0; }();
+	// NEUS_LA_AT: where in the backward the lookahead is issued (one rank; with a group it goes out with the counters'
+	// exchange). 0 right after the loss, 1 after the training encode (the default since the march cut made the sampling
+	// small: it no longer shares the gather-bound encode, 0.770 -> 0.759 ms/step at step 800, 0.876 -> 0.854 at step 1600,
+	// profiles/r06la_issue_point_ab.txt; round 5, with the full march: 1 as 0, r05la_issue_point_ab.txt), 2 after the
+	// training MLP kernels, 3 after the weight-gradient reduction, 4 after the scatter (2 and 3 slower in both rounds)
+	const int la_at = [] { const char* e = std::getenv("NEUS_LA_AT"); return e ? std::atoi(e) : 1; }();
 	std::function<void()> la_deferred;
 	void la_fire(int at) {
 		if (la_deferred && at >= la_at) { auto f = std::move(la_deferred); la_deferred = nullptr; f(); }
@@ -1849,6 +1851,28 @@ struct NeusTestbed {
 			abort_pending = true;
 			abort_direct = !coll_on();
 		}
+		// ---- lookahead: the next step's ray sampling beside this step's backward (la_on; see the members)
+		const bool get_loss = training_step % 16 == 0;
+		const StepCounterArgs sca{st.p, batch, max_samples, world, cfg.fixed_rays_per_batch, progressive ? chunk_cnt.p : nullptr, nch};
+		bool counters_done = false;
+		const uint32_t cs1 = training_step + 1;  // the next step's canonical step (static scenes)
+		const uint32_t n_prep1 = std::min(16u, std::max(1u, cs1 / 16u));
+		const bool la_go = la_on && la_next_in_call && !dyn && !use_delta && !profiling && !dbg_loss_replay &&
+		                   !dbg_lds_fill && g_dbg_lds_fill == 0 && g_dbg_xcd_shift == 0 && cs1 % 16 != 0 && cs1 % n_prep1 != 0 &&
+		                   !(get_loss && loss_pending);
+		// with a group, the all-reduced word goes to the host from the step counters' launch that the lookahead puts right
+		// behind the exchange (a system-scope store, as k_loss_grad's at one rank); otherwise by a copy and an event
+		uint32_t* abort_host_ctr = nullptr;
+		if (risky && coll_on() && la_go) {
+			if (!abort_word) {
+				void* p = nullptr;
+				HIP_CHECK(hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped));
+				abort_word = (volatile uint32_t*)p;
+			}
+			*abort_word = ~0u;
+			abort_host_ctr = (uint32_t*)abort_word;
+			abort_direct = true;
+		}
 		if (risky && !abort_direct) {
 			// the all-reduced abort word to the host, off the step's stream (the backward starts at once)
 			if (!ev_abort) {
@@ -1862,22 +1886,13 @@ struct NeusTestbed {
 			HIP_CHECK(hipEventRecord(ev_abort, aux_stream));
 			abort_pending = true;
 		}
-		// ---- lookahead: the next step's ray sampling beside this step's backward (la_on; see the members)
-		const bool get_loss = training_step % 16 == 0;
-		const StepCounterArgs sca{st.p, batch, max_samples, world, cfg.fixed_rays_per_batch, progressive ? chunk_cnt.p : nullptr, nch};
-		bool counters_done = false;
 		{
-			const uint32_t cs1 = training_step + 1;  // the next step's canonical step (static scenes)
-			const uint32_t n_prep1 = std::min(16u, std::max(1u, cs1 / 16u));
-			const bool la_go = la_on && la_next_in_call && !dyn && !use_delta && !profiling && !dbg_loss_replay &&
-			                   !dbg_lds_fill && g_dbg_lds_fill == 0 && g_dbg_xcd_shift == 0 && cs1 % 16 != 0 && cs1 % n_prep1 != 0 &&
-			                   !(get_loss && loss_pending);
 			if (la_go) {
 				// the host's StepState readback first (its place in the step without the lookahead: nothing it reads is
 				// written between here and there - the ranks' counts are already summed), then the step counters the next
 				// step's sampling reads; both behind the counters' exchange (cs)
 				if (get_loss) HIP_CHECK(hipMemcpyAsync(pinned + 64, st.p, sizeof(StepState), hipMemcpyDeviceToHost, cs));
-				launch_step_counters(cs, st.p, batch, max_samples, world, cfg.fixed_rays_per_batch, sca.eval_cnt, sca.n_eval);
+				launch_step_counters(cs, st.p, batch, max_samples, world, cfg.fixed_rays_per_batch, sca.eval_cnt, sca.n_eval, abort_host_ctr);
 				counters_done = true;
 				if (!la_stream) {
 					// the lookahead stream at the lowest priority: the backward's workgroups are dispatched first and the march's
