@@ -193,12 +193,15 @@ struct NeusTestbed {
 	bool la_pending = false, la_next_in_call = false;
 	uint64_t la_steps = 0, adam_split_steps = 0;  // (stats: lookahead_steps, adam_split_steps)
 	const bool la_stat = [] { const char* e = std::getenv("NEUS_LA_STAT"); return e && e[0] == '1'; }();
-	// NEUS_LA_AT: where in the backward the lookahead is issued (one rank; with a group it goes out with the counters'
-	// exchange). 0 right after the loss, 1 after the training encode (the default since the march cut made the sampling
-	// small: it no longer shares the gather-bound encode, 0.770 -> 0.759 ms/step at step 800, 0.876 -> 0.854 at step 1600,
-	// profiles/r06la_issue_point_ab.txt; round 5, with the full march: 1 as 0, r05la_issue_point_ab.txt), 2 after the
-	// training MLP kernels, 3 after the weight-gradient reduction, 4 after the scatter (2 and 3 slower in both rounds)
-	const int la_at = [] { const char* e = std::getenv("NEUS_LA_AT"); return e ? std::atoi(e) : 1; }();
+	// Where in the backward the lookahead is issued (one rank; with a group it goes out with the counters' exchange):
+	// 0 right after the loss, 1 after the training encode, 2 after the training MLP kernels, 3 after the weight-gradient
+	// reduction, 4 after the scatter. A cut march's sampling is small and goes after the encode (it then no longer shares
+	// the gather-bound encode: 0.770 -> 0.759 ms/step at step 800, 0.876 -> 0.854 at step 1600,
+	// profiles/r06la_issue_point_ab.txt); a full march needs the whole backward to hide in and goes right after the loss
+	// (round 5: 1 as 0, 2 and 3 slower, r05la_issue_point_ab.txt). NEUS_LA_AT / NEUS_LA_AT_FULL override the two.
+	const int la_at_cut = [] { const char* e = std::getenv("NEUS_LA_AT"); return e ? std::atoi(e) : 1; }();
+	const int la_at_full = [] { const char* e = std::getenv("NEUS_LA_AT_FULL"); return e ? std::atoi(e) : 0; }();
+	int la_at = 0;  // the pending lookahead's issue point
 	std::function<void()> la_deferred;
 	void la_fire(int at) {
 		if (la_deferred && at >= la_at) { auto f = std::move(la_deferred); la_deferred = nullptr; f(); }
@@ -1921,6 +1924,7 @@ struct NeusTestbed {
 				la_cut = cut_for(training_step + 1, prog1, call_left <= 1, false);
 				la_mcut = march_cut_for(training_step + 1, la_cut && ray_sort, call_left - 1);
 				const bool cut1 = la_cut, mcut1 = la_mcut;
+				la_at = mcut1 ? la_at_cut : la_at_full;
 				la_deferred = [this, cs, dp, r1, prog1, cut1, mcut1] {
 					HIP_CHECK(hipEventRecord(ev_la_start, cs));
 					HIP_CHECK(hipStreamWaitEvent(la_stream, ev_la_start, 0));
