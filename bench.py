@@ -131,6 +131,9 @@ def kernel_table(levels):
         # Adam + EMA: 14 B per parameter + 34 B per stepped parameter (adam_bytes); the replay advances the optimizer
         # (after the timed steps)
         "adam_ema": (12, 48, 0),
+        # the march of a cut step (the march cut: the slots below the compaction cut's estimate); last, it leaves a cut
+        # march's state behind
+        "march_cut": (13, 40, 0),
     }
 
 
@@ -410,8 +413,11 @@ def main():
     inf = step_inference(it, levels)
     # per-kernel timing of the other kernels after that, on the final state (hipEvents on the testbed stream)
     kern = kernel_rooflines(tb, levels)
-    per_step = {k: v["ms"] for k, v in kern.items() if k != "inference"}
+    per_step = {k: v["ms"] for k, v in kern.items() if k not in ("inference", "march_cut")}
     per_step["inference_step"] = inf["ms_per_step"]
+    # the step's march: the cut march on the steps that cut it, the full march on the others (the replays time both)
+    fcut = d["mcut"] / max(1, args.steps)
+    per_step["march"] = round(fcut * kern["march_cut"]["ms"] + (1 - fcut) * kern["march"]["ms"], 4)
     dom = max(per_step, key=per_step.get)
     dk = inf if dom == "inference_step" else kern[dom]
     mlp = ("mlp_train_rgb", "mlp_train_density")

@@ -320,7 +320,9 @@ int neus_debug_time_kernel(NeusTestbed* tb, int kernel, int variant, int iters, 
  * kernel: 0 ray generation + march (units: ray slots), 1 coordinate write, 2 loss transmittance scan,
  * 3 fused inference, 4 loss alpha (units: pre-compaction samples), 5 training MLP, 6 weight gradients,
  * 7 grid-gradient scatter, 8 training-batch grid encode, 9 / 10 the colour / density training-MLP kernel alone
- * (units: compacted samples), 12 the Adam / EMA pass (units: parameters; the replays advance the optimizer). */
+ * (units: compacted samples), 12 the Adam / EMA pass (units: parameters; the replays advance the optimizer), 13 ray
+ * generation + march of a cut step (the march cut: only the slots below the compaction cut's estimate; units: those
+ * slots; it leaves the state of a cut march behind, so it goes after the other replays). */
 int neus_testbed_time_kernel(NeusTestbed* tb, int kernel, int iters, float* ms_out, uint32_t* units_out);
 // Development statistic of the last step's march: per ray {march_step calls, skip-loop additions,
 // samples} (3 x u32 per ray, n rays; cone_angle 0 only).

@@ -2576,6 +2576,12 @@ int neus_testbed_time_kernel(NeusTestbed* tb, int kernel, int iters, float* ms_o
 		// work units of one launch: ray slots (march), pre-compaction samples (write, inference, loss),
 		// compacted training samples (encode, MLP, weight gradients, grid scatter), parameters (Adam / EMA)
 		*units_out = kernel == 0 ? MAX_RAYS : kernel <= 4 ? h.n_kept : kernel == 12 ? tb->lay.P : tb->batch;
+		if (kernel == 13) {  // the slots a cut march generates and marches
+			uint32_t est = MAX_RAYS;
+			HIP_CHECK(hipMemcpy(&est, tb->cutw.p + CW_EST, 4, hipMemcpyDeviceToHost));
+			const uint32_t e0 = h.march_est ? std::min(h.march_est, MAX_RAYS) : MAX_RAYS;
+			*units_out = std::min(est, e0);
+		}
 	});
 }
 static void time_kernel_impl(NeusTestbed* tb, int kernel, int variant, int iters, float* ms_out) {
@@ -2637,6 +2643,13 @@ static void time_kernel_impl(NeusTestbed* tb, int kernel, int variant, int iters
 				break;
 			}
 			case 12: t.optimizer_step(t.grads.p); break;  // the Adam / EMA pass on the last gradient (advances the optimizer)
+			case 13: {  // the march of a cut step: ray generation + the march over the slots below the cut's estimate
+				MarchWork mw = t.mwork;
+				mw.est_cut = t.cutw.p + CW_EST;
+				launch_march_count(s, MAX_RAYS, t.max_samples, t.st.p, dp, t.ds, t.bitfield.p, lin, t.rng.state, t.rng.inc, t.rays.p, t.startt.p, t.nreq.p,
+				                   mw, nullptr, 0, t.ray_cull ? t.occ_bbox.p : nullptr);
+				break;
+			}
 			default: throw std::runtime_error("unknown kernel id");
 			}
 		}
