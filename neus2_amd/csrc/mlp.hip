@@ -1701,7 +1701,8 @@ void launch_nerf_infer(hipStream_t s, uint32_t L, uint32_t W, const uint32_t* n_
 	// same 3 waves per SIMD, amdgpu_waves_per_eu)
 	static const bool pipe = [] { const char* e = std::getenv("NEUS_INFER_PIPE"); return !(e && e[0] == '0'); }();
 	const bool all = pipe && valid_level + 1 >= L;
-	auto xg = [&](uint32_t b) { return a.xcd_parts ? std::max(8u, b & ~7u) : b; };
+	static const uint32_t grid_cap = [] { const char* e = std::getenv("NEUS_INFER_GRID"); return e ? (uint32_t)std::atoi(e) : 0u; }();  // (development)
+	auto xg = [&](uint32_t b) { if (grid_cap) b = std::min(b, grid_cap); return a.xcd_parts ? std::max(8u, b & ~7u) : b; };
 	dbg_lds_gate(s);
 	const hipEvent_t ev0 = g_infer_ev[0], ev1 = g_infer_ev[1];
 	g_infer_ev[0] = g_infer_ev[1] = nullptr;

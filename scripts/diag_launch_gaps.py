@@ -21,7 +21,8 @@ tb.reload_network_from_file(os.path.join(ROOT, "configs", "nerf", "base.json"), 
 tb.train_steps(40)
 tb.synchronize()
 iters = int(os.environ.get("ITERS", "10"))
+variant = int(os.environ.get("VARIANT", "98"))  # 98: back to back, no event between the launches
 for kid in (3, 8, 2):
     ms = C.c_float()
-    check(lib().neus_debug_time_kernel(tb.handle, kid, 0, iters, C.byref(ms)))
+    check(lib().neus_debug_time_kernel(tb.handle, kid, variant, iters, C.byref(ms)))
     print("kernel", kid, "ms per launch", round(ms.value, 4), flush=True)
