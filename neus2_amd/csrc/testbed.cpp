@@ -2644,6 +2644,29 @@ static void time_kernel_impl(NeusTestbed* tb, int kernel, int variant, int iters
 				break;
 			}
 			case 12: t.optimizer_step(t.grads.p); break;  // the Adam / EMA pass on the last gradient (advances the optimizer)
+			case 14: {  // development: the occupancy update's density pass (k_nerf_density MODE 2 into the scratch grid) on the
+				        // current state: variant 0 both halves (after step 256), 1 the uniform half, 2 the occupancy-biased half
+				const uint32_t nc = GRID3 * (t.max_cascade + 1);
+				const uint32_t n_u = variant == 2 ? 0u : nc / 4, n_nu = variant == 1 ? 0u : nc / 4;
+				pcg32 r = t.density_grid_rng;
+				const pcg32 rng_u = r;
+				r.advance();
+				const pcg32 rng_nu = r;
+				OccSampling os{};
+				os.n_u = n_u; os.n_nu = n_nu; os.lo = 0;
+				os.rng_u_state = rng_u.state; os.rng_u_inc = rng_u.inc; os.rng_nu_state = rng_nu.state; os.rng_nu_inc = rng_nu.inc;
+				os.step = t.density_grid_ema_step; os.n_cascades = t.max_cascade + 1; os.thresh_nu = NERF_MIN_OPTICAL_THICKNESS;
+				for (int d = 0; d < 3; ++d) { os.amin[d] = t.ds.aabb_min[d]; os.diag[d] = t.ds.aabb_max[d] - t.ds.aabb_min[d]; }
+				os.grid_in = t.density_grid.p; os.grid_tmp = t.density_tmp.p;
+				os.jt = t.jump_table();
+				if (n_u) {
+					if (!t.occ_ulist.p) t.occ_ulist.alloc(GRID3);
+					launch_occ_uniform_list(s, n_u, t.density_grid_ema_step, 0, n_u, t.occ_ulist.p, t.scan_tmp.p);
+					os.ulist = t.occ_ulist.p; os.n_ulist = n_u;
+				}
+				launch_occ_density(s, t.lay.L, t.lay.W, n_u + n_nu, os, t.gl, valid, t.params_h.p + t.lay.grid_off, t.mlp);
+				break;
+			}
 			case 13: {  // the march of a cut step: ray generation + the march over the slots below the cut's estimate
 				MarchWork mw = t.mwork;
 				mw.est_cut = t.cutw.p + CW_EST;
