@@ -233,7 +233,15 @@ struct OccSampling {
 	// is uniform sample ulist[k], the rest are the nonuniform samples in index order
 	const uint32_t* ulist;
 	uint32_t n_ulist;
+	// (with ulist) the rank's occupancy-biased samples in the order of their coarse cells (launch_occ_nu_list; nullable):
+	// work item n_ulist + k is occupancy-biased sample nulist[k] of the rank
+	const uint32_t* nulist = nullptr;
 };
+// The occupancy-biased samples [0, n) of a rank (global index g0 + k) binned by their coarse cell (cascade, 8^3-cell
+// Morton block: n_cascades x 4096 bins) into `list` - the order the density pass evaluates them in, for coherent
+// gathers; each sample's value and the max splat do not depend on it. key [n], bins [2 * n_cascades * 4096] scratch.
+void launch_occ_nu_list(hipStream_t s, uint32_t n, uint32_t g0, const OccSampling& os, uint32_t* key, uint32_t* bins, uint32_t* list, void* scan_tmp,
+                        size_t scan_tmp_bytes);
 // Cell-ordered list of the uniform samples [lo, hi) (n_u <= 128^3): the uniform hash (the first try always taken) maps
 // sample i to cell ((i + step n_u) 56924617 + 96925573) mod 2^21 bijectively, so walking the cells in (Morton) order and
 // inverting gives the samples in spatially coherent order; one look-back-scan pass (scan_tmp: a scan_temp_bytes state),

@@ -868,7 +868,8 @@ __global__ void __launch_bounds__(256) k_nerf_density(uint32_t n, const float* _
 			grid_sample_cell(cell, os.rng_u_state, os.rng_u_inc, os.amin, os.diag, x, os.jt);
 		} else if (MODE == 2) {
 			// cell-ordered uniform samples first (coherent gathers), then the nonuniform ones of the rank's range
-			const uint32_t g = os.ulist ? (ic < os.n_ulist ? os.ulist[ic] : max(os.lo, os.n_u) + (ic - os.n_ulist)) : os.lo + ic;
+			const uint32_t kk = ic - os.n_ulist;
+			const uint32_t g = os.ulist ? (ic < os.n_ulist ? os.ulist[ic] : max(os.lo, os.n_u) + (os.nulist ? os.nulist[kk] : kk)) : os.lo + ic;
 			const bool uni = g < os.n_u;
 			grid_sample(uni ? os.n_u : os.n_nu, uni ? g : g - os.n_u, uni ? os.rng_u_state : os.rng_nu_state, uni ? os.rng_u_inc : os.rng_nu_inc,
 			            os.step, os.amin, os.diag, os.grid_in, os.n_cascades, uni ? -0.01f : os.thresh_nu, x, cell, os.jt);
@@ -1768,6 +1769,33 @@ void launch_occ_uniform_list(hipStream_t s, uint32_t n_u, uint32_t step, uint32_
 	static_assert(GRID3 % SCAN_TILE == 0 && GRID3 / SCAN_TILE <= SCAN_MAX_TILES, "uniform list tiles");
 	dbg_lds_gate(s);
 	k_occ_uniform_list<<<GRID3 / SCAN_TILE, SCAN_THREADS, 0, s>>>(n_u, step, lo, hi, list, (ScanState*)scan_tmp, scan_next_tag(scan_tmp));
+}
+__global__ void __launch_bounds__(256) k_occ_nu_keys(uint32_t n, uint32_t g0, const OccSampling os, uint32_t* __restrict__ key,
+                                                     uint32_t* __restrict__ hist) {
+	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+		const uint32_t i = g0 + k;
+		pcg32 rng(os.rng_nu_state, os.rng_nu_inc);
+		pcg_advance(rng, (uint64_t)(uint32_t)(i * 4), os.jt);
+		const uint32_t idx = grid_sample_pick(os.n_nu, i, rng, os.step, os.grid_in, os.n_cascades, os.thresh_nu);
+		const uint32_t b = (idx / GRID3) * 4096u + ((idx % GRID3) >> 9);
+		key[k] = b;
+		atomicAdd(&hist[b], 1u);
+	}
+}
+__global__ void __launch_bounds__(256) k_occ_nu_place(uint32_t n, const uint32_t* __restrict__ key, uint32_t* __restrict__ cursor,
+                                                      uint32_t* __restrict__ list) {
+	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) list[atomicAdd(&cursor[key[k]], 1u)] = k;
+}
+void launch_occ_nu_list(hipStream_t s, uint32_t n, uint32_t g0, const OccSampling& os, uint32_t* key, uint32_t* bins, uint32_t* list, void* scan_tmp,
+                        size_t scan_tmp_bytes) {
+	if (n == 0) return;
+	const uint32_t nb = os.n_cascades * 4096u;
+	if (hipMemsetAsync(bins, 0, (size_t)nb * 4, s) != hipSuccess) throw std::runtime_error("launch_occ_nu_list: memset failed");
+	const uint32_t blocks = std::min<uint32_t>((n + 255) / 256, 2048);
+	dbg_lds_gate(s);
+	k_occ_nu_keys<<<blocks, 256, 0, s>>>(n, g0, os, key, bins);
+	launch_exclusive_scan(s, scan_tmp, scan_tmp_bytes, bins, bins + nb, nb);
+	k_occ_nu_place<<<blocks, 256, 0, s>>>(n, key, bins + nb, list);
 }
 void launch_occ_density(hipStream_t s, uint32_t L, uint32_t W, uint32_t n, const OccSampling& os, const GridLevels& gl, uint32_t valid_level,
                         const half_t* grid, const MlpPtrs& w) {

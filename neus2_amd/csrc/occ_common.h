@@ -8,12 +8,10 @@
 
 namespace neus {
 
-__device__ __forceinline__ void grid_sample(uint32_t n_elements, uint32_t i, uint64_t rng_state, uint64_t rng_inc, uint32_t step,
-                                            const float amin[3], const float diag[3], const float* __restrict__ grid_in, uint32_t n_cascades,
-                                            float thresh, float pos[3], uint32_t& idx_out, const PcgJumpTable& jt) {
-#pragma clang fp contract(off)  // the same bits in every translation unit (and as the oracle's restatement)
-	pcg32 rng(rng_state, rng_inc);
-	pcg_advance(rng, (uint64_t)(uint32_t)(i * 4), jt);
+// the cascade level and the cell (level * 128^3 + Morton index) of sample i, the rng advanced past the level draw
+__device__ __forceinline__ uint32_t grid_sample_pick(uint32_t n_elements, uint32_t i, pcg32& rng, uint32_t step, const float* __restrict__ grid_in,
+                                                     uint32_t n_cascades, float thresh) {
+#pragma clang fp contract(off)
 	const uint32_t level = (uint32_t)(rng.next_float() * n_cascades) % n_cascades;
 	uint32_t idx = 0;
 	for (uint32_t j = 0; j < 10; ++j) {
@@ -21,6 +19,17 @@ __device__ __forceinline__ void grid_sample(uint32_t n_elements, uint32_t i, uin
 		idx += level * GRID3;
 		if (grid_in[idx] > thresh) break;
 	}
+	return idx;
+}
+
+__device__ __forceinline__ void grid_sample(uint32_t n_elements, uint32_t i, uint64_t rng_state, uint64_t rng_inc, uint32_t step,
+                                            const float amin[3], const float diag[3], const float* __restrict__ grid_in, uint32_t n_cascades,
+                                            float thresh, float pos[3], uint32_t& idx_out, const PcgJumpTable& jt) {
+#pragma clang fp contract(off)  // the same bits in every translation unit (and as the oracle's restatement)
+	pcg32 rng(rng_state, rng_inc);
+	pcg_advance(rng, (uint64_t)(uint32_t)(i * 4), jt);
+	const uint32_t idx = grid_sample_pick(n_elements, i, rng, step, grid_in, n_cascades, thresh);
+	const uint32_t level = idx / GRID3;
 	const uint32_t pi = idx % GRID3;
 	const uint32_t x = morton3D_invert(pi >> 0), y = morton3D_invert(pi >> 1), z = morton3D_invert(pi >> 2);
 	const float rx = rng.next_float(), ry = rng.next_float(), rz = rng.next_float();

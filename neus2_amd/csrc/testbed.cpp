@@ -430,6 +430,11 @@ struct NeusTestbed {
 	// NEUS_MARCH_CUT=0 turns it off.
 	bool march_cut_on = [] { const char* e = std::getenv("NEUS_MARCH_CUT"); return !(e && e[0] == '0'); }();
 	bool force_full = false;      // the step being re-run marches every slot
+	// the occupancy-biased samples binned by their coarse cell before the density pass (NEUS_OCC_NU_SORT=1): bitwise the
+	// same grid, but 0.756-0.764 -> 0.765-0.771 ms/step at step 800 (profiles/r06occ_nu_sort_ab.txt: the binning's
+	// atomics on the few occupied bins cost more than the pass saves); off
+	bool occ_nu_sort = [] { const char* e = std::getenv("NEUS_OCC_NU_SORT"); return e && e[0] == '1'; }();
+	Dev<uint32_t> occ_nu_key, occ_nu_list, occ_nu_bins;
 	bool abort_direct = false;            // the last risky step's word comes through abort_word (one rank)
 	volatile uint32_t* abort_word = nullptr;  // host-coherent pinned word k_loss_grad stores the witness to (one rank)
 	uint32_t mcut_div = [] { const char* e = std::getenv("NEUS_DBG_MARCH_CUT_DIV"); return e ? (uint32_t)std::max(1, std::atoi(e)) : 1u; }();  // test hook
@@ -1242,6 +1247,15 @@ struct NeusTestbed {
 				if (!occ_ulist.p) occ_ulist.alloc(GRID3);
 				launch_occ_uniform_list(s, n_uniform, density_grid_ema_step, u_lo, u_hi, occ_ulist.p, scan_tmp.p);
 				os.ulist = occ_ulist.p; os.n_ulist = u_hi - u_lo;
+				// (occ_nu_sort: the occupancy-biased samples binned by their coarse cell as well; in index order the biased half
+				// takes 294 of the pass's 479 us, the cell-ordered uniform half 187 - profiles/r06occ_split.txt)
+				const uint32_t nu_lo = std::max(lo, n_uniform), n_nu_rank = hi > nu_lo ? hi - nu_lo : 0u;
+				if (occ_nu_sort && n_nu_rank) {
+					if (occ_nu_key.n < n_nu_rank) { occ_nu_key.alloc(n_nu_rank); occ_nu_list.alloc(n_nu_rank); }
+					occ_nu_bins.alloc(2 * 4096 * (size_t)(max_cascade + 1));
+					launch_occ_nu_list(s, n_nu_rank, nu_lo - n_uniform, os, occ_nu_key.p, occ_nu_bins.p, occ_nu_list.p, scan_tmp.p, scan_tmp_bytes);
+					os.nulist = occ_nu_list.p;
+				}
 			}
 			launch_occ_density(s, lay.L, lay.W, N, os, gl, valid, params_h.p + lay.grid_off, mlp);
 		} else {
